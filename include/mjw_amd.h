@@ -1,0 +1,172 @@
+/*
+ * mjw_amd.h -- C ABI of the MI355X batched MuJoCo stepper (libmjw_amd.so).
+ *
+ * Drop-in boundary for the `mjw.step(m, d)` path of mujoco_warp.  Each entry
+ * point replaces one reference function (file:line in mujoco_warp/_src):
+ *
+ *   mjw_step              <- forward.step                 forward.py:1003-1018
+ *   mjw_forward           <- forward.forward              forward.py:972-1000
+ *   mjw_fwd_position      <- forward.fwd_position         forward.py:513-537
+ *   mjw_fwd_velocity      <- forward.fwd_velocity         forward.py:592-613
+ *   mjw_fwd_actuation     <- forward.fwd_actuation        forward.py:836-927
+ *   mjw_fwd_acceleration  <- forward.fwd_acceleration     forward.py:949-969
+ *   mjw_solve             <- solver.solve                 solver.py:3296-3343
+ *   mjw_euler             <- forward.euler                forward.py:326-354
+ *   mjw_ctrl_noise        <- benchmark.ctrl_noise         _src/benchmark.py:41-83
+ *
+ * Ownership: the caller owns every buffer (device pointers below); the library
+ * never allocates or frees device memory and keeps no global mutable state.
+ * All launches are asynchronous on the caller's HIP stream (graph capturable).
+ * Return value: 0 on success, nonzero HIP error code otherwise
+ * (mjw_last_error() gives the message).
+ *
+ * Field lists are X-macros: the Python host (mujoco_warp_amd/_lib.py) parses
+ * them to build byte-identical ctypes structs.
+ */
+#ifndef MJW_AMD_H
+#define MJW_AMD_H
+
+#include <stdint.h>
+
+#define MJW_ABI_VERSION 1
+
+/* ---- model: int scalars ---- */
+#define MJW_MODEL_INT_SCALARS(X)                                                                   \
+  X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
+  X(nxn) X(nlevel) X(nlimited) X(nmaxcondim) X(nmaxpyramid) X(nv_pad) X(nJmom)                    \
+  X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations) X(opt_ls_iterations)             \
+  X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)
+
+/* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
+#define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
+  X(opt_timestep, 1) X(opt_tolerance, 1) X(opt_ls_tolerance, 1) X(opt_impratio_invsqrt, 1)        \
+  X(opt_gravity, 3) X(stat_meaninertia, 1)                                                         \
+  X(qpos0, nq) X(qpos_spring, nq)                                                                  \
+  X(body_pos, nbody * 3) X(body_quat, nbody * 4) X(body_ipos, nbody * 3) X(body_iquat, nbody * 4) \
+  X(body_mass, nbody) X(body_subtreemass, nbody) X(body_inertia, nbody * 3)                       \
+  X(body_invweight0, nbody * 2)                                                                    \
+  X(jnt_solref, njnt * 2) X(jnt_solimp, njnt * 5) X(jnt_pos, njnt * 3) X(jnt_axis, njnt * 3)      \
+  X(jnt_stiffness, njnt) X(jnt_range, njnt * 2) X(jnt_actfrcrange, njnt * 2) X(jnt_margin, njnt)  \
+  X(dof_solref, nv * 2) X(dof_solimp, nv * 5) X(dof_frictionloss, nv) X(dof_armature, nv)         \
+  X(dof_damping, nv) X(dof_invweight0, nv)                                                         \
+  X(geom_solmix, ngeom) X(geom_solref, ngeom * 2) X(geom_solimp, ngeom * 5) X(geom_size, ngeom * 3) \
+  X(geom_aabb, ngeom * 6) X(geom_rbound, ngeom) X(geom_pos, ngeom * 3) X(geom_quat, ngeom * 4)    \
+  X(geom_friction, ngeom * 3) X(geom_margin, ngeom) X(geom_gap, ngeom)                             \
+  X(site_pos, nsite * 3) X(site_quat, nsite * 4)                                                   \
+  X(cam_pos, ncam * 3) X(cam_quat, ncam * 4) X(cam_poscom0, ncam * 3) X(cam_pos0, ncam * 3)       \
+  X(cam_mat0, ncam * 9)                                                                            \
+  X(light_pos, nlight * 3) X(light_dir, nlight * 3) X(light_poscom0, nlight * 3)                  \
+  X(light_pos0, nlight * 3) X(light_dir0, nlight * 3)                                              \
+  X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
+  X(actuator_ctrlrange, nu * 2) X(actuator_forcerange, nu * 2) X(actuator_actrange, nu * 2)       \
+  X(actuator_gear, nu * 6)
+
+/* ---- model: int arrays (never batched) ---- */
+#define MJW_MODEL_INT_ARRAYS(X)                                                                    \
+  X(body_parentid, nbody) X(body_rootid, nbody) X(body_weldid, nbody) X(body_mocapid, nbody)      \
+  X(body_jntnum, nbody) X(body_jntadr, nbody) X(body_dofnum, nbody) X(body_dofadr, nbody)         \
+  X(body_subtree_end, nbody) X(level_body, nbody) X(level_adr, nlevel + 1)                        \
+  X(jnt_type, njnt) X(jnt_qposadr, njnt) X(jnt_dofadr, njnt) X(jnt_bodyid, njnt)                  \
+  X(jnt_limited, njnt) X(jnt_actfrclimited, njnt) X(jnt_limited_slide_hinge_adr, nlimited)        \
+  X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \
+  X(geom_type, ngeom) X(geom_condim, ngeom) X(geom_bodyid, ngeom) X(geom_priority, ngeom)         \
+  X(site_bodyid, nsite)                                                                            \
+  X(cam_mode, ncam) X(cam_bodyid, ncam) X(cam_targetbodyid, ncam)                                 \
+  X(light_mode, nlight) X(light_bodyid, nlight) X(light_targetbodyid, nlight)                     \
+  X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
+  X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
+  X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
+  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)
+
+/* ---- data: float arrays, (nworld, count) world-major like mujoco_warp types.Data ---- */
+#define MJW_DATA_REAL_ARRAYS(X)                                                                    \
+  X(time, 1) X(qpos, nq) X(qvel, nv) X(act, na) X(ctrl, nu) X(qacc_warmstart, nv)                 \
+  X(qfrc_applied, nv) X(xfrc_applied, nbody * 6) X(mocap_pos, nmocap * 3) X(mocap_quat, nmocap * 4) \
+  X(qacc, nv) X(act_dot, na) X(energy, 2)                                                          \
+  X(xpos, nbody * 3) X(xquat, nbody * 4) X(xmat, nbody * 9) X(xipos, nbody * 3) X(ximat, nbody * 9) \
+  X(xanchor, njnt * 3) X(xaxis, njnt * 3) X(geom_xpos, ngeom * 3) X(geom_xmat, ngeom * 9)         \
+  X(site_xpos, nsite * 3) X(site_xmat, nsite * 9) X(cam_xpos, ncam * 3) X(cam_xmat, ncam * 9)     \
+  X(light_xpos, nlight * 3) X(light_xdir, nlight * 3)                                              \
+  X(subtree_com, nbody * 3) X(cdof, nv * 6) X(cinert, nbody * 10) X(crb, nbody * 10)              \
+  X(qM, nv_pad * nv_pad) X(qLD, nv * nv)                                                           \
+  X(actuator_length, nu) X(actuator_moment, nJmom) X(actuator_velocity, nu) X(actuator_force, nu) \
+  X(cvel, nbody * 6) X(cdof_dot, nv * 6) X(qfrc_bias, nv) X(qfrc_spring, nv) X(qfrc_damper, nv)   \
+  X(qfrc_gravcomp, nv) X(qfrc_passive, nv) X(qfrc_actuator, nv) X(qfrc_smooth, nv)                \
+  X(qacc_smooth, nv) X(qfrc_constraint, nv) X(cacc, nbody * 6) X(cfrc_int, nbody * 6)             \
+  X(cfrc_ext, nbody * 6)                                                                           \
+  X(efc_J, njmax_pad * nv_pad) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax_pad)         \
+  X(efc_vel, njmax) X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax)             \
+  X(efc_Ma, nv)
+
+/* ---- data: int arrays, (nworld, count) ---- */
+#define MJW_DATA_INT_ARRAYS(X)                                                                     \
+  X(ne, 1) X(nf, 1) X(nl, 1) X(nefc, 1) X(solver_niter, 1)                                         \
+  X(moment_rownnz, nu) X(moment_rowadr, nu) X(moment_colind, nJmom)                                \
+  X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax_pad)
+
+/* ---- contact pool: float arrays, (naconmax, count) ---- */
+#define MJW_CONTACT_REAL_ARRAYS(X)                                                                 \
+  X(contact_dist, 1) X(contact_pos, 3) X(contact_frame, 9) X(contact_includemargin, 1)            \
+  X(contact_friction, 5) X(contact_solref, 2) X(contact_solreffriction, 2) X(contact_solimp, 5)
+
+/* ---- contact pool: int arrays, (naconmax, count) ---- */
+#define MJW_CONTACT_INT_ARRAYS(X)                                                                  \
+  X(contact_dim, 1) X(contact_geom, 2) X(contact_efc_address, nmaxpyramid) X(contact_worldid, 1)  \
+  X(contact_type, 1) X(contact_geomcollisionid, 1)
+
+typedef struct mjw_model_t {
+#define MJW_DECL_I(name) int32_t name;
+#define MJW_DECL_RA(name, n) const float* name; int32_t name##_nb; int32_t name##_cnt;
+#define MJW_DECL_IA(name, n) const int32_t* name;
+  MJW_MODEL_INT_SCALARS(MJW_DECL_I)
+  MJW_MODEL_REAL_ARRAYS(MJW_DECL_RA)
+  MJW_MODEL_INT_ARRAYS(MJW_DECL_IA)
+} mjw_model_t;
+
+typedef struct mjw_data_t {
+  int32_t nworld;     /* worlds held by these buffers */
+  int32_t njmax;      /* max constraint rows per world */
+  int32_t njmax_pad;  /* padded row count of efc_J / efc_D / efc_state */
+  int32_t naconmax;   /* contact pool capacity (all worlds) */
+  int32_t world_offset; /* global id of world 0 (multi-GPU sharding); affects ctrl noise only */
+  int32_t pad_;
+  int32_t* nacon;      /* (1,) contacts written this step (may exceed naconmax) */
+  int32_t* ncollision; /* (1,) broadphase pairs this step */
+#define MJW_DECL_DRA(name, n) float* name;
+#define MJW_DECL_DIA(name, n) int32_t* name;
+  MJW_DATA_REAL_ARRAYS(MJW_DECL_DRA)
+  MJW_DATA_INT_ARRAYS(MJW_DECL_DIA)
+  MJW_CONTACT_REAL_ARRAYS(MJW_DECL_DRA)
+  MJW_CONTACT_INT_ARRAYS(MJW_DECL_DIA)
+} mjw_data_t;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int mjw_abi_version(void);
+const char* mjw_last_error(void);
+/* sizeof checks for the Python binding */
+int mjw_sizeof_model(void);
+int mjw_sizeof_data(void);
+/* per-world LDS bytes the fused step needs for this model and njmax */
+int mjw_lds_bytes(const mjw_model_t* m, int njmax);
+
+/* stream: a hipStream_t (NULL = default stream) */
+int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+int mjw_fwd_velocity(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+int mjw_fwd_actuation(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+int mjw_fwd_acceleration(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+int mjw_solve(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+/* per-step control noise (Ornstein-Uhlenbeck + Halton) of the reference benchmark;
+ * center: device float[nu] or NULL; world ids are d->world_offset + local id */
+int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* center, int step, float std, float rate,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,34 @@
+"""Builds libmjw_amd.so in-tree with hipcc for gfx950 (`python -m mujoco_warp_amd.build`)."""
+
+import os
+import subprocess
+import sys
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(_PKG)
+SOURCES = [os.path.join(_PKG, "csrc", "mjw_step.hip")]
+HEADERS = [os.path.join(_PKG, "csrc", "mjw_math.h"), os.path.join(_ROOT, "include", "mjw_amd.h")]
+OUT = os.path.join(_PKG, "libmjw_amd.so")
+ARCH = os.environ.get("MJW_OFFLOAD_ARCH", "gfx950")
+
+
+def needs_build():
+  if not os.path.exists(OUT):
+    return True
+  t = os.path.getmtime(OUT)
+  return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
+
+
+def build(force=False, verbose=False):
+  if not force and not needs_build():
+    return OUT
+  cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-I", os.path.join(_ROOT, "include"),
+         "-o", OUT] + SOURCES
+  if verbose:
+    print(" ".join(cmd))
+  subprocess.run(cmd, check=True)
+  return OUT
+
+
+if __name__ == "__main__":
+  print(build(force="--force" in sys.argv, verbose=True))

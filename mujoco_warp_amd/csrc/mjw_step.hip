@@ -1,0 +1,2000 @@
+// mjw_step.hip -- world-per-wavefront batched MuJoCo step for MI355X (gfx950).
+//
+// One 64-lane wavefront owns one world for a whole stage group (or the whole
+// step): lanes map to bodies / dofs / geom pairs / constraint rows, tree
+// recursions run level by level inside the wave, per-world working state lives
+// in LDS, and the CG/Newton convergence loop runs per world inside the kernel
+// (no batch-wide solver tail, no graph conditionals).  Algorithms restate the
+// reference pipeline mujoco_warp/_src/forward.py:1003-1018; each stage cites
+// the reference file:line it follows.
+//
+// Global memory: Model fields are read-only (L2/scalar-cache resident); Data
+// fields keep mujoco_warp's world-major shapes (nworld, ...), read once and
+// written once per stage group with lane-contiguous (coalesced) accesses.
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "mjw_amd.h"
+#include "mjw_math.h"
+
+namespace mjw {
+
+constexpr int LPW = 64;   // lanes per world (one wavefront)
+constexpr int CREC = 32;  // floats per staged contact record
+constexpr int CMAX = 32;  // staged contacts per collision round
+
+enum : int { ST_POS = 1, ST_VEL = 2, ST_ACT = 4, ST_ACC = 8, ST_SOLVE = 16, ST_EULER = 32 };
+enum : int { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
+enum : int { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3 };
+enum : int {
+  DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16, DSBL_SPRING = 32,
+  DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512, DSBL_ACTUATION = 2048,
+  DSBL_REFSAFE = 4096, DSBL_EULERDAMP = 1 << 15
+};
+enum : int { ENBL_ENERGY = 2 };
+enum : int { CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
+enum : int { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3 };
+enum : int { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
+enum : int { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
+enum : int { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
+
+// per-world LDS layout (offsets in 4-byte words)
+struct Lay {
+  int qpos, qvel, xpos, xquat, xmat, xipos, ximat, xanchor, xaxis, gxpos, gxmat;
+  int subtree_com, cinert, crb, cdof, cdof_dot, cvel, cacc, cfrc;
+  int qM, L, H, nvs;
+  int qfrc_smooth, qacc_smooth, qacc, Ma, qfrc_constraint, qfrc_bias, qfrc_passive, qfrc_actuator, vec;
+  int J, efc_D, efc_aref, efc_pos, efc_margin, efc_vel, efc_frictionloss, efc_type, efc_id, efc_force, efc_state;
+  int Jaref, jv, rowcon;
+  int act_len, act_vel, act_force, act_mom, act_momdof, act_nnz;
+  int con, scratch, iscratch;
+  int total;
+};
+
+__host__ inline Lay make_layout(const mjw_model_t& m, int njmax) {
+  Lay L;
+  int o = 0;
+  auto take = [&](int n) { int r = o; o += (n + 3) & ~3; return r; };
+  int nv = m.nv, nb = m.nbody, nj = m.njnt, ng = m.ngeom, nu = m.nu;
+  L.nvs = nv | 1;  // odd row stride: conflict-free row and column access
+  L.qpos = take(m.nq); L.qvel = take(nv);
+  L.xpos = take(nb * 3); L.xquat = take(nb * 4); L.xmat = take(nb * 9); L.xipos = take(nb * 3); L.ximat = take(nb * 9);
+  L.xanchor = take(nj * 3); L.xaxis = take(nj * 3); L.gxpos = take(ng * 3); L.gxmat = take(ng * 9);
+  L.subtree_com = take(nb * 3); L.cinert = take(nb * 10); L.crb = take(nb * 10); L.cdof = take(nv * 6);
+  L.cdof_dot = take(nv * 6); L.cvel = take(nb * 6); L.cacc = take(nb * 6); L.cfrc = take(nb * 6);
+  L.qM = take(nv * L.nvs); L.L = take(nv * L.nvs);
+  L.H = (m.opt_solver == SOLVER_NEWTON) ? take(nv * L.nvs) : L.L;
+  L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv); L.qacc = take(nv); L.Ma = take(nv); L.qfrc_constraint = take(nv);
+  L.qfrc_bias = take(nv); L.qfrc_passive = take(nv); L.qfrc_actuator = take(nv); L.vec = take(2 * nv);
+  L.J = take(njmax * L.nvs);
+  L.efc_D = take(njmax); L.efc_aref = take(njmax); L.efc_pos = take(njmax); L.efc_margin = take(njmax);
+  L.efc_vel = take(njmax); L.efc_frictionloss = take(njmax); L.efc_type = take(njmax); L.efc_id = take(njmax);
+  L.efc_force = take(njmax); L.efc_state = take(njmax); L.Jaref = take(njmax); L.jv = take(njmax); L.rowcon = take(njmax);
+  L.act_len = take(nu); L.act_vel = take(nu); L.act_force = take(nu); L.act_mom = take(nu * 6); L.act_momdof = take(nu * 6);
+  L.act_nnz = take(nu);
+  L.con = take(CMAX * CREC);
+  L.scratch = take(64);
+  L.iscratch = take(64);
+  L.total = o;
+  return L;
+}
+
+// -------------------------------------------------------------------------------------------
+// wave-level collectives
+// -------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// inclusive prefix sum of small non-negative ints across the wave
+__device__ __forceinline__ int wave_scan_incl(int v) {
+  int lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int t = __shfl_up(v, off, 64);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
+
+#define WSYNC() __syncthreads()
+
+// batched model field base pointer for world w (types.py "*" semantics: worldid % nb)
+__device__ __forceinline__ const float* mb(const float* p, int nb, int cnt, int w) {
+  return nb <= 1 ? p : p + (long)(w % nb) * cnt;
+}
+#define MR(name) mb(m.name, m.name##_nb, m.name##_cnt, wid)
+
+struct WS {
+  float* s;  // LDS base of this world
+  int* si;   // same, as ints
+  int wid;   // world index within the launch
+  int lane;
+};
+
+// -------------------------------------------------------------------------------------------
+// smooth.py: kinematics (smooth.py:44-224, 357-415)
+// -------------------------------------------------------------------------------------------
+__device__ void kinematics(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  const float* qpos = s + L.qpos;
+  const float* body_pos = MR(body_pos);
+  const float* body_quat = MR(body_quat);
+  const float* jnt_pos = MR(jnt_pos);
+  const float* jnt_axis = MR(jnt_axis);
+  const float* qpos0 = MR(qpos0);
+  float* xpos = s + L.xpos;
+  float* xquat = s + L.xquat;
+  if (lane == 0) {
+    xpos[0] = xpos[1] = xpos[2] = 0.0f;
+    xquat[0] = 1.0f; xquat[1] = xquat[2] = xquat[3] = 0.0f;
+  }
+  WSYNC();
+  for (int lvl = 1; lvl < m.nlevel; lvl++) {
+    int beg = m.level_adr[lvl], end = m.level_adr[lvl + 1];
+    for (int idx = beg + lane; idx < end; idx += LPW) {
+      int b = m.level_body[idx];
+      int pid = m.body_parentid[b];
+      int jntadr = m.body_jntadr[b], jntnum = m.body_jntnum[b];
+      if (jntnum == 1 && m.jnt_type[jntadr] == JNT_FREE) {
+        int qa = m.jnt_qposadr[jntadr];
+        float q[4] = {qpos[qa + 3], qpos[qa + 4], qpos[qa + 5], qpos[qa + 6]};
+        normalize4(q);
+        for (int i = 0; i < 3; i++) xpos[3 * b + i] = qpos[qa + i];
+        for (int i = 0; i < 4; i++) xquat[4 * b + i] = q[i];
+        for (int i = 0; i < 3; i++) {
+          s[L.xanchor + 3 * jntadr + i] = qpos[qa + i];
+          s[L.xaxis + 3 * jntadr + i] = jnt_axis[3 * jntadr + i];
+        }
+        continue;
+      }
+      float pos[3], quat[4];
+      int mocapid = m.body_mocapid[b];
+      if (mocapid >= 0) {
+        for (int i = 0; i < 3; i++) pos[i] = d.mocap_pos[(long)wid * m.nmocap * 3 + 3 * mocapid + i];
+        for (int i = 0; i < 4; i++) quat[i] = d.mocap_quat[(long)wid * m.nmocap * 4 + 4 * mocapid + i];
+      } else {
+        for (int i = 0; i < 3; i++) pos[i] = body_pos[3 * b + i];
+        for (int i = 0; i < 4; i++) quat[i] = body_quat[4 * b + i];
+      }
+      {
+        float pq[4] = {xquat[4 * pid], xquat[4 * pid + 1], xquat[4 * pid + 2], xquat[4 * pid + 3]};
+        float t[3];
+        rot_vec_quat(t, pos, pq);
+        for (int i = 0; i < 3; i++) pos[i] = t[i] + xpos[3 * pid + i];
+        mul_quat(quat, pq, quat);
+      }
+      for (int k = 0; k < jntnum; k++) {
+        int j = jntadr + k;
+        int qa = m.jnt_qposadr[j];
+        const float* ax = jnt_axis + 3 * j;
+        const float* jp = jnt_pos + 3 * j;
+        float xanchor[3], xaxis[3], t[3];
+        rot_vec_quat(t, jp, quat);
+        for (int i = 0; i < 3; i++) xanchor[i] = t[i] + pos[i];
+        rot_vec_quat(xaxis, ax, quat);
+        int jt = m.jnt_type[j];
+        if (jt == JNT_BALL) {
+          float ql[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]};
+          normalize4(ql);
+          mul_quat(quat, quat, ql);
+          rot_vec_quat(t, jp, quat);
+          for (int i = 0; i < 3; i++) pos[i] = xanchor[i] - t[i];
+        } else if (jt == JNT_SLIDE) {
+          float dq = qpos[qa] - qpos0[qa];
+          for (int i = 0; i < 3; i++) pos[i] += xaxis[i] * dq;
+        } else if (jt == JNT_HINGE) {
+          float ql[4];
+          axis_angle_to_quat(ql, ax, qpos[qa] - qpos0[qa]);
+          mul_quat(quat, quat, ql);
+          rot_vec_quat(t, jp, quat);
+          for (int i = 0; i < 3; i++) pos[i] = xanchor[i] - t[i];
+        }
+        for (int i = 0; i < 3; i++) {
+          s[L.xanchor + 3 * j + i] = xanchor[i];
+          s[L.xaxis + 3 * j + i] = xaxis[i];
+        }
+      }
+      normalize4(quat);
+      for (int i = 0; i < 3; i++) xpos[3 * b + i] = pos[i];
+      for (int i = 0; i < 4; i++) xquat[4 * b + i] = quat[i];
+    }
+    WSYNC();
+  }
+  // body matrices / inertial frames (smooth.py:146-173)
+  const float* body_ipos = MR(body_ipos);
+  const float* body_iquat = MR(body_iquat);
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float q[4] = {xquat[4 * b], xquat[4 * b + 1], xquat[4 * b + 2], xquat[4 * b + 3]};
+    float mat[9], t[3], qi[4], imat[9];
+    quat_to_mat(mat, q);
+    rot_vec_quat(t, body_ipos + 3 * b, q);
+    float xi[3] = {xpos[3 * b] + t[0], xpos[3 * b + 1] + t[1], xpos[3 * b + 2] + t[2]};
+    mul_quat(qi, q, body_iquat + 4 * b);
+    quat_to_mat(imat, qi);
+    for (int i = 0; i < 9; i++) { s[L.xmat + 9 * b + i] = mat[i]; s[L.ximat + 9 * b + i] = imat[i]; }
+    for (int i = 0; i < 3; i++) s[L.xipos + 3 * b + i] = xi[i];
+    long gb = (long)wid * m.nbody;
+    for (int i = 0; i < 3; i++) { d.xpos[(gb + b) * 3 + i] = xpos[3 * b + i]; d.xipos[(gb + b) * 3 + i] = xi[i]; }
+    for (int i = 0; i < 4; i++) d.xquat[(gb + b) * 4 + i] = q[i];
+    for (int i = 0; i < 9; i++) { d.xmat[(gb + b) * 9 + i] = mat[i]; d.ximat[(gb + b) * 9 + i] = imat[i]; }
+  }
+  for (int j = lane; j < m.njnt; j += LPW) {
+    long gj = (long)wid * m.njnt + j;
+    for (int i = 0; i < 3; i++) { d.xanchor[gj * 3 + i] = s[L.xanchor + 3 * j + i]; d.xaxis[gj * 3 + i] = s[L.xaxis + 3 * j + i]; }
+  }
+  // geoms (smooth.py:176-203) -- static world geoms evaluate to the same pose
+  const float* geom_pos = MR(geom_pos);
+  const float* geom_quat = MR(geom_quat);
+  for (int g = lane; g < m.ngeom; g += LPW) {
+    int b = m.geom_bodyid[g];
+    float q[4] = {xquat[4 * b], xquat[4 * b + 1], xquat[4 * b + 2], xquat[4 * b + 3]};
+    float t[3], gq[4], gm[9];
+    rot_vec_quat(t, geom_pos + 3 * g, q);
+    mul_quat(gq, q, geom_quat + 4 * g);
+    quat_to_mat(gm, gq);
+    long gg = (long)wid * m.ngeom + g;
+    for (int i = 0; i < 3; i++) {
+      float v = xpos[3 * b + i] + t[i];
+      s[L.gxpos + 3 * g + i] = v;
+      d.geom_xpos[gg * 3 + i] = v;
+    }
+    for (int i = 0; i < 9; i++) { s[L.gxmat + 9 * g + i] = gm[i]; d.geom_xmat[gg * 9 + i] = gm[i]; }
+  }
+  const float* site_pos = MR(site_pos);
+  const float* site_quat = MR(site_quat);
+  for (int si = lane; si < m.nsite; si += LPW) {
+    int b = m.site_bodyid[si];
+    float q[4] = {xquat[4 * b], xquat[4 * b + 1], xquat[4 * b + 2], xquat[4 * b + 3]};
+    float t[3], sq[4], sm[9];
+    rot_vec_quat(t, site_pos + 3 * si, q);
+    mul_quat(sq, q, site_quat + 4 * si);
+    quat_to_mat(sm, sq);
+    long gs = (long)wid * m.nsite + si;
+    for (int i = 0; i < 3; i++) d.site_xpos[gs * 3 + i] = xpos[3 * b + i] + t[i];
+    for (int i = 0; i < 9; i++) d.site_xmat[gs * 9 + i] = sm[i];
+  }
+  WSYNC();
+}
+
+// smooth.py:463-632: subtree com (contiguous DFS subtree ranges), cinert, cdof
+__device__ void com_pos(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  const float* body_mass = MR(body_mass);
+  const float* body_subtreemass = MR(body_subtreemass);
+  const float* body_inertia = MR(body_inertia);
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    int end = m.body_subtree_end[b];
+    for (int j = b; j < end; j++) {
+      float ms = body_mass[j];
+      for (int i = 0; i < 3; i++) acc[i] += s[L.xipos + 3 * j + i] * ms;
+    }
+    float mass = body_subtreemass[b];
+    if (mass != 0.0f)
+      for (int i = 0; i < 3; i++) acc[i] /= mass;
+    long gb = (long)wid * m.nbody + b;
+    for (int i = 0; i < 3; i++) { s[L.subtree_com + 3 * b + i] = acc[i]; d.subtree_com[gb * 3 + i] = acc[i]; }
+  }
+  WSYNC();
+  for (int b = lane; b < m.nbody; b += LPW) {
+    const float* mat = s + L.ximat + 9 * b;
+    const float* inert = body_inertia + 3 * b;
+    float mass = body_mass[b];
+    int root = m.body_rootid[b];
+    float dif[3];
+    for (int i = 0; i < 3; i++) dif[i] = s[L.xipos + 3 * b + i] - s[L.subtree_com + 3 * root + i];
+    float tmp[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        tmp[3 * i + j] = mat[3 * i] * inert[0] * mat[3 * j] + mat[3 * i + 1] * inert[1] * mat[3 * j + 1] +
+                         mat[3 * i + 2] * inert[2] * mat[3 * j + 2];
+    float res[10];
+    res[0] = tmp[0] + mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+    res[1] = tmp[4] + mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+    res[2] = tmp[8] + mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+    res[3] = tmp[1] - mass * dif[0] * dif[1];
+    res[4] = tmp[2] - mass * dif[0] * dif[2];
+    res[5] = tmp[5] - mass * dif[1] * dif[2];
+    res[6] = mass * dif[0];
+    res[7] = mass * dif[1];
+    res[8] = mass * dif[2];
+    res[9] = mass;
+    long gb = (long)wid * m.nbody + b;
+    for (int i = 0; i < 10; i++) { s[L.cinert + 10 * b + i] = res[i]; d.cinert[gb * 10 + i] = res[i]; }
+  }
+  for (int i = lane; i < m.nv; i += LPW) {
+    int j = m.dof_jntid[i];
+    int b = m.jnt_bodyid[j], jt = m.jnt_type[j], k = i - m.jnt_dofadr[j];
+    int root = m.body_rootid[b];
+    float off[3], r[6];
+    for (int a = 0; a < 3; a++) off[a] = s[L.subtree_com + 3 * root + a] - s[L.xanchor + 3 * j + a];
+    if ((jt == JNT_FREE && k >= 3) || jt == JNT_BALL) {
+      int c = jt == JNT_FREE ? k - 3 : k;
+      float ax[3] = {s[L.xmat + 9 * b + c], s[L.xmat + 9 * b + 3 + c], s[L.xmat + 9 * b + 6 + c]};
+      r[0] = ax[0]; r[1] = ax[1]; r[2] = ax[2];
+      cross3(r + 3, ax, off);
+    } else if (jt == JNT_FREE) {
+      r[0] = r[1] = r[2] = 0.0f;
+      r[3] = k == 0 ? 1.0f : 0.0f; r[4] = k == 1 ? 1.0f : 0.0f; r[5] = k == 2 ? 1.0f : 0.0f;
+    } else if (jt == JNT_SLIDE) {
+      r[0] = r[1] = r[2] = 0.0f;
+      for (int a = 0; a < 3; a++) r[3 + a] = s[L.xaxis + 3 * j + a];
+    } else {
+      float ax[3] = {s[L.xaxis + 3 * j], s[L.xaxis + 3 * j + 1], s[L.xaxis + 3 * j + 2]};
+      r[0] = ax[0]; r[1] = ax[1]; r[2] = ax[2];
+      cross3(r + 3, ax, off);
+    }
+    long gd = (long)wid * m.nv + i;
+    for (int a = 0; a < 6; a++) { s[L.cdof + 6 * i + a] = r[a]; d.cdof[gd * 6 + a] = r[a]; }
+  }
+  WSYNC();
+}
+
+// smooth.py:635-803
+__device__ void camlight(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  const float* s = w.s;
+  const float* cam_pos = MR(cam_pos);
+  const float* cam_quat = MR(cam_quat);
+  const float* cam_pos0 = MR(cam_pos0);
+  const float* cam_poscom0 = MR(cam_poscom0);
+  const float* cam_mat0 = MR(cam_mat0);
+  for (int c = lane; c < m.ncam; c += LPW) {
+    int mode = m.cam_mode[c], b = m.cam_bodyid[c], tgt = m.cam_targetbodyid[c];
+    bool is_target = mode == CAM_TARGETBODY || mode == CAM_TARGETBODYCOM;
+    float cx[3], cm[9];
+    const float* xq = s + L.xquat + 4 * b;
+    const float* xp = s + L.xpos + 3 * b;
+    if ((is_target && tgt < 0) || mode == CAM_FIXED) {
+      float t[3], q[4];
+      rot_vec_quat(t, cam_pos + 3 * c, xq);
+      for (int i = 0; i < 3; i++) cx[i] = xp[i] + t[i];
+      mul_quat(q, xq, cam_quat + 4 * c);
+      quat_to_mat(cm, q);
+    } else if (mode == CAM_TRACK) {
+      for (int i = 0; i < 9; i++) cm[i] = cam_mat0[9 * c + i];
+      for (int i = 0; i < 3; i++) cx[i] = xp[i] + cam_pos0[3 * c + i];
+    } else if (mode == CAM_TRACKCOM) {
+      for (int i = 0; i < 9; i++) cm[i] = cam_mat0[9 * c + i];
+      for (int i = 0; i < 3; i++) cx[i] = s[L.subtree_com + 3 * b + i] + cam_poscom0[3 * c + i];
+    } else {
+      float t[3], m1[3], m2[3], m3[3];
+      rot_vec_quat(t, cam_pos + 3 * c, xq);
+      for (int i = 0; i < 3; i++) cx[i] = xp[i] + t[i];
+      const float* tp = mode == CAM_TARGETBODYCOM ? s + L.subtree_com + 3 * tgt : s + L.xpos + 3 * tgt;
+      for (int i = 0; i < 3; i++) m3[i] = cx[i] - tp[i];
+      normalize3(m3);
+      float z[3] = {0.0f, 0.0f, 1.0f};
+      cross3(m1, z, m3);
+      normalize3(m1);
+      cross3(m2, m3, m1);
+      normalize3(m2);
+      for (int i = 0; i < 3; i++) { cm[3 * i] = m1[i]; cm[3 * i + 1] = m2[i]; cm[3 * i + 2] = m3[i]; }
+    }
+    long gc = (long)wid * m.ncam + c;
+    for (int i = 0; i < 3; i++) d.cam_xpos[gc * 3 + i] = cx[i];
+    for (int i = 0; i < 9; i++) d.cam_xmat[gc * 9 + i] = cm[i];
+  }
+  const float* light_pos = MR(light_pos);
+  const float* light_dir = MR(light_dir);
+  const float* light_pos0 = MR(light_pos0);
+  const float* light_poscom0 = MR(light_poscom0);
+  const float* light_dir0 = MR(light_dir0);
+  for (int l = lane; l < m.nlight; l += LPW) {
+    int mode = m.light_mode[l], b = m.light_bodyid[l], tgt = m.light_targetbodyid[l];
+    bool is_target = mode == CAM_TARGETBODY || mode == CAM_TARGETBODYCOM;
+    float lx[3], ld[3];
+    const float* xq = s + L.xquat + 4 * b;
+    const float* xp = s + L.xpos + 3 * b;
+    bool norm = true;
+    if ((is_target && tgt < 0) || mode == CAM_FIXED) {
+      float t[3];
+      rot_vec_quat(t, light_pos + 3 * l, xq);
+      for (int i = 0; i < 3; i++) lx[i] = xp[i] + t[i];
+      rot_vec_quat(ld, light_dir + 3 * l, xq);
+      norm = !(is_target && tgt < 0);  // smooth.py:732 returns before normalize
+    } else if (mode == CAM_TRACK) {
+      for (int i = 0; i < 3; i++) { ld[i] = light_dir0[3 * l + i]; lx[i] = xp[i] + light_pos0[3 * l + i]; }
+    } else if (mode == CAM_TRACKCOM) {
+      for (int i = 0; i < 3; i++) { ld[i] = light_dir0[3 * l + i]; lx[i] = s[L.subtree_com + 3 * b + i] + light_poscom0[3 * l + i]; }
+    } else {
+      float t[3];
+      rot_vec_quat(t, light_pos + 3 * l, xq);
+      for (int i = 0; i < 3; i++) lx[i] = xp[i] + t[i];
+      const float* tp = mode == CAM_TARGETBODYCOM ? s + L.subtree_com + 3 * tgt : s + L.xpos + 3 * tgt;
+      for (int i = 0; i < 3; i++) ld[i] = tp[i] - lx[i];
+    }
+    if (norm) normalize3(ld);
+    long gl = (long)wid * m.nlight + l;
+    for (int i = 0; i < 3; i++) { d.light_xpos[gl * 3 + i] = lx[i]; d.light_xdir[gl * 3 + i] = ld[i]; }
+  }
+}
+
+// smooth.py:806-912: composite inertia (subtree ranges) and dense qM
+__device__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  const float* dof_armature = MR(dof_armature);
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float acc[10];
+    for (int i = 0; i < 10; i++) acc[i] = s[L.cinert + 10 * b + i];
+    if (b > 0) {
+      int end = m.body_subtree_end[b];
+      for (int j = b + 1; j < end; j++)
+        for (int i = 0; i < 10; i++) acc[i] += s[L.cinert + 10 * j + i];
+    }
+    long gb = (long)wid * m.nbody + b;
+    for (int i = 0; i < 10; i++) { s[L.crb + 10 * b + i] = acc[i]; d.crb[gb * 10 + i] = acc[i]; }
+  }
+  const int nv = m.nv, nvs = L.nvs;
+  float* M = s + L.qM;
+  for (int e = lane; e < nv * nvs; e += LPW) M[e] = 0.0f;
+  WSYNC();
+  for (int i = lane; i < nv; i += LPW) {
+    int b = m.dof_bodyid[i];
+    float buf[6], cd[6];
+    for (int a = 0; a < 6; a++) cd[a] = s[L.cdof + 6 * i + a];
+    inert_vec(buf, s + L.crb + 10 * b, cd);
+    float Mii = dof_armature[i];
+    Mii += cd[0] * buf[0] + cd[1] * buf[1] + cd[2] * buf[2] + cd[3] * buf[3] + cd[4] * buf[4] + cd[5] * buf[5];
+    M[i * nvs + i] = Mii;
+    int j = m.dof_parentid[i];
+    while (j >= 0) {
+      const float* cj = s + L.cdof + 6 * j;
+      float q = cj[0] * buf[0] + cj[1] * buf[1] + cj[2] * buf[2] + cj[3] * buf[3] + cj[4] * buf[4] + cj[5] * buf[5];
+      M[i * nvs + j] = q;
+      M[j * nvs + i] = q;
+      j = m.dof_parentid[j];
+    }
+  }
+  WSYNC();
+  const int np = m.nv_pad;
+  float* gM = d.qM + (long)wid * np * np;
+  for (int e = lane; e < np * np; e += LPW) {
+    int r = e / np, c = e - r * np;
+    gM[e] = (r < nv && c < nv) ? M[r * nvs + c] : 0.0f;
+  }
+}
+
+// -------------------------------------------------------------------------------------------
+// dense Cholesky (wp.tile_cholesky) and solve (wp.tile_cholesky_solve), lane = row
+// -------------------------------------------------------------------------------------------
+__device__ void cholesky(float* A, int n, int nvs, int lane) {
+  // in place: lower triangle of A becomes L (A = L L^T), upper set to zero
+  for (int j = 0; j < n; j++) {
+    float ljj = sqrtf(A[j * nvs + j]);
+    float inv = 1.0f / ljj;
+    WSYNC();
+    if (lane < n) {
+      if (lane > j) A[lane * nvs + j] *= inv;
+      else if (lane == j) A[j * nvs + j] = ljj;
+    }
+    WSYNC();
+    if (lane > j && lane < n) {
+      float lij = A[lane * nvs + j];
+      for (int k = j + 1; k <= lane; k++) A[lane * nvs + k] -= lij * A[k * nvs + j];
+    }
+    WSYNC();
+  }
+  for (int e = lane; e < n * nvs; e += LPW) {
+    int r = e / nvs, c = e - r * nvs;
+    if (c > r) A[e] = 0.0f;
+  }
+  WSYNC();
+}
+
+// x = (L L^T)^-1 y ; y held per lane (lane = dof), result per lane
+__device__ float cholesky_solve(const float* Lm, int n, int nvs, int lane, float y) {
+  for (int j = 0; j < n; j++) {
+    float yj = __shfl(y, j, 64) / Lm[j * nvs + j];
+    if (lane == j) y = yj;
+    else if (lane > j && lane < n) y -= Lm[lane * nvs + j] * yj;
+  }
+  for (int k = n - 1; k >= 0; k--) {
+    float xk = __shfl(y, k, 64) / Lm[k * nvs + k];
+    if (lane == k) y = xk;
+    else if (lane < k) y -= Lm[k * nvs + lane] * xk;
+  }
+  return lane < n ? y : 0.0f;
+}
+
+// -------------------------------------------------------------------------------------------
+// collision (collision_driver.py / collision_core.py / collision_primitive_core.py)
+// -------------------------------------------------------------------------------------------
+struct Con2 {
+  float dist[2];
+  float pos[2][3];
+  float frame[2][9];
+  int n;
+};
+
+// collision_primitive_core.py:106-111
+__device__ __forceinline__ float plane_sphere(float* pos, const float* n, const float* ppos, const float* spos, float r) {
+  float dif[3] = {spos[0] - ppos[0], spos[1] - ppos[1], spos[2] - ppos[2]};
+  float dist = dot3(dif, n) - r;
+  for (int i = 0; i < 3; i++) pos[i] = spos[i] - n[i] * (r + 0.5f * dist);
+  return dist;
+}
+
+// collision_primitive_core.py:114-143
+__device__ __forceinline__ float sphere_sphere(float* pos, float* n, const float* p1, float r1, const float* p2, float r2) {
+  float dir[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  float dist = sqrtf(dot3(dir, dir));
+  if (dist == 0.0f) { n[0] = 1.0f; n[1] = 0.0f; n[2] = 0.0f; }
+  else { n[0] = dir[0] / dist; n[1] = dir[1] / dist; n[2] = dir[2] / dist; }
+  dist = dist - (r1 + r2);
+  for (int i = 0; i < 3; i++) pos[i] = p1[i] + n[i] * (r1 + 0.5f * dist);
+  return dist;
+}
+
+// math.py:268-273
+__device__ __forceinline__ void closest_segment_point(float* r, const float* a, const float* b, const float* pt) {
+  float ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, pa[3] = {pt[0] - a[0], pt[1] - a[1], pt[2] - a[2]};
+  float t = dot3(pa, ab) / (dot3(ab, ab) + 1e-6f);
+  t = clampf(t, 0.0f, 1.0f);
+  for (int i = 0; i < 3; i++) r[i] = a[i] + t * ab[i];
+}
+
+// collision_primitive_core.py:181-308
+__device__ void capsule_capsule(Con2& out, const float* p1, const float* ax1, float r1, float hl1, const float* p2,
+                                const float* ax2, float r2, float hl2, float margin) {
+  float a1[3], a2[3], dif[3];
+  for (int i = 0; i < 3; i++) { a1[i] = ax1[i] * hl1; a2[i] = ax2[i] * hl2; dif[i] = p1[i] - p2[i]; }
+  float ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+  float u = -dot3(a1, dif), v = dot3(a2, dif);
+  float det = ma * mc - mb * mb;
+  out.n = 0;
+  float v1[3], v2[3], pos[3], nrm[3];
+  if (fabsf(det) >= MJW_MINVAL) {
+    float inv = 1.0f / det;
+    float x1 = (mc * u - mb * v) * inv, x2 = (ma * v - mb * u) * inv;
+    if (x1 > 1.0f) { x1 = 1.0f; x2 = (v - mb) / mc; }
+    else if (x1 < -1.0f) { x1 = -1.0f; x2 = (v + mb) / mc; }
+    if (x2 > 1.0f) { x2 = 1.0f; x1 = clampf((u - mb) / ma, -1.0f, 1.0f); }
+    else if (x2 < -1.0f) { x2 = -1.0f; x1 = clampf((u + mb) / ma, -1.0f, 1.0f); }
+    for (int i = 0; i < 3; i++) { v1[i] = p1[i] + a1[i] * x1; v2[i] = p2[i] + a2[i] * x2; }
+    float dist = sphere_sphere(pos, nrm, v1, r1, v2, r2);
+    if (dist <= margin) {
+      out.dist[0] = dist;
+      for (int i = 0; i < 3; i++) out.pos[0][i] = pos[i];
+      make_frame(out.frame[0], nrm);
+      out.n = 1;
+    }
+    return;
+  }
+  int cnt = 0;
+  for (int t = 0; t < 4; t++) {
+    if (t >= 2 && cnt >= 2) break;
+    float x;
+    if (t == 0) { x = clampf((v - mb) / mc, -1.0f, 1.0f); for (int i = 0; i < 3; i++) { v1[i] = p1[i] + a1[i]; v2[i] = p2[i] + a2[i] * x; } }
+    else if (t == 1) { x = clampf((v + mb) / mc, -1.0f, 1.0f); for (int i = 0; i < 3; i++) { v1[i] = p1[i] - a1[i]; v2[i] = p2[i] + a2[i] * x; } }
+    else if (t == 2) { x = clampf((u - mb) / ma, -1.0f, 1.0f); for (int i = 0; i < 3; i++) { v2[i] = p2[i] + a2[i]; v1[i] = p1[i] + a1[i] * x; } }
+    else { x = clampf((u + mb) / ma, -1.0f, 1.0f); for (int i = 0; i < 3; i++) { v2[i] = p2[i] - a2[i]; v1[i] = p1[i] + a1[i] * x; } }
+    float dist = sphere_sphere(pos, nrm, v1, r1, v2, r2);
+    if (dist <= margin) {
+      out.dist[cnt] = dist;
+      for (int i = 0; i < 3; i++) out.pos[cnt][i] = pos[i];
+      make_frame(out.frame[cnt], nrm);
+      cnt++;
+    }
+  }
+  out.n = cnt;
+}
+
+// collision_primitive_core.py:311-361
+__device__ void plane_capsule(Con2& out, const float* n, const float* ppos, const float* cpos, const float* axis, float r, float hl) {
+  float nd = dot3(n, axis);
+  float tmp[3] = {axis[0] - n[0] * nd, axis[1] - n[1] * nd, axis[2] - n[2] * nd};
+  float bn = sqrtf(dot3(tmp, tmp));
+  float b[3];
+  if (bn == 0.0f) { b[0] = tmp[0]; b[1] = tmp[1]; b[2] = tmp[2]; }
+  else { b[0] = tmp[0] / bn; b[1] = tmp[1] / bn; b[2] = tmp[2] / bn; }
+  if (bn < 0.5f) {
+    if (-0.5f < n[1] && n[1] < 0.5f) { b[0] = 0.0f; b[1] = 1.0f; b[2] = 0.0f; }
+    else { b[0] = 0.0f; b[1] = 0.0f; b[2] = 1.0f; }
+  }
+  float c[3];
+  cross3(c, n, b);
+  float e1[3], e2[3];
+  for (int i = 0; i < 3; i++) { e1[i] = cpos[i] + axis[i] * hl; e2[i] = cpos[i] - axis[i] * hl; }
+  out.dist[0] = plane_sphere(out.pos[0], n, ppos, e1, r);
+  out.dist[1] = plane_sphere(out.pos[1], n, ppos, e2, r);
+  for (int k = 0; k < 2; k++) {
+    out.frame[k][0] = n[0]; out.frame[k][1] = n[1]; out.frame[k][2] = n[2];
+    out.frame[k][3] = b[0]; out.frame[k][4] = b[1]; out.frame[k][5] = b[2];
+    out.frame[k][6] = c[0]; out.frame[k][7] = c[1]; out.frame[k][8] = c[2];
+  }
+  out.n = 2;
+}
+
+// collision_driver.py:217-271
+__device__ bool obb_filter(const float* c1, const float* c2, const float* s1, const float* s2, float margin, const float* xp1,
+                           const float* xp2, const float* xm1, const float* xm2) {
+  float xc0[3], xc1[3];
+  matvec3(xc0, xm1, c1);
+  matvec3(xc1, xm2, c2);
+  for (int i = 0; i < 3; i++) { xc0[i] += xp1[i]; xc1[i] += xp2[i]; }
+  for (int j = 0; j < 2; j++) {
+    const float* xmj = j == 0 ? xm1 : xm2;
+    for (int k = 0; k < 3; k++) {
+      float nk[3] = {xmj[k], xmj[3 + k], xmj[6 + k]};
+      float proj0 = dot3(xc0, nk), proj1 = dot3(xc1, nk);
+      float rad[2];
+      for (int i = 0; i < 2; i++) {
+        const float* xmi = i == 0 ? xm1 : xm2;
+        const float* size = i == 0 ? s1 : s2;
+        float n0[3] = {xmi[0], xmi[3], xmi[6]}, n1[3] = {xmi[1], xmi[4], xmi[7]}, n2[3] = {xmi[2], xmi[5], xmi[8]};
+        rad[i] = fabsf(size[0] * dot3(n0, nk)) + fabsf(size[1] * dot3(n1, nk)) + fabsf(size[2] * dot3(n2, nk));
+      }
+      if (rad[0] + rad[1] + margin < fabsf(proj1 - proj0)) return false;
+    }
+  }
+  return true;
+}
+
+// collision_driver.py:116-213
+__device__ bool aabb_filter(const float* c1, const float* c2, const float* s1, const float* s2, float margin, const float* xp1,
+                            const float* xp2, const float* xm1, const float* xm2) {
+  float cen1[3], cen2[3];
+  matvec3(cen1, xm1, c1);
+  matvec3(cen2, xm2, c2);
+  for (int i = 0; i < 3; i++) { cen1[i] += xp1[i]; cen2[i] += xp2[i]; }
+  float mx1[3] = {-MJW_MAXVAL, -MJW_MAXVAL, -MJW_MAXVAL}, mn1[3] = {MJW_MAXVAL, MJW_MAXVAL, MJW_MAXVAL};
+  float mx2[3] = {-MJW_MAXVAL, -MJW_MAXVAL, -MJW_MAXVAL}, mn2[3] = {MJW_MAXVAL, MJW_MAXVAL, MJW_MAXVAL};
+  for (int c = 0; c < 8; c++) {
+    float sg0 = (c & 4) ? 1.0f : -1.0f, sg1 = (c & 2) ? 1.0f : -1.0f, sg2 = (c & 1) ? 1.0f : -1.0f;
+    float cr1[3] = {sg0 * s1[0], sg1 * s1[1], sg2 * s1[2]}, cr2[3] = {sg0 * s2[0], sg1 * s2[1], sg2 * s2[2]}, p1[3], p2[3];
+    matvec3(p1, xm1, cr1);
+    matvec3(p2, xm2, cr2);
+    for (int a = 0; a < 3; a++) {
+      mx1[a] = fmaxf(mx1[a], p1[a]); mn1[a] = fminf(mn1[a], p1[a]);
+      mx2[a] = fmaxf(mx2[a], p2[a]); mn2[a] = fminf(mn2[a], p2[a]);
+    }
+  }
+  for (int a = 0; a < 3; a++) {
+    if (cen1[a] + mx1[a] + margin < cen2[a] + mn2[a]) return false;
+    if (cen2[a] + mx2[a] + margin < cen1[a] + mn1[a]) return false;
+  }
+  return true;
+}
+
+// collision_driver.py:274-321
+__device__ bool broadphase_filter(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2) {
+  const float* geom_aabb = MR(geom_aabb);
+  const float* geom_rbound = MR(geom_rbound);
+  const float* geom_margin = MR(geom_margin);
+  float rb1 = geom_rbound[g1], rb2 = geom_rbound[g2];
+  float mg1 = geom_margin[g1], mg2 = geom_margin[g2];
+  const float* xp1 = s + L.gxpos + 3 * g1;
+  const float* xp2 = s + L.gxpos + 3 * g2;
+  const float* xm1 = s + L.gxmat + 9 * g1;
+  const float* xm2 = s + L.gxmat + 9 * g2;
+  int filt = m.opt_broadphase_filter;
+  if (rb1 == 0.0f || rb2 == 0.0f) {
+    if (filt & FILTER_PLANE) {
+      if (rb1 == 0.0f) {
+        float dif[3] = {xp2[0] - xp1[0], xp2[1] - xp1[1], xp2[2] - xp1[2]}, n[3] = {xm1[2], xm1[5], xm1[8]};
+        return dot3(dif, n) <= rb2 + mg1 + mg2;
+      } else {
+        float dif[3] = {xp1[0] - xp2[0], xp1[1] - xp2[1], xp1[2] - xp2[2]}, n[3] = {xm2[2], xm2[5], xm2[8]};
+        return dot3(dif, n) <= rb1 + mg1 + mg2;
+      }
+    }
+    return true;
+  }
+  if (filt & FILTER_SPHERE) {
+    float bound = rb1 + rb2 + mg1 + mg2;
+    float dif[3] = {xp2[0] - xp1[0], xp2[1] - xp1[1], xp2[2] - xp1[2]};
+    if (!(dot3(dif, dif) <= bound * bound)) return false;
+  }
+  if (filt & FILTER_AABB)
+    if (!aabb_filter(geom_aabb + 6 * g1, geom_aabb + 6 * g2, geom_aabb + 6 * g1 + 3, geom_aabb + 6 * g2 + 3, mg1 + mg2, xp1, xp2, xm1, xm2))
+      return false;
+  if (filt & FILTER_OBB)
+    if (!obb_filter(geom_aabb + 6 * g1, geom_aabb + 6 * g2, geom_aabb + 6 * g1 + 3, geom_aabb + 6 * g2 + 3, mg1 + mg2, xp1, xp2, xm1, xm2))
+      return false;
+  return true;
+}
+
+// narrowphase of one pair (collision_primitive.py:280-662); pair is type-sorted on the host
+__device__ void narrowphase(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2, float margin, Con2& c) {
+  const float* geom_size = MR(geom_size);
+  int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  const float* p1 = s + L.gxpos + 3 * g1;
+  const float* p2 = s + L.gxpos + 3 * g2;
+  const float* r1 = s + L.gxmat + 9 * g1;
+  const float* r2 = s + L.gxmat + 9 * g2;
+  const float* s1 = geom_size + 3 * g1;
+  const float* s2 = geom_size + 3 * g2;
+  float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
+  c.n = 0;
+  if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) {
+    c.dist[0] = plane_sphere(c.pos[0], n1, p1, p2, s2[0]);
+    make_frame(c.frame[0], n1);
+    c.n = 1;
+  } else if (t1 == GEOM_PLANE && t2 == GEOM_CAPSULE) {
+    plane_capsule(c, n1, p1, p2, n2, s2[0], s2[1]);
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
+    float nrm[3];
+    c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], p2, s2[0]);
+    make_frame(c.frame[0], nrm);
+    c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
+    float a[3], b[3], pt[3], nrm[3];
+    for (int i = 0; i < 3; i++) { a[i] = p2[i] - n2[i] * s2[1]; b[i] = p2[i] + n2[i] * s2[1]; }
+    closest_segment_point(pt, a, b, p1);
+    c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], pt, s2[0]);
+    make_frame(c.frame[0], nrm);
+    c.n = 1;
+  } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
+    capsule_capsule(c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], margin);
+  }
+}
+
+// collision_core.py:235-341 (geom mixing; explicit <pair> entries are not produced by this build's compiler)
+__device__ void contact_params(const mjw_model_t& m, int wid, int g1, int g2, float* margin, float* gap, int* condim,
+                               float* friction, float* solref, float* solimp) {
+  const float* geom_solmix = MR(geom_solmix);
+  const float* geom_friction = MR(geom_friction);
+  const float* geom_solref = MR(geom_solref);
+  const float* geom_solimp = MR(geom_solimp);
+  const float* geom_margin = MR(geom_margin);
+  const float* geom_gap = MR(geom_gap);
+  float s1 = geom_solmix[g1], s2 = geom_solmix[g2];
+  int c1 = m.geom_condim[g1], c2 = m.geom_condim[g2];
+  int p1 = m.geom_priority[g1], p2 = m.geom_priority[g2];
+  float mix, fr[3];
+  if (p1 > p2) { mix = 1.0f; *condim = c1; for (int i = 0; i < 3; i++) fr[i] = geom_friction[3 * g1 + i]; }
+  else if (p2 > p1) { mix = 0.0f; *condim = c2; for (int i = 0; i < 3; i++) fr[i] = geom_friction[3 * g2 + i]; }
+  else {
+    mix = safe_div(s1, s1 + s2);
+    if (s1 < MJW_MINVAL && s2 < MJW_MINVAL) mix = 0.5f;
+    else if (s1 < MJW_MINVAL && s2 >= MJW_MINVAL) mix = 0.0f;
+    else if (s1 >= MJW_MINVAL && s2 < MJW_MINVAL) mix = 1.0f;
+    *condim = c1 > c2 ? c1 : c2;
+    for (int i = 0; i < 3; i++) fr[i] = fmaxf(geom_friction[3 * g1 + i], geom_friction[3 * g2 + i]);
+  }
+  friction[0] = fr[0]; friction[1] = fr[0]; friction[2] = fr[1]; friction[3] = fr[2]; friction[4] = fr[2];
+  const float* sr1 = geom_solref + 2 * g1;
+  const float* sr2 = geom_solref + 2 * g2;
+  if (sr1[0] > 0.0f && sr2[0] > 0.0f) {
+    for (int i = 0; i < 2; i++) solref[i] = mix * sr1[i] + (1.0f - mix) * sr2[i];
+  } else {
+    for (int i = 0; i < 2; i++) solref[i] = fminf(sr1[i], sr2[i]);
+  }
+  for (int i = 0; i < 5; i++) solimp[i] = mix * geom_solimp[5 * g1 + i] + (1.0f - mix) * geom_solimp[5 * g2 + i];
+  *margin = geom_margin[g1] + geom_margin[g2];
+  *gap = geom_gap[g1] + geom_gap[g2];
+  for (int i = 0; i < 5; i++) friction[i] = fmaxf(MJW_MINMU, friction[i]);
+}
+
+// -------------------------------------------------------------------------------------------
+// constraint.py
+// -------------------------------------------------------------------------------------------
+// constraint.py:52-121 (writes LDS row scalars)
+__device__ void efc_row(const mjw_model_t& m, const Lay& L, float* s, int wid, int r, float pos_aref, float pos_imp,
+                        float invweight, const float* solref, const float* solimp, float margin, float vel, float frictionloss,
+                        int type, int id) {
+  float timestep = MR(opt_timestep)[0];
+  float timeconst = solref[0], dampratio = solref[1];
+  float dmin = solimp[0], dmax = solimp[1], width = solimp[2], mid = solimp[3], power = solimp[4];
+  if (!(m.opt_disableflags & DSBL_REFSAFE)) timeconst = fmaxf(timeconst, 2.0f * timestep);
+  dmin = clampf(dmin, MJW_MINIMP, MJW_MAXIMP);
+  dmax = clampf(dmax, MJW_MINIMP, MJW_MAXIMP);
+  width = fmaxf(MJW_MINVAL, width);
+  mid = clampf(mid, MJW_MINIMP, MJW_MAXIMP);
+  power = fmaxf(1.0f, power);
+  float dmax_sq = dmax * dmax;
+  float k = 1.0f / (dmax_sq * timeconst * timeconst * dampratio * dampratio);
+  float b = 2.0f / (dmax * timeconst);
+  if (solref[0] <= 0.0f) k = -solref[0] / dmax_sq;
+  if (solref[1] <= 0.0f) b = -solref[1] / dmax;
+  float imp_x = fabsf(pos_imp) / width;
+  float imp_a = (1.0f / powf(mid, power - 1.0f)) * powf(imp_x, power);
+  float imp_b = 1.0f - (1.0f / powf(1.0f - mid, power - 1.0f)) * powf(1.0f - imp_x, power);
+  float imp_y = imp_x < mid ? imp_a : imp_b;
+  float imp = dmin + imp_y * (dmax - dmin);
+  imp = clampf(imp, dmin, dmax);
+  if (imp_x > 1.0f) imp = dmax;
+  s[L.efc_D + r] = 1.0f / fmaxf(invweight * (1.0f - imp) / imp, MJW_MINVAL);
+  s[L.efc_vel + r] = vel;
+  s[L.efc_aref + r] = -k * imp * pos_aref - b * vel;
+  s[L.efc_pos + r] = pos_aref + margin;
+  s[L.efc_margin + r] = margin;
+  s[L.efc_frictionloss + r] = frictionloss;
+  int* si = reinterpret_cast<int*>(s);
+  si[L.efc_type + r] = type;
+  si[L.efc_id + r] = id;
+}
+
+// support.py:396-432 restricted to one dof; returns jacp, jacr (zero when not in tree)
+__device__ __forceinline__ void jac_dof(const mjw_model_t& m, const Lay& L, const float* s, const float* point, int bodyid,
+                                        int dofid, float* jacp, float* jacr) {
+  int db = m.dof_bodyid[dofid];
+  bool in_tree = db == 0;
+  int p = bodyid;
+  while (p != 0) {
+    if (p == db) { in_tree = true; break; }
+    p = m.body_parentid[p];
+  }
+  if (!in_tree) { jacp[0] = jacp[1] = jacp[2] = jacr[0] = jacr[1] = jacr[2] = 0.0f; return; }
+  int root = m.body_rootid[bodyid];
+  float off[3];
+  for (int i = 0; i < 3; i++) off[i] = point[i] - s[L.subtree_com + 3 * root + i];
+  const float* cd = s + L.cdof + 6 * dofid;
+  float c[3];
+  cross3(c, cd, off);
+  for (int i = 0; i < 3; i++) { jacp[i] = cd[3 + i] + c[i]; jacr[i] = cd[i]; }
+}
+
+// collision_driver.py:754-789 + constraint.py:2209-2779 (friction-dof, limits, pyramidal contacts)
+__device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  int* si = w.si;
+  const int nv = m.nv, nvs = L.nvs, njmax = d.njmax;
+  const float* qvel = s + L.qvel;
+  int nefc = 0, nf = 0, nl = 0;
+  const bool dsbl_constraint = m.opt_disableflags & DSBL_CONSTRAINT;
+
+  // --- friction dof rows (constraint.py:1113-1190)
+  if (!dsbl_constraint && !(m.opt_disableflags & DSBL_FRICTIONLOSS)) {
+    const float* dof_frictionloss = MR(dof_frictionloss);
+    const float* dof_invweight0 = MR(dof_invweight0);
+    const float* dof_solref = MR(dof_solref);
+    const float* dof_solimp = MR(dof_solimp);
+    for (int base = 0; base < nv; base += LPW) {
+      int i = base + lane;
+      bool act = i < nv && dof_frictionloss[i] > 0.0f;
+      unsigned long long bal = __ballot(act);
+      int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
+      int r = nefc + rank;
+      if (act && r < njmax) {
+        for (int k = 0; k < nv; k++) s[L.J + r * nvs + k] = (k == i) ? 1.0f : 0.0f;
+        efc_row(m, L, s, wid, r, 0.0f, 0.0f, dof_invweight0[i], dof_solref + 2 * i, dof_solimp + 5 * i, 0.0f, qvel[i],
+                dof_frictionloss[i], CNSTR_FRICTION_DOF, i);
+      }
+      int cnt = __popcll(bal);
+      nefc += cnt;
+      nf += cnt;
+    }
+  }
+  // --- joint limits (constraint.py:1316-1418)
+  if (!dsbl_constraint && !(m.opt_disableflags & DSBL_LIMIT)) {
+    const float* jnt_range = MR(jnt_range);
+    const float* jnt_margin = MR(jnt_margin);
+    const float* jnt_solref = MR(jnt_solref);
+    const float* jnt_solimp = MR(jnt_solimp);
+    const float* dof_invweight0 = MR(dof_invweight0);
+    for (int base = 0; base < m.nlimited; base += LPW) {
+      int idx = base + lane;
+      bool act = false;
+      int j = 0;
+      float pos = 0.0f, dmn = 0.0f, dmx = 0.0f, jm = 0.0f;
+      if (idx < m.nlimited) {
+        j = m.jnt_limited_slide_hinge_adr[idx];
+        float q = s[L.qpos + m.jnt_qposadr[j]];
+        dmn = q - jnt_range[2 * j];
+        dmx = jnt_range[2 * j + 1] - q;
+        jm = jnt_margin[j];
+        pos = fminf(dmn, dmx) - jm;
+        act = pos < 0.0f;
+      }
+      unsigned long long bal = __ballot(act);
+      int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
+      int r = nefc + rank;
+      if (act && r < njmax) {
+        int da = m.jnt_dofadr[j];
+        float Jv = (float)(dmn < dmx) * 2.0f - 1.0f;
+        for (int k = 0; k < nv; k++) s[L.J + r * nvs + k] = (k == da) ? Jv : 0.0f;
+        efc_row(m, L, s, wid, r, pos, pos, dof_invweight0[da], jnt_solref + 2 * j, jnt_solimp + 5 * j, jm, Jv * qvel[da], 0.0f,
+                CNSTR_LIMIT_JOINT, j);
+      }
+      int cnt = __popcll(bal);
+      nefc += cnt;
+      nl += cnt;
+    }
+  }
+
+  // --- collision + contact rows (collision_driver.py:697-789, constraint.py:1668-1936)
+  int ncon_total = 0;
+  const bool do_contact = d.naconmax > 0 && !(m.opt_disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT));
+  if (do_contact) {
+    const float* body_invweight0 = MR(body_invweight0);
+    const float impratio_invsqrt = MR(opt_impratio_invsqrt)[0];
+    int ncollision = 0;
+    int round = 0;
+    while (true) {
+      const int rbeg = round * CMAX, rend = rbeg + CMAX;
+      int running = 0;  // contacts found so far (world-local, in pair order)
+      for (int base = 0; base < m.nxn; base += LPW) {
+        int p = base + lane;
+        Con2 c;
+        c.n = 0;
+        bool pass = false;
+        int g1 = 0, g2 = 0;
+        float margin = 0.0f, gap = 0.0f, friction[5], solref[2], solimp[5];
+        int condim = 0;
+        if (p < m.nxn) {
+          g1 = m.nxn_geom_pair[2 * p];
+          g2 = m.nxn_geom_pair[2 * p + 1];
+          int pairid1 = m.nxn_pairid[2 * p + 1];
+          pass = broadphase_filter(m, L, s, wid, g1, g2) || pairid1 >= 0;
+          if (pass) {
+            contact_params(m, wid, g1, g2, &margin, &gap, &condim, friction, solref, solimp);
+            narrowphase(m, L, s, wid, g1, g2, margin, c);
+          }
+        }
+        if (round == 0) ncollision += __popcll(__ballot(pass));
+        // active contacts (write_contact collision_core.py:199-213)
+        int pairid0 = p < m.nxn ? m.nxn_pairid[2 * p] : -2;
+        bool a0 = c.n > 0 && c.dist[0] < margin && pairid0 >= -1;
+        bool a1 = c.n > 1 && c.dist[1] < margin && pairid0 >= -1;
+        int cnt = (int)a0 + (int)a1;
+        int incl = wave_scan_incl(cnt);
+        int first = running + incl - cnt;
+        int k = 0;
+        for (int sub = 0; sub < 2; sub++) {
+          bool a = sub == 0 ? a0 : a1;
+          if (!a) continue;
+          int idx = first + k;
+          k++;
+          if (idx >= rbeg && idx < rend) {
+            float* rec = s + L.con + (idx - rbeg) * CREC;
+            rec[0] = c.dist[sub];
+            rec[1] = margin - gap;
+            for (int i = 0; i < 3; i++) rec[2 + i] = c.pos[sub][i];
+            for (int i = 0; i < 9; i++) rec[5 + i] = c.frame[sub][i];
+            for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
+            rec[19] = solref[0]; rec[20] = solref[1];
+            rec[21] = 0.0f; rec[22] = 0.0f;
+            for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
+            int* reci = reinterpret_cast<int*>(rec);
+            reci[28] = condim;
+            reci[29] = g1;
+            reci[30] = g2;
+          }
+        }
+        running += __shfl(incl, 63, 64);
+      }
+      ncon_total = running;
+      if (round == 0 && lane == 0) atomicAdd(d.ncollision, ncollision);
+      int nstage = min(CMAX, running - rbeg);
+      if (nstage <= 0) break;
+      // global pool slot for this round (one atomic per world per round)
+      int gbase = 0;
+      if (lane == 0) gbase = atomicAdd(d.nacon, nstage);
+      gbase = __shfl(gbase, 0, 64);
+      WSYNC();
+      // rows per staged contact (pyramidal: 1 or 2*(condim-1)), prefix over contacts
+      int nrow = 0;
+      if (lane < nstage) {
+        const float* rec = s + L.con + lane * CREC;
+        int condim = reinterpret_cast<const int*>(rec)[28];
+        float pos = rec[0] - rec[1];
+        nrow = pos < 0.0f ? (condim == 1 ? 1 : 2 * (condim - 1)) : 0;
+        reinterpret_cast<int*>(s + L.con + lane * CREC)[31] = gbase + lane;
+      }
+      int rincl = wave_scan_incl(nrow);
+      int rfirst = nefc + rincl - nrow;
+      if (lane < nstage) si[L.iscratch + lane] = rfirst;
+      int nrow_total = __shfl(rincl, 63, 64);
+      WSYNC();
+      // write contacts to the global pool (collision_core.py:213-231)
+      if (lane < nstage) {
+        const float* rec = s + L.con + lane * CREC;
+        const int* reci = reinterpret_cast<const int*>(rec);
+        int cid = gbase + lane;
+        if (cid < d.naconmax) {
+          d.contact_dist[cid] = rec[0];
+          for (int i = 0; i < 3; i++) d.contact_pos[3L * cid + i] = rec[2 + i];
+          for (int i = 0; i < 9; i++) d.contact_frame[9L * cid + i] = rec[5 + i];
+          d.contact_includemargin[cid] = rec[1];
+          for (int i = 0; i < 5; i++) d.contact_friction[5L * cid + i] = rec[14 + i];
+          for (int i = 0; i < 2; i++) { d.contact_solref[2L * cid + i] = rec[19 + i]; d.contact_solreffriction[2L * cid + i] = 0.0f; }
+          for (int i = 0; i < 5; i++) d.contact_solimp[5L * cid + i] = rec[23 + i];
+          d.contact_dim[cid] = reci[28];
+          d.contact_geom[2L * cid] = reci[29];
+          d.contact_geom[2L * cid + 1] = reci[30];
+          d.contact_worldid[cid] = wid;
+          d.contact_type[cid] = 1;
+          d.contact_geomcollisionid[cid] = 0;
+          int npr = nrow;
+          for (int i = 0; i < m.nmaxpyramid; i++) {
+            int r = rfirst + i;
+            d.contact_efc_address[(long)cid * m.nmaxpyramid + i] = (i < npr && r < njmax) ? r : -1;
+          }
+        }
+      }
+      // J entries: lane = dof, loop over staged contacts
+      for (int cc = 0; cc < nstage; cc++) {
+        const float* rec = s + L.con + cc * CREC;
+        const int* reci = reinterpret_cast<const int*>(rec);
+        int condim = reci[28];
+        int r0 = si[L.iscratch + cc];
+        float pos = rec[0] - rec[1];
+        if (!(pos < 0.0f)) continue;
+        int nr = condim == 1 ? 1 : 2 * (condim - 1);
+        int b1 = m.body_weldid[m.geom_bodyid[reci[29]]];
+        int b2 = m.body_weldid[m.geom_bodyid[reci[30]]];
+        const float* cpos = rec + 2;
+        const float* frame = rec + 5;
+        for (int i = lane; i < nv; i += LPW) {
+          float j1p[3], j1r[3], j2p[3], j2r[3];
+          jac_dof(m, L, s, cpos, b1, i, j1p, j1r);
+          jac_dof(m, L, s, cpos, b2, i, j2p, j2r);
+          float jdp[3] = {j2p[0] - j1p[0], j2p[1] - j1p[1], j2p[2] - j1p[2]};
+          float jdr[3] = {j2r[0] - j1r[0], j2r[1] - j1r[1], j2r[2] - j1r[2]};
+          float Jn = frame[0] * jdp[0] + frame[1] * jdp[1] + frame[2] * jdp[2];
+          for (int dimid = 0; dimid < nr; dimid++) {
+            int r = r0 + dimid;
+            if (r >= njmax) break;
+            float Jval = Jn;
+            if (condim > 1) {
+              int dimid2 = dimid / 2 + 1;
+              float frii = rec[14 + dimid2 - 1];
+              float Ji;
+              if (dimid2 < 3) Ji = frame[3 * dimid2] * jdp[0] + frame[3 * dimid2 + 1] * jdp[1] + frame[3 * dimid2 + 2] * jdp[2];
+              else Ji = frame[3 * (dimid2 - 3)] * jdr[0] + frame[3 * (dimid2 - 3) + 1] * jdr[1] + frame[3 * (dimid2 - 3) + 2] * jdr[2];
+              Jval = (dimid % 2 == 0) ? Jval + Ji * frii : Jval - Ji * frii;
+            }
+            s[L.J + r * nvs + i] = Jval;
+          }
+        }
+      }
+      WSYNC();
+      // row scalars: lane = contact row (constraint.py:1776-1936)
+      for (int rr = lane; rr < nrow_total; rr += LPW) {
+        int r = nefc + rr;
+        if (r >= njmax) continue;
+        // find owning staged contact (rows are contiguous per contact)
+        int cc = 0;
+        while (cc + 1 < nstage && si[L.iscratch + cc + 1] <= r) cc++;
+        const float* rec = s + L.con + cc * CREC;
+        const int* reci = reinterpret_cast<const int*>(rec);
+        int condim = reci[28];
+        int dimid = r - si[L.iscratch + cc];
+        int g1 = reci[29], g2 = reci[30];
+        int body1 = m.geom_bodyid[g1], body2 = m.geom_bodyid[g2];
+        float invweight = body_invweight0[2 * body1] + body_invweight0[2 * body2];
+        if (condim > 1) {
+          float fri0 = rec[14];
+          invweight = invweight + fri0 * fri0 * invweight;
+          invweight = invweight * 2.0f * fri0 * fri0 * impratio_invsqrt * impratio_invsqrt;
+        }
+        float Jqvel = 0.0f;
+        for (int k = nv - 1; k >= 0; k--) Jqvel += s[L.J + r * nvs + k] * qvel[k];
+        float pos = rec[0] - rec[1];
+        int type = condim == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
+        efc_row(m, L, s, wid, r, pos, pos, invweight, rec + 19, rec + 23, rec[1], Jqvel, 0.0f, type, reci[31]);
+        (void)dimid;
+      }
+      nefc += nrow_total;
+      WSYNC();
+      if (running <= rend) break;
+      round++;
+    }
+  }
+  (void)ncon_total;
+  WSYNC();
+  // write rows to global (efc arrays are (nworld, njmax[_pad]))
+  const int nrows = min(nefc, njmax);
+  const int np = m.nv_pad;
+  float* gJ = d.efc_J + (long)wid * d.njmax_pad * np;
+  for (int e = lane; e < nrows * np; e += LPW) {
+    int r = e / np, c = e - r * np;
+    gJ[e] = c < nv ? s[L.J + r * nvs + c] : 0.0f;
+  }
+  for (int r = lane; r < nrows; r += LPW) {
+    long gr = (long)wid * njmax + r;
+    d.efc_pos[gr] = s[L.efc_pos + r];
+    d.efc_margin[gr] = s[L.efc_margin + r];
+    d.efc_D[(long)wid * d.njmax_pad + r] = s[L.efc_D + r];
+    d.efc_vel[gr] = s[L.efc_vel + r];
+    d.efc_aref[gr] = s[L.efc_aref + r];
+    d.efc_frictionloss[gr] = s[L.efc_frictionloss + r];
+    d.efc_type[gr] = si[L.efc_type + r];
+    d.efc_id[gr] = si[L.efc_id + r];
+  }
+  if (lane == 0) {
+    d.ne[wid] = 0;
+    d.nf[wid] = nf;
+    d.nl[wid] = nl;
+    d.nefc[wid] = nefc;
+    si[L.iscratch + 60] = 0;
+    si[L.iscratch + 61] = nf;
+    si[L.iscratch + 62] = nefc;
+  }
+  WSYNC();
+}
+
+// smooth.py:2041-2147 (joint transmissions; moment rows packed in actuator order)
+__device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  int* si = w.si;
+  const float* gear_all = MR(actuator_gear);
+  for (int a = lane; a < m.nu; a += LPW) {
+    // rowadr = sum of previous actuators' nnz (deterministic order)
+    int rowadr = 0;
+    for (int a2 = 0; a2 < a; a2++) {
+      int jt2 = m.jnt_type[m.actuator_trnid[2 * a2]];
+      rowadr += jt2 == JNT_FREE ? 6 : (jt2 == JNT_BALL ? 3 : 1);
+    }
+    const float* gear = gear_all + 6 * a;
+    int trn = m.actuator_trntype[a];
+    int j = m.actuator_trnid[2 * a];
+    int jt = m.jnt_type[j], qa = m.jnt_qposadr[j], va = m.jnt_dofadr[j];
+    const float* qpos = s + L.qpos;
+    float mom[6] = {0, 0, 0, 0, 0, 0};
+    int nnz;
+    float length;
+    if (jt == JNT_FREE) {
+      nnz = 6;
+      length = 0.0f;
+      if (trn == 1) {
+        float q[4] = {qpos[qa + 3], qpos[qa + 4], qpos[qa + 5], qpos[qa + 6]}, qn[4], ga[3];
+        normalize4(q);
+        qn[0] = q[0]; qn[1] = -q[1]; qn[2] = -q[2]; qn[3] = -q[3];
+        rot_vec_quat(ga, gear + 3, qn);
+        for (int i = 0; i < 3; i++) { mom[i] = gear[i]; mom[3 + i] = ga[i]; }
+      } else {
+        for (int i = 0; i < 6; i++) mom[i] = gear[i];
+      }
+    } else if (jt == JNT_BALL) {
+      nnz = 3;
+      float q[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]}, aa[3];
+      normalize4(q);
+      quat_to_vel(aa, q);
+      float ga[3] = {gear[0], gear[1], gear[2]};
+      if (trn == 1) {
+        float qn[4] = {q[0], -q[1], -q[2], -q[3]};
+        rot_vec_quat(ga, ga, qn);
+      }
+      length = dot3(aa, ga);
+      for (int i = 0; i < 3; i++) mom[i] = ga[i];
+    } else {
+      nnz = 1;
+      length = qpos[qa] * gear[0];
+      mom[0] = gear[0];
+    }
+    s[L.act_len + a] = length;
+    si[L.act_nnz + a] = nnz;
+    long gu = (long)wid * m.nu + a;
+    d.actuator_length[gu] = length;
+    d.moment_rownnz[gu] = nnz;
+    d.moment_rowadr[gu] = rowadr;
+    for (int k = 0; k < 6; k++) {
+      s[L.act_mom + 6 * a + k] = k < nnz ? mom[k] : 0.0f;
+      si[L.act_momdof + 6 * a + k] = k < nnz ? va + k : 0;
+    }
+    for (int k = 0; k < nnz; k++) {
+      d.actuator_moment[(long)wid * m.nJmom + rowadr + k] = mom[k];
+      d.moment_colind[(long)wid * m.nJmom + rowadr + k] = va + k;
+    }
+  }
+  WSYNC();
+}
+
+// -------------------------------------------------------------------------------------------
+// velocity (forward.py:592-613): actuator velocity, com_vel, passive, rne
+// -------------------------------------------------------------------------------------------
+__device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  int* si = w.si;
+  const float* qvel = s + L.qvel;
+  const float* qpos = s + L.qpos;
+  const int nv = m.nv;
+  // forward.py:540-562
+  for (int a = lane; a < m.nu; a += LPW) {
+    float v = 0.0f;
+    for (int k = 0; k < si[L.act_nnz + a]; k++) v += s[L.act_mom + 6 * a + k] * qvel[si[L.act_momdof + 6 * a + k]];
+    s[L.act_vel + a] = v;
+    d.actuator_velocity[(long)wid * m.nu + a] = v;
+  }
+  // smooth.py:1935-2038 com_vel, level by level
+  float* cvel = s + L.cvel;
+  float* cdof_dot = s + L.cdof_dot;
+  for (int e = lane; e < 6; e += LPW) cvel[e] = 0.0f;
+  for (int e = lane; e < nv * 6; e += LPW) cdof_dot[e] = 0.0f;
+  WSYNC();
+  for (int lvl = 1; lvl < m.nlevel; lvl++) {
+    int beg = m.level_adr[lvl], end = m.level_adr[lvl + 1];
+    for (int idx = beg + lane; idx < end; idx += LPW) {
+      int b = m.level_body[idx];
+      int p = m.body_parentid[b];
+      float cv[6];
+      for (int i = 0; i < 6; i++) cv[i] = cvel[6 * p + i];
+      int dofid = m.body_dofadr[b];
+      for (int j = m.body_jntadr[b]; j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
+        int jt = m.jnt_type[j];
+        const float* cd = s + L.cdof;
+        if (jt == JNT_FREE) {
+          for (int k = 0; k < 3; k++)
+            for (int i = 0; i < 6; i++) cv[i] += cd[6 * (dofid + k) + i] * qvel[dofid + k];
+          for (int k = 3; k < 6; k++) motion_cross(cdof_dot + 6 * (dofid + k), cv, cd + 6 * (dofid + k));
+          for (int k = 3; k < 6; k++)
+            for (int i = 0; i < 6; i++) cv[i] += cd[6 * (dofid + k) + i] * qvel[dofid + k];
+          dofid += 6;
+        } else if (jt == JNT_BALL) {
+          for (int k = 0; k < 3; k++) motion_cross(cdof_dot + 6 * (dofid + k), cv, cd + 6 * (dofid + k));
+          for (int k = 0; k < 3; k++)
+            for (int i = 0; i < 6; i++) cv[i] += cd[6 * (dofid + k) + i] * qvel[dofid + k];
+          dofid += 3;
+        } else {
+          motion_cross(cdof_dot + 6 * dofid, cv, cd + 6 * dofid);
+          for (int i = 0; i < 6; i++) cv[i] += cd[6 * dofid + i] * qvel[dofid];
+          dofid += 1;
+        }
+      }
+      for (int i = 0; i < 6; i++) cvel[6 * b + i] = cv[i];
+    }
+    WSYNC();
+  }
+  for (int e = lane; e < m.nbody * 6; e += LPW) d.cvel[(long)wid * m.nbody * 6 + e] = cvel[e];
+  for (int e = lane; e < nv * 6; e += LPW) d.cdof_dot[(long)wid * nv * 6 + e] = cdof_dot[e];
+  // passive.py:70-179, 535-563
+  const int dsbl_spring = m.opt_disableflags & DSBL_SPRING, dsbl_damper = m.opt_disableflags & DSBL_DAMPER;
+  float* qfrc_passive = s + L.qfrc_passive;
+  float* spring = s + L.vec;
+  float* damper = s + L.vec + nv;
+  for (int i = lane; i < nv; i += LPW) { spring[i] = 0.0f; damper[i] = 0.0f; }
+  WSYNC();
+  if (!(dsbl_spring && dsbl_damper)) {
+    const float* jnt_stiffness = MR(jnt_stiffness);
+    const float* dof_damping = MR(dof_damping);
+    const float* qpos_spring = MR(qpos_spring);
+    for (int j = lane; j < m.njnt; j += LPW) {
+      int da = m.jnt_dofadr[j], qa = m.jnt_qposadr[j], jt = m.jnt_type[j];
+      float stiff = jnt_stiffness[j], damp = dof_damping[da];
+      bool hs = stiff != 0.0f && !dsbl_spring, hd = damp != 0.0f && !dsbl_damper;
+      if (jt == JNT_FREE) {
+        if (hs) {
+          for (int i = 0; i < 3; i++) spring[da + i] = -stiff * (qpos[qa + i] - qpos_spring[qa + i]);
+          float rot[4] = {qpos[qa + 3], qpos[qa + 4], qpos[qa + 5], qpos[qa + 6]}, dif[3];
+          normalize4(rot);
+          quat_sub(dif, rot, qpos_spring + qa + 3);
+          for (int i = 0; i < 3; i++) spring[da + 3 + i] = -stiff * dif[i];
+        }
+        if (hd)
+          for (int i = 0; i < 6; i++) damper[da + i] = -damp * qvel[da + i];
+      } else if (jt == JNT_BALL) {
+        if (hs) {
+          float rot[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]}, dif[3];
+          normalize4(rot);
+          quat_sub(dif, rot, qpos_spring + qa);
+          for (int i = 0; i < 3; i++) spring[da + i] = -stiff * dif[i];
+        }
+        if (hd)
+          for (int i = 0; i < 3; i++) damper[da + i] = -damp * qvel[da + i];
+      } else {
+        if (hs) spring[da] = -stiff * (qpos[qa] - qpos_spring[qa]);
+        if (hd) damper[da] = -damp * qvel[da];
+      }
+    }
+  }
+  WSYNC();
+  for (int i = lane; i < nv; i += LPW) {
+    float p = spring[i] + damper[i];
+    qfrc_passive[i] = p;
+    long gi = (long)wid * nv + i;
+    d.qfrc_spring[gi] = spring[i];
+    d.qfrc_damper[gi] = damper[i];
+    d.qfrc_gravcomp[gi] = 0.0f;
+    d.qfrc_passive[gi] = p;
+  }
+  // rne (smooth.py:1112-1274, flg_acc = False)
+  float* cacc = s + L.cacc;
+  if (lane < 6) {
+    const float* grav = MR(opt_gravity);
+    cacc[lane] = (lane >= 3 && !(m.opt_disableflags & DSBL_GRAVITY)) ? -grav[lane - 3] : 0.0f;
+  }
+  WSYNC();
+  for (int lvl = 1; lvl < m.nlevel; lvl++) {
+    int beg = m.level_adr[lvl], end = m.level_adr[lvl + 1];
+    for (int idx = beg + lane; idx < end; idx += LPW) {
+      int b = m.level_body[idx];
+      int p = m.body_parentid[b];
+      float acc[6];
+      for (int i = 0; i < 6; i++) acc[i] = cacc[6 * p + i];
+      for (int k = 0; k < m.body_dofnum[b]; k++) {
+        int dof = m.body_dofadr[b] + k;
+        for (int i = 0; i < 6; i++) acc[i] += cdof_dot[6 * dof + i] * qvel[dof];
+      }
+      for (int i = 0; i < 6; i++) cacc[6 * b + i] = acc[i];
+    }
+    WSYNC();
+  }
+  float* cfrc = s + L.cfrc;
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float f[6] = {0, 0, 0, 0, 0, 0};
+    if (b > 0) {
+      float f1[6], iv[6], f2[6];
+      inert_vec(f1, s + L.cinert + 10 * b, cacc + 6 * b);
+      inert_vec(iv, s + L.cinert + 10 * b, cvel + 6 * b);
+      motion_cross_force(f2, cvel + 6 * b, iv);
+      for (int i = 0; i < 6; i++) f[i] = f1[i] + f2[i];
+    }
+    for (int i = 0; i < 6; i++) cfrc[6 * b + i] = f[i];
+  }
+  WSYNC();
+  // backward accumulation = subtree sums; keep result in cvel-sized scratch (cfrc_int)
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+    int end = m.body_subtree_end[b];
+    for (int j = (b == 0 ? 1 : b); j < end; j++)
+      for (int i = 0; i < 6; i++) acc[i] += cfrc[6 * j + i];
+    long gb = (long)wid * m.nbody + b;
+    for (int i = 0; i < 6; i++) { d.cfrc_int[gb * 6 + i] = acc[i]; d.cacc[gb * 6 + i] = cacc[6 * b + i]; }
+    // store back into cacc slot? no: qfrc_bias needs cfrc_int of dof bodies -> reuse cdof_dot-free scratch below
+    for (int i = 0; i < 6; i++) s[L.cvel + 6 * b + i] = acc[i];  // cvel no longer needed after this point
+  }
+  WSYNC();
+  for (int i = lane; i < nv; i += LPW) {
+    int b = m.dof_bodyid[i];
+    const float* cd = s + L.cdof + 6 * i;
+    const float* ci = s + L.cvel + 6 * b;
+    float v = cd[0] * ci[0] + cd[1] * ci[1] + cd[2] * ci[2] + cd[3] * ci[3] + cd[4] * ci[4] + cd[5] * ci[5];
+    s[L.qfrc_bias + i] = v;
+    d.qfrc_bias[(long)wid * nv + i] = v;
+  }
+  WSYNC();
+}
+
+// forward.py:616-927 (actuator force, qfrc_actuator)
+__device__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  int* si = w.si;
+  const int nv = m.nv;
+  float* qfrc_act = s + L.qfrc_actuator;
+  if (!m.nu || (m.opt_disableflags & DSBL_ACTUATION)) {
+    for (int i = lane; i < nv; i += LPW) { qfrc_act[i] = 0.0f; d.qfrc_actuator[(long)wid * nv + i] = 0.0f; }
+    for (int a = lane; a < m.na; a += LPW) d.act_dot[(long)wid * m.na + a] = 0.0f;
+    WSYNC();
+    return;
+  }
+  const float* ctrlrange = MR(actuator_ctrlrange);
+  const float* forcerange = MR(actuator_forcerange);
+  const float* gainprm = MR(actuator_gainprm);
+  const float* biasprm = MR(actuator_biasprm);
+  const float* dynprm = MR(actuator_dynprm);
+  for (int a = lane; a < m.nu; a += LPW) {
+    float ctrl = d.ctrl[(long)wid * m.nu + a];
+    if (m.actuator_ctrllimited[a] && !(m.opt_disableflags & DSBL_CLAMPCTRL))
+      ctrl = clampf(ctrl, ctrlrange[2 * a], ctrlrange[2 * a + 1]);
+    float ctrl_act = ctrl;
+    int act_first = m.actuator_actadr[a];
+    if (m.na && act_first >= 0) {
+      int act_last = act_first + m.actuator_actnum[a] - 1;
+      int dt = m.actuator_dyntype[a];
+      float act = d.act[(long)wid * m.na + act_last];
+      float act_dot = 0.0f;
+      if (dt == 1) act_dot = ctrl;                                               // INTEGRATOR
+      else if (dt == 2 || dt == 3) act_dot = (ctrl - act) / fmaxf(dynprm[10 * a], MJW_MINVAL);  // FILTER(EXACT)
+      d.act_dot[(long)wid * m.na + act_last] = act_dot;
+      ctrl_act = act;  // actearly not supported by this build's compiler
+    }
+    float len = s[L.act_len + a], vel = s[L.act_vel + a];
+    const float* gp = gainprm + 10 * a;
+    const float* bp = biasprm + 10 * a;
+    float gain = 0.0f, bias = 0.0f;
+    int gt = m.actuator_gaintype[a], bt = m.actuator_biastype[a];
+    if (gt == 0) gain = gp[0];
+    else if (gt == 1) gain = gp[0] + gp[1] * len + gp[2] * vel;
+    if (bt == 1) bias = bp[0] + bp[1] * len + bp[2] * vel;
+    float force = gain * ctrl_act + bias;
+    if (m.actuator_forcelimited[a]) force = clampf(force, forcerange[2 * a], forcerange[2 * a + 1]);
+    s[L.act_force + a] = force;
+    d.actuator_force[(long)wid * m.nu + a] = force;
+  }
+  WSYNC();
+  const float* jnt_actfrcrange = MR(jnt_actfrcrange);
+  for (int i = lane; i < nv; i += LPW) {
+    float q = 0.0f;
+    for (int a = 0; a < m.nu; a++)
+      for (int k = 0; k < si[L.act_nnz + a]; k++)
+        if (si[L.act_momdof + 6 * a + k] == i) q += s[L.act_mom + 6 * a + k] * s[L.act_force + a];
+    int j = m.dof_jntid[i];
+    if (m.jnt_actfrclimited[j]) q = clampf(q, jnt_actfrcrange[2 * j], jnt_actfrcrange[2 * j + 1]);
+    qfrc_act[i] = q;
+    d.qfrc_actuator[(long)wid * nv + i] = q;
+  }
+  WSYNC();
+}
+
+// forward.py:930-969 + support.py:174-237 (xfrc) + factor_solve_i (smooth.py:2860-2928)
+__device__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  const int nv = m.nv, nvs = L.nvs;
+  float qs = 0.0f;
+  if (lane < nv) {
+    int i = lane;
+    long gi = (long)wid * nv + i;
+    qs = s[L.qfrc_passive + i] - s[L.qfrc_bias + i] + s[L.qfrc_actuator + i] + d.qfrc_applied[gi];
+    // xfrc_accumulate: bodies in the subtree of dof_bodyid form the DFS range [db, subtree_end)
+    const float* cd = s + L.cdof + 6 * i;
+    int db = m.dof_bodyid[i];
+    float acc = 0.0f;
+    const float* xfrc = d.xfrc_applied + (long)wid * m.nbody * 6;
+    for (int b = db; b < m.body_subtree_end[db]; b++) {
+      const float* ft = xfrc + 6 * b;
+      if (ft[0] == 0.0f && ft[1] == 0.0f && ft[2] == 0.0f && ft[3] == 0.0f && ft[4] == 0.0f && ft[5] == 0.0f) continue;
+      float off[3], c[3];
+      for (int k = 0; k < 3; k++) off[k] = s[L.xipos + 3 * b + k] - s[L.subtree_com + 3 * m.body_rootid[b] + k];
+      cross3(c, cd, off);
+      acc += cd[3] * ft[0] + cd[4] * ft[1] + cd[5] * ft[2] + cd[0] * ft[3] + cd[1] * ft[4] + cd[2] * ft[5] + dot3(c, ft);
+    }
+    qs += acc;
+    s[L.qfrc_smooth + i] = qs;
+    d.qfrc_smooth[gi] = qs;
+  }
+  // factor qM -> L (copy then in-place Cholesky)
+  float* Lm = s + L.L;
+  for (int e = lane; e < nv * nvs; e += LPW) Lm[e] = s[L.qM + e];
+  WSYNC();
+  cholesky(Lm, nv, nvs, lane);
+  float qacc_smooth = cholesky_solve(Lm, nv, nvs, lane, qs);
+  if (lane < nv) {
+    s[L.qacc_smooth + lane] = qacc_smooth;
+    d.qacc_smooth[(long)wid * nv + lane] = qacc_smooth;
+  }
+  float* gL = d.qLD + (long)wid * nv * nv;
+  for (int e = lane; e < nv * nv; e += LPW) {
+    int r = e / nv, c = e - r * nv;
+    gL[e] = Lm[r * nvs + c];
+  }
+  WSYNC();
+}
+
+// -------------------------------------------------------------------------------------------
+// solver.py: primal CG / Newton (pyramidal), per-world convergence loop
+// -------------------------------------------------------------------------------------------
+struct Vec3 {
+  float c, g, h;
+};
+
+__device__ __forceinline__ void eval_row(float D, float jaref, float jv, float fl, int r, int ne, int nf, float alpha, Vec3& o) {
+  float x = jaref + alpha * jv;
+  if (r >= ne + nf) {
+    if (x < 0.0f) { float jvD = jv * D; o.c += 0.5f * D * x * x; o.g += jvD * x; o.h += jv * jvD; }
+    return;
+  }
+  if (r >= ne) {
+    float rf = safe_div(fl, D);
+    if ((-rf < x) && (x < rf)) { float jvD = jv * D; o.c += 0.5f * D * x * x; o.g += jvD * x; o.h += jv * jvD; }
+    else if (x <= -rf) { o.c += fl * (-0.5f * rf - x); o.g += -fl * jv; }
+    else { o.c += fl * (-0.5f * rf + x); o.g += fl * jv; }
+    return;
+  }
+  float jvD = jv * D;
+  o.c += 0.5f * D * x * x; o.g += jvD * x; o.h += jv * jvD;
+}
+
+__device__ __forceinline__ bool in_bracket(const Vec3& x, const Vec3& y) {
+  return (x.g < y.g && y.g < 0.0f) || (x.g > y.g && y.g > 0.0f);
+}
+
+// update_constraint (solver.py:2154-2219): returns (cost, gauss); sets force/state; qfrc_constraint per lane
+__device__ void update_constraint(const Lay& L, float* s, int lane, int nv, int nvs, int nefc, int ne, int nf, float ma,
+                                  float qfrc_smooth, float qacc, float qacc_smooth, float& cost, float& gauss, float& qfrc_c) {
+  int* si = reinterpret_cast<int*>(s);
+  float c = 0.0f;
+  for (int r = lane; r < nefc; r += LPW) {
+    float D = s[L.efc_D + r], Jaref = s[L.Jaref + r];
+    float f;
+    int st;
+    if (r < ne) { f = -D * Jaref; st = STATE_QUADRATIC; c += 0.5f * D * Jaref * Jaref; }
+    else if (r < ne + nf) {
+      float fl = s[L.efc_frictionloss + r], rf = safe_div(fl, D);
+      if (Jaref <= -rf) { f = fl; st = STATE_LINEARNEG; c += -fl * (0.5f * rf + Jaref); }
+      else if (Jaref >= rf) { f = -fl; st = STATE_LINEARPOS; c += -fl * (0.5f * rf - Jaref); }
+      else { f = -D * Jaref; st = STATE_QUADRATIC; c += 0.5f * D * Jaref * Jaref; }
+    } else {
+      if (Jaref >= 0.0f) { f = 0.0f; st = STATE_SATISFIED; }
+      else { f = -D * Jaref; st = STATE_QUADRATIC; c += 0.5f * D * Jaref * Jaref; }
+    }
+    s[L.efc_force + r] = f;
+    si[L.efc_state + r] = st;
+  }
+  WSYNC();
+  float q = 0.0f;
+  if (lane < nv)
+    for (int r = 0; r < nefc; r++) q += s[L.J + r * nvs + lane] * s[L.efc_force + r];
+  qfrc_c = q;
+  float gl = lane < nv ? (ma - qfrc_smooth) * (qacc - qacc_smooth) : 0.0f;
+  float g = 0.5f * wave_sum(gl);
+  gauss = g;
+  cost = wave_sum(c) + g;
+}
+
+__device__ void solve(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  int* si = w.si;
+  const int nv = m.nv, nvs = L.nvs, njmax = d.njmax;
+  const int nefc_all = si[L.iscratch + 62];
+  const int nefc = min(nefc_all, njmax);
+  const int ne = si[L.iscratch + 60], nf = si[L.iscratch + 61];
+  const bool inl = lane < nv;
+  float qfrc_smooth = inl ? s[L.qfrc_smooth + lane] : 0.0f;
+  float qacc_smooth = inl ? s[L.qacc_smooth + lane] : 0.0f;
+  long gi = (long)wid * nv + lane;
+  if (njmax == 0 || nv == 0) {
+    if (inl) d.qacc[gi] = qacc_smooth;
+    if (lane == 0) d.solver_niter[wid] = 0;
+    return;
+  }
+  const float* M = s + L.qM;
+  const float* Lm = s + L.L;
+  float* vec = s + L.vec;
+  const float tolerance = MR(opt_tolerance)[0];
+  const float ls_tolerance = MR(opt_ls_tolerance)[0];
+  const float meaninertia = MR(stat_meaninertia)[0];
+  const bool newton = m.opt_solver == SOLVER_NEWTON;
+  // qacc init (solver.py:3308-3311)
+  float qacc = 0.0f;
+  if (inl) qacc = (m.opt_disableflags & DSBL_WARMSTART) ? qacc_smooth : d.qacc_warmstart[gi];
+  // Jaref = J qacc - aref, Ma = M qacc
+  if (inl) vec[lane] = qacc;
+  WSYNC();
+  for (int r = lane; r < nefc; r += LPW) {
+    float acc = 0.0f;
+    for (int k = 0; k < nv; k++) acc += s[L.J + r * nvs + k] * vec[k];
+    s[L.Jaref + r] = acc - s[L.efc_aref + r];
+  }
+  float ma = 0.0f;
+  if (inl)
+    for (int k = 0; k < nv; k++) ma += M[lane * nvs + k] * vec[k];
+  WSYNC();
+  float cost = MJW_MAXVAL, prev_cost, gauss, qfrc_c;
+  prev_cost = cost;
+  update_constraint(L, s, lane, nv, nvs, nefc, ne, nf, ma, qfrc_smooth, qacc, qacc_smooth, cost, gauss, qfrc_c);
+  float* H = s + L.H;
+  // update_gradient (solver.py:2879-3008)
+  auto update_gradient = [&](float& grad, float& Mgrad, float& grad_dot) {
+    grad = inl ? ma - qfrc_smooth - qfrc_c : 0.0f;
+    grad_dot = wave_sum(grad * grad);
+    if (!newton) {
+      Mgrad = cholesky_solve(Lm, nv, nvs, lane, grad);
+    } else {
+      // H = M + J' diag(D * QUADRATIC) J, Cholesky, solve
+      if (inl)
+        for (int k = 0; k < nv; k++) {
+          float h = M[lane * nvs + k];
+          for (int r = 0; r < nefc; r++) {
+            if (si[L.efc_state + r] != STATE_QUADRATIC) continue;
+            h += s[L.efc_D + r] * s[L.J + r * nvs + lane] * s[L.J + r * nvs + k];
+          }
+          H[lane * nvs + k] = h;
+        }
+      WSYNC();
+      cholesky(H, nv, nvs, lane);
+      Mgrad = cholesky_solve(H, nv, nvs, lane, grad);
+    }
+  };
+  float grad, Mgrad, grad_dot;
+  update_gradient(grad, Mgrad, grad_dot);
+  float search = -Mgrad;
+  float search_dot = wave_sum(search * search);
+  int niter = 0;
+  const float scale = 1.0f / (meaninertia * (float)nv);
+  if (m.opt_iterations != 0) {
+    bool done = false;
+    while (!done) {
+      // ---- linesearch (solver.py:886-1341, 1662-1703)
+      if (inl) vec[lane] = search;
+      WSYNC();
+      float mv = 0.0f;
+      if (inl)
+        for (int k = 0; k < nv; k++) mv += M[lane * nvs + k] * vec[k];
+      float jv = 0.0f, jaref = 0.0f, Dr = 0.0f, flr = 0.0f;
+      const int r = lane;  // row per lane (njmax <= 64 handled below by rows loop)
+      for (int rr = lane; rr < nefc; rr += LPW) {
+        float acc = 0.0f;
+        for (int k = 0; k < nv; k++) acc += s[L.J + rr * nvs + k] * vec[k];
+        s[L.jv + rr] = acc;
+      }
+      WSYNC();
+      (void)r;
+      float snorm = sqrtf(search_dot);
+      float gtol = fmaxf(tolerance * ls_tolerance * snorm * meaninertia * (float)nv, 1e-6f);
+      // quad_gauss
+      float q1 = wave_sum(inl ? search * (ma - qfrc_smooth) : 0.0f);
+      float q2 = wave_sum(inl ? 0.5f * search * mv : 0.0f);
+      float qg0 = gauss;
+      auto eval_all = [&](float alpha) {
+        Vec3 o = {0.0f, 0.0f, 0.0f};
+        for (int rr = lane; rr < nefc; rr += LPW) {
+          Dr = s[L.efc_D + rr]; jaref = s[L.Jaref + rr]; jv = s[L.jv + rr]; flr = s[L.efc_frictionloss + rr];
+          eval_row(Dr, jaref, jv, flr, rr, ne, nf, alpha, o);
+        }
+        o.c = wave_sum(o.c); o.g = wave_sum(o.g); o.h = wave_sum(o.h);
+        return o;
+      };
+      Vec3 p0 = eval_all(0.0f);
+      p0.c += qg0; p0.g += q1; p0.h += 2.0f * q2;
+      float lo_alpha_in = -safe_div(p0.g, p0.h);
+      Vec3 lo_in = eval_all(lo_alpha_in);
+      lo_in.c += lo_alpha_in * lo_alpha_in * q2 + lo_alpha_in * q1 + qg0;
+      lo_in.g += 2.0f * lo_alpha_in * q2 + q1;
+      lo_in.h += 2.0f * q2;
+      float alpha;
+      bool initial_converged = fabsf(lo_in.g) < gtol && lo_in.c < p0.c;
+      if (!initial_converged) {
+        alpha = 0.0f;
+        bool lo_less = lo_in.g < p0.g;
+        Vec3 lo = lo_less ? lo_in : p0;
+        float lo_alpha = lo_less ? lo_alpha_in : 0.0f;
+        Vec3 hi = lo_less ? p0 : lo_in;
+        float hi_alpha = lo_less ? 0.0f : lo_alpha_in;
+        for (int it = 0; it < m.opt_ls_iterations; it++) {
+          float lo_next_alpha = lo_alpha - safe_div(lo.g, lo.h);
+          float hi_next_alpha = hi_alpha - safe_div(hi.g, hi.h);
+          float mid_alpha = 0.5f * (lo_alpha + hi_alpha);
+          Vec3 ln = {0.0f, 0.0f, 0.0f}, hn = {0.0f, 0.0f, 0.0f}, md = {0.0f, 0.0f, 0.0f};
+          for (int rr = lane; rr < nefc; rr += LPW) {
+            float D = s[L.efc_D + rr], ja = s[L.Jaref + rr], j = s[L.jv + rr], fl = s[L.efc_frictionloss + rr];
+            eval_row(D, ja, j, fl, rr, ne, nf, lo_next_alpha, ln);
+            eval_row(D, ja, j, fl, rr, ne, nf, hi_next_alpha, hn);
+            eval_row(D, ja, j, fl, rr, ne, nf, mid_alpha, md);
+          }
+          ln.c = wave_sum(ln.c); ln.g = wave_sum(ln.g); ln.h = wave_sum(ln.h);
+          hn.c = wave_sum(hn.c); hn.g = wave_sum(hn.g); hn.h = wave_sum(hn.h);
+          md.c = wave_sum(md.c); md.g = wave_sum(md.g); md.h = wave_sum(md.h);
+          ln.c += lo_next_alpha * lo_next_alpha * q2 + lo_next_alpha * q1 + qg0; ln.g += 2.0f * lo_next_alpha * q2 + q1; ln.h += 2.0f * q2;
+          hn.c += hi_next_alpha * hi_next_alpha * q2 + hi_next_alpha * q1 + qg0; hn.g += 2.0f * hi_next_alpha * q2 + q1; hn.h += 2.0f * q2;
+          md.c += mid_alpha * mid_alpha * q2 + mid_alpha * q1 + qg0; md.g += 2.0f * mid_alpha * q2 + q1; md.h += 2.0f * q2;
+          bool s1 = in_bracket(lo, ln);
+          if (s1) { lo = ln; lo_alpha = lo_next_alpha; }
+          bool s2 = in_bracket(lo, md);
+          if (s2) { lo = md; lo_alpha = mid_alpha; }
+          bool s3 = in_bracket(lo, hn);
+          if (s3) { lo = hn; lo_alpha = hi_next_alpha; }
+          bool swap_lo = s1 || s2 || s3;
+          bool h1 = in_bracket(hi, hn);
+          if (h1) { hi = hn; hi_alpha = hi_next_alpha; }
+          bool h2 = in_bracket(hi, md);
+          if (h2) { hi = md; hi_alpha = mid_alpha; }
+          bool h3 = in_bracket(hi, ln);
+          if (h3) { hi = ln; hi_alpha = lo_next_alpha; }
+          bool swap_hi = h1 || h2 || h3;
+          bool ls_done = (!swap_lo && !swap_hi) || (lo.g < 0.0f && lo.g > -gtol) || (hi.g > 0.0f && hi.g < gtol);
+          bool improved = lo.c < p0.c || hi.c < p0.c;
+          bool lo_better = lo.c < hi.c;
+          if (improved && lo_better) alpha = lo_alpha;
+          if (improved && !lo_better) alpha = hi_alpha;
+          if (ls_done) break;
+        }
+      } else {
+        alpha = lo_alpha_in;
+      }
+      qacc += alpha * search;
+      ma += alpha * mv;
+      for (int rr = lane; rr < nefc; rr += LPW) s[L.Jaref + rr] += alpha * s[L.jv + rr];
+      WSYNC();
+      // ---- CG bookkeeping, update constraint + gradient (solver.py:3187-3254)
+      float prev_grad = grad, prev_Mgrad = Mgrad;
+      prev_cost = cost;
+      update_constraint(L, s, lane, nv, nvs, nefc, ne, nf, ma, qfrc_smooth, qacc, qacc_smooth, cost, gauss, qfrc_c);
+      update_gradient(grad, Mgrad, grad_dot);
+      float beta = 0.0f;
+      if (!newton) {
+        float num = wave_sum(inl ? grad * (Mgrad - prev_Mgrad) : 0.0f);
+        float den = wave_sum(inl ? prev_grad * prev_Mgrad : 0.0f);
+        beta = fmaxf(0.0f, num / fmaxf(MJW_MINVAL, den));
+      }
+      search = inl ? (-Mgrad + (newton ? 0.0f : beta * search)) : 0.0f;
+      search_dot = wave_sum(search * search);
+      niter++;
+      float improvement = (prev_cost - cost) * scale;
+      float gradient = sqrtf(grad_dot) * scale;
+      done = (improvement < tolerance) || (gradient < tolerance) || niter == m.opt_iterations;
+    }
+  }
+  // outputs
+  if (inl) {
+    s[L.qacc + lane] = qacc;
+    s[L.Ma + lane] = ma;
+    d.qacc[gi] = qacc;
+    d.efc_Ma[gi] = ma;
+    d.qfrc_constraint[gi] = qfrc_c;
+  }
+  for (int rr = lane; rr < nefc; rr += LPW) {
+    d.efc_force[(long)wid * njmax + rr] = s[L.efc_force + rr];
+    d.efc_state[(long)wid * d.njmax_pad + rr] = si[L.efc_state + rr];
+  }
+  if (lane == 0) d.solver_niter[wid] = niter;
+  WSYNC();
+}
+
+// forward.py:51-354 (_advance + euler; implicit damping when EULERDAMP is enabled)
+__device__ void euler(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  const int nv = m.nv, nvs = L.nvs;
+  const float dt = MR(opt_timestep)[0];
+  float qacc = lane < nv ? s[L.qacc + lane] : 0.0f;
+  float qacc_adv = qacc;
+  if (!(m.opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER))) {
+    const float* dof_damping = MR(dof_damping);
+    float* Lm = s + L.L;
+    for (int e = lane; e < nv * nvs; e += LPW) {
+      int r = e / nvs, c = e - r * nvs;
+      Lm[e] = s[L.qM + e] + ((r == c && r < nv) ? dt * dof_damping[r] : 0.0f);
+    }
+    WSYNC();
+    cholesky(Lm, nv, nvs, lane);
+    qacc_adv = cholesky_solve(Lm, nv, nvs, lane, lane < nv ? s[L.Ma + lane] : 0.0f);
+  }
+  // activations (forward.py:132-168)
+  const float* actrange = MR(actuator_actrange);
+  for (int a = lane; a < m.nu; a += LPW) {
+    int adr = m.actuator_actadr[a];
+    for (int j = adr; adr >= 0 && j < adr + m.actuator_actnum[a]; j++) {
+      long ga = (long)wid * m.na + j;
+      float act = d.act[ga] + d.act_dot[ga] * dt;
+      if (m.actuator_actlimited[a]) act = clampf(act, actrange[2 * a], actrange[2 * a + 1]);
+      d.act[ga] = act;
+    }
+  }
+  float* qvel = s + L.qvel;
+  if (lane < nv) {
+    float v = qvel[lane] + qacc_adv * dt;
+    qvel[lane] = v;
+    d.qvel[(long)wid * nv + lane] = v;
+    d.qacc_warmstart[(long)wid * nv + lane] = qacc;
+  }
+  WSYNC();
+  for (int j = lane; j < m.njnt; j += LPW) {
+    int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j], jt = m.jnt_type[j];
+    float* gq = d.qpos + (long)wid * m.nq;
+    const float* qpos = s + L.qpos;
+    if (jt == JNT_FREE) {
+      for (int i = 0; i < 3; i++) gq[qa + i] = qpos[qa + i] + dt * qvel[da + i];
+      float qn[4];
+      quat_integrate(qn, qpos + qa + 3, qvel + da + 3, dt);
+      for (int i = 0; i < 4; i++) gq[qa + 3 + i] = qn[i];
+    } else if (jt == JNT_BALL) {
+      float qn[4];
+      quat_integrate(qn, qpos + qa, qvel + da, dt);
+      for (int i = 0; i < 4; i++) gq[qa + i] = qn[i];
+    } else {
+      gq[qa] = qpos[qa] + dt * qvel[da];
+    }
+  }
+  if (lane == 0) d.time[wid] = d.time[wid] + dt;
+}
+
+// -------------------------------------------------------------------------------------------
+// input loaders for stage kernels that do not start at fwd_position
+// -------------------------------------------------------------------------------------------
+__device__ void load_state(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  for (int i = lane; i < m.nq; i += LPW) w.s[L.qpos + i] = d.qpos[(long)wid * m.nq + i];
+  for (int i = lane; i < m.nv; i += LPW) w.s[L.qvel + i] = d.qvel[(long)wid * m.nv + i];
+}
+
+__device__ void load_smooth(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w, int stages) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  int* si = w.si;
+  const int nv = m.nv, nvs = L.nvs, np = m.nv_pad;
+  if (stages & (ST_VEL | ST_ACC)) {
+    for (int e = lane; e < nv * 6; e += LPW) s[L.cdof + e] = d.cdof[(long)wid * nv * 6 + e];
+    for (int e = lane; e < m.nbody * 10; e += LPW) s[L.cinert + e] = d.cinert[(long)wid * m.nbody * 10 + e];
+    for (int e = lane; e < m.nbody * 3; e += LPW) {
+      s[L.xipos + e] = d.xipos[(long)wid * m.nbody * 3 + e];
+      s[L.subtree_com + e] = d.subtree_com[(long)wid * m.nbody * 3 + e];
+    }
+  }
+  if (stages & (ST_VEL | ST_ACT)) {
+    for (int a = lane; a < m.nu; a += LPW) {
+      long gu = (long)wid * m.nu + a;
+      int nnz = d.moment_rownnz[gu], adr = d.moment_rowadr[gu];
+      si[L.act_nnz + a] = nnz;
+      for (int k = 0; k < 6; k++) {
+        s[L.act_mom + 6 * a + k] = k < nnz ? d.actuator_moment[(long)wid * m.nJmom + adr + k] : 0.0f;
+        si[L.act_momdof + 6 * a + k] = k < nnz ? d.moment_colind[(long)wid * m.nJmom + adr + k] : 0;
+      }
+      s[L.act_len + a] = d.actuator_length[gu];
+      if (!(stages & ST_VEL)) s[L.act_vel + a] = d.actuator_velocity[gu];
+    }
+  }
+  if (stages & (ST_ACC | ST_SOLVE | ST_EULER)) {
+    for (int e = lane; e < nv * nvs; e += LPW) {
+      int r = e / nvs, c = e - r * nvs;
+      s[L.qM + e] = c < nv ? d.qM[(long)wid * np * np + r * np + c] : 0.0f;
+    }
+  }
+  if ((stages & ST_ACC) && !(stages & ST_VEL)) {
+    for (int i = lane; i < nv; i += LPW) {
+      long gi = (long)wid * nv + i;
+      s[L.qfrc_passive + i] = d.qfrc_passive[gi];
+      s[L.qfrc_bias + i] = d.qfrc_bias[gi];
+    }
+  }
+  if ((stages & ST_ACC) && !(stages & ST_ACT)) {
+    for (int i = lane; i < nv; i += LPW) s[L.qfrc_actuator + i] = d.qfrc_actuator[(long)wid * nv + i];
+  }
+  if ((stages & ST_SOLVE) && !(stages & ST_ACC)) {
+    for (int e = lane; e < nv * nvs; e += LPW) {
+      int r = e / nvs, c = e - r * nvs;
+      s[L.L + e] = (c < nv) ? d.qLD[(long)wid * nv * nv + r * nv + c] : 0.0f;
+    }
+    for (int i = lane; i < nv; i += LPW) {
+      long gi = (long)wid * nv + i;
+      s[L.qfrc_smooth + i] = d.qfrc_smooth[gi];
+      s[L.qacc_smooth + i] = d.qacc_smooth[gi];
+    }
+  }
+  if ((stages & ST_SOLVE) && !(stages & ST_POS)) {
+    int nefc = d.nefc[wid];
+    int nrows = min(nefc, d.njmax);
+    for (int e = lane; e < nrows * nvs; e += LPW) {
+      int r = e / nvs, c = e - r * nvs;
+      s[L.J + e] = c < nv ? d.efc_J[(long)wid * d.njmax_pad * np + r * np + c] : 0.0f;
+    }
+    for (int r = lane; r < nrows; r += LPW) {
+      long gr = (long)wid * d.njmax + r;
+      s[L.efc_D + r] = d.efc_D[(long)wid * d.njmax_pad + r];
+      s[L.efc_aref + r] = d.efc_aref[gr];
+      s[L.efc_frictionloss + r] = d.efc_frictionloss[gr];
+    }
+    if (lane == 0) {
+      si[L.iscratch + 60] = d.ne[wid];
+      si[L.iscratch + 61] = d.nf[wid];
+      si[L.iscratch + 62] = nefc;
+    }
+  }
+  if ((stages & ST_EULER) && !(stages & ST_SOLVE)) {
+    for (int i = lane; i < nv; i += LPW) {
+      long gi = (long)wid * nv + i;
+      s[L.qacc + i] = d.qacc[gi];
+      s[L.Ma + i] = d.efc_Ma[gi];
+    }
+  }
+  WSYNC();
+}
+
+template <int STAGES>
+__global__ void __launch_bounds__(64) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  WS w;
+  w.s = smem;
+  w.si = reinterpret_cast<int*>(smem);
+  w.wid = blockIdx.x;
+  w.lane = lane_id();
+  if (w.wid >= d.nworld) return;
+  load_state(m, d, L, w);
+  if (STAGES != ST_POS) load_smooth(m, d, L, w, STAGES);
+  WSYNC();
+  if (STAGES & ST_POS) {
+    kinematics(m, d, L, w);
+    com_pos(m, d, L, w);
+    camlight(m, d, L, w);
+    crb_qM(m, d, L, w);
+    collision_and_constraints(m, d, L, w);
+    transmission(m, d, L, w);
+  }
+  if (STAGES & ST_VEL) fwd_velocity(m, d, L, w);
+  if ((STAGES & ST_POS) && (STAGES & ST_VEL) && w.lane < 2 && !(m.opt_enableflags & ENBL_ENERGY))
+    d.energy[(long)w.wid * 2 + w.lane] = 0.0f;
+  if (STAGES & ST_ACT) fwd_actuation(m, d, L, w);
+  if (STAGES & ST_ACC) fwd_acceleration(m, d, L, w);
+  if (STAGES & ST_SOLVE) solve(m, d, L, w);
+  if (STAGES & ST_EULER) euler(m, d, L, w);
+}
+
+// benchmark.py:41-83
+__global__ void ctrl_noise_kernel(const mjw_model_t m, const mjw_data_t d, const float* center, int step, float std, float rate_) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= d.nworld * m.nu) return;
+  int w = t / m.nu, a = t - w * m.nu;
+  int wid = w;
+  int worldid = d.world_offset + w;
+  float rate = expf(-MR(opt_timestep)[0] / rate_);
+  float scale = std * sqrtf(1.0f - rate * rate);
+  float midpoint = 0.0f, halfrange = 1.0f;
+  const float* cr = MR(actuator_ctrlrange) + 2 * a;
+  bool lim = m.actuator_ctrllimited[a];
+  if (lim) { midpoint = 0.5f * (cr[1] + cr[0]); halfrange = 0.5f * (cr[1] - cr[0]); }
+  if (center) midpoint = center[a];
+  float c = rate * d.ctrl[t] + (1.0f - rate) * midpoint;
+  c += scale * halfrange * (2.0f * halton((step + 1) * (worldid + 1), a + 2) - 1.0f);
+  if (lim) c = clampf(c, cr[0], cr[1]);
+  d.ctrl[t] = c;
+}
+
+}  // namespace mjw
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+namespace {
+thread_local std::string g_err;
+
+int set_err(hipError_t e, const char* where) {
+  if (e == hipSuccess) return 0;
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return (int)e;
+}
+
+template <int STAGES>
+int launch(const mjw_model_t* m, const mjw_data_t* d, void* stream, const char* name) {
+  if (!m || !d) { g_err = std::string(name) + ": null model/data"; return -1; }
+  if (d->nworld <= 0) return 0;
+  if (m->nv > 64 || m->nbody > 4096) { g_err = std::string(name) + ": model too large for the dense world-per-wave path"; return -2; }
+  mjw::Lay L = mjw::make_layout(*m, d->njmax);
+  size_t lds = (size_t)L.total * 4;
+  if (lds > 160 * 1024) { g_err = std::string(name) + ": per-world LDS working set exceeds 160 KiB"; return -3; }
+  hipStream_t s = (hipStream_t)stream;
+  if (STAGES & mjw::ST_POS) {
+    hipError_t e = hipMemsetAsync(d->nacon, 0, sizeof(int32_t), s);
+    if (e == hipSuccess) e = hipMemsetAsync(d->ncollision, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return set_err(e, name);
+  }
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  hipLaunchKernelGGL(mjw::mjw_kernel<STAGES>, dim3(d->nworld), dim3(64), lds, s, *m, *d, L);
+  return set_err(hipGetLastError(), name);
+}
+}  // namespace
+
+extern "C" {
+
+int mjw_abi_version(void) { return MJW_ABI_VERSION; }
+const char* mjw_last_error(void) { return g_err.c_str(); }
+int mjw_sizeof_model(void) { return (int)sizeof(mjw_model_t); }
+int mjw_sizeof_data(void) { return (int)sizeof(mjw_data_t); }
+int mjw_lds_bytes(const mjw_model_t* m, int njmax) { return mjw::make_layout(*m, njmax).total * 4; }
+
+int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return launch<mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE | mjw::ST_EULER>(m, d, stream, "mjw_step");
+}
+int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return launch<mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE>(m, d, stream, "mjw_forward");
+}
+int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return launch<mjw::ST_POS>(m, d, stream, "mjw_fwd_position");
+}
+int mjw_fwd_velocity(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return launch<mjw::ST_VEL>(m, d, stream, "mjw_fwd_velocity");
+}
+int mjw_fwd_actuation(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return launch<mjw::ST_ACT>(m, d, stream, "mjw_fwd_actuation");
+}
+int mjw_fwd_acceleration(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return launch<mjw::ST_ACC>(m, d, stream, "mjw_fwd_acceleration");
+}
+int mjw_solve(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return launch<mjw::ST_SOLVE>(m, d, stream, "mjw_solve");
+}
+int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return launch<mjw::ST_EULER>(m, d, stream, "mjw_euler");
+}
+
+int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* center, int step, float std, float rate, void* stream) {
+  int n = d->nworld * m->nu;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(mjw::ctrl_noise_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, *m, *d, center, step, std, rate);
+  return set_err(hipGetLastError(), "mjw_ctrl_noise");
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+"""Pipeline entry points (mirror mujoco_warp/_src/forward.py).
+
+`step(m, d)` (forward.py:1003-1018) runs the whole forward pass and the Euler
+integrator as ONE fused world-per-wavefront HIP kernel on the current torch
+stream.  The stage functions (`fwd_position`, `fwd_velocity`, ...) launch the
+same device code restricted to one stage group; they exist for parity testing
+and for models that install Python callbacks (types.Callback), which are
+invoked between stage launches exactly where the reference calls them.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .io import cdata, cmodel
+from .types import Data, DisableBit, Model
+
+
+def _stream(d: Data):
+  if d.device.type != "cuda":
+    raise RuntimeError("mujoco_warp_amd runs on the ROCm device only (no CPU fallback): pass device='cuda'")
+  return torch.cuda.current_stream(d.device).cuda_stream
+
+
+def _call(fn: str, m: Model, d: Data):
+  L = _lib.lib()
+  cm, cd = cmodel(m), cdata(d)
+  _lib.check(getattr(L, fn)(cm, cd, _stream(d)), fn)
+
+
+def _has_callbacks(m: Model) -> bool:
+  cb = m.callback
+  return any(getattr(cb, f) is not None for f in ("control", "passive", "act_dyn", "act_gain", "act_bias", "contactfilter"))
+
+
+def fwd_position(m: Model, d: Data):
+  """Position-dependent computations (forward.py:513-537)."""
+  _call("mjw_fwd_position", m, d)
+  if m.callback.contactfilter is not None:
+    m.callback.contactfilter(m, d)
+
+
+def fwd_velocity(m: Model, d: Data):
+  """Velocity-dependent computations (forward.py:592-613)."""
+  _call("mjw_fwd_velocity", m, d)
+  if m.callback.passive is not None:
+    m.callback.passive(m, d)
+
+
+def fwd_actuation(m: Model, d: Data):
+  """Actuation-dependent computations (forward.py:836-927)."""
+  _call("mjw_fwd_actuation", m, d)
+
+
+def fwd_acceleration(m: Model, d: Data, factorize: bool = True):
+  """qfrc_smooth and qacc_smooth (forward.py:949-969); always factorizes qM."""
+  _call("mjw_fwd_acceleration", m, d)
+
+
+def solve(m: Model, d: Data):
+  """Constraint solver (solver.py:3296-3343)."""
+  _call("mjw_solve", m, d)
+
+
+def euler(m: Model, d: Data):
+  """Euler integrator, semi-implicit in velocity (forward.py:326-354)."""
+  _call("mjw_euler", m, d)
+
+
+def _forward_staged(m: Model, d: Data):
+  fwd_position(m, d)
+  fwd_velocity(m, d)
+  if not (m.opt.disableflags & DisableBit.ACTUATION) and m.callback.control is not None:
+    m.callback.control(m, d)
+  fwd_actuation(m, d)
+  fwd_acceleration(m, d)
+  solve(m, d)
+
+
+def forward(m: Model, d: Data):
+  """Forward dynamics (forward.py:972-1000)."""
+  if _has_callbacks(m):
+    _forward_staged(m, d)
+  else:
+    _call("mjw_forward", m, d)
+
+
+def step(m: Model, d: Data):
+  """Advance simulation (forward.py:1003-1018)."""
+  if _has_callbacks(m):
+    _forward_staged(m, d)
+    euler(m, d)
+  else:
+    _call("mjw_step", m, d)
+
+
+def ctrl_noise(m: Model, d: Data, step_index: int, center: torch.Tensor | None = None, std: float = 0.01, rate: float = 0.1):
+  """Per-step OU + Halton control noise of the reference benchmark (_src/benchmark.py:41-83)."""
+  L = _lib.lib()
+  ptr = None if center is None or center.numel() == 0 else center.data_ptr()
+  _lib.check(L.mjw_ctrl_noise(cmodel(m), cdata(d), ptr, int(step_index), float(std), float(rate), _stream(d)), "mjw_ctrl_noise")

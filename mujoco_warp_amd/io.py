@@ -1,0 +1,548 @@
+"""Host I/O: put_model / put_data / make_data / get_data_into / reset_data / override_model.
+
+Mirrors mujoco_warp/_src/io.py: `put_model` (io.py:77-647) turns a compiled
+model (this package's `mjcf.MjModel`, or a real `mujoco.MjModel` when that
+package is importable) into device tensors plus the derived index arrays the
+kernels need; `put_data` (io.py:1016-1240) tiles one host state over `nworld`
+worlds; array shapes follow `types.Data` (types.py:1702-1896).  All device
+memory is owned by torch tensors; the C ABI only receives their pointers.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import types
+from .types import BroadphaseFilter, DisableBit, JointType
+
+# reference io.py:650-661
+def _round_up(x, k):
+  return ((x + k - 1) // k) * k
+
+
+def _padded_sizes(nv: int, njmax: int, is_sparse: bool):
+  tile = types.TILE_SIZE_JTDAJ_SPARSE if is_sparse else types.TILE_SIZE_JTDAJ_DENSE
+  njmax_pad = _round_up(njmax, tile)
+  nv_pad = _round_up(nv, tile) if (is_sparse or nv > 32) else _round_up(nv, 4)
+  return njmax_pad, nv_pad
+
+
+def is_sparse(mjm) -> bool:
+  """io.py:67-74."""
+  if mjm.opt.jacobian == types.JacobianType.AUTO:
+    return mjm.nv > 32
+  return mjm.opt.jacobian == types.JacobianType.SPARSE
+
+
+def _device(device=None):
+  if device is not None:
+    return torch.device(device)
+  return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+def _f32(a, device):
+  return torch.as_tensor(np.ascontiguousarray(np.asarray(a, dtype=np.float32)), device=device)
+
+
+def _i32(a, device):
+  return torch.as_tensor(np.ascontiguousarray(np.asarray(a).astype(np.int32)), device=device)
+
+
+def nxn_geom_pairs(mjm):
+  """Filtered NXN candidate pairs and pair ids (io.py:269-358)."""
+  filterparent = not (mjm.opt.disableflags & DisableBit.FILTERPARENT)
+  g1, g2 = np.triu_indices(mjm.ngeom, k=1)
+  bodyid1, bodyid2 = mjm.geom_bodyid[g1], mjm.geom_bodyid[g2]
+  weldid1, weldid2 = mjm.body_weldid[bodyid1], mjm.body_weldid[bodyid2]
+  weld_parentid1 = mjm.body_weldid[mjm.body_parentid[weldid1]]
+  weld_parentid2 = mjm.body_weldid[mjm.body_parentid[weldid2]]
+  self_collision = weldid1 == weldid2
+  parent_child = filterparent & (weldid1 != 0) & (weldid2 != 0) & ((weldid1 == weld_parentid2) | (weldid2 == weld_parentid1))
+  mask = np.array((mjm.geom_contype[g1] & mjm.geom_conaffinity[g2]) | (mjm.geom_contype[g2] & mjm.geom_conaffinity[g1]), dtype=bool)
+  exclude = np.isin((bodyid1 << 16) + bodyid2, getattr(mjm, "exclude_signature", np.zeros(0, dtype=np.int32)))
+  pairid_contact = -np.ones(len(g1), dtype=np.int32)
+  pairid_contact[~(mask & ~self_collision & ~parent_child & ~exclude)] = -2
+  if getattr(mjm, "npair", 0):
+    raise NotImplementedError("explicit <contact><pair> entries are not supported yet")
+  pairid_collision = -np.ones(len(g1), dtype=np.int32)
+  include = pairid_contact > -2
+  pairs = np.stack([g1, g2], axis=1)[include].astype(np.int32)
+  pairid = np.stack([pairid_contact, pairid_collision], axis=1)[include].astype(np.int32)
+  return pairs, pairid
+
+
+# real model fields: header name -> (attribute on Model, MjModel source attr)
+def _model_attr(name):
+  if name.startswith("opt_"):
+    return ("opt", name[4:])
+  if name.startswith("stat_"):
+    return ("stat", name[5:])
+  return (None, name)
+
+
+_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE}
+
+
+def put_model(mjm, device=None) -> types.Model:
+  """Creates a model on device (reference io.py:77-647)."""
+  dev = _device(device)
+  # feature checks (io.py:89-144): the MI355X path supports the primitive-geom dense subset
+  for g in np.unique(mjm.geom_type):
+    if int(g) not in _SUPPORTED_GEOMS:
+      raise NotImplementedError(f"geom type {types.GeomType(int(g)).name} not supported.")
+  if mjm.opt.integrator not in (types.IntegratorType.EULER,):
+    raise NotImplementedError(f"{types.IntegratorType(mjm.opt.integrator).name} is unsupported.")
+  if mjm.opt.cone != types.ConeType.PYRAMIDAL:
+    raise NotImplementedError("ELLIPTIC is unsupported.")
+  if mjm.opt.solver not in (types.SolverType.CG, types.SolverType.NEWTON):
+    raise NotImplementedError(f"{types.SolverType(mjm.opt.solver).name} is unsupported.")
+  if getattr(mjm.opt, "noslip_iterations", 0) > 0:
+    raise NotImplementedError("noslip solver not implemented.")
+  if is_sparse(mjm):
+    raise NotImplementedError("sparse Jacobian / nv > 32 models are not supported by this build yet.")
+  if getattr(mjm, "ntendon", 0) or getattr(mjm, "neq", 0) or getattr(mjm, "nsensor", 0) or getattr(mjm, "nflex", 0):
+    raise NotImplementedError("tendons / equality constraints / sensors / flex are not supported by this build yet.")
+  if np.any(mjm.actuator_trntype > types.TrnType.JOINTINPARENT):
+    raise NotImplementedError("only joint transmissions are supported.")
+
+  nv = mjm.nv
+  opt = types.Option()
+  o = mjm.opt
+  opt.timestep = _f32([o.timestep], dev)
+  opt.tolerance = _f32([max(o.tolerance, 1e-6)], dev)  # io.py:185
+  opt.ls_tolerance = _f32([o.ls_tolerance], dev)
+  opt.ccd_tolerance = _f32([getattr(o, "ccd_tolerance", 1e-6)], dev)
+  opt.density = _f32([o.density], dev)
+  opt.viscosity = _f32([o.viscosity], dev)
+  opt.gravity = _f32(np.asarray(o.gravity).reshape(1, 3), dev)
+  opt.wind = _f32(np.asarray(o.wind).reshape(1, 3), dev)
+  opt.magnetic = _f32(np.asarray(o.magnetic).reshape(1, 3), dev)
+  opt.impratio_invsqrt = _f32([1.0 / np.sqrt(max(o.impratio, types.MJ_MINVAL))], dev)  # io.py:178-179
+  opt.integrator, opt.cone, opt.solver, opt.jacobian = int(o.integrator), int(o.cone), int(o.solver), int(o.jacobian)
+  opt.iterations, opt.ls_iterations = int(o.iterations), int(o.ls_iterations)
+  opt.disableflags, opt.enableflags = int(o.disableflags), int(o.enableflags)
+  stat = types.Statistic(meaninertia=_f32([mjm.stat.meaninertia], dev))
+
+  m = types.Model()
+  m.opt = opt
+  m.stat = stat
+  m.callback = types.Callback()
+  m.device = dev
+  for n in ("nq", "nv", "nu", "na", "nbody", "njnt", "ngeom", "nsite", "ncam", "nlight", "nmocap", "nM", "nC"):
+    setattr(m, n, int(getattr(mjm, n)))
+  m.ntendon = 0
+  m.neq = 0
+  m.nsensor = 0
+  m.nsensordata = 0
+  m.nflex = 0
+  m.is_sparse = False
+  njmax_pad_unused, m.nv_pad = _padded_sizes(nv, 0, False)
+  m.nmaxcondim = int(np.concatenate(([0], mjm.geom_condim)).max())
+  m.nmaxpyramid = int(max(1, 2 * (m.nmaxcondim - 1)))
+  m.block_dim = None
+
+  # derived tree arrays (io.py:234-258): levels; DFS subtree ranges (bodies are in DFS pre-order)
+  depth = np.zeros(mjm.nbody, dtype=int)
+  for i in range(1, mjm.nbody):
+    depth[i] = depth[mjm.body_parentid[i]] + 1
+  order = np.argsort(depth, kind="stable")
+  m.nlevel = int(depth.max()) + 1 if mjm.nbody else 0
+  level_adr = np.searchsorted(depth[order], np.arange(m.nlevel + 1))
+  subtree_end = np.arange(mjm.nbody) + 1
+  for i in range(mjm.nbody - 1, 0, -1):
+    p = mjm.body_parentid[i]
+    subtree_end[p] = max(subtree_end[p], subtree_end[i])
+  m.body_tree = tuple(torch.as_tensor(order[level_adr[i] : level_adr[i + 1]].astype(np.int32), device=dev) for i in range(m.nlevel))
+  # host-side sanity: DFS pre-order is required for subtree ranges
+  for i in range(1, mjm.nbody):
+    assert mjm.body_parentid[i] < i, "bodies must be in DFS pre-order"
+
+  jnt_limited_sh = np.nonzero(mjm.jnt_limited & np.isin(mjm.jnt_type, (JointType.SLIDE, JointType.HINGE)))[0]
+  if np.any(mjm.jnt_limited & (mjm.jnt_type == JointType.BALL)):
+    raise NotImplementedError("ball joint limits are not supported by this build yet.")
+  pairs, pairid = nxn_geom_pairs(mjm)
+  typed = pairs.copy()
+  swap = mjm.geom_type[typed[:, 0]] > mjm.geom_type[typed[:, 1]]
+  typed[swap] = typed[swap][:, ::-1]
+  m.nxn_geom_pair_filtered = _i32(pairs, dev)
+  m.nxn_pairid_filtered = _i32(pairid, dev)
+  m.nxn_geom_pair_typed = _i32(typed, dev)
+  m.nxn = len(pairs)
+  m.nlimited = len(jnt_limited_sh)
+  m.nJmom = int(sum({JointType.FREE: 6, JointType.BALL: 3}.get(int(mjm.jnt_type[mjm.actuator_trnid[a, 0]]), 1) for a in range(mjm.nu)))
+
+  derived_int = dict(
+    body_subtree_end=subtree_end,
+    level_body=order,
+    level_adr=level_adr,
+    jnt_limited_slide_hinge_adr=jnt_limited_sh,
+  )
+  m.body_subtree_end = _i32(subtree_end, dev)
+  m.level_body = _i32(order, dev)
+  m.level_adr = _i32(level_adr, dev)
+  m.jnt_limited_slide_hinge_adr = _i32(jnt_limited_sh, dev)
+
+  # real arrays (batched with leading dim 1)
+  for name, cnt in _lib.MODEL_REAL_ARRAYS:
+    grp, attr = _model_attr(name)
+    if grp is not None:
+      continue
+    val = np.asarray(getattr(mjm, attr), dtype=np.float64)
+    setattr(m, attr, _f32(val.reshape((1,) + val.shape), dev))
+  for name, cnt in _lib.MODEL_INT_ARRAYS:
+    if name in derived_int or name in ("nxn_geom_pair", "nxn_pairid"):
+      continue
+    setattr(m, name, _i32(np.asarray(getattr(mjm, name)), dev))
+  # extra reference fields kept for API parity
+  for name in ("dof_Madr", "M_rownnz", "M_rowadr", "M_colind", "mapM2M", "body_geomnum", "body_geomadr", "geom_contype", "geom_conaffinity", "exclude_signature"):
+    if hasattr(mjm, name):
+      setattr(m, name, _i32(np.asarray(getattr(mjm, name)), dev))
+  m._mjm_sizes = dict(nq=mjm.nq, nv=nv)
+  return m
+
+
+def _nb(t: torch.Tensor):
+  return int(t.shape[0])
+
+
+def cmodel(m: types.Model) -> _lib.CModel:
+  """Builds (and caches) the C model view holding the device pointers of `m`."""
+  tensors = []
+  for name, _ in _lib.MODEL_REAL_ARRAYS:
+    grp, attr = _model_attr(name)
+    t = getattr(getattr(m, grp), attr) if grp else getattr(m, attr)
+    tensors.append(t)
+  for name, _ in _lib.MODEL_INT_ARRAYS:
+    attr = {"nxn_geom_pair": "nxn_geom_pair_typed", "nxn_pairid": "nxn_pairid_filtered"}.get(name, name)
+    tensors.append(getattr(m, attr))
+  cache = getattr(m, "_cmodel_cache", None)
+  scal = tuple(int(getattr(m.opt, n[4:]) if n.startswith("opt_") else getattr(m, n)) for n in _lib.MODEL_INT_SCALARS if n != "opt_broadphase_filter")
+  if cache is not None and cache[1] == scal and len(cache[2]) == len(tensors) and all(a is b for a, b in zip(cache[2], tensors)):
+    return cache[0]
+  c = _lib.CModel()
+  for n in _lib.MODEL_INT_SCALARS:
+    if n == "opt_broadphase_filter":
+      v = int(m.opt.broadphase_filter)
+    elif n.startswith("opt_"):
+      v = int(getattr(m.opt, n[4:]))
+    else:
+      v = int(getattr(m, n))
+    setattr(c, n, v)
+  sizes = {n: getattr(c, n) for n in _lib.MODEL_INT_SCALARS}
+  i = 0
+  for name, cnt in _lib.MODEL_REAL_ARRAYS:
+    t = tensors[i]
+    i += 1
+    if t.dtype != torch.float32 or not t.is_contiguous():
+      raise TypeError(f"model field {name} must be a contiguous float32 tensor")
+    count = int(eval(cnt, {}, sizes))
+    nb = _nb(t) if t.dim() > 0 else 1
+    if t.numel() != nb * count:
+      raise ValueError(f"model field {name}: expected {count} values per batch entry, got shape {tuple(t.shape)}")
+    setattr(c, name, t.data_ptr())
+    setattr(c, name + "_nb", nb)
+    setattr(c, name + "_cnt", count)
+  for name, cnt in _lib.MODEL_INT_ARRAYS:
+    t = tensors[i]
+    i += 1
+    count = int(eval(cnt, {}, sizes))
+    if t.numel() != count:
+      raise ValueError(f"model field {name}: expected {count} values, got {t.numel()}")
+    setattr(c, name, t.data_ptr())
+  m._cmodel_cache = (c, scal, tensors)
+  return c
+
+
+# Data field trailing shapes (types.py:1702-1896)
+def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
+  nb, nv, nq, nu, na, nj, ng = m.nbody, m.nv, m.nq, m.nu, m.na, m.njnt, m.ngeom
+  np_ = m.nv_pad
+  real = dict(
+    time=(), qpos=(nq,), qvel=(nv,), act=(na,), ctrl=(nu,), qacc_warmstart=(nv,), qfrc_applied=(nv,),
+    xfrc_applied=(nb, 6), mocap_pos=(m.nmocap, 3), mocap_quat=(m.nmocap, 4), qacc=(nv,), act_dot=(na,), energy=(2,),
+    xpos=(nb, 3), xquat=(nb, 4), xmat=(nb, 3, 3), xipos=(nb, 3), ximat=(nb, 3, 3), xanchor=(nj, 3), xaxis=(nj, 3),
+    geom_xpos=(ng, 3), geom_xmat=(ng, 3, 3), site_xpos=(m.nsite, 3), site_xmat=(m.nsite, 3, 3),
+    cam_xpos=(m.ncam, 3), cam_xmat=(m.ncam, 3, 3), light_xpos=(m.nlight, 3), light_xdir=(m.nlight, 3),
+    subtree_com=(nb, 3), cdof=(nv, 6), cinert=(nb, 10), crb=(nb, 10), qM=(np_, np_), qLD=(nv, nv),
+    actuator_length=(nu,), actuator_moment=(m.nJmom,), actuator_velocity=(nu,), actuator_force=(nu,),
+    cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,),
+    qfrc_passive=(nv,), qfrc_actuator=(nv,), qfrc_smooth=(nv,), qacc_smooth=(nv,), qfrc_constraint=(nv,),
+    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6),
+    efc_J=(njmax_pad, np_), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
+    efc_aref=(njmax,), efc_frictionloss=(njmax,), efc_force=(njmax,), efc_Ma=(nv,),
+  )
+  ints = dict(
+    ne=(), nf=(), nl=(), nefc=(), solver_niter=(), moment_rownnz=(nu,), moment_rowadr=(nu,), moment_colind=(m.nJmom,),
+    efc_type=(njmax,), efc_id=(njmax,), efc_state=(njmax_pad,),
+  )
+  creal = dict(
+    contact_dist=(), contact_pos=(3,), contact_frame=(3, 3), contact_includemargin=(), contact_friction=(5,),
+    contact_solref=(2,), contact_solreffriction=(2,), contact_solimp=(5,),
+  )
+  cint = dict(contact_dim=(), contact_geom=(2,), contact_efc_address=(m.nmaxpyramid,), contact_worldid=(), contact_type=(), contact_geomcollisionid=())
+  return real, ints, creal, cint
+
+
+def _valid_sizes():
+  return (2 + (np.arange(19) % 2)) * (2 ** (np.arange(19) // 2 + 3))
+
+
+def _default_nconmax(mjm, mjd=None) -> int:
+  """io.py:664-674."""
+  nconmax = max(mjm.nv * 0.35 * (getattr(mjm, "nhfield", 0) > 0) * 10 + 45, getattr(mjd, "ncon", 0) if mjd is not None else 0)
+  vs = _valid_sizes()
+  return int(vs[np.searchsorted(vs, nconmax)])
+
+
+def _default_njmax(mjm, mjd=None) -> int:
+  """io.py:677-687."""
+  njmax = max(mjm.nv * 2.26 * (getattr(mjm, "nhfield", 0) > 0) * 18 + 53, getattr(mjd, "nefc", 0) if mjd is not None else 0)
+  vs = _valid_sizes()
+  return int(vs[np.searchsorted(vs, njmax)])
+
+
+def _alloc_data(m, nworld, nconmax, njmax, naconmax, device):
+  if nworld < 1:
+    raise ValueError("nworld must be >= 1")
+  if nconmax is None:
+    nconmax = _default_nconmax(m)
+  if njmax is None:
+    njmax = _default_njmax(m)
+  if nconmax < 0:
+    raise ValueError("nconmax must be >= 0")
+  if njmax < 0:
+    raise ValueError("njmax must be >= 0")
+  if naconmax is None:
+    naconmax = nconmax * nworld
+  if naconmax < 0:
+    raise ValueError("naconmax must be >= 0")
+  njmax_pad, _ = _padded_sizes(m.nv, njmax, False)
+  real, ints, creal, cint = _data_shapes(m, nworld, njmax, njmax_pad, naconmax)
+  d = types.Data()
+  d.nworld, d.njmax, d.njmax_pad, d.naconmax, d.nconmax = nworld, njmax, njmax_pad, naconmax, nconmax
+  d.njmax_nnz = njmax * m.nv
+  d.world_offset = 0
+  d.device = device
+  d.efc = types.Constraint()
+  d.contact = types.Contact()
+  for name, shp in real.items():
+    t = torch.zeros((nworld,) + shp, dtype=torch.float32, device=device)
+    _set_data_field(d, name, t)
+  for name, shp in ints.items():
+    t = torch.zeros((nworld,) + shp, dtype=torch.int32, device=device)
+    _set_data_field(d, name, t)
+  for name, shp in creal.items():
+    _set_data_field(d, name, torch.zeros((naconmax,) + shp, dtype=torch.float32, device=device))
+  for name, shp in cint.items():
+    _set_data_field(d, name, torch.zeros((naconmax,) + shp, dtype=torch.int32, device=device))
+  d.contact.efc_address.fill_(-1)
+  d.nacon = torch.zeros(1, dtype=torch.int32, device=device)
+  d.ncollision = torch.zeros(1, dtype=torch.int32, device=device)
+  d.sensordata = torch.zeros((nworld, 0), dtype=torch.float32, device=device)
+  d.eq_active = torch.zeros((nworld, 0), dtype=torch.bool, device=device)
+  d.efc.J_rownnz = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
+  d.efc.J_rowadr = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
+  d.efc.J_colind = torch.zeros((nworld, 0, 0), dtype=torch.int32, device=device)
+  d.mocap_quat[..., 0] = 1.0
+  d.xquat[..., 0] = 1.0
+  return d
+
+
+def _set_data_field(d, name, t):
+  if name.startswith("efc_") and name != "efc_Ma":
+    setattr(d.efc, name[4:], t)
+  elif name == "efc_Ma":
+    d.efc.Ma = t
+  elif name.startswith("contact_"):
+    setattr(d.contact, name[8:], t)
+  else:
+    setattr(d, name, t)
+
+
+def _get_data_field(d, name):
+  if name.startswith("efc_"):
+    return getattr(d.efc, name[4:])
+  if name.startswith("contact_"):
+    return getattr(d.contact, name[8:])
+  return getattr(d, name)
+
+
+def cdata(d: types.Data) -> _lib.CData:
+  """Builds (and caches) the C data view holding the device pointers of `d`."""
+  names = [n for n, _ in _lib.DATA_REAL_ARRAYS + _lib.DATA_INT_ARRAYS + _lib.CONTACT_REAL_ARRAYS + _lib.CONTACT_INT_ARRAYS]
+  tensors = [_get_data_field(d, n) for n in names] + [d.nacon, d.ncollision]
+  cache = getattr(d, "_cdata_cache", None)
+  key = (d.nworld, d.njmax, d.njmax_pad, d.naconmax, d.world_offset)
+  if cache is not None and cache[1] == key and all(a is b for a, b in zip(cache[2], tensors)):
+    return cache[0]
+  c = _lib.CData()
+  c.nworld, c.njmax, c.njmax_pad, c.naconmax, c.world_offset = key
+  for n, t in zip(names, tensors):
+    if not t.is_contiguous():
+      raise TypeError(f"data field {n} must be contiguous")
+    setattr(c, n, t.data_ptr())
+  c.nacon = d.nacon.data_ptr()
+  c.ncollision = d.ncollision.data_ptr()
+  d._cdata_cache = (c, key, tensors)
+  return c
+
+
+def make_data(mjm, nworld: int = 1, nconmax: Optional[int] = None, njmax: Optional[int] = None, naconmax: Optional[int] = None, device=None, m: Optional[types.Model] = None) -> types.Data:
+  """Creates a data object on device (io.py:859) initialised to qpos0 / zero state."""
+  dev = _device(device)
+  if m is None:
+    m = put_model(mjm, device=dev)
+  d = _alloc_data(m, nworld, nconmax, njmax, naconmax, dev)
+  d.qpos[:] = torch.as_tensor(np.asarray(mjm.qpos0, dtype=np.float32), device=dev)
+  if mjm.nmocap:
+    for b in np.nonzero(mjm.body_mocapid >= 0)[0]:
+      k = mjm.body_mocapid[b]
+      d.mocap_pos[:, k] = torch.as_tensor(np.asarray(mjm.body_pos[b], dtype=np.float32), device=dev)
+      d.mocap_quat[:, k] = torch.as_tensor(np.asarray(mjm.body_quat[b], dtype=np.float32), device=dev)
+  return d
+
+
+def put_data(mjm, mjd, nworld: int = 1, nconmax: Optional[int] = None, nccdmax: Optional[int] = None, njmax: Optional[int] = None, njmax_nnz: Optional[int] = None, naconmax: Optional[int] = None, naccdmax: Optional[int] = None, device=None, m: Optional[types.Model] = None) -> types.Data:
+  """Moves one host state to the device, tiled over nworld worlds (io.py:1016-1240)."""
+  dev = _device(device)
+  if m is None:
+    m = put_model(mjm, device=dev)
+  if nconmax is None:
+    nconmax = _default_nconmax(mjm, mjd)
+  if njmax is None:
+    njmax = _default_njmax(mjm, mjd)
+  if nconmax < 0:
+    raise ValueError("nconmax must be >= 0")
+  if njmax < 0:
+    raise ValueError("njmax must be >= 0")
+  ncon = int(getattr(mjd, "ncon", 0))
+  if naconmax is None and ncon > nconmax:
+    raise ValueError(f"nconmax overflow (nconmax must be >= {ncon})")
+  if int(getattr(mjd, "nefc", 0)) > njmax:
+    raise ValueError(f"njmax overflow (njmax must be >= {mjd.nefc})")
+  d = _alloc_data(m, nworld, nconmax, njmax, naconmax, dev)
+
+  def tile(name, val, shape):
+    if val is None:
+      return
+    arr = np.asarray(val, dtype=np.float64).reshape(shape)
+    getattr(d, name)[:] = torch.as_tensor(arr.astype(np.float32), device=dev)
+
+  tile("time", np.full(nworld, float(np.asarray(mjd.time).reshape(-1)[0] if np.ndim(mjd.time) else mjd.time)), (nworld,))
+  tile("qpos", mjd.qpos, (mjm.nq,))
+  tile("qvel", mjd.qvel, (mjm.nv,))
+  tile("act", mjd.act, (mjm.na,))
+  tile("ctrl", mjd.ctrl, (mjm.nu,))
+  tile("qacc_warmstart", mjd.qacc_warmstart, (mjm.nv,))
+  tile("qfrc_applied", mjd.qfrc_applied, (mjm.nv,))
+  tile("xfrc_applied", mjd.xfrc_applied, (mjm.nbody, 6))
+  if mjm.nmocap:
+    tile("mocap_pos", mjd.mocap_pos, (mjm.nmocap, 3))
+    tile("mocap_quat", mjd.mocap_quat, (mjm.nmocap, 4))
+  if hasattr(mjd, "qacc"):
+    tile("qacc", mjd.qacc, (mjm.nv,))
+  d.solver_niter.fill_(int(np.asarray(getattr(mjd, "solver_niter", [0])).reshape(-1)[0]))
+  return d
+
+
+def get_data_into(result, mjm, d: types.Data, world_id: int = 0):
+  """Copies one world of `d` into a host MjData-like object (io.py:1243-1455)."""
+  if world_id < 0 or world_id >= d.nworld:
+    raise ValueError(f"world_id {world_id} out of range")
+  for name in ("qpos", "qvel", "act", "ctrl", "qacc_warmstart", "qfrc_applied", "qacc", "act_dot", "xpos", "xquat", "xipos", "xanchor",
+               "xaxis", "geom_xpos", "site_xpos", "cam_xpos", "light_xpos", "light_xdir", "subtree_com", "cdof", "cinert", "crb",
+               "actuator_length", "actuator_velocity", "actuator_force", "cvel", "cdof_dot", "qfrc_bias", "qfrc_spring", "qfrc_damper",
+               "qfrc_gravcomp", "qfrc_passive", "qfrc_actuator", "qfrc_smooth", "qacc_smooth", "qfrc_constraint", "cacc", "cfrc_int",
+               "cfrc_ext", "xfrc_applied", "mocap_pos", "mocap_quat", "energy"):
+    if hasattr(result, name) or isinstance(result, object):
+      val = getattr(d, name)[world_id].detach().cpu().numpy().astype(np.float64)
+      try:
+        cur = getattr(result, name)
+        cur[...] = val.reshape(np.shape(cur))
+      except AttributeError:
+        setattr(result, name, val)
+  for name in ("xmat", "ximat", "geom_xmat", "site_xmat", "cam_xmat"):
+    val = getattr(d, name)[world_id].detach().cpu().numpy().astype(np.float64).reshape(-1, 9)
+    try:
+      cur = getattr(result, name)
+      cur[...] = val.reshape(np.shape(cur))
+    except AttributeError:
+      setattr(result, name, val)
+  result.time = float(d.time[world_id])
+  nv = mjm.nv
+  result.qM_dense = d.qM[world_id, :nv, :nv].detach().cpu().numpy().astype(np.float64)
+  result.qLD_dense = d.qLD[world_id].detach().cpu().numpy().astype(np.float64)
+  # constraints of this world
+  nefc = int(d.nefc[world_id])
+  nrows = min(nefc, d.njmax)
+  result.nefc = nefc
+  result.efc_J = d.efc.J[world_id, :nrows, :nv].detach().cpu().numpy().astype(np.float64)
+  for f in ("pos", "margin", "D", "vel", "aref", "frictionloss", "force"):
+    setattr(result, "efc_" + f, getattr(d.efc, f)[world_id, :nrows].detach().cpu().numpy().astype(np.float64))
+  for f in ("type", "id", "state"):
+    setattr(result, "efc_" + f, getattr(d.efc, f)[world_id, :nrows].detach().cpu().numpy())
+  # contacts of this world, in pool order
+  nacon = min(int(d.nacon[0]), d.naconmax)
+  wid = d.contact.worldid[:nacon].detach().cpu().numpy()
+  sel = np.nonzero(wid == world_id)[0]
+  result.ncon = len(sel)
+  result.contact = types.Contact(**{
+    f: getattr(d.contact, f)[:nacon].detach().cpu().numpy()[sel]
+    for f in ("dist", "pos", "frame", "includemargin", "friction", "solref", "solreffriction", "solimp", "dim", "geom", "efc_address")
+  })
+  result.solver_niter = np.array([int(d.solver_niter[world_id])])
+  return result
+
+
+def reset_data(m: types.Model, d: types.Data, reset: Optional[torch.Tensor] = None):
+  """Resets worlds (all, or where `reset` is True) to the model's default state (io.py:1458)."""
+  mask = torch.ones(d.nworld, dtype=torch.bool, device=d.qpos.device) if reset is None else reset.to(torch.bool)
+  idx = torch.nonzero(mask).reshape(-1)
+  if idx.numel() == 0:
+    return
+  qpos0 = m.qpos0[0] if m.qpos0.shape[0] == 1 else m.qpos0[idx]
+  d.qpos[idx] = qpos0
+  for name in ("qvel", "act", "ctrl", "qacc_warmstart", "qfrc_applied", "xfrc_applied", "qacc", "act_dot"):
+    getattr(d, name)[idx] = 0
+  d.time[idx] = 0
+  d.solver_niter[idx] = 0
+
+
+def override_model(model, overrides: Sequence[str] | dict):
+  """Applies 'opt.solver=cg' style overrides (io.py:2498-2588) to an MjModel or Model."""
+  enums = {
+    "solver": types.SolverType,
+    "integrator": types.IntegratorType,
+    "cone": types.ConeType,
+    "jacobian": types.JacobianType,
+  }
+  items = overrides.items() if isinstance(overrides, dict) else [s.split("=", 1) for s in overrides]
+  for key, val in items:
+    key = key.strip()
+    val = str(val).strip()
+    obj = model
+    parts = key.split(".")
+    for p in parts[:-1]:
+      obj = getattr(obj, p)
+    leaf = parts[-1]
+    if leaf in enums:
+      v = int(enums[leaf][val.upper()])
+    elif leaf in ("iterations", "ls_iterations", "disableflags", "enableflags", "ccd_iterations"):
+      v = int(val)
+    else:
+      try:
+        v = float(val)
+      except ValueError:
+        v = val
+    cur = getattr(obj, leaf)
+    if isinstance(cur, torch.Tensor):
+      cur.fill_(float(v))
+    else:
+      setattr(obj, leaf, v)
+  return model

@@ -1,0 +1,1417 @@
+"""MJCF -> host model compiler (numpy, fp64).
+
+mujoco_warp's `put_model` consumes a compiled `mujoco.MjModel`
+(`mujoco_warp/_src/io.py:77-647`).  The MuJoCo C compiler is not available in
+this image, so this module compiles the MJCF subset used by the benchmark
+models into an `MjModel`-shaped host object with MuJoCo's field names and
+conventions:
+
+* defaults classes / childclass inheritance, degree->radian conversion;
+* body / joint / dof / geom / site / camera / light / actuator / keyframe tables;
+* inertia from geoms (mass = density * volume, capsule/sphere/box/... inertia,
+  principal axes), `fromto` geom frames;
+* derived tree arrays (rootid, weldid, dof_parentid, dof_Madr, M CSR layout);
+* qpos0-dependent constants computed exactly like the reference's
+  `set_const_0` (`io.py:2222-2407`): `stat.meaninertia`, `dof_invweight0`,
+  `body_invweight0`, `cam/light *0`, `actuator_acc0`.
+
+`put_model` also accepts a real `mujoco.MjModel` (duck typed) when the
+`mujoco` package is importable.
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import xml.etree.ElementTree as ET
+from typing import Optional
+
+import numpy as np
+
+from .types import (
+  BiasType,
+  CamLightType,
+  ConeType,
+  DisableBit,
+  DynType,
+  EnableBit,
+  GainType,
+  GeomType,
+  IntegratorType,
+  JacobianType,
+  JointType,
+  SolverType,
+  TrnType,
+)
+
+MJ_MINVAL = 1e-15
+
+_DISABLE_NAMES = {
+  "constraint": DisableBit.CONSTRAINT,
+  "equality": DisableBit.EQUALITY,
+  "frictionloss": DisableBit.FRICTIONLOSS,
+  "limit": DisableBit.LIMIT,
+  "contact": DisableBit.CONTACT,
+  "spring": DisableBit.SPRING,
+  "damper": DisableBit.DAMPER,
+  "gravity": DisableBit.GRAVITY,
+  "clampctrl": DisableBit.CLAMPCTRL,
+  "warmstart": DisableBit.WARMSTART,
+  "filterparent": DisableBit.FILTERPARENT,
+  "actuation": DisableBit.ACTUATION,
+  "refsafe": DisableBit.REFSAFE,
+  "sensor": DisableBit.SENSOR,
+  "midphase": DisableBit.MIDPHASE,
+  "eulerdamp": DisableBit.EULERDAMP,
+  "autoreset": DisableBit.AUTORESET,
+  "nativeccd": DisableBit.NATIVECCD,
+  "island": DisableBit.ISLAND,
+}
+_ENABLE_NAMES = {
+  "override": EnableBit.OVERRIDE,
+  "energy": EnableBit.ENERGY,
+  "fwdinv": EnableBit.FWDINV,
+  "invdiscrete": EnableBit.INVDISCRETE,
+  "multiccd": EnableBit.MULTICCD,
+}
+_GEOM_TYPES = {
+  "plane": GeomType.PLANE,
+  "hfield": GeomType.HFIELD,
+  "sphere": GeomType.SPHERE,
+  "capsule": GeomType.CAPSULE,
+  "ellipsoid": GeomType.ELLIPSOID,
+  "cylinder": GeomType.CYLINDER,
+  "box": GeomType.BOX,
+  "mesh": GeomType.MESH,
+  "sdf": GeomType.SDF,
+}
+_JOINT_TYPES = {"free": JointType.FREE, "ball": JointType.BALL, "slide": JointType.SLIDE, "hinge": JointType.HINGE}
+_CAMLIGHT_MODES = {
+  "fixed": CamLightType.FIXED,
+  "track": CamLightType.TRACK,
+  "trackcom": CamLightType.TRACKCOM,
+  "targetbody": CamLightType.TARGETBODY,
+  "targetbodycom": CamLightType.TARGETBODYCOM,
+}
+_INTEGRATORS = {
+  "euler": IntegratorType.EULER,
+  "rk4": IntegratorType.RK4,
+  "implicit": IntegratorType.IMPLICIT,
+  "implicitfast": IntegratorType.IMPLICITFAST,
+}
+_SOLVERS = {"pgs": SolverType.PGS, "cg": SolverType.CG, "newton": SolverType.NEWTON}
+_CONES = {"pyramidal": ConeType.PYRAMIDAL, "elliptic": ConeType.ELLIPTIC}
+_JACOBIANS = {"dense": JacobianType.DENSE, "sparse": JacobianType.SPARSE, "auto": JacobianType.AUTO}
+_ACTUATOR_TAGS = ("motor", "position", "velocity", "general", "intvelocity", "damper")
+
+# MuJoCo default element attribute values (MJCF reference defaults).
+_GEOM_DEFAULTS = dict(
+  type="sphere",
+  contype=1,
+  conaffinity=1,
+  condim=3,
+  group=0,
+  priority=0,
+  size=[0.0, 0.0, 0.0],
+  friction=[1.0, 0.005, 0.0001],
+  solmix=1.0,
+  solref=[0.02, 1.0],
+  solimp=[0.9, 0.95, 0.001, 0.5, 2.0],
+  margin=0.0,
+  gap=0.0,
+  density=1000.0,
+)
+_JOINT_DEFAULTS = dict(
+  type="hinge",
+  pos=[0.0, 0.0, 0.0],
+  axis=[0.0, 0.0, 1.0],
+  stiffness=0.0,
+  damping=0.0,
+  armature=0.0,
+  frictionloss=0.0,
+  springref=0.0,
+  ref=0.0,
+  margin=0.0,
+  solreflimit=[0.02, 1.0],
+  solimplimit=[0.9, 0.95, 0.001, 0.5, 2.0],
+  solreffriction=[0.02, 1.0],
+  solimpfriction=[0.9, 0.95, 0.001, 0.5, 2.0],
+  limited="auto",
+  range=[0.0, 0.0],
+  actuatorfrclimited="auto",
+  actuatorfrcrange=[0.0, 0.0],
+  actuatorgravcomp="false",
+)
+
+
+def _floats(s, n=None):
+  vals = [float(x) for x in str(s).split()]
+  if n is not None and len(vals) < n:
+    raise ValueError(f"expected {n} values, got '{s}'")
+  return vals
+
+
+def _merge_vec(default, given):
+  """MJCF partial vectors keep the trailing default values (e.g. friction='.7')."""
+  out = list(default)
+  for i, v in enumerate(given[: len(out)]):
+    out[i] = v
+  return out
+
+
+def quat_mul(a, b):
+  return np.array(
+    [
+      a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+      a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+      a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+      a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0],
+    ]
+  )
+
+
+def quat_to_mat(q):
+  w, x, y, z = q
+  return np.array(
+    [
+      [w * w + x * x - y * y - z * z, 2 * (x * y - w * z), 2 * (x * z + w * y)],
+      [2 * (x * y + w * z), w * w - x * x + y * y - z * z, 2 * (y * z - w * x)],
+      [2 * (x * z - w * y), 2 * (y * z + w * x), w * w - x * x - y * y + z * z],
+    ]
+  )
+
+
+def mat_to_quat(R):
+  """Rotation matrix -> unit quaternion (w first, w >= 0)."""
+  tr = R[0, 0] + R[1, 1] + R[2, 2]
+  if tr > 0:
+    s = math.sqrt(tr + 1.0) * 2
+    q = [0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s]
+  elif R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]:
+    s = math.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2]) * 2
+    q = [(R[2, 1] - R[1, 2]) / s, 0.25 * s, (R[0, 1] + R[1, 0]) / s, (R[0, 2] + R[2, 0]) / s]
+  elif R[1, 1] > R[2, 2]:
+    s = math.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2]) * 2
+    q = [(R[0, 2] - R[2, 0]) / s, (R[0, 1] + R[1, 0]) / s, 0.25 * s, (R[1, 2] + R[2, 1]) / s]
+  else:
+    s = math.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1]) * 2
+    q = [(R[1, 0] - R[0, 1]) / s, (R[0, 2] + R[2, 0]) / s, (R[1, 2] + R[2, 1]) / s, 0.25 * s]
+  q = np.array(q)
+  if q[0] < 0:
+    q = -q
+  return q / np.linalg.norm(q)
+
+
+def z2quat(vec):
+  """Minimal rotation taking +z to `vec` (MuJoCo mjuu_z2quat convention)."""
+  v = np.asarray(vec, dtype=float)
+  n = np.linalg.norm(v)
+  if n < MJ_MINVAL:
+    return np.array([1.0, 0, 0, 0])
+  v = v / n
+  axis = np.cross([0.0, 0.0, 1.0], v)
+  s = np.linalg.norm(axis)
+  if s < 1e-10:
+    if v[2] < 0:
+      return np.array([0.0, 1.0, 0.0, 0.0])
+    return np.array([1.0, 0, 0, 0])
+  axis = axis / s
+  ang = math.atan2(s, v[2])
+  return np.array([math.cos(ang / 2), *(axis * math.sin(ang / 2))])
+
+
+def rot_vec(q, v):
+  return quat_to_mat(q) @ np.asarray(v, dtype=float)
+
+
+class MjOption:
+  def __init__(self):
+    self.timestep = 0.002
+    self.impratio = 1.0
+    self.tolerance = 1e-8
+    self.ls_tolerance = 0.01
+    self.noslip_tolerance = 1e-6
+    self.ccd_tolerance = 1e-6
+    self.gravity = np.array([0.0, 0.0, -9.81])
+    self.wind = np.zeros(3)
+    self.magnetic = np.array([0.0, -0.5, 0.0])
+    self.density = 0.0
+    self.viscosity = 0.0
+    self.o_margin = 0.0
+    self.o_solref = np.array([0.02, 1.0])
+    self.o_solimp = np.array([0.9, 0.95, 0.001, 0.5, 2.0])
+    self.o_friction = np.array([1.0, 1.0, 0.005, 0.0001, 0.0001])
+    self.integrator = int(IntegratorType.EULER)
+    self.cone = int(ConeType.PYRAMIDAL)
+    self.jacobian = int(JacobianType.AUTO)
+    self.solver = int(SolverType.NEWTON)
+    self.iterations = 100
+    self.ls_iterations = 50
+    self.noslip_iterations = 0
+    self.ccd_iterations = 35
+    self.disableflags = 0
+    self.enableflags = 0
+
+
+class MjStatistic:
+  def __init__(self):
+    self.meaninertia = 1.0
+    self.meanmass = 1.0
+    self.meansize = 1.0
+    self.extent = 1.0
+    self.center = np.zeros(3)
+
+
+class MjModel:
+  """Host model with MuJoCo `mjModel` field names (subset used by the stepper)."""
+
+  def __init__(self):
+    self.opt = MjOption()
+    self.stat = MjStatistic()
+
+  def __repr__(self):
+    return f"MjModel(nq={self.nq}, nv={self.nv}, nu={self.nu}, nbody={self.nbody}, ngeom={self.ngeom})"
+
+
+class MjData:
+  """Host state container mirroring the `mujoco.MjData` fields consumed by put_data."""
+
+  def __init__(self, m: MjModel):
+    self.time = 0.0
+    self.qpos = m.qpos0.copy()
+    self.qvel = np.zeros(m.nv)
+    self.act = np.zeros(m.na)
+    self.qacc_warmstart = np.zeros(m.nv)
+    self.ctrl = np.zeros(m.nu)
+    self.qfrc_applied = np.zeros(m.nv)
+    self.xfrc_applied = np.zeros((m.nbody, 6))
+    self.mocap_pos = np.zeros((m.nmocap, 3))
+    self.mocap_quat = np.tile([1.0, 0, 0, 0], (m.nmocap, 1))
+    self.eq_active = m.eq_active0.copy() if m.neq else np.zeros(0, dtype=np.uint8)
+    self.qacc = np.zeros(m.nv)
+    self.act_dot = np.zeros(m.na)
+    self.ncon = 0
+    self.nefc = 0
+    self.solver_niter = np.zeros(1, dtype=int)
+    for i, bid in enumerate(np.nonzero(m.body_mocapid >= 0)[0]):
+      self.mocap_pos[m.body_mocapid[bid]] = m.body_pos[bid]
+      self.mocap_quat[m.body_mocapid[bid]] = m.body_quat[bid]
+
+
+def reset_data_keyframe(m: MjModel, d: MjData, key: int):
+  """mj_resetDataKeyframe for the fields the stepper consumes."""
+  fresh = MjData(m)
+  d.__dict__.update(fresh.__dict__)
+  d.time = float(m.key_time[key])
+  d.qpos[:] = m.key_qpos[key]
+  d.qvel[:] = m.key_qvel[key]
+  if m.na:
+    d.act[:] = m.key_act[key]
+  if m.nu:
+    d.ctrl[:] = m.key_ctrl[key]
+  if m.nmocap:
+    d.mocap_pos[:] = m.key_mpos[key].reshape(-1, 3)
+    d.mocap_quat[:] = m.key_mquat[key].reshape(-1, 4)
+
+
+# ---------------------------------------------------------------------------------------------
+# parsing
+# ---------------------------------------------------------------------------------------------
+
+
+class _Default:
+  def __init__(self, name, parent=None):
+    self.name = name
+    self.attrs = {k: dict(v) for k, v in (parent.attrs.items() if parent else [])}
+
+  def get(self, kind):
+    return self.attrs.setdefault(kind, {})
+
+
+class _Body:
+  def __init__(self, name, parent, childclass):
+    self.name = name
+    self.parent = parent
+    self.childclass = childclass
+    self.pos = np.zeros(3)
+    self.quat = np.array([1.0, 0, 0, 0])
+    self.inertial = None
+    self.mocap = False
+    self.gravcomp = 0.0
+    self.joints = []
+    self.geoms = []
+    self.sites = []
+    self.cams = []
+    self.lights = []
+    self.children = []
+
+
+def _orientation(attrs, angle_scale, eulerseq="xyz"):
+  """Frame orientation from quat / axisangle / euler / xyaxes / zaxis attributes."""
+  if "quat" in attrs:
+    q = np.array(_floats(attrs["quat"], 4))
+    return q / np.linalg.norm(q)
+  if "axisangle" in attrs:
+    v = _floats(attrs["axisangle"], 4)
+    axis = np.array(v[:3]) / np.linalg.norm(v[:3])
+    ang = v[3] * angle_scale
+    return np.array([math.cos(ang / 2), *(axis * math.sin(ang / 2))])
+  if "euler" in attrs:
+    e = np.array(_floats(attrs["euler"], 3)) * angle_scale
+    q = np.array([1.0, 0, 0, 0])
+    for i, ax in enumerate(eulerseq):
+      axis = {"x": [1, 0, 0], "y": [0, 1, 0], "z": [0, 0, 1], "X": [1, 0, 0], "Y": [0, 1, 0], "Z": [0, 0, 1]}[ax]
+      r = np.array([math.cos(e[i] / 2), *(np.array(axis) * math.sin(e[i] / 2))])
+      q = quat_mul(q, r) if ax.islower() else quat_mul(r, q)
+    return q / np.linalg.norm(q)
+  if "xyaxes" in attrs:
+    v = _floats(attrs["xyaxes"], 6)
+    x = np.array(v[:3]) / np.linalg.norm(v[:3])
+    y = np.array(v[3:6])
+    y = y - x * np.dot(x, y)
+    y = y / np.linalg.norm(y)
+    z = np.cross(x, y)
+    return mat_to_quat(np.stack([x, y, z], axis=1))
+  if "zaxis" in attrs:
+    return z2quat(_floats(attrs["zaxis"], 3))
+  return None
+
+
+class _Compiler:
+  def __init__(self, root: ET.Element, basedir: str):
+    self.root = root
+    self.basedir = basedir
+    self.angle_scale = math.pi / 180.0
+    self.eulerseq = "xyz"
+    self.autolimits = True
+    self.inertiafromgeom = "auto"
+    self.defaults = {}
+    self.m = MjModel()
+
+  # -- defaults ------------------------------------------------------------------------------
+  def _parse_default(self, elem, parent):
+    name = elem.get("class", "main")
+    d = _Default(name, parent)
+    for child in elem:
+      if child.tag == "default":
+        continue
+      kind = "actuator" if child.tag in _ACTUATOR_TAGS else child.tag
+      attrs = d.get(kind)
+      attrs.update(child.attrib)
+      if kind == "actuator":
+        attrs["__tag__"] = child.tag
+    self.defaults[name] = d
+    for child in elem:
+      if child.tag == "default":
+        self._parse_default(child, d)
+
+  def _resolve(self, kind, elem, childclass):
+    cls = elem.get("class", childclass or "main")
+    d = self.defaults.get(cls)
+    if d is None:
+      raise ValueError(f"unknown default class '{cls}'")
+    out = dict(d.attrs.get(kind, {}))
+    out.update(elem.attrib)
+    return out
+
+  # -- tree ----------------------------------------------------------------------------------
+  def _parse_body(self, elem, parent, childclass):
+    if elem.tag == "worldbody":
+      body = _Body("world", None, None)
+    else:
+      childclass = elem.get("childclass", childclass)
+      body = _Body(elem.get("name", ""), parent, childclass)
+      body.pos = np.array(_floats(elem.get("pos", "0 0 0"), 3))
+      q = _orientation(elem.attrib, self.angle_scale, self.eulerseq)
+      if q is not None:
+        body.quat = q
+      body.mocap = elem.get("mocap", "false") == "true"
+      body.gravcomp = float(elem.get("gravcomp", 0.0))
+    for child in elem:
+      tag = child.tag
+      if tag == "body":
+        body.children.append(self._parse_body(child, body, childclass))
+      elif tag == "joint":
+        body.joints.append(self._resolve("joint", child, childclass))
+      elif tag == "freejoint":
+        a = {"type": "free", "name": child.get("name", "")}
+        body.joints.append(a)
+      elif tag == "geom":
+        body.geoms.append(self._resolve("geom", child, childclass))
+      elif tag == "site":
+        body.sites.append(self._resolve("site", child, childclass))
+      elif tag == "camera":
+        body.cams.append(self._resolve("camera", child, childclass))
+      elif tag == "light":
+        body.lights.append(self._resolve("light", child, childclass))
+      elif tag == "inertial":
+        body.inertial = dict(child.attrib)
+      elif tag == "frame":
+        raise NotImplementedError("<frame> is not supported by the MJCF compiler")
+    return body
+
+  def _include(self, root):
+    """Inline <include file=...> elements (recursive)."""
+    for parent in list(root.iter()):
+      for i, child in enumerate(list(parent)):
+        if child.tag == "include":
+          path = os.path.join(self.basedir, child.get("file"))
+          sub = ET.parse(path).getroot()
+          self._include(sub)
+          parent.remove(child)
+          for j, c in enumerate(list(sub)):
+            parent.insert(i + j, c)
+
+  # -- main ----------------------------------------------------------------------------------
+  def compile(self) -> MjModel:
+    root = self.root
+    self._include(root)
+    m = self.m
+    m.model_name = root.get("model", "MuJoCo Model")
+
+    comp = root.find("compiler")
+    if comp is not None:
+      if comp.get("angle", "degree") == "radian":
+        self.angle_scale = 1.0
+      self.eulerseq = comp.get("eulerseq", "xyz")
+      self.autolimits = comp.get("autolimits", "true") == "true"
+      self.inertiafromgeom = comp.get("inertiafromgeom", "auto")
+
+    for opt in root.findall("option"):
+      self._parse_option(opt)
+
+    # defaults (top-level <default> is class 'main')
+    top = _Default("main")
+    self.defaults["main"] = top
+    for dflt in root.findall("default"):
+      for child in dflt:
+        if child.tag == "default":
+          self._parse_default(child, top)
+        else:
+          kind = "actuator" if child.tag in _ACTUATOR_TAGS else child.tag
+          top.get(kind).update(child.attrib)
+          if kind == "actuator":
+            top.get(kind)["__tag__"] = child.tag
+
+    world = _Body("world", None, None)
+    for wb in root.findall("worldbody"):
+      wbody = self._parse_body(wb, None, None)
+      world.joints += wbody.joints
+      world.geoms += wbody.geoms
+      world.sites += wbody.sites
+      world.cams += wbody.cams
+      world.lights += wbody.lights
+      for c in wbody.children:
+        c.parent = world
+        world.children.append(c)
+
+    # DFS pre-order body list
+    bodies = []
+
+    def visit(b):
+      bodies.append(b)
+      for c in b.children:
+        visit(c)
+
+    visit(world)
+    self.bodies = bodies
+    self._build_tables(root)
+    return m
+
+  def _parse_option(self, opt):
+    o = self.m.opt
+    a = opt.attrib
+    for k in ("timestep", "impratio", "tolerance", "ls_tolerance", "noslip_tolerance", "ccd_tolerance", "density", "viscosity", "o_margin"):
+      if k in a:
+        setattr(o, k, float(a[k]))
+    for k in ("iterations", "ls_iterations", "noslip_iterations", "ccd_iterations"):
+      if k in a:
+        setattr(o, k, int(a[k]))
+    for k in ("gravity", "wind", "magnetic"):
+      if k in a:
+        setattr(o, k, np.array(_floats(a[k], 3)))
+    if "integrator" in a:
+      o.integrator = int(_INTEGRATORS[a["integrator"].lower()])
+    if "solver" in a:
+      o.solver = int(_SOLVERS[a["solver"].lower()])
+    if "cone" in a:
+      o.cone = int(_CONES[a["cone"].lower()])
+    if "jacobian" in a:
+      o.jacobian = int(_JACOBIANS[a["jacobian"].lower()])
+    for flag in opt.findall("flag"):
+      for k, v in flag.attrib.items():
+        if k in _DISABLE_NAMES:
+          if v == "disable":
+            o.disableflags |= int(_DISABLE_NAMES[k])
+          else:
+            o.disableflags &= ~int(_DISABLE_NAMES[k])
+        elif k in _ENABLE_NAMES:
+          if v == "enable":
+            o.enableflags |= int(_ENABLE_NAMES[k])
+          else:
+            o.enableflags &= ~int(_ENABLE_NAMES[k])
+
+  # ---------------------------------------------------------------------------------------
+  def _build_tables(self, root):
+    m = self.m
+    bodies = self.bodies
+    nbody = len(bodies)
+    bid = {id(b): i for i, b in enumerate(bodies)}
+    m.nbody = nbody
+    m.body_names = [b.name for b in bodies]
+    m.body_parentid = np.array([bid[id(b.parent)] if b.parent is not None else 0 for b in bodies], dtype=np.int32)
+    m.body_pos = np.array([b.pos for b in bodies])
+    m.body_quat = np.array([b.quat for b in bodies])
+    m.body_gravcomp = np.array([b.gravcomp for b in bodies])
+
+    # mocap
+    mocapid = -np.ones(nbody, dtype=np.int32)
+    nmocap = 0
+    for i, b in enumerate(bodies):
+      if b.mocap:
+        mocapid[i] = nmocap
+        nmocap += 1
+    m.body_mocapid = mocapid
+    m.nmocap = nmocap
+
+    # joints / dofs
+    jnt_rows, dof_rows = [], []
+    body_jntadr = -np.ones(nbody, dtype=np.int32)
+    body_jntnum = np.zeros(nbody, dtype=np.int32)
+    body_dofadr = -np.ones(nbody, dtype=np.int32)
+    body_dofnum = np.zeros(nbody, dtype=np.int32)
+    nq = 0
+    for i, b in enumerate(bodies):
+      if b.joints:
+        body_jntadr[i] = len(jnt_rows)
+      body_jntnum[i] = len(b.joints)
+      ndof_b = 0
+      for ja in b.joints:
+        jtype = _JOINT_TYPES[ja.get("type", "hinge")]
+        free = ja.get("type") == "free" and len(ja) <= 2  # <freejoint/>: no defaults
+        get = (lambda k, d=None: ja.get(k, _JOINT_DEFAULTS.get(k) if d is None else d)) if not free else (lambda k, d=None: _JOINT_DEFAULTS.get(k) if d is None else d)
+        row = dict(
+          name=ja.get("name", ""),
+          type=int(jtype),
+          bodyid=i,
+          qposadr=nq,
+          dofadr=len(dof_rows),
+          pos=np.array(_floats(get("pos")) if isinstance(get("pos"), str) else get("pos"), dtype=float),
+          axis=np.array(_floats(get("axis")) if isinstance(get("axis"), str) else get("axis"), dtype=float),
+        )
+        nrm = np.linalg.norm(row["axis"])
+        row["axis"] = row["axis"] / nrm if nrm > 0 else np.array([0.0, 0.0, 1.0])
+
+        def fval(k):
+          v = get(k)
+          return float(v) if isinstance(v, str) else float(v)
+
+        def vval(k, n):
+          v = get(k)
+          given = _floats(v) if isinstance(v, str) else list(v)
+          return np.array(_merge_vec(_JOINT_DEFAULTS[k], given))[:n]
+
+        ascale = self.angle_scale if jtype in (JointType.HINGE, JointType.BALL) else 1.0
+        rng = get("range")
+        rng = (np.array(_floats(rng), dtype=float) if isinstance(rng, str) else np.array(rng, dtype=float)) * ascale
+        lim = get("limited")
+        if lim == "auto":
+          limited = bool(self.autolimits and ("range" in ja) and jtype != JointType.FREE)
+        else:
+          limited = lim == "true"
+        afl = get("actuatorfrclimited")
+        afr = get("actuatorfrcrange")
+        afr = np.array(_floats(afr)) if isinstance(afr, str) else np.array(afr, dtype=float)
+        if afl == "auto":
+          afl = bool(self.autolimits and "actuatorfrcrange" in ja)
+        else:
+          afl = afl == "true"
+        row.update(
+          stiffness=fval("stiffness"),
+          damping=fval("damping"),
+          armature=fval("armature"),
+          frictionloss=fval("frictionloss"),
+          springref=fval("springref") * (self.angle_scale if jtype == JointType.HINGE else 1.0),
+          ref=fval("ref") * (self.angle_scale if jtype == JointType.HINGE else 1.0),
+          margin=fval("margin"),
+          solref=vval("solreflimit", 2),
+          solimp=vval("solimplimit", 5),
+          solreffriction=vval("solreffriction", 2),
+          solimpfriction=vval("solimpfriction", 5),
+          limited=limited,
+          range=rng,
+          actfrclimited=afl,
+          actfrcrange=afr,
+          actgravcomp=get("actuatorgravcomp") == "true",
+        )
+        ndof = {JointType.FREE: 6, JointType.BALL: 3}.get(jtype, 1)
+        nqj = {JointType.FREE: 7, JointType.BALL: 4}.get(jtype, 1)
+        for k in range(ndof):
+          dof_rows.append(dict(bodyid=i, jntid=len(jnt_rows), **{kk: row[kk] for kk in ("armature", "damping", "frictionloss", "solreffriction", "solimpfriction")}))
+        ndof_b += ndof
+        nq += nqj
+        jnt_rows.append(row)
+      if ndof_b:
+        body_dofadr[i] = len(dof_rows) - ndof_b
+      body_dofnum[i] = ndof_b
+
+    njnt = len(jnt_rows)
+    nv = len(dof_rows)
+    m.njnt, m.nv, m.nq = njnt, nv, nq
+    m.body_jntadr, m.body_jntnum, m.body_dofadr, m.body_dofnum = body_jntadr, body_jntnum, body_dofadr, body_dofnum
+    m.jnt_names = [r["name"] for r in jnt_rows]
+    m.jnt_type = np.array([r["type"] for r in jnt_rows], dtype=np.int32)
+    m.jnt_bodyid = np.array([r["bodyid"] for r in jnt_rows], dtype=np.int32)
+    m.jnt_qposadr = np.array([r["qposadr"] for r in jnt_rows], dtype=np.int32)
+    m.jnt_dofadr = np.array([r["dofadr"] for r in jnt_rows], dtype=np.int32)
+    m.jnt_pos = np.array([r["pos"] for r in jnt_rows]).reshape(njnt, 3)
+    m.jnt_axis = np.array([r["axis"] for r in jnt_rows]).reshape(njnt, 3)
+    m.jnt_stiffness = np.array([r["stiffness"] for r in jnt_rows])
+    m.jnt_limited = np.array([r["limited"] for r in jnt_rows], dtype=bool)
+    m.jnt_range = np.array([r["range"] for r in jnt_rows]).reshape(njnt, 2)
+    m.jnt_margin = np.array([r["margin"] for r in jnt_rows])
+    m.jnt_solref = np.array([r["solref"] for r in jnt_rows]).reshape(njnt, 2)
+    m.jnt_solimp = np.array([r["solimp"] for r in jnt_rows]).reshape(njnt, 5)
+    m.jnt_actfrclimited = np.array([r["actfrclimited"] for r in jnt_rows], dtype=bool)
+    m.jnt_actfrcrange = np.array([r["actfrcrange"] for r in jnt_rows]).reshape(njnt, 2)
+    m.jnt_actgravcomp = np.array([r["actgravcomp"] for r in jnt_rows], dtype=np.int32)
+
+    m.dof_bodyid = np.array([r["bodyid"] for r in dof_rows], dtype=np.int32)
+    m.dof_jntid = np.array([r["jntid"] for r in dof_rows], dtype=np.int32)
+    m.dof_armature = np.array([r["armature"] for r in dof_rows])
+    m.dof_damping = np.array([r["damping"] for r in dof_rows])
+    m.dof_frictionloss = np.array([r["frictionloss"] for r in dof_rows])
+    m.dof_solref = np.array([r["solreffriction"] for r in dof_rows]).reshape(nv, 2)
+    m.dof_solimp = np.array([r["solimpfriction"] for r in dof_rows]).reshape(nv, 5)
+
+    # qpos0 / qpos_spring
+    qpos0 = np.zeros(nq)
+    qpos_spring = np.zeros(nq)
+    for j, r in enumerate(jnt_rows):
+      a = r["qposadr"]
+      if r["type"] == JointType.FREE:
+        b = bodies[r["bodyid"]]
+        qpos0[a : a + 3] = b.pos
+        qpos0[a + 3 : a + 7] = b.quat
+        qpos_spring[a : a + 7] = qpos0[a : a + 7]
+      elif r["type"] == JointType.BALL:
+        qpos0[a : a + 4] = [1, 0, 0, 0]
+        qpos_spring[a : a + 4] = [1, 0, 0, 0]
+      else:
+        qpos0[a] = r["ref"]
+        qpos_spring[a] = r["springref"]
+    m.qpos0 = qpos0
+    m.qpos_spring = qpos_spring
+
+    # body tree arrays
+    parent = m.body_parentid
+    rootid = np.zeros(nbody, dtype=np.int32)
+    weldid = np.zeros(nbody, dtype=np.int32)
+    for i in range(1, nbody):
+      rootid[i] = i if parent[i] == 0 else rootid[parent[i]]
+      weldid[i] = i if body_jntnum[i] > 0 else weldid[parent[i]]
+    m.body_rootid, m.body_weldid = rootid, weldid
+
+    # dof_parentid: previous dof along the kinematic chain
+    dof_parentid = -np.ones(nv, dtype=np.int32)
+    for i in range(nbody):
+      if body_dofnum[i] == 0:
+        continue
+      # last dof of nearest ancestor with dofs
+      p = parent[i]
+      prev = -1
+      while p > 0:
+        if body_dofnum[p] > 0:
+          prev = body_dofadr[p] + body_dofnum[p] - 1
+          break
+        p = parent[p]
+      for k in range(body_dofnum[i]):
+        dof_parentid[body_dofadr[i] + k] = prev
+        prev = body_dofadr[i] + k
+    m.dof_parentid = dof_parentid
+
+    # sparse M layout (MuJoCo dof_Madr: diagonal then ancestors)
+    dof_Madr = np.zeros(nv, dtype=np.int32)
+    nM = 0
+    for i in range(nv):
+      dof_Madr[i] = nM
+      j = i
+      while j >= 0:
+        nM += 1
+        j = dof_parentid[j]
+    m.dof_Madr = dof_Madr
+    m.nM = nM
+    # CSR lower triangle (ancestors ascending, diagonal last) used by the sparse LDL
+    M_rownnz = np.zeros(nv, dtype=np.int32)
+    M_rowadr = np.zeros(nv, dtype=np.int32)
+    colind, mapM2M = [], []
+    for i in range(nv):
+      anc = []
+      j = i
+      k = 0
+      while j >= 0:
+        anc.append((j, dof_Madr[i] + k))
+        j = dof_parentid[j]
+        k += 1
+      anc = anc[::-1]
+      M_rowadr[i] = len(colind)
+      M_rownnz[i] = len(anc)
+      for j, madr in anc:
+        colind.append(j)
+        mapM2M.append(madr)
+    m.M_rownnz, m.M_rowadr = M_rownnz, M_rowadr
+    m.M_colind = np.array(colind, dtype=np.int32)
+    m.mapM2M = np.array(mapM2M, dtype=np.int32)
+    m.nC = nM
+
+    self._build_geoms()
+    self._build_inertia()
+    self._build_sites_cams_lights()
+    self._build_actuators(root)
+    self._build_contact(root)
+    self._build_keys(root)
+    m.neq = 0
+    m.eq_active0 = np.zeros(0, dtype=np.uint8)
+    m.ntendon = 0
+    m.nsensor = 0
+    m.nsensordata = 0
+    m.nflex = 0
+    m.nhfield = 0
+    m.nmesh = 0
+    m.body_subtreemass = self._subtreemass()
+    set_const(m)
+
+  # ---------------------------------------------------------------------------------------
+  def _build_geoms(self):
+    m = self.m
+    rows = []
+    for i, b in enumerate(self.bodies):
+      for ga in b.geoms:
+        rows.append(self._geom(ga, i))
+    ng = len(rows)
+    m.ngeom = ng
+    m.geom_names = [r["name"] for r in rows]
+    m.geom_type = np.array([r["type"] for r in rows], dtype=np.int32)
+    m.geom_bodyid = np.array([r["bodyid"] for r in rows], dtype=np.int32)
+    m.geom_contype = np.array([r["contype"] for r in rows], dtype=np.int32)
+    m.geom_conaffinity = np.array([r["conaffinity"] for r in rows], dtype=np.int32)
+    m.geom_condim = np.array([r["condim"] for r in rows], dtype=np.int32)
+    m.geom_priority = np.array([r["priority"] for r in rows], dtype=np.int32)
+    m.geom_group = np.array([r["group"] for r in rows], dtype=np.int32)
+    m.geom_size = np.array([r["size"] for r in rows]).reshape(ng, 3)
+    m.geom_pos = np.array([r["pos"] for r in rows]).reshape(ng, 3)
+    m.geom_quat = np.array([r["quat"] for r in rows]).reshape(ng, 4)
+    m.geom_friction = np.array([r["friction"] for r in rows]).reshape(ng, 3)
+    m.geom_solmix = np.array([r["solmix"] for r in rows])
+    m.geom_solref = np.array([r["solref"] for r in rows]).reshape(ng, 2)
+    m.geom_solimp = np.array([r["solimp"] for r in rows]).reshape(ng, 5)
+    m.geom_margin = np.array([r["margin"] for r in rows])
+    m.geom_gap = np.array([r["gap"] for r in rows])
+    m.geom_rbound = np.array([r["rbound"] for r in rows])
+    m.geom_aabb = np.array([r["aabb"] for r in rows]).reshape(ng, 6)
+    m.geom_dataid = -np.ones(ng, dtype=np.int32)
+    m.geom_mass_ = np.array([r["mass"] for r in rows])
+    m.geom_inertia_ = np.array([r["inertia"] for r in rows]).reshape(ng, 3)
+    m.geom_rgba = np.tile([0.5, 0.5, 0.5, 1.0], (ng, 1))
+    body_geomadr = -np.ones(m.nbody, dtype=np.int32)
+    body_geomnum = np.zeros(m.nbody, dtype=np.int32)
+    for g, r in enumerate(rows):
+      b = r["bodyid"]
+      if body_geomnum[b] == 0:
+        body_geomadr[b] = g
+      body_geomnum[b] += 1
+    m.body_geomadr, m.body_geomnum = body_geomadr, body_geomnum
+
+  def _geom(self, ga, bodyid):
+    gtype = _GEOM_TYPES[ga.get("type", _GEOM_DEFAULTS["type"])]
+    if gtype in (GeomType.MESH, GeomType.HFIELD, GeomType.SDF):
+      raise NotImplementedError(f"geom type {gtype.name} not supported by the MJCF compiler")
+
+    def vec(k, n):
+      given = _floats(ga[k]) if k in ga else []
+      return np.array(_merge_vec(_GEOM_DEFAULTS[k], given))[:n]
+
+    size = vec("size", 3)
+    pos = np.array(_floats(ga.get("pos", "0 0 0"), 3))
+    quat = _orientation(ga, self.angle_scale, self.eulerseq)
+    quat = np.array([1.0, 0, 0, 0]) if quat is None else quat
+    if "fromto" in ga:
+      ft = np.array(_floats(ga["fromto"], 6))
+      a, b = ft[:3], ft[3:]
+      pos = 0.5 * (a + b)
+      quat = z2quat(b - a)
+      hl = 0.5 * np.linalg.norm(b - a)
+      if gtype in (GeomType.CAPSULE, GeomType.CYLINDER):
+        size[1] = hl
+      elif gtype == GeomType.BOX:
+        size[2] = hl
+      elif gtype == GeomType.ELLIPSOID:
+        size[2] = hl
+    r = size[0]
+    if gtype == GeomType.SPHERE:
+      vol = 4.0 / 3.0 * math.pi * r**3
+      rbound = r
+      aabb = [0, 0, 0, r, r, r]
+    elif gtype == GeomType.CAPSULE:
+      vol = math.pi * r * r * 2 * size[1] + 4.0 / 3.0 * math.pi * r**3
+      rbound = r + size[1]
+      aabb = [0, 0, 0, r, r, size[1] + r]
+    elif gtype == GeomType.CYLINDER:
+      vol = math.pi * r * r * 2 * size[1]
+      rbound = math.sqrt(r * r + size[1] ** 2)
+      aabb = [0, 0, 0, r, r, size[1]]
+    elif gtype == GeomType.BOX:
+      vol = 8 * size[0] * size[1] * size[2]
+      rbound = float(np.linalg.norm(size))
+      aabb = [0, 0, 0, size[0], size[1], size[2]]
+    elif gtype == GeomType.ELLIPSOID:
+      vol = 4.0 / 3.0 * math.pi * size[0] * size[1] * size[2]
+      rbound = float(np.max(size))
+      aabb = [0, 0, 0, size[0], size[1], size[2]]
+    elif gtype == GeomType.PLANE:
+      vol = 0.0
+      rbound = 0.0
+      aabb = [0, 0, 0, size[0], size[1], 0.0]
+    else:
+      raise NotImplementedError(gtype)
+    density = float(ga.get("density", _GEOM_DEFAULTS["density"]))
+    mass = float(ga["mass"]) if "mass" in ga else density * vol
+    inertia = _geom_inertia(gtype, size, mass)
+    return dict(
+      name=ga.get("name", ""),
+      type=int(gtype),
+      bodyid=bodyid,
+      contype=int(ga.get("contype", 1)),
+      conaffinity=int(ga.get("conaffinity", 1)),
+      condim=int(ga.get("condim", 3)),
+      priority=int(ga.get("priority", 0)),
+      group=int(ga.get("group", 0)),
+      size=size,
+      pos=pos,
+      quat=quat,
+      friction=vec("friction", 3),
+      solmix=float(ga.get("solmix", 1.0)),
+      solref=vec("solref", 2),
+      solimp=vec("solimp", 5),
+      margin=float(ga.get("margin", 0.0)),
+      gap=float(ga.get("gap", 0.0)),
+      rbound=rbound,
+      aabb=aabb,
+      mass=mass if gtype != GeomType.PLANE else 0.0,
+      inertia=inertia,
+    )
+
+  def _build_inertia(self):
+    """Body inertial frames from <inertial> or from geoms (MuJoCo inertiafromgeom='auto')."""
+    m = self.m
+    nb = m.nbody
+    m.body_mass = np.zeros(nb)
+    m.body_ipos = np.zeros((nb, 3))
+    m.body_iquat = np.tile([1.0, 0, 0, 0], (nb, 1))
+    m.body_inertia = np.zeros((nb, 3))
+    for i, b in enumerate(self.bodies):
+      if i == 0:
+        continue
+      if b.inertial is not None and self.inertiafromgeom != "true":
+        ia = b.inertial
+        m.body_mass[i] = float(ia["mass"])
+        m.body_ipos[i] = _floats(ia.get("pos", "0 0 0"), 3)
+        if "fullinertia" in ia:
+          f = _floats(ia["fullinertia"], 6)
+          I = np.array([[f[0], f[3], f[4]], [f[3], f[1], f[5]], [f[4], f[5], f[2]]])
+          w, V = _eig3(I)
+          iq = mat_to_quat(V)
+          m.body_iquat[i] = quat_mul(np.array([1.0, 0, 0, 0]), iq)
+          m.body_inertia[i] = w
+        else:
+          q = _orientation(ia, self.angle_scale, self.eulerseq)
+          m.body_iquat[i] = q if q is not None else [1, 0, 0, 0]
+          m.body_inertia[i] = _floats(ia["diaginertia"], 3)
+        continue
+      geoms = [g for g in range(m.ngeom) if m.geom_bodyid[g] == i and m.geom_type[g] != GeomType.PLANE]
+      if not geoms:
+        continue
+      mass = sum(m.geom_mass_[g] for g in geoms)
+      if mass < MJ_MINVAL:
+        continue
+      com = sum(m.geom_mass_[g] * m.geom_pos[g] for g in geoms) / mass
+      I = np.zeros((3, 3))
+      for g in geoms:
+        R = quat_to_mat(m.geom_quat[g])
+        I += R @ np.diag(m.geom_inertia_[g]) @ R.T
+        dvec = m.geom_pos[g] - com
+        I += m.geom_mass_[g] * (np.dot(dvec, dvec) * np.eye(3) - np.outer(dvec, dvec))
+      m.body_mass[i] = mass
+      m.body_ipos[i] = com
+      if len(geoms) == 1:
+        # single geom: inertial frame = geom frame (diagonal inertia in geom frame)
+        m.body_iquat[i] = m.geom_quat[geoms[0]]
+        m.body_inertia[i] = m.geom_inertia_[geoms[0]]
+      else:
+        w, V = _eig3(I)
+        m.body_iquat[i] = mat_to_quat(V)
+        m.body_inertia[i] = w
+
+  def _subtreemass(self):
+    m = self.m
+    st = m.body_mass.copy()
+    for i in range(m.nbody - 1, 0, -1):
+      st[m.body_parentid[i]] += st[i]
+    return st
+
+  def _build_sites_cams_lights(self):
+    m = self.m
+    srows, crows, lrows = [], [], []
+    for i, b in enumerate(self.bodies):
+      for sa in b.sites:
+        q = _orientation(sa, self.angle_scale, self.eulerseq)
+        srows.append(dict(bodyid=i, pos=_floats(sa.get("pos", "0 0 0"), 3), quat=q if q is not None else [1, 0, 0, 0], name=sa.get("name", "")))
+      for ca in b.cams:
+        q = _orientation(ca, self.angle_scale, self.eulerseq)
+        crows.append(
+          dict(
+            bodyid=i,
+            name=ca.get("name", ""),
+            mode=int(_CAMLIGHT_MODES[ca.get("mode", "fixed")]),
+            target=ca.get("target"),
+            pos=_floats(ca.get("pos", "0 0 0"), 3),
+            quat=q if q is not None else [1, 0, 0, 0],
+            fovy=float(ca.get("fovy", 45.0)),
+          )
+        )
+      for la in b.lights:
+        d = np.array(_floats(la.get("dir", "0 0 -1"), 3))
+        d = d / max(np.linalg.norm(d), MJ_MINVAL)
+        lrows.append(
+          dict(
+            bodyid=i,
+            name=la.get("name", ""),
+            mode=int(_CAMLIGHT_MODES[la.get("mode", "fixed")]),
+            target=la.get("target"),
+            pos=_floats(la.get("pos", "0 0 0"), 3),
+            dir=d,
+          )
+        )
+    name2body = {b.name: i for i, b in enumerate(self.bodies)}
+    m.nsite = len(srows)
+    m.site_names = [r["name"] for r in srows]
+    m.site_bodyid = np.array([r["bodyid"] for r in srows], dtype=np.int32)
+    m.site_pos = np.array([r["pos"] for r in srows]).reshape(-1, 3)
+    m.site_quat = np.array([r["quat"] for r in srows]).reshape(-1, 4)
+    m.ncam = len(crows)
+    m.cam_names = [r["name"] for r in crows]
+    m.cam_bodyid = np.array([r["bodyid"] for r in crows], dtype=np.int32)
+    m.cam_mode = np.array([r["mode"] for r in crows], dtype=np.int32)
+    m.cam_targetbodyid = np.array([name2body[r["target"]] if r["target"] else -1 for r in crows], dtype=np.int32)
+    m.cam_pos = np.array([r["pos"] for r in crows]).reshape(-1, 3)
+    m.cam_quat = np.array([r["quat"] for r in crows]).reshape(-1, 4)
+    m.cam_fovy = np.array([r["fovy"] for r in crows])
+    m.nlight = len(lrows)
+    m.light_names = [r["name"] for r in lrows]
+    m.light_bodyid = np.array([r["bodyid"] for r in lrows], dtype=np.int32)
+    m.light_mode = np.array([r["mode"] for r in lrows], dtype=np.int32)
+    m.light_targetbodyid = np.array([name2body[r["target"]] if r["target"] else -1 for r in lrows], dtype=np.int32)
+    m.light_pos = np.array([r["pos"] for r in lrows]).reshape(-1, 3)
+    m.light_dir = np.array([r["dir"] for r in lrows]).reshape(-1, 3)
+
+  def _build_actuators(self, root):
+    m = self.m
+    name2jnt = {n: i for i, n in enumerate(m.jnt_names) if n}
+    rows = []
+    for act in root.findall("actuator"):
+      for el in act:
+        if el.tag not in _ACTUATOR_TAGS:
+          raise NotImplementedError(f"actuator <{el.tag}> not supported")
+        cls = el.get("class", "main")
+        a = dict(self.defaults[cls].attrs.get("actuator", {}))
+        a.update(el.attrib)
+        tag = el.tag
+        gear = _merge_vec([1, 0, 0, 0, 0, 0], _floats(a.get("gear", "1")))
+        ctrlrange = _floats(a.get("ctrlrange", "0 0"), 2)
+        forcerange = _floats(a.get("forcerange", "0 0"), 2)
+        actrange = _floats(a.get("actrange", "0 0"), 2)
+
+        def limited(key, rkey):
+          v = a.get(key, "auto")
+          if v == "auto":
+            return bool(self.autolimits and rkey in a)
+          return v == "true"
+
+        gainprm = np.zeros(10)
+        biasprm = np.zeros(10)
+        dynprm = np.zeros(10)
+        dynprm[0] = 1.0
+        gaintype, biastype, dyntype = GainType.FIXED, BiasType.NONE, DynType.NONE
+        if tag == "motor":
+          gainprm[0] = 1.0
+        elif tag == "position":
+          kp = float(a.get("kp", 1.0))
+          kv = float(a.get("kv", 0.0))
+          gainprm[0] = kp
+          biastype = BiasType.AFFINE
+          biasprm[:3] = [0.0, -kp, -kv]
+          tc = float(a.get("timeconst", 0.0))
+          if tc > 0:
+            dyntype = DynType.FILTEREXACT
+            dynprm[0] = tc
+        elif tag == "velocity":
+          kv = float(a.get("kv", 1.0))
+          gainprm[0] = kv
+          biastype = BiasType.AFFINE
+          biasprm[:3] = [0.0, 0.0, -kv]
+        elif tag == "damper":
+          kv = float(a.get("kv", 1.0))
+          gaintype = GainType.AFFINE
+          gainprm[:3] = [0.0, 0.0, -kv]
+        elif tag == "intvelocity":
+          kp = float(a.get("kp", 1.0))
+          gainprm[0] = kp
+          biastype = BiasType.AFFINE
+          biasprm[:3] = [0.0, -kp, 0.0]
+          dyntype = DynType.INTEGRATOR
+        else:  # general
+          gaintype = {"fixed": GainType.FIXED, "affine": GainType.AFFINE, "muscle": GainType.MUSCLE, "user": GainType.USER}[a.get("gaintype", "fixed")]
+          biastype = {"none": BiasType.NONE, "affine": BiasType.AFFINE, "muscle": BiasType.MUSCLE, "user": BiasType.USER}[a.get("biastype", "none")]
+          dyntype = {"none": DynType.NONE, "integrator": DynType.INTEGRATOR, "filter": DynType.FILTER, "filterexact": DynType.FILTEREXACT, "muscle": DynType.MUSCLE, "user": DynType.USER}[a.get("dyntype", "none")]
+          gainprm[:] = _merge_vec([1] + [0] * 9, _floats(a.get("gainprm", "1")))
+          biasprm[:] = _merge_vec([0] * 10, _floats(a.get("biasprm", "0")))
+          dynprm[:] = _merge_vec([1] + [0] * 9, _floats(a.get("dynprm", "1")))
+        if "joint" in a:
+          trntype, trnid = TrnType.JOINT, [name2jnt[a["joint"]], -1]
+        elif "jointinparent" in a:
+          trntype, trnid = TrnType.JOINTINPARENT, [name2jnt[a["jointinparent"]], -1]
+        else:
+          raise NotImplementedError("only joint transmissions are supported by the MJCF compiler")
+        rows.append(
+          dict(
+            name=a.get("name", ""),
+            trntype=int(trntype),
+            trnid=trnid,
+            gear=gear,
+            gaintype=int(gaintype),
+            biastype=int(biastype),
+            dyntype=int(dyntype),
+            gainprm=gainprm,
+            biasprm=biasprm,
+            dynprm=dynprm,
+            ctrllimited=limited("ctrllimited", "ctrlrange"),
+            forcelimited=limited("forcelimited", "forcerange"),
+            actlimited=limited("actlimited", "actrange"),
+            ctrlrange=ctrlrange,
+            forcerange=forcerange,
+            actrange=actrange,
+            actearly=a.get("actearly", "false") == "true",
+          )
+        )
+    nu = len(rows)
+    m.nu = nu
+    m.actuator_names = [r["name"] for r in rows]
+    m.actuator_trntype = np.array([r["trntype"] for r in rows], dtype=np.int32)
+    m.actuator_trnid = np.array([r["trnid"] for r in rows], dtype=np.int32).reshape(nu, 2)
+    m.actuator_gear = np.array([r["gear"] for r in rows]).reshape(nu, 6)
+    m.actuator_gaintype = np.array([r["gaintype"] for r in rows], dtype=np.int32)
+    m.actuator_biastype = np.array([r["biastype"] for r in rows], dtype=np.int32)
+    m.actuator_dyntype = np.array([r["dyntype"] for r in rows], dtype=np.int32)
+    m.actuator_gainprm = np.array([r["gainprm"] for r in rows]).reshape(nu, 10)
+    m.actuator_biasprm = np.array([r["biasprm"] for r in rows]).reshape(nu, 10)
+    m.actuator_dynprm = np.array([r["dynprm"] for r in rows]).reshape(nu, 10)
+    m.actuator_ctrllimited = np.array([r["ctrllimited"] for r in rows], dtype=bool)
+    m.actuator_forcelimited = np.array([r["forcelimited"] for r in rows], dtype=bool)
+    m.actuator_actlimited = np.array([r["actlimited"] for r in rows], dtype=bool)
+    m.actuator_ctrlrange = np.array([r["ctrlrange"] for r in rows]).reshape(nu, 2)
+    m.actuator_forcerange = np.array([r["forcerange"] for r in rows]).reshape(nu, 2)
+    m.actuator_actrange = np.array([r["actrange"] for r in rows]).reshape(nu, 2)
+    m.actuator_actearly = np.array([r["actearly"] for r in rows], dtype=bool)
+    m.actuator_cranklength = np.zeros(nu)
+    m.actuator_lengthrange = np.zeros((nu, 2))
+    actadr = -np.ones(nu, dtype=np.int32)
+    actnum = np.zeros(nu, dtype=np.int32)
+    na = 0
+    for i, r in enumerate(rows):
+      if r["dyntype"] != DynType.NONE:
+        actadr[i] = na
+        actnum[i] = 1
+        na += 1
+    m.actuator_actadr, m.actuator_actnum, m.na = actadr, actnum, na
+
+  def _build_contact(self, root):
+    m = self.m
+    name2body = {b.name: i for i, b in enumerate(self.bodies)}
+    sigs = []
+    m.npair = 0
+    for c in root.findall("contact"):
+      for el in c:
+        if el.tag == "exclude":
+          b1, b2 = name2body[el.get("body1")], name2body[el.get("body2")]
+          b1, b2 = min(b1, b2), max(b1, b2)
+          sigs.append((b1 << 16) + b2)
+        elif el.tag == "pair":
+          raise NotImplementedError("<contact><pair> is not supported by the MJCF compiler yet")
+    m.exclude_signature = np.array(sigs, dtype=np.int32)
+    m.nexclude = len(sigs)
+
+  def _build_keys(self, root):
+    m = self.m
+    keys = []
+    for kf in root.findall("keyframe"):
+      for k in kf.findall("key"):
+        keys.append(k)
+    m.nkey = len(keys)
+    m.key_names = [k.get("name", "") for k in keys]
+    m.key_time = np.array([float(k.get("time", 0.0)) for k in keys])
+    m.key_qpos = np.array([_floats(k.get("qpos")) if k.get("qpos") else m.qpos0 for k in keys]).reshape(m.nkey, m.nq)
+    m.key_qvel = np.array([_floats(k.get("qvel")) if k.get("qvel") else np.zeros(m.nv) for k in keys]).reshape(m.nkey, m.nv)
+    m.key_act = np.array([_floats(k.get("act")) if k.get("act") else np.zeros(m.na) for k in keys]).reshape(m.nkey, m.na)
+    m.key_ctrl = np.array([_floats(k.get("ctrl")) if k.get("ctrl") else np.zeros(m.nu) for k in keys]).reshape(m.nkey, m.nu)
+    m.key_mpos = np.zeros((m.nkey, 3 * m.nmocap))
+    m.key_mquat = np.tile(np.tile([1.0, 0, 0, 0], m.nmocap), (m.nkey, 1))
+
+
+def _geom_inertia(gtype, size, mass):
+  """Principal moments of a solid geom of the given mass (MuJoCo mjCGeom inertia)."""
+  r = size[0]
+  if gtype == GeomType.SPHERE:
+    i = 2.0 * mass * r * r / 5.0
+    return np.array([i, i, i])
+  if gtype == GeomType.CAPSULE:
+    h = 2.0 * size[1]
+    sphere_mass = mass * 4.0 * r / (4.0 * r + 3.0 * h)
+    cyl_mass = mass - sphere_mass
+    i0 = cyl_mass * (3 * r * r + h * h) / 12.0
+    i2 = cyl_mass * r * r / 2.0
+    sph = 2.0 * sphere_mass * r * r / 5.0
+    i0 += sph + sphere_mass * h * (3 * r + 2 * h) / 8.0
+    i2 += sph
+    return np.array([i0, i0, i2])
+  if gtype == GeomType.CYLINDER:
+    h = 2.0 * size[1]
+    i0 = mass * (3 * r * r + h * h) / 12.0
+    return np.array([i0, i0, mass * r * r / 2.0])
+  if gtype == GeomType.BOX:
+    s = size
+    return np.array([mass * (s[1] ** 2 + s[2] ** 2) / 3.0, mass * (s[0] ** 2 + s[2] ** 2) / 3.0, mass * (s[0] ** 2 + s[1] ** 2) / 3.0])
+  if gtype == GeomType.ELLIPSOID:
+    s = size
+    return np.array([mass * (s[1] ** 2 + s[2] ** 2) / 5.0, mass * (s[0] ** 2 + s[2] ** 2) / 5.0, mass * (s[0] ** 2 + s[1] ** 2) / 5.0])
+  return np.zeros(3)
+
+
+def _eig3(I):
+  """Symmetric 3x3 eigendecomposition, eigenvalues descending, right-handed eigenvector frame."""
+  w, V = np.linalg.eigh(I)
+  order = np.argsort(-w)
+  w, V = w[order], V[:, order]
+  if np.linalg.det(V) < 0:
+    V[:, 2] = -V[:, 2]
+  return w, V
+
+
+# ---------------------------------------------------------------------------------------------
+# set_const: qpos0-dependent constants (reference io.py:2222-2407), fp64 host restatement
+# ---------------------------------------------------------------------------------------------
+
+
+def _kinematics_qpos0(m: MjModel):
+  """Forward kinematics + subtree com + cdof + composite inertia + dense qM at qpos0 (fp64)."""
+  nb, nv = m.nbody, m.nv
+  qpos = m.qpos0
+  xpos = np.zeros((nb, 3))
+  xquat = np.tile([1.0, 0, 0, 0], (nb, 1)).astype(float)
+  xanchor = np.zeros((m.njnt, 3))
+  xaxis = np.zeros((m.njnt, 3))
+  for b in range(1, nb):
+    p = m.body_parentid[b]
+    ja, jn = m.body_jntadr[b], m.body_jntnum[b]
+    if jn == 1 and m.jnt_type[ja] == JointType.FREE:
+      a = m.jnt_qposadr[ja]
+      xpos[b] = qpos[a : a + 3]
+      q = qpos[a + 3 : a + 7]
+      xquat[b] = q / np.linalg.norm(q)
+      xanchor[ja] = xpos[b]
+      xaxis[ja] = m.jnt_axis[ja]
+      continue
+    pos = rot_vec(xquat[p], m.body_pos[b]) + xpos[p]
+    quat = quat_mul(xquat[p], m.body_quat[b])
+    for j in range(ja, ja + jn) if jn else []:
+      a = m.jnt_qposadr[j]
+      xanchor[j] = rot_vec(quat, m.jnt_pos[j]) + pos
+      xaxis[j] = rot_vec(quat, m.jnt_axis[j])
+      t = m.jnt_type[j]
+      if t == JointType.BALL:
+        ql = qpos[a : a + 4] / np.linalg.norm(qpos[a : a + 4])
+        quat = quat_mul(quat, ql)
+        pos = xanchor[j] - rot_vec(quat, m.jnt_pos[j])
+      elif t == JointType.SLIDE:
+        pos = pos + xaxis[j] * (qpos[a] - m.qpos0[a])
+      elif t == JointType.HINGE:
+        ang = qpos[a] - m.qpos0[a]
+        ql = np.array([math.cos(ang / 2), *(m.jnt_axis[j] * math.sin(ang / 2))])
+        quat = quat_mul(quat, ql)
+        pos = xanchor[j] - rot_vec(quat, m.jnt_pos[j])
+    xpos[b] = pos
+    xquat[b] = quat / np.linalg.norm(quat)
+  xmat = np.array([quat_to_mat(q) for q in xquat])
+  xipos = np.array([xpos[b] + rot_vec(xquat[b], m.body_ipos[b]) for b in range(nb)])
+  ximat = np.array([quat_to_mat(quat_mul(xquat[b], m.body_iquat[b])) for b in range(nb)])
+  # subtree com
+  st = xipos * m.body_mass[:, None]
+  for b in range(nb - 1, 0, -1):
+    st[m.body_parentid[b]] += st[b]
+  subtree_com = np.zeros((nb, 3))
+  for b in range(nb):
+    if m.body_subtreemass[b] != 0:
+      subtree_com[b] = st[b] / m.body_subtreemass[b]
+  # cinert (6x6 spatial inertia about subtree com of root), cdof
+  cinert = np.zeros((nb, 6, 6))
+  for b in range(1, nb):
+    R = ximat[b]
+    Ib = R @ np.diag(m.body_inertia[b]) @ R.T
+    d = xipos[b] - subtree_com[m.body_rootid[b]]
+    mass = m.body_mass[b]
+    cd = _skew(d)
+    cinert[b, :3, :3] = Ib - mass * cd @ cd
+    cinert[b, :3, 3:] = mass * cd
+    cinert[b, 3:, :3] = -mass * cd
+    cinert[b, 3:, 3:] = mass * np.eye(3)
+  cdof = np.zeros((nv, 6))
+  for j in range(m.njnt):
+    b = m.jnt_bodyid[j]
+    da = m.jnt_dofadr[j]
+    off = subtree_com[m.body_rootid[b]] - xanchor[j]
+    t = m.jnt_type[j]
+    if t == JointType.FREE:
+      cdof[da : da + 3, 3:] = np.eye(3)
+      for k in range(3):
+        ax = xmat[b][:, k]
+        cdof[da + 3 + k] = np.concatenate([ax, np.cross(ax, off)])
+    elif t == JointType.BALL:
+      for k in range(3):
+        ax = xmat[b][:, k]
+        cdof[da + k] = np.concatenate([ax, np.cross(ax, off)])
+    elif t == JointType.SLIDE:
+      cdof[da] = np.concatenate([np.zeros(3), xaxis[j]])
+    else:
+      cdof[da] = np.concatenate([xaxis[j], np.cross(xaxis[j], off)])
+  crb = cinert.copy()
+  for b in range(nb - 1, 0, -1):
+    p = m.body_parentid[b]
+    if p > 0:
+      crb[p] += crb[b]
+  M = np.zeros((nv, nv))
+  for i in range(nv):
+    buf = crb[m.dof_bodyid[i]] @ cdof[i]
+    j = i
+    while j >= 0:
+      M[i, j] += cdof[j] @ buf
+      j = m.dof_parentid[j]
+    M[i, i] += m.dof_armature[i]
+  M = np.tril(M) + np.tril(M, -1).T
+  return dict(xpos=xpos, xquat=xquat, xmat=xmat, xipos=xipos, subtree_com=subtree_com, cdof=cdof, M=M)
+
+
+def _skew(v):
+  return np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
+
+
+def set_const(m: MjModel):
+  """Compute qpos0-dependent constants exactly as io.set_const_0 (io.py:2222-2407) does."""
+  nv, nb = m.nv, m.nbody
+  k = _kinematics_qpos0(m)
+  M = k["M"]
+  m.stat.meaninertia = float(np.trace(M) / nv) if nv else 1.0
+  Minv = np.linalg.inv(M) if nv else np.zeros((0, 0))
+  # dof_invweight0 (io.py:1802-1843)
+  diag = np.diag(Minv) if nv else np.zeros(0)
+  inv = np.zeros(nv)
+  for i in range(nv):
+    j = m.dof_jntid[i]
+    t, da = m.jnt_type[j], m.jnt_dofadr[j]
+    if t == JointType.FREE:
+      inv[i] = diag[da : da + 3].mean() if i < da + 3 else diag[da + 3 : da + 6].mean()
+    elif t == JointType.BALL:
+      inv[i] = diag[da : da + 3].mean()
+    else:
+      inv[i] = diag[i]
+  m.dof_invweight0 = inv
+  # body_invweight0 (io.py:1846-1956)
+  biw = np.zeros((nb, 2))
+  for b in range(1, nb):
+    if m.body_weldid[b] == 0 or nv == 0:
+      continue
+    bb = b
+    while bb > 0 and m.body_dofnum[bb] == 0:
+      bb = m.body_parentid[bb]
+    if bb == 0:
+      continue
+    off = k["xipos"][b] - k["subtree_com"][m.body_rootid[b]]
+    J = np.zeros((6, nv))
+    d = m.body_dofadr[bb] + m.body_dofnum[bb] - 1
+    while d >= 0:
+      ang, lin = k["cdof"][d, :3], k["cdof"][d, 3:]
+      J[:3, d] = lin + np.cross(ang, off)
+      J[3:, d] = ang
+      d = m.dof_parentid[d]
+    A = J @ Minv @ J.T
+    tr, rot = np.trace(A[:3, :3]) / 3.0, np.trace(A[3:, 3:]) / 3.0
+    if tr < MJ_MINVAL and rot > MJ_MINVAL:
+      tr = rot
+    elif rot < MJ_MINVAL and tr > MJ_MINVAL:
+      rot = tr
+    biw[b] = [tr, rot]
+  m.body_invweight0 = biw
+  # cameras / lights at qpos0 (fixed-frame placement), io.py:2005-2053
+  xpos, xquat, sc = k["xpos"], k["xquat"], k["subtree_com"]
+  m.cam_pos0 = np.zeros((m.ncam, 3))
+  m.cam_poscom0 = np.zeros((m.ncam, 3))
+  m.cam_mat0 = np.zeros((m.ncam, 9))
+  for c in range(m.ncam):
+    b = m.cam_bodyid[c]
+    cx = xpos[b] + rot_vec(xquat[b], m.cam_pos[c])
+    cm = quat_to_mat(quat_mul(xquat[b], m.cam_quat[c]))
+    m.cam_pos0[c] = cx - xpos[b]
+    t = m.cam_targetbodyid[c]
+    m.cam_poscom0[c] = cx - sc[t if t >= 0 else b]
+    m.cam_mat0[c] = cm.reshape(-1)
+  m.light_pos0 = np.zeros((m.nlight, 3))
+  m.light_poscom0 = np.zeros((m.nlight, 3))
+  m.light_dir0 = np.zeros((m.nlight, 3))
+  for l in range(m.nlight):
+    b = m.light_bodyid[l]
+    lx = xpos[b] + rot_vec(xquat[b], m.light_pos[l])
+    ld = rot_vec(xquat[b], m.light_dir[l])
+    m.light_pos0[l] = lx - xpos[b]
+    t = m.light_targetbodyid[l]
+    m.light_poscom0[l] = lx - sc[t if t >= 0 else b]
+    m.light_dir0[l] = ld
+  # actuator_acc0 = ||M^-1 moment|| (io.py:2367-2380); joint transmissions only
+  acc0 = np.zeros(m.nu)
+  for a in range(m.nu):
+    vec = np.zeros(nv)
+    j = m.actuator_trnid[a, 0]
+    t = m.jnt_type[j]
+    da = m.jnt_dofadr[j]
+    if t == JointType.FREE:
+      vec[da : da + 6] = m.actuator_gear[a]
+    elif t == JointType.BALL:
+      vec[da : da + 3] = m.actuator_gear[a, :3]
+    else:
+      vec[da] = m.actuator_gear[a, 0]
+    acc0[a] = np.linalg.norm(Minv @ vec)
+  m.actuator_acc0 = acc0
+
+
+def load_model_from_string(xml: str, basedir: str = ".") -> MjModel:
+  return _Compiler(ET.fromstring(xml), basedir).compile()
+
+
+def load_model(path: str) -> MjModel:
+  """Compile an MJCF file (analogue of `mujoco.MjModel.from_xml_path`)."""
+  root = ET.parse(path).getroot()
+  return _Compiler(root, os.path.dirname(os.path.abspath(path))).compile()
+
+
+def is_sparse(m) -> bool:
+  """Dense/sparse switch of the reference (io.py:67-74)."""
+  if m.opt.jacobian == JacobianType.AUTO:
+    return m.nv > 32
+  return m.opt.jacobian == JacobianType.SPARSE

@@ -1,0 +1,298 @@
+"""Enums, constants and the Model / Data containers of the MI355X stepper.
+
+Mirrors the public type surface of mujoco_warp (`mujoco_warp/_src/types.py`):
+enum names/values (`types.py:74-638`), the `Option` (`:706-772`), `Statistic`
+(`:776`), `Model` (`:833-1603`), `Contact` (`:1617-1655`), `Constraint`
+(`:1658-1699`) and `Data` (`:1702-1896`) dataclasses.  Array fields are
+`torch.Tensor`s on the ROCm device instead of `wp.array`s.  Batched model
+fields (`"*"` leading dim in the reference) keep the reference semantics: the
+leading dimension is 1 or nworld and is indexed `worldid % shape[0]`.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import enum
+from typing import Any, Callable, Optional
+
+MJ_MINVAL = 1e-15
+MJ_MAXVAL = 1e10
+MJ_MINIMP = 0.0001
+MJ_MAXIMP = 0.9999
+MJ_MAXCONPAIR = 50
+MJ_MINMU = 1e-5
+
+TILE_SIZE_JTDAJ_SPARSE = 16
+TILE_SIZE_JTDAJ_DENSE = 16
+
+
+class BroadphaseType(enum.IntEnum):
+  NXN = 0
+  SAP_TILE = 1
+  SAP_SEGMENTED = 2
+
+
+class BroadphaseFilter(enum.IntFlag):
+  PLANE = 1
+  SPHERE = 2
+  AABB = 4
+  OBB = 8
+
+
+class CamLightType(enum.IntEnum):
+  FIXED = 0
+  TRACK = 1
+  TRACKCOM = 2
+  TARGETBODY = 3
+  TARGETBODYCOM = 4
+
+
+class DisableBit(enum.IntFlag):
+  CONSTRAINT = 1 << 0
+  EQUALITY = 1 << 1
+  FRICTIONLOSS = 1 << 2
+  LIMIT = 1 << 3
+  CONTACT = 1 << 4
+  SPRING = 1 << 5
+  DAMPER = 1 << 6
+  GRAVITY = 1 << 7
+  CLAMPCTRL = 1 << 8
+  WARMSTART = 1 << 9
+  FILTERPARENT = 1 << 10
+  ACTUATION = 1 << 11
+  REFSAFE = 1 << 12
+  SENSOR = 1 << 13
+  MIDPHASE = 1 << 14
+  EULERDAMP = 1 << 15
+  AUTORESET = 1 << 16
+  NATIVECCD = 1 << 17
+  ISLAND = 1 << 18
+
+
+class EnableBit(enum.IntFlag):
+  OVERRIDE = 1 << 0
+  ENERGY = 1 << 1
+  FWDINV = 1 << 2
+  INVDISCRETE = 1 << 3
+  MULTICCD = 1 << 4
+
+
+class TrnType(enum.IntEnum):
+  JOINT = 0
+  JOINTINPARENT = 1
+  SLIDERCRANK = 2
+  TENDON = 3
+  SITE = 4
+  BODY = 5
+
+
+class DynType(enum.IntEnum):
+  NONE = 0
+  INTEGRATOR = 1
+  FILTER = 2
+  FILTEREXACT = 3
+  MUSCLE = 4
+  USER = 5
+
+
+class GainType(enum.IntEnum):
+  FIXED = 0
+  AFFINE = 1
+  MUSCLE = 2
+  USER = 3
+
+
+class BiasType(enum.IntEnum):
+  NONE = 0
+  AFFINE = 1
+  MUSCLE = 2
+  USER = 3
+
+
+class JointType(enum.IntEnum):
+  FREE = 0
+  BALL = 1
+  SLIDE = 2
+  HINGE = 3
+
+
+class ConeType(enum.IntEnum):
+  PYRAMIDAL = 0
+  ELLIPTIC = 1
+
+
+class IntegratorType(enum.IntEnum):
+  EULER = 0
+  RK4 = 1
+  IMPLICIT = 2
+  IMPLICITFAST = 3
+
+
+class GeomType(enum.IntEnum):
+  PLANE = 0
+  HFIELD = 1
+  SPHERE = 2
+  CAPSULE = 3
+  ELLIPSOID = 4
+  CYLINDER = 5
+  BOX = 6
+  MESH = 7
+  SDF = 8
+
+
+class SolverType(enum.IntEnum):
+  PGS = 0
+  CG = 1
+  NEWTON = 2
+
+
+class JacobianType(enum.IntEnum):
+  DENSE = 0
+  SPARSE = 1
+  AUTO = 2
+
+
+class ConstraintState(enum.IntEnum):
+  SATISFIED = 0
+  QUADRATIC = 1
+  LINEARNEG = 2
+  LINEARPOS = 3
+  CONE = 4
+
+
+class ConstraintType(enum.IntEnum):
+  EQUALITY = 0
+  FRICTION_DOF = 1
+  FRICTION_TENDON = 2
+  LIMIT_JOINT = 3
+  LIMIT_TENDON = 4
+  CONTACT_FRICTIONLESS = 5
+  CONTACT_PYRAMIDAL = 6
+  CONTACT_ELLIPTIC = 7
+
+
+class ContactType(enum.IntFlag):
+  CONSTRAINT = 1
+  SENSOR = 2
+
+
+class ObjType(enum.IntEnum):
+  UNKNOWN = 0
+  BODY = 1
+  XBODY = 2
+  JOINT = 3
+  DOF = 4
+  GEOM = 5
+  SITE = 6
+  CAMERA = 7
+
+
+class EqType(enum.IntEnum):
+  CONNECT = 0
+  WELD = 1
+  JOINT = 2
+  TENDON = 3
+  FLEX = 4
+
+
+class State(enum.IntFlag):
+  """mjtState bitflags used by get_state / set_state (types.py:598-638)."""
+
+  TIME = 1 << 0
+  QPOS = 1 << 1
+  QVEL = 1 << 2
+  ACT = 1 << 3
+  WARMSTART = 1 << 4
+  CTRL = 1 << 5
+  QFRC_APPLIED = 1 << 6
+  XFRC_APPLIED = 1 << 7
+  EQ_ACTIVE = 1 << 8
+  MOCAP_POS = 1 << 9
+  MOCAP_QUAT = 1 << 10
+  USERDATA = 1 << 11
+  PLUGIN = 1 << 12
+  NSTATE = 13
+  PHYSICS = QPOS | QVEL | ACT
+  FULLPHYSICS = TIME | PHYSICS | PLUGIN
+  USER = CTRL | QFRC_APPLIED | XFRC_APPLIED | EQ_ACTIVE | MOCAP_POS | MOCAP_QUAT | USERDATA
+  INTEGRATION = FULLPHYSICS | USER | WARMSTART
+
+
+@dataclasses.dataclass
+class Option:
+  """Physics options (types.py:706-772).  Batched fields are (nb,) tensors."""
+
+  timestep: Any = None
+  tolerance: Any = None
+  ls_tolerance: Any = None
+  ccd_tolerance: Any = None
+  density: Any = None
+  viscosity: Any = None
+  gravity: Any = None
+  wind: Any = None
+  magnetic: Any = None
+  impratio_invsqrt: Any = None
+  integrator: int = 0
+  cone: int = 0
+  solver: int = 2
+  jacobian: int = 2
+  iterations: int = 100
+  ls_iterations: int = 50
+  ccd_iterations: int = 35
+  disableflags: int = 0
+  enableflags: int = 0
+  # warp-only fields (io.py:187-199)
+  ls_parallel: bool = False
+  ls_parallel_min_step: float = 1e-6
+  broadphase: int = BroadphaseType.NXN
+  broadphase_filter: int = BroadphaseFilter.PLANE | BroadphaseFilter.SPHERE | BroadphaseFilter.OBB
+  graph_conditional: bool = True
+  run_collision_detection: bool = True
+  contact_sensor_maxmatch: int = 64
+
+
+@dataclasses.dataclass
+class Statistic:
+  meaninertia: Any = None
+
+
+@dataclasses.dataclass
+class Callback:
+  """User callbacks (types.py:810-830); the fused HIP path runs when all are None."""
+
+  control: Optional[Callable] = None
+  passive: Optional[Callable] = None
+  act_dyn: Optional[Callable] = None
+  act_gain: Optional[Callable] = None
+  act_bias: Optional[Callable] = None
+  contactfilter: Optional[Callable] = None
+
+
+class _Container:
+  """Attribute bag with a stable field order; used for Model / Data / Contact / Constraint."""
+
+  def __init__(self, **kw):
+    self.__dict__.update(kw)
+
+  def fields(self):
+    return list(self.__dict__.keys())
+
+  def __repr__(self):
+    names = ", ".join(self.__dict__.keys())
+    return f"{type(self).__name__}({names})"
+
+
+class Model(_Container):
+  """Device model.  Field names follow mujoco_warp `types.Model` (types.py:833-1603)."""
+
+
+class Data(_Container):
+  """Device data.  Field names follow mujoco_warp `types.Data` (types.py:1702-1896)."""
+
+
+class Contact(_Container):
+  """Global contact pool (types.py:1617-1655): arrays of length naconmax, filled [0, nacon)."""
+
+
+class Constraint(_Container):
+  """Per-world constraint rows (types.py:1658-1699): (nworld, njmax[_pad]) arrays."""

@@ -1,0 +1,1636 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY (see oracle.h header comment).
+ *
+ * Serial, per-world restatement of mujoco_warp's `step` (forward.py:1003-1018)
+ * for the primitive-geom, dense-Jacobian path: kinematics -> com_pos ->
+ * camlight -> crb/qM -> collision (NXN + primitive narrowphase) ->
+ * make_constraint -> transmission -> velocity -> passive -> rne -> actuation ->
+ * acceleration (Cholesky factor/solve) -> CG / Newton solver -> Euler.
+ * Every function cites the reference file:line it follows.  Worlds are
+ * independent; orc_step() runs them in an OpenMP loop (CPU baseline leg).
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MINVAL ((real)1e-15)
+#define MAXVAL ((real)1e10)
+#define MINIMP ((real)0.0001)
+#define MAXIMP ((real)0.9999)
+#define MINMU ((real)1e-5)
+
+enum { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
+enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6 };
+enum { DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16,
+       DSBL_SPRING = 32, DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512,
+       DSBL_FILTERPARENT = 1024, DSBL_ACTUATION = 2048, DSBL_REFSAFE = 4096, DSBL_EULERDAMP = 1 << 15 };
+enum { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
+enum { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3 };
+enum { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
+enum { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICITFAST = 3 };
+enum { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
+enum { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
+enum { BIAS_NONE = 0, BIAS_AFFINE = 1 };
+enum { TRN_JOINT = 0, TRN_JOINTINPARENT = 1 };
+enum { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
+
+/* =============================================================================================
+ * math helpers (mujoco_warp/_src/math.py)
+ * ============================================================================================= */
+static inline real dot3(const real* a, const real* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void cross3(real* r, const real* a, const real* b) {
+  real t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static inline real clampr(real x, real lo, real hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static inline real maxr(real a, real b) { return a > b ? a : b; }
+static inline real minr(real a, real b) { return a < b ? a : b; }
+static inline real safe_div(real x, real y) { return x / (y != 0 ? y : MINVAL); } /* math.py:317-319 */
+
+/* wp.normalize: zero vector stays zero */
+static inline void normalize3(real* v) {
+  real n = sqrt(dot3(v, v));
+  if (n > 0) { v[0] /= n; v[1] /= n; v[2] /= n; } else { v[0] = v[1] = v[2] = 0; }
+}
+static inline void normalize4(real* q) {
+  real n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n > 0) { q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n; } else { q[0] = q[1] = q[2] = q[3] = 0; }
+}
+
+/* math.py:23-30 */
+static void mul_quat(real* r, const real* u, const real* v) {
+  real t0 = u[0] * v[0] - u[1] * v[1] - u[2] * v[2] - u[3] * v[3];
+  real t1 = u[0] * v[1] + u[1] * v[0] + u[2] * v[3] - u[3] * v[2];
+  real t2 = u[0] * v[2] - u[1] * v[3] + u[2] * v[0] + u[3] * v[1];
+  real t3 = u[0] * v[3] + u[1] * v[2] - u[2] * v[1] + u[3] * v[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+
+/* math.py:44-49 */
+static void rot_vec_quat(real* r, const real* vec, const real* q) {
+  real s = q[0], u[3] = {q[1], q[2], q[3]}, c[3];
+  real uv = dot3(u, vec), uu = dot3(u, u);
+  cross3(c, u, vec);
+  real t[3];
+  for (int i = 0; i < 3; i++) t[i] = 2 * (uv * u[i]) + (s * s - uu) * vec[i] + 2 * s * c[i];
+  r[0] = t[0]; r[1] = t[1]; r[2] = t[2];
+}
+
+/* math.py:52-56 */
+static void axis_angle_to_quat(real* q, const real* axis, real angle) {
+  real s = sin(angle * (real)0.5), c = cos(angle * (real)0.5);
+  q[0] = c; q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+}
+
+/* math.py:59-83 (row-major 3x3) */
+static void quat_to_mat(real* m, const real* q) {
+  real q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  real q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3], q22 = q[2] * q[2];
+  real q23 = q[2] * q[3], q33 = q[3] * q[3];
+  m[0] = q00 + q11 - q22 - q33; m[1] = 2 * (q12 - q03); m[2] = 2 * (q13 + q02);
+  m[3] = 2 * (q12 + q03); m[4] = q00 - q11 + q22 - q33; m[5] = 2 * (q23 - q01);
+  m[6] = 2 * (q13 - q02); m[7] = 2 * (q23 + q01); m[8] = q00 - q11 - q22 + q33;
+}
+
+/* math.py:120-130 mju_mulInertVec */
+static void inert_vec(real* r, const real* i, const real* v) {
+  real t[6];
+  t[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  t[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  t[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  t[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  t[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  t[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+  memcpy(r, t, sizeof(t));
+}
+
+/* math.py:133-144 */
+static void motion_cross(real* r, const real* u, const real* v) {
+  real a[3], b[3], c[3];
+  cross3(a, u, v);
+  cross3(b, u + 3, v);
+  cross3(c, u, v + 3);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+
+/* math.py:147-158 */
+static void motion_cross_force(real* r, const real* v, const real* f) {
+  real a[3], b[3], c[3];
+  cross3(a, v, f);
+  cross3(b, v + 3, f + 3);
+  cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+
+/* math.py:161-174 */
+static void quat_to_vel(real* r, const real* q) {
+  real axis[3] = {q[1], q[2], q[3]};
+  real s = sqrt(dot3(axis, axis));
+  if (s == 0) { r[0] = r[1] = r[2] = 0; return; }
+  real speed = 2 * atan2(s, q[0]);
+  if (speed > (real)M_PI) speed -= 2 * (real)M_PI;
+  for (int i = 0; i < 3; i++) r[i] = axis[i] * speed / s;
+}
+
+/* math.py:177-185 */
+static void quat_sub(real* r, const real* qa, const real* qb) {
+  real qneg[4] = {qb[0], -qb[1], -qb[2], -qb[3]}, qdif[4];
+  mul_quat(qdif, qneg, qa);
+  quat_to_vel(r, qdif);
+}
+
+/* math.py:188-199 */
+static void quat_integrate(real* res, const real* qin, const real* vin, real dt) {
+  real v[3] = {vin[0], vin[1], vin[2]};
+  real n = sqrt(dot3(v, v));
+  normalize3(v);
+  real qr[4], q[4] = {qin[0], qin[1], qin[2], qin[3]};
+  axis_angle_to_quat(qr, v, dt * n);
+  normalize4(q);
+  mul_quat(res, q, qr);
+  normalize4(res);
+}
+
+/* math.py:202-213 */
+static void orthogonals(real* b, real* c, const real* a) {
+  int usey = (-0.5 < a[1]) && (a[1] < 0.5);
+  b[0] = 0; b[1] = usey ? 1 : 0; b[2] = usey ? 0 : 1;
+  real d = dot3(a, b);
+  for (int i = 0; i < 3; i++) b[i] -= a[i] * d;
+  normalize3(b);
+  if (sqrt(dot3(a, a)) == 0) b[0] = b[1] = b[2] = 0;
+  cross3(c, a, b);
+}
+
+/* math.py:246-257: rows = (normal, tangent1, tangent2) */
+static void make_frame(real* f, const real* ain) {
+  real a[3] = {ain[0], ain[1], ain[2]}, b[3], c[3];
+  normalize3(a);
+  orthogonals(b, c, a);
+  f[0] = a[0]; f[1] = a[1]; f[2] = a[2];
+  f[3] = b[0]; f[4] = b[1]; f[5] = b[2];
+  f[6] = c[0]; f[7] = c[1]; f[8] = c[2];
+}
+
+/* math.py:268-281 */
+static void closest_segment_point(real* r, const real* a, const real* b, const real* pt) {
+  real ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, pa[3] = {pt[0] - a[0], pt[1] - a[1], pt[2] - a[2]};
+  real t = dot3(pa, ab) / (dot3(ab, ab) + (real)1e-6);
+  t = clampr(t, 0, 1);
+  for (int i = 0; i < 3; i++) r[i] = a[i] + t * ab[i];
+}
+
+static real closest_segment_point_and_dist(real* r, const real* a, const real* b, const real* pt) {
+  closest_segment_point(r, a, b, pt);
+  real d[3] = {pt[0] - r[0], pt[1] - r[1], pt[2] - r[2]};
+  return dot3(d, d);
+}
+
+static real normalize_with_norm(real* r, const real* x) {
+  real n = sqrt(dot3(x, x));
+  if (n == 0) { r[0] = x[0]; r[1] = x[1]; r[2] = x[2]; return 0; }
+  r[0] = x[0] / n; r[1] = x[1] / n; r[2] = x[2] / n;
+  return n;
+}
+
+/* math.py:284-314 */
+void orc_closest_segment_to_segment_points(const real* a0, const real* a1, const real* b0, const real* b1,
+                                           real* best_a, real* best_b) {
+  real da[3] = {a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2]}, db[3] = {b1[0] - b0[0], b1[1] - b0[1], b1[2] - b0[2]};
+  real dir_a[3], dir_b[3];
+  real len_a = normalize_with_norm(dir_a, da), len_b = normalize_with_norm(dir_b, db);
+  real ha = len_a * (real)0.5, hb = len_b * (real)0.5;
+  real am[3], bm[3], tr[3];
+  for (int i = 0; i < 3; i++) { am[i] = a0[i] + dir_a[i] * ha; bm[i] = b0[i] + dir_b[i] * hb; tr[i] = am[i] - bm[i]; }
+  real dadb = dot3(dir_a, dir_b), dat = dot3(dir_a, tr), dbt = dot3(dir_b, tr);
+  real denom = 1 - dadb * dadb;
+  real ota = (-dat + dadb * dbt) / (denom + (real)1e-6);
+  real otb = dbt + ota * dadb;
+  real ta = clampr(ota, -ha, ha), tb = clampr(otb, -hb, hb);
+  real ba[3], bb[3], na[3], nb[3];
+  for (int i = 0; i < 3; i++) { ba[i] = am[i] + dir_a[i] * ta; bb[i] = bm[i] + dir_b[i] * tb; }
+  real d1 = closest_segment_point_and_dist(na, a0, a1, bb);
+  real d2 = closest_segment_point_and_dist(nb, b0, b1, ba);
+  if (d1 < d2) { memcpy(best_a, na, 3 * sizeof(real)); memcpy(best_b, bb, 3 * sizeof(real)); }
+  else { memcpy(best_a, ba, 3 * sizeof(real)); memcpy(best_b, nb, 3 * sizeof(real)); }
+}
+
+/* math.py:322-333 */
+int orc_upper_tri_index(int n, int i, int j) { return (i * (2 * n - i - 3)) / 2 + j - 1; }
+int orc_upper_trid_index(int n, int i, int j) {
+  if (j < i) { int t = i; i = j; j = t; }
+  return (i * (2 * n - i - 1)) / 2 + j;
+}
+
+/* util_misc.py:59-73 */
+real orc_halton(int index, int base) {
+  int n0 = index;
+  real b = (real)base, f = (real)1 / b, hn = 0;
+  while (n0 > 0) {
+    int n1 = n0 / base;
+    int r = n0 - n1 * base;
+    hn += f * (real)r;
+    f /= b;
+    n0 = n1;
+  }
+  return hn;
+}
+
+/* benchmark.py:41-83 (world ids are global: worldid = world_offset + w) */
+void orc_ctrl_noise(const orc_model* m, real* ctrl, const real* center, int ncenter, int step, real std,
+                    real rate_, int nworld, int world_offset) {
+  for (int w = 0; w < nworld; w++) {
+    int worldid = world_offset + w;
+    for (int a = 0; a < m->nu; a++) {
+      real rate = exp(-m->opt_timestep / rate_);
+      real scale = std * sqrt(1 - rate * rate);
+      real midpoint = 0, halfrange = 1;
+      const real* cr = m->actuator_ctrlrange + 2 * a;
+      if (m->actuator_ctrllimited[a]) { midpoint = (real)0.5 * (cr[1] + cr[0]); halfrange = (real)0.5 * (cr[1] - cr[0]); }
+      if (ncenter > 0) midpoint = center[a];
+      real* c = ctrl + (size_t)w * m->nu + a;
+      real v = rate * (*c) + (1 - rate) * midpoint;
+      v += scale * halfrange * (2 * orc_halton((step + 1) * (worldid + 1), a + 2) - 1);
+      if (m->actuator_ctrllimited[a]) v = clampr(v, cr[0], cr[1]);
+      *c = v;
+    }
+  }
+}
+
+/* =============================================================================================
+ * per-world view
+ * ============================================================================================= */
+static void world_view(const orc_model* m, const orc_data* b, int w, orc_data* o) {
+  int nq = m->nq, nv = m->nv, nu = m->nu, na = m->na, nbody = m->nbody, njnt = m->njnt;
+  int ngeom = m->ngeom, nsite = m->nsite, ncam = m->ncam, nlight = m->nlight, nmocap = m->nmocap;
+  int njmax = b->njmax, nconmax = b->nconmax;
+  (void)nq; (void)nv; (void)nu; (void)na; (void)nbody; (void)njnt; (void)ngeom; (void)nsite; (void)ncam;
+  (void)nlight; (void)nmocap; (void)njmax; (void)nconmax;
+  o->njmax = njmax;
+  o->nconmax = nconmax;
+#define ORC_OFF(name, n) o->name = b->name + (size_t)w * (size_t)(n);
+  ORC_DATA_REAL_ARRAYS(ORC_OFF)
+  ORC_DATA_INT_ARRAYS(ORC_OFF)
+#undef ORC_OFF
+}
+
+/* =============================================================================================
+ * smooth.py
+ * ============================================================================================= */
+
+/* smooth.py:44-143 (_kinematics_branch) + :146-224 (inertial frames, matrices, geoms, sites) */
+static void kinematics(const orc_model* m, orc_data* d) {
+  real* xpos = d->xpos;
+  real* xquat = d->xquat;
+  /* world body */
+  xpos[0] = xpos[1] = xpos[2] = 0;
+  xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
+  for (int b = 1; b < m->nbody; b++) {
+    int pid = m->body_parentid[b];
+    int jntadr = m->body_jntadr[b], jntnum = m->body_jntnum[b];
+    if (jntnum == 1 && m->jnt_type[jntadr] == JNT_FREE) {
+      int qa = m->jnt_qposadr[jntadr];
+      real q[4] = {d->qpos[qa + 3], d->qpos[qa + 4], d->qpos[qa + 5], d->qpos[qa + 6]};
+      normalize4(q);
+      for (int i = 0; i < 3; i++) xpos[3 * b + i] = d->qpos[qa + i];
+      memcpy(xquat + 4 * b, q, sizeof(q));
+      for (int i = 0; i < 3; i++) { d->xanchor[3 * jntadr + i] = d->qpos[qa + i]; d->xaxis[3 * jntadr + i] = m->jnt_axis[3 * jntadr + i]; }
+      continue;
+    }
+    real pos[3], quat[4];
+    int mocapid = m->body_mocapid[b];
+    if (mocapid >= 0) {
+      memcpy(pos, d->mocap_pos + 3 * mocapid, 3 * sizeof(real));
+      memcpy(quat, d->mocap_quat + 4 * mocapid, 4 * sizeof(real));
+    } else {
+      memcpy(pos, m->body_pos + 3 * b, 3 * sizeof(real));
+      memcpy(quat, m->body_quat + 4 * b, 4 * sizeof(real));
+    }
+    if (pid >= 0) {
+      real t[3];
+      rot_vec_quat(t, pos, xquat + 4 * pid);
+      for (int i = 0; i < 3; i++) pos[i] = t[i] + xpos[3 * pid + i];
+      mul_quat(quat, xquat + 4 * pid, quat);
+    }
+    for (int k = 0; k < jntnum; k++) {
+      int j = jntadr + k;
+      int qa = m->jnt_qposadr[j];
+      const real* axis = m->jnt_axis + 3 * j;
+      const real* jpos = m->jnt_pos + 3 * j;
+      real xanchor[3], xaxis[3], t[3];
+      rot_vec_quat(t, jpos, quat);
+      for (int i = 0; i < 3; i++) xanchor[i] = t[i] + pos[i];
+      rot_vec_quat(xaxis, axis, quat);
+      int jt = m->jnt_type[j];
+      if (jt == JNT_BALL) {
+        real ql[4] = {d->qpos[qa], d->qpos[qa + 1], d->qpos[qa + 2], d->qpos[qa + 3]};
+        normalize4(ql);
+        mul_quat(quat, quat, ql);
+        rot_vec_quat(t, jpos, quat);
+        for (int i = 0; i < 3; i++) pos[i] = xanchor[i] - t[i];
+      } else if (jt == JNT_SLIDE) {
+        real dq = d->qpos[qa] - m->qpos0[qa];
+        for (int i = 0; i < 3; i++) pos[i] += xaxis[i] * dq;
+      } else if (jt == JNT_HINGE) {
+        real ql[4];
+        axis_angle_to_quat(ql, axis, d->qpos[qa] - m->qpos0[qa]);
+        mul_quat(quat, quat, ql);
+        rot_vec_quat(t, jpos, quat);
+        for (int i = 0; i < 3; i++) pos[i] = xanchor[i] - t[i];
+      }
+      memcpy(d->xanchor + 3 * j, xanchor, sizeof(xanchor));
+      memcpy(d->xaxis + 3 * j, xaxis, sizeof(xaxis));
+    }
+    normalize4(quat);
+    memcpy(xpos + 3 * b, pos, sizeof(pos));
+    memcpy(xquat + 4 * b, quat, sizeof(quat));
+  }
+  for (int b = 0; b < m->nbody; b++) {
+    real q[4], t[3];
+    quat_to_mat(d->xmat + 9 * b, xquat + 4 * b);
+    rot_vec_quat(t, m->body_ipos + 3 * b, xquat + 4 * b);
+    for (int i = 0; i < 3; i++) d->xipos[3 * b + i] = xpos[3 * b + i] + t[i];
+    mul_quat(q, xquat + 4 * b, m->body_iquat + 4 * b);
+    quat_to_mat(d->ximat + 9 * b, q);
+  }
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = m->geom_bodyid[g];
+    /* smooth.py:195-198: static world geoms are computed once (at put_data) */
+    if (m->body_weldid[b] == 0 && m->body_mocapid[m->body_rootid[b]] == -1) {
+      real q[4], t[3];
+      /* world frame is identity: pose equals the model pose */
+      rot_vec_quat(t, m->geom_pos + 3 * g, xquat + 4 * b);
+      for (int i = 0; i < 3; i++) d->geom_xpos[3 * g + i] = xpos[3 * b + i] + t[i];
+      mul_quat(q, xquat + 4 * b, m->geom_quat + 4 * g);
+      quat_to_mat(d->geom_xmat + 9 * g, q);
+      continue;
+    }
+    real q[4], t[3];
+    rot_vec_quat(t, m->geom_pos + 3 * g, xquat + 4 * b);
+    for (int i = 0; i < 3; i++) d->geom_xpos[3 * g + i] = xpos[3 * b + i] + t[i];
+    mul_quat(q, xquat + 4 * b, m->geom_quat + 4 * g);
+    quat_to_mat(d->geom_xmat + 9 * g, q);
+  }
+  for (int s = 0; s < m->nsite; s++) {
+    int b = m->site_bodyid[s];
+    real q[4], t[3];
+    rot_vec_quat(t, m->site_pos + 3 * s, xquat + 4 * b);
+    for (int i = 0; i < 3; i++) d->site_xpos[3 * s + i] = xpos[3 * b + i] + t[i];
+    mul_quat(q, xquat + 4 * b, m->site_quat + 4 * s);
+    quat_to_mat(d->site_xmat + 9 * s, q);
+  }
+}
+
+/* smooth.py:463-632 (subtree com, cinert, cdof) */
+static void com_pos(const orc_model* m, orc_data* d) {
+  int nb = m->nbody;
+  real* sc = d->subtree_com;
+  for (int b = 0; b < nb; b++)
+    for (int i = 0; i < 3; i++) sc[3 * b + i] = d->xipos[3 * b + i] * m->body_mass[b];
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    for (int i = 0; i < 3; i++) sc[3 * p + i] += sc[3 * b + i];
+  }
+  for (int b = 0; b < nb; b++) {
+    real mass = m->body_subtreemass[b];
+    if (mass != 0)
+      for (int i = 0; i < 3; i++) sc[3 * b + i] /= mass;
+  }
+  /* _cinert smooth.py:510-553 */
+  for (int b = 0; b < nb; b++) {
+    const real* mat = d->ximat + 9 * b;
+    const real* inert = m->body_inertia + 3 * b;
+    real mass = m->body_mass[b];
+    real dif[3];
+    for (int i = 0; i < 3; i++) dif[i] = d->xipos[3 * b + i] - sc[3 * m->body_rootid[b] + i];
+    real tmp[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        real s = 0;
+        for (int k = 0; k < 3; k++) s += mat[3 * i + k] * inert[k] * mat[3 * j + k];
+        tmp[3 * i + j] = s;
+      }
+    real* res = d->cinert + 10 * b;
+    res[0] = tmp[0] + mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+    res[1] = tmp[4] + mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+    res[2] = tmp[8] + mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+    res[3] = tmp[1] - mass * dif[0] * dif[1];
+    res[4] = tmp[2] - mass * dif[0] * dif[2];
+    res[5] = tmp[5] - mass * dif[1] * dif[2];
+    res[6] = mass * dif[0];
+    res[7] = mass * dif[1];
+    res[8] = mass * dif[2];
+    res[9] = mass;
+  }
+  /* _cdof smooth.py:556-598 */
+  for (int j = 0; j < m->njnt; j++) {
+    int b = m->jnt_bodyid[j], da = m->jnt_dofadr[j], jt = m->jnt_type[j];
+    const real* xaxis = d->xaxis + 3 * j;
+    const real* xmat = d->xmat + 9 * b;
+    real off[3];
+    for (int i = 0; i < 3; i++) off[i] = sc[3 * m->body_rootid[b] + i] - d->xanchor[3 * j + i];
+    real* cd = d->cdof;
+    if (jt == JNT_FREE || jt == JNT_BALL) {
+      int rot0 = da;
+      if (jt == JNT_FREE) {
+        for (int k = 0; k < 3; k++) {
+          real* r = cd + 6 * (da + k);
+          memset(r, 0, 6 * sizeof(real));
+          r[3 + k] = 1;
+        }
+        rot0 = da + 3;
+      }
+      for (int k = 0; k < 3; k++) {
+        real ax[3] = {xmat[k], xmat[3 + k], xmat[6 + k]}; /* column k of xmat */
+        real* r = cd + 6 * (rot0 + k);
+        r[0] = ax[0]; r[1] = ax[1]; r[2] = ax[2];
+        cross3(r + 3, ax, off);
+      }
+    } else if (jt == JNT_SLIDE) {
+      real* r = cd + 6 * da;
+      r[0] = r[1] = r[2] = 0;
+      r[3] = xaxis[0]; r[4] = xaxis[1]; r[5] = xaxis[2];
+    } else {
+      real* r = cd + 6 * da;
+      r[0] = xaxis[0]; r[1] = xaxis[1]; r[2] = xaxis[2];
+      cross3(r + 3, xaxis, off);
+    }
+  }
+}
+
+/* smooth.py:635-803 (camlight) */
+static void camlight(const orc_model* m, orc_data* d) {
+  for (int c = 0; c < m->ncam; c++) {
+    int mode = m->cam_mode[c], b = m->cam_bodyid[c], tgt = m->cam_targetbodyid[c];
+    int is_target = (mode == CAM_TARGETBODY) || (mode == CAM_TARGETBODYCOM);
+    real* cx = d->cam_xpos + 3 * c;
+    real* cm = d->cam_xmat + 9 * c;
+    if ((is_target && tgt < 0) || mode == CAM_FIXED) {
+      real t[3], q[4];
+      rot_vec_quat(t, m->cam_pos + 3 * c, d->xquat + 4 * b);
+      for (int i = 0; i < 3; i++) cx[i] = d->xpos[3 * b + i] + t[i];
+      mul_quat(q, d->xquat + 4 * b, m->cam_quat + 4 * c);
+      quat_to_mat(cm, q);
+    } else if (mode == CAM_TRACK) {
+      memcpy(cm, m->cam_mat0 + 9 * c, 9 * sizeof(real));
+      for (int i = 0; i < 3; i++) cx[i] = d->xpos[3 * b + i] + m->cam_pos0[3 * c + i];
+    } else if (mode == CAM_TRACKCOM) {
+      memcpy(cm, m->cam_mat0 + 9 * c, 9 * sizeof(real));
+      for (int i = 0; i < 3; i++) cx[i] = d->subtree_com[3 * b + i] + m->cam_poscom0[3 * c + i];
+    } else {
+      real t[3], pos[3], m1[3], m2[3], m3[3];
+      rot_vec_quat(t, m->cam_pos + 3 * c, d->xquat + 4 * b);
+      for (int i = 0; i < 3; i++) cx[i] = d->xpos[3 * b + i] + t[i];
+      const real* tp = (mode == CAM_TARGETBODYCOM) ? d->subtree_com + 3 * tgt : d->xpos + 3 * tgt;
+      for (int i = 0; i < 3; i++) { pos[i] = tp[i]; m3[i] = cx[i] - pos[i]; }
+      normalize3(m3);
+      real z[3] = {0, 0, 1};
+      cross3(m1, z, m3);
+      normalize3(m1);
+      cross3(m2, m3, m1);
+      normalize3(m2);
+      for (int i = 0; i < 3; i++) { cm[3 * i] = m1[i]; cm[3 * i + 1] = m2[i]; cm[3 * i + 2] = m3[i]; }
+    }
+  }
+  for (int l = 0; l < m->nlight; l++) {
+    int mode = m->light_mode[l], b = m->light_bodyid[l], tgt = m->light_targetbodyid[l];
+    int is_target = (mode == CAM_TARGETBODY) || (mode == CAM_TARGETBODYCOM);
+    real* lx = d->light_xpos + 3 * l;
+    real* ld = d->light_xdir + 3 * l;
+    if ((is_target && tgt < 0) || mode == CAM_FIXED) {
+      real t[3];
+      rot_vec_quat(t, m->light_pos + 3 * l, d->xquat + 4 * b);
+      for (int i = 0; i < 3; i++) lx[i] = d->xpos[3 * b + i] + t[i];
+      rot_vec_quat(ld, m->light_dir + 3 * l, d->xquat + 4 * b);
+      if (is_target && tgt < 0) continue; /* smooth.py:732 returns before normalize */
+    } else if (mode == CAM_TRACK) {
+      memcpy(ld, m->light_dir0 + 3 * l, 3 * sizeof(real));
+      for (int i = 0; i < 3; i++) lx[i] = d->xpos[3 * b + i] + m->light_pos0[3 * l + i];
+    } else if (mode == CAM_TRACKCOM) {
+      memcpy(ld, m->light_dir0 + 3 * l, 3 * sizeof(real));
+      for (int i = 0; i < 3; i++) lx[i] = d->subtree_com[3 * b + i] + m->light_poscom0[3 * l + i];
+    } else {
+      real t[3];
+      rot_vec_quat(t, m->light_pos + 3 * l, d->xquat + 4 * b);
+      for (int i = 0; i < 3; i++) lx[i] = d->xpos[3 * b + i] + t[i];
+      const real* tp = (mode == CAM_TARGETBODYCOM) ? d->subtree_com + 3 * tgt : d->xpos + 3 * tgt;
+      for (int i = 0; i < 3; i++) ld[i] = tp[i] - lx[i];
+    }
+    normalize3(ld);
+  }
+}
+
+/* smooth.py:806-912 (crb accumulate + dense qM) */
+static void crb(const orc_model* m, orc_data* d) {
+  int nb = m->nbody, nv = m->nv;
+  memcpy(d->crb, d->cinert, (size_t)nb * 10 * sizeof(real));
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    if (p == 0) continue;
+    for (int i = 0; i < 10; i++) d->crb[10 * p + i] += d->crb[10 * b + i];
+  }
+  memset(d->qM, 0, (size_t)nv * nv * sizeof(real));
+  for (int i = 0; i < nv; i++) {
+    int b = m->dof_bodyid[i];
+    real buf[6];
+    inert_vec(buf, d->crb + 10 * b, d->cdof + 6 * i);
+    real Mii = m->dof_armature[i];
+    real s = 0;
+    for (int k = 0; k < 6; k++) s += d->cdof[6 * i + k] * buf[k];
+    Mii += s;
+    d->qM[i * nv + i] = Mii;
+    int j = m->dof_parentid[i];
+    while (j >= 0) {
+      real q = 0;
+      for (int k = 0; k < 6; k++) q += d->cdof[6 * j + k] * buf[k];
+      d->qM[i * nv + j] += q;
+      d->qM[j * nv + i] += q;
+      j = m->dof_parentid[j];
+    }
+  }
+}
+
+/* dense Cholesky M = L L^T (wp.tile_cholesky), L stored lower in qLD (row-major, nv x nv) */
+static void cholesky(int n, const real* M, real* L) {
+  memset(L, 0, (size_t)n * n * sizeof(real));
+  for (int j = 0; j < n; j++) {
+    real s = M[j * n + j];
+    for (int k = 0; k < j; k++) s -= L[j * n + k] * L[j * n + k];
+    real ljj = sqrt(s);
+    L[j * n + j] = ljj;
+    for (int i = j + 1; i < n; i++) {
+      real t = M[i * n + j];
+      for (int k = 0; k < j; k++) t -= L[i * n + k] * L[j * n + k];
+      L[i * n + j] = t / ljj;
+    }
+  }
+}
+
+/* wp.tile_cholesky_solve: x = (L L^T)^-1 y */
+static void cholesky_solve(int n, const real* L, const real* y, real* x) {
+  real tmp[512];
+  real* z = n <= 512 ? tmp : (real*)malloc(n * sizeof(real));
+  for (int i = 0; i < n; i++) {
+    real s = y[i];
+    for (int k = 0; k < i; k++) s -= L[i * n + k] * z[k];
+    z[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    real s = z[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * n + i] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+  if (z != tmp) free(z);
+}
+
+/* smooth.py:2041-2147 (_transmission, joint transmissions; dense moment rows) */
+static void transmission(const orc_model* m, orc_data* d) {
+  int nv = m->nv;
+  memset(d->actuator_moment, 0, (size_t)m->nu * nv * sizeof(real));
+  for (int a = 0; a < m->nu; a++) {
+    const real* gear = m->actuator_gear + 6 * a;
+    int trn = m->actuator_trntype[a];
+    real* mom = d->actuator_moment + (size_t)a * nv;
+    if (trn == TRN_JOINT || trn == TRN_JOINTINPARENT) {
+      int j = m->actuator_trnid[2 * a];
+      int jt = m->jnt_type[j], qa = m->jnt_qposadr[j], va = m->jnt_dofadr[j];
+      if (jt == JNT_FREE) {
+        d->actuator_length[a] = 0;
+        if (trn == TRN_JOINTINPARENT) {
+          real q[4] = {d->qpos[qa + 3], d->qpos[qa + 4], d->qpos[qa + 5], d->qpos[qa + 6]}, qn[4], ga[3];
+          normalize4(q);
+          qn[0] = q[0]; qn[1] = -q[1]; qn[2] = -q[2]; qn[3] = -q[3];
+          rot_vec_quat(ga, gear + 3, qn);
+          for (int i = 0; i < 3; i++) { mom[va + i] = gear[i]; mom[va + 3 + i] = ga[i]; }
+        } else {
+          for (int i = 0; i < 6; i++) mom[va + i] = gear[i];
+        }
+      } else if (jt == JNT_BALL) {
+        real q[4] = {d->qpos[qa], d->qpos[qa + 1], d->qpos[qa + 2], d->qpos[qa + 3]}, aa[3];
+        normalize4(q);
+        quat_to_vel(aa, q);
+        real ga[3] = {gear[0], gear[1], gear[2]};
+        if (trn == TRN_JOINTINPARENT) {
+          real qn[4] = {q[0], -q[1], -q[2], -q[3]};
+          rot_vec_quat(ga, ga, qn);
+        }
+        d->actuator_length[a] = dot3(aa, ga);
+        for (int i = 0; i < 3; i++) mom[va + i] = ga[i];
+      } else {
+        d->actuator_length[a] = d->qpos[qa] * gear[0];
+        mom[va] = gear[0];
+      }
+    }
+  }
+}
+
+/* smooth.py:1935-2038 (com_vel) */
+static void com_vel(const orc_model* m, orc_data* d) {
+  memset(d->cvel, 0, 6 * sizeof(real));
+  memset(d->cdof_dot, 0, (size_t)m->nv * 6 * sizeof(real));
+  for (int b = 1; b < m->nbody; b++) {
+    int p = m->body_parentid[b];
+    real cvel[6];
+    memcpy(cvel, d->cvel + 6 * p, sizeof(cvel));
+    int dofid = m->body_dofadr[b];
+    for (int j = m->body_jntadr[b]; j < m->body_jntadr[b] + m->body_jntnum[b]; j++) {
+      int jt = m->jnt_type[j];
+      const real* cd = d->cdof;
+      if (jt == JNT_FREE) {
+        for (int k = 0; k < 3; k++)
+          for (int i = 0; i < 6; i++) cvel[i] += cd[6 * (dofid + k) + i] * d->qvel[dofid + k];
+        for (int k = 3; k < 6; k++) motion_cross(d->cdof_dot + 6 * (dofid + k), cvel, cd + 6 * (dofid + k));
+        for (int k = 3; k < 6; k++)
+          for (int i = 0; i < 6; i++) cvel[i] += cd[6 * (dofid + k) + i] * d->qvel[dofid + k];
+        dofid += 6;
+      } else if (jt == JNT_BALL) {
+        for (int k = 0; k < 3; k++) motion_cross(d->cdof_dot + 6 * (dofid + k), cvel, cd + 6 * (dofid + k));
+        for (int k = 0; k < 3; k++)
+          for (int i = 0; i < 6; i++) cvel[i] += cd[6 * (dofid + k) + i] * d->qvel[dofid + k];
+        dofid += 3;
+      } else {
+        motion_cross(d->cdof_dot + 6 * dofid, cvel, cd + 6 * dofid);
+        for (int i = 0; i < 6; i++) cvel[i] += cd[6 * dofid + i] * d->qvel[dofid];
+        dofid += 1;
+      }
+    }
+    memcpy(d->cvel + 6 * b, cvel, sizeof(cvel));
+  }
+}
+
+/* smooth.py:1112-1274 (rne, flg_acc = False) */
+static void rne(const orc_model* m, orc_data* d) {
+  int nb = m->nbody;
+  real* cacc = d->cacc;
+  memset(cacc, 0, 6 * sizeof(real));
+  if (!(m->opt_disableflags & DSBL_GRAVITY))
+    for (int i = 0; i < 3; i++) cacc[3 + i] = -m->opt_gravity[i];
+  for (int b = 1; b < nb; b++) {
+    int p = m->body_parentid[b];
+    real acc[6];
+    memcpy(acc, cacc + 6 * p, sizeof(acc));
+    for (int k = 0; k < m->body_dofnum[b]; k++) {
+      int dof = m->body_dofadr[b] + k;
+      for (int i = 0; i < 6; i++) acc[i] += d->cdof_dot[6 * dof + i] * d->qvel[dof];
+    }
+    memcpy(cacc + 6 * b, acc, sizeof(acc));
+  }
+  real* cfrc = d->cfrc_int;
+  memset(cfrc, 0, 6 * sizeof(real));
+  for (int b = 1; b < nb; b++) {
+    real f1[6], iv[6], f2[6];
+    inert_vec(f1, d->cinert + 10 * b, cacc + 6 * b);
+    inert_vec(iv, d->cinert + 10 * b, d->cvel + 6 * b);
+    motion_cross_force(f2, d->cvel + 6 * b, iv);
+    for (int i = 0; i < 6; i++) cfrc[6 * b + i] = f1[i] + f2[i];
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    for (int i = 0; i < 6; i++) cfrc[6 * p + i] += cfrc[6 * b + i];
+  }
+  for (int i = 0; i < m->nv; i++) {
+    int b = m->dof_bodyid[i];
+    real s = 0;
+    for (int k = 0; k < 6; k++) s += d->cdof[6 * i + k] * cfrc[6 * b + k];
+    d->qfrc_bias[i] = s;
+  }
+}
+
+/* passive.py:70-179 (+ _qfrc_passive :535-563) */
+static void passive(const orc_model* m, orc_data* d) {
+  int nv = m->nv;
+  int dsbl_spring = m->opt_disableflags & DSBL_SPRING, dsbl_damper = m->opt_disableflags & DSBL_DAMPER;
+  memset(d->qfrc_spring, 0, nv * sizeof(real));
+  memset(d->qfrc_damper, 0, nv * sizeof(real));
+  if (dsbl_spring && dsbl_damper) { memset(d->qfrc_passive, 0, nv * sizeof(real)); return; }
+  for (int j = 0; j < m->njnt; j++) {
+    int da = m->jnt_dofadr[j], qa = m->jnt_qposadr[j], jt = m->jnt_type[j];
+    real stiff = m->jnt_stiffness[j], damp = m->dof_damping[da];
+    int has_s = stiff != 0 && !dsbl_spring, has_d = damp != 0 && !dsbl_damper;
+    if (jt == JNT_FREE) {
+      if (has_s) {
+        for (int i = 0; i < 3; i++) d->qfrc_spring[da + i] = -stiff * (d->qpos[qa + i] - m->qpos_spring[qa + i]);
+        real rot[4] = {d->qpos[qa + 3], d->qpos[qa + 4], d->qpos[qa + 5], d->qpos[qa + 6]}, dif[3];
+        normalize4(rot);
+        quat_sub(dif, rot, m->qpos_spring + qa + 3);
+        for (int i = 0; i < 3; i++) d->qfrc_spring[da + 3 + i] = -stiff * dif[i];
+      }
+      if (has_d)
+        for (int i = 0; i < 6; i++) d->qfrc_damper[da + i] = -damp * d->qvel[da + i];
+    } else if (jt == JNT_BALL) {
+      if (has_s) {
+        real rot[4] = {d->qpos[qa], d->qpos[qa + 1], d->qpos[qa + 2], d->qpos[qa + 3]}, dif[3];
+        normalize4(rot);
+        quat_sub(dif, rot, m->qpos_spring + qa);
+        for (int i = 0; i < 3; i++) d->qfrc_spring[da + i] = -stiff * dif[i];
+      }
+      if (has_d)
+        for (int i = 0; i < 3; i++) d->qfrc_damper[da + i] = -damp * d->qvel[da + i];
+    } else {
+      if (has_s) d->qfrc_spring[da] = -stiff * (d->qpos[qa] - m->qpos_spring[qa]);
+      if (has_d) d->qfrc_damper[da] = -damp * d->qvel[da];
+    }
+  }
+  for (int i = 0; i < nv; i++) d->qfrc_passive[i] = d->qfrc_spring[i] + d->qfrc_damper[i];
+}
+
+/* =============================================================================================
+ * collision (collision_driver.py, collision_core.py, collision_primitive*.py)
+ * ============================================================================================= */
+typedef struct {
+  real dist[2];
+  real pos[2][3];
+  real frame[2][9];
+  int n;
+} contacts2;
+
+/* collision_driver.py:90-103 */
+static int plane_filter(real size1, real size2, real margin1, real margin2, const real* xpos1, const real* xpos2,
+                        const real* xmat1, const real* xmat2) {
+  if (size1 == 0) {
+    real dif[3] = {xpos2[0] - xpos1[0], xpos2[1] - xpos1[1], xpos2[2] - xpos1[2]};
+    real n[3] = {xmat1[2], xmat1[5], xmat1[8]};
+    return dot3(dif, n) <= size2 + margin1 + margin2;
+  } else if (size2 == 0) {
+    real dif[3] = {xpos1[0] - xpos2[0], xpos1[1] - xpos2[1], xpos1[2] - xpos2[2]};
+    real n[3] = {xmat2[2], xmat2[5], xmat2[8]};
+    return dot3(dif, n) <= size1 + margin1 + margin2;
+  }
+  return 1;
+}
+
+/* collision_driver.py:106-111 */
+static int sphere_filter(real size1, real size2, real margin1, real margin2, const real* xpos1, const real* xpos2) {
+  real bound = size1 + size2 + margin1 + margin2;
+  real dif[3] = {xpos2[0] - xpos1[0], xpos2[1] - xpos1[1], xpos2[2] - xpos1[2]};
+  return dot3(dif, dif) <= bound * bound;
+}
+
+static void matvec3(real* r, const real* M, const real* v) {
+  real t[3];
+  for (int i = 0; i < 3; i++) t[i] = M[3 * i] * v[0] + M[3 * i + 1] * v[1] + M[3 * i + 2] * v[2];
+  r[0] = t[0]; r[1] = t[1]; r[2] = t[2];
+}
+
+/* collision_driver.py:116-213 */
+static int aabb_filter(const real* c1, const real* c2, const real* s1, const real* s2, real m1, real m2, const real* xp1,
+                       const real* xp2, const real* xm1, const real* xm2) {
+  real cen1[3], cen2[3];
+  matvec3(cen1, xm1, c1); matvec3(cen2, xm2, c2);
+  for (int i = 0; i < 3; i++) { cen1[i] += xp1[i]; cen2[i] += xp2[i]; }
+  real margin = m1 + m2;
+  real mx1[3] = {-MAXVAL, -MAXVAL, -MAXVAL}, mn1[3] = {MAXVAL, MAXVAL, MAXVAL};
+  real mx2[3] = {-MAXVAL, -MAXVAL, -MAXVAL}, mn2[3] = {MAXVAL, MAXVAL, MAXVAL};
+  real sgn[2] = {-1, 1};
+  for (int i = 0; i < 2; i++)
+    for (int j = 0; j < 2; j++)
+      for (int k = 0; k < 2; k++) {
+        real cr1[3] = {sgn[i] * s1[0], sgn[j] * s1[1], sgn[k] * s1[2]}, p1[3];
+        real cr2[3] = {sgn[i] * s2[0], sgn[j] * s2[1], sgn[k] * s2[2]}, p2[3];
+        matvec3(p1, xm1, cr1); matvec3(p2, xm2, cr2);
+        for (int a = 0; a < 3; a++) {
+          if (p1[a] > mx1[a]) mx1[a] = p1[a];
+          if (p1[a] < mn1[a]) mn1[a] = p1[a];
+          if (p2[a] > mx2[a]) mx2[a] = p2[a];
+          if (p2[a] < mn2[a]) mn2[a] = p2[a];
+        }
+      }
+  for (int a = 0; a < 3; a++) {
+    if (cen1[a] + mx1[a] + margin < cen2[a] + mn2[a]) return 0;
+    if (cen2[a] + mx2[a] + margin < cen1[a] + mn1[a]) return 0;
+  }
+  return 1;
+}
+
+/* collision_driver.py:217-271 */
+static int obb_filter(const real* c1, const real* c2, const real* s1, const real* s2, real m1, real m2, const real* xp1,
+                      const real* xp2, const real* xm1, const real* xm2) {
+  real margin = m1 + m2;
+  real xc[2][3], nrm[6][3];
+  matvec3(xc[0], xm1, c1); matvec3(xc[1], xm2, c2);
+  for (int i = 0; i < 3; i++) { xc[0][i] += xp1[i]; xc[1][i] += xp2[i]; }
+  for (int k = 0; k < 3; k++)
+    for (int i = 0; i < 3; i++) { nrm[k][i] = xm1[3 * i + k]; nrm[3 + k][i] = xm2[3 * i + k]; }
+  for (int j = 0; j < 2; j++)
+    for (int k = 0; k < 3; k++) {
+      real proj[2], radius[2];
+      for (int i = 0; i < 2; i++) {
+        proj[i] = dot3(xc[i], nrm[3 * j + k]);
+        const real* size = i == 0 ? s1 : s2;
+        radius[i] = fabs(size[0] * dot3(nrm[3 * i + 0], nrm[3 * j + k])) + fabs(size[1] * dot3(nrm[3 * i + 1], nrm[3 * j + k])) +
+                    fabs(size[2] * dot3(nrm[3 * i + 2], nrm[3 * j + k]));
+      }
+      if (radius[0] + radius[1] + margin < fabs(proj[1] - proj[0])) return 0;
+    }
+  return 1;
+}
+
+/* collision_driver.py:274-321 */
+static int broadphase_filter(const orc_model* m, const orc_data* d, int g1, int g2) {
+  int filt = m->opt_broadphase_filter;
+  const real *c1 = m->geom_aabb + 6 * g1, *c2 = m->geom_aabb + 6 * g2;
+  const real *s1 = c1 + 3, *s2 = c2 + 3;
+  real rb1 = m->geom_rbound[g1], rb2 = m->geom_rbound[g2];
+  real mg1 = m->geom_margin[g1], mg2 = m->geom_margin[g2];
+  const real *xp1 = d->geom_xpos + 3 * g1, *xp2 = d->geom_xpos + 3 * g2;
+  const real *xm1 = d->geom_xmat + 9 * g1, *xm2 = d->geom_xmat + 9 * g2;
+  if (rb1 == 0 || rb2 == 0) {
+    if (filt & FILTER_PLANE) return plane_filter(rb1, rb2, mg1, mg2, xp1, xp2, xm1, xm2);
+  } else {
+    if (filt & FILTER_SPHERE)
+      if (!sphere_filter(rb1, rb2, mg1, mg2, xp1, xp2)) return 0;
+    if (filt & FILTER_AABB)
+      if (!aabb_filter(c1, c2, s1, s2, mg1, mg2, xp1, xp2, xm1, xm2)) return 0;
+    if (filt & FILTER_OBB)
+      if (!obb_filter(c1, c2, s1, s2, mg1, mg2, xp1, xp2, xm1, xm2)) return 0;
+  }
+  return 1;
+}
+
+/* collision_primitive_core.py:106-111 */
+static real plane_sphere(real* pos, const real* n, const real* ppos, const real* spos, real r) {
+  real dif[3] = {spos[0] - ppos[0], spos[1] - ppos[1], spos[2] - ppos[2]};
+  real dist = dot3(dif, n) - r;
+  for (int i = 0; i < 3; i++) pos[i] = spos[i] - n[i] * (r + (real)0.5 * dist);
+  return dist;
+}
+
+/* collision_primitive_core.py:114-143 */
+static real sphere_sphere(real* pos, real* n, const real* p1, real r1, const real* p2, real r2) {
+  real dir[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  real dist = sqrt(dot3(dir, dir));
+  if (dist == 0) { n[0] = 1; n[1] = 0; n[2] = 0; }
+  else { n[0] = dir[0] / dist; n[1] = dir[1] / dist; n[2] = dir[2] / dist; }
+  dist = dist - (r1 + r2);
+  for (int i = 0; i < 3; i++) pos[i] = p1[i] + n[i] * (r1 + (real)0.5 * dist);
+  return dist;
+}
+
+/* collision_primitive_core.py:146-178 */
+static real sphere_capsule(real* pos, real* n, const real* spos, real sr, const real* cpos, const real* axis, real cr, real chl) {
+  real a[3], b[3], pt[3];
+  for (int i = 0; i < 3; i++) { a[i] = cpos[i] - axis[i] * chl; b[i] = cpos[i] + axis[i] * chl; }
+  closest_segment_point(pt, a, b, spos);
+  return sphere_sphere(pos, n, spos, sr, pt, cr);
+}
+
+/* collision_primitive_core.py:181-308 */
+static void capsule_capsule(contacts2* out, const real* p1, const real* ax1, real r1, real hl1, const real* p2, const real* ax2,
+                            real r2, real hl2, real margin) {
+  real axis1[3], axis2[3], dif[3];
+  for (int i = 0; i < 3; i++) { axis1[i] = ax1[i] * hl1; axis2[i] = ax2[i] * hl2; dif[i] = p1[i] - p2[i]; }
+  real ma = dot3(axis1, axis1), mb = -dot3(axis1, axis2), mc = dot3(axis2, axis2);
+  real u = -dot3(axis1, dif), v = dot3(axis2, dif);
+  real det = ma * mc - mb * mb;
+  out->n = 0;
+  out->dist[0] = out->dist[1] = INFINITY;
+  real v1[3], v2[3], pos[3], nrm[3];
+  if (fabs(det) >= MINVAL) {
+    real inv = 1 / det;
+    real x1 = (mc * u - mb * v) * inv, x2 = (ma * v - mb * u) * inv;
+    if (x1 > 1) { x1 = 1; x2 = (v - mb) / mc; }
+    else if (x1 < -1) { x1 = -1; x2 = (v + mb) / mc; }
+    if (x2 > 1) { x2 = 1; x1 = clampr((u - mb) / ma, -1, 1); }
+    else if (x2 < -1) { x2 = -1; x1 = clampr((u + mb) / ma, -1, 1); }
+    for (int i = 0; i < 3; i++) { v1[i] = p1[i] + axis1[i] * x1; v2[i] = p2[i] + axis2[i] * x2; }
+    real dist = sphere_sphere(pos, nrm, v1, r1, v2, r2);
+    if (dist <= margin) {
+      out->dist[0] = dist;
+      memcpy(out->pos[0], pos, sizeof(pos));
+      make_frame(out->frame[0], nrm);
+      out->n = 1;
+    }
+    return;
+  }
+  int cnt = 0;
+  for (int t = 0; t < 4; t++) {
+    if (t >= 2 && cnt >= 2) break;
+    real x;
+    if (t == 0) { for (int i = 0; i < 3; i++) v1[i] = p1[i] + axis1[i]; x = clampr((v - mb) / mc, -1, 1); for (int i = 0; i < 3; i++) v2[i] = p2[i] + axis2[i] * x; }
+    else if (t == 1) { for (int i = 0; i < 3; i++) v1[i] = p1[i] - axis1[i]; x = clampr((v + mb) / mc, -1, 1); for (int i = 0; i < 3; i++) v2[i] = p2[i] + axis2[i] * x; }
+    else if (t == 2) { for (int i = 0; i < 3; i++) v2[i] = p2[i] + axis2[i]; x = clampr((u - mb) / ma, -1, 1); for (int i = 0; i < 3; i++) v1[i] = p1[i] + axis1[i] * x; }
+    else { for (int i = 0; i < 3; i++) v2[i] = p2[i] - axis2[i]; x = clampr((u + mb) / ma, -1, 1); for (int i = 0; i < 3; i++) v1[i] = p1[i] + axis1[i] * x; }
+    real dist = sphere_sphere(pos, nrm, v1, r1, v2, r2);
+    if (dist <= margin) {
+      out->dist[cnt] = dist;
+      memcpy(out->pos[cnt], pos, sizeof(pos));
+      make_frame(out->frame[cnt], nrm);
+      cnt++;
+    }
+  }
+  out->n = cnt;
+}
+
+/* collision_primitive_core.py:311-361 */
+static void plane_capsule(contacts2* out, const real* n, const real* ppos, const real* cpos, const real* axis, real r, real hl) {
+  real b[3], tmp[3];
+  real nd = dot3(n, axis);
+  for (int i = 0; i < 3; i++) tmp[i] = axis[i] - n[i] * nd;
+  real bn = normalize_with_norm(b, tmp);
+  if (bn < 0.5) {
+    if (-0.5 < n[1] && n[1] < 0.5) { b[0] = 0; b[1] = 1; b[2] = 0; }
+    else { b[0] = 0; b[1] = 0; b[2] = 1; }
+  }
+  real c[3];
+  cross3(c, n, b);
+  real frame[9] = {n[0], n[1], n[2], b[0], b[1], b[2], c[0], c[1], c[2]};
+  real e1[3], e2[3];
+  for (int i = 0; i < 3; i++) { e1[i] = cpos[i] + axis[i] * hl; e2[i] = cpos[i] - axis[i] * hl; }
+  out->dist[0] = plane_sphere(out->pos[0], n, ppos, e1, r);
+  out->dist[1] = plane_sphere(out->pos[1], n, ppos, e2, r);
+  memcpy(out->frame[0], frame, sizeof(frame));
+  memcpy(out->frame[1], frame, sizeof(frame));
+  out->n = 2;
+}
+
+/* collision_core.py:235-341 (geom-geom mixing; explicit <pair> not supported here) */
+static void contact_params(const orc_model* m, int g1, int g2, real* margin, real* gap, int* condim, real* friction,
+                           real* solref, real* solreffriction, real* solimp) {
+  real s1 = m->geom_solmix[g1], s2 = m->geom_solmix[g2];
+  int c1 = m->geom_condim[g1], c2 = m->geom_condim[g2];
+  int p1 = m->geom_priority[g1], p2 = m->geom_priority[g2];
+  real mix, fr[3];
+  if (p1 > p2) { mix = 1; *condim = c1; memcpy(fr, m->geom_friction + 3 * g1, sizeof(fr)); }
+  else if (p2 > p1) { mix = 0; *condim = c2; memcpy(fr, m->geom_friction + 3 * g2, sizeof(fr)); }
+  else {
+    mix = safe_div(s1, s1 + s2);
+    if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
+    else if (s1 < MINVAL && s2 >= MINVAL) mix = 0;
+    else if (s1 >= MINVAL && s2 < MINVAL) mix = 1;
+    *condim = c1 > c2 ? c1 : c2;
+    for (int i = 0; i < 3; i++) fr[i] = maxr(m->geom_friction[3 * g1 + i], m->geom_friction[3 * g2 + i]);
+  }
+  friction[0] = fr[0]; friction[1] = fr[0]; friction[2] = fr[1]; friction[3] = fr[2]; friction[4] = fr[2];
+  const real *sr1 = m->geom_solref + 2 * g1, *sr2 = m->geom_solref + 2 * g2;
+  if (sr1[0] > 0 && sr2[0] > 0) {
+    for (int i = 0; i < 2; i++) solref[i] = mix * sr1[i] + (1 - mix) * sr2[i];
+  } else {
+    for (int i = 0; i < 2; i++) solref[i] = minr(sr1[i], sr2[i]);
+  }
+  solreffriction[0] = solreffriction[1] = 0;
+  for (int i = 0; i < 5; i++) solimp[i] = mix * m->geom_solimp[5 * g1 + i] + (1 - mix) * m->geom_solimp[5 * g2 + i];
+  *margin = m->geom_margin[g1] + m->geom_margin[g2];
+  *gap = m->geom_gap[g1] + m->geom_gap[g2];
+  for (int i = 0; i < 5; i++) friction[i] = maxr(MINMU, friction[i]);
+}
+
+/* collision_driver.py:697-789 + collision_primitive.py:1300-1454 (+ write_contact collision_core.py:159-232) */
+static void collision(const orc_model* m, orc_data* d) {
+  *d->ncon = 0;
+  *d->ncollision = 0;
+  if (m->opt_disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT)) return;
+  for (int p = 0; p < m->nxn; p++) {
+    int g1 = m->nxn_geom_pair[2 * p], g2 = m->nxn_geom_pair[2 * p + 1];
+    int pairid0 = m->nxn_pairid[2 * p], pairid1 = m->nxn_pairid[2 * p + 1];
+    if (!(broadphase_filter(m, d, g1, g2) || pairid1 >= 0)) continue;
+    (*d->ncollision)++;
+    if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
+    real margin, gap, friction[5], solref[2], solreffriction[2], solimp[5];
+    int condim;
+    contact_params(m, g1, g2, &margin, &gap, &condim, friction, solref, solreffriction, solimp);
+    int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+    const real *p1 = d->geom_xpos + 3 * g1, *p2 = d->geom_xpos + 3 * g2;
+    const real *r1 = d->geom_xmat + 9 * g1, *r2 = d->geom_xmat + 9 * g2;
+    const real *s1 = m->geom_size + 3 * g1, *s2 = m->geom_size + 3 * g2;
+    real n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
+    contacts2 c;
+    c.n = 0;
+    if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) {
+      c.dist[0] = plane_sphere(c.pos[0], n1, p1, p2, s2[0]);
+      make_frame(c.frame[0], n1);
+      c.n = 1;
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_CAPSULE) {
+      plane_capsule(&c, n1, p1, p2, n2, s2[0], s2[1]);
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
+      real nrm[3];
+      c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], p2, s2[0]);
+      make_frame(c.frame[0], nrm);
+      c.n = 1;
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
+      real nrm[3];
+      c.dist[0] = sphere_capsule(c.pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]);
+      make_frame(c.frame[0], nrm);
+      c.n = 1;
+    } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
+      capsule_capsule(&c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], margin);
+    } else {
+      continue; /* pair type not supported by the oracle (not on the benchmark path) */
+    }
+    for (int k = 0; k < c.n; k++) {
+      real dist = c.dist[k];
+      int active = dist < margin;
+      if ((pairid0 == -2 || !active) && pairid1 == -1) continue;
+      if (!(pairid0 >= -1 && active)) continue; /* sensor-only contacts are not produced here */
+      int cid = *d->ncon;
+      if (cid >= d->nconmax) { (*d->ncon)++; continue; }
+      d->con_dist[cid] = dist;
+      memcpy(d->con_pos + 3 * cid, c.pos[k], 3 * sizeof(real));
+      memcpy(d->con_frame + 9 * cid, c.frame[k], 9 * sizeof(real));
+      d->con_includemargin[cid] = margin - gap;
+      memcpy(d->con_friction + 5 * cid, friction, 5 * sizeof(real));
+      memcpy(d->con_solref + 2 * cid, solref, 2 * sizeof(real));
+      memcpy(d->con_solreffriction + 2 * cid, solreffriction, 2 * sizeof(real));
+      memcpy(d->con_solimp + 5 * cid, solimp, 5 * sizeof(real));
+      d->con_dim[cid] = condim;
+      d->con_geom[2 * cid] = g1;
+      d->con_geom[2 * cid + 1] = g2;
+      for (int i = 0; i < 10; i++) d->con_efc_address[10 * cid + i] = -1;
+      (*d->ncon)++;
+    }
+  }
+}
+
+/* =============================================================================================
+ * constraint.py
+ * ============================================================================================= */
+
+/* constraint.py:52-121 */
+static void efc_row(const orc_model* m, orc_data* d, int efcid, real pos_aref, real pos_imp, real invweight, const real* solref,
+                    const real* solimp, real margin, real vel, real frictionloss, int type, int id) {
+  real timeconst = solref[0], dampratio = solref[1];
+  real dmin = solimp[0], dmax = solimp[1], width = solimp[2], mid = solimp[3], power = solimp[4];
+  if (!(m->opt_disableflags & DSBL_REFSAFE)) timeconst = maxr(timeconst, 2 * m->opt_timestep);
+  dmin = clampr(dmin, MINIMP, MAXIMP);
+  dmax = clampr(dmax, MINIMP, MAXIMP);
+  width = maxr(MINVAL, width);
+  mid = clampr(mid, MINIMP, MAXIMP);
+  power = maxr(1, power);
+  real dmax_sq = dmax * dmax;
+  real k = 1 / (dmax_sq * timeconst * timeconst * dampratio * dampratio);
+  real b = 2 / (dmax * timeconst);
+  if (solref[0] <= 0) k = -solref[0] / dmax_sq;
+  if (solref[1] <= 0) b = -solref[1] / dmax;
+  real imp_x = fabs(pos_imp) / width;
+  real imp_a = (1 / pow(mid, power - 1)) * pow(imp_x, power);
+  real imp_b = 1 - (1 / pow(1 - mid, power - 1)) * pow(1 - imp_x, power);
+  real imp_y = imp_x < mid ? imp_a : imp_b;
+  real imp = dmin + imp_y * (dmax - dmin);
+  imp = clampr(imp, dmin, dmax);
+  if (imp_x > 1) imp = dmax;
+  d->efc_D[efcid] = 1 / maxr(invweight * (1 - imp) / imp, MINVAL);
+  d->efc_vel[efcid] = vel;
+  d->efc_aref[efcid] = -k * imp * pos_aref - b * vel;
+  d->efc_pos[efcid] = pos_aref + margin;
+  d->efc_margin[efcid] = margin;
+  d->efc_frictionloss[efcid] = frictionloss;
+  d->efc_type[efcid] = type;
+  d->efc_id[efcid] = id;
+}
+
+/* support.py:396-432 */
+static int jac_dof(const orc_model* m, const orc_data* d, const real* point, int bodyid, int dofid, real* jacp, real* jacr) {
+  int db = m->dof_bodyid[dofid];
+  int in_tree = db == 0;
+  int p = bodyid;
+  while (p != 0) {
+    if (p == db) { in_tree = 1; break; }
+    p = m->body_parentid[p];
+  }
+  if (!in_tree) { jacp[0] = jacp[1] = jacp[2] = jacr[0] = jacr[1] = jacr[2] = 0; return 0; }
+  real off[3];
+  for (int i = 0; i < 3; i++) off[i] = point[i] - d->subtree_com[3 * m->body_rootid[bodyid] + i];
+  const real* cd = d->cdof + 6 * dofid;
+  real c[3];
+  cross3(c, cd, off);
+  for (int i = 0; i < 3; i++) { jacp[i] = cd[3 + i] + c[i]; jacr[i] = cd[i]; }
+  return 1;
+}
+
+/* constraint.py:2209-2779 (equality / friction / limit / contact, in that order) */
+static void make_constraint(const orc_model* m, orc_data* d) {
+  int nv = m->nv, njmax = d->njmax;
+  *d->ne = *d->nf = *d->nl = *d->nefc = 0;
+  if (m->opt_disableflags & DSBL_CONSTRAINT) return;
+  /* friction dof constraint.py:1113-1190 */
+  if (!(m->opt_disableflags & DSBL_FRICTIONLOSS)) {
+    for (int i = 0; i < nv; i++) {
+      real fl = m->dof_frictionloss[i];
+      if (fl <= 0) continue;
+      (*d->nf)++;
+      int efcid = (*d->nefc)++;
+      if (efcid >= njmax) continue;
+      real* J = d->efc_J + (size_t)efcid * nv;
+      memset(J, 0, nv * sizeof(real));
+      J[i] = 1;
+      efc_row(m, d, efcid, 0, 0, m->dof_invweight0[i], m->dof_solref + 2 * i, m->dof_solimp + 5 * i, 0, d->qvel[i], fl,
+              CNSTR_FRICTION_DOF, i);
+    }
+  }
+  /* limit slide/hinge constraint.py:1316-1418 */
+  if (!(m->opt_disableflags & DSBL_LIMIT)) {
+    for (int j = 0; j < m->njnt; j++) {
+      int jt = m->jnt_type[j];
+      if (!m->jnt_limited[j] || !(jt == JNT_SLIDE || jt == JNT_HINGE)) continue;
+      const real* rng = m->jnt_range + 2 * j;
+      real q = d->qpos[m->jnt_qposadr[j]];
+      real dmn = q - rng[0], dmx = rng[1] - q;
+      real pos = minr(dmn, dmx) - m->jnt_margin[j];
+      if (!(pos < 0)) continue;
+      (*d->nl)++;
+      int efcid = (*d->nefc)++;
+      if (efcid >= njmax) continue;
+      int da = m->jnt_dofadr[j];
+      real Jv = (real)(dmn < dmx) * 2 - 1;
+      real* J = d->efc_J + (size_t)efcid * nv;
+      memset(J, 0, nv * sizeof(real));
+      J[da] = Jv;
+      efc_row(m, d, efcid, pos, pos, m->dof_invweight0[da], m->jnt_solref + 2 * j, m->jnt_solimp + 5 * j, m->jnt_margin[j],
+              Jv * d->qvel[da], 0, CNSTR_LIMIT_JOINT, j);
+    }
+  }
+  /* contact pyramidal constraint.py:1668-1936 */
+  if (!(m->opt_disableflags & DSBL_CONTACT)) {
+    int ncon = *d->ncon < d->nconmax ? *d->ncon : d->nconmax;
+    for (int c = 0; c < ncon; c++) {
+      int condim = d->con_dim[c];
+      int nrow = condim == 1 ? 1 : 2 * (condim - 1);
+      real includemargin = d->con_includemargin[c];
+      real pos = d->con_dist[c] - includemargin;
+      if (!(pos < 0)) continue;
+      int g1 = d->con_geom[2 * c], g2 = d->con_geom[2 * c + 1];
+      int body1 = m->geom_bodyid[g1], body2 = m->geom_bodyid[g2];
+      real iw_base = m->body_invweight0[2 * body1] + m->body_invweight0[2 * body2];
+      int w1 = m->body_weldid[body1], w2 = m->body_weldid[body2];
+      const real* frame = d->con_frame + 9 * c;
+      const real* cpos = d->con_pos + 3 * c;
+      for (int dimid = 0; dimid < nrow; dimid++) {
+        int efcid = (*d->nefc)++;
+        if (efcid >= njmax) { d->con_efc_address[10 * c + dimid] = -1; continue; }
+        d->con_efc_address[10 * c + dimid] = efcid;
+        real invweight = iw_base;
+        real frii = 0;
+        int dimid2 = dimid / 2 + 1;
+        if (condim > 1) {
+          real fri0 = d->con_friction[5 * c];
+          frii = d->con_friction[5 * c + dimid2 - 1];
+          invweight = invweight + fri0 * fri0 * invweight;
+          invweight = invweight * 2 * fri0 * fri0 * m->opt_impratio_invsqrt * m->opt_impratio_invsqrt;
+        }
+        real* J = d->efc_J + (size_t)efcid * nv;
+        real Jqvel = 0;
+        for (int i = nv - 1; i >= 0; i--) {
+          real j1p[3], j1r[3], j2p[3], j2r[3];
+          jac_dof(m, d, cpos, w1, i, j1p, j1r);
+          jac_dof(m, d, cpos, w2, i, j2p, j2r);
+          real Jval = 0, Ji = 0;
+          for (int x = 0; x < 3; x++) {
+            real jd = j2p[x] - j1p[x];
+            Jval += frame[x] * jd;
+            if (condim > 1) {
+              if (dimid2 < 3) Ji += frame[3 * dimid2 + x] * jd;
+              else Ji += frame[3 * (dimid2 - 3) + x] * (j2r[x] - j1r[x]);
+            }
+          }
+          if (condim > 1) {
+            if (dimid % 2 == 0) Jval += Ji * frii;
+            else Jval -= Ji * frii;
+          }
+          J[i] = Jval;
+          Jqvel += Jval * d->qvel[i];
+        }
+        int type = condim == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
+        efc_row(m, d, efcid, pos, pos, invweight, d->con_solref + 2 * c, d->con_solimp + 5 * c, includemargin, Jqvel, 0, type, c);
+      }
+    }
+  }
+}
+
+/* =============================================================================================
+ * forward.py stages
+ * ============================================================================================= */
+
+/* forward.py:513-537 (factorize=False) */
+static void fwd_position(const orc_model* m, orc_data* d) {
+  kinematics(m, d);
+  com_pos(m, d);
+  camlight(m, d);
+  crb(m, d);
+  collision(m, d);
+  make_constraint(m, d);
+  transmission(m, d);
+}
+
+/* forward.py:540-613 */
+static void fwd_velocity(const orc_model* m, orc_data* d) {
+  for (int a = 0; a < m->nu; a++) {
+    real v = 0;
+    for (int i = 0; i < m->nv; i++) v += d->actuator_moment[(size_t)a * m->nv + i] * d->qvel[i];
+    d->actuator_velocity[a] = v;
+  }
+  com_vel(m, d);
+  passive(m, d);
+  rne(m, d);
+}
+
+/* forward.py:616-927 (na = 0 path + general gain/bias) */
+static void fwd_actuation(const orc_model* m, orc_data* d) {
+  int nv = m->nv;
+  if (!m->nu || (m->opt_disableflags & DSBL_ACTUATION)) {
+    memset(d->qfrc_actuator, 0, nv * sizeof(real));
+    return;
+  }
+  for (int a = 0; a < m->nu; a++) {
+    real ctrl = d->ctrl[a];
+    if (m->actuator_ctrllimited[a] && !(m->opt_disableflags & DSBL_CLAMPCTRL))
+      ctrl = clampr(ctrl, m->actuator_ctrlrange[2 * a], m->actuator_ctrlrange[2 * a + 1]);
+    real ctrl_act = ctrl;
+    int act_first = m->actuator_actadr[a];
+    if (m->na && act_first >= 0) ctrl_act = d->act[act_first + m->actuator_actnum[a] - 1];
+    real len = d->actuator_length[a], vel = d->actuator_velocity[a];
+    const real* gp = m->actuator_gainprm + 10 * a;
+    const real* bp = m->actuator_biasprm + 10 * a;
+    real gain = 0, bias = 0;
+    if (m->actuator_gaintype[a] == GAIN_FIXED) gain = gp[0];
+    else if (m->actuator_gaintype[a] == GAIN_AFFINE) gain = gp[0] + gp[1] * len + gp[2] * vel;
+    if (m->actuator_biastype[a] == BIAS_AFFINE) bias = bp[0] + bp[1] * len + bp[2] * vel;
+    real force = gain * ctrl_act + bias;
+    if (m->actuator_forcelimited[a]) force = clampr(force, m->actuator_forcerange[2 * a], m->actuator_forcerange[2 * a + 1]);
+    d->actuator_force[a] = force;
+  }
+  memset(d->qfrc_actuator, 0, nv * sizeof(real));
+  for (int a = 0; a < m->nu; a++)
+    for (int i = 0; i < nv; i++) d->qfrc_actuator[i] += d->actuator_moment[(size_t)a * nv + i] * d->actuator_force[a];
+  for (int i = 0; i < nv; i++) {
+    int j = m->dof_jntid[i];
+    if (m->jnt_actfrclimited[j]) d->qfrc_actuator[i] = clampr(d->qfrc_actuator[i], m->jnt_actfrcrange[2 * j], m->jnt_actfrcrange[2 * j + 1]);
+  }
+}
+
+/* support.py:174-237 (apply_ft, flg_add) */
+static void xfrc_accumulate(const orc_model* m, orc_data* d, real* qfrc) {
+  for (int i = 0; i < m->nv; i++) {
+    const real* cd = d->cdof + 6 * i;
+    int db = m->dof_bodyid[i];
+    real acc = 0;
+    for (int b = db; b < m->nbody; b++) {
+      const real* ft = d->xfrc_applied + 6 * b;
+      if (ft[0] == 0 && ft[1] == 0 && ft[2] == 0 && ft[3] == 0 && ft[4] == 0 && ft[5] == 0) continue;
+      int p = b;
+      while (p != 0 && p != db) p = m->body_parentid[p];
+      if (p == 0) continue;
+      real off[3], c[3];
+      for (int k = 0; k < 3; k++) off[k] = d->xipos[3 * b + k] - d->subtree_com[3 * m->body_rootid[b] + k];
+      cross3(c, cd, off);
+      acc += cd[3] * ft[0] + cd[4] * ft[1] + cd[5] * ft[2] + cd[0] * ft[3] + cd[1] * ft[4] + cd[2] * ft[5] + dot3(c, ft);
+    }
+    qfrc[i] += acc;
+  }
+}
+
+/* forward.py:930-969 (factorize = True) */
+static void fwd_acceleration(const orc_model* m, orc_data* d) {
+  int nv = m->nv;
+  for (int i = 0; i < nv; i++)
+    d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i] + d->qfrc_applied[i];
+  xfrc_accumulate(m, d, d->qfrc_smooth);
+  cholesky(nv, d->qM, d->qLD);
+  cholesky_solve(nv, d->qLD, d->qfrc_smooth, d->qacc_smooth);
+}
+
+/* =============================================================================================
+ * solver.py (primal CG / Newton, pyramidal cones, iterative linesearch)
+ * ============================================================================================= */
+typedef struct {
+  real* Jaref; real* jv;
+  real* grad; real* Mgrad; real* search; real* mv; real* prev_grad; real* prev_Mgrad;
+  real* H; real* HL;
+  real cost, prev_cost, gauss, search_dot, grad_dot;
+  int done;
+} solver_ctx;
+
+static void matvec(int n, const real* M, const real* x, real* y) {
+  for (int i = 0; i < n; i++) {
+    real s = 0;
+    for (int j = 0; j < n; j++) s += M[i * n + j] * x[j];
+    y[i] = s;
+  }
+}
+
+/* solver.py:2154-2219 + 1805-1951 (non-elliptic) + 1987-2051 */
+static void update_constraint(const orc_model* m, orc_data* d, solver_ctx* c) {
+  int nv = m->nv, nefc = *d->nefc < d->njmax ? *d->nefc : d->njmax;
+  int ne = *d->ne, nf = *d->nf;
+  c->gauss = 0;
+  c->prev_cost = c->cost;
+  c->cost = 0;
+  for (int r = 0; r < nefc; r++) {
+    real D = d->efc_D[r], Jaref = c->Jaref[r];
+    int state;
+    if (r < ne) {
+      d->efc_force[r] = -D * Jaref; state = STATE_QUADRATIC; c->cost += (real)0.5 * D * Jaref * Jaref;
+    } else if (r < ne + nf) {
+      real f = d->efc_frictionloss[r], rf = safe_div(f, D);
+      if (Jaref <= -rf) { d->efc_force[r] = f; state = STATE_LINEARNEG; c->cost += -f * ((real)0.5 * rf + Jaref); }
+      else if (Jaref >= rf) { d->efc_force[r] = -f; state = STATE_LINEARPOS; c->cost += -f * ((real)0.5 * rf - Jaref); }
+      else { d->efc_force[r] = -D * Jaref; state = STATE_QUADRATIC; c->cost += (real)0.5 * D * Jaref * Jaref; }
+    } else {
+      if (Jaref >= 0) { d->efc_force[r] = 0; state = STATE_SATISFIED; }
+      else { d->efc_force[r] = -D * Jaref; state = STATE_QUADRATIC; c->cost += (real)0.5 * D * Jaref * Jaref; }
+    }
+    d->efc_state[r] = state;
+  }
+  for (int i = 0; i < nv; i++) {
+    real s = 0;
+    for (int r = 0; r < nefc; r++) s += d->efc_J[(size_t)r * nv + i] * d->efc_force[r];
+    d->qfrc_constraint[i] = s;
+  }
+  real g = 0;
+  for (int i = 0; i < nv; i++) g += (d->efc_Ma[i] - d->qfrc_smooth[i]) * (d->qacc[i] - d->qacc_smooth[i]);
+  c->gauss += (real)0.5 * g;
+  c->cost += (real)0.5 * g;
+}
+
+/* solver.py:2879-3008 (CG: Mgrad = M^-1 grad; Newton: H = M + J' D_active J, Cholesky) */
+static void update_gradient(const orc_model* m, orc_data* d, solver_ctx* c) {
+  int nv = m->nv, nefc = *d->nefc < d->njmax ? *d->nefc : d->njmax;
+  c->grad_dot = 0;
+  for (int i = 0; i < nv; i++) {
+    real g = d->efc_Ma[i] - d->qfrc_smooth[i] - d->qfrc_constraint[i];
+    c->grad[i] = g;
+    c->grad_dot += g * g;
+  }
+  if (m->opt_solver == SOLVER_CG) {
+    cholesky_solve(nv, d->qLD, c->grad, c->Mgrad);
+  } else {
+    memcpy(c->H, d->qM, (size_t)nv * nv * sizeof(real));
+    for (int r = 0; r < nefc; r++) {
+      if (d->efc_state[r] != STATE_QUADRATIC) continue;
+      real D = d->efc_D[r];
+      const real* J = d->efc_J + (size_t)r * nv;
+      for (int i = 0; i < nv; i++) {
+        if (J[i] == 0) continue;
+        for (int j = 0; j < nv; j++) c->H[i * nv + j] += D * J[i] * J[j];
+      }
+    }
+    cholesky(nv, c->H, c->HL);
+    cholesky_solve(nv, c->HL, c->grad, c->Mgrad);
+  }
+}
+
+/* per-row (cost, grad, hess) for pyramidal cones, solver.py:570-598 */
+static void eval_row(const orc_data* d, const solver_ctx* c, int r, int ne, int nf, real alpha, real* out) {
+  real D = d->efc_D[r], jaref = c->Jaref[r], jv = c->jv[r];
+  real x = jaref + alpha * jv;
+  if (r >= ne + nf) {
+    if (x < 0) { real jvD = jv * D; out[0] += (real)0.5 * D * x * x; out[1] += jvD * x; out[2] += jv * jvD; }
+    return;
+  }
+  if (r >= ne) {
+    real f = d->efc_frictionloss[r], rf = safe_div(f, D);
+    if ((-rf < x) && (x < rf)) { real jvD = jv * D; out[0] += (real)0.5 * D * x * x; out[1] += jvD * x; out[2] += jv * jvD; }
+    else if (x <= -rf) { out[0] += f * (-(real)0.5 * rf - x); out[1] += -f * jv; }
+    else { out[0] += f * (-(real)0.5 * rf + x); out[1] += f * jv; }
+    return;
+  }
+  real jvD = jv * D;
+  out[0] += (real)0.5 * D * x * x; out[1] += jvD * x; out[2] += jv * jvD;
+}
+
+static int in_bracket(const real* x, const real* y) { return (x[1] < y[1] && y[1] < 0) || (x[1] > y[1] && y[1] > 0); }
+
+/* solver.py:886-1341 (linesearch_iterative) + :1662-1703 */
+static void linesearch(const orc_model* m, orc_data* d, solver_ctx* c) {
+  int nv = m->nv, ne = *d->ne, nf = *d->nf;
+  int nefc = *d->nefc < d->njmax ? *d->nefc : d->njmax;
+  matvec(nv, d->qM, c->search, c->mv);
+  for (int r = 0; r < nefc; r++) {
+    real s = 0;
+    const real* J = d->efc_J + (size_t)r * nv;
+    for (int i = 0; i < nv; i++) s += J[i] * c->search[i];
+    c->jv[r] = s;
+  }
+  real snorm = sqrt(c->search_dot);
+  real scale = m->stat_meaninertia * (real)nv;
+  real gtol = maxr(m->opt_tolerance * m->opt_ls_tolerance * snorm * scale, (real)1e-6);
+  real p0s[3] = {0, 0, 0};
+  for (int r = 0; r < nefc; r++) eval_row(d, c, r, ne, nf, 0, p0s);
+  real qg1 = 0, qg2 = 0;
+  for (int i = 0; i < nv; i++) {
+    qg1 += c->search[i] * (d->efc_Ma[i] - d->qfrc_smooth[i]);
+    qg2 += (real)0.5 * c->search[i] * c->mv[i];
+  }
+  real qg[3] = {c->gauss, qg1, qg2};
+  real p0[3] = {qg[0] + p0s[0], qg[1] + p0s[1], 2 * qg[2] + p0s[2]};
+#define EVAL_GAUSS(out, a) { out[0] = (a) * (a) * qg[2] + (a) * qg[1] + qg[0]; out[1] = 2 * (a) * qg[2] + qg[1]; out[2] = 2 * qg[2]; }
+  real lo_alpha_in = -safe_div(p0[1], p0[2]);
+  real lo_in[3];
+  EVAL_GAUSS(lo_in, lo_alpha_in);
+  for (int r = 0; r < nefc; r++) eval_row(d, c, r, ne, nf, lo_alpha_in, lo_in);
+  real alpha;
+  int initial_converged = fabs(lo_in[1]) < gtol && lo_in[0] < p0[0];
+  if (!initial_converged) {
+    alpha = 0;
+    int lo_less = lo_in[1] < p0[1];
+    real lo[3], hi[3], lo_alpha, hi_alpha;
+    if (lo_less) { memcpy(lo, lo_in, sizeof(lo)); lo_alpha = lo_alpha_in; memcpy(hi, p0, sizeof(hi)); hi_alpha = 0; }
+    else { memcpy(lo, p0, sizeof(lo)); lo_alpha = 0; memcpy(hi, lo_in, sizeof(hi)); hi_alpha = lo_alpha_in; }
+    for (int it = 0; it < m->opt_ls_iterations; it++) {
+      real lo_next_alpha = lo_alpha - safe_div(lo[1], lo[2]);
+      real hi_next_alpha = hi_alpha - safe_div(hi[1], hi[2]);
+      real mid_alpha = (real)0.5 * (lo_alpha + hi_alpha);
+      real lo_next[3], hi_next[3], mid[3];
+      EVAL_GAUSS(lo_next, lo_next_alpha);
+      EVAL_GAUSS(hi_next, hi_next_alpha);
+      EVAL_GAUSS(mid, mid_alpha);
+      for (int r = 0; r < nefc; r++) {
+        eval_row(d, c, r, ne, nf, lo_next_alpha, lo_next);
+        eval_row(d, c, r, ne, nf, hi_next_alpha, hi_next);
+        eval_row(d, c, r, ne, nf, mid_alpha, mid);
+      }
+      int s1 = in_bracket(lo, lo_next);
+      if (s1) { memcpy(lo, lo_next, sizeof(lo)); lo_alpha = lo_next_alpha; }
+      int s2 = in_bracket(lo, mid);
+      if (s2) { memcpy(lo, mid, sizeof(lo)); lo_alpha = mid_alpha; }
+      int s3 = in_bracket(lo, hi_next);
+      if (s3) { memcpy(lo, hi_next, sizeof(lo)); lo_alpha = hi_next_alpha; }
+      int swap_lo = s1 || s2 || s3;
+      int h1 = in_bracket(hi, hi_next);
+      if (h1) { memcpy(hi, hi_next, sizeof(hi)); hi_alpha = hi_next_alpha; }
+      int h2 = in_bracket(hi, mid);
+      if (h2) { memcpy(hi, mid, sizeof(hi)); hi_alpha = mid_alpha; }
+      int h3 = in_bracket(hi, lo_next);
+      if (h3) { memcpy(hi, lo_next, sizeof(hi)); hi_alpha = lo_next_alpha; }
+      int swap_hi = h1 || h2 || h3;
+      int ls_done = (!swap_lo && !swap_hi) || (lo[1] < 0 && lo[1] > -gtol) || (hi[1] > 0 && hi[1] < gtol);
+      int improved = lo[0] < p0[0] || hi[0] < p0[0];
+      int lo_better = lo[0] < hi[0];
+      if (improved && lo_better) alpha = lo_alpha;
+      if (improved && !lo_better) alpha = hi_alpha;
+      if (ls_done) break;
+    }
+  } else {
+    alpha = lo_alpha_in;
+  }
+#undef EVAL_GAUSS
+  for (int i = 0; i < nv; i++) { d->qacc[i] += alpha * c->search[i]; d->efc_Ma[i] += alpha * c->mv[i]; }
+  for (int r = 0; r < nefc; r++) c->Jaref[r] += alpha * c->jv[r];
+}
+
+/* solver.py:3296-3343 (+ init_context :3257-3293, iteration :3187-3254) */
+static void solve(const orc_model* m, orc_data* d) {
+  int nv = m->nv, njmax = d->njmax;
+  if (njmax == 0 || nv == 0) {
+    memcpy(d->qacc, d->qacc_smooth, nv * sizeof(real));
+    *d->solver_niter = 0;
+    return;
+  }
+  real* buf = (real*)calloc((size_t)2 * njmax + 8 * (size_t)nv + 2 * (size_t)nv * nv, sizeof(real));
+  solver_ctx c;
+  c.Jaref = buf; c.jv = buf + njmax;
+  c.grad = buf + 2 * njmax; c.Mgrad = c.grad + nv; c.search = c.Mgrad + nv; c.mv = c.search + nv;
+  c.prev_grad = c.mv + nv; c.prev_Mgrad = c.prev_grad + nv; c.H = c.prev_Mgrad + 2 * nv; c.HL = c.H + nv * nv;
+  if (!(m->opt_disableflags & DSBL_WARMSTART)) memcpy(d->qacc, d->qacc_warmstart, nv * sizeof(real));
+  else memcpy(d->qacc, d->qacc_smooth, nv * sizeof(real));
+  int nefc = *d->nefc < njmax ? *d->nefc : njmax;
+  *d->solver_niter = 0;
+  c.search_dot = 0;
+  c.cost = MAXVAL;
+  c.done = 0;
+  for (int r = 0; r < nefc; r++) {
+    real s = 0;
+    for (int i = 0; i < nv; i++) s += d->efc_J[(size_t)r * nv + i] * d->qacc[i];
+    c.Jaref[r] = s - d->efc_aref[r];
+  }
+  matvec(nv, d->qM, d->qacc, d->efc_Ma);
+  update_constraint(m, d, &c);
+  update_gradient(m, d, &c);
+  for (int i = 0; i < nv; i++) { c.search[i] = -c.Mgrad[i]; c.search_dot += c.search[i] * c.search[i]; }
+  real scale = 1 / (m->stat_meaninertia * (real)nv);
+  if (m->opt_iterations != 0) {
+    while (!c.done) {
+      linesearch(m, d, &c);
+      if (m->opt_solver == SOLVER_CG) {
+        memcpy(c.prev_grad, c.grad, nv * sizeof(real));
+        memcpy(c.prev_Mgrad, c.Mgrad, nv * sizeof(real));
+      }
+      update_constraint(m, d, &c);
+      update_gradient(m, d, &c);
+      real beta = 0;
+      if (m->opt_solver == SOLVER_CG) {
+        real num = 0, den = 0;
+        for (int i = 0; i < nv; i++) {
+          num += c.grad[i] * (c.Mgrad[i] - c.prev_Mgrad[i]);
+          den += c.prev_grad[i] * c.prev_Mgrad[i];
+        }
+        beta = maxr(0, num / maxr(MINVAL, den));
+      }
+      c.search_dot = 0;
+      for (int i = 0; i < nv; i++) {
+        real s = -c.Mgrad[i];
+        if (m->opt_solver == SOLVER_CG) s += beta * c.search[i];
+        c.search[i] = s;
+        c.search_dot += s * s;
+      }
+      (*d->solver_niter)++;
+      real improvement = (c.prev_cost - c.cost) * scale;
+      real gradient = sqrt(c.grad_dot) * scale;
+      int done = (improvement < m->opt_tolerance) || (gradient < m->opt_tolerance);
+      if (done || *d->solver_niter == m->opt_iterations) c.done = 1;
+    }
+  }
+  *d->solver_cost = c.cost;
+  free(buf);
+}
+
+/* forward.py:51-354 (_advance + euler with optional implicit damping) */
+static void euler(const orc_model* m, orc_data* d) {
+  int nv = m->nv;
+  real dt = m->opt_timestep;
+  real* qacc_adv = d->qacc;
+  real* tmp = NULL;
+  if (!(m->opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER))) {
+    tmp = (real*)malloc(((size_t)2 * nv * nv + nv) * sizeof(real));
+    real* Mi = tmp;
+    real* L = tmp + (size_t)nv * nv;
+    real* q = L + (size_t)nv * nv;
+    memcpy(Mi, d->qM, (size_t)nv * nv * sizeof(real));
+    for (int i = 0; i < nv; i++) Mi[i * nv + i] += dt * m->dof_damping[i];
+    cholesky(nv, Mi, L);
+    cholesky_solve(nv, L, d->efc_Ma, q);
+    qacc_adv = q;
+  }
+  /* _next_activation: na-sized, skipped when na == 0 */
+  for (int a = 0; a < m->nu; a++) {
+    int adr = m->actuator_actadr[a];
+    for (int j = adr; j >= 0 && j < adr + m->actuator_actnum[a]; j++) {
+      real act = d->act[j] + d->act_dot[j] * dt;
+      if (m->actuator_actlimited[a]) act = clampr(act, m->actuator_actrange[2 * a], m->actuator_actrange[2 * a + 1]);
+      d->act[j] = act;
+    }
+  }
+  for (int i = 0; i < nv; i++) d->qvel[i] = d->qvel[i] + qacc_adv[i] * dt;
+  for (int j = 0; j < m->njnt; j++) {
+    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j], jt = m->jnt_type[j];
+    if (jt == JNT_FREE) {
+      for (int i = 0; i < 3; i++) d->qpos[qa + i] = d->qpos[qa + i] + dt * d->qvel[da + i];
+      real qn[4];
+      quat_integrate(qn, d->qpos + qa + 3, d->qvel + da + 3, dt);
+      memcpy(d->qpos + qa + 3, qn, sizeof(qn));
+    } else if (jt == JNT_BALL) {
+      real qn[4];
+      quat_integrate(qn, d->qpos + qa, d->qvel + da, dt);
+      memcpy(d->qpos + qa, qn, sizeof(qn));
+    } else {
+      d->qpos[qa] = d->qpos[qa] + dt * d->qvel[da];
+    }
+  }
+  d->time[0] += dt;
+  memcpy(d->qacc_warmstart, d->qacc, nv * sizeof(real));
+  free(tmp);
+}
+
+/* forward.py:972-1000 */
+static void forward_world(const orc_model* m, orc_data* d) {
+  fwd_position(m, d);
+  fwd_velocity(m, d);
+  fwd_actuation(m, d);
+  fwd_acceleration(m, d);
+  solve(m, d);
+}
+
+/* forward.py:1003-1018 */
+static void step_world(const orc_model* m, orc_data* d) {
+  forward_world(m, d);
+  euler(m, d);
+}
+
+int orc_real_size(void) { return (int)sizeof(real); }
+
+#define ORC_BATCH(fn, body)                                                                       \
+  void fn(const orc_model* m, const orc_data* b, int nworld) {                                   \
+    for (int w = 0; w < nworld; w++) { orc_data d; world_view(m, b, w, &d); body(m, &d); }      \
+  }
+ORC_BATCH(orc_fwd_position, fwd_position)
+ORC_BATCH(orc_fwd_velocity, fwd_velocity)
+ORC_BATCH(orc_fwd_actuation, fwd_actuation)
+ORC_BATCH(orc_fwd_acceleration, fwd_acceleration)
+ORC_BATCH(orc_solve, solve)
+ORC_BATCH(orc_euler, euler)
+
+void orc_step(const orc_model* m, const orc_data* b, int nworld, int nthread) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthread > 0 ? nthread : 1)
+#endif
+  for (int w = 0; w < nworld; w++) {
+    orc_data d;
+    world_view(m, b, w, &d);
+    step_world(m, &d);
+  }
+  (void)nthread;
+}
+
+void orc_forward(const orc_model* m, const orc_data* b, int nworld, int nthread) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthread > 0 ? nthread : 1)
+#endif
+  for (int w = 0; w < nworld; w++) {
+    orc_data d;
+    world_view(m, b, w, &d);
+    forward_world(m, &d);
+  }
+  (void)nthread;
+}

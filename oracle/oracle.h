@@ -1,0 +1,149 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C, fp64 by default, fp32 with -DORC_REAL=float) of the
+ * mujoco_warp `step` path for one world at a time.  Each function cites the
+ * reference file:line it restates.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library; the product never does.
+ *
+ * Parity status: the reference (Warp + MuJoCo C) cannot run in this image, so
+ * this oracle is pinned by (a) the reference's MuJoCo-free known-answer tests
+ * (math_test.py segment/segment and triangular-index KATs) and (b) analytic
+ * invariants (see tests/test_oracle.py).  Whole-pipeline outputs are otherwise
+ * "parity unpinned" against MuJoCo C.
+ *
+ * Field lists are X-macros so that the Python ctypes side can build the exact
+ * same structs by parsing this header (tests/oracle_ctypes.py).
+ */
+#ifndef MJW_ORACLE_H
+#define MJW_ORACLE_H
+
+#ifndef ORC_REAL
+#define ORC_REAL double
+#endif
+typedef ORC_REAL real;
+
+/* ---- model: int scalars ---- */
+#define ORC_MODEL_INT_SCALARS(X)                                                                   \
+  X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
+  X(nxn) X(nmaxpyramid) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
+  X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)
+
+/* ---- model: real scalars ---- */
+#define ORC_MODEL_REAL_SCALARS(X)                                                                  \
+  X(opt_timestep) X(opt_tolerance) X(opt_ls_tolerance) X(opt_impratio_invsqrt) X(stat_meaninertia)
+
+/* ---- model: real arrays (name, element count) ---- */
+#define ORC_MODEL_REAL_ARRAYS(X)                                                                   \
+  X(opt_gravity, 3)                                                                                \
+  X(qpos0, nq) X(qpos_spring, nq)                                                                  \
+  X(body_pos, nbody * 3) X(body_quat, nbody * 4) X(body_ipos, nbody * 3) X(body_iquat, nbody * 4) \
+  X(body_mass, nbody) X(body_subtreemass, nbody) X(body_inertia, nbody * 3)                       \
+  X(body_invweight0, nbody * 2)                                                                    \
+  X(jnt_solref, njnt * 2) X(jnt_solimp, njnt * 5) X(jnt_pos, njnt * 3) X(jnt_axis, njnt * 3)      \
+  X(jnt_stiffness, njnt) X(jnt_range, njnt * 2) X(jnt_actfrcrange, njnt * 2) X(jnt_margin, njnt)  \
+  X(dof_solref, nv * 2) X(dof_solimp, nv * 5) X(dof_frictionloss, nv) X(dof_armature, nv)         \
+  X(dof_damping, nv) X(dof_invweight0, nv)                                                         \
+  X(geom_solmix, ngeom) X(geom_solref, ngeom * 2) X(geom_solimp, ngeom * 5) X(geom_size, ngeom * 3) \
+  X(geom_aabb, ngeom * 6) X(geom_rbound, ngeom) X(geom_pos, ngeom * 3) X(geom_quat, ngeom * 4)    \
+  X(geom_friction, ngeom * 3) X(geom_margin, ngeom) X(geom_gap, ngeom)                             \
+  X(site_pos, nsite * 3) X(site_quat, nsite * 4)                                                   \
+  X(cam_pos, ncam * 3) X(cam_quat, ncam * 4) X(cam_poscom0, ncam * 3) X(cam_pos0, ncam * 3)       \
+  X(cam_mat0, ncam * 9)                                                                            \
+  X(light_pos, nlight * 3) X(light_dir, nlight * 3) X(light_poscom0, nlight * 3)                  \
+  X(light_pos0, nlight * 3) X(light_dir0, nlight * 3)                                              \
+  X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
+  X(actuator_ctrlrange, nu * 2) X(actuator_forcerange, nu * 2) X(actuator_actrange, nu * 2)       \
+  X(actuator_gear, nu * 6)
+
+/* ---- model: int arrays (name, element count) ---- */
+#define ORC_MODEL_INT_ARRAYS(X)                                                                    \
+  X(body_parentid, nbody) X(body_rootid, nbody) X(body_weldid, nbody) X(body_mocapid, nbody)      \
+  X(body_jntnum, nbody) X(body_jntadr, nbody) X(body_dofnum, nbody) X(body_dofadr, nbody)         \
+  X(jnt_type, njnt) X(jnt_qposadr, njnt) X(jnt_dofadr, njnt) X(jnt_bodyid, njnt)                  \
+  X(jnt_limited, njnt) X(jnt_actfrclimited, njnt)                                                  \
+  X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \
+  X(geom_type, ngeom) X(geom_condim, ngeom) X(geom_bodyid, ngeom) X(geom_priority, ngeom)         \
+  X(site_bodyid, nsite)                                                                            \
+  X(cam_mode, ncam) X(cam_bodyid, ncam) X(cam_targetbodyid, ncam)                                 \
+  X(light_mode, nlight) X(light_bodyid, nlight) X(light_targetbodyid, nlight)                     \
+  X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
+  X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
+  X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
+  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)
+
+/* ---- per-world data: real arrays (name, element count per world) ---- */
+#define ORC_DATA_REAL_ARRAYS(X)                                                                    \
+  X(time, 1) X(qpos, nq) X(qvel, nv) X(act, na) X(ctrl, nu) X(qacc_warmstart, nv)                 \
+  X(qfrc_applied, nv) X(xfrc_applied, nbody * 6) X(mocap_pos, nmocap * 3) X(mocap_quat, nmocap * 4) \
+  X(qacc, nv) X(act_dot, na)                                                                       \
+  X(xpos, nbody * 3) X(xquat, nbody * 4) X(xmat, nbody * 9) X(xipos, nbody * 3) X(ximat, nbody * 9) \
+  X(xanchor, njnt * 3) X(xaxis, njnt * 3) X(geom_xpos, ngeom * 3) X(geom_xmat, ngeom * 9)         \
+  X(site_xpos, nsite * 3) X(site_xmat, nsite * 9) X(cam_xpos, ncam * 3) X(cam_xmat, ncam * 9)     \
+  X(light_xpos, nlight * 3) X(light_xdir, nlight * 3)                                              \
+  X(subtree_com, nbody * 3) X(cdof, nv * 6) X(cinert, nbody * 10) X(crb, nbody * 10)              \
+  X(qM, nv * nv) X(qLD, nv * nv)                                                                   \
+  X(actuator_length, nu) X(actuator_moment, nu * nv) X(actuator_velocity, nu) X(actuator_force, nu) \
+  X(cvel, nbody * 6) X(cdof_dot, nv * 6) X(qfrc_bias, nv) X(qfrc_spring, nv) X(qfrc_damper, nv)   \
+  X(qfrc_passive, nv) X(qfrc_actuator, nv) X(qfrc_smooth, nv) X(qacc_smooth, nv)                  \
+  X(qfrc_constraint, nv) X(cacc, nbody * 6) X(cfrc_int, nbody * 6)                                 \
+  X(efc_J, njmax * nv) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax) X(efc_vel, njmax)   \
+  X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax) X(efc_Ma, nv)                 \
+  X(con_dist, nconmax) X(con_pos, nconmax * 3) X(con_frame, nconmax * 9)                          \
+  X(con_includemargin, nconmax) X(con_friction, nconmax * 5) X(con_solref, nconmax * 2)           \
+  X(con_solreffriction, nconmax * 2) X(con_solimp, nconmax * 5) X(solver_cost, 1)
+
+/* ---- per-world data: int arrays ---- */
+#define ORC_DATA_INT_ARRAYS(X)                                                                     \
+  X(ne, 1) X(nf, 1) X(nl, 1) X(nefc, 1) X(ncon, 1) X(ncollision, 1) X(solver_niter, 1)            \
+  X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax)                                          \
+  X(con_dim, nconmax) X(con_geom, nconmax * 2) X(con_efc_address, nconmax * 10)
+
+typedef struct orc_model {
+#define ORC_DECL_I(name) int name;
+#define ORC_DECL_R(name) real name;
+#define ORC_DECL_RA(name, n) const real* name;
+#define ORC_DECL_IA(name, n) const int* name;
+  ORC_MODEL_INT_SCALARS(ORC_DECL_I)
+  ORC_MODEL_REAL_SCALARS(ORC_DECL_R)
+  ORC_MODEL_REAL_ARRAYS(ORC_DECL_RA)
+  ORC_MODEL_INT_ARRAYS(ORC_DECL_IA)
+} orc_model;
+
+typedef struct orc_data {
+  int njmax;
+  int nconmax;
+#define ORC_DECL_DRA(name, n) real* name;
+#define ORC_DECL_DIA(name, n) int* name;
+  ORC_DATA_REAL_ARRAYS(ORC_DECL_DRA)
+  ORC_DATA_INT_ARRAYS(ORC_DECL_DIA)
+} orc_data;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* batched entry points: `d` points at world 0 of (nworld, ...) arrays */
+int orc_real_size(void);
+void orc_step(const orc_model* m, const orc_data* d, int nworld, int nthread);
+void orc_forward(const orc_model* m, const orc_data* d, int nworld, int nthread);
+/* stage entry points (one stage for all worlds) */
+void orc_fwd_position(const orc_model* m, const orc_data* d, int nworld);
+void orc_fwd_velocity(const orc_model* m, const orc_data* d, int nworld);
+void orc_fwd_actuation(const orc_model* m, const orc_data* d, int nworld);
+void orc_fwd_acceleration(const orc_model* m, const orc_data* d, int nworld);
+void orc_solve(const orc_model* m, const orc_data* d, int nworld);
+void orc_euler(const orc_model* m, const orc_data* d, int nworld);
+/* math KATs (math_test.py) */
+void orc_closest_segment_to_segment_points(const real* a0, const real* a1, const real* b0, const real* b1,
+                                           real* best_a, real* best_b);
+int orc_upper_tri_index(int n, int i, int j);
+int orc_upper_trid_index(int n, int i, int j);
+real orc_halton(int index, int base);
+void orc_ctrl_noise(const orc_model* m, real* ctrl, const real* center, int ncenter, int step, real std,
+                    real rate, int nworld, int world_offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,240 @@
+"""ctypes binding of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  It parses the X-macro field lists of oracle.h so the ctypes
+structs match the C structs exactly, builds the oracle model from a host
+`MjModel` (the NXN pair filter is restated independently of the product, from
+mujoco_warp/_src/io.py:269-358), and runs the oracle over (nworld, ...) numpy
+state arrays.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_BUILD = os.path.join(_HERE, "_build")
+
+
+def build():
+  subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def _macro_entries(text, macro):
+  m = re.search(r"#define\s+" + macro + r"\(X\)(.*?)(?:\n\s*\n|\n/\*)", text, re.S)
+  if not m:
+    raise RuntimeError(f"macro {macro} not found in oracle.h")
+  body = m.group(1).replace("\\\n", " ")
+  return re.findall(r"X\(\s*([A-Za-z_0-9]+)\s*(?:,\s*([^)]*))?\)", body)
+
+
+with open(os.path.join(_HERE, "oracle.h")) as f:
+  _HDR = f.read()
+MODEL_INT_SCALARS = [n for n, _ in _macro_entries(_HDR, "ORC_MODEL_INT_SCALARS")]
+MODEL_REAL_SCALARS = [n for n, _ in _macro_entries(_HDR, "ORC_MODEL_REAL_SCALARS")]
+MODEL_REAL_ARRAYS = _macro_entries(_HDR, "ORC_MODEL_REAL_ARRAYS")
+MODEL_INT_ARRAYS = _macro_entries(_HDR, "ORC_MODEL_INT_ARRAYS")
+DATA_REAL_ARRAYS = _macro_entries(_HDR, "ORC_DATA_REAL_ARRAYS")
+DATA_INT_ARRAYS = _macro_entries(_HDR, "ORC_DATA_INT_ARRAYS")
+
+_LIBS = {}
+
+
+def _lib(real_bits):
+  if real_bits not in _LIBS:
+    path = os.path.join(_BUILD, f"liborc{real_bits}.so")
+    if not os.path.exists(path):
+      build()
+    lib = ctypes.CDLL(path)
+    _LIBS[real_bits] = lib
+  return _LIBS[real_bits]
+
+
+def _structs(real_bits):
+  creal = ctypes.c_double if real_bits == 64 else ctypes.c_float
+  mfields = [(n, ctypes.c_int) for n in MODEL_INT_SCALARS]
+  mfields += [(n, creal) for n in MODEL_REAL_SCALARS]
+  mfields += [(n, ctypes.POINTER(creal)) for n, _ in MODEL_REAL_ARRAYS]
+  mfields += [(n, ctypes.POINTER(ctypes.c_int)) for n, _ in MODEL_INT_ARRAYS]
+  dfields = [("njmax", ctypes.c_int), ("nconmax", ctypes.c_int)]
+  dfields += [(n, ctypes.POINTER(creal)) for n, _ in DATA_REAL_ARRAYS]
+  dfields += [(n, ctypes.POINTER(ctypes.c_int)) for n, _ in DATA_INT_ARRAYS]
+
+  class OrcModel(ctypes.Structure):
+    _fields_ = mfields
+
+  class OrcData(ctypes.Structure):
+    _fields_ = dfields
+
+  return creal, OrcModel, OrcData
+
+
+def nxn_pairs(mjm):
+  """NXN candidate pair list (restatement of io.py:269-358, contact pairs only)."""
+  ng = mjm.ngeom
+  g1, g2 = np.triu_indices(ng, k=1)
+  b1, b2 = mjm.geom_bodyid[g1], mjm.geom_bodyid[g2]
+  w1, w2 = mjm.body_weldid[b1], mjm.body_weldid[b2]
+  wp1 = mjm.body_weldid[mjm.body_parentid[w1]]
+  wp2 = mjm.body_weldid[mjm.body_parentid[w2]]
+  filterparent = not (mjm.opt.disableflags & (1 << 10))
+  self_col = w1 == w2
+  parent_child = filterparent & (w1 != 0) & (w2 != 0) & ((w1 == wp2) | (w2 == wp1))
+  mask = ((mjm.geom_contype[g1] & mjm.geom_conaffinity[g2]) | (mjm.geom_contype[g2] & mjm.geom_conaffinity[g1])).astype(bool)
+  excl = np.isin((b1 << 16) + b2, getattr(mjm, "exclude_signature", np.zeros(0, dtype=np.int32)))
+  keep = mask & ~self_col & ~parent_child & ~excl
+  pairs = np.stack([g1[keep], g2[keep]], axis=1).astype(np.int32)
+  pairid = np.stack([-np.ones(keep.sum()), -np.ones(keep.sum())], axis=1).astype(np.int32)
+  return pairs, pairid
+
+
+class OracleModel:
+  """Oracle view of a host MjModel (one, unbatched model)."""
+
+  def __init__(self, mjm, real_bits=64, overrides=None):
+    self.real_bits = real_bits
+    self.lib = _lib(real_bits)
+    self.creal, self.StructM, self.StructD = _structs(real_bits)
+    self.dtype = np.float64 if real_bits == 64 else np.float32
+    self.mjm = mjm
+    pairs, pairid = nxn_pairs(mjm)
+    o = mjm.opt
+    vals = dict(
+      nq=mjm.nq, nv=mjm.nv, nu=mjm.nu, na=mjm.na, nbody=mjm.nbody, njnt=mjm.njnt, ngeom=mjm.ngeom, nsite=mjm.nsite,
+      ncam=mjm.ncam, nlight=mjm.nlight, nmocap=mjm.nmocap, nxn=len(pairs),
+      nmaxpyramid=max(1, 2 * (int(np.concatenate(([0], mjm.geom_condim)).max()) - 1)),
+      opt_integrator=o.integrator, opt_cone=o.cone, opt_solver=o.solver, opt_iterations=o.iterations,
+      opt_ls_iterations=o.ls_iterations, opt_disableflags=o.disableflags, opt_enableflags=o.enableflags,
+      opt_broadphase_filter=1 | 2 | 8,
+      opt_timestep=o.timestep, opt_tolerance=max(o.tolerance, 1e-6), opt_ls_tolerance=o.ls_tolerance,
+      opt_impratio_invsqrt=1.0 / np.sqrt(max(o.impratio, 1e-15)), stat_meaninertia=mjm.stat.meaninertia,
+    )
+    if overrides:
+      vals.update(overrides)
+    self.sizes = {k: int(v) for k, v in vals.items() if k in MODEL_INT_SCALARS}
+    arrays = dict(
+      opt_gravity=o.gravity, nxn_geom_pair=pairs, nxn_pairid=pairid,
+      cam_mat0=getattr(mjm, "cam_mat0", np.zeros((mjm.ncam, 9))),
+    )
+    self._keep = []
+    s = self.StructM()
+    for n in MODEL_INT_SCALARS:
+      setattr(s, n, int(vals[n]))
+    for n in MODEL_REAL_SCALARS:
+      setattr(s, n, float(vals[n]))
+    for n, cnt in MODEL_REAL_ARRAYS:
+      a = arrays[n] if n in arrays else getattr(mjm, n)
+      a = np.ascontiguousarray(np.asarray(a, dtype=self.dtype).reshape(-1))
+      assert a.size == eval(cnt, {}, self.sizes), (n, a.size)
+      self._keep.append(a)
+      setattr(s, n, a.ctypes.data_as(ctypes.POINTER(self.creal)))
+    for n, cnt in MODEL_INT_ARRAYS:
+      a = arrays[n] if n in arrays else getattr(mjm, n)
+      a = np.ascontiguousarray(np.asarray(a).astype(np.int32).reshape(-1))
+      assert a.size == eval(cnt, {}, self.sizes), (n, a.size)
+      self._keep.append(a)
+      setattr(s, n, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    self.struct = s
+    self.nxn = len(pairs)
+
+
+class OracleData:
+  """(nworld, ...) numpy state/output arrays driven by the oracle."""
+
+  def __init__(self, om: OracleModel, nworld: int, njmax: int, nconmax: int):
+    self.om = om
+    self.nworld, self.njmax, self.nconmax = nworld, njmax, nconmax
+    sizes = dict(om.sizes, njmax=njmax, nconmax=nconmax)
+    self.arrays = {}
+    s = om.StructD()
+    s.njmax, s.nconmax = njmax, nconmax
+    for n, cnt in DATA_REAL_ARRAYS:
+      a = np.zeros((nworld, max(eval(cnt, {}, sizes), 0)), dtype=om.dtype)
+      self.arrays[n] = a
+      setattr(s, n, a.ctypes.data_as(ctypes.POINTER(om.creal)))
+    for n, cnt in DATA_INT_ARRAYS:
+      a = np.zeros((nworld, max(eval(cnt, {}, sizes), 0)), dtype=np.int32)
+      self.arrays[n] = a
+      setattr(s, n, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    self.struct = s
+    m = om.mjm
+    self.arrays["qpos"][:] = m.qpos0
+    if m.nmocap:
+      self.arrays["mocap_quat"][:] = np.tile([1.0, 0, 0, 0], m.nmocap)
+
+  def __getattr__(self, name):
+    arrays = self.__dict__.get("arrays")
+    if arrays is not None and name in arrays:
+      return arrays[name]
+    raise AttributeError(name)
+
+  def _call(self, fn, *extra):
+    getattr(self.om.lib, fn)(ctypes.byref(self.om.struct), ctypes.byref(self.struct), ctypes.c_int(self.nworld), *extra)
+
+  def step(self, nthread=1):
+    self._call("orc_step", ctypes.c_int(nthread))
+
+  def forward(self, nthread=1):
+    self._call("orc_forward", ctypes.c_int(nthread))
+
+  def fwd_position(self):
+    self._call("orc_fwd_position")
+
+  def fwd_velocity(self):
+    self._call("orc_fwd_velocity")
+
+  def fwd_actuation(self):
+    self._call("orc_fwd_actuation")
+
+  def fwd_acceleration(self):
+    self._call("orc_fwd_acceleration")
+
+  def solve(self):
+    self._call("orc_solve")
+
+  def euler(self):
+    self._call("orc_euler")
+
+  def ctrl_noise(self, step, center=None, std=0.01, rate=0.1, world_offset=0):
+    om = self.om
+    c = np.zeros(0, dtype=om.dtype) if center is None else np.ascontiguousarray(center, dtype=om.dtype)
+    om.lib.orc_ctrl_noise(
+      ctypes.byref(om.struct),
+      self.arrays["ctrl"].ctypes.data_as(ctypes.POINTER(om.creal)),
+      c.ctypes.data_as(ctypes.POINTER(om.creal)),
+      ctypes.c_int(c.size),
+      ctypes.c_int(step),
+      om.creal(std),
+      om.creal(rate),
+      ctypes.c_int(self.nworld),
+      ctypes.c_int(world_offset),
+    )
+
+
+def kat_closest_segment_points(a0, a1, b0, b1, real_bits=64):
+  lib = _lib(real_bits)
+  creal = ctypes.c_double if real_bits == 64 else ctypes.c_float
+  dt = np.float64 if real_bits == 64 else np.float32
+  args = [np.ascontiguousarray(x, dtype=dt) for x in (a0, a1, b0, b1)]
+  ba, bb = np.zeros(3, dt), np.zeros(3, dt)
+  lib.orc_closest_segment_to_segment_points(*[x.ctypes.data_as(ctypes.POINTER(creal)) for x in args + [ba, bb]])
+  return ba, bb
+
+
+def kat_upper_tri_index(n, i, j):
+  return _lib(64).orc_upper_tri_index(n, i, j)
+
+
+def kat_upper_trid_index(n, i, j):
+  return _lib(64).orc_upper_trid_index(n, i, j)
+
+
+def halton(index, base):
+  f = _lib(64).orc_halton
+  f.restype = ctypes.c_double
+  return f(ctypes.c_int(index), ctypes.c_int(base))
