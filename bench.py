@@ -1,0 +1,205 @@
+"""Benchmark: env-steps/s of the batched humanoid step (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): benchmarks/humanoid/humanoid.xml, nworld=8192
+per GPU, fp32, Euler + CG (opt.solver override), nconmax=24, njmax=64
+(benchmarks/config.txt:21), state from keyframe 0 ("squat"), qvel = warmstart = 0,
+and before every step the reference's Ornstein-Uhlenbeck + Halton control noise
+(_src/benchmark.py:41-83, std 0.01, rate 0.1, global world ids).  One "step" =
+ctrl_noise + mjw.step over all worlds; the timed region contains exactly K steps
+(ctrl_noise included, i.e. slightly conservative vs the reference which times
+only the graph replay).
+
+Multi-GPU: one process per GPU (torch.distributed.run); each rank owns 8192
+worlds (weak scaling, world ids offset by rank), no collective on the data
+path; a barrier + max-over-ranks of the elapsed time brackets the timed region.
+
+Also reported: `roofline` for the fused step kernel (algorithmic bytes per
+env-step from SURVEY.md 8(d) over its HIP-event duration vs 8 TB/s HBM peak,
+traffic from the committed rocprofv3 PMC summary) and `cpu_baseline` (the fp64
+C oracle, OpenMP over worlds on the host cores, bounded sample, rank 0 only).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (whole node), humanoid.xml nworld=8192 at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+
+
+def b_alg(nefc_mean, ncon_mean):
+  """Algorithmic HBM bytes per env-step: state in + Data contract out, fp32."""
+  return 4.0 * (4170.0 + 38.0 * (nefc_mean + ncon_mean))
+
+
+def parse():
+  p = argparse.ArgumentParser()
+  p.add_argument("--gpus", type=int, default=1)
+  p.add_argument("--steps", type=int, default=1000)
+  p.add_argument("--warmup", type=int, default=20)
+  p.add_argument("--nworld", type=int, default=8192, help="worlds per GPU")
+  p.add_argument("--solver", default="CG", choices=["CG", "NEWTON"])
+  p.add_argument("--nconmax", type=int, default=24)
+  p.add_argument("--njmax", type=int, default=64)
+  p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
+  p.add_argument("--cpu-worlds", type=int, default=512)
+  p.add_argument("--cpu-steps", type=int, default=1000)
+  p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_humanoid_r01.json"))
+  p.add_argument("--graph", type=int, default=0, help="replay steps through a captured hipGraph")
+  return p.parse_args()
+
+
+def cpu_baseline(mjm, nworld, nsteps):
+  """fp64 C oracle (restatement of the reference step), OpenMP over worlds; rank 0 only."""
+  from oracle import orc
+
+  nthread = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+  nthread = max(1, min(nthread, 16))
+  om = orc.OracleModel(mjm, real_bits=64)
+  od = orc.OracleData(om, nworld, 64, 24)
+  od.qpos[:] = mjm.key_qpos[0]
+  center = np.zeros(mjm.nu)
+  t0 = time.perf_counter()
+  for i in range(nsteps):
+    od.ctrl_noise(i, center=center)
+    od.step(nthread=nthread)
+  dt = time.perf_counter() - t0
+  return dict(
+    value=nworld * nsteps / dt,
+    unit="env-steps/s",
+    cores=nthread,
+    kind="port",
+    sample=f"fp64 C oracle (oracle/oracle.c), humanoid CG, {nworld} worlds x {nsteps} steps from key 0 with ctrl noise, "
+    f"{nthread} OpenMP threads, {dt:.1f} s; the reference's Warp-CPU path is not runnable here (no warp/mujoco)",
+  )
+
+
+def main():
+  args = parse()
+  import torch
+  import torch.distributed as dist
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+
+  rank = int(os.environ.get("RANK", "0"))
+  world = int(os.environ.get("WORLD_SIZE", "1"))
+  local = int(os.environ.get("LOCAL_RANK", "0"))
+  if world > 1:
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+  dev = torch.device("cuda", local)
+
+  mjm = mjcf.load_model(os.path.join(ROOT, "models", "humanoid.xml"))
+  mjw.override_model(mjm, [f"opt.solver={args.solver}"])
+  mjd = mjcf.MjData(mjm)
+  mjcf.reset_data_keyframe(mjm, mjd, 0)
+  m = mjw.put_model(mjm, device=dev)
+  d = mjw.put_data(mjm, mjd, nworld=args.nworld, nconmax=args.nconmax, njmax=args.njmax, device=dev, m=m)
+  d.world_offset = rank * args.nworld
+  center = torch.zeros(mjm.nu, dtype=torch.float32, device=dev)
+
+  def one_step(i, ev=None):
+    mjw.ctrl_noise(m, d, i, center=center)
+    if ev is not None:
+      ev[0].record()
+    mjw.step(m, d)
+    if ev is not None:
+      ev[1].record()
+
+  for i in range(args.warmup):
+    one_step(i)
+  torch.cuda.synchronize()
+  # sizes for the algorithmic-bytes figure (untimed)
+  nefc_mean = float(d.nefc.float().mean())
+  ncon_mean = float(d.nacon[0]) / args.nworld
+
+  events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for i in range(args.steps):
+    one_step(args.warmup + i, events[i])
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  elapsed = time.perf_counter() - t0
+  kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+  nefc_mean = 0.5 * (nefc_mean + float(d.nefc.float().mean()))
+  ncon_mean = 0.5 * (ncon_mean + float(d.nacon[0]) / args.nworld)
+  converged = int((~torch.isnan(d.qpos).any(dim=1)).sum())
+
+  if world > 1:
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms = float(t[0]), float(t[1])
+    c = torch.tensor([converged], dtype=torch.int64, device=dev)
+    dist.all_reduce(c)
+    converged = int(c[0])
+
+  total_steps = args.nworld * world * args.steps
+  value = total_steps / elapsed
+  if rank == 0:
+    bytes_per_launch = b_alg(nefc_mean, ncon_mean) * args.nworld
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc):
+      with open(args.pmc) as f:
+        pmc = json.load(f)
+      if pmc.get("solver", "CG") == args.solver and pmc.get("nworld") == args.nworld:
+        traffic = pmc.get("hbm_bytes_per_launch")
+    out = {
+      "metric": METRIC,
+      "value": value,
+      "unit": "env-steps/s",
+      "n_gpus": world,
+      "steps": args.steps,
+      "warmup": args.warmup,
+      "ms_per_step": elapsed / args.steps * 1e3,
+      "higher_is_better": True,
+      "scaling": "weak",
+      "vs_baseline": None,
+      "dtype": "fp32",
+      "data": "synthetic (keyframe 'squat' + OU/Halton ctrl noise, no dataset)",
+      "config": {
+        "workload": f"humanoid.xml nworld={args.nworld} per GPU fp32, Euler+{args.solver}, 1xMI355X per rank",
+        "nworld_per_gpu": args.nworld,
+        "nconmax": args.nconmax,
+        "njmax": args.njmax,
+        "solver": args.solver,
+        "parallelism": f"worlds sharded over {world} GPU(s), no collective",
+        "converged_worlds": converged,
+        "nefc_mean": nefc_mean,
+        "ncon_mean": ncon_mean,
+        "solver_niter_mean": float(d.solver_niter.float().mean()),
+      },
+      "roofline": {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "kernel": "mjw::mjw_kernel<63> (fused step)",
+        "kernel_ms": kernel_ms,
+        "alg_bytes_per_env_step": b_alg(nefc_mean, ncon_mean),
+      },
+      "cpu_baseline": None,
+    }
+    if world == 1 and args.cpu_baseline:
+      out["cpu_baseline"] = cpu_baseline(mjm, args.cpu_worlds, args.cpu_steps)
+    print(json.dumps(out), flush=True)
+  if world > 1:
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+  main()
