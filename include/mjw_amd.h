@@ -163,6 +163,11 @@ int mjw_solve(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 /* per-step control noise (Ornstein-Uhlenbeck + Halton) of the reference benchmark;
  * center: device float[nu] or NULL; world ids are d->world_offset + local id */
+/* Device self-checks of the wave primitives of the dense path (no reference counterpart):
+ * which = 0: in = n x 64 floats, out[w] = sum of chunk w, out[n + 64w + l] = in[64w + l] + in[64w + (l^32)];
+ * which = 1: in = n row-major 32x32 SPD matrices, out = their inverses (Cholesky + MFMA X^T X). */
+int mjw_selftest(int which, const float* in, float* out, int n, void* stream);
+
 int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* center, int step, float std, float rate,
                    void* stream);
 

@@ -6,8 +6,8 @@ import sys
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_PKG)
-SOURCES = [os.path.join(_PKG, "csrc", "mjw_step.hip")]
-HEADERS = [os.path.join(_PKG, "csrc", "mjw_math.h"), os.path.join(_ROOT, "include", "mjw_amd.h")]
+SOURCES = [os.path.join(_PKG, "csrc", n) for n in ("mjw_step.hip", "mjw_dense.hip")]
+HEADERS = [os.path.join(_PKG, "csrc", n) for n in ("mjw_math.h", "mjw_common.h")] + [os.path.join(_ROOT, "include", "mjw_amd.h")]
 OUT = os.path.join(_PKG, "libmjw_amd.so")
 ARCH = os.environ.get("MJW_OFFLOAD_ARCH", "gfx950")
 
@@ -22,11 +22,24 @@ def needs_build():
 def build(force=False, verbose=False):
   if not force and not needs_build():
     return OUT
-  cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-I", os.path.join(_ROOT, "include"),
-         "-o", OUT] + SOURCES
+  # one object per translation unit, compiled in parallel, then linked
+  flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(_ROOT, "include")]
+  objs, procs = [], []
+  for src in SOURCES:
+    obj = os.path.join(_PKG, "csrc", os.path.basename(src) + ".o")
+    cmd = ["hipcc"] + flags + ["-c", src, "-o", obj]
+    if verbose:
+      print(" ".join(cmd))
+    procs.append(subprocess.Popen(cmd))
+    objs.append(obj)
+  if any(p.wait() != 0 for p in procs):
+    raise RuntimeError("hipcc failed")
+  cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs
   if verbose:
     print(" ".join(cmd))
   subprocess.run(cmd, check=True)
+  for o in objs:
+    os.remove(o)
   return OUT
 
 

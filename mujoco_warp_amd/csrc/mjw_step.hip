@@ -12,36 +12,9 @@
 // fields keep mujoco_warp's world-major shapes (nworld, ...), read once and
 // written once per stage group with lane-contiguous (coalesced) accesses.
 
-#include <hip/hip_runtime.h>
-
-#include <cstdio>
-#include <cstring>
-#include <mutex>
-#include <string>
-
-#include "mjw_amd.h"
-#include "mjw_math.h"
+#include "mjw_common.h"
 
 namespace mjw {
-
-constexpr int LPW = 64;   // lanes per world (one wavefront)
-constexpr int CREC = 32;  // floats per staged contact record
-constexpr int CMAX = 32;  // staged contacts per collision round
-
-enum : int { ST_POS = 1, ST_VEL = 2, ST_ACT = 4, ST_ACC = 8, ST_SOLVE = 16, ST_EULER = 32 };
-enum : int { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
-enum : int { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3 };
-enum : int {
-  DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16, DSBL_SPRING = 32,
-  DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512, DSBL_ACTUATION = 2048,
-  DSBL_REFSAFE = 4096, DSBL_EULERDAMP = 1 << 15
-};
-enum : int { ENBL_ENERGY = 2 };
-enum : int { CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
-enum : int { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3 };
-enum : int { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
-enum : int { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
-enum : int { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
 
 // per-world LDS layout (offsets in 4-byte words)
 struct Lay {
@@ -53,12 +26,16 @@ struct Lay {
   int Jaref, jv, rowcon;
   int act_len, act_vel, act_force, act_mom, act_momdof, act_nnz;
   int con, scratch, iscratch;
+  int nofactor;
   int total;
 };
 
-__host__ inline Lay make_layout(const mjw_model_t& m, int njmax) {
+// nofactor: the kernel stops at qfrc_smooth and the dense kernel does factor/solve/euler,
+// so the Cholesky / Newton / solver row scratch is not allocated
+__host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor = false) {
   Lay L;
   int o = 0;
+  L.nofactor = nofactor;
   auto take = [&](int n) { int r = o; o += (n + 3) & ~3; return r; };
   int nv = m.nv, nb = m.nbody, nj = m.njnt, ng = m.ngeom, nu = m.nu;
   L.nvs = nv | 1;  // odd row stride: conflict-free row and column access
@@ -67,14 +44,20 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax) {
   L.xanchor = take(nj * 3); L.xaxis = take(nj * 3); L.gxpos = take(ng * 3); L.gxmat = take(ng * 9);
   L.subtree_com = take(nb * 3); L.cinert = take(nb * 10); L.crb = take(nb * 10); L.cdof = take(nv * 6);
   L.cdof_dot = take(nv * 6); L.cvel = take(nb * 6); L.cacc = take(nb * 6); L.cfrc = take(nb * 6);
-  L.qM = take(nv * L.nvs); L.L = take(nv * L.nvs);
-  L.H = (m.opt_solver == SOLVER_NEWTON) ? take(nv * L.nvs) : L.L;
+  L.qM = take(nv * L.nvs);
+  L.L = nofactor ? L.qM : take(nv * L.nvs);
+  L.H = (m.opt_solver == SOLVER_NEWTON && !nofactor) ? take(nv * L.nvs) : L.L;
   L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv); L.qacc = take(nv); L.Ma = take(nv); L.qfrc_constraint = take(nv);
   L.qfrc_bias = take(nv); L.qfrc_passive = take(nv); L.qfrc_actuator = take(nv); L.vec = take(2 * nv);
   L.J = take(njmax * L.nvs);
   L.efc_D = take(njmax); L.efc_aref = take(njmax); L.efc_pos = take(njmax); L.efc_margin = take(njmax);
   L.efc_vel = take(njmax); L.efc_frictionloss = take(njmax); L.efc_type = take(njmax); L.efc_id = take(njmax);
-  L.efc_force = take(njmax); L.efc_state = take(njmax); L.Jaref = take(njmax); L.jv = take(njmax); L.rowcon = take(njmax);
+  if (nofactor) {
+    L.efc_force = L.efc_state = L.Jaref = L.jv = -1;
+  } else {
+    L.efc_force = take(njmax); L.efc_state = take(njmax); L.Jaref = take(njmax); L.jv = take(njmax);
+  }
+  L.rowcon = take(njmax);
   L.act_len = take(nu); L.act_vel = take(nu); L.act_force = take(nu); L.act_mom = take(nu * 6); L.act_momdof = take(nu * 6);
   L.act_nnz = take(nu);
   L.con = take(CMAX * CREC);
@@ -107,12 +90,6 @@ __device__ __forceinline__ int wave_scan_incl(int v) {
 }
 
 #define WSYNC() __syncthreads()
-
-// batched model field base pointer for world w (types.py "*" semantics: worldid % nb)
-__device__ __forceinline__ const float* mb(const float* p, int nb, int cnt, int w) {
-  return nb <= 1 ? p : p + (long)(w % nb) * cnt;
-}
-#define MR(name) mb(m.name, m.name##_nb, m.name##_cnt, wid)
 
 struct WS {
   float* s;  // LDS base of this world
@@ -1443,6 +1420,7 @@ __device__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, cons
     s[L.qfrc_smooth + i] = qs;
     d.qfrc_smooth[gi] = qs;
   }
+  if (L.nofactor) return;  // the dense kernel factors qM (mjw_dense.h)
   // factor qM -> L (copy then in-place Cholesky)
   float* Lm = s + L.L;
   for (int e = lane; e < nv * nvs; e += LPW) Lm[e] = s[L.qM + e];
@@ -1935,14 +1913,11 @@ int set_err(hipError_t e, const char* where) {
 }
 
 template <int STAGES>
-int launch(const mjw_model_t* m, const mjw_data_t* d, void* stream, const char* name) {
-  if (!m || !d) { g_err = std::string(name) + ": null model/data"; return -1; }
-  if (d->nworld <= 0) return 0;
-  if (m->nv > 64 || m->nbody > 4096) { g_err = std::string(name) + ": model too large for the dense world-per-wave path"; return -2; }
-  mjw::Lay L = mjw::make_layout(*m, d->njmax);
+int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, const char* name) {
+  constexpr bool nofactor = (STAGES & mjw::ST_NOFACTOR) != 0;
+  mjw::Lay L = mjw::make_layout(*m, d->njmax, nofactor);
   size_t lds = (size_t)L.total * 4;
   if (lds > 160 * 1024) { g_err = std::string(name) + ": per-world LDS working set exceeds 160 KiB"; return -3; }
-  hipStream_t s = (hipStream_t)stream;
   if (STAGES & mjw::ST_POS) {
     hipError_t e = hipMemsetAsync(d->nacon, 0, sizeof(int32_t), s);
     if (e == hipSuccess) e = hipMemsetAsync(d->ncollision, 0, sizeof(int32_t), s);
@@ -1955,6 +1930,46 @@ int launch(const mjw_model_t* m, const mjw_data_t* d, void* stream, const char* 
   hipLaunchKernelGGL(mjw::mjw_kernel<STAGES>, dim3(d->nworld), dim3(64), lds, s, *m, *d, L);
   return set_err(hipGetLastError(), name);
 }
+
+// the register-resident path (mjw_dense.h) covers worlds with nv <= 32 and njmax <= 64
+bool dense_ok(const mjw_model_t* m, const mjw_data_t* d) { return m->nv <= 32 && d->njmax <= 64; }
+
+// stage groups: ST_* bits of the stages to run, in pipeline order
+int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, const char* name) {
+  using namespace mjw;
+  if (!m || !d) { g_err = std::string(name) + ": null model/data"; return -1; }
+  if (d->nworld <= 0) return 0;
+  if (m->nv > 64 || m->nbody > 4096) { g_err = std::string(name) + ": model too large for the dense world-per-wave path"; return -2; }
+  hipStream_t s = (hipStream_t)stream;
+  int rc = 0;
+  if (dense_ok(m, d)) {
+    // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel
+    switch (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC)) {
+      case 0: break;
+      case ST_POS | ST_VEL | ST_ACT | ST_ACC: rc = launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_NOFACTOR>(m, d, s, name); break;
+      case ST_POS: rc = launch_generic<ST_POS>(m, d, s, name); break;
+      case ST_VEL: rc = launch_generic<ST_VEL>(m, d, s, name); break;
+      case ST_ACT: rc = launch_generic<ST_ACT>(m, d, s, name); break;
+      case ST_ACC: rc = launch_generic<ST_ACC | ST_NOFACTOR>(m, d, s, name); break;
+      default: g_err = std::string(name) + ": unsupported stage group"; return -4;
+    }
+    if (rc) return rc;
+    int f = ((stages & ST_ACC) ? DF_FACTOR : 0) | ((stages & ST_SOLVE) ? DF_SOLVE : 0) | ((stages & ST_EULER) ? DF_EULER : 0);
+    if (f == 0) return 0;
+    return set_err((hipError_t)dense_launch(f, m, d, s), name);
+  }
+  switch (stages) {
+    case ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE | ST_EULER: return launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE | ST_EULER>(m, d, s, name);
+    case ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE: return launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE>(m, d, s, name);
+    case ST_POS: return launch_generic<ST_POS>(m, d, s, name);
+    case ST_VEL: return launch_generic<ST_VEL>(m, d, s, name);
+    case ST_ACT: return launch_generic<ST_ACT>(m, d, s, name);
+    case ST_ACC: return launch_generic<ST_ACC>(m, d, s, name);
+    case ST_SOLVE: return launch_generic<ST_SOLVE>(m, d, s, name);
+    case ST_EULER: return launch_generic<ST_EULER>(m, d, s, name);
+    default: g_err = std::string(name) + ": unsupported stage group"; return -4;
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -1966,28 +1981,28 @@ int mjw_sizeof_data(void) { return (int)sizeof(mjw_data_t); }
 int mjw_lds_bytes(const mjw_model_t* m, int njmax) { return mjw::make_layout(*m, njmax).total * 4; }
 
 int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return launch<mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE | mjw::ST_EULER>(m, d, stream, "mjw_step");
+  return run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE | mjw::ST_EULER, "mjw_step");
 }
 int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return launch<mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE>(m, d, stream, "mjw_forward");
+  return run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE, "mjw_forward");
 }
 int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return launch<mjw::ST_POS>(m, d, stream, "mjw_fwd_position");
+  return run(m, d, stream, mjw::ST_POS, "mjw_fwd_position");
 }
 int mjw_fwd_velocity(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return launch<mjw::ST_VEL>(m, d, stream, "mjw_fwd_velocity");
+  return run(m, d, stream, mjw::ST_VEL, "mjw_fwd_velocity");
 }
 int mjw_fwd_actuation(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return launch<mjw::ST_ACT>(m, d, stream, "mjw_fwd_actuation");
+  return run(m, d, stream, mjw::ST_ACT, "mjw_fwd_actuation");
 }
 int mjw_fwd_acceleration(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return launch<mjw::ST_ACC>(m, d, stream, "mjw_fwd_acceleration");
+  return run(m, d, stream, mjw::ST_ACC, "mjw_fwd_acceleration");
 }
 int mjw_solve(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return launch<mjw::ST_SOLVE>(m, d, stream, "mjw_solve");
+  return run(m, d, stream, mjw::ST_SOLVE, "mjw_solve");
 }
 int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return launch<mjw::ST_EULER>(m, d, stream, "mjw_euler");
+  return run(m, d, stream, mjw::ST_EULER, "mjw_euler");
 }
 
 int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* center, int step, float std, float rate, void* stream) {

@@ -1,0 +1,58 @@
+"""Device self-checks of the dense path's wave primitives (mjw_dense.hip) through the C ABI.
+
+dsum (DPP reduction), xhalf_add (v_permlane32_swap) and spd_inverse (register Cholesky +
+v_mfma_f32_32x32x2_f32 X^T X) are checked against numpy on seeded inputs; the MFMA
+accumulator layout is exercised with asymmetric-in-rows data (random SPD matrices).
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(which, x, nout):
+  torch = pytest.importorskip("torch")
+  if not torch.cuda.is_available():
+    pytest.skip("no GPU")
+  from mujoco_warp_amd import _lib
+
+  L = _lib.lib()
+  n = x.shape[0]
+  xin = torch.as_tensor(x, dtype=torch.float32, device="cuda").contiguous()
+  out = torch.full((nout,), float("nan"), dtype=torch.float32, device="cuda")
+  rc = L.mjw_selftest(which, ctypes.c_void_p(xin.data_ptr()), ctypes.c_void_p(out.data_ptr()), n, None)
+  assert rc == 0, L.mjw_last_error()
+  torch.cuda.synchronize()
+  return out.cpu().numpy()
+
+
+def test_wave_sum_and_half_swap():
+  rng = np.random.default_rng(0)
+  n = 256
+  x = rng.normal(size=(n, 64)).astype(np.float32)
+  x[0] = np.arange(64)  # exact integers: total 2016
+  out = _run(0, x, n + n * 64)
+  assert out[0] == 2016.0
+  np.testing.assert_allclose(out[:n], x.astype(np.float64).sum(1), rtol=1e-5, atol=1e-5)
+  half = out[n:].reshape(n, 64)
+  want = x + np.roll(x, 32, axis=1)
+  np.testing.assert_allclose(half, want, rtol=1e-6, atol=1e-6)
+  assert np.array_equal(half[:, :32], half[:, 32:])
+
+
+def test_spd_inverse_mfma_layout():
+  rng = np.random.default_rng(1)
+  n = 128
+  A = rng.normal(size=(n, 32, 32))
+  M = A @ A.transpose(0, 2, 1) / 32 + np.eye(32) * 0.5
+  M[1] = np.diag(np.arange(1, 33, dtype=np.float64))  # diagonal: exact row/column placement
+  out = _run(1, M.astype(np.float32).reshape(n, -1), n * 1024).reshape(n, 32, 32)
+  np.testing.assert_allclose(np.diag(out[1]), 1.0 / np.arange(1, 33), rtol=1e-6)
+  assert np.abs(out[1] - np.diag(np.diag(out[1]))).max() == 0.0
+  want = np.linalg.inv(M)
+  err = np.abs(out - want).max(axis=(1, 2)) / np.abs(want).max(axis=(1, 2))
+  assert err.max() < 1e-4, err.max()
+  assert np.array_equal(out, out.transpose(0, 2, 1))  # X^T X is bitwise symmetric
