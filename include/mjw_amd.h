@@ -28,7 +28,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 1
+#define MJW_ABI_VERSION 2
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -65,7 +65,7 @@
 #define MJW_MODEL_INT_ARRAYS(X)                                                                    \
   X(body_parentid, nbody) X(body_rootid, nbody) X(body_weldid, nbody) X(body_mocapid, nbody)      \
   X(body_jntnum, nbody) X(body_jntadr, nbody) X(body_dofnum, nbody) X(body_dofadr, nbody)         \
-  X(body_subtree_end, nbody) X(level_body, nbody) X(level_adr, nlevel + 1)                        \
+  X(body_subtree_end, nbody) X(body_level, nbody) X(level_body, nbody) X(level_adr, nlevel + 1)    \
   X(jnt_type, njnt) X(jnt_qposadr, njnt) X(jnt_dofadr, njnt) X(jnt_bodyid, njnt)                  \
   X(jnt_limited, njnt) X(jnt_actfrclimited, njnt) X(jnt_limited_slide_hinge_adr, nlimited)        \
   X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \

@@ -19,14 +19,18 @@ def needs_build():
   return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
 
 
-def build(force=False, verbose=False):
-  if not force and not needs_build():
+def build(force=False, verbose=False, out=None, defines=()):
+  """Compile SOURCES into `out` (default libmjw_amd.so); `defines` e.g. ("MJW_PROFILE",)."""
+  OUT_ = out or OUT
+  if out is None and not force and not needs_build():
     return OUT
   # one object per translation unit, compiled in parallel, then linked
   flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(_ROOT, "include")]
+  flags += [f"-D{x}" for x in defines]
+  tag = "_".join(defines).lower()
   objs, procs = [], []
   for src in SOURCES:
-    obj = os.path.join(_PKG, "csrc", os.path.basename(src) + ".o")
+    obj = os.path.join(_PKG, "csrc", os.path.basename(src) + tag + ".o")
     cmd = ["hipcc"] + flags + ["-c", src, "-o", obj]
     if verbose:
       print(" ".join(cmd))
@@ -34,13 +38,13 @@ def build(force=False, verbose=False):
     objs.append(obj)
   if any(p.wait() != 0 for p in procs):
     raise RuntimeError("hipcc failed")
-  cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs
+  cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT_] + objs
   if verbose:
     print(" ".join(cmd))
   subprocess.run(cmd, check=True)
   for o in objs:
     os.remove(o)
-  return OUT
+  return OUT_
 
 
 if __name__ == "__main__":

@@ -40,6 +40,56 @@ __device__ __forceinline__ const float* mb(const float* p, int nb, int cnt, int 
 #define MR(name) mb(m.name, m.name##_nb, m.name##_cnt, wid)
 
 
+// ---- wave primitives ------------------------------------------------------------------------
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ float dpp_src(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROWMASK, 0xf, false));
+}
+
+__device__ __forceinline__ float rdlane(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
+
+// full 64-lane sum, wave-uniform result (must be called with all lanes active)
+__device__ __forceinline__ float dsum(float x) {
+  x += dpp_src<0xb1>(x);        // quad_perm [1,0,3,2]
+  x += dpp_src<0x4e>(x);        // quad_perm [2,3,0,1]  -> quad sums
+  x += dpp_src<0x124>(x);       // row_ror:4
+  x += dpp_src<0x128>(x);       // row_ror:8            -> row (16-lane) sums
+  x += dpp_src<0x142, 0xa>(x);  // row_bcast:15 into rows 1,3
+  x += dpp_src<0x143, 0xc>(x);  // row_bcast:31 into rows 2,3 -> lane 63 holds the total
+  return rdlane(x, 63);
+}
+
+// opt-in phase timers (build with -DMJW_PROFILE): per-phase s_memtime deltas summed over
+// all waves into the translation unit's own g_prof[] (phase ids below), read back with
+// mjw_prof_read (generic kernel) and mjw_prof_read_dense (dense kernel)
+enum : int {
+  PH_LOAD = 0, PH_KIN, PH_COM, PH_CAM, PH_CRB, PH_COLL, PH_TRN, PH_VEL, PH_ACT, PH_ACC, PH_GSOLVE, PH_GEULER,
+  PH_DFACTOR, PH_DSOLVE, PH_DEULER, PH_N
+};
+#ifdef MJW_PROFILE
+static __device__ unsigned long long g_prof[PH_N];
+#define PROF_T0() unsigned long long _pt = __builtin_amdgcn_s_memtime()
+#define PROF_MARK(ph)                                                            \
+  do {                                                                           \
+    unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[ph], _nt - _pt);              \
+    _pt = _nt;                                                                   \
+  } while (0)
+#define MJW_PROF_READER(fname)                                                                  \
+  extern "C" int fname(unsigned long long* out, int reset) {                                    \
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(mjw::g_prof), sizeof(unsigned long long) * mjw::PH_N); \
+    if (e == hipSuccess && reset) {                                                             \
+      unsigned long long z[mjw::PH_N] = {};                                                     \
+      e = hipMemcpyToSymbol(HIP_SYMBOL(mjw::g_prof), z, sizeof(z));                              \
+    }                                                                                           \
+    return (int)e;                                                                              \
+  }
+#else
+#define MJW_PROF_READER(fname)
+#define PROF_T0() (void)0
+#define PROF_MARK(ph) (void)0
+#endif
+
 // dense (register-resident) factor / solve / euler kernel launcher, mjw_dense.hip
 enum : int { DF_FACTOR = 1, DF_SOLVE = 2, DF_EULER = 4 };
 int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);

@@ -28,25 +28,6 @@ constexpr int DSS = 36;             // LDS row stride of the 32x32 scratch (16-B
 constexpr int DJ_WORDS = 64 * DJS;  // 2112
 constexpr int DS_WORDS = 32 * DSS;  // 1152
 
-// ---- wave primitives ------------------------------------------------------------------------
-template <int CTRL, int ROWMASK = 0xf>
-__device__ __forceinline__ float dpp_src(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROWMASK, 0xf, false));
-}
-
-__device__ __forceinline__ float rdlane(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
-
-// full 64-lane sum, wave-uniform result (must be called with all lanes active)
-__device__ __forceinline__ float dsum(float x) {
-  x += dpp_src<0xb1>(x);        // quad_perm [1,0,3,2]
-  x += dpp_src<0x4e>(x);        // quad_perm [2,3,0,1]  -> quad sums
-  x += dpp_src<0x124>(x);       // row_ror:4
-  x += dpp_src<0x128>(x);       // row_ror:8            -> row (16-lane) sums
-  x += dpp_src<0x142, 0xa>(x);  // row_bcast:15 into rows 1,3
-  x += dpp_src<0x143, 0xc>(x);  // row_bcast:31 into rows 2,3 -> lane 63 holds the total
-  return rdlane(x, 63);
-}
-
 // lanes l and l^32 both receive p(l) + p(l^32)
 __device__ __forceinline__ float xhalf_add(float p) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(p), __float_as_uint(p), false, false);
@@ -254,6 +235,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d) {
   const long gi = (long)wid * nv + c;
   const int nvq = (nv + 3) >> 2;
 
+  PROF_T0();
   float qacc = 0.0f, ma = 0.0f;
   f32x16 Mm = {}, Mi = {};
   float qfrc_smooth = 0.0f, qacc_smooth = 0.0f;
@@ -279,6 +261,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d) {
     if ((FLAGS & DF_FACTOR) && lo && dof) d.qacc_smooth[gi] = qacc_smooth;
   }
 
+  PROF_MARK(PH_DFACTOR);
   if (FLAGS & DF_SOLVE) {
     const int njmax = d.njmax;
     const int nefc = min(d.nefc[wid], njmax);
@@ -457,6 +440,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d) {
     }
   }
 
+  PROF_MARK(PH_DSOLVE);
   if (FLAGS & DF_EULER) {
     // ---- forward.py:51-354 (_advance + euler)
     const float dt = MR(opt_timestep)[0];
@@ -518,6 +502,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d) {
     }
     if (lane == 0) d.time[wid] = d.time[wid] + dt;
   }
+  PROF_MARK(PH_DEULER);
 }
 
 // device self-checks of the primitives above (mjw_selftest): which = 0 -> per-wave dsum and
@@ -567,6 +552,8 @@ int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream
 }
 
 }  // namespace mjw
+
+MJW_PROF_READER(mjw_prof_read_dense)
 
 extern "C" int mjw_selftest(int which, const float* in, float* out, int n, void* stream) {
   if (n <= 0) return 0;

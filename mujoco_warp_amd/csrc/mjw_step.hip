@@ -25,7 +25,7 @@ struct Lay {
   int J, efc_D, efc_aref, efc_pos, efc_margin, efc_vel, efc_frictionloss, efc_type, efc_id, efc_force, efc_state;
   int Jaref, jv, rowcon;
   int act_len, act_vel, act_force, act_mom, act_momdof, act_nnz;
-  int con, scratch, iscratch;
+  int con, cmax, jqvel, plist, scratch, iscratch;
   int nofactor;
   int total;
 };
@@ -49,18 +49,25 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
   L.H = (m.opt_solver == SOLVER_NEWTON && !nofactor) ? take(nv * L.nvs) : L.L;
   L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv); L.qacc = take(nv); L.Ma = take(nv); L.qfrc_constraint = take(nv);
   L.qfrc_bias = take(nv); L.qfrc_passive = take(nv); L.qfrc_actuator = take(nv); L.vec = take(2 * nv);
-  L.J = take(njmax * L.nvs);
-  L.efc_D = take(njmax); L.efc_aref = take(njmax); L.efc_pos = take(njmax); L.efc_margin = take(njmax);
-  L.efc_vel = take(njmax); L.efc_frictionloss = take(njmax); L.efc_type = take(njmax); L.efc_id = take(njmax);
+  // nofactor ("direct") mode: constraint rows go straight to global memory (the dense kernel
+  // reads them from there), so J and the row scalars get no LDS; contact staging reuses the
+  // qM region, which is dead once crb_qM has copied qM out
   if (nofactor) {
+    L.J = L.efc_D = L.efc_aref = L.efc_pos = L.efc_margin = L.efc_vel = L.efc_frictionloss = L.efc_type = L.efc_id = -1;
     L.efc_force = L.efc_state = L.Jaref = L.jv = -1;
   } else {
+    L.J = take(njmax * L.nvs);
+    L.efc_D = take(njmax); L.efc_aref = take(njmax); L.efc_pos = take(njmax); L.efc_margin = take(njmax);
+    L.efc_vel = take(njmax); L.efc_frictionloss = take(njmax); L.efc_type = take(njmax); L.efc_id = take(njmax);
     L.efc_force = take(njmax); L.efc_state = take(njmax); L.Jaref = take(njmax); L.jv = take(njmax);
   }
-  L.rowcon = take(njmax);
+  L.rowcon = -1;
+  L.jqvel = take(njmax);
+  L.plist = take(m.nxn);
   L.act_len = take(nu); L.act_vel = take(nu); L.act_force = take(nu); L.act_mom = take(nu * 6); L.act_momdof = take(nu * 6);
   L.act_nnz = take(nu);
-  L.con = take(CMAX * CREC);
+  L.cmax = nofactor ? CMAX / 2 : CMAX;
+  L.con = (nofactor && nv * L.nvs >= L.cmax * CREC) ? L.qM : take(L.cmax * CREC);
   L.scratch = take(64);
   L.iscratch = take(64);
   L.total = o;
@@ -70,11 +77,7 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
 // -------------------------------------------------------------------------------------------
 // wave-level collectives
 // -------------------------------------------------------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+__device__ __forceinline__ float wave_sum(float v) { return dsum(v); }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
@@ -112,81 +115,116 @@ __device__ void kinematics(const mjw_model_t& m, const mjw_data_t& d, const Lay&
   const float* qpos0 = MR(qpos0);
   float* xpos = s + L.xpos;
   float* xquat = s + L.xquat;
+  float* xanc = s + L.xanchor;
+  float* xax = s + L.xaxis;
   if (lane == 0) {
     xpos[0] = xpos[1] = xpos[2] = 0.0f;
     xquat[0] = 1.0f; xquat[1] = xquat[2] = xquat[3] = 0.0f;
   }
-  WSYNC();
-  for (int lvl = 1; lvl < m.nlevel; lvl++) {
-    int beg = m.level_adr[lvl], end = m.level_adr[lvl + 1];
-    for (int idx = beg + lane; idx < end; idx += LPW) {
-      int b = m.level_body[idx];
-      int pid = m.body_parentid[b];
-      int jntadr = m.body_jntadr[b], jntnum = m.body_jntnum[b];
+  // Pass 1 (all bodies in parallel): the body pose relative to its parent frame after its
+  // joints, and each joint's anchor / axis in the parent frame.  smooth.py:44-144 composes the
+  // same chain in world frame level by level; world = parent o local is the same product.
+  // Pass 2 (level by level, LDS only): world pose = parent world pose o local pose.
+  for (int b0 = 0; b0 < m.nbody; b0 += LPW) {
+    const int b = b0 + lane;
+    const bool ok = b > 0 && b < m.nbody;
+    int par = 0, lv = 0;
+    bool absolute = false;
+    float lp[3] = {0.0f, 0.0f, 0.0f}, lq[4] = {1.0f, 0.0f, 0.0f, 0.0f};
+    if (ok) {
+      par = m.body_parentid[b];
+      lv = m.body_level[b];
+      const int jntadr = m.body_jntadr[b], jntnum = m.body_jntnum[b];
       if (jntnum == 1 && m.jnt_type[jntadr] == JNT_FREE) {
+        // free joints live in top-level bodies: the pose is qpos itself (world frame)
+        absolute = true;
         int qa = m.jnt_qposadr[jntadr];
-        float q[4] = {qpos[qa + 3], qpos[qa + 4], qpos[qa + 5], qpos[qa + 6]};
-        normalize4(q);
-        for (int i = 0; i < 3; i++) xpos[3 * b + i] = qpos[qa + i];
-        for (int i = 0; i < 4; i++) xquat[4 * b + i] = q[i];
+        for (int i = 0; i < 4; i++) lq[i] = qpos[qa + 3 + i];
+        normalize4(lq);
         for (int i = 0; i < 3; i++) {
-          s[L.xanchor + 3 * jntadr + i] = qpos[qa + i];
-          s[L.xaxis + 3 * jntadr + i] = jnt_axis[3 * jntadr + i];
+          lp[i] = qpos[qa + i];
+          xanc[3 * jntadr + i] = qpos[qa + i];
+          xax[3 * jntadr + i] = jnt_axis[3 * jntadr + i];
         }
-        continue;
-      }
-      float pos[3], quat[4];
-      int mocapid = m.body_mocapid[b];
-      if (mocapid >= 0) {
-        for (int i = 0; i < 3; i++) pos[i] = d.mocap_pos[(long)wid * m.nmocap * 3 + 3 * mocapid + i];
-        for (int i = 0; i < 4; i++) quat[i] = d.mocap_quat[(long)wid * m.nmocap * 4 + 4 * mocapid + i];
       } else {
-        for (int i = 0; i < 3; i++) pos[i] = body_pos[3 * b + i];
-        for (int i = 0; i < 4; i++) quat[i] = body_quat[4 * b + i];
-      }
-      {
-        float pq[4] = {xquat[4 * pid], xquat[4 * pid + 1], xquat[4 * pid + 2], xquat[4 * pid + 3]};
-        float t[3];
-        rot_vec_quat(t, pos, pq);
-        for (int i = 0; i < 3; i++) pos[i] = t[i] + xpos[3 * pid + i];
-        mul_quat(quat, pq, quat);
-      }
-      for (int k = 0; k < jntnum; k++) {
-        int j = jntadr + k;
-        int qa = m.jnt_qposadr[j];
-        const float* ax = jnt_axis + 3 * j;
-        const float* jp = jnt_pos + 3 * j;
-        float xanchor[3], xaxis[3], t[3];
-        rot_vec_quat(t, jp, quat);
-        for (int i = 0; i < 3; i++) xanchor[i] = t[i] + pos[i];
-        rot_vec_quat(xaxis, ax, quat);
-        int jt = m.jnt_type[j];
-        if (jt == JNT_BALL) {
-          float ql[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]};
-          normalize4(ql);
-          mul_quat(quat, quat, ql);
-          rot_vec_quat(t, jp, quat);
-          for (int i = 0; i < 3; i++) pos[i] = xanchor[i] - t[i];
-        } else if (jt == JNT_SLIDE) {
-          float dq = qpos[qa] - qpos0[qa];
-          for (int i = 0; i < 3; i++) pos[i] += xaxis[i] * dq;
-        } else if (jt == JNT_HINGE) {
-          float ql[4];
-          axis_angle_to_quat(ql, ax, qpos[qa] - qpos0[qa]);
-          mul_quat(quat, quat, ql);
-          rot_vec_quat(t, jp, quat);
-          for (int i = 0; i < 3; i++) pos[i] = xanchor[i] - t[i];
+        int mocapid = m.body_mocapid[b];
+        if (mocapid >= 0) {
+          for (int i = 0; i < 3; i++) lp[i] = d.mocap_pos[(long)wid * m.nmocap * 3 + 3 * mocapid + i];
+          for (int i = 0; i < 4; i++) lq[i] = d.mocap_quat[(long)wid * m.nmocap * 4 + 4 * mocapid + i];
+        } else {
+          for (int i = 0; i < 3; i++) lp[i] = body_pos[3 * b + i];
+          for (int i = 0; i < 4; i++) lq[i] = body_quat[4 * b + i];
         }
-        for (int i = 0; i < 3; i++) {
-          s[L.xanchor + 3 * j + i] = xanchor[i];
-          s[L.xaxis + 3 * j + i] = xaxis[i];
+        for (int k = 0; k < jntnum; k++) {
+          const int j = jntadr + k;
+          const int qa = m.jnt_qposadr[j], jt = m.jnt_type[j];
+          const float* ax = jnt_axis + 3 * j;
+          const float* jp = jnt_pos + 3 * j;
+          float anc[3], axis[3], t[3];
+          rot_vec_quat(t, jp, lq);
+          for (int i = 0; i < 3; i++) anc[i] = t[i] + lp[i];
+          rot_vec_quat(axis, ax, lq);
+          if (jt == JNT_BALL) {
+            float ql[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]};
+            normalize4(ql);
+            mul_quat(lq, lq, ql);
+            rot_vec_quat(t, jp, lq);
+            for (int i = 0; i < 3; i++) lp[i] = anc[i] - t[i];
+          } else if (jt == JNT_SLIDE) {
+            float dq = qpos[qa] - qpos0[qa];
+            for (int i = 0; i < 3; i++) lp[i] += axis[i] * dq;
+          } else if (jt == JNT_HINGE) {
+            float ql[4];
+            axis_angle_to_quat(ql, ax, qpos[qa] - qpos0[qa]);
+            mul_quat(lq, lq, ql);
+            rot_vec_quat(t, jp, lq);
+            for (int i = 0; i < 3; i++) lp[i] = anc[i] - t[i];
+          }
+          for (int i = 0; i < 3; i++) {
+            xanc[3 * j + i] = anc[i];
+            xax[3 * j + i] = axis[i];
+          }
         }
       }
-      normalize4(quat);
-      for (int i = 0; i < 3; i++) xpos[3 * b + i] = pos[i];
-      for (int i = 0; i < 4; i++) xquat[4 * b + i] = quat[i];
     }
-    WSYNC();
+    for (int lvl = 1; lvl < m.nlevel; lvl++) {
+      if (ok && lv == lvl) {
+        float q[4], t[3];
+        if (absolute) {
+          for (int i = 0; i < 4; i++) q[i] = lq[i];
+          for (int i = 0; i < 3; i++) t[i] = lp[i];
+        } else {
+          float pq[4] = {xquat[4 * par], xquat[4 * par + 1], xquat[4 * par + 2], xquat[4 * par + 3]};
+          rot_vec_quat(t, lp, pq);
+          for (int i = 0; i < 3; i++) t[i] += xpos[3 * par + i];
+          mul_quat(q, pq, lq);
+          normalize4(q);
+        }
+        for (int i = 0; i < 3; i++) xpos[3 * b + i] = t[i];
+        for (int i = 0; i < 4; i++) xquat[4 * b + i] = q[i];
+      }
+      WSYNC();
+    }
+  }
+  // joint anchors / axes to world frame (free joints are already there)
+  for (int j = lane; j < m.njnt; j += LPW) {
+    long gj = (long)wid * m.njnt + j;
+    float anc[3], axis[3];
+    for (int i = 0; i < 3; i++) { anc[i] = xanc[3 * j + i]; axis[i] = xax[3 * j + i]; }
+    if (m.jnt_type[j] != JNT_FREE) {
+      int p = m.body_parentid[m.jnt_bodyid[j]];
+      float pq[4] = {xquat[4 * p], xquat[4 * p + 1], xquat[4 * p + 2], xquat[4 * p + 3]}, t[3];
+      rot_vec_quat(t, anc, pq);
+      for (int i = 0; i < 3; i++) anc[i] = t[i] + xpos[3 * p + i];
+      rot_vec_quat(t, axis, pq);
+      for (int i = 0; i < 3; i++) axis[i] = t[i];
+    }
+    for (int i = 0; i < 3; i++) {
+      xanc[3 * j + i] = anc[i];
+      xax[3 * j + i] = axis[i];
+      d.xanchor[gj * 3 + i] = anc[i];
+      d.xaxis[gj * 3 + i] = axis[i];
+    }
   }
   // body matrices / inertial frames (smooth.py:146-173)
   const float* body_ipos = MR(body_ipos);
@@ -205,10 +243,6 @@ __device__ void kinematics(const mjw_model_t& m, const mjw_data_t& d, const Lay&
     for (int i = 0; i < 3; i++) { d.xpos[(gb + b) * 3 + i] = xpos[3 * b + i]; d.xipos[(gb + b) * 3 + i] = xi[i]; }
     for (int i = 0; i < 4; i++) d.xquat[(gb + b) * 4 + i] = q[i];
     for (int i = 0; i < 9; i++) { d.xmat[(gb + b) * 9 + i] = mat[i]; d.ximat[(gb + b) * 9 + i] = imat[i]; }
-  }
-  for (int j = lane; j < m.njnt; j += LPW) {
-    long gj = (long)wid * m.njnt + j;
-    for (int i = 0; i < 3; i++) { d.xanchor[gj * 3 + i] = s[L.xanchor + 3 * j + i]; d.xaxis[gj * 3 + i] = s[L.xaxis + 3 * j + i]; }
   }
   // geoms (smooth.py:176-203) -- static world geoms evaluate to the same pose
   const float* geom_pos = MR(geom_pos);
@@ -761,7 +795,7 @@ __device__ void contact_params(const mjw_model_t& m, int wid, int g1, int g2, fl
 // constraint.py
 // -------------------------------------------------------------------------------------------
 // constraint.py:52-121 (writes LDS row scalars)
-__device__ void efc_row(const mjw_model_t& m, const Lay& L, float* s, int wid, int r, float pos_aref, float pos_imp,
+__device__ void efc_row(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, float* s, int wid, int r, float pos_aref, float pos_imp,
                         float invweight, const float* solref, const float* solimp, float margin, float vel, float frictionloss,
                         int type, int id) {
   float timestep = MR(opt_timestep)[0];
@@ -785,15 +819,28 @@ __device__ void efc_row(const mjw_model_t& m, const Lay& L, float* s, int wid, i
   float imp = dmin + imp_y * (dmax - dmin);
   imp = clampf(imp, dmin, dmax);
   if (imp_x > 1.0f) imp = dmax;
-  s[L.efc_D + r] = 1.0f / fmaxf(invweight * (1.0f - imp) / imp, MJW_MINVAL);
-  s[L.efc_vel + r] = vel;
-  s[L.efc_aref + r] = -k * imp * pos_aref - b * vel;
-  s[L.efc_pos + r] = pos_aref + margin;
-  s[L.efc_margin + r] = margin;
-  s[L.efc_frictionloss + r] = frictionloss;
-  int* si = reinterpret_cast<int*>(s);
-  si[L.efc_type + r] = type;
-  si[L.efc_id + r] = id;
+  float D = 1.0f / fmaxf(invweight * (1.0f - imp) / imp, MJW_MINVAL);
+  float aref = -k * imp * pos_aref - b * vel;
+  long gr = (long)wid * d.njmax + r;
+  d.efc_D[(long)wid * d.njmax_pad + r] = D;
+  d.efc_vel[gr] = vel;
+  d.efc_aref[gr] = aref;
+  d.efc_pos[gr] = pos_aref + margin;
+  d.efc_margin[gr] = margin;
+  d.efc_frictionloss[gr] = frictionloss;
+  d.efc_type[gr] = type;
+  d.efc_id[gr] = id;
+  if (L.efc_D >= 0) {  // generic fused solver reads them from LDS
+    s[L.efc_D + r] = D;
+    s[L.efc_aref + r] = aref;
+    s[L.efc_frictionloss + r] = frictionloss;
+  }
+}
+
+// one entry of constraint Jacobian row r (LDS in the generic layout, else global efc_J)
+__device__ __forceinline__ void put_J(const mjw_data_t& d, const Lay& L, float* s, int wid, int np, int r, int k, float v) {
+  if (L.J >= 0) s[L.J + r * L.nvs + k] = v;
+  else d.efc_J[((long)wid * d.njmax_pad + r) * np + k] = v;
 }
 
 // support.py:396-432 restricted to one dof; returns jacp, jacr (zero when not in tree)
@@ -825,6 +872,10 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
   const float* qvel = s + L.qvel;
   int nefc = 0, nf = 0, nl = 0;
   const bool dsbl_constraint = m.opt_disableflags & DSBL_CONSTRAINT;
+  const int np = m.nv_pad;
+  const int kJ = L.J >= 0 ? nv : np;  // global rows also get their zero padding
+  const int CM = L.cmax;
+  WSYNC();  // contact staging may alias the qM region read by crb_qM
 
   // --- friction dof rows (constraint.py:1113-1190)
   if (!dsbl_constraint && !(m.opt_disableflags & DSBL_FRICTIONLOSS)) {
@@ -839,8 +890,8 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
       int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
       int r = nefc + rank;
       if (act && r < njmax) {
-        for (int k = 0; k < nv; k++) s[L.J + r * nvs + k] = (k == i) ? 1.0f : 0.0f;
-        efc_row(m, L, s, wid, r, 0.0f, 0.0f, dof_invweight0[i], dof_solref + 2 * i, dof_solimp + 5 * i, 0.0f, qvel[i],
+        for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, (k == i) ? 1.0f : 0.0f);
+        efc_row(m, d, L, s, wid, r, 0.0f, 0.0f, dof_invweight0[i], dof_solref + 2 * i, dof_solimp + 5 * i, 0.0f, qvel[i],
                 dof_frictionloss[i], CNSTR_FRICTION_DOF, i);
       }
       int cnt = __popcll(bal);
@@ -875,8 +926,8 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
       if (act && r < njmax) {
         int da = m.jnt_dofadr[j];
         float Jv = (float)(dmn < dmx) * 2.0f - 1.0f;
-        for (int k = 0; k < nv; k++) s[L.J + r * nvs + k] = (k == da) ? Jv : 0.0f;
-        efc_row(m, L, s, wid, r, pos, pos, dof_invweight0[da], jnt_solref + 2 * j, jnt_solimp + 5 * j, jm, Jv * qvel[da], 0.0f,
+        for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, (k == da) ? Jv : 0.0f);
+        efc_row(m, d, L, s, wid, r, pos, pos, dof_invweight0[da], jnt_solref + 2 * j, jnt_solimp + 5 * j, jm, Jv * qvel[da], 0.0f,
                 CNSTR_LIMIT_JOINT, j);
       }
       int cnt = __popcll(bal);
@@ -891,64 +942,81 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
   if (do_contact) {
     const float* body_invweight0 = MR(body_invweight0);
     const float impratio_invsqrt = MR(opt_impratio_invsqrt)[0];
-    int ncollision = 0;
+    // broadphase over all pairs once; survivors (in pair order) -> plist
+    int npass = 0;
+    int* plist = si + L.plist;
+    for (int base = 0; base < m.nxn; base += LPW) {
+      int p = base + lane;
+      bool pass = false;
+      if (p < m.nxn) {
+        int g1 = m.nxn_geom_pair[2 * p], g2 = m.nxn_geom_pair[2 * p + 1];
+        pass = m.nxn_pairid[2 * p + 1] >= 0 || broadphase_filter(m, L, s, wid, g1, g2);
+      }
+      unsigned long long bal = __ballot(pass);
+      int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
+      if (pass) plist[npass + rank] = p;
+      npass += __popcll(bal);
+    }
+    if (lane == 0 && npass > 0) atomicAdd(d.ncollision, npass);
+    WSYNC();
+    const float* geom_margin = MR(geom_margin);
     int round = 0;
     while (true) {
-      const int rbeg = round * CMAX, rend = rbeg + CMAX;
+      const int rbeg = round * CM, rend = rbeg + CM;
       int running = 0;  // contacts found so far (world-local, in pair order)
-      for (int base = 0; base < m.nxn; base += LPW) {
-        int p = base + lane;
+      for (int base = 0; base < npass; base += LPW) {
+        int k = base + lane;
         Con2 c;
         c.n = 0;
-        bool pass = false;
-        int g1 = 0, g2 = 0;
-        float margin = 0.0f, gap = 0.0f, friction[5], solref[2], solimp[5];
-        int condim = 0;
-        if (p < m.nxn) {
+        int g1 = 0, g2 = 0, pairid0 = -2;
+        float margin = 0.0f;
+        if (k < npass) {
+          int p = plist[k];
           g1 = m.nxn_geom_pair[2 * p];
           g2 = m.nxn_geom_pair[2 * p + 1];
-          int pairid1 = m.nxn_pairid[2 * p + 1];
-          pass = broadphase_filter(m, L, s, wid, g1, g2) || pairid1 >= 0;
-          if (pass) {
-            contact_params(m, wid, g1, g2, &margin, &gap, &condim, friction, solref, solimp);
-            narrowphase(m, L, s, wid, g1, g2, margin, c);
-          }
+          pairid0 = m.nxn_pairid[2 * p];
+          margin = geom_margin[g1] + geom_margin[g2];
+          narrowphase(m, L, s, wid, g1, g2, margin, c);
         }
-        if (round == 0) ncollision += __popcll(__ballot(pass));
         // active contacts (write_contact collision_core.py:199-213)
-        int pairid0 = p < m.nxn ? m.nxn_pairid[2 * p] : -2;
         bool a0 = c.n > 0 && c.dist[0] < margin && pairid0 >= -1;
         bool a1 = c.n > 1 && c.dist[1] < margin && pairid0 >= -1;
         int cnt = (int)a0 + (int)a1;
         int incl = wave_scan_incl(cnt);
         int first = running + incl - cnt;
-        int k = 0;
-        for (int sub = 0; sub < 2; sub++) {
-          bool a = sub == 0 ? a0 : a1;
-          if (!a) continue;
-          int idx = first + k;
-          k++;
-          if (idx >= rbeg && idx < rend) {
-            float* rec = s + L.con + (idx - rbeg) * CREC;
-            rec[0] = c.dist[sub];
-            rec[1] = margin - gap;
-            for (int i = 0; i < 3; i++) rec[2 + i] = c.pos[sub][i];
-            for (int i = 0; i < 9; i++) rec[5 + i] = c.frame[sub][i];
-            for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
-            rec[19] = solref[0]; rec[20] = solref[1];
-            rec[21] = 0.0f; rec[22] = 0.0f;
-            for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
-            int* reci = reinterpret_cast<int*>(rec);
-            reci[28] = condim;
-            reci[29] = g1;
-            reci[30] = g2;
+        bool stage0 = a0 && first >= rbeg && first < rend;
+        bool stage1 = a1 && first + (int)a0 >= rbeg && first + (int)a0 < rend;
+        if (stage0 || stage1) {
+          float gap, friction[5], solref[2], solimp[5];
+          int condim;
+          contact_params(m, wid, g1, g2, &margin, &gap, &condim, friction, solref, solimp);
+          int kk = 0;
+          for (int sub = 0; sub < 2; sub++) {
+            bool a = sub == 0 ? a0 : a1;
+            if (!a) continue;
+            int idx = first + kk;
+            kk++;
+            if (idx >= rbeg && idx < rend) {
+              float* rec = s + L.con + (idx - rbeg) * CREC;
+              rec[0] = c.dist[sub];
+              rec[1] = margin - gap;
+              for (int i = 0; i < 3; i++) rec[2 + i] = c.pos[sub][i];
+              for (int i = 0; i < 9; i++) rec[5 + i] = c.frame[sub][i];
+              for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
+              rec[19] = solref[0]; rec[20] = solref[1];
+              rec[21] = 0.0f; rec[22] = 0.0f;
+              for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
+              int* reci = reinterpret_cast<int*>(rec);
+              reci[28] = condim;
+              reci[29] = g1;
+              reci[30] = g2;
+            }
           }
         }
         running += __shfl(incl, 63, 64);
       }
       ncon_total = running;
-      if (round == 0 && lane == 0) atomicAdd(d.ncollision, ncollision);
-      int nstage = min(CMAX, running - rbeg);
+      int nstage = min(CM, running - rbeg);
       if (nstage <= 0) break;
       // global pool slot for this round (one atomic per world per round)
       int gbase = 0;
@@ -995,7 +1063,7 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
           }
         }
       }
-      // J entries: lane = dof, loop over staged contacts
+      // J entries: lane = dof, loop over staged contacts; efc_vel = J qvel by wave reduction
       for (int cc = 0; cc < nstage; cc++) {
         const float* rec = s + L.con + cc * CREC;
         const int* reci = reinterpret_cast<const int*>(rec);
@@ -1008,27 +1076,31 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
         int b2 = m.body_weldid[m.geom_bodyid[reci[30]]];
         const float* cpos = rec + 2;
         const float* frame = rec + 5;
-        for (int i = lane; i < nv; i += LPW) {
+        const int i = lane;
+        float jdp[3] = {0.0f, 0.0f, 0.0f}, jdr[3] = {0.0f, 0.0f, 0.0f};
+        if (i < nv) {
           float j1p[3], j1r[3], j2p[3], j2r[3];
           jac_dof(m, L, s, cpos, b1, i, j1p, j1r);
           jac_dof(m, L, s, cpos, b2, i, j2p, j2r);
-          float jdp[3] = {j2p[0] - j1p[0], j2p[1] - j1p[1], j2p[2] - j1p[2]};
-          float jdr[3] = {j2r[0] - j1r[0], j2r[1] - j1r[1], j2r[2] - j1r[2]};
-          float Jn = frame[0] * jdp[0] + frame[1] * jdp[1] + frame[2] * jdp[2];
-          for (int dimid = 0; dimid < nr; dimid++) {
-            int r = r0 + dimid;
-            if (r >= njmax) break;
-            float Jval = Jn;
-            if (condim > 1) {
-              int dimid2 = dimid / 2 + 1;
-              float frii = rec[14 + dimid2 - 1];
-              float Ji;
-              if (dimid2 < 3) Ji = frame[3 * dimid2] * jdp[0] + frame[3 * dimid2 + 1] * jdp[1] + frame[3 * dimid2 + 2] * jdp[2];
-              else Ji = frame[3 * (dimid2 - 3)] * jdr[0] + frame[3 * (dimid2 - 3) + 1] * jdr[1] + frame[3 * (dimid2 - 3) + 2] * jdr[2];
-              Jval = (dimid % 2 == 0) ? Jval + Ji * frii : Jval - Ji * frii;
-            }
-            s[L.J + r * nvs + i] = Jval;
+          for (int k = 0; k < 3; k++) { jdp[k] = j2p[k] - j1p[k]; jdr[k] = j2r[k] - j1r[k]; }
+        }
+        const float qv = i < nv ? qvel[i] : 0.0f;
+        float Jn = frame[0] * jdp[0] + frame[1] * jdp[1] + frame[2] * jdp[2];
+        for (int dimid = 0; dimid < nr; dimid++) {
+          int r = r0 + dimid;
+          if (r >= njmax) break;
+          float Jval = Jn;
+          if (condim > 1) {
+            int dimid2 = dimid / 2 + 1;
+            float frii = rec[14 + dimid2 - 1];
+            float Ji;
+            if (dimid2 < 3) Ji = frame[3 * dimid2] * jdp[0] + frame[3 * dimid2 + 1] * jdp[1] + frame[3 * dimid2 + 2] * jdp[2];
+            else Ji = frame[3 * (dimid2 - 3)] * jdr[0] + frame[3 * (dimid2 - 3) + 1] * jdr[1] + frame[3 * (dimid2 - 3) + 2] * jdr[2];
+            Jval = (dimid % 2 == 0) ? Jval + Ji * frii : Jval - Ji * frii;
           }
+          if (i < kJ) put_J(d, L, s, wid, np, r, i, i < nv ? Jval : 0.0f);
+          float jq = dsum(i < nv ? Jval * qv : 0.0f);
+          if (lane == 0) s[L.jqvel + r] = jq;
         }
       }
       WSYNC();
@@ -1051,11 +1123,10 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
           invweight = invweight + fri0 * fri0 * invweight;
           invweight = invweight * 2.0f * fri0 * fri0 * impratio_invsqrt * impratio_invsqrt;
         }
-        float Jqvel = 0.0f;
-        for (int k = nv - 1; k >= 0; k--) Jqvel += s[L.J + r * nvs + k] * qvel[k];
+        float Jqvel = s[L.jqvel + r];
         float pos = rec[0] - rec[1];
         int type = condim == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
-        efc_row(m, L, s, wid, r, pos, pos, invweight, rec + 19, rec + 23, rec[1], Jqvel, 0.0f, type, reci[31]);
+        efc_row(m, d, L, s, wid, r, pos, pos, invweight, rec + 19, rec + 23, rec[1], Jqvel, 0.0f, type, reci[31]);
         (void)dimid;
       }
       nefc += nrow_total;
@@ -1068,22 +1139,12 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
   WSYNC();
   // write rows to global (efc arrays are (nworld, njmax[_pad]))
   const int nrows = min(nefc, njmax);
-  const int np = m.nv_pad;
-  float* gJ = d.efc_J + (long)wid * d.njmax_pad * np;
-  for (int e = lane; e < nrows * np; e += LPW) {
-    int r = e / np, c = e - r * np;
-    gJ[e] = c < nv ? s[L.J + r * nvs + c] : 0.0f;
-  }
-  for (int r = lane; r < nrows; r += LPW) {
-    long gr = (long)wid * njmax + r;
-    d.efc_pos[gr] = s[L.efc_pos + r];
-    d.efc_margin[gr] = s[L.efc_margin + r];
-    d.efc_D[(long)wid * d.njmax_pad + r] = s[L.efc_D + r];
-    d.efc_vel[gr] = s[L.efc_vel + r];
-    d.efc_aref[gr] = s[L.efc_aref + r];
-    d.efc_frictionloss[gr] = s[L.efc_frictionloss + r];
-    d.efc_type[gr] = si[L.efc_type + r];
-    d.efc_id[gr] = si[L.efc_id + r];
+  if (L.J >= 0) {
+    float* gJ = d.efc_J + (long)wid * d.njmax_pad * np;
+    for (int e = lane; e < nrows * np; e += LPW) {
+      int r = e / np, c = e - r * np;
+      gJ[e] = c < nv ? s[L.J + r * nvs + c] : 0.0f;
+    }
   }
   if (lane == 0) {
     d.ne[wid] = 0;
@@ -1182,45 +1243,49 @@ __device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const La
     s[L.act_vel + a] = v;
     d.actuator_velocity[(long)wid * m.nu + a] = v;
   }
-  // smooth.py:1935-2038 com_vel, level by level
+  // smooth.py:1935-2038 com_vel.  Inside a body the joint loop adds cdof*qvel joint by joint
+  // and takes cdof_dot = cvel_partial x cdof; the partial sum is split into the parent's cvel
+  // (level pass, LDS only) and the body-local part (one pass over dofs in parallel).
   float* cvel = s + L.cvel;
   float* cdof_dot = s + L.cdof_dot;
-  for (int e = lane; e < 6; e += LPW) cvel[e] = 0.0f;
-  for (int e = lane; e < nv * 6; e += LPW) cdof_dot[e] = 0.0f;
+  float* cacc = s + L.cacc;
+  const float* cd = s + L.cdof;
+  float* dv = s + L.cfrc;  // per-body local increments (cfrc is produced later)
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+    const int adr = m.body_dofadr[b], num = m.body_dofnum[b];
+    for (int k = adr; k < adr + num; k++)
+      for (int i = 0; i < 6; i++) acc[i] += cd[6 * k + i] * qvel[k];
+    for (int i = 0; i < 6; i++) { dv[6 * b + i] = acc[i]; cvel[6 * b + i] = 0.0f; }
+  }
   WSYNC();
-  for (int lvl = 1; lvl < m.nlevel; lvl++) {
-    int beg = m.level_adr[lvl], end = m.level_adr[lvl + 1];
-    for (int idx = beg + lane; idx < end; idx += LPW) {
-      int b = m.level_body[idx];
-      int p = m.body_parentid[b];
+  for (int b0 = 0; b0 < m.nbody; b0 += LPW) {
+    const int b = b0 + lane;
+    const bool ok = b > 0 && b < m.nbody;
+    const int par = ok ? m.body_parentid[b] : 0, lv = ok ? m.body_level[b] : 0;
+    for (int lvl = 1; lvl < m.nlevel; lvl++) {
+      if (ok && lv == lvl)
+        for (int i = 0; i < 6; i++) cvel[6 * b + i] = cvel[6 * par + i] + dv[6 * b + i];
+      WSYNC();
+    }
+  }
+  // cdof_dot per dof: (cvel[parent] + dofs of the body added before this joint) x cdof;
+  // a free joint's rotational dofs also see its translational dofs, which get cdof_dot = 0
+  for (int k = lane; k < nv; k += LPW) {
+    const int b = m.dof_bodyid[k], j = m.dof_jntid[k], jt = m.jnt_type[j];
+    const int ja = m.jnt_dofadr[j], p = m.body_parentid[b];
+    float out[6] = {0, 0, 0, 0, 0, 0};
+    if (!(jt == JNT_FREE && k < ja + 3)) {
       float cv[6];
       for (int i = 0; i < 6; i++) cv[i] = cvel[6 * p + i];
-      int dofid = m.body_dofadr[b];
-      for (int j = m.body_jntadr[b]; j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
-        int jt = m.jnt_type[j];
-        const float* cd = s + L.cdof;
-        if (jt == JNT_FREE) {
-          for (int k = 0; k < 3; k++)
-            for (int i = 0; i < 6; i++) cv[i] += cd[6 * (dofid + k) + i] * qvel[dofid + k];
-          for (int k = 3; k < 6; k++) motion_cross(cdof_dot + 6 * (dofid + k), cv, cd + 6 * (dofid + k));
-          for (int k = 3; k < 6; k++)
-            for (int i = 0; i < 6; i++) cv[i] += cd[6 * (dofid + k) + i] * qvel[dofid + k];
-          dofid += 6;
-        } else if (jt == JNT_BALL) {
-          for (int k = 0; k < 3; k++) motion_cross(cdof_dot + 6 * (dofid + k), cv, cd + 6 * (dofid + k));
-          for (int k = 0; k < 3; k++)
-            for (int i = 0; i < 6; i++) cv[i] += cd[6 * (dofid + k) + i] * qvel[dofid + k];
-          dofid += 3;
-        } else {
-          motion_cross(cdof_dot + 6 * dofid, cv, cd + 6 * dofid);
-          for (int i = 0; i < 6; i++) cv[i] += cd[6 * dofid + i] * qvel[dofid];
-          dofid += 1;
-        }
-      }
-      for (int i = 0; i < 6; i++) cvel[6 * b + i] = cv[i];
+      const int end = jt == JNT_FREE ? ja + 3 : ja;
+      for (int q = m.body_dofadr[b]; q < end; q++)
+        for (int i = 0; i < 6; i++) cv[i] += cd[6 * q + i] * qvel[q];
+      motion_cross(out, cv, cd + 6 * k);
     }
-    WSYNC();
+    for (int i = 0; i < 6; i++) cdof_dot[6 * k + i] = out[i];
   }
+  WSYNC();
   for (int e = lane; e < m.nbody * 6; e += LPW) d.cvel[(long)wid * m.nbody * 6 + e] = cvel[e];
   for (int e = lane; e < nv * 6; e += LPW) d.cdof_dot[(long)wid * nv * 6 + e] = cdof_dot[e];
   // passive.py:70-179, 535-563
@@ -1273,27 +1338,30 @@ __device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const La
     d.qfrc_gravcomp[gi] = 0.0f;
     d.qfrc_passive[gi] = p;
   }
-  // rne (smooth.py:1112-1274, flg_acc = False)
-  float* cacc = s + L.cacc;
-  if (lane < 6) {
-    const float* grav = MR(opt_gravity);
-    cacc[lane] = (lane >= 3 && !(m.opt_disableflags & DSBL_GRAVITY)) ? -grav[lane - 3] : 0.0f;
+  // rne (smooth.py:1112-1274, flg_acc = False): cacc[b] = cacc[parent] + sum cdof_dot qvel
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+    if (b == 0) {
+      const float* grav = MR(opt_gravity);
+      if (!(m.opt_disableflags & DSBL_GRAVITY))
+        for (int i = 0; i < 3; i++) acc[3 + i] = -grav[i];
+    } else {
+      const int adr = m.body_dofadr[b], num = m.body_dofnum[b];
+      for (int k = adr; k < adr + num; k++)
+        for (int i = 0; i < 6; i++) acc[i] += cdof_dot[6 * k + i] * qvel[k];
+    }
+    for (int i = 0; i < 6; i++) cacc[6 * b + i] = acc[i];
   }
   WSYNC();
-  for (int lvl = 1; lvl < m.nlevel; lvl++) {
-    int beg = m.level_adr[lvl], end = m.level_adr[lvl + 1];
-    for (int idx = beg + lane; idx < end; idx += LPW) {
-      int b = m.level_body[idx];
-      int p = m.body_parentid[b];
-      float acc[6];
-      for (int i = 0; i < 6; i++) acc[i] = cacc[6 * p + i];
-      for (int k = 0; k < m.body_dofnum[b]; k++) {
-        int dof = m.body_dofadr[b] + k;
-        for (int i = 0; i < 6; i++) acc[i] += cdof_dot[6 * dof + i] * qvel[dof];
-      }
-      for (int i = 0; i < 6; i++) cacc[6 * b + i] = acc[i];
+  for (int b0 = 0; b0 < m.nbody; b0 += LPW) {
+    const int b = b0 + lane;
+    const bool ok = b > 0 && b < m.nbody;
+    const int par = ok ? m.body_parentid[b] : 0, lv = ok ? m.body_level[b] : 0;
+    for (int lvl = 1; lvl < m.nlevel; lvl++) {
+      if (ok && lv == lvl)
+        for (int i = 0; i < 6; i++) cacc[6 * b + i] += cacc[6 * par + i];
+      WSYNC();
     }
-    WSYNC();
   }
   float* cfrc = s + L.cfrc;
   for (int b = lane; b < m.nbody; b += LPW) {
@@ -1772,7 +1840,8 @@ __device__ void load_smooth(const mjw_model_t& m, const mjw_data_t& d, const Lay
   float* s = w.s;
   int* si = w.si;
   const int nv = m.nv, nvs = L.nvs, np = m.nv_pad;
-  if (stages & (ST_VEL | ST_ACC)) {
+  // only inputs whose producing stage is not part of this launch
+  if ((stages & (ST_VEL | ST_ACC)) && !(stages & ST_POS)) {
     for (int e = lane; e < nv * 6; e += LPW) s[L.cdof + e] = d.cdof[(long)wid * nv * 6 + e];
     for (int e = lane; e < m.nbody * 10; e += LPW) s[L.cinert + e] = d.cinert[(long)wid * m.nbody * 10 + e];
     for (int e = lane; e < m.nbody * 3; e += LPW) {
@@ -1780,7 +1849,7 @@ __device__ void load_smooth(const mjw_model_t& m, const mjw_data_t& d, const Lay
       s[L.subtree_com + e] = d.subtree_com[(long)wid * m.nbody * 3 + e];
     }
   }
-  if (stages & (ST_VEL | ST_ACT)) {
+  if ((stages & (ST_VEL | ST_ACT)) && !(stages & ST_POS)) {
     for (int a = lane; a < m.nu; a += LPW) {
       long gu = (long)wid * m.nu + a;
       int nnz = d.moment_rownnz[gu], adr = d.moment_rowadr[gu];
@@ -1793,7 +1862,7 @@ __device__ void load_smooth(const mjw_model_t& m, const mjw_data_t& d, const Lay
       if (!(stages & ST_VEL)) s[L.act_vel + a] = d.actuator_velocity[gu];
     }
   }
-  if (stages & (ST_ACC | ST_SOLVE | ST_EULER)) {
+  if ((stages & (ST_ACC | ST_SOLVE | ST_EULER)) && !(stages & ST_POS) && !(stages & ST_NOFACTOR)) {
     for (int e = lane; e < nv * nvs; e += LPW) {
       int r = e / nvs, c = e - r * nvs;
       s[L.qM + e] = c < nv ? d.qM[(long)wid * np * np + r * np + c] : 0.0f;
@@ -1858,24 +1927,37 @@ __global__ void __launch_bounds__(64) mjw_kernel(const mjw_model_t m, const mjw_
   w.wid = blockIdx.x;
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
+  PROF_T0();
   load_state(m, d, L, w);
-  if (STAGES != ST_POS) load_smooth(m, d, L, w, STAGES);
+  load_smooth(m, d, L, w, STAGES);
   WSYNC();
+  PROF_MARK(PH_LOAD);
   if (STAGES & ST_POS) {
     kinematics(m, d, L, w);
+    PROF_MARK(PH_KIN);
     com_pos(m, d, L, w);
+    PROF_MARK(PH_COM);
     camlight(m, d, L, w);
+    PROF_MARK(PH_CAM);
     crb_qM(m, d, L, w);
+    PROF_MARK(PH_CRB);
     collision_and_constraints(m, d, L, w);
+    PROF_MARK(PH_COLL);
     transmission(m, d, L, w);
+    PROF_MARK(PH_TRN);
   }
   if (STAGES & ST_VEL) fwd_velocity(m, d, L, w);
   if ((STAGES & ST_POS) && (STAGES & ST_VEL) && w.lane < 2 && !(m.opt_enableflags & ENBL_ENERGY))
     d.energy[(long)w.wid * 2 + w.lane] = 0.0f;
+  PROF_MARK(PH_VEL);
   if (STAGES & ST_ACT) fwd_actuation(m, d, L, w);
+  PROF_MARK(PH_ACT);
   if (STAGES & ST_ACC) fwd_acceleration(m, d, L, w);
+  PROF_MARK(PH_ACC);
   if (STAGES & ST_SOLVE) solve(m, d, L, w);
+  PROF_MARK(PH_GSOLVE);
   if (STAGES & ST_EULER) euler(m, d, L, w);
+  PROF_MARK(PH_GEULER);
 }
 
 // benchmark.py:41-83
@@ -1972,13 +2054,18 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
 }
 }  // namespace
 
+MJW_PROF_READER(mjw_prof_read)
+
 extern "C" {
 
 int mjw_abi_version(void) { return MJW_ABI_VERSION; }
 const char* mjw_last_error(void) { return g_err.c_str(); }
 int mjw_sizeof_model(void) { return (int)sizeof(mjw_model_t); }
 int mjw_sizeof_data(void) { return (int)sizeof(mjw_data_t); }
-int mjw_lds_bytes(const mjw_model_t* m, int njmax) { return mjw::make_layout(*m, njmax).total * 4; }
+int mjw_lds_bytes(const mjw_model_t* m, int njmax) {
+  // per-world dynamic LDS of the forward kernel mjw_step launches (direct layout on the dense path)
+  return mjw::make_layout(*m, njmax, m->nv <= 32 && njmax <= 64).total * 4;
+}
 
 int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE | mjw::ST_EULER, "mjw_step");

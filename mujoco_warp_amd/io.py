@@ -179,11 +179,13 @@ def put_model(mjm, device=None) -> types.Model:
 
   derived_int = dict(
     body_subtree_end=subtree_end,
+    body_level=depth,
     level_body=order,
     level_adr=level_adr,
     jnt_limited_slide_hinge_adr=jnt_limited_sh,
   )
   m.body_subtree_end = _i32(subtree_end, dev)
+  m.body_level = _i32(depth, dev)
   m.level_body = _i32(order, dev)
   m.level_adr = _i32(level_adr, dev)
   m.jnt_limited_slide_hinge_adr = _i32(jnt_limited_sh, dev)

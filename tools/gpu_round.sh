@@ -12,4 +12,8 @@ timeout -k 10 300 python bench.py --steps "$STEPS" --cpu-baseline 0 > gpurun_out
 tail -1 gpurun_out/bench.log
 timeout -k 10 300 python tools/stage_times.py 8192 100 ${SOLVER:-CG} > gpurun_out/stages.log 2>&1 || exit $?
 tail -1 gpurun_out/stages.log
+if [ -f mujoco_warp_amd/libmjw_amd_prof.so ]; then
+  timeout -k 10 300 python tools/phase_prof.py 8192 100 ${SOLVER:-CG} > gpurun_out/phase.json 2>&1 || exit $?
+  cat gpurun_out/phase.json
+fi
 exit $rc
