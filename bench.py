@@ -13,10 +13,17 @@ Multi-GPU: one process per GPU (torch.distributed.run); each rank owns 8192
 worlds (weak scaling, world ids offset by rank), no collective on the data
 path; a barrier + max-over-ranks of the elapsed time brackets the timed region.
 
-Also reported: `roofline` for the fused step kernel (algorithmic bytes per
-env-step from SURVEY.md 8(d) over its HIP-event duration vs 8 TB/s HBM peak,
-traffic from the committed rocprofv3 PMC summary) and `cpu_baseline` (the fp64
-C oracle, OpenMP over worlds on the host cores, bounded sample, rank 0 only).
+A step is two kernels on the torch stream: the forward kernel
+mjw::mjw_kernel<79> (kinematics, com, crb/qM, collision, constraint rows,
+transmission, velocity, rne, actuation, qfrc_smooth) and the dense kernel
+mjw::dense_kernel<7,false> (Cholesky + M^-1, CG solve, Euler).  Both are timed
+live with HIP events recorded on that stream around each launch (mjw_step_events).
+
+Also reported: `roofline` for the dominant (forward) kernel: its algorithmic
+bytes per env-step (SURVEY.md 8(d)'s B_alg split by kernel) x nworld
+over its HIP-event duration vs 8 TB/s HBM peak, traffic from the committed
+rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, KB -> B); and `cpu_baseline`
+(the fp64 C oracle, OpenMP over worlds on the host cores, bounded sample, rank 0).
 """
 
 import argparse
@@ -37,6 +44,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 def b_alg(nefc_mean, ncon_mean):
   """Algorithmic HBM bytes per env-step: state in + Data contract out, fp32."""
   return 4.0 * (4170.0 + 38.0 * (nefc_mean + ncon_mean))
+
+
+def b_alg_dense(nefc_mean):
+  """Share of B_alg written by the dense kernel: qLD 729 + qacc_smooth 27 + solver outputs 86 +
+  integrator 83 words, plus efc force/state (2 words per row)."""
+  return 4.0 * (925.0 + 2.0 * nefc_mean)
+
+
+def b_alg_forward(nefc_mean, ncon_mean):
+  """Share of B_alg of the forward kernel: state inputs + every other Data output (36 words per row)."""
+  return b_alg(nefc_mean, ncon_mean) - b_alg_dense(nefc_mean)
 
 
 def parse():
@@ -106,13 +124,14 @@ def main():
   d.world_offset = rank * args.nworld
   center = torch.zeros(mjm.nu, dtype=torch.float32, device=dev)
 
+  from mujoco_warp_amd.forward import step_timed
+
   def one_step(i, ev=None):
     mjw.ctrl_noise(m, d, i, center=center)
-    if ev is not None:
-      ev[0].record()
-    mjw.step(m, d)
-    if ev is not None:
-      ev[1].record()
+    if ev is None:
+      mjw.step(m, d)
+    else:
+      step_timed(m, d, *ev)
 
   for i in range(args.warmup):
     one_step(i)
@@ -121,7 +140,11 @@ def main():
   nefc_mean = float(d.nefc.float().mean())
   ncon_mean = float(d.nacon[0]) / args.nworld
 
-  events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+  events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+  for ev in events:  # torch creates the HIP event on first record; mjw_step_events re-records it
+    for e in ev:
+      e.record()
+  torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   torch.cuda.synchronize()
@@ -132,7 +155,9 @@ def main():
   if world > 1:
     dist.barrier()
   elapsed = time.perf_counter() - t0
-  kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+  fwd_ms = float(np.mean([a.elapsed_time(b) for a, b, c in events]))
+  dense_ms = float(np.mean([b.elapsed_time(c) for a, b, c in events]))
+  kernel_ms = fwd_ms
   nefc_mean = 0.5 * (nefc_mean + float(d.nefc.float().mean()))
   ncon_mean = 0.5 * (ncon_mean + float(d.nacon[0]) / args.nworld)
   converged = int((~torch.isnan(d.qpos).any(dim=1)).sum())
@@ -148,14 +173,14 @@ def main():
   total_steps = args.nworld * world * args.steps
   value = total_steps / elapsed
   if rank == 0:
-    bytes_per_launch = b_alg(nefc_mean, ncon_mean) * args.nworld
+    bytes_per_launch = b_alg_forward(nefc_mean, ncon_mean) * args.nworld
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.pmc):
       with open(args.pmc) as f:
         pmc = json.load(f)
       if pmc.get("solver", "CG") == args.solver and pmc.get("nworld") == args.nworld:
-        traffic = pmc.get("hbm_bytes_per_launch")
+        traffic = pmc.get("kernels", {}).get("forward", {}).get("hbm_bytes_per_launch")
     out = {
       "metric": METRIC,
       "value": value,
@@ -188,9 +213,17 @@ def main():
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic,
-        "kernel": "mjw::mjw_kernel<63> (fused step)",
+        "kernel": "mjw::mjw_kernel<79> (forward: position/velocity/actuation/qfrc_smooth)",
         "kernel_ms": kernel_ms,
-        "alg_bytes_per_env_step": b_alg(nefc_mean, ncon_mean),
+        "alg_bytes_per_env_step": b_alg_forward(nefc_mean, ncon_mean),
+        "other_kernels": {
+          "mjw::dense_kernel<7,false> (factor/CG/Euler)": {
+            "ms": dense_ms,
+            "alg_bytes_per_env_step": b_alg_dense(nefc_mean),
+            "achieved_GBs": b_alg_dense(nefc_mean) * args.nworld / (dense_ms * 1e-3) / 1e9,
+          }
+        },
+        "step_alg_bytes_per_env_step": b_alg(nefc_mean, ncon_mean),
       },
       "cpu_baseline": None,
     }

@@ -154,6 +154,12 @@ int mjw_lds_bytes(const mjw_model_t* m, int njmax);
 
 /* stream: a hipStream_t (NULL = default stream) */
 int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+/* mjw_step with timing: hipEvent_t handles recorded on `stream` before the forward kernel,
+ * between the forward and the dense factor/solve/euler kernel, and after it (bench.py uses
+ * this to time the dominant kernel live; on the generic path only ev_begin/ev_end bracket it).
+ * No reference counterpart (the reference times with wp.ScopedTimer/event_trace, benchmark.py). */
+int mjw_step_events(const mjw_model_t* m, const mjw_data_t* d, void* stream, void* ev_begin, void* ev_mid, void* ev_end);
+
 int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_velocity(const mjw_model_t* m, const mjw_data_t* d, void* stream);

@@ -2016,6 +2016,10 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
 // the register-resident path (mjw_dense.h) covers worlds with nv <= 32 and njmax <= 64
 bool dense_ok(const mjw_model_t* m, const mjw_data_t* d) { return m->nv <= 32 && d->njmax <= 64; }
 
+// optional timing events for the next run(): before the forward kernel, between it and
+// the dense kernel, after the dense kernel (mjw_step_events)
+thread_local hipEvent_t g_ev[3] = {nullptr, nullptr, nullptr};
+
 // stage groups: ST_* bits of the stages to run, in pipeline order
 int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, const char* name) {
   using namespace mjw;
@@ -2026,6 +2030,7 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   int rc = 0;
   if (dense_ok(m, d)) {
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel
+    if (g_ev[0]) (void)hipEventRecord(g_ev[0], s);
     switch (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC)) {
       case 0: break;
       case ST_POS | ST_VEL | ST_ACT | ST_ACC: rc = launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_NOFACTOR>(m, d, s, name); break;
@@ -2036,9 +2041,11 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
       default: g_err = std::string(name) + ": unsupported stage group"; return -4;
     }
     if (rc) return rc;
+    if (g_ev[1]) (void)hipEventRecord(g_ev[1], s);
     int f = ((stages & ST_ACC) ? DF_FACTOR : 0) | ((stages & ST_SOLVE) ? DF_SOLVE : 0) | ((stages & ST_EULER) ? DF_EULER : 0);
-    if (f == 0) return 0;
-    return set_err((hipError_t)dense_launch(f, m, d, s), name);
+    if (f != 0) rc = set_err((hipError_t)dense_launch(f, m, d, s), name);
+    if (g_ev[2]) (void)hipEventRecord(g_ev[2], s);
+    return rc;
   }
   switch (stages) {
     case ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE | ST_EULER: return launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE | ST_EULER>(m, d, s, name);
@@ -2069,6 +2076,14 @@ int mjw_lds_bytes(const mjw_model_t* m, int njmax) {
 
 int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE | mjw::ST_EULER, "mjw_step");
+}
+int mjw_step_events(const mjw_model_t* m, const mjw_data_t* d, void* stream, void* ev_begin, void* ev_mid, void* ev_end) {
+  g_ev[0] = (hipEvent_t)ev_begin;
+  g_ev[1] = (hipEvent_t)ev_mid;
+  g_ev[2] = (hipEvent_t)ev_end;
+  int rc = run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE | mjw::ST_EULER, "mjw_step_events");
+  g_ev[0] = g_ev[1] = g_ev[2] = nullptr;
+  return rc;
 }
 int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE, "mjw_forward");

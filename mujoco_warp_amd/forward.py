@@ -1,8 +1,11 @@
 """Pipeline entry points (mirror mujoco_warp/_src/forward.py).
 
 `step(m, d)` (forward.py:1003-1018) runs the whole forward pass and the Euler
-integrator as ONE fused world-per-wavefront HIP kernel on the current torch
-stream.  The stage functions (`fwd_position`, `fwd_velocity`, ...) launch the
+integrator on the current torch stream as two world-per-wavefront HIP kernels:
+the forward kernel (kinematics ... qfrc_smooth, collision and constraint rows)
+and, for models with nv <= 32 and njmax <= 64, the register-resident dense
+factor / solve / integrate kernel (otherwise one generic fused kernel).  The
+stage functions (`fwd_position`, `fwd_velocity`, ...) launch the
 same device code restricted to one stage group; they exist for parity testing
 and for models that install Python callbacks (types.Callback), which are
 invoked between stage launches exactly where the reference calls them.
@@ -27,6 +30,18 @@ def _call(fn: str, m: Model, d: Data):
   L = _lib.lib()
   cm, cd = cmodel(m), cdata(d)
   _lib.check(getattr(L, fn)(cm, cd, _stream(d)), fn)
+
+
+def step_timed(m: Model, d: Data, ev_begin, ev_mid, ev_end):
+  """`step` that records torch.cuda.Event objects around its kernels (bench.py).
+
+  The events must already exist (torch creates them on their first `record()`)."""
+  for e in (ev_begin, ev_mid, ev_end):
+    if not e.cuda_event:
+      raise ValueError("step_timed: record each event once before passing it")
+  L = _lib.lib()
+  rc = L.mjw_step_events(cmodel(m), cdata(d), _stream(d), ev_begin.cuda_event, ev_mid.cuda_event, ev_end.cuda_event)
+  _lib.check(rc, "mjw_step_events")
 
 
 def _has_callbacks(m: Model) -> bool:

@@ -1,0 +1,65 @@
+"""Summarise rocprofv3 CSV output into profiles/: kernel-trace stats + per-kernel HBM traffic.
+
+usage: python tools/pmc_traffic.py <stats_dir> <fetch_dir> <write_dir> <out.json> [nworld] [solver]
+  stats_dir : rocprofv3 --kernel-trace --stats --output-format csv output directory
+  fetch_dir : rocprofv3 --pmc FETCH_SIZE --output-format csv output directory
+  write_dir : rocprofv3 --pmc WRITE_SIZE --output-format csv output directory
+Traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes (MI355X_MICROARCH.md HBM section:
+FETCH_SIZE counts half the bytes of wide streaming reads on gfx950; units are KB), averaged over
+the dispatches of each kernel.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNELS = {"forward": "mjw_kernel<79>", "dense": "dense_kernel<7, false>"}
+
+
+def rows(d, pattern):
+  out = []
+  for f in glob.glob(os.path.join(d, "**", pattern), recursive=True):
+    with open(f) as fh:
+      out += list(csv.DictReader(fh))
+  return out
+
+
+def counter_avg(d, counter):
+  vals = {k: [] for k in KERNELS}
+  for r in rows(d, "*counter_collection.csv"):
+    name = r.get("Kernel_Name", "")
+    if r.get("Counter_Name") != counter:
+      continue
+    for k, pat in KERNELS.items():
+      if pat in name.replace("mjw::", ""):
+        vals[k].append(float(r["Counter_Value"]))
+  return {k: (sum(v) / len(v) if v else None, len(v)) for k, v in vals.items()}
+
+
+def main():
+  stats_dir, fetch_dir, write_dir, out = sys.argv[1:5]
+  nworld = int(sys.argv[5]) if len(sys.argv) > 5 else 8192
+  solver = sys.argv[6] if len(sys.argv) > 6 else "CG"
+  fetch = counter_avg(fetch_dir, "FETCH_SIZE")
+  write = counter_avg(write_dir, "WRITE_SIZE")
+  stats = rows(stats_dir, "*kernel_stats.csv")
+  res = {"nworld": nworld, "solver": solver, "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024",
+         "kernels": {}}
+  for k, pat in KERNELS.items():
+    f, nf = fetch[k]
+    w, nw = write[k]
+    st = [r for r in stats if pat in r.get("Name", "").replace("mjw::", "")]
+    res["kernels"][k] = {
+      "pattern": pat,
+      "fetch_size_kb": f, "write_size_kb": w, "dispatches": [nf, nw],
+      "hbm_bytes_per_launch": (2 * f + w) * 1024 if f is not None and w is not None else None,
+      "avg_ns_rocprof": float(st[0]["AverageNs"]) if st else None,
+    }
+  with open(out, "w") as fh:
+    json.dump(res, fh, indent=1)
+  print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+  main()
