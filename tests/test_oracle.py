@@ -4,6 +4,9 @@ KATs restated from mujoco_warp/_src/math_test.py:27-131 (segment/segment closest
 points, triangular index maps) and util_misc.halton (util_misc.py:59-73).
 """
 
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -11,37 +14,34 @@ from oracle import orc
 from tests.common import HUMANOID, humanoid_model, oracle_from_state, random_states
 
 
-# ---- math_test.py KATs ----------------------------------------------------------------------
-@pytest.mark.parametrize(
-  "a0,a1,b0,b1,ea,eb,places",
-  [
-    ([0.73432405, 0.12372768, 0.20272314], [1.10600128, 0.88555209, 0.65209485], [0.85599262, 0.61736299, 0.9843583],
-     [1.84270939, 0.92891793, 1.36343326], [1.09063, 0.85404, 0.63351], [0.99596, 0.66156, 1.03813], 5),
-    ([0, 0, -1], [0, 0, 1], [-1, 0, 0], [1, 0, 0], [0, 0, 0], [0, 0, 0], 5),
-    ([0.2, 0.2, 0], [1, 1, 0], [0.2, 0.4, 0], [1, 2, 0], [0.3, 0.3, 0], [0.2, 0.4, 0], 2),
-    ([0, 0, -1], [0, 0, 1], [1, 0, -1], [1, 0, 1], [0, 0, 0], [1, 0, 0], 5),
-    ([0, 0, -1], [0, 0, 1], [1, 0, 1], [1, 0, 3], [0, 0, 1], [1, 0, 1], 5),
-    ([0, 0, -1], [0, 0, -1], [1, 0, 0.1], [1, 0, 0.1], [0, 0, -1], [1, 0, 0.1], 5),
-    ([0, 0, -1], [0, 0, 1], [0, 0, -1], [0, 0, 1], [0, 0, 0], [0, 0, 0], 5),
-  ],
-)
-def test_closest_segment_points_kat(a0, a1, b0, b1, ea, eb, places):
-  ba, bb = orc.kat_closest_segment_points(a0, a1, b0, b1)
-  np.testing.assert_almost_equal(ba, ea, places)
-  np.testing.assert_almost_equal(bb, eb, places)
+# ---- math_test.py KATs (tests/golden/math_kat.json, extracted by tests/golden/make_golden.py) ----
+_KAT = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "math_kat.json")))
 
 
-@pytest.mark.parametrize("n", [2, 10])
-def test_upper_tri_index_kat(n):
-  arr = [orc.kat_upper_tri_index(n, i, j) for i in range(n) for j in range(i + 1, n)]
-  assert arr == list(range(n * (n - 1) // 2))
+@pytest.mark.parametrize("case", _KAT["closest_segment_points"], ids=lambda c: c["name"])
+def test_closest_segment_points_kat(case):
+  ba, bb = orc.kat_closest_segment_points(case["a0"], case["a1"], case["b0"], case["b1"])
+  np.testing.assert_almost_equal(ba, case["best_a"], case["places"])
+  np.testing.assert_almost_equal(bb, case["best_b"], case["places"])
 
 
-@pytest.mark.parametrize("n", [1, 10])
-def test_upper_trid_index_kat(n):
-  arr = [orc.kat_upper_trid_index(n, i, j) for i in range(n) for j in range(i, n)]
-  assert arr == list(range(n * (n + 1) // 2))
-  assert orc.kat_upper_trid_index(10, 1, 5) == orc.kat_upper_trid_index(10, 5, 1)
+@pytest.mark.parametrize("case", _KAT["triangular_index"], ids=lambda c: c["name"])
+def test_triangular_index_kat(case):
+  if case["fn"] == "upper_tri_index":
+    n = case["n"]
+    arr = [orc.kat_upper_tri_index(n, i, j) for i in range(n) for j in range(i + 1, n)]
+    assert arr == list(range(case["count"]))
+  elif case["fn"] == "upper_trid_index":
+    n = case["n"]
+    arr = [orc.kat_upper_trid_index(n, i, j) for i in range(n) for j in range(i, n)]
+    assert arr == list(range(case["count"]))
+  else:
+    a = case["args"]
+    assert orc.kat_upper_trid_index(*a[:3]) == orc.kat_upper_trid_index(*a[3:])
+
+
+def test_golden_fixture_is_complete():
+  assert len(_KAT["closest_segment_points"]) == 7 and len(_KAT["triangular_index"]) == 5
 
 
 def test_halton_known_values():
