@@ -67,7 +67,7 @@ def parse():
   p.add_argument("--nconmax", type=int, default=24)
   p.add_argument("--njmax", type=int, default=64)
   p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
-  p.add_argument("--cpu-worlds", type=int, default=512)
+  p.add_argument("--cpu-worlds", type=int, default=1024)
   p.add_argument("--cpu-steps", type=int, default=1000)
   p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_humanoid_r01.json"))
   p.add_argument("--graph", type=int, default=0, help="replay steps through a captured hipGraph")

@@ -60,12 +60,13 @@ __device__ __forceinline__ float symv(const f32x16& A, const float* vec, int h) 
 template <bool STORE_L = false>
 __device__ __forceinline__ f32x16 spd_inverse(float (&a)[32], int lane, float* S = nullptr) {
   const int c = lane & 31;
-  // right-looking Cholesky, rows in lanes (wp.tile_cholesky, smooth.py:2860-2928)
+  // right-looking Cholesky, rows in lanes (wp.tile_cholesky, smooth.py:2860-2928);
+  // 1/L[j][j] by v_rsq_f32 keeps the per-column critical path short
 #pragma unroll
   for (int j = 0; j < 32; j++) {
-    float dj = sqrtf(rdlane(a[j], j));
-    float inv = 1.0f / dj;
-    a[j] = (c > j) ? a[j] * inv : (c == j ? dj : 0.0f);
+    float piv = rdlane(a[j], j);
+    float inv = __builtin_amdgcn_rsqf(piv);
+    a[j] = (c > j) ? a[j] * inv : (c == j ? piv * inv : 0.0f);
 #pragma unroll
     for (int k = j + 1; k < 32; k++) a[k] = fmaf(-a[j], rdlane(a[j], k), a[k]);
   }
@@ -74,24 +75,65 @@ __device__ __forceinline__ f32x16 spd_inverse(float (&a)[32], int lane, float* S
 #pragma unroll
     for (int q = 0; q < 8; q++) rw[q] = f32x4{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
   }
-  // X = L^-1, lane computes column c by forward substitution; L[j][k] = readlane(a[k], j)
+  // X = L^-1, lane computes column c by right-looking forward substitution (critical path
+  // 32 steps, the other updates are independent); L[j][k] = readlane(a[k], j)
   float x[32];
 #pragma unroll
-  for (int j = 0; j < 32; j++) {
-    float acc = (c == j) ? 1.0f : 0.0f;
+  for (int j = 0; j < 32; j++) x[j] = (c == j) ? 1.0f : 0.0f;
 #pragma unroll
-    for (int k = 0; k < j; k++) acc = fmaf(-rdlane(a[k], j), x[k], acc);
-    x[j] = acc / rdlane(a[j], j);
+  for (int k = 0; k < 32; k++) {
+    x[k] *= __builtin_amdgcn_rcpf(rdlane(a[k], k));
+#pragma unroll
+    for (int j = k + 1; j < 32; j++) x[j] = fmaf(-rdlane(a[k], j), x[k], x[j]);
   }
-  // A^-1 = X^T X : 16 x (32x32x2) f32 MFMA, operand for k-step t is X[2t + h][c]
+  // A^-1 = X^T X : 16 x (32x32x2) f32 MFMA in two independent chains, operand X[2t + h][c]
   const bool hi = lane >= 32;
-  f32x16 r = {};
+  f32x16 r0 = {}, r1 = {};
 #pragma unroll
-  for (int t = 0; t < 16; t++) {
-    float v = hi ? x[2 * t + 1] : x[2 * t];
-    r = __builtin_amdgcn_mfma_f32_32x32x2f32(v, v, r, 0, 0, 0);
+  for (int t = 0; t < 16; t += 2) {
+    float v0 = hi ? x[2 * t + 1] : x[2 * t];
+    float v1 = hi ? x[2 * t + 3] : x[2 * t + 2];
+    r0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, v0, r0, 0, 0, 0);
+    r1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, v1, r1, 0, 0, 0);
   }
-  return r;
+  return r0 + r1;
+}
+
+// Cholesky in place (rows in lanes) and L rows -> S; no inverse
+__device__ __forceinline__ void chol_factor(float (&a)[32], int lane, float* S) {
+  const int c = lane & 31;
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    float piv = rdlane(a[j], j);
+    float inv = __builtin_amdgcn_rsqf(piv);
+    a[j] = (c > j) ? a[j] * inv : (c == j ? piv * inv : 0.0f);
+#pragma unroll
+    for (int k = j + 1; k < 32; k++) a[k] = fmaf(-a[j], rdlane(a[j], k), a[k]);
+  }
+  __syncthreads();
+  if (lane < 32) {
+    f32x4* rw = reinterpret_cast<f32x4*>(S + c * DSS);
+#pragma unroll
+    for (int q = 0; q < 8; q++) rw[q] = f32x4{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
+  }
+  __syncthreads();
+}
+
+// (L L^T) x = b for a dof vector b (lane c, both halves): forward sweep with L rows in
+// registers, backward sweep with L columns read from S (wp.tile_cholesky_solve)
+__device__ __forceinline__ float chol_solve(const float (&a)[32], const float* S, int lane, float b) {
+  const int c = lane & 31;
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    float yk = rdlane(b, k) * __builtin_amdgcn_rcpf(rdlane(a[k], k));
+    b = (c > k) ? fmaf(-a[k], yk, b) : (c == k ? yk : b);
+  }
+#pragma unroll
+  for (int k = 31; k >= 0; k--) {
+    float xk = rdlane(b, k) * __builtin_amdgcn_rcpf(S[k * DSS + k]);
+    b = (c < k) ? fmaf(-S[k * DSS + c], xk, b) : (c == k ? xk : b);
+  }
+  return b;
 }
 
 // stage an n x n block (global row stride gs) into S with identity padding to 32x32,
@@ -345,11 +387,12 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d) {
             f32x4 v = rw[q];
             a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
           }
-          Mi = spd_inverse(a, lane);
+          chol_factor(a, lane, S);
+          Mgrad = chol_solve(a, S, lane, grad);
         } else {
           __syncthreads();
+          Mgrad = symv(Mi, vd2, h);
         }
-        Mgrad = symv(Mi, vd2, h);
         if (!dof) Mgrad = 0.0f;
       };
 

@@ -14,6 +14,8 @@
 
 #include "mjw_common.h"
 
+#include <cstdlib>
+
 namespace mjw {
 
 // per-world LDS layout (offsets in 4-byte words)
@@ -586,6 +588,7 @@ __device__ void capsule_capsule(Con2& out, const float* p1, const float* ax1, fl
     return;
   }
   int cnt = 0;
+#pragma unroll
   for (int t = 0; t < 4; t++) {
     if (t >= 2 && cnt >= 2) break;
     float x;
@@ -595,9 +598,16 @@ __device__ void capsule_capsule(Con2& out, const float* p1, const float* ax1, fl
     else { x = clampf((u + mb) / ma, -1.0f, 1.0f); for (int i = 0; i < 3; i++) { v2[i] = p2[i] - a2[i]; v1[i] = p1[i] + a1[i] * x; } }
     float dist = sphere_sphere(pos, nrm, v1, r1, v2, r2);
     if (dist <= margin) {
-      out.dist[cnt] = dist;
-      for (int i = 0; i < 3; i++) out.pos[cnt][i] = pos[i];
-      make_frame(out.frame[cnt], nrm);
+      // slot index kept compile-time (no scratch): slot 0 first, then slot 1
+      if (cnt == 0) {
+        out.dist[0] = dist;
+        for (int i = 0; i < 3; i++) out.pos[0][i] = pos[i];
+        make_frame(out.frame[0], nrm);
+      } else {
+        out.dist[1] = dist;
+        for (int i = 0; i < 3; i++) out.pos[1][i] = pos[i];
+        make_frame(out.frame[1], nrm);
+      }
       cnt++;
     }
   }
@@ -991,6 +1001,7 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
           int condim;
           contact_params(m, wid, g1, g2, &margin, &gap, &condim, friction, solref, solimp);
           int kk = 0;
+#pragma unroll
           for (int sub = 0; sub < 2; sub++) {
             bool a = sub == 0 ? a0 : a1;
             if (!a) continue;
@@ -1218,9 +1229,12 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, const La
       s[L.act_mom + 6 * a + k] = k < nnz ? mom[k] : 0.0f;
       si[L.act_momdof + 6 * a + k] = k < nnz ? va + k : 0;
     }
-    for (int k = 0; k < nnz; k++) {
-      d.actuator_moment[(long)wid * m.nJmom + rowadr + k] = mom[k];
-      d.moment_colind[(long)wid * m.nJmom + rowadr + k] = va + k;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      if (k < nnz) {
+        d.actuator_moment[(long)wid * m.nJmom + rowadr + k] = mom[k];
+        d.moment_colind[(long)wid * m.nJmom + rowadr + k] = va + k;
+      }
     }
   }
   WSYNC();
@@ -1999,6 +2013,11 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   constexpr bool nofactor = (STAGES & mjw::ST_NOFACTOR) != 0;
   mjw::Lay L = mjw::make_layout(*m, d->njmax, nofactor);
   size_t lds = (size_t)L.total * 4;
+  static const size_t lds_pad = [] {  // occupancy experiments only (MJW_LDS_PAD bytes)
+    const char* e = getenv("MJW_LDS_PAD");
+    return e ? (size_t)atol(e) : (size_t)0;
+  }();
+  lds += lds_pad;
   if (lds > 160 * 1024) { g_err = std::string(name) + ": per-world LDS working set exceeds 160 KiB"; return -3; }
   if (STAGES & mjw::ST_POS) {
     hipError_t e = hipMemsetAsync(d->nacon, 0, sizeof(int32_t), s);
