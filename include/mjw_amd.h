@@ -28,12 +28,12 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 2
+#define MJW_ABI_VERSION 3
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
   X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
-  X(nxn) X(nlevel) X(nlimited) X(nmaxcondim) X(nmaxpyramid) X(nv_pad) X(nJmom)                    \
+  X(nxn) X(nlevel) X(nlimited) X(nmaxcondim) X(nmaxpyramid) X(nv_pad) X(nJmom) X(neq)            \
   X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations) X(opt_ls_iterations)             \
   X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)
 
@@ -59,7 +59,8 @@
   X(light_pos0, nlight * 3) X(light_dir0, nlight * 3)                                              \
   X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
   X(actuator_ctrlrange, nu * 2) X(actuator_forcerange, nu * 2) X(actuator_actrange, nu * 2)       \
-  X(actuator_gear, nu * 6)
+  X(actuator_gear, nu * 6)                                                                         \
+  X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)
 
 /* ---- model: int arrays (never batched) ---- */
 #define MJW_MODEL_INT_ARRAYS(X)                                                                    \
@@ -76,7 +77,8 @@
   X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
-  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)
+  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)                                                 \
+  X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)
 
 /* ---- data: float arrays, (nworld, count) world-major like mujoco_warp types.Data ---- */
 #define MJW_DATA_REAL_ARRAYS(X)                                                                    \
@@ -102,7 +104,7 @@
 #define MJW_DATA_INT_ARRAYS(X)                                                                     \
   X(ne, 1) X(nf, 1) X(nl, 1) X(nefc, 1) X(solver_niter, 1)                                         \
   X(moment_rownnz, nu) X(moment_rowadr, nu) X(moment_colind, nJmom)                                \
-  X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax_pad)
+  X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax_pad) X(eq_active, neq)
 
 /* ---- contact pool: float arrays, (naconmax, count) ---- */
 #define MJW_CONTACT_REAL_ARRAYS(X)                                                                 \

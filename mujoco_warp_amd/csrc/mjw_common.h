@@ -20,14 +20,19 @@ constexpr int CMAX = 32;  // staged contacts per collision round
 
 enum : int { ST_POS = 1, ST_VEL = 2, ST_ACT = 4, ST_ACC = 8, ST_SOLVE = 16, ST_EULER = 32, ST_NOFACTOR = 64 };
 enum : int { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
-enum : int { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3 };
+enum : int { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_BOX = 6 };
+enum : int { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
+enum : int { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICIT = 2, INT_IMPLICITFAST = 3 };
+enum : int { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
+enum : int { BIAS_NONE = 0, BIAS_AFFINE = 1 };
+enum : int { DYN_NONE = 0 };
 enum : int {
   DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16, DSBL_SPRING = 32,
   DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512, DSBL_ACTUATION = 2048,
   DSBL_REFSAFE = 4096, DSBL_EULERDAMP = 1 << 15
 };
 enum : int { ENBL_ENERGY = 2 };
-enum : int { CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
+enum : int { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
 enum : int { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3 };
 enum : int { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
 enum : int { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };

@@ -137,9 +137,9 @@ __device__ __forceinline__ float chol_solve(const float (&a)[32], const float* S
 }
 
 // stage an n x n block (global row stride gs) into S with identity padding to 32x32,
-// plus an optional diagonal term; returns row (lane&31) in a[] and M in accumulator layout
-__device__ __forceinline__ void stage_spd(const float* g, int gs, int n, const float* diag_add, float diag_scale, float* S,
-                                          int lane, float (&a)[32], f32x16& Macc) {
+// plus an optional diagonal term
+__device__ __forceinline__ void stage_fill(const float* g, int gs, int n, const float* diag_add, float diag_scale, float* S,
+                                           int lane) {
   for (int e = lane; e < 32 * 32; e += 64) {
     int r = e >> 5, k = e & 31;
     float v;
@@ -152,6 +152,10 @@ __device__ __forceinline__ void stage_spd(const float* g, int gs, int n, const f
     S[r * DSS + k] = v;
   }
   __syncthreads();
+}
+
+// rows (lane&31) of the staged matrix into a[], and the n x n block in accumulator layout
+__device__ __forceinline__ void stage_rows(int n, const float* S, int lane, float (&a)[32], f32x16& Macc) {
   const int c = lane & 31, h = lane >> 5;
   const f32x4* row = reinterpret_cast<const f32x4*>(S + c * DSS);
 #pragma unroll
@@ -165,6 +169,33 @@ __device__ __forceinline__ void stage_spd(const float* g, int gs, int n, const f
     Macc[r] = (i < n && c < n) ? S[i * DSS + c] : 0.0f;
   }
   __syncthreads();
+}
+
+__device__ __forceinline__ void stage_spd(const float* g, int gs, int n, const float* diag_add, float diag_scale, float* S,
+                                          int lane, float (&a)[32], f32x16& Macc) {
+  stage_fill(g, gs, n, diag_add, diag_scale, S, lane);
+  stage_rows(n, S, lane, a, Macc);
+}
+
+// derivative.py:36-107 (_qderiv_actuator_passive_vel): d force / d velocity scale of actuator a
+__device__ __forceinline__ float actuator_vel_deriv(const mjw_model_t& m, const mjw_data_t& d, int wid, int a) {
+  const float* gainprm = MR(actuator_gainprm) + 10 * a;
+  const float* biasprm = MR(actuator_biasprm) + 10 * a;
+  float gain = m.actuator_gaintype[a] == GAIN_AFFINE ? gainprm[2] : 0.0f;
+  float bias = m.actuator_biastype[a] == BIAS_AFFINE ? biasprm[2] : 0.0f;
+  if (bias == 0.0f && gain == 0.0f) return 0.0f;
+  if (m.actuator_forcelimited[a]) {
+    float f = d.actuator_force[(long)wid * m.nu + a];
+    const float* fr = MR(actuator_forcerange) + 2 * a;
+    if (f <= fr[0] || f >= fr[1]) return 0.0f;
+  }
+  float vel = bias;
+  if (m.actuator_dyntype[a] != DYN_NONE) {
+    if (gain != 0.0f) vel += gain * d.act[(long)wid * m.na + m.actuator_actadr[a] + m.actuator_actnum[a] - 1];
+  } else if (gain != 0.0f) {
+    vel += gain * d.ctrl[(long)wid * m.nu + a];
+  }
+  return vel;
 }
 
 // lane r: sum_k J[r][k] v[k] over k < 4*nq
@@ -493,12 +524,41 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d) {
     }
     float qacc_adv = qacc;
     __syncthreads();
-    // implicit damping only in the Euler-only kernel (dense_launch splits the step when enabled)
-    if (FLAGS == DF_EULER && !(m.opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER))) {
-      // implicit damping: (M + dt diag(damping)) qacc_adv = M qacc (forward.py:322-340)
+    // implicit integration only in the Euler-only kernel (dense_launch splits the step when needed)
+    const int fl = m.opt_disableflags;
+    const bool implicitfast = m.opt_integrator == INT_IMPLICITFAST;
+    const bool need_implicit = implicitfast ? (fl & (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) != (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)
+                                            : !(fl & (DSBL_EULERDAMP | DSBL_DAMPER));
+    if (FLAGS == DF_EULER && need_implicit) {
+      // euler damping: (M + dt diag(damping)) qacc_adv = M qacc (forward.py:322-340); implicitfast:
+      // (M - dt qDeriv) qacc_adv = M qacc, qDeriv = sum_a vel_a m_a m_a' - diag(damping) on the
+      // ancestor pattern of qM (forward.py:494-510, derivative.py:320-416)
       float a[32];
       f32x16 Md;
-      stage_spd(d.qM + (long)wid * np * np, np, nv, MR(dof_damping), dt, S, lane, a, Md);
+      stage_fill(d.qM + (long)wid * np * np, np, nv, (fl & DSBL_DAMPER) ? nullptr : MR(dof_damping), dt, S, lane);
+      if (implicitfast && m.nu > 0 && !(fl & DSBL_ACTUATION)) {
+        for (int u = 0; u < m.nu; u++) {
+          float vel = actuator_vel_deriv(m, d, wid, u);
+          if (vel == 0.0f) continue;
+          const long gu = (long)wid * m.nu + u;
+          const int nnz = d.moment_rownnz[gu], adr = d.moment_rowadr[gu];
+          if (lane < nnz * nnz) {
+            const int k1 = lane / nnz, k2 = lane - k1 * nnz;
+            const long base = (long)wid * m.nJmom + adr;
+            const int i = d.moment_colind[base + k1], j = d.moment_colind[base + k2];
+            int p = i;
+            while (p > j) p = m.dof_parentid[p];
+            if (p == j && i < 32 && j < 32) {
+              float v = dt * vel * d.actuator_moment[base + k1] * d.actuator_moment[base + k2];
+              S[i * DSS + j] -= v;
+              if (i != j) S[j * DSS + i] -= v;
+            }
+          }
+          __syncthreads();
+        }
+      }
+      stage_rows(nv, S, lane, a, Md);
+      __syncthreads();
       f32x16 Mdi = spd_inverse(a, lane);
       if (lo) vd[c] = ma;
       __syncthreads();
@@ -580,7 +640,11 @@ hipError_t launch_flags(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s
 }
 
 int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
-  if ((flags & DF_EULER) && flags != DF_EULER && !(m->opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER))) {
+  const int fl = m->opt_disableflags;
+  const bool implicit_int = m->opt_integrator == INT_IMPLICITFAST
+                                ? (fl & (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) != (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)
+                                : !(fl & (DSBL_EULERDAMP | DSBL_DAMPER));
+  if ((flags & DF_EULER) && flags != DF_EULER && implicit_int) {
     int rc = dense_launch(flags & ~DF_EULER, m, d, s);
     return rc ? rc : dense_launch(DF_EULER, m, d, s);
   }

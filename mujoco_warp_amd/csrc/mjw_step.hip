@@ -640,6 +640,19 @@ __device__ void plane_capsule(Con2& out, const float* n, const float* ppos, cons
   out.n = 2;
 }
 
+// collision_primitive_core.py:395-443: corner k (bit i of k selects +/- size[i]) against the plane
+__device__ __forceinline__ float plane_box_corner(int k, const float* n, const float* ppos, const float* bpos, const float* bmat,
+                                                  const float* bsize, float* pos) {
+  float dif[3] = {bpos[0] - ppos[0], bpos[1] - ppos[1], bpos[2] - ppos[2]};
+  float center_dist = dot3(dif, n);
+  float cl[3] = {(k & 1) ? bsize[0] : -bsize[0], (k & 2) ? bsize[1] : -bsize[1], (k & 4) ? bsize[2] : -bsize[2]};
+  float corner[3];
+  matvec3(corner, bmat, cl);
+  float cdist = center_dist + dot3(n, corner);
+  for (int i = 0; i < 3; i++) pos[i] = corner[i] + bpos[i] - 0.5f * n[i] * cdist;
+  return cdist;
+}
+
 // collision_driver.py:217-271
 __device__ bool obb_filter(const float* c1, const float* c2, const float* s1, const float* s2, float margin, const float* xp1,
                            const float* xp2, const float* xm1, const float* xm2) {
@@ -880,13 +893,56 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
   int* si = w.si;
   const int nv = m.nv, nvs = L.nvs, njmax = d.njmax;
   const float* qvel = s + L.qvel;
-  int nefc = 0, nf = 0, nl = 0;
+  int nefc = 0, nf = 0, nl = 0, ne = 0;
   const bool dsbl_constraint = m.opt_disableflags & DSBL_CONSTRAINT;
   const int np = m.nv_pad;
   const int kJ = L.J >= 0 ? nv : np;  // global rows also get their zero padding
   const int CM = L.cmax;
   WSYNC();  // contact staging may alias the qM region read by crb_qM
 
+  // --- joint equality rows (constraint.py:367-495), in equality index order
+  if (!dsbl_constraint && !(m.opt_disableflags & DSBL_EQUALITY) && m.neq > 0) {
+    const float* eq_data = MR(eq_data);
+    const float* eq_solref = MR(eq_solref);
+    const float* eq_solimp = MR(eq_solimp);
+    const float* qpos0 = MR(qpos0);
+    const float* dof_invweight0 = MR(dof_invweight0);
+    const float* qpos = s + L.qpos;
+    for (int base = 0; base < m.neq; base += LPW) {
+      int e = base + lane;
+      bool act = e < m.neq && m.eq_type[e] == EQ_JOINT && d.eq_active[(long)wid * m.neq + e] != 0;
+      unsigned long long bal = __ballot(act);
+      int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
+      int r = nefc + rank;
+      if (act && r < njmax) {
+        const float* data = eq_data + 11 * e;
+        int j1 = m.eq_obj1id[e], j2 = m.eq_obj2id[e];
+        int da1 = m.jnt_dofadr[j1], qa1 = m.jnt_qposadr[j1];
+        int da2 = -1;
+        float pos, Jqvel, invweight, d2 = 0.0f;
+        if (j2 > -1) {
+          int qa2 = m.jnt_qposadr[j2];
+          da2 = m.jnt_dofadr[j2];
+          float dif = qpos[qa2] - qpos0[qa2];
+          float rhs = data[0] + dif * (data[1] + dif * (data[2] + dif * (data[3] + dif * data[4])));
+          d2 = data[1] + dif * (2.0f * data[2] + dif * (3.0f * data[3] + dif * 4.0f * data[4]));
+          pos = qpos[qa1] - qpos0[qa1] - rhs;
+          Jqvel = qvel[da1] - qvel[da2] * d2;
+          invweight = dof_invweight0[da1] + dof_invweight0[da2];
+        } else {
+          pos = qpos[qa1] - qpos0[qa1] - data[0];
+          Jqvel = qvel[da1];
+          invweight = dof_invweight0[da1];
+        }
+        for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, k == da1 ? 1.0f : (k == da2 ? -d2 : 0.0f));
+        efc_row(m, d, L, s, wid, r, pos, pos, invweight, eq_solref + 2 * e, eq_solimp + 5 * e, 0.0f, Jqvel, 0.0f,
+                CNSTR_EQUALITY, e);
+      }
+      int cnt = __popcll(bal);
+      nefc += cnt;
+      ne += cnt;
+    }
+  }
   // --- friction dof rows (constraint.py:1113-1190)
   if (!dsbl_constraint && !(m.opt_disableflags & DSBL_FRICTIONLOSS)) {
     const float* dof_frictionloss = MR(dof_frictionloss);
@@ -980,26 +1036,67 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
         c.n = 0;
         int g1 = 0, g2 = 0, pairid0 = -2;
         float margin = 0.0f;
+        unsigned bmask = 0;  // plane-box: active corners (collision_primitive.py:737-790 writes all 8)
+        bool pbox = false;
         if (k < npass) {
           int p = plist[k];
           g1 = m.nxn_geom_pair[2 * p];
           g2 = m.nxn_geom_pair[2 * p + 1];
           pairid0 = m.nxn_pairid[2 * p];
           margin = geom_margin[g1] + geom_margin[g2];
-          narrowphase(m, L, s, wid, g1, g2, margin, c);
+          pbox = m.geom_type[g1] == GEOM_PLANE && m.geom_type[g2] == GEOM_BOX;
+          if (pbox) {
+            const float* r1 = s + L.gxmat + 9 * g1;
+            float n1[3] = {r1[2], r1[5], r1[8]}, cp[3];
+            for (int q = 0; q < 8; q++) {
+              float dist = plane_box_corner(q, n1, s + L.gxpos + 3 * g1, s + L.gxpos + 3 * g2, s + L.gxmat + 9 * g2,
+                                            MR(geom_size) + 3 * g2, cp);
+              if (dist < margin && pairid0 >= -1) bmask |= 1u << q;
+            }
+          } else {
+            narrowphase(m, L, s, wid, g1, g2, margin, c);
+          }
         }
         // active contacts (write_contact collision_core.py:199-213)
         bool a0 = c.n > 0 && c.dist[0] < margin && pairid0 >= -1;
         bool a1 = c.n > 1 && c.dist[1] < margin && pairid0 >= -1;
-        int cnt = (int)a0 + (int)a1;
+        int cnt = pbox ? __popc(bmask) : (int)a0 + (int)a1;
         int incl = wave_scan_incl(cnt);
         int first = running + incl - cnt;
         bool stage0 = a0 && first >= rbeg && first < rend;
         bool stage1 = a1 && first + (int)a0 >= rbeg && first + (int)a0 < rend;
-        if (stage0 || stage1) {
+        bool stagebox = cnt > 0 && pbox && first < rend && first + cnt > rbeg;
+        if (stage0 || stage1 || stagebox) {
           float gap, friction[5], solref[2], solimp[5];
           int condim;
           contact_params(m, wid, g1, g2, &margin, &gap, &condim, friction, solref, solimp);
+          if (pbox) {
+            const float* r1 = s + L.gxmat + 9 * g1;
+            float n1[3] = {r1[2], r1[5], r1[8]}, frame[9];
+            make_frame(frame, n1);
+            int kk = 0;
+            for (int q = 0; q < 8; q++) {
+              if (!(bmask & (1u << q))) continue;
+              int idx = first + kk;
+              kk++;
+              if (idx < rbeg || idx >= rend) continue;
+              float* rec = s + L.con + (idx - rbeg) * CREC;
+              float cp[3];
+              rec[0] = plane_box_corner(q, n1, s + L.gxpos + 3 * g1, s + L.gxpos + 3 * g2, s + L.gxmat + 9 * g2,
+                                        MR(geom_size) + 3 * g2, cp);
+              rec[1] = margin - gap;
+              for (int i = 0; i < 3; i++) rec[2 + i] = cp[i];
+              for (int i = 0; i < 9; i++) rec[5 + i] = frame[i];
+              for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
+              rec[19] = solref[0]; rec[20] = solref[1];
+              rec[21] = 0.0f; rec[22] = 0.0f;
+              for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
+              int* reci = reinterpret_cast<int*>(rec);
+              reci[28] = condim;
+              reci[29] = g1;
+              reci[30] = g2;
+            }
+          }
           int kk = 0;
 #pragma unroll
           for (int sub = 0; sub < 2; sub++) {
@@ -1158,11 +1255,11 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
     }
   }
   if (lane == 0) {
-    d.ne[wid] = 0;
+    d.ne[wid] = ne;
     d.nf[wid] = nf;
     d.nl[wid] = nl;
     d.nefc[wid] = nefc;
-    si[L.iscratch + 60] = 0;
+    si[L.iscratch + 60] = ne;
     si[L.iscratch + 61] = nf;
     si[L.iscratch + 62] = nefc;
   }

@@ -86,7 +86,9 @@ def _model_attr(name):
   return (None, name)
 
 
-_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE}
+_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.BOX, types.GeomType.MESH}
+# narrowphase pairs built on the device (type-sorted): collision_primitive.py:1280-1300 subset
+_SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3)}
 
 
 def put_model(mjm, device=None) -> types.Model:
@@ -96,7 +98,7 @@ def put_model(mjm, device=None) -> types.Model:
   for g in np.unique(mjm.geom_type):
     if int(g) not in _SUPPORTED_GEOMS:
       raise NotImplementedError(f"geom type {types.GeomType(int(g)).name} not supported.")
-  if mjm.opt.integrator not in (types.IntegratorType.EULER,):
+  if mjm.opt.integrator not in (types.IntegratorType.EULER, types.IntegratorType.IMPLICITFAST):
     raise NotImplementedError(f"{types.IntegratorType(mjm.opt.integrator).name} is unsupported.")
   if mjm.opt.cone != types.ConeType.PYRAMIDAL:
     raise NotImplementedError("ELLIPTIC is unsupported.")
@@ -106,8 +108,16 @@ def put_model(mjm, device=None) -> types.Model:
     raise NotImplementedError("noslip solver not implemented.")
   if is_sparse(mjm):
     raise NotImplementedError("sparse Jacobian / nv > 32 models are not supported by this build yet.")
-  if getattr(mjm, "ntendon", 0) or getattr(mjm, "neq", 0) or getattr(mjm, "nsensor", 0) or getattr(mjm, "nflex", 0):
-    raise NotImplementedError("tendons / equality constraints / sensors / flex are not supported by this build yet.")
+  if getattr(mjm, "ntendon", 0) or getattr(mjm, "nsensor", 0) or getattr(mjm, "nflex", 0):
+    raise NotImplementedError("tendons / sensors / flex are not supported by this build yet.")
+  if getattr(mjm, "neq", 0) and np.any(mjm.eq_type != types.EqType.JOINT):
+    raise NotImplementedError("only joint equality constraints are supported by this build yet.")
+  pairs_chk, _ = nxn_geom_pairs(mjm)
+  for g1, g2 in pairs_chk:
+    t = tuple(sorted((int(mjm.geom_type[g1]), int(mjm.geom_type[g2]))))
+    if t not in _SUPPORTED_PAIRS:
+      names = tuple(types.GeomType(x).name for x in t)
+      raise NotImplementedError(f"collision between {names[0]} and {names[1]} is not supported by this build yet.")
   if np.any(mjm.actuator_trntype > types.TrnType.JOINTINPARENT):
     raise NotImplementedError("only joint transmissions are supported.")
 
@@ -137,7 +147,7 @@ def put_model(mjm, device=None) -> types.Model:
   for n in ("nq", "nv", "nu", "na", "nbody", "njnt", "ngeom", "nsite", "ncam", "nlight", "nmocap", "nM", "nC"):
     setattr(m, n, int(getattr(mjm, n)))
   m.ntendon = 0
-  m.neq = 0
+  m.neq = int(getattr(mjm, "neq", 0))
   m.nsensor = 0
   m.nsensordata = 0
   m.nflex = 0
@@ -281,7 +291,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
   )
   ints = dict(
     ne=(), nf=(), nl=(), nefc=(), solver_niter=(), moment_rownnz=(nu,), moment_rowadr=(nu,), moment_colind=(m.nJmom,),
-    efc_type=(njmax,), efc_id=(njmax,), efc_state=(njmax_pad,),
+    efc_type=(njmax,), efc_id=(njmax,), efc_state=(njmax_pad,), eq_active=(m.neq,),
   )
   creal = dict(
     contact_dist=(), contact_pos=(3,), contact_frame=(3, 3), contact_includemargin=(), contact_friction=(5,),
@@ -347,7 +357,6 @@ def _alloc_data(m, nworld, nconmax, njmax, naconmax, device):
   d.nacon = torch.zeros(1, dtype=torch.int32, device=device)
   d.ncollision = torch.zeros(1, dtype=torch.int32, device=device)
   d.sensordata = torch.zeros((nworld, 0), dtype=torch.float32, device=device)
-  d.eq_active = torch.zeros((nworld, 0), dtype=torch.bool, device=device)
   d.efc.J_rownnz = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
   d.efc.J_rowadr = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
   d.efc.J_colind = torch.zeros((nworld, 0, 0), dtype=torch.int32, device=device)
@@ -402,6 +411,8 @@ def make_data(mjm, nworld: int = 1, nconmax: Optional[int] = None, njmax: Option
     m = put_model(mjm, device=dev)
   d = _alloc_data(m, nworld, nconmax, njmax, naconmax, dev)
   d.qpos[:] = torch.as_tensor(np.asarray(mjm.qpos0, dtype=np.float32), device=dev)
+  if m.neq:  # int32 on the device (the reference's bool), initialised from eq_active0
+    d.eq_active[:] = torch.as_tensor(np.asarray(mjm.eq_active0, dtype=np.int32), device=dev)
   if mjm.nmocap:
     for b in np.nonzero(mjm.body_mocapid >= 0)[0]:
       k = mjm.body_mocapid[b]
@@ -449,6 +460,9 @@ def put_data(mjm, mjd, nworld: int = 1, nconmax: Optional[int] = None, nccdmax: 
     tile("mocap_quat", mjd.mocap_quat, (mjm.nmocap, 4))
   if hasattr(mjd, "qacc"):
     tile("qacc", mjd.qacc, (mjm.nv,))
+  if m.neq:
+    eqa = getattr(mjd, "eq_active", mjm.eq_active0)
+    d.eq_active[:] = torch.as_tensor(np.asarray(eqa, dtype=np.int32).reshape(m.neq), device=dev)
   d.solver_niter.fill_(int(np.asarray(getattr(mjd, "solver_niter", [0])).reshape(-1)[0]))
   return d
 

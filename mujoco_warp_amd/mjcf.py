@@ -35,6 +35,7 @@ from .types import (
   DisableBit,
   DynType,
   EnableBit,
+  EqType,
   GainType,
   GeomType,
   IntegratorType,
@@ -770,8 +771,7 @@ class _Compiler:
     self._build_actuators(root)
     self._build_contact(root)
     self._build_keys(root)
-    m.neq = 0
-    m.eq_active0 = np.zeros(0, dtype=np.uint8)
+    self._build_equality(root)
     m.ntendon = 0
     m.nsensor = 0
     m.nsensordata = 0
@@ -824,8 +824,11 @@ class _Compiler:
 
   def _geom(self, ga, bodyid):
     gtype = _GEOM_TYPES[ga.get("type", _GEOM_DEFAULTS["type"])]
-    if gtype in (GeomType.MESH, GeomType.HFIELD, GeomType.SDF):
+    if gtype in (GeomType.HFIELD, GeomType.SDF):
       raise NotImplementedError(f"geom type {gtype.name} not supported by the MJCF compiler")
+    # mesh geoms: the mesh file is not read (no mesh collision or mesh-derived inertia here), so
+    # the geom keeps its declared frame; put_model rejects meshes that can collide and bodies
+    # whose inertia would come from a mesh.
 
     def vec(k, n):
       given = _floats(ga[k]) if k in ga else []
@@ -872,6 +875,10 @@ class _Compiler:
       vol = 0.0
       rbound = 0.0
       aabb = [0, 0, 0, size[0], size[1], 0.0]
+    elif gtype == GeomType.MESH:
+      vol = 0.0
+      rbound = 0.0
+      aabb = [0, 0, 0, 0, 0, 0]
     else:
       raise NotImplementedError(gtype)
     density = float(ga.get("density", _GEOM_DEFAULTS["density"]))
@@ -929,6 +936,8 @@ class _Compiler:
           m.body_inertia[i] = _floats(ia["diaginertia"], 3)
         continue
       geoms = [g for g in range(m.ngeom) if m.geom_bodyid[g] == i and m.geom_type[g] != GeomType.PLANE]
+      if any(m.geom_type[g] == GeomType.MESH for g in geoms):
+        raise NotImplementedError(f"body {b.name}: inertia from mesh geoms needs the mesh file (give <inertial>)")
       if not geoms:
         continue
       mass = sum(m.geom_mass_[g] for g in geoms)
@@ -1133,6 +1142,36 @@ class _Compiler:
         actnum[i] = 1
         na += 1
     m.actuator_actadr, m.actuator_actnum, m.na = actadr, actnum, na
+
+  def _build_equality(self, root):
+    """<equality>: joint couplings (constraint.py:367-495); other kinds are not built yet."""
+    m = self.m
+    name2jnt = {n: i for i, n in enumerate(m.jnt_names)}
+    rows = []
+    for eq in root.findall("equality"):
+      for el in eq:
+        a = dict(self.defaults[el.get("class", "main")].attrs.get("equality", {}))
+        a.update(el.attrib)
+        if el.tag != "joint":
+          raise NotImplementedError(f"<equality><{el.tag}> is not supported by the MJCF compiler yet")
+        data = np.zeros(11)
+        data[:5] = _merge_vec([0, 1, 0, 0, 0], _floats(a.get("polycoef", "0 1 0 0 0")))
+        rows.append(dict(
+          name=a.get("name", ""), type=int(EqType.JOINT), obj1=name2jnt[a["joint1"]],
+          obj2=name2jnt[a["joint2"]] if "joint2" in a else -1, data=data,
+          solref=_merge_vec([0.02, 1.0], _floats(a.get("solref", "0.02 1"))),
+          solimp=_merge_vec([0.9, 0.95, 0.001, 0.5, 2.0], _floats(a.get("solimp", "0.9 0.95 0.001 0.5 2"))),
+          active=a.get("active", "true") == "true"))
+    m.neq = len(rows)
+    m.eq_names = [r["name"] for r in rows]
+    m.eq_type = np.array([r["type"] for r in rows], dtype=np.int32)
+    m.eq_obj1id = np.array([r["obj1"] for r in rows], dtype=np.int32)
+    m.eq_obj2id = np.array([r["obj2"] for r in rows], dtype=np.int32)
+    m.eq_objtype = np.full(m.neq, 3, dtype=np.int32)  # mjOBJ_JOINT
+    m.eq_data = np.array([r["data"] for r in rows]).reshape(m.neq, 11)
+    m.eq_solref = np.array([r["solref"] for r in rows]).reshape(m.neq, 2)
+    m.eq_solimp = np.array([r["solimp"] for r in rows]).reshape(m.neq, 5)
+    m.eq_active0 = np.array([r["active"] for r in rows], dtype=np.uint8)
 
   def _build_contact(self, root):
     m = self.m

@@ -32,6 +32,9 @@ enum { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
 enum { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICITFAST = 3 };
 enum { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
 enum { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
+enum { DYN_NONE = 0 };
+enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
+enum { INTEGRATOR_EULER = 0, INTEGRATOR_RK4 = 1, INTEGRATOR_IMPLICIT = 2, INTEGRATOR_IMPLICITFAST = 3 };
 enum { BIAS_NONE = 0, BIAS_AFFINE = 1 };
 enum { TRN_JOINT = 0, TRN_JOINTINPARENT = 1 };
 enum { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
@@ -266,10 +269,10 @@ void orc_ctrl_noise(const orc_model* m, real* ctrl, const real* center, int ncen
  * ============================================================================================= */
 static void world_view(const orc_model* m, const orc_data* b, int w, orc_data* o) {
   int nq = m->nq, nv = m->nv, nu = m->nu, na = m->na, nbody = m->nbody, njnt = m->njnt;
-  int ngeom = m->ngeom, nsite = m->nsite, ncam = m->ncam, nlight = m->nlight, nmocap = m->nmocap;
+  int ngeom = m->ngeom, nsite = m->nsite, ncam = m->ncam, nlight = m->nlight, nmocap = m->nmocap, neq = m->neq;
   int njmax = b->njmax, nconmax = b->nconmax;
   (void)nq; (void)nv; (void)nu; (void)na; (void)nbody; (void)njnt; (void)ngeom; (void)nsite; (void)ncam;
-  (void)nlight; (void)nmocap; (void)njmax; (void)nconmax;
+  (void)nlight; (void)nmocap; (void)njmax; (void)nconmax; (void)neq;
   o->njmax = njmax;
   o->nconmax = nconmax;
 #define ORC_OFF(name, n) o->name = b->name + (size_t)w * (size_t)(n);
@@ -979,6 +982,19 @@ static void contact_params(const orc_model* m, int g1, int g2, real* margin, rea
 }
 
 /* collision_driver.py:697-789 + collision_primitive.py:1300-1454 (+ write_contact collision_core.py:159-232) */
+/* collision_primitive_core.py:395-443: corner k of the box against the plane */
+static void plane_box_corner(int k, const real* n, const real* ppos, const real* bpos, const real* brot, const real* bsize,
+                             real* dist, real* pos) {
+  real dif[3] = {bpos[0] - ppos[0], bpos[1] - ppos[1], bpos[2] - ppos[2]};
+  real center_dist = dot3(dif, n);
+  real cl[3] = {(k & 1) ? bsize[0] : -bsize[0], (k & 2) ? bsize[1] : -bsize[1], (k & 4) ? bsize[2] : -bsize[2]};
+  real corner[3];
+  matvec3(corner, brot, cl);
+  real cdist = center_dist + dot3(n, corner);
+  *dist = cdist;
+  for (int i = 0; i < 3; i++) pos[i] = corner[i] + bpos[i] - 0.5 * n[i] * cdist;
+}
+
 static void collision(const orc_model* m, orc_data* d) {
   *d->ncon = 0;
   *d->ncollision = 0;
@@ -1017,19 +1033,26 @@ static void collision(const orc_model* m, orc_data* d) {
       c.n = 1;
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
       capsule_capsule(&c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], margin);
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {
+      c.n = 8; /* all 8 corners are candidates (collision_primitive.py:737-790) */
     } else {
       continue; /* pair type not supported by the oracle (not on the benchmark path) */
     }
     for (int k = 0; k < c.n; k++) {
-      real dist = c.dist[k];
+      if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {
+        plane_box_corner(k, n1, p1, p2, r2, s2, &c.dist[0], c.pos[0]);
+        make_frame(c.frame[0], n1);
+      }
+      int kk = (t1 == GEOM_PLANE && t2 == GEOM_BOX) ? 0 : k;
+      real dist = c.dist[kk];
       int active = dist < margin;
       if ((pairid0 == -2 || !active) && pairid1 == -1) continue;
       if (!(pairid0 >= -1 && active)) continue; /* sensor-only contacts are not produced here */
       int cid = *d->ncon;
       if (cid >= d->nconmax) { (*d->ncon)++; continue; }
       d->con_dist[cid] = dist;
-      memcpy(d->con_pos + 3 * cid, c.pos[k], 3 * sizeof(real));
-      memcpy(d->con_frame + 9 * cid, c.frame[k], 9 * sizeof(real));
+      memcpy(d->con_pos + 3 * cid, c.pos[kk], 3 * sizeof(real));
+      memcpy(d->con_frame + 9 * cid, c.frame[kk], 9 * sizeof(real));
       d->con_includemargin[cid] = margin - gap;
       memcpy(d->con_friction + 5 * cid, friction, 5 * sizeof(real));
       memcpy(d->con_solref + 2 * cid, solref, 2 * sizeof(real));
@@ -1105,6 +1128,37 @@ static void make_constraint(const orc_model* m, orc_data* d) {
   int nv = m->nv, njmax = d->njmax;
   *d->ne = *d->nf = *d->nl = *d->nefc = 0;
   if (m->opt_disableflags & DSBL_CONSTRAINT) return;
+  /* equality joint constraint.py:367-495 (rows in equality index order) */
+  if (!(m->opt_disableflags & DSBL_EQUALITY)) {
+    for (int e = 0; e < m->neq; e++) {
+      if (m->eq_type[e] != EQ_JOINT || !d->eq_active[e]) continue;
+      (*d->ne)++;
+      int efcid = (*d->nefc)++;
+      if (efcid >= njmax) continue;
+      int j1 = m->eq_obj1id[e], j2 = m->eq_obj2id[e];
+      const real* data = m->eq_data + 11 * e;
+      int da1 = m->jnt_dofadr[j1], qa1 = m->jnt_qposadr[j1];
+      real* J = d->efc_J + (size_t)efcid * nv;
+      memset(J, 0, nv * sizeof(real));
+      J[da1] = 1;
+      real pos, Jqvel, invweight;
+      if (j2 > -1) {
+        int qa2 = m->jnt_qposadr[j2], da2 = m->jnt_dofadr[j2];
+        real dif = d->qpos[qa2] - m->qpos0[qa2];
+        real rhs = data[0] + dif * (data[1] + dif * (data[2] + dif * (data[3] + dif * data[4])));
+        real deriv_2 = data[1] + dif * (2 * data[2] + dif * (3 * data[3] + dif * 4 * data[4]));
+        pos = d->qpos[qa1] - m->qpos0[qa1] - rhs;
+        Jqvel = d->qvel[da1] - d->qvel[da2] * deriv_2;
+        invweight = m->dof_invweight0[da1] + m->dof_invweight0[da2];
+        J[da2] = -deriv_2;
+      } else {
+        pos = d->qpos[qa1] - m->qpos0[qa1] - data[0];
+        Jqvel = d->qvel[da1];
+        invweight = m->dof_invweight0[da1];
+      }
+      efc_row(m, d, efcid, pos, pos, invweight, m->eq_solref + 2 * e, m->eq_solimp + 5 * e, 0, Jqvel, 0, CNSTR_EQUALITY, e);
+    }
+  }
   /* friction dof constraint.py:1113-1190 */
   if (!(m->opt_disableflags & DSBL_FRICTIONLOSS)) {
     for (int i = 0; i < nv; i++) {
@@ -1537,22 +1591,10 @@ static void solve(const orc_model* m, orc_data* d) {
 }
 
 /* forward.py:51-354 (_advance + euler with optional implicit damping) */
-static void euler(const orc_model* m, orc_data* d) {
+/* forward.py:213-274 _advance */
+static void euler_advance(const orc_model* m, orc_data* d, const real* qacc_adv) {
   int nv = m->nv;
   real dt = m->opt_timestep;
-  real* qacc_adv = d->qacc;
-  real* tmp = NULL;
-  if (!(m->opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER))) {
-    tmp = (real*)malloc(((size_t)2 * nv * nv + nv) * sizeof(real));
-    real* Mi = tmp;
-    real* L = tmp + (size_t)nv * nv;
-    real* q = L + (size_t)nv * nv;
-    memcpy(Mi, d->qM, (size_t)nv * nv * sizeof(real));
-    for (int i = 0; i < nv; i++) Mi[i * nv + i] += dt * m->dof_damping[i];
-    cholesky(nv, Mi, L);
-    cholesky_solve(nv, L, d->efc_Ma, q);
-    qacc_adv = q;
-  }
   /* _next_activation: na-sized, skipped when na == 0 */
   for (int a = 0; a < m->nu; a++) {
     int adr = m->actuator_actadr[a];
@@ -1580,7 +1622,86 @@ static void euler(const orc_model* m, orc_data* d) {
   }
   d->time[0] += dt;
   memcpy(d->qacc_warmstart, d->qacc, nv * sizeof(real));
+}
+
+/* forward.py:326-354 euler (implicit damping when EULERDAMP is enabled) */
+static void euler(const orc_model* m, orc_data* d) {
+  int nv = m->nv;
+  real dt = m->opt_timestep;
+  if (m->opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER)) {
+    euler_advance(m, d, d->qacc);
+    return;
+  }
+  real* tmp = (real*)malloc(((size_t)2 * nv * nv + nv) * sizeof(real));
+  real* Mi = tmp;
+  real* L = tmp + (size_t)nv * nv;
+  real* q = L + (size_t)nv * nv;
+  memcpy(Mi, d->qM, (size_t)nv * nv * sizeof(real));
+  for (int i = 0; i < nv; i++) Mi[i * nv + i] += dt * m->dof_damping[i];
+  cholesky(nv, Mi, L);
+  cholesky_solve(nv, L, d->efc_Ma, q);
+  euler_advance(m, d, q);
   free(tmp);
+}
+
+static void implicit(const orc_model* m, orc_data* d);
+
+/* forward.py:1003-1018: the integrator selected by the model */
+static void integrate(const orc_model* m, orc_data* d) {
+  if (m->opt_integrator == INTEGRATOR_IMPLICITFAST) implicit(m, d);
+  else euler(m, d);
+}
+
+/* derivative.py:36-107 _qderiv_actuator_passive_vel: d(actuator force)/d(velocity) scale */
+static real actuator_vel_deriv(const orc_model* m, const orc_data* d, int a) {
+  real gain = m->actuator_gaintype[a] == GAIN_AFFINE ? m->actuator_gainprm[10 * a + 2] : 0;
+  real bias = m->actuator_biastype[a] == BIAS_AFFINE ? m->actuator_biasprm[10 * a + 2] : 0;
+  if (bias == 0 && gain == 0) return 0;
+  if (m->actuator_forcelimited[a]) {
+    real f = d->actuator_force[a];
+    if (f <= m->actuator_forcerange[2 * a] || f >= m->actuator_forcerange[2 * a + 1]) return 0;
+  }
+  real vel = bias;
+  if (m->actuator_dyntype[a] != DYN_NONE) {
+    if (gain != 0) vel += gain * d->act[m->actuator_actadr[a] + m->actuator_actnum[a] - 1]; /* actearly not supported */
+  } else if (gain != 0) {
+    vel += gain * d->ctrl[a];
+  }
+  return vel;
+}
+
+/* forward.py:494-510 implicit() + derivative.py:320-416 deriv_smooth_vel (implicitfast):
+ * (qM - dt * qDeriv) qacc = Ma with qDeriv = sum_a vel_a m_a m_a' - diag(damping) on the tree pattern */
+static void implicit(const orc_model* m, orc_data* d) {
+  int nv = m->nv;
+  real dt = m->opt_timestep;
+  int flags = m->opt_disableflags;
+  if ((flags & (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) == (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) {
+    euler_advance(m, d, d->qacc);
+    return;
+  }
+  real* A = (real*)malloc(((size_t)2 * nv * nv + nv + m->nu) * sizeof(real));
+  real* L = A + (size_t)nv * nv;
+  real* q = L + (size_t)nv * nv;
+  real* vel = q + nv;
+  for (int a = 0; a < m->nu; a++) vel[a] = (flags & DSBL_ACTUATION) ? 0 : actuator_vel_deriv(m, d, a);
+  for (int i = 0; i < nv; i++)
+    for (int j = 0; j < nv; j++) A[i * nv + j] = 0;
+  for (int i = 0; i < nv; i++) {
+    for (int j = i; j > -1; j = m->dof_parentid[j]) { /* qM_fullm pattern (io.py:601-607) */
+      real qd = 0;
+      for (int a = 0; a < m->nu; a++)
+        if (vel[a] != 0) qd += d->actuator_moment[a * nv + i] * d->actuator_moment[a * nv + j] * vel[a];
+      if (!(flags & DSBL_DAMPER) && i == j) qd -= m->dof_damping[i];
+      qd *= dt;
+      A[i * nv + j] = d->qM[i * nv + j] - qd;
+      A[j * nv + i] = A[i * nv + j];
+    }
+  }
+  cholesky(nv, A, L);
+  cholesky_solve(nv, L, d->efc_Ma, q);
+  euler_advance(m, d, q);
+  free(A);
 }
 
 /* forward.py:972-1000 */
@@ -1595,7 +1716,7 @@ static void forward_world(const orc_model* m, orc_data* d) {
 /* forward.py:1003-1018 */
 static void step_world(const orc_model* m, orc_data* d) {
   forward_world(m, d);
-  euler(m, d);
+  integrate(m, d);
 }
 
 int orc_real_size(void) { return (int)sizeof(real); }
@@ -1609,7 +1730,7 @@ ORC_BATCH(orc_fwd_velocity, fwd_velocity)
 ORC_BATCH(orc_fwd_actuation, fwd_actuation)
 ORC_BATCH(orc_fwd_acceleration, fwd_acceleration)
 ORC_BATCH(orc_solve, solve)
-ORC_BATCH(orc_euler, euler)
+ORC_BATCH(orc_euler, integrate)
 
 void orc_step(const orc_model* m, const orc_data* b, int nworld, int nthread) {
 #ifdef _OPENMP

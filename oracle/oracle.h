@@ -26,7 +26,7 @@ typedef ORC_REAL real;
 /* ---- model: int scalars ---- */
 #define ORC_MODEL_INT_SCALARS(X)                                                                   \
   X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
-  X(nxn) X(nmaxpyramid) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
+  X(nxn) X(nmaxpyramid) X(neq) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)
 
 /* ---- model: real scalars ---- */
@@ -54,7 +54,8 @@ typedef ORC_REAL real;
   X(light_pos0, nlight * 3) X(light_dir0, nlight * 3)                                              \
   X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
   X(actuator_ctrlrange, nu * 2) X(actuator_forcerange, nu * 2) X(actuator_actrange, nu * 2)       \
-  X(actuator_gear, nu * 6)
+  X(actuator_gear, nu * 6)                                                                         \
+  X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)
 
 /* ---- model: int arrays (name, element count) ---- */
 #define ORC_MODEL_INT_ARRAYS(X)                                                                    \
@@ -70,7 +71,8 @@ typedef ORC_REAL real;
   X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
-  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)
+  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)                                                 \
+  X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)
 
 /* ---- per-world data: real arrays (name, element count per world) ---- */
 #define ORC_DATA_REAL_ARRAYS(X)                                                                    \
@@ -97,7 +99,7 @@ typedef ORC_REAL real;
 #define ORC_DATA_INT_ARRAYS(X)                                                                     \
   X(ne, 1) X(nf, 1) X(nl, 1) X(nefc, 1) X(ncon, 1) X(ncollision, 1) X(solver_niter, 1)            \
   X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax)                                          \
-  X(con_dim, nconmax) X(con_geom, nconmax * 2) X(con_efc_address, nconmax * 10)
+  X(con_dim, nconmax) X(con_geom, nconmax * 2) X(con_efc_address, nconmax * 10) X(eq_active, neq)
 
 typedef struct orc_model {
 #define ORC_DECL_I(name) int name;

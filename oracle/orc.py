@@ -106,7 +106,7 @@ class OracleModel:
     o = mjm.opt
     vals = dict(
       nq=mjm.nq, nv=mjm.nv, nu=mjm.nu, na=mjm.na, nbody=mjm.nbody, njnt=mjm.njnt, ngeom=mjm.ngeom, nsite=mjm.nsite,
-      ncam=mjm.ncam, nlight=mjm.nlight, nmocap=mjm.nmocap, nxn=len(pairs),
+      ncam=mjm.ncam, nlight=mjm.nlight, nmocap=mjm.nmocap, nxn=len(pairs), neq=mjm.neq,
       nmaxpyramid=max(1, 2 * (int(np.concatenate(([0], mjm.geom_condim)).max()) - 1)),
       opt_integrator=o.integrator, opt_cone=o.cone, opt_solver=o.solver, opt_iterations=o.iterations,
       opt_ls_iterations=o.ls_iterations, opt_disableflags=o.disableflags, opt_enableflags=o.enableflags,
@@ -166,6 +166,8 @@ class OracleData:
     self.arrays["qpos"][:] = m.qpos0
     if m.nmocap:
       self.arrays["mocap_quat"][:] = np.tile([1.0, 0, 0, 0], m.nmocap)
+    if m.neq:
+      self.arrays["eq_active"][:] = np.asarray(m.eq_active0, dtype=np.int32)
 
   def __getattr__(self, name):
     arrays = self.__dict__.get("arrays")

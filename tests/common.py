@@ -11,6 +11,15 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HUMANOID = os.path.join(ROOT, "models", "humanoid.xml")
+FRANKA = os.path.join(ROOT, "models", "franka_emika_panda", "scene.xml")
+
+# free boxes over a plane (plane-box narrowphase); boxes do not collide with each other
+# (contype 2 / conaffinity 1) because box-box is not built yet
+BOXES_XML = """<mujoco><option timestep="0.002"/><worldbody><geom type="plane" size="5 5 .1"/>
+<body pos="-.5 0 .2"><freejoint/><geom type="box" size=".1 .08 .06" contype="2" conaffinity="1"/></body>
+<body pos=".0 0 .2"><freejoint/><geom type="box" size=".05 .12 .04" contype="2" conaffinity="1"/></body>
+<body pos=".5 0 .2"><freejoint/><geom type="box" size=".07 .07 .07" contype="2" conaffinity="1" condim="1"/></body>
+</worldbody></mujoco>"""
 
 
 def humanoid_model(solver="CG", iterations=None, ls_iterations=None):
@@ -23,6 +32,45 @@ def humanoid_model(solver="CG", iterations=None, ls_iterations=None):
   if ls_iterations is not None:
     m.opt.ls_iterations = ls_iterations
   return m
+
+
+def franka_model(solver=None):
+  from mujoco_warp_amd import mjcf
+
+  m = mjcf.load_model(FRANKA)
+  if solver is not None:
+    m.opt.solver = {"CG": 1, "NEWTON": 2}[solver]
+  return m
+
+
+def franka_states(mjm, nworld, seed=0, qvel_noise=0.3):
+  """Joint positions uniform inside the joint ranges, controls inside ctrlrange (seeded)."""
+  rng = np.random.default_rng(seed)
+  lo, hi = mjm.jnt_range[:, 0], mjm.jnt_range[:, 1]
+  qpos = lo + (hi - lo) * rng.uniform(0.05, 0.95, (nworld, mjm.nq))
+  qvel = rng.normal(0, qvel_noise, (nworld, mjm.nv))
+  cr = mjm.actuator_ctrlrange
+  ctrl = cr[:, 0] + (cr[:, 1] - cr[:, 0]) * rng.uniform(0, 1, (nworld, mjm.nu))
+  return qpos, qvel, ctrl
+
+
+def boxes_states(mjm, nworld, seed=0):
+  """Three free boxes at random orientations, lowered so that corners touch or penetrate the plane."""
+  from mujoco_warp_amd.mjcf import quat_to_mat
+
+  rng = np.random.default_rng(seed)
+  qpos = np.tile(mjm.qpos0, (nworld, 1))
+  for w in range(nworld):
+    for b in range(3):
+      q = rng.normal(size=4)
+      q /= np.linalg.norm(q)
+      R = quat_to_mat(q)
+      half = mjm.geom_size[1 + b]
+      lowest = np.abs(R @ np.diag(half)).sum(axis=1)[2]  # half extent along z
+      qpos[w, 7 * b + 2] = lowest - rng.uniform(-0.004, 0.01)
+      qpos[w, 7 * b + 3 : 7 * b + 7] = q
+  qvel = rng.normal(0, 0.2, (nworld, mjm.nv))
+  return qpos, qvel, np.zeros((nworld, mjm.nu))
 
 
 def random_states(mjm, nworld, seed=0, key=0, qpos_noise=0.05, qvel_noise=0.5, ctrl_noise=1.0):

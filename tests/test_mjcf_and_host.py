@@ -116,9 +116,9 @@ def test_unsupported_features_raise():
   import mujoco_warp_amd as mjw
   from mujoco_warp_amd import mjcf
 
-  box = mjcf.load_model_from_string('<mujoco><worldbody><body><freejoint/><geom type="box" size=".1 .1 .1"/></body></worldbody></mujoco>')
+  cyl = mjcf.load_model_from_string('<mujoco><worldbody><body><freejoint/><geom type="cylinder" size=".1 .1"/></body></worldbody></mujoco>')
   with pytest.raises(NotImplementedError):
-    mjw.put_model(box, device="cpu")
+    mjw.put_model(cyl, device="cpu")
 
 
 # ---- C ABI ------------------------------------------------------------------------------------
