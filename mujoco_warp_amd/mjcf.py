@@ -21,6 +21,7 @@ conventions:
 
 from __future__ import annotations
 
+import copy
 import math
 import os
 import xml.etree.ElementTree as ET
@@ -448,8 +449,63 @@ class _Compiler:
       elif tag == "inertial":
         body.inertial = dict(child.attrib)
       elif tag == "frame":
-        raise NotImplementedError("<frame> is not supported by the MJCF compiler")
+        for sub in self._flatten_frame(child):
+          self._parse_frame_child(sub, body, childclass)
     return body
+
+  def _parse_frame_child(self, child, body, childclass):
+    """A child of a <frame> whose pose has already been composed with the frame's."""
+    tag = child.tag
+    if tag == "body":
+      body.children.append(self._parse_body(child, body, childclass))
+    elif tag == "joint":
+      body.joints.append(self._resolve("joint", child, childclass))
+    elif tag == "geom":
+      body.geoms.append(self._resolve("geom", child, childclass))
+    elif tag == "site":
+      body.sites.append(self._resolve("site", child, childclass))
+    elif tag == "camera":
+      body.cams.append(self._resolve("camera", child, childclass))
+    elif tag == "light":
+      body.lights.append(self._resolve("light", child, childclass))
+
+  def _flatten_frame(self, frame):
+    """<frame pos quat/euler/...>: compose the frame transform into each child (MJCF frame semantics)."""
+    if frame.get("childclass") is not None and len(frame):
+      raise NotImplementedError("<frame childclass=...> is not supported by the MJCF compiler")
+    fpos = np.array(_floats(frame.get("pos", "0 0 0"), 3))
+    fq = _orientation(frame.attrib, self.angle_scale, self.eulerseq)
+    fq = np.array([1.0, 0, 0, 0]) if fq is None else np.asarray(fq, dtype=float)
+    R = quat_to_mat(fq)
+    out = []
+    for child in list(frame):
+      if child.tag == "frame":
+        subs = self._flatten_frame(child)
+      else:
+        subs = [child]
+      for c in subs:
+        c = copy.deepcopy(c)
+        a = c.attrib
+        if c.tag == "geom" and "fromto" in a:
+          ft = np.array(_floats(a["fromto"], 6))
+          p0, p1 = R @ ft[:3] + fpos, R @ ft[3:] + fpos
+          a["fromto"] = " ".join(repr(float(x)) for x in np.concatenate([p0, p1]))
+        elif c.tag in ("body", "geom", "site", "camera", "light", "joint"):
+          pos = np.array(_floats(a.get("pos", "0 0 0"), 3))
+          a["pos"] = " ".join(repr(float(x)) for x in (R @ pos + fpos))
+          if c.tag == "joint":
+            if "axis" in a:
+              a["axis"] = " ".join(repr(float(x)) for x in (R @ np.array(_floats(a["axis"], 3))))
+          elif c.tag == "light" and "dir" in a:
+            a["dir"] = " ".join(repr(float(x)) for x in (R @ np.array(_floats(a["dir"], 3))))
+          else:
+            q = _orientation(a, self.angle_scale, self.eulerseq)
+            q = np.array([1.0, 0, 0, 0]) if q is None else np.asarray(q, dtype=float)
+            for k in ("quat", "euler", "axisangle", "xyaxes", "zaxis"):
+              a.pop(k, None)
+            a["quat"] = " ".join(repr(float(x)) for x in quat_mul(fq, q))
+        out.append(c)
+    return out
 
   def _include(self, root):
     """Inline <include file=...> elements (recursive)."""
