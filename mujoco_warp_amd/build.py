@@ -6,8 +6,8 @@ import sys
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_PKG)
-SOURCES = [os.path.join(_PKG, "csrc", n) for n in ("mjw_step.hip", "mjw_dense.hip")]
-HEADERS = [os.path.join(_PKG, "csrc", n) for n in ("mjw_math.h", "mjw_common.h")] + [os.path.join(_ROOT, "include", "mjw_amd.h")]
+SOURCES = [os.path.join(_PKG, "csrc", n) for n in ("mjw_step.hip", "mjw_dense.hip", "mjw_sensor.hip")]
+HEADERS = [os.path.join(_PKG, "csrc", n) for n in ("mjw_math.h", "mjw_common.h", "mjw_sensor.h")] + [os.path.join(_ROOT, "include", "mjw_amd.h")]
 OUT = os.path.join(_PKG, "libmjw_amd.so")
 ARCH = os.environ.get("MJW_OFFLOAD_ARCH", "gfx950")
 
@@ -25,7 +25,7 @@ def build(force=False, verbose=False, out=None, defines=()):
   if out is None and not force and not needs_build():
     return OUT
   # one object per translation unit, compiled in parallel, then linked
-  flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(_ROOT, "include")]
+  flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=on", "-fPIC", "-I", os.path.join(_ROOT, "include")]
   flags += [f"-D{x}" for x in defines]
   tag = "_".join(defines).lower()
   objs, procs = [], []

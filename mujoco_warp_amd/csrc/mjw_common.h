@@ -29,7 +29,17 @@ enum : int { DYN_NONE = 0 };
 enum : int {
   DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16, DSBL_SPRING = 32,
   DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512, DSBL_ACTUATION = 2048,
-  DSBL_REFSAFE = 4096, DSBL_EULERDAMP = 1 << 15
+  DSBL_REFSAFE = 4096, DSBL_SENSOR = 8192, DSBL_EULERDAMP = 1 << 15
+};
+enum : int { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
+enum : int { DATATYPE_REAL = 0, DATATYPE_POSITIVE = 1 };
+enum : int { STAGE_POS = 1, STAGE_VEL = 2, STAGE_ACC = 3 };
+enum : int {
+  SENS_ACCELEROMETER = 1, SENS_VELOCIMETER = 2, SENS_GYRO = 3, SENS_FORCE = 4, SENS_TORQUE = 5, SENS_MAGNETOMETER = 6,
+  SENS_JOINTPOS = 9, SENS_JOINTVEL = 10, SENS_ACTUATORPOS = 13, SENS_ACTUATORVEL = 14, SENS_ACTUATORFRC = 15,
+  SENS_JOINTACTFRC = 16, SENS_BALLQUAT = 18, SENS_BALLANGVEL = 19, SENS_FRAMEPOS = 26, SENS_FRAMEQUAT = 27,
+  SENS_FRAMEXAXIS = 28, SENS_FRAMEYAXIS = 29, SENS_FRAMEZAXIS = 30, SENS_FRAMELINVEL = 31, SENS_FRAMEANGVEL = 32,
+  SENS_FRAMELINACC = 33, SENS_FRAMEANGACC = 34, SENS_SUBTREECOM = 35, SENS_CLOCK = 45
 };
 enum : int { ENBL_ENERGY = 2 };
 enum : int { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
@@ -98,5 +108,7 @@ static __device__ unsigned long long g_prof[PH_N];
 // dense (register-resident) factor / solve / euler kernel launcher, mjw_dense.hip
 enum : int { DF_FACTOR = 1, DF_SOLVE = 2, DF_EULER = 4 };
 int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
+// post-solve sensors of every stage + rne_postconstraint, mjw_sensor.hip (no-op without sensors)
+int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
 
 }  // namespace mjw

@@ -653,6 +653,179 @@ __device__ __forceinline__ float plane_box_corner(int k, const float* n, const f
   return cdist;
 }
 
+// a[i] for a runtime i in 0..2 without dynamic register indexing (keeps the arrays in VGPRs)
+__device__ __forceinline__ float sel3(const float* a, int i) { return i == 0 ? a[0] : (i == 1 ? a[1] : a[2]); }
+
+__device__ __forceinline__ void mat_t_vec3(float* r, const float* M, const float* v) {
+  for (int i = 0; i < 3; i++) r[i] = M[i] * v[0] + M[3 + i] * v[1] + M[6 + i] * v[2];
+}
+
+// collision_primitive_core.py:1103-1155
+__device__ float sphere_box(float* pos, float* nrm, const float* spos, float r, const float* bpos, const float* brot,
+                            const float* bsize) {
+  float dif[3] = {spos[0] - bpos[0], spos[1] - bpos[1], spos[2] - bpos[2]}, center[3], clamped[3], tmp[3];
+  mat_t_vec3(center, brot, dif);
+  for (int i = 0; i < 3; i++) { clamped[i] = fmaxf(-bsize[i], fminf(bsize[i], center[i])); tmp[i] = clamped[i] - center[i]; }
+  float dist = sqrtf(dot3(tmp, tmp));
+  float cdir[3] = {tmp[0], tmp[1], tmp[2]};
+  if (dist != 0.0f) for (int i = 0; i < 3; i++) cdir[i] = tmp[i] / dist;
+  float lp[3], dst;
+  if (dist <= MJW_MINVAL) {
+    float closest = 2.0f * (bsize[0] + bsize[1] + bsize[2]);
+    int k = 0;
+    for (int i = 0; i < 6; i++) {
+      float fd = fabsf(((i & 1) ? 1.0f : -1.0f) * bsize[i >> 1] - center[i >> 1]);
+      if (closest > fd) { closest = fd; k = i; }
+    }
+    const float sgn = (k & 1) ? -1.0f : 1.0f;
+    float nearest[3] = {(k >> 1) == 0 ? sgn : 0.0f, (k >> 1) == 1 ? sgn : 0.0f, (k >> 1) == 2 ? sgn : 0.0f};
+    for (int i = 0; i < 3; i++) lp[i] = center[i] + nearest[i] * (r - closest) / 2.0f;
+    matvec3(nrm, brot, nearest);
+    dst = -closest - r;
+  } else {
+    for (int i = 0; i < 3; i++) lp[i] = 0.5f * (clamped[i] + (center[i] + cdir[i] * r));
+    matvec3(nrm, brot, cdir);
+    dst = dist - r;
+  }
+  float w3[3];
+  matvec3(w3, brot, lp);
+  for (int i = 0; i < 3; i++) pos[i] = bpos[i] + w3[i];
+  return dst;
+}
+
+// collision_primitive_core.py:1158-1480 (MuJoCo's capsule-box): up to 2 contacts
+__device__ void capsule_box(Con2& out, const float* cpos, const float* cax, float cr, float chl, const float* bpos, const float* brot,
+                            const float* bsize) {
+  float dif[3] = {cpos[0] - bpos[0], cpos[1] - bpos[1], cpos[2] - bpos[2]}, pos[3], axis[3], ha[3];
+  mat_t_vec3(pos, brot, dif);
+  mat_t_vec3(axis, brot, cax);
+  for (int i = 0; i < 3; i++) ha[i] = axis[i] * chl;
+  const int axisdir = (ha[0] > 0.0f) + 2 * (ha[1] > 0.0f) + 4 * (ha[2] > 0.0f);
+  float bestdist = 1.0e32f, bestsegmentpos = -12.0f;
+  int cltype = -4, clface = -12;
+  // faces closest to one capsule end
+  for (int i = -1; i < 2; i += 2) {
+    float tip[3], bp[3];
+    for (int k = 0; k < 3; k++) { tip[k] = pos[k] + (float)i * ha[k]; bp[k] = tip[k]; }
+    int n_out = 0, ax_out = -1;
+    for (int j = 0; j < 3; j++) {
+      if (bp[j] < -bsize[j]) { n_out++; ax_out = j; bp[j] = -bsize[j]; }
+      else if (bp[j] > bsize[j]) { n_out++; ax_out = j; bp[j] = bsize[j]; }
+    }
+    if (n_out > 1) continue;
+    float dd[3] = {bp[0] - tip[0], bp[1] - tip[1], bp[2] - tip[2]};
+    float dist = dot3(dd, dd);
+    if (dist < bestdist) { bestdist = dist; bestsegmentpos = (float)i; cltype = -2 + i; clface = ax_out; }
+  }
+  // box edges
+  int clcorner = -123, cledge = -123;
+  float bestboxpos = 0.0f;
+  for (int i = 0; i < 8; i++) {
+    for (int j = 0; j < 3; j++) {
+      if (i & (1 << j)) continue;
+      float bpt[3] = {(i & 1) ? bsize[0] : -bsize[0], (i & 2) ? bsize[1] : -bsize[1], (i & 4) ? bsize[2] : -bsize[2]};
+      bpt[j] = 0.0f;
+      float df[3] = {bpt[0] - pos[0], bpt[1] - pos[1], bpt[2] - pos[2]};
+      float u = -bsize[j] * df[j], v = dot3(ha, df);
+      float ma = bsize[j] * bsize[j], mb = -bsize[j] * ha[j], mc = chl * chl;
+      float det = ma * mc - mb * mb;
+      if (fabsf(det) < MJW_MINVAL) continue;
+      float idet = 1.0f / det;
+      float x1 = (mc * u - mb * v) * idet, x2 = (ma * v - mb * u) * idet;
+      int s1 = 1, s2 = 1;
+      if (x1 > 1.0f) { x1 = 1.0f; s1 = 2; x2 = safe_div(v - mb, mc); }
+      else if (x1 < -1.0f) { x1 = -1.0f; s1 = 0; x2 = safe_div(v + mb, mc); }
+      const bool x2_over = x2 > 1.0f;
+      if (x2_over || x2 < -1.0f) {
+        if (x2_over) { x2 = 1.0f; s2 = 2; x1 = safe_div(u - mb, ma); }
+        else { x2 = -1.0f; s2 = 0; x1 = safe_div(u + mb, ma); }
+        if (x1 > 1.0f) { x1 = 1.0f; s1 = 2; }
+        else if (x1 < -1.0f) { x1 = -1.0f; s1 = 0; }
+      }
+      for (int k = 0; k < 3; k++) df[k] -= ha[k] * x2;
+      df[j] += bsize[j] * x1;
+      const int ct = s1 * 3 + s2;
+      float dsq = dot3(df, df);
+      if (dsq < bestdist - MJW_MINVAL) {
+        bestdist = dsq; bestsegmentpos = x2; bestboxpos = x1;
+        clcorner = i + (1 << j) * (ct / 6);
+        cledge = j;
+        cltype = ct;
+      }
+    }
+  }
+  out.n = 0;
+  if (cltype == -4) return;
+  float secondpos = -4.0f;
+  int c1;
+  if (cltype >= 0 && cltype / 3 != 1) {  // closest to a box corner
+    c1 = axisdir ^ clcorner;
+    if (c1 != 0 && c1 != 7) {
+      int mul, ax = 0, ax1 = 0, ax2 = 0;
+      if (c1 == 1 || c1 == 2 || c1 == 4) mul = 1;
+      else { mul = -1; c1 = 7 - c1; }
+      if (c1 == 1) { ax = 0; ax1 = 1; ax2 = 2; }
+      else if (c1 == 2) { ax = 1; ax1 = 2; ax2 = 0; }
+      else if (c1 == 4) { ax = 2; ax1 = 0; ax2 = 1; }
+      if (sel3(axis, ax) * sel3(axis, ax) > 0.5f) {
+        float mm = 2.0f * safe_div(sel3(bsize, ax), fabsf(sel3(ha, ax)));
+        secondpos = fminf(1.0f - (float)mul * bestsegmentpos, mm);
+      } else {
+        float mm = 2.0f * fminf(safe_div(sel3(bsize, ax1), fabsf(sel3(ha, ax1))), safe_div(sel3(bsize, ax2), fabsf(sel3(ha, ax2))));
+        secondpos = -fminf(1.0f + (float)mul * bestsegmentpos, mm);
+      }
+      secondpos *= (float)mul;
+    }
+  } else if (cltype >= 0 && cltype / 3 == 1) {  // on a box edge
+    c1 = axisdir ^ clcorner;
+    c1 &= 7 - (1 << cledge);
+    if (c1 == 1 || c1 == 2 || c1 == 4) {
+      int ax1 = 0, ax2 = 0, ax = cledge, mul;
+      if (cledge == 0) { ax1 = 1; ax2 = 2; }
+      if (cledge == 1) { ax1 = 2; ax2 = 0; }
+      if (cledge == 2) { ax1 = 0; ax2 = 1; }
+      if (fabsf(sel3(axis, ax1)) > fabsf(sel3(axis, ax2))) ax1 = ax2;
+      ax2 = 3 - ax - ax1;
+      if (c1 & (1 << ax2)) { mul = 1; secondpos = 1.0f - bestsegmentpos; }
+      else { mul = -1; secondpos = 1.0f + bestsegmentpos; }
+      float e1 = 2.0f * safe_div(sel3(bsize, ax2), fabsf(sel3(ha, ax2)));
+      secondpos = fminf(e1, secondpos);
+      float e2 = (((axisdir & (1 << ax)) != 0) == ((c1 & (1 << ax2)) != 0)) ? 1.0f - bestboxpos : 1.0f + bestboxpos;
+      e1 = sel3(bsize, ax) * safe_div(e2, fabsf(sel3(ha, ax)));
+      secondpos = fminf(e1, secondpos);
+      secondpos *= (float)mul;
+    }
+  } else if (clface != -1) {  // a capsule end closest to a face
+    const int mul = cltype == -3 ? 1 : -1;
+    secondpos = 2.0f;
+    float tmp1[3] = {pos[0] - ha[0] * mul, pos[1] - ha[1] * mul, pos[2] - ha[2] * mul};
+    for (int i = 0; i < 3; i++) {
+      if (i == clface) continue;
+      float ha_r = safe_div((float)mul, ha[i]);
+      float e1 = (bsize[i] - tmp1[i]) * ha_r;
+      if (0.0f < e1 && e1 < secondpos) secondpos = e1;
+      e1 = (-bsize[i] - tmp1[i]) * ha_r;
+      if (0.0f < e1 && e1 < secondpos) secondpos = e1;
+    }
+    secondpos *= (float)mul;
+  }
+  float l[3], g[3], nrm[3];
+  for (int i = 0; i < 3; i++) l[i] = pos[i] + ha[i] * bestsegmentpos;
+  matvec3(g, brot, l);
+  for (int i = 0; i < 3; i++) g[i] += bpos[i];
+  out.dist[0] = sphere_box(out.pos[0], nrm, g, cr, bpos, brot, bsize);
+  make_frame(out.frame[0], nrm);
+  out.n = 1;
+  if (secondpos > -3.0f) {
+    for (int i = 0; i < 3; i++) l[i] = pos[i] + ha[i] * (secondpos + bestsegmentpos);
+    matvec3(g, brot, l);
+    for (int i = 0; i < 3; i++) g[i] += bpos[i];
+    out.dist[1] = sphere_box(out.pos[1], nrm, g, cr, bpos, brot, bsize);
+    make_frame(out.frame[1], nrm);
+    out.n = 2;
+  }
+}
+
 // collision_driver.py:217-271
 __device__ bool obb_filter(const float* c1, const float* c2, const float* s1, const float* s2, float margin, const float* xp1,
                            const float* xp2, const float* xm1, const float* xm2) {
@@ -774,6 +947,13 @@ __device__ void narrowphase(const mjw_model_t& m, const Lay& L, const float* s, 
     c.n = 1;
   } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
     capsule_capsule(c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], margin);
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_BOX) {  // collision_primitive.py:1047-1114
+    float nrm[3];
+    c.dist[0] = sphere_box(c.pos[0], nrm, p1, s1[0], p2, r2, s2);
+    make_frame(c.frame[0], nrm);
+    c.n = 1;
+  } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {  // collision_primitive.py:1117-1199
+    capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
   }
 }
 
@@ -2144,6 +2324,10 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   if (m->nv > 64 || m->nbody > 4096) { g_err = std::string(name) + ": model too large for the dense world-per-wave path"; return -2; }
   hipStream_t s = (hipStream_t)stream;
   int rc = 0;
+  // sensors (all stages, one kernel after the solver and before the integrator): only the fused
+  // forward / step (the stage entry points, like the reference's fwd_* functions, compute none)
+  const bool full = (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE)) == (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE);
+  const bool acc_sensors = full && m->nsensor > 0 && !(m->opt_disableflags & DSBL_SENSOR);
   if (dense_ok(m, d)) {
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel
     if (g_ev[0]) (void)hipEventRecord(g_ev[0], s);
@@ -2159,8 +2343,21 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     if (rc) return rc;
     if (g_ev[1]) (void)hipEventRecord(g_ev[1], s);
     int f = ((stages & ST_ACC) ? DF_FACTOR : 0) | ((stages & ST_SOLVE) ? DF_SOLVE : 0) | ((stages & ST_EULER) ? DF_EULER : 0);
-    if (f != 0) rc = set_err((hipError_t)dense_launch(f, m, d, s), name);
+    if (acc_sensors) {
+      // sensor_pos / _vel / _acc sit before the integrator (forward.py:981-998, step :1003-1018)
+      rc = set_err((hipError_t)dense_launch(f & ~DF_EULER, m, d, s), name);
+      if (!rc) rc = set_err((hipError_t)sensor_launch(m, d, s), name);
+      if (!rc && (f & DF_EULER)) rc = set_err((hipError_t)dense_launch(DF_EULER, m, d, s), name);
+    } else if (f != 0) {
+      rc = set_err((hipError_t)dense_launch(f, m, d, s), name);
+    }
     if (g_ev[2]) (void)hipEventRecord(g_ev[2], s);
+    return rc;
+  }
+  if (acc_sensors) {
+    rc = launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE>(m, d, s, name);
+    if (!rc) rc = set_err((hipError_t)sensor_launch(m, d, s), name);
+    if (!rc && (stages & ST_EULER)) rc = launch_generic<ST_EULER>(m, d, s, name);
     return rc;
   }
   switch (stages) {

@@ -88,7 +88,7 @@ def _model_attr(name):
 
 _SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.BOX, types.GeomType.MESH}
 # narrowphase pairs built on the device (type-sorted): collision_primitive.py:1280-1300 subset
-_SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3)}
+_SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6)}
 
 
 def put_model(mjm, device=None) -> types.Model:
@@ -108,8 +108,11 @@ def put_model(mjm, device=None) -> types.Model:
     raise NotImplementedError("noslip solver not implemented.")
   if is_sparse(mjm):
     raise NotImplementedError("sparse Jacobian / nv > 32 models are not supported by this build yet.")
-  if getattr(mjm, "ntendon", 0) or getattr(mjm, "nsensor", 0) or getattr(mjm, "nflex", 0):
-    raise NotImplementedError("tendons / sensors / flex are not supported by this build yet.")
+  if getattr(mjm, "ntendon", 0) or getattr(mjm, "nflex", 0):
+    raise NotImplementedError("tendons / flex are not supported by this build yet.")
+  for st in np.unique(getattr(mjm, "sensor_type", np.zeros(0, dtype=np.int32))):
+    if int(st) not in types.SUPPORTED_SENSORS:
+      raise NotImplementedError(f"sensor type {int(st)} is not supported by this build yet.")
   if getattr(mjm, "neq", 0) and np.any(mjm.eq_type != types.EqType.JOINT):
     raise NotImplementedError("only joint equality constraints are supported by this build yet.")
   pairs_chk, _ = nxn_geom_pairs(mjm)
@@ -148,8 +151,11 @@ def put_model(mjm, device=None) -> types.Model:
     setattr(m, n, int(getattr(mjm, n)))
   m.ntendon = 0
   m.neq = int(getattr(mjm, "neq", 0))
-  m.nsensor = 0
-  m.nsensordata = 0
+  m.nsensor = int(getattr(mjm, "nsensor", 0))
+  m.nsensordata = int(getattr(mjm, "nsensordata", 0))
+  stypes = np.asarray(getattr(mjm, "sensor_type", np.zeros(0, dtype=np.int32)))
+  m.sensor_rne_postconstraint = int(np.isin(stypes, list(types.RNE_POSTCONSTRAINT_SENSORS)).any())  # io.py:542-551
+  m.nsensor_acc = int((np.asarray(getattr(mjm, "sensor_needstage", np.zeros(0))) == types.Stage.ACC).sum())
   m.nflex = 0
   m.is_sparse = False
   njmax_pad_unused, m.nv_pad = _padded_sizes(nv, 0, False)
@@ -285,7 +291,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     actuator_length=(nu,), actuator_moment=(m.nJmom,), actuator_velocity=(nu,), actuator_force=(nu,),
     cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,),
     qfrc_passive=(nv,), qfrc_actuator=(nv,), qfrc_smooth=(nv,), qacc_smooth=(nv,), qfrc_constraint=(nv,),
-    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6),
+    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,),
     efc_J=(njmax_pad, np_), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
     efc_aref=(njmax,), efc_frictionloss=(njmax,), efc_force=(njmax,), efc_Ma=(nv,),
   )
@@ -356,7 +362,6 @@ def _alloc_data(m, nworld, nconmax, njmax, naconmax, device):
   d.contact.efc_address.fill_(-1)
   d.nacon = torch.zeros(1, dtype=torch.int32, device=device)
   d.ncollision = torch.zeros(1, dtype=torch.int32, device=device)
-  d.sensordata = torch.zeros((nworld, 0), dtype=torch.float32, device=device)
   d.efc.J_rownnz = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
   d.efc.J_rowadr = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
   d.efc.J_colind = torch.zeros((nworld, 0, 0), dtype=torch.int32, device=device)
@@ -475,7 +480,7 @@ def get_data_into(result, mjm, d: types.Data, world_id: int = 0):
                "xaxis", "geom_xpos", "site_xpos", "cam_xpos", "light_xpos", "light_xdir", "subtree_com", "cdof", "cinert", "crb",
                "actuator_length", "actuator_velocity", "actuator_force", "cvel", "cdof_dot", "qfrc_bias", "qfrc_spring", "qfrc_damper",
                "qfrc_gravcomp", "qfrc_passive", "qfrc_actuator", "qfrc_smooth", "qacc_smooth", "qfrc_constraint", "cacc", "cfrc_int",
-               "cfrc_ext", "xfrc_applied", "mocap_pos", "mocap_quat", "energy"):
+               "cfrc_ext", "xfrc_applied", "mocap_pos", "mocap_quat", "energy", "sensordata"):
     if hasattr(result, name) or isinstance(result, object):
       val = getattr(d, name)[world_id].detach().cpu().numpy().astype(np.float64)
       try:

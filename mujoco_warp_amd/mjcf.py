@@ -33,6 +33,7 @@ from .types import (
   BiasType,
   CamLightType,
   ConeType,
+  DataType,
   DisableBit,
   DynType,
   EnableBit,
@@ -42,7 +43,10 @@ from .types import (
   IntegratorType,
   JacobianType,
   JointType,
+  ObjType,
+  SensorType,
   SolverType,
+  Stage,
   TrnType,
 )
 
@@ -828,9 +832,8 @@ class _Compiler:
     self._build_contact(root)
     self._build_keys(root)
     self._build_equality(root)
+    self._build_sensors(root)
     m.ntendon = 0
-    m.nsensor = 0
-    m.nsensordata = 0
     m.nflex = 0
     m.nhfield = 0
     m.nmesh = 0
@@ -1228,6 +1231,78 @@ class _Compiler:
     m.eq_solref = np.array([r["solref"] for r in rows]).reshape(m.neq, 2)
     m.eq_solimp = np.array([r["solimp"] for r in rows]).reshape(m.neq, 5)
     m.eq_active0 = np.array([r["active"] for r in rows], dtype=np.uint8)
+
+  # <sensor> element -> (type, dim, datatype, needstage, object attribute, objtype)
+  _SENSORS = {
+    "accelerometer": (SensorType.ACCELEROMETER, 3, DataType.REAL, Stage.ACC, "site", ObjType.SITE),
+    "velocimeter": (SensorType.VELOCIMETER, 3, DataType.REAL, Stage.VEL, "site", ObjType.SITE),
+    "gyro": (SensorType.GYRO, 3, DataType.REAL, Stage.VEL, "site", ObjType.SITE),
+    "force": (SensorType.FORCE, 3, DataType.REAL, Stage.ACC, "site", ObjType.SITE),
+    "torque": (SensorType.TORQUE, 3, DataType.REAL, Stage.ACC, "site", ObjType.SITE),
+    "magnetometer": (SensorType.MAGNETOMETER, 3, DataType.REAL, Stage.POS, "site", ObjType.SITE),
+    "jointpos": (SensorType.JOINTPOS, 1, DataType.REAL, Stage.POS, "joint", ObjType.JOINT),
+    "jointvel": (SensorType.JOINTVEL, 1, DataType.REAL, Stage.VEL, "joint", ObjType.JOINT),
+    "actuatorpos": (SensorType.ACTUATORPOS, 1, DataType.REAL, Stage.POS, "actuator", ObjType.ACTUATOR),
+    "actuatorvel": (SensorType.ACTUATORVEL, 1, DataType.REAL, Stage.VEL, "actuator", ObjType.ACTUATOR),
+    "actuatorfrc": (SensorType.ACTUATORFRC, 1, DataType.REAL, Stage.ACC, "actuator", ObjType.ACTUATOR),
+    "jointactuatorfrc": (SensorType.JOINTACTFRC, 1, DataType.REAL, Stage.ACC, "joint", ObjType.JOINT),
+    "ballquat": (SensorType.BALLQUAT, 4, DataType.QUATERNION, Stage.POS, "joint", ObjType.JOINT),
+    "ballangvel": (SensorType.BALLANGVEL, 3, DataType.REAL, Stage.VEL, "joint", ObjType.JOINT),
+    "framepos": (SensorType.FRAMEPOS, 3, DataType.REAL, Stage.POS, None, None),
+    "framequat": (SensorType.FRAMEQUAT, 4, DataType.QUATERNION, Stage.POS, None, None),
+    "framexaxis": (SensorType.FRAMEXAXIS, 3, DataType.AXIS, Stage.POS, None, None),
+    "frameyaxis": (SensorType.FRAMEYAXIS, 3, DataType.AXIS, Stage.POS, None, None),
+    "framezaxis": (SensorType.FRAMEZAXIS, 3, DataType.AXIS, Stage.POS, None, None),
+    "framelinvel": (SensorType.FRAMELINVEL, 3, DataType.REAL, Stage.VEL, None, None),
+    "frameangvel": (SensorType.FRAMEANGVEL, 3, DataType.REAL, Stage.VEL, None, None),
+    "framelinacc": (SensorType.FRAMELINACC, 3, DataType.REAL, Stage.ACC, None, None),
+    "frameangacc": (SensorType.FRAMEANGACC, 3, DataType.REAL, Stage.ACC, None, None),
+    "subtreecom": (SensorType.SUBTREECOM, 3, DataType.REAL, Stage.POS, "body", ObjType.BODY),
+    "clock": (SensorType.CLOCK, 1, DataType.REAL, Stage.POS, None, ObjType.UNKNOWN),
+  }
+  _OBJTYPES = {"body": ObjType.BODY, "xbody": ObjType.XBODY, "geom": ObjType.GEOM, "site": ObjType.SITE, "camera": ObjType.CAMERA}
+
+  def _build_sensors(self, root):
+    """<sensor>: the sensor table (mjModel sensor_* fields; sensor.py reads them)."""
+    m = self.m
+    names = {
+      ObjType.BODY: {n: i for i, n in enumerate(m.body_names)},
+      ObjType.XBODY: {n: i for i, n in enumerate(m.body_names)},
+      ObjType.GEOM: {n: i for i, n in enumerate(m.geom_names) if n},
+      ObjType.SITE: {n: i for i, n in enumerate(m.site_names) if n},
+      ObjType.CAMERA: {n: i for i, n in enumerate(m.cam_names) if n},
+      ObjType.JOINT: {n: i for i, n in enumerate(m.jnt_names) if n},
+      ObjType.ACTUATOR: {n: i for i, n in enumerate(m.actuator_names) if n},
+    }
+    rows = []
+    adr = 0
+    for sec in root.findall("sensor"):
+      for el in sec:
+        if el.tag not in self._SENSORS:
+          raise NotImplementedError(f"sensor <{el.tag}> is not supported by this build yet")
+        a = dict(self.defaults[el.get("class", "main")].attrs.get("sensor", {}))
+        a.update(el.attrib)
+        stype, dim, dtype, stage, key, otype = self._SENSORS[el.tag]
+        objid, reftype, refid = -1, ObjType.UNKNOWN, -1
+        if key is not None:
+          objid = names[otype][a[key]]
+        elif otype is None:  # frame sensors: objtype / objname (+ optional reftype / refname)
+          otype = self._OBJTYPES[a["objtype"]]
+          objid = names[otype][a["objname"]]
+          if "refname" in a:
+            reftype = self._OBJTYPES[a["reftype"]]
+            refid = names[reftype][a["refname"]]
+        rows.append(dict(name=a.get("name", ""), type=int(stype), datatype=int(dtype), needstage=int(stage), objtype=int(otype),
+                         objid=objid, reftype=int(reftype), refid=refid, dim=dim, adr=adr, cutoff=float(a.get("cutoff", 0.0)),
+                         noise=float(a.get("noise", 0.0))))
+        adr += dim
+    m.nsensor = len(rows)
+    m.nsensordata = adr
+    m.sensor_names = [r["name"] for r in rows]
+    for f in ("type", "datatype", "needstage", "objtype", "objid", "reftype", "refid", "dim", "adr"):
+      setattr(m, "sensor_" + f, np.array([r[f] for r in rows], dtype=np.int32))
+    m.sensor_cutoff = np.array([r["cutoff"] for r in rows], dtype=np.float64)
+    m.sensor_noise = np.array([r["noise"] for r in rows], dtype=np.float64)
 
   def _build_contact(self, root):
     m = self.m

@@ -185,6 +185,85 @@ class ObjType(enum.IntEnum):
   GEOM = 5
   SITE = 6
   CAMERA = 7
+  LIGHT = 8
+  ACTUATOR = 19
+
+
+class SensorType(enum.IntEnum):
+  """mjtSensor (types.py:466-524 takes the values from mujoco.mjtSensor; restated from MuJoCo's
+  mjmodel.h since `mujoco` is not importable here)."""
+
+  TOUCH = 0
+  ACCELEROMETER = 1
+  VELOCIMETER = 2
+  GYRO = 3
+  FORCE = 4
+  TORQUE = 5
+  MAGNETOMETER = 6
+  RANGEFINDER = 7
+  CAMPROJECTION = 8
+  JOINTPOS = 9
+  JOINTVEL = 10
+  TENDONPOS = 11
+  TENDONVEL = 12
+  ACTUATORPOS = 13
+  ACTUATORVEL = 14
+  ACTUATORFRC = 15
+  JOINTACTFRC = 16
+  TENDONACTFRC = 17
+  BALLQUAT = 18
+  BALLANGVEL = 19
+  JOINTLIMITPOS = 20
+  JOINTLIMITVEL = 21
+  JOINTLIMITFRC = 22
+  TENDONLIMITPOS = 23
+  TENDONLIMITVEL = 24
+  TENDONLIMITFRC = 25
+  FRAMEPOS = 26
+  FRAMEQUAT = 27
+  FRAMEXAXIS = 28
+  FRAMEYAXIS = 29
+  FRAMEZAXIS = 30
+  FRAMELINVEL = 31
+  FRAMEANGVEL = 32
+  FRAMELINACC = 33
+  FRAMEANGACC = 34
+  SUBTREECOM = 35
+  SUBTREELINVEL = 36
+  SUBTREEANGMOM = 37
+  CLOCK = 45  # after INSIDESITE, GEOMDIST, GEOMNORMAL, GEOMFROMTO, CONTACT, E_POTENTIAL, E_KINETIC
+
+
+class DataType(enum.IntEnum):
+  """mjtDataType (types.py:158-166)."""
+
+  REAL = 0
+  POSITIVE = 1
+  AXIS = 2
+  QUATERNION = 3
+
+
+class Stage(enum.IntEnum):
+  """mjtStage (types.py:530-540)."""
+
+  NONE = 0
+  POS = 1
+  VEL = 2
+  ACC = 3
+
+
+# sensors built on the device path (sensor.py:459-706, 1251-1373, 1697-1997 subset)
+SUPPORTED_SENSORS = {
+  SensorType.ACCELEROMETER, SensorType.VELOCIMETER, SensorType.GYRO, SensorType.FORCE, SensorType.TORQUE,
+  SensorType.MAGNETOMETER, SensorType.JOINTPOS, SensorType.JOINTVEL, SensorType.ACTUATORPOS, SensorType.ACTUATORVEL,
+  SensorType.ACTUATORFRC, SensorType.JOINTACTFRC, SensorType.BALLQUAT, SensorType.BALLANGVEL, SensorType.FRAMEPOS,
+  SensorType.FRAMEQUAT, SensorType.FRAMEXAXIS, SensorType.FRAMEYAXIS, SensorType.FRAMEZAXIS, SensorType.FRAMELINVEL,
+  SensorType.FRAMEANGVEL, SensorType.FRAMELINACC, SensorType.FRAMEANGACC, SensorType.SUBTREECOM, SensorType.CLOCK,
+}
+# sensors that need rne_postconstraint (io.py:542-551)
+RNE_POSTCONSTRAINT_SENSORS = {
+  SensorType.ACCELEROMETER, SensorType.FORCE, SensorType.TORQUE, SensorType.FRAMELINACC, SensorType.FRAMEANGACC,
+}
 
 
 class EqType(enum.IntEnum):

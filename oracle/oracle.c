@@ -25,7 +25,7 @@ enum { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
 enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6 };
 enum { DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16,
        DSBL_SPRING = 32, DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512,
-       DSBL_FILTERPARENT = 1024, DSBL_ACTUATION = 2048, DSBL_REFSAFE = 4096, DSBL_EULERDAMP = 1 << 15 };
+       DSBL_FILTERPARENT = 1024, DSBL_ACTUATION = 2048, DSBL_REFSAFE = 4096, DSBL_SENSOR = 8192, DSBL_EULERDAMP = 1 << 15 };
 enum { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
 enum { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3 };
 enum { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
@@ -270,7 +270,8 @@ void orc_ctrl_noise(const orc_model* m, real* ctrl, const real* center, int ncen
 static void world_view(const orc_model* m, const orc_data* b, int w, orc_data* o) {
   int nq = m->nq, nv = m->nv, nu = m->nu, na = m->na, nbody = m->nbody, njnt = m->njnt;
   int ngeom = m->ngeom, nsite = m->nsite, ncam = m->ncam, nlight = m->nlight, nmocap = m->nmocap, neq = m->neq;
-  int njmax = b->njmax, nconmax = b->nconmax;
+  int njmax = b->njmax, nconmax = b->nconmax, nsensordata = m->nsensordata;
+  (void)nsensordata;
   (void)nq; (void)nv; (void)nu; (void)na; (void)nbody; (void)njnt; (void)ngeom; (void)nsite; (void)ncam;
   (void)nlight; (void)nmocap; (void)njmax; (void)nconmax; (void)neq;
   o->njmax = njmax;
@@ -995,6 +996,184 @@ static void plane_box_corner(int k, const real* n, const real* ppos, const real*
   for (int i = 0; i < 3; i++) pos[i] = corner[i] + bpos[i] - 0.5 * n[i] * cdist;
 }
 
+
+/* collision_primitive_core.py:1103-1155 sphere_box */
+static real sphere_box(real* pos, real* nrm, const real* spos, real r, const real* bpos, const real* brot, const real* bsize) {
+  real dif[3] = {spos[0] - bpos[0], spos[1] - bpos[1], spos[2] - bpos[2]}, center[3], clamped[3], cdir[3], tmp[3];
+  for (int i = 0; i < 3; i++) center[i] = brot[i] * dif[0] + brot[3 + i] * dif[1] + brot[6 + i] * dif[2];
+  for (int i = 0; i < 3; i++) { clamped[i] = maxr(-bsize[i], minr(bsize[i], center[i])); tmp[i] = clamped[i] - center[i]; }
+  real dist = normalize_with_norm(cdir, tmp);
+  real lp[3], dst;
+  if (dist <= MINVAL) {
+    real closest = 2 * (bsize[0] + bsize[1] + bsize[2]);
+    int k = 0;
+    for (int i = 0; i < 6; i++) {
+      real fd = fabs((i % 2 ? 1.0 : -1.0) * bsize[i / 2] - center[i / 2]);
+      if (closest > fd) { closest = fd; k = i; }
+    }
+    real nearest[3] = {0, 0, 0};
+    nearest[k / 2] = (k % 2) ? -1 : 1;
+    for (int i = 0; i < 3; i++) lp[i] = center[i] + nearest[i] * (r - closest) / 2;
+    matvec3(nrm, brot, nearest);
+    dst = -closest - r;
+  } else {
+    for (int i = 0; i < 3; i++) lp[i] = 0.5 * (clamped[i] + center[i] + cdir[i] * r);
+    matvec3(nrm, brot, cdir);
+    dst = dist - r;
+  }
+  real w[3];
+  matvec3(w, brot, lp);
+  for (int i = 0; i < 3; i++) pos[i] = bpos[i] + w[i];
+  return dst;
+}
+
+/* collision_primitive_core.py:1158-1480 capsule_box (MuJoCo's mjc_CapsuleBox): up to 2 contacts */
+static void capsule_box(contacts2* out, const real* cpos, const real* cax, real cr, real chl, const real* bpos, const real* brot,
+                        const real* bsize) {
+  real dif[3] = {cpos[0] - bpos[0], cpos[1] - bpos[1], cpos[2] - bpos[2]}, pos[3], axis[3], ha[3];
+  for (int i = 0; i < 3; i++) {
+    pos[i] = brot[i] * dif[0] + brot[3 + i] * dif[1] + brot[6 + i] * dif[2];
+    axis[i] = brot[i] * cax[0] + brot[3 + i] * cax[1] + brot[6 + i] * cax[2];
+  }
+  for (int i = 0; i < 3; i++) ha[i] = axis[i] * chl;
+  int axisdir = (ha[0] > 0) + 2 * (ha[1] > 0) + 4 * (ha[2] > 0);
+  real bestdist = 1e32, bestsegmentpos = -12;
+  int cltype = -4, clface = -12;
+  for (int i = -1; i < 2; i += 2) {
+    real tip[3], bp[3];
+    for (int k = 0; k < 3; k++) { tip[k] = pos[k] + i * ha[k]; bp[k] = tip[k]; }
+    int n_out = 0, ax_out = -1;
+    for (int j = 0; j < 3; j++) {
+      if (bp[j] < -bsize[j]) { n_out++; ax_out = j; bp[j] = -bsize[j]; }
+      else if (bp[j] > bsize[j]) { n_out++; ax_out = j; bp[j] = bsize[j]; }
+    }
+    if (n_out > 1) continue;
+    real dd[3] = {bp[0] - tip[0], bp[1] - tip[1], bp[2] - tip[2]};
+    real dist = dot3(dd, dd);
+    if (dist < bestdist) { bestdist = dist; bestsegmentpos = i; cltype = -2 + i; clface = ax_out; }
+  }
+  int clcorner = -123, cledge = -123;
+  real bestboxpos = 0;
+  for (int i = 0; i < 8; i++) {
+    for (int j = 0; j < 3; j++) {
+      if (i & (1 << j)) continue;
+      real bpt[3] = {(i & 1) ? bsize[0] : -bsize[0], (i & 2) ? bsize[1] : -bsize[1], (i & 4) ? bsize[2] : -bsize[2]};
+      bpt[j] = 0;
+      real df[3] = {bpt[0] - pos[0], bpt[1] - pos[1], bpt[2] - pos[2]};
+      real u = -bsize[j] * df[j], v = dot3(ha, df);
+      real ma = bsize[j] * bsize[j], mb = -bsize[j] * ha[j], mc = chl * chl;
+      real det = ma * mc - mb * mb;
+      if (fabs(det) < MINVAL) continue;
+      real idet = 1 / det;
+      real x1 = (mc * u - mb * v) * idet, x2 = (ma * v - mb * u) * idet;
+      int s1 = 1, s2 = 1;
+      if (x1 > 1) { x1 = 1; s1 = 2; x2 = safe_div(v - mb, mc); }
+      else if (x1 < -1) { x1 = -1; s1 = 0; x2 = safe_div(v + mb, mc); }
+      int x2_over = x2 > 1;
+      if (x2_over || x2 < -1) {
+        if (x2_over) { x2 = 1; s2 = 2; x1 = safe_div(u - mb, ma); }
+        else { x2 = -1; s2 = 0; x1 = safe_div(u + mb, ma); }
+        if (x1 > 1) { x1 = 1; s1 = 2; }
+        else if (x1 < -1) { x1 = -1; s1 = 0; }
+      }
+      for (int k = 0; k < 3; k++) df[k] -= ha[k] * x2;
+      df[j] += bsize[j] * x1;
+      int ct = s1 * 3 + s2;
+      real dsq = dot3(df, df);
+      if (dsq < bestdist - MINVAL) {
+        bestdist = dsq; bestsegmentpos = x2; bestboxpos = x1;
+        int c2 = ct / 6;
+        clcorner = i + (1 << j) * c2;
+        cledge = j;
+        cltype = ct;
+      }
+    }
+  }
+  real secondpos = -4;
+  real uu = ha[0] * bsize[1], vv = ha[1] * bsize[0];
+  int w_neg = ha[0] * pos[1] - ha[1] * pos[0] < 0;
+  real best = -1;
+  int c1 = 0;
+  real ee1 = uu - vv, ee2 = uu + vv;
+  if (fabs(ee1) > best) { best = fabs(ee1); c1 = ((ee1 < 0) == w_neg) ? 0 : 3; }
+  if (fabs(ee2) > best) { best = fabs(ee2); c1 = ((ee2 > 0) == w_neg) ? 1 : 2; }
+  out->n = 0;
+  if (cltype == -4) return;
+  if (cltype >= 0 && cltype / 3 != 1) {
+    c1 = axisdir ^ clcorner;
+    if (c1 != 0 && c1 != 7) {
+      int mul, ax = 0, ax1 = 0, ax2 = 0;
+      if (c1 == 1 || c1 == 2 || c1 == 4) mul = 1;
+      else { mul = -1; c1 = 7 - c1; }
+      if (c1 == 1) { ax = 0; ax1 = 1; ax2 = 2; }
+      else if (c1 == 2) { ax = 1; ax1 = 2; ax2 = 0; }
+      else if (c1 == 4) { ax = 2; ax1 = 0; ax2 = 1; }
+      if (axis[ax] * axis[ax] > 0.5) {
+        real mm = 2 * safe_div(bsize[ax], fabs(ha[ax]));
+        secondpos = minr(1 - mul * bestsegmentpos, mm);
+      } else {
+        real mm = 2 * minr(safe_div(bsize[ax1], fabs(ha[ax1])), safe_div(bsize[ax2], fabs(ha[ax2])));
+        secondpos = -minr(1 + mul * bestsegmentpos, mm);
+      }
+      secondpos *= mul;
+    }
+  } else if (cltype >= 0 && cltype / 3 == 1) {
+    c1 = axisdir ^ clcorner;
+    c1 &= 7 - (1 << cledge);
+    if (c1 == 1 || c1 == 2 || c1 == 4) {
+      int ax1 = 0, ax2 = 0, ax = cledge, mul;
+      if (cledge == 0) { ax1 = 1; ax2 = 2; }
+      if (cledge == 1) { ax1 = 2; ax2 = 0; }
+      if (cledge == 2) { ax1 = 0; ax2 = 1; }
+      if (fabs(axis[ax1]) > fabs(axis[ax2])) ax1 = ax2;
+      ax2 = 3 - ax - ax1;
+      if (c1 & (1 << ax2)) { mul = 1; secondpos = 1 - bestsegmentpos; }
+      else { mul = -1; secondpos = 1 + bestsegmentpos; }
+      real e1 = 2 * safe_div(bsize[ax2], fabs(ha[ax2]));
+      secondpos = minr(e1, secondpos);
+      real e2;
+      if (((axisdir & (1 << ax)) != 0) == ((c1 & (1 << ax2)) != 0)) e2 = 1 - bestboxpos;
+      else e2 = 1 + bestboxpos;
+      e1 = bsize[ax] * safe_div(e2, fabs(ha[ax]));
+      secondpos = minr(e1, secondpos);
+      secondpos *= mul;
+    }
+  } else if (cltype < 0) {
+    if (clface != -1) {
+      int mul = cltype == -3 ? 1 : -1;
+      secondpos = 2;
+      real tmp1[3] = {pos[0] - ha[0] * mul, pos[1] - ha[1] * mul, pos[2] - ha[2] * mul};
+      for (int i = 0; i < 3; i++) {
+        if (i != clface) {
+          real ha_r = safe_div((real)mul, ha[i]);
+          real e1 = (bsize[i] - tmp1[i]) * ha_r;
+          if (0 < e1 && e1 < secondpos) secondpos = e1;
+          e1 = (-bsize[i] - tmp1[i]) * ha_r;
+          if (0 < e1 && e1 < secondpos) secondpos = e1;
+        }
+      }
+      secondpos *= mul;
+    }
+  }
+  real l1[3], g1[3];
+  for (int i = 0; i < 3; i++) l1[i] = pos[i] + ha[i] * bestsegmentpos;
+  matvec3(g1, brot, l1);
+  for (int i = 0; i < 3; i++) g1[i] += bpos[i];
+  real nrm[3];
+  out->dist[0] = sphere_box(out->pos[0], nrm, g1, cr, bpos, brot, bsize);
+  make_frame(out->frame[0], nrm);
+  out->n = 1;
+  if (secondpos > -3) {
+    real l2[3], g2[3];
+    for (int i = 0; i < 3; i++) l2[i] = pos[i] + ha[i] * (secondpos + bestsegmentpos);
+    matvec3(g2, brot, l2);
+    for (int i = 0; i < 3; i++) g2[i] += bpos[i];
+    out->dist[1] = sphere_box(out->pos[1], nrm, g2, cr, bpos, brot, bsize);
+    make_frame(out->frame[1], nrm);
+    out->n = 2;
+  }
+}
+
 static void collision(const orc_model* m, orc_data* d) {
   *d->ncon = 0;
   *d->ncollision = 0;
@@ -1033,6 +1212,13 @@ static void collision(const orc_model* m, orc_data* d) {
       c.n = 1;
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
       capsule_capsule(&c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], margin);
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_BOX) { /* collision_primitive.py:1047-1114 */
+      real nrm[3];
+      c.dist[0] = sphere_box(c.pos[0], nrm, p1, s1[0], p2, r2, s2);
+      make_frame(c.frame[0], nrm);
+      c.n = 1;
+    } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) { /* collision_primitive.py:1117-1199 */
+      capsule_box(&c, p1, n1, s1[0], s1[1], p2, r2, s2);
     } else if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {
       c.n = 8; /* all 8 corners are candidates (collision_primitive.py:737-790) */
     } else {
@@ -1704,13 +1890,365 @@ static void implicit(const orc_model* m, orc_data* d) {
   free(A);
 }
 
+
+/* =============================================================================================
+ * sensor.py (position / velocity / acceleration sensors) + smooth.py rne_postconstraint
+ * ============================================================================================= */
+enum { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
+enum { DATATYPE_REAL = 0, DATATYPE_POSITIVE = 1 };
+enum { STAGE_POS = 1, STAGE_VEL = 2, STAGE_ACC = 3 };
+enum {
+  SENS_ACCELEROMETER = 1, SENS_VELOCIMETER = 2, SENS_GYRO = 3, SENS_FORCE = 4, SENS_TORQUE = 5, SENS_MAGNETOMETER = 6,
+  SENS_JOINTPOS = 9, SENS_JOINTVEL = 10, SENS_ACTUATORPOS = 13, SENS_ACTUATORVEL = 14, SENS_ACTUATORFRC = 15,
+  SENS_JOINTACTFRC = 16, SENS_BALLQUAT = 18, SENS_BALLANGVEL = 19, SENS_FRAMEPOS = 26, SENS_FRAMEQUAT = 27,
+  SENS_FRAMEXAXIS = 28, SENS_FRAMEYAXIS = 29, SENS_FRAMEZAXIS = 30, SENS_FRAMELINVEL = 31, SENS_FRAMEANGVEL = 32,
+  SENS_FRAMELINACC = 33, SENS_FRAMEANGACC = 34, SENS_SUBTREECOM = 35, SENS_CLOCK = 45
+};
+
+/* sensor.py:54-110 _write_scalar / _write_vector: cutoff clamps REAL, caps POSITIVE */
+static void sensor_write(const orc_model* m, orc_data* d, int s, const real* v, int dim) {
+  real cutoff = m->sensor_cutoff[s];
+  int dt = m->sensor_datatype[s];
+  real* out = d->sensordata + m->sensor_adr[s];
+  for (int i = 0; i < dim; i++) {
+    real x = v[i];
+    if (cutoff > 0 && dt == DATATYPE_REAL) x = clampr(x, -cutoff, cutoff);
+    else if (cutoff > 0 && dt == DATATYPE_POSITIVE) x = minr(x, cutoff);
+    out[i] = x;
+  }
+}
+
+/* object frame position / rotation / body (sensor.py:282-340, :1011-1050) */
+static void obj_frame(const orc_model* m, const orc_data* d, int type, int id, const real** pos, const real** mat, int* body) {
+  static const real zero[3] = {0, 0, 0};
+  static const real eye[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  *pos = zero; *mat = eye; *body = 0;
+  if (type == OBJ_BODY) { *pos = d->xipos + 3 * id; *mat = d->ximat + 9 * id; *body = id; }
+  else if (type == OBJ_XBODY) { *pos = d->xpos + 3 * id; *mat = d->xmat + 9 * id; *body = id; }
+  else if (type == OBJ_GEOM) { *pos = d->geom_xpos + 3 * id; *mat = d->geom_xmat + 9 * id; *body = m->geom_bodyid[id]; }
+  else if (type == OBJ_SITE) { *pos = d->site_xpos + 3 * id; *mat = d->site_xmat + 9 * id; *body = m->site_bodyid[id]; }
+  else if (type == OBJ_CAMERA) { *pos = d->cam_xpos + 3 * id; *mat = d->cam_xmat + 9 * id; *body = m->cam_bodyid[id]; }
+}
+
+/* r = M^T v */
+static void mat_t_vec(real* r, const real* M, const real* v) {
+  for (int i = 0; i < 3; i++) r[i] = M[i] * v[0] + M[3 + i] * v[1] + M[6 + i] * v[2];
+}
+
+/* sensor.py:394-446 _frame_quat */
+static void frame_quat(const orc_model* m, const orc_data* d, int type, int id, real* q) {
+  q[0] = 1; q[1] = q[2] = q[3] = 0;
+  if (type == OBJ_BODY) mul_quat(q, d->xquat + 4 * id, m->body_iquat + 4 * id);
+  else if (type == OBJ_XBODY) memcpy(q, d->xquat + 4 * id, 4 * sizeof(real));
+  else if (type == OBJ_GEOM) mul_quat(q, d->xquat + 4 * m->geom_bodyid[id], m->geom_quat + 4 * id);
+  else if (type == OBJ_SITE) mul_quat(q, d->xquat + 4 * m->site_bodyid[id], m->site_quat + 4 * id);
+  else if (type == OBJ_CAMERA) mul_quat(q, d->xquat + 4 * m->cam_bodyid[id], m->cam_quat + 4 * id);
+}
+
+/* sensor.py:459-706 (_sensor_pos, supported types) */
+static void sensor_pos(const orc_model* m, orc_data* d) {
+  for (int s = 0; s < m->nsensor; s++) {
+    if (m->sensor_needstage[s] != STAGE_POS) continue;
+    int t = m->sensor_type[s], id = m->sensor_objid[s], ot = m->sensor_objtype[s];
+    int rid = m->sensor_refid[s], rt = m->sensor_reftype[s];
+    real v[4] = {0, 0, 0, 0};
+    if (t == SENS_MAGNETOMETER) {
+      mat_t_vec(v, d->site_xmat + 9 * id, m->opt_magnetic);
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_JOINTPOS) {
+      v[0] = d->qpos[m->jnt_qposadr[id]];
+      sensor_write(m, d, s, v, 1);
+    } else if (t == SENS_ACTUATORPOS) {
+      v[0] = d->actuator_length[id];
+      sensor_write(m, d, s, v, 1);
+    } else if (t == SENS_BALLQUAT) {
+      memcpy(v, d->qpos + m->jnt_qposadr[id], 4 * sizeof(real));
+      normalize4(v);
+      sensor_write(m, d, s, v, 4);
+    } else if (t == SENS_FRAMEPOS) {
+      const real *p, *R; int b;
+      obj_frame(m, d, ot, id, &p, &R, &b);
+      if (rid == -1) { memcpy(v, p, 3 * sizeof(real)); }
+      else {
+        /* reference branch order (sensor.py:323-336): the XBODY test reads objtype */
+        const real *pr, *Rr; int br;
+        if (rt == OBJ_BODY) obj_frame(m, d, OBJ_BODY, rid, &pr, &Rr, &br);
+        else if (ot == OBJ_XBODY) obj_frame(m, d, OBJ_XBODY, rid, &pr, &Rr, &br);
+        else if (rt == OBJ_GEOM || rt == OBJ_SITE || rt == OBJ_CAMERA) obj_frame(m, d, rt, rid, &pr, &Rr, &br);
+        else obj_frame(m, d, OBJ_UNKNOWN, rid, &pr, &Rr, &br);
+        real dif[3] = {p[0] - pr[0], p[1] - pr[1], p[2] - pr[2]};
+        mat_t_vec(v, Rr, dif);
+      }
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_FRAMEXAXIS || t == SENS_FRAMEYAXIS || t == SENS_FRAMEZAXIS) {
+      int ax = t - SENS_FRAMEXAXIS;
+      const real *p, *R; int b;
+      obj_frame(m, d, ot, id, &p, &R, &b);
+      real a[3] = {R[ax], R[3 + ax], R[6 + ax]};
+      if (rid == -1) memcpy(v, a, 3 * sizeof(real));
+      else {
+        const real *pr, *Rr; int br;
+        obj_frame(m, d, rt, rid, &pr, &Rr, &br);
+        mat_t_vec(v, Rr, a);
+      }
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_FRAMEQUAT) {
+      real q[4];
+      frame_quat(m, d, ot, id, q);
+      if (rid == -1) memcpy(v, q, sizeof(q));
+      else {
+        real qr[4], qi[4];
+        frame_quat(m, d, rt, rid, qr);
+        qi[0] = qr[0]; qi[1] = -qr[1]; qi[2] = -qr[2]; qi[3] = -qr[3];
+        mul_quat(v, qi, q);
+      }
+      sensor_write(m, d, s, v, 4);
+    } else if (t == SENS_SUBTREECOM) {
+      memcpy(v, d->subtree_com + 3 * id, 3 * sizeof(real));
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_CLOCK) {
+      v[0] = d->time[0];
+      sensor_write(m, d, s, v, 1);
+    }
+  }
+}
+
+/* sensor.py:1011-1050 _cvel_offset */
+static void cvel_offset(const orc_model* m, const orc_data* d, int type, int id, const real** cvel, real* off) {
+  const real *p, *R; int b;
+  obj_frame(m, d, type, id, &p, &R, &b);
+  *cvel = d->cvel + 6 * b;
+  const real* com = d->subtree_com + 3 * m->body_rootid[b];
+  for (int i = 0; i < 3; i++) off[i] = p[i] - com[i];
+}
+
+/* sensor.py:1251-1373 (_sensor_vel, supported types) */
+static void sensor_vel(const orc_model* m, orc_data* d) {
+  for (int s = 0; s < m->nsensor; s++) {
+    if (m->sensor_needstage[s] != STAGE_VEL) continue;
+    int t = m->sensor_type[s], id = m->sensor_objid[s], ot = m->sensor_objtype[s];
+    int rid = m->sensor_refid[s], rt = m->sensor_reftype[s];
+    real v[3] = {0, 0, 0};
+    if (t == SENS_VELOCIMETER || t == SENS_GYRO) {
+      int b = m->site_bodyid[id];
+      const real* cv = d->cvel + 6 * b;
+      const real* R = d->site_xmat + 9 * id;
+      if (t == SENS_GYRO) mat_t_vec(v, R, cv);
+      else { /* sensor.py:909-931 */
+        const real* com = d->subtree_com + 3 * m->body_rootid[b];
+        real dif[3], c[3], lin[3];
+        for (int i = 0; i < 3; i++) dif[i] = d->site_xpos[3 * id + i] - com[i];
+        cross3(c, dif, cv);
+        for (int i = 0; i < 3; i++) lin[i] = cv[3 + i] - c[i];
+        mat_t_vec(v, R, lin);
+      }
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_JOINTVEL) {
+      v[0] = d->qvel[m->jnt_dofadr[id]];
+      sensor_write(m, d, s, v, 1);
+    } else if (t == SENS_ACTUATORVEL) {
+      v[0] = d->actuator_velocity[id];
+      sensor_write(m, d, s, v, 1);
+    } else if (t == SENS_BALLANGVEL) {
+      memcpy(v, d->qvel + m->jnt_dofadr[id], 3 * sizeof(real));
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_FRAMELINVEL) { /* sensor.py:1053-1156 */
+      const real *p, *R, *pr, *Rr; int b, br;
+      obj_frame(m, d, ot, id, &p, &R, &b);
+      obj_frame(m, d, rt, rid, &pr, &Rr, &br);
+      const real *cv, *cvr;
+      real off[3], offr[3], c[3], xl[3];
+      cvel_offset(m, d, ot, id, &cv, off);
+      cvel_offset(m, d, rt, rid, &cvr, offr);
+      cross3(c, off, cv);
+      for (int i = 0; i < 3; i++) xl[i] = cv[3 + i] - c[i];
+      if (rid > -1) {
+        real cr[3], xlr[3], rvec[3], rc[3], rel[3];
+        cross3(cr, offr, cvr);
+        for (int i = 0; i < 3; i++) { xlr[i] = cvr[3 + i] - cr[i]; rvec[i] = p[i] - pr[i]; }
+        cross3(rc, rvec, cvr);
+        for (int i = 0; i < 3; i++) rel[i] = xl[i] - xlr[i] + rc[i];
+        mat_t_vec(v, Rr, rel);
+      } else memcpy(v, xl, sizeof(xl));
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_FRAMEANGVEL) { /* sensor.py:1159-1238 */
+      const real *cv, *cvr;
+      real off[3];
+      cvel_offset(m, d, ot, id, &cv, off);
+      if (rid > -1) {
+        const real *pr, *Rr; int br;
+        obj_frame(m, d, rt, rid, &pr, &Rr, &br);
+        cvel_offset(m, d, rt, rid, &cvr, off);
+        real dw[3] = {cv[0] - cvr[0], cv[1] - cvr[1], cv[2] - cvr[2]};
+        mat_t_vec(v, Rr, dw);
+      } else memcpy(v, cv, 3 * sizeof(real));
+      sensor_write(m, d, s, v, 3);
+    }
+  }
+}
+
+/* support.py:241-308 contact force (pyramidal decode, to world frame) */
+static void contact_force_world(const orc_data* d, int c, real* f6) {
+  real f[6] = {0, 0, 0, 0, 0, 0};
+  int condim = d->con_dim[c];
+  int adr = d->con_efc_address[10 * c];
+  if (adr >= 0) {
+    if (condim == 1) f[0] = d->efc_force[adr];
+    else {
+      for (int i = 0; i < condim - 1; i++) {
+        int a = 2 * i + adr;
+        real d1 = a < d->njmax ? d->efc_force[a] : 0, d2 = a + 1 < d->njmax ? d->efc_force[a + 1] : 0;
+        f[0] += d1 + d2;
+        f[i + 1] = (d1 - d2) * d->con_friction[5 * c + i];
+      }
+    }
+  }
+  const real* F = d->con_frame + 9 * c;
+  for (int i = 0; i < 3; i++) {
+    f6[i] = f[0] * F[i] + f[1] * F[3 + i] + f[2] * F[6 + i];
+    f6[3 + i] = f[3] * F[i] + f[4] * F[3 + i] + f[5] * F[6 + i];
+  }
+}
+
+/* smooth.py:1276-1499 rne_postconstraint: cfrc_ext (xfrc_applied + contacts), cacc with qacc, cfrc_int */
+static void rne_postconstraint(const orc_model* m, orc_data* d) {
+  int nb = m->nbody;
+  memset(d->cfrc_ext, 0, 6 * sizeof(real));
+  for (int b = 1; b < nb; b++) { /* smooth.py:1278-1295 */
+    const real* xf = d->xfrc_applied + 6 * b;
+    const real* com = d->subtree_com + 3 * m->body_rootid[b];
+    real off[3], c[3];
+    for (int i = 0; i < 3; i++) off[i] = com[i] - d->xipos[3 * b + i];
+    cross3(c, off, xf);
+    for (int i = 0; i < 3; i++) { d->cfrc_ext[6 * b + i] = xf[3 + i] - c[i]; d->cfrc_ext[6 * b + 3 + i] = xf[i]; }
+  }
+  int ncon = *d->ncon < d->nconmax ? *d->ncon : d->nconmax;
+  for (int c = 0; c < ncon; c++) { /* smooth.py:1447-1495 */
+    int id1 = m->geom_bodyid[d->con_geom[2 * c]], id2 = m->geom_bodyid[d->con_geom[2 * c + 1]];
+    if (id1 == 0 && id2 == 0) continue;
+    real f6[6];
+    contact_force_world(d, c, f6);
+    const real* pos = d->con_pos + 3 * c;
+    for (int k = 0; k < 2; k++) {
+      int b = k == 0 ? id1 : id2;
+      if (!b) continue;
+      const real* com = d->subtree_com + 3 * m->body_rootid[b];
+      real off[3], cr[3];
+      for (int i = 0; i < 3; i++) off[i] = com[i] - pos[i];
+      cross3(cr, off, f6);
+      real sg = k == 0 ? -1 : 1;
+      for (int i = 0; i < 3; i++) {
+        d->cfrc_ext[6 * b + i] += sg * (f6[3 + i] - cr[i]);
+        d->cfrc_ext[6 * b + 3 + i] += sg * f6[i];
+      }
+    }
+  }
+  real* cacc = d->cacc;
+  memset(cacc, 0, 6 * sizeof(real));
+  if (!(m->opt_disableflags & DSBL_GRAVITY))
+    for (int i = 0; i < 3; i++) cacc[3 + i] = -m->opt_gravity[i];
+  for (int b = 1; b < nb; b++) {
+    int p = m->body_parentid[b];
+    real acc[6];
+    memcpy(acc, cacc + 6 * p, sizeof(acc));
+    for (int k = 0; k < m->body_dofnum[b]; k++) {
+      int dof = m->body_dofadr[b] + k;
+      for (int i = 0; i < 6; i++) acc[i] += d->cdof_dot[6 * dof + i] * d->qvel[dof] + d->cdof[6 * dof + i] * d->qacc[dof];
+    }
+    memcpy(cacc + 6 * b, acc, sizeof(acc));
+  }
+  real* cfrc = d->cfrc_int;
+  memset(cfrc, 0, 6 * sizeof(real));
+  for (int b = 1; b < nb; b++) {
+    real f1[6], iv[6], f2[6];
+    inert_vec(f1, d->cinert + 10 * b, cacc + 6 * b);
+    inert_vec(iv, d->cinert + 10 * b, d->cvel + 6 * b);
+    motion_cross_force(f2, d->cvel + 6 * b, iv);
+    for (int i = 0; i < 6; i++) cfrc[6 * b + i] = f1[i] + f2[i] - d->cfrc_ext[6 * b + i];
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    for (int i = 0; i < 6; i++) cfrc[6 * p + i] += cfrc[6 * b + i];
+  }
+}
+
+/* sensor.py:2447-2680 (_sensor_acc, supported types) */
+static void sensor_acc(const orc_model* m, orc_data* d) {
+  int post = 0;
+  for (int s = 0; s < m->nsensor; s++) {
+    int t = m->sensor_type[s];
+    post |= t == SENS_ACCELEROMETER || t == SENS_FORCE || t == SENS_TORQUE || t == SENS_FRAMELINACC || t == SENS_FRAMEANGACC;
+  }
+  if (post) rne_postconstraint(m, d);
+  for (int s = 0; s < m->nsensor; s++) {
+    if (m->sensor_needstage[s] != STAGE_ACC) continue;
+    int t = m->sensor_type[s], id = m->sensor_objid[s], ot = m->sensor_objtype[s];
+    real v[3] = {0, 0, 0};
+    if (t == SENS_ACCELEROMETER || t == SENS_FRAMELINACC) { /* sensor.py:1451-1480, 1619-1667 */
+      const real *p, *R; int b;
+      if (t == SENS_ACCELEROMETER) obj_frame(m, d, OBJ_SITE, id, &p, &R, &b);
+      else obj_frame(m, d, ot, id, &p, &R, &b);
+      const real* cv = d->cvel + 6 * b;
+      const real* ca = d->cacc + 6 * b;
+      const real* com = d->subtree_com + 3 * m->body_rootid[b];
+      real dif[3], c1[3], c2[3], lin[3], acc[3], corr[3];
+      for (int i = 0; i < 3; i++) dif[i] = p[i] - com[i];
+      cross3(c1, dif, cv);
+      cross3(c2, dif, ca);
+      for (int i = 0; i < 3; i++) { lin[i] = cv[3 + i] - c1[i]; acc[i] = ca[3 + i] - c2[i]; }
+      if (t == SENS_ACCELEROMETER) {
+        real ang_l[3], lin_l[3], acc_l[3];
+        mat_t_vec(ang_l, R, cv);
+        mat_t_vec(lin_l, R, lin);
+        mat_t_vec(acc_l, R, acc);
+        cross3(corr, ang_l, lin_l);
+        for (int i = 0; i < 3; i++) v[i] = acc_l[i] + corr[i];
+      } else {
+        cross3(corr, cv, lin);
+        for (int i = 0; i < 3; i++) v[i] = acc[i] + corr[i];
+      }
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_FORCE || t == SENS_TORQUE) { /* sensor.py:1483-1518 */
+      int b = m->site_bodyid[id];
+      const real* cf = d->cfrc_int + 6 * b;
+      const real* R = d->site_xmat + 9 * id;
+      if (t == SENS_FORCE) mat_t_vec(v, R, cf + 3);
+      else {
+        const real* com = d->subtree_com + 3 * m->body_rootid[b];
+        real dif[3], c[3], tq[3];
+        for (int i = 0; i < 3; i++) dif[i] = d->site_xpos[3 * id + i] - com[i];
+        cross3(c, dif, cf + 3);
+        for (int i = 0; i < 3; i++) tq[i] = cf[i] - c[i];
+        mat_t_vec(v, R, tq);
+      }
+      sensor_write(m, d, s, v, 3);
+    } else if (t == SENS_ACTUATORFRC) {
+      v[0] = d->actuator_force[id];
+      sensor_write(m, d, s, v, 1);
+    } else if (t == SENS_JOINTACTFRC) {
+      v[0] = d->qfrc_actuator[m->jnt_dofadr[id]];
+      sensor_write(m, d, s, v, 1);
+    } else if (t == SENS_FRAMEANGACC) { /* sensor.py:1670-1694 */
+      const real *p, *R; int b;
+      obj_frame(m, d, ot == OBJ_BODY ? OBJ_XBODY : ot, id, &p, &R, &b);
+      memcpy(v, d->cacc + 6 * b, 3 * sizeof(real));
+      sensor_write(m, d, s, v, 3);
+    }
+  }
+}
+
 /* forward.py:972-1000 */
 static void forward_world(const orc_model* m, orc_data* d) {
+  int sensors = m->nsensor > 0 && !(m->opt_disableflags & DSBL_SENSOR);
   fwd_position(m, d);
+  if (m->nsensordata) memset(d->sensordata, 0, (size_t)m->nsensordata * sizeof(real));
+  if (sensors) sensor_pos(m, d);
   fwd_velocity(m, d);
+  if (sensors) sensor_vel(m, d);
   fwd_actuation(m, d);
   fwd_acceleration(m, d);
   solve(m, d);
+  if (sensors) sensor_acc(m, d);
 }
 
 /* forward.py:1003-1018 */

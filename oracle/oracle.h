@@ -26,7 +26,7 @@ typedef ORC_REAL real;
 /* ---- model: int scalars ---- */
 #define ORC_MODEL_INT_SCALARS(X)                                                                   \
   X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
-  X(nxn) X(nmaxpyramid) X(neq) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
+  X(nxn) X(nmaxpyramid) X(neq) X(nsensor) X(nsensordata) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)
 
 /* ---- model: real scalars ---- */
@@ -35,7 +35,7 @@ typedef ORC_REAL real;
 
 /* ---- model: real arrays (name, element count) ---- */
 #define ORC_MODEL_REAL_ARRAYS(X)                                                                   \
-  X(opt_gravity, 3)                                                                                \
+  X(opt_gravity, 3) X(opt_magnetic, 3) X(sensor_cutoff, nsensor)                                   \
   X(qpos0, nq) X(qpos_spring, nq)                                                                  \
   X(body_pos, nbody * 3) X(body_quat, nbody * 4) X(body_ipos, nbody * 3) X(body_iquat, nbody * 4) \
   X(body_mass, nbody) X(body_subtreemass, nbody) X(body_inertia, nbody * 3)                       \
@@ -72,7 +72,10 @@ typedef ORC_REAL real;
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
   X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)                                                 \
-  X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)
+  X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)                                             \
+  X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
+  X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
+  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)
 
 /* ---- per-world data: real arrays (name, element count per world) ---- */
 #define ORC_DATA_REAL_ARRAYS(X)                                                                    \
@@ -88,7 +91,8 @@ typedef ORC_REAL real;
   X(actuator_length, nu) X(actuator_moment, nu * nv) X(actuator_velocity, nu) X(actuator_force, nu) \
   X(cvel, nbody * 6) X(cdof_dot, nv * 6) X(qfrc_bias, nv) X(qfrc_spring, nv) X(qfrc_damper, nv)   \
   X(qfrc_passive, nv) X(qfrc_actuator, nv) X(qfrc_smooth, nv) X(qacc_smooth, nv)                  \
-  X(qfrc_constraint, nv) X(cacc, nbody * 6) X(cfrc_int, nbody * 6)                                 \
+  X(qfrc_constraint, nv) X(cacc, nbody * 6) X(cfrc_int, nbody * 6) X(cfrc_ext, nbody * 6)         \
+  X(sensordata, nsensordata)                                                                       \
   X(efc_J, njmax * nv) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax) X(efc_vel, njmax)   \
   X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax) X(efc_Ma, nv)                 \
   X(con_dist, nconmax) X(con_pos, nconmax * 3) X(con_frame, nconmax * 9)                          \

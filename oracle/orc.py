@@ -107,6 +107,7 @@ class OracleModel:
     vals = dict(
       nq=mjm.nq, nv=mjm.nv, nu=mjm.nu, na=mjm.na, nbody=mjm.nbody, njnt=mjm.njnt, ngeom=mjm.ngeom, nsite=mjm.nsite,
       ncam=mjm.ncam, nlight=mjm.nlight, nmocap=mjm.nmocap, nxn=len(pairs), neq=mjm.neq,
+      nsensor=getattr(mjm, "nsensor", 0), nsensordata=getattr(mjm, "nsensordata", 0),
       nmaxpyramid=max(1, 2 * (int(np.concatenate(([0], mjm.geom_condim)).max()) - 1)),
       opt_integrator=o.integrator, opt_cone=o.cone, opt_solver=o.solver, opt_iterations=o.iterations,
       opt_ls_iterations=o.ls_iterations, opt_disableflags=o.disableflags, opt_enableflags=o.enableflags,
@@ -118,7 +119,7 @@ class OracleModel:
       vals.update(overrides)
     self.sizes = {k: int(v) for k, v in vals.items() if k in MODEL_INT_SCALARS}
     arrays = dict(
-      opt_gravity=o.gravity, nxn_geom_pair=pairs, nxn_pairid=pairid,
+      opt_gravity=o.gravity, opt_magnetic=o.magnetic, nxn_geom_pair=pairs, nxn_pairid=pairid,
       cam_mat0=getattr(mjm, "cam_mat0", np.zeros((mjm.ncam, 9))),
     )
     self._keep = []
