@@ -41,20 +41,46 @@ METRIC = "env-steps/sec (whole node), humanoid.xml nworld=8192 at 1/2/4/8 MI355X
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 
 
-def b_alg(nefc_mean, ncon_mean):
-  """Algorithmic HBM bytes per env-step: state in + Data contract out, fp32."""
-  return 4.0 * (4170.0 + 38.0 * (nefc_mean + ncon_mean))
+# benchmark configurations (BASELINE.json configs; benchmarks/config.txt sizes)
+MODELS = {
+  # C2, the headline: humanoid, Euler + CG override, keyframe 0 ("squat")
+  "humanoid": dict(path="models/humanoid.xml", nworld=8192, nconmax=24, njmax=64, solver="CG", key=0),
+  # C3: franka (implicitfast, model-default Newton), no keyframe -> ctrl noise around ctrlrange midpoints
+  "franka": dict(path="models/franka_emika_panda/scene.xml", nworld=16384, nconmax=1, njmax=5, solver=None, key=None),
+  # C4: apollo (Euler, model-default Newton, IMU sensors, box-box CCD), keyframe "stand"
+  "apollo": dict(path="models/apptronik_apollo/scene_flat.xml", nworld=4096, nconmax=16, njmax=64, solver=None, key=0),
+}
 
 
-def b_alg_dense(nefc_mean):
-  """Share of B_alg written by the dense kernel: qLD 729 + qacc_smooth 27 + solver outputs 86 +
-  integrator 83 words, plus efc force/state (2 words per row)."""
-  return 4.0 * (925.0 + 2.0 * nefc_mean)
+def step_words(mjm, nv_pad):
+  """Algorithmic words per env-step of SURVEY.md 8(d), from the model sizes: (state inputs, fixed
+  Data-contract outputs of the forward kernels, fixed outputs of the dense kernel).  For the
+  humanoid: 233 + 3012 + 925 = 4170 words."""
+  nq, nv, nu, nb, nj, ng = mjm.nq, mjm.nv, mjm.nu, mjm.nbody, mjm.njnt, mjm.ngeom
+  nJmom = nu  # joint transmissions: one moment entry per actuator
+  w_in = nq + nv + nu + nv + nv + 6 * nb + 1  # qpos qvel ctrl qacc_warmstart qfrc_applied xfrc_applied time
+  kin = nb * (3 + 4 + 9 + 3 + 9) + nj * 6 + ng * 12 + mjm.nsite * 12
+  camlight = mjm.ncam * 12 + mjm.nlight * 6
+  com = 3 * nb + 10 * nb + 6 * nv
+  crb = 10 * nb + nv_pad * nv_pad
+  trn = nu + nJmom + 3 * nu
+  vel = 6 * nb + 6 * nv + nu
+  passive = 3 * nv
+  rne = nv + 12 * nb
+  act = nu + 2 * nv
+  sensors = getattr(mjm, "nsensordata", 0)
+  fwd_out = kin + camlight + com + crb + trn + vel + passive + rne + act + sensors + 2
+  dense_out = nv * nv + nv + (3 * nv + 5) + (nq + 2 * nv + 1)  # qLD, qacc_smooth, solver, integrator
+  return w_in, fwd_out, dense_out
 
 
-def b_alg_forward(nefc_mean, ncon_mean):
-  """Share of B_alg of the forward kernel: state inputs + every other Data output (36 words per row)."""
-  return b_alg(nefc_mean, ncon_mean) - b_alg_dense(nefc_mean)
+def b_alg_parts(words, nefc_mean, ncon_mean, nv_pad):
+  """(forward, dense) algorithmic bytes per env-step: per constraint row 10 scalars + a J row of
+  nv_pad (2 of them, force / state, written by the dense kernel), per contact 38 words."""
+  w_in, fwd_out, dense_out = words
+  fwd = 4.0 * (w_in + fwd_out + (8.0 + nv_pad) * nefc_mean + 38.0 * ncon_mean)
+  dense = 4.0 * (dense_out + 2.0 * nefc_mean)
+  return fwd, dense
 
 
 def parse():
@@ -62,28 +88,37 @@ def parse():
   p.add_argument("--gpus", type=int, default=1)
   p.add_argument("--steps", type=int, default=1000)
   p.add_argument("--warmup", type=int, default=20)
-  p.add_argument("--nworld", type=int, default=8192, help="worlds per GPU")
-  p.add_argument("--solver", default="CG", choices=["CG", "NEWTON"])
-  p.add_argument("--nconmax", type=int, default=24)
-  p.add_argument("--njmax", type=int, default=64)
+  p.add_argument("--model", default="humanoid", choices=sorted(MODELS), help="benchmark config (default: the headline C2)")
+  p.add_argument("--nworld", type=int, default=None, help="worlds per GPU (default: the config's)")
+  p.add_argument("--solver", default=None, choices=["CG", "NEWTON"], help="override opt.solver (default: the config's)")
+  p.add_argument("--nconmax", type=int, default=None)
+  p.add_argument("--njmax", type=int, default=None)
   p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
   p.add_argument("--cpu-worlds", type=int, default=1024)
   p.add_argument("--cpu-steps", type=int, default=1000)
   p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_humanoid_r01.json"))
   p.add_argument("--graph", type=int, default=0, help="replay steps through a captured hipGraph")
-  return p.parse_args()
+  a = p.parse_args()
+  cfg = MODELS[a.model]
+  for k in ("nworld", "nconmax", "njmax", "solver"):
+    if getattr(a, k) is None:
+      setattr(a, k, cfg[k])
+  return a
 
 
-def cpu_baseline(mjm, nworld, nsteps):
+def cpu_baseline(mjm, nworld, nsteps, key, njmax, nconmax, model):
   """fp64 C oracle (restatement of the reference step), OpenMP over worlds; rank 0 only."""
   from oracle import orc
 
   nthread = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
   nthread = max(1, min(nthread, 16))
   om = orc.OracleModel(mjm, real_bits=64)
-  od = orc.OracleData(om, nworld, 64, 24)
-  od.qpos[:] = mjm.key_qpos[0]
-  center = np.zeros(mjm.nu)
+  od = orc.OracleData(om, nworld, njmax, nconmax)
+  center = None
+  if key is not None:
+    od.qpos[:] = mjm.key_qpos[key]
+    od.ctrl[:] = mjm.key_ctrl[key]
+    center = mjm.key_ctrl[key]
   t0 = time.perf_counter()
   for i in range(nsteps):
     od.ctrl_noise(i, center=center)
@@ -94,7 +129,7 @@ def cpu_baseline(mjm, nworld, nsteps):
     unit="env-steps/s",
     cores=nthread,
     kind="port",
-    sample=f"fp64 C oracle (oracle/oracle.c), humanoid CG, {nworld} worlds x {nsteps} steps from key 0 with ctrl noise, "
+    sample=f"fp64 C oracle (oracle/oracle.c), {model}, {nworld} worlds x {nsteps} steps with ctrl noise, "
     f"{nthread} OpenMP threads, {dt:.1f} s; the reference's Warp-CPU path is not runnable here (no warp/mujoco)",
   )
 
@@ -115,14 +150,19 @@ def main():
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
   dev = torch.device("cuda", local)
 
-  mjm = mjcf.load_model(os.path.join(ROOT, "models", "humanoid.xml"))
-  mjw.override_model(mjm, [f"opt.solver={args.solver}"])
+  cfg = MODELS[args.model]
+  mjm = mjcf.load_model(os.path.join(ROOT, cfg["path"]))
+  if args.solver is not None:
+    mjw.override_model(mjm, [f"opt.solver={args.solver}"])
+  solver_name = {1: "CG", 2: "NEWTON"}[int(mjm.opt.solver)]
   mjd = mjcf.MjData(mjm)
-  mjcf.reset_data_keyframe(mjm, mjd, 0)
+  center = None
+  if cfg["key"] is not None:  # testspeed: keyframe state, ctrl noise around the keyframe ctrl
+    mjcf.reset_data_keyframe(mjm, mjd, cfg["key"])
+    center = torch.as_tensor(np.asarray(mjm.key_ctrl[cfg["key"]], dtype=np.float32), device=dev)
   m = mjw.put_model(mjm, device=dev)
   d = mjw.put_data(mjm, mjd, nworld=args.nworld, nconmax=args.nconmax, njmax=args.njmax, device=dev, m=m)
   d.world_offset = rank * args.nworld
-  center = torch.zeros(mjm.nu, dtype=torch.float32, device=dev)
 
   from mujoco_warp_amd.forward import step_timed
 
@@ -173,16 +213,18 @@ def main():
   total_steps = args.nworld * world * args.steps
   value = total_steps / elapsed
   if rank == 0:
-    bytes_per_launch = b_alg_forward(nefc_mean, ncon_mean) * args.nworld
+    words = step_words(mjm, m.nv_pad)
+    fwd_b, dense_b = b_alg_parts(words, nefc_mean, ncon_mean, m.nv_pad)
+    bytes_per_launch = fwd_b * args.nworld
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.pmc):
       with open(args.pmc) as f:
         pmc = json.load(f)
-      if pmc.get("solver", "CG") == args.solver and pmc.get("nworld") == args.nworld:
+      if pmc.get("solver", "CG") == solver_name and pmc.get("nworld") == args.nworld and pmc.get("model", "humanoid") == args.model:
         traffic = pmc.get("kernels", {}).get("forward", {}).get("hbm_bytes_per_launch")
     out = {
-      "metric": METRIC,
+      "metric": METRIC if args.model == "humanoid" else f"env-steps/sec (whole node), {args.model} nworld={args.nworld} per GPU",
       "value": value,
       "unit": "env-steps/s",
       "n_gpus": world,
@@ -193,13 +235,14 @@ def main():
       "scaling": "weak",
       "vs_baseline": None,
       "dtype": "fp32",
-      "data": "synthetic (keyframe 'squat' + OU/Halton ctrl noise, no dataset)",
+      "data": "synthetic (keyframe state + OU/Halton ctrl noise of benchmark.py, no dataset)",
       "config": {
-        "workload": f"humanoid.xml nworld={args.nworld} per GPU fp32, Euler+{args.solver}, 1xMI355X per rank",
+        "workload": f"{os.path.basename(cfg['path'])} ({args.model}) nworld={args.nworld} per GPU fp32, "
+        f"{['Euler', 'RK4', 'implicit', 'implicitfast'][int(mjm.opt.integrator)]}+{solver_name}, 1xMI355X per rank",
         "nworld_per_gpu": args.nworld,
         "nconmax": args.nconmax,
         "njmax": args.njmax,
-        "solver": args.solver,
+        "solver": solver_name,
         "parallelism": f"worlds sharded over {world} GPU(s), no collective",
         "converged_worlds": converged,
         "nefc_mean": nefc_mean,
@@ -213,22 +256,23 @@ def main():
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic,
-        "kernel": "mjw::mjw_kernel<79> (forward: position/velocity/actuation/qfrc_smooth)",
+        "kernel": "mjw::mjw_kernel<79> (forward: position/velocity/actuation/qfrc_smooth)"
+        + (" + mjw::ccd_kernel (convex pre-pass)" if m.nxn_ccd else ""),
         "kernel_ms": kernel_ms,
-        "alg_bytes_per_env_step": b_alg_forward(nefc_mean, ncon_mean),
+        "alg_bytes_per_env_step": fwd_b,
         "other_kernels": {
-          "mjw::dense_kernel<7,false> (factor/CG/Euler)": {
+          "mjw::dense_kernel (factor/solve/Euler)" + (" + mjw::sensor_acc_kernel" if m.nsensor else ""): {
             "ms": dense_ms,
-            "alg_bytes_per_env_step": b_alg_dense(nefc_mean),
-            "achieved_GBs": b_alg_dense(nefc_mean) * args.nworld / (dense_ms * 1e-3) / 1e9,
+            "alg_bytes_per_env_step": dense_b,
+            "achieved_GBs": dense_b * args.nworld / (dense_ms * 1e-3) / 1e9,
           }
         },
-        "step_alg_bytes_per_env_step": b_alg(nefc_mean, ncon_mean),
+        "step_alg_bytes_per_env_step": fwd_b + dense_b,
       },
       "cpu_baseline": None,
     }
     if world == 1 and args.cpu_baseline:
-      out["cpu_baseline"] = cpu_baseline(mjm, args.cpu_worlds, args.cpu_steps)
+      out["cpu_baseline"] = cpu_baseline(mjm, args.cpu_worlds, args.cpu_steps, cfg["key"], args.njmax, args.nconmax, args.model)
     print(json.dumps(out), flush=True)
   if world > 1:
     dist.destroy_process_group()

@@ -28,19 +28,21 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 4
+#define MJW_ABI_VERSION 5
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
   X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
   X(nxn) X(nlevel) X(nlimited) X(nmaxcondim) X(nmaxpyramid) X(nv_pad) X(nJmom) X(neq)            \
   X(nsensor) X(nsensordata) X(sensor_rne_postconstraint) X(nsensor_acc)                           \
+  X(nxn_ccd) X(opt_ccd_iterations) X(ccd_epa_iterations)                                           \
   X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations) X(opt_ls_iterations)             \
   X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
   X(opt_timestep, 1) X(opt_tolerance, 1) X(opt_ls_tolerance, 1) X(opt_impratio_invsqrt, 1)        \
+  X(opt_ccd_tolerance, 1)                                                                          \
   X(opt_gravity, 3) X(opt_magnetic, 3) X(stat_meaninertia, 1)                                      \
   X(qpos0, nq) X(qpos_spring, nq)                                                                  \
   X(body_pos, nbody * 3) X(body_quat, nbody * 4) X(body_ipos, nbody * 3) X(body_iquat, nbody * 4) \
@@ -79,7 +81,7 @@
   X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
-  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)                                                 \
+  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2) X(nxn_ccdid, nxn)                               \
   X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)                                             \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
@@ -103,7 +105,7 @@
   X(cfrc_ext, nbody * 6)                                                                           \
   X(efc_J, njmax_pad * nv_pad) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax_pad)         \
   X(efc_vel, njmax) X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax)             \
-  X(efc_Ma, nv) X(sensordata, nsensordata)
+  X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 17)
 
 /* ---- data: int arrays, (nworld, count) ---- */
 #define MJW_DATA_INT_ARRAYS(X)                                                                     \

@@ -13,6 +13,7 @@
 // written once per stage group with lane-contiguous (coalesced) accesses.
 
 #include "mjw_common.h"
+#include "mjw_ccd.h"
 
 #include <cstdlib>
 
@@ -27,14 +28,14 @@ struct Lay {
   int J, efc_D, efc_aref, efc_pos, efc_margin, efc_vel, efc_frictionloss, efc_type, efc_id, efc_force, efc_state;
   int Jaref, jv, rowcon;
   int act_len, act_vel, act_force, act_mom, act_momdof, act_nnz;
-  int con, cmax, jqvel, plist, scratch, iscratch;
+  int con, cmax, jqvel, plist, scratch, iscratch, ccd;
   int nofactor;
   int total;
 };
 
 // nofactor: the kernel stops at qfrc_smooth and the dense kernel does factor/solve/euler,
 // so the Cholesky / Newton / solver row scratch is not allocated
-__host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor = false) {
+__host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor = false, bool ccd = false) {
   Lay L;
   int o = 0;
   L.nofactor = nofactor;
@@ -72,6 +73,13 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
   L.con = (nofactor && nv * L.nvs >= L.cmax * CREC) ? L.qM : take(L.cmax * CREC);
   L.scratch = take(64);
   L.iscratch = take(64);
+  // convex-collision (GJK/EPA) workspace: the cdof_dot..cfrc block is dead until fwd_velocity,
+  // so it holds the workspace when it fits; otherwise the workspace gets its own LDS
+  L.ccd = -1;
+  if (ccd && m.nxn_ccd > 0) {
+    const int need = ccd_layout(m.ccd_epa_iterations).total;
+    L.ccd = (L.qM - L.cdof_dot >= need) ? L.cdof_dot : take(need);
+  }
   L.total = o;
   return L;
 }
@@ -106,7 +114,7 @@ struct WS {
 // -------------------------------------------------------------------------------------------
 // smooth.py: kinematics (smooth.py:44-224, 357-415)
 // -------------------------------------------------------------------------------------------
-__device__ void kinematics(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void kinematics(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   const float* qpos = s + L.qpos;
@@ -281,7 +289,7 @@ __device__ void kinematics(const mjw_model_t& m, const mjw_data_t& d, const Lay&
 }
 
 // smooth.py:463-632: subtree com (contiguous DFS subtree ranges), cinert, cdof
-__device__ void com_pos(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void com_pos(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   const float* body_mass = MR(body_mass);
@@ -356,7 +364,7 @@ __device__ void com_pos(const mjw_model_t& m, const mjw_data_t& d, const Lay& L,
 }
 
 // smooth.py:635-803
-__device__ void camlight(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void camlight(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   const float* s = w.s;
   const float* cam_pos = MR(cam_pos);
@@ -436,7 +444,7 @@ __device__ void camlight(const mjw_model_t& m, const mjw_data_t& d, const Lay& L
 }
 
 // smooth.py:806-912: composite inertia (subtree ranges) and dense qM
-__device__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   const float* dof_armature = MR(dof_armature);
@@ -484,7 +492,7 @@ __device__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, 
 // -------------------------------------------------------------------------------------------
 // dense Cholesky (wp.tile_cholesky) and solve (wp.tile_cholesky_solve), lane = row
 // -------------------------------------------------------------------------------------------
-__device__ void cholesky(float* A, int n, int nvs, int lane) {
+__device__ __forceinline__ void cholesky(float* A, int n, int nvs, int lane) {
   // in place: lower triangle of A becomes L (A = L L^T), upper set to zero
   for (int j = 0; j < n; j++) {
     float ljj = sqrtf(A[j * nvs + j]);
@@ -509,7 +517,7 @@ __device__ void cholesky(float* A, int n, int nvs, int lane) {
 }
 
 // x = (L L^T)^-1 y ; y held per lane (lane = dof), result per lane
-__device__ float cholesky_solve(const float* Lm, int n, int nvs, int lane, float y) {
+__device__ __forceinline__ float cholesky_solve(const float* Lm, int n, int nvs, int lane, float y) {
   for (int j = 0; j < n; j++) {
     float yj = __shfl(y, j, 64) / Lm[j * nvs + j];
     if (lane == j) y = yj;
@@ -561,7 +569,7 @@ __device__ __forceinline__ void closest_segment_point(float* r, const float* a, 
 }
 
 // collision_primitive_core.py:181-308
-__device__ void capsule_capsule(Con2& out, const float* p1, const float* ax1, float r1, float hl1, const float* p2,
+__device__ __forceinline__ void capsule_capsule(Con2& out, const float* p1, const float* ax1, float r1, float hl1, const float* p2,
                                 const float* ax2, float r2, float hl2, float margin) {
   float a1[3], a2[3], dif[3];
   for (int i = 0; i < 3; i++) { a1[i] = ax1[i] * hl1; a2[i] = ax2[i] * hl2; dif[i] = p1[i] - p2[i]; }
@@ -615,7 +623,7 @@ __device__ void capsule_capsule(Con2& out, const float* p1, const float* ax1, fl
 }
 
 // collision_primitive_core.py:311-361
-__device__ void plane_capsule(Con2& out, const float* n, const float* ppos, const float* cpos, const float* axis, float r, float hl) {
+__device__ __forceinline__ void plane_capsule(Con2& out, const float* n, const float* ppos, const float* cpos, const float* axis, float r, float hl) {
   float nd = dot3(n, axis);
   float tmp[3] = {axis[0] - n[0] * nd, axis[1] - n[1] * nd, axis[2] - n[2] * nd};
   float bn = sqrtf(dot3(tmp, tmp));
@@ -661,7 +669,7 @@ __device__ __forceinline__ void mat_t_vec3(float* r, const float* M, const float
 }
 
 // collision_primitive_core.py:1103-1155
-__device__ float sphere_box(float* pos, float* nrm, const float* spos, float r, const float* bpos, const float* brot,
+__device__ __forceinline__ float sphere_box(float* pos, float* nrm, const float* spos, float r, const float* bpos, const float* brot,
                             const float* bsize) {
   float dif[3] = {spos[0] - bpos[0], spos[1] - bpos[1], spos[2] - bpos[2]}, center[3], clamped[3], tmp[3];
   mat_t_vec3(center, brot, dif);
@@ -694,7 +702,7 @@ __device__ float sphere_box(float* pos, float* nrm, const float* spos, float r, 
 }
 
 // collision_primitive_core.py:1158-1480 (MuJoCo's capsule-box): up to 2 contacts
-__device__ void capsule_box(Con2& out, const float* cpos, const float* cax, float cr, float chl, const float* bpos, const float* brot,
+__device__ __forceinline__ void capsule_box(Con2& out, const float* cpos, const float* cax, float cr, float chl, const float* bpos, const float* brot,
                             const float* bsize) {
   float dif[3] = {cpos[0] - bpos[0], cpos[1] - bpos[1], cpos[2] - bpos[2]}, pos[3], axis[3], ha[3];
   mat_t_vec3(pos, brot, dif);
@@ -827,7 +835,7 @@ __device__ void capsule_box(Con2& out, const float* cpos, const float* cax, floa
 }
 
 // collision_driver.py:217-271
-__device__ bool obb_filter(const float* c1, const float* c2, const float* s1, const float* s2, float margin, const float* xp1,
+__device__ __forceinline__ bool obb_filter(const float* c1, const float* c2, const float* s1, const float* s2, float margin, const float* xp1,
                            const float* xp2, const float* xm1, const float* xm2) {
   float xc0[3], xc1[3];
   matvec3(xc0, xm1, c1);
@@ -852,7 +860,7 @@ __device__ bool obb_filter(const float* c1, const float* c2, const float* s1, co
 }
 
 // collision_driver.py:116-213
-__device__ bool aabb_filter(const float* c1, const float* c2, const float* s1, const float* s2, float margin, const float* xp1,
+__device__ __forceinline__ bool aabb_filter(const float* c1, const float* c2, const float* s1, const float* s2, float margin, const float* xp1,
                             const float* xp2, const float* xm1, const float* xm2) {
   float cen1[3], cen2[3];
   matvec3(cen1, xm1, c1);
@@ -878,7 +886,7 @@ __device__ bool aabb_filter(const float* c1, const float* c2, const float* s1, c
 }
 
 // collision_driver.py:274-321
-__device__ bool broadphase_filter(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2) {
+__device__ __forceinline__ bool broadphase_filter(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2) {
   const float* geom_aabb = MR(geom_aabb);
   const float* geom_rbound = MR(geom_rbound);
   const float* geom_margin = MR(geom_margin);
@@ -916,7 +924,7 @@ __device__ bool broadphase_filter(const mjw_model_t& m, const Lay& L, const floa
 }
 
 // narrowphase of one pair (collision_primitive.py:280-662); pair is type-sorted on the host
-__device__ void narrowphase(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2, float margin, Con2& c) {
+__device__ __forceinline__ void narrowphase(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2, float margin, Con2& c) {
   const float* geom_size = MR(geom_size);
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   const float* p1 = s + L.gxpos + 3 * g1;
@@ -958,7 +966,7 @@ __device__ void narrowphase(const mjw_model_t& m, const Lay& L, const float* s, 
 }
 
 // collision_core.py:235-341 (geom mixing; explicit <pair> entries are not produced by this build's compiler)
-__device__ void contact_params(const mjw_model_t& m, int wid, int g1, int g2, float* margin, float* gap, int* condim,
+__device__ __forceinline__ void contact_params(const mjw_model_t& m, int wid, int g1, int g2, float* margin, float* gap, int* condim,
                                float* friction, float* solref, float* solimp) {
   const float* geom_solmix = MR(geom_solmix);
   const float* geom_friction = MR(geom_friction);
@@ -998,7 +1006,7 @@ __device__ void contact_params(const mjw_model_t& m, int wid, int g1, int g2, fl
 // constraint.py
 // -------------------------------------------------------------------------------------------
 // constraint.py:52-121 (writes LDS row scalars)
-__device__ void efc_row(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, float* s, int wid, int r, float pos_aref, float pos_imp,
+__device__ __forceinline__ void efc_row(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, float* s, int wid, int r, float pos_aref, float pos_imp,
                         float invweight, const float* solref, const float* solimp, float margin, float vel, float frictionloss,
                         int type, int id) {
   float timestep = MR(opt_timestep)[0];
@@ -1067,7 +1075,7 @@ __device__ __forceinline__ void jac_dof(const mjw_model_t& m, const Lay& L, cons
 }
 
 // collision_driver.py:754-789 + constraint.py:2209-2779 (friction-dof, limits, pyramidal contacts)
-__device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   int* si = w.si;
@@ -1218,6 +1226,7 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
         float margin = 0.0f;
         unsigned bmask = 0;  // plane-box: active corners (collision_primitive.py:737-790 writes all 8)
         bool pbox = false;
+        bool ccd = false;  // convex pair: GJK/EPA below (collision_driver.py:74, collision_convex.py:701-890)
         if (k < npass) {
           int p = plist[k];
           g1 = m.nxn_geom_pair[2 * p];
@@ -1225,7 +1234,9 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
           pairid0 = m.nxn_pairid[2 * p];
           margin = geom_margin[g1] + geom_margin[g2];
           pbox = m.geom_type[g1] == GEOM_PLANE && m.geom_type[g2] == GEOM_BOX;
-          if (pbox) {
+          ccd = m.geom_type[g1] == GEOM_BOX && m.geom_type[g2] == GEOM_BOX;
+          if (ccd) {
+          } else if (pbox) {
             const float* r1 = s + L.gxmat + 9 * g1;
             float n1[3] = {r1[2], r1[5], r1[8]}, cp[3];
             for (int q = 0; q < 8; q++) {
@@ -1237,15 +1248,29 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
             narrowphase(m, L, s, wid, g1, g2, margin, c);
           }
         }
+        // convex pairs: results of the CCD pre-pass (ccd_kernel), c.n contacts at distance c.dist[0]
+        // with frame c.frame[0], points in c.pos[0], c.pos[1], c.frame[1][0..2], c.frame[1][3..5]
+        if (ccd) {
+          const float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[plist[k]]) * CCD_OUT;
+          c.n = (int)out[0];
+          c.dist[0] = out[1];
+          make_frame(c.frame[0], out + 2);
+          for (int i = 0; i < 3; i++) {
+            c.pos[0][i] = out[5 + i];
+            c.pos[1][i] = out[8 + i];
+            c.frame[1][i] = out[11 + i];
+            c.frame[1][3 + i] = out[14 + i];
+          }
+        }
         // active contacts (write_contact collision_core.py:199-213)
-        bool a0 = c.n > 0 && c.dist[0] < margin && pairid0 >= -1;
-        bool a1 = c.n > 1 && c.dist[1] < margin && pairid0 >= -1;
-        int cnt = pbox ? __popc(bmask) : (int)a0 + (int)a1;
+        bool a0 = !ccd && c.n > 0 && c.dist[0] < margin && pairid0 >= -1;
+        bool a1 = !ccd && c.n > 1 && c.dist[1] < margin && pairid0 >= -1;
+        int cnt = pbox ? __popc(bmask) : (ccd ? (pairid0 >= -1 && c.dist[0] < margin ? c.n : 0) : (int)a0 + (int)a1);
         int incl = wave_scan_incl(cnt);
         int first = running + incl - cnt;
         bool stage0 = a0 && first >= rbeg && first < rend;
         bool stage1 = a1 && first + (int)a0 >= rbeg && first + (int)a0 < rend;
-        bool stagebox = cnt > 0 && pbox && first < rend && first + cnt > rbeg;
+        bool stagebox = cnt > 0 && (pbox || ccd) && first < rend && first + cnt > rbeg;
         if (stage0 || stage1 || stagebox) {
           float gap, friction[5], solref[2], solimp[5];
           int condim;
@@ -1267,6 +1292,26 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
               rec[1] = margin - gap;
               for (int i = 0; i < 3; i++) rec[2 + i] = cp[i];
               for (int i = 0; i < 9; i++) rec[5 + i] = frame[i];
+              for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
+              rec[19] = solref[0]; rec[20] = solref[1];
+              rec[21] = 0.0f; rec[22] = 0.0f;
+              for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
+              int* reci = reinterpret_cast<int*>(rec);
+              reci[28] = condim;
+              reci[29] = g1;
+              reci[30] = g2;
+            }
+          }
+          if (ccd) {
+            for (int q = 0; q < c.n; q++) {
+              int idx = first + q;
+              if (idx < rbeg || idx >= rend) continue;
+              float* rec = s + L.con + (idx - rbeg) * CREC;
+              rec[0] = c.dist[0];
+              rec[1] = margin - gap;
+              for (int i = 0; i < 3; i++)
+                rec[2 + i] = q == 0 ? c.pos[0][i] : (q == 1 ? c.pos[1][i] : (q == 2 ? c.frame[1][i] : c.frame[1][3 + i]));
+              for (int i = 0; i < 9; i++) rec[5 + i] = c.frame[0][i];
               for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
               rec[19] = solref[0]; rec[20] = solref[1];
               rec[21] = 0.0f; rec[22] = 0.0f;
@@ -1447,7 +1492,7 @@ __device__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t
 }
 
 // smooth.py:2041-2147 (joint transmissions; moment rows packed in actuator order)
-__device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   int* si = w.si;
@@ -1520,7 +1565,7 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, const La
 // -------------------------------------------------------------------------------------------
 // velocity (forward.py:592-613): actuator velocity, com_vel, passive, rne
 // -------------------------------------------------------------------------------------------
-__device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   int* si = w.si;
@@ -1691,7 +1736,7 @@ __device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const La
 }
 
 // forward.py:616-927 (actuator force, qfrc_actuator)
-__device__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   int* si = w.si;
@@ -1753,7 +1798,7 @@ __device__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, const L
 }
 
 // forward.py:930-969 + support.py:174-237 (xfrc) + factor_solve_i (smooth.py:2860-2928)
-__device__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   const int nv = m.nv, nvs = L.nvs;
@@ -1827,7 +1872,7 @@ __device__ __forceinline__ bool in_bracket(const Vec3& x, const Vec3& y) {
 }
 
 // update_constraint (solver.py:2154-2219): returns (cost, gauss); sets force/state; qfrc_constraint per lane
-__device__ void update_constraint(const Lay& L, float* s, int lane, int nv, int nvs, int nefc, int ne, int nf, float ma,
+__device__ __forceinline__ void update_constraint(const Lay& L, float* s, int lane, int nv, int nvs, int nefc, int ne, int nf, float ma,
                                   float qfrc_smooth, float qacc, float qacc_smooth, float& cost, float& gauss, float& qfrc_c) {
   int* si = reinterpret_cast<int*>(s);
   float c = 0.0f;
@@ -1859,7 +1904,7 @@ __device__ void update_constraint(const Lay& L, float* s, int lane, int nv, int 
   cost = wave_sum(c) + g;
 }
 
-__device__ void solve(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void solve(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   int* si = w.si;
@@ -2060,7 +2105,7 @@ __device__ void solve(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, W
 }
 
 // forward.py:51-354 (_advance + euler; implicit damping when EULERDAMP is enabled)
-__device__ void euler(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void euler(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   const int nv = m.nv, nvs = L.nvs;
@@ -2120,13 +2165,13 @@ __device__ void euler(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, W
 // -------------------------------------------------------------------------------------------
 // input loaders for stage kernels that do not start at fwd_position
 // -------------------------------------------------------------------------------------------
-__device__ void load_state(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+__device__ __forceinline__ void load_state(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   for (int i = lane; i < m.nq; i += LPW) w.s[L.qpos + i] = d.qpos[(long)wid * m.nq + i];
   for (int i = lane; i < m.nv; i += LPW) w.s[L.qvel + i] = d.qvel[(long)wid * m.nv + i];
 }
 
-__device__ void load_smooth(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w, int stages) {
+__device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w, int stages) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   int* si = w.si;
@@ -2251,6 +2296,47 @@ __global__ void __launch_bounds__(64) mjw_kernel(const mjw_model_t m, const mjw_
   PROF_MARK(PH_GEULER);
 }
 
+// -------------------------------------------------------------------------------------------
+// convex collision pre-pass (collision_convex.py:701-890): one wave per world recomputes the
+// geom frames (same kinematics code as the forward kernel), applies the broadphase filter to the
+// convex pairs and runs GJK / EPA / multi-contact on the survivors, one pair at a time with the
+// whole wave in lockstep over an LDS workspace.  Results go to d.ccd_out, which the forward
+// kernel's narrowphase reads, so the (large) CCD code never shares a kernel with the hot path.
+// -------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  WS w;
+  w.s = smem;
+  w.si = reinterpret_cast<int*>(smem);
+  w.wid = blockIdx.x;
+  w.lane = lane_id();
+  if (w.wid >= d.nworld) return;
+  const int wid = w.wid;
+  load_state(m, d, L, w);
+  WSYNC();
+  kinematics(m, d, L, w);
+  float* s = w.s;
+  const float* geom_margin = MR(geom_margin);
+  const float* gsize = MR(geom_size);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations);
+  float* W = s + L.ccd;
+  for (int p = 0; p < m.nxn; p++) {
+    const int slot = m.nxn_ccdid[p];
+    if (slot < 0) continue;
+    const int g1 = m.nxn_geom_pair[2 * p], g2 = m.nxn_geom_pair[2 * p + 1];
+    const bool pass = m.nxn_pairid[2 * p + 1] >= 0 || broadphase_filter(m, L, s, wid, g1, g2);
+    int nc = 0;
+    if (pass) {
+      put_cgeom(W + CL.geoms, s + L.gxpos + 3 * g1, s + L.gxmat + 9 * g1, gsize + 3 * g1, m.geom_type[g1]);
+      put_cgeom(W + CL.geoms + CGEOM_WORDS, s + L.gxpos + 3 * g2, s + L.gxmat + 9 * g2, gsize + 3 * g2, m.geom_type[g2]);
+      nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, geom_margin[g1] + geom_margin[g2]);
+    }
+    float* out = d.ccd_out + ((long)wid * m.nxn_ccd + slot) * CCD_OUT;
+    const int lane = w.lane;
+    if (lane < CCD_OUT) out[lane] = lane == 0 ? (float)nc : (nc > 0 ? W[CL.out + lane - 1] : 0.0f);
+  }
+}
+
 // benchmark.py:41-83
 __global__ void ctrl_noise_kernel(const mjw_model_t m, const mjw_data_t d, const float* center, int step, float std, float rate_) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2300,6 +2386,16 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
     hipError_t e = hipMemsetAsync(d->nacon, 0, sizeof(int32_t), s);
     if (e == hipSuccess) e = hipMemsetAsync(d->ncollision, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return set_err(e, name);
+    if (m->nxn_ccd > 0 && d->naconmax > 0 && !(m->opt_disableflags & (mjw::DSBL_CONSTRAINT | mjw::DSBL_CONTACT))) {
+      static std::once_flag once_ccd;
+      std::call_once(once_ccd, [] {
+        (void)hipFuncSetAttribute((const void*)mjw::ccd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      });
+      const mjw::Lay LC = mjw::make_layout(*m, d->njmax, nofactor, true);
+      hipLaunchKernelGGL(mjw::ccd_kernel, dim3(d->nworld), dim3(64), (size_t)LC.total * 4, s, *m, *d, LC);
+      e = hipGetLastError();
+      if (e != hipSuccess) return set_err(e, name);
+    }
   }
   static std::once_flag once;
   std::call_once(once, [] {

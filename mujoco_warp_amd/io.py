@@ -88,7 +88,11 @@ def _model_attr(name):
 
 _SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.BOX, types.GeomType.MESH}
 # narrowphase pairs built on the device (type-sorted): collision_primitive.py:1280-1300 subset
-_SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6)}
+_SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6), (6, 6)}
+# pairs routed through GJK/EPA (the CONVEX entries of collision_driver.py:42-76 built here)
+_CCD_PAIRS = {(6, 6)}
+# every CONVEX entry of the reference table (heightfields excluded), for the EPA iteration cap
+_CONVEX_TABLE = {(2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
 
 
 def put_model(mjm, device=None) -> types.Model:
@@ -121,6 +125,9 @@ def put_model(mjm, device=None) -> types.Model:
     if t not in _SUPPORTED_PAIRS:
       names = tuple(types.GeomType(x).name for x in t)
       raise NotImplementedError(f"collision between {names[0]} and {names[1]} is not supported by this build yet.")
+  if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
+      tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) == (6, 6) for a, b in pairs_chk):
+    raise NotImplementedError("box-box with NATIVECCD disabled (primitive box_box) is not supported by this build yet.")
   if np.any(mjm.actuator_trntype > types.TrnType.JOINTINPARENT):
     raise NotImplementedError("only joint transmissions are supported.")
 
@@ -131,6 +138,7 @@ def put_model(mjm, device=None) -> types.Model:
   opt.tolerance = _f32([max(o.tolerance, 1e-6)], dev)  # io.py:185
   opt.ls_tolerance = _f32([o.ls_tolerance], dev)
   opt.ccd_tolerance = _f32([getattr(o, "ccd_tolerance", 1e-6)], dev)
+  opt.ccd_iterations = int(getattr(o, "ccd_iterations", 35))
   opt.density = _f32([o.density], dev)
   opt.viscosity = _f32([o.viscosity], dev)
   opt.gravity = _f32(np.asarray(o.gravity).reshape(1, 3), dev)
@@ -190,6 +198,14 @@ def put_model(mjm, device=None) -> types.Model:
   m.nxn_pairid_filtered = _i32(pairid, dev)
   m.nxn_geom_pair_typed = _i32(typed, dev)
   m.nxn = len(pairs)
+  kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in pairs]
+  m.nxn_ccd = int(sum(k in _CCD_PAIRS for k in kinds))
+  ccdid = np.cumsum([k in _CCD_PAIRS for k in kinds]) - 1
+  m.nxn_ccdid = _i32(np.where([k in _CCD_PAIRS for k in kinds], ccdid, -1) if kinds else np.zeros(0), dev)
+  nconvex = sum(k in _CONVEX_TABLE for k in kinds)
+  nboxbox = sum(k == (6, 6) for k in kinds)
+  # collision_convex.py:1127: EPA iteration cap
+  m.ccd_epa_iterations = 16 if nconvex and nboxbox == nconvex else int(getattr(mjm.opt, "ccd_iterations", 35))
   m.nlimited = len(jnt_limited_sh)
   m.nJmom = int(sum({JointType.FREE: 6, JointType.BALL: 3}.get(int(mjm.jnt_type[mjm.actuator_trnid[a, 0]]), 1) for a in range(mjm.nu)))
 
@@ -214,7 +230,7 @@ def put_model(mjm, device=None) -> types.Model:
     val = np.asarray(getattr(mjm, attr), dtype=np.float64)
     setattr(m, attr, _f32(val.reshape((1,) + val.shape), dev))
   for name, cnt in _lib.MODEL_INT_ARRAYS:
-    if name in derived_int or name in ("nxn_geom_pair", "nxn_pairid"):
+    if name in derived_int or name in ("nxn_geom_pair", "nxn_pairid", "nxn_ccdid"):
       continue
     setattr(m, name, _i32(np.asarray(getattr(mjm, name)), dev))
   # extra reference fields kept for API parity
@@ -291,7 +307,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     actuator_length=(nu,), actuator_moment=(m.nJmom,), actuator_velocity=(nu,), actuator_force=(nu,),
     cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,),
     qfrc_passive=(nv,), qfrc_actuator=(nv,), qfrc_smooth=(nv,), qacc_smooth=(nv,), qfrc_constraint=(nv,),
-    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,),
+    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 17,),
     efc_J=(njmax_pad, np_), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
     efc_aref=(njmax,), efc_frictionloss=(njmax,), efc_force=(njmax,), efc_Ma=(nv,),
   )

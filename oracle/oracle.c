@@ -997,6 +997,8 @@ static void plane_box_corner(int k, const real* n, const real* ppos, const real*
 }
 
 
+#include "oracle_ccd.h"
+
 /* collision_primitive_core.py:1103-1155 sphere_box */
 static real sphere_box(real* pos, real* nrm, const real* spos, real r, const real* bpos, const real* brot, const real* bsize) {
   real dif[3] = {spos[0] - bpos[0], spos[1] - bpos[1], spos[2] - bpos[2]}, center[3], clamped[3], cdir[3], tmp[3];
@@ -1219,6 +1221,33 @@ static void collision(const orc_model* m, orc_data* d) {
       c.n = 1;
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) { /* collision_primitive.py:1117-1199 */
       capsule_box(&c, p1, n1, s1[0], s1[1], p2, r2, s2);
+    } else if (t1 == GEOM_BOX && t2 == GEOM_BOX) { /* convex (GJK/EPA) pair, collision_convex.py:701-890 */
+      ccd_geom cg1, cg2;
+      cg1.type = t1; cg2.type = t2;
+      memcpy(cg1.pos, p1, sizeof(cg1.pos)); memcpy(cg1.rot, r1, sizeof(cg1.rot)); memcpy(cg1.size, s1, sizeof(cg1.size));
+      memcpy(cg2.pos, p2, sizeof(cg2.pos)); memcpy(cg2.rot, r2, sizeof(cg2.rot)); memcpy(cg2.size, s2, sizeof(cg2.size));
+      real cdist, cnrm[3], cpts[4][3], cframe[9];
+      int nc = ccd_pair(&cg1, &cg2, m->opt_ccd_tolerance, m->opt_ccd_iterations, m->ccd_epa_iterations, margin, &cdist, cnrm, cpts);
+      make_frame(cframe, cnrm);
+      for (int k = 0; k < nc; k++) {
+        if (!(cdist < margin) || pairid0 < -1) continue;
+        int cid = *d->ncon;
+        if (cid >= d->nconmax) { (*d->ncon)++; continue; }
+        d->con_dist[cid] = cdist;
+        memcpy(d->con_pos + 3 * cid, cpts[k], 3 * sizeof(real));
+        memcpy(d->con_frame + 9 * cid, cframe, 9 * sizeof(real));
+        d->con_includemargin[cid] = margin - gap;
+        memcpy(d->con_friction + 5 * cid, friction, 5 * sizeof(real));
+        memcpy(d->con_solref + 2 * cid, solref, 2 * sizeof(real));
+        memcpy(d->con_solreffriction + 2 * cid, solreffriction, 2 * sizeof(real));
+        memcpy(d->con_solimp + 5 * cid, solimp, 5 * sizeof(real));
+        d->con_dim[cid] = condim;
+        d->con_geom[2 * cid] = g1;
+        d->con_geom[2 * cid + 1] = g2;
+        for (int i = 0; i < 10; i++) d->con_efc_address[10 * cid + i] = -1;
+        (*d->ncon)++;
+      }
+      continue;
     } else if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {
       c.n = 8; /* all 8 corners are candidates (collision_primitive.py:737-790) */
     } else {

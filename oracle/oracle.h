@@ -27,11 +27,13 @@ typedef ORC_REAL real;
 #define ORC_MODEL_INT_SCALARS(X)                                                                   \
   X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
   X(nxn) X(nmaxpyramid) X(neq) X(nsensor) X(nsensordata) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
-  X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)
+  X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)             \
+  X(opt_ccd_iterations) X(ccd_epa_iterations)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
-  X(opt_timestep) X(opt_tolerance) X(opt_ls_tolerance) X(opt_impratio_invsqrt) X(stat_meaninertia)
+  X(opt_timestep) X(opt_tolerance) X(opt_ls_tolerance) X(opt_impratio_invsqrt) X(stat_meaninertia)         \
+  X(opt_ccd_tolerance)
 
 /* ---- model: real arrays (name, element count) ---- */
 #define ORC_MODEL_REAL_ARRAYS(X)                                                                   \

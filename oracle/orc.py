@@ -93,6 +93,17 @@ def nxn_pairs(mjm):
   return pairs, pairid
 
 
+# convex (GJK/EPA) entries of MJ_COLLISION_TABLE without heightfields (collision_driver.py:42-76)
+CONVEX_PAIRS = {(2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
+
+
+def ccd_epa_iterations(mjm, pairs):
+  """EPA iteration cap: 16 when every convex pair is box-box, else opt.ccd_iterations (collision_convex.py:1127)."""
+  convex = [t for t in (tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in pairs) if t in CONVEX_PAIRS]
+  nboxbox = sum(t == (6, 6) for t in convex)
+  return 16 if convex and nboxbox == len(convex) else int(getattr(mjm.opt, "ccd_iterations", 35))
+
+
 class OracleModel:
   """Oracle view of a host MjModel (one, unbatched model)."""
 
@@ -112,6 +123,8 @@ class OracleModel:
       opt_integrator=o.integrator, opt_cone=o.cone, opt_solver=o.solver, opt_iterations=o.iterations,
       opt_ls_iterations=o.ls_iterations, opt_disableflags=o.disableflags, opt_enableflags=o.enableflags,
       opt_broadphase_filter=1 | 2 | 8,
+      opt_ccd_iterations=getattr(o, "ccd_iterations", 35), ccd_epa_iterations=ccd_epa_iterations(mjm, pairs),
+      opt_ccd_tolerance=getattr(o, "ccd_tolerance", 1e-6),
       opt_timestep=o.timestep, opt_tolerance=max(o.tolerance, 1e-6), opt_ls_tolerance=o.ls_tolerance,
       opt_impratio_invsqrt=1.0 / np.sqrt(max(o.impratio, 1e-15)), stat_meaninertia=mjm.stat.meaninertia,
     )
