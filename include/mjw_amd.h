@@ -12,6 +12,7 @@
  *   mjw_fwd_acceleration  <- forward.fwd_acceleration     forward.py:949-969
  *   mjw_solve             <- solver.solve                 solver.py:3296-3343
  *   mjw_euler             <- forward.euler                forward.py:326-354
+ *   mjw_sensor            <- sensor.sensor_pos/_vel/_acc  sensor.py:761,1377,2447
  *   mjw_ctrl_noise        <- benchmark.ctrl_noise         _src/benchmark.py:41-83
  *
  * Ownership: the caller owns every buffer (device pointers below); the library
@@ -176,6 +177,10 @@ int mjw_fwd_actuation(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_acceleration(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_solve(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+/* sensors of the stages in `stages` (bit 0: sensor_pos, sensor.py:761; bit 1: sensor_vel, :1377;
+ * bit 2: sensor_acc with rne_postconstraint, :2447) from the Data of the current step; mjw_step /
+ * mjw_forward run all three themselves, the stage entry points above run none */
+int mjw_sensor(const mjw_model_t* m, const mjw_data_t* d, int stages, void* stream);
 /* per-step control noise (Ornstein-Uhlenbeck + Halton) of the reference benchmark;
  * center: device float[nu] or NULL; world ids are d->world_offset + local id */
 /* Device self-checks of the wave primitives of the dense path (no reference counterpart):

@@ -14,8 +14,14 @@ from .forward import fwd_acceleration
 from .forward import fwd_actuation
 from .forward import fwd_position
 from .forward import fwd_velocity
+from .forward import implicit
+from .forward import sensor_acc
+from .forward import sensor_pos
+from .forward import sensor_vel
 from .forward import solve
 from .forward import step
+from .forward import step1
+from .forward import step2
 from .io import get_data_into
 from .io import make_data
 from .io import override_model
@@ -27,6 +33,11 @@ from .mjcf import MjModel
 from .mjcf import load_model
 from .mjcf import load_model_from_string
 from .mjcf import reset_data_keyframe
+from .support import contact_force
+from .support import get_state
+from .support import mul_m
+from .support import set_state
+from .support import state_size
 from .types import BiasType
 from .types import BroadphaseFilter
 from .types import BroadphaseType

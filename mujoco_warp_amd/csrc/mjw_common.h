@@ -109,6 +109,6 @@ static __device__ unsigned long long g_prof[PH_N];
 enum : int { DF_FACTOR = 1, DF_SOLVE = 2, DF_EULER = 4 };
 int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
 // post-solve sensors of every stage + rne_postconstraint, mjw_sensor.hip (no-op without sensors)
-int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
+int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages = 7);
 
 }  // namespace mjw

@@ -30,7 +30,8 @@ __host__ inline SLay make_slayout(const mjw_model_t& m) {
   return L;
 }
 
-__global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L) {
+// stages: bit 0 position, bit 1 velocity, bit 2 acceleration sensors (+ rne_postconstraint)
+__global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L, int stages) {
   extern __shared__ __attribute__((aligned(16))) float s[];
   const int wid = blockIdx.x, lane = threadIdx.x & 63;
   if (wid >= d.nworld) return;
@@ -52,7 +53,7 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   float* cfrc = s + L.cfrc;
   float* cext = s + L.cext;
   const float* cvel = s + L.cvel;
-  if (m.sensor_rne_postconstraint) {
+  if ((stages & 4) && m.sensor_rne_postconstraint) {
     // cfrc_ext = xfrc_applied moved to the subtree com (smooth.py:1278-1295)
     const float* xipos = d.xipos + wb * 3;
     for (int b = lane; b < nb; b += LPW) {
@@ -179,12 +180,12 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   const float time = d.time[wid];
   for (int k = lane; k < m.nsensor; k += LPW) {
     const int st = m.sensor_needstage[k];
-    if (st == STAGE_POS || st == STAGE_VEL)
+    if ((st == STAGE_POS && (stages & 1)) || (st == STAGE_VEL && (stages & 2)))
       sensor_posvel_one(m, d, wid, F, k, d.qpos + (long)wid * m.nq, s + L.qvel, d.actuator_length + (long)wid * m.nu,
                         d.actuator_velocity + (long)wid * m.nu, time);
   }
   // acceleration sensors (sensor.py:1697-1997, supported types), lane = sensor
-  for (int k = lane; k < m.nsensor; k += LPW) {
+  for (int k = lane; k < m.nsensor && (stages & 4); k += LPW) {
     if (m.sensor_needstage[k] != STAGE_ACC) continue;
     const int t = m.sensor_type[k], id = m.sensor_objid[k], ot = m.sensor_objtype[k];
     float v[3] = {0, 0, 0};
@@ -241,13 +242,18 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   }
 }
 
-int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
-  if (d->nworld <= 0 || m->nsensor == 0 || (m->opt_disableflags & DSBL_SENSOR)) return 0;
+int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages) {
+  if (d->nworld <= 0 || m->nsensor == 0 || (m->opt_disableflags & DSBL_SENSOR) || !stages) return 0;
   SLay L = make_slayout(*m);
   size_t lds = (size_t)L.total * 4;
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(sensor_acc_kernel, dim3(d->nworld), dim3(64), lds, s, *m, *d, L);
+  hipLaunchKernelGGL(sensor_acc_kernel, dim3(d->nworld), dim3(64), lds, s, *m, *d, L, stages);
   return (int)hipGetLastError();
 }
 
 }  // namespace mjw
+
+extern "C" int mjw_sensor(const mjw_model_t* m, const mjw_data_t* d, int stages, void* stream) {
+  if (!m || !d) return -1;
+  return mjw::sensor_launch(m, d, (hipStream_t)stream, stages & 7);
+}

@@ -83,6 +83,50 @@ def euler(m: Model, d: Data):
   _call("mjw_euler", m, d)
 
 
+def _sensor(m: Model, d: Data, stages: int):
+  L = _lib.lib()
+  _lib.check(L.mjw_sensor(cmodel(m), cdata(d), int(stages), _stream(d)), "mjw_sensor")
+
+
+def sensor_pos(m: Model, d: Data):
+  """Position-dependent sensors (sensor.py:761); valid after fwd_position."""
+  _sensor(m, d, 1)
+
+
+def sensor_vel(m: Model, d: Data):
+  """Velocity-dependent sensors (sensor.py:1377); valid after fwd_velocity."""
+  _sensor(m, d, 2)
+
+
+def sensor_acc(m: Model, d: Data):
+  """Acceleration-dependent sensors with rne_postconstraint (sensor.py:2447); valid after solve."""
+  _sensor(m, d, 4)
+
+
+def implicit(m: Model, d: Data):
+  """Implicit-in-velocity integration (forward.py:494-510); the integrator kernel dispatches on
+  opt.integrator, so this is the same launch as `euler` for implicitfast models."""
+  _call("mjw_euler", m, d)
+
+
+def step1(m: Model, d: Data):
+  """First half of `step` (forward.py:1022-1047): position and velocity stages with their sensors."""
+  fwd_position(m, d)
+  sensor_pos(m, d)
+  fwd_velocity(m, d)
+  sensor_vel(m, d)
+
+
+def step2(m: Model, d: Data):
+  """Second half of `step` after the user has set its inputs (forward.py:1050-1064): actuation,
+  acceleration, solver, acceleration sensors, integration."""
+  fwd_actuation(m, d)
+  fwd_acceleration(m, d)
+  solve(m, d)
+  sensor_acc(m, d)
+  euler(m, d)
+
+
 def _forward_staged(m: Model, d: Data):
   fwd_position(m, d)
   fwd_velocity(m, d)
@@ -91,6 +135,7 @@ def _forward_staged(m: Model, d: Data):
   fwd_actuation(m, d)
   fwd_acceleration(m, d)
   solve(m, d)
+  _sensor(m, d, 7)
 
 
 def forward(m: Model, d: Data):

@@ -1,0 +1,151 @@
+"""Reference API surface around the step path: get_state / set_state,
+contact_force, mul_m, step1 / step2, the sensor stage functions.
+
+CPU tests run the torch-side helpers on CPU tensors; `-m gpu` tests check that the split / staged
+entry points reproduce the fused step.
+"""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.common import HUMANOID, ROOT, np_
+
+APOLLO = os.path.join(ROOT, "models", "apptronik_apollo", "scene_flat.xml")
+
+
+def _cpu_data(path, nworld=3):
+  import mujoco_warp_amd as mjw
+
+  mjm = mjw.load_model(path)
+  m = mjw.put_model(mjm, device="cpu")
+  d = mjw.make_data(mjm, nworld=nworld, nconmax=8, njmax=32, device="cpu", m=m)
+  return mjm, m, d
+
+
+def test_state_roundtrip_and_size():
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd.types import State
+
+  mjm, m, d = _cpu_data(HUMANOID)
+  g = torch.Generator().manual_seed(0)
+  for name in ("qpos", "qvel", "ctrl", "qacc_warmstart", "qfrc_applied", "xfrc_applied", "time"):
+    getattr(d, name).copy_(torch.rand(getattr(d, name).shape, generator=g))
+  sig = int(State.INTEGRATION)
+  n = mjw.state_size(m, sig)
+  assert n == 1 + mjm.nq + mjm.nv + mjm.na + mjm.nv + mjm.nu + mjm.nv + 6 * mjm.nbody  # mj_stateSize
+  st = torch.zeros((d.nworld, n))
+  mjw.get_state(m, d, st, sig)
+  assert torch.equal(st[:, 1 : 1 + mjm.nq], d.qpos)
+  _, _, d2 = _cpu_data(HUMANOID)
+  mjw.set_state(m, d2, st, sig)
+  for name in ("qpos", "qvel", "ctrl", "qacc_warmstart", "qfrc_applied", "xfrc_applied", "time"):
+    assert torch.equal(getattr(d2, name), getattr(d, name)), name
+  # per-world mask: only world 1 is written
+  _, _, d3 = _cpu_data(HUMANOID)
+  mjw.set_state(m, d3, st, int(State.QPOS), active=torch.tensor([False, True, False]))
+  assert torch.equal(d3.qpos[1], st[1, : mjm.nq]) and torch.equal(d3.qpos[0], torch.as_tensor(mjm.qpos0, dtype=torch.float32))
+  with pytest.raises(ValueError):
+    mjw.get_state(m, d, st, 1 << 13)
+
+
+def test_contact_force_decodes_pyramid():
+  """Pyramidal rows (f1+, f1-, f2+, f2-) -> normal = sum, tangent_i = (f_i+ - f_i-) mu_i (support.py:241-263)."""
+  import mujoco_warp_amd as mjw
+
+  mjm, m, d = _cpu_data(HUMANOID)
+  d.nacon[0] = 2
+  d.contact.dim[:2] = torch.tensor([3, 1])
+  d.contact.worldid[:2] = torch.tensor([1, 2])
+  d.contact.efc_address[0, :4] = torch.tensor([5, 6, 7, 8])
+  d.contact.efc_address[1, :1] = torch.tensor([3])
+  d.contact.friction[0] = torch.tensor([0.5, 0.25, 0.1, 0.1, 0.1])
+  d.efc.force[1, 5:9] = torch.tensor([1.0, 2.0, 4.0, 3.0])
+  d.efc.force[2, 3] = 7.0
+  R = torch.tensor([[0.0, 0.0, 1.0], [1.0, 0.0, 0.0], [0.0, 1.0, 0.0]])
+  d.contact.frame[0] = R
+  force = torch.zeros((3, 6))
+  mjw.contact_force(m, d, torch.tensor([0, 1, 5]), False, force)
+  np.testing.assert_allclose(force[0].numpy(), [10.0, -0.5, 0.25, 0, 0, 0], atol=1e-6)
+  np.testing.assert_allclose(force[1].numpy(), [7.0, 0, 0, 0, 0, 0])
+  assert torch.all(force[2] == 0)  # id >= nacon
+  mjw.contact_force(m, d, torch.tensor([0]), True, force[:1])
+  np.testing.assert_allclose(force[0, :3].numpy(), (torch.tensor([10.0, -0.5, 0.25]) @ R).numpy(), atol=1e-6)
+
+
+def test_mul_m_dense():
+  import mujoco_warp_amd as mjw
+
+  mjm, m, d = _cpu_data(HUMANOID)
+  nv = mjm.nv
+  A = torch.rand((d.nworld, nv, nv))
+  d.qM[:, :nv, :nv] = A + A.transpose(1, 2)
+  v = torch.rand((d.nworld, nv))
+  res = torch.zeros_like(v)
+  mjw.mul_m(m, d, res, v, skip=torch.tensor([False, True, False]))
+  want = torch.einsum("wij,wj->wi", d.qM[:, :nv, :nv], v)
+  assert torch.allclose(res[0], want[0]) and torch.all(res[1] == 0) and torch.allclose(res[2], want[2])
+
+
+# ---- GPU ---------------------------------------------------------------------------------------
+def _apollo_gpu(nworld=16, seed=0):
+  import mujoco_warp_amd as mjw
+  from tests.common import gpu_from_state
+
+  mjm = mjw.load_model(APOLLO)
+  rng = np.random.default_rng(seed)
+  qpos = np.tile(mjm.key_qpos[0], (nworld, 1))
+  qpos[:, 7:] += rng.normal(0, 0.05, (nworld, mjm.nq - 7))
+  qvel = rng.normal(0, 0.2, (nworld, mjm.nv))
+  ctrl = np.tile(mjm.key_ctrl[0], (nworld, 1))
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=64, nconmax=16)
+  m2, d2 = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=64, nconmax=16)
+  return mjm, m, d, m2, d2
+
+
+@pytest.mark.gpu
+def test_gpu_step1_step2_equals_step():
+  import mujoco_warp_amd as mjw
+
+  mjm, m, d, m2, d2 = _apollo_gpu()
+  for _ in range(3):
+    mjw.step(m, d)
+    mjw.step1(m2, d2)
+    mjw.step2(m2, d2)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(np_(d.qpos), np_(d2.qpos))
+  np.testing.assert_array_equal(np_(d.sensordata), np_(d2.sensordata))
+
+
+@pytest.mark.gpu
+def test_gpu_callbacks_take_the_staged_path_with_sensors():
+  import mujoco_warp_amd as mjw
+
+  mjm, m, d, m2, d2 = _apollo_gpu(seed=1)
+  calls = []
+  m2.callback.control = lambda mm, dd: calls.append(1)
+  mjw.forward(m, d)
+  mjw.forward(m2, d2)
+  torch.cuda.synchronize()
+  assert calls == [1]
+  np.testing.assert_array_equal(np_(d.sensordata), np_(d2.sensordata))
+  np.testing.assert_array_equal(np_(d.qacc), np_(d2.qacc))
+
+
+@pytest.mark.gpu
+def test_gpu_get_set_state_roundtrip():
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd.types import State
+
+  mjm, m, d, m2, d2 = _apollo_gpu(seed=2)
+  mjw.step(m, d)
+  sig = int(State.FULLPHYSICS | State.CTRL | State.WARMSTART)
+  st = torch.zeros((d.nworld, mjw.state_size(m, sig)), device=d.qpos.device)
+  mjw.get_state(m, d, st, sig)
+  mjw.set_state(m2, d2, st, sig)
+  mjw.step(m, d)
+  mjw.step(m2, d2)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(np_(d.qpos), np_(d2.qpos))
