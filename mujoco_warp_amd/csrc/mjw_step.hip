@@ -1054,16 +1054,13 @@ __device__ __forceinline__ void put_J(const mjw_data_t& d, const Lay& L, float* 
   else d.efc_J[((long)wid * d.njmax_pad + r) * np + k] = v;
 }
 
-// support.py:396-432 restricted to one dof; returns jacp, jacr (zero when not in tree)
+// support.py:396-432 restricted to one dof; returns jacp, jacr (zero when not in tree).  The
+// reference walks bodyid's ancestors looking for the dof's body; with bodies in DFS pre-order that
+// is the range test db <= bodyid < subtree_end(db), so the per-lane (db, dend) pair is loaded once
+// by the caller instead of a chain of dependent parent loads per contact.
 __device__ __forceinline__ void jac_dof(const mjw_model_t& m, const Lay& L, const float* s, const float* point, int bodyid,
-                                        int dofid, float* jacp, float* jacr) {
-  int db = m.dof_bodyid[dofid];
-  bool in_tree = db == 0;
-  int p = bodyid;
-  while (p != 0) {
-    if (p == db) { in_tree = true; break; }
-    p = m.body_parentid[p];
-  }
+                                        int dofid, int db, int dend, float* jacp, float* jacr) {
+  const bool in_tree = db == 0 || (bodyid >= db && bodyid < dend);
   if (!in_tree) { jacp[0] = jacp[1] = jacp[2] = jacr[0] = jacr[1] = jacr[2] = 0.0f; return; }
   int root = m.body_rootid[bodyid];
   float off[3];
@@ -1086,6 +1083,9 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
   const int np = m.nv_pad;
   const int kJ = L.J >= 0 ? nv : np;  // global rows also get their zero padding
   const int CM = L.cmax;
+  // this lane's dof body and its DFS subtree end (jac_dof's ancestor test), loaded once
+  const int dof_db = lane < nv ? m.dof_bodyid[lane] : 0;
+  const int dof_dend = lane < nv ? m.body_subtree_end[dof_db] : 0;
   WSYNC();  // contact staging may alias the qM region read by crb_qM
 
   // --- joint equality rows (constraint.py:367-495), in equality index order
@@ -1413,8 +1413,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         float jdp[3] = {0.0f, 0.0f, 0.0f}, jdr[3] = {0.0f, 0.0f, 0.0f};
         if (i < nv) {
           float j1p[3], j1r[3], j2p[3], j2r[3];
-          jac_dof(m, L, s, cpos, b1, i, j1p, j1r);
-          jac_dof(m, L, s, cpos, b2, i, j2p, j2r);
+          jac_dof(m, L, s, cpos, b1, i, dof_db, dof_dend, j1p, j1r);
+          jac_dof(m, L, s, cpos, b2, i, dof_db, dof_dend, j2p, j2r);
           for (int k = 0; k < 3; k++) { jdp[k] = j2p[k] - j1p[k]; jdr[k] = j2r[k] - j1r[k]; }
         }
         const float qv = i < nv ? qvel[i] : 0.0f;
@@ -1497,13 +1497,18 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
   float* s = w.s;
   int* si = w.si;
   const float* gear_all = MR(actuator_gear);
-  for (int a = lane; a < m.nu; a += LPW) {
-    // rowadr = sum of previous actuators' nnz (deterministic order)
-    int rowadr = 0;
-    for (int a2 = 0; a2 < a; a2++) {
-      int jt2 = m.jnt_type[m.actuator_trnid[2 * a2]];
-      rowadr += jt2 == JNT_FREE ? 6 : (jt2 == JNT_BALL ? 3 : 1);
+  int carry = 0;  // moment rows are packed in actuator order: rowadr = exclusive scan of nnz
+  for (int a0 = 0; a0 < m.nu; a0 += LPW) {
+    const int a = a0 + lane;
+    int my_nnz = 0;
+    if (a < m.nu) {
+      const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
+      my_nnz = jt0 == JNT_FREE ? 6 : (jt0 == JNT_BALL ? 3 : 1);
     }
+    const int incl = wave_scan_incl(my_nnz);
+    const int rowadr = carry + incl - my_nnz;
+    carry += __shfl(incl, 63, 64);
+    if (a >= m.nu) continue;
     const float* gear = gear_all + 6 * a;
     int trn = m.actuator_trntype[a];
     int j = m.actuator_trnid[2 * a];
@@ -1802,25 +1807,36 @@ __device__ __forceinline__ void fwd_acceleration(const mjw_model_t& m, const mjw
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
   const int nv = m.nv, nvs = L.nvs;
+  // xfrc_accumulate (support.py:174-237): the body force (f, t) applied at xipos maps to dof i as
+  // jac(xipos)^T (f, t) = cdof_i . W_b with W_b = (t + off x f, f), off = xipos - subtree_com(root).
+  // Summing W over the DFS subtree range [db, subtree_end) of the dof's body gives one 6-vector
+  // dot per dof; the xfrc rows are read once, coalesced (cacc / cfrc LDS slots are dead here).
+  float* Wb = s + L.cacc;
+  float* Ws = s + L.cfrc;
+  const float* xfrc = d.xfrc_applied + (long)wid * m.nbody * 6;
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float f[3] = {xfrc[6 * b], xfrc[6 * b + 1], xfrc[6 * b + 2]}, off[3], c[3];
+    for (int k = 0; k < 3; k++) off[k] = s[L.xipos + 3 * b + k] - s[L.subtree_com + 3 * m.body_rootid[b] + k];
+    cross3(c, off, f);
+    for (int k = 0; k < 3; k++) { Wb[6 * b + k] = xfrc[6 * b + 3 + k] + c[k]; Wb[6 * b + 3 + k] = f[k]; }
+  }
+  WSYNC();
+  for (int b = lane; b < m.nbody; b += LPW) {
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+    const int end = m.body_subtree_end[b];
+    for (int j = b; j < end; j++)
+      for (int k = 0; k < 6; k++) acc[k] += Wb[6 * j + k];
+    for (int k = 0; k < 6; k++) Ws[6 * b + k] = acc[k];
+  }
+  WSYNC();
   float qs = 0.0f;
   if (lane < nv) {
     int i = lane;
     long gi = (long)wid * nv + i;
     qs = s[L.qfrc_passive + i] - s[L.qfrc_bias + i] + s[L.qfrc_actuator + i] + d.qfrc_applied[gi];
-    // xfrc_accumulate: bodies in the subtree of dof_bodyid form the DFS range [db, subtree_end)
     const float* cd = s + L.cdof + 6 * i;
-    int db = m.dof_bodyid[i];
-    float acc = 0.0f;
-    const float* xfrc = d.xfrc_applied + (long)wid * m.nbody * 6;
-    for (int b = db; b < m.body_subtree_end[db]; b++) {
-      const float* ft = xfrc + 6 * b;
-      if (ft[0] == 0.0f && ft[1] == 0.0f && ft[2] == 0.0f && ft[3] == 0.0f && ft[4] == 0.0f && ft[5] == 0.0f) continue;
-      float off[3], c[3];
-      for (int k = 0; k < 3; k++) off[k] = s[L.xipos + 3 * b + k] - s[L.subtree_com + 3 * m.body_rootid[b] + k];
-      cross3(c, cd, off);
-      acc += cd[3] * ft[0] + cd[4] * ft[1] + cd[5] * ft[2] + cd[0] * ft[3] + cd[1] * ft[4] + cd[2] * ft[5] + dot3(c, ft);
-    }
-    qs += acc;
+    const float* W = Ws + 6 * m.dof_bodyid[i];
+    qs += cd[0] * W[0] + cd[1] * W[1] + cd[2] * W[2] + cd[3] * W[3] + cd[4] * W[4] + cd[5] * W[5];
     s[L.qfrc_smooth + i] = qs;
     d.qfrc_smooth[gi] = qs;
   }
