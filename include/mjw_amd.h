@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 5
+#define MJW_ABI_VERSION 6
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -82,6 +82,7 @@
   X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
+  X(actuator_actearly, nu)                                                                         \
   X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2) X(nxn_ccdid, nxn)                               \
   X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)                                             \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
@@ -106,7 +107,8 @@
   X(cfrc_ext, nbody * 6)                                                                           \
   X(efc_J, njmax_pad * nv_pad) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax_pad)         \
   X(efc_vel, njmax) X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax)             \
-  X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 17)
+  X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 17)                                 \
+  X(qpos_t0, nq) X(qvel_t0, nv) X(act_t0, na) X(qvel_rk, nv) X(qacc_rk, nv) X(act_dot_rk, na)
 
 /* ---- data: int arrays, (nworld, count) ---- */
 #define MJW_DATA_INT_ARRAYS(X)                                                                     \
@@ -181,6 +183,14 @@ int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream);
  * bit 2: sensor_acc with rne_postconstraint, :2447) from the Data of the current step; mjw_step /
  * mjw_forward run all three themselves, the stage entry points above run none */
 int mjw_sensor(const mjw_model_t* m, const mjw_data_t* d, int stages, void* stream);
+/* Runge-Kutta 4 (forward.py:457-491 rungekutta4): expects `forward` to have run on the current state
+ * (mjw_step does this itself for RK4 models); runs three more forward passes and advances the state.
+ * The t0 copies and the weighted sums live in the Data workspace fields qpos_t0 ... act_dot_rk. */
+int mjw_rungekutta4(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+/* one RK4 bookkeeping op, for hosts that run `forward` themselves between them (Python callbacks):
+ * op 0 = save t0 and accumulate B[0] (scale), 1 = _rk_perturb_state (forward.py:357-399),
+ * 2 = _rk_accumulate (:402-454), 3 = restore t0 and _advance (:484-491, :213-274) */
+int mjw_rk4_op(const mjw_model_t* m, const mjw_data_t* d, int op, float scale, void* stream);
 /* per-step control noise (Ornstein-Uhlenbeck + Halton) of the reference benchmark;
  * center: device float[nu] or NULL; world ids are d->world_offset + local id */
 /* Device self-checks of the wave primitives of the dense path (no reference counterpart):

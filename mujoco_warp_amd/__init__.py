@@ -20,6 +20,7 @@ from .forward import sensor_pos
 from .forward import sensor_vel
 from .forward import solve
 from .forward import step
+from .forward import rungekutta4
 from .forward import step1
 from .forward import step2
 from .io import get_data_into

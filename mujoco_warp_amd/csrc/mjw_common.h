@@ -25,7 +25,7 @@ enum : int { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
 enum : int { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICIT = 2, INT_IMPLICITFAST = 3 };
 enum : int { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
 enum : int { BIAS_NONE = 0, BIAS_AFFINE = 1 };
-enum : int { DYN_NONE = 0 };
+enum : int { DYN_NONE = 0, DYN_INTEGRATOR = 1, DYN_FILTER = 2, DYN_FILTEREXACT = 3, DYN_MUSCLE = 4, DYN_USER = 5 };
 enum : int {
   DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16, DSBL_SPRING = 32,
   DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512, DSBL_ACTUATION = 2048,
@@ -53,6 +53,22 @@ __device__ __forceinline__ const float* mb(const float* p, int nb, int cnt, int 
   return nb <= 1 ? p : p + (long)(w % nb) * cnt;
 }
 #define MR(name) mb(m.name, m.name##_nb, m.name##_cnt, wid)
+
+// support.py:38-64 next_act: one activation advanced by scale * act_dot over the timestep dt
+// (FILTEREXACT integrates the first-order filter exactly; USER activations are left to the user)
+__device__ __forceinline__ float next_act(float dt, int dyntype, float tau_prm, const float* actrange, float act, float act_dot,
+                                          float scale, bool clamp) {
+  float a;
+  if (dyntype == DYN_FILTEREXACT) {
+    const float tau = fmaxf(MJW_MINVAL, tau_prm);
+    a = act + scale * act_dot * tau * (1.0f - expf(-dt / tau));
+  } else if (dyntype == DYN_USER) {
+    return act;
+  } else {
+    a = act + scale * act_dot * dt;
+  }
+  return clamp ? clampf(a, actrange[0], actrange[1]) : a;
+}
 
 
 // ---- wave primitives ------------------------------------------------------------------------
@@ -109,6 +125,8 @@ static __device__ unsigned long long g_prof[PH_N];
 enum : int { DF_FACTOR = 1, DF_SOLVE = 2, DF_EULER = 4 };
 int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
 // post-solve sensors of every stage + rne_postconstraint, mjw_sensor.hip (no-op without sensors)
+enum : int { RK_BEGIN = 0, RK_PERTURB = 1, RK_ACCUM = 2, RK_END = 3 };
+int rk4_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int op, float scale);
 int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages = 7);
 
 }  // namespace mjw

@@ -191,7 +191,12 @@ __device__ __forceinline__ float actuator_vel_deriv(const mjw_model_t& m, const 
   }
   float vel = bias;
   if (m.actuator_dyntype[a] != DYN_NONE) {
-    if (gain != 0.0f) vel += gain * d.act[(long)wid * m.na + m.actuator_actadr[a] + m.actuator_actnum[a] - 1];
+    if (gain != 0.0f) {  // derivative.py:86-101: actearly differentiates at the next activation
+      const long ga = (long)wid * m.na + m.actuator_actadr[a] + m.actuator_actnum[a] - 1;
+      vel += gain * (m.actuator_actearly[a] ? next_act(MR(opt_timestep)[0], m.actuator_dyntype[a], MR(actuator_dynprm)[10 * a], MR(actuator_actrange) + 2 * a,
+                                                       d.act[ga], d.act_dot[ga], 1.0f, m.actuator_actlimited[a] != 0)
+                                            : d.act[ga]);
+    }
   } else if (gain != 0.0f) {
     vel += gain * d.ctrl[(long)wid * m.nu + a];
   }
@@ -571,9 +576,8 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d) {
       int adr = m.actuator_actadr[u];
       for (int j = adr; adr >= 0 && j < adr + m.actuator_actnum[u]; j++) {
         long ga = (long)wid * m.na + j;
-        float act = d.act[ga] + d.act_dot[ga] * dt;
-        if (m.actuator_actlimited[u]) act = clampf(act, actrange[2 * u], actrange[2 * u + 1]);
-        d.act[ga] = act;
+        d.act[ga] = next_act(dt, m.actuator_dyntype[u], MR(actuator_dynprm)[10 * u], actrange + 2 * u, d.act[ga], d.act_dot[ga], 1.0f,
+                             m.actuator_actlimited[u] != 0);
       }
     }
     float qvel = dof ? d.qvel[gi] + qacc_adv * dt : 0.0f;

@@ -1769,10 +1769,13 @@ __device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_da
       int dt = m.actuator_dyntype[a];
       float act = d.act[(long)wid * m.na + act_last];
       float act_dot = 0.0f;
-      if (dt == 1) act_dot = ctrl;                                               // INTEGRATOR
-      else if (dt == 2 || dt == 3) act_dot = (ctrl - act) / fmaxf(dynprm[10 * a], MJW_MINVAL);  // FILTER(EXACT)
+      if (dt == DYN_INTEGRATOR) act_dot = ctrl;
+      else if (dt == DYN_FILTER || dt == DYN_FILTEREXACT) act_dot = (ctrl - act) / fmaxf(dynprm[10 * a], MJW_MINVAL);
       d.act_dot[(long)wid * m.na + act_last] = act_dot;
-      ctrl_act = act;  // actearly not supported by this build's compiler
+      // actearly (forward.py:682-697): the force sees the activation of the next step
+      ctrl_act = m.actuator_actearly[a] ? next_act(MR(opt_timestep)[0], dt, dynprm[10 * a], MR(actuator_actrange) + 2 * a, act, act_dot, 1.0f,
+                                                   m.actuator_actlimited[a] != 0)
+                                        : act;
     }
     float len = s[L.act_len + a], vel = s[L.act_vel + a];
     const float* gp = gainprm + 10 * a;
@@ -2145,9 +2148,8 @@ __device__ __forceinline__ void euler(const mjw_model_t& m, const mjw_data_t& d,
     int adr = m.actuator_actadr[a];
     for (int j = adr; adr >= 0 && j < adr + m.actuator_actnum[a]; j++) {
       long ga = (long)wid * m.na + j;
-      float act = d.act[ga] + d.act_dot[ga] * dt;
-      if (m.actuator_actlimited[a]) act = clampf(act, actrange[2 * a], actrange[2 * a + 1]);
-      d.act[ga] = act;
+      d.act[ga] = next_act(dt, m.actuator_dyntype[a], MR(actuator_dynprm)[10 * a], actrange + 2 * a, d.act[ga], d.act_dot[ga], 1.0f,
+                           m.actuator_actlimited[a] != 0);
     }
   }
   float* qvel = s + L.qvel;
@@ -2484,6 +2486,33 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     default: g_err = std::string(name) + ": unsupported stage group"; return -4;
   }
 }
+
+constexpr int ST_FORWARD = mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE;
+
+// forward.py:457-491 rungekutta4, after `forward` ran on the current state: three more forward
+// passes at the perturbed states, each followed by the accumulation of its stage derivative
+int rungekutta4(const mjw_model_t* m, const mjw_data_t* d, void* stream, const char* name) {
+  using namespace mjw;
+  hipStream_t s = (hipStream_t)stream;
+  const float A[3] = {0.5f, 0.5f, 1.0f};
+  const float B[4] = {1.0f / 6.0f, 1.0f / 3.0f, 1.0f / 3.0f, 1.0f / 6.0f};
+  int rc = set_err((hipError_t)rk4_launch(m, d, s, RK_BEGIN, B[0]), name);
+  for (int i = 0; i < 3 && !rc; i++) {
+    rc = set_err((hipError_t)rk4_launch(m, d, s, RK_PERTURB, A[i]), name);
+    if (!rc) rc = run(m, d, stream, ST_FORWARD, name);
+    if (!rc) rc = set_err((hipError_t)rk4_launch(m, d, s, RK_ACCUM, B[i + 1]), name);
+  }
+  return rc ? rc : set_err((hipError_t)rk4_launch(m, d, s, RK_END, 0.0f), name);
+}
+
+// forward.py:1003-1018 step: forward, then the integrator the model selects
+int step(const mjw_model_t* m, const mjw_data_t* d, void* stream, const char* name) {
+  if (m && d && m->opt_integrator == mjw::INT_RK4) {
+    const int rc = run(m, d, stream, ST_FORWARD, name);
+    return rc ? rc : rungekutta4(m, d, stream, name);
+  }
+  return run(m, d, stream, ST_FORWARD | mjw::ST_EULER, name);
+}
 }  // namespace
 
 MJW_PROF_READER(mjw_prof_read)
@@ -2499,14 +2528,21 @@ int mjw_lds_bytes(const mjw_model_t* m, int njmax) {
   return mjw::make_layout(*m, njmax, m->nv <= 32 && njmax <= 64).total * 4;
 }
 
-int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
-  return run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE | mjw::ST_EULER, "mjw_step");
+int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream) { return step(m, d, stream, "mjw_step"); }
+int mjw_rungekutta4(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  if (!m || !d) { g_err = "mjw_rungekutta4: null model/data"; return -1; }
+  return rungekutta4(m, d, stream, "mjw_rungekutta4");
+}
+int mjw_rk4_op(const mjw_model_t* m, const mjw_data_t* d, int op, float scale, void* stream) {
+  if (!m || !d) { g_err = "mjw_rk4_op: null model/data"; return -1; }
+  if (op < mjw::RK_BEGIN || op > mjw::RK_END) { g_err = "mjw_rk4_op: op must be 0..3"; return -4; }
+  return set_err((hipError_t)mjw::rk4_launch(m, d, (hipStream_t)stream, op, scale), "mjw_rk4_op");
 }
 int mjw_step_events(const mjw_model_t* m, const mjw_data_t* d, void* stream, void* ev_begin, void* ev_mid, void* ev_end) {
   g_ev[0] = (hipEvent_t)ev_begin;
   g_ev[1] = (hipEvent_t)ev_mid;
   g_ev[2] = (hipEvent_t)ev_end;
-  int rc = run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE | mjw::ST_EULER, "mjw_step_events");
+  int rc = step(m, d, stream, "mjw_step_events");
   g_ev[0] = g_ev[1] = g_ev[2] = nullptr;
   return rc;
 }

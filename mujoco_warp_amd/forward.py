@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from .io import cdata, cmodel
-from .types import Data, DisableBit, Model
+from .types import Data, DisableBit, IntegratorType, Model
 
 
 def _stream(d: Data):
@@ -109,6 +109,37 @@ def implicit(m: Model, d: Data):
   _call("mjw_euler", m, d)
 
 
+def _rk4_op(m: Model, d: Data, op: int, scale: float):
+  L = _lib.lib()
+  _lib.check(L.mjw_rk4_op(cmodel(m), cdata(d), int(op), float(scale), _stream(d)), "mjw_rk4_op")
+
+
+def rungekutta4(m: Model, d: Data):
+  """Runge-Kutta explicit order 4 integrator (forward.py:457-491); call after `forward`.
+
+  Without Python callbacks the three inner forward passes and the bookkeeping run inside the
+  library (mjw_rungekutta4); with callbacks the inner passes go through `forward` here so the
+  callbacks see every stage, and the bookkeeping launches the same device ops one by one."""
+  if not _has_callbacks(m):
+    _call("mjw_rungekutta4", m, d)
+    return
+  A = (0.5, 0.5, 1.0)
+  B = (1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0)
+  _rk4_op(m, d, 0, B[0])
+  for i in range(3):
+    _rk4_op(m, d, 1, A[i])
+    forward(m, d)
+    _rk4_op(m, d, 2, B[i + 1])
+  _rk4_op(m, d, 3, 0.0)
+
+
+def _integrate(m: Model, d: Data):
+  if m.opt.integrator == IntegratorType.RK4:
+    rungekutta4(m, d)
+  else:
+    euler(m, d)
+
+
 def step1(m: Model, d: Data):
   """First half of `step` (forward.py:1022-1047): position and velocity stages with their sensors."""
   fwd_position(m, d)
@@ -124,7 +155,7 @@ def step2(m: Model, d: Data):
   fwd_acceleration(m, d)
   solve(m, d)
   sensor_acc(m, d)
-  euler(m, d)
+  _integrate(m, d)
 
 
 def _forward_staged(m: Model, d: Data):
@@ -150,7 +181,7 @@ def step(m: Model, d: Data):
   """Advance simulation (forward.py:1003-1018)."""
   if _has_callbacks(m):
     _forward_staged(m, d)
-    euler(m, d)
+    _integrate(m, d)
   else:
     _call("mjw_step", m, d)
 

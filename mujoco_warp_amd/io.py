@@ -102,7 +102,7 @@ def put_model(mjm, device=None) -> types.Model:
   for g in np.unique(mjm.geom_type):
     if int(g) not in _SUPPORTED_GEOMS:
       raise NotImplementedError(f"geom type {types.GeomType(int(g)).name} not supported.")
-  if mjm.opt.integrator not in (types.IntegratorType.EULER, types.IntegratorType.IMPLICITFAST):
+  if mjm.opt.integrator not in (types.IntegratorType.EULER, types.IntegratorType.RK4, types.IntegratorType.IMPLICITFAST):
     raise NotImplementedError(f"{types.IntegratorType(mjm.opt.integrator).name} is unsupported.")
   if mjm.opt.cone != types.ConeType.PYRAMIDAL:
     raise NotImplementedError("ELLIPTIC is unsupported.")
@@ -128,6 +128,9 @@ def put_model(mjm, device=None) -> types.Model:
   if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
       tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) == (6, 6) for a, b in pairs_chk):
     raise NotImplementedError("box-box with NATIVECCD disabled (primitive box_box) is not supported by this build yet.")
+  if mjm.nu and (np.any(mjm.actuator_dyntype == types.DynType.MUSCLE) or np.any(mjm.actuator_gaintype == types.GainType.MUSCLE)
+                 or np.any(mjm.actuator_biastype == types.BiasType.MUSCLE)):
+    raise NotImplementedError("muscle actuators are not supported by this build yet.")
   if np.any(mjm.actuator_trntype > types.TrnType.JOINTINPARENT):
     raise NotImplementedError("only joint transmissions are supported.")
 
@@ -310,6 +313,8 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 17,),
     efc_J=(njmax_pad, np_), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
     efc_aref=(njmax,), efc_frictionloss=(njmax,), efc_force=(njmax,), efc_Ma=(nv,),
+    # RK4 workspace (forward.py:462-472 temporaries; kept resident so a step allocates nothing)
+    qpos_t0=(nq,), qvel_t0=(nv,), act_t0=(na,), qvel_rk=(nv,), qacc_rk=(nv,), act_dot_rk=(na,),
   )
   ints = dict(
     ne=(), nf=(), nl=(), nefc=(), solver_niter=(), moment_rownnz=(nu,), moment_rowadr=(nu,), moment_colind=(m.nJmom,),

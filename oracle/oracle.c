@@ -32,7 +32,7 @@ enum { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
 enum { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICITFAST = 3 };
 enum { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
 enum { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
-enum { DYN_NONE = 0 };
+enum { DYN_NONE = 0, DYN_INTEGRATOR = 1, DYN_FILTER = 2, DYN_FILTEREXACT = 3, DYN_MUSCLE = 4, DYN_USER = 5 };
 enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
 enum { INTEGRATOR_EULER = 0, INTEGRATOR_RK4 = 1, INTEGRATOR_IMPLICIT = 2, INTEGRATOR_IMPLICITFAST = 3 };
 enum { BIAS_NONE = 0, BIAS_AFFINE = 1 };
@@ -1495,11 +1495,27 @@ static void fwd_velocity(const orc_model* m, orc_data* d) {
   rne(m, d);
 }
 
-/* forward.py:616-927 (na = 0 path + general gain/bias) */
+/* support.py:38-64 next_act */
+static real next_act(const orc_model* m, int a, real act, real act_dot, real scale, int clamp) {
+  real dt = m->opt_timestep, r;
+  int dyn = m->actuator_dyntype[a];
+  if (dyn == DYN_FILTEREXACT) {
+    real tau = maxr(MINVAL, m->actuator_dynprm[10 * a]);
+    r = act + scale * act_dot * tau * (1 - exp(-dt / tau));
+  } else if (dyn == DYN_USER) {
+    return act;
+  } else {
+    r = act + scale * act_dot * dt;
+  }
+  return clamp ? clampr(r, m->actuator_actrange[2 * a], m->actuator_actrange[2 * a + 1]) : r;
+}
+
+/* forward.py:616-927: activation dynamics (integrator / filter / filterexact), actearly, gain/bias */
 static void fwd_actuation(const orc_model* m, orc_data* d) {
   int nv = m->nv;
   if (!m->nu || (m->opt_disableflags & DSBL_ACTUATION)) {
     memset(d->qfrc_actuator, 0, nv * sizeof(real));
+    if (m->na) memset(d->act_dot, 0, m->na * sizeof(real));
     return;
   }
   for (int a = 0; a < m->nu; a++) {
@@ -1508,7 +1524,14 @@ static void fwd_actuation(const orc_model* m, orc_data* d) {
       ctrl = clampr(ctrl, m->actuator_ctrlrange[2 * a], m->actuator_ctrlrange[2 * a + 1]);
     real ctrl_act = ctrl;
     int act_first = m->actuator_actadr[a];
-    if (m->na && act_first >= 0) ctrl_act = d->act[act_first + m->actuator_actnum[a] - 1];
+    if (m->na && act_first >= 0) {
+      int last = act_first + m->actuator_actnum[a] - 1, dyn = m->actuator_dyntype[a];
+      real act = d->act[last], act_dot = 0;
+      if (dyn == DYN_INTEGRATOR) act_dot = ctrl;
+      else if (dyn == DYN_FILTER || dyn == DYN_FILTEREXACT) act_dot = (ctrl - act) / maxr(m->actuator_dynprm[10 * a], MINVAL);
+      d->act_dot[last] = act_dot;
+      ctrl_act = m->actuator_actearly[a] ? next_act(m, a, act, act_dot, 1, m->actuator_actlimited[a]) : act;
+    }
     real len = d->actuator_length[a], vel = d->actuator_velocity[a];
     const real* gp = m->actuator_gainprm + 10 * a;
     const real* bp = m->actuator_biasprm + 10 * a;
@@ -1814,9 +1837,7 @@ static void euler_advance(const orc_model* m, orc_data* d, const real* qacc_adv)
   for (int a = 0; a < m->nu; a++) {
     int adr = m->actuator_actadr[a];
     for (int j = adr; j >= 0 && j < adr + m->actuator_actnum[a]; j++) {
-      real act = d->act[j] + d->act_dot[j] * dt;
-      if (m->actuator_actlimited[a]) act = clampr(act, m->actuator_actrange[2 * a], m->actuator_actrange[2 * a + 1]);
-      d->act[j] = act;
+      d->act[j] = next_act(m, a, d->act[j], d->act_dot[j], 1, m->actuator_actlimited[a]);
     }
   }
   for (int i = 0; i < nv; i++) d->qvel[i] = d->qvel[i] + qacc_adv[i] * dt;
@@ -1878,7 +1899,10 @@ static real actuator_vel_deriv(const orc_model* m, const orc_data* d, int a) {
   }
   real vel = bias;
   if (m->actuator_dyntype[a] != DYN_NONE) {
-    if (gain != 0) vel += gain * d->act[m->actuator_actadr[a] + m->actuator_actnum[a] - 1]; /* actearly not supported */
+    if (gain != 0) {
+      int adr = m->actuator_actadr[a] + m->actuator_actnum[a] - 1;
+      vel += gain * (m->actuator_actearly[a] ? next_act(m, a, d->act[adr], d->act_dot[adr], 1, m->actuator_actlimited[a]) : d->act[adr]);
+    }
   } else if (gain != 0) {
     vel += gain * d->ctrl[a];
   }
@@ -2280,10 +2304,69 @@ static void forward_world(const orc_model* m, orc_data* d) {
   if (sensors) sensor_acc(m, d);
 }
 
+/* forward.py:51-109 _next_position: out = in (+) dt * scale * qvel (quaternions integrated) */
+static void next_position(const orc_model* m, const real* qin, const real* qvel, real scale, real* qout) {
+  real dt = m->opt_timestep;
+  for (int j = 0; j < m->njnt; j++) {
+    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j], jt = m->jnt_type[j];
+    real w[3], qn[4];
+    if (jt == JNT_FREE) {
+      for (int i = 0; i < 3; i++) qout[qa + i] = qin[qa + i] + dt * (qvel[da + i] * scale);
+      for (int i = 0; i < 3; i++) w[i] = qvel[da + 3 + i] * scale;
+      quat_integrate(qn, qin + qa + 3, w, dt);
+      memcpy(qout + qa + 3, qn, sizeof(qn));
+    } else if (jt == JNT_BALL) {
+      for (int i = 0; i < 3; i++) w[i] = qvel[da + i] * scale;
+      quat_integrate(qn, qin + qa, w, dt);
+      memcpy(qout + qa, qn, sizeof(qn));
+    } else {
+      qout[qa] = qin[qa] + dt * qvel[da] * scale;
+    }
+  }
+}
+
+/* forward.py:457-491 rungekutta4 (tableau A = diag(1/2, 1/2, 1), B = (1/6, 1/3, 1/3, 1/6)) with
+ * _rk_perturb_state :357-399, _rk_accumulate :402-454 and _advance :213-274; after forward_world */
+static void rungekutta4(const orc_model* m, orc_data* d) {
+  const real A[3] = {0.5, 0.5, 1.0}, B[4] = {1.0 / 6, 1.0 / 3, 1.0 / 3, 1.0 / 6};
+  int nq = m->nq, nv = m->nv, na = m->na;
+  real dt = m->opt_timestep;
+  real* buf = (real*)malloc(((size_t)nq + 3 * nv + 2 * na + 1) * sizeof(real));
+  real *qpos0 = buf, *qvel0 = qpos0 + nq, *qvel_rk = qvel0 + nv, *qacc_rk = qvel_rk + nv, *act0 = qacc_rk + nv, *act_dot_rk = act0 + na;
+  memcpy(qpos0, d->qpos, nq * sizeof(real));
+  memcpy(qvel0, d->qvel, nv * sizeof(real));
+  memcpy(act0, d->act, na * sizeof(real));
+  for (int i = 0; i < nv; i++) { qvel_rk[i] = B[0] * d->qvel[i]; qacc_rk[i] = B[0] * d->qacc[i]; }
+  for (int i = 0; i < na; i++) act_dot_rk[i] = B[0] * d->act_dot[i];
+  for (int k = 0; k < 3; k++) {
+    next_position(m, qpos0, d->qvel, A[k], d->qpos);
+    for (int i = 0; i < nv; i++) d->qvel[i] = qvel0[i] + A[k] * d->qacc[i] * dt;
+    for (int a = 0; a < m->nu; a++) {
+      int adr = m->actuator_actadr[a];
+      for (int j = adr; adr >= 0 && j < adr + m->actuator_actnum[a]; j++) d->act[j] = next_act(m, a, act0[j], d->act_dot[j], A[k], 0);
+    }
+    forward_world(m, d);
+    for (int i = 0; i < nv; i++) { qvel_rk[i] += B[k + 1] * d->qvel[i]; qacc_rk[i] += B[k + 1] * d->qacc[i]; }
+    for (int i = 0; i < na; i++) act_dot_rk[i] += B[k + 1] * d->act_dot[i];
+  }
+  memcpy(d->act, act0, na * sizeof(real));
+  memcpy(d->act_dot, act_dot_rk, na * sizeof(real));
+  for (int a = 0; a < m->nu; a++) {
+    int adr = m->actuator_actadr[a];
+    for (int j = adr; adr >= 0 && j < adr + m->actuator_actnum[a]; j++) d->act[j] = next_act(m, a, d->act[j], d->act_dot[j], 1, m->actuator_actlimited[a]);
+  }
+  for (int i = 0; i < nv; i++) d->qvel[i] = qvel0[i] + qacc_rk[i] * dt;
+  next_position(m, qpos0, qvel_rk, 1, d->qpos);
+  d->time[0] += dt;
+  memcpy(d->qacc_warmstart, d->qacc, nv * sizeof(real));
+  free(buf);
+}
+
 /* forward.py:1003-1018 */
 static void step_world(const orc_model* m, orc_data* d) {
   forward_world(m, d);
-  integrate(m, d);
+  if (m->opt_integrator == INTEGRATOR_RK4) rungekutta4(m, d);
+  else integrate(m, d);
 }
 
 int orc_real_size(void) { return (int)sizeof(real); }

@@ -73,6 +73,7 @@ typedef ORC_REAL real;
   X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
+  X(actuator_actearly, nu)                                                                         \
   X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)                                                 \
   X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)                                             \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
