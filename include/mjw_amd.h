@@ -29,12 +29,13 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 6
+#define MJW_ABI_VERSION 7
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
   X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
-  X(nxn) X(nlevel) X(nlimited) X(nmaxcondim) X(nmaxpyramid) X(nv_pad) X(nJmom) X(neq)            \
+  X(nxn) X(nlevel) X(nlimited) X(nlimited_ball) X(nmaxcondim) X(nmaxpyramid) X(nv_pad) X(nJmom)    \
+  X(neq) X(neq_cw)                                                                                 \
   X(nsensor) X(nsensordata) X(sensor_rne_postconstraint) X(nsensor_acc)                           \
   X(nxn_ccd) X(opt_ccd_iterations) X(ccd_epa_iterations)                                           \
   X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations) X(opt_ls_iterations)             \
@@ -74,6 +75,7 @@
   X(body_subtree_end, nbody) X(body_level, nbody) X(level_body, nbody) X(level_adr, nlevel + 1)    \
   X(jnt_type, njnt) X(jnt_qposadr, njnt) X(jnt_dofadr, njnt) X(jnt_bodyid, njnt)                  \
   X(jnt_limited, njnt) X(jnt_actfrclimited, njnt) X(jnt_limited_slide_hinge_adr, nlimited)        \
+  X(jnt_limited_ball_adr, nlimited_ball)                                                           \
   X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \
   X(geom_type, ngeom) X(geom_condim, ngeom) X(geom_bodyid, ngeom) X(geom_priority, ngeom)         \
   X(site_bodyid, nsite)                                                                            \
@@ -84,7 +86,7 @@
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
   X(actuator_actearly, nu)                                                                         \
   X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2) X(nxn_ccdid, nxn)                               \
-  X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)                                             \
+  X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq) X(eq_objtype, neq)                                             \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
   X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)

@@ -43,6 +43,15 @@ __device__ __forceinline__ void mul_quat(float* r, const float* u, const float* 
   r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
 }
 
+// math.py:33-41: q * (0, axis)
+__device__ __forceinline__ void quat_mul_axis(float* r, const float* q, const float* a) {
+  float t0 = -q[1] * a[0] - q[2] * a[1] - q[3] * a[2];
+  float t1 = q[0] * a[0] + q[2] * a[2] - q[3] * a[1];
+  float t2 = q[0] * a[1] + q[3] * a[0] - q[1] * a[2];
+  float t3 = q[0] * a[2] + q[1] * a[1] - q[2] * a[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+
 // math.py:44-49
 __device__ __forceinline__ void rot_vec_quat(float* r, const float* vec, const float* q) {
   float s = q[0];

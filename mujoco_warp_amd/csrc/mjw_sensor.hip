@@ -69,10 +69,50 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
       for (int i = 0; i < 6; i++) cext[6 * b + i] = f[i];
     }
     __syncthreads();
-    // cfrc_ext += contact forces (smooth.py:1447-1495, support.py:241-308); contacts visited in
-    // constraint-row order (each contact at its first row), lane = body
     const int nefc = min(d.nefc[wid], d.njmax);
     const long wr = (long)wid * d.njmax;
+    // cfrc_ext += connect / weld forces (smooth.py:1296-1430): their rows lead the efc block
+    // (all connects, then all welds), lane = body
+    if (m.neq_cw > 0) {
+      const int ne = min(d.ne[wid], nefc);
+      const float* xpos = d.xpos + wb * 3;
+      const float* xmat = d.xmat + wb * 9;
+      int r = 0;
+      while (r < ne) {
+        const int id = d.efc_id[wr + r];
+        const int et = m.eq_type[id];
+        if (et != EQ_CONNECT && et != EQ_WELD) break;  // joint equality rows follow
+        const bool weld = et == EQ_WELD;
+        float frc[3], trq[3] = {0, 0, 0};
+        for (int i = 0; i < 3; i++) frc[i] = d.efc_force[wr + r + i];
+        if (weld)
+          for (int i = 0; i < 3; i++) trq[i] = d.efc_force[wr + r + 3 + i];
+        const bool body_sem = m.eq_objtype[id] == OBJ_BODY;
+        const int o1 = m.eq_obj1id[id], o2 = m.eq_obj2id[id];
+        const int b1 = body_sem ? o1 : m.site_bodyid[o1], b2 = body_sem ? o2 : m.site_bodyid[o2];
+        const float* data = MR(eq_data) + 11 * id;
+        for (int b = lane; b < nb; b += LPW) {
+          for (int k = 0; k < 2; k++) {
+            const int bk = k == 0 ? b1 : b2;
+            if (b == 0 || b != bk) continue;
+            const float* off = body_sem ? (data + ((k == 0) != weld ? 0 : 3)) : MR(site_pos) + 3 * (k == 0 ? o1 : o2);
+            float pos[3], dif[3], c[3];
+            matvec3(pos, xmat + 9 * b, off);
+            for (int i = 0; i < 3; i++) dif[i] = s[L.com + 3 * m.body_rootid[b] + i] - (pos[i] + xpos[3 * b + i]);
+            cross3(c, dif, frc);
+            const float sg = k == 0 ? 1.0f : -1.0f;
+            for (int i = 0; i < 3; i++) {
+              cext[6 * b + i] += sg * (trq[i] - c[i]);
+              cext[6 * b + 3 + i] += sg * frc[i];
+            }
+          }
+        }
+        r += weld ? 6 : 3;
+      }
+      __syncthreads();
+    }
+    // cfrc_ext += contact forces (smooth.py:1447-1495, support.py:241-308); contacts visited in
+    // constraint-row order (each contact at its first row), lane = body
     for (int r = 0; r < nefc; r++) {
       const int type = d.efc_type[wr + r];
       if (type != CNSTR_CONTACT_FRICTIONLESS && type != CNSTR_CONTACT_PYRAMIDAL) continue;

@@ -1071,6 +1071,92 @@ __device__ __forceinline__ void jac_dof(const mjw_model_t& m, const Lay& L, cons
   for (int i = 0; i < 3; i++) { jacp[i] = cd[3 + i] + c[i]; jacr[i] = cd[i]; }
 }
 
+// constraint.py:124-365 (_equality_connect) and :792-1110 (_equality_weld): rows r0 .. r0+2 (+5).
+// The anchor / orientation geometry is wave-uniform; lane i holds dof i of the Jacobian rows, and
+// each row's J.qvel is a wave sum.  Lane k < nrow then writes row r0 + k's scalars.
+__device__ __forceinline__ void eq_connect_weld(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, float* s, int wid, int lane,
+                                                int e, int r0, bool weld, int dof_db, int dof_dend, int kJ, int np) {
+  const float* data = MR(eq_data) + 11 * e;
+  const int o1 = m.eq_obj1id[e], o2 = m.eq_obj2id[e];
+  const bool site = m.eq_objtype[e] == OBJ_SITE && m.nsite > 0;
+  const float* xpos = s + L.xpos;
+  const float* xquat = s + L.xquat;
+  const float* xmat = s + L.xmat;
+  int b1, b2;
+  float p1[3], p2[3], q[4] = {1, 0, 0, 0}, q1[4] = {1, 0, 0, 0};
+  if (site) {
+    const float* site_pos = MR(site_pos);
+    const float* site_quat = MR(site_quat);
+    b1 = m.site_bodyid[o1];
+    b2 = m.site_bodyid[o2];
+    rot_vec_quat(p1, site_pos + 3 * o1, xquat + 4 * b1);  // smooth.py:223 site_xpos
+    rot_vec_quat(p2, site_pos + 3 * o2, xquat + 4 * b2);
+    for (int k = 0; k < 3; k++) { p1[k] += xpos[3 * b1 + k]; p2[k] += xpos[3 * b2 + k]; }
+    if (weld) {
+      float t[4];
+      mul_quat(q, xquat + 4 * b1, site_quat + 4 * o1);
+      mul_quat(t, xquat + 4 * b2, site_quat + 4 * o2);
+      q1[0] = t[0]; q1[1] = -t[1]; q1[2] = -t[2]; q1[3] = -t[3];
+    }
+  } else {
+    b1 = o1;
+    b2 = o2;
+    // connect: anchor1 = data[0:3] on body1, anchor2 = data[3:6] on body2; weld swaps them
+    const float* a1 = weld ? data + 3 : data;
+    const float* a2 = weld ? data : data + 3;
+    matvec3(p1, xmat + 9 * b1, a1);
+    matvec3(p2, xmat + 9 * b2, a2);
+    for (int k = 0; k < 3; k++) { p1[k] = xpos[3 * b1 + k] + p1[k]; p2[k] = xpos[3 * b2 + k] + p2[k]; }
+    if (weld) {
+      mul_quat(q, xquat + 4 * b1, data + 6);
+      q1[0] = xquat[4 * b2]; q1[1] = -xquat[4 * b2 + 1]; q1[2] = -xquat[4 * b2 + 2]; q1[3] = -xquat[4 * b2 + 3];
+    }
+  }
+  const float torquescale = data[10];
+  float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
+  if (lane < m.nv) {
+    float j1p[3], j1r[3], j2p[3], j2r[3];
+    jac_dof(m, L, s, p1, b1, lane, dof_db, dof_dend, j1p, j1r);
+    jac_dof(m, L, s, p2, b2, lane, dof_db, dof_dend, j2p, j2r);
+    for (int k = 0; k < 3; k++) jp[k] = j1p[k] - j2p[k];
+    if (weld) {
+      float dr[3], t[4], u[4];
+      for (int k = 0; k < 3; k++) dr[k] = (j1r[k] - j2r[k]) * torquescale;
+      quat_mul_axis(t, q1, dr);
+      mul_quat(u, t, q);
+      for (int k = 0; k < 3; k++) jr[k] = 0.5f * u[1 + k];
+    }
+  }
+  const float qv = lane < m.nv ? s[L.qvel + lane] : 0.0f;
+  const int nrow = weld ? 6 : 3;
+  float myjq = 0.0f;
+  for (int k = 0; k < nrow; k++) {
+    const float v = k < 3 ? sel3(jp, k) : sel3(jr, k - 3);
+    if (lane < kJ) put_J(d, L, s, wid, np, r0 + k, lane, lane < m.nv ? v : 0.0f);
+    const float jq = dsum(lane < m.nv ? v * qv : 0.0f);
+    if (lane == k) myjq = jq;
+  }
+  float cpos[3], crot[3] = {0, 0, 0};
+  for (int k = 0; k < 3; k++) cpos[k] = p1[k] - p2[k];
+  float pos_imp;
+  if (weld) {
+    float cq[4];
+    mul_quat(cq, q1, q);
+    for (int k = 0; k < 3; k++) crot[k] = cq[1 + k] * torquescale;
+    pos_imp = sqrtf(dot3(cpos, cpos) + dot3(crot, crot));
+  } else {
+    pos_imp = sqrtf(dot3(cpos, cpos));
+  }
+  if (lane < nrow) {
+    const float* biw = MR(body_invweight0);
+    const int c = lane < 3 ? 0 : 1;
+    const float invweight = biw[2 * b1 + c] + biw[2 * b2 + c];
+    const float pos = lane < 3 ? sel3(cpos, lane) : sel3(crot, lane - 3);
+    efc_row(m, d, L, s, wid, r0 + lane, pos, pos_imp, invweight, MR(eq_solref) + 2 * e, MR(eq_solimp) + 5 * e, 0.0f, myjq, 0.0f,
+            CNSTR_EQUALITY, e);
+  }
+}
+
 // collision_driver.py:754-789 + constraint.py:2209-2779 (friction-dof, limits, pyramidal contacts)
 __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
@@ -1088,6 +1174,18 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
   const int dof_dend = lane < nv ? m.body_subtree_end[dof_db] : 0;
   WSYNC();  // contact staging may alias the qM region read by crb_qM
 
+  // --- connect rows, then weld rows (constraint.py:124-365, 792-1110), each in equality index order
+  if (!dsbl_constraint && !(m.opt_disableflags & DSBL_EQUALITY) && m.neq_cw > 0) {
+    for (int weld = 0; weld < 2; weld++) {
+      for (int e = 0; e < m.neq; e++) {
+        if (m.eq_type[e] != (weld ? EQ_WELD : EQ_CONNECT) || !d.eq_active[(long)wid * m.neq + e]) continue;
+        const int nrow = weld ? 6 : 3, r0 = nefc;
+        nefc += nrow;
+        ne += nrow;
+        if (r0 + nrow <= njmax) eq_connect_weld(m, d, L, s, wid, lane, e, r0, weld != 0, dof_db, dof_dend, kJ, np);
+      }
+    }
+  }
   // --- joint equality rows (constraint.py:367-495), in equality index order
   if (!dsbl_constraint && !(m.opt_disableflags & DSBL_EQUALITY) && m.neq > 0) {
     const float* eq_data = MR(eq_data);
@@ -1151,6 +1249,47 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       int cnt = __popcll(bal);
       nefc += cnt;
       nf += cnt;
+    }
+  }
+  // --- ball joint limits (constraint.py:1421-1543): one row on the joint's 3 dofs along -axis
+  if (!dsbl_constraint && !(m.opt_disableflags & DSBL_LIMIT) && m.nlimited_ball > 0) {
+    const float* jnt_range = MR(jnt_range);
+    const float* jnt_margin = MR(jnt_margin);
+    const float* jnt_solref = MR(jnt_solref);
+    const float* jnt_solimp = MR(jnt_solimp);
+    const float* dof_invweight0 = MR(dof_invweight0);
+    for (int base = 0; base < m.nlimited_ball; base += LPW) {
+      const int idx = base + lane;
+      bool act = false;
+      int j = 0;
+      float pos = 0.0f, axis[3] = {0, 0, 0}, jm = 0.0f;
+      if (idx < m.nlimited_ball) {
+        j = m.jnt_limited_ball_adr[idx];
+        const float* qp = s + L.qpos + m.jnt_qposadr[j];
+        float q[4] = {qp[0], qp[1], qp[2], qp[3]}, aa[3];
+        normalize4(q);
+        quat_to_vel(aa, q);
+        const float angle = sqrtf(dot3(aa, aa));  // math.py:261-265 normalize_with_norm
+        for (int k = 0; k < 3; k++) axis[k] = angle == 0.0f ? aa[k] : aa[k] / angle;
+        jm = jnt_margin[j];
+        pos = fmaxf(jnt_range[2 * j], jnt_range[2 * j + 1]) - angle - jm;
+        act = pos < 0.0f;
+      }
+      unsigned long long bal = __ballot(act);
+      int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
+      int r = nefc + rank;
+      if (act && r < njmax) {
+        const int da = m.jnt_dofadr[j];
+        for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, (k >= da && k < da + 3) ? -sel3(axis, k - da) : 0.0f);
+        float Jqvel = -axis[0] * qvel[da];
+        Jqvel -= axis[1] * qvel[da + 1];
+        Jqvel -= axis[2] * qvel[da + 2];
+        efc_row(m, d, L, s, wid, r, pos, pos, dof_invweight0[da], jnt_solref + 2 * j, jnt_solimp + 5 * j, jm, Jqvel, 0.0f,
+                CNSTR_LIMIT_JOINT, j);
+      }
+      int cnt = __popcll(bal);
+      nefc += cnt;
+      nl += cnt;
     }
   }
   // --- joint limits (constraint.py:1316-1418)

@@ -117,8 +117,8 @@ def put_model(mjm, device=None) -> types.Model:
   for st in np.unique(getattr(mjm, "sensor_type", np.zeros(0, dtype=np.int32))):
     if int(st) not in types.SUPPORTED_SENSORS:
       raise NotImplementedError(f"sensor type {int(st)} is not supported by this build yet.")
-  if getattr(mjm, "neq", 0) and np.any(mjm.eq_type != types.EqType.JOINT):
-    raise NotImplementedError("only joint equality constraints are supported by this build yet.")
+  if getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD, types.EqType.JOINT))):
+    raise NotImplementedError("only connect, weld and joint equality constraints are supported by this build yet.")
   pairs_chk, _ = nxn_geom_pairs(mjm)
   for g1, g2 in pairs_chk:
     t = tuple(sorted((int(mjm.geom_type[g1]), int(mjm.geom_type[g2]))))
@@ -191,8 +191,7 @@ def put_model(mjm, device=None) -> types.Model:
     assert mjm.body_parentid[i] < i, "bodies must be in DFS pre-order"
 
   jnt_limited_sh = np.nonzero(mjm.jnt_limited & np.isin(mjm.jnt_type, (JointType.SLIDE, JointType.HINGE)))[0]
-  if np.any(mjm.jnt_limited & (mjm.jnt_type == JointType.BALL)):
-    raise NotImplementedError("ball joint limits are not supported by this build yet.")
+  jnt_limited_ball = np.nonzero(mjm.jnt_limited & (mjm.jnt_type == JointType.BALL))[0]
   pairs, pairid = nxn_geom_pairs(mjm)
   typed = pairs.copy()
   swap = mjm.geom_type[typed[:, 0]] > mjm.geom_type[typed[:, 1]]
@@ -210,6 +209,8 @@ def put_model(mjm, device=None) -> types.Model:
   # collision_convex.py:1127: EPA iteration cap
   m.ccd_epa_iterations = 16 if nconvex and nboxbox == nconvex else int(getattr(mjm.opt, "ccd_iterations", 35))
   m.nlimited = len(jnt_limited_sh)
+  m.nlimited_ball = len(jnt_limited_ball)
+  m.neq_cw = int(np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD)).sum()) if mjm.neq else 0
   m.nJmom = int(sum({JointType.FREE: 6, JointType.BALL: 3}.get(int(mjm.jnt_type[mjm.actuator_trnid[a, 0]]), 1) for a in range(mjm.nu)))
 
   derived_int = dict(
@@ -218,12 +219,14 @@ def put_model(mjm, device=None) -> types.Model:
     level_body=order,
     level_adr=level_adr,
     jnt_limited_slide_hinge_adr=jnt_limited_sh,
+    jnt_limited_ball_adr=jnt_limited_ball,
   )
   m.body_subtree_end = _i32(subtree_end, dev)
   m.body_level = _i32(depth, dev)
   m.level_body = _i32(order, dev)
   m.level_adr = _i32(level_adr, dev)
   m.jnt_limited_slide_hinge_adr = _i32(jnt_limited_sh, dev)
+  m.jnt_limited_ball_adr = _i32(jnt_limited_ball, dev)
 
   # real arrays (batched with leading dim 1)
   for name, cnt in _lib.MODEL_REAL_ARRAYS:

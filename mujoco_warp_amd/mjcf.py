@@ -1203,21 +1203,42 @@ class _Compiler:
     m.actuator_actadr, m.actuator_actnum, m.na = actadr, actnum, na
 
   def _build_equality(self, root):
-    """<equality>: joint couplings (constraint.py:367-495); other kinds are not built yet."""
+    """<equality>: connect (constraint.py:124-365), weld (:792-1110) and joint (:367-495) couplings.
+
+    eq_data follows MuJoCo's layout: connect = (anchor1, anchor2); weld = (anchor, relpose pos,
+    relpose quat, torquescale).  The offsets MuJoCo derives at qpos0 (connect anchor2, weld relpose
+    when its quaternion is zero) are filled in by set_const."""
     m = self.m
     name2jnt = {n: i for i, n in enumerate(m.jnt_names)}
+    name2body = {n: i for i, n in enumerate(m.body_names)}
+    name2site = {n: i for i, n in enumerate(getattr(m, "site_names", []))}
     rows = []
     for eq in root.findall("equality"):
       for el in eq:
         a = dict(self.defaults[el.get("class", "main")].attrs.get("equality", {}))
         a.update(el.attrib)
-        if el.tag != "joint":
-          raise NotImplementedError(f"<equality><{el.tag}> is not supported by the MJCF compiler yet")
         data = np.zeros(11)
-        data[:5] = _merge_vec([0, 1, 0, 0, 0], _floats(a.get("polycoef", "0 1 0 0 0")))
+        objtype = int(ObjType.JOINT)
+        if el.tag == "joint":
+          etype, obj1 = EqType.JOINT, name2jnt[a["joint1"]]
+          obj2 = name2jnt[a["joint2"]] if "joint2" in a else -1
+          data[:5] = _merge_vec([0, 1, 0, 0, 0], _floats(a.get("polycoef", "0 1 0 0 0")))
+        elif el.tag in ("connect", "weld"):
+          etype = EqType.CONNECT if el.tag == "connect" else EqType.WELD
+          if "site1" in a:
+            objtype, obj1 = int(ObjType.SITE), name2site[a["site1"]]
+            obj2 = name2site[a["site2"]]
+          else:
+            objtype, obj1 = int(ObjType.BODY), name2body[a["body1"]]
+            obj2 = name2body[a["body2"]] if "body2" in a else 0
+          data[:3] = _floats(a.get("anchor", "0 0 0"), 3)
+          if etype == EqType.WELD:
+            data[3:10] = _merge_vec([0, 1, 0, 0, 0, 0, 0], _floats(a.get("relpose", "0 1 0 0 0 0 0")))
+            data[10] = float(a.get("torquescale", 1.0))
+        else:
+          raise NotImplementedError(f"<equality><{el.tag}> is not supported by the MJCF compiler yet")
         rows.append(dict(
-          name=a.get("name", ""), type=int(EqType.JOINT), obj1=name2jnt[a["joint1"]],
-          obj2=name2jnt[a["joint2"]] if "joint2" in a else -1, data=data,
+          name=a.get("name", ""), type=int(etype), obj1=obj1, obj2=obj2, objtype=objtype, data=data,
           solref=_merge_vec([0.02, 1.0], _floats(a.get("solref", "0.02 1"))),
           solimp=_merge_vec([0.9, 0.95, 0.001, 0.5, 2.0], _floats(a.get("solimp", "0.9 0.95 0.001 0.5 2"))),
           active=a.get("active", "true") == "true"))
@@ -1226,7 +1247,7 @@ class _Compiler:
     m.eq_type = np.array([r["type"] for r in rows], dtype=np.int32)
     m.eq_obj1id = np.array([r["obj1"] for r in rows], dtype=np.int32)
     m.eq_obj2id = np.array([r["obj2"] for r in rows], dtype=np.int32)
-    m.eq_objtype = np.full(m.neq, 3, dtype=np.int32)  # mjOBJ_JOINT
+    m.eq_objtype = np.array([r["objtype"] for r in rows], dtype=np.int32)
     m.eq_data = np.array([r["data"] for r in rows]).reshape(m.neq, 11)
     m.eq_solref = np.array([r["solref"] for r in rows]).reshape(m.neq, 2)
     m.eq_solimp = np.array([r["solimp"] for r in rows]).reshape(m.neq, 5)
@@ -1529,6 +1550,22 @@ def set_const(m: MjModel):
       rot = tr
     biw[b] = [tr, rot]
   m.body_invweight0 = biw
+  # connect / weld offsets at qpos0 (MuJoCo's compiler; the reference reads them from eq_data,
+  # constraint.py:199-209, 855-866): connect anchor2 = body2-frame image of body1's anchor; weld
+  # relpose (when its quaternion is zero) = body1-frame pose of body2's anchor and orientation
+  for e in range(getattr(m, "neq", 0)):
+    if m.eq_objtype[e] != ObjType.BODY or m.eq_type[e] not in (EqType.CONNECT, EqType.WELD):
+      continue
+    b1, b2, dat = m.eq_obj1id[e], m.eq_obj2id[e], m.eq_data[e]
+    R1, R2 = quat_to_mat(k["xquat"][b1]), quat_to_mat(k["xquat"][b2])
+    if m.eq_type[e] == EqType.CONNECT:
+      p = k["xpos"][b1] + R1 @ dat[:3]
+      dat[3:6] = R2.T @ (p - k["xpos"][b2])
+    elif not np.any(dat[6:10]):
+      p = k["xpos"][b2] + R2 @ dat[:3]
+      dat[3:6] = R1.T @ (p - k["xpos"][b1])
+      q1 = k["xquat"][b1]
+      dat[6:10] = quat_mul(np.array([q1[0], -q1[1], -q1[2], -q1[3]]), k["xquat"][b2])
   # cameras / lights at qpos0 (fixed-frame placement), io.py:2005-2053
   xpos, xquat, sc = k["xpos"], k["xquat"], k["subtree_com"]
   m.cam_pos0 = np.zeros((m.ncam, 3))

@@ -34,6 +34,7 @@ enum { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_T
 enum { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
 enum { DYN_NONE = 0, DYN_INTEGRATOR = 1, DYN_FILTER = 2, DYN_FILTEREXACT = 3, DYN_MUSCLE = 4, DYN_USER = 5 };
 enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
+enum { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum { INTEGRATOR_EULER = 0, INTEGRATOR_RK4 = 1, INTEGRATOR_IMPLICIT = 2, INTEGRATOR_IMPLICITFAST = 3 };
 enum { BIAS_NONE = 0, BIAS_AFFINE = 1 };
 enum { TRN_JOINT = 0, TRN_JOINTINPARENT = 1 };
@@ -1338,11 +1339,94 @@ static int jac_dof(const orc_model* m, const orc_data* d, const real* point, int
   return 1;
 }
 
+/* constraint.py:124-365 _equality_connect / :792-1110 _equality_weld, rows efcid .. efcid+2 (+5) */
+static void eq_connect_weld(const orc_model* m, orc_data* d, int e, int efcid, int weld) {
+  int nv = m->nv;
+  const real* data = m->eq_data + 11 * e;
+  int o1 = m->eq_obj1id[e], o2 = m->eq_obj2id[e], b1, b2;
+  real p1[3], p2[3], q[4] = {1, 0, 0, 0}, q1[4] = {1, 0, 0, 0};
+  if (m->eq_objtype[e] == OBJ_SITE && m->nsite > 0) {
+    b1 = m->site_bodyid[o1];
+    b2 = m->site_bodyid[o2];
+    memcpy(p1, d->site_xpos + 3 * o1, sizeof(p1));
+    memcpy(p2, d->site_xpos + 3 * o2, sizeof(p2));
+    if (weld) {
+      real t[4];
+      mul_quat(q, d->xquat + 4 * b1, m->site_quat + 4 * o1);
+      mul_quat(t, d->xquat + 4 * b2, m->site_quat + 4 * o2);
+      q1[0] = t[0]; q1[1] = -t[1]; q1[2] = -t[2]; q1[3] = -t[3];
+    }
+  } else {
+    b1 = o1;
+    b2 = o2;
+    const real* a1 = weld ? data + 3 : data; /* the weld reads its anchors swapped (:855-856) */
+    const real* a2 = weld ? data : data + 3;
+    matvec3(p1, d->xmat + 9 * b1, a1);
+    matvec3(p2, d->xmat + 9 * b2, a2);
+    for (int k = 0; k < 3; k++) { p1[k] += d->xpos[3 * b1 + k]; p2[k] += d->xpos[3 * b2 + k]; }
+    if (weld) {
+      mul_quat(q, d->xquat + 4 * b1, data + 6);
+      const real* x2 = d->xquat + 4 * b2;
+      q1[0] = x2[0]; q1[1] = -x2[1]; q1[2] = -x2[2]; q1[3] = -x2[3];
+    }
+  }
+  real ts = data[10], jq[6] = {0, 0, 0, 0, 0, 0};
+  int nrow = weld ? 6 : 3;
+  for (int i = 0; i < nv; i++) {
+    real j1p[3], j1r[3], j2p[3], j2r[3], v[6];
+    jac_dof(m, d, p1, b1, i, j1p, j1r);
+    jac_dof(m, d, p2, b2, i, j2p, j2r);
+    for (int k = 0; k < 3; k++) v[k] = j1p[k] - j2p[k];
+    if (weld) {
+      real dr[3], t[4], u[4];
+      for (int k = 0; k < 3; k++) dr[k] = (j1r[k] - j2r[k]) * ts;
+      t[0] = -q1[1] * dr[0] - q1[2] * dr[1] - q1[3] * dr[2]; /* math.py:33-41 quat_mul_axis */
+      t[1] = q1[0] * dr[0] + q1[2] * dr[2] - q1[3] * dr[1];
+      t[2] = q1[0] * dr[1] + q1[3] * dr[0] - q1[1] * dr[2];
+      t[3] = q1[0] * dr[2] + q1[1] * dr[1] - q1[2] * dr[0];
+      mul_quat(u, t, q);
+      for (int k = 0; k < 3; k++) v[3 + k] = 0.5 * u[1 + k];
+    }
+    for (int k = 0; k < nrow; k++) {
+      d->efc_J[(size_t)(efcid + k) * nv + i] = v[k];
+      jq[k] += v[k] * d->qvel[i];
+    }
+  }
+  real cpos[6], pos_imp;
+  for (int k = 0; k < 3; k++) cpos[k] = p1[k] - p2[k];
+  if (weld) {
+    real cq[4];
+    mul_quat(cq, q1, q);
+    for (int k = 0; k < 3; k++) cpos[3 + k] = cq[1 + k] * ts;
+    pos_imp = sqrt(dot3(cpos, cpos) + dot3(cpos + 3, cpos + 3));
+  } else {
+    pos_imp = sqrt(dot3(cpos, cpos));
+  }
+  for (int k = 0; k < nrow; k++) {
+    int c = k < 3 ? 0 : 1;
+    real iw = m->body_invweight0[2 * b1 + c] + m->body_invweight0[2 * b2 + c];
+    efc_row(m, d, efcid + k, cpos[k], pos_imp, iw, m->eq_solref + 2 * e, m->eq_solimp + 5 * e, 0, jq[k], 0, CNSTR_EQUALITY, e);
+  }
+}
+
 /* constraint.py:2209-2779 (equality / friction / limit / contact, in that order) */
 static void make_constraint(const orc_model* m, orc_data* d) {
   int nv = m->nv, njmax = d->njmax;
   *d->ne = *d->nf = *d->nl = *d->nefc = 0;
   if (m->opt_disableflags & DSBL_CONSTRAINT) return;
+  /* connect, then weld (constraint.py:2221-2330 launch order), each in equality index order */
+  if (!(m->opt_disableflags & DSBL_EQUALITY)) {
+    for (int weld = 0; weld < 2; weld++) {
+      for (int e = 0; e < m->neq; e++) {
+        if (m->eq_type[e] != (weld ? EQ_WELD : EQ_CONNECT) || !d->eq_active[e]) continue;
+        int nrow = weld ? 6 : 3;
+        int efcid = *d->nefc;
+        *d->ne += nrow;
+        *d->nefc += nrow;
+        if (efcid + nrow <= njmax) eq_connect_weld(m, d, e, efcid, weld);
+      }
+    }
+  }
   /* equality joint constraint.py:367-495 (rows in equality index order) */
   if (!(m->opt_disableflags & DSBL_EQUALITY)) {
     for (int e = 0; e < m->neq; e++) {
@@ -1387,6 +1471,31 @@ static void make_constraint(const orc_model* m, orc_data* d) {
       J[i] = 1;
       efc_row(m, d, efcid, 0, 0, m->dof_invweight0[i], m->dof_solref + 2 * i, m->dof_solimp + 5 * i, 0, d->qvel[i], fl,
               CNSTR_FRICTION_DOF, i);
+    }
+  }
+  /* limit ball constraint.py:1421-1543 */
+  if (!(m->opt_disableflags & DSBL_LIMIT)) {
+    for (int j = 0; j < m->njnt; j++) {
+      if (!m->jnt_limited[j] || m->jnt_type[j] != JNT_BALL) continue;
+      real q[4], aa[3], axis[3];
+      memcpy(q, d->qpos + m->jnt_qposadr[j], sizeof(q));
+      normalize4(q);
+      quat_to_vel(aa, q);
+      real angle = sqrt(dot3(aa, aa));
+      for (int k = 0; k < 3; k++) axis[k] = angle == 0 ? aa[k] : aa[k] / angle;
+      const real* rng = m->jnt_range + 2 * j;
+      real pos = maxr(rng[0], rng[1]) - angle - m->jnt_margin[j];
+      if (!(pos < 0)) continue;
+      (*d->nl)++;
+      int efcid = (*d->nefc)++;
+      if (efcid >= njmax) continue;
+      int da = m->jnt_dofadr[j];
+      real* J = d->efc_J + (size_t)efcid * nv;
+      memset(J, 0, nv * sizeof(real));
+      real Jqvel = 0;
+      for (int k = 0; k < 3; k++) { J[da + k] = -axis[k]; Jqvel -= axis[k] * d->qvel[da + k]; }
+      efc_row(m, d, efcid, pos, pos, m->dof_invweight0[da], m->jnt_solref + 2 * j, m->jnt_solimp + 5 * j, m->jnt_margin[j], Jqvel, 0,
+              CNSTR_LIMIT_JOINT, j);
     }
   }
   /* limit slide/hinge constraint.py:1316-1418 */
@@ -1947,7 +2056,6 @@ static void implicit(const orc_model* m, orc_data* d) {
 /* =============================================================================================
  * sensor.py (position / velocity / acceleration sensors) + smooth.py rne_postconstraint
  * ============================================================================================= */
-enum { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum { DATATYPE_REAL = 0, DATATYPE_POSITIVE = 1 };
 enum { STAGE_POS = 1, STAGE_VEL = 2, STAGE_ACC = 3 };
 enum {
@@ -2174,6 +2282,35 @@ static void rne_postconstraint(const orc_model* m, orc_data* d) {
     for (int i = 0; i < 3; i++) off[i] = com[i] - d->xipos[3 * b + i];
     cross3(c, off, xf);
     for (int i = 0; i < 3; i++) { d->cfrc_ext[6 * b + i] = xf[3 + i] - c[i]; d->cfrc_ext[6 * b + 3 + i] = xf[i]; }
+  }
+  /* connect / weld forces, smooth.py:1296-1430 (rows lead the efc block: connects, then welds) */
+  int ne = *d->ne < *d->nefc ? *d->ne : *d->nefc;
+  if (ne > d->njmax) ne = d->njmax;
+  for (int r = 0; r < ne;) {
+    int id = d->efc_id[r], et = m->eq_type[id];
+    if (et != EQ_CONNECT && et != EQ_WELD) break;
+    int weld = et == EQ_WELD, body_sem = m->eq_objtype[id] == OBJ_BODY;
+    real frc[3], trq[3] = {0, 0, 0};
+    for (int i = 0; i < 3; i++) frc[i] = d->efc_force[r + i];
+    if (weld)
+      for (int i = 0; i < 3; i++) trq[i] = d->efc_force[r + 3 + i];
+    int o[2] = {m->eq_obj1id[id], m->eq_obj2id[id]};
+    const real* data = m->eq_data + 11 * id;
+    for (int k = 0; k < 2; k++) {
+      int b = body_sem ? o[k] : m->site_bodyid[o[k]];
+      if (!b) continue;
+      const real* off = body_sem ? data + (((k == 0) != weld) ? 0 : 3) : m->site_pos + 3 * o[k];
+      real pos[3], dif[3], c[3];
+      matvec3(pos, d->xmat + 9 * b, off);
+      for (int i = 0; i < 3; i++) dif[i] = d->subtree_com[3 * m->body_rootid[b] + i] - (pos[i] + d->xpos[3 * b + i]);
+      cross3(c, dif, frc);
+      real sg = k == 0 ? 1 : -1;
+      for (int i = 0; i < 3; i++) {
+        d->cfrc_ext[6 * b + i] += sg * (trq[i] - c[i]);
+        d->cfrc_ext[6 * b + 3 + i] += sg * frc[i];
+      }
+    }
+    r += weld ? 6 : 3;
   }
   int ncon = *d->ncon < d->nconmax ? *d->ncon : d->nconmax;
   for (int c = 0; c < ncon; c++) { /* smooth.py:1447-1495 */

@@ -75,7 +75,7 @@ typedef ORC_REAL real;
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
   X(actuator_actearly, nu)                                                                         \
   X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)                                                 \
-  X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq)                                             \
+  X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq) X(eq_objtype, neq)                           \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
   X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)
