@@ -15,7 +15,7 @@
 namespace mjw {
 
 constexpr int LPW = 64;   // lanes per world (one wavefront)
-constexpr int CREC = 32;  // floats per staged contact record
+constexpr int CREC = 33;  // words per staged contact record (odd: lane-per-record access is bank-conflict free)
 constexpr int CMAX = 32;  // staged contacts per collision round
 
 enum : int { ST_POS = 1, ST_VEL = 2, ST_ACT = 4, ST_ACC = 8, ST_SOLVE = 16, ST_EULER = 32, ST_NOFACTOR = 64 };
@@ -95,11 +95,20 @@ __device__ __forceinline__ float dsum(float x) {
 // mjw_prof_read (generic kernel) and mjw_prof_read_dense (dense kernel)
 enum : int {
   PH_LOAD = 0, PH_KIN, PH_COM, PH_CAM, PH_CRB, PH_COLL, PH_TRN, PH_VEL, PH_ACT, PH_ACC, PH_GSOLVE, PH_GEULER,
-  PH_DFACTOR, PH_DSOLVE, PH_DEULER, PH_N
+  PH_DFACTOR, PH_DSOLVE, PH_DEULER,
+  // sub-phases of PH_COLL (reported separately, not added to the total)
+  PH_C_ROWS0, PH_C_BROAD, PH_C_NARROW, PH_C_POOL, PH_C_JROWS, PH_C_SCAL, PH_C_TAIL, PH_N
 };
 #ifdef MJW_PROFILE
 static __device__ unsigned long long g_prof[PH_N];
 #define PROF_T0() unsigned long long _pt = __builtin_amdgcn_s_memtime()
+#define PROF_T0_SUB() unsigned long long _pts = __builtin_amdgcn_s_memtime()
+#define PROF_MARK_SUB(ph)                                                        \
+  do {                                                                           \
+    unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[ph], _nt - _pts);             \
+    _pts = _nt;                                                                  \
+  } while (0)
 #define PROF_MARK(ph)                                                            \
   do {                                                                           \
     unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
@@ -119,6 +128,8 @@ static __device__ unsigned long long g_prof[PH_N];
 #define MJW_PROF_READER(fname)
 #define PROF_T0() (void)0
 #define PROF_MARK(ph) (void)0
+#define PROF_T0_SUB() (void)0
+#define PROF_MARK_SUB(ph) (void)0
 #endif
 
 // dense (register-resident) factor / solve / euler kernel launcher, mjw_dense.hip

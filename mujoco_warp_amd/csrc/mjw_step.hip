@@ -1058,17 +1058,21 @@ __device__ __forceinline__ void put_J(const mjw_data_t& d, const Lay& L, float* 
 // reference walks bodyid's ancestors looking for the dof's body; with bodies in DFS pre-order that
 // is the range test db <= bodyid < subtree_end(db), so the per-lane (db, dend) pair is loaded once
 // by the caller instead of a chain of dependent parent loads per contact.
-__device__ __forceinline__ void jac_dof(const mjw_model_t& m, const Lay& L, const float* s, const float* point, int bodyid,
-                                        int dofid, int db, int dend, float* jacp, float* jacr) {
+__device__ __forceinline__ void jac_dof_root(const Lay& L, const float* s, const float* point, int bodyid, int root, int dofid, int db,
+                                             int dend, float* jacp, float* jacr) {
   const bool in_tree = db == 0 || (bodyid >= db && bodyid < dend);
   if (!in_tree) { jacp[0] = jacp[1] = jacp[2] = jacr[0] = jacr[1] = jacr[2] = 0.0f; return; }
-  int root = m.body_rootid[bodyid];
   float off[3];
   for (int i = 0; i < 3; i++) off[i] = point[i] - s[L.subtree_com + 3 * root + i];
   const float* cd = s + L.cdof + 6 * dofid;
   float c[3];
   cross3(c, cd, off);
   for (int i = 0; i < 3; i++) { jacp[i] = cd[3 + i] + c[i]; jacr[i] = cd[i]; }
+}
+
+__device__ __forceinline__ void jac_dof(const mjw_model_t& m, const Lay& L, const float* s, const float* point, int bodyid,
+                                        int dofid, int db, int dend, float* jacp, float* jacr) {
+  jac_dof_root(L, s, point, bodyid, m.body_rootid[bodyid], dofid, db, dend, jacp, jacr);
 }
 
 // constraint.py:124-365 (_equality_connect) and :792-1110 (_equality_weld): rows r0 .. r0+2 (+5).
@@ -1173,6 +1177,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
   const int dof_db = lane < nv ? m.dof_bodyid[lane] : 0;
   const int dof_dend = lane < nv ? m.body_subtree_end[dof_db] : 0;
   WSYNC();  // contact staging may alias the qM region read by crb_qM
+  PROF_T0_SUB();
 
   // --- connect rows, then weld rows (constraint.py:124-365, 792-1110), each in equality index order
   if (!dsbl_constraint && !(m.opt_disableflags & DSBL_EQUALITY) && m.neq_cw > 0) {
@@ -1329,6 +1334,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
     }
   }
 
+  PROF_MARK_SUB(PH_C_ROWS0);
   // --- collision + contact rows (collision_driver.py:697-789, constraint.py:1668-1936)
   int ncon_total = 0;
   const bool do_contact = d.naconmax > 0 && !(m.opt_disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT));
@@ -1352,6 +1358,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
     }
     if (lane == 0 && npass > 0) atomicAdd(d.ncollision, npass);
     WSYNC();
+    PROF_MARK_SUB(PH_C_BROAD);
     const float* geom_margin = MR(geom_margin);
     int round = 0;
     while (true) {
@@ -1414,6 +1421,11 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           float gap, friction[5], solref[2], solimp[5];
           int condim;
           contact_params(m, wid, g1, g2, &margin, &gap, &condim, friction, solref, solimp);
+          // body and weld-body ids, packed: resolved here for all staged pairs at once instead of
+          // per contact inside the serial row loops below
+          const int cb1 = m.geom_bodyid[g1], cb2 = m.geom_bodyid[g2];
+          const int cbodies = cb1 | (cb2 << 16), cwelds = m.body_weldid[cb1] | (m.body_weldid[cb2] << 16);
+          const int croots = m.body_rootid[cb1] | (m.body_rootid[cb2] << 16);
           if (pbox) {
             const float* r1 = s + L.gxmat + 9 * g1;
             float n1[3] = {r1[2], r1[5], r1[8]}, frame[9];
@@ -1433,7 +1445,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
               for (int i = 0; i < 9; i++) rec[5 + i] = frame[i];
               for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
               rec[19] = solref[0]; rec[20] = solref[1];
-              rec[21] = 0.0f; rec[22] = 0.0f;
+              reinterpret_cast<int*>(rec)[21] = cwelds; reinterpret_cast<int*>(rec)[22] = cbodies;
+              reinterpret_cast<int*>(rec)[32] = croots;
               for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
               int* reci = reinterpret_cast<int*>(rec);
               reci[28] = condim;
@@ -1453,7 +1466,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
               for (int i = 0; i < 9; i++) rec[5 + i] = c.frame[0][i];
               for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
               rec[19] = solref[0]; rec[20] = solref[1];
-              rec[21] = 0.0f; rec[22] = 0.0f;
+              reinterpret_cast<int*>(rec)[21] = cwelds; reinterpret_cast<int*>(rec)[22] = cbodies;
+              reinterpret_cast<int*>(rec)[32] = croots;
               for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
               int* reci = reinterpret_cast<int*>(rec);
               reci[28] = condim;
@@ -1476,7 +1490,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
               for (int i = 0; i < 9; i++) rec[5 + i] = c.frame[sub][i];
               for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
               rec[19] = solref[0]; rec[20] = solref[1];
-              rec[21] = 0.0f; rec[22] = 0.0f;
+              reinterpret_cast<int*>(rec)[21] = cwelds; reinterpret_cast<int*>(rec)[22] = cbodies;
+              reinterpret_cast<int*>(rec)[32] = croots;
               for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
               int* reci = reinterpret_cast<int*>(rec);
               reci[28] = condim;
@@ -1489,6 +1504,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       }
       ncon_total = running;
       int nstage = min(CM, running - rbeg);
+      PROF_MARK_SUB(PH_C_NARROW);
       if (nstage <= 0) break;
       // global pool slot for this round (one atomic per world per round)
       int gbase = 0;
@@ -1535,6 +1551,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           }
         }
       }
+      PROF_MARK_SUB(PH_C_POOL);
       // J entries: lane = dof, loop over staged contacts; efc_vel = J qvel by wave reduction
       for (int cc = 0; cc < nstage; cc++) {
         const float* rec = s + L.con + cc * CREC;
@@ -1544,16 +1561,15 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         float pos = rec[0] - rec[1];
         if (!(pos < 0.0f)) continue;
         int nr = condim == 1 ? 1 : 2 * (condim - 1);
-        int b1 = m.body_weldid[m.geom_bodyid[reci[29]]];
-        int b2 = m.body_weldid[m.geom_bodyid[reci[30]]];
+        const int b1 = reci[21] & 0xffff, b2 = reci[21] >> 16;
         const float* cpos = rec + 2;
         const float* frame = rec + 5;
         const int i = lane;
         float jdp[3] = {0.0f, 0.0f, 0.0f}, jdr[3] = {0.0f, 0.0f, 0.0f};
         if (i < nv) {
           float j1p[3], j1r[3], j2p[3], j2r[3];
-          jac_dof(m, L, s, cpos, b1, i, dof_db, dof_dend, j1p, j1r);
-          jac_dof(m, L, s, cpos, b2, i, dof_db, dof_dend, j2p, j2r);
+          jac_dof_root(L, s, cpos, b1, reci[32] & 0xffff, i, dof_db, dof_dend, j1p, j1r);
+          jac_dof_root(L, s, cpos, b2, reci[32] >> 16, i, dof_db, dof_dend, j2p, j2r);
           for (int k = 0; k < 3; k++) { jdp[k] = j2p[k] - j1p[k]; jdr[k] = j2r[k] - j1r[k]; }
         }
         const float qv = i < nv ? qvel[i] : 0.0f;
@@ -1576,6 +1592,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         }
       }
       WSYNC();
+      PROF_MARK_SUB(PH_C_JROWS);
       // row scalars: lane = contact row (constraint.py:1776-1936)
       for (int rr = lane; rr < nrow_total; rr += LPW) {
         int r = nefc + rr;
@@ -1587,8 +1604,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         const int* reci = reinterpret_cast<const int*>(rec);
         int condim = reci[28];
         int dimid = r - si[L.iscratch + cc];
-        int g1 = reci[29], g2 = reci[30];
-        int body1 = m.geom_bodyid[g1], body2 = m.geom_bodyid[g2];
+        const int body1 = reci[22] & 0xffff, body2 = reci[22] >> 16;
         float invweight = body_invweight0[2 * body1] + body_invweight0[2 * body2];
         if (condim > 1) {
           float fri0 = rec[14];
@@ -1603,6 +1619,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       }
       nefc += nrow_total;
       WSYNC();
+      PROF_MARK_SUB(PH_C_SCAL);
       if (running <= rend) break;
       round++;
     }
@@ -1628,6 +1645,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
     si[L.iscratch + 62] = nefc;
   }
   WSYNC();
+  PROF_MARK_SUB(PH_C_TAIL);
 }
 
 // smooth.py:2041-2147 (joint transmissions; moment rows packed in actuator order)

@@ -25,6 +25,8 @@ from mujoco_warp_amd import _lib, mjcf  # noqa: E402
 
 PHASES = ["load", "kinematics", "com_pos", "camlight", "crb_qM", "collision+constraints", "transmission", "fwd_velocity",
           "fwd_actuation", "fwd_acceleration", "generic_solve", "generic_euler", "dense_factor", "dense_solve", "dense_euler"]
+# sub-phases of collision+constraints (not part of the total)
+SUB = ["c:eq_friction_limits", "c:broadphase", "c:narrowphase_staging", "c:pool_write", "c:contact_J", "c:row_scalars", "c:tail"]
 nworld = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 solver = sys.argv[3] if len(sys.argv) > 3 else "CG"
@@ -36,7 +38,7 @@ m = mjw.put_model(mjm, device="cuda")
 d = mjw.put_data(mjm, mjd, nworld=nworld, nconmax=24, njmax=64, device="cuda", m=m)
 center = torch.zeros(mjm.nu, device="cuda")
 L = _lib.lib()
-buf = (ctypes.c_ulonglong * len(PHASES))()
+buf = (ctypes.c_ulonglong * (len(PHASES) + len(SUB)))()
 for i in range(20):
   mjw.ctrl_noise(m, d, i, center=center)
   mjw.step(m, d)
@@ -50,13 +52,14 @@ for i in range(nsteps):
   mjw.step(m, d)
 e1.record()
 torch.cuda.synchronize()
-a = (ctypes.c_ulonglong * len(PHASES))()
-b = (ctypes.c_ulonglong * len(PHASES))()
+a = (ctypes.c_ulonglong * (len(PHASES) + len(SUB)))()
+b = (ctypes.c_ulonglong * (len(PHASES) + len(SUB)))()
 L.mjw_prof_read(a, 0)
 L.mjw_prof_read_dense(b, 0)
 tot = [a[i] + b[i] for i in range(len(PHASES))]
 s = sum(tot) or 1
 out = {"nworld": nworld, "solver": solver, "ms_per_step": e0.elapsed_time(e1) / nsteps,
        "wave_cycles_per_world_step": {p: tot[i] / (nworld * nsteps) for i, p in enumerate(PHASES) if tot[i]},
-       "share": {p: round(tot[i] / s, 4) for i, p in enumerate(PHASES) if tot[i]}}
+       "share": {p: round(tot[i] / s, 4) for i, p in enumerate(PHASES) if tot[i]},
+       "collision_subphase_cycles_per_world_step": {p: a[len(PHASES) + i] / (nworld * nsteps) for i, p in enumerate(SUB)}}
 print(json.dumps(out, indent=1))
