@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 7
+#define MJW_ABI_VERSION 8
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -39,7 +39,9 @@
   X(nsensor) X(nsensordata) X(sensor_rne_postconstraint) X(nsensor_acc)                           \
   X(nxn_ccd) X(opt_ccd_iterations) X(ccd_epa_iterations)                                           \
   X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations) X(opt_ls_iterations)             \
-  X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)
+  X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)                                  \
+  X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
+  X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -66,7 +68,10 @@
   X(actuator_ctrlrange, nu * 2) X(actuator_forcerange, nu * 2) X(actuator_actrange, nu * 2)       \
   X(actuator_gear, nu * 6)                                                                         \
   X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)                               \
-  X(sensor_cutoff, nsensor)
+  X(sensor_cutoff, nsensor)                                                                        \
+  X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
+  X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)                                \
+  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)
 
 /* ---- model: int arrays (never batched) ---- */
 #define MJW_MODEL_INT_ARRAYS(X)                                                                    \
@@ -89,9 +94,20 @@
   X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq) X(eq_objtype, neq)                                             \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
-  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)
+  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)                     \
+  X(M_rownnz, nv) X(M_rowadr, nv) X(M_colind, nM) X(tree_dofadr, ntree + 1)                        \
+  X(flex_dim, nflex) X(flex_vertadr, nflex) X(flex_edgeadr, nflex) X(flex_edgenum, nflex)          \
+  X(flex_elemadr, nflex) X(flex_elemnum, nflex) X(flex_elemdataadr, nflex) X(flex_elemedgeadr, nflex) \
+  X(flex_condim, nflex) X(flex_cgeomadr, nflex + 1) X(flex_cgeom, nflexcg) X(plane_geom, nplane)   \
+  X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert) X(flex_edge, nflexedge * 2)          \
+  X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata) X(flex_elemedge, nflexelem * 3)      \
+  X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)
 
-/* ---- data: float arrays, (nworld, count) world-major like mujoco_warp types.Data ---- */
+/* ---- data: float arrays, (nworld, count) world-major like mujoco_warp types.Data ----
+ * Sparse models (is_sparse, the reference's io.py:67-74 switch) store qM / qLD as (nworld, nM) rows of
+ * ancestors ascending then the diagonal (M_rowadr / M_colind), and efc_J as (nworld, njmax_pad, njrow)
+ * with efc_J_colind / efc_J_rownnz; dense models keep qM (nv_pad, nv_pad), qLD (nv, nv), efc_J
+ * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt / ncon_world are sparse-path workspace (size 0 when dense). */
 #define MJW_DATA_REAL_ARRAYS(X)                                                                    \
   X(time, 1) X(qpos, nq) X(qvel, nv) X(act, na) X(ctrl, nu) X(qacc_warmstart, nv)                 \
   X(qfrc_applied, nv) X(xfrc_applied, nbody * 6) X(mocap_pos, nmocap * 3) X(mocap_quat, nmocap * 4) \
@@ -110,13 +126,18 @@
   X(efc_J, njmax_pad * nv_pad) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax_pad)         \
   X(efc_vel, njmax) X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax)             \
   X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 17)                                 \
-  X(qpos_t0, nq) X(qvel_t0, nv) X(act_t0, na) X(qvel_rk, nv) X(qacc_rk, nv) X(act_dot_rk, na)
+  X(qpos_t0, nq) X(qvel_t0, nv) X(act_t0, na) X(qvel_rk, nv) X(qacc_rk, nv) X(act_dot_rk, na)     \
+  X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
+  X(flexedge_J, nflexedge * 6) X(flex_frc, nflexelem * 9 + nflexedge * 12)                        \
+  X(sp_body, nbody * 6) X(sp_vec, nv * 10) X(sp_row, njmax * 2) X(sp_LD, nM)
 
 /* ---- data: int arrays, (nworld, count) ---- */
 #define MJW_DATA_INT_ARRAYS(X)                                                                     \
   X(ne, 1) X(nf, 1) X(nl, 1) X(nefc, 1) X(solver_niter, 1)                                         \
   X(moment_rownnz, nu) X(moment_rowadr, nu) X(moment_colind, nJmom)                                \
-  X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax_pad) X(eq_active, neq)
+  X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax_pad) X(eq_active, neq)                   \
+  X(efc_J_colind, njmax_pad * njrow) X(efc_J_rownnz, njmax) X(efc_JT_rowind, njmax_pad * njrow)   \
+  X(efc_JT_adr, nv + 1) X(sp_cnt, nv + 1) X(ncon_world, 2)
 
 /* ---- contact pool: float arrays, (naconmax, count) ---- */
 #define MJW_CONTACT_REAL_ARRAYS(X)                                                                 \
@@ -126,7 +147,7 @@
 /* ---- contact pool: int arrays, (naconmax, count) ---- */
 #define MJW_CONTACT_INT_ARRAYS(X)                                                                  \
   X(contact_dim, 1) X(contact_geom, 2) X(contact_efc_address, nmaxpyramid) X(contact_worldid, 1)  \
-  X(contact_type, 1) X(contact_geomcollisionid, 1)
+  X(contact_type, 1) X(contact_geomcollisionid, 1) X(contact_flex, 2) X(contact_vert, 2)
 
 typedef struct mjw_model_t {
 #define MJW_DECL_I(name) int32_t name;

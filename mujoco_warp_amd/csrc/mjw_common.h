@@ -139,5 +139,7 @@ int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream
 enum : int { RK_BEGIN = 0, RK_PERTURB = 1, RK_ACCUM = 2, RK_END = 3 };
 int rk4_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int op, float scale);
 int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages = 7);
+// workgroup-per-world pipeline of sparse / flex models (m->is_sparse), mjw_sparse.hip; ST_* stage bits
+int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
 
 }  // namespace mjw

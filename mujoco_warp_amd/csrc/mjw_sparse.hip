@@ -1,0 +1,2091 @@
+// mjw_sparse.hip -- workgroup-per-world step for large, sparse and flex models (m.is_sparse).
+//
+// The world-per-wavefront kernels (mjw_step.hip / mjw_dense.hip) keep a whole world in LDS and
+// registers, which stops at nv ~ 64.  Models past that -- the reference's sparse path
+// (io.py:67-74: jacobian=sparse or nv > 32), e.g. the cloth benchmarks with a 30x30 flexcomp
+// (nv = 2706, ~2600 constraint rows) -- run here instead:
+//
+//   * one 256-thread workgroup owns one world; per-world state stays in HBM (L2 resident while
+//     the workgroup runs); threads stride over bodies / dofs / trees / pairs / rows;
+//   * tree recursions avoid level launches: subtree sums walk DFS subtree ranges, velocity and
+//     acceleration propagation walk the ancestor chain, so no atomics and no per-level sync
+//     beyond the kinematics levels;
+//   * M and its factor use the ancestor-row sparse layout (M_rowadr / M_colind, diagonal last);
+//     the L'DL factor and solves run one kinematic tree per thread (smooth.py:1003-1064, 2813-2846);
+//   * constraint Jacobian rows are sparse (efc_J_colind / efc_J_rownnz, njrow slots per row);
+//     the solver builds the transposed (column) index once per solve, so J'f is a deterministic
+//     per-dof gather instead of atomics;
+//   * contacts and rows are emitted in a deterministic per-world order with block scans.
+//
+// Stages restate the reference (file:line per function) and oracle/oracle.c restates the same
+// algorithms on the CPU for the parity tests.
+
+#include "mjw_common.h"
+#include "mjw_narrow.h"
+
+namespace mjw {
+namespace sp {
+
+#define MR_W(name) (MR(name)[0])
+
+constexpr int BLK = 256;
+constexpr int NWAVE = BLK / 64;
+enum : int { EQ_FLEX = 4 };
+
+struct Smem {
+  float red[NWAVE][16];
+  int iscan[NWAVE];
+  int ival[8];
+};
+
+__device__ __forceinline__ int tid() { return (int)threadIdx.x; }
+
+// block-wide sums of N <= 16 floats; every thread gets the same (bitwise) totals
+template <int N>
+__device__ __forceinline__ void block_sum(float (&v)[N], Smem& sm) {
+  const int lane = tid() & 63, wv = tid() >> 6;
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = dsum(v[k]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < N; k++) sm.red[wv][k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    float s = 0.0f;
+    for (int w = 0; w < NWAVE; w++) s += sm.red[w][k];
+    v[k] = s;
+  }
+}
+
+__device__ __forceinline__ float block_sum1(float x, Smem& sm) {
+  float v[1] = {x};
+  block_sum<1>(v, sm);
+  return v[0];
+}
+
+// exclusive block scan of ints; `total` gets the block total (uniform)
+__device__ __forceinline__ int block_scan(int v, int& total, Smem& sm) {
+  const int lane = tid() & 63, wv = tid() >> 6;
+  int incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  __syncthreads();
+  if (lane == 63) sm.iscan[wv] = incl;
+  __syncthreads();
+  int off = 0;
+  total = 0;
+  for (int w = 0; w < NWAVE; w++) {
+    if (w < wv) off += sm.iscan[w];
+    total += sm.iscan[w];
+  }
+  return off + incl - v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// smooth.py:44-224 kinematics (level passes over bodies, then frames of geoms / sites / flex verts)
+// ---------------------------------------------------------------------------------------------
+__device__ void kinematics(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const int nb = m.nbody;
+  float* xpos = d.xpos + (long)wid * nb * 3;
+  float* xquat = d.xquat + (long)wid * nb * 4;
+  const float* qpos = d.qpos + (long)wid * m.nq;
+  const float* body_pos = MR(body_pos);
+  const float* body_quat = MR(body_quat);
+  const float* qpos0 = MR(qpos0);
+  const float* jnt_axis = MR(jnt_axis);
+  const float* jnt_pos = MR(jnt_pos);
+  float* xanchor = d.xanchor + (long)wid * m.njnt * 3;
+  float* xaxis = d.xaxis + (long)wid * m.njnt * 3;
+  if (tid() == 0) {
+    xpos[0] = xpos[1] = xpos[2] = 0.0f;
+    xquat[0] = 1.0f;
+    xquat[1] = xquat[2] = xquat[3] = 0.0f;
+  }
+  __syncthreads();
+  for (int lev = 1; lev < m.nlevel; lev++) {
+    for (int k = m.level_adr[lev] + tid(); k < m.level_adr[lev + 1]; k += BLK) {
+      const int b = m.level_body[k];
+      const int pid = m.body_parentid[b], ja = m.body_jntadr[b], jn = m.body_jntnum[b];
+      if (jn == 1 && m.jnt_type[ja] == JNT_FREE) {
+        const int qa = m.jnt_qposadr[ja];
+        float q[4] = {qpos[qa + 3], qpos[qa + 4], qpos[qa + 5], qpos[qa + 6]};
+        normalize4(q);
+        for (int i = 0; i < 3; i++) {
+          xpos[3 * b + i] = qpos[qa + i];
+          xanchor[3 * ja + i] = qpos[qa + i];
+          xaxis[3 * ja + i] = jnt_axis[3 * ja + i];
+        }
+        for (int i = 0; i < 4; i++) xquat[4 * b + i] = q[i];
+        continue;
+      }
+      float pos[3], quat[4];
+      const int mid = m.body_mocapid[b];
+      if (mid >= 0) {
+        for (int i = 0; i < 3; i++) pos[i] = d.mocap_pos[((long)wid * m.nmocap + mid) * 3 + i];
+        for (int i = 0; i < 4; i++) quat[i] = d.mocap_quat[((long)wid * m.nmocap + mid) * 4 + i];
+      } else {
+        for (int i = 0; i < 3; i++) pos[i] = body_pos[3 * b + i];
+        for (int i = 0; i < 4; i++) quat[i] = body_quat[4 * b + i];
+      }
+      float t[3];
+      rot_vec_quat(t, pos, xquat + 4 * pid);
+      for (int i = 0; i < 3; i++) pos[i] = t[i] + xpos[3 * pid + i];
+      mul_quat(quat, xquat + 4 * pid, quat);
+      for (int j = ja; j < ja + jn; j++) {
+        const int qa = m.jnt_qposadr[j], jt = m.jnt_type[j];
+        const float* axis = jnt_axis + 3 * j;
+        const float* jp = jnt_pos + 3 * j;
+        float xa[3], xx[3];
+        rot_vec_quat(t, jp, quat);
+        for (int i = 0; i < 3; i++) xa[i] = t[i] + pos[i];
+        rot_vec_quat(xx, axis, quat);
+        if (jt == JNT_BALL) {
+          float ql[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]};
+          normalize4(ql);
+          mul_quat(quat, quat, ql);
+          rot_vec_quat(t, jp, quat);
+          for (int i = 0; i < 3; i++) pos[i] = xa[i] - t[i];
+        } else if (jt == JNT_SLIDE) {
+          const float dq = qpos[qa] - qpos0[qa];
+          for (int i = 0; i < 3; i++) pos[i] += xx[i] * dq;
+        } else if (jt == JNT_HINGE) {
+          float ql[4];
+          axis_angle_to_quat(ql, axis, qpos[qa] - qpos0[qa]);
+          mul_quat(quat, quat, ql);
+          rot_vec_quat(t, jp, quat);
+          for (int i = 0; i < 3; i++) pos[i] = xa[i] - t[i];
+        }
+        for (int i = 0; i < 3; i++) {
+          xanchor[3 * j + i] = xa[i];
+          xaxis[3 * j + i] = xx[i];
+        }
+      }
+      normalize4(quat);
+      for (int i = 0; i < 3; i++) xpos[3 * b + i] = pos[i];
+      for (int i = 0; i < 4; i++) xquat[4 * b + i] = quat[i];
+    }
+    __syncthreads();
+  }
+  const float* body_ipos = MR(body_ipos);
+  const float* body_iquat = MR(body_iquat);
+  for (int b = tid(); b < nb; b += BLK) {
+    float q[4], t[3];
+    quat_to_mat(d.xmat + ((long)wid * nb + b) * 9, xquat + 4 * b);
+    rot_vec_quat(t, body_ipos + 3 * b, xquat + 4 * b);
+    for (int i = 0; i < 3; i++) d.xipos[((long)wid * nb + b) * 3 + i] = xpos[3 * b + i] + t[i];
+    mul_quat(q, xquat + 4 * b, body_iquat + 4 * b);
+    quat_to_mat(d.ximat + ((long)wid * nb + b) * 9, q);
+  }
+  const float* geom_pos = MR(geom_pos);
+  const float* geom_quat = MR(geom_quat);
+  for (int g = tid(); g < m.ngeom; g += BLK) {
+    const int b = m.geom_bodyid[g];
+    float q[4], t[3];
+    rot_vec_quat(t, geom_pos + 3 * g, xquat + 4 * b);
+    for (int i = 0; i < 3; i++) d.geom_xpos[((long)wid * m.ngeom + g) * 3 + i] = xpos[3 * b + i] + t[i];
+    mul_quat(q, xquat + 4 * b, geom_quat + 4 * g);
+    quat_to_mat(d.geom_xmat + ((long)wid * m.ngeom + g) * 9, q);
+  }
+  const float* site_pos = MR(site_pos);
+  const float* site_quat = MR(site_quat);
+  for (int s = tid(); s < m.nsite; s += BLK) {
+    const int b = m.site_bodyid[s];
+    float q[4], t[3];
+    rot_vec_quat(t, site_pos + 3 * s, xquat + 4 * b);
+    for (int i = 0; i < 3; i++) d.site_xpos[((long)wid * m.nsite + s) * 3 + i] = xpos[3 * b + i] + t[i];
+    mul_quat(q, xquat + 4 * b, site_quat + 4 * s);
+    quat_to_mat(d.site_xmat + ((long)wid * m.nsite + s) * 9, q);
+  }
+  // smooth.py:228-258 _flex_vertices (flexcomp vertices are centered on their bodies)
+  for (int v = tid(); v < m.nflexvert; v += BLK) {
+    const int b = m.flex_vertbodyid[v];
+    for (int i = 0; i < 3; i++) d.flexvert_xpos[((long)wid * m.nflexvert + v) * 3 + i] = xpos[3 * b + i];
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// smooth.py:463-632 com_pos: subtree com (DFS subtree-range sums), cinert, cdof
+// ---------------------------------------------------------------------------------------------
+__device__ void com_pos(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const int nb = m.nbody;
+  const float* xipos = d.xipos + (long)wid * nb * 3;
+  const float* body_mass = MR(body_mass);
+  const float* body_subtreemass = MR(body_subtreemass);
+  float* sc = d.subtree_com + (long)wid * nb * 3;
+  for (int b = tid(); b < nb; b += BLK) {
+    float s[3] = {0.0f, 0.0f, 0.0f};
+    for (int c = b; c < m.body_subtree_end[b]; c++)
+      for (int i = 0; i < 3; i++) s[i] += xipos[3 * c + i] * body_mass[c];
+    const float mass = body_subtreemass[b];
+    for (int i = 0; i < 3; i++) sc[3 * b + i] = mass != 0.0f ? s[i] / mass : s[i];
+  }
+  __syncthreads();
+  const float* body_inertia = MR(body_inertia);
+  for (int b = tid(); b < nb; b += BLK) {
+    const float* mat = d.ximat + ((long)wid * nb + b) * 9;
+    const float* inert = body_inertia + 3 * b;
+    const float mass = body_mass[b];
+    const int root = m.body_rootid[b];
+    float dif[3], tmp[9];
+    for (int i = 0; i < 3; i++) dif[i] = xipos[3 * b + i] - sc[3 * root + i];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        float s = 0.0f;
+        for (int k = 0; k < 3; k++) s += mat[3 * i + k] * inert[k] * mat[3 * j + k];
+        tmp[3 * i + j] = s;
+      }
+    float* r = d.cinert + ((long)wid * nb + b) * 10;
+    r[0] = tmp[0] + mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+    r[1] = tmp[4] + mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+    r[2] = tmp[8] + mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+    r[3] = tmp[1] - mass * dif[0] * dif[1];
+    r[4] = tmp[2] - mass * dif[0] * dif[2];
+    r[5] = tmp[5] - mass * dif[1] * dif[2];
+    r[6] = mass * dif[0];
+    r[7] = mass * dif[1];
+    r[8] = mass * dif[2];
+    r[9] = mass;
+  }
+  float* cd = d.cdof + (long)wid * m.nv * 6;
+  for (int j = tid(); j < m.njnt; j += BLK) {
+    const int b = m.jnt_bodyid[j], da = m.jnt_dofadr[j], jt = m.jnt_type[j];
+    const float* xaxis = d.xaxis + ((long)wid * m.njnt + j) * 3;
+    const float* xmat = d.xmat + ((long)wid * nb + b) * 9;
+    float off[3];
+    for (int i = 0; i < 3; i++) off[i] = sc[3 * m.body_rootid[b] + i] - d.xanchor[((long)wid * m.njnt + j) * 3 + i];
+    if (jt == JNT_FREE || jt == JNT_BALL) {
+      int rot0 = da;
+      if (jt == JNT_FREE) {
+        for (int k = 0; k < 3; k++)
+          for (int i = 0; i < 6; i++) cd[6 * (da + k) + i] = (i == 3 + k) ? 1.0f : 0.0f;
+        rot0 = da + 3;
+      }
+      for (int k = 0; k < 3; k++) {
+        float ax[3] = {xmat[k], xmat[3 + k], xmat[6 + k]};
+        float* r = cd + 6 * (rot0 + k);
+        r[0] = ax[0];
+        r[1] = ax[1];
+        r[2] = ax[2];
+        cross3(r + 3, ax, off);
+      }
+    } else if (jt == JNT_SLIDE) {
+      float* r = cd + 6 * da;
+      r[0] = r[1] = r[2] = 0.0f;
+      r[3] = xaxis[0];
+      r[4] = xaxis[1];
+      r[5] = xaxis[2];
+    } else {
+      float* r = cd + 6 * da;
+      r[0] = xaxis[0];
+      r[1] = xaxis[1];
+      r[2] = xaxis[2];
+      cross3(r + 3, xaxis, off);
+    }
+  }
+  __syncthreads();
+}
+
+// smooth.py:635-803 camlight
+__device__ void camlight(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const float* xpos = d.xpos + (long)wid * m.nbody * 3;
+  const float* xquat = d.xquat + (long)wid * m.nbody * 4;
+  const float* sc = d.subtree_com + (long)wid * m.nbody * 3;
+  const float* cam_pos = MR(cam_pos);
+  const float* cam_quat = MR(cam_quat);
+  const float* cam_pos0 = MR(cam_pos0);
+  const float* cam_poscom0 = MR(cam_poscom0);
+  const float* cam_mat0 = MR(cam_mat0);
+  for (int c = tid(); c < m.ncam; c += BLK) {
+    const int mode = m.cam_mode[c], b = m.cam_bodyid[c], tgt = m.cam_targetbodyid[c];
+    const bool is_target = mode == CAM_TARGETBODY || mode == CAM_TARGETBODYCOM;
+    float* cx = d.cam_xpos + ((long)wid * m.ncam + c) * 3;
+    float* cm = d.cam_xmat + ((long)wid * m.ncam + c) * 9;
+    if ((is_target && tgt < 0) || mode == CAM_FIXED) {
+      float t[3], q[4];
+      rot_vec_quat(t, cam_pos + 3 * c, xquat + 4 * b);
+      for (int i = 0; i < 3; i++) cx[i] = xpos[3 * b + i] + t[i];
+      mul_quat(q, xquat + 4 * b, cam_quat + 4 * c);
+      quat_to_mat(cm, q);
+    } else if (mode == CAM_TRACK) {
+      for (int i = 0; i < 9; i++) cm[i] = cam_mat0[9 * c + i];
+      for (int i = 0; i < 3; i++) cx[i] = xpos[3 * b + i] + cam_pos0[3 * c + i];
+    } else if (mode == CAM_TRACKCOM) {
+      for (int i = 0; i < 9; i++) cm[i] = cam_mat0[9 * c + i];
+      for (int i = 0; i < 3; i++) cx[i] = sc[3 * b + i] + cam_poscom0[3 * c + i];
+    } else {
+      float t[3], m1[3], m2[3], m3[3];
+      rot_vec_quat(t, cam_pos + 3 * c, xquat + 4 * b);
+      for (int i = 0; i < 3; i++) cx[i] = xpos[3 * b + i] + t[i];
+      const float* tp = mode == CAM_TARGETBODYCOM ? sc + 3 * tgt : xpos + 3 * tgt;
+      for (int i = 0; i < 3; i++) m3[i] = cx[i] - tp[i];
+      normalize3(m3);
+      float z[3] = {0.0f, 0.0f, 1.0f};
+      cross3(m1, z, m3);
+      normalize3(m1);
+      cross3(m2, m3, m1);
+      normalize3(m2);
+      for (int i = 0; i < 3; i++) {
+        cm[3 * i] = m1[i];
+        cm[3 * i + 1] = m2[i];
+        cm[3 * i + 2] = m3[i];
+      }
+    }
+  }
+  const float* light_pos = MR(light_pos);
+  const float* light_dir = MR(light_dir);
+  const float* light_pos0 = MR(light_pos0);
+  const float* light_poscom0 = MR(light_poscom0);
+  const float* light_dir0 = MR(light_dir0);
+  for (int l = tid(); l < m.nlight; l += BLK) {
+    const int mode = m.light_mode[l], b = m.light_bodyid[l], tgt = m.light_targetbodyid[l];
+    const bool is_target = mode == CAM_TARGETBODY || mode == CAM_TARGETBODYCOM;
+    float* lx = d.light_xpos + ((long)wid * m.nlight + l) * 3;
+    float* ld = d.light_xdir + ((long)wid * m.nlight + l) * 3;
+    if ((is_target && tgt < 0) || mode == CAM_FIXED) {
+      float t[3];
+      rot_vec_quat(t, light_pos + 3 * l, xquat + 4 * b);
+      for (int i = 0; i < 3; i++) lx[i] = xpos[3 * b + i] + t[i];
+      rot_vec_quat(ld, light_dir + 3 * l, xquat + 4 * b);
+      if (is_target && tgt < 0) continue;
+    } else if (mode == CAM_TRACK) {
+      for (int i = 0; i < 3; i++) {
+        ld[i] = light_dir0[3 * l + i];
+        lx[i] = xpos[3 * b + i] + light_pos0[3 * l + i];
+      }
+    } else if (mode == CAM_TRACKCOM) {
+      for (int i = 0; i < 3; i++) {
+        ld[i] = light_dir0[3 * l + i];
+        lx[i] = sc[3 * b + i] + light_poscom0[3 * l + i];
+      }
+    } else {
+      float t[3];
+      rot_vec_quat(t, light_pos + 3 * l, xquat + 4 * b);
+      for (int i = 0; i < 3; i++) lx[i] = xpos[3 * b + i] + t[i];
+      const float* tp = mode == CAM_TARGETBODYCOM ? sc + 3 * tgt : xpos + 3 * tgt;
+      for (int i = 0; i < 3; i++) ld[i] = tp[i] - lx[i];
+    }
+    normalize3(ld);
+  }
+}
+
+// smooth.py:261-355 _flex_edges: length, velocity, d(length)/dq over the vertex bodies' own dofs
+__device__ void flex_edges(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const float* fx = d.flexvert_xpos + (long)wid * m.nflexvert * 3;
+  const float* sc = d.subtree_com + (long)wid * m.nbody * 3;
+  const float* cdof = d.cdof + (long)wid * m.nv * 6;
+  const float* qvel = d.qvel + (long)wid * m.nv;
+  for (int f = 0; f < m.nflex; f++) {
+    const int ea = m.flex_edgeadr[f], vb = m.flex_vertadr[f];
+    for (int e = ea + tid(); e < ea + m.flex_edgenum[f]; e += BLK) {
+      const int v[2] = {vb + m.flex_edge[2 * e], vb + m.flex_edge[2 * e + 1]};
+      float vec[3], dir[3];
+      for (int i = 0; i < 3; i++) vec[i] = fx[3 * v[1] + i] - fx[3 * v[0] + i];
+      float len = sqrtf(dot3(vec, vec));
+      for (int i = 0; i < 3; i++) dir[i] = len == 0.0f ? vec[i] : vec[i] / len;
+      float J[6] = {0, 0, 0, 0, 0, 0}, vel = 0.0f;
+      int slot = 0;
+      for (int s2 = 0; s2 < 2; s2++) {
+        const int b = m.flex_vertbodyid[v[s2]];
+        float off[3];
+        for (int i = 0; i < 3; i++) off[i] = fx[3 * v[s2] + i] - sc[3 * m.body_rootid[b] + i];
+        for (int k = 0; k < m.body_dofnum[b] && slot < 6; k++) {
+          const int dof = m.body_dofadr[b] + k;
+          const float* c = cdof + 6 * dof;
+          float cr[3], jp[3];
+          cross3(cr, c, off);
+          for (int i = 0; i < 3; i++) jp[i] = c[3 + i] + cr[i];
+          const float jv = s2 ? dot3(jp, dir) : -dot3(jp, dir);
+          vel += jv * qvel[dof];
+          J[slot++] = jv;
+        }
+      }
+      d.flexedge_length[(long)wid * m.nflexedge + e] = len;
+      d.flexedge_velocity[(long)wid * m.nflexedge + e] = vel;
+      for (int k = 0; k < 6; k++) d.flexedge_J[((long)wid * m.nflexedge + e) * 6 + k] = J[k];
+    }
+  }
+}
+
+// smooth.py:806-912 crb (subtree-range sums) + sparse qM rows (ancestors ascending, diagonal last)
+__device__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const int nb = m.nbody;
+  const float* cinert = d.cinert + (long)wid * nb * 10;
+  float* crb = d.crb + (long)wid * nb * 10;
+  for (int b = tid(); b < nb; b += BLK) {
+    float s[10];
+    for (int i = 0; i < 10; i++) s[i] = cinert[10 * b + i];
+    if (b > 0)
+      for (int c = b + 1; c < m.body_subtree_end[b]; c++)
+        for (int i = 0; i < 10; i++) s[i] += cinert[10 * c + i];
+    for (int i = 0; i < 10; i++) crb[10 * b + i] = s[i];
+  }
+  __syncthreads();
+  const float* cdof = d.cdof + (long)wid * m.nv * 6;
+  const float* armature = MR(dof_armature);
+  float* qM = d.qM + (long)wid * m.nM;
+  for (int i = tid(); i < m.nv; i += BLK) {
+    float buf[6];
+    inert_vec(buf, crb + 10 * m.dof_bodyid[i], cdof + 6 * i);
+    const int adr = m.M_rowadr[i], nnz = m.M_rownnz[i];
+    float s = armature[i];
+    for (int k = 0; k < 6; k++) s += cdof[6 * i + k] * buf[k];
+    qM[adr + nnz - 1] = s;
+    int j = m.dof_parentid[i];
+    for (int p = nnz - 2; p >= 0; p--, j = m.dof_parentid[j]) {
+      float q = 0.0f;
+      for (int k = 0; k < 6; k++) q += cdof[6 * j + k] * buf[k];
+      qM[adr + p] = q;
+    }
+  }
+  __syncthreads();
+}
+
+// M = L' D L per kinematic tree (smooth.py:1003-1064, mj_factorM order): LD = factor(M + diag(add))
+__device__ void factor_trees(const mjw_model_t& m, const float* M, float* LD, const float* add, float add_scale) {
+  for (int t = tid(); t < m.ntree; t += BLK) {
+    const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
+    for (int k = a; k < e; k++) {
+      const int adr = m.M_rowadr[k], nnz = m.M_rownnz[k];
+      for (int p = 0; p < nnz; p++) LD[adr + p] = M[adr + p];
+      if (add) LD[adr + nnz - 1] += add_scale * add[k];
+    }
+    for (int k = e - 1; k >= a; k--) {
+      const int adr = m.M_rowadr[k], nnz = m.M_rownnz[k];
+      const float dk = LD[adr + nnz - 1];
+      for (int p = nnz - 2; p >= 0; p--) {
+        const int i = m.M_colind[adr + p];
+        const float tmp = LD[adr + p] / dk;
+        const int adri = m.M_rowadr[i];
+        for (int q = 0; q <= p; q++) LD[adri + q] -= tmp * LD[adr + q];
+        LD[adr + p] = tmp;
+      }
+    }
+  }
+}
+
+// x = (L' D L)^-1 x in place, per tree (smooth.py:2813-2846)
+__device__ void solve_trees(const mjw_model_t& m, const float* LD, float* x) {
+  for (int t = tid(); t < m.ntree; t += BLK) {
+    const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
+    for (int k = e - 1; k >= a; k--) {
+      const int adr = m.M_rowadr[k], nnz = m.M_rownnz[k];
+      const float xk = x[k];
+      for (int p = 0; p < nnz - 1; p++) x[m.M_colind[adr + p]] -= LD[adr + p] * xk;
+    }
+    for (int k = a; k < e; k++) x[k] /= LD[m.M_rowadr[k] + m.M_rownnz[k] - 1];
+    for (int k = a; k < e; k++) {
+      const int adr = m.M_rowadr[k], nnz = m.M_rownnz[k];
+      float s = x[k];
+      for (int p = 0; p < nnz - 1; p++) s -= LD[adr + p] * x[m.M_colind[adr + p]];
+      x[k] = s;
+    }
+  }
+}
+
+// y = M x (support.py:67-101 sparse mul_m), per tree: lower rows plus their transposes
+__device__ void mul_m_trees(const mjw_model_t& m, const float* M, const float* x, float* y) {
+  for (int t = tid(); t < m.ntree; t += BLK) {
+    const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
+    for (int k = a; k < e; k++) y[k] = 0.0f;
+    for (int k = a; k < e; k++) {
+      const int adr = m.M_rowadr[k], nnz = m.M_rownnz[k];
+      float s = M[adr + nnz - 1] * x[k];
+      for (int p = 0; p < nnz - 1; p++) {
+        const int i = m.M_colind[adr + p];
+        s += M[adr + p] * x[i];
+        y[i] += M[adr + p] * x[k];
+      }
+      y[k] += s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// collision: geom pairs (collision_driver.py:697-789 + primitive narrowphase), flex triangles vs
+// geoms (collision_flex.py:381-529) and flex vertices vs planes (:261-378)
+// ---------------------------------------------------------------------------------------------
+struct Cand {
+  float dist;
+  float pos[3];
+  float nrm[3];
+};
+
+// collision_primitive_core.py:1495-1597
+__device__ __forceinline__ float tri_sign(const float* p1, const float* p2, const float* p3) {
+  const float a = (p1[0] - p3[0]) * (p2[1] - p3[1]) - (p2[0] - p3[0]) * (p1[1] - p3[1]);
+  return (float)((a > 0.0f) - (a < 0.0f));
+}
+
+__device__ __forceinline__ void tri_seg(float* r, const float* p, const float* u, const float* v) {
+  const float uv[2] = {v[0] - u[0], v[1] - u[1]}, up[2] = {p[0] - u[0], p[1] - u[1]};
+  const float a = (uv[0] * up[0] + uv[1] * up[1]) / fmaxf(MJW_MINVAL, uv[0] * uv[0] + uv[1] * uv[1]);
+  if (a <= 0.0f) { r[0] = u[0]; r[1] = u[1]; }
+  else if (a >= 1.0f) { r[0] = v[0]; r[1] = v[1]; }
+  else { r[0] = u[0] + a * uv[0]; r[1] = u[1] + a * uv[1]; }
+}
+
+__device__ float sphere_triangle(float* pos, float* nrm, const float* sp, float sr, const float* t1, const float* t2, const float* t3,
+                                 float tr) {
+  float S[3], A[3], B[3], N[3], P[3], V1[3], V2[3], X[3];
+  for (int i = 0; i < 3; i++) { S[i] = sp[i] - t1[i]; A[i] = t2[i] - t1[i]; B[i] = t3[i] - t1[i]; }
+  cross3(N, A, B);
+  normalize3(N);
+  const float dstS = dot3(N, S);
+  for (int i = 0; i < 3; i++) P[i] = S[i] - dstS * N[i];
+  const float lenA = sqrtf(dot3(A, A));
+  for (int i = 0; i < 3; i++) V1[i] = A[i];
+  normalize3(V1);
+  cross3(V2, N, A);
+  normalize3(V2);
+  const float o[2] = {0.0f, 0.0f}, a[2] = {lenA, 0.0f}, b[2] = {dot3(V1, B), dot3(V2, B)}, p[2] = {dot3(V1, P), dot3(V2, P)};
+  const float s1 = tri_sign(p, o, a), s2 = tri_sign(p, a, b), s3 = tri_sign(p, b, o);
+  if (s1 == s2 && s2 == s3) {
+    for (int i = 0; i < 3; i++) X[i] = P[i];
+  } else {
+    float x0[2], x1[2], x2[2];
+    tri_seg(x0, p, o, a);
+    tri_seg(x1, p, a, b);
+    tri_seg(x2, p, b, o);
+    const float d0 = hypotf(p[0] - x0[0], p[1] - x0[1]), d1 = hypotf(p[0] - x1[0], p[1] - x1[1]), d2 = hypotf(p[0] - x2[0], p[1] - x2[1]);
+    const float* xs = (d0 < d1 && d0 < d2) ? x0 : (d1 < d2 ? x1 : x2);
+    for (int i = 0; i < 3; i++) X[i] = xs[0] * V1[i] + xs[1] * V2[i];
+  }
+  for (int i = 0; i < 3; i++) nrm[i] = X[i] - S[i];
+  const float dst = sqrtf(dot3(nrm, nrm));
+  if (dst > MJW_MINVAL) for (int i = 0; i < 3; i++) nrm[i] /= dst;
+  else for (int i = 0; i < 3; i++) nrm[i] = N[i];
+  const float dist = dst - sr - tr;
+  for (int i = 0; i < 3; i++) pos[i] = sp[i] + nrm[i] * (sr + 0.5f * dist);
+  return dist;
+}
+
+// triangle vs sphere/capsule/box/cylinder: up to 2 candidates (collision_primitive_core.py:1600-1990)
+__device__ int geom_triangle(Cand* c, int gt, const float* gp, const float* gr, const float* gs, const float* const* t, float tr) {
+  int n = 0;
+  const float ax[3] = {gr[2], gr[5], gr[8]};
+  if (gt == GEOM_SPHERE) {
+    c[0].dist = sphere_triangle(c[0].pos, c[0].nrm, gp, gs[0], t[0], t[1], t[2], tr);
+    return 1;
+  }
+  if (gt == GEOM_CAPSULE) {
+    float p1[3], p2[3], ab[3];
+    for (int i = 0; i < 3; i++) { p1[i] = gp[i] - ax[i] * gs[1]; p2[i] = gp[i] + ax[i] * gs[1]; ab[i] = p2[i] - p1[i]; }
+    c[n].dist = sphere_triangle(c[n].pos, c[n].nrm, p1, gs[0], t[0], t[1], t[2], tr);
+    if (c[n].dist < MJW_MAXVAL) n++;
+    c[n].dist = sphere_triangle(c[n].pos, c[n].nrm, p2, gs[0], t[0], t[1], t[2], tr);
+    if (c[n].dist < MJW_MAXVAL) n++;
+    const float ab2 = 4.0f * gs[1] * gs[1];
+    for (int vi = 0; vi < 3 && n < 2; vi++) {
+      float vec[3], cl[3], df[3];
+      for (int i = 0; i < 3; i++) vec[i] = t[vi][i] - p1[i];
+      const float tp = dot3(vec, ab) / fmaxf(MJW_MINVAL, ab2);
+      if (tp > MJW_MINVAL && tp < 1.0f - MJW_MINVAL) {
+        for (int i = 0; i < 3; i++) { cl[i] = p1[i] + ab[i] * tp; df[i] = t[vi][i] - cl[i]; }
+        const float draw = sqrtf(dot3(df, df));
+        if (draw > MJW_MINVAL) {
+          for (int i = 0; i < 3; i++) {
+            c[n].nrm[i] = df[i] / draw;
+            c[n].pos[i] = (cl[i] + t[vi][i] + c[n].nrm[i] * (gs[0] - tr)) * 0.5f;
+          }
+          c[n].dist = draw - gs[0] - tr;
+          n++;
+        }
+      }
+    }
+    return n;
+  }
+  if (gt == GEOM_BOX) {
+    for (int vi = 0; vi < 3; vi++) {
+      float df[3], loc[3];
+      for (int i = 0; i < 3; i++) df[i] = t[vi][i] - gp[i];
+      for (int i = 0; i < 3; i++) loc[i] = gr[i] * df[0] + gr[3 + i] * df[1] + gr[6 + i] * df[2];
+      int maxaxis = 0;
+      float maxval = fabsf(loc[0]) - gs[0];
+      for (int j = 1; j < 3; j++) {
+        const float v = fabsf(loc[j]) - gs[j];
+        if (v > maxval) { maxval = v; maxaxis = j; }
+      }
+      bool inside = true;
+      for (int j = 0; j < 3; j++) if (fabsf(loc[j]) > gs[j] + tr) inside = false;
+      if (inside && n < 2) {
+        float nl[3] = {0.0f, 0.0f, 0.0f};
+        nl[maxaxis] = (float)((loc[maxaxis] > 0.0f) - (loc[maxaxis] < 0.0f));
+        matvec3(c[n].nrm, gr, nl);
+        const float dd = maxval - tr, off = tr + dd * 0.5f;
+        for (int i = 0; i < 3; i++) c[n].pos[i] = t[vi][i] - c[n].nrm[i] * off;
+        c[n].dist = dd;
+        n++;
+      }
+    }
+    for (int i = 0; i < 8 && n < 2; i++) {
+      float vec[3] = {(i & 1) ? gs[0] : -gs[0], (i & 2) ? gs[1] : -gs[1], (i & 4) ? gs[2] : -gs[2]}, corner[3];
+      matvec3(corner, gr, vec);
+      for (int k = 0; k < 3; k++) corner[k] += gp[k];
+      c[n].dist = sphere_triangle(c[n].pos, c[n].nrm, corner, 0.0f, t[0], t[1], t[2], tr);
+      if (c[n].dist < MJW_MAXVAL) n++;
+    }
+    return n;
+  }
+  // cylinder
+  const float cr = gs[0], hh = gs[1];
+  float p1[3], p2[3], ab[3];
+  for (int i = 0; i < 3; i++) { p1[i] = gp[i] - ax[i] * hh; p2[i] = gp[i] + ax[i] * hh; ab[i] = p2[i] - p1[i]; }
+  const float ab2 = 4.0f * hh * hh;
+  for (int vi = 0; vi < 3 && n < 2; vi++) {
+    const float* vert = t[vi];
+    float vec[3];
+    for (int i = 0; i < 3; i++) vec[i] = vert[i] - p1[i];
+    const float tp = dot3(vec, ab) / fmaxf(MJW_MINVAL, ab2);
+    if (tp > MJW_MINVAL && tp < 1.0f - MJW_MINVAL) {
+      float cl[3], df[3];
+      for (int i = 0; i < 3; i++) { cl[i] = p1[i] + ab[i] * tp; df[i] = vert[i] - cl[i]; }
+      const float draw = sqrtf(dot3(df, df));
+      if (draw < cr + tr) {
+        if (draw > MJW_MINVAL) {
+          for (int i = 0; i < 3; i++) { c[n].nrm[i] = df[i] / draw; c[n].pos[i] = (cl[i] + vert[i] + c[n].nrm[i] * (cr - tr)) * 0.5f; }
+          c[n].dist = draw - cr - tr;
+        } else {
+          const float L = sqrtf(ab2), d2 = (1.0f - tp) * L, d1 = tp * L;
+          if (d2 < cr && d2 < d1) {
+            for (int i = 0; i < 3; i++) { c[n].nrm[i] = ax[i]; c[n].pos[i] = vert[i]; }
+            c[n].dist = -d2 - tr;
+          } else if (d1 < cr) {
+            for (int i = 0; i < 3; i++) { c[n].nrm[i] = -ax[i]; c[n].pos[i] = vert[i]; }
+            c[n].dist = -d1 - tr;
+          } else {
+            float e1[3], e2[3];
+            for (int i = 0; i < 3; i++) { e1[i] = t[1][i] - t[0][i]; e2[i] = t[2][i] - t[0][i]; }
+            cross3(c[n].nrm, e1, e2);
+            normalize3(c[n].nrm);
+            for (int i = 0; i < 3; i++) c[n].pos[i] = cl[i];
+            c[n].dist = -cr - tr;
+          }
+        }
+        n++;
+      }
+    } else {
+      const float* pe = tp <= MJW_MINVAL ? p1 : p2;
+      const float sg = tp <= MJW_MINVAL ? -1.0f : 1.0f;
+      float df[3], perp[3];
+      for (int i = 0; i < 3; i++) df[i] = vert[i] - pe[i];
+      const float sd = dot3(df, ax);
+      for (int i = 0; i < 3; i++) perp[i] = df[i] - ax[i] * sd;
+      const float pl = sqrtf(dot3(perp, perp));
+      if (pl < cr) {
+        const float dd = sg * sd - tr;
+        for (int i = 0; i < 3; i++) { c[n].nrm[i] = sg * ax[i]; c[n].pos[i] = vert[i] - c[n].nrm[i] * (tr + dd * 0.5f); }
+        c[n].dist = dd;
+        n++;
+      } else if (pl < cr + tr) {
+        float ep[3], de[3];
+        for (int i = 0; i < 3; i++) { ep[i] = pe[i] + perp[i] / pl * cr; de[i] = vert[i] - ep[i]; }
+        const float draw = sqrtf(dot3(de, de));
+        if (draw > MJW_MINVAL) {
+          const float dd = draw - tr;
+          for (int i = 0; i < 3; i++) { c[n].nrm[i] = de[i] / draw; c[n].pos[i] = vert[i] - c[n].nrm[i] * (tr + dd * 0.5f); }
+          c[n].dist = dd;
+          n++;
+        }
+      }
+    }
+  }
+  return n;
+}
+
+// collision_primitive_core.py:519-613 plane_cylinder candidate k
+__device__ void plane_cylinder_k(int k, const float* n, const float* pp, const float* cc, const float* cax, float r, float hh, float* dist,
+                                 float* pos) {
+  float axis[3] = {cax[0], cax[1], cax[2]};
+  float prjaxis = dot3(n, axis);
+  if (prjaxis > 0.0f) {
+    for (int i = 0; i < 3; i++) axis[i] = -axis[i];
+    prjaxis = -prjaxis;
+  }
+  const float df[3] = {cc[0] - pp[0], cc[1] - pp[1], cc[2] - pp[2]};
+  const float dist0 = dot3(df, n);
+  float vec[3];
+  for (int i = 0; i < 3; i++) vec[i] = axis[i] * prjaxis - n[i];
+  const float len2 = dot3(vec, vec);
+  if (len2 >= 1e-12f) {
+    const float s = safe_div(r, sqrtf(len2));
+    for (int i = 0; i < 3; i++) vec[i] *= s;
+  } else {
+    vec[0] = r;
+    vec[1] = vec[2] = 0.0f;
+  }
+  const float prjvec = dot3(vec, n);
+  for (int i = 0; i < 3; i++) axis[i] *= hh;
+  prjaxis *= hh;
+  if (k == 0) {
+    *dist = dist0 + prjaxis + prjvec;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + vec[i] + axis[i] - n[i] * (*dist * 0.5f);
+  } else if (k == 1) {
+    *dist = dist0 - prjaxis + prjvec;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + vec[i] - axis[i] - n[i] * (*dist * 0.5f);
+  } else {
+    *dist = dist0 + prjaxis - prjvec * 0.5f;
+    float v1[3];
+    cross3(v1, vec, axis);
+    normalize3(v1);
+    const float s = r * sqrtf(3.0f) * 0.5f, sg = k == 2 ? 1.0f : -1.0f;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + sg * v1[i] * s + axis[i] - vec[i] * 0.5f - n[i] * (*dist * 0.5f);
+  }
+}
+
+// collision_driver.py:274-321 on global frames
+__device__ bool broadphase(const mjw_model_t& m, int wid, const float* gx, const float* gm, int g1, int g2) {
+  const float* geom_aabb = MR(geom_aabb);
+  const float* geom_rbound = MR(geom_rbound);
+  const float* geom_margin = MR(geom_margin);
+  const float rb1 = geom_rbound[g1], rb2 = geom_rbound[g2], mg1 = geom_margin[g1], mg2 = geom_margin[g2];
+  const float *xp1 = gx + 3 * g1, *xp2 = gx + 3 * g2, *xm1 = gm + 9 * g1, *xm2 = gm + 9 * g2;
+  const int filt = m.opt_broadphase_filter;
+  if (rb1 == 0.0f || rb2 == 0.0f) {
+    if (filt & FILTER_PLANE) {
+      if (rb1 == 0.0f) {
+        float dif[3] = {xp2[0] - xp1[0], xp2[1] - xp1[1], xp2[2] - xp1[2]}, n[3] = {xm1[2], xm1[5], xm1[8]};
+        return dot3(dif, n) <= rb2 + mg1 + mg2;
+      }
+      float dif[3] = {xp1[0] - xp2[0], xp1[1] - xp2[1], xp1[2] - xp2[2]}, n[3] = {xm2[2], xm2[5], xm2[8]};
+      return dot3(dif, n) <= rb1 + mg1 + mg2;
+    }
+    return true;
+  }
+  if (filt & FILTER_SPHERE) {
+    const float bound = rb1 + rb2 + mg1 + mg2;
+    float dif[3] = {xp2[0] - xp1[0], xp2[1] - xp1[1], xp2[2] - xp1[2]};
+    if (!(dot3(dif, dif) <= bound * bound)) return false;
+  }
+  if (filt & FILTER_AABB)
+    if (!aabb_filter(geom_aabb + 6 * g1, geom_aabb + 6 * g2, geom_aabb + 6 * g1 + 3, geom_aabb + 6 * g2 + 3, mg1 + mg2, xp1, xp2, xm1, xm2))
+      return false;
+  if (filt & FILTER_OBB)
+    if (!obb_filter(geom_aabb + 6 * g1, geom_aabb + 6 * g2, geom_aabb + 6 * g1 + 3, geom_aabb + 6 * g2 + 3, mg1 + mg2, xp1, xp2, xm1, xm2))
+      return false;
+  return true;
+}
+
+struct ConOut {
+  float margin, includemargin;
+  int condim, g1, g2, flex, vert;
+  float friction[5], solref[2], solreffriction[2], solimp[5];
+};
+
+// `frame` (9, optional) keeps the narrowphase's own tangents (plane_capsule / capsule_capsule align
+// them with the capsule axis, collision_primitive.py); otherwise make_frame(nrm) (math.py:246-257)
+__device__ void write_contact(const mjw_model_t& m, const mjw_data_t& d, int wid, int slot, const ConOut& o, float dist, const float* pos,
+                              const float* nrm, const float* frame = nullptr) {
+  if (slot < 0 || slot >= d.naconmax) return;
+  d.contact_dist[slot] = dist;
+  for (int i = 0; i < 3; i++) d.contact_pos[3 * (long)slot + i] = pos[i];
+  float fr[9];
+  if (frame) {
+    for (int i = 0; i < 9; i++) fr[i] = frame[i];
+  } else {
+    make_frame(fr, nrm);
+  }
+  for (int i = 0; i < 9; i++) d.contact_frame[9 * (long)slot + i] = fr[i];
+  d.contact_includemargin[slot] = o.includemargin;
+  for (int i = 0; i < 5; i++) d.contact_friction[5 * (long)slot + i] = o.friction[i];
+  for (int i = 0; i < 2; i++) d.contact_solref[2 * (long)slot + i] = o.solref[i];
+  for (int i = 0; i < 2; i++) d.contact_solreffriction[2 * (long)slot + i] = o.solreffriction[i];
+  for (int i = 0; i < 5; i++) d.contact_solimp[5 * (long)slot + i] = o.solimp[i];
+  d.contact_dim[slot] = o.condim;
+  d.contact_geom[2 * (long)slot] = o.g1;
+  d.contact_geom[2 * (long)slot + 1] = o.g2;
+  d.contact_flex[2 * (long)slot] = -1;
+  d.contact_flex[2 * (long)slot + 1] = o.flex;
+  d.contact_vert[2 * (long)slot] = -1;
+  d.contact_vert[2 * (long)slot + 1] = o.vert;
+  for (int i = 0; i < m.nmaxpyramid; i++) d.contact_efc_address[(long)slot * m.nmaxpyramid + i] = -1;
+  d.contact_worldid[slot] = wid;
+  d.contact_type[slot] = 1;
+  d.contact_geomcollisionid[slot] = 0;
+}
+
+// one collision item: a geom pair, a (flex element, collidable geom) pair or a (flex vertex, plane)
+// pair.  Returns the number of contacts; writes them from pool slot `base` when base >= 0.
+__device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed) {
+  const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
+  const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;
+  const float* geom_size = MR(geom_size);
+  int cnt = 0;
+  if (item < m.nxn) {
+    int g1 = m.nxn_geom_pair[2 * item], g2 = m.nxn_geom_pair[2 * item + 1];
+    if (!(broadphase(m, wid, gx, gm, g1, g2) || m.nxn_pairid[2 * item + 1] >= 0)) return 0;
+    if (npassed) (*npassed)++;
+    ConOut o;
+    float gap;
+    contact_params(m, wid, g1, g2, &o.margin, &gap, &o.condim, o.friction, o.solref, o.solimp);
+    o.includemargin = o.margin - gap;
+    o.solreffriction[0] = o.solreffriction[1] = 0.0f;
+    o.g1 = g1;
+    o.g2 = g2;
+    o.flex = o.vert = -1;
+    const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+    const float *p1 = gx + 3 * g1, *p2 = gx + 3 * g2, *r1 = gm + 9 * g1, *r2 = gm + 9 * g2;
+    const float *s1 = geom_size + 3 * g1, *s2 = geom_size + 3 * g2;
+    const float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
+    const int ncand = (t1 == GEOM_PLANE && t2 == GEOM_BOX) ? 8 : ((t1 == GEOM_PLANE && t2 == GEOM_CYLINDER) ? 4 : 2);
+    Con2 c;
+    c.n = 0;
+    if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) {
+      c.dist[0] = plane_sphere(c.pos[0], n1, p1, p2, s2[0]);
+      make_frame(c.frame[0], n1);
+      c.n = 1;
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_CAPSULE) {
+      plane_capsule(c, n1, p1, p2, n2, s2[0], s2[1]);
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
+      float nrm[3];
+      c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], p2, s2[0]);
+      make_frame(c.frame[0], nrm);
+      c.n = 1;
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
+      float a[3], b[3], pt[3], nrm[3];
+      for (int i = 0; i < 3; i++) { a[i] = p2[i] - n2[i] * s2[1]; b[i] = p2[i] + n2[i] * s2[1]; }
+      closest_segment_point(pt, a, b, p1);
+      c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], pt, s2[0]);
+      make_frame(c.frame[0], nrm);
+      c.n = 1;
+    } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
+      capsule_capsule(c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], o.margin);
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_BOX) {
+      float nrm[3];
+      c.dist[0] = sphere_box(c.pos[0], nrm, p1, s1[0], p2, r2, s2);
+      make_frame(c.frame[0], nrm);
+      c.n = 1;
+    } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {
+      capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
+    }
+    const int nk = ncand == 2 ? c.n : ncand;
+    for (int k = 0; k < nk; k++) {
+      float dist, pos[3], nrm[3];
+      if (ncand == 8) {
+        dist = plane_box_corner(k, n1, p1, p2, r2, s2, pos);
+        for (int i = 0; i < 3; i++) nrm[i] = n1[i];
+      } else if (ncand == 4) {
+        plane_cylinder_k(k, n1, p1, p2, n2, s2[0], s2[1], &dist, pos);
+        for (int i = 0; i < 3; i++) nrm[i] = n1[i];
+      } else {
+        dist = c.dist[k];
+        for (int i = 0; i < 3; i++) { pos[i] = c.pos[k][i]; nrm[i] = c.frame[k][i]; }
+      }
+      if (!(dist < o.margin) || m.nxn_pairid[2 * item] < -1) continue;
+      if (base >= 0) write_contact(m, d, wid, base + cnt, o, dist, pos, nrm, ncand == 2 ? c.frame[k] : nullptr);
+      cnt++;
+    }
+    return cnt;
+  }
+  item -= m.nxn;
+  const float* fx = d.flexvert_xpos + (long)wid * m.nflexvert * 3;
+  for (int f = 0; f < m.nflex; f++) {
+    const int ncg = m.flex_cgeomadr[f + 1] - m.flex_cgeomadr[f];
+    const int nitem = m.flex_dim[f] == 2 ? m.flex_elemnum[f] * ncg : 0;
+    if (item >= nitem) {
+      item -= nitem;
+      continue;
+    }
+    const int el = item / ncg, g = m.flex_cgeom[m.flex_cgeomadr[f] + item % ncg];
+    const int* ev = m.flex_elem + m.flex_elemdataadr[f] + 3 * el;
+    const float* t[3];
+    float cen[3] = {0.0f, 0.0f, 0.0f}, rad = 0.0f;
+    for (int k = 0; k < 3; k++) {
+      t[k] = fx + 3 * (m.flex_vertadr[f] + ev[k]);
+      for (int i = 0; i < 3; i++) cen[i] += t[k][i] * (1.0f / 3.0f);
+    }
+    for (int k = 0; k < 3; k++) {
+      float dv[3] = {t[k][0] - cen[0], t[k][1] - cen[1], t[k][2] - cen[2]};
+      rad = fmaxf(rad, sqrtf(dot3(dv, dv)));
+    }
+    const float tr = MR(flex_radius)[f];
+    const float margin = MR(geom_margin)[g] + MR(flex_margin)[f];
+    // exact bounding-sphere cull: every candidate distance is at least the sphere gap
+    float dg[3] = {gx[3 * g] - cen[0], gx[3 * g + 1] - cen[1], gx[3 * g + 2] - cen[2]};
+    const float bound = MR(geom_rbound)[g] + rad + tr + fmaxf(margin, 0.0f) + 1e-5f;
+    if (dot3(dg, dg) > bound * bound) return 0;
+    Cand c[2];
+    const int n = geom_triangle(c, m.geom_type[g], gx + 3 * g, gm + 9 * g, geom_size + 3 * g, t, tr);
+    ConOut o;
+    const float* gf = MR(geom_friction) + 3 * g;
+    o.friction[0] = o.friction[1] = fmaxf(MJW_MINMU, gf[0]);
+    o.friction[2] = fmaxf(MJW_MINMU, gf[1]);
+    o.friction[3] = o.friction[4] = fmaxf(MJW_MINMU, gf[2]);
+    for (int i = 0; i < 2; i++) { o.solref[i] = MR(geom_solref)[2 * g + i]; o.solreffriction[i] = 0.0f; }
+    for (int i = 0; i < 5; i++) o.solimp[i] = MR(geom_solimp)[5 * g + i];
+    o.margin = o.includemargin = margin;
+    o.condim = m.geom_condim[g];
+    o.g1 = g;
+    o.g2 = -1;
+    o.flex = f;
+    o.vert = ev[0];
+    for (int k = 0; k < n; k++) {
+      if (!(c[k].dist < margin) || c[k].dist >= MJW_MAXVAL) continue;
+      if (base >= 0) write_contact(m, d, wid, base + cnt, o, c[k].dist, c[k].pos, c[k].nrm);
+      cnt++;
+    }
+    return cnt;
+  }
+  // flex vertex vs plane
+  const int v = item / max(m.nplane, 1), g = m.plane_geom[item % max(m.nplane, 1)];
+  const int f = m.flex_vertflexid[v];
+  const float *pp = gx + 3 * g, *pr = gm + 9 * g;
+  const float n[3] = {pr[2], pr[5], pr[8]};
+  const float* x = fx + 3 * v;
+  const float df[3] = {x[0] - pp[0], x[1] - pp[1], x[2] - pp[2]};
+  const float margin = MR(geom_margin)[g] + MR(flex_margin)[f];
+  const float fr = MR(flex_radius)[f];
+  const float dist = dot3(df, n) - fr;
+  if (!(dist < margin)) return 0;
+  if (base >= 0) {
+    ConOut o;
+    const float *gf = MR(geom_friction) + 3 * g, *ff = MR(flex_friction) + 3 * f;
+    const float f0 = fmaxf(gf[0], ff[0]), f1 = fmaxf(gf[1], ff[1]), f2 = fmaxf(gf[2], ff[2]);
+    o.friction[0] = o.friction[1] = fmaxf(MJW_MINMU, f0);
+    o.friction[2] = fmaxf(MJW_MINMU, f1);
+    o.friction[3] = o.friction[4] = fmaxf(MJW_MINMU, f2);
+    for (int i = 0; i < 2; i++) { o.solref[i] = MR(geom_solref)[2 * g + i]; o.solreffriction[i] = 0.0f; }
+    for (int i = 0; i < 5; i++) o.solimp[i] = MR(geom_solimp)[5 * g + i];
+    o.margin = o.includemargin = margin;
+    o.condim = max(m.geom_condim[g], m.flex_condim[f]);
+    o.g1 = g;
+    o.g2 = -1;
+    o.flex = f;
+    o.vert = v - m.flex_vertadr[f];
+    float pos[3];
+    for (int i = 0; i < 3; i++) pos[i] = x[i] - n[i] * (dist * 0.5f + fr);
+    write_contact(m, d, wid, base, o, dist, pos, n);
+  }
+  return 1;
+}
+
+__device__ int ncollide_items(const mjw_model_t& m) {
+  int n = m.nxn + m.nflexvert * m.nplane;
+  for (int f = 0; f < m.nflex; f++)
+    if (m.flex_dim[f] == 2) n += m.flex_elemnum[f] * (m.flex_cgeomadr[f + 1] - m.flex_cgeomadr[f]);
+  return n;
+}
+
+// count, reserve one contiguous pool range per world, then write in item order
+__device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Smem& sm) {
+  int* ncw = d.ncon_world + 2 * (long)wid;
+  if (m.opt_disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT)) {
+    if (tid() == 0) { ncw[0] = 0; ncw[1] = 0; }
+    __syncthreads();
+    return;
+  }
+  const int nitem = ncollide_items(m);
+  int cnt = 0, passed = 0;
+  for (int it = tid(); it < nitem; it += BLK) cnt += collide_item(m, d, wid, it, -1, &passed);
+  float v[2] = {(float)cnt, (float)passed};
+  block_sum<2>(v, sm);
+  const int total = (int)v[0];
+  if (tid() == 0) {
+    sm.ival[0] = total ? atomicAdd(d.nacon, total) : 0;
+    if (v[1] > 0.0f) atomicAdd(d.ncollision, (int)v[1]);
+    ncw[0] = sm.ival[0];
+    ncw[1] = total;
+  }
+  __syncthreads();
+  int run = sm.ival[0];
+  if (total) {
+    for (int c0 = 0; c0 < nitem; c0 += BLK) {
+      const int it = c0 + tid();
+      const int n = it < nitem ? collide_item(m, d, wid, it, -1, nullptr) : 0;
+      int chunk;
+      const int off = block_scan(n, chunk, sm);
+      if (n) collide_item(m, d, wid, it, run + off, nullptr);
+      run += chunk;
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// constraint.py make_constraint (joint / flex equality, friction, limits, pyramidal contacts)
+// ---------------------------------------------------------------------------------------------
+// constraint.py:52-121 _efc_row (scalars) + the sparse J row
+__device__ void put_row(const mjw_model_t& m, const mjw_data_t& d, int wid, int r, int nnz, const int* cols, const float* vals, float pos_aref,
+                        float pos_imp, float invweight, const float* solref, const float* solimp, float margin, float frictionloss, int type,
+                        int id) {
+  const float* qvel = d.qvel + (long)wid * m.nv;
+  const long jr = ((long)wid * d.njmax_pad + r) * m.njrow;
+  float vel = 0.0f;
+  for (int k = 0; k < m.njrow; k++) {
+    const bool on = k < nnz;
+    d.efc_J[jr + k] = on ? vals[k] : 0.0f;
+    d.efc_J_colind[jr + k] = on ? cols[k] : 0;
+    if (on) vel += vals[k] * qvel[cols[k]];
+  }
+  d.efc_J_rownnz[(long)wid * d.njmax + r] = nnz;
+  const float timestep = MR(opt_timestep)[0];
+  float timeconst = solref[0], dampratio = solref[1];
+  float dmin = solimp[0], dmax = solimp[1], width = solimp[2], mid = solimp[3], power = solimp[4];
+  if (!(m.opt_disableflags & DSBL_REFSAFE)) timeconst = fmaxf(timeconst, 2.0f * timestep);
+  dmin = clampf(dmin, MJW_MINIMP, MJW_MAXIMP);
+  dmax = clampf(dmax, MJW_MINIMP, MJW_MAXIMP);
+  width = fmaxf(MJW_MINVAL, width);
+  mid = clampf(mid, MJW_MINIMP, MJW_MAXIMP);
+  power = fmaxf(1.0f, power);
+  const float dmax_sq = dmax * dmax;
+  float k = 1.0f / (dmax_sq * timeconst * timeconst * dampratio * dampratio);
+  float b = 2.0f / (dmax * timeconst);
+  if (solref[0] <= 0.0f) k = -solref[0] / dmax_sq;
+  if (solref[1] <= 0.0f) b = -solref[1] / dmax;
+  const float imp_x = fabsf(pos_imp) / width;
+  const float imp_a = (1.0f / powf(mid, power - 1.0f)) * powf(imp_x, power);
+  const float imp_b = 1.0f - (1.0f / powf(1.0f - mid, power - 1.0f)) * powf(1.0f - imp_x, power);
+  float imp = dmin + (imp_x < mid ? imp_a : imp_b) * (dmax - dmin);
+  imp = clampf(imp, dmin, dmax);
+  if (imp_x > 1.0f) imp = dmax;
+  const long gr = (long)wid * d.njmax + r;
+  d.efc_D[(long)wid * d.njmax_pad + r] = 1.0f / fmaxf(invweight * (1.0f - imp) / imp, MJW_MINVAL);
+  d.efc_vel[gr] = vel;
+  d.efc_aref[gr] = -k * imp * pos_aref - b * vel;
+  d.efc_pos[gr] = pos_aref + margin;
+  d.efc_margin[gr] = margin;
+  d.efc_frictionloss[gr] = frictionloss;
+  d.efc_type[gr] = type;
+  d.efc_id[gr] = id;
+}
+
+// rows contributed by item i of a category (cat: 0 eq joint, 1 flex edge of eq e, 2 friction dof,
+// 3 limit joint, 4 contact); writes them from row r0 when r0 >= 0
+__device__ int make_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int cat, int i, int e, int r0) {
+  const float* qpos = d.qpos + (long)wid * m.nq;
+  const float* qpos0 = MR(qpos0);
+  const float* dof_invweight0 = MR(dof_invweight0);
+  const int njmax = d.njmax;
+  if (cat == 0) {
+    if (m.eq_type[i] != EQ_JOINT || !d.eq_active[(long)wid * m.neq + i]) return 0;
+    if (r0 < 0 || r0 >= njmax) return 1;
+    const int j1 = m.eq_obj1id[i], j2 = m.eq_obj2id[i];
+    const float* data = MR(eq_data) + 11 * i;
+    const int da1 = m.jnt_dofadr[j1], qa1 = m.jnt_qposadr[j1];
+    int cols[2] = {da1, 0};
+    float vals[2] = {1.0f, 0.0f}, pos, iw;
+    int nnz = 1;
+    if (j2 > -1) {
+      const int qa2 = m.jnt_qposadr[j2], da2 = m.jnt_dofadr[j2];
+      const float dif = qpos[qa2] - qpos0[qa2];
+      const float rhs = data[0] + dif * (data[1] + dif * (data[2] + dif * (data[3] + dif * data[4])));
+      const float deriv_2 = data[1] + dif * (2.0f * data[2] + dif * (3.0f * data[3] + dif * 4.0f * data[4]));
+      pos = qpos[qa1] - qpos0[qa1] - rhs;
+      iw = dof_invweight0[da1] + dof_invweight0[da2];
+      cols[1] = da2;
+      vals[1] = -deriv_2;
+      nnz = 2;
+    } else {
+      pos = qpos[qa1] - qpos0[qa1] - data[0];
+      iw = dof_invweight0[da1];
+    }
+    put_row(m, d, wid, r0, nnz, cols, vals, pos, pos, iw, MR(eq_solref) + 2 * i, MR(eq_solimp) + 5 * i, 0.0f, 0.0f, CNSTR_EQUALITY, i);
+    return 1;
+  }
+  if (cat == 1) {  // constraint.py:677-790, edge i of the flex of equality e
+    if (r0 < 0 || r0 >= njmax) return 1;
+    const int f = m.eq_obj1id[e];
+    const int v[2] = {m.flex_vertadr[f] + m.flex_edge[2 * i], m.flex_vertadr[f] + m.flex_edge[2 * i + 1]};
+    int cols[6];
+    float vals[6];
+    int nnz = 0;
+    for (int s2 = 0; s2 < 2; s2++) {
+      const int b = m.flex_vertbodyid[v[s2]];
+      for (int k = 0; k < m.body_dofnum[b] && nnz < 6; k++) {
+        cols[nnz] = m.body_dofadr[b] + k;
+        vals[nnz] = d.flexedge_J[((long)wid * m.nflexedge + i) * 6 + nnz];
+        nnz++;
+      }
+    }
+    const float pos = d.flexedge_length[(long)wid * m.nflexedge + i] - MR(flexedge_length0)[i];
+    put_row(m, d, wid, r0, nnz, cols, vals, pos, pos, MR(flexedge_invweight0)[i], MR(eq_solref) + 2 * e, MR(eq_solimp) + 5 * e, 0.0f, 0.0f,
+            CNSTR_EQUALITY, e);
+    return 1;
+  }
+  if (cat == 2) {  // constraint.py:1113-1190
+    const float fl = MR(dof_frictionloss)[i];
+    if (fl <= 0.0f) return 0;
+    if (r0 < 0 || r0 >= njmax) return 1;
+    const float one = 1.0f;
+    put_row(m, d, wid, r0, 1, &i, &one, 0.0f, 0.0f, dof_invweight0[i], MR(dof_solref) + 2 * i, MR(dof_solimp) + 5 * i, 0.0f, fl,
+            CNSTR_FRICTION_DOF, i);
+    return 1;
+  }
+  if (cat == 3) {  // constraint.py:1316-1418
+    const int jt = m.jnt_type[i];
+    if (!m.jnt_limited[i] || !(jt == JNT_SLIDE || jt == JNT_HINGE)) return 0;
+    const float* rng = MR(jnt_range) + 2 * i;
+    const float q = qpos[m.jnt_qposadr[i]];
+    const float dmn = q - rng[0], dmx = rng[1] - q;
+    const float margin = MR(jnt_margin)[i];
+    const float pos = fminf(dmn, dmx) - margin;
+    if (!(pos < 0.0f)) return 0;
+    if (r0 < 0 || r0 >= njmax) return 1;
+    const int da = m.jnt_dofadr[i];
+    const float Jv = (float)(dmn < dmx) * 2.0f - 1.0f;
+    put_row(m, d, wid, r0, 1, &da, &Jv, pos, pos, dof_invweight0[da], MR(jnt_solref) + 2 * i, MR(jnt_solimp) + 5 * i, margin, 0.0f,
+            CNSTR_LIMIT_JOINT, i);
+    return 1;
+  }
+  // cat 4: contact pyramidal (constraint.py:1668-1936); i = pool slot
+  const int condim = d.contact_dim[i];
+  const int nrow = condim == 1 ? 1 : 2 * (condim - 1);
+  const float includemargin = d.contact_includemargin[i];
+  const float pos = d.contact_dist[i] - includemargin;
+  if (!(pos < 0.0f)) return 0;
+  if (r0 < 0) return nrow;
+  const int g1 = d.contact_geom[2 * (long)i], g2 = d.contact_geom[2 * (long)i + 1];
+  const int body1 = g1 >= 0 ? m.geom_bodyid[g1] : m.flex_vertbodyid[m.flex_vertadr[d.contact_flex[2 * (long)i]] + d.contact_vert[2 * (long)i]];
+  const int body2 =
+    g2 >= 0 ? m.geom_bodyid[g2] : m.flex_vertbodyid[m.flex_vertadr[d.contact_flex[2 * (long)i + 1]] + d.contact_vert[2 * (long)i + 1]];
+  const float* biw = MR(body_invweight0);
+  const float iw_base = biw[2 * body1] + biw[2 * body2];
+  const int w1 = m.body_weldid[body1], w2 = m.body_weldid[body2];
+  const float* frame = d.contact_frame + 9 * (long)i;
+  const float* cpos = d.contact_pos + 3 * (long)i;
+  const float* sc = d.subtree_com + (long)wid * m.nbody * 3;
+  const float* cdof = d.cdof + (long)wid * m.nv * 6;
+  float off1[3], off2[3];
+  for (int x = 0; x < 3; x++) {
+    off1[x] = cpos[x] - sc[3 * m.body_rootid[w1] + x];
+    off2[x] = cpos[x] - sc[3 * m.body_rootid[w2] + x];
+  }
+  const float* fr = d.contact_friction + 5 * (long)i;
+  const float iri = MR(opt_impratio_invsqrt)[0];
+  for (int dimid = 0; dimid < nrow; dimid++) {
+    const int r = r0 + dimid;
+    if (r >= njmax) {
+      d.contact_efc_address[(long)i * m.nmaxpyramid + dimid] = -1;
+      continue;
+    }
+    d.contact_efc_address[(long)i * m.nmaxpyramid + dimid] = r;
+    float invweight = iw_base, frii = 0.0f;
+    const int dimid2 = dimid / 2 + 1;
+    if (condim > 1) {
+      const float fri0 = fr[0];
+      frii = fr[dimid2 - 1];
+      invweight = invweight + fri0 * fri0 * invweight;
+      invweight = invweight * 2.0f * fri0 * fri0 * iri * iri;
+    }
+    // union of the two weld bodies' dof chains, descending
+    const long jr = ((long)wid * d.njmax_pad + r) * m.njrow;
+    int i1 = w1 > 0 ? m.body_dofadr[w1] + m.body_dofnum[w1] - 1 : -1;
+    int i2 = w2 > 0 ? m.body_dofadr[w2] + m.body_dofnum[w2] - 1 : -1;
+    int nnz = 0;
+    float vel = 0.0f;
+    const float* qvel = d.qvel + (long)wid * m.nv;
+    while ((i1 >= 0 || i2 >= 0) && nnz < m.njrow) {
+      const int dof = max(i1, i2);
+      const bool in1 = dof == i1, in2 = dof == i2;
+      const float* c = cdof + 6 * dof;
+      float j1p[3] = {0, 0, 0}, j2p[3] = {0, 0, 0}, j1r[3] = {0, 0, 0}, j2r[3] = {0, 0, 0}, cr[3];
+      if (in1) {
+        cross3(cr, c, off1);
+        for (int x = 0; x < 3; x++) { j1p[x] = c[3 + x] + cr[x]; j1r[x] = c[x]; }
+        i1 = m.dof_parentid[i1];
+      }
+      if (in2) {
+        cross3(cr, c, off2);
+        for (int x = 0; x < 3; x++) { j2p[x] = c[3 + x] + cr[x]; j2r[x] = c[x]; }
+        i2 = m.dof_parentid[i2];
+      }
+      float Jval = 0.0f, Ji = 0.0f;
+      for (int x = 0; x < 3; x++) {
+        const float jd = j2p[x] - j1p[x];
+        Jval += frame[x] * jd;
+        if (condim > 1) {
+          if (dimid2 < 3) Ji += frame[3 * dimid2 + x] * jd;
+          else Ji += frame[3 * (dimid2 - 3) + x] * (j2r[x] - j1r[x]);
+        }
+      }
+      if (condim > 1) Jval += (dimid % 2 == 0) ? Ji * frii : -Ji * frii;
+      d.efc_J[jr + nnz] = Jval;
+      d.efc_J_colind[jr + nnz] = dof;
+      vel += Jval * qvel[dof];
+      nnz++;
+    }
+    for (int k = nnz; k < m.njrow; k++) {
+      d.efc_J[jr + k] = 0.0f;
+      d.efc_J_colind[jr + k] = 0;
+    }
+    d.efc_J_rownnz[(long)wid * njmax + r] = nnz;
+    const int type = condim == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
+    const float* sr = d.contact_solref + 2 * (long)i;
+    const float* si = d.contact_solimp + 5 * (long)i;
+    // same scalar math as put_row, keeping the J row written above
+    const float timestep = MR(opt_timestep)[0];
+    float timeconst = sr[0], dampratio = sr[1];
+    float dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
+    if (!(m.opt_disableflags & DSBL_REFSAFE)) timeconst = fmaxf(timeconst, 2.0f * timestep);
+    dmin = clampf(dmin, MJW_MINIMP, MJW_MAXIMP);
+    dmax = clampf(dmax, MJW_MINIMP, MJW_MAXIMP);
+    width = fmaxf(MJW_MINVAL, width);
+    mid = clampf(mid, MJW_MINIMP, MJW_MAXIMP);
+    power = fmaxf(1.0f, power);
+    const float dmax_sq = dmax * dmax;
+    float kk = 1.0f / (dmax_sq * timeconst * timeconst * dampratio * dampratio);
+    float bb = 2.0f / (dmax * timeconst);
+    if (sr[0] <= 0.0f) kk = -sr[0] / dmax_sq;
+    if (sr[1] <= 0.0f) bb = -sr[1] / dmax;
+    const float imp_x = fabsf(pos) / width;
+    const float imp_a = (1.0f / powf(mid, power - 1.0f)) * powf(imp_x, power);
+    const float imp_b = 1.0f - (1.0f / powf(1.0f - mid, power - 1.0f)) * powf(1.0f - imp_x, power);
+    float imp = dmin + (imp_x < mid ? imp_a : imp_b) * (dmax - dmin);
+    imp = clampf(imp, dmin, dmax);
+    if (imp_x > 1.0f) imp = dmax;
+    const long gr = (long)wid * njmax + r;
+    d.efc_D[(long)wid * d.njmax_pad + r] = 1.0f / fmaxf(invweight * (1.0f - imp) / imp, MJW_MINVAL);
+    d.efc_vel[gr] = vel;
+    d.efc_aref[gr] = -kk * imp * pos - bb * vel;
+    d.efc_pos[gr] = pos + includemargin;
+    d.efc_margin[gr] = includemargin;
+    d.efc_frictionloss[gr] = 0.0f;
+    d.efc_type[gr] = type;
+    d.efc_id[gr] = i;
+  }
+  return nrow;
+}
+
+__device__ void make_constraint(const mjw_model_t& m, const mjw_data_t& d, int wid, Smem& sm) {
+  int run = 0, ne = 0, nf = 0, nl = 0;
+  const int dsbl = m.opt_disableflags;
+  if (!(dsbl & DSBL_CONSTRAINT)) {
+    const int ncon_base = d.ncon_world[2 * (long)wid], ncon = d.ncon_world[2 * (long)wid + 1];
+    for (int cat = 0; cat < 5; cat++) {
+      if (cat <= 1 && (dsbl & DSBL_EQUALITY)) continue;
+      if (cat == 2 && (dsbl & DSBL_FRICTIONLOSS)) continue;
+      if (cat == 3 && (dsbl & DSBL_LIMIT)) continue;
+      if (cat == 4 && (dsbl & DSBL_CONTACT)) continue;
+      const int start = run;
+      const int neqs = cat == 1 ? m.neq : 1;
+      for (int e = 0; e < neqs; e++) {
+        int n_items, i0 = 0;
+        if (cat == 0) n_items = m.neq;
+        else if (cat == 1) {
+          if (m.eq_type[e] != EQ_FLEX || !d.eq_active[(long)wid * m.neq + e]) continue;
+          const int f = m.eq_obj1id[e];
+          i0 = m.flex_edgeadr[f];
+          n_items = m.flex_edgenum[f];
+        } else if (cat == 2) n_items = m.nv;
+        else if (cat == 3) n_items = m.njnt;
+        else {
+          i0 = ncon_base;
+          n_items = min(ncon, max(d.naconmax - ncon_base, 0));
+        }
+        for (int c0 = 0; c0 < n_items; c0 += BLK) {
+          const int it = c0 + tid();
+          const int n = it < n_items ? make_rows(m, d, wid, cat, i0 + it, e, -1) : 0;
+          int chunk;
+          const int off = block_scan(n, chunk, sm);
+          if (n) make_rows(m, d, wid, cat, i0 + it, e, run + off);
+          run += chunk;
+        }
+      }
+      if (cat <= 1) ne += run - start;
+      else if (cat == 2) nf += run - start;
+      else if (cat == 3) nl += run - start;
+    }
+  }
+  if (tid() == 0) {
+    d.ne[wid] = ne;
+    d.nf[wid] = nf;
+    d.nl[wid] = nl;
+    d.nefc[wid] = run;
+  }
+  __syncthreads();
+}
+
+// smooth.py:2041-2147 joint transmissions (packed moment rows, actuator order)
+__device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid, Smem& sm) {
+  const float* gear_all = MR(actuator_gear);
+  const float* qpos = d.qpos + (long)wid * m.nq;
+  int carry = 0;
+  for (int a0 = 0; a0 < m.nu; a0 += BLK) {
+    const int a = a0 + tid();
+    int nnz = 0;
+    if (a < m.nu) {
+      const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
+      nnz = jt0 == JNT_FREE ? 6 : (jt0 == JNT_BALL ? 3 : 1);
+    }
+    int chunk;
+    const int rowadr = carry + block_scan(nnz, chunk, sm);
+    carry += chunk;
+    if (a >= m.nu) continue;
+    const float* gear = gear_all + 6 * a;
+    const int trn = m.actuator_trntype[a], j = m.actuator_trnid[2 * a];
+    const int jt = m.jnt_type[j], qa = m.jnt_qposadr[j], va = m.jnt_dofadr[j];
+    float mom[6] = {0, 0, 0, 0, 0, 0}, length;
+    if (jt == JNT_FREE) {
+      length = 0.0f;
+      if (trn == 1) {
+        float q[4] = {qpos[qa + 3], qpos[qa + 4], qpos[qa + 5], qpos[qa + 6]}, ga[3];
+        normalize4(q);
+        float qn[4] = {q[0], -q[1], -q[2], -q[3]};
+        rot_vec_quat(ga, gear + 3, qn);
+        for (int i = 0; i < 3; i++) { mom[i] = gear[i]; mom[3 + i] = ga[i]; }
+      } else {
+        for (int i = 0; i < 6; i++) mom[i] = gear[i];
+      }
+    } else if (jt == JNT_BALL) {
+      float q[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]}, aa[3];
+      normalize4(q);
+      quat_to_vel(aa, q);
+      float ga[3] = {gear[0], gear[1], gear[2]};
+      if (trn == 1) {
+        float qn[4] = {q[0], -q[1], -q[2], -q[3]};
+        rot_vec_quat(ga, ga, qn);
+      }
+      length = dot3(aa, ga);
+      for (int i = 0; i < 3; i++) mom[i] = ga[i];
+    } else {
+      length = qpos[qa] * gear[0];
+      mom[0] = gear[0];
+    }
+    const long gu = (long)wid * m.nu + a;
+    d.actuator_length[gu] = length;
+    d.moment_rownnz[gu] = nnz;
+    d.moment_rowadr[gu] = rowadr;
+    for (int k = 0; k < nnz; k++) {
+      d.actuator_moment[(long)wid * m.nJmom + rowadr + k] = mom[k];
+      d.moment_colind[(long)wid * m.nJmom + rowadr + k] = va + k;
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// velocity: actuator velocity, com_vel (smooth.py:1935-2038), passive (passive.py:70-179, 566-725),
+// rne (smooth.py:1112-1274)
+// ---------------------------------------------------------------------------------------------
+__device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const int nb = m.nbody, nv = m.nv;
+  const float* qvel = d.qvel + (long)wid * nv;
+  const float* cdof = d.cdof + (long)wid * nv * 6;
+  for (int a = tid(); a < m.nu; a += BLK) {
+    const long gu = (long)wid * m.nu + a;
+    float v = 0.0f;
+    for (int k = 0; k < d.moment_rownnz[gu]; k++) {
+      const long p = (long)wid * m.nJmom + d.moment_rowadr[gu] + k;
+      v += d.actuator_moment[p] * qvel[d.moment_colind[p]];
+    }
+    d.actuator_velocity[gu] = v;
+  }
+  // com_vel: cvel of the parent = sum over the ancestors' dofs; then this body's joints in order
+  float* cvel_all = d.cvel + (long)wid * nb * 6;
+  float* cdot = d.cdof_dot + (long)wid * nv * 6;
+  for (int b = tid(); b < nb; b += BLK) {
+    float cv[6] = {0, 0, 0, 0, 0, 0};
+    for (int p = m.body_parentid[b]; p > 0; p = m.body_parentid[p])
+      for (int k = 0; k < m.body_dofnum[p]; k++) {
+        const int dof = m.body_dofadr[p] + k;
+        for (int i = 0; i < 6; i++) cv[i] += cdof[6 * dof + i] * qvel[dof];
+      }
+    if (b > 0) {
+      int dof = m.body_dofadr[b];
+      for (int j = m.body_jntadr[b]; j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
+        const int jt = m.jnt_type[j];
+        if (jt == JNT_FREE) {
+          for (int k = 0; k < 3; k++) {
+            for (int i = 0; i < 6; i++) { cv[i] += cdof[6 * (dof + k) + i] * qvel[dof + k]; cdot[6 * (dof + k) + i] = 0.0f; }
+          }
+          for (int k = 3; k < 6; k++) motion_cross(cdot + 6 * (dof + k), cv, cdof + 6 * (dof + k));
+          for (int k = 3; k < 6; k++)
+            for (int i = 0; i < 6; i++) cv[i] += cdof[6 * (dof + k) + i] * qvel[dof + k];
+          dof += 6;
+        } else if (jt == JNT_BALL) {
+          for (int k = 0; k < 3; k++) motion_cross(cdot + 6 * (dof + k), cv, cdof + 6 * (dof + k));
+          for (int k = 0; k < 3; k++)
+            for (int i = 0; i < 6; i++) cv[i] += cdof[6 * (dof + k) + i] * qvel[dof + k];
+          dof += 3;
+        } else {
+          motion_cross(cdot + 6 * dof, cv, cdof + 6 * dof);
+          for (int i = 0; i < 6; i++) cv[i] += cdof[6 * dof + i] * qvel[dof];
+          dof += 1;
+        }
+      }
+    }
+    for (int i = 0; i < 6; i++) cvel_all[6 * b + i] = cv[i];
+  }
+  // passive: joint springs / dampers
+  const int dsbl_spring = m.opt_disableflags & DSBL_SPRING, dsbl_damper = m.opt_disableflags & DSBL_DAMPER;
+  float* qs = d.qfrc_spring + (long)wid * nv;
+  float* qd = d.qfrc_damper + (long)wid * nv;
+  const float* qpos = d.qpos + (long)wid * m.nq;
+  const float* stiffness = MR(jnt_stiffness);
+  const float* damping = MR(dof_damping);
+  const float* qpos_spring = MR(qpos_spring);
+  for (int j = tid(); j < m.njnt; j += BLK) {
+    const int da = m.jnt_dofadr[j], qa = m.jnt_qposadr[j], jt = m.jnt_type[j];
+    const int nd = jt == JNT_FREE ? 6 : (jt == JNT_BALL ? 3 : 1);
+    for (int k = 0; k < nd; k++) qs[da + k] = qd[da + k] = 0.0f;
+    if (dsbl_spring && dsbl_damper) continue;
+    const float stiff = stiffness[j], damp = damping[da];
+    const bool has_s = stiff != 0.0f && !dsbl_spring, has_d = damp != 0.0f && !dsbl_damper;
+    if (jt == JNT_FREE) {
+      if (has_s) {
+        for (int i = 0; i < 3; i++) qs[da + i] = -stiff * (qpos[qa + i] - qpos_spring[qa + i]);
+        float rot[4] = {qpos[qa + 3], qpos[qa + 4], qpos[qa + 5], qpos[qa + 6]}, dif[3];
+        normalize4(rot);
+        quat_sub(dif, rot, qpos_spring + qa + 3);
+        for (int i = 0; i < 3; i++) qs[da + 3 + i] = -stiff * dif[i];
+      }
+      if (has_d) for (int i = 0; i < 6; i++) qd[da + i] = -damp * qvel[da + i];
+    } else if (jt == JNT_BALL) {
+      if (has_s) {
+        float rot[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]}, dif[3];
+        normalize4(rot);
+        quat_sub(dif, rot, qpos_spring + qa);
+        for (int i = 0; i < 3; i++) qs[da + i] = -stiff * dif[i];
+      }
+      if (has_d) for (int i = 0; i < 3; i++) qd[da + i] = -damp * qvel[da + i];
+    } else {
+      if (has_s) qs[da] = -stiff * (qpos[qa] - qpos_spring[qa]);
+      if (has_d) qd[da] = -damp * qvel[da];
+    }
+  }
+  // flex elasticity (per element) and bending (per edge) into scratch, gathered per vertex below
+  float* frc = d.flex_frc + (long)wid * (m.nflexelem * 9 + m.nflexedge * 12);
+  const float* fx = d.flexvert_xpos + (long)wid * m.nflexvert * 3;
+  if (!(dsbl_spring && dsbl_damper) && !dsbl_spring) {
+    const float dt = MR(opt_timestep)[0];
+    const float* stiff = MR(flex_stiffness);
+    for (int f = 0; f < m.nflex; f++) {
+      if (m.flex_dim[f] != 2) continue;
+      const float kD = (dt > 0.0f && !dsbl_damper) ? MR(flex_damping)[f] / dt : 0.0f;
+      const int vb = m.flex_vertadr[f];
+      for (int el = tid(); el < m.flex_elemnum[f]; el += BLK) {
+        const int elemid = m.flex_elemadr[f] + el;
+        const int* ev = m.flex_elem + m.flex_elemdataadr[f] + 3 * el;
+        const int e2[3][2] = {{1, 2}, {2, 0}, {0, 1}};
+        float grad[3][6], elong[3], force[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+        for (int e = 0; e < 3; e++) {
+          const float* x0 = fx + 3 * (vb + ev[e2[e][0]]);
+          const float* x1 = fx + 3 * (vb + ev[e2[e][1]]);
+          for (int i = 0; i < 3; i++) { grad[e][i] = x0[i] - x1[i]; grad[e][3 + i] = x1[i] - x0[i]; }
+          const int idx = m.flex_edgeadr[f] + m.flex_elemedge[m.flex_elemedgeadr[f] + 3 * el + e];
+          const float vel = d.flexedge_velocity[(long)wid * m.nflexedge + idx];
+          const float def = d.flexedge_length[(long)wid * m.nflexedge + idx], ref = MR(flexedge_length0)[idx];
+          const float prev = def - vel * dt;
+          elong[e] = def * def - ref * ref + (def * def - prev * prev) * kD;
+        }
+        float metric[3][3];
+        int id = 0;
+        for (int a = 0; a < 3; a++)
+          for (int b = a; b < 3; b++) { metric[a][b] = metric[b][a] = stiff[21 * elemid + id]; id++; }
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++)
+            for (int s2 = 0; s2 < 2; s2++)
+              for (int x = 0; x < 3; x++) force[e2[b][s2]][x] -= elong[a] * grad[b][3 * s2 + x] * metric[a][b];
+        for (int k = 0; k < 3; k++)
+          for (int x = 0; x < 3; x++) frc[9 * elemid + 3 * k + x] = force[k][x];
+      }
+      for (int e = m.flex_edgeadr[f] + tid(); e < m.flex_edgeadr[f] + m.flex_edgenum[f]; e += BLK) {
+        float* out = frc + 9 * m.nflexelem + 12 * e;
+        if (m.flex_edgeflap[2 * e + 1] == -1) {
+          for (int k = 0; k < 12; k++) out[k] = 0.0f;
+          continue;
+        }
+        const int v[4] = {vb + m.flex_edge[2 * e], vb + m.flex_edge[2 * e + 1], vb + m.flex_edgeflap[2 * e], vb + m.flex_edgeflap[2 * e + 1]};
+        const float* B = MR(flex_bending) + 17 * e;
+        float fr4[4][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+        if (B[16] != 0.0f) {
+          float a1[3], a2[3], a3[3];
+          for (int i = 0; i < 3; i++) {
+            a1[i] = fx[3 * v[1] + i] - fx[3 * v[0] + i];
+            a2[i] = fx[3 * v[2] + i] - fx[3 * v[0] + i];
+            a3[i] = fx[3 * v[3] + i] - fx[3 * v[0] + i];
+          }
+          cross3(fr4[1], a2, a3);
+          cross3(fr4[2], a3, a1);
+          cross3(fr4[3], a1, a2);
+          for (int i = 0; i < 3; i++) fr4[0][i] = -(fr4[1][i] + fr4[2][i] + fr4[3][i]);
+        }
+        for (int i = 0; i < 4; i++)
+          for (int x = 0; x < 3; x++) {
+            float s = 0.0f;
+            for (int j = 0; j < 4; j++) s -= B[4 * i + j] * fx[3 * v[j] + x];
+            out[3 * i + x] = s - B[16] * fr4[i][x];
+          }
+      }
+    }
+  }
+  __syncthreads();
+  // per-vertex gather in a fixed order (flexvert_inc: 4*nflexelem... encoded contributions)
+  if (!(dsbl_spring && dsbl_damper) && !dsbl_spring) {
+    for (int v = tid(); v < m.nflexvert; v += BLK) {
+      const int b = m.flex_vertbodyid[v];
+      if (m.body_dofnum[b] == 0) continue;
+      float s[3] = {0.0f, 0.0f, 0.0f};
+      for (int p = m.flexvert_incadr[v]; p < m.flexvert_incadr[v + 1]; p++) {
+        const int code = m.flexvert_inc[p];  // 3*elem + k (element vertex slot) or 3*nflexelem + 4*edge + k
+        const float* src = code < 3 * m.nflexelem ? frc + 3 * code : frc + 9 * m.nflexelem + 3 * (code - 3 * m.nflexelem);
+        for (int x = 0; x < 3; x++) s[x] += src[x];
+      }
+      for (int x = 0; x < 3; x++) qs[m.body_dofadr[b] + x] += s[x];
+    }
+  }
+  __syncthreads();
+  float* qp = d.qfrc_passive + (long)wid * nv;
+  for (int i = tid(); i < nv; i += BLK) qp[i] = qs[i] + qd[i];
+  // rne: cacc by ancestor walk, body forces into scratch, subtree sums, projection on cdof
+  float* cacc = d.cacc + (long)wid * nb * 6;
+  float* body_f = d.sp_body + (long)wid * nb * 6;
+  const float* cinert = d.cinert + (long)wid * nb * 10;
+  const float* grav = MR(opt_gravity);
+  const bool gravity = !(m.opt_disableflags & DSBL_GRAVITY);
+  for (int b = tid(); b < nb; b += BLK) {
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+    if (gravity) for (int i = 0; i < 3; i++) acc[3 + i] = -grav[i];
+    for (int p = b; p > 0; p = m.body_parentid[p])
+      for (int k = 0; k < m.body_dofnum[p]; k++) {
+        const int dof = m.body_dofadr[p] + k;
+        for (int i = 0; i < 6; i++) acc[i] += cdot[6 * dof + i] * qvel[dof];
+      }
+    for (int i = 0; i < 6; i++) cacc[6 * b + i] = acc[i];
+    if (b == 0) {
+      for (int i = 0; i < 6; i++) body_f[i] = 0.0f;
+      continue;
+    }
+    float f1[6], iv[6], f2[6];
+    inert_vec(f1, cinert + 10 * b, acc);
+    inert_vec(iv, cinert + 10 * b, cvel_all + 6 * b);
+    motion_cross_force(f2, cvel_all + 6 * b, iv);
+    for (int i = 0; i < 6; i++) body_f[6 * b + i] = f1[i] + f2[i];
+  }
+  __syncthreads();
+  float* cfrc = d.cfrc_int + (long)wid * nb * 6;
+  for (int b = tid(); b < nb; b += BLK) {
+    float s[6] = {0, 0, 0, 0, 0, 0};
+    for (int c = b; c < m.body_subtree_end[b]; c++)
+      for (int i = 0; i < 6; i++) s[i] += body_f[6 * c + i];
+    for (int i = 0; i < 6; i++) cfrc[6 * b + i] = s[i];
+  }
+  __syncthreads();
+  float* bias = d.qfrc_bias + (long)wid * nv;
+  for (int i = tid(); i < nv; i += BLK) {
+    const float* c = cfrc + 6 * m.dof_bodyid[i];
+    float s = 0.0f;
+    for (int k = 0; k < 6; k++) s += cdof[6 * i + k] * c[k];
+    bias[i] = s;
+  }
+  __syncthreads();
+}
+
+// forward.py:616-927 actuation (gain / bias / activation dynamics, joint actuator force limits)
+__device__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const int nv = m.nv;
+  float* qa = d.qfrc_actuator + (long)wid * nv;
+  if (!m.nu || (m.opt_disableflags & DSBL_ACTUATION)) {
+    for (int i = tid(); i < nv; i += BLK) qa[i] = 0.0f;
+    for (int a = tid(); a < m.na; a += BLK) d.act_dot[(long)wid * m.na + a] = 0.0f;
+    __syncthreads();
+    return;
+  }
+  const float* ctrlrange = MR(actuator_ctrlrange);
+  const float* forcerange = MR(actuator_forcerange);
+  const float* gainprm = MR(actuator_gainprm);
+  const float* biasprm = MR(actuator_biasprm);
+  const float* dynprm = MR(actuator_dynprm);
+  for (int a = tid(); a < m.nu; a += BLK) {
+    float ctrl = d.ctrl[(long)wid * m.nu + a];
+    if (m.actuator_ctrllimited[a] && !(m.opt_disableflags & DSBL_CLAMPCTRL)) ctrl = clampf(ctrl, ctrlrange[2 * a], ctrlrange[2 * a + 1]);
+    float ctrl_act = ctrl;
+    const int act_first = m.actuator_actadr[a];
+    if (m.na && act_first >= 0) {
+      const int last = act_first + m.actuator_actnum[a] - 1, dt = m.actuator_dyntype[a];
+      const float act = d.act[(long)wid * m.na + last];
+      float act_dot = 0.0f;
+      if (dt == DYN_INTEGRATOR) act_dot = ctrl;
+      else if (dt == DYN_FILTER || dt == DYN_FILTEREXACT) act_dot = (ctrl - act) / fmaxf(dynprm[10 * a], MJW_MINVAL);
+      d.act_dot[(long)wid * m.na + last] = act_dot;
+      ctrl_act = m.actuator_actearly[a]
+                   ? next_act(MR(opt_timestep)[0], dt, dynprm[10 * a], MR(actuator_actrange) + 2 * a, act, act_dot, 1.0f, m.actuator_actlimited[a] != 0)
+                   : act;
+    }
+    const long gu = (long)wid * m.nu + a;
+    const float len = d.actuator_length[gu], vel = d.actuator_velocity[gu];
+    const float *gp = gainprm + 10 * a, *bp = biasprm + 10 * a;
+    float gain = 0.0f, bias = 0.0f;
+    if (m.actuator_gaintype[a] == GAIN_FIXED) gain = gp[0];
+    else if (m.actuator_gaintype[a] == GAIN_AFFINE) gain = gp[0] + gp[1] * len + gp[2] * vel;
+    if (m.actuator_biastype[a] == BIAS_AFFINE) bias = bp[0] + bp[1] * len + bp[2] * vel;
+    float force = gain * ctrl_act + bias;
+    if (m.actuator_forcelimited[a]) force = clampf(force, forcerange[2 * a], forcerange[2 * a + 1]);
+    d.actuator_force[gu] = force;
+  }
+  __syncthreads();
+  const float* jfr = MR(jnt_actfrcrange);
+  for (int i = tid(); i < nv; i += BLK) {
+    float q = 0.0f;
+    for (int a = 0; a < m.nu; a++) {
+      const long gu = (long)wid * m.nu + a;
+      const int adr = d.moment_rowadr[gu];
+      for (int k = 0; k < d.moment_rownnz[gu]; k++)
+        if (d.moment_colind[(long)wid * m.nJmom + adr + k] == i) q += d.actuator_moment[(long)wid * m.nJmom + adr + k] * d.actuator_force[gu];
+    }
+    const int j = m.dof_jntid[i];
+    if (m.jnt_actfrclimited[j]) q = clampf(q, jfr[2 * j], jfr[2 * j + 1]);
+    qa[i] = q;
+  }
+  __syncthreads();
+}
+
+// forward.py:930-969 + support.py:174-237 (xfrc over the dof's subtree) + tree factor / solve
+__device__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const int nv = m.nv;
+  const float* cdof = d.cdof + (long)wid * nv * 6;
+  const float* xfrc = d.xfrc_applied + (long)wid * m.nbody * 6;
+  const float* xipos = d.xipos + (long)wid * m.nbody * 3;
+  const float* sc = d.subtree_com + (long)wid * m.nbody * 3;
+  float* qs = d.qfrc_smooth + (long)wid * nv;
+  float* qacc_s = d.qacc_smooth + (long)wid * nv;
+  for (int i = tid(); i < nv; i += BLK) {
+    float v = d.qfrc_passive[(long)wid * nv + i] - d.qfrc_bias[(long)wid * nv + i] + d.qfrc_actuator[(long)wid * nv + i] +
+              d.qfrc_applied[(long)wid * nv + i];
+    const float* cd = cdof + 6 * i;
+    const int db = m.dof_bodyid[i];
+    for (int b = db; b < m.body_subtree_end[db]; b++) {
+      const float* ft = xfrc + 6 * b;
+      if (ft[0] == 0.0f && ft[1] == 0.0f && ft[2] == 0.0f && ft[3] == 0.0f && ft[4] == 0.0f && ft[5] == 0.0f) continue;
+      float off[3], c[3];
+      for (int k = 0; k < 3; k++) off[k] = xipos[3 * b + k] - sc[3 * m.body_rootid[b] + k];
+      cross3(c, cd, off);
+      v += cd[3] * ft[0] + cd[4] * ft[1] + cd[5] * ft[2] + cd[0] * ft[3] + cd[1] * ft[4] + cd[2] * ft[5] + dot3(c, ft);
+    }
+    qs[i] = v;
+    qacc_s[i] = v;
+  }
+  factor_trees(m, d.qM + (long)wid * m.nM, d.qLD + (long)wid * m.nM, nullptr, 0.0f);
+  __syncthreads();
+  solve_trees(m, d.qLD + (long)wid * m.nM, qacc_s);
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(BLK) forward_kernel(const mjw_model_t m, const mjw_data_t d, int stages) {
+  __shared__ Smem sm;
+  const int wid = blockIdx.x;
+  if (stages & ST_POS) {
+    kinematics(m, d, wid);
+    com_pos(m, d, wid);
+    camlight(m, d, wid);
+    flex_edges(m, d, wid);
+    crb_qM(m, d, wid);
+    collision(m, d, wid, sm);
+    make_constraint(m, d, wid, sm);
+    transmission(m, d, wid, sm);
+  }
+  if (stages & ST_VEL) fwd_velocity(m, d, wid);
+  if (stages & ST_ACT) fwd_actuation(m, d, wid);
+  if (stages & ST_ACC) fwd_acceleration(m, d, wid);
+}
+
+// ---------------------------------------------------------------------------------------------
+// solver.py CG (primal, pyramidal): init_context :3257-3293, iteration :3187-3254, exact
+// iterative linesearch :886-1341, update_constraint :2154-2219, update_gradient :2879-3008
+// ---------------------------------------------------------------------------------------------
+struct SolveCtx {
+  int nv, nefc, ne, nf, njrow;
+  const float* J;
+  const int* Jcol;
+  const int* Jnnz;
+  const int* JT_adr;
+  const int* JT_ind;
+  const float* D;
+  const float* fl;
+  const float* aref;
+  float* force;
+  int* state;
+  float *Jaref, *jv;
+  float *qacc, *Ma, *qfrc_c;
+  const float *qfrc_s, *qacc_s;
+  float *grad, *Mgrad, *search, *mv, *pgrad, *pMgrad;
+  const float *M, *LD;
+  float cost, prev_cost, gauss, search_dot, grad_dot;
+};
+
+__device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, float* o) {
+  const float D = c.D[r], jaref = c.Jaref[r], jv = c.jv[r];
+  const float x = jaref + alpha * jv;
+  if (r >= c.ne + c.nf) {
+    if (x < 0.0f) {
+      const float jvD = jv * D;
+      o[0] += 0.5f * D * x * x;
+      o[1] += jvD * x;
+      o[2] += jv * jvD;
+    }
+    return;
+  }
+  if (r >= c.ne) {
+    const float f = c.fl[r], rf = safe_div(f, D);
+    if (-rf < x && x < rf) {
+      const float jvD = jv * D;
+      o[0] += 0.5f * D * x * x;
+      o[1] += jvD * x;
+      o[2] += jv * jvD;
+    } else if (x <= -rf) {
+      o[0] += f * (-0.5f * rf - x);
+      o[1] += -f * jv;
+    } else {
+      o[0] += f * (-0.5f * rf + x);
+      o[1] += f * jv;
+    }
+    return;
+  }
+  const float jvD = jv * D;
+  o[0] += 0.5f * D * x * x;
+  o[1] += jvD * x;
+  o[2] += jv * jvD;
+}
+
+__device__ void update_constraint(SolveCtx& c, Smem& sm) {
+  float cost = 0.0f;
+  for (int r = tid(); r < c.nefc; r += BLK) {
+    const float D = c.D[r], jaref = c.Jaref[r];
+    float f;
+    int st;
+    if (r < c.ne) {
+      f = -D * jaref;
+      st = STATE_QUADRATIC;
+      cost += 0.5f * D * jaref * jaref;
+    } else if (r < c.ne + c.nf) {
+      const float fl = c.fl[r], rf = safe_div(fl, D);
+      if (jaref <= -rf) { f = fl; st = STATE_LINEARNEG; cost += -fl * (0.5f * rf + jaref); }
+      else if (jaref >= rf) { f = -fl; st = STATE_LINEARPOS; cost += -fl * (0.5f * rf - jaref); }
+      else { f = -D * jaref; st = STATE_QUADRATIC; cost += 0.5f * D * jaref * jaref; }
+    } else {
+      if (jaref >= 0.0f) { f = 0.0f; st = STATE_SATISFIED; }
+      else { f = -D * jaref; st = STATE_QUADRATIC; cost += 0.5f * D * jaref * jaref; }
+    }
+    c.force[r] = f;
+    c.state[r] = st;
+  }
+  __syncthreads();
+  float g = 0.0f;
+  for (int i = tid(); i < c.nv; i += BLK) {
+    float s = 0.0f;
+    for (int p = c.JT_adr[i]; p < c.JT_adr[i + 1]; p++) {
+      const int code = c.JT_ind[p];
+      s += c.J[code] * c.force[code / c.njrow];
+    }
+    c.qfrc_c[i] = s;
+    g += (c.Ma[i] - c.qfrc_s[i]) * (c.qacc[i] - c.qacc_s[i]);
+  }
+  float v[2] = {cost, g};
+  block_sum<2>(v, sm);
+  c.prev_cost = c.cost;
+  c.gauss = 0.5f * v[1];
+  c.cost = v[0] + 0.5f * v[1];
+}
+
+__device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
+  float gd = 0.0f;
+  for (int i = tid(); i < c.nv; i += BLK) {
+    const float g = c.Ma[i] - c.qfrc_s[i] - c.qfrc_c[i];
+    c.grad[i] = g;
+    c.Mgrad[i] = g;
+    gd += g * g;
+  }
+  c.grad_dot = block_sum1(gd, sm);  // syncs
+  solve_trees(m, c.LD, c.Mgrad);
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool in_bracket(const float* x, const float* y) {
+  return (x[1] < y[1] && y[1] < 0.0f) || (x[1] > y[1] && y[1] > 0.0f);
+}
+
+__device__ void linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm) {
+  mul_m_trees(m, c.M, c.search, c.mv);
+  for (int r = tid(); r < c.nefc; r += BLK) {
+    const float* J = c.J + (long)r * c.njrow;
+    const int* col = c.Jcol + (long)r * c.njrow;
+    float s = 0.0f;
+    for (int k = 0; k < c.Jnnz[r]; k++) s += J[k] * c.search[col[k]];
+    c.jv[r] = s;
+  }
+  __syncthreads();
+  const float snorm = sqrtf(c.search_dot);
+  const float scale = MR_W(stat_meaninertia) * (float)c.nv;
+  const float gtol = fmaxf(MR_W(opt_tolerance) * MR_W(opt_ls_tolerance) * snorm * scale, 1e-6f);
+  float v5[5] = {0, 0, 0, 0, 0};
+  for (int r = tid(); r < c.nefc; r += BLK) eval_row(c, r, 0.0f, v5);
+  for (int i = tid(); i < c.nv; i += BLK) {
+    v5[3] += c.search[i] * (c.Ma[i] - c.qfrc_s[i]);
+    v5[4] += 0.5f * c.search[i] * c.mv[i];
+  }
+  block_sum<5>(v5, sm);
+  const float qg0 = c.gauss, qg1 = v5[3], qg2 = v5[4];
+  const float p0[3] = {qg0 + v5[0], qg1 + v5[1], 2.0f * qg2 + v5[2]};
+  auto gauss_at = [&](float a, float* o) {
+    o[0] = a * a * qg2 + a * qg1 + qg0;
+    o[1] = 2.0f * a * qg2 + qg1;
+    o[2] = 2.0f * qg2;
+  };
+  const float lo_alpha_in = -safe_div(p0[1], p0[2]);
+  float lo_in[3] = {0, 0, 0};
+  for (int r = tid(); r < c.nefc; r += BLK) eval_row(c, r, lo_alpha_in, lo_in);
+  block_sum<3>(lo_in, sm);
+  {
+    float g[3];
+    gauss_at(lo_alpha_in, g);
+    for (int k = 0; k < 3; k++) lo_in[k] += g[k];
+  }
+  float alpha;
+  if (!(fabsf(lo_in[1]) < gtol && lo_in[0] < p0[0])) {
+    alpha = 0.0f;
+    float lo[3], hi[3], lo_alpha, hi_alpha;
+    if (lo_in[1] < p0[1]) {
+      for (int k = 0; k < 3; k++) { lo[k] = lo_in[k]; hi[k] = p0[k]; }
+      lo_alpha = lo_alpha_in;
+      hi_alpha = 0.0f;
+    } else {
+      for (int k = 0; k < 3; k++) { lo[k] = p0[k]; hi[k] = lo_in[k]; }
+      lo_alpha = 0.0f;
+      hi_alpha = lo_alpha_in;
+    }
+    for (int it = 0; it < m.opt_ls_iterations; it++) {
+      const float lo_next_alpha = lo_alpha - safe_div(lo[1], lo[2]);
+      const float hi_next_alpha = hi_alpha - safe_div(hi[1], hi[2]);
+      const float mid_alpha = 0.5f * (lo_alpha + hi_alpha);
+      float v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (int r = tid(); r < c.nefc; r += BLK) {
+        eval_row(c, r, lo_next_alpha, v9);
+        eval_row(c, r, hi_next_alpha, v9 + 3);
+        eval_row(c, r, mid_alpha, v9 + 6);
+      }
+      block_sum<9>(v9, sm);
+      float lo_next[3], hi_next[3], mid[3], g[3];
+      gauss_at(lo_next_alpha, g);
+      for (int k = 0; k < 3; k++) lo_next[k] = g[k] + v9[k];
+      gauss_at(hi_next_alpha, g);
+      for (int k = 0; k < 3; k++) hi_next[k] = g[k] + v9[3 + k];
+      gauss_at(mid_alpha, g);
+      for (int k = 0; k < 3; k++) mid[k] = g[k] + v9[6 + k];
+      const bool s1 = in_bracket(lo, lo_next);
+      if (s1) { for (int k = 0; k < 3; k++) lo[k] = lo_next[k]; lo_alpha = lo_next_alpha; }
+      const bool s2 = in_bracket(lo, mid);
+      if (s2) { for (int k = 0; k < 3; k++) lo[k] = mid[k]; lo_alpha = mid_alpha; }
+      const bool s3 = in_bracket(lo, hi_next);
+      if (s3) { for (int k = 0; k < 3; k++) lo[k] = hi_next[k]; lo_alpha = hi_next_alpha; }
+      const bool h1 = in_bracket(hi, hi_next);
+      if (h1) { for (int k = 0; k < 3; k++) hi[k] = hi_next[k]; hi_alpha = hi_next_alpha; }
+      const bool h2 = in_bracket(hi, mid);
+      if (h2) { for (int k = 0; k < 3; k++) hi[k] = mid[k]; hi_alpha = mid_alpha; }
+      const bool h3 = in_bracket(hi, lo_next);
+      if (h3) { for (int k = 0; k < 3; k++) hi[k] = lo_next[k]; hi_alpha = lo_next_alpha; }
+      const bool done = (!(s1 || s2 || s3) && !(h1 || h2 || h3)) || (lo[1] < 0.0f && lo[1] > -gtol) || (hi[1] > 0.0f && hi[1] < gtol);
+      const bool improved = lo[0] < p0[0] || hi[0] < p0[0];
+      if (improved) alpha = lo[0] < hi[0] ? lo_alpha : hi_alpha;
+      if (done) break;
+    }
+  } else {
+    alpha = lo_alpha_in;
+  }
+  for (int i = tid(); i < c.nv; i += BLK) {
+    c.qacc[i] += alpha * c.search[i];
+    c.Ma[i] += alpha * c.mv[i];
+  }
+  for (int r = tid(); r < c.nefc; r += BLK) c.Jaref[r] += alpha * c.jv[r];
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const mjw_data_t d) {
+  __shared__ Smem sm;
+  const int wid = blockIdx.x;
+  const int nv = m.nv, njmax = d.njmax;
+  float* qacc = d.qacc + (long)wid * nv;
+  const float* qacc_s = d.qacc_smooth + (long)wid * nv;
+  if (njmax == 0 || nv == 0) {
+    for (int i = tid(); i < nv; i += BLK) qacc[i] = qacc_s[i];
+    if (tid() == 0) d.solver_niter[wid] = 0;
+    return;
+  }
+  SolveCtx c;
+  c.nv = nv;
+  c.nefc = min(d.nefc[wid], njmax);
+  c.ne = d.ne[wid];
+  c.nf = d.nf[wid];
+  c.njrow = m.njrow;
+  c.J = d.efc_J + (long)wid * d.njmax_pad * m.njrow;
+  c.Jcol = d.efc_J_colind + (long)wid * d.njmax_pad * m.njrow;
+  c.Jnnz = d.efc_J_rownnz + (long)wid * njmax;
+  int* JT_adr = d.efc_JT_adr + (long)wid * (nv + 1);
+  int* JT_ind = d.efc_JT_rowind + (long)wid * d.njmax_pad * m.njrow;
+  int* cnt = d.sp_cnt + (long)wid * (nv + 1);
+  c.JT_adr = JT_adr;
+  c.JT_ind = JT_ind;
+  c.D = d.efc_D + (long)wid * d.njmax_pad;
+  c.fl = d.efc_frictionloss + (long)wid * njmax;
+  c.aref = d.efc_aref + (long)wid * njmax;
+  c.force = d.efc_force + (long)wid * njmax;
+  c.state = d.efc_state + (long)wid * d.njmax_pad;
+  c.Jaref = d.sp_row + (long)wid * njmax * 2;
+  c.jv = c.Jaref + njmax;
+  c.qacc = qacc;
+  c.Ma = d.efc_Ma + (long)wid * nv;
+  c.qfrc_c = d.qfrc_constraint + (long)wid * nv;
+  c.qfrc_s = d.qfrc_smooth + (long)wid * nv;
+  c.qacc_s = qacc_s;
+  float* vec = d.sp_vec + (long)wid * nv * 10;
+  c.grad = vec;
+  c.Mgrad = vec + nv;
+  c.search = vec + 2 * nv;
+  c.mv = vec + 3 * nv;
+  c.pgrad = vec + 4 * nv;
+  c.pMgrad = vec + 5 * nv;
+  c.M = d.qM + (long)wid * m.nM;
+  c.LD = d.qLD + (long)wid * m.nM;
+  const float* warm = d.qacc_warmstart + (long)wid * nv;
+  const bool ws = !(m.opt_disableflags & DSBL_WARMSTART);
+  // transposed index of J: counts, scan, fill, per-column sort (deterministic J'f)
+  for (int i = tid(); i <= nv; i += BLK) cnt[i] = 0;
+  for (int i = tid(); i < nv; i += BLK) qacc[i] = ws ? warm[i] : qacc_s[i];
+  __syncthreads();
+  for (int r = tid(); r < c.nefc; r += BLK)
+    for (int k = 0; k < c.Jnnz[r]; k++) atomicAdd(&cnt[c.Jcol[(long)r * m.njrow + k]], 1);
+  __syncthreads();
+  int run = 0;
+  for (int c0 = 0; c0 < nv; c0 += BLK) {
+    const int i = c0 + tid();
+    const int n = i < nv ? cnt[i] : 0;
+    int chunk;
+    const int off = block_scan(n, chunk, sm);
+    if (i < nv) { JT_adr[i] = run + off; cnt[i] = run + off; }
+    run += chunk;
+  }
+  if (tid() == 0) JT_adr[nv] = run;
+  __syncthreads();
+  for (int r = tid(); r < c.nefc; r += BLK)
+    for (int k = 0; k < c.Jnnz[r]; k++) {
+      const int pos = atomicAdd(&cnt[c.Jcol[(long)r * m.njrow + k]], 1);
+      JT_ind[pos] = r * m.njrow + k;
+    }
+  __syncthreads();
+  for (int i = tid(); i < nv; i += BLK) {
+    for (int p = JT_adr[i] + 1; p < JT_adr[i + 1]; p++) {
+      const int key = JT_ind[p];
+      int q = p - 1;
+      while (q >= JT_adr[i] && JT_ind[q] > key) { JT_ind[q + 1] = JT_ind[q]; q--; }
+      JT_ind[q + 1] = key;
+    }
+  }
+  for (int r = tid(); r < c.nefc; r += BLK) {
+    float s = 0.0f;
+    for (int k = 0; k < c.Jnnz[r]; k++) s += c.J[(long)r * m.njrow + k] * qacc[c.Jcol[(long)r * m.njrow + k]];
+    c.Jaref[r] = s - c.aref[r];
+  }
+  __syncthreads();
+  mul_m_trees(m, c.M, qacc, c.Ma);
+  __syncthreads();
+  c.cost = MJW_MAXVAL;
+  update_constraint(c, sm);
+  update_gradient(m, c, sm);
+  float sd = 0.0f;
+  for (int i = tid(); i < nv; i += BLK) {
+    c.search[i] = -c.Mgrad[i];
+    sd += c.Mgrad[i] * c.Mgrad[i];
+  }
+  c.search_dot = block_sum1(sd, sm);
+  const float scale = 1.0f / (MR_W(stat_meaninertia) * (float)nv);
+  const float tol = MR_W(opt_tolerance);
+  int niter = 0;
+  if (m.opt_iterations != 0) {
+    for (;;) {
+      linesearch(m, c, wid, sm);
+      for (int i = tid(); i < nv; i += BLK) {
+        c.pgrad[i] = c.grad[i];
+        c.pMgrad[i] = c.Mgrad[i];
+      }
+      __syncthreads();
+      update_constraint(c, sm);
+      update_gradient(m, c, sm);
+      float nd[2] = {0.0f, 0.0f};
+      for (int i = tid(); i < nv; i += BLK) {
+        nd[0] += c.grad[i] * (c.Mgrad[i] - c.pMgrad[i]);
+        nd[1] += c.pgrad[i] * c.pMgrad[i];
+      }
+      block_sum<2>(nd, sm);
+      const float beta = fmaxf(0.0f, nd[0] / fmaxf(MJW_MINVAL, nd[1]));
+      float s2 = 0.0f;
+      for (int i = tid(); i < nv; i += BLK) {
+        const float v = -c.Mgrad[i] + beta * c.search[i];
+        c.search[i] = v;
+        s2 += v * v;
+      }
+      c.search_dot = block_sum1(s2, sm);
+      niter++;
+      const float improvement = (c.prev_cost - c.cost) * scale;
+      const float gradient = sqrtf(c.grad_dot) * scale;
+      if (improvement < tol || gradient < tol || niter == m.opt_iterations) break;
+    }
+  }
+  if (tid() == 0) d.solver_niter[wid] = niter;
+}
+
+// forward.py:326-354 euler with implicit damping (sparse: factor M + dt*diag(damping) per tree)
+__global__ void __launch_bounds__(BLK) euler_kernel(const mjw_model_t m, const mjw_data_t d) {
+  const int wid = blockIdx.x;
+  const int nv = m.nv;
+  const float dt = MR_W(opt_timestep);
+  float* qvel = d.qvel + (long)wid * nv;
+  float* qpos = d.qpos + (long)wid * m.nq;
+  const float* qacc = d.qacc + (long)wid * nv;
+  const float* adv = qacc;
+  if (!(m.opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER))) {
+    float* LD2 = d.sp_LD + (long)wid * m.nM;
+    float* q = d.sp_vec + (long)wid * nv * 10 + 6 * nv;
+    factor_trees(m, d.qM + (long)wid * m.nM, LD2, MR(dof_damping), dt);
+    for (int i = tid(); i < nv; i += BLK) q[i] = d.efc_Ma[(long)wid * nv + i];
+    __syncthreads();
+    solve_trees(m, LD2, q);
+    __syncthreads();
+    adv = q;
+  }
+  for (int a = tid(); a < m.nu; a += BLK) {
+    const int adr = m.actuator_actadr[a];
+    for (int j = adr; adr >= 0 && j < adr + m.actuator_actnum[a]; j++) {
+      const long g = (long)wid * m.na + j;
+      d.act[g] = next_act(dt, m.actuator_dyntype[a], MR(actuator_dynprm)[10 * a], MR(actuator_actrange) + 2 * a, d.act[g], d.act_dot[g], 1.0f,
+                          m.actuator_actlimited[a] != 0);
+    }
+  }
+  for (int i = tid(); i < nv; i += BLK) qvel[i] += adv[i] * dt;
+  __syncthreads();
+  for (int j = tid(); j < m.njnt; j += BLK) {
+    const int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j], jt = m.jnt_type[j];
+    if (jt == JNT_FREE) {
+      for (int i = 0; i < 3; i++) qpos[qa + i] += dt * qvel[da + i];
+      float qn[4];
+      quat_integrate(qn, qpos + qa + 3, qvel + da + 3, dt);
+      for (int i = 0; i < 4; i++) qpos[qa + 3 + i] = qn[i];
+    } else if (jt == JNT_BALL) {
+      float qn[4];
+      quat_integrate(qn, qpos + qa, qvel + da, dt);
+      for (int i = 0; i < 4; i++) qpos[qa + i] = qn[i];
+    } else {
+      qpos[qa] += dt * qvel[da];
+    }
+  }
+  for (int i = tid(); i < nv; i += BLK) d.qacc_warmstart[(long)wid * nv + i] = qacc[i];
+  if (tid() == 0) d.time[wid] += dt;
+}
+
+}  // namespace sp
+
+// launcher used by the C entry points (mjw_step.hip) for models with m->is_sparse
+int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
+  const int nw = d->nworld;
+  if (nw <= 0) return 0;
+  if (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC))
+    hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC));
+  if (stages & ST_SOLVE) hipLaunchKernelGGL(sp::solve_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
+  if (stages & ST_EULER) hipLaunchKernelGGL(sp::euler_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
+  return (int)hipGetLastError();
+}
+
+}  // namespace mjw

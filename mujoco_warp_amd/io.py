@@ -86,9 +86,12 @@ def _model_attr(name):
   return (None, name)
 
 
-_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.BOX, types.GeomType.MESH}
+_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.BOX, types.GeomType.MESH,
+                    types.GeomType.CYLINDER}
 # narrowphase pairs built on the device (type-sorted): collision_primitive.py:1280-1300 subset
 _SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6), (6, 6)}
+# extra pairs of the sparse path (plane-cylinder, collision_primitive.py:964-1040)
+_SPARSE_PAIRS = {(0, 5)}
 # pairs routed through GJK/EPA (the CONVEX entries of collision_driver.py:42-76 built here)
 _CCD_PAIRS = {(6, 6)}
 # every CONVEX entry of the reference table (heightfields excluded), for the EPA iteration cap
@@ -110,19 +113,34 @@ def put_model(mjm, device=None) -> types.Model:
     raise NotImplementedError(f"{types.SolverType(mjm.opt.solver).name} is unsupported.")
   if getattr(mjm.opt, "noslip_iterations", 0) > 0:
     raise NotImplementedError("noslip solver not implemented.")
-  if is_sparse(mjm):
-    raise NotImplementedError("sparse Jacobian / nv > 32 models are not supported by this build yet.")
-  if getattr(mjm, "ntendon", 0) or getattr(mjm, "nflex", 0):
-    raise NotImplementedError("tendons / flex are not supported by this build yet.")
+  sparse = is_sparse(mjm) or getattr(mjm, "nflex", 0) > 0
+  if getattr(mjm, "ntendon", 0):
+    raise NotImplementedError("tendons are not supported by this build yet.")
+  if sparse:
+    # the workgroup-per-world sparse / flex pipeline (csrc/mjw_sparse.hip) covers this subset
+    if mjm.opt.solver != types.SolverType.CG:
+      raise NotImplementedError("sparse / flex models: only the CG solver is supported by this build yet.")
+    if mjm.opt.integrator != types.IntegratorType.EULER:
+      raise NotImplementedError("sparse / flex models: only the Euler integrator is supported by this build yet.")
+    if getattr(mjm, "nsensor", 0):
+      raise NotImplementedError("sparse / flex models: sensors are not supported by this build yet.")
+    if getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.JOINT, types.EqType.FLEX))):
+      raise NotImplementedError("sparse / flex models: only joint and flex equality constraints are supported by this build yet.")
+    if np.any(mjm.jnt_limited & (mjm.jnt_type == JointType.BALL)):
+      raise NotImplementedError("sparse / flex models: ball joint limits are not supported by this build yet.")
+    if getattr(mjm, "nflex", 0) and np.any(mjm.flex_dim != 2):
+      raise NotImplementedError("only dim-2 flexes are supported by this build yet.")
   for st in np.unique(getattr(mjm, "sensor_type", np.zeros(0, dtype=np.int32))):
     if int(st) not in types.SUPPORTED_SENSORS:
       raise NotImplementedError(f"sensor type {int(st)} is not supported by this build yet.")
-  if getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD, types.EqType.JOINT))):
+  if not sparse and getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD, types.EqType.JOINT))):
     raise NotImplementedError("only connect, weld and joint equality constraints are supported by this build yet.")
   pairs_chk, _ = nxn_geom_pairs(mjm)
   for g1, g2 in pairs_chk:
     t = tuple(sorted((int(mjm.geom_type[g1]), int(mjm.geom_type[g2]))))
-    if t not in _SUPPORTED_PAIRS:
+    if sparse and t in _CCD_PAIRS:
+      raise NotImplementedError("sparse / flex models: box-box (convex) collisions are not supported by this build yet.")
+    if t not in (_SUPPORTED_PAIRS | _SPARSE_PAIRS if sparse else _SUPPORTED_PAIRS):
       names = tuple(types.GeomType(x).name for x in t)
       raise NotImplementedError(f"collision between {names[0]} and {names[1]} is not supported by this build yet.")
   if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
@@ -167,8 +185,7 @@ def put_model(mjm, device=None) -> types.Model:
   stypes = np.asarray(getattr(mjm, "sensor_type", np.zeros(0, dtype=np.int32)))
   m.sensor_rne_postconstraint = int(np.isin(stypes, list(types.RNE_POSTCONSTRAINT_SENSORS)).any())  # io.py:542-551
   m.nsensor_acc = int((np.asarray(getattr(mjm, "sensor_needstage", np.zeros(0))) == types.Stage.ACC).sum())
-  m.nflex = 0
-  m.is_sparse = False
+  m.is_sparse = bool(sparse)
   njmax_pad_unused, m.nv_pad = _padded_sizes(nv, 0, False)
   m.nmaxcondim = int(np.concatenate(([0], mjm.geom_condim)).max())
   m.nmaxpyramid = int(max(1, 2 * (m.nmaxcondim - 1)))
@@ -213,7 +230,57 @@ def put_model(mjm, device=None) -> types.Model:
   m.neq_cw = int(np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD)).sum()) if mjm.neq else 0
   m.nJmom = int(sum({JointType.FREE: 6, JointType.BALL: 3}.get(int(mjm.jnt_type[mjm.actuator_trnid[a, 0]]), 1) for a in range(mjm.nu)))
 
+  # sparse path: kinematic trees as dof ranges (a tree starts at every dof without a parent dof),
+  # J row width = the longest union of two dof chains (+ the 6 dofs of a flex edge)
+  dof_parent = np.asarray(mjm.dof_parentid)
+  starts = np.nonzero(dof_parent < 0)[0] if nv else np.zeros(0, dtype=int)
+  tree_dofadr = np.concatenate([starts, [nv]]).astype(np.int32)
+  chain = np.zeros(nv, dtype=int)
+  for i in range(nv):
+    chain[i] = 1 + (chain[dof_parent[i]] if dof_parent[i] >= 0 else 0)
+  maxchain = int(chain.max()) if nv else 0
+  m.ntree = len(starts)
+  nflex = int(getattr(mjm, "nflex", 0))
+  m.njrow = max(2 * maxchain, 6 if nflex else 0, 2) if sparse else m.nv_pad
+  # flex collision candidates (collision_flex.py:381-529 tests every sphere / capsule / box / cylinder
+  # geom whose contype / conaffinity matches) and planes (:261-378)
+  cg_adr, cg = [0], []
+  for f in range(nflex):
+    for g in range(mjm.ngeom):
+      if int(mjm.geom_type[g]) in (2, 3, 5, 6) and ((mjm.geom_contype[g] & mjm.flex_conaffinity[f]) or (mjm.flex_contype[f] & mjm.geom_conaffinity[g])):
+        cg.append(g)
+    cg_adr.append(len(cg))
+  planes = np.nonzero(mjm.geom_type == 0)[0] if nflex else np.zeros(0, dtype=int)
+  # per-vertex contribution lists of the flex passive forces (element slots, then bending slots)
+  nfv = int(getattr(mjm, "nflexvert", 0))
+  inc = [[] for _ in range(nfv)]
+  for f in range(nflex):
+    vb = mjm.flex_vertadr[f]
+    for el in range(mjm.flex_elemnum[f]):
+      eg = mjm.flex_elemadr[f] + el
+      for k in range(3):
+        inc[vb + mjm.flex_elem[mjm.flex_elemdataadr[f] + 3 * el + k]].append(3 * eg + k)
+  nelem = int(getattr(mjm, "nflexelem", 0))
+  for f in range(nflex):
+    vb = mjm.flex_vertadr[f]
+    for e in range(mjm.flex_edgeadr[f], mjm.flex_edgeadr[f] + mjm.flex_edgenum[f]):
+      if mjm.flex_edgeflap[e, 1] < 0:
+        continue
+      vs = (mjm.flex_edge[e, 0], mjm.flex_edge[e, 1], mjm.flex_edgeflap[e, 0], mjm.flex_edgeflap[e, 1])
+      for k, v in enumerate(vs):
+        inc[vb + v].append(3 * nelem + 4 * e + k)
+  inc_adr = np.concatenate([[0], np.cumsum([len(x) for x in inc])]).astype(np.int32)
+  inc_flat = np.array([c for x in inc for c in x], dtype=np.int32)
+  m.nflex, m.nflexvert, m.nflexedge = nflex, nfv, int(getattr(mjm, "nflexedge", 0))
+  m.nflexelem, m.nflexelemdata = nelem, int(getattr(mjm, "nflexelemdata", 0))
+  m.nflexinc, m.nflexcg, m.nplane = len(inc_flat), len(cg), len(planes)
   derived_int = dict(
+    tree_dofadr=tree_dofadr,
+    flex_cgeomadr=np.array(cg_adr, dtype=np.int32),
+    flex_cgeom=np.array(cg, dtype=np.int32),
+    plane_geom=planes.astype(np.int32),
+    flexvert_incadr=inc_adr,
+    flexvert_inc=inc_flat,
     body_subtree_end=subtree_end,
     body_level=depth,
     level_body=order,
@@ -221,6 +288,9 @@ def put_model(mjm, device=None) -> types.Model:
     jnt_limited_slide_hinge_adr=jnt_limited_sh,
     jnt_limited_ball_adr=jnt_limited_ball,
   )
+  for k_, v_ in derived_int.items():
+    if k_ in ("tree_dofadr", "flex_cgeomadr", "flex_cgeom", "plane_geom", "flexvert_incadr", "flexvert_inc"):
+      setattr(m, k_, _i32(v_, dev))
   m.body_subtree_end = _i32(subtree_end, dev)
   m.body_level = _i32(depth, dev)
   m.level_body = _i32(order, dev)
@@ -302,6 +372,7 @@ def cmodel(m: types.Model) -> _lib.CModel:
 # Data field trailing shapes (types.py:1702-1896)
 def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
   nb, nv, nq, nu, na, nj, ng = m.nbody, m.nv, m.nq, m.nu, m.na, m.njnt, m.ngeom
+  sp = int(bool(m.is_sparse))
   np_ = m.nv_pad
   real = dict(
     time=(), qpos=(nq,), qvel=(nv,), act=(na,), ctrl=(nu,), qacc_warmstart=(nv,), qfrc_applied=(nv,),
@@ -309,25 +380,33 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     xpos=(nb, 3), xquat=(nb, 4), xmat=(nb, 3, 3), xipos=(nb, 3), ximat=(nb, 3, 3), xanchor=(nj, 3), xaxis=(nj, 3),
     geom_xpos=(ng, 3), geom_xmat=(ng, 3, 3), site_xpos=(m.nsite, 3), site_xmat=(m.nsite, 3, 3),
     cam_xpos=(m.ncam, 3), cam_xmat=(m.ncam, 3, 3), light_xpos=(m.nlight, 3), light_xdir=(m.nlight, 3),
-    subtree_com=(nb, 3), cdof=(nv, 6), cinert=(nb, 10), crb=(nb, 10), qM=(np_, np_), qLD=(nv, nv),
+    subtree_com=(nb, 3), cdof=(nv, 6), cinert=(nb, 10), crb=(nb, 10),
+    qM=(m.nM,) if sp else (np_, np_), qLD=(m.nM,) if sp else (nv, nv),
     actuator_length=(nu,), actuator_moment=(m.nJmom,), actuator_velocity=(nu,), actuator_force=(nu,),
     cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,),
     qfrc_passive=(nv,), qfrc_actuator=(nv,), qfrc_smooth=(nv,), qacc_smooth=(nv,), qfrc_constraint=(nv,),
     cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 17,),
-    efc_J=(njmax_pad, np_), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
+    efc_J=(njmax_pad, m.njrow), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
     efc_aref=(njmax,), efc_frictionloss=(njmax,), efc_force=(njmax,), efc_Ma=(nv,),
     # RK4 workspace (forward.py:462-472 temporaries; kept resident so a step allocates nothing)
     qpos_t0=(nq,), qvel_t0=(nv,), act_t0=(na,), qvel_rk=(nv,), qacc_rk=(nv,), act_dot_rk=(na,),
+    # flex (smooth.py:228-355) and the sparse path's workspace (size 0 on the dense path)
+    flexvert_xpos=(m.nflexvert, 3), flexedge_length=(m.nflexedge,), flexedge_velocity=(m.nflexedge,),
+    flexedge_J=(m.nflexedge, 6), flex_frc=(m.nflexelem * 9 + m.nflexedge * 12,),
+    sp_body=(nb * 6 * sp,), sp_vec=(nv * 10 * sp,), sp_row=(njmax * 2 * sp,), sp_LD=(m.nM * sp,),
   )
   ints = dict(
     ne=(), nf=(), nl=(), nefc=(), solver_niter=(), moment_rownnz=(nu,), moment_rowadr=(nu,), moment_colind=(m.nJmom,),
     efc_type=(njmax,), efc_id=(njmax,), efc_state=(njmax_pad,), eq_active=(m.neq,),
+    efc_J_colind=(njmax_pad * sp, m.njrow), efc_J_rownnz=(njmax * sp,), efc_JT_rowind=(njmax_pad * m.njrow * sp,),
+    efc_JT_adr=((nv + 1) * sp,), sp_cnt=((nv + 1) * sp,), ncon_world=(2,),
   )
   creal = dict(
     contact_dist=(), contact_pos=(3,), contact_frame=(3, 3), contact_includemargin=(), contact_friction=(5,),
     contact_solref=(2,), contact_solreffriction=(2,), contact_solimp=(5,),
   )
-  cint = dict(contact_dim=(), contact_geom=(2,), contact_efc_address=(m.nmaxpyramid,), contact_worldid=(), contact_type=(), contact_geomcollisionid=())
+  cint = dict(contact_dim=(), contact_geom=(2,), contact_efc_address=(m.nmaxpyramid,), contact_worldid=(), contact_type=(), contact_geomcollisionid=(),
+              contact_flex=(2,), contact_vert=(2,))
   return real, ints, creal, cint
 
 
@@ -386,9 +465,7 @@ def _alloc_data(m, nworld, nconmax, njmax, naconmax, device):
   d.contact.efc_address.fill_(-1)
   d.nacon = torch.zeros(1, dtype=torch.int32, device=device)
   d.ncollision = torch.zeros(1, dtype=torch.int32, device=device)
-  d.efc.J_rownnz = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
   d.efc.J_rowadr = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
-  d.efc.J_colind = torch.zeros((nworld, 0, 0), dtype=torch.int32, device=device)
   d.mocap_quat[..., 0] = 1.0
   d.xquat[..., 0] = 1.0
   return d

@@ -392,6 +392,7 @@ class _Compiler:
     self.autolimits = True
     self.inertiafromgeom = "auto"
     self.defaults = {}
+    self.flexcomps = []
     self.m = MjModel()
 
   # -- defaults ------------------------------------------------------------------------------
@@ -455,7 +456,79 @@ class _Compiler:
       elif tag == "frame":
         for sub in self._flatten_frame(child):
           self._parse_frame_child(sub, body, childclass)
+      elif tag == "flexcomp":
+        self._flexcomp(child, body, childclass)
+      elif tag == "flex":
+        raise NotImplementedError("<flex> elements (explicit flex meshes) are not supported; use <flexcomp type='grid'>")
     return body
+
+  def _flexcomp(self, el, parent, childclass):
+    """<flexcomp type="grid" dim="2">: one body per vertex, each a child of `parent` at the vertex
+    position with three slide joints (x, y, z) -- MuJoCo's flexcomp dof="full" -- and the vertex
+    mass mass/npoint.  Elements, edges and flaps are built after the body tree is indexed
+    (`_build_flex`).  Grid ordering: point (ix, iy, iz) has index (ix*cy + iy)*cz + iz and sits at
+    spacing * (i - (count-1)/2) (MuJoCo user_flexcomp.cc, restated: parity unpinned, no MuJoCo here)."""
+    a = el.attrib
+    ftype = a.get("type", "grid")
+    if ftype != "grid":
+      raise NotImplementedError(f"flexcomp type '{ftype}' is not supported (grid only)")
+    dim = int(a.get("dim", 2))
+    if dim != 2:
+      raise NotImplementedError("only dim=2 flexcomp grids are supported")
+    if a.get("dof", "full") != "full":
+      raise NotImplementedError("only flexcomp dof='full' is supported")
+    count = [int(x) for x in _floats(a.get("count", "10 10 1"), 3)]
+    if count[2] != 1:
+      raise NotImplementedError("dim=2 grid needs count[2] == 1")
+    spacing = np.array(_floats(a.get("spacing", "0.02 0.02 0.02"), 3))
+    pos = np.array(_floats(a.get("pos", "0 0 0"), 3))
+    q = _orientation(a, self.angle_scale, self.eulerseq)
+    R = quat_to_mat(np.array([1.0, 0, 0, 0]) if q is None else np.asarray(q, dtype=float))
+    name = a.get("name", f"flex{len(self.flexcomps)}")
+    npnt = count[0] * count[1] * count[2]
+    mass = float(a.get("mass", 1.0))
+    pts = []
+    for ix in range(count[0]):
+      for iy in range(count[1]):
+        for iz in range(count[2]):
+          loc = spacing * (np.array([ix, iy, iz]) - 0.5 * (np.array(count) - 1))
+          pts.append(R @ loc + pos)
+    elems = []
+    cy = count[1]
+    for ix in range(count[0] - 1):
+      for iy in range(count[1] - 1):
+        v00, v10, v11, v01 = ix * cy + iy, (ix + 1) * cy + iy, (ix + 1) * cy + iy + 1, ix * cy + iy + 1
+        elems += [(v00, v10, v11), (v00, v11, v01)]
+    bodies = []
+    for i, p in enumerate(pts):
+      b = _Body(f"{name}_{i}", parent, childclass)
+      b.pos = np.asarray(p, dtype=float)
+      b.inertial = {"pos": "0 0 0", "mass": repr(mass / npnt), "diaginertia": "0 0 0"}
+      for ax in ("1 0 0", "0 1 0", "0 0 1"):
+        b.joints.append({"type": "slide", "axis": ax, "name": f"{name}_{i}_{'xyz'[len(b.joints)]}"})
+      parent.children.append(b)
+      bodies.append(b)
+    edge = el.find("edge")
+    elast = el.find("elasticity")
+    contact = el.find("contact")
+    ea = edge.attrib if edge is not None else {}
+    la = elast.attrib if elast is not None else {}
+    ca = contact.attrib if contact is not None else {}
+    self.flexcomps.append(dict(
+      name=name, dim=dim, bodies=bodies, elems=np.array(elems, dtype=np.int32).reshape(-1, 3),
+      radius=float(a.get("radius", 0.005)),
+      edge_equality=ea.get("equality", "false") == "true",
+      edge_solref=_merge_vec([0.02, 1.0], _floats(ea.get("solref", "0.02 1"))),
+      edge_solimp=_merge_vec([0.9, 0.95, 0.001, 0.5, 2.0], _floats(ea.get("solimp", "0.9 0.95 0.001 0.5 2"))),
+      young=float(la.get("young", 0.0)), poisson=float(la.get("poisson", 0.0)),
+      thickness=float(la.get("thickness", -1.0)), damping=float(la.get("damping", 0.0)),
+      elastic2d={"none": 0, "bend": 1, "stretch": 2, "both": 3}[la.get("elastic2d", "none")],
+      contype=int(ca.get("contype", 1)), conaffinity=int(ca.get("conaffinity", 1)), condim=int(ca.get("condim", 3)),
+      friction=_merge_vec([1.0, 0.005, 0.0001], _floats(ca.get("friction", "1 0.005 0.0001"))),
+      solref=_merge_vec([0.02, 1.0], _floats(ca.get("solref", "0.02 1"))),
+      solimp=_merge_vec([0.9, 0.95, 0.001, 0.5, 2.0], _floats(ca.get("solimp", "0.9 0.95 0.001 0.5 2"))),
+      margin=float(ca.get("margin", 0.0)), gap=float(ca.get("gap", 0.0)),
+    ))
 
   def _parse_frame_child(self, child, body, childclass):
     """A child of a <frame> whose pose has already been composed with the frame's."""
@@ -831,16 +904,111 @@ class _Compiler:
     self._build_actuators(root)
     self._build_contact(root)
     self._build_keys(root)
+    self._build_flex()
     self._build_equality(root)
     self._build_sensors(root)
     m.ntendon = 0
-    m.nflex = 0
     m.nhfield = 0
     m.nmesh = 0
     m.body_subtreemass = self._subtreemass()
     set_const(m)
 
   # ---------------------------------------------------------------------------------------
+  def _build_flex(self):
+    """mjModel flex_* tables of the flexcomps (MuJoCo user_flex.cc semantics, restated).
+
+    Edges are numbered in first-encounter order over the elements, each triangle contributing its
+    edges (1,2), (2,0), (0,1) -- the local edge order of passive.py:_flex_elasticity (:606-613).
+    flex_edgeflap holds the vertex opposite the edge in its first and second triangle (-1 on the
+    boundary).  flex_bending holds the 16 coefficients of the discrete quadratic bending energy of
+    the edge's two triangles (cotangent weights, Wardetzky et al. 2007 / Bergou et al. 2006) scaled
+    by mu*thickness^3 / (8*(A0 + A1)) with mu = young / (2*(1+poisson)), and a zero 17th (flat rest
+    shape); flex_stiffness (membrane) is zero unless elastic2d includes stretch, which is not
+    supported.  These compiler constants are parity unpinned: MuJoCo's compiler is not available."""
+    m = self.m
+    bid = {id(b): i for i, b in enumerate(self.bodies)}
+    fl = self.flexcomps
+    m.nflex = len(fl)
+    vertadr, vertnum, edgeadr, edgenum, elemadr, elemnum, elemdataadr, elemedgeadr = [], [], [], [], [], [], [], []
+    vertbodyid, edges, flaps, elemdata, elemedge, bending, stiffness, length0, vertflexid = [], [], [], [], [], [], [], [], []
+    for f, fc in enumerate(fl):
+      if fc["elastic2d"] >= 2 and fc["young"] > 0:
+        raise NotImplementedError("flex membrane (stretch) elasticity is not supported by the MJCF compiler yet")
+      vb = [bid[id(b)] for b in fc["bodies"]]
+      x = np.array([b.pos for b in fc["bodies"]])  # vertex bodies are children of the world body
+      if any(m.body_parentid[b] != 0 for b in vb):
+        raise NotImplementedError("flexcomp vertex bodies must be children of the world body")
+      vertadr.append(len(vertbodyid))
+      vertnum.append(len(vb))
+      vertbodyid += vb
+      vertflexid += [f] * len(vb)
+      el = fc["elems"]
+      elemadr.append(len(elemedge) // 3)
+      elemnum.append(len(el))
+      elemdataadr.append(len(elemdata))
+      elemedgeadr.append(len(elemedge))
+      eid, fe, tri_of_edge = {}, [], []
+      for t, tri in enumerate(el):
+        for a_, b_ in ((1, 2), (2, 0), (0, 1)):
+          key = (min(tri[a_], tri[b_]), max(tri[a_], tri[b_]))
+          if key not in eid:
+            eid[key] = len(fe)
+            fe.append(key)
+            tri_of_edge.append([])
+          tri_of_edge[eid[key]].append((t, 3 - a_ - b_))
+          elemedge.append(eid[key])
+        elemdata += [int(v) for v in tri]
+      edgeadr.append(len(edges))
+      edgenum.append(len(fe))
+      mu = fc["young"] / (2.0 * (1.0 + fc["poisson"]))
+      for e, (v0, v1) in enumerate(fe):
+        edges.append((v0, v1))
+        fp = [int(el[t][k]) for t, k in tri_of_edge[e]][:2] + [-1]
+        flaps.append((fp[0], fp[1]))
+        length0.append(float(np.linalg.norm(x[v1] - x[v0])))
+        coef = np.zeros(17)
+        if fc["elastic2d"] in (1, 3) and fp[1] >= 0 and fc["thickness"] > 0 and mu > 0:
+          coef[:16] = _bending_coef(x[[v0, v1, fp[0], fp[1]]], mu, fc["thickness"])
+        bending.append(coef)
+      stiffness += [np.zeros(21)] * len(el)
+    m.flex_dim = np.array([fc["dim"] for fc in fl], dtype=np.int32)
+    m.flex_vertadr, m.flex_vertnum = np.array(vertadr, dtype=np.int32), np.array(vertnum, dtype=np.int32)
+    m.flex_edgeadr, m.flex_edgenum = np.array(edgeadr, dtype=np.int32), np.array(edgenum, dtype=np.int32)
+    m.flex_elemadr, m.flex_elemnum = np.array(elemadr, dtype=np.int32), np.array(elemnum, dtype=np.int32)
+    m.flex_elemdataadr = np.array(elemdataadr, dtype=np.int32)
+    m.flex_elemedgeadr = np.array(elemedgeadr, dtype=np.int32)
+    m.nflexvert, m.nflexedge, m.nflexelem, m.nflexelemdata = len(vertbodyid), len(edges), len(elemedge) // 3, len(elemdata)
+    m.flex_vertbodyid = np.array(vertbodyid, dtype=np.int32)
+    m.flex_vertflexid = np.array(vertflexid, dtype=np.int32)
+    m.flex_vert = np.zeros((m.nflexvert, 3))
+    m.flex_centered = np.ones(m.nflex, dtype=np.int32)
+    m.flex_edge = np.array(edges, dtype=np.int32).reshape(-1, 2)
+    m.flex_edgeflap = np.array(flaps, dtype=np.int32).reshape(-1, 2)
+    m.flex_elem = np.array(elemdata, dtype=np.int32)
+    m.flex_elemedge = np.array(elemedge, dtype=np.int32)
+    m.flexedge_length0 = np.array(length0)
+    m.flex_bending = np.array(bending).reshape(-1, 17)
+    m.flex_stiffness = np.array(stiffness).reshape(-1, 21)
+    m.flex_damping = np.array([fc["damping"] for fc in fl])
+    m.flex_radius = np.array([fc["radius"] for fc in fl])
+    m.flex_margin = np.array([fc["margin"] for fc in fl])
+    m.flex_gap = np.array([fc["gap"] for fc in fl])
+    m.flex_condim = np.array([fc["condim"] for fc in fl], dtype=np.int32)
+    m.flex_friction = np.array([fc["friction"] for fc in fl]).reshape(-1, 3)
+    m.flex_solref = np.array([fc["solref"] for fc in fl]).reshape(-1, 2)
+    m.flex_solimp = np.array([fc["solimp"] for fc in fl]).reshape(-1, 5)
+    m.flex_contype = np.array([fc["contype"] for fc in fl], dtype=np.int32)
+    m.flex_conaffinity = np.array([fc["conaffinity"] for fc in fl], dtype=np.int32)
+    # flexedge_invweight0 = J M^-1 J' at qpos0 for the vertex-own-dof edge Jacobian (smooth.py:261-355):
+    # each vertex body carries three orthogonal slide dofs and the vertex mass
+    iw = []
+    for f in range(m.nflex):
+      for e in range(m.flex_edgenum[f]):
+        vs = m.flex_edge[m.flex_edgeadr[f] + e] + m.flex_vertadr[f]
+        bs = [m.flex_vertbodyid[v] for v in vs]
+        iw.append(sum(1.0 / m.body_mass[b] for b in bs if m.body_dofnum[b]))
+    m.flexedge_invweight0 = np.array(iw)
+
   def _build_geoms(self):
     m = self.m
     rows = []
@@ -1213,6 +1381,12 @@ class _Compiler:
     name2body = {n: i for i, n in enumerate(m.body_names)}
     name2site = {n: i for i, n in enumerate(getattr(m, "site_names", []))}
     rows = []
+    # <flexcomp><edge equality="true"/>: one FLEX equality per flex, added when the flexcomp is
+    # parsed, i.e. ahead of the <equality> section (constraint.py:677-790 reads eq_obj1id = flex id)
+    for f, fc in enumerate(self.flexcomps):
+      if fc["edge_equality"]:
+        rows.append(dict(name="", type=int(EqType.FLEX), obj1=f, obj2=-1, objtype=int(ObjType.UNKNOWN), data=np.zeros(11),
+                         solref=fc["edge_solref"], solimp=fc["edge_solimp"], active=True))
     for eq in root.findall("equality"):
       for el in eq:
         a = dict(self.defaults[el.get("class", "main")].attrs.get("equality", {}))
@@ -1350,12 +1524,29 @@ class _Compiler:
     m.nkey = len(keys)
     m.key_names = [k.get("name", "") for k in keys]
     m.key_time = np.array([float(k.get("time", 0.0)) for k in keys])
-    m.key_qpos = np.array([_floats(k.get("qpos")) if k.get("qpos") else m.qpos0 for k in keys]).reshape(m.nkey, m.nq)
+    # a key shorter than nq (flexcomp dofs are appended after the keyed joints) is completed with qpos0
+    m.key_qpos = np.array([np.concatenate([_floats(k.get("qpos")), m.qpos0[len(_floats(k.get("qpos"))):]]) if k.get("qpos") else m.qpos0
+                           for k in keys]).reshape(m.nkey, m.nq)
     m.key_qvel = np.array([_floats(k.get("qvel")) if k.get("qvel") else np.zeros(m.nv) for k in keys]).reshape(m.nkey, m.nv)
     m.key_act = np.array([_floats(k.get("act")) if k.get("act") else np.zeros(m.na) for k in keys]).reshape(m.nkey, m.na)
     m.key_ctrl = np.array([_floats(k.get("ctrl")) if k.get("ctrl") else np.zeros(m.nu) for k in keys]).reshape(m.nkey, m.nu)
     m.key_mpos = np.zeros((m.nkey, 3 * m.nmocap))
     m.key_mquat = np.tile(np.tile([1.0, 0, 0, 0], m.nmocap), (m.nkey, 1))
+
+
+def _bending_coef(x, mu, thickness):
+  """16 coefficients of the quadratic bending energy of one interior edge: x = (edge v0, edge v1,
+  flap of triangle 0, flap of triangle 1).  Q = c c' * mu h^3 / (8 (A0 + A1)), c the cotangent
+  weights; Q annihilates translations and any flat configuration of the four vertices."""
+  e0, e1, e2, e3, e4 = x[1] - x[0], x[2] - x[0], x[3] - x[0], x[2] - x[1], x[3] - x[1]
+
+  def cot(a, b):
+    return float(np.dot(a, b) / max(np.linalg.norm(np.cross(a, b)), MJ_MINVAL))
+
+  c01, c02, c03, c04 = cot(e0, e1), cot(e0, e2), cot(-e0, e3), cot(-e0, e4)
+  a0, a1 = 0.5 * np.linalg.norm(np.cross(e0, e1)), 0.5 * np.linalg.norm(np.cross(e0, e2))
+  c = np.array([c03 + c04, c01 + c02, -(c01 + c03), -(c02 + c04)])
+  return (np.outer(c, c) * mu * thickness**3 / (8.0 * (a0 + a1))).reshape(-1)
 
 
 def _geom_inertia(gtype, size, mass):
@@ -1542,7 +1733,8 @@ def set_const(m: MjModel):
       J[:3, d] = lin + np.cross(ang, off)
       J[3:, d] = ang
       d = m.dof_parentid[d]
-    A = J @ Minv @ J.T
+    cols = np.nonzero(np.any(J != 0, axis=0))[0]
+    A = J[:, cols] @ Minv[np.ix_(cols, cols)] @ J[:, cols].T
     tr, rot = np.trace(A[:3, :3]) / 3.0, np.trace(A[3:, 3:]) / 3.0
     if tr < MJ_MINVAL and rot > MJ_MINVAL:
       tr = rot

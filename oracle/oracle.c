@@ -33,7 +33,7 @@ enum { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICITFAST = 3 };
 enum { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
 enum { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
 enum { DYN_NONE = 0, DYN_INTEGRATOR = 1, DYN_FILTER = 2, DYN_FILTEREXACT = 3, DYN_MUSCLE = 4, DYN_USER = 5 };
-enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
+enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2, EQ_FLEX = 4 };
 enum { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum { INTEGRATOR_EULER = 0, INTEGRATOR_RK4 = 1, INTEGRATOR_IMPLICIT = 2, INTEGRATOR_IMPLICITFAST = 3 };
 enum { BIAS_NONE = 0, BIAS_AFFINE = 1 };
@@ -272,6 +272,8 @@ static void world_view(const orc_model* m, const orc_data* b, int w, orc_data* o
   int nq = m->nq, nv = m->nv, nu = m->nu, na = m->na, nbody = m->nbody, njnt = m->njnt;
   int ngeom = m->ngeom, nsite = m->nsite, ncam = m->ncam, nlight = m->nlight, nmocap = m->nmocap, neq = m->neq;
   int njmax = b->njmax, nconmax = b->nconmax, nsensordata = m->nsensordata;
+  int nflexvert = m->nflexvert, nflexedge = m->nflexedge;
+  (void)nflexvert; (void)nflexedge;
   (void)nsensordata;
   (void)nq; (void)nv; (void)nu; (void)na; (void)nbody; (void)njnt; (void)ngeom; (void)nsite; (void)ncam;
   (void)nlight; (void)nmocap; (void)njmax; (void)nconmax; (void)neq;
@@ -529,6 +531,116 @@ static void camlight(const orc_model* m, orc_data* d) {
   }
 }
 
+static void matvec3(real* r, const real* M, const real* v);
+
+/* smooth.py:228-258 _flex_vertices, :261-355 _flex_edges (edge length, velocity and the Jacobian of
+ * the edge length w.r.t. the two vertex bodies' own dofs -- the reference's "TODO: use Jacobian"
+ * form; flexedge_J holds body 1's dofs then body 2's, 6 slots per edge) */
+static void flex_kinematics(const orc_model* m, orc_data* d) {
+  for (int v = 0; v < m->nflexvert; v++) {
+    int b = m->flex_vertbodyid[v], f = m->flex_vertflexid[v];
+    if (m->flex_centered[f]) {
+      for (int i = 0; i < 3; i++) d->flexvert_xpos[3 * v + i] = d->xpos[3 * b + i];
+    } else {
+      real t[3];
+      matvec3(t, d->xmat + 9 * b, m->flex_vert + 3 * v);
+      for (int i = 0; i < 3; i++) d->flexvert_xpos[3 * v + i] = t[i] + d->xpos[3 * b + i];
+    }
+  }
+  for (int f = 0; f < m->nflex; f++) {
+    for (int e = m->flex_edgeadr[f]; e < m->flex_edgeadr[f] + m->flex_edgenum[f]; e++) {
+      int v[2] = {m->flex_vertadr[f] + m->flex_edge[2 * e], m->flex_vertadr[f] + m->flex_edge[2 * e + 1]};
+      const real* p1 = d->flexvert_xpos + 3 * v[0];
+      const real* p2 = d->flexvert_xpos + 3 * v[1];
+      real vec[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]}, dir[3];
+      d->flexedge_length[e] = normalize_with_norm(dir, vec);
+      real vel = 0;
+      real* J = d->flexedge_J + 6 * e;
+      for (int k = 0; k < 6; k++) J[k] = 0;
+      int slot = 0;
+      for (int s2 = 0; s2 < 2; s2++) {
+        int b = m->flex_vertbodyid[v[s2]];
+        const real* p = s2 ? p2 : p1;
+        real off[3];
+        for (int i = 0; i < 3; i++) off[i] = p[i] - d->subtree_com[3 * m->body_rootid[b] + i];
+        for (int k = 0; k < m->body_dofnum[b]; k++) {
+          int dof = m->body_dofadr[b] + k;
+          const real* cd = d->cdof + 6 * dof;
+          real c[3], jacp[3];
+          cross3(c, cd, off);
+          for (int i = 0; i < 3; i++) jacp[i] = cd[3 + i] + c[i];
+          real jv = dot3(jacp, dir) * (s2 ? 1 : -1);
+          vel += jv * d->qvel[dof];
+          J[slot++] = jv;
+        }
+      }
+      d->flexedge_velocity[e] = vel;
+    }
+  }
+}
+
+/* passive.py:566-662 _flex_elasticity and :665-725 _flex_bending, accumulated into qfrc_spring */
+static void flex_passive(const orc_model* m, orc_data* d) {
+  static const int edges2[3][2] = {{1, 2}, {2, 0}, {0, 1}};
+  for (int f = 0; f < m->nflex; f++) {
+    if (m->flex_dim[f] != 2) continue;
+    real kD = (m->opt_timestep > 0 && !(m->opt_disableflags & DSBL_DAMPER)) ? m->flex_damping[f] / m->opt_timestep : 0;
+    for (int el = 0; el < m->flex_elemnum[f]; el++) {
+      int elemid = m->flex_elemadr[f] + el;
+      const int* ev = m->flex_elem + m->flex_elemdataadr[f] + 3 * el;
+      int vb = m->flex_vertadr[f];
+      real grad[3][6], elong[3], metric[3][3], force[3][3] = {{0}};
+      for (int e = 0; e < 3; e++) {
+        const real* x0 = d->flexvert_xpos + 3 * (vb + ev[edges2[e][0]]);
+        const real* x1 = d->flexvert_xpos + 3 * (vb + ev[edges2[e][1]]);
+        for (int i = 0; i < 3; i++) { grad[e][i] = x0[i] - x1[i]; grad[e][3 + i] = x1[i] - x0[i]; }
+        int idx = m->flex_edgeadr[f] + m->flex_elemedge[m->flex_elemedgeadr[f] + 3 * el + e];
+        real vel = d->flexedge_velocity[idx], def = d->flexedge_length[idx], ref = m->flexedge_length0[idx];
+        real prev = def - vel * m->opt_timestep;
+        elong[e] = def * def - ref * ref + (def * def - prev * prev) * kD;
+      }
+      int id = 0;
+      for (int a = 0; a < 3; a++)
+        for (int b = a; b < 3; b++) { metric[a][b] = metric[b][a] = m->flex_stiffness[21 * elemid + id]; id++; }
+      for (int e1 = 0; e1 < 3; e1++)
+        for (int e2 = 0; e2 < 3; e2++)
+          for (int i = 0; i < 2; i++)
+            for (int x = 0; x < 3; x++) force[edges2[e2][i]][x] -= elong[e1] * grad[e2][3 * i + x] * metric[e1][e2];
+      for (int k = 0; k < 3; k++) {
+        int b = m->flex_vertbodyid[vb + ev[k]];
+        if (m->body_dofnum[b] == 0) continue;
+        for (int x = 0; x < 3; x++) d->qfrc_spring[m->body_dofadr[b] + x] += force[k][x];
+      }
+    }
+    for (int e = m->flex_edgeadr[f]; e < m->flex_edgeadr[f] + m->flex_edgenum[f]; e++) {
+      if (m->flex_edgeflap[2 * e + 1] == -1) continue;
+      int vb = m->flex_vertadr[f];
+      int v[4] = {vb + m->flex_edge[2 * e], vb + m->flex_edge[2 * e + 1], vb + m->flex_edgeflap[2 * e], vb + m->flex_edgeflap[2 * e + 1]};
+      const real* B = m->flex_bending + 17 * e;
+      real frc[4][3] = {{0}};
+      if (B[16] != 0) {
+        const real *v0 = d->flexvert_xpos + 3 * v[0], *v1 = d->flexvert_xpos + 3 * v[1];
+        const real *v2 = d->flexvert_xpos + 3 * v[2], *v3 = d->flexvert_xpos + 3 * v[3];
+        real a1[3], a2[3], a3[3];
+        for (int i = 0; i < 3; i++) { a1[i] = v1[i] - v0[i]; a2[i] = v2[i] - v0[i]; a3[i] = v3[i] - v0[i]; }
+        cross3(frc[1], a2, a3);
+        cross3(frc[2], a3, a1);
+        cross3(frc[3], a1, a2);
+        for (int i = 0; i < 3; i++) frc[0][i] = -(frc[1][i] + frc[2][i] + frc[3][i]);
+      }
+      for (int i = 0; i < 4; i++) {
+        int b = m->flex_vertbodyid[v[i]];
+        for (int x = 0; x < 3; x++) {
+          real fx = 0;
+          for (int j = 0; j < 4; j++) fx -= B[4 * i + j] * d->flexvert_xpos[3 * v[j] + x];
+          fx -= B[16] * frc[i][x];
+          if (m->body_dofnum[b]) d->qfrc_spring[m->body_dofadr[b] + x] += fx;
+        }
+      }
+    }
+  }
+}
+
 /* smooth.py:806-912 (crb accumulate + dense qM) */
 static void crb(const orc_model* m, orc_data* d) {
   int nb = m->nbody, nv = m->nv;
@@ -590,6 +702,41 @@ static void cholesky_solve(int n, const real* L, const real* y, real* x) {
     x[i] = s / L[i * n + i];
   }
   if (z != tmp) free(z);
+}
+
+/* sparse path (is_sparse): M = L' D L over the kinematic tree (smooth.py:1003-1064 _factor_i_sparse,
+ * the level-scheduled form of MuJoCo's mj_factorM) on dense storage: only ancestor entries are touched,
+ * so the cost is O(nv * depth^2).  qLD holds D on the diagonal and L (unit, strictly lower) below it. */
+static void factor_tree(const orc_model* m, int n, const real* M, real* L) {
+  memcpy(L, M, (size_t)n * n * sizeof(real));
+  for (int k = n - 1; k >= 0; k--) {
+    for (int i = m->dof_parentid[k]; i >= 0; i = m->dof_parentid[i]) {
+      real tmp = L[(size_t)k * n + i] / L[(size_t)k * n + k];
+      for (int j = i; j >= 0; j = m->dof_parentid[j]) L[(size_t)i * n + j] -= tmp * L[(size_t)k * n + j];
+      L[(size_t)k * n + i] = tmp;
+    }
+  }
+}
+
+/* smooth.py:2813-2846 _solve_LD_sparse: x = (L' D L)^-1 y */
+static void solve_tree(const orc_model* m, int n, const real* L, const real* y, real* x) {
+  if (x != y) memcpy(x, y, (size_t)n * sizeof(real));
+  for (int k = n - 1; k >= 0; k--)
+    for (int i = m->dof_parentid[k]; i >= 0; i = m->dof_parentid[i]) x[i] -= L[(size_t)k * n + i] * x[k];
+  for (int k = 0; k < n; k++) x[k] /= L[(size_t)k * n + k];
+  for (int k = 0; k < n; k++)
+    for (int i = m->dof_parentid[k]; i >= 0; i = m->dof_parentid[i]) x[k] -= L[(size_t)k * n + i] * x[i];
+}
+
+/* factor_m / solve_m: the dense tile Cholesky or the sparse tree LDL, as the reference dispatches */
+static void factor_m(const orc_model* m, int n, const real* M, real* L) {
+  if (m->is_sparse) factor_tree(m, n, M, L);
+  else cholesky(n, M, L);
+}
+
+static void solve_m(const orc_model* m, int n, const real* L, const real* y, real* x) {
+  if (m->is_sparse) solve_tree(m, n, L, y, x);
+  else cholesky_solve(n, L, y, x);
 }
 
 /* smooth.py:2041-2147 (_transmission, joint transmissions; dense moment rows) */
@@ -740,6 +887,7 @@ static void passive(const orc_model* m, orc_data* d) {
       if (has_d) d->qfrc_damper[da] = -damp * d->qvel[da];
     }
   }
+  if (!dsbl_spring) flex_passive(m, d);
   for (int i = 0; i < nv; i++) d->qfrc_passive[i] = d->qfrc_spring[i] + d->qfrc_damper[i];
 }
 
@@ -1177,6 +1325,42 @@ static void capsule_box(contacts2* out, const real* cpos, const real* cax, real 
   }
 }
 
+static void flex_collision(const orc_model* m, orc_data* d);
+
+/* collision_primitive_core.py:519-613 plane_cylinder: candidate k of 4 (both cap rims nearest the plane,
+ * then two points of a triangle on the nearer cap) */
+static void plane_cylinder_k(int k, const real* n, const real* ppos, const real* cc, const real* cax, real r, real hh, real* dist,
+                             real* pos) {
+  real axis[3] = {cax[0], cax[1], cax[2]};
+  real prjaxis = dot3(n, axis);
+  if (prjaxis > 0) { for (int i = 0; i < 3; i++) axis[i] = -axis[i]; prjaxis = -prjaxis; }
+  real df[3] = {cc[0] - ppos[0], cc[1] - ppos[1], cc[2] - ppos[2]};
+  real dist0 = dot3(df, n);
+  real vec[3];
+  for (int i = 0; i < 3; i++) vec[i] = axis[i] * prjaxis - n[i];
+  real len2 = dot3(vec, vec);
+  if (len2 >= 1e-12) { real sc = safe_div(r, sqrt(len2)); for (int i = 0; i < 3; i++) vec[i] *= sc; }
+  else { vec[0] = r; vec[1] = 0; vec[2] = 0; }
+  real prjvec = dot3(vec, n);
+  for (int i = 0; i < 3; i++) axis[i] *= hh;
+  prjaxis *= hh;
+  if (k == 0) {
+    *dist = dist0 + prjaxis + prjvec;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + vec[i] + axis[i] - n[i] * (*dist * (real)0.5);
+  } else if (k == 1) {
+    *dist = dist0 - prjaxis + prjvec;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + vec[i] - axis[i] - n[i] * (*dist * (real)0.5);
+  } else {
+    real prjvec1 = -prjvec * (real)0.5;
+    *dist = dist0 + prjaxis + prjvec1;
+    real v1[3];
+    cross3(v1, vec, axis);
+    normalize3(v1);
+    real sc = r * sqrt((real)3) * (real)0.5, sg = k == 2 ? 1 : -1;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + sg * v1[i] * sc + axis[i] - vec[i] * (real)0.5 - n[i] * (*dist * (real)0.5);
+  }
+}
+
 static void collision(const orc_model* m, orc_data* d) {
   *d->ncon = 0;
   *d->ncollision = 0;
@@ -1245,12 +1429,15 @@ static void collision(const orc_model* m, orc_data* d) {
         d->con_dim[cid] = condim;
         d->con_geom[2 * cid] = g1;
         d->con_geom[2 * cid + 1] = g2;
+      d->con_flex[2 * cid] = d->con_flex[2 * cid + 1] = d->con_vert[2 * cid] = d->con_vert[2 * cid + 1] = -1;
         for (int i = 0; i < 10; i++) d->con_efc_address[10 * cid + i] = -1;
         (*d->ncon)++;
       }
       continue;
     } else if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {
       c.n = 8; /* all 8 corners are candidates (collision_primitive.py:737-790) */
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_CYLINDER) {
+      c.n = 4; /* collision_primitive.py:964-1040 */
     } else {
       continue; /* pair type not supported by the oracle (not on the benchmark path) */
     }
@@ -1259,7 +1446,11 @@ static void collision(const orc_model* m, orc_data* d) {
         plane_box_corner(k, n1, p1, p2, r2, s2, &c.dist[0], c.pos[0]);
         make_frame(c.frame[0], n1);
       }
-      int kk = (t1 == GEOM_PLANE && t2 == GEOM_BOX) ? 0 : k;
+      if (t1 == GEOM_PLANE && t2 == GEOM_CYLINDER) {
+        plane_cylinder_k(k, n1, p1, p2, n2, s2[0], s2[1], &c.dist[0], c.pos[0]);
+        make_frame(c.frame[0], n1);
+      }
+      int kk = (t1 == GEOM_PLANE && (t2 == GEOM_BOX || t2 == GEOM_CYLINDER)) ? 0 : k;
       real dist = c.dist[kk];
       int active = dist < margin;
       if ((pairid0 == -2 || !active) && pairid1 == -1) continue;
@@ -1277,8 +1468,272 @@ static void collision(const orc_model* m, orc_data* d) {
       d->con_dim[cid] = condim;
       d->con_geom[2 * cid] = g1;
       d->con_geom[2 * cid + 1] = g2;
+      d->con_flex[2 * cid] = d->con_flex[2 * cid + 1] = d->con_vert[2 * cid] = d->con_vert[2 * cid + 1] = -1;
       for (int i = 0; i < 10; i++) d->con_efc_address[10 * cid + i] = -1;
       (*d->ncon)++;
+    }
+  }
+  flex_collision(m, d);
+}
+
+/* ---- flex collision (collision_flex.py) ----------------------------------------------------- */
+
+/* collision_primitive_core.py:1495-1515 */
+static real tri_area_sign(const real* p1, const real* p2, const real* p3) {
+  real a = (p1[0] - p3[0]) * (p2[1] - p3[1]) - (p2[0] - p3[0]) * (p1[1] - p3[1]);
+  return (real)((a > 0) - (a < 0));
+}
+
+static void tri_point_segment(real* r, const real* p, const real* u, const real* v) {
+  real uv[2] = {v[0] - u[0], v[1] - u[1]}, up[2] = {p[0] - u[0], p[1] - u[1]};
+  real a = (uv[0] * up[0] + uv[1] * up[1]) / maxr(MINVAL, uv[0] * uv[0] + uv[1] * uv[1]);
+  if (a <= 0) { r[0] = u[0]; r[1] = u[1]; }
+  else if (a >= 1) { r[0] = v[0]; r[1] = v[1]; }
+  else { r[0] = u[0] + a * uv[0]; r[1] = u[1] + a * uv[1]; }
+}
+
+/* collision_primitive_core.py:1518-1597 sphere_triangle (mjraw_SphereTriangle) */
+static real sphere_triangle(real* pos, real* nrm, const real* sp, real sr, const real* t1, const real* t2, const real* t3,
+                            real tr) {
+  real S[3], A[3], B[3], N[3], P[3], V1[3], V2[3], X[3];
+  for (int i = 0; i < 3; i++) { S[i] = sp[i] - t1[i]; A[i] = t2[i] - t1[i]; B[i] = t3[i] - t1[i]; }
+  cross3(N, A, B);
+  normalize3(N);
+  real dstS = dot3(N, S);
+  for (int i = 0; i < 3; i++) P[i] = S[i] - dstS * N[i];
+  real lenA = sqrt(dot3(A, A));
+  for (int i = 0; i < 3; i++) V1[i] = A[i];
+  normalize3(V1);
+  cross3(V2, N, A);
+  normalize3(V2);
+  real o[2] = {0, 0}, a[2] = {lenA, 0}, b[2] = {dot3(V1, B), dot3(V2, B)}, p[2] = {dot3(V1, P), dot3(V2, P)};
+  real s1 = tri_area_sign(p, o, a), s2 = tri_area_sign(p, a, b), s3 = tri_area_sign(p, b, o);
+  if (s1 == s2 && s2 == s3) {
+    for (int i = 0; i < 3; i++) X[i] = P[i];
+  } else {
+    real x0[2], x1[2], x2[2];
+    tri_point_segment(x0, p, o, a);
+    tri_point_segment(x1, p, a, b);
+    tri_point_segment(x2, p, b, o);
+    real d0 = hypot(p[0] - x0[0], p[1] - x0[1]), d1 = hypot(p[0] - x1[0], p[1] - x1[1]), d2 = hypot(p[0] - x2[0], p[1] - x2[1]);
+    const real* xs = (d0 < d1 && d0 < d2) ? x0 : (d1 < d2 ? x1 : x2);
+    for (int i = 0; i < 3; i++) X[i] = xs[0] * V1[i] + xs[1] * V2[i];
+  }
+  for (int i = 0; i < 3; i++) nrm[i] = X[i] - S[i];
+  real dst = sqrt(dot3(nrm, nrm));
+  if (dst > MINVAL) for (int i = 0; i < 3; i++) nrm[i] /= dst;
+  else for (int i = 0; i < 3; i++) nrm[i] = N[i];
+  real dist = dst - sr - tr;
+  for (int i = 0; i < 3; i++) pos[i] = sp[i] + nrm[i] * (sr + (real)0.5 * dist);
+  return dist;
+}
+
+static void put2(contacts2* c, real dist, const real* pos, const real* nrm) {
+  c->dist[c->n] = dist;
+  memcpy(c->pos[c->n], pos, 3 * sizeof(real));
+  memcpy(c->frame[c->n], nrm, 3 * sizeof(real)); /* normal only; the frame is made by the writer */
+  c->n++;
+}
+
+/* collision_primitive_core.py:1600-1714 box_triangle */
+static void box_triangle(contacts2* c, const real* bp, const real* br, const real* bs, const real* const* t, real tr) {
+  for (int vi = 0; vi < 3; vi++) {
+    real diff[3], loc[3];
+    for (int i = 0; i < 3; i++) diff[i] = t[vi][i] - bp[i];
+    for (int i = 0; i < 3; i++) loc[i] = br[i] * diff[0] + br[3 + i] * diff[1] + br[6 + i] * diff[2];
+    int maxaxis = 0;
+    real maxval = fabs(loc[0]) - bs[0];
+    for (int j = 1; j < 3; j++) { real v = fabs(loc[j]) - bs[j]; if (v > maxval) { maxval = v; maxaxis = j; } }
+    int inside = 1;
+    for (int j = 0; j < 3; j++) if (fabs(loc[j]) > bs[j] + tr) inside = 0;
+    if (inside && c->n < 2) {
+      real nl[3] = {0, 0, 0}, ng[3], p[3];
+      nl[maxaxis] = (real)((loc[maxaxis] > 0) - (loc[maxaxis] < 0));
+      matvec3(ng, br, nl);
+      real dd = maxval - tr, off = tr + dd * (real)0.5;
+      for (int i = 0; i < 3; i++) p[i] = t[vi][i] - ng[i] * off;
+      put2(c, dd, p, ng);
+    }
+  }
+  for (int i = 0; i < 8 && c->n < 2; i++) {
+    real vec[3] = {(i & 1) ? bs[0] : -bs[0], (i & 2) ? bs[1] : -bs[1], (i & 4) ? bs[2] : -bs[2]}, corner[3], p[3], n[3];
+    matvec3(corner, br, vec);
+    for (int k = 0; k < 3; k++) corner[k] += bp[k];
+    real dd = sphere_triangle(p, n, corner, 0, t[0], t[1], t[2], tr);
+    if (dd < MAXVAL) put2(c, dd, p, n);
+  }
+}
+
+/* collision_primitive_core.py:1717-1819 capsule_triangle */
+static void capsule_triangle(contacts2* c, const real* cp, const real* ax, real cr, real hl, const real* const* t, real tr) {
+  real p1[3], p2[3], ab[3], p[3], n[3];
+  for (int i = 0; i < 3; i++) { p1[i] = cp[i] - ax[i] * hl; p2[i] = cp[i] + ax[i] * hl; ab[i] = p2[i] - p1[i]; }
+  real dd = sphere_triangle(p, n, p1, cr, t[0], t[1], t[2], tr);
+  if (dd < MAXVAL) put2(c, dd, p, n);
+  dd = sphere_triangle(p, n, p2, cr, t[0], t[1], t[2], tr);
+  if (dd < MAXVAL && c->n < 2) put2(c, dd, p, n);
+  real ab2 = 4 * hl * hl;
+  for (int vi = 0; vi < 3 && c->n < 2; vi++) {
+    real vec[3], cl[3], df[3];
+    for (int i = 0; i < 3; i++) vec[i] = t[vi][i] - p1[i];
+    real tp = dot3(vec, ab) / maxr(MINVAL, ab2);
+    if (tp > MINVAL && tp < 1 - MINVAL) {
+      for (int i = 0; i < 3; i++) { cl[i] = p1[i] + ab[i] * tp; df[i] = t[vi][i] - cl[i]; }
+      real draw = sqrt(dot3(df, df));
+      if (draw > MINVAL) {
+        for (int i = 0; i < 3; i++) { n[i] = df[i] / draw; p[i] = (cl[i] + t[vi][i] + n[i] * (cr - tr)) * (real)0.5; }
+        put2(c, draw - cr - tr, p, n);
+      }
+    }
+  }
+}
+
+/* collision_primitive_core.py:1822-1990 cylinder_triangle */
+static void cylinder_triangle(contacts2* c, const real* cp, const real* ax, real cr, real hh, const real* const* t, real tr) {
+  real p1[3], p2[3], ab[3];
+  for (int i = 0; i < 3; i++) { p1[i] = cp[i] - ax[i] * hh; p2[i] = cp[i] + ax[i] * hh; ab[i] = p2[i] - p1[i]; }
+  real ab2 = 4 * hh * hh;
+  for (int vi = 0; vi < 3 && c->n < 2; vi++) {
+    const real* vert = t[vi];
+    real vec[3], p[3], n[3], dd;
+    for (int i = 0; i < 3; i++) vec[i] = vert[i] - p1[i];
+    real tp = dot3(vec, ab) / maxr(MINVAL, ab2);
+    if (tp > MINVAL && tp < 1 - MINVAL) {
+      real cl[3], df[3];
+      for (int i = 0; i < 3; i++) { cl[i] = p1[i] + ab[i] * tp; df[i] = vert[i] - cl[i]; }
+      real draw = sqrt(dot3(df, df));
+      if (draw < cr + tr) {
+        if (draw > MINVAL) {
+          for (int i = 0; i < 3; i++) { n[i] = df[i] / draw; p[i] = (cl[i] + vert[i] + n[i] * (cr - tr)) * (real)0.5; }
+          dd = draw - cr - tr;
+        } else {
+          real L = sqrt(ab2), d2 = (1 - tp) * L, d1 = tp * L;
+          if (d2 < cr && d2 < d1) {
+            for (int i = 0; i < 3; i++) { n[i] = ax[i]; p[i] = vert[i]; }
+            dd = -d2 - tr;
+          } else if (d1 < cr) {
+            for (int i = 0; i < 3; i++) { n[i] = -ax[i]; p[i] = vert[i]; }
+            dd = -d1 - tr;
+          } else {
+            real e1[3], e2[3];
+            for (int i = 0; i < 3; i++) { e1[i] = t[1][i] - t[0][i]; e2[i] = t[2][i] - t[0][i]; }
+            cross3(n, e1, e2);
+            normalize3(n);
+            for (int i = 0; i < 3; i++) p[i] = cl[i];
+            dd = -cr - tr;
+          }
+        }
+        put2(c, dd, p, n);
+      }
+    } else {
+      const real* pe = tp <= MINVAL ? p1 : p2;
+      real sgn = tp <= MINVAL ? -1 : 1;
+      real df[3], perp[3];
+      for (int i = 0; i < 3; i++) df[i] = vert[i] - pe[i];
+      real sd = dot3(df, ax);
+      for (int i = 0; i < 3; i++) perp[i] = df[i] - ax[i] * sd;
+      real pl = sqrt(dot3(perp, perp));
+      if (pl < cr) {
+        dd = sgn * sd - tr;
+        for (int i = 0; i < 3; i++) { n[i] = sgn * ax[i]; p[i] = vert[i] - n[i] * (tr + dd * (real)0.5); }
+        put2(c, dd, p, n);
+      } else if (pl < cr + tr) {
+        real ep[3], de[3];
+        for (int i = 0; i < 3; i++) { ep[i] = pe[i] + perp[i] / pl * cr; de[i] = vert[i] - ep[i]; }
+        real draw = sqrt(dot3(de, de));
+        if (draw > MINVAL) {
+          dd = draw - tr;
+          for (int i = 0; i < 3; i++) { n[i] = de[i] / draw; p[i] = vert[i] - n[i] * (tr + dd * (real)0.5); }
+          put2(c, dd, p, n);
+        }
+      }
+    }
+  }
+}
+
+/* collision_flex.py:32-88 _write_flex_contact: geom[0] = geom, flex[1] / vert[1] = the flex vertex */
+static void write_flex_contact(const orc_model* m, orc_data* d, real dist, const real* pos, const real* nrm, real margin,
+                               int condim, const real* friction, const real* solref, const real* solimp, int g, int f, int vert) {
+  if (dist >= margin || dist >= MAXVAL) return;
+  int cid = *d->ncon;
+  if (cid >= d->nconmax) { (*d->ncon)++; return; }
+  d->con_dist[cid] = dist;
+  memcpy(d->con_pos + 3 * cid, pos, 3 * sizeof(real));
+  make_frame(d->con_frame + 9 * cid, nrm);
+  d->con_includemargin[cid] = margin;
+  memcpy(d->con_friction + 5 * cid, friction, 5 * sizeof(real));
+  memcpy(d->con_solref + 2 * cid, solref, 2 * sizeof(real));
+  d->con_solreffriction[2 * cid] = d->con_solreffriction[2 * cid + 1] = 0;
+  memcpy(d->con_solimp + 5 * cid, solimp, 5 * sizeof(real));
+  d->con_dim[cid] = condim;
+  d->con_geom[2 * cid] = g;
+  d->con_geom[2 * cid + 1] = -1;
+  d->con_flex[2 * cid] = -1;
+  d->con_flex[2 * cid + 1] = f;
+  d->con_vert[2 * cid] = -1;
+  d->con_vert[2 * cid + 1] = vert;
+  for (int i = 0; i < 10; i++) d->con_efc_address[10 * cid + i] = -1;
+  (*d->ncon)++;
+  (void)m;
+}
+
+/* collision_flex.py:381-529 (dim-2 elements vs sphere / capsule / box / cylinder, every geom tested
+ * -- the reference has no flex broadphase) and :261-378 (vertices vs planes) */
+static void flex_collision(const orc_model* m, orc_data* d) {
+  for (int f = 0; f < m->nflex; f++) {
+    if (m->flex_dim[f] != 2) continue;
+    real tr = m->flex_radius[f], tm = m->flex_margin[f];
+    for (int el = 0; el < m->flex_elemnum[f]; el++) {
+      const int* ev = m->flex_elem + m->flex_elemdataadr[f] + 3 * el;
+      const real* t[3];
+      for (int k = 0; k < 3; k++) t[k] = d->flexvert_xpos + 3 * (m->flex_vertadr[f] + ev[k]);
+      for (int g = 0; g < m->ngeom; g++) {
+        int gt = m->geom_type[g];
+        if (gt != GEOM_SPHERE && gt != GEOM_CAPSULE && gt != GEOM_BOX && gt != GEOM_CYLINDER) continue;
+        if (!((m->geom_contype[g] & m->flex_conaffinity[f]) || (m->flex_contype[f] & m->geom_conaffinity[g]))) continue;
+        real margin = m->geom_margin[g] + tm;
+        const real *gp = d->geom_xpos + 3 * g, *gr = d->geom_xmat + 9 * g, *gs = m->geom_size + 3 * g;
+        const real* gf = m->geom_friction + 3 * g;
+        real fr[5] = {maxr(MINMU, gf[0]), maxr(MINMU, gf[0]), maxr(MINMU, gf[1]), maxr(MINMU, gf[2]), maxr(MINMU, gf[2])};
+        real ax[3] = {gr[2], gr[5], gr[8]};
+        contacts2 c;
+        c.n = 0;
+        if (gt == GEOM_SPHERE) {
+          real p[3], n[3];
+          real dd = sphere_triangle(p, n, gp, gs[0], t[0], t[1], t[2], tr);
+          put2(&c, dd, p, n);
+        } else if (gt == GEOM_CAPSULE) {
+          capsule_triangle(&c, gp, ax, gs[0], gs[1], t, tr);
+        } else if (gt == GEOM_BOX) {
+          box_triangle(&c, gp, gr, gs, t, tr);
+        } else {
+          cylinder_triangle(&c, gp, ax, gs[0], gs[1], t, tr);
+        }
+        for (int k = 0; k < c.n; k++)
+          if (c.dist[k] < margin)
+            write_flex_contact(m, d, c.dist[k], c.pos[k], c.frame[k], margin, m->geom_condim[g], fr, m->geom_solref + 2 * g,
+                               m->geom_solimp + 5 * g, g, f, ev[0]);
+      }
+    }
+  }
+  for (int v = 0; v < m->nflexvert; v++) {
+    int f = m->flex_vertflexid[v];
+    const real* x = d->flexvert_xpos + 3 * v;
+    for (int g = 0; g < m->ngeom; g++) {
+      if (m->geom_type[g] != GEOM_PLANE) continue;
+      const real *pp = d->geom_xpos + 3 * g, *pr = d->geom_xmat + 9 * g;
+      real n[3] = {pr[2], pr[5], pr[8]}, df[3] = {x[0] - pp[0], x[1] - pp[1], x[2] - pp[2]};
+      real margin = m->geom_margin[g] + m->flex_margin[f];
+      real dist = dot3(df, n) - m->flex_radius[f];
+      if (!(dist < margin)) continue;
+      const real *gf = m->geom_friction + 3 * g, *ff = m->flex_friction + 3 * f;
+      real f0 = maxr(gf[0], ff[0]), f1 = maxr(gf[1], ff[1]), f2 = maxr(gf[2], ff[2]);
+      real fr[5] = {maxr(MINMU, f0), maxr(MINMU, f0), maxr(MINMU, f1), maxr(MINMU, f2), maxr(MINMU, f2)};
+      real p[3];
+      for (int i = 0; i < 3; i++) p[i] = x[i] - n[i] * (dist * (real)0.5 + m->flex_radius[f]);
+      int condim = m->geom_condim[g] > m->flex_condim[f] ? m->geom_condim[g] : m->flex_condim[f];
+      write_flex_contact(m, d, dist, p, n, margin, condim, fr, m->geom_solref + 2 * g, m->geom_solimp + 5 * g, g, f,
+                         v - m->flex_vertadr[f]);
     }
   }
 }
@@ -1458,6 +1913,35 @@ static void make_constraint(const orc_model* m, orc_data* d) {
       efc_row(m, d, efcid, pos, pos, invweight, m->eq_solref + 2 * e, m->eq_solimp + 5 * e, 0, Jqvel, 0, CNSTR_EQUALITY, e);
     }
   }
+  /* equality flex constraint.py:677-790: one row per edge of each flex with an active FLEX equality */
+  if (!(m->opt_disableflags & DSBL_EQUALITY)) {
+    for (int e = 0; e < m->neq; e++) {
+      if (m->eq_type[e] != EQ_FLEX || !d->eq_active[e]) continue;
+      int f = m->eq_obj1id[e];
+      for (int ed = m->flex_edgeadr[f]; ed < m->flex_edgeadr[f] + m->flex_edgenum[f]; ed++) {
+        (*d->ne)++;
+        int efcid = (*d->nefc)++;
+        if (efcid >= njmax) continue;
+        real* J = d->efc_J + (size_t)efcid * nv;
+        memset(J, 0, nv * sizeof(real));
+        int v[2] = {m->flex_vertadr[f] + m->flex_edge[2 * ed], m->flex_vertadr[f] + m->flex_edge[2 * ed + 1]};
+        int slot = 0;
+        real Jqvel = 0;
+        for (int s2 = 0; s2 < 2; s2++) {
+          int b = m->flex_vertbodyid[v[s2]];
+          for (int k = 0; k < m->body_dofnum[b]; k++) {
+            int dof = m->body_dofadr[b] + k;
+            J[dof] += d->flexedge_J[6 * ed + slot];
+            Jqvel += d->flexedge_J[6 * ed + slot] * d->qvel[dof];
+            slot++;
+          }
+        }
+        real pos = d->flexedge_length[ed] - m->flexedge_length0[ed];
+        efc_row(m, d, efcid, pos, pos, m->flexedge_invweight0[ed], m->eq_solref + 2 * e, m->eq_solimp + 5 * e, 0, Jqvel, 0,
+                CNSTR_EQUALITY, e);
+      }
+    }
+  }
   /* friction dof constraint.py:1113-1190 */
   if (!(m->opt_disableflags & DSBL_FRICTIONLOSS)) {
     for (int i = 0; i < nv; i++) {
@@ -1530,7 +2014,9 @@ static void make_constraint(const orc_model* m, orc_data* d) {
       real pos = d->con_dist[c] - includemargin;
       if (!(pos < 0)) continue;
       int g1 = d->con_geom[2 * c], g2 = d->con_geom[2 * c + 1];
-      int body1 = m->geom_bodyid[g1], body2 = m->geom_bodyid[g2];
+      /* constraint.py:1758-1771: a flex side resolves to its vertex body */
+      int body1 = g1 >= 0 ? m->geom_bodyid[g1] : m->flex_vertbodyid[m->flex_vertadr[d->con_flex[2 * c]] + d->con_vert[2 * c]];
+      int body2 = g2 >= 0 ? m->geom_bodyid[g2] : m->flex_vertbodyid[m->flex_vertadr[d->con_flex[2 * c + 1]] + d->con_vert[2 * c + 1]];
       real iw_base = m->body_invweight0[2 * body1] + m->body_invweight0[2 * body2];
       int w1 = m->body_weldid[body1], w2 = m->body_weldid[body2];
       const real* frame = d->con_frame + 9 * c;
@@ -1586,6 +2072,7 @@ static void fwd_position(const orc_model* m, orc_data* d) {
   kinematics(m, d);
   com_pos(m, d);
   camlight(m, d);
+  flex_kinematics(m, d);
   crb(m, d);
   collision(m, d);
   make_constraint(m, d);
@@ -1688,8 +2175,8 @@ static void fwd_acceleration(const orc_model* m, orc_data* d) {
   for (int i = 0; i < nv; i++)
     d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i] + d->qfrc_applied[i];
   xfrc_accumulate(m, d, d->qfrc_smooth);
-  cholesky(nv, d->qM, d->qLD);
-  cholesky_solve(nv, d->qLD, d->qfrc_smooth, d->qacc_smooth);
+  factor_m(m, nv, d->qM, d->qLD);
+  solve_m(m, nv, d->qLD, d->qfrc_smooth, d->qacc_smooth);
 }
 
 /* =============================================================================================
@@ -1755,7 +2242,7 @@ static void update_gradient(const orc_model* m, orc_data* d, solver_ctx* c) {
     c->grad_dot += g * g;
   }
   if (m->opt_solver == SOLVER_CG) {
-    cholesky_solve(nv, d->qLD, c->grad, c->Mgrad);
+    solve_m(m, nv, d->qLD, c->grad, c->Mgrad);
   } else {
     memcpy(c->H, d->qM, (size_t)nv * nv * sizeof(real));
     for (int r = 0; r < nefc; r++) {
@@ -1983,8 +2470,8 @@ static void euler(const orc_model* m, orc_data* d) {
   real* q = L + (size_t)nv * nv;
   memcpy(Mi, d->qM, (size_t)nv * nv * sizeof(real));
   for (int i = 0; i < nv; i++) Mi[i * nv + i] += dt * m->dof_damping[i];
-  cholesky(nv, Mi, L);
-  cholesky_solve(nv, L, d->efc_Ma, q);
+  factor_m(m, nv, Mi, L);
+  solve_m(m, nv, L, d->efc_Ma, q);
   euler_advance(m, d, q);
   free(tmp);
 }
@@ -2046,8 +2533,8 @@ static void implicit(const orc_model* m, orc_data* d) {
       A[j * nv + i] = A[i * nv + j];
     }
   }
-  cholesky(nv, A, L);
-  cholesky_solve(nv, L, d->efc_Ma, q);
+  factor_m(m, nv, A, L);
+  solve_m(m, nv, L, d->efc_Ma, q);
   euler_advance(m, d, q);
   free(A);
 }

@@ -28,7 +28,8 @@ typedef ORC_REAL real;
   X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
   X(nxn) X(nmaxpyramid) X(neq) X(nsensor) X(nsensordata) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)             \
-  X(opt_ccd_iterations) X(ccd_epa_iterations)
+  X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
+  X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
@@ -57,7 +58,10 @@ typedef ORC_REAL real;
   X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
   X(actuator_ctrlrange, nu * 2) X(actuator_forcerange, nu * 2) X(actuator_actrange, nu * 2)       \
   X(actuator_gear, nu * 6)                                                                         \
-  X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)
+  X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)                               \
+  X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
+  X(flex_vert, nflexvert * 3) X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)    \
+  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)
 
 /* ---- model: int arrays (name, element count) ---- */
 #define ORC_MODEL_INT_ARRAYS(X)                                                                    \
@@ -78,7 +82,14 @@ typedef ORC_REAL real;
   X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq) X(eq_objtype, neq)                           \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
-  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)
+  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)                     \
+  X(geom_contype, ngeom) X(geom_conaffinity, ngeom)                                                \
+  X(flex_dim, nflex) X(flex_vertadr, nflex) X(flex_vertnum, nflex) X(flex_edgeadr, nflex)          \
+  X(flex_edgenum, nflex) X(flex_elemadr, nflex) X(flex_elemnum, nflex) X(flex_elemdataadr, nflex)  \
+  X(flex_elemedgeadr, nflex) X(flex_contype, nflex) X(flex_conaffinity, nflex) X(flex_condim, nflex) \
+  X(flex_centered, nflex) X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert)              \
+  X(flex_edge, nflexedge * 2) X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata)          \
+  X(flex_elemedge, nflexelem * 3)
 
 /* ---- per-world data: real arrays (name, element count per world) ---- */
 #define ORC_DATA_REAL_ARRAYS(X)                                                                    \
@@ -100,13 +111,16 @@ typedef ORC_REAL real;
   X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax) X(efc_Ma, nv)                 \
   X(con_dist, nconmax) X(con_pos, nconmax * 3) X(con_frame, nconmax * 9)                          \
   X(con_includemargin, nconmax) X(con_friction, nconmax * 5) X(con_solref, nconmax * 2)           \
-  X(con_solreffriction, nconmax * 2) X(con_solimp, nconmax * 5) X(solver_cost, 1)
+  X(con_solreffriction, nconmax * 2) X(con_solimp, nconmax * 5) X(solver_cost, 1)                 \
+  X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
+  X(flexedge_J, nflexedge * 6)
 
 /* ---- per-world data: int arrays ---- */
 #define ORC_DATA_INT_ARRAYS(X)                                                                     \
   X(ne, 1) X(nf, 1) X(nl, 1) X(nefc, 1) X(ncon, 1) X(ncollision, 1) X(solver_niter, 1)            \
   X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax)                                          \
-  X(con_dim, nconmax) X(con_geom, nconmax * 2) X(con_efc_address, nconmax * 10) X(eq_active, neq)
+  X(con_dim, nconmax) X(con_geom, nconmax * 2) X(con_efc_address, nconmax * 10) X(eq_active, neq) \
+  X(con_flex, nconmax * 2) X(con_vert, nconmax * 2)
 
 typedef struct orc_model {
 #define ORC_DECL_I(name) int name;

@@ -127,6 +127,9 @@ class OracleModel:
       opt_ccd_tolerance=getattr(o, "ccd_tolerance", 1e-6),
       opt_timestep=o.timestep, opt_tolerance=max(o.tolerance, 1e-6), opt_ls_tolerance=o.ls_tolerance,
       opt_impratio_invsqrt=1.0 / np.sqrt(max(o.impratio, 1e-15)), stat_meaninertia=mjm.stat.meaninertia,
+      is_sparse=int(getattr(mjm.opt, "jacobian", 2) == 1 or (getattr(mjm.opt, "jacobian", 2) == 2 and mjm.nv > 32)),
+      nflex=getattr(mjm, "nflex", 0), nflexvert=getattr(mjm, "nflexvert", 0), nflexedge=getattr(mjm, "nflexedge", 0),
+      nflexelem=getattr(mjm, "nflexelem", 0), nflexelemdata=getattr(mjm, "nflexelemdata", 0),
     )
     if overrides:
       vals.update(overrides)

@@ -116,7 +116,11 @@ def test_unsupported_features_raise():
   import mujoco_warp_amd as mjw
   from mujoco_warp_amd import mjcf
 
-  cyl = mjcf.load_model_from_string('<mujoco><worldbody><body><freejoint/><geom type="cylinder" size=".1 .1"/></body></worldbody></mujoco>')
+  ell = mjcf.load_model_from_string('<mujoco><worldbody><body><freejoint/><geom type="ellipsoid" size=".1 .1 .2"/></body></worldbody></mujoco>')
+  with pytest.raises(NotImplementedError):
+    mjw.put_model(ell, device="cpu")
+  # cylinders collide only on the sparse path (plane-cylinder); a dense model with a cylinder pair raises
+  cyl = mjcf.load_model_from_string('<mujoco><worldbody><geom type="plane" size="1 1 .1"/><body><freejoint/><geom type="cylinder" size=".1 .1"/></body></worldbody></mujoco>')
   with pytest.raises(NotImplementedError):
     mjw.put_model(cyl, device="cpu")
 
