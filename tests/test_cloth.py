@@ -142,7 +142,9 @@ def test_gpu_cloth_position_stage_parity(mjm):
     g_idx, o_idx = np.array([p[0] for p in pairs]), np.array([p[1] for p in pairs])
     np.testing.assert_array_equal(d.efc.type[w].cpu().numpy()[g_idx], od.efc_type[w][o_idx])
     assert_close(f"J[w{w}]", Jg[g_idx], Jo[o_idx], rtol=1e-4, atol=2e-5)
-    for f, rt, at in (("pos", 1e-4, 2e-6), ("D", 1e-4, 1e-6), ("vel", 1e-4, 1e-6), ("aref", 2e-3, 2e-4)):
+    # aref = -k imp pos - b vel: the mannequin rests on the floor at dist ~0, and solref .003 gives
+    # k ~ 1e4 / s^2, so fp32 distance rounding (~1e-7) alone moves aref by ~1e-3
+    for f, rt, at in (("pos", 1e-4, 2e-6), ("D", 1e-4, 1e-6), ("vel", 1e-4, 1e-6), ("aref", 2e-3, 2e-3)):
       assert_close(f"efc_{f}[w{w}]", np_(getattr(d.efc, f)[w])[g_idx], getattr(od, "efc_" + f)[w][o_idx], rtol=rt, atol=at)
 
 
