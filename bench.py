@@ -49,28 +49,41 @@ MODELS = {
   "franka": dict(path="models/franka_emika_panda/scene.xml", nworld=16384, nconmax=1, njmax=5, solver=None, key=None),
   # C4: apollo (Euler, model-default Newton, IMU sensors, box-box CCD), keyframe "stand"
   "apollo": dict(path="models/apptronik_apollo/scene_flat.xml", nworld=4096, nconmax=16, njmax=64, solver=None, key=0),
+  # C5 stand-in: the reference's `cloth` benchmark (benchmarks/cloth/scene.xml, config.txt:19: nconmax 200,
+  # njmax 3000, 100 steps) -- the same 30x30 flex towel as aloha_cloth over a mannequin instead of the
+  # mesh arms; sparse path (mjw_sparse.hip), CG, starts from qpos0 (towel falls onto the mannequin)
+  "cloth": dict(path="models/cloth/scene.xml", nworld=1024, nconmax=200, njmax=3000, solver=None, key=None, steps=100,
+                cpu_worlds=16, cpu_steps=8),
+  # C5: aloha_cloth (benchmarks/aloha_cloth/scene.xml: two mesh arms + the 30x30 towel lying on the
+  # table), keyframe "neutral_pose", 100 steps (config.txt:13).  The towel's 1682 triangles touch the
+  # table box twice each (3364 contacts, ~16k rows), so config.txt's nconmax 920 / njmax 6300 would
+  # truncate both; this run sizes them so that nothing is dropped
+  "aloha_cloth": dict(path="models/aloha_cloth/scene.xml", nworld=1024, nconmax=4096, njmax=16384, solver=None, key=0, steps=100,
+                      cpu_worlds=16, cpu_steps=2),
 }
 
 
-def step_words(mjm, nv_pad):
+def step_words(mjm, nv_pad, sparse=False):
   """Algorithmic words per env-step of SURVEY.md 8(d), from the model sizes: (state inputs, fixed
   Data-contract outputs of the forward kernels, fixed outputs of the dense kernel).  For the
-  humanoid: 233 + 3012 + 925 = 4170 words."""
+  humanoid: 233 + 3012 + 925 = 4170 words.  Sparse models store qM / qLD as nM ancestor entries
+  and add the flex outputs (vertex positions, edge length / velocity / Jacobian)."""
   nq, nv, nu, nb, nj, ng = mjm.nq, mjm.nv, mjm.nu, mjm.nbody, mjm.njnt, mjm.ngeom
   nJmom = nu  # joint transmissions: one moment entry per actuator
   w_in = nq + nv + nu + nv + nv + 6 * nb + 1  # qpos qvel ctrl qacc_warmstart qfrc_applied xfrc_applied time
   kin = nb * (3 + 4 + 9 + 3 + 9) + nj * 6 + ng * 12 + mjm.nsite * 12
   camlight = mjm.ncam * 12 + mjm.nlight * 6
   com = 3 * nb + 10 * nb + 6 * nv
-  crb = 10 * nb + nv_pad * nv_pad
+  crb = 10 * nb + (int(mjm.nM) if sparse else nv_pad * nv_pad)
   trn = nu + nJmom + 3 * nu
   vel = 6 * nb + 6 * nv + nu
   passive = 3 * nv
   rne = nv + 12 * nb
   act = nu + 2 * nv
   sensors = getattr(mjm, "nsensordata", 0)
-  fwd_out = kin + camlight + com + crb + trn + vel + passive + rne + act + sensors + 2
-  dense_out = nv * nv + nv + (3 * nv + 5) + (nq + 2 * nv + 1)  # qLD, qacc_smooth, solver, integrator
+  flex = 3 * getattr(mjm, "nflexvert", 0) + 8 * getattr(mjm, "nflexedge", 0)
+  fwd_out = kin + camlight + com + crb + trn + vel + passive + rne + act + sensors + flex + 2
+  dense_out = (int(mjm.nM) if sparse else nv * nv) + nv + (3 * nv + 5) + (nq + 2 * nv + 1)  # qLD, qacc_smooth, solver, integrator
   return w_in, fwd_out, dense_out
 
 
@@ -86,7 +99,7 @@ def b_alg_parts(words, nefc_mean, ncon_mean, nv_pad):
 def parse():
   p = argparse.ArgumentParser()
   p.add_argument("--gpus", type=int, default=1)
-  p.add_argument("--steps", type=int, default=1000)
+  p.add_argument("--steps", type=int, default=None, help="timed steps (default: the config's, 1000 unless stated)")
   p.add_argument("--warmup", type=int, default=20)
   p.add_argument("--model", default="humanoid", choices=sorted(MODELS), help="benchmark config (default: the headline C2)")
   p.add_argument("--nworld", type=int, default=None, help="worlds per GPU (default: the config's)")
@@ -94,8 +107,8 @@ def parse():
   p.add_argument("--nconmax", type=int, default=None)
   p.add_argument("--njmax", type=int, default=None)
   p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
-  p.add_argument("--cpu-worlds", type=int, default=1024)
-  p.add_argument("--cpu-steps", type=int, default=1000)
+  p.add_argument("--cpu-worlds", type=int, default=None, help="CPU baseline sample worlds (default: the config's, 1024)")
+  p.add_argument("--cpu-steps", type=int, default=None, help="CPU baseline sample steps (default: the config's, 1000)")
   p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_humanoid_r01.json"))
   p.add_argument("--graph", type=int, default=0, help="replay steps through a captured hipGraph")
   a = p.parse_args()
@@ -103,6 +116,9 @@ def parse():
   for k in ("nworld", "nconmax", "njmax", "solver"):
     if getattr(a, k) is None:
       setattr(a, k, cfg[k])
+  for k, dflt in (("steps", 1000), ("cpu_worlds", 1024), ("cpu_steps", 1000)):
+    if getattr(a, k) is None:
+      setattr(a, k, cfg.get(k, dflt))
   return a
 
 
@@ -213,8 +229,9 @@ def main():
   total_steps = args.nworld * world * args.steps
   value = total_steps / elapsed
   if rank == 0:
-    words = step_words(mjm, m.nv_pad)
-    fwd_b, dense_b = b_alg_parts(words, nefc_mean, ncon_mean, m.nv_pad)
+    words = step_words(mjm, m.nv_pad, bool(m.is_sparse))
+    # a sparse efc row carries njrow values + njrow column indices instead of an nv_pad dense row
+    fwd_b, dense_b = b_alg_parts(words, nefc_mean, ncon_mean, 2 * m.njrow if m.is_sparse else m.nv_pad)
     bytes_per_launch = fwd_b * args.nworld
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
@@ -256,12 +273,14 @@ def main():
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic,
-        "kernel": "mjw::mjw_kernel<79> (forward: position/velocity/actuation/qfrc_smooth)"
-        + (" + mjw::ccd_kernel (convex pre-pass)" if m.nxn_ccd else ""),
+        "kernel": ("mjw::sp::forward_kernel + mjw::sp::solve_kernel (sparse path: forward + CG)" if m.is_sparse else
+                   "mjw::mjw_kernel<79> (forward: position/velocity/actuation/qfrc_smooth)"
+                   + (" + mjw::ccd_kernel (convex pre-pass)" if m.nxn_ccd else "")),
         "kernel_ms": kernel_ms,
         "alg_bytes_per_env_step": fwd_b,
         "other_kernels": {
-          "mjw::dense_kernel (factor/solve/Euler)" + (" + mjw::sensor_acc_kernel" if m.nsensor else ""): {
+          ("mjw::sp::euler_kernel" if m.is_sparse else
+           "mjw::dense_kernel (factor/solve/Euler)" + (" + mjw::sensor_acc_kernel" if m.nsensor else "")): {
             "ms": dense_ms,
             "alg_bytes_per_env_step": dense_b,
             "achieved_GBs": dense_b * args.nworld / (dense_ms * 1e-3) / 1e9,

@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 8
+#define MJW_ABI_VERSION 9
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -41,7 +41,8 @@
   X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations) X(opt_ls_iterations)             \
   X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)                                  \
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
-  X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane)
+  X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
+  X(nmesh) X(nmeshvert)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -71,7 +72,8 @@
   X(sensor_cutoff, nsensor)                                                                        \
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)                                \
-  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)
+  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)                              \
+  X(mesh_vert, nmeshvert * 3)
 
 /* ---- model: int arrays (never batched) ---- */
 #define MJW_MODEL_INT_ARRAYS(X)                                                                    \
@@ -101,7 +103,8 @@
   X(flex_condim, nflex) X(flex_cgeomadr, nflex + 1) X(flex_cgeom, nflexcg) X(plane_geom, nplane)   \
   X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert) X(flex_edge, nflexedge * 2)          \
   X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata) X(flex_elemedge, nflexelem * 3)      \
-  X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)
+  X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)                                     \
+  X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)
 
 /* ---- data: float arrays, (nworld, count) world-major like mujoco_warp types.Data ----
  * Sparse models (is_sparse, the reference's io.py:67-74 switch) store qM / qLD as (nworld, nM) rows of

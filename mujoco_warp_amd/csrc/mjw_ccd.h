@@ -21,8 +21,8 @@ constexpr float CCD_INTERSECT_TOL = 0.0000003f;
 constexpr unsigned CCD_FACE_DELETED = 0x80000000u;
 constexpr unsigned CCD_FACE_INVALID = 0x40000000u;
 
-// one geom in the workspace: pos[3] rot[9] size[3] margin type
-constexpr int CGEOM_WORDS = 17;
+// one geom in the workspace: pos[3] rot[9] size[3] margin type mesh_vertadr mesh_vertnum
+constexpr int CGEOM_WORDS = 19;
 // per-pair result record in HBM (d.ccd_out): count, dist, normal[3], points[4][3]
 constexpr int CCD_OUT = 17;
 
@@ -54,6 +54,8 @@ __host__ __device__ inline CcdLay ccd_layout(int it) {
 struct CGeom {
   float pos[3], rot[9], size[3], margin;
   int type;
+  const float* mv;  // mesh vertices (geom frame), GEOM_MESH only
+  int nvert;
 };
 
 __device__ __forceinline__ float ccd_sign(float x) { return x < 0.0f ? -1.0f : 1.0f; }  // wp.sign
@@ -86,6 +88,28 @@ __device__ __forceinline__ void ccd_support(const CGeom& g, const float* dir, fl
     float dd = sqrtf(ld[0] * ld[0] + ld[1] * ld[1]);
     if (dd > CCD_MINVAL) { res[0] = ld[0] * g.size[0] / dd; res[1] = ld[1] * g.size[0] / dd; }
     res[2] = ccd_sign(ld[2]) * g.size[1];
+  } else if (g.type == GEOM_MESH) {
+    // collision_gjk.py:136-151 exhaustive search over the vertices, spread over the wave: each lane
+    // keeps its strided subset's first maximum, a butterfly then keeps the largest (lowest index on
+    // ties), i.e. the sequential loop's first strict maximum.  Every lane calls this in lockstep.
+    float best = -CCD_FLOAT_MAX;
+    int bi = 0x7fffffff;
+    for (int i = (int)(threadIdx.x & 63); i < g.nvert; i += 64) {
+      const float* v = g.mv + 3 * i;
+      const float dd = v[0] * ld[0] + v[1] * ld[1] + v[2] * ld[2];
+      if (dd > best) { best = dd; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (bi < g.nvert) {
+      const float* v = g.mv + 3 * bi;
+      res[0] = v[0]; res[1] = v[1]; res[2] = v[2];
+      *vidx = bi;
+    }
   }
   rot_apply(pt, g.rot, res[0], res[1], res[2]);
   for (int i = 0; i < 3; i++) pt[i] += g.pos[i];
@@ -893,37 +917,43 @@ __device__ __forceinline__ int multicontact_box(const CcdWS& w, int fidx, const 
 // collision_gjk.py:2200-2345 ccd + collision_convex.py:763-852: contacts of one convex pair.
 // Returns the contact count (0: not penetrating); *dist is corrected by +margin, `normal` is
 // unnormalized (frame = make_frame(normal)), points in pts (stride 3, up to 4).
-__device__ __forceinline__ void put_cgeom(float* dst, const float* pos, const float* rot, const float* size, int type) {
+__device__ __forceinline__ void put_cgeom(float* dst, const float* pos, const float* rot, const float* size, int type, int vertadr = 0,
+                                          int nvert = 0) {
   for (int i = 0; i < 3; i++) { dst[i] = pos[i]; dst[12 + i] = size[i]; }
   for (int i = 0; i < 9; i++) dst[3 + i] = rot[i];
   dst[15] = 0.0f;
   dst[16] = __int_as_float(type);
+  dst[17] = __int_as_float(vertadr);
+  dst[18] = __int_as_float(nvert);
 }
 
-__device__ __forceinline__ CGeom get_cgeom(const float* src) {
+__device__ __forceinline__ CGeom get_cgeom(const float* src, const float* mesh_vert) {
   CGeom g;
   for (int i = 0; i < 3; i++) { g.pos[i] = src[i]; g.size[i] = src[12 + i]; }
   for (int i = 0; i < 9; i++) g.rot[i] = src[3 + i];
   g.margin = src[15];
   g.type = __float_as_int(src[16]);
+  g.mv = mesh_vert ? mesh_vert + 3 * (long)__float_as_int(src[17]) : nullptr;
+  g.nvert = mesh_vert ? __float_as_int(src[18]) : 0;
   return g;
 }
 
 // The pair's geoms are read from the workspace (put_cgeom at L.geoms); the outputs are written to
 // L.out: [0] dist, [1..3] normal, [4..15] points.  Only scalars and the LDS base cross the call, so
 // the (non-inlined) CCD code does not touch the caller's register budget.
-__device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, int gjk_it, float margin) {
+__device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, int gjk_it, float margin, const float* mesh_vert = nullptr) {
   CcdWS w;
   w.W = W;
   w.L = ccd_layout(epa_it);
-  CGeom g1 = get_cgeom(W + w.L.geoms), g2 = get_cgeom(W + w.L.geoms + CGEOM_WORDS);
+  CGeom g1 = get_cgeom(W + w.L.geoms, mesh_vert), g2 = get_cgeom(W + w.L.geoms + CGEOM_WORDS, mesh_vert);
   float* dist_out = W + w.L.out;
   float* normal = W + w.L.out + 1;
   float* pts = W + w.L.out + 4;
   g1.margin = margin;
   g2.margin = margin;
   float cutoff = 0.0f;
-  const int discrete = (g1.type == GEOM_BOX) && (g2.type == GEOM_BOX) && margin == 0.0f;
+  // collision_gjk.py:91-94 _discrete_geoms: boxes and meshes (polytopes)
+  const int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH) && (g2.type == GEOM_BOX || g2.type == GEOM_MESH) && margin == 0.0f;
   float full1 = 0.0f, full2 = 0.0f, size1 = 0.0f, size2 = 0.0f;
   if (g1.type == GEOM_SPHERE || g1.type == GEOM_CAPSULE) { size1 = g1.size[0]; full1 = size1 + 0.5f * g1.margin; g1.margin = 0.0f; g1.size[0] = 0.0f; }
   if (g2.type == GEOM_SPHERE || g2.type == GEOM_CAPSULE) { size2 = g2.size[0]; full2 = size2 + 0.5f * g2.margin; g2.margin = 0.0f; g2.size[0] = 0.0f; }

@@ -21,6 +21,7 @@
 // algorithms on the CPU for the parity tests.
 
 #include "mjw_common.h"
+#include "mjw_ccd.h"
 #include "mjw_narrow.h"
 
 namespace mjw {
@@ -738,6 +739,72 @@ __device__ void plane_cylinder_k(int k, const float* n, const float* pp, const f
   }
 }
 
+// collision_primitive.py:52-139, 257-277 plane_convex, exhaustive-search branch (the reference takes it
+// for meshes without a hull graph; with one it hill-climbs the hull, which reaches the same deepest
+// vertex a): the deepest vertex a, then among vertices within 1e-3 of its depth the one farthest from
+// a (b), farthest from line ab (c) and from the triangle's other edges (d); each distinct vertex is a
+// contact at its own depth.  One thread, serial over the vertices (rare: plane-near meshes only).
+__device__ int plane_mesh(const float* nw, const float* ppos, const float* gpos, const float* R, const float* mv, int nvert, float* dist,
+                          float (*pos)[3]) {
+  constexpr float HUGE_ = 1e6f;
+  const float d0[3] = {ppos[0] - gpos[0], ppos[1] - gpos[1], ppos[2] - gpos[2]};
+  float pl[3], n[3];
+  for (int i = 0; i < 3; i++) {
+    pl[i] = R[i] * d0[0] + R[3 + i] * d0[1] + R[6 + i] * d0[2];
+    n[i] = R[i] * nw[0] + R[3 + i] * nw[1] + R[6 + i] * nw[2];
+  }
+  auto sup = [&](const float* v) { return (pl[0] - v[0]) * n[0] + (pl[1] - v[1]) * n[1] + (pl[2] - v[2]) * n[2]; };
+  int idx[4] = {-1, -1, -1, -1};
+  float maxs = -HUGE_, a[3] = {0, 0, 0}, b[3] = {0, 0, 0}, c[3] = {0, 0, 0};
+  for (int i = 0; i < nvert; i++) {
+    const float s = sup(mv + 3 * i);
+    if (s > maxs) { maxs = s; idx[0] = i; a[0] = mv[3 * i]; a[1] = mv[3 * i + 1]; a[2] = mv[3 * i + 2]; }
+  }
+  if (maxs < 0.0f) return 0;
+  const float thr = maxs - 1e-3f;
+  float best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const float* v = mv + 3 * i;
+    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
+    const float dv[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]};
+    const float dd = dot3(dv, dv) + mask;
+    if (dd > best) { idx[1] = i; best = dd; b[0] = v[0]; b[1] = v[1]; b[2] = v[2]; }
+  }
+  float ab[3], t[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+  cross3(ab, n, t);
+  best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const float* v = mv + 3 * i;
+    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
+    const float ap[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]};
+    const float dd = fabsf(dot3(ap, ab)) + mask;
+    if (dd > best) { idx[2] = i; best = dd; c[0] = v[0]; c[1] = v[1]; c[2] = v[2]; }
+  }
+  float ac[3], bc[3], t1[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]}, t2[3] = {b[0] - c[0], b[1] - c[1], b[2] - c[2]};
+  cross3(ac, n, t1);
+  cross3(bc, n, t2);
+  best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const float* v = mv + 3 * i;
+    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
+    const float ap[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]}, bp[3] = {b[0] - v[0], b[1] - v[1], b[2] - v[2]};
+    const float dd = (fabsf(dot3(ap, ac)) + mask) + (fabsf(dot3(bp, bc)) + mask);
+    if (dd > best) { idx[3] = i; best = dd; }
+  }
+  int cnt = 0;
+  for (int i = 3; i >= 0; i--) {
+    int count = 0;
+    for (int j = 0; j <= i; j++) count += idx[j] == idx[i];
+    if (count != 1) continue;
+    const float* v = mv + 3 * idx[i];
+    const float dd = -sup(v);
+    for (int k = 0; k < 3; k++) pos[cnt][k] = gpos[k] + R[3 * k] * v[0] + R[3 * k + 1] * v[1] + R[3 * k + 2] * v[2] - 0.5f * dd * nw[k];
+    dist[cnt] = dd;
+    cnt++;
+  }
+  return cnt;
+}
+
 // collision_driver.py:274-321 on global frames
 __device__ bool broadphase(const mjw_model_t& m, int wid, const float* gx, const float* gm, int g1, int g2) {
   const float* geom_aabb = MR(geom_aabb);
@@ -779,9 +846,9 @@ struct ConOut {
 
 // `frame` (9, optional) keeps the narrowphase's own tangents (plane_capsule / capsule_capsule align
 // them with the capsule axis, collision_primitive.py); otherwise make_frame(nrm) (math.py:246-257)
-__device__ void write_contact(const mjw_model_t& m, const mjw_data_t& d, int wid, int slot, const ConOut& o, float dist, const float* pos,
-                              const float* nrm, const float* frame = nullptr) {
-  if (slot < 0 || slot >= d.naconmax) return;
+__device__ void write_contact(const mjw_model_t& m, const mjw_data_t& d, int wid, int slot, int lim, const ConOut& o, float dist,
+                              const float* pos, const float* nrm, const float* frame = nullptr) {
+  if (slot < 0 || slot >= lim || slot >= d.naconmax) return;
   d.contact_dist[slot] = dist;
   for (int i = 0; i < 3; i++) d.contact_pos[3 * (long)slot + i] = pos[i];
   float fr[9];
@@ -811,7 +878,7 @@ __device__ void write_contact(const mjw_model_t& m, const mjw_data_t& d, int wid
 
 // one collision item: a geom pair, a (flex element, collidable geom) pair or a (flex vertex, plane)
 // pair.  Returns the number of contacts; writes them from pool slot `base` when base >= 0.
-__device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed) {
+__device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed, int lim = 0x7fffffff) {
   const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
   const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;
   const float* geom_size = MR(geom_size);
@@ -832,6 +899,28 @@ __device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, 
     const float *p1 = gx + 3 * g1, *p2 = gx + 3 * g2, *r1 = gm + 9 * g1, *r2 = gm + 9 * g2;
     const float *s1 = geom_size + 3 * g1, *s2 = geom_size + 3 * g2;
     const float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
+    const int ccdslot = m.nxn_ccdid[item];
+    if (ccdslot >= 0) {
+      // convex pair: results of the CCD pre-pass (ccd_kernel below), n contacts at one distance with
+      // frame make_frame(normal) (collision_convex.py:763-852)
+      const float* out = d.ccd_out + ((long)wid * m.nxn_ccd + ccdslot) * CCD_OUT;
+      const int n = (int)out[0];
+      const float dist = out[1];
+      if (!(dist < o.margin) || m.nxn_pairid[2 * item] < -1) return 0;
+      for (int k = 0; k < n && base >= 0; k++) write_contact(m, d, wid, base + k, lim, o, dist, out + 5 + 3 * k, out + 2);
+      return n;
+    }
+    if (t1 == GEOM_PLANE && t2 == GEOM_MESH) {
+      float pd[4], pp[4][3];
+      const int mid = m.geom_dataid[g2];
+      const int n = plane_mesh(n1, p1, p2, r2, MR(mesh_vert) + 3 * (long)m.mesh_vertadr[mid], m.mesh_vertnum[mid], pd, pp);
+      for (int k = 0; k < n; k++) {
+        if (!(pd[k] < o.margin) || m.nxn_pairid[2 * item] < -1) continue;
+        if (base >= 0) write_contact(m, d, wid, base + cnt, lim, o, pd[k], pp[k], n1);
+        cnt++;
+      }
+      return cnt;
+    }
     const int ncand = (t1 == GEOM_PLANE && t2 == GEOM_BOX) ? 8 : ((t1 == GEOM_PLANE && t2 == GEOM_CYLINDER) ? 4 : 2);
     Con2 c;
     c.n = 0;
@@ -877,7 +966,7 @@ __device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, 
         for (int i = 0; i < 3; i++) { pos[i] = c.pos[k][i]; nrm[i] = c.frame[k][i]; }
       }
       if (!(dist < o.margin) || m.nxn_pairid[2 * item] < -1) continue;
-      if (base >= 0) write_contact(m, d, wid, base + cnt, o, dist, pos, nrm, ncand == 2 ? c.frame[k] : nullptr);
+      if (base >= 0) write_contact(m, d, wid, base + cnt, lim, o, dist, pos, nrm, ncand == 2 ? c.frame[k] : nullptr);
       cnt++;
     }
     return cnt;
@@ -926,7 +1015,7 @@ __device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, 
     o.vert = ev[0];
     for (int k = 0; k < n; k++) {
       if (!(c[k].dist < margin) || c[k].dist >= MJW_MAXVAL) continue;
-      if (base >= 0) write_contact(m, d, wid, base + cnt, o, c[k].dist, c[k].pos, c[k].nrm);
+      if (base >= 0) write_contact(m, d, wid, base + cnt, lim, o, c[k].dist, c[k].pos, c[k].nrm);
       cnt++;
     }
     return cnt;
@@ -959,7 +1048,7 @@ __device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, 
     o.vert = v - m.flex_vertadr[f];
     float pos[3];
     for (int i = 0; i < 3; i++) pos[i] = x[i] - n[i] * (dist * 0.5f + fr);
-    write_contact(m, d, wid, base, o, dist, pos, n);
+    write_contact(m, d, wid, base, lim, o, dist, pos, n);
   }
   return 1;
 }
@@ -984,22 +1073,27 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
   for (int it = tid(); it < nitem; it += BLK) cnt += collide_item(m, d, wid, it, -1, &passed);
   float v[2] = {(float)cnt, (float)passed};
   block_sum<2>(v, sm);
+  // every world keeps at most its share naconmax / nworld of the pool, in item order: the kept set
+  // is then the oracle's per-world nconmax cut and independent of the other worlds (and of sharding);
+  // the reference's global atomic pool drops an arbitrary overflow instead
   const int total = (int)v[0];
+  const int keep = min(total, d.naconmax / max(d.nworld, 1));
   if (tid() == 0) {
-    sm.ival[0] = total ? atomicAdd(d.nacon, total) : 0;
+    sm.ival[0] = keep ? atomicAdd(d.nacon, keep) : 0;
     if (v[1] > 0.0f) atomicAdd(d.ncollision, (int)v[1]);
     ncw[0] = sm.ival[0];
-    ncw[1] = total;
+    ncw[1] = keep;
   }
   __syncthreads();
-  int run = sm.ival[0];
-  if (total) {
-    for (int c0 = 0; c0 < nitem; c0 += BLK) {
+  const int start = sm.ival[0], lim = start + keep;
+  int run = start;
+  if (keep) {
+    for (int c0 = 0; c0 < nitem && run < lim; c0 += BLK) {
       const int it = c0 + tid();
       const int n = it < nitem ? collide_item(m, d, wid, it, -1, nullptr) : 0;
       int chunk;
       const int off = block_scan(n, chunk, sm);
-      if (n) collide_item(m, d, wid, it, run + off, nullptr);
+      if (n && run + off < lim) collide_item(m, d, wid, it, run + off, nullptr, lim);
       run += chunk;
     }
   }
@@ -1666,15 +1760,20 @@ __device__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, int 
   __syncthreads();
 }
 
+// the position stage in two halves around the convex pre-pass (models with CCD pairs)
+enum : int { SP_POS_A = 1 << 8, SP_POS_B = 1 << 9 };
+
 __global__ void __launch_bounds__(BLK) forward_kernel(const mjw_model_t m, const mjw_data_t d, int stages) {
   __shared__ Smem sm;
   const int wid = blockIdx.x;
-  if (stages & ST_POS) {
+  if (stages & (ST_POS | SP_POS_A)) {
     kinematics(m, d, wid);
     com_pos(m, d, wid);
     camlight(m, d, wid);
     flex_edges(m, d, wid);
     crb_qM(m, d, wid);
+  }
+  if (stages & (ST_POS | SP_POS_B)) {
     collision(m, d, wid, sm);
     make_constraint(m, d, wid, sm);
     transmission(m, d, wid, sm);
@@ -1682,6 +1781,47 @@ __global__ void __launch_bounds__(BLK) forward_kernel(const mjw_model_t m, const
   if (stages & ST_VEL) fwd_velocity(m, d, wid);
   if (stages & ST_ACT) fwd_actuation(m, d, wid);
   if (stages & ST_ACC) fwd_acceleration(m, d, wid);
+}
+
+// convex pre-pass (collision_convex.py:701-890): one wave per world applies the broadphase to the
+// convex pairs 64 at a time, then runs GJK / EPA (mjw_ccd.h) on each survivor with the whole wave in
+// lockstep over an LDS workspace; mesh supports are wave-parallel vertex scans.  Results go to
+// d.ccd_out, which collide_item reads for the same (broadphase-passing) pairs.
+__global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wid = blockIdx.x, lane = (int)threadIdx.x;
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations);
+  float* W = smem;
+  int* list = reinterpret_cast<int*>(smem + CL.total);
+  const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
+  const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;
+  const float* gsize = MR(geom_size);
+  const float* gmargin = MR(geom_margin);
+  const float* mesh_vert = MR(mesh_vert);
+  for (int p0 = 0; p0 < m.nxn; p0 += 64) {
+    const int p = p0 + lane;
+    bool pass = false;
+    if (p < m.nxn && m.nxn_ccdid[p] >= 0)
+      pass = m.nxn_pairid[2 * p + 1] >= 0 || broadphase(m, wid, gx, gm, m.nxn_geom_pair[2 * p], m.nxn_geom_pair[2 * p + 1]);
+    const unsigned long long bal = __ballot(pass);
+    if (pass) list[__popcll(bal & ((1ull << lane) - 1ull))] = p;
+    __syncthreads();
+    const int nsurv = __popcll(bal);
+    for (int k = 0; k < nsurv; k++) {
+      const int q = list[k];
+      const int g1 = m.nxn_geom_pair[2 * q], g2 = m.nxn_geom_pair[2 * q + 1];
+      const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+      const int md1 = t1 == GEOM_MESH ? m.geom_dataid[g1] : -1, md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
+      put_cgeom(W + CL.geoms, gx + 3 * g1, gm + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0, md1 >= 0 ? m.mesh_vertnum[md1] : 0);
+      put_cgeom(W + CL.geoms + CGEOM_WORDS, gx + 3 * g2, gm + 9 * g2, gsize + 3 * g2, t2, md2 >= 0 ? m.mesh_vertadr[md2] : 0,
+                md2 >= 0 ? m.mesh_vertnum[md2] : 0);
+      __syncthreads();
+      const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, gmargin[g1] + gmargin[g2], mesh_vert);
+      float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[q]) * CCD_OUT;
+      if (lane < CCD_OUT) out[lane] = lane == 0 ? (float)nc : (nc > 0 ? W[CL.out + lane - 1] : 0.0f);
+      __syncthreads();
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2081,8 +2221,16 @@ __global__ void __launch_bounds__(BLK) euler_kernel(const mjw_model_t m, const m
 int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
   const int nw = d->nworld;
   if (nw <= 0) return 0;
-  if (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC))
-    hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC));
+  int fwd = stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC);
+  const bool ccd = (stages & ST_POS) && m->nxn_ccd > 0 && d->naconmax > 0 && !(m->opt_disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT));
+  if (ccd) {
+    // frames first, then the convex pre-pass, then collision onward
+    hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, (int)sp::SP_POS_A);
+    const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations).total + 64) * 4;
+    hipLaunchKernelGGL(sp::ccd_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
+    fwd = (fwd & ~ST_POS) | sp::SP_POS_B;
+  }
+  if (fwd) hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
   if (stages & ST_SOLVE) hipLaunchKernelGGL(sp::solve_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
   if (stages & ST_EULER) hipLaunchKernelGGL(sp::euler_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
   return (int)hipGetLastError();

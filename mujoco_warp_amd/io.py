@@ -90,10 +90,13 @@ _SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.
                     types.GeomType.CYLINDER}
 # narrowphase pairs built on the device (type-sorted): collision_primitive.py:1280-1300 subset
 _SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6), (6, 6)}
-# extra pairs of the sparse path (plane-cylinder, collision_primitive.py:964-1040)
-_SPARSE_PAIRS = {(0, 5)}
+# extra pairs of the sparse path (plane-cylinder, collision_primitive.py:964-1040; plane-mesh
+# plane_convex, :52-300)
+_SPARSE_PAIRS = {(0, 5), (0, 7)}
 # pairs routed through GJK/EPA (the CONVEX entries of collision_driver.py:42-76 built here)
 _CCD_PAIRS = {(6, 6)}
+# ... and on the sparse path, which also runs the mesh pairs (sphere / capsule / box / mesh vs mesh)
+_SPARSE_CCD_PAIRS = {(6, 6), (2, 7), (3, 7), (6, 7), (7, 7)}
 # every CONVEX entry of the reference table (heightfields excluded), for the EPA iteration cap
 _CONVEX_TABLE = {(2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
 
@@ -138,9 +141,7 @@ def put_model(mjm, device=None) -> types.Model:
   pairs_chk, _ = nxn_geom_pairs(mjm)
   for g1, g2 in pairs_chk:
     t = tuple(sorted((int(mjm.geom_type[g1]), int(mjm.geom_type[g2]))))
-    if sparse and t in _CCD_PAIRS:
-      raise NotImplementedError("sparse / flex models: box-box (convex) collisions are not supported by this build yet.")
-    if t not in (_SUPPORTED_PAIRS | _SPARSE_PAIRS if sparse else _SUPPORTED_PAIRS):
+    if t not in (_SUPPORTED_PAIRS | _SPARSE_PAIRS | _SPARSE_CCD_PAIRS if sparse else _SUPPORTED_PAIRS):
       names = tuple(types.GeomType(x).name for x in t)
       raise NotImplementedError(f"collision between {names[0]} and {names[1]} is not supported by this build yet.")
   if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
@@ -218,9 +219,11 @@ def put_model(mjm, device=None) -> types.Model:
   m.nxn_geom_pair_typed = _i32(typed, dev)
   m.nxn = len(pairs)
   kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in pairs]
-  m.nxn_ccd = int(sum(k in _CCD_PAIRS for k in kinds))
-  ccdid = np.cumsum([k in _CCD_PAIRS for k in kinds]) - 1
-  m.nxn_ccdid = _i32(np.where([k in _CCD_PAIRS for k in kinds], ccdid, -1) if kinds else np.zeros(0), dev)
+  ccd_set = _SPARSE_CCD_PAIRS if sparse else _CCD_PAIRS
+  m.nxn_ccd = int(sum(k in ccd_set for k in kinds))
+  ccdid = np.cumsum([k in ccd_set for k in kinds]) - 1
+  m.nxn_ccdid = _i32(np.where([k in ccd_set for k in kinds], ccdid, -1) if kinds else np.zeros(0), dev)
+  m.nmesh, m.nmeshvert = int(getattr(mjm, "nmesh", 0)), int(getattr(mjm, "nmeshvert", 0))
   nconvex = sum(k in _CONVEX_TABLE for k in kinds)
   nboxbox = sum(k == (6, 6) for k in kinds)
   # collision_convex.py:1127: EPA iteration cap

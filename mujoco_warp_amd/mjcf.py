@@ -391,6 +391,9 @@ class _Compiler:
     self.eulerseq = "xyz"
     self.autolimits = True
     self.inertiafromgeom = "auto"
+    self.meshdir = ""
+    self.boundmass = 0.0
+    self.boundinertia = 0.0
     self.defaults = {}
     self.flexcomps = []
     self.m = MjModel()
@@ -610,6 +613,9 @@ class _Compiler:
       self.eulerseq = comp.get("eulerseq", "xyz")
       self.autolimits = comp.get("autolimits", "true") == "true"
       self.inertiafromgeom = comp.get("inertiafromgeom", "auto")
+      self.meshdir = comp.get("meshdir", "")
+      self.boundmass = float(comp.get("boundmass", 0.0))
+      self.boundinertia = float(comp.get("boundinertia", 0.0))
 
     for opt in root.findall("option"):
       self._parse_option(opt)
@@ -898,6 +904,7 @@ class _Compiler:
     m.mapM2M = np.array(mapM2M, dtype=np.int32)
     m.nC = nM
 
+    self._load_meshes(root)
     self._build_geoms()
     self._build_inertia()
     self._build_sites_cams_lights()
@@ -909,11 +916,42 @@ class _Compiler:
     self._build_sensors(root)
     m.ntendon = 0
     m.nhfield = 0
-    m.nmesh = 0
     m.body_subtreemass = self._subtreemass()
     set_const(m)
 
   # ---------------------------------------------------------------------------------------
+  def _load_meshes(self, root):
+    """<asset><mesh>: vertices of STL / OBJ files, scaled, repeated vertices removed in
+    first-occurrence order (MuJoCo user_mesh.cc).  The vertices stay in the file's frame: MuJoCo also
+    moves them to the mesh's inertial frame and folds that offset into geom_pos / geom_quat, which
+    leaves the world-space geometry -- and so every contact -- unchanged; only the reported
+    geom_xpos / geom_xmat of mesh geoms differ (parity unpinned: no MuJoCo here)."""
+    m = self.m
+    self.mesh_id = {}
+    self.mesh_data = []  # (vertices (n, 3) float64, triangles (t, 3) int)
+    for asset in root.findall("asset"):
+      for me in asset.findall("mesh"):
+        a = self._resolve("mesh", me, None)
+        if "file" not in a:
+          raise NotImplementedError("<mesh> without a file (inline vertex / user meshes) is not supported")
+        path = os.path.join(self.basedir, self.meshdir, a["file"])
+        v, f = _read_mesh_file(path)
+        v = v * np.array(_merge_vec([1.0, 1.0, 1.0], _floats(a.get("scale", "1 1 1"))))
+        _, first, inv = np.unique(v, axis=0, return_index=True, return_inverse=True)
+        order = np.argsort(first)  # unique rows in first-occurrence order
+        remap = np.empty(len(order), dtype=np.int64)
+        remap[order] = np.arange(len(order))
+        v = v[first[order]]
+        f = remap[inv.reshape(-1)[f]]
+        name = a.get("name") or os.path.splitext(os.path.basename(a["file"]))[0]
+        self.mesh_id[name] = len(self.mesh_data)
+        self.mesh_data.append((v, f))
+    m.nmesh = len(self.mesh_data)
+    m.mesh_vertnum = np.array([len(v) for v, _ in self.mesh_data], dtype=np.int32)
+    m.mesh_vertadr = np.concatenate([[0], np.cumsum(m.mesh_vertnum)[:-1]]).astype(np.int32) if m.nmesh else np.zeros(0, np.int32)
+    m.mesh_vert = np.concatenate([v for v, _ in self.mesh_data]) if m.nmesh else np.zeros((0, 3))
+    m.nmeshvert = int(m.mesh_vertnum.sum())
+
   def _build_flex(self):
     """mjModel flex_* tables of the flexcomps (MuJoCo user_flex.cc semantics, restated).
 
@@ -1036,7 +1074,8 @@ class _Compiler:
     m.geom_gap = np.array([r["gap"] for r in rows])
     m.geom_rbound = np.array([r["rbound"] for r in rows])
     m.geom_aabb = np.array([r["aabb"] for r in rows]).reshape(ng, 6)
-    m.geom_dataid = -np.ones(ng, dtype=np.int32)
+    m.geom_dataid = np.array([r["dataid"] for r in rows], dtype=np.int32)
+    self.geom_mesh_props = [(r["mesh_com"], r["mesh_I"]) for r in rows]
     m.geom_mass_ = np.array([r["mass"] for r in rows])
     m.geom_inertia_ = np.array([r["inertia"] for r in rows]).reshape(ng, 3)
     m.geom_rgba = np.tile([0.5, 0.5, 0.5, 1.0], (ng, 1))
@@ -1103,14 +1142,25 @@ class _Compiler:
       rbound = 0.0
       aabb = [0, 0, 0, size[0], size[1], 0.0]
     elif gtype == GeomType.MESH:
-      vol = 0.0
-      rbound = 0.0
-      aabb = [0, 0, 0, 0, 0, 0]
+      if ga.get("mesh") not in self.mesh_id:
+        raise ValueError(f"geom {ga.get('name', '')}: unknown mesh '{ga.get('mesh')}'")
+      dataid = self.mesh_id[ga["mesh"]]
+      mv, mf = self.mesh_data[dataid]
+      vol, mesh_com, mesh_I1 = _mesh_mass_props(mv, mf)
+      rbound = float(np.sqrt((mv * mv).sum(axis=1).max()))
+      lo, hi = mv.min(axis=0), mv.max(axis=0)
+      aabb = list(0.5 * (lo + hi)) + list(0.5 * (hi - lo))
+      size = 0.5 * (hi - lo)
     else:
       raise NotImplementedError(gtype)
     density = float(ga.get("density", _GEOM_DEFAULTS["density"]))
     mass = float(ga["mass"]) if "mass" in ga else density * vol
-    inertia = _geom_inertia(gtype, size, mass)
+    if gtype == GeomType.MESH:
+      inertia = np.zeros(3)
+      # full inertia about the mesh COM in the geom frame (unit-density integrals scaled to mass)
+      mesh_I = mesh_I1 * (mass / vol) if vol > MJ_MINVAL else np.zeros((3, 3))
+    else:
+      inertia = _geom_inertia(gtype, size, mass)
     return dict(
       name=ga.get("name", ""),
       type=int(gtype),
@@ -1133,6 +1183,9 @@ class _Compiler:
       aabb=aabb,
       mass=mass if gtype != GeomType.PLANE else 0.0,
       inertia=inertia,
+      dataid=dataid if gtype == GeomType.MESH else -1,
+      mesh_com=mesh_com if gtype == GeomType.MESH else None,
+      mesh_I=mesh_I if gtype == GeomType.MESH else None,
     )
 
   def _build_inertia(self):
@@ -1162,24 +1215,33 @@ class _Compiler:
           m.body_iquat[i] = q if q is not None else [1, 0, 0, 0]
           m.body_inertia[i] = _floats(ia["diaginertia"], 3)
         continue
-      geoms = [g for g in range(m.ngeom) if m.geom_bodyid[g] == i and m.geom_type[g] != GeomType.PLANE]
-      if any(m.geom_type[g] == GeomType.MESH for g in geoms):
-        raise NotImplementedError(f"body {b.name}: inertia from mesh geoms needs the mesh file (give <inertial>)")
+      # massless geoms (e.g. density="0" visual meshes) do not shape the inertial frame
+      geoms = [g for g in range(m.ngeom) if m.geom_bodyid[g] == i and m.geom_type[g] != GeomType.PLANE and m.geom_mass_[g] > 0]
       if not geoms:
         continue
       mass = sum(m.geom_mass_[g] for g in geoms)
       if mass < MJ_MINVAL:
         continue
-      com = sum(m.geom_mass_[g] * m.geom_pos[g] for g in geoms) / mass
-      I = np.zeros((3, 3))
+      # per geom: COM and inertia about it, in the body frame (meshes: COM offset + full tensor)
+      gcom, gI = {}, {}
       for g in geoms:
         R = quat_to_mat(m.geom_quat[g])
-        I += R @ np.diag(m.geom_inertia_[g]) @ R.T
-        dvec = m.geom_pos[g] - com
+        mc, mI = self.geom_mesh_props[g]
+        if m.geom_type[g] == GeomType.MESH:
+          gcom[g] = m.geom_pos[g] + R @ mc
+          gI[g] = R @ mI @ R.T
+        else:
+          gcom[g] = m.geom_pos[g]
+          gI[g] = R @ np.diag(m.geom_inertia_[g]) @ R.T
+      com = sum(m.geom_mass_[g] * gcom[g] for g in geoms) / mass
+      I = np.zeros((3, 3))
+      for g in geoms:
+        I += gI[g]
+        dvec = gcom[g] - com
         I += m.geom_mass_[g] * (np.dot(dvec, dvec) * np.eye(3) - np.outer(dvec, dvec))
       m.body_mass[i] = mass
       m.body_ipos[i] = com
-      if len(geoms) == 1:
+      if len(geoms) == 1 and m.geom_type[geoms[0]] != GeomType.MESH:
         # single geom: inertial frame = geom frame (diagonal inertia in geom frame)
         m.body_iquat[i] = m.geom_quat[geoms[0]]
         m.body_inertia[i] = m.geom_inertia_[geoms[0]]
@@ -1187,6 +1249,12 @@ class _Compiler:
         w, V = _eig3(I)
         m.body_iquat[i] = mat_to_quat(V)
         m.body_inertia[i] = w
+    # <compiler boundmass / boundinertia>: lower bounds on every body except the world, flexcomp
+    # vertex bodies included (MuJoCo user_body.cc; parity unpinned)
+    if self.boundmass > 0:
+      m.body_mass[1:] = np.maximum(m.body_mass[1:], self.boundmass)
+    if self.boundinertia > 0:
+      m.body_inertia[1:] = np.maximum(m.body_inertia[1:], self.boundinertia)
 
   def _subtreemass(self):
     m = self.m
@@ -1547,6 +1615,59 @@ def _bending_coef(x, mu, thickness):
   a0, a1 = 0.5 * np.linalg.norm(np.cross(e0, e1)), 0.5 * np.linalg.norm(np.cross(e0, e2))
   c = np.array([c03 + c04, c01 + c02, -(c01 + c03), -(c02 + c04)])
   return (np.outer(c, c) * mu * thickness**3 / (8.0 * (a0 + a1))).reshape(-1)
+
+
+def _read_mesh_file(path):
+  """(vertices (n, 3) float64, triangles (t, 3) int64) of a binary / ASCII STL or an OBJ file."""
+  ext = os.path.splitext(path)[1].lower()
+  with open(path, "rb") as fh:
+    buf = fh.read()
+  if ext == ".stl":
+    if buf[:5] == b"solid" and b"facet" in buf[:1024]:  # ASCII STL
+      vals = [ln.split()[1:4] for ln in buf.decode("ascii", "replace").splitlines() if ln.strip().startswith("vertex")]
+      v = np.array(vals, dtype=np.float64)
+    else:
+      n = int(np.frombuffer(buf, dtype="<u4", count=1, offset=80)[0])
+      rec = np.dtype([("n", "<f4", 3), ("v", "<f4", 9), ("a", "<u2")])
+      v = np.frombuffer(buf, dtype=rec, count=n, offset=84)["v"].reshape(-1, 3).astype(np.float64)
+    return v, np.arange(len(v)).reshape(-1, 3)
+  if ext == ".obj":
+    verts, faces = [], []
+    for ln in buf.decode("utf-8", "replace").splitlines():
+      p = ln.split()
+      if not p:
+        continue
+      if p[0] == "v":
+        verts.append([float(x) for x in p[1:4]])
+      elif p[0] == "f":
+        idx = [int(t.split("/")[0]) for t in p[1:]]
+        idx = [i - 1 if i > 0 else len(verts) + i for i in idx]
+        for k in range(1, len(idx) - 1):  # fan triangulation
+          faces.append([idx[0], idx[k], idx[k + 1]])
+    return np.array(verts, dtype=np.float64).reshape(-1, 3), np.array(faces, dtype=np.int64).reshape(-1, 3)
+  raise NotImplementedError(f"mesh file type '{ext}' is not supported (STL / OBJ only)")
+
+
+def _mesh_mass_props(v, f):
+  """(volume, COM, inertia about the COM at unit density) of a closed triangle mesh from signed
+  tetrahedra against the origin (MuJoCo's exact-volume mesh inertia; |volume| so that inverted
+  winding still gives a positive mass)."""
+  if len(f) == 0:
+    return 0.0, np.zeros(3), np.zeros((3, 3))
+  a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
+  dv = np.einsum("ij,ij->i", a, np.cross(b, c)) / 6.0
+  vol = dv.sum()
+  if abs(vol) < 1e-300:
+    return 0.0, np.zeros(3), np.zeros((3, 3))
+  com = (dv[:, None] * (a + b + c) / 4.0).sum(axis=0) / vol
+  # second moments of each tetrahedron (origin, a, b, c): dv/20 (sum_i x_i x_i^T + s s^T), s = a+b+c
+  s = a + b + c
+  C = (dv[:, None, None] / 20.0 * (np.einsum("ij,ik->ijk", a, a) + np.einsum("ij,ik->ijk", b, b) + np.einsum("ij,ik->ijk", c, c)
+                                   + np.einsum("ij,ik->ijk", s, s))).sum(axis=0)
+  C = C - vol * np.outer(com, com)  # covariance about the COM
+  I = np.trace(C) * np.eye(3) - C
+  sign = 1.0 if vol > 0 else -1.0
+  return abs(vol), com, sign * I
 
 
 def _geom_inertia(gtype, size, mass):

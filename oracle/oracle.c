@@ -22,7 +22,7 @@
 #define MINMU ((real)1e-5)
 
 enum { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
-enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6 };
+enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6, GEOM_MESH = 7 };
 enum { DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16,
        DSBL_SPRING = 32, DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512,
        DSBL_FILTERPARENT = 1024, DSBL_ACTUATION = 2048, DSBL_REFSAFE = 4096, DSBL_SENSOR = 8192, DSBL_EULERDAMP = 1 << 15 };
@@ -1361,6 +1361,69 @@ static void plane_cylinder_k(int k, const real* n, const real* ppos, const real*
   }
 }
 
+/* collision_primitive.py:52-139, 257-277 plane_convex, exhaustive-search branch: the deepest vertex a,
+ * then among the vertices within 1e-3 of its depth the one farthest from a (b), farthest from line ab
+ * (c), and from the triangle's other edges (d); each distinct vertex is a contact at its own depth. */
+static int plane_mesh(const real* nw, const real* ppos, const real* gpos, const real* R, const real* mv, int nvert, real* dist,
+                      real pos[4][3]) {
+  const real HUGE_ = 1e6;
+  real d0[3] = {ppos[0] - gpos[0], ppos[1] - gpos[1], ppos[2] - gpos[2]}, pl[3], n[3];
+  for (int i = 0; i < 3; i++) {
+    pl[i] = R[i] * d0[0] + R[3 + i] * d0[1] + R[6 + i] * d0[2];
+    n[i] = R[i] * nw[0] + R[3 + i] * nw[1] + R[6 + i] * nw[2];
+  }
+#define PM_SUP(v) ((pl[0] - (v)[0]) * n[0] + (pl[1] - (v)[1]) * n[1] + (pl[2] - (v)[2]) * n[2])
+  int idx[4] = {-1, -1, -1, -1};
+  real maxs = -HUGE_, a[3] = {0, 0, 0}, b[3] = {0, 0, 0}, c[3] = {0, 0, 0};
+  for (int i = 0; i < nvert; i++) {
+    real s = PM_SUP(mv + 3 * i);
+    if (s > maxs) { maxs = s; idx[0] = i; memcpy(a, mv + 3 * i, sizeof(a)); }
+  }
+  if (maxs < 0) return 0;
+  real thr = maxs - (real)1e-3, best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const real* v = mv + 3 * i;
+    real mask = PM_SUP(v) > thr ? 0 : -HUGE_;
+    real dv[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]};
+    real dd = dot3(dv, dv) + mask;
+    if (dd > best) { idx[1] = i; best = dd; memcpy(b, v, sizeof(b)); }
+  }
+  real ab[3], t[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+  cross3(ab, n, t);
+  best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const real* v = mv + 3 * i;
+    real mask = PM_SUP(v) > thr ? 0 : -HUGE_;
+    real ap[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]};
+    real dd = fabs(dot3(ap, ab)) + mask;
+    if (dd > best) { idx[2] = i; best = dd; memcpy(c, v, sizeof(c)); }
+  }
+  real ac[3], bc[3], t1[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]}, t2[3] = {b[0] - c[0], b[1] - c[1], b[2] - c[2]};
+  cross3(ac, n, t1);
+  cross3(bc, n, t2);
+  best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const real* v = mv + 3 * i;
+    real mask = PM_SUP(v) > thr ? 0 : -HUGE_;
+    real ap[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]}, bp[3] = {b[0] - v[0], b[1] - v[1], b[2] - v[2]};
+    real dd = (fabs(dot3(ap, ac)) + mask) + (fabs(dot3(bp, bc)) + mask);
+    if (dd > best) { idx[3] = i; best = dd; }
+  }
+  int cnt = 0;
+  for (int i = 3; i >= 0; i--) {
+    int count = 0;
+    for (int j = 0; j <= i; j++) count += idx[j] == idx[i];
+    if (count != 1) continue;
+    const real* v = mv + 3 * idx[i];
+    real dd = -PM_SUP(v);
+    for (int k = 0; k < 3; k++) pos[cnt][k] = gpos[k] + R[3 * k] * v[0] + R[3 * k + 1] * v[1] + R[3 * k + 2] * v[2] - (real)0.5 * dd * nw[k];
+    dist[cnt] = dd;
+    cnt++;
+  }
+#undef PM_SUP
+  return cnt;
+}
+
 static void collision(const orc_model* m, orc_data* d) {
   *d->ncon = 0;
   *d->ncollision = 0;
@@ -1406,11 +1469,41 @@ static void collision(const orc_model* m, orc_data* d) {
       c.n = 1;
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) { /* collision_primitive.py:1117-1199 */
       capsule_box(&c, p1, n1, s1[0], s1[1], p2, r2, s2);
-    } else if (t1 == GEOM_BOX && t2 == GEOM_BOX) { /* convex (GJK/EPA) pair, collision_convex.py:701-890 */
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_MESH) { /* collision_primitive.py:52-277, 810-870 plane_convex */
+      real pd[4], pp[4][3], fr[9];
+      int md = m->geom_dataid[g2];
+      int n = plane_mesh(n1, p1, p2, r2, m->mesh_vert + 3 * m->mesh_vertadr[md], m->mesh_vertnum[md], pd, pp);
+      make_frame(fr, n1);
+      for (int k = 0; k < n; k++) {
+        if (!(pd[k] < margin) || pairid0 < -1) continue;
+        int cid = *d->ncon;
+        if (cid >= d->nconmax) { (*d->ncon)++; continue; }
+        d->con_dist[cid] = pd[k];
+        memcpy(d->con_pos + 3 * cid, pp[k], 3 * sizeof(real));
+        memcpy(d->con_frame + 9 * cid, fr, 9 * sizeof(real));
+        d->con_includemargin[cid] = margin - gap;
+        memcpy(d->con_friction + 5 * cid, friction, 5 * sizeof(real));
+        memcpy(d->con_solref + 2 * cid, solref, 2 * sizeof(real));
+        memcpy(d->con_solreffriction + 2 * cid, solreffriction, 2 * sizeof(real));
+        memcpy(d->con_solimp + 5 * cid, solimp, 5 * sizeof(real));
+        d->con_dim[cid] = condim;
+        d->con_geom[2 * cid] = g1;
+        d->con_geom[2 * cid + 1] = g2;
+        d->con_flex[2 * cid] = d->con_flex[2 * cid + 1] = d->con_vert[2 * cid] = d->con_vert[2 * cid + 1] = -1;
+        for (int i = 0; i < 10; i++) d->con_efc_address[10 * cid + i] = -1;
+        (*d->ncon)++;
+      }
+      continue;
+    } else if ((t1 == GEOM_BOX && t2 == GEOM_BOX) || (t2 == GEOM_MESH && (t1 == GEOM_SPHERE || t1 == GEOM_CAPSULE || t1 == GEOM_BOX || t1 == GEOM_MESH))) {
+      /* convex (GJK/EPA) pair, collision_convex.py:701-890 */
       ccd_geom cg1, cg2;
       cg1.type = t1; cg2.type = t2;
       memcpy(cg1.pos, p1, sizeof(cg1.pos)); memcpy(cg1.rot, r1, sizeof(cg1.rot)); memcpy(cg1.size, s1, sizeof(cg1.size));
       memcpy(cg2.pos, p2, sizeof(cg2.pos)); memcpy(cg2.rot, r2, sizeof(cg2.rot)); memcpy(cg2.size, s2, sizeof(cg2.size));
+      cg1.vert = t1 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g1]] : NULL;
+      cg1.nvert = t1 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g1]] : 0;
+      cg2.vert = t2 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g2]] : NULL;
+      cg2.nvert = t2 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g2]] : 0;
       real cdist, cnrm[3], cpts[4][3], cframe[9];
       int nc = ccd_pair(&cg1, &cg2, m->opt_ccd_tolerance, m->opt_ccd_iterations, m->ccd_epa_iterations, margin, &cdist, cnrm, cpts);
       make_frame(cframe, cnrm);

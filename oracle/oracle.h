@@ -29,7 +29,7 @@ typedef ORC_REAL real;
   X(nxn) X(nmaxpyramid) X(neq) X(nsensor) X(nsensordata) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)             \
   X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
-  X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata)
+  X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
@@ -61,7 +61,7 @@ typedef ORC_REAL real;
   X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)                               \
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flex_vert, nflexvert * 3) X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)    \
-  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)
+  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17) X(mesh_vert, nmeshvert * 3)
 
 /* ---- model: int arrays (name, element count) ---- */
 #define ORC_MODEL_INT_ARRAYS(X)                                                                    \
@@ -89,7 +89,7 @@ typedef ORC_REAL real;
   X(flex_elemedgeadr, nflex) X(flex_contype, nflex) X(flex_conaffinity, nflex) X(flex_condim, nflex) \
   X(flex_centered, nflex) X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert)              \
   X(flex_edge, nflexedge * 2) X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata)          \
-  X(flex_elemedge, nflexelem * 3)
+  X(flex_elemedge, nflexelem * 3) X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)
 
 /* ---- per-world data: real arrays (name, element count per world) ---- */
 #define ORC_DATA_REAL_ARRAYS(X)                                                                    \

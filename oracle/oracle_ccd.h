@@ -25,6 +25,8 @@ static real ccd_edge_tol(void) { return sin((real)0.0016); }
 typedef struct {
   real pos[3], rot[9], size[3], margin;
   int type;
+  const real* vert; /* mesh vertices in the geom frame (GEOM_MESH) */
+  int nvert;
 } ccd_geom;
 
 typedef struct {
@@ -59,6 +61,13 @@ static ccd_sp ccd_support(const ccd_geom* g, const real* dir) {
     real dd = sqrt(ld[0] * ld[0] + ld[1] * ld[1]);
     if (dd > CCD_MINVAL) { res[0] = ld[0] * g->size[0] / dd; res[1] = ld[1] * g->size[0] / dd; }
     res[2] = ccd_sign(ld[2]) * g->size[1];
+  } else if (g->type == GEOM_MESH) { /* collision_gjk.py:136-151: exhaustive, first strict maximum */
+    real best = -CCD_FLOAT_MAX;
+    for (int i = 0; i < g->nvert; i++) {
+      const real* v = g->vert + 3 * i;
+      real dd = v[0] * ld[0] + v[1] * ld[1] + v[2] * ld[2];
+      if (dd > best) { best = dd; sp.vertex_index = i; res[0] = v[0]; res[1] = v[1]; res[2] = v[2]; }
+    }
   }
   for (int i = 0; i < 3; i++) sp.point[i] = g->rot[3 * i] * res[0] + g->rot[3 * i + 1] * res[1] + g->rot[3 * i + 2] * res[2] + g->pos[i];
   if (g->margin > 0)
@@ -864,7 +873,9 @@ static int ccd_pair(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, 
   g1.margin = margin;
   g2.margin = margin;
   real cutoff = 0;
-  int discrete = (g1.type == GEOM_BOX) && (g2.type == GEOM_BOX) && g1.margin == 0 && g2.margin == 0;
+  /* collision_gjk.py:91-94, 2226: boxes and meshes are discrete */
+  int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH) && (g2.type == GEOM_BOX || g2.type == GEOM_MESH) && g1.margin == 0 &&
+                 g2.margin == 0;
   real full1 = 0, full2 = 0, size1 = 0, size2 = 0;
   if (g1.type == GEOM_SPHERE || g1.type == GEOM_CAPSULE) {
     size1 = g1.size[0]; full1 = size1 + 0.5 * g1.margin; g1.margin = 0; g1.size[0] = 0;

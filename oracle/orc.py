@@ -130,6 +130,7 @@ class OracleModel:
       is_sparse=int(getattr(mjm.opt, "jacobian", 2) == 1 or (getattr(mjm.opt, "jacobian", 2) == 2 and mjm.nv > 32)),
       nflex=getattr(mjm, "nflex", 0), nflexvert=getattr(mjm, "nflexvert", 0), nflexedge=getattr(mjm, "nflexedge", 0),
       nflexelem=getattr(mjm, "nflexelem", 0), nflexelemdata=getattr(mjm, "nflexelemdata", 0),
+      nmesh=getattr(mjm, "nmesh", 0), nmeshvert=getattr(mjm, "nmeshvert", 0),
     )
     if overrides:
       vals.update(overrides)

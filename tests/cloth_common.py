@@ -21,6 +21,31 @@ def cloth_model():
   return mjcf.load_model(CLOTH)
 
 
+ALOHA = os.path.join(ROOT, "models", "aloha_cloth", "scene.xml")
+
+
+def aloha_model():
+  from mujoco_warp_amd import mjcf
+
+  return mjcf.load_model(ALOHA)
+
+
+def aloha_states(mjm, nworld, seed=0, qnoise=0.05, vnoise=0.1):
+  """Keyframe 0 (neutral pose, towel on the table) with seeded arm joint / velocity noise."""
+  from mujoco_warp_amd import mjcf
+
+  rng = np.random.default_rng(seed)
+  d = mjcf.MjData(mjm)
+  mjcf.reset_data_keyframe(mjm, d, 0)
+  qpos = np.tile(d.qpos, (nworld, 1))
+  na = 16  # the two arms' joints come first (the flexcomp's slide joints follow)
+  qpos[:, :na] += rng.normal(0, qnoise, (nworld, na)) * (np.arange(na) % 8 < 6)
+  qvel = np.zeros((nworld, mjm.nv))
+  qvel[:, :na] = rng.normal(0, vnoise, (nworld, na))
+  ctrl = np.tile(d.ctrl, (nworld, 1))
+  return qpos, qvel, ctrl
+
+
 def flex_vert_adr(mjm, kind="qpos"):
   """(nflexvert, 3) qpos (or dof) addresses of the slide joints that carry each flex vertex."""
   out = np.full((mjm.nflexvert, 3), -1, dtype=np.int64)

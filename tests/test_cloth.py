@@ -16,10 +16,22 @@ optimum, short rollouts, and determinism across copies of one world.
 import numpy as np
 import pytest
 
-from tests.cloth_common import cloth_model, cloth_states, dense_J, dense_qM, flex_vert_adr, gpu_contacts, oracle_contacts
+from tests.cloth_common import (aloha_model, aloha_states, cloth_model, cloth_states, dense_J, dense_qM, flex_vert_adr, gpu_contacts,
+                                 oracle_contacts)
 from tests.common import assert_close, gpu_from_state, np_, oracle_from_state
 
 NJMAX, NCONMAX = 3000, 200
+# aloha_cloth: the towel lies on the table, 2 contacts per triangle (3364) and ~16k rows -- sized so
+# that nothing overflows (the reference config's 920 / 6300 would cut both)
+ALOHA_NJMAX, ALOHA_NCONMAX = 16384, 4096
+
+
+def _setup(which, nworld, seed):
+  if which == "aloha":
+    mjm = aloha_model()
+    return (mjm,) + aloha_states(mjm, nworld, seed=seed) + (ALOHA_NJMAX, ALOHA_NCONMAX)
+  mjm = cloth_model()
+  return (mjm,) + cloth_states(mjm, nworld, seed=seed) + (NJMAX, NCONMAX)
 
 
 @pytest.fixture(scope="module")
@@ -108,13 +120,14 @@ def _match_rows(d, od, w, gc, oc):
 
 
 @pytest.mark.gpu
-def test_gpu_cloth_position_stage_parity(mjm):
+@pytest.mark.parametrize("which", ["cloth", "aloha"])
+def test_gpu_cloth_position_stage_parity(which):
   import torch
 
   import mujoco_warp_amd as mjw
 
-  nworld = 3
-  qpos, qvel, ctrl = cloth_states(mjm, nworld, seed=1)
+  nworld = 2
+  mjm, qpos, qvel, ctrl, NJMAX, NCONMAX = _setup(which, nworld, seed=1)
   m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=NJMAX, nconmax=NCONMAX)
   om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=NJMAX, nconmax=NCONMAX)
   mjw.fwd_position(m, d)
@@ -130,6 +143,7 @@ def test_gpu_cloth_position_stage_parity(mjm):
     assert (int(d.ne[w]), int(d.nf[w]), int(d.nl[w]), int(d.nefc[w])) == (int(od.ne[w, 0]), int(od.nf[w, 0]), int(od.nl[w, 0]), int(od.nefc[w, 0]))
     gc, oc = gpu_contacts(d, w), oracle_contacts(od, w)
     assert len(gc) == len(oc) and any(c["flex"][1] == 0 for c in gc)
+    assert int(od.ncon[w, 0]) <= NCONMAX
     for a, b in zip(gc, oc):
       assert (a["geom"], a["flex"], a["vert"], a["dim"]) == (b["geom"], b["flex"], b["vert"], b["dim"])
       assert abs(a["dist"] - b["dist"]) < 2e-6
@@ -149,15 +163,16 @@ def test_gpu_cloth_position_stage_parity(mjm):
 
 
 @pytest.mark.gpu
-def test_gpu_cloth_smooth_forces_and_cg_cost(mjm):
+@pytest.mark.parametrize("which", ["cloth", "aloha"])
+def test_gpu_cloth_smooth_forces_and_cg_cost(which):
   """qfrc_passive / qacc_smooth to fp32 accuracy; the device CG solution's fp64 cost within the
   reference's CG tolerance of the oracle optimum (solver_test.py:317 uses 1.025x)."""
   import torch
 
   import mujoco_warp_amd as mjw
 
-  nworld = 3
-  qpos, qvel, ctrl = cloth_states(mjm, nworld, seed=2)
+  nworld = 2
+  mjm, qpos, qvel, ctrl, NJMAX, NCONMAX = _setup(which, nworld, seed=2)
   m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=NJMAX, nconmax=NCONMAX)
   om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=NJMAX, nconmax=NCONMAX)
   mjw.forward(m, d)
@@ -181,13 +196,14 @@ def test_gpu_cloth_smooth_forces_and_cg_cost(mjm):
 
 
 @pytest.mark.gpu
-def test_gpu_cloth_rollout_parity_and_determinism(mjm):
+@pytest.mark.parametrize("which", ["cloth", "aloha"])
+def test_gpu_cloth_rollout_parity_and_determinism(which):
   import torch
 
   import mujoco_warp_amd as mjw
 
   nworld = 2
-  qpos, qvel, ctrl = cloth_states(mjm, nworld, seed=4)
+  mjm, qpos, qvel, ctrl, NJMAX, NCONMAX = _setup(which, nworld, seed=4)
   m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=NJMAX, nconmax=NCONMAX)
   om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=NJMAX, nconmax=NCONMAX)
   for _ in range(3):
@@ -197,7 +213,7 @@ def test_gpu_cloth_rollout_parity_and_determinism(mjm):
   assert_close("qpos", np_(d.qpos), od.qpos, rtol=1e-3, atol=1e-4)
   assert_close("qvel", np_(d.qvel), od.qvel, rtol=0.1, atol=1e-2)
   # copies of one world stay bitwise equal over a longer rollout, and nothing blows up
-  rep = 64
+  rep = 64 if which == "cloth" else 16
   m2, d2 = gpu_from_state(mjm, np.repeat(qpos[:1], rep, 0), np.repeat(qvel[:1], rep, 0), np.repeat(ctrl[:1], rep, 0), njmax=NJMAX, nconmax=NCONMAX)
   for _ in range(100):
     mjw.step(m2, d2)

@@ -1,7 +1,8 @@
-"""Diagnostic: sparse / flex pipeline (csrc/mjw_sparse.hip) vs the fp64 oracle on the cloth scene.
+"""Diagnostic: sparse / flex pipeline (csrc/mjw_sparse.hip) vs the fp64 oracle on the cloth scene
+(or aloha_cloth).
 
 Prints the worst relative error per stage instead of asserting, so one GPU call shows every
-mismatch.  Usage: python tools/cloth_diag.py [nworld] [nstep]
+mismatch.  Usage: python tools/cloth_diag.py [nworld] [nstep] [cloth|aloha]
 """
 
 import os
@@ -35,9 +36,17 @@ def main():
 
   nworld = int(sys.argv[1]) if len(sys.argv) > 1 else 2
   nstep = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-  mjm = cloth_model()
-  qpos, qvel, ctrl = cloth_states(mjm, nworld, seed=0)
-  njmax, nconmax = 3000, 200
+  which = sys.argv[3] if len(sys.argv) > 3 else "cloth"
+  if which == "aloha":
+    from tests.cloth_common import aloha_model, aloha_states
+
+    mjm = aloha_model()
+    qpos, qvel, ctrl = aloha_states(mjm, nworld, seed=0)
+    njmax, nconmax = 16384, 4096
+  else:
+    mjm = cloth_model()
+    qpos, qvel, ctrl = cloth_states(mjm, nworld, seed=0)
+    njmax, nconmax = 3000, 200
   m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=nconmax)
   om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=nconmax)
   t = time.time()
@@ -82,6 +91,7 @@ def main():
     print(f"step {s}: qpos", rel(np_(d2.qpos), od2.qpos), " qvel", rel(np_(d2.qvel), od2.qvel), flush=True)
   # timing
   m3, d3 = gpu_from_state(mjm, np.repeat(qpos[:1], 256, 0), np.repeat(qvel[:1], 256, 0), np.repeat(ctrl[:1], 256, 0), njmax=njmax, nconmax=nconmax)
+  print("ncollision", int(d.ncollision), "nacon", int(d.nacon))
   for _ in range(3):
     mjw.step(m3, d3)
   torch.cuda.synchronize()
