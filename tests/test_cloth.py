@@ -107,9 +107,9 @@ def _efc_cost(J, D, aref, types_, M, qacc_smooth, qacc):
 
 
 def _match_rows(d, od, w, gc, oc):
-  """(gpu row, oracle row) pairs: equality rows by index, contact rows through the matched
-  contacts (gc / oc are the key-sorted contact lists of the two sides)."""
-  pairs = [(r, r) for r in range(int(od.ne[w, 0]))]
+  """(gpu row, oracle row) pairs: equality / friction / limit rows by index, contact rows through
+  the matched contacts (gc / oc are the key-sorted contact lists of the two sides)."""
+  pairs = [(r, r) for r in range(int(od.ne[w, 0]) + int(od.nf[w, 0]) + int(od.nl[w, 0]))]
   for a, b in zip(gc, oc):
     ga = d.contact.efc_address[a["slot"]].cpu().numpy()
     oa = od.con_efc_address[w, 10 * b["slot"] : 10 * b["slot"] + 10]
