@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 9
+#define MJW_ABI_VERSION 10
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -109,7 +109,7 @@
 /* ---- data: float arrays, (nworld, count) world-major like mujoco_warp types.Data ----
  * Sparse models (is_sparse, the reference's io.py:67-74 switch) store qM / qLD as (nworld, nM) rows of
  * ancestors ascending then the diagonal (M_rowadr / M_colind), and efc_J as (nworld, njmax_pad, njrow)
- * with efc_J_colind / efc_J_rownnz; dense models keep qM (nv_pad, nv_pad), qLD (nv, nv), efc_J
+ * stored slot-major (slot k of row r at [k * njmax_pad + r]) with efc_J_colind / efc_J_rownnz; dense models keep qM (nv_pad, nv_pad), qLD (nv, nv), efc_J
  * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt / ncon_world are sparse-path workspace (size 0 when dense). */
 #define MJW_DATA_REAL_ARRAYS(X)                                                                    \
   X(time, 1) X(qpos, nq) X(qvel, nv) X(act, na) X(ctrl, nu) X(qacc_warmstart, nv)                 \
@@ -132,7 +132,8 @@
   X(qpos_t0, nq) X(qvel_t0, nv) X(act_t0, na) X(qvel_rk, nv) X(qacc_rk, nv) X(act_dot_rk, na)     \
   X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
   X(flexedge_J, nflexedge * 6) X(flex_frc, nflexelem * 9 + nflexedge * 12)                        \
-  X(sp_body, nbody * 6) X(sp_vec, nv * 10) X(sp_row, njmax * 2) X(sp_LD, nM)
+  X(sp_body, nbody * 6) X(sp_vec, nv * 10) X(sp_row, njmax * 2) X(sp_LD, nM)                     \
+  X(efc_JT_val, njmax_pad * njrow)
 
 /* ---- data: int arrays, (nworld, count) ---- */
 #define MJW_DATA_INT_ARRAYS(X)                                                                     \

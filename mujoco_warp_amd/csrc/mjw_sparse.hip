@@ -12,7 +12,9 @@
 //     beyond the kinematics levels;
 //   * M and its factor use the ancestor-row sparse layout (M_rowadr / M_colind, diagonal last);
 //     the L'DL factor and solves run one kinematic tree per thread (smooth.py:1003-1064, 2813-2846);
-//   * constraint Jacobian rows are sparse (efc_J_colind / efc_J_rownnz, njrow slots per row);
+//   * constraint Jacobian rows are sparse (efc_J_colind / efc_J_rownnz, njrow slots per row) and
+//     stored slot-major (ELL: slot k of every row contiguous, (nworld, njrow, njmax_pad)), so the
+//     row-parallel passes read only the slots a row uses, coalesced across the wave;
 //     the solver builds the transposed (column) index once per solve, so J'f is a deterministic
 //     per-dof gather instead of atomics;
 //   * contacts and rows are emitted in a deterministic per-world order with block scans.
@@ -30,6 +32,24 @@ namespace sp {
 #define MR_W(name) (MR(name)[0])
 
 constexpr int BLK = 256;
+constexpr int SP_LDS_CNT_MAX = 8192;  // column counters of the J transpose live in LDS up to this nv + 1
+
+// opt-in phase timers of this path (build with -DMJW_PROFILE; tools/sparse_prof.py): s_memtime
+// deltas summed over waves, read back with mjw_prof_read_sparse
+enum : int { SPH_KIN = 0, SPH_FLEX, SPH_CRB, SPH_COLL, SPH_CON, SPH_VEL, SPH_ACT, SPH_ACC, SPH_SINIT, SPH_SLS, SPH_SUPD, SPH_SCG, SPH_N };
+#ifdef MJW_PROFILE
+static __device__ unsigned long long g_sprof[SPH_N];
+#define SPROF_T0() unsigned long long _spt = __builtin_amdgcn_s_memtime()
+#define SPROF_MARK(ph)                                                           \
+  do {                                                                           \
+    unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_sprof[ph], _nt - _spt);            \
+    _spt = _nt;                                                                  \
+  } while (0)
+#else
+#define SPROF_T0() (void)0
+#define SPROF_MARK(ph) (void)0
+#endif
 constexpr int NWAVE = BLK / 64;
 enum : int { EQ_FLEX = 4 };
 
@@ -1108,13 +1128,12 @@ __device__ void put_row(const mjw_model_t& m, const mjw_data_t& d, int wid, int 
                         float pos_imp, float invweight, const float* solref, const float* solimp, float margin, float frictionloss, int type,
                         int id) {
   const float* qvel = d.qvel + (long)wid * m.nv;
-  const long jr = ((long)wid * d.njmax_pad + r) * m.njrow;
+  const long jb = (long)wid * m.njrow * d.njmax_pad + r, P = d.njmax_pad;
   float vel = 0.0f;
-  for (int k = 0; k < m.njrow; k++) {
-    const bool on = k < nnz;
-    d.efc_J[jr + k] = on ? vals[k] : 0.0f;
-    d.efc_J_colind[jr + k] = on ? cols[k] : 0;
-    if (on) vel += vals[k] * qvel[cols[k]];
+  for (int k = 0; k < nnz; k++) {
+    d.efc_J[jb + k * P] = vals[k];
+    d.efc_J_colind[jb + k * P] = cols[k];
+    vel += vals[k] * qvel[cols[k]];
   }
   d.efc_J_rownnz[(long)wid * d.njmax + r] = nnz;
   const float timestep = MR(opt_timestep)[0];
@@ -1267,7 +1286,7 @@ __device__ int make_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int
       invweight = invweight * 2.0f * fri0 * fri0 * iri * iri;
     }
     // union of the two weld bodies' dof chains, descending
-    const long jr = ((long)wid * d.njmax_pad + r) * m.njrow;
+    const long jb = (long)wid * m.njrow * d.njmax_pad + r, P = d.njmax_pad;
     int i1 = w1 > 0 ? m.body_dofadr[w1] + m.body_dofnum[w1] - 1 : -1;
     int i2 = w2 > 0 ? m.body_dofadr[w2] + m.body_dofnum[w2] - 1 : -1;
     int nnz = 0;
@@ -1298,14 +1317,10 @@ __device__ int make_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int
         }
       }
       if (condim > 1) Jval += (dimid % 2 == 0) ? Ji * frii : -Ji * frii;
-      d.efc_J[jr + nnz] = Jval;
-      d.efc_J_colind[jr + nnz] = dof;
+      d.efc_J[jb + nnz * P] = Jval;
+      d.efc_J_colind[jb + nnz * P] = dof;
       vel += Jval * qvel[dof];
       nnz++;
-    }
-    for (int k = nnz; k < m.njrow; k++) {
-      d.efc_J[jr + k] = 0.0f;
-      d.efc_J_colind[jr + k] = 0;
     }
     d.efc_J_rownnz[(long)wid * njmax + r] = nnz;
     const int type = condim == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
@@ -1766,21 +1781,30 @@ enum : int { SP_POS_A = 1 << 8, SP_POS_B = 1 << 9 };
 __global__ void __launch_bounds__(BLK) forward_kernel(const mjw_model_t m, const mjw_data_t d, int stages) {
   __shared__ Smem sm;
   const int wid = blockIdx.x;
+  SPROF_T0();
   if (stages & (ST_POS | SP_POS_A)) {
     kinematics(m, d, wid);
     com_pos(m, d, wid);
     camlight(m, d, wid);
+    SPROF_MARK(SPH_KIN);
     flex_edges(m, d, wid);
+    SPROF_MARK(SPH_FLEX);
     crb_qM(m, d, wid);
+    SPROF_MARK(SPH_CRB);
   }
   if (stages & (ST_POS | SP_POS_B)) {
     collision(m, d, wid, sm);
+    SPROF_MARK(SPH_COLL);
     make_constraint(m, d, wid, sm);
     transmission(m, d, wid, sm);
+    SPROF_MARK(SPH_CON);
   }
   if (stages & ST_VEL) fwd_velocity(m, d, wid);
+  SPROF_MARK(SPH_VEL);
   if (stages & ST_ACT) fwd_actuation(m, d, wid);
+  SPROF_MARK(SPH_ACT);
   if (stages & ST_ACC) fwd_acceleration(m, d, wid);
+  SPROF_MARK(SPH_ACC);
 }
 
 // convex pre-pass (collision_convex.py:701-890): one wave per world applies the broadphase to the
@@ -1829,12 +1853,13 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
 // iterative linesearch :886-1341, update_constraint :2154-2219, update_gradient :2879-3008
 // ---------------------------------------------------------------------------------------------
 struct SolveCtx {
-  int nv, nefc, ne, nf, njrow;
-  const float* J;
+  int nv, nefc, ne, nf, njrow, P;
+  const float* J;     // slot-major: slot k of row r at J[k * P + r]
   const int* Jcol;
   const int* Jnnz;
-  const int* JT_adr;
+  const int* JT_adr;  // J transposed (CSR by dof): rows JT_ind[p], values JT_val[p]
   const int* JT_ind;
+  const float* JT_val;
   const float* D;
   const float* fl;
   const float* aref;
@@ -1882,10 +1907,16 @@ __device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, 
   o[2] += jv * jvD;
 }
 
-__device__ void update_constraint(SolveCtx& c, Smem& sm) {
+// `alpha`: the linesearch step still to be applied to Jaref (fused here: Jaref += alpha * jv)
+__device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   float cost = 0.0f;
   for (int r = tid(); r < c.nefc; r += BLK) {
-    const float D = c.D[r], jaref = c.Jaref[r];
+    const float D = c.D[r];
+    float jaref = c.Jaref[r];
+    if (alpha != 0.0f) {
+      jaref += alpha * c.jv[r];
+      c.Jaref[r] = jaref;
+    }
     float f;
     int st;
     if (r < c.ne) {
@@ -1908,10 +1939,7 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm) {
   float g = 0.0f;
   for (int i = tid(); i < c.nv; i += BLK) {
     float s = 0.0f;
-    for (int p = c.JT_adr[i]; p < c.JT_adr[i + 1]; p++) {
-      const int code = c.JT_ind[p];
-      s += c.J[code] * c.force[code / c.njrow];
-    }
+    for (int p = c.JT_adr[i]; p < c.JT_adr[i + 1]; p++) s += c.JT_val[p] * c.force[c.JT_ind[p]];
     c.qfrc_c[i] = s;
     g += (c.Ma[i] - c.qfrc_s[i]) * (c.qacc[i] - c.qacc_s[i]);
   }
@@ -1939,21 +1967,21 @@ __device__ __forceinline__ bool in_bracket(const float* x, const float* y) {
   return (x[1] < y[1] && y[1] < 0.0f) || (x[1] > y[1] && y[1] > 0.0f);
 }
 
-__device__ void linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm) {
+// returns the step; qacc / Ma are updated here, Jaref by update_constraint
+__device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm) {
   mul_m_trees(m, c.M, c.search, c.mv);
+  // jv = J search, fused with the alpha = 0 evaluation of each row (same thread)
+  float v5[5] = {0, 0, 0, 0, 0};
   for (int r = tid(); r < c.nefc; r += BLK) {
-    const float* J = c.J + (long)r * c.njrow;
-    const int* col = c.Jcol + (long)r * c.njrow;
     float s = 0.0f;
-    for (int k = 0; k < c.Jnnz[r]; k++) s += J[k] * c.search[col[k]];
+    for (int k = 0; k < c.Jnnz[r]; k++) s += c.J[(long)k * c.P + r] * c.search[c.Jcol[(long)k * c.P + r]];
     c.jv[r] = s;
+    eval_row(c, r, 0.0f, v5);
   }
   __syncthreads();
   const float snorm = sqrtf(c.search_dot);
   const float scale = MR_W(stat_meaninertia) * (float)c.nv;
   const float gtol = fmaxf(MR_W(opt_tolerance) * MR_W(opt_ls_tolerance) * snorm * scale, 1e-6f);
-  float v5[5] = {0, 0, 0, 0, 0};
-  for (int r = tid(); r < c.nefc; r += BLK) eval_row(c, r, 0.0f, v5);
   for (int i = tid(); i < c.nv; i += BLK) {
     v5[3] += c.search[i] * (c.Ma[i] - c.qfrc_s[i]);
     v5[4] += 0.5f * c.search[i] * c.mv[i];
@@ -2030,8 +2058,8 @@ __device__ void linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm)
     c.qacc[i] += alpha * c.search[i];
     c.Ma[i] += alpha * c.mv[i];
   }
-  for (int r = tid(); r < c.nefc; r += BLK) c.Jaref[r] += alpha * c.jv[r];
   __syncthreads();
+  return alpha;
 }
 
 __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const mjw_data_t d) {
@@ -2045,20 +2073,27 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
     if (tid() == 0) d.solver_niter[wid] = 0;
     return;
   }
+  SPROF_T0();
   SolveCtx c;
   c.nv = nv;
   c.nefc = min(d.nefc[wid], njmax);
   c.ne = d.ne[wid];
   c.nf = d.nf[wid];
   c.njrow = m.njrow;
+  const long P = d.njmax_pad;
+  c.P = (int)P;
   c.J = d.efc_J + (long)wid * d.njmax_pad * m.njrow;
   c.Jcol = d.efc_J_colind + (long)wid * d.njmax_pad * m.njrow;
   c.Jnnz = d.efc_J_rownnz + (long)wid * njmax;
   int* JT_adr = d.efc_JT_adr + (long)wid * (nv + 1);
   int* JT_ind = d.efc_JT_rowind + (long)wid * d.njmax_pad * m.njrow;
-  int* cnt = d.sp_cnt + (long)wid * (nv + 1);
+  // column counters in LDS when they fit (sparse_launch sizes the dynamic LDS), else in HBM
+  extern __shared__ int s_cnt[];
+  int* cnt = (nv + 1) <= SP_LDS_CNT_MAX ? s_cnt : d.sp_cnt + (long)wid * (nv + 1);
+  float* JT_val = d.efc_JT_val + (long)wid * d.njmax_pad * m.njrow;
   c.JT_adr = JT_adr;
   c.JT_ind = JT_ind;
+  c.JT_val = JT_val;
   c.D = d.efc_D + (long)wid * d.njmax_pad;
   c.fl = d.efc_frictionloss + (long)wid * njmax;
   c.aref = d.efc_aref + (long)wid * njmax;
@@ -2087,7 +2122,7 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   for (int i = tid(); i < nv; i += BLK) qacc[i] = ws ? warm[i] : qacc_s[i];
   __syncthreads();
   for (int r = tid(); r < c.nefc; r += BLK)
-    for (int k = 0; k < c.Jnnz[r]; k++) atomicAdd(&cnt[c.Jcol[(long)r * m.njrow + k]], 1);
+    for (int k = 0; k < c.Jnnz[r]; k++) atomicAdd(&cnt[c.Jcol[k * P + r]], 1);
   __syncthreads();
   int run = 0;
   for (int c0 = 0; c0 < nv; c0 += BLK) {
@@ -2100,24 +2135,32 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   }
   if (tid() == 0) JT_adr[nv] = run;
   __syncthreads();
-  for (int r = tid(); r < c.nefc; r += BLK)
-    for (int k = 0; k < c.Jnnz[r]; k++) {
-      const int pos = atomicAdd(&cnt[c.Jcol[(long)r * m.njrow + k]], 1);
-      JT_ind[pos] = r * m.njrow + k;
-    }
-  __syncthreads();
-  for (int i = tid(); i < nv; i += BLK) {
-    for (int p = JT_adr[i] + 1; p < JT_adr[i + 1]; p++) {
-      const int key = JT_ind[p];
-      int q = p - 1;
-      while (q >= JT_adr[i] && JT_ind[q] > key) { JT_ind[q + 1] = JT_ind[q]; q--; }
-      JT_ind[q + 1] = key;
-    }
-  }
+  // fill carries the values (and computes Jaref on the way); the per-column sort of the
+  // (row * njrow + slot) codes then fixes the summation order of J'f whatever the atomics did
   for (int r = tid(); r < c.nefc; r += BLK) {
     float s = 0.0f;
-    for (int k = 0; k < c.Jnnz[r]; k++) s += c.J[(long)r * m.njrow + k] * qacc[c.Jcol[(long)r * m.njrow + k]];
+    for (int k = 0; k < c.Jnnz[r]; k++) {
+      const float v = c.J[k * P + r];
+      const int col = c.Jcol[k * P + r];
+      const int pos = atomicAdd(&cnt[col], 1);
+      JT_ind[pos] = r * m.njrow + k;
+      JT_val[pos] = v;
+      s += v * qacc[col];
+    }
     c.Jaref[r] = s - c.aref[r];
+  }
+  __syncthreads();
+  for (int i = tid(); i < nv; i += BLK) {
+    const int a = JT_adr[i], b = JT_adr[i + 1];
+    for (int p = a + 1; p < b; p++) {
+      const int key = JT_ind[p];
+      const float kv = JT_val[p];
+      int q = p - 1;
+      while (q >= a && JT_ind[q] > key) { JT_ind[q + 1] = JT_ind[q]; JT_val[q + 1] = JT_val[q]; q--; }
+      JT_ind[q + 1] = key;
+      JT_val[q + 1] = kv;
+    }
+    for (int p = a; p < b; p++) JT_ind[p] /= m.njrow;  // code -> row
   }
   __syncthreads();
   mul_m_trees(m, c.M, qacc, c.Ma);
@@ -2134,16 +2177,19 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   const float scale = 1.0f / (MR_W(stat_meaninertia) * (float)nv);
   const float tol = MR_W(opt_tolerance);
   int niter = 0;
+  SPROF_MARK(SPH_SINIT);
   if (m.opt_iterations != 0) {
     for (;;) {
-      linesearch(m, c, wid, sm);
+      const float alpha = linesearch(m, c, wid, sm);
+      SPROF_MARK(SPH_SLS);
       for (int i = tid(); i < nv; i += BLK) {
         c.pgrad[i] = c.grad[i];
         c.pMgrad[i] = c.Mgrad[i];
       }
       __syncthreads();
-      update_constraint(c, sm);
+      update_constraint(c, sm, alpha);
       update_gradient(m, c, sm);
+      SPROF_MARK(SPH_SUPD);
       float nd[2] = {0.0f, 0.0f};
       for (int i = tid(); i < nv; i += BLK) {
         nd[0] += c.grad[i] * (c.Mgrad[i] - c.pMgrad[i]);
@@ -2159,6 +2205,7 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
       }
       c.search_dot = block_sum1(s2, sm);
       niter++;
+      SPROF_MARK(SPH_SCG);
       const float improvement = (c.prev_cost - c.cost) * scale;
       const float gradient = sqrtf(c.grad_dot) * scale;
       if (improvement < tol || gradient < tol || niter == m.opt_iterations) break;
@@ -2217,6 +2264,17 @@ __global__ void __launch_bounds__(BLK) euler_kernel(const mjw_model_t m, const m
 
 }  // namespace sp
 
+#ifdef MJW_PROFILE
+extern "C" int mjw_prof_read_sparse(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(sp::g_sprof), sizeof(unsigned long long) * sp::SPH_N);
+  if (e == hipSuccess && reset) {
+    unsigned long long z[sp::SPH_N] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(sp::g_sprof), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
+
 // launcher used by the C entry points (mjw_step.hip) for models with m->is_sparse
 int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
   const int nw = d->nworld;
@@ -2231,7 +2289,10 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
     fwd = (fwd & ~ST_POS) | sp::SP_POS_B;
   }
   if (fwd) hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
-  if (stages & ST_SOLVE) hipLaunchKernelGGL(sp::solve_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
+  if (stages & ST_SOLVE) {
+    const size_t lds = (m->nv + 1) <= sp::SP_LDS_CNT_MAX ? (size_t)(m->nv + 1) * 4 : 0;
+    hipLaunchKernelGGL(sp::solve_kernel, dim3(nw), dim3(sp::BLK), lds, s, *m, *d);
+  }
   if (stages & ST_EULER) hipLaunchKernelGGL(sp::euler_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
   return (int)hipGetLastError();
 }

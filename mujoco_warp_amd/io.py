@@ -389,7 +389,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,),
     qfrc_passive=(nv,), qfrc_actuator=(nv,), qfrc_smooth=(nv,), qacc_smooth=(nv,), qfrc_constraint=(nv,),
     cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 17,),
-    efc_J=(njmax_pad, m.njrow), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
+    efc_J=(m.njrow, njmax_pad) if sp else (njmax_pad, m.njrow), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
     efc_aref=(njmax,), efc_frictionloss=(njmax,), efc_force=(njmax,), efc_Ma=(nv,),
     # RK4 workspace (forward.py:462-472 temporaries; kept resident so a step allocates nothing)
     qpos_t0=(nq,), qvel_t0=(nv,), act_t0=(na,), qvel_rk=(nv,), qacc_rk=(nv,), act_dot_rk=(na,),
@@ -397,11 +397,12 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     flexvert_xpos=(m.nflexvert, 3), flexedge_length=(m.nflexedge,), flexedge_velocity=(m.nflexedge,),
     flexedge_J=(m.nflexedge, 6), flex_frc=(m.nflexelem * 9 + m.nflexedge * 12,),
     sp_body=(nb * 6 * sp,), sp_vec=(nv * 10 * sp,), sp_row=(njmax * 2 * sp,), sp_LD=(m.nM * sp,),
+    efc_JT_val=(njmax_pad * m.njrow * sp,),
   )
   ints = dict(
     ne=(), nf=(), nl=(), nefc=(), solver_niter=(), moment_rownnz=(nu,), moment_rowadr=(nu,), moment_colind=(m.nJmom,),
     efc_type=(njmax,), efc_id=(njmax,), efc_state=(njmax_pad,), eq_active=(m.neq,),
-    efc_J_colind=(njmax_pad * sp, m.njrow), efc_J_rownnz=(njmax * sp,), efc_JT_rowind=(njmax_pad * m.njrow * sp,),
+    efc_J_colind=(m.njrow * sp, njmax_pad), efc_J_rownnz=(njmax * sp,), efc_JT_rowind=(njmax_pad * m.njrow * sp,),
     efc_JT_adr=((nv + 1) * sp,), sp_cnt=((nv + 1) * sp,), ncon_world=(2,),
   )
   creal = dict(
@@ -601,13 +602,30 @@ def get_data_into(result, mjm, d: types.Data, world_id: int = 0):
       setattr(result, name, val)
   result.time = float(d.time[world_id])
   nv = mjm.nv
-  result.qM_dense = d.qM[world_id, :nv, :nv].detach().cpu().numpy().astype(np.float64)
-  result.qLD_dense = d.qLD[world_id].detach().cpu().numpy().astype(np.float64)
-  # constraints of this world
   nefc = int(d.nefc[world_id])
   nrows = min(nefc, d.njmax)
   result.nefc = nefc
-  result.efc_J = d.efc.J[world_id, :nrows, :nv].detach().cpu().numpy().astype(np.float64)
+  if d.efc.J_colind.numel():  # sparse path: ancestor-row qM / qLD, slot-major J (densified here)
+    qm = d.qM[world_id].detach().cpu().numpy().astype(np.float64)
+    M = np.zeros((nv, nv))
+    for i in range(nv):
+      for k in range(mjm.M_rownnz[i]):
+        j = mjm.M_colind[mjm.M_rowadr[i] + k]
+        M[i, j] = M[j, i] = qm[mjm.M_rowadr[i] + k]
+    result.qM_dense = M
+    result.qLD_sparse = d.qLD[world_id].detach().cpu().numpy().astype(np.float64)
+    vals = d.efc.J[world_id, :, :nrows].detach().cpu().numpy().astype(np.float64)
+    cols = d.efc.J_colind[world_id, :, :nrows].cpu().numpy()
+    nnz = d.efc.J_rownnz[world_id, :nrows].cpu().numpy()
+    J = np.zeros((nrows, nv))
+    for r in range(nrows):
+      for k in range(nnz[r]):
+        J[r, cols[k, r]] += vals[k, r]
+    result.efc_J = J
+  else:
+    result.qM_dense = d.qM[world_id, :nv, :nv].detach().cpu().numpy().astype(np.float64)
+    result.qLD_dense = d.qLD[world_id].detach().cpu().numpy().astype(np.float64)
+    result.efc_J = d.efc.J[world_id, :nrows, :nv].detach().cpu().numpy().astype(np.float64)
   for f in ("pos", "margin", "D", "vel", "aref", "frictionloss", "force"):
     setattr(result, "efc_" + f, getattr(d.efc, f)[world_id, :nrows].detach().cpu().numpy().astype(np.float64))
   for f in ("type", "id", "state"):

@@ -86,14 +86,14 @@ def dense_qM(mjm, qm_sparse):
 
 
 def dense_J(d, w, n, nv):
-  """First n sparse efc rows of world w (efc_J values / colind / rownnz) -> dense (n, nv)."""
-  vals = d.efc.J[w, :n].detach().cpu().numpy().astype(np.float64)
-  cols = d.efc.J_colind[w, :n].cpu().numpy()
+  """First n sparse efc rows of world w (slot-major efc_J values / colind, rownnz) -> dense (n, nv)."""
+  vals = d.efc.J[w, :, :n].detach().cpu().numpy().astype(np.float64)
+  cols = d.efc.J_colind[w, :, :n].cpu().numpy()
   nnz = d.efc.J_rownnz[w, :n].cpu().numpy()
   J = np.zeros((n, nv))
   for r in range(n):
     for k in range(nnz[r]):
-      J[r, cols[r, k]] += vals[r, k]
+      J[r, cols[k, r]] += vals[k, r]
   return J
 
 
