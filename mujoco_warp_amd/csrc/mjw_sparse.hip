@@ -1873,8 +1873,7 @@ struct SolveCtx {
   float cost, prev_cost, gauss, search_dot, grad_dot;
 };
 
-__device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, float* o) {
-  const float D = c.D[r], jaref = c.Jaref[r], jv = c.jv[r];
+__device__ __forceinline__ void eval_row_v(const SolveCtx& c, int r, float D, float jaref, float jv, float alpha, float* o) {
   const float x = jaref + alpha * jv;
   if (r >= c.ne + c.nf) {
     if (x < 0.0f) {
@@ -1907,16 +1906,57 @@ __device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, 
   o[2] += jv * jvD;
 }
 
+__device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, float* o) {
+  eval_row_v(c, r, c.D[r], c.Jaref[r], c.jv[r], alpha, o);
+}
+
+// eval_row at NA step sizes over every row (o: NA x 3 sums).  The row passes are latency bound, so
+// each thread loads RU rows (r0, r0 + BLK, ...: the same per-thread order as a plain strided loop,
+// hence the same sums) before evaluating any of them.
+constexpr int RU = 4;
+template <int NA>
+__device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas, float* o) {
+  for (int r0 = tid(); r0 < c.nefc; r0 += RU * BLK) {
+    float D[RU], ja[RU], jv[RU];
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+      const int r = r0 + u * BLK;
+      const bool ok = r < c.nefc;
+      D[u] = ok ? c.D[r] : 0.0f;
+      ja[u] = ok ? c.Jaref[r] : 0.0f;
+      jv[u] = ok ? c.jv[r] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+      const int r = r0 + u * BLK;
+      if (r < c.nefc) {
+#pragma unroll
+        for (int a = 0; a < NA; a++) eval_row_v(c, r, D[u], ja[u], jv[u], alphas[a], o + 3 * a);
+      }
+    }
+  }
+}
+
 // `alpha`: the linesearch step still to be applied to Jaref (fused here: Jaref += alpha * jv)
 __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   float cost = 0.0f;
-  for (int r = tid(); r < c.nefc; r += BLK) {
-    const float D = c.D[r];
-    float jaref = c.Jaref[r];
-    if (alpha != 0.0f) {
-      jaref += alpha * c.jv[r];
-      c.Jaref[r] = jaref;
-    }
+  for (int r0 = tid(); r0 < c.nefc; r0 += RU * BLK) {
+  float Du[RU], jau[RU];
+#pragma unroll
+  for (int u = 0; u < RU; u++) {
+    const int r = r0 + u * BLK;
+    const bool ok = r < c.nefc;
+    Du[u] = ok ? c.D[r] : 0.0f;
+    jau[u] = ok ? c.Jaref[r] : 0.0f;
+    if (ok && alpha != 0.0f) jau[u] += alpha * c.jv[r];
+  }
+#pragma unroll
+  for (int u = 0; u < RU; u++) {
+    const int r = r0 + u * BLK;
+    if (r >= c.nefc) break;
+    const float D = Du[u];
+    const float jaref = jau[u];
+    if (alpha != 0.0f) c.Jaref[r] = jaref;
     float f;
     int st;
     if (r < c.ne) {
@@ -1934,6 +1974,7 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
     }
     c.force[r] = f;
     c.state[r] = st;
+  }
   }
   __syncthreads();
   float g = 0.0f;
@@ -1996,7 +2037,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
   };
   const float lo_alpha_in = -safe_div(p0[1], p0[2]);
   float lo_in[3] = {0, 0, 0};
-  for (int r = tid(); r < c.nefc; r += BLK) eval_row(c, r, lo_alpha_in, lo_in);
+  eval_rows<1>(c, &lo_alpha_in, lo_in);
   block_sum<3>(lo_in, sm);
   {
     float g[3];
@@ -2021,11 +2062,8 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
       const float hi_next_alpha = hi_alpha - safe_div(hi[1], hi[2]);
       const float mid_alpha = 0.5f * (lo_alpha + hi_alpha);
       float v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (int r = tid(); r < c.nefc; r += BLK) {
-        eval_row(c, r, lo_next_alpha, v9);
-        eval_row(c, r, hi_next_alpha, v9 + 3);
-        eval_row(c, r, mid_alpha, v9 + 6);
-      }
+      const float al[3] = {lo_next_alpha, hi_next_alpha, mid_alpha};
+      eval_rows<3>(c, al, v9);
       block_sum<9>(v9, sm);
       float lo_next[3], hi_next[3], mid[3], g[3];
       gauss_at(lo_next_alpha, g);
