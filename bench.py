@@ -109,13 +109,15 @@ def parse():
   p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
   p.add_argument("--cpu-worlds", type=int, default=None, help="CPU baseline sample worlds (default: the config's, 1024)")
   p.add_argument("--cpu-steps", type=int, default=None, help="CPU baseline sample steps (default: the config's, 1000)")
-  p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_humanoid_r01.json"))
+  p.add_argument("--pmc", default=None, help="PMC traffic summary (default: profiles/pmc_<model>_r01.json)")
   p.add_argument("--graph", type=int, default=0, help="replay steps through a captured hipGraph")
   a = p.parse_args()
   cfg = MODELS[a.model]
   for k in ("nworld", "nconmax", "njmax", "solver"):
     if getattr(a, k) is None:
       setattr(a, k, cfg[k])
+  if a.pmc is None:
+    a.pmc = os.path.join(ROOT, "profiles", f"pmc_{a.model}_r01.json")
   for k, dflt in (("steps", 1000), ("cpu_worlds", 1024), ("cpu_steps", 1000)):
     if getattr(a, k) is None:
       setattr(a, k, cfg.get(k, dflt))
@@ -239,7 +241,9 @@ def main():
       with open(args.pmc) as f:
         pmc = json.load(f)
       if pmc.get("solver", "CG") == solver_name and pmc.get("nworld") == args.nworld and pmc.get("model", "humanoid") == args.model:
-        traffic = pmc.get("kernels", {}).get("forward", {}).get("hbm_bytes_per_launch")
+        fk = pmc.get("kernels", {}).get("forward", {})
+        # sparse path: the timed region is forward (x2 around the convex pre-pass) + solve
+        traffic = fk.get("hbm_bytes_per_step_forward_plus_solve") if m.is_sparse else fk.get("hbm_bytes_per_launch")
     out = {
       "metric": METRIC if args.model == "humanoid" else f"env-steps/sec (whole node), {args.model} nworld={args.nworld} per GPU",
       "value": value,

@@ -33,6 +33,7 @@ namespace sp {
 
 constexpr int BLK = 256;
 constexpr int SP_LDS_CNT_MAX = 8192;  // column counters of the J transpose live in LDS up to this nv + 1
+constexpr int SP_LDS_ITEMS_MAX = 48 * 1024;  // per-item contact counts of the collision pass in LDS up to this
 
 // opt-in phase timers of this path (build with -DMJW_PROFILE; tools/sparse_prof.py): s_memtime
 // deltas summed over waves, read back with mjw_prof_read_sparse
@@ -1089,8 +1090,17 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
     return;
   }
   const int nitem = ncollide_items(m);
+  // per-item contact counts kept in LDS (forward_kernel's dynamic LDS, sized by sparse_launch), so
+  // the scan pass needs no second narrowphase evaluation; larger models recount
+  extern __shared__ unsigned char s_items[];
+  // the same bound sparse_launch sizes the LDS with (>= nitem)
+  const bool cached = (long)m.nxn + (long)m.nflexvert * m.nplane + (long)m.nflexelem * m.nflexcg <= SP_LDS_ITEMS_MAX;
   int cnt = 0, passed = 0;
-  for (int it = tid(); it < nitem; it += BLK) cnt += collide_item(m, d, wid, it, -1, &passed);
+  for (int it = tid(); it < nitem; it += BLK) {
+    const int n = collide_item(m, d, wid, it, -1, &passed);
+    cnt += n;
+    if (cached) s_items[it] = (unsigned char)n;
+  }
   float v[2] = {(float)cnt, (float)passed};
   block_sum<2>(v, sm);
   // every world keeps at most its share naconmax / nworld of the pool, in item order: the kept set
@@ -1110,7 +1120,7 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
   if (keep) {
     for (int c0 = 0; c0 < nitem && run < lim; c0 += BLK) {
       const int it = c0 + tid();
-      const int n = it < nitem ? collide_item(m, d, wid, it, -1, nullptr) : 0;
+      const int n = it < nitem ? (cached ? (int)s_items[it] : collide_item(m, d, wid, it, -1, nullptr)) : 0;
       int chunk;
       const int off = block_scan(n, chunk, sm);
       if (n && run + off < lim) collide_item(m, d, wid, it, run + off, nullptr, lim);
@@ -2326,7 +2336,12 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
     hipLaunchKernelGGL(sp::ccd_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
     fwd = (fwd & ~ST_POS) | sp::SP_POS_B;
   }
-  if (fwd) hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
+  if (fwd) {
+    // collision items (upper bound of ncollide_items): one LDS byte each when they fit
+    const long nitem = (long)m->nxn + (long)m->nflexvert * m->nplane + (long)m->nflexelem * m->nflexcg;
+    const size_t lds = ((fwd & (ST_POS | sp::SP_POS_B)) && nitem <= sp::SP_LDS_ITEMS_MAX) ? (size_t)((nitem + 3) & ~3L) : 0;
+    hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), lds, s, *m, *d, fwd);
+  }
   if (stages & ST_SOLVE) {
     const size_t lds = (m->nv + 1) <= sp::SP_LDS_CNT_MAX ? (size_t)(m->nv + 1) * 4 : 0;
     hipLaunchKernelGGL(sp::solve_kernel, dim3(nw), dim3(sp::BLK), lds, s, *m, *d);

@@ -1,6 +1,7 @@
 """Summarise rocprofv3 CSV output into profiles/: kernel-trace stats + per-kernel HBM traffic.
 
-usage: python tools/pmc_traffic.py <stats_dir> <fetch_dir> <write_dir> <out.json> [nworld] [solver]
+usage: python tools/pmc_traffic.py <stats_dir> <fetch_dir> <write_dir> <out.json> [nworld] [solver] [model]
+  model     : humanoid (default: the dense path's kernels) or a sparse-path model (cloth, aloha_cloth)
   stats_dir : rocprofv3 --kernel-trace --stats --output-format csv output directory
   fetch_dir : rocprofv3 --pmc FETCH_SIZE --output-format csv output directory
   write_dir : rocprofv3 --pmc WRITE_SIZE --output-format csv output directory
@@ -15,6 +16,7 @@ import os
 import sys
 
 KERNELS = {"forward": "mjw_kernel<79>", "dense": "dense_kernel<7, false>"}
+SPARSE_KERNELS = {"forward": "sp::forward_kernel", "solve": "sp::solve_kernel", "ccd": "sp::ccd_kernel", "euler": "sp::euler_kernel"}
 
 
 def rows(d, pattern):
@@ -38,13 +40,17 @@ def counter_avg(d, counter):
 
 
 def main():
+  global KERNELS
   stats_dir, fetch_dir, write_dir, out = sys.argv[1:5]
   nworld = int(sys.argv[5]) if len(sys.argv) > 5 else 8192
   solver = sys.argv[6] if len(sys.argv) > 6 else "CG"
+  model = sys.argv[7] if len(sys.argv) > 7 else "humanoid"
+  if model != "humanoid" and model in ("cloth", "aloha_cloth"):
+    KERNELS = SPARSE_KERNELS
   fetch = counter_avg(fetch_dir, "FETCH_SIZE")
   write = counter_avg(write_dir, "WRITE_SIZE")
   stats = rows(stats_dir, "*kernel_stats.csv")
-  res = {"nworld": nworld, "solver": solver, "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024",
+  res = {"nworld": nworld, "solver": solver, "model": model, "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024",
          "kernels": {}}
   for k, pat in KERNELS.items():
     f, nf = fetch[k]
@@ -56,6 +62,13 @@ def main():
       "hbm_bytes_per_launch": (2 * f + w) * 1024 if f is not None and w is not None else None,
       "avg_ns_rocprof": float(st[0]["AverageNs"]) if st else None,
     }
+  if KERNELS is SPARSE_KERNELS:
+    # per step: forward twice when the convex pre-pass splits the position stage, solve once
+    k = res["kernels"]
+    nfwd = 2 if k["ccd"]["dispatches"][0] else 1
+    parts = [k["forward"]["hbm_bytes_per_launch"], k["solve"]["hbm_bytes_per_launch"]]
+    if None not in parts:
+      k["forward"]["hbm_bytes_per_step_forward_plus_solve"] = nfwd * parts[0] + parts[1]
   with open(out, "w") as fh:
     json.dump(res, fh, indent=1)
   print(json.dumps(res, indent=1))
