@@ -1926,7 +1926,7 @@ __device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, 
 constexpr int RU = 4;
 template <int NA>
 __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas, float* o) {
-  for (int r0 = tid(); r0 < c.nefc; r0 += RU * BLK) {
+  for (int r0 = c.ne + tid(); r0 < c.nefc; r0 += RU * BLK) {  // equality rows: folded into the quadratic
     float D[RU], ja[RU], jv[RU];
 #pragma unroll
     for (int u = 0; u < RU; u++) {
@@ -1990,7 +1990,19 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   float g = 0.0f;
   for (int i = tid(); i < c.nv; i += BLK) {
     float s = 0.0f;
-    for (int p = c.JT_adr[i]; p < c.JT_adr[i + 1]; p++) s += c.JT_val[p] * c.force[c.JT_ind[p]];
+    // 4 entries in flight (index loads, then the dependent force gathers), same summation order
+    const int pa = c.JT_adr[i], pb = c.JT_adr[i + 1];
+    int p = pa;
+    for (; p + 4 <= pb; p += 4) {
+      const int r0 = c.JT_ind[p], r1 = c.JT_ind[p + 1], r2 = c.JT_ind[p + 2], r3 = c.JT_ind[p + 3];
+      const float v0 = c.JT_val[p], v1 = c.JT_val[p + 1], v2 = c.JT_val[p + 2], v3 = c.JT_val[p + 3];
+      const float f0 = c.force[r0], f1 = c.force[r1], f2 = c.force[r2], f3 = c.force[r3];
+      s += v0 * f0;
+      s += v1 * f1;
+      s += v2 * f2;
+      s += v3 * f3;
+    }
+    for (; p < pb; p++) s += c.JT_val[p] * c.force[c.JT_ind[p]];
     c.qfrc_c[i] = s;
     g += (c.Ma[i] - c.qfrc_s[i]) * (c.qacc[i] - c.qacc_s[i]);
   }
@@ -2022,12 +2034,48 @@ __device__ __forceinline__ bool in_bracket(const float* x, const float* y) {
 __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm) {
   mul_m_trees(m, c.M, c.search, c.mv);
   // jv = J search, fused with the alpha = 0 evaluation of each row (same thread)
-  float v5[5] = {0, 0, 0, 0, 0};
-  for (int r = tid(); r < c.nefc; r += BLK) {
-    float s = 0.0f;
-    for (int k = 0; k < c.Jnnz[r]; k++) s += c.J[(long)k * c.P + r] * c.search[c.Jcol[(long)k * c.P + r]];
+  // equality rows are quadratic for every step size: their cost 0.5 D (Jaref + a jv)^2 is folded
+  // into the Gauss quadratic once here (v5[5..7]), and the line-search passes skip them
+  float v5[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r0 = tid(); r0 < c.nefc; r0 += RU * BLK) {
+    // RU rows interleaved so their (column -> search) gathers overlap; per-row order unchanged
+    int nz[RU], kmax = 0;
+    float acc[RU];
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+      const int r = r0 + u * BLK;
+      nz[u] = r < c.nefc ? c.Jnnz[r] : 0;
+      kmax = max(kmax, nz[u]);
+      acc[u] = 0.0f;
+    }
+    for (int k = 0; k < kmax; k++) {
+      float v[RU];
+      int col[RU];
+#pragma unroll
+      for (int u = 0; u < RU; u++) {
+        const long q = (long)k * c.P + r0 + u * BLK;
+        v[u] = k < nz[u] ? c.J[q] : 0.0f;
+        col[u] = k < nz[u] ? c.Jcol[q] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < RU; u++)
+        if (k < nz[u]) acc[u] += v[u] * c.search[col[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+    const int r = r0 + u * BLK;
+    if (r >= c.nefc) break;
+    const float s = acc[u];
     c.jv[r] = s;
-    eval_row(c, r, 0.0f, v5);
+    if (r < c.ne) {
+      const float D = c.D[r], ja = c.Jaref[r];
+      v5[5] += 0.5f * D * ja * ja;
+      v5[6] += D * ja * s;
+      v5[7] += 0.5f * D * s * s;
+    } else {
+      eval_row(c, r, 0.0f, v5);
+    }
+    }
   }
   __syncthreads();
   const float snorm = sqrtf(c.search_dot);
@@ -2037,8 +2085,8 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
     v5[3] += c.search[i] * (c.Ma[i] - c.qfrc_s[i]);
     v5[4] += 0.5f * c.search[i] * c.mv[i];
   }
-  block_sum<5>(v5, sm);
-  const float qg0 = c.gauss, qg1 = v5[3], qg2 = v5[4];
+  block_sum<8>(v5, sm);
+  const float qg0 = c.gauss + v5[5], qg1 = v5[3] + v5[6], qg2 = v5[4] + v5[7];
   const float p0[3] = {qg0 + v5[0], qg1 + v5[1], 2.0f * qg2 + v5[2]};
   auto gauss_at = [&](float a, float* o) {
     o[0] = a * a * qg2 + a * qg1 + qg0;
