@@ -491,10 +491,58 @@ __device__ void factor_trees(const mjw_model_t& m, const float* M, float* LD, co
   }
 }
 
+// chain trees of at most 4 dofs (each dof's parent is the previous one: a flex vertex's slide x/y/z)
+// run in registers with every load issued up front; row k of such a tree holds columns a..a+k
+constexpr int CHAIN = 4;
+__device__ __forceinline__ bool chain_tree(const mjw_model_t& m, int a, int e) {
+  if (e - a > CHAIN) return false;
+  for (int k = a + 1; k < e; k++)
+    if (m.dof_parentid[k] != k - 1) return false;
+  return true;
+}
+
+// the tree's lower triangle (L[k][p], p <= k, diagonal at p = k) and x into registers
+__device__ __forceinline__ void chain_load(const mjw_model_t& m, const float* A, const float* x, int a, int n, float (&L)[CHAIN][CHAIN],
+                                           float (&xs)[CHAIN]) {
+#pragma unroll
+  for (int k = 0; k < CHAIN; k++) {
+    xs[k] = k < n ? x[a + k] : 0.0f;
+    const int adr = k < n ? m.M_rowadr[a + k] : 0;
+#pragma unroll
+    for (int p = 0; p <= k; p++) L[k][p] = k < n ? A[adr + p] : 0.0f;
+  }
+}
+
 // x = (L' D L)^-1 x in place, per tree (smooth.py:2813-2846)
 __device__ void solve_trees(const mjw_model_t& m, const float* LD, float* x) {
   for (int t = tid(); t < m.ntree; t += BLK) {
     const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
+    if (chain_tree(m, a, e)) {
+      const int n = e - a;
+      float L[CHAIN][CHAIN], xs[CHAIN];
+      chain_load(m, LD, x, a, n, L, xs);
+#pragma unroll
+      for (int k = CHAIN - 1; k >= 0; k--)
+        if (k < n) {
+#pragma unroll
+          for (int p = 0; p < k; p++) xs[p] -= L[k][p] * xs[k];
+        }
+#pragma unroll
+      for (int k = 0; k < CHAIN; k++)
+        if (k < n) xs[k] /= L[k][k];
+#pragma unroll
+      for (int k = 0; k < CHAIN; k++)
+        if (k < n) {
+          float sk = xs[k];
+#pragma unroll
+          for (int p = 0; p < k; p++) sk -= L[k][p] * xs[p];
+          xs[k] = sk;
+        }
+#pragma unroll
+      for (int k = 0; k < CHAIN; k++)
+        if (k < n) x[a + k] = xs[k];
+      continue;
+    }
     for (int k = e - 1; k >= a; k--) {
       const int adr = m.M_rowadr[k], nnz = m.M_rownnz[k];
       const float xk = x[k];
@@ -514,6 +562,23 @@ __device__ void solve_trees(const mjw_model_t& m, const float* LD, float* x) {
 __device__ void mul_m_trees(const mjw_model_t& m, const float* M, const float* x, float* y) {
   for (int t = tid(); t < m.ntree; t += BLK) {
     const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
+    if (chain_tree(m, a, e)) {
+      const int n = e - a;
+      float L[CHAIN][CHAIN], xs[CHAIN];
+      chain_load(m, M, x, a, n, L, xs);
+#pragma unroll
+      for (int k = 0; k < CHAIN; k++)
+        if (k < n) {
+          float sk = L[k][k] * xs[k];
+#pragma unroll
+          for (int p = 0; p < k; p++) sk += L[k][p] * xs[p];
+#pragma unroll
+          for (int j = k + 1; j < CHAIN; j++)
+            if (j < n) sk += L[j][k] * xs[j];
+          y[a + k] = sk;
+        }
+      continue;
+    }
     for (int k = a; k < e; k++) y[k] = 0.0f;
     for (int k = a; k < e; k++) {
       const int adr = m.M_rowadr[k], nnz = m.M_rownnz[k];
