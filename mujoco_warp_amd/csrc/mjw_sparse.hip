@@ -653,7 +653,7 @@ __device__ float sphere_triangle(float* pos, float* nrm, const float* sp, float 
 }
 
 // triangle vs sphere/capsule/box/cylinder: up to 2 candidates (collision_primitive_core.py:1600-1990)
-__device__ int geom_triangle(Cand* c, int gt, const float* gp, const float* gr, const float* gs, const float* const* t, float tr) {
+__device__ __noinline__ int geom_triangle(Cand* c, int gt, const float* gp, const float* gr, const float* gs, const float* const* t, float tr) {
   int n = 0;
   const float ax[3] = {gr[2], gr[5], gr[8]};
   if (gt == GEOM_SPHERE) {
@@ -830,7 +830,7 @@ __device__ void plane_cylinder_k(int k, const float* n, const float* pp, const f
 // vertex a): the deepest vertex a, then among vertices within 1e-3 of its depth the one farthest from
 // a (b), farthest from line ab (c) and from the triangle's other edges (d); each distinct vertex is a
 // contact at its own depth.  One thread, serial over the vertices (rare: plane-near meshes only).
-__device__ int plane_mesh(const float* nw, const float* ppos, const float* gpos, const float* R, const float* mv, int nvert, float* dist,
+__device__ __noinline__ int plane_mesh(const float* nw, const float* ppos, const float* gpos, const float* R, const float* mv, int nvert, float* dist,
                           float (*pos)[3]) {
   constexpr float HUGE_ = 1e6f;
   const float d0[3] = {ppos[0] - gpos[0], ppos[1] - gpos[1], ppos[2] - gpos[2]};
@@ -962,9 +962,28 @@ __device__ void write_contact(const mjw_model_t& m, const mjw_data_t& d, int wid
   d.contact_geomcollisionid[slot] = 0;
 }
 
+// out-of-line copies of the (force-inlined, shared with the dense kernel) primitive narrowphase:
+// collide_item runs three ways per step, and inlining every pair type into it spilled to scratch
+__device__ __noinline__ void nl_capsule_capsule(Con2& c, const float* p1, const float* n1, float r1, float h1, const float* p2,
+                                                const float* n2, float r2, float h2, float margin) {
+  capsule_capsule(c, p1, n1, r1, h1, p2, n2, r2, h2, margin);
+}
+__device__ __noinline__ void nl_capsule_box(Con2& c, const float* p1, const float* n1, float r1, float h1, const float* p2,
+                                            const float* r2, const float* s2) {
+  capsule_box(c, p1, n1, r1, h1, p2, r2, s2);
+}
+__device__ __noinline__ void nl_plane_capsule(Con2& c, const float* n1, const float* p1, const float* p2, const float* n2, float r,
+                                              float h) {
+  plane_capsule(c, n1, p1, p2, n2, r, h);
+}
+__device__ __noinline__ float nl_sphere_box(float* pos, float* nrm, const float* p1, float r, const float* p2, const float* r2,
+                                            const float* s2) {
+  return sphere_box(pos, nrm, p1, r, p2, r2, s2);
+}
+
 // one collision item: a geom pair, a (flex element, collidable geom) pair or a (flex vertex, plane)
 // pair.  Returns the number of contacts; writes them from pool slot `base` when base >= 0.
-__device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed, int lim = 0x7fffffff) {
+__device__ __noinline__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed, int lim = 0x7fffffff) {
   const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
   const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;
   const float* geom_size = MR(geom_size);
@@ -1015,7 +1034,7 @@ __device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, 
       make_frame(c.frame[0], n1);
       c.n = 1;
     } else if (t1 == GEOM_PLANE && t2 == GEOM_CAPSULE) {
-      plane_capsule(c, n1, p1, p2, n2, s2[0], s2[1]);
+      nl_plane_capsule(c, n1, p1, p2, n2, s2[0], s2[1]);
     } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
       float nrm[3];
       c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], p2, s2[0]);
@@ -1029,14 +1048,14 @@ __device__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, 
       make_frame(c.frame[0], nrm);
       c.n = 1;
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
-      capsule_capsule(c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], o.margin);
+      nl_capsule_capsule(c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], o.margin);
     } else if (t1 == GEOM_SPHERE && t2 == GEOM_BOX) {
       float nrm[3];
-      c.dist[0] = sphere_box(c.pos[0], nrm, p1, s1[0], p2, r2, s2);
+      c.dist[0] = nl_sphere_box(c.pos[0], nrm, p1, s1[0], p2, r2, s2);
       make_frame(c.frame[0], nrm);
       c.n = 1;
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {
-      capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
+      nl_capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
     }
     const int nk = ncand == 2 ? c.n : ncand;
     for (int k = 0; k < nk; k++) {
@@ -1850,14 +1869,18 @@ __device__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, int 
   __syncthreads();
 }
 
-// the position stage in two halves around the convex pre-pass (models with CCD pairs)
-enum : int { SP_POS_A = 1 << 8, SP_POS_B = 1 << 9 };
+// The forward stages as separate kernels (one instantiation per group): every stage already keeps
+// its state in HBM, so splitting costs a launch, while one fused kernel took the register maximum of
+// all stages (248 VGPRs, 3.4 KB scratch per lane, 2 waves / SIMD).  POS_A: frames to qM; COLL:
+// collision; CON: constraint rows + transmission; the convex pre-pass runs between POS_A and COLL.
+enum : int { SP_POS_A = 1 << 8, SP_POS_B = 1 << 9, SP_COLL = 1 << 10, SP_CON = 1 << 11 };
 
+template <int S>
 __global__ void __launch_bounds__(BLK) forward_kernel(const mjw_model_t m, const mjw_data_t d, int stages) {
   __shared__ Smem sm;
   const int wid = blockIdx.x;
   SPROF_T0();
-  if (stages & (ST_POS | SP_POS_A)) {
+  if constexpr ((S & SP_POS_A) != 0) {
     kinematics(m, d, wid);
     com_pos(m, d, wid);
     camlight(m, d, wid);
@@ -1867,19 +1890,23 @@ __global__ void __launch_bounds__(BLK) forward_kernel(const mjw_model_t m, const
     crb_qM(m, d, wid);
     SPROF_MARK(SPH_CRB);
   }
-  if (stages & (ST_POS | SP_POS_B)) {
+  if constexpr ((S & SP_COLL) != 0) {
     collision(m, d, wid, sm);
     SPROF_MARK(SPH_COLL);
+  }
+  if constexpr ((S & SP_CON) != 0) {
     make_constraint(m, d, wid, sm);
     transmission(m, d, wid, sm);
     SPROF_MARK(SPH_CON);
   }
-  if (stages & ST_VEL) fwd_velocity(m, d, wid);
-  SPROF_MARK(SPH_VEL);
-  if (stages & ST_ACT) fwd_actuation(m, d, wid);
-  SPROF_MARK(SPH_ACT);
-  if (stages & ST_ACC) fwd_acceleration(m, d, wid);
-  SPROF_MARK(SPH_ACC);
+  if constexpr ((S & ST_VEL) != 0) {
+    if (stages & ST_VEL) fwd_velocity(m, d, wid);
+    SPROF_MARK(SPH_VEL);
+    if (stages & ST_ACT) fwd_actuation(m, d, wid);
+    SPROF_MARK(SPH_ACT);
+    if (stages & ST_ACC) fwd_acceleration(m, d, wid);
+    SPROF_MARK(SPH_ACC);
+  }
 }
 
 // convex pre-pass (collision_convex.py:701-890): one wave per world applies the broadphase to the
@@ -2440,21 +2467,23 @@ extern "C" int mjw_prof_read_sparse(unsigned long long* out, int reset) {
 int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
   const int nw = d->nworld;
   if (nw <= 0) return 0;
-  int fwd = stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC);
+  const int fwd = stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC);
   const bool ccd = (stages & ST_POS) && m->nxn_ccd > 0 && d->naconmax > 0 && !(m->opt_disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT));
-  if (ccd) {
-    // frames first, then the convex pre-pass, then collision onward
-    hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, (int)sp::SP_POS_A);
-    const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations).total + 64) * 4;
-    hipLaunchKernelGGL(sp::ccd_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
-    fwd = (fwd & ~ST_POS) | sp::SP_POS_B;
-  }
-  if (fwd) {
+  if (fwd & ST_POS) {
+    // frames, [the convex pre-pass,] collision, constraint rows
+    hipLaunchKernelGGL(sp::forward_kernel<sp::SP_POS_A>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
+    if (ccd) {
+      const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations).total + 64) * 4;
+      hipLaunchKernelGGL(sp::ccd_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
+    }
     // collision items (upper bound of ncollide_items): one LDS byte each when they fit
     const long nitem = (long)m->nxn + (long)m->nflexvert * m->nplane + (long)m->nflexelem * m->nflexcg;
-    const size_t lds = ((fwd & (ST_POS | sp::SP_POS_B)) && nitem <= sp::SP_LDS_ITEMS_MAX) ? (size_t)((nitem + 3) & ~3L) : 0;
-    hipLaunchKernelGGL(sp::forward_kernel, dim3(nw), dim3(sp::BLK), lds, s, *m, *d, fwd);
+    const size_t lds = nitem <= sp::SP_LDS_ITEMS_MAX ? (size_t)((nitem + 3) & ~3L) : 0;
+    hipLaunchKernelGGL(sp::forward_kernel<sp::SP_COLL>, dim3(nw), dim3(sp::BLK), lds, s, *m, *d, fwd);
+    hipLaunchKernelGGL(sp::forward_kernel<sp::SP_CON>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
   }
+  if (fwd & (ST_VEL | ST_ACT | ST_ACC))
+    hipLaunchKernelGGL(sp::forward_kernel<ST_VEL>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
   if (stages & ST_SOLVE) {
     const size_t lds = (m->nv + 1) <= sp::SP_LDS_CNT_MAX ? (size_t)(m->nv + 1) * 4 : 0;
     hipLaunchKernelGGL(sp::solve_kernel, dim3(nw), dim3(sp::BLK), lds, s, *m, *d);
