@@ -54,10 +54,13 @@ static __device__ unsigned long long g_sprof[SPH_N];
 constexpr int NWAVE = BLK / 64;
 enum : int { EQ_FLEX = 4 };
 
+constexpr int SP_FBOX = 4;  // flexes whose bounding box the collision pass keeps (culls triangle-geom items)
+
 struct Smem {
   float red[NWAVE][16];
   int iscan[NWAVE];
   int ival[8];
+  float fbox[SP_FBOX][6];  // per flex: min xyz, max xyz of its vertices
 };
 
 __device__ __forceinline__ int tid() { return (int)threadIdx.x; }
@@ -983,7 +986,8 @@ __device__ __noinline__ float nl_sphere_box(float* pos, float* nrm, const float*
 
 // one collision item: a geom pair, a (flex element, collidable geom) pair or a (flex vertex, plane)
 // pair.  Returns the number of contacts; writes them from pool slot `base` when base >= 0.
-__device__ __noinline__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed, int lim = 0x7fffffff) {
+__device__ __noinline__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed, int lim = 0x7fffffff,
+                                        const float* fbox = nullptr) {
   const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
   const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;
   const float* geom_size = MR(geom_size);
@@ -1086,6 +1090,16 @@ __device__ __noinline__ int collide_item(const mjw_model_t& m, const mjw_data_t&
       continue;
     }
     const int el = item / ncg, g = m.flex_cgeom[m.flex_cgeomadr[f] + item % ncg];
+    if (fbox && f < SP_FBOX) {
+      // flex-level cull (exact: every candidate lies within the flex's vertex box grown by the
+      // radius, the margin and the geom's bounding sphere)
+      const float* b = fbox + 6 * f;
+      const float grow = MR(geom_rbound)[g] + MR(flex_radius)[f] + fmaxf(MR(geom_margin)[g] + MR(flex_margin)[f], 0.0f) + 1e-5f;
+      const float* gp = gx + 3 * g;
+      if (gp[0] < b[0] - grow || gp[1] < b[1] - grow || gp[2] < b[2] - grow || gp[0] > b[3] + grow || gp[1] > b[4] + grow ||
+          gp[2] > b[5] + grow)
+        return 0;
+    }
     const int* ev = m.flex_elem + m.flex_elemdataadr[f] + 3 * el;
     const float* t[3];
     float cen[3] = {0.0f, 0.0f, 0.0f}, rad = 0.0f;
@@ -1177,11 +1191,40 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
   // per-item contact counts kept in LDS (forward_kernel's dynamic LDS, sized by sparse_launch), so
   // the scan pass needs no second narrowphase evaluation; larger models recount
   extern __shared__ unsigned char s_items[];
+  // vertex bounding box of each (of the first SP_FBOX) flex: block min-reduction of (min, -max)
+  const float* fbox = nullptr;
+  if (m.nflex > 0) {
+    const float* fx = d.flexvert_xpos + (long)wid * m.nflexvert * 3;
+    for (int f = 0; f < min(m.nflex, SP_FBOX); f++) {
+      float v[6] = {MJW_MAXVAL, MJW_MAXVAL, MJW_MAXVAL, MJW_MAXVAL, MJW_MAXVAL, MJW_MAXVAL};
+      const int v0 = m.flex_vertadr[f], v1 = f + 1 < m.nflex ? m.flex_vertadr[f + 1] : m.nflexvert;
+      for (int i = v0 + tid(); i < v1; i += BLK)
+        for (int k = 0; k < 3; k++) {
+          v[k] = fminf(v[k], fx[3 * i + k]);
+          v[3 + k] = fminf(v[3 + k], -fx[3 * i + k]);
+        }
+      const int lane = tid() & 63, wv = tid() >> 6;
+#pragma unroll
+      for (int k = 0; k < 6; k++)
+        for (int o = 32; o > 0; o >>= 1) v[k] = fminf(v[k], __shfl_xor(v[k], o, 64));
+      __syncthreads();
+      if (lane == 0)
+        for (int k = 0; k < 6; k++) sm.red[wv][k] = v[k];
+      __syncthreads();
+      if (tid() < 6) {
+        float r = sm.red[0][tid()];
+        for (int w = 1; w < NWAVE; w++) r = fminf(r, sm.red[w][tid()]);
+        sm.fbox[f][tid()] = tid() < 3 ? r : -r;
+      }
+      __syncthreads();
+    }
+    fbox = &sm.fbox[0][0];
+  }
   // the same bound sparse_launch sizes the LDS with (>= nitem)
   const bool cached = (long)m.nxn + (long)m.nflexvert * m.nplane + (long)m.nflexelem * m.nflexcg <= SP_LDS_ITEMS_MAX;
   int cnt = 0, passed = 0;
   for (int it = tid(); it < nitem; it += BLK) {
-    const int n = collide_item(m, d, wid, it, -1, &passed);
+    const int n = collide_item(m, d, wid, it, -1, &passed, 0x7fffffff, fbox);
     cnt += n;
     if (cached) s_items[it] = (unsigned char)n;
   }
@@ -1204,10 +1247,10 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
   if (keep) {
     for (int c0 = 0; c0 < nitem && run < lim; c0 += BLK) {
       const int it = c0 + tid();
-      const int n = it < nitem ? (cached ? (int)s_items[it] : collide_item(m, d, wid, it, -1, nullptr)) : 0;
+      const int n = it < nitem ? (cached ? (int)s_items[it] : collide_item(m, d, wid, it, -1, nullptr, 0x7fffffff, fbox)) : 0;
       int chunk;
       const int off = block_scan(n, chunk, sm);
-      if (n && run + off < lim) collide_item(m, d, wid, it, run + off, nullptr, lim);
+      if (n && run + off < lim) collide_item(m, d, wid, it, run + off, nullptr, lim, fbox);
       run += chunk;
     }
   }
@@ -1876,7 +1919,7 @@ __device__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, int 
 enum : int { SP_POS_A = 1 << 8, SP_POS_B = 1 << 9, SP_COLL = 1 << 10, SP_CON = 1 << 11 };
 
 template <int S>
-__global__ void __launch_bounds__(BLK) forward_kernel(const mjw_model_t m, const mjw_data_t d, int stages) {
+__global__ void __launch_bounds__(BLK, 4) forward_kernel(const mjw_model_t m, const mjw_data_t d, int stages) {
   __shared__ Smem sm;
   const int wid = blockIdx.x;
   SPROF_T0();
