@@ -656,7 +656,7 @@ __device__ float sphere_triangle(float* pos, float* nrm, const float* sp, float 
 }
 
 // triangle vs sphere/capsule/box/cylinder: up to 2 candidates (collision_primitive_core.py:1600-1990)
-__device__ __noinline__ int geom_triangle(Cand* c, int gt, const float* gp, const float* gr, const float* gs, const float* const* t, float tr) {
+__device__ __forceinline__ int geom_triangle(Cand* c, int gt, const float* gp, const float* gr, const float* gs, const float* const* t, float tr) {
   int n = 0;
   const float ax[3] = {gr[2], gr[5], gr[8]};
   if (gt == GEOM_SPHERE) {
@@ -986,7 +986,7 @@ __device__ __noinline__ float nl_sphere_box(float* pos, float* nrm, const float*
 
 // one collision item: a geom pair, a (flex element, collidable geom) pair or a (flex vertex, plane)
 // pair.  Returns the number of contacts; writes them from pool slot `base` when base >= 0.
-__device__ __noinline__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed, int lim = 0x7fffffff,
+__device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed, int lim = 0x7fffffff,
                                         const float* fbox = nullptr) {
   const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
   const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;

@@ -63,9 +63,9 @@ def main():
       "avg_ns_rocprof": float(st[0]["AverageNs"]) if st else None,
     }
   if KERNELS is SPARSE_KERNELS:
-    # per step: forward twice when the convex pre-pass splits the position stage, solve once
+    # per step: every forward-stage launch (frames / collision / rows / velocity) and one solve
     k = res["kernels"]
-    nfwd = 2 if k["ccd"]["dispatches"][0] else 1
+    nfwd = k["forward"]["dispatches"][0] / max(1, k["solve"]["dispatches"][0])
     parts = [k["forward"]["hbm_bytes_per_launch"], k["solve"]["hbm_bytes_per_launch"]]
     if None not in parts:
       k["forward"]["hbm_bytes_per_step_forward_plus_solve"] = nfwd * parts[0] + parts[1]
