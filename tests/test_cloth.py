@@ -222,3 +222,34 @@ def test_gpu_cloth_rollout_parity_and_determinism(which):
   assert np.isfinite(q).all()
   assert (q == q[:1]).all()
   assert int(d2.nacon) <= rep * NCONMAX
+
+
+@pytest.mark.gpu
+def test_gpu_aloha_sharding_is_bitwise_invariant():
+  """SURVEY §8(e) on the sparse path: two shards (world_offset 0 / 8) of a 16-world aloha_cloth
+  rollout with the benchmark's control noise equal the single 16-world run bitwise -- worlds never
+  read each other, and each keeps its own share of the contact pool."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  mjm = aloha_model()
+  nworld, half = 16, 8
+  qpos, qvel, ctrl = aloha_states(mjm, nworld, seed=6)
+  center = torch.as_tensor(np.asarray(ctrl[0], dtype=np.float32), device="cuda")
+
+  def run(lo, hi):
+    m, d = gpu_from_state(mjm, qpos[lo:hi], qvel[lo:hi], ctrl[lo:hi], njmax=ALOHA_NJMAX, nconmax=ALOHA_NCONMAX)
+    d.world_offset = lo
+    for i in range(10):
+      mjw.ctrl_noise(m, d, i, center=center)
+      mjw.step(m, d)
+    torch.cuda.synchronize()
+    return d.qpos.cpu().numpy(), d.qvel.cpu().numpy()
+
+  q_all, v_all = run(0, nworld)
+  q0, v0 = run(0, half)
+  q1, v1 = run(half, nworld)
+  np.testing.assert_array_equal(np.concatenate([q0, q1]), q_all)
+  np.testing.assert_array_equal(np.concatenate([v0, v1]), v_all)
+  assert np.isfinite(q_all).all()
