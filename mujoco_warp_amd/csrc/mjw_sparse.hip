@@ -32,6 +32,7 @@ namespace sp {
 #define MR_W(name) (MR(name)[0])
 
 constexpr int BLK = 256;
+constexpr int SORTN = 32;  // J-transpose segments up to this length are sorted in registers
 constexpr int SP_LDS_CNT_MAX = 8192;  // column counters of the J transpose live in LDS up to this nv + 1
 constexpr int SP_LDS_ITEMS_MAX = 48 * 1024;  // per-item contact counts of the collision pass in LDS up to this
 
@@ -2293,6 +2294,10 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
   return alpha;
 }
 
+// PART 0: qacc from the warmstart, Jaref, and the transposed index of J; PART 1: the CG iterations.
+// Two launches so that the index build (register-resident segment sorts) and the solver loop each
+// get their own register budget.
+template <int PART>
 __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const mjw_data_t d) {
   __shared__ Smem sm;
   const int wid = blockIdx.x;
@@ -2300,6 +2305,7 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   float* qacc = d.qacc + (long)wid * nv;
   const float* qacc_s = d.qacc_smooth + (long)wid * nv;
   if (njmax == 0 || nv == 0) {
+    if (PART == 0) return;
     for (int i = tid(); i < nv; i += BLK) qacc[i] = qacc_s[i];
     if (tid() == 0) d.solver_niter[wid] = 0;
     return;
@@ -2348,6 +2354,7 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   c.LD = d.qLD + (long)wid * m.nM;
   const float* warm = d.qacc_warmstart + (long)wid * nv;
   const bool ws = !(m.opt_disableflags & DSBL_WARMSTART);
+  if constexpr (PART == 0) {
   // transposed index of J: counts, scan, fill, per-column sort (deterministic J'f)
   for (int i = tid(); i <= nv; i += BLK) cnt[i] = 0;
   for (int i = tid(); i < nv; i += BLK) qacc[i] = ws ? warm[i] : qacc_s[i];
@@ -2383,6 +2390,37 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   __syncthreads();
   for (int i = tid(); i < nv; i += BLK) {
     const int a = JT_adr[i], b = JT_adr[i + 1];
+    if (b - a <= SORTN) {
+      // short segment: loaded at once, odd-even transposition network in registers
+      const int n = b - a;
+      int key[SORTN];
+      float val[SORTN];
+#pragma unroll
+      for (int j = 0; j < SORTN; j++) {
+        key[j] = j < n ? JT_ind[a + j] : 0x7fffffff;
+        val[j] = j < n ? JT_val[a + j] : 0.0f;
+      }
+#pragma unroll
+      for (int r = 0; r < SORTN; r++) {
+#pragma unroll
+        for (int j = r & 1; j + 1 < SORTN; j += 2) {
+          const bool sw = key[j] > key[j + 1];
+          const int k0 = key[j], k1 = key[j + 1];
+          const float v0 = val[j], v1 = val[j + 1];
+          key[j] = sw ? k1 : k0;
+          key[j + 1] = sw ? k0 : k1;
+          val[j] = sw ? v1 : v0;
+          val[j + 1] = sw ? v0 : v1;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < SORTN; j++)
+        if (j < n) {
+          JT_ind[a + j] = key[j] / m.njrow;  // code -> row
+          JT_val[a + j] = val[j];
+        }
+      continue;
+    }
     for (int p = a + 1; p < b; p++) {
       const int key = JT_ind[p];
       const float kv = JT_val[p];
@@ -2393,7 +2431,8 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
     }
     for (int p = a; p < b; p++) JT_ind[p] /= m.njrow;  // code -> row
   }
-  __syncthreads();
+  return;
+  }
   mul_m_trees(m, c.M, qacc, c.Ma);
   __syncthreads();
   c.cost = MJW_MAXVAL;
@@ -2529,7 +2568,8 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
     hipLaunchKernelGGL(sp::forward_kernel<ST_VEL>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
   if (stages & ST_SOLVE) {
     const size_t lds = (m->nv + 1) <= sp::SP_LDS_CNT_MAX ? (size_t)(m->nv + 1) * 4 : 0;
-    hipLaunchKernelGGL(sp::solve_kernel, dim3(nw), dim3(sp::BLK), lds, s, *m, *d);
+    hipLaunchKernelGGL(sp::solve_kernel<0>, dim3(nw), dim3(sp::BLK), lds, s, *m, *d);
+    hipLaunchKernelGGL(sp::solve_kernel<1>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
   }
   if (stages & ST_EULER) hipLaunchKernelGGL(sp::euler_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
   return (int)hipGetLastError();
