@@ -224,6 +224,12 @@ int mjw_rk4_op(const mjw_model_t* m, const mjw_data_t* d, int op, float scale, v
  * which = 0: in = n x 64 floats, out[w] = sum of chunk w, out[n + 64w + l] = in[64w + l] + in[64w + (l^32)];
  * which = 1: in = n row-major 32x32 SPD matrices, out = their inverses (Cholesky + MFMA X^T X). */
 int mjw_selftest(int which, const float* in, float* out, int n, void* stream);
+/* Device replay of the reference's collision known-answer tests (csrc/mjw_kat.hip, tests/test_gpu_golden.py):
+ * which = 0: ccd() as collision_gjk_test.py:34-265 `_geom_dist` calls it (+ box multi-contact), one record of
+ *            48 floats per case in `in`, aux = {max ccd_iterations, mesh vertices...}, 8 floats out per case;
+ * which = 1: sphere / capsule / box / cylinder vs triangle (collision_primitive_core_test.py), 32 floats in,
+ *            16 out per case, aux unused. */
+int mjw_kat(int which, const float* in, const float* aux, float* out, int n, void* stream);
 
 int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* center, int step, float std, float rate,
                    void* stream);

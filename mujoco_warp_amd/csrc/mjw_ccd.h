@@ -938,9 +938,67 @@ __device__ __forceinline__ CGeom get_cgeom(const float* src, const float* mesh_v
   return g;
 }
 
-// The pair's geoms are read from the workspace (put_cgeom at L.geoms); the outputs are written to
-// L.out: [0] dist, [1..3] normal, [4..15] points.  Only scalars and the LDS base cross the call, so
-// the (non-inlined) CCD code does not touch the caller's register budget.
+// collision_gjk.py:2200-2345 ccd: distance (or depth) of one convex pair and its first witness points.
+// Returns the reference's ncon (1, or 0 when EPA fails); *idx = EPA face for box multi-contact or -1.
+// g1 / g2 carry their margins on entry and leave with the sizes / margins the final GJK / EPA used
+// (what multicontact_box needs); the polytope stays in the workspace.
+__device__ __forceinline__ int ccd_raw(const CcdWS& w, int epa_it, float tolerance, int gjk_it, float cutoff, CGeom& g1, CGeom& g2, float* dist,
+                                       float* x1, float* x2, int* idx) {
+  *idx = -1;
+  // collision_gjk.py:91-94 _discrete_geoms: boxes and meshes (polytopes)
+  const int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH) && (g2.type == GEOM_BOX || g2.type == GEOM_MESH) &&
+                       g1.margin == 0.0f && g2.margin == 0.0f;
+  float full1 = 0.0f, full2 = 0.0f, size1 = 0.0f, size2 = 0.0f;
+  if (g1.type == GEOM_SPHERE || g1.type == GEOM_CAPSULE) { size1 = g1.size[0]; full1 = size1 + 0.5f * g1.margin; g1.margin = 0.0f; g1.size[0] = 0.0f; }
+  if (g2.type == GEOM_SPHERE || g2.type == GEOM_CAPSULE) { size2 = g2.size[0]; full2 = size2 + 0.5f * g2.margin; g2.margin = 0.0f; g2.size[0] = 0.0f; }
+  GjkOut r;
+  if (size1 + size2 > 0.0f) {
+    cutoff += full1 + full2;
+    r = gjk(w, tolerance, gjk_it, g1, g2, cutoff, discrete);
+    if (r.dist > tolerance) {  // shallow: inflate (collision_gjk.py:194-213)
+      if (r.dist == CCD_FLOAT_MAX) { *dist = r.dist; st3(x1, r.x1); st3(x2, r.x2); return 1; }
+      float n[3] = {r.x2[0] - r.x1[0], r.x2[1] - r.x1[1], r.x2[2] - r.x1[2]};
+      normalize3(n);
+      for (int i = 0; i < 3; i++) { x1[i] = r.x1[i] + (full1 > 0.0f ? full1 * n[i] : 0.0f); x2[i] = r.x2[i] - (full2 > 0.0f ? full2 * n[i] : 0.0f); }
+      *dist = r.dist - (full1 + full2);
+      return 1;
+    }
+    g1.margin = full1 - size1; g1.size[0] = size1;
+    g2.margin = full2 - size2; g2.size[0] = size2;
+    cutoff -= full1 + full2;
+  }
+  r = gjk(w, tolerance, gjk_it, g1, g2, cutoff, discrete);
+  *dist = r.dist;
+  st3(x1, r.x1);
+  st3(x2, r.x2);
+  if (r.dist > tolerance || r.dim < 2) return 1;
+  int nvert = 0, nface = 0, status;
+  if (r.dim == 2) {
+    status = polytope2(w, &nvert, &nface, g1, g2);
+    if (status == -1) status = polytope3(w, &nvert, &nface, r.dist, g1, g2);
+  } else if (r.dim == 4) {
+    status = polytope4(w, &nvert, &nface);
+    if (status == -1) status = polytope3(w, &nvert, &nface, r.dist, g1, g2);
+  } else {
+    status = polytope3(w, &nvert, &nface, r.dist, g1, g2);
+  }
+  if (status) return 1;  // origin on the boundary: not penetrating
+  const int f = epa(w, nvert, nface, tolerance, epa_it, g1, g2, discrete, dist, x1, x2);
+  if (f == -1) {
+    *dist = CCD_FLOAT_MAX;
+    for (int i = 0; i < 3; i++) x1[i] = x2[i] = 0.0f;
+    return 0;
+  }
+  // multi-contact: no margin, boxes only in this build (the reference also takes meshes with polygon data)
+  *idx = (g1.margin != 0.0f || g2.margin != 0.0f || !(g1.type == GEOM_BOX && g2.type == GEOM_BOX)) ? -1 : f;
+  return 1;
+}
+
+// collision_convex.py:763-852 (eval_ccd_write_contact): contacts of one convex pair.  The pair's geoms
+// are read from the workspace (put_cgeom at L.geoms); the outputs are written to L.out: [0] dist
+// (corrected by +margin), [1..3] normal (unnormalized; frame = make_frame(normal)), [4..15] up to 4
+// points.  Returns the contact count (0: not penetrating).  Only scalars and the LDS base cross the
+// call, so the CCD code does not touch the caller's register budget.
 __device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, int gjk_it, float margin, const float* mesh_vert = nullptr) {
   CcdWS w;
   w.W = W;
@@ -951,56 +1009,9 @@ __device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, i
   float* pts = W + w.L.out + 4;
   g1.margin = margin;
   g2.margin = margin;
-  float cutoff = 0.0f;
-  // collision_gjk.py:91-94 _discrete_geoms: boxes and meshes (polytopes)
-  const int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH) && (g2.type == GEOM_BOX || g2.type == GEOM_MESH) && margin == 0.0f;
-  float full1 = 0.0f, full2 = 0.0f, size1 = 0.0f, size2 = 0.0f;
-  if (g1.type == GEOM_SPHERE || g1.type == GEOM_CAPSULE) { size1 = g1.size[0]; full1 = size1 + 0.5f * g1.margin; g1.margin = 0.0f; g1.size[0] = 0.0f; }
-  if (g2.type == GEOM_SPHERE || g2.type == GEOM_CAPSULE) { size2 = g2.size[0]; full2 = size2 + 0.5f * g2.margin; g2.margin = 0.0f; g2.size[0] = 0.0f; }
   float d, x1[3], x2[3];
-  int idx = -1;
-  GjkOut r;
-  bool done = false;
-  if (size1 + size2 > 0.0f) {
-    cutoff += full1 + full2;
-    r = gjk(w, tolerance, gjk_it, g1, g2, cutoff, discrete);
-    if (r.dist > tolerance) {
-      if (r.dist == CCD_FLOAT_MAX) return 0;
-      float n[3] = {r.x2[0] - r.x1[0], r.x2[1] - r.x1[1], r.x2[2] - r.x1[2]};
-      normalize3(n);
-      for (int i = 0; i < 3; i++) { x1[i] = r.x1[i] + (full1 > 0.0f ? full1 * n[i] : 0.0f); x2[i] = r.x2[i] - (full2 > 0.0f ? full2 * n[i] : 0.0f); }
-      d = r.dist - (full1 + full2);
-      done = true;
-    } else {
-      g1.margin = full1 - size1; g1.size[0] = size1;
-      g2.margin = full2 - size2; g2.size[0] = size2;
-      cutoff -= full1 + full2;
-    }
-  }
-  if (!done) {
-    r = gjk(w, tolerance, gjk_it, g1, g2, cutoff, discrete);
-    d = r.dist;
-    st3(x1, r.x1);
-    st3(x2, r.x2);
-    if (!(r.dist > tolerance || r.dim < 2)) {
-      int nvert = 0, nface = 0, status;
-      if (r.dim == 2) {
-        status = polytope2(w, &nvert, &nface, g1, g2);
-        if (status == -1) status = polytope3(w, &nvert, &nface, r.dist, g1, g2);
-      } else if (r.dim == 4) {
-        status = polytope4(w, &nvert, &nface);
-        if (status == -1) status = polytope3(w, &nvert, &nface, r.dist, g1, g2);
-      } else {
-        status = polytope3(w, &nvert, &nface, r.dist, g1, g2);
-      }
-      if (!status) {
-        idx = epa(w, nvert, nface, tolerance, epa_it, g1, g2, discrete, &d, x1, x2);
-        if (idx == -1) return 0;
-        if (g1.margin != 0.0f || g2.margin != 0.0f) idx = -1;
-        if (!(g1.type == GEOM_BOX && g2.type == GEOM_BOX)) idx = -1;
-      }
-    }
-  }
+  int idx;
+  if (!ccd_raw(w, epa_it, tolerance, gjk_it, 0.0f, g1, g2, &d, x1, x2, &idx)) return 0;
   if (d >= 0.0f) return 0;
   *dist_out = d + margin;
   int n = 1;

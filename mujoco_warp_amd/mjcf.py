@@ -932,10 +932,13 @@ class _Compiler:
     for asset in root.findall("asset"):
       for me in asset.findall("mesh"):
         a = self._resolve("mesh", me, None)
-        if "file" not in a:
-          raise NotImplementedError("<mesh> without a file (inline vertex / user meshes) is not supported")
-        path = os.path.join(self.basedir, self.meshdir, a["file"])
-        v, f = _read_mesh_file(path)
+        if "file" in a:
+          v, f = _read_mesh_file(os.path.join(self.basedir, self.meshdir, a["file"]))
+        elif "vertex" in a:  # inline mesh: vertices, faces given or the convex hull (MuJoCo user_mesh.cc)
+          v = np.array(_floats(a["vertex"]), dtype=np.float64).reshape(-1, 3)
+          f = np.array(_floats(a["face"]), dtype=np.int64).reshape(-1, 3) if "face" in a else _hull_faces(v)
+        else:
+          raise NotImplementedError("<mesh> needs a file or inline vertices")
         v = v * np.array(_merge_vec([1.0, 1.0, 1.0], _floats(a.get("scale", "1 1 1"))))
         _, first, inv = np.unique(v, axis=0, return_index=True, return_inverse=True)
         order = np.argsort(first)  # unique rows in first-occurrence order
@@ -943,7 +946,7 @@ class _Compiler:
         remap[order] = np.arange(len(order))
         v = v[first[order]]
         f = remap[inv.reshape(-1)[f]]
-        name = a.get("name") or os.path.splitext(os.path.basename(a["file"]))[0]
+        name = a.get("name") or os.path.splitext(os.path.basename(a.get("file", "")))[0]
         self.mesh_id[name] = len(self.mesh_data)
         self.mesh_data.append((v, f))
     m.nmesh = len(self.mesh_data)
@@ -1918,6 +1921,19 @@ def set_const(m: MjModel):
       vec[da] = m.actuator_gear[a, 0]
     acc0[a] = np.linalg.norm(Minv @ vec)
   m.actuator_acc0 = acc0
+
+
+def _hull_faces(v):
+  """Outward-oriented triangles of the convex hull of `v` (inline meshes without faces)."""
+  from scipy.spatial import ConvexHull
+
+  h = ConvexHull(v)
+  c = v.mean(axis=0)
+  f = h.simplices.astype(np.int64).copy()
+  for k, (i, j, l) in enumerate(f):
+    if np.dot(np.cross(v[j] - v[i], v[l] - v[i]), v[i] - c) < 0:
+      f[k] = (i, l, j)
+  return f
 
 
 def load_model_from_string(xml: str, basedir: str = ".") -> MjModel:

@@ -3122,3 +3122,66 @@ void orc_forward(const orc_model* m, const orc_data* b, int nworld, int nthread)
   }
   (void)nthread;
 }
+
+/* ---- known-answer entry points: the reference's own collision unit tests, restated as data ----------
+ * (tests/golden/make_golden.py extracts their inputs and expected values; tests/test_golden.py runs them) */
+
+/* collision_gjk_test.py:34-265 _geom_dist: ccd(tolerance, cutoff 1e30, iterations, iterations) of two geoms
+ * carrying `margin`, then (multiccd) multicontact.  out = dist, x1[3], x2[3]; returns ncon, or -1 for a
+ * multi-contact request this build does not restate (mesh polygons). */
+int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* size, const real* mesh_vert, const int* vertadr,
+                const int* vertnum, real margin, real tolerance, int iterations, int multiccd, real* out) {
+  ccd_geom g[2], h1, h2;
+  for (int k = 0; k < 2; k++) {
+    memcpy(g[k].pos, pos + 3 * k, 3 * sizeof(real));
+    memcpy(g[k].rot, mat + 9 * k, 9 * sizeof(real));
+    memcpy(g[k].size, size + 3 * k, 3 * sizeof(real));
+    g[k].margin = margin;
+    g[k].type = type[k];
+    g[k].vert = type[k] == GEOM_MESH ? mesh_vert + 3 * vertadr[k] : NULL;
+    g[k].nvert = type[k] == GEOM_MESH ? vertnum[k] : 0;
+  }
+  polytope* pt = ccd_polytope();
+  real d, x1[3], x2[3];
+  int idx;
+  int ncon = ccd_raw(&g[0], &g[1], tolerance, (real)1e30, iterations, iterations, pt, &d, x1, x2, &idx, &h1, &h2);
+  if (multiccd && (type[0] == GEOM_MESH || type[1] == GEOM_MESH)) return -1;
+  if (multiccd && idx > -1) {
+    real w1[4][3], w2[4][3];
+    ncon = multicontact_box(pt, idx, x1, x2, &h1, &h2, w1, w2);
+  }
+  out[0] = d;
+  for (int i = 0; i < 3; i++) { out[1 + i] = x1[i]; out[4 + i] = x2[i]; }
+  return ncon;
+}
+
+/* collision_primitive_core_test.py: sphere_triangle (gt = SPHERE), box_triangle, capsule_triangle and
+ * cylinder_triangle (collision_primitive_core.py:1518-1990); capsule / cylinder take their axis from column
+ * 2 of `gr`.  out = 2 x (dist, pos[3], normal[3]); returns the number of candidates. */
+int orc_kat_geom_triangle(int gt, const real* gp, const real* gr, const real* gs, const real* tri, real tr, real* out) {
+  const real* t[3] = {tri, tri + 3, tri + 6};
+  real ax[3] = {gr[2], gr[5], gr[8]};
+  contacts2 c;
+  c.n = 0;
+  if (gt == GEOM_SPHERE) {
+    real p[3], n[3];
+    real dd = sphere_triangle(p, n, gp, gs[0], t[0], t[1], t[2], tr);
+    put2(&c, dd, p, n);
+  } else if (gt == GEOM_CAPSULE) {
+    capsule_triangle(&c, gp, ax, gs[0], gs[1], t, tr);
+  } else if (gt == GEOM_BOX) {
+    box_triangle(&c, gp, gr, gs, t, tr);
+  } else if (gt == GEOM_CYLINDER) {
+    cylinder_triangle(&c, gp, ax, gs[0], gs[1], t, tr);
+  } else {
+    return -1;
+  }
+  for (int k = 0; k < 2; k++) {
+    out[7 * k] = k < c.n ? c.dist[k] : MAXVAL;
+    for (int i = 0; i < 3; i++) {
+      out[7 * k + 1 + i] = k < c.n ? c.pos[k][i] : 0;
+      out[7 * k + 4 + i] = k < c.n ? c.frame[k][i] : 0;
+    }
+  }
+  return c.n;
+}

@@ -163,6 +163,10 @@ void orc_closest_segment_to_segment_points(const real* a0, const real* a1, const
 int orc_upper_tri_index(int n, int i, int j);
 int orc_upper_trid_index(int n, int i, int j);
 real orc_halton(int index, int base);
+/* collision KATs (collision_gjk_test.py, collision_primitive_core_test.py) */
+int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* size, const real* mesh_vert, const int* vertadr,
+                const int* vertnum, real margin, real tolerance, int iterations, int multiccd, real* out);
+int orc_kat_geom_triangle(int gt, const real* gp, const real* gr, const real* gs, const real* tri, real tr, real* out);
 void orc_ctrl_noise(const orc_model* m, real* ctrl, const real* center, int ncenter, int step, real std,
                     real rate, int nworld, int world_offset);
 

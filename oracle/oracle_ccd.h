@@ -859,20 +859,14 @@ static int multicontact_box(const polytope* pt, int fidx, const real* x1, const 
   return polygon_clip(f1, nf1, f2, nf2, n1[ri], ad, w1, w2);
 }
 
-/* collision_gjk.py:2200-2345 ccd (+ collision_convex.py:763-852 eval_ccd_write_contact): contacts of one
- * convex pair.  Returns the number of contacts (0 when not penetrating), all at distance *dist
- * (already corrected by +margin) with normal `normal` (unnormalized; the frame is make_frame(normal)). */
-static int ccd_pair(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, int gjk_iter, int epa_iter, real margin,
-                    real* dist_out, real* normal, real pts[4][3]) {
-  static polytope pt_store;
-#ifdef _OPENMP
-#pragma omp threadprivate(pt_store)
-#endif
-  polytope* pt = &pt_store;
+/* collision_gjk.py:2200-2345 ccd: distance (or penetration depth) of one convex pair and its first
+ * witness points.  Returns the reference's ncon (1, or 0 when EPA fails with FLOAT_MAX); *idx is the
+ * EPA face for box multi-contact (-1 otherwise); the polytope stays in `pt` for multicontact_box.
+ * Geoms carry their margin (the caller sets it, collision_convex.py:770-771). */
+static int ccd_raw(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, real cutoff, int gjk_iter, int epa_iter, polytope* pt,
+                   real* dist, real* x1, real* x2, int* idx, ccd_geom* g1out, ccd_geom* g2out) {
   ccd_geom g1 = *g1in, g2 = *g2in;
-  g1.margin = margin;
-  g2.margin = margin;
-  real cutoff = 0;
+  *idx = -1;
   /* collision_gjk.py:91-94, 2226: boxes and meshes are discrete */
   int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH) && (g2.type == GEOM_BOX || g2.type == GEOM_MESH) && g1.margin == 0 &&
                  g2.margin == 0;
@@ -883,31 +877,36 @@ static int ccd_pair(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, 
   if (g2.type == GEOM_SPHERE || g2.type == GEOM_CAPSULE) {
     size2 = g2.size[0]; full2 = size2 + 0.5 * g2.margin; g2.margin = 0; g2.size[0] = 0;
   }
-  real d, x1[3], x2[3];
-  int idx = -1;
+  *g1out = g1;
+  *g2out = g2;
   gjk_result r;
   if (size1 + size2 > 0) {
     cutoff += full1 + full2;
     r = gjk(tolerance, gjk_iter, &g1, &g2, g1.pos, g2.pos, cutoff, discrete);
-    if (r.dist > tolerance) {
-      if (r.dist == CCD_FLOAT_MAX) return 0;
+    if (r.dist > tolerance) { /* shallow penetration: inflate (collision_gjk.py:194-213 _inflate) */
+      if (r.dist == CCD_FLOAT_MAX) {
+        *dist = r.dist;
+        memcpy(x1, r.x1, 3 * sizeof(real));
+        memcpy(x2, r.x2, 3 * sizeof(real));
+        return 1;
+      }
       real n[3] = {r.x2[0] - r.x1[0], r.x2[1] - r.x1[1], r.x2[2] - r.x1[2]};
       normalize3(n);
       for (int i = 0; i < 3; i++) { x1[i] = r.x1[i] + (full1 > 0 ? full1 * n[i] : 0); x2[i] = r.x2[i] - (full2 > 0 ? full2 * n[i] : 0); }
-      d = r.dist - (full1 + full2);
-      goto write;
+      *dist = r.dist - (full1 + full2);
+      return 1;
     }
     g1.margin = full1 - size1; g1.size[0] = size1;
     g2.margin = full2 - size2; g2.size[0] = size2;
     cutoff -= full1 + full2;
   }
+  *g1out = g1;
+  *g2out = g2;
   r = gjk(tolerance, gjk_iter, &g1, &g2, g1.pos, g2.pos, cutoff, discrete);
-  if (r.dist > tolerance || r.dim < 2) {
-    d = r.dist;
-    memcpy(x1, r.x1, sizeof(x1));
-    memcpy(x2, r.x2, sizeof(x2));
-    goto write;
-  }
+  *dist = r.dist;
+  memcpy(x1, r.x1, 3 * sizeof(real));
+  memcpy(x2, r.x2, 3 * sizeof(real));
+  if (r.dist > tolerance || r.dim < 2) return 1;
   memset(pt, 0, sizeof(*pt));
   pt->cap_vert = 10 + 2 * epa_iter;
   pt->cap_face = 6 + CCD_MAX_EPAFACES * epa_iter;
@@ -921,17 +920,40 @@ static int ccd_pair(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, 
   } else {
     status = polytope3(pt, r.dist, &r, &g1, &g2);
   }
-  if (status) {
-    d = r.dist;
-    memcpy(x1, r.x1, sizeof(x1));
-    memcpy(x2, r.x2, sizeof(x2));
-    goto write;
+  if (status) return 1; /* origin on the boundary: not penetrating */
+  int f = epa(tolerance, epa_iter, pt, &g1, &g2, discrete, dist, x1, x2);
+  if (f == -1) {
+    *dist = CCD_FLOAT_MAX;
+    for (int i = 0; i < 3; i++) x1[i] = x2[i] = 0;
+    return 0;
   }
-  idx = epa(tolerance, epa_iter, pt, &g1, &g2, discrete, &d, x1, x2);
-  if (idx == -1) return 0; /* FLOAT_MAX distance */
-  if (g1.margin != 0 || g2.margin != 0) idx = -1;
-  if (!((g1.type == GEOM_BOX) && (g2.type == GEOM_BOX))) idx = -1;
-write:
+  /* multicontact: no margin, boxes only in this build (the reference also takes meshes with polygon data) */
+  if (g1.margin != 0 || g2.margin != 0) f = -1;
+  if (!((g1.type == GEOM_BOX) && (g2.type == GEOM_BOX))) f = -1;
+  *idx = f;
+  return 1;
+}
+
+static polytope* ccd_polytope(void) {
+  static polytope pt_store;
+#ifdef _OPENMP
+#pragma omp threadprivate(pt_store)
+#endif
+  return &pt_store;
+}
+
+/* collision_convex.py:763-852 (eval_ccd_write_contact): contacts of one convex pair.  Returns the number
+ * of contacts (0 when not penetrating), all at distance *dist (already corrected by +margin) with normal
+ * `normal` (unnormalized; the frame is make_frame(normal)). */
+static int ccd_pair(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, int gjk_iter, int epa_iter, real margin,
+                    real* dist_out, real* normal, real pts[4][3]) {
+  polytope* pt = ccd_polytope();
+  ccd_geom g1 = *g1in, g2 = *g2in, h1, h2;
+  g1.margin = margin;
+  g2.margin = margin;
+  real d, x1[3], x2[3];
+  int idx;
+  if (!ccd_raw(&g1, &g2, tolerance, 0, gjk_iter, epa_iter, pt, &d, x1, x2, &idx, &h1, &h2)) return 0;
   if (d >= 0) return 0;
   d += margin;
   *dist_out = d;
@@ -939,7 +961,7 @@ write:
   int n = 1;
   memcpy(w1[0], x1, sizeof(x1));
   memcpy(w2[0], x2, sizeof(x2));
-  if (idx > -1) n = multicontact_box(pt, idx, x1, x2, &g1, &g2, w1, w2);
+  if (idx > -1) n = multicontact_box(pt, idx, x1, x2, &h1, &h2, w1, w2);
   for (int i = 0; i < n; i++)
     for (int k = 0; k < 3; k++) pts[i][k] = 0.5 * (w1[i][k] + w2[i][k]);
   for (int k = 0; k < 3; k++) normal[k] = w1[0][k] - w2[0][k];

@@ -254,6 +254,40 @@ def kat_upper_trid_index(n, i, j):
   return _lib(64).orc_upper_trid_index(n, i, j)
 
 
+def kat_ccd(types, pos, mat, size, margin, tolerance, iterations, multiccd, mesh_vert=None, vertadr=(0, 0), vertnum=(0, 0),
+            real_bits=64):
+  """collision_gjk_test.py _geom_dist on the oracle: (ncon, dist, x1, x2); ncon -1 = not restated."""
+  lib = _lib(real_bits)
+  creal = ctypes.c_double if real_bits == 64 else ctypes.c_float
+  dt = np.float64 if real_bits == 64 else np.float32
+  P = lambda a: a.ctypes.data_as(ctypes.POINTER(creal))
+  I = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+  t = np.ascontiguousarray(types, dtype=np.int32)
+  pos, mat, size = (np.ascontiguousarray(x, dtype=dt).reshape(-1) for x in (pos, mat, size))
+  mv = np.ascontiguousarray(np.zeros(3) if mesh_vert is None else mesh_vert, dtype=dt).reshape(-1)
+  va, vn = np.ascontiguousarray(vertadr, dtype=np.int32), np.ascontiguousarray(vertnum, dtype=np.int32)
+  out = np.zeros(7, dt)
+  f = lib.orc_kat_ccd
+  f.restype = ctypes.c_int
+  n = f(I(t), P(pos), P(mat), P(size), P(mv), I(va), I(vn), creal(margin), creal(tolerance), ctypes.c_int(iterations),
+        ctypes.c_int(int(multiccd)), P(out))
+  return n, float(out[0]), out[1:4].copy(), out[4:7].copy()
+
+
+def kat_geom_triangle(gt, gp, gr, gs, tri, tr, real_bits=64):
+  """collision_primitive_core_test.py on the oracle: (n, out[2, 7] = dist, pos, normal)."""
+  lib = _lib(real_bits)
+  creal = ctypes.c_double if real_bits == 64 else ctypes.c_float
+  dt = np.float64 if real_bits == 64 else np.float32
+  P = lambda a: a.ctypes.data_as(ctypes.POINTER(creal))
+  gp, gr, gs, tri = (np.ascontiguousarray(x, dtype=dt).reshape(-1) for x in (gp, gr, gs, tri))
+  out = np.zeros(14, dt)
+  f = lib.orc_kat_geom_triangle
+  f.restype = ctypes.c_int
+  n = f(ctypes.c_int(gt), P(gp), P(gr), P(gs), P(tri), creal(tr), P(out))
+  return n, out.reshape(2, 7).copy()
+
+
 def halton(index, base):
   f = _lib(64).orc_halton
   f.restype = ctypes.c_double
