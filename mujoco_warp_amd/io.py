@@ -335,14 +335,12 @@ def cmodel(m: types.Model) -> _lib.CModel:
     attr = {"nxn_geom_pair": "nxn_geom_pair_typed", "nxn_pairid": "nxn_pairid_filtered"}.get(name, name)
     tensors.append(getattr(m, attr))
   cache = getattr(m, "_cmodel_cache", None)
-  scal = tuple(int(getattr(m.opt, n[4:]) if n.startswith("opt_") else getattr(m, n)) for n in _lib.MODEL_INT_SCALARS if n != "opt_broadphase_filter")
+  scal = tuple(int(getattr(m.opt, n[4:]) if n.startswith("opt_") else getattr(m, n)) for n in _lib.MODEL_INT_SCALARS)
   if cache is not None and cache[1] == scal and len(cache[2]) == len(tensors) and all(a is b for a, b in zip(cache[2], tensors)):
     return cache[0]
   c = _lib.CModel()
   for n in _lib.MODEL_INT_SCALARS:
-    if n == "opt_broadphase_filter":
-      v = int(m.opt.broadphase_filter)
-    elif n.startswith("opt_"):
+    if n.startswith("opt_"):
       v = int(getattr(m.opt, n[4:]))
     else:
       v = int(getattr(m, n))

@@ -122,7 +122,7 @@ class OracleModel:
       nmaxpyramid=max(1, 2 * (int(np.concatenate(([0], mjm.geom_condim)).max()) - 1)),
       opt_integrator=o.integrator, opt_cone=o.cone, opt_solver=o.solver, opt_iterations=o.iterations,
       opt_ls_iterations=o.ls_iterations, opt_disableflags=o.disableflags, opt_enableflags=o.enableflags,
-      opt_broadphase_filter=1 | 2 | 8,
+      opt_broadphase_filter=int(getattr(o, "broadphase_filter", 1 | 2 | 8)),
       opt_ccd_iterations=getattr(o, "ccd_iterations", 35), ccd_epa_iterations=ccd_epa_iterations(mjm, pairs),
       opt_ccd_tolerance=getattr(o, "ccd_tolerance", 1e-6),
       opt_timestep=o.timestep, opt_tolerance=max(o.tolerance, 1e-6), opt_ls_tolerance=o.ls_tolerance,

@@ -9,6 +9,9 @@ The test files are parsed with `ast` as text; no reference code is imported or e
                                                     checks on dist, ncon, witness points and normal
   mujoco_warp/_src/collision_primitive_core_test.py sphere / box / capsule / cylinder vs triangle cases:
                                                     literal inputs and their checks on dist / normal
+  mujoco_warp/_src/broadphase_test.py               NXN broadphase pair counts (d.ncollision): scene,
+                                                    keyframe(s), broadphase_filter, disableflags and the
+                                                    expected count of every assertion
 The tests read only the JSON (the reference does not exist on the GPU box).
 """
 
@@ -217,16 +220,119 @@ def triangle_cases(ref):
   return cases
 
 
+_FILTER = {"PLANE": 1, "SPHERE": 2, "AABB": 4, "OBB": 8}  # types.BroadphaseFilter
+_DISABLE = {"FILTERPARENT": 1 << 10}  # types.DisableBit
+
+
+def _flags(node, env):
+  """BroadphaseFilter / DisableBit expressions: X.NAME, names bound to them, `|` combinations."""
+  if isinstance(node, ast.BinOp) and isinstance(node.op, ast.BitOr):
+    return _flags(node.left, env) | _flags(node.right, env)
+  if isinstance(node, ast.Attribute):
+    base = ast.unparse(node.value)
+    if base.endswith("BroadphaseFilter"):
+      return _FILTER[node.attr]
+    if base.endswith("DisableBit"):
+      return _DISABLE[node.attr]
+    if base in ("self", "BroadphaseTest"):
+      return env[node.attr]
+  if isinstance(node, ast.Name):
+    return env[node.id]
+  if isinstance(node, ast.Constant):
+    return int(node.value)
+  raise ValueError(ast.unparse(node))
+
+
+def broadphase_cases(ref):
+  """broadphase_test.py: NXN broadphase pair counts (d.ncollision) per scene / keyframe / filter."""
+  path = os.path.join(ref, "mujoco_warp", "_src", "broadphase_test.py")
+  tree = ast.parse(open(path).read())
+  cls = [n for n in tree.body if isinstance(n, ast.ClassDef)][0]
+  env = {}
+  for st in cls.body:  # class-level filter combinations
+    if isinstance(st, ast.Assign) and isinstance(st.targets[0], ast.Name):
+      env[st.targets[0].id] = _flags(st.value, env)
+  cases = []
+  for fn in [n for n in cls.body if isinstance(n, ast.FunctionDef) and n.name.startswith("test_")]:
+    local = dict(env)
+    params = [{}]
+    for dec in fn.decorator_list:
+      if not isinstance(dec, ast.Call):
+        continue
+      name = ast.unparse(dec.func)
+      argnames = [a.arg for a in fn.args.args[1:]]
+      if name.endswith("parameters"):
+        params = [dict(zip(argnames, [(_flags(e, local) if isinstance(e, (ast.Attribute, ast.BinOp)) else _lit(e, local)) for e in t.elts]))
+                  for t in dec.args]
+      elif name.endswith("product"):
+        for kw in dec.keywords:
+          if kw.arg == "filter":
+            params = [dict(filter=_flags(e, local)) for e in kw.value.elts]
+    for prm in params:
+      xmlvars, keyof, filt, disable, contype0, pending = {}, {}, None, 0, None, None
+      for st in fn.body:
+        if isinstance(st, ast.Assign) and isinstance(st.targets[0], ast.Name) and isinstance(st.value, (ast.Attribute, ast.BinOp)):
+          try:  # local filter names (plane = BroadphaseFilter.PLANE, plane_sphere = plane | sphere)
+            local[st.targets[0].id] = _flags(st.value, local)
+          except (ValueError, KeyError):
+            pass
+        if isinstance(st, ast.Assign) and isinstance(st.targets[0], ast.Name):
+          if isinstance(st.value, ast.Constant) and isinstance(st.value.value, str):
+            xmlvars[st.targets[0].id] = st.value.value
+          elif isinstance(st.value, ast.JoinedStr):  # f-string scene with the test parameters
+            parts = [v.value if isinstance(v, ast.Constant) else str(prm[ast.unparse(v.value)]) for v in st.value.values]
+            xmlvars[st.targets[0].id] = "".join(parts)
+        if isinstance(st, ast.Assign) and isinstance(st.value, ast.Call) and ast.unparse(st.value.func) == "test_data.fixture":
+          kw = {k.arg: k.value for k in st.value.keywords}
+          xml = xmlvars[kw["xml"].id]
+          key = int(_lit(kw["keyframe"], {})) if "keyframe" in kw else 0
+          if "overrides" in kw:
+            disable = int(prm[ast.unparse(kw["overrides"].values[0])])
+          names = [e.id for e in st.targets[0].elts if isinstance(e, ast.Name)]
+          for n in names:
+            keyof[n] = key
+          contype0 = None
+          pending = dict(xml=xml, keys=[key])
+        if isinstance(st, ast.Assign) and isinstance(st.targets[0], ast.Attribute) and ast.unparse(st.targets[0]).endswith("opt.broadphase_filter"):
+          filt = _flags(st.value, local) if not isinstance(st.value, ast.Name) else prm.get(st.value.id, local.get(st.value.id))
+        if isinstance(st, ast.Assign) and isinstance(st.targets[0], ast.Subscript) and ast.unparse(st.targets[0]).endswith("geom_contype[:3]"):
+          contype0 = int(_lit(st.value, {}))
+        if isinstance(st, ast.Assign) and isinstance(st.value, ast.Call) and ast.unparse(st.value.func) == "mjw.make_data":
+          # two worlds whose geom frames come from two keyframes' mjData (np.vstack of mjdA / mjdB)
+          pass
+        if isinstance(st, ast.Assign) and ast.unparse(st.targets[0]).endswith("geom_xpos") and "vstack" in ast.unparse(st.value):
+          srcs = [n.id for n in ast.walk(st.value) if isinstance(n, ast.Name) and n.id.startswith("mjd")]
+          pending = dict(xml=pending["xml"], keys=[keyof[n] for n in srcs])
+        if isinstance(st, ast.Expr) and isinstance(st.value, ast.Call):
+          call = st.value
+          fname = ast.unparse(call.func)
+          if (fname.endswith("assert_allclose") or fname.endswith("assertEqual")) and "ncollision" in ast.unparse(call.args[0]):
+            want = int(_lit(call.args[1], dict(local, **prm)))
+            if fname.endswith("assert_allclose") and not isinstance(call.args[1], ast.Constant) and not isinstance(call.args[1], ast.Name):
+              continue
+            case = dict(name=f"{fn.name}", source=f"broadphase_test.py:{call.lineno}", xml=pending["xml"], keys=pending["keys"],
+                        filter=filt if filt is not None else prm.get("filter", 1 | 2 | 8), disableflags=disable, ncollision=want)
+            if contype0 is not None:
+              case["geom_contype_first3"] = contype0
+            if fn.name == "test_broadphase" and case["filter"] is None:
+              case["filter"] = prm["filter"]
+            cases.append(case)
+  return cases
+
+
 def main(ref):
   gjk, skipped = gjk_cases(ref)
   tri = triangle_cases(ref)
+  bp = broadphase_cases(ref)
   out = dict(generated_by="tests/golden/make_golden_collision.py",
-             reference=["mujoco_warp/_src/collision_gjk_test.py", "mujoco_warp/_src/collision_primitive_core_test.py"],
-             gjk=gjk, gjk_not_extracted=skipped, triangle=tri)
+             reference=["mujoco_warp/_src/collision_gjk_test.py", "mujoco_warp/_src/collision_primitive_core_test.py",
+                        "mujoco_warp/_src/broadphase_test.py"],
+             gjk=gjk, gjk_not_extracted=skipped, triangle=tri, broadphase=bp)
   dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "collision_kat.json")
   with open(dst, "w") as f:
     json.dump(out, f, indent=1)
-  print(f"wrote {dst}: {len(gjk)} gjk cases ({len(skipped)} not extracted: {skipped}), {len(tri)} triangle cases")
+  print(f"wrote {dst}: {len(gjk)} gjk cases ({len(skipped)} not extracted: {skipped}), {len(tri)} triangle cases, "
+        f"{len(bp)} broadphase cases")
 
 
 if __name__ == "__main__":

@@ -108,3 +108,17 @@ def check(case, res):
       np.testing.assert_allclose(got, want, atol=c["atol"], err_msg=where)
     else:
       raise AssertionError(f"unknown check {c}")
+
+
+def broadphase_model(case):
+  """Compiled scene of a broadphase_test.py case with its filter / disableflags / contype edits, and the
+  per-world qpos of its keyframe(s)."""
+  import mujoco_warp_amd as mjw
+
+  mjm = mjw.load_model_from_string(case["xml"])
+  mjm.opt.broadphase_filter = int(case["filter"])
+  mjm.opt.disableflags = int(mjm.opt.disableflags) | int(case["disableflags"])
+  if "geom_contype_first3" in case:
+    mjm.geom_contype[:3] = case["geom_contype_first3"]
+  qpos = np.stack([np.asarray(mjm.key_qpos[k], np.float64) for k in case["keys"]])
+  return mjm, qpos

@@ -34,6 +34,11 @@ def _setup(which, nworld, seed):
   return (mjm,) + cloth_states(mjm, nworld, seed=seed) + (NJMAX, NCONMAX)
 
 
+def _normwise(name, got, want, tol):
+  e = np.abs(got - want).max(axis=1) / (np.abs(want).max(axis=1) + 1e-30)
+  assert e.max() <= tol, f"{name}: normwise error {e.max():.3e} > {tol}"
+
+
 @pytest.fixture(scope="module")
 def mjm():
   return cloth_model()
@@ -183,6 +188,9 @@ def test_gpu_cloth_smooth_forces_and_cg_cost(which):
   assert_close("qfrc_passive", np_(d.qfrc_passive), od.qfrc_passive, rtol=1e-3, atol=5e-7)
   assert_close("qfrc_bias", np_(d.qfrc_bias), od.qfrc_bias, rtol=1e-5, atol=1e-4)
   assert_close("qacc_smooth", np_(d.qacc_smooth), od.qacc_smooth, rtol=1e-2, atol=5e-3)
+  # normwise per world, the bar that does not depend on near-zero components: measured 1.1e-5 (cloth)
+  # and 5.7e-7 (aloha_cloth) after one step, profiles/r02_cloth_parity_probe.json
+  _normwise("qacc_smooth", np_(d.qacc_smooth), od.qacc_smooth, 1e-4)
   for w in range(nworld):
     n = int(od.nefc[w, 0])
     J = od.efc_J[w].reshape(NJMAX, nv)[:n]
@@ -210,8 +218,13 @@ def test_gpu_cloth_rollout_parity_and_determinism(which):
     mjw.step(m, d)
     od.step()
   torch.cuda.synchronize()
+  # three fp32 CG solves of 2700 dofs / ~3-15k rows each stop at slightly different iterates than the
+  # fp64 oracle's (iteration counts differ by a few), and the next step starts from there: measured
+  # normwise qpos 1.6e-5 and qvel 8.5e-3 (cloth), 4.7e-7 / 3.4e-4 (aloha_cloth) after 3 steps
+  # (tools/cloth_parity_probe.py -> profiles/r02_cloth_parity_probe.json)
   assert_close("qpos", np_(d.qpos), od.qpos, rtol=1e-3, atol=1e-4)
-  assert_close("qvel", np_(d.qvel), od.qvel, rtol=0.1, atol=1e-2)
+  _normwise("qpos", np_(d.qpos), od.qpos, 1e-4)
+  _normwise("qvel", np_(d.qvel), od.qvel, 2e-2)
   # copies of one world stay bitwise equal over a longer rollout, and nothing blows up
   rep = 64 if which == "cloth" else 16
   m2, d2 = gpu_from_state(mjm, np.repeat(qpos[:1], rep, 0), np.repeat(qvel[:1], rep, 0), np.repeat(ctrl[:1], rep, 0), njmax=NJMAX, nconmax=NCONMAX)

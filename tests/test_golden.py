@@ -61,3 +61,16 @@ def test_oracle_fp64_reproduces_mujoco_c():
       assert abs(dist - c["mjc64"]) < 1e-15, (case["name"], dist, c["mjc64"])
       done += 1
   assert done >= 1
+
+
+@pytest.mark.parametrize("case", KAT["broadphase"], ids=[f"{c['source']}-f{c['filter']}-k{c['keys']}" for c in KAT["broadphase"]])
+def test_oracle_broadphase_kat(case):
+  """NXN broadphase pair counts of broadphase_test.py (filters, margins, filterparent, contype)."""
+  import numpy as np
+
+  mjm, qpos = gk.broadphase_model(case)
+  om = orc.OracleModel(mjm)
+  od = orc.OracleData(om, len(qpos), 64, 64)
+  od.qpos[:] = qpos
+  od.fwd_position()
+  assert int(np.sum(od.ncollision)) == case["ncollision"], case["source"]

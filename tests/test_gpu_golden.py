@@ -104,3 +104,19 @@ def test_hip_matches_fp32_oracle_kat(gjk_results):
     o = gjk_results[c["name"]]
     assert int(o[0]) == n, c["name"]
     assert abs(o[1] - d) <= max(1e-6, 1e-4 * abs(d)), (c["name"], o[1], d)
+
+
+@pytest.mark.parametrize("case", KAT["broadphase"], ids=[f"{c['source']}-f{c['filter']}-k{c['keys']}" for c in KAT["broadphase"]])
+def test_hip_broadphase_kat(case):
+  """NXN broadphase pair counts of broadphase_test.py on the forward kernel (d.ncollision after
+  fwd_position): plane / sphere / AABB / OBB filter combinations, margins, filterparent, contype."""
+  import mujoco_warp_amd as mjw
+
+  mjm, qpos = gk.broadphase_model(case)
+  m = mjw.put_model(mjm, device="cuda")
+  m.opt.broadphase_filter = int(case["filter"])
+  d = mjw.make_data(mjm, nworld=len(qpos), nconmax=16, njmax=64, device="cuda", m=m)
+  d.qpos[:] = torch.as_tensor(qpos, dtype=torch.float32, device="cuda")
+  mjw.fwd_position(m, d)
+  torch.cuda.synchronize()
+  assert int(d.ncollision[0]) == case["ncollision"], case["source"]
