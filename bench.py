@@ -9,9 +9,11 @@ ctrl_noise + mjw.step over all worlds; the timed region contains exactly K steps
 (ctrl_noise included, i.e. slightly conservative vs the reference which times
 only the graph replay).
 
-Multi-GPU: one process per GPU (torch.distributed.run); each rank owns 8192
-worlds (weak scaling, world ids offset by rank), no collective on the data
-path; a barrier + max-over-ranks of the elapsed time brackets the timed region.
+Multi-GPU: one process per GPU (torch.distributed.run, or `--gpus N` alone, which
+starts the N ranks itself); each rank owns 8192 worlds (weak scaling, world ids
+offset by rank) or `--scaling strong` splits --nworld over the ranks; no
+collective on the data path: a gloo (host) barrier + max-over-ranks of the
+elapsed time brackets the timed region.
 
 A step is two kernels on the torch stream: the forward kernel
 mjw::mjw_kernel<79> (kinematics, com, crb/qM, collision, constraint rows,
@@ -109,64 +111,157 @@ def parse():
   p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
   p.add_argument("--cpu-worlds", type=int, default=None, help="CPU baseline sample worlds (default: the config's, 1024)")
   p.add_argument("--cpu-steps", type=int, default=None, help="CPU baseline sample steps (default: the config's, 1000)")
-  p.add_argument("--pmc", default=None, help="PMC traffic summary (default: profiles/pmc_<model>_r01.json)")
-  p.add_argument("--graph", type=int, default=0, help="replay steps through a captured hipGraph")
+  p.add_argument("--pmc", default=None, help="PMC traffic summary (default: the newest profiles/pmc_<model>_rNN.json)")
+  p.add_argument("--graph", type=int, default=0, help="capture mjw.step once as a hipGraph and replay it every step "
+                 "(benchmark.py:123-155: ctrl noise is launched outside the graph); per-kernel events are then unavailable")
+  p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                 help="weak: --nworld worlds per rank; strong: --nworld worlds in total, split over the ranks")
+  p.add_argument("--dump-qpos", default=None, help="directory: each rank writes its final qpos + world offset (tests)")
   a = p.parse_args()
   cfg = MODELS[a.model]
   for k in ("nworld", "nconmax", "njmax", "solver"):
     if getattr(a, k) is None:
       setattr(a, k, cfg[k])
-  if a.pmc is None:
-    a.pmc = os.path.join(ROOT, "profiles", f"pmc_{a.model}_r01.json")
+  if a.pmc is None:  # the latest round's summary for this model
+    import glob
+
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{a.model}_r[0-9]*.json")))
+    a.pmc = found[-1] if found else ""
   for k, dflt in (("steps", 1000), ("cpu_worlds", 1024), ("cpu_steps", 1000)):
     if getattr(a, k) is None:
       setattr(a, k, cfg.get(k, dflt))
   return a
 
 
+def _host_cpu():
+  """(logical CPUs of the host, CPUs this process may run on, model name) for the cpu_baseline record."""
+  model = None
+  try:
+    with open("/proc/cpuinfo") as f:
+      for line in f:
+        if line.startswith("model name"):
+          model = line.split(":", 1)[1].strip()
+          break
+  except OSError:
+    pass
+  try:
+    allowed = len(os.sched_getaffinity(0))
+  except AttributeError:
+    allowed = os.cpu_count() or 1
+  return os.cpu_count() or 1, allowed, model
+
+
 def cpu_baseline(mjm, nworld, nsteps, key, njmax, nconmax, model):
-  """fp64 C oracle (restatement of the reference step), OpenMP over worlds; rank 0 only."""
+  """C oracle (restatement of the reference step), OpenMP over worlds on every CPU this process may use;
+  rank 0 only.  fp64 is the parity oracle and the reported value; the fp32 build (the path's arithmetic
+  type) is timed on the same sample next to it."""
   from oracle import orc
 
-  nthread = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-  nthread = max(1, min(nthread, 16))
-  om = orc.OracleModel(mjm, real_bits=64)
-  od = orc.OracleData(om, nworld, njmax, nconmax)
-  center = None
-  if key is not None:
-    od.qpos[:] = mjm.key_qpos[key]
-    od.ctrl[:] = mjm.key_ctrl[key]
-    center = mjm.key_ctrl[key]
-  t0 = time.perf_counter()
-  for i in range(nsteps):
-    od.ctrl_noise(i, center=center)
-    od.step(nthread=nthread)
-  dt = time.perf_counter() - t0
+  nproc, allowed, cpu_model = _host_cpu()
+  # the box grants its share through OMP_NUM_THREADS / the affinity mask; use all of it
+  nthread = int(os.environ.get("OMP_NUM_THREADS", "0")) or allowed
+  nthread = max(1, min(nthread, allowed))
+  rates = {}
+  for bits in (64, 32):
+    om = orc.OracleModel(mjm, real_bits=bits)
+    od = orc.OracleData(om, nworld, njmax, nconmax)
+    center = None
+    if key is not None:
+      od.qpos[:] = mjm.key_qpos[key]
+      od.ctrl[:] = mjm.key_ctrl[key]
+      center = mjm.key_ctrl[key]
+    t0 = time.perf_counter()
+    for i in range(nsteps):
+      od.ctrl_noise(i, center=center)
+      od.step(nthread=nthread)
+    rates[bits] = (nworld * nsteps / (time.perf_counter() - t0), time.perf_counter() - t0)
   return dict(
-    value=nworld * nsteps / dt,
+    value=rates[64][0],
     unit="env-steps/s",
     cores=nthread,
     kind="port",
-    sample=f"fp64 C oracle (oracle/oracle.c), {model}, {nworld} worlds x {nsteps} steps with ctrl noise, "
-    f"{nthread} OpenMP threads, {dt:.1f} s; the reference's Warp-CPU path is not runnable here (no warp/mujoco)",
+    value_fp32=rates[32][0],
+    host_nproc=nproc,
+    host_cpus_allowed=allowed,
+    cpu_model=cpu_model,
+    sample=f"C oracle (oracle/oracle.c), {model}, {nworld} worlds x {nsteps} steps with ctrl noise, {nthread} OpenMP "
+    f"threads (host: {nproc} logical CPUs, {allowed} allowed), fp64 {rates[64][1]:.1f} s (value), fp32 "
+    f"{rates[32][1]:.1f} s (value_fp32); the reference's Warp-CPU path is not runnable here (no warp/mujoco)",
   )
+
+
+def pmc_traffic(path, model, nworld, solver_name, sparse):
+  """HBM bytes per launch from a committed rocprofv3 PMC summary, only when that summary was taken on the
+  same workload AND on a kernel build from the current sources (its `csrc_sha` equals build.sources_hash())."""
+  from mujoco_warp_amd import build as _build
+
+  if not os.path.exists(path):
+    return None, "no PMC summary"
+  with open(path) as f:
+    pmc = json.load(f)
+  if pmc.get("solver", "CG") != solver_name or pmc.get("nworld") != nworld or pmc.get("model", "humanoid") != model:
+    return None, f"PMC summary {os.path.basename(path)} is for another workload"
+  if pmc.get("csrc_sha") != _build.sources_hash():
+    return None, f"PMC summary {os.path.basename(path)} predates the current kernel sources"
+  fk = pmc.get("kernels", {}).get("forward", {})
+  # sparse path: the timed region is forward (x2 around the convex pre-pass) + solve
+  key = "hbm_bytes_per_step_forward_plus_solve" if sparse else "hbm_bytes_per_launch"
+  return fk.get(key), os.path.basename(path)
+
+
+def _free_port():
+  import socket
+
+  s = socket.socket()
+  s.bind(("127.0.0.1", 0))
+  port = s.getsockname()[1]
+  s.close()
+  return port
+
+
+def launch_ranks(nranks):
+  """`bench.py --gpus N` run directly: this parent never touches HIP; it starts N ranks through
+  torch.distributed.run (one process per GPU) as a child and exits with its status."""
+  import subprocess
+
+  env = dict(os.environ)
+  env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
+         "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+  return subprocess.call(cmd, env=env)
 
 
 def main():
   args = parse()
+  if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    sys.exit(launch_ranks(args.gpus))
+
   import torch
   import torch.distributed as dist
 
   import mujoco_warp_amd as mjw
   from mujoco_warp_amd import mjcf
+  from mujoco_warp_amd.shard import strong_shard, weak_shard
 
   rank = int(os.environ.get("RANK", "0"))
   world = int(os.environ.get("WORLD_SIZE", "1"))
   local = int(os.environ.get("LOCAL_RANK", "0"))
+  if world != args.gpus:
+    raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
   if world > 1:
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-  dev = torch.device("cuda", local)
+    # the barrier and the max/sum of scalars go over gloo (host); the data path has no collective
+    dist.init_process_group("gloo")
+  # one rank per GPU; more ranks than devices (a rehearsal on a 1-GPU box) share them round-robin
+  ndev = torch.cuda.device_count()
+  if ndev == 0:
+    raise SystemExit("bench.py needs a ROCm device")
+  dev = torch.device("cuda", local % ndev)
+  torch.cuda.set_device(dev)
+
+  if args.scaling == "weak":
+    offset, nworld = weak_shard(args.nworld, rank)
+  else:
+    offset, nworld = strong_shard(args.nworld, rank, world)
 
   cfg = MODELS[args.model]
   mjm = mjcf.load_model(os.path.join(ROOT, cfg["path"]))
@@ -179,14 +274,18 @@ def main():
     mjcf.reset_data_keyframe(mjm, mjd, cfg["key"])
     center = torch.as_tensor(np.asarray(mjm.key_ctrl[cfg["key"]], dtype=np.float32), device=dev)
   m = mjw.put_model(mjm, device=dev)
-  d = mjw.put_data(mjm, mjd, nworld=args.nworld, nconmax=args.nconmax, njmax=args.njmax, device=dev, m=m)
-  d.world_offset = rank * args.nworld
+  d = mjw.put_data(mjm, mjd, nworld=nworld, nconmax=args.nconmax, njmax=args.njmax, device=dev, m=m)
+  d.world_offset = offset
 
   from mujoco_warp_amd.forward import step_timed
 
+  graph = None
+
   def one_step(i, ev=None):
     mjw.ctrl_noise(m, d, i, center=center)
-    if ev is None:
+    if graph is not None:
+      graph.replay()
+    elif ev is None:
       mjw.step(m, d)
     else:
       step_timed(m, d, *ev)
@@ -194,56 +293,70 @@ def main():
   for i in range(args.warmup):
     one_step(i)
   torch.cuda.synchronize()
+  if args.graph:
+    # capture after warmup (benchmark.py:123-155 captures fn(m, d) once and replays it every step)
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+      mjw.step(m, d)
+    # capture does not execute: the state is unchanged, the replays below advance it
+    torch.cuda.synchronize()
   # sizes for the algorithmic-bytes figure (untimed)
   nefc_mean = float(d.nefc.float().mean())
-  ncon_mean = float(d.nacon[0]) / args.nworld
+  ncon_mean = float(d.nacon[0]) / nworld
 
-  events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
-  for ev in events:  # torch creates the HIP event on first record; mjw_step_events re-records it
-    for e in ev:
-      e.record()
+  events = None
+  if graph is None:
+    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    for ev in events:  # torch creates the HIP event on first record; mjw_step_events re-records it
+      for e in ev:
+        e.record()
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   for i in range(args.steps):
-    one_step(args.warmup + i, events[i])
+    one_step(args.warmup + i, None if events is None else events[i])
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   elapsed = time.perf_counter() - t0
-  fwd_ms = float(np.mean([a.elapsed_time(b) for a, b, c in events]))
-  dense_ms = float(np.mean([b.elapsed_time(c) for a, b, c in events]))
+  if events is not None:
+    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b, c in events]))
+    dense_ms = float(np.mean([b.elapsed_time(c) for a, b, c in events]))
+  else:
+    fwd_ms = dense_ms = float("nan")
   kernel_ms = fwd_ms
   nefc_mean = 0.5 * (nefc_mean + float(d.nefc.float().mean()))
-  ncon_mean = 0.5 * (ncon_mean + float(d.nacon[0]) / args.nworld)
+  ncon_mean = 0.5 * (ncon_mean + float(d.nacon[0]) / nworld)
   converged = int((~torch.isnan(d.qpos).any(dim=1)).sum())
+  if args.dump_qpos:
+    os.makedirs(args.dump_qpos, exist_ok=True)
+    np.savez(os.path.join(args.dump_qpos, f"qpos_rank{rank}.npz"), qpos=d.qpos.cpu().numpy(), offset=offset)
 
+  total_worlds = nworld
   if world > 1:
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kernel_ms, dense_ms], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms = float(t[0]), float(t[1])
-    c = torch.tensor([converged], dtype=torch.int64, device=dev)
+    elapsed, kernel_ms, dense_ms = (float(x) for x in t)
+    c = torch.tensor([converged, nworld], dtype=torch.int64)
     dist.all_reduce(c)
-    converged = int(c[0])
+    converged, total_worlds = int(c[0]), int(c[1])
 
-  total_steps = args.nworld * world * args.steps
-  value = total_steps / elapsed
+  value = total_worlds * args.steps / elapsed
   if rank == 0:
     words = step_words(mjm, m.nv_pad, bool(m.is_sparse))
     # a sparse efc row carries njrow values + njrow column indices instead of an nv_pad dense row
     fwd_b, dense_b = b_alg_parts(words, nefc_mean, ncon_mean, 2 * m.njrow if m.is_sparse else m.nv_pad)
-    bytes_per_launch = fwd_b * args.nworld
+    bytes_per_launch = fwd_b * nworld
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.pmc):
-      with open(args.pmc) as f:
-        pmc = json.load(f)
-      if pmc.get("solver", "CG") == solver_name and pmc.get("nworld") == args.nworld and pmc.get("model", "humanoid") == args.model:
-        fk = pmc.get("kernels", {}).get("forward", {})
-        # sparse path: the timed region is forward (x2 around the convex pre-pass) + solve
-        traffic = fk.get("hbm_bytes_per_step_forward_plus_solve") if m.is_sparse else fk.get("hbm_bytes_per_launch")
+    traffic, traffic_src = pmc_traffic(args.pmc, args.model, nworld, solver_name, bool(m.is_sparse))
+    if args.scaling == "weak":
+      parallelism = f"{args.nworld} worlds per rank on {world} GPU(s) (weak), no collective"
+    else:
+      parallelism = f"{args.nworld} worlds split over {world} GPU(s) (strong), no collective"
     out = {
       "metric": METRIC if args.model == "humanoid" else f"env-steps/sec (whole node), {args.model} nworld={args.nworld} per GPU",
       "value": value,
@@ -253,18 +366,21 @@ def main():
       "warmup": args.warmup,
       "ms_per_step": elapsed / args.steps * 1e3,
       "higher_is_better": True,
-      "scaling": "weak",
+      "scaling": args.scaling,
       "vs_baseline": None,
       "dtype": "fp32",
       "data": "synthetic (keyframe state + OU/Halton ctrl noise of benchmark.py, no dataset)",
       "config": {
-        "workload": f"{os.path.basename(cfg['path'])} ({args.model}) nworld={args.nworld} per GPU fp32, "
+        "workload": f"{os.path.basename(cfg['path'])} ({args.model}) nworld={args.nworld} "
+        f"{'per GPU' if args.scaling == 'weak' else 'total'} fp32, "
         f"{['Euler', 'RK4', 'implicit', 'implicitfast'][int(mjm.opt.integrator)]}+{solver_name}, 1xMI355X per rank",
-        "nworld_per_gpu": args.nworld,
+        "nworld_per_gpu": nworld,
+        "nworld_total": total_worlds,
         "nconmax": args.nconmax,
         "njmax": args.njmax,
         "solver": solver_name,
-        "parallelism": f"worlds sharded over {world} GPU(s), no collective",
+        "parallelism": parallelism,
+        "graph": bool(args.graph),
         "converged_worlds": converged,
         "nefc_mean": nefc_mean,
         "ncon_mean": ncon_mean,
@@ -277,6 +393,7 @@ def main():
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic,
+        "traffic_source": traffic_src,
         "kernel": ("mjw::sp::forward_kernel + mjw::sp::solve_kernel (sparse path: forward + CG)" if m.is_sparse else
                    "mjw::mjw_kernel<79> (forward: position/velocity/actuation/qfrc_smooth)"
                    + (" + mjw::ccd_kernel (convex pre-pass)" if m.nxn_ccd else "")),
@@ -287,7 +404,7 @@ def main():
            "mjw::dense_kernel (factor/solve/Euler)" + (" + mjw::sensor_acc_kernel" if m.nsensor else "")): {
             "ms": dense_ms,
             "alg_bytes_per_env_step": dense_b,
-            "achieved_GBs": dense_b * args.nworld / (dense_ms * 1e-3) / 1e9,
+            "achieved_GBs": dense_b * nworld / (dense_ms * 1e-3) / 1e9,
           }
         },
         "step_alg_bytes_per_env_step": fwd_b + dense_b,

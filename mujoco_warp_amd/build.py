@@ -12,6 +12,18 @@ OUT = os.path.join(_PKG, "libmjw_amd.so")
 ARCH = os.environ.get("MJW_OFFLOAD_ARCH", "gfx950")
 
 
+def sources_hash():
+  """Short sha256 over the kernel sources and headers: binds a committed rocprof summary to the build it
+  was taken on (bench.py reports PMC traffic only when the hashes agree)."""
+  import hashlib
+
+  h = hashlib.sha256()
+  for p in sorted(SOURCES + HEADERS):
+    with open(p, "rb") as f:
+      h.update(os.path.basename(p).encode() + b"\0" + f.read())
+  return h.hexdigest()[:16]
+
+
 def needs_build():
   if not os.path.exists(OUT):
     return True

@@ -1129,7 +1129,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         const float* rec = s + L.con + lane * CREC;
         int condim = reinterpret_cast<const int*>(rec)[28];
         float pos = rec[0] - rec[1];
-        nrow = pos < 0.0f ? (condim == 1 ? 1 : 2 * (condim - 1)) : 0;
+        // a contact past the global pool is dropped with its rows (collision_core.py:212-231)
+        nrow = (pos < 0.0f && gbase + lane < d.naconmax) ? (condim == 1 ? 1 : 2 * (condim - 1)) : 0;
         reinterpret_cast<int*>(s + L.con + lane * CREC)[31] = gbase + lane;
       }
       int rincl = wave_scan_incl(nrow);
@@ -1171,7 +1172,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         int condim = reci[28];
         int r0 = si[L.iscratch + cc];
         float pos = rec[0] - rec[1];
-        if (!(pos < 0.0f)) continue;
+        if (!(pos < 0.0f) || gbase + cc >= d.naconmax) continue;
         int nr = condim == 1 ? 1 : 2 * (condim - 1);
         const int b1 = reci[21] & 0xffff, b2 = reci[21] >> 16;
         const float* cpos = rec + 2;
@@ -2125,6 +2126,13 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
 }
 
 // benchmark.py:41-83
+// clears the contact pool counters at the start of the position stage.  A kernel, not
+// hipMemsetAsync: in a captured hipGraph the 4-byte memset node was observed to race the
+// forward kernel (stale counts, contacts dropped past the pool), kernel nodes stay ordered
+__global__ void reset_counters_kernel(int* nacon, int* ncollision) {
+  if (threadIdx.x == 0) { nacon[0] = 0; ncollision[0] = 0; }
+}
+
 __global__ void ctrl_noise_kernel(const mjw_model_t m, const mjw_data_t d, const float* center, int step, float std, float rate_) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.nworld * m.nu) return;
@@ -2170,8 +2178,8 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   lds += lds_pad;
   if (lds > 160 * 1024) { g_err = std::string(name) + ": per-world LDS working set exceeds 160 KiB"; return -3; }
   if (STAGES & mjw::ST_POS) {
-    hipError_t e = hipMemsetAsync(d->nacon, 0, sizeof(int32_t), s);
-    if (e == hipSuccess) e = hipMemsetAsync(d->ncollision, 0, sizeof(int32_t), s);
+    hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(e, name);
     if (m->nxn_ccd > 0 && d->naconmax > 0 && !(m->opt_disableflags & (mjw::DSBL_CONSTRAINT | mjw::DSBL_CONTACT))) {
       static std::once_flag once_ccd;
@@ -2208,8 +2216,8 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     // workgroup-per-world sparse / flex pipeline (mjw_sparse.hip); no sensors on this path
     hipStream_t s = (hipStream_t)stream;
     if (stages & ST_POS) {
-      hipError_t e = hipMemsetAsync(d->nacon, 0, sizeof(int32_t), s);
-      if (e == hipSuccess) e = hipMemsetAsync(d->ncollision, 0, sizeof(int32_t), s);
+      hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision);
+      hipError_t e = hipGetLastError();
       if (e != hipSuccess) return set_err(e, name);
     }
     if (g_ev[0]) (void)hipEventRecord(g_ev[0], s);

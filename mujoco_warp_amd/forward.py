@@ -44,16 +44,27 @@ def step_timed(m: Model, d: Data, ev_begin, ev_mid, ev_end):
   _lib.check(rc, "mjw_step_events")
 
 
+# callbacks whose reference call sites fall inside one fused launch of this path: act_dyn / act_gain /
+# act_bias run between _actuator_force and the moment map (forward.py:876-881), contactfilter between
+# the narrowphase and make_constraint (collision_driver.py:788); they are refused instead of being run
+# where they could no longer change the step
+_UNSUPPORTED_CALLBACKS = {
+  "act_dyn": "forward.py:876", "act_gain": "forward.py:878", "act_bias": "forward.py:880", "contactfilter": "collision_driver.py:788",
+}
+
+
 def _has_callbacks(m: Model) -> bool:
   cb = m.callback
-  return any(getattr(cb, f) is not None for f in ("control", "passive", "act_dyn", "act_gain", "act_bias", "contactfilter"))
+  for f, where in _UNSUPPORTED_CALLBACKS.items():
+    if getattr(cb, f) is not None:
+      raise NotImplementedError(f"callback.{f} (called at reference {where}) is not supported: the stage it hooks into is one fused HIP launch")
+  return any(getattr(cb, f) is not None for f in ("control", "passive"))
 
 
 def fwd_position(m: Model, d: Data):
   """Position-dependent computations (forward.py:513-537)."""
+  _has_callbacks(m)
   _call("mjw_fwd_position", m, d)
-  if m.callback.contactfilter is not None:
-    m.callback.contactfilter(m, d)
 
 
 def fwd_velocity(m: Model, d: Data):
@@ -65,6 +76,7 @@ def fwd_velocity(m: Model, d: Data):
 
 def fwd_actuation(m: Model, d: Data):
   """Actuation-dependent computations (forward.py:836-927)."""
+  _has_callbacks(m)
   _call("mjw_fwd_actuation", m, d)
 
 

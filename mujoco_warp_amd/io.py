@@ -313,7 +313,8 @@ def put_model(mjm, device=None) -> types.Model:
       continue
     setattr(m, name, _i32(np.asarray(getattr(mjm, name)), dev))
   # extra reference fields kept for API parity
-  for name in ("dof_Madr", "M_rownnz", "M_rowadr", "M_colind", "mapM2M", "body_geomnum", "body_geomadr", "geom_contype", "geom_conaffinity", "exclude_signature"):
+  for name in ("dof_Madr", "M_rownnz", "M_rowadr", "M_colind", "mapM2M", "body_geomnum", "body_geomadr", "geom_contype", "geom_conaffinity", "exclude_signature",
+               "eq_active0", "body_mocapid"):
     if hasattr(mjm, name):
       setattr(m, name, _i32(np.asarray(getattr(mjm, name)), dev))
   m._mjm_sizes = dict(nq=mjm.nq, nv=nv)
@@ -430,7 +431,22 @@ def _default_njmax(mjm, mjd=None) -> int:
   return int(vs[np.searchsorted(vs, njmax)])
 
 
-def _alloc_data(m, nworld, nconmax, njmax, naconmax, device):
+def _resolve_batch_size(na, n, nworld, default):
+  """io.py:850-855."""
+  if na is not None:
+    return na
+  if n is not None:
+    return n * nworld
+  return default
+
+
+def _alloc_data(m, nworld, nconmax, njmax, naconmax, device, nccdmax=None, njmax_nnz=None, naccdmax=None):
+  """Sizes and checks of make_data (io.py:885-932), then the device arrays.
+
+  nccdmax / naccdmax bound the convex (GJK/EPA) contacts in the reference's separate CCD pool; here the
+  convex pre-pass writes into a fixed per-pair slot (Data.ccd_out) and its contacts join the one pool, so
+  they are validated and recorded only.  njmax_nnz (sparse J non-zeros) is recorded: the sparse path keeps
+  efc_J slot-major with a fixed row width m.njrow, so njmax * njrow values are allocated."""
   if nworld < 1:
     raise ValueError("nworld must be >= 1")
   if nconmax is None:
@@ -441,15 +457,27 @@ def _alloc_data(m, nworld, nconmax, njmax, naconmax, device):
     raise ValueError("nconmax must be >= 0")
   if njmax < 0:
     raise ValueError("njmax must be >= 0")
-  if naconmax is None:
-    naconmax = nconmax * nworld
+  naconmax = _resolve_batch_size(naconmax, nconmax, nworld, 0)
   if naconmax < 0:
     raise ValueError("naconmax must be >= 0")
+  naccdmax = _resolve_batch_size(naccdmax, nccdmax, nworld, naconmax)
+  if naccdmax < 0:
+    raise ValueError("naccdmax must be >= 0")
+  elif naccdmax > naconmax:
+    raise ValueError(f"naccdmax ({naccdmax}) must be <= naconmax ({naconmax})")
+  if nccdmax is None:
+    nccdmax = nconmax
+  elif nccdmax < 0:
+    raise ValueError("nccdmax must be >= 0")
+  elif nccdmax > nconmax:
+    raise ValueError(f"nccdmax ({nccdmax}) must be <= nconmax ({nconmax})")
+  if njmax_nnz is None:
+    njmax_nnz = njmax * m.nv
   njmax_pad, _ = _padded_sizes(m.nv, njmax, False)
   real, ints, creal, cint = _data_shapes(m, nworld, njmax, njmax_pad, naconmax)
   d = types.Data()
   d.nworld, d.njmax, d.njmax_pad, d.naconmax, d.nconmax = nworld, njmax, njmax_pad, naconmax, nconmax
-  d.njmax_nnz = njmax * m.nv
+  d.njmax_nnz, d.nccdmax, d.naccdmax = int(njmax_nnz), int(nccdmax), int(naccdmax)
   d.world_offset = 0
   d.device = device
   d.efc = types.Constraint()
@@ -512,12 +540,14 @@ def cdata(d: types.Data) -> _lib.CData:
   return c
 
 
-def make_data(mjm, nworld: int = 1, nconmax: Optional[int] = None, njmax: Optional[int] = None, naconmax: Optional[int] = None, device=None, m: Optional[types.Model] = None) -> types.Data:
-  """Creates a data object on device (io.py:859) initialised to qpos0 / zero state."""
+def make_data(mjm, nworld: int = 1, nconmax: Optional[int] = None, nccdmax: Optional[int] = None, njmax: Optional[int] = None,
+              njmax_nnz: Optional[int] = None, naconmax: Optional[int] = None, naccdmax: Optional[int] = None, device=None,
+              m: Optional[types.Model] = None) -> types.Data:
+  """Creates a data object on device (io.py:859-868) initialised to qpos0 / zero state."""
   dev = _device(device)
   if m is None:
     m = put_model(mjm, device=dev)
-  d = _alloc_data(m, nworld, nconmax, njmax, naconmax, dev)
+  d = _alloc_data(m, nworld, nconmax, njmax, naconmax, dev, nccdmax=nccdmax, njmax_nnz=njmax_nnz, naccdmax=naccdmax)
   d.qpos[:] = torch.as_tensor(np.asarray(mjm.qpos0, dtype=np.float32), device=dev)
   if m.neq:  # int32 on the device (the reference's bool), initialised from eq_active0
     d.eq_active[:] = torch.as_tensor(np.asarray(mjm.eq_active0, dtype=np.int32), device=dev)
@@ -547,7 +577,7 @@ def put_data(mjm, mjd, nworld: int = 1, nconmax: Optional[int] = None, nccdmax: 
     raise ValueError(f"nconmax overflow (nconmax must be >= {ncon})")
   if int(getattr(mjd, "nefc", 0)) > njmax:
     raise ValueError(f"njmax overflow (njmax must be >= {mjd.nefc})")
-  d = _alloc_data(m, nworld, nconmax, njmax, naconmax, dev)
+  d = _alloc_data(m, nworld, nconmax, njmax, naconmax, dev, nccdmax=nccdmax, njmax_nnz=njmax_nnz, naccdmax=naccdmax)
 
   def tile(name, val, shape):
     if val is None:
@@ -642,17 +672,54 @@ def get_data_into(result, mjm, d: types.Data, world_id: int = 0):
 
 
 def reset_data(m: types.Model, d: types.Data, reset: Optional[torch.Tensor] = None):
-  """Resets worlds (all, or where `reset` is True) to the model's default state (io.py:1458)."""
-  mask = torch.ones(d.nworld, dtype=torch.bool, device=d.qpos.device) if reset is None else reset.to(torch.bool)
+  """Clear data, set defaults; optionally by world (io.py:1458-1691).
+
+  For every world where `reset` is True (all worlds when it is None): qpos <- qpos0 (batched, indexed by
+  world), eq_active <- eq_active0, mocap_pos / mocap_quat <- body_pos / body_quat of the mocap bodies;
+  qvel, act, ctrl, qacc_warmstart, qfrc_applied, xfrc_applied, qacc, act_dot, sensordata, energy, time, qM,
+  solver_niter and the ne / nf / nl / nefc counters cleared; that world's contacts in the global pool
+  cleared (efc_address -1, reset_contact :1575-1622).  The pool counter nacon is cleared only when world 0
+  is reset (the reference does it from world 0's thread, :1558-1559), and after the contact clear
+  (the clear reads nacon, :1577)."""
+  dev = d.qpos.device
+  mask = torch.ones(d.nworld, dtype=torch.bool, device=dev) if reset is None else reset.to(device=dev, dtype=torch.bool)
+  if mask.shape != (d.nworld,):
+    raise ValueError(f"reset mask must have shape ({d.nworld},), got {tuple(mask.shape)}")
   idx = torch.nonzero(mask).reshape(-1)
   if idx.numel() == 0:
     return
-  qpos0 = m.qpos0[0] if m.qpos0.shape[0] == 1 else m.qpos0[idx]
-  d.qpos[idx] = qpos0
-  for name in ("qvel", "act", "ctrl", "qacc_warmstart", "qfrc_applied", "xfrc_applied", "qacc", "act_dot"):
+  gid = idx  # world ids of this Data (batched model fields are indexed worldid % nb)
+
+  def _rows(t):
+    return t[0] if t.shape[0] == 1 else t[gid % t.shape[0]]
+
+  # contacts of the reset worlds (before nacon is touched)
+  nacon = min(int(d.nacon[0]), d.naconmax)
+  if nacon:
+    wid = d.contact.worldid[:nacon].long()
+    hit = torch.nonzero((wid < 0) | mask[wid.clamp(min=0)]).reshape(-1)
+    if hit.numel():
+      for f in ("dist", "pos", "frame", "includemargin", "friction", "solref", "solreffriction", "solimp", "dim", "geom", "flex", "vert",
+                "worldid", "type", "geomcollisionid"):
+        getattr(d.contact, f)[hit] = 0
+      d.contact.efc_address[hit] = -1
+  d.qpos[idx] = _rows(m.qpos0)
+  for name in ("qvel", "act", "ctrl", "qacc_warmstart", "qfrc_applied", "xfrc_applied", "qacc", "act_dot", "sensordata", "energy", "qM"):
+    t = getattr(d, name)
+    if t.numel():
+      t[idx] = 0
+  for name in ("time", "solver_niter", "ne", "nf", "nl", "nefc"):
     getattr(d, name)[idx] = 0
-  d.time[idx] = 0
-  d.solver_niter[idx] = 0
+  if d.eq_active.numel():
+    d.eq_active[idx] = m.eq_active0.to(torch.int32)
+  if d.mocap_pos.numel():
+    bodies = torch.nonzero(m.body_mocapid >= 0).reshape(-1)
+    mid = m.body_mocapid[bodies].long()
+    bp, bq = _rows(m.body_pos), _rows(m.body_quat)  # (nbody, k) or (nreset, nbody, k)
+    d.mocap_pos[idx.view(-1, 1), mid.view(1, -1)] = bp[..., bodies, :] if bp.dim() == 3 else bp[bodies].expand(idx.numel(), -1, -1)
+    d.mocap_quat[idx.view(-1, 1), mid.view(1, -1)] = bq[..., bodies, :] if bq.dim() == 3 else bq[bodies].expand(idx.numel(), -1, -1)
+  if bool(mask[0]):
+    d.nacon.zero_()
 
 
 def override_model(model, overrides: Sequence[str] | dict):

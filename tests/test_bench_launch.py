@@ -1,0 +1,78 @@
+"""bench.py as the driver runs it: `--gpus N` starts N ranks itself (one process per GPU, gloo barrier,
+no collective on the data path), weak and strong sharding, hipGraph replay.
+
+On the 1-GPU box the two ranks share the device round-robin; each rank's final qpos must equal the
+matching world range of a single-process run of the same global worlds (ctrl noise is indexed by global
+world id through world_offset)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, timeout=240):
+  env = dict(os.environ)
+  env.pop("WORLD_SIZE", None)
+  env.pop("RANK", None)
+  env.pop("LOCAL_RANK", None)
+  out = subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+  assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+  lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+  assert len(lines) == 1, out.stdout
+  return json.loads(lines[0])
+
+
+def test_launcher_command_without_gpu(monkeypatch):
+  """`--gpus 2` with no WORLD_SIZE re-launches itself through torch.distributed.run (parent never touches HIP)."""
+  sys.path.insert(0, ROOT)
+  import bench
+
+  seen = {}
+
+  def fake_call(cmd, env=None):
+    seen["cmd"], seen["env"] = cmd, env
+    return 0
+
+  monkeypatch.setattr(subprocess, "call", fake_call)
+  monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+  assert bench.launch_ranks(2) == 0
+  cmd = seen["cmd"]
+  assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=2" in cmd
+  assert "127.0.0.1" in cmd and cmd[-4:] == ["--gpus", "2", "--steps", "3"]
+  assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+@pytest.mark.gpu
+def test_gpu_bench_two_ranks_weak_equals_single(tmp_path):
+  common = ["--steps", "5", "--warmup", "2", "--cpu-baseline", "0"]
+  two = _run(["--gpus", "2", "--nworld", "256", "--dump-qpos", str(tmp_path / "two")] + common)
+  assert two["n_gpus"] == 2 and two["scaling"] == "weak"
+  assert two["config"]["nworld_total"] == 512 and two["config"]["converged_worlds"] == 512
+  one = _run(["--gpus", "1", "--nworld", "512", "--dump-qpos", str(tmp_path / "one")] + common)
+  assert one["n_gpus"] == 1
+  q1 = np.load(tmp_path / "one" / "qpos_rank0.npz")["qpos"]
+  for r in range(2):
+    z = np.load(tmp_path / "two" / f"qpos_rank{r}.npz")
+    off = int(z["offset"])
+    assert off == 256 * r
+    np.testing.assert_array_equal(z["qpos"], q1[off:off + 256])
+
+
+@pytest.mark.gpu
+def test_gpu_bench_two_ranks_strong_and_graph(tmp_path):
+  common = ["--steps", "5", "--warmup", "2", "--cpu-baseline", "0", "--nworld", "301"]
+  strong = _run(["--gpus", "2", "--scaling", "strong", "--dump-qpos", str(tmp_path / "s")] + common)
+  assert strong["scaling"] == "strong" and strong["config"]["nworld_total"] == 301
+  graph = _run(["--gpus", "1", "--graph", "1", "--dump-qpos", str(tmp_path / "g")] + common)
+  assert graph["config"]["graph"] is True
+  qg = np.load(tmp_path / "g" / "qpos_rank0.npz")["qpos"]
+  got = [np.load(tmp_path / "s" / f"qpos_rank{r}.npz") for r in range(2)]
+  assert [int(z["offset"]) for z in got] == [0, 151]
+  np.testing.assert_array_equal(np.concatenate([z["qpos"] for z in got]), qg)

@@ -2,7 +2,7 @@
 # rocprofv3 passes for the round's profiles/: kernel-trace stats of the bench command, then
 # FETCH_SIZE and WRITE_SIZE in separate passes (never combined with trace domains).
 cd "$(dirname "$0")/.." || exit 1
-R=${ROUND:-r01}
+R=${ROUND:-r02}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 rm -rf gpurun_out/prof_stats gpurun_out/prof_fetch gpurun_out/prof_write

@@ -3,7 +3,7 @@
 # then FETCH_SIZE and WRITE_SIZE in separate passes (never combined with trace domains).
 cd "$(dirname "$0")/.." || exit 1
 M=${1:-aloha_cloth}
-R=${ROUND:-r01}
+R=${ROUND:-r02}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 rm -rf gpurun_out/sprof_stats gpurun_out/sprof_fetch gpurun_out/sprof_write

@@ -50,7 +50,10 @@ def main():
   fetch = counter_avg(fetch_dir, "FETCH_SIZE")
   write = counter_avg(write_dir, "WRITE_SIZE")
   stats = rows(stats_dir, "*kernel_stats.csv")
-  res = {"nworld": nworld, "solver": solver, "model": model, "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024",
+  sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+  from mujoco_warp_amd import build as _build
+
+  res = {"nworld": nworld, "solver": solver, "model": model, "csrc_sha": _build.sources_hash(), "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024",
          "kernels": {}}
   for k, pat in KERNELS.items():
     f, nf = fetch[k]
