@@ -15,11 +15,14 @@ offset by rank) or `--scaling strong` splits --nworld over the ranks; no
 collective on the data path: a gloo (host) barrier + max-over-ranks of the
 elapsed time brackets the timed region.
 
-A step is two kernels on the torch stream: the forward kernel
+A step is a counter reset and two kernels on the torch stream: the forward kernel
 mjw::mjw_kernel<79> (kinematics, com, crb/qM, collision, constraint rows,
 transmission, velocity, rne, actuation, qfrc_smooth) and the dense kernel
-mjw::dense_kernel<7,false> (Cholesky + M^-1, CG solve, Euler).  Both are timed
-live with HIP events recorded on that stream around each launch (mjw_step_events).
+mjw::dense_kernel<7,false> (Cholesky + M^-1, CG solve, Euler).  As in the
+reference's benchmark (benchmark.py:123-155) the step is captured once as a
+hipGraph and replayed every step, the control noise launched before each replay;
+every 10th timed step instead runs eagerly with HIP events recorded on that stream
+around each kernel (mjw_step_events), which gives the per-kernel durations.
 
 Also reported: `roofline` for the dominant (forward) kernel: its algorithmic
 bytes per env-step (SURVEY.md 8(d)'s B_alg split by kernel) x nworld
@@ -112,10 +115,16 @@ def parse():
   p.add_argument("--cpu-worlds", type=int, default=None, help="CPU baseline sample worlds (default: the config's, 1024)")
   p.add_argument("--cpu-steps", type=int, default=None, help="CPU baseline sample steps (default: the config's, 1000)")
   p.add_argument("--pmc", default=None, help="PMC traffic summary (default: the newest profiles/pmc_<model>_rNN.json)")
-  p.add_argument("--graph", type=int, default=0, help="capture mjw.step once as a hipGraph and replay it every step "
-                 "(benchmark.py:123-155: ctrl noise is launched outside the graph); per-kernel events are then unavailable")
+  p.add_argument("--graph", type=int, default=1, help="capture mjw.step once as a hipGraph and replay it every step "
+                 "(benchmark.py:123-155: ctrl noise is launched outside the graph); 0 = launch the step eagerly")
+  p.add_argument("--event-every", type=int, default=10,
+                 help="every E-th timed step runs eagerly with HIP events around its kernels (the per-kernel "
+                 "durations of `roofline`); the others replay the graph (events on every step cost ~6%%)")
   p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                  help="weak: --nworld worlds per rank; strong: --nworld worlds in total, split over the ranks")
+  p.add_argument("--streams", type=int, default=1,
+                 help="independent world shards per rank, each with its own Data and HIP stream (measured slower "
+                 "than one batch on the humanoid: 12.2 vs 13.9 M env-steps/s)")
   p.add_argument("--dump-qpos", default=None, help="directory: each rank writes its final qpos + world offset (tests)")
   a = p.parse_args()
   cfg = MODELS[a.model]
@@ -192,7 +201,8 @@ def cpu_baseline(mjm, nworld, nsteps, key, njmax, nconmax, model):
 
 def pmc_traffic(path, model, nworld, solver_name, sparse):
   """HBM bytes per launch from a committed rocprofv3 PMC summary, only when that summary was taken on the
-  same workload AND on a kernel build from the current sources (its `csrc_sha` equals build.sources_hash())."""
+  same workload (`nworld` = worlds per launch) AND on a kernel build from the current sources (its
+  `csrc_sha` equals build.sources_hash())."""
   from mujoco_warp_amd import build as _build
 
   if not os.path.exists(path):
@@ -274,67 +284,88 @@ def main():
     mjcf.reset_data_keyframe(mjm, mjd, cfg["key"])
     center = torch.as_tensor(np.asarray(mjm.key_ctrl[cfg["key"]], dtype=np.float32), device=dev)
   m = mjw.put_model(mjm, device=dev)
-  d = mjw.put_data(mjm, mjd, nworld=nworld, nconmax=args.nconmax, njmax=args.njmax, device=dev, m=m)
-  d.world_offset = offset
+  # the rank's worlds run as `--streams` independent shards (own Data, own HIP stream, world ids
+  # offset like ranks), so one shard's launch tail overlaps the other's next kernels; nothing
+  # synchronises the shards inside the timed region
+  nshard = max(1, min(args.streams, nworld))
+  shards = []
+  for k in range(nshard):
+    soff, scnt = strong_shard(nworld, k, nshard)
+    dk = mjw.put_data(mjm, mjd, nworld=scnt, nconmax=args.nconmax, njmax=args.njmax, device=dev, m=m)
+    dk.world_offset = offset + soff
+    shards.append(dk)
+  # one batch runs on the current stream; shards each get a stream of their own (not the legacy
+  # default stream, which would synchronise with the others)
+  streams = [torch.cuda.current_stream(dev)] if nshard == 1 else [torch.cuda.Stream(device=dev) for _ in range(nshard)]
 
   from mujoco_warp_amd.forward import step_timed
 
-  graph = None
+  graphs = None
 
   def one_step(i, ev=None):
-    mjw.ctrl_noise(m, d, i, center=center)
-    if graph is not None:
-      graph.replay()
-    elif ev is None:
-      mjw.step(m, d)
-    else:
-      step_timed(m, d, *ev)
+    for k, (dk, st) in enumerate(zip(shards, streams)):
+      with torch.cuda.stream(st):
+        mjw.ctrl_noise(m, dk, i, center=center)
+        if ev is not None and k == 0:
+          step_timed(m, dk, *ev)  # shard 0's kernels are the timed launches
+        elif graphs is not None:
+          graphs[k].replay()
+        else:
+          mjw.step(m, dk)
 
   for i in range(args.warmup):
     one_step(i)
   torch.cuda.synchronize()
   if args.graph:
     # capture after warmup (benchmark.py:123-155 captures fn(m, d) once and replays it every step)
-    s = torch.cuda.Stream(device=dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=s):
-      mjw.step(m, d)
+    graphs = []
+    for dk in shards:
+      cs = torch.cuda.Stream(device=dev)
+      cs.wait_stream(torch.cuda.current_stream(dev))
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g, stream=cs):
+        mjw.step(m, dk)
+      graphs.append(g)
     # capture does not execute: the state is unchanged, the replays below advance it
     torch.cuda.synchronize()
-  # sizes for the algorithmic-bytes figure (untimed)
-  nefc_mean = float(d.nefc.float().mean())
-  ncon_mean = float(d.nacon[0]) / nworld
 
-  events = None
-  if graph is None:
-    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
-    for ev in events:  # torch creates the HIP event on first record; mjw_step_events re-records it
-      for e in ev:
-        e.record()
+  def sizes():
+    nefc = sum(float(dk.nefc.float().sum()) for dk in shards) / nworld
+    ncon = sum(float(dk.nacon[0]) for dk in shards) / nworld
+    return nefc, ncon
+
+  # sizes for the algorithmic-bytes figure (untimed)
+  nefc_mean, ncon_mean = sizes()
+
+  # per-kernel HIP events on every `event_every`-th timed step (every step without a graph)
+  every = 1 if graphs is None else max(1, args.event_every)
+  events = {i: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for i in range(0, args.steps, every)}
+  for ev in events.values():  # torch creates the HIP event on first record; mjw_step_events re-records it
+    for e in ev:
+      e.record()
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   for i in range(args.steps):
-    one_step(args.warmup + i, None if events is None else events[i])
+    one_step(args.warmup + i, events.get(i))
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   elapsed = time.perf_counter() - t0
-  if events is not None:
-    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b, c in events]))
-    dense_ms = float(np.mean([b.elapsed_time(c) for a, b, c in events]))
-  else:
-    fwd_ms = dense_ms = float("nan")
+  fwd_ms = float(np.mean([a.elapsed_time(b) for a, b, c in events.values()]))
+  dense_ms = float(np.mean([b.elapsed_time(c) for a, b, c in events.values()]))
   kernel_ms = fwd_ms
-  nefc_mean = 0.5 * (nefc_mean + float(d.nefc.float().mean()))
-  ncon_mean = 0.5 * (ncon_mean + float(d.nacon[0]) / nworld)
-  converged = int((~torch.isnan(d.qpos).any(dim=1)).sum())
+  n2, c2 = sizes()
+  nefc_mean, ncon_mean = 0.5 * (nefc_mean + n2), 0.5 * (ncon_mean + c2)
+  qpos_all = torch.cat([dk.qpos for dk in shards])
+  converged = int((~torch.isnan(qpos_all).any(dim=1)).sum())
+  solver_niter_mean = float(torch.cat([dk.solver_niter for dk in shards]).float().mean())
   if args.dump_qpos:
     os.makedirs(args.dump_qpos, exist_ok=True)
-    np.savez(os.path.join(args.dump_qpos, f"qpos_rank{rank}.npz"), qpos=d.qpos.cpu().numpy(), offset=offset)
+    np.savez(os.path.join(args.dump_qpos, f"qpos_rank{rank}.npz"), qpos=qpos_all.cpu().numpy(), offset=offset)
+  d = shards[0]
 
   total_worlds = nworld
   if world > 1:
@@ -350,13 +381,16 @@ def main():
     words = step_words(mjm, m.nv_pad, bool(m.is_sparse))
     # a sparse efc row carries njrow values + njrow column indices instead of an nv_pad dense row
     fwd_b, dense_b = b_alg_parts(words, nefc_mean, ncon_mean, 2 * m.njrow if m.is_sparse else m.nv_pad)
-    bytes_per_launch = fwd_b * nworld
+    # worlds per timed forward launch: shard 0's
+    nlaunch = d.nworld
+    bytes_per_launch = fwd_b * nlaunch
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.pmc, args.model, nworld, solver_name, bool(m.is_sparse))
+    traffic, traffic_src = pmc_traffic(args.pmc, args.model, nlaunch, solver_name, bool(m.is_sparse))
     if args.scaling == "weak":
       parallelism = f"{args.nworld} worlds per rank on {world} GPU(s) (weak), no collective"
     else:
       parallelism = f"{args.nworld} worlds split over {world} GPU(s) (strong), no collective"
+    parallelism += f"; {nshard} stream shard(s) per rank"
     out = {
       "metric": METRIC if args.model == "humanoid" else f"env-steps/sec (whole node), {args.model} nworld={args.nworld} per GPU",
       "value": value,
@@ -381,10 +415,12 @@ def main():
         "solver": solver_name,
         "parallelism": parallelism,
         "graph": bool(args.graph),
+        "timed_kernel_launches": len(events),
         "converged_worlds": converged,
         "nefc_mean": nefc_mean,
         "ncon_mean": ncon_mean,
-        "solver_niter_mean": float(d.solver_niter.float().mean()),
+        "solver_niter_mean": solver_niter_mean,
+        "streams": nshard,
       },
       "roofline": {
         "bound": "hbm",
@@ -398,13 +434,14 @@ def main():
                    "mjw::mjw_kernel<79> (forward: position/velocity/actuation/qfrc_smooth)"
                    + (" + mjw::ccd_kernel (convex pre-pass)" if m.nxn_ccd else "")),
         "kernel_ms": kernel_ms,
+        "worlds_per_launch": nlaunch,
         "alg_bytes_per_env_step": fwd_b,
         "other_kernels": {
           ("mjw::sp::euler_kernel" if m.is_sparse else
            "mjw::dense_kernel (factor/solve/Euler)" + (" + mjw::sensor_acc_kernel" if m.nsensor else "")): {
             "ms": dense_ms,
             "alg_bytes_per_env_step": dense_b,
-            "achieved_GBs": dense_b * nworld / (dense_ms * 1e-3) / 1e9,
+            "achieved_GBs": dense_b * nlaunch / (dense_ms * 1e-3) / 1e9,
           }
         },
         "step_alg_bytes_per_env_step": fwd_b + dense_b,

@@ -134,11 +134,12 @@ static __device__ unsigned long long g_prof[PH_N];
 
 // dense (register-resident) factor / solve / euler kernel launcher, mjw_dense.hip
 enum : int { DF_FACTOR = 1, DF_SOLVE = 2, DF_EULER = 4 };
-int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
+// worlds [w0, w0 + count) of d (count < 0: all from w0)
+int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int w0 = 0, int count = -1);
 // post-solve sensors of every stage + rne_postconstraint, mjw_sensor.hip (no-op without sensors)
 enum : int { RK_BEGIN = 0, RK_PERTURB = 1, RK_ACCUM = 2, RK_END = 3 };
 int rk4_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int op, float scale);
-int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages = 7);
+int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages = 7, int w0 = 0, int count = -1);
 // workgroup-per-world pipeline of sparse / flex models (m->is_sparse), mjw_sparse.hip; ST_* stage bits
 int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
 

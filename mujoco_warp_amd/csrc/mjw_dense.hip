@@ -293,7 +293,7 @@ __device__ __forceinline__ float row_force(const Row& w, int& state, float& cost
 // ---- the kernel ---------------------------------------------------------------------------
 template <int FLAGS, bool NEWTON>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
-dense_kernel(const mjw_model_t m, const mjw_data_t d) {
+dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   constexpr bool NT = NEWTON && (FLAGS & DF_SOLVE);
   constexpr int S_OFF = NT ? DJ_WORDS : 0;  // CG: the 32x32 scratch aliases J (used before J is staged)
   constexpr int V_OFF = NT ? DJ_WORDS + DS_WORDS : DJ_WORDS;
@@ -304,7 +304,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d) {
   float* vd2 = vd + 64;          // second dof buffer
   float* vr = vd + 128;          // row vector buffer (64)
   float* vr2 = vd + 192;         // second row buffer (Newton weights)
-  const int wid = blockIdx.x;
+  const int wid = w0 + (int)blockIdx.x;
   if (wid >= d.nworld) return;
   const int lane = threadIdx.x, c = lane & 31, h = lane >> 5;
   const int nv = m.nv, np = m.nv_pad;
@@ -635,29 +635,31 @@ __global__ void __launch_bounds__(64) selftest_kernel(int which, const float* in
 }
 
 template <int FLAGS>
-hipError_t launch_flags(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
+hipError_t launch_flags(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int w0, int count) {
   if (m->opt_solver == SOLVER_NEWTON)
-    hipLaunchKernelGGL((dense_kernel<FLAGS, true>), dim3(d->nworld), dim3(64), 0, s, *m, *d);
+    hipLaunchKernelGGL((dense_kernel<FLAGS, true>), dim3(count), dim3(64), 0, s, *m, *d, w0);
   else
-    hipLaunchKernelGGL((dense_kernel<FLAGS, false>), dim3(d->nworld), dim3(64), 0, s, *m, *d);
+    hipLaunchKernelGGL((dense_kernel<FLAGS, false>), dim3(count), dim3(64), 0, s, *m, *d, w0);
   return hipGetLastError();
 }
 
-int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
+int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int w0, int count) {
+  if (count < 0) count = d->nworld - w0;
+  if (count <= 0) return 0;
   const int fl = m->opt_disableflags;
   const bool implicit_int = m->opt_integrator == INT_IMPLICITFAST
                                 ? (fl & (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) != (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)
                                 : !(fl & (DSBL_EULERDAMP | DSBL_DAMPER));
   if ((flags & DF_EULER) && flags != DF_EULER && implicit_int) {
-    int rc = dense_launch(flags & ~DF_EULER, m, d, s);
-    return rc ? rc : dense_launch(DF_EULER, m, d, s);
+    int rc = dense_launch(flags & ~DF_EULER, m, d, s, w0, count);
+    return rc ? rc : dense_launch(DF_EULER, m, d, s, w0, count);
   }
   switch (flags) {
-    case DF_FACTOR | DF_SOLVE | DF_EULER: return (int)launch_flags<DF_FACTOR | DF_SOLVE | DF_EULER>(m, d, s);
-    case DF_FACTOR | DF_SOLVE: return (int)launch_flags<DF_FACTOR | DF_SOLVE>(m, d, s);
-    case DF_FACTOR: return (int)launch_flags<DF_FACTOR>(m, d, s);
-    case DF_SOLVE: return (int)launch_flags<DF_SOLVE>(m, d, s);
-    case DF_EULER: return (int)launch_flags<DF_EULER>(m, d, s);
+    case DF_FACTOR | DF_SOLVE | DF_EULER: return (int)launch_flags<DF_FACTOR | DF_SOLVE | DF_EULER>(m, d, s, w0, count);
+    case DF_FACTOR | DF_SOLVE: return (int)launch_flags<DF_FACTOR | DF_SOLVE>(m, d, s, w0, count);
+    case DF_FACTOR: return (int)launch_flags<DF_FACTOR>(m, d, s, w0, count);
+    case DF_SOLVE: return (int)launch_flags<DF_SOLVE>(m, d, s, w0, count);
+    case DF_EULER: return (int)launch_flags<DF_EULER>(m, d, s, w0, count);
     default: return (int)hipErrorInvalidValue;
   }
 }

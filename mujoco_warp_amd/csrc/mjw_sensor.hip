@@ -31,9 +31,9 @@ __host__ inline SLay make_slayout(const mjw_model_t& m) {
 }
 
 // stages: bit 0 position, bit 1 velocity, bit 2 acceleration sensors (+ rne_postconstraint)
-__global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L, int stages) {
+__global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L, int stages, int w0) {
   extern __shared__ __attribute__((aligned(16))) float s[];
-  const int wid = blockIdx.x, lane = threadIdx.x & 63;
+  const int wid = w0 + (int)blockIdx.x, lane = threadIdx.x & 63;
   if (wid >= d.nworld) return;
   const int nb = m.nbody, nv = m.nv;
   const long wb = (long)wid * nb;
@@ -282,12 +282,13 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   }
 }
 
-int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages) {
-  if (d->nworld <= 0 || m->nsensor == 0 || (m->opt_disableflags & DSBL_SENSOR) || !stages) return 0;
+int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages, int w0, int count) {
+  if (count < 0) count = d->nworld - w0;
+  if (count <= 0 || m->nsensor == 0 || (m->opt_disableflags & DSBL_SENSOR) || !stages) return 0;
   SLay L = make_slayout(*m);
   size_t lds = (size_t)L.total * 4;
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(sensor_acc_kernel, dim3(d->nworld), dim3(64), lds, s, *m, *d, L, stages);
+  hipLaunchKernelGGL(sensor_acc_kernel, dim3(count), dim3(64), lds, s, *m, *d, L, stages, w0);
   return (int)hipGetLastError();
 }
 

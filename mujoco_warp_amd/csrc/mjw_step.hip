@@ -16,6 +16,7 @@
 #include "mjw_ccd.h"
 #include "mjw_narrow.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace mjw {
@@ -28,7 +29,7 @@ struct Lay {
   int qfrc_smooth, qacc_smooth, qacc, Ma, qfrc_constraint, qfrc_bias, qfrc_passive, qfrc_actuator, vec;
   int J, efc_D, efc_aref, efc_pos, efc_margin, efc_vel, efc_frictionloss, efc_type, efc_id, efc_force, efc_state;
   int Jaref, jv, rowcon;
-  int act_len, act_vel, act_force, act_mom, act_momdof, act_nnz;
+  int act_len, act_vel, act_force, act_mom, act_momdof, act_nnz, amax;
   int con, cmax, jqvel, plist, scratch, iscratch, ccd;
   int nofactor;
   int total;
@@ -41,45 +42,69 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
   int o = 0;
   L.nofactor = nofactor;
   auto take = [&](int n) { int r = o; o += (n + 3) & ~3; return r; };
+  auto r4 = [](int n) { return (n + 3) & ~3; };
+  int usz = 0;  // size of the direct-mode region U
   int nv = m.nv, nb = m.nbody, nj = m.njnt, ng = m.ngeom, nu = m.nu;
   L.nvs = nv | 1;  // odd row stride: conflict-free row and column access
   L.qpos = take(m.nq); L.qvel = take(nv);
-  L.xpos = take(nb * 3); L.xquat = take(nb * 4); L.xmat = take(nb * 9); L.xipos = take(nb * 3); L.ximat = take(nb * 9);
+  L.xpos = take(nb * 3); L.xquat = take(nb * 4); L.xmat = take(nb * 9); L.xipos = take(nb * 3);
   L.xanchor = take(nj * 3); L.xaxis = take(nj * 3); L.gxpos = take(ng * 3); L.gxmat = take(ng * 9);
   L.subtree_com = take(nb * 3); L.cinert = take(nb * 10); L.crb = take(nb * 10); L.cdof = take(nv * 6);
-  L.cdof_dot = take(nv * 6); L.cvel = take(nb * 6); L.cacc = take(nb * 6); L.cfrc = take(nb * 6);
-  L.qM = take(nv * L.nvs);
-  L.L = nofactor ? L.qM : take(nv * L.nvs);
-  L.H = (m.opt_solver == SOLVER_NEWTON && !nofactor) ? take(nv * L.nvs) : L.L;
-  L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv); L.qacc = take(nv); L.Ma = take(nv); L.qfrc_constraint = take(nv);
-  L.qfrc_bias = take(nv); L.qfrc_passive = take(nv); L.qfrc_actuator = take(nv); L.vec = take(2 * nv);
-  // nofactor ("direct") mode: constraint rows go straight to global memory (the dense kernel
-  // reads them from there), so J and the row scalars get no LDS; contact staging reuses the
-  // qM region, which is dead once crb_qM has copied qM out
+  L.cmax = nofactor ? CMAX / 2 : CMAX;
   if (nofactor) {
+    // direct mode (the dense path's forward kernel): constraint rows go straight to global memory
+    // (the dense kernel reads them from there) and factor / solve / integrate run elsewhere, so the
+    // world's LDS holds one region U whose contents follow the stage lifetimes:
+    //   kinematics .. com_pos : ximat
+    //   crb_qM                : qM (copied out to global)
+    //   collision             : contact staging, broadphase survivors, J.qvel per row
+    //   velocity .. accel.    : cdof_dot, cvel, cacc, cfrc, passive scratch (vec)
+    const int u_pos = r4(nb * 9);
+    const int u_qM = r4(nv * L.nvs);
+    const int u_col = r4(L.cmax * CREC) + r4(m.nxn) + r4(njmax);
+    const int u_vel = r4(nv * 6) + 3 * r4(nb * 6) + r4(2 * nv);
+    usz = std::max(std::max(u_pos, u_qM), std::max(u_col, u_vel));
+    const int U = take(usz);
+    L.ximat = U;
+    L.qM = L.L = L.H = U;
+    L.con = U; L.plist = U + r4(L.cmax * CREC); L.jqvel = L.plist + r4(m.nxn);
+    L.cdof_dot = U; L.cvel = U + r4(nv * 6); L.cacc = L.cvel + r4(nb * 6); L.cfrc = L.cacc + r4(nb * 6); L.vec = L.cfrc + r4(nb * 6);
+    L.qfrc_smooth = take(nv); L.qfrc_bias = take(nv); L.qfrc_passive = take(nv); L.qfrc_actuator = take(nv);
+    L.qacc_smooth = L.qacc = L.Ma = L.qfrc_constraint = -1;  // produced by the dense kernel
     L.J = L.efc_D = L.efc_aref = L.efc_pos = L.efc_margin = L.efc_vel = L.efc_frictionloss = L.efc_type = L.efc_id = -1;
     L.efc_force = L.efc_state = L.Jaref = L.jv = -1;
   } else {
+    L.ximat = take(nb * 9);
+    L.cdof_dot = take(nv * 6); L.cvel = take(nb * 6); L.cacc = take(nb * 6); L.cfrc = take(nb * 6);
+    L.qM = take(nv * L.nvs);
+    L.L = take(nv * L.nvs);
+    L.H = (m.opt_solver == SOLVER_NEWTON) ? take(nv * L.nvs) : L.L;
+    L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv); L.qacc = take(nv); L.Ma = take(nv); L.qfrc_constraint = take(nv);
+    L.qfrc_bias = take(nv); L.qfrc_passive = take(nv); L.qfrc_actuator = take(nv); L.vec = take(2 * nv);
     L.J = take(njmax * L.nvs);
     L.efc_D = take(njmax); L.efc_aref = take(njmax); L.efc_pos = take(njmax); L.efc_margin = take(njmax);
     L.efc_vel = take(njmax); L.efc_frictionloss = take(njmax); L.efc_type = take(njmax); L.efc_id = take(njmax);
     L.efc_force = take(njmax); L.efc_state = take(njmax); L.Jaref = take(njmax); L.jv = take(njmax);
+    L.jqvel = take(njmax);
+    L.plist = take(m.nxn);
+    L.con = take(L.cmax * CREC);
   }
   L.rowcon = -1;
-  L.jqvel = take(njmax);
-  L.plist = take(m.nxn);
-  L.act_len = take(nu); L.act_vel = take(nu); L.act_force = take(nu); L.act_mom = take(nu * 6); L.act_momdof = take(nu * 6);
+  // moment slots per actuator: 1 when every transmission has one non-zero (nJmom == nu: hinge / slide
+  // joints), else 6 (free / ball joints)
+  L.amax = m.nJmom == nu ? 1 : 6;
+  L.act_len = take(nu); L.act_vel = take(nu); L.act_force = take(nu); L.act_mom = take(nu * L.amax); L.act_momdof = take(nu * L.amax);
   L.act_nnz = take(nu);
-  L.cmax = nofactor ? CMAX / 2 : CMAX;
-  L.con = (nofactor && nv * L.nvs >= L.cmax * CREC) ? L.qM : take(L.cmax * CREC);
   L.scratch = take(64);
   L.iscratch = take(64);
-  // convex-collision (GJK/EPA) workspace: the cdof_dot..cfrc block is dead until fwd_velocity,
-  // so it holds the workspace when it fits; otherwise the workspace gets its own LDS
+  // convex-collision (GJK/EPA) workspace of the pre-pass kernel, which runs kinematics only: in
+  // direct mode the region U (ximat is dead there), else the cdof_dot..cfrc block when it fits;
+  // otherwise the workspace gets its own LDS
   L.ccd = -1;
   if (ccd && m.nxn_ccd > 0) {
     const int need = ccd_layout(m.ccd_epa_iterations).total;
-    L.ccd = (L.qM - L.cdof_dot >= need) ? L.cdof_dot : take(need);
+    if (nofactor) L.ccd = (usz >= need) ? L.ximat : take(need);
+    else L.ccd = (L.qM - L.cdof_dot >= need) ? L.cdof_dot : take(need);
   }
   L.total = o;
   return L;
@@ -1322,9 +1347,9 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
     d.actuator_length[gu] = length;
     d.moment_rownnz[gu] = nnz;
     d.moment_rowadr[gu] = rowadr;
-    for (int k = 0; k < 6; k++) {
-      s[L.act_mom + 6 * a + k] = k < nnz ? mom[k] : 0.0f;
-      si[L.act_momdof + 6 * a + k] = k < nnz ? va + k : 0;
+    for (int k = 0; k < L.amax; k++) {
+      s[L.act_mom + L.amax * a + k] = k < nnz ? mom[k] : 0.0f;
+      si[L.act_momdof + L.amax * a + k] = k < nnz ? va + k : 0;
     }
 #pragma unroll
     for (int k = 0; k < 6; k++) {
@@ -1350,7 +1375,7 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
   // forward.py:540-562
   for (int a = lane; a < m.nu; a += LPW) {
     float v = 0.0f;
-    for (int k = 0; k < si[L.act_nnz + a]; k++) v += s[L.act_mom + 6 * a + k] * qvel[si[L.act_momdof + 6 * a + k]];
+    for (int k = 0; k < si[L.act_nnz + a]; k++) v += s[L.act_mom + L.amax * a + k] * qvel[si[L.act_momdof + L.amax * a + k]];
     s[L.act_vel + a] = v;
     d.actuator_velocity[(long)wid * m.nu + a] = v;
   }
@@ -1566,7 +1591,7 @@ __device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_da
     float q = 0.0f;
     for (int a = 0; a < m.nu; a++)
       for (int k = 0; k < si[L.act_nnz + a]; k++)
-        if (si[L.act_momdof + 6 * a + k] == i) q += s[L.act_mom + 6 * a + k] * s[L.act_force + a];
+        if (si[L.act_momdof + L.amax * a + k] == i) q += s[L.act_mom + L.amax * a + k] * s[L.act_force + a];
     int j = m.dof_jntid[i];
     if (m.jnt_actfrclimited[j]) q = clampf(q, jnt_actfrcrange[2 * j], jnt_actfrcrange[2 * j + 1]);
     qfrc_act[i] = q;
@@ -1978,9 +2003,9 @@ __device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data
       long gu = (long)wid * m.nu + a;
       int nnz = d.moment_rownnz[gu], adr = d.moment_rowadr[gu];
       si[L.act_nnz + a] = nnz;
-      for (int k = 0; k < 6; k++) {
-        s[L.act_mom + 6 * a + k] = k < nnz ? d.actuator_moment[(long)wid * m.nJmom + adr + k] : 0.0f;
-        si[L.act_momdof + 6 * a + k] = k < nnz ? d.moment_colind[(long)wid * m.nJmom + adr + k] : 0;
+      for (int k = 0; k < L.amax; k++) {
+        s[L.act_mom + L.amax * a + k] = k < nnz ? d.actuator_moment[(long)wid * m.nJmom + adr + k] : 0.0f;
+        si[L.act_momdof + L.amax * a + k] = k < nnz ? d.moment_colind[(long)wid * m.nJmom + adr + k] : 0;
       }
       s[L.act_len + a] = d.actuator_length[gu];
       if (!(stages & ST_VEL)) s[L.act_vel + a] = d.actuator_velocity[gu];
@@ -2043,12 +2068,15 @@ __device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data
 }
 
 template <int STAGES>
-__global__ void __launch_bounds__(64) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L) {
+// 4 waves per SIMD (<= 128 VGPRs): with the direct-mode LDS layout (9.8 KB per humanoid world)
+// this is 16 worlds per CU; the collision narrowphase spills ~40 registers to scratch for it
+// (measured: forward kernel 0.326 -> 0.303 ms at nworld 8192 against the unconstrained 160 VGPRs)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   WS w;
   w.s = smem;
   w.si = reinterpret_cast<int*>(smem);
-  w.wid = blockIdx.x;
+  w.wid = w0 + (int)blockIdx.x;
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
   PROF_T0();
@@ -2091,12 +2119,12 @@ __global__ void __launch_bounds__(64) mjw_kernel(const mjw_model_t m, const mjw_
 // whole wave in lockstep over an LDS workspace.  Results go to d.ccd_out, which the forward
 // kernel's narrowphase reads, so the (large) CCD code never shares a kernel with the hot path.
 // -------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L) {
+__global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   WS w;
   w.s = smem;
   w.si = reinterpret_cast<int*>(smem);
-  w.wid = blockIdx.x;
+  w.wid = w0 + (int)blockIdx.x;
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
   const int wid = w.wid;
@@ -2166,9 +2194,18 @@ int set_err(hipError_t e, const char* where) {
   return (int)e;
 }
 
+hipError_t reset_counters(const mjw_data_t* d, hipStream_t s) {
+  hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision);
+  return hipGetLastError();
+}
+
+// worlds [w0, w0 + count) of d; the pool counters are cleared by the caller (run) before the
+// position stage of any world range
 template <int STAGES>
-int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, const char* name) {
+int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, const char* name, int w0 = 0, int count = -1) {
   constexpr bool nofactor = (STAGES & mjw::ST_NOFACTOR) != 0;
+  if (count < 0) count = d->nworld - w0;
+  if (count <= 0) return 0;
   mjw::Lay L = mjw::make_layout(*m, d->njmax, nofactor);
   size_t lds = (size_t)L.total * 4;
   static const size_t lds_pad = [] {  // occupancy experiments only (MJW_LDS_PAD bytes)
@@ -2178,17 +2215,14 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   lds += lds_pad;
   if (lds > 160 * 1024) { g_err = std::string(name) + ": per-world LDS working set exceeds 160 KiB"; return -3; }
   if (STAGES & mjw::ST_POS) {
-    hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return set_err(e, name);
     if (m->nxn_ccd > 0 && d->naconmax > 0 && !(m->opt_disableflags & (mjw::DSBL_CONSTRAINT | mjw::DSBL_CONTACT))) {
       static std::once_flag once_ccd;
       std::call_once(once_ccd, [] {
         (void)hipFuncSetAttribute((const void*)mjw::ccd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       });
       const mjw::Lay LC = mjw::make_layout(*m, d->njmax, nofactor, true);
-      hipLaunchKernelGGL(mjw::ccd_kernel, dim3(d->nworld), dim3(64), (size_t)LC.total * 4, s, *m, *d, LC);
-      e = hipGetLastError();
+      hipLaunchKernelGGL(mjw::ccd_kernel, dim3(count), dim3(64), (size_t)LC.total * 4, s, *m, *d, LC, w0);
+      hipError_t e = hipGetLastError();
       if (e != hipSuccess) return set_err(e, name);
     }
   }
@@ -2196,7 +2230,7 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   std::call_once(once, [] {
     (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
-  hipLaunchKernelGGL(mjw::mjw_kernel<STAGES>, dim3(d->nworld), dim3(64), lds, s, *m, *d, L);
+  hipLaunchKernelGGL(mjw::mjw_kernel<STAGES>, dim3(count), dim3(64), lds, s, *m, *d, L, w0);
   return set_err(hipGetLastError(), name);
 }
 
@@ -2230,35 +2264,46 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   if (m->nv > 64 || m->nbody > 4096) { g_err = std::string(name) + ": model too large for the dense world-per-wave path"; return -2; }
   hipStream_t s = (hipStream_t)stream;
   int rc = 0;
+  if (stages & ST_POS) {
+    rc = set_err(reset_counters(d, s), name);
+    if (rc) return rc;
+  }
   // sensors (all stages, one kernel after the solver and before the integrator): only the fused
   // forward / step (the stage entry points, like the reference's fwd_* functions, compute none)
   const bool full = (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE)) == (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE);
   const bool acc_sensors = full && m->nsensor > 0 && !(m->opt_disableflags & DSBL_SENSOR);
   if (dense_ok(m, d)) {
-    // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel
-    if (g_ev[0]) (void)hipEventRecord(g_ev[0], s);
-    switch (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC)) {
-      case 0: break;
-      case ST_POS | ST_VEL | ST_ACT | ST_ACC: rc = launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_NOFACTOR>(m, d, s, name); break;
-      case ST_POS: rc = launch_generic<ST_POS>(m, d, s, name); break;
-      case ST_VEL: rc = launch_generic<ST_VEL>(m, d, s, name); break;
-      case ST_ACT: rc = launch_generic<ST_ACT>(m, d, s, name); break;
-      case ST_ACC: rc = launch_generic<ST_ACC | ST_NOFACTOR>(m, d, s, name); break;
-      default: g_err = std::string(name) + ": unsupported stage group"; return -4;
-    }
-    if (rc) return rc;
-    if (g_ev[1]) (void)hipEventRecord(g_ev[1], s);
-    int f = ((stages & ST_ACC) ? DF_FACTOR : 0) | ((stages & ST_SOLVE) ? DF_SOLVE : 0) | ((stages & ST_EULER) ? DF_EULER : 0);
-    if (acc_sensors) {
-      // sensor_pos / _vel / _acc sit before the integrator (forward.py:981-998, step :1003-1018)
-      rc = set_err((hipError_t)dense_launch(f & ~DF_EULER, m, d, s), name);
-      if (!rc) rc = set_err((hipError_t)sensor_launch(m, d, s), name);
-      if (!rc && (f & DF_EULER)) rc = set_err((hipError_t)dense_launch(DF_EULER, m, d, s), name);
-    } else if (f != 0) {
-      rc = set_err((hipError_t)dense_launch(f, m, d, s), name);
-    }
-    if (g_ev[2]) (void)hipEventRecord(g_ev[2], s);
-    return rc;
+    // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel, for the
+    // world range [w0, w0 + cnt) on stream st; `timed` records the optional bench events.
+    // (A two-stream split of one batch inside the step was measured and gave nothing: the join
+    // that ends the step serialises the halves' tails again)
+    auto pipeline = [&](hipStream_t st, int w0, int cnt, bool timed) -> int {
+      int r = 0;
+      if (timed && g_ev[0]) (void)hipEventRecord(g_ev[0], st);
+      switch (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC)) {
+        case 0: break;
+        case ST_POS | ST_VEL | ST_ACT | ST_ACC: r = launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_NOFACTOR>(m, d, st, name, w0, cnt); break;
+        case ST_POS: r = launch_generic<ST_POS>(m, d, st, name, w0, cnt); break;
+        case ST_VEL: r = launch_generic<ST_VEL>(m, d, st, name, w0, cnt); break;
+        case ST_ACT: r = launch_generic<ST_ACT>(m, d, st, name, w0, cnt); break;
+        case ST_ACC: r = launch_generic<ST_ACC | ST_NOFACTOR>(m, d, st, name, w0, cnt); break;
+        default: g_err = std::string(name) + ": unsupported stage group"; return -4;
+      }
+      if (r) return r;
+      if (timed && g_ev[1]) (void)hipEventRecord(g_ev[1], st);
+      int f = ((stages & ST_ACC) ? DF_FACTOR : 0) | ((stages & ST_SOLVE) ? DF_SOLVE : 0) | ((stages & ST_EULER) ? DF_EULER : 0);
+      if (acc_sensors) {
+        // sensor_pos / _vel / _acc sit before the integrator (forward.py:981-998, step :1003-1018)
+        r = set_err((hipError_t)dense_launch(f & ~DF_EULER, m, d, st, w0, cnt), name);
+        if (!r) r = set_err((hipError_t)sensor_launch(m, d, st, 7, w0, cnt), name);
+        if (!r && (f & DF_EULER)) r = set_err((hipError_t)dense_launch(DF_EULER, m, d, st, w0, cnt), name);
+      } else if (f != 0) {
+        r = set_err((hipError_t)dense_launch(f, m, d, st, w0, cnt), name);
+      }
+      if (timed && g_ev[2]) (void)hipEventRecord(g_ev[2], st);
+      return r;
+    };
+    return pipeline(s, 0, d->nworld, true);
   }
   if (acc_sensors) {
     rc = launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE>(m, d, s, name);

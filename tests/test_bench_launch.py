@@ -51,7 +51,7 @@ def test_launcher_command_without_gpu(monkeypatch):
 
 @pytest.mark.gpu
 def test_gpu_bench_two_ranks_weak_equals_single(tmp_path):
-  common = ["--steps", "5", "--warmup", "2", "--cpu-baseline", "0"]
+  common = ["--steps", "5", "--warmup", "2", "--cpu-baseline", "0", "--graph", "0"]
   two = _run(["--gpus", "2", "--nworld", "256", "--dump-qpos", str(tmp_path / "two")] + common)
   assert two["n_gpus"] == 2 and two["scaling"] == "weak"
   assert two["config"]["nworld_total"] == 512 and two["config"]["converged_worlds"] == 512
@@ -68,10 +68,11 @@ def test_gpu_bench_two_ranks_weak_equals_single(tmp_path):
 @pytest.mark.gpu
 def test_gpu_bench_two_ranks_strong_and_graph(tmp_path):
   common = ["--steps", "5", "--warmup", "2", "--cpu-baseline", "0", "--nworld", "301"]
-  strong = _run(["--gpus", "2", "--scaling", "strong", "--dump-qpos", str(tmp_path / "s")] + common)
+  strong = _run(["--gpus", "2", "--scaling", "strong", "--graph", "0", "--dump-qpos", str(tmp_path / "s")] + common)
   assert strong["scaling"] == "strong" and strong["config"]["nworld_total"] == 301
-  graph = _run(["--gpus", "1", "--graph", "1", "--dump-qpos", str(tmp_path / "g")] + common)
-  assert graph["config"]["graph"] is True
+  # graph replay (eager steps with events every 2nd step) over two stream shards of one rank
+  graph = _run(["--gpus", "1", "--graph", "1", "--event-every", "2", "--streams", "2", "--dump-qpos", str(tmp_path / "g")] + common)
+  assert graph["config"]["graph"] is True and graph["config"]["streams"] == 2 and graph["config"]["timed_kernel_launches"] == 3
   qg = np.load(tmp_path / "g" / "qpos_rank0.npz")["qpos"]
   got = [np.load(tmp_path / "s" / f"qpos_rank{r}.npz") for r in range(2)]
   assert [int(z["offset"]) for z in got] == [0, 151]

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 CSV output into profiles/: kernel-trace stats + per-kernel HBM traffic.
 
-usage: python tools/pmc_traffic.py <stats_dir> <fetch_dir> <write_dir> <out.json> [nworld] [solver] [model]
+usage: python tools/pmc_traffic.py <stats_dir> <fetch_dir> <write_dir> <out.json> [worlds per launch] [solver] [model]
   model     : humanoid (default: the dense path's kernels) or a sparse-path model (cloth, aloha_cloth)
   stats_dir : rocprofv3 --kernel-trace --stats --output-format csv output directory
   fetch_dir : rocprofv3 --pmc FETCH_SIZE --output-format csv output directory
