@@ -138,18 +138,22 @@ __device__ __forceinline__ float chol_solve(const float (&a)[32], const float* S
 
 // stage an n x n block (global row stride gs) into S with identity padding to 32x32,
 // plus an optional diagonal term
+// (all 16 loads per lane are issued before the first LDS write: one global-latency wait per
+// staging instead of one per element, which a load -> wait -> ds_write loop costs)
 __device__ __forceinline__ void stage_fill(const float* g, int gs, int n, const float* diag_add, float diag_scale, float* S,
                                            int lane) {
-  for (int e = lane; e < 32 * 32; e += 64) {
-    int r = e >> 5, k = e & 31;
-    float v;
-    if (r < n && k < n) {
-      v = g[r * gs + k];
-      if (diag_add && r == k) v += diag_scale * diag_add[r];
-    } else {
-      v = (r == k) ? 1.0f : 0.0f;
-    }
-    S[r * DSS + k] = v;
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const int e = lane + 64 * q, r = e >> 5, k = e & 31;
+    v[q] = g[(r < n && k < n) ? r * gs + k : 0];
+  }
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const int e = lane + 64 * q, r = e >> 5, k = e & 31;
+    float x = (r < n && k < n) ? v[q] : ((r == k) ? 1.0f : 0.0f);
+    if (diag_add && r == k && r < n) x += diag_scale * diag_add[r];
+    S[r * DSS + k] = x;
   }
   __syncthreads();
 }
@@ -297,13 +301,14 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   constexpr bool NT = NEWTON && (FLAGS & DF_SOLVE);
   constexpr int S_OFF = NT ? DJ_WORDS : 0;  // CG: the 32x32 scratch aliases J (used before J is staged)
   constexpr int V_OFF = NT ? DJ_WORDS + DS_WORDS : DJ_WORDS;
-  __shared__ __attribute__((aligned(16))) float sm[V_OFF + 4 * 64];
+  __shared__ __attribute__((aligned(16))) float sm[V_OFF + 5 * 64];
   float* Jl = sm;
   float* S = sm + S_OFF;
   float* vd = sm + V_OFF;        // dof vector broadcast buffer (32)
   float* vd2 = vd + 64;          // second dof buffer
   float* vr = vd + 128;          // row vector buffer (64)
   float* vr2 = vd + 192;         // second row buffer (Newton weights)
+  float* vq = vd + 256;          // qpos (Euler)
   const int wid = w0 + (int)blockIdx.x;
   if (wid >= d.nworld) return;
   const int lane = threadIdx.x, c = lane & 31, h = lane >> 5;
@@ -312,6 +317,29 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   const bool lo = lane < 32;
   const long gi = (long)wid * nv + c;
   const int nvq = (nv + 3) >> 2;
+
+  // per-world inputs of the later phases, loaded up front so that their global latency overlaps
+  // the qM staging and the factorisation instead of stalling each phase
+  const int nq = m.nq;
+  const bool qpos_lds = nq <= 64;
+  float pf_qfrc_smooth = 0.0f, pf_warm = 0.0f, pf_qvel = 0.0f, pf_qpos = 0.0f, pf_D = 0.0f, pf_aref = 0.0f, pf_fl = 0.0f;
+  int pf_nefc = 0, pf_ne = 0, pf_nf = 0;
+  if ((FLAGS & (DF_FACTOR | DF_SOLVE)) && dof) pf_qfrc_smooth = d.qfrc_smooth[gi];
+  if (FLAGS & DF_SOLVE) {
+    if (dof) pf_warm = d.qacc_warmstart[gi];
+    pf_nefc = d.nefc[wid];
+    pf_ne = d.ne[wid];
+    pf_nf = d.nf[wid];
+    if (lane < d.njmax) {
+      pf_D = d.efc_D[(long)wid * d.njmax_pad + lane];
+      pf_aref = d.efc_aref[(long)wid * d.njmax + lane];
+      pf_fl = d.efc_frictionloss[(long)wid * d.njmax + lane];
+    }
+  }
+  if (FLAGS & DF_EULER) {
+    if (dof) pf_qvel = d.qvel[gi];
+    if (qpos_lds && lane < nq) pf_qpos = d.qpos[(long)wid * nq + lane];
+  }
 
   PROF_T0();
   float qacc = 0.0f, ma = 0.0f;
@@ -331,7 +359,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
         gL[e] = S[r * DSS + k];
       }
     }
-    qfrc_smooth = dof ? d.qfrc_smooth[gi] : 0.0f;
+    qfrc_smooth = pf_qfrc_smooth;
     if (lo) vd[c] = qfrc_smooth;
     __syncthreads();
     qacc_smooth = symv(Mi, vd, h);
@@ -342,8 +370,8 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   PROF_MARK(PH_DFACTOR);
   if (FLAGS & DF_SOLVE) {
     const int njmax = d.njmax;
-    const int nefc = min(d.nefc[wid], njmax);
-    const int ne = d.ne[wid], nf = d.nf[wid];
+    const int nefc = min(pf_nefc, njmax);
+    const int ne = pf_ne, nf = pf_nf;
     __syncthreads();  // S (aliasing J for CG) is free again
     if (njmax == 0 || nv == 0) {
       qacc = qacc_smooth;
@@ -356,17 +384,27 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
       }
       if (lane == 0) d.solver_niter[wid] = 0;
     } else {
-      // stage J (zero padded to 64 x 32)
+      // stage J (zero padded to 64 x 32), 16 loads in flight per lane and batch
       const float* gJ = d.efc_J + (long)wid * d.njmax_pad * np;
-      for (int e = lane; e < 64 * 32; e += 64) {
-        int r = e >> 5, k = e & 31;
-        Jl[r * DJS + k] = (r < nefc && k < nv) ? gJ[r * np + k] : 0.0f;
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int e = lane + 64 * (16 * half + q), r = e >> 5, k = e & 31;
+          v[q] = gJ[(r < nefc && k < nv) ? r * np + k : 0];
+        }
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int e = lane + 64 * (16 * half + q), r = e >> 5, k = e & 31;
+          Jl[r * DJS + k] = (r < nefc && k < nv) ? v[q] : 0.0f;
+        }
       }
       Row w;
       const bool row = lane < nefc;
-      w.D = row ? d.efc_D[(long)wid * d.njmax_pad + lane] : 0.0f;
-      float aref = row ? d.efc_aref[(long)wid * njmax + lane] : 0.0f;
-      w.fl = row ? d.efc_frictionloss[(long)wid * njmax + lane] : 0.0f;
+      w.D = row ? pf_D : 0.0f;
+      float aref = row ? pf_aref : 0.0f;
+      w.fl = row ? pf_fl : 0.0f;
       w.rf = safe_div(w.fl, w.D);
       w.cls = lane < ne ? 0 : (lane < ne + nf ? 1 : 2);
       w.jv = 0.0f;
@@ -374,7 +412,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
       const float ls_tolerance = MR(opt_ls_tolerance)[0];
       const float meaninertia = MR(stat_meaninertia)[0];
       // qacc init (solver.py:3308-3311)
-      qacc = dof ? ((m.opt_disableflags & DSBL_WARMSTART) ? qacc_smooth : d.qacc_warmstart[gi]) : 0.0f;
+      qacc = dof ? ((m.opt_disableflags & DSBL_WARMSTART) ? qacc_smooth : pf_warm) : 0.0f;
       if (lo) vd[c] = qacc;
       __syncthreads();
       ma = symv(Mm, vd, h);
@@ -580,7 +618,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
                              m.actuator_actlimited[u] != 0);
       }
     }
-    float qvel = dof ? d.qvel[gi] + qacc_adv * dt : 0.0f;
+    float qvel = dof ? pf_qvel + qacc_adv * dt : 0.0f;
     if (lo) {
       vd2[c] = qvel;
       if (dof) {
@@ -588,8 +626,10 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
         d.qacc_warmstart[gi] = qacc;
       }
     }
+    if (qpos_lds) vq[lane] = pf_qpos;
     __syncthreads();
-    float* gq = d.qpos + (long)wid * m.nq;
+    // positions are integrated in LDS and written back coalesced (global when nq > 64)
+    float* gq = qpos_lds ? vq : d.qpos + (long)wid * nq;
     for (int j = lane; j < m.njnt; j += 64) {
       int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j], jt = m.jnt_type[j];
       if (jt == JNT_FREE) {
@@ -606,6 +646,10 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
       } else {
         gq[qa] = gq[qa] + dt * vd2[da];
       }
+    }
+    if (qpos_lds) {
+      __syncthreads();
+      if (lane < nq) d.qpos[(long)wid * nq + lane] = vq[lane];
     }
     if (lane == 0) d.time[wid] = d.time[wid] + dt;
   }

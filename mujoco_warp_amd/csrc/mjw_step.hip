@@ -321,11 +321,16 @@ __device__ __forceinline__ void com_pos(const mjw_model_t& m, const mjw_data_t& 
   const float* body_mass = MR(body_mass);
   const float* body_subtreemass = MR(body_subtreemass);
   const float* body_inertia = MR(body_inertia);
+  // body masses in the (still unused) crb slots, so that the subtree sums below read LDS only
+  // instead of one dependent global load of body_mass per subtree body
+  float* bm = s + L.crb;
+  for (int b = lane; b < m.nbody; b += LPW) bm[b] = body_mass[b];
+  WSYNC();
   for (int b = lane; b < m.nbody; b += LPW) {
     float acc[3] = {0.0f, 0.0f, 0.0f};
     int end = m.body_subtree_end[b];
     for (int j = b; j < end; j++) {
-      float ms = body_mass[j];
+      const float ms = bm[j];
       for (int i = 0; i < 3; i++) acc[i] += s[L.xipos + 3 * j + i] * ms;
     }
     float mass = body_subtreemass[b];
@@ -488,6 +493,12 @@ __device__ __forceinline__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d
   const int nv = m.nv, nvs = L.nvs;
   float* M = s + L.qM;
   for (int e = lane; e < nv * nvs; e += LPW) M[e] = 0.0f;
+  // dof parents in LDS (iscratch is free until the collision stage): the ancestor walks below
+  // then chain LDS reads instead of dependent global loads
+  int* dpar = w.si + L.iscratch;
+  const bool dpar_lds = nv <= 64;
+  if (dpar_lds)
+    for (int i = lane; i < nv; i += LPW) dpar[i] = m.dof_parentid[i];
   WSYNC();
   for (int i = lane; i < nv; i += LPW) {
     int b = m.dof_bodyid[i];
@@ -497,13 +508,13 @@ __device__ __forceinline__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d
     float Mii = dof_armature[i];
     Mii += cd[0] * buf[0] + cd[1] * buf[1] + cd[2] * buf[2] + cd[3] * buf[3] + cd[4] * buf[4] + cd[5] * buf[5];
     M[i * nvs + i] = Mii;
-    int j = m.dof_parentid[i];
+    int j = dpar_lds ? dpar[i] : m.dof_parentid[i];
     while (j >= 0) {
       const float* cj = s + L.cdof + 6 * j;
       float q = cj[0] * buf[0] + cj[1] * buf[1] + cj[2] * buf[2] + cj[3] * buf[3] + cj[4] * buf[4] + cj[5] * buf[5];
       M[i * nvs + j] = q;
       M[j * nvs + i] = q;
-      j = m.dof_parentid[j];
+      j = dpar_lds ? dpar[j] : m.dof_parentid[j];
     }
   }
   WSYNC();
