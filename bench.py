@@ -131,11 +131,15 @@ def parse():
   for k in ("nworld", "nconmax", "njmax", "solver"):
     if getattr(a, k) is None:
       setattr(a, k, cfg[k])
-  if a.pmc is None:  # the latest round's summary for this model
+  if a.pmc is None:  # the committed summary for this model taken on the current kernel sources, else the latest
     import glob
 
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{a.model}_r[0-9]*.json")))
-    a.pmc = found[-1] if found else ""
+    from mujoco_warp_amd import build as _build
+
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{a.model}_r[0-9]*.json")), key=os.path.getmtime)
+    sha = _build.sources_hash()
+    same = [f for f in found if json.load(open(f)).get("csrc_sha") == sha]
+    a.pmc = (same or found or [""])[-1]
   for k, dflt in (("steps", 1000), ("cpu_worlds", 1024), ("cpu_steps", 1000)):
     if getattr(a, k) is None:
       setattr(a, k, cfg.get(k, dflt))

@@ -1,659 +1,17 @@
-// mjw_dense.hip -- register-resident factor / solve / integrate path for small dense worlds
-// (nv <= 32 dofs, <= 64 constraint rows).
-//
-// One 64-lane wavefront owns one world.  Compared with the generic LDS path in
-// mjw_step.hip this path
-//   * keeps the mass matrix M and its inverse in the 32x32 MFMA accumulator layout
-//     (16 VGPRs each: lane l holds column l&31, rows 8*(r>>2) + 4*(l>>5) + (r&3)),
-//   * factors M = L L^T with rows in lanes and v_readlane broadcasts (no barriers),
-//     forms X = L^-1 with columns in lanes, and M^-1 = X^T X with 16
-//     v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains),
-//   * stages the constraint Jacobian once in LDS (odd row stride: conflict-free row
-//     and column reads) and keeps one constraint row per lane in VGPRs,
-//   * reduces over the wave with DPP (quad_perm / row_ror / row_bcast) + one readlane
-//     instead of LDS-crossbar shuffles.
-// The CG preconditioner M^-1 grad is therefore one 16-FMA matvec per iteration instead
-// of two serial triangular solves (solver.py:2879-2895 restated with an explicit
-// inverse; the minimiser and the termination tests are unchanged).
+// mjw_dense.hip -- the dense factor / solve / integrate kernel (device code in mjw_dense.h), its
+// launcher and the device self-checks of its wave primitives.
 
-#include "mjw_common.h"
+#include "mjw_dense.h"
 
 namespace mjw {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int DJS = 33;             // LDS row stride of J (odd: conflict-free rows and columns)
-constexpr int DSS = 36;             // LDS row stride of the 32x32 scratch (16-B aligned rows)
-constexpr int DJ_WORDS = 64 * DJS;  // 2112
-constexpr int DS_WORDS = 32 * DSS;  // 1152
-
-// lanes l and l^32 both receive p(l) + p(l^32)
-__device__ __forceinline__ float xhalf_add(float p) {
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(p), __float_as_uint(p), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-// row of register r of a 32x32 MFMA accumulator in lane half h
-__device__ __forceinline__ constexpr int acc_row(int r, int h) { return 8 * (r >> 2) + 4 * h + (r & 3); }
-
-// (A v) for symmetric A in accumulator layout; v = vec[0..31] in LDS (16-B aligned).
-// Result in lanes c and c+32.
-__device__ __forceinline__ float symv(const f32x16& A, const float* vec, int h) {
-  const f32x4* v4 = reinterpret_cast<const f32x4*>(vec);
-  float p0 = 0.0f, p1 = 0.0f;
-#pragma unroll
-  for (int g = 0; g < 4; g++) {
-    f32x4 q = v4[2 * g + h];
-    p0 = fmaf(A[4 * g + 0], q.x, p0);
-    p1 = fmaf(A[4 * g + 1], q.y, p1);
-    p0 = fmaf(A[4 * g + 2], q.z, p0);
-    p1 = fmaf(A[4 * g + 3], q.w, p1);
-  }
-  return xhalf_add(p0 + p1);
-}
-
-// SPD inverse.  a[k] = row (lane&31) of an SPD 32x32 matrix (identity-padded past n).
-// On return a[] holds row (lane&31) of L (A = L L^T, upper part zero); the result is
-// A^-1 in accumulator layout.  All broadcasts are v_readlane into SGPRs, so the only
-// live VGPR arrays are a[32], x[32] and the accumulator.
-template <bool STORE_L = false>
-__device__ __forceinline__ f32x16 spd_inverse(float (&a)[32], int lane, float* S = nullptr) {
-  const int c = lane & 31;
-  // right-looking Cholesky, rows in lanes (wp.tile_cholesky, smooth.py:2860-2928);
-  // 1/L[j][j] by v_rsq_f32 keeps the per-column critical path short
-#pragma unroll
-  for (int j = 0; j < 32; j++) {
-    float piv = rdlane(a[j], j);
-    float inv = __builtin_amdgcn_rsqf(piv);
-    a[j] = (c > j) ? a[j] * inv : (c == j ? piv * inv : 0.0f);
-#pragma unroll
-    for (int k = j + 1; k < 32; k++) a[k] = fmaf(-a[j], rdlane(a[j], k), a[k]);
-  }
-  if (STORE_L && lane < 32) {
-    f32x4* rw = reinterpret_cast<f32x4*>(S + c * DSS);
-#pragma unroll
-    for (int q = 0; q < 8; q++) rw[q] = f32x4{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
-  }
-  // X = L^-1, lane computes column c by right-looking forward substitution (critical path
-  // 32 steps, the other updates are independent); L[j][k] = readlane(a[k], j)
-  float x[32];
-#pragma unroll
-  for (int j = 0; j < 32; j++) x[j] = (c == j) ? 1.0f : 0.0f;
-#pragma unroll
-  for (int k = 0; k < 32; k++) {
-    x[k] *= __builtin_amdgcn_rcpf(rdlane(a[k], k));
-#pragma unroll
-    for (int j = k + 1; j < 32; j++) x[j] = fmaf(-rdlane(a[k], j), x[k], x[j]);
-  }
-  // A^-1 = X^T X : 16 x (32x32x2) f32 MFMA in two independent chains, operand X[2t + h][c]
-  const bool hi = lane >= 32;
-  f32x16 r0 = {}, r1 = {};
-#pragma unroll
-  for (int t = 0; t < 16; t += 2) {
-    float v0 = hi ? x[2 * t + 1] : x[2 * t];
-    float v1 = hi ? x[2 * t + 3] : x[2 * t + 2];
-    r0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, v0, r0, 0, 0, 0);
-    r1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, v1, r1, 0, 0, 0);
-  }
-  return r0 + r1;
-}
-
-// Cholesky in place (rows in lanes) and L rows -> S; no inverse
-__device__ __forceinline__ void chol_factor(float (&a)[32], int lane, float* S) {
-  const int c = lane & 31;
-#pragma unroll
-  for (int j = 0; j < 32; j++) {
-    float piv = rdlane(a[j], j);
-    float inv = __builtin_amdgcn_rsqf(piv);
-    a[j] = (c > j) ? a[j] * inv : (c == j ? piv * inv : 0.0f);
-#pragma unroll
-    for (int k = j + 1; k < 32; k++) a[k] = fmaf(-a[j], rdlane(a[j], k), a[k]);
-  }
-  __syncthreads();
-  if (lane < 32) {
-    f32x4* rw = reinterpret_cast<f32x4*>(S + c * DSS);
-#pragma unroll
-    for (int q = 0; q < 8; q++) rw[q] = f32x4{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
-  }
-  __syncthreads();
-}
-
-// (L L^T) x = b for a dof vector b (lane c, both halves): forward sweep with L rows in
-// registers, backward sweep with L columns read from S (wp.tile_cholesky_solve)
-__device__ __forceinline__ float chol_solve(const float (&a)[32], const float* S, int lane, float b) {
-  const int c = lane & 31;
-#pragma unroll
-  for (int k = 0; k < 32; k++) {
-    float yk = rdlane(b, k) * __builtin_amdgcn_rcpf(rdlane(a[k], k));
-    b = (c > k) ? fmaf(-a[k], yk, b) : (c == k ? yk : b);
-  }
-#pragma unroll
-  for (int k = 31; k >= 0; k--) {
-    float xk = rdlane(b, k) * __builtin_amdgcn_rcpf(S[k * DSS + k]);
-    b = (c < k) ? fmaf(-S[k * DSS + c], xk, b) : (c == k ? xk : b);
-  }
-  return b;
-}
-
-// stage an n x n block (global row stride gs) into S with identity padding to 32x32,
-// plus an optional diagonal term
-// (all 16 loads per lane are issued before the first LDS write: one global-latency wait per
-// staging instead of one per element, which a load -> wait -> ds_write loop costs)
-__device__ __forceinline__ void stage_fill(const float* g, int gs, int n, const float* diag_add, float diag_scale, float* S,
-                                           int lane) {
-  float v[16];
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const int e = lane + 64 * q, r = e >> 5, k = e & 31;
-    v[q] = g[(r < n && k < n) ? r * gs + k : 0];
-  }
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const int e = lane + 64 * q, r = e >> 5, k = e & 31;
-    float x = (r < n && k < n) ? v[q] : ((r == k) ? 1.0f : 0.0f);
-    if (diag_add && r == k && r < n) x += diag_scale * diag_add[r];
-    S[r * DSS + k] = x;
-  }
-  __syncthreads();
-}
-
-// rows (lane&31) of the staged matrix into a[], and the n x n block in accumulator layout
-__device__ __forceinline__ void stage_rows(int n, const float* S, int lane, float (&a)[32], f32x16& Macc) {
-  const int c = lane & 31, h = lane >> 5;
-  const f32x4* row = reinterpret_cast<const f32x4*>(S + c * DSS);
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    f32x4 v = row[q];
-    a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-  }
-#pragma unroll
-  for (int r = 0; r < 16; r++) {
-    int i = acc_row(r, h);
-    Macc[r] = (i < n && c < n) ? S[i * DSS + c] : 0.0f;
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void stage_spd(const float* g, int gs, int n, const float* diag_add, float diag_scale, float* S,
-                                          int lane, float (&a)[32], f32x16& Macc) {
-  stage_fill(g, gs, n, diag_add, diag_scale, S, lane);
-  stage_rows(n, S, lane, a, Macc);
-}
-
-// derivative.py:36-107 (_qderiv_actuator_passive_vel): d force / d velocity scale of actuator a
-__device__ __forceinline__ float actuator_vel_deriv(const mjw_model_t& m, const mjw_data_t& d, int wid, int a) {
-  const float* gainprm = MR(actuator_gainprm) + 10 * a;
-  const float* biasprm = MR(actuator_biasprm) + 10 * a;
-  float gain = m.actuator_gaintype[a] == GAIN_AFFINE ? gainprm[2] : 0.0f;
-  float bias = m.actuator_biastype[a] == BIAS_AFFINE ? biasprm[2] : 0.0f;
-  if (bias == 0.0f && gain == 0.0f) return 0.0f;
-  if (m.actuator_forcelimited[a]) {
-    float f = d.actuator_force[(long)wid * m.nu + a];
-    const float* fr = MR(actuator_forcerange) + 2 * a;
-    if (f <= fr[0] || f >= fr[1]) return 0.0f;
-  }
-  float vel = bias;
-  if (m.actuator_dyntype[a] != DYN_NONE) {
-    if (gain != 0.0f) {  // derivative.py:86-101: actearly differentiates at the next activation
-      const long ga = (long)wid * m.na + m.actuator_actadr[a] + m.actuator_actnum[a] - 1;
-      vel += gain * (m.actuator_actearly[a] ? next_act(MR(opt_timestep)[0], m.actuator_dyntype[a], MR(actuator_dynprm)[10 * a], MR(actuator_actrange) + 2 * a,
-                                                       d.act[ga], d.act_dot[ga], 1.0f, m.actuator_actlimited[a] != 0)
-                                            : d.act[ga]);
-    }
-  } else if (gain != 0.0f) {
-    vel += gain * d.ctrl[(long)wid * m.nu + a];
-  }
-  return vel;
-}
-
-// lane r: sum_k J[r][k] v[k] over k < 4*nq
-__device__ __forceinline__ float gemv_rows(const float* Jl, const float* vec, int lane, int nq) {
-  const f32x4* v4 = reinterpret_cast<const f32x4*>(vec);
-  const float* jr = Jl + lane * DJS;
-  float p0 = 0.0f, p1 = 0.0f;
-  for (int q = 0; q < nq; q++) {
-    f32x4 v = v4[q];
-    p0 = fmaf(jr[4 * q + 0], v.x, p0);
-    p1 = fmaf(jr[4 * q + 1], v.y, p1);
-    p0 = fmaf(jr[4 * q + 2], v.z, p0);
-    p1 = fmaf(jr[4 * q + 3], v.w, p1);
-  }
-  return p0 + p1;
-}
-
-// lane c (both halves): sum_r J[r][c] f[r]; half h sums rows 32h + [0, 4*nq)
-__device__ __forceinline__ float gemv_cols(const float* Jl, const float* fvec, int lane, int nq) {
-  const int c = lane & 31, h = lane >> 5;
-  const f32x4* f4 = reinterpret_cast<const f32x4*>(fvec + 32 * h);
-  const float* jc = Jl + 32 * h * DJS + c;
-  float p0 = 0.0f, p1 = 0.0f;
-  for (int q = 0; q < nq; q++) {
-    f32x4 f = f4[q];
-    p0 = fmaf(jc[(4 * q + 0) * DJS], f.x, p0);
-    p1 = fmaf(jc[(4 * q + 1) * DJS], f.y, p1);
-    p0 = fmaf(jc[(4 * q + 2) * DJS], f.z, p0);
-    p1 = fmaf(jc[(4 * q + 3) * DJS], f.w, p1);
-  }
-  return xhalf_add(p0 + p1);
-}
-
-// ---- solver row math (solver.py:886-1341 linesearch, 2154-2219 update_constraint) -----------
-// cls: 0 = equality (always quadratic), 1 = friction loss, 2 = one-sided (limit / contact)
-struct Row {
-  float D, jaref, jv, fl, rf;
-  int cls;
-};
-
-__device__ __forceinline__ void row_eval(const Row& w, float alpha, float& c, float& g, float& hh) {
-  float x = fmaf(alpha, w.jv, w.jaref);
-  bool quad = (w.cls == 0) || (w.cls == 2 && x < 0.0f) || (w.cls == 1 && -w.rf < x && x < w.rf);
-  float jvD = w.jv * w.D;
-  if (quad) {
-    c = 0.5f * w.D * x * x; g = jvD * x; hh = w.jv * jvD;
-  } else if (w.cls == 1) {
-    bool neg = x <= -w.rf;
-    c = w.fl * (-0.5f * w.rf + (neg ? -x : x));
-    g = neg ? -w.fl * w.jv : w.fl * w.jv;
-    hh = 0.0f;
-  } else {
-    c = 0.0f; g = 0.0f; hh = 0.0f;
-  }
-}
-
-struct Pt {
-  float alpha, c, g, h;
-};
-
-__device__ __forceinline__ Pt ls_point(const Row& w, float alpha, float q1, float q2, float qg0) {
-  float c, g, hh;
-  row_eval(w, alpha, c, g, hh);
-  Pt p;
-  p.alpha = alpha;
-  p.c = dsum(c) + alpha * alpha * q2 + alpha * q1 + qg0;
-  p.g = dsum(g) + 2.0f * alpha * q2 + q1;
-  p.h = dsum(hh) + 2.0f * q2;
-  return p;
-}
-
-__device__ __forceinline__ bool bracket(const Pt& x, const Pt& y) { return (x.g < y.g && y.g < 0.0f) || (x.g > y.g && y.g > 0.0f); }
-
-// force / state / cost of one row at its current jaref
-__device__ __forceinline__ float row_force(const Row& w, int& state, float& cost) {
-  float f;
-  cost = 0.0f;
-  if (w.cls == 1) {
-    if (w.jaref <= -w.rf) { f = w.fl; state = STATE_LINEARNEG; cost = -w.fl * (0.5f * w.rf + w.jaref); }
-    else if (w.jaref >= w.rf) { f = -w.fl; state = STATE_LINEARPOS; cost = -w.fl * (0.5f * w.rf - w.jaref); }
-    else { f = -w.D * w.jaref; state = STATE_QUADRATIC; cost = 0.5f * w.D * w.jaref * w.jaref; }
-  } else if (w.cls == 2 && w.jaref >= 0.0f) {
-    f = 0.0f; state = STATE_SATISFIED;
-  } else {
-    f = -w.D * w.jaref; state = STATE_QUADRATIC; cost = 0.5f * w.D * w.jaref * w.jaref;
-  }
-  return f;
-}
-
-// ---- the kernel ---------------------------------------------------------------------------
 template <int FLAGS, bool NEWTON>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
 dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
-  constexpr bool NT = NEWTON && (FLAGS & DF_SOLVE);
-  constexpr int S_OFF = NT ? DJ_WORDS : 0;  // CG: the 32x32 scratch aliases J (used before J is staged)
-  constexpr int V_OFF = NT ? DJ_WORDS + DS_WORDS : DJ_WORDS;
-  __shared__ __attribute__((aligned(16))) float sm[V_OFF + 5 * 64];
-  float* Jl = sm;
-  float* S = sm + S_OFF;
-  float* vd = sm + V_OFF;        // dof vector broadcast buffer (32)
-  float* vd2 = vd + 64;          // second dof buffer
-  float* vr = vd + 128;          // row vector buffer (64)
-  float* vr2 = vd + 192;         // second row buffer (Newton weights)
-  float* vq = vd + 256;          // qpos (Euler)
+  __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON>()];
   const int wid = w0 + (int)blockIdx.x;
   if (wid >= d.nworld) return;
-  const int lane = threadIdx.x, c = lane & 31, h = lane >> 5;
-  const int nv = m.nv, np = m.nv_pad;
-  const bool dof = c < nv;      // lane holds a dof value (both halves)
-  const bool lo = lane < 32;
-  const long gi = (long)wid * nv + c;
-  const int nvq = (nv + 3) >> 2;
-
-  // per-world inputs of the later phases, loaded up front so that their global latency overlaps
-  // the qM staging and the factorisation instead of stalling each phase
-  const int nq = m.nq;
-  const bool qpos_lds = nq <= 64;
-  float pf_qfrc_smooth = 0.0f, pf_warm = 0.0f, pf_qvel = 0.0f, pf_qpos = 0.0f, pf_D = 0.0f, pf_aref = 0.0f, pf_fl = 0.0f;
-  int pf_nefc = 0, pf_ne = 0, pf_nf = 0;
-  if ((FLAGS & (DF_FACTOR | DF_SOLVE)) && dof) pf_qfrc_smooth = d.qfrc_smooth[gi];
-  if (FLAGS & DF_SOLVE) {
-    if (dof) pf_warm = d.qacc_warmstart[gi];
-    pf_nefc = d.nefc[wid];
-    pf_ne = d.ne[wid];
-    pf_nf = d.nf[wid];
-    if (lane < d.njmax) {
-      pf_D = d.efc_D[(long)wid * d.njmax_pad + lane];
-      pf_aref = d.efc_aref[(long)wid * d.njmax + lane];
-      pf_fl = d.efc_frictionloss[(long)wid * d.njmax + lane];
-    }
-  }
-  if (FLAGS & DF_EULER) {
-    if (dof) pf_qvel = d.qvel[gi];
-    if (qpos_lds && lane < nq) pf_qpos = d.qpos[(long)wid * nq + lane];
-  }
-
-  PROF_T0();
-  float qacc = 0.0f, ma = 0.0f;
-  f32x16 Mm = {}, Mi = {};
-  float qfrc_smooth = 0.0f, qacc_smooth = 0.0f;
-  if (FLAGS & (DF_FACTOR | DF_SOLVE)) {
-    // ---- factor M, form M^-1, qacc_smooth (smooth.py:2860-2928 factor_solve_i)
-    float a[32];
-    stage_spd(d.qM + (long)wid * np * np, np, nv, nullptr, 0.0f, S, lane, a, Mm);
-    Mi = spd_inverse<(FLAGS & DF_FACTOR) != 0>(a, lane, S);
-    if (FLAGS & DF_FACTOR) {
-      // L rows -> qLD (nv x nv) through S for coalesced stores
-      __syncthreads();
-      float* gL = d.qLD + (long)wid * nv * nv;
-      for (int e = lane; e < nv * nv; e += 64) {
-        int r = e / nv, k = e - r * nv;
-        gL[e] = S[r * DSS + k];
-      }
-    }
-    qfrc_smooth = pf_qfrc_smooth;
-    if (lo) vd[c] = qfrc_smooth;
-    __syncthreads();
-    qacc_smooth = symv(Mi, vd, h);
-    if (!dof) qacc_smooth = 0.0f;
-    if ((FLAGS & DF_FACTOR) && lo && dof) d.qacc_smooth[gi] = qacc_smooth;
-  }
-
-  PROF_MARK(PH_DFACTOR);
-  if (FLAGS & DF_SOLVE) {
-    const int njmax = d.njmax;
-    const int nefc = min(pf_nefc, njmax);
-    const int ne = pf_ne, nf = pf_nf;
-    __syncthreads();  // S (aliasing J for CG) is free again
-    if (njmax == 0 || nv == 0) {
-      qacc = qacc_smooth;
-      if (lo) vd[c] = qacc;
-      __syncthreads();
-      ma = symv(Mm, vd, h);
-      if (lo && dof) {
-        d.qacc[gi] = qacc;
-        d.efc_Ma[gi] = ma;
-      }
-      if (lane == 0) d.solver_niter[wid] = 0;
-    } else {
-      // stage J (zero padded to 64 x 32), 16 loads in flight per lane and batch
-      const float* gJ = d.efc_J + (long)wid * d.njmax_pad * np;
-#pragma unroll
-      for (int half = 0; half < 2; half++) {
-        float v[16];
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int e = lane + 64 * (16 * half + q), r = e >> 5, k = e & 31;
-          v[q] = gJ[(r < nefc && k < nv) ? r * np + k : 0];
-        }
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int e = lane + 64 * (16 * half + q), r = e >> 5, k = e & 31;
-          Jl[r * DJS + k] = (r < nefc && k < nv) ? v[q] : 0.0f;
-        }
-      }
-      Row w;
-      const bool row = lane < nefc;
-      w.D = row ? pf_D : 0.0f;
-      float aref = row ? pf_aref : 0.0f;
-      w.fl = row ? pf_fl : 0.0f;
-      w.rf = safe_div(w.fl, w.D);
-      w.cls = lane < ne ? 0 : (lane < ne + nf ? 1 : 2);
-      w.jv = 0.0f;
-      const float tolerance = MR(opt_tolerance)[0];
-      const float ls_tolerance = MR(opt_ls_tolerance)[0];
-      const float meaninertia = MR(stat_meaninertia)[0];
-      // qacc init (solver.py:3308-3311)
-      qacc = dof ? ((m.opt_disableflags & DSBL_WARMSTART) ? qacc_smooth : pf_warm) : 0.0f;
-      if (lo) vd[c] = qacc;
-      __syncthreads();
-      ma = symv(Mm, vd, h);
-      w.jaref = gemv_rows(Jl, vd, lane, nvq) - aref;
-      const int nrq = (min(nefc, 32) + 3) >> 2;
-
-      float cost, gauss, qfrc_c, grad, Mgrad, grad_dot;
-      int state = STATE_SATISFIED;
-      float force = 0.0f;
-      auto update_constraint = [&]() {
-        float rc;
-        force = row_force(w, state, rc);
-        if (!row) { force = 0.0f; rc = 0.0f; }
-        vr[lane] = force;
-        __syncthreads();
-        qfrc_c = gemv_cols(Jl, vr, lane, nrq);
-        gauss = 0.5f * dsum(lo ? (ma - qfrc_smooth) * (qacc - qacc_smooth) : 0.0f);
-        cost = dsum(rc) + gauss;
-      };
-      auto update_gradient = [&]() {
-        grad = dof ? ma - qfrc_smooth - qfrc_c : 0.0f;
-        grad_dot = dsum(lo ? grad * grad : 0.0f);
-        if (lo) vd2[c] = grad;
-        if (NEWTON) {
-          // H = M + J' diag(D * quadratic) J (solver.py:2896-3008): 32x32x2 MFMA over row pairs
-          vr2[lane] = (row && state == STATE_QUADRATIC) ? w.D : 0.0f;
-          __syncthreads();
-          f32x16 H = Mm;
-          const int npair = (nefc + 1) >> 1;
-          for (int t = 0; t < npair; t++) {
-            int r = 2 * t + h;
-            float jrc = Jl[r * DJS + c];
-            H = __builtin_amdgcn_mfma_f32_32x32x2f32(jrc, vr2[r] * jrc, H, 0, 0, 0);
-          }
-          // identity-pad rows/cols >= nv, then rows into lanes through S
-#pragma unroll
-          for (int q = 0; q < 16; q++) {
-            int i = acc_row(q, h);
-            S[i * DSS + c] = (i < nv && c < nv) ? H[q] : (i == c ? 1.0f : 0.0f);
-          }
-          __syncthreads();
-          float a[32];
-          const f32x4* rw = reinterpret_cast<const f32x4*>(S + c * DSS);
-#pragma unroll
-          for (int q = 0; q < 8; q++) {
-            f32x4 v = rw[q];
-            a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-          }
-          chol_factor(a, lane, S);
-          Mgrad = chol_solve(a, S, lane, grad);
-        } else {
-          __syncthreads();
-          Mgrad = symv(Mi, vd2, h);
-        }
-        if (!dof) Mgrad = 0.0f;
-      };
-
-      float prev_cost;
-      update_constraint();
-      update_gradient();
-      float search = -Mgrad;
-      float search_dot = dsum(lo ? search * search : 0.0f);
-      int niter = 0;
-      const float scale = 1.0f / (meaninertia * (float)nv);
-      bool done = m.opt_iterations == 0;
-      while (!done) {
-        // ---- linesearch (solver.py:886-1341, 1662-1703)
-        if (lo) vd[c] = search;
-        __syncthreads();
-        float mv = symv(Mm, vd, h);
-        w.jv = gemv_rows(Jl, vd, lane, nvq);
-        const float snorm = sqrtf(search_dot);
-        const float gtol = fmaxf(tolerance * ls_tolerance * snorm * meaninertia * (float)nv, 1e-6f);
-        const float q1 = dsum(lo ? search * (ma - qfrc_smooth) : 0.0f);
-        const float q2 = dsum(lo ? 0.5f * search * mv : 0.0f);
-        const float qg0 = gauss;
-        Pt p0 = ls_point(w, 0.0f, q1, q2, qg0);
-        float lo_alpha_in = -safe_div(p0.g, p0.h);
-        Pt lo_in = ls_point(w, lo_alpha_in, q1, q2, qg0);
-        float alpha;
-        if (fabsf(lo_in.g) < gtol && lo_in.c < p0.c) {
-          alpha = lo_alpha_in;
-        } else {
-          alpha = 0.0f;
-          bool lo_less = lo_in.g < p0.g;
-          Pt plo = lo_less ? lo_in : p0;
-          Pt phi = lo_less ? p0 : lo_in;
-          for (int it = 0; it < m.opt_ls_iterations; it++) {
-            Pt ln = ls_point(w, plo.alpha - safe_div(plo.g, plo.h), q1, q2, qg0);
-            Pt hn = ls_point(w, phi.alpha - safe_div(phi.g, phi.h), q1, q2, qg0);
-            Pt md = ls_point(w, 0.5f * (plo.alpha + phi.alpha), q1, q2, qg0);
-            bool s1 = bracket(plo, ln);
-            if (s1) plo = ln;
-            bool s2 = bracket(plo, md);
-            if (s2) plo = md;
-            bool s3 = bracket(plo, hn);
-            if (s3) plo = hn;
-            bool h1 = bracket(phi, hn);
-            if (h1) phi = hn;
-            bool h2 = bracket(phi, md);
-            if (h2) phi = md;
-            bool h3 = bracket(phi, ln);
-            if (h3) phi = ln;
-            bool ls_done = (!(s1 || s2 || s3) && !(h1 || h2 || h3)) || (plo.g < 0.0f && plo.g > -gtol) ||
-                           (phi.g > 0.0f && phi.g < gtol);
-            bool improved = plo.c < p0.c || phi.c < p0.c;
-            if (improved) alpha = plo.c < phi.c ? plo.alpha : phi.alpha;
-            if (ls_done) break;
-          }
-        }
-        qacc = fmaf(alpha, search, qacc);
-        ma = fmaf(alpha, mv, ma);
-        w.jaref = fmaf(alpha, w.jv, w.jaref);
-        // ---- update constraint + gradient, CG direction (solver.py:3187-3254)
-        float prev_grad = grad, prev_Mgrad = Mgrad;
-        prev_cost = cost;
-        update_constraint();
-        update_gradient();
-        float beta = 0.0f;
-        if (!NEWTON) {
-          float num = dsum(lo ? grad * (Mgrad - prev_Mgrad) : 0.0f);
-          float den = dsum(lo ? prev_grad * prev_Mgrad : 0.0f);
-          beta = fmaxf(0.0f, num / fmaxf(MJW_MINVAL, den));
-        }
-        search = dof ? (-Mgrad + beta * search) : 0.0f;
-        search_dot = dsum(lo ? search * search : 0.0f);
-        niter++;
-        float improvement = (prev_cost - cost) * scale;
-        float gradient = sqrtf(grad_dot) * scale;
-        done = (improvement < tolerance) || (gradient < tolerance) || niter == m.opt_iterations;
-      }
-      if (lo && dof) {
-        d.qacc[gi] = qacc;
-        d.efc_Ma[gi] = ma;
-        d.qfrc_constraint[gi] = qfrc_c;
-      }
-      if (row) {
-        d.efc_force[(long)wid * njmax + lane] = force;
-        d.efc_state[(long)wid * d.njmax_pad + lane] = state;
-      }
-      if (lane == 0) d.solver_niter[wid] = niter;
-    }
-  }
-
-  PROF_MARK(PH_DSOLVE);
-  if (FLAGS & DF_EULER) {
-    // ---- forward.py:51-354 (_advance + euler)
-    const float dt = MR(opt_timestep)[0];
-    if (!(FLAGS & DF_SOLVE)) {
-      qacc = dof ? d.qacc[gi] : 0.0f;
-      ma = dof ? d.efc_Ma[gi] : 0.0f;
-    }
-    float qacc_adv = qacc;
-    __syncthreads();
-    // implicit integration only in the Euler-only kernel (dense_launch splits the step when needed)
-    const int fl = m.opt_disableflags;
-    const bool implicitfast = m.opt_integrator == INT_IMPLICITFAST;
-    const bool need_implicit = implicitfast ? (fl & (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) != (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)
-                                            : !(fl & (DSBL_EULERDAMP | DSBL_DAMPER));
-    if (FLAGS == DF_EULER && need_implicit) {
-      // euler damping: (M + dt diag(damping)) qacc_adv = M qacc (forward.py:322-340); implicitfast:
-      // (M - dt qDeriv) qacc_adv = M qacc, qDeriv = sum_a vel_a m_a m_a' - diag(damping) on the
-      // ancestor pattern of qM (forward.py:494-510, derivative.py:320-416)
-      float a[32];
-      f32x16 Md;
-      stage_fill(d.qM + (long)wid * np * np, np, nv, (fl & DSBL_DAMPER) ? nullptr : MR(dof_damping), dt, S, lane);
-      if (implicitfast && m.nu > 0 && !(fl & DSBL_ACTUATION)) {
-        for (int u = 0; u < m.nu; u++) {
-          float vel = actuator_vel_deriv(m, d, wid, u);
-          if (vel == 0.0f) continue;
-          const long gu = (long)wid * m.nu + u;
-          const int nnz = d.moment_rownnz[gu], adr = d.moment_rowadr[gu];
-          if (lane < nnz * nnz) {
-            const int k1 = lane / nnz, k2 = lane - k1 * nnz;
-            const long base = (long)wid * m.nJmom + adr;
-            const int i = d.moment_colind[base + k1], j = d.moment_colind[base + k2];
-            int p = i;
-            while (p > j) p = m.dof_parentid[p];
-            if (p == j && i < 32 && j < 32) {
-              float v = dt * vel * d.actuator_moment[base + k1] * d.actuator_moment[base + k2];
-              S[i * DSS + j] -= v;
-              if (i != j) S[j * DSS + i] -= v;
-            }
-          }
-          __syncthreads();
-        }
-      }
-      stage_rows(nv, S, lane, a, Md);
-      __syncthreads();
-      f32x16 Mdi = spd_inverse(a, lane);
-      if (lo) vd[c] = ma;
-      __syncthreads();
-      qacc_adv = symv(Mdi, vd, h);
-      if (!dof) qacc_adv = 0.0f;
-    }
-    // activations (forward.py:132-168)
-    const float* actrange = MR(actuator_actrange);
-    for (int u = lane; u < m.nu; u += 64) {
-      int adr = m.actuator_actadr[u];
-      for (int j = adr; adr >= 0 && j < adr + m.actuator_actnum[u]; j++) {
-        long ga = (long)wid * m.na + j;
-        d.act[ga] = next_act(dt, m.actuator_dyntype[u], MR(actuator_dynprm)[10 * u], actrange + 2 * u, d.act[ga], d.act_dot[ga], 1.0f,
-                             m.actuator_actlimited[u] != 0);
-      }
-    }
-    float qvel = dof ? pf_qvel + qacc_adv * dt : 0.0f;
-    if (lo) {
-      vd2[c] = qvel;
-      if (dof) {
-        d.qvel[gi] = qvel;
-        d.qacc_warmstart[gi] = qacc;
-      }
-    }
-    if (qpos_lds) vq[lane] = pf_qpos;
-    __syncthreads();
-    // positions are integrated in LDS and written back coalesced (global when nq > 64)
-    float* gq = qpos_lds ? vq : d.qpos + (long)wid * nq;
-    for (int j = lane; j < m.njnt; j += 64) {
-      int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j], jt = m.jnt_type[j];
-      if (jt == JNT_FREE) {
-        float q[4], qn[4];
-        for (int i = 0; i < 3; i++) gq[qa + i] = gq[qa + i] + dt * vd2[da + i];
-        for (int i = 0; i < 4; i++) q[i] = gq[qa + 3 + i];
-        quat_integrate(qn, q, vd2 + da + 3, dt);
-        for (int i = 0; i < 4; i++) gq[qa + 3 + i] = qn[i];
-      } else if (jt == JNT_BALL) {
-        float q[4], qn[4];
-        for (int i = 0; i < 4; i++) q[i] = gq[qa + i];
-        quat_integrate(qn, q, vd2 + da, dt);
-        for (int i = 0; i < 4; i++) gq[qa + i] = qn[i];
-      } else {
-        gq[qa] = gq[qa] + dt * vd2[da];
-      }
-    }
-    if (qpos_lds) {
-      __syncthreads();
-      if (lane < nq) d.qpos[(long)wid * nq + lane] = vq[lane];
-    }
-    if (lane == 0) d.time[wid] = d.time[wid] + dt;
-  }
-  PROF_MARK(PH_DEULER);
+  dense_world<FLAGS, NEWTON>(m, d, wid, sm);
 }
 
 // device self-checks of the primitives above (mjw_selftest): which = 0 -> per-wave dsum and

@@ -23,6 +23,8 @@
 // algorithms on the CPU for the parity tests.
 
 #include "mjw_common.h"
+
+#include <cstdlib>
 #include "mjw_ccd.h"
 #include "mjw_narrow.h"
 #include "mjw_flexcol.h"
@@ -32,6 +34,9 @@ namespace sp {
 
 #define MR_W(name) (MR(name)[0])
 
+// 256 threads per world: measured best on aloha_cloth (512, with or without an 80 / 64 VGPR cap on
+// the solve, and 256 with a 64 VGPR cap were 12-25 % slower; so was capping the solve's residency
+// to fit the per-world row state in the 256 MB MALL: DESIGN 3.6)
 constexpr int BLK = 256;
 constexpr int SORTN = 32;  // J-transpose segments up to this length are sorted in registers
 constexpr int SP_LDS_CNT_MAX = 8192;  // column counters of the J transpose live in LDS up to this nv + 1

@@ -2078,18 +2078,9 @@ __device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data
   WSYNC();
 }
 
+// the stages in STAGES of world w.wid by the calling wavefront
 template <int STAGES>
-// 4 waves per SIMD (<= 128 VGPRs): with the direct-mode LDS layout (9.8 KB per humanoid world)
-// this is 16 worlds per CU; the collision narrowphase spills ~40 registers to scratch for it
-// (measured: forward kernel 0.326 -> 0.303 ms at nworld 8192 against the unconstrained 160 VGPRs)
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  WS w;
-  w.s = smem;
-  w.si = reinterpret_cast<int*>(smem);
-  w.wid = w0 + (int)blockIdx.x;
-  w.lane = lane_id();
-  if (w.wid >= d.nworld) return;
+__device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   PROF_T0();
   load_state(m, d, L, w);
   load_smooth(m, d, L, w, STAGES);
@@ -2121,6 +2112,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mj
   PROF_MARK(PH_GSOLVE);
   if (STAGES & ST_EULER) euler(m, d, L, w);
   PROF_MARK(PH_GEULER);
+}
+
+// 4 waves per SIMD (<= 128 VGPRs): with the direct-mode LDS layout (9.8 KB per humanoid world)
+// this is 16 worlds per CU; the collision narrowphase spills ~40 registers to scratch for it
+// (measured: forward kernel 0.326 -> 0.303 ms at nworld 8192 against the unconstrained 160 VGPRs)
+template <int STAGES>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  WS w;
+  w.s = smem;
+  w.si = reinterpret_cast<int*>(smem);
+  w.wid = w0 + (int)blockIdx.x;
+  w.lane = lane_id();
+  if (w.wid >= d.nworld) return;
+  run_stages<STAGES>(m, d, L, w);
 }
 
 // -------------------------------------------------------------------------------------------
@@ -2286,8 +2292,9 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   if (dense_ok(m, d)) {
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel, for the
     // world range [w0, w0 + cnt) on stream st; `timed` records the optional bench events.
-    // (A two-stream split of one batch inside the step was measured and gave nothing: the join
-    // that ends the step serialises the halves' tails again)
+    // (Measured and dropped, DESIGN 4: a two-stream split of one batch inside the step -- the join
+    // that ends the step serialises the halves' tails again -- and one fused forward + dense
+    // kernel -- 128 VGPRs then spill in the solver loop, 0.637 vs 0.598 ms per step.)
     auto pipeline = [&](hipStream_t st, int w0, int cnt, bool timed) -> int {
       int r = 0;
       if (timed && g_ev[0]) (void)hipEventRecord(g_ev[0], st);
