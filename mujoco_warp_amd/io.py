@@ -321,6 +321,29 @@ def put_model(mjm, device=None) -> types.Model:
   return m
 
 
+# derived topology the C views carry beyond the reference Model fields
+DERIVED_INT_ARRAYS = {
+  "body_subtree_end": "body_subtree_end", "body_level": "body_level", "level_body": "level_body", "level_adr": "level_adr",
+  "jnt_limited_slide_hinge_adr": "jnt_limited_slide_hinge_adr", "jnt_limited_ball_adr": "jnt_limited_ball_adr",
+  "nxn_geom_pair": "nxn_geom_pair_typed", "nxn_pairid": "nxn_pairid_filtered", "nxn_ccdid": "nxn_ccdid",
+  "tree_dofadr": "tree_dofadr", "flex_cgeomadr": "flex_cgeomadr", "flex_cgeom": "flex_cgeom", "plane_geom": "plane_geom",
+  "flexvert_incadr": "flexvert_incadr", "flexvert_inc": "flexvert_inc",
+}
+DERIVED_SCALARS = ("nxn", "nxn_ccd", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow",
+                   "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane")
+
+
+def derive_model_fields(mjm) -> dict:
+  """Host helper for a reference-side binding: the derived index arrays and sizes of mjw_model_t that the
+  reference Model does not hold (DFS subtree ends, level lists, filtered / type-sorted NXN pairs, convex-pair
+  ids, sparse-path tree and flex incidence lists), computed from MjModel fields exactly as put_model does.
+  Returns {name: int32 numpy array or int}; the caller uploads the arrays once."""
+  m = put_model(mjm, device="cpu")
+  out = {name: getattr(m, attr).numpy().astype(np.int32).copy() for name, attr in DERIVED_INT_ARRAYS.items()}
+  out.update({name: int(getattr(m, name)) for name in DERIVED_SCALARS})
+  return out
+
+
 def _nb(t: torch.Tensor):
   return int(t.shape[0])
 

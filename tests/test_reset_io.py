@@ -204,3 +204,27 @@ def test_gpu_contact_pool_overflow_drops_rows():
     ncontact_rows += int(con.sum())
   # the stored contacts keep their rows: dropping past the pool removes rows, never the pool's own
   assert 0 < ncontact_rows < sum(int(full.nefc[w]) for w in range(4))
+
+
+def test_derive_model_fields_for_reference_binding():
+  """io.derive_model_fields: the derived arrays a reference-side binding uploads."""
+  import numpy as np
+
+  from mujoco_warp_amd import io
+  from tests.common import humanoid_model
+
+  mjm = humanoid_model()
+  f = io.derive_model_fields(mjm)
+  assert f["nxn"] == 161 and f["nxn_geom_pair"].shape == (161, 2) and f["nxn_ccd"] == 0
+  par = np.asarray(mjm.body_parentid)
+  # DFS subtree ranges: every body's descendants lie in [b, subtree_end[b])
+  for b in range(1, mjm.nbody):
+    p = par[b]
+    assert p <= b < f["body_subtree_end"][p] and f["body_subtree_end"][b] <= f["body_subtree_end"][p]
+    assert f["body_level"][b] == f["body_level"][p] + 1
+  # level lists: level_body[level_adr[l]:level_adr[l+1]] are the bodies of depth l
+  for lv in range(f["nlevel"]):
+    bodies = f["level_body"][f["level_adr"][lv]:f["level_adr"][lv + 1]]
+    assert (f["body_level"][bodies] == lv).all()
+  assert f["nlimited"] == len(f["jnt_limited_slide_hinge_adr"]) == 21
+  assert f["nJmom"] == mjm.nu and f["nv_pad"] == 28
