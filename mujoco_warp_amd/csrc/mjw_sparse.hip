@@ -25,6 +25,8 @@
 #include "mjw_common.h"
 
 #include <cstdlib>
+#include <mutex>
+
 #include "mjw_ccd.h"
 #include "mjw_narrow.h"
 #include "mjw_flexcol.h"
@@ -38,6 +40,7 @@ namespace sp {
 // the solve, and 256 with a 64 VGPR cap were 12-25 % slower; so was capping the solve's residency
 // to fit the per-world row state in the 256 MB MALL: DESIGN 3.6)
 constexpr int BLK = 256;
+constexpr int SOLVE_LDS_THREADS = 1024;  // threads per world of the LDS-resident CG (solve_kernel<2>)
 constexpr int SORTN = 32;  // J-transpose segments up to this length are sorted in registers
 constexpr int SP_LDS_CNT_MAX = 8192;  // column counters of the J transpose live in LDS up to this nv + 1
 constexpr int SP_LDS_ITEMS_MAX = 48 * 1024;  // per-item contact counts of the collision pass in LDS up to this
@@ -63,14 +66,19 @@ enum : int { EQ_FLEX = 4 };
 
 constexpr int SP_FBOX = 4;  // flexes whose bounding box the collision pass keeps (culls triangle-geom items)
 
+constexpr int NWAVE_MAX = 16;  // the LDS-resident solve runs 1024-thread worlds
+
 struct Smem {
-  float red[NWAVE][16];
-  int iscan[NWAVE];
+  float red[NWAVE_MAX][16];
+  float red2[2][NWAVE_MAX][16];  // double-buffered partials of block_sum_db
+  int iscan[NWAVE_MAX];
   int ival[8];
   float fbox[SP_FBOX][6];  // per flex: min xyz, max xyz of its vertices
 };
 
 __device__ __forceinline__ int tid() { return (int)threadIdx.x; }
+// threads per world of the running kernel (BLK, or 1024 for the LDS-resident solve)
+__device__ __forceinline__ int nthr() { return (int)blockDim.x; }
 
 // block-wide sums of N <= 16 floats; every thread gets the same (bitwise) totals
 template <int N>
@@ -87,7 +95,7 @@ __device__ __forceinline__ void block_sum(float (&v)[N], Smem& sm) {
 #pragma unroll
   for (int k = 0; k < N; k++) {
     float s = 0.0f;
-    for (int w = 0; w < NWAVE; w++) s += sm.red[w][k];
+    for (int w = 0; w < (nthr() >> 6); w++) s += sm.red[w][k];
     v[k] = s;
   }
 }
@@ -95,6 +103,36 @@ __device__ __forceinline__ void block_sum(float (&v)[N], Smem& sm) {
 __device__ __forceinline__ float block_sum1(float x, Smem& sm) {
   float v[1] = {x};
   block_sum<1>(v, sm);
+  return v[0];
+}
+
+// block_sum with one barrier: consecutive calls alternate between two partial buffers (`phase`,
+// uniform over the block), so a wave that runs ahead into the next call never overwrites partials
+// another wave is still reading -- that would take a second buffer-reuse barrier per call.  The
+// remaining barrier still orders every memory operation issued before the call.
+template <int N>
+__device__ __forceinline__ void block_sum_db(float (&v)[N], Smem& sm, int& phase) {
+  const int lane = tid() & 63, wv = tid() >> 6;
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = dsum(v[k]);
+  float(*red)[16] = sm.red2[phase];
+  phase ^= 1;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < N; k++) red[wv][k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    float t = 0.0f;
+    for (int w = 0; w < (nthr() >> 6); w++) t += red[w][k];
+    v[k] = t;
+  }
+}
+
+__device__ __forceinline__ float block_sum1_db(float x, Smem& sm, int& phase) {
+  float v[1] = {x};
+  block_sum_db<1>(v, sm, phase);
   return v[0];
 }
 
@@ -525,7 +563,7 @@ __device__ __forceinline__ void chain_load(const mjw_model_t& m, const float* A,
 
 // x = (L' D L)^-1 x in place, per tree (smooth.py:2813-2846)
 __device__ void solve_trees(const mjw_model_t& m, const float* LD, float* x) {
-  for (int t = tid(); t < m.ntree; t += BLK) {
+  for (int t = tid(); t < m.ntree; t += nthr()) {
     const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
     if (chain_tree(m, a, e)) {
       const int n = e - a;
@@ -570,7 +608,7 @@ __device__ void solve_trees(const mjw_model_t& m, const float* LD, float* x) {
 
 // y = M x (support.py:67-101 sparse mul_m), per tree: lower rows plus their transposes
 __device__ void mul_m_trees(const mjw_model_t& m, const float* M, const float* x, float* y) {
-  for (int t = tid(); t < m.ntree; t += BLK) {
+  for (int t = tid(); t < m.ntree; t += nthr()) {
     const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
     if (chain_tree(m, a, e)) {
       const int n = e - a;
@@ -1835,6 +1873,7 @@ struct SolveCtx {
   float *grad, *Mgrad, *search, *mv, *pgrad, *pMgrad;
   const float *M, *LD;
   float cost, prev_cost, gauss, search_dot, grad_dot;
+  int rphase;  // block_sum_db buffer parity (uniform)
 };
 
 __device__ __forceinline__ void eval_row_v(const SolveCtx& c, int r, float D, float jaref, float jv, float alpha, float* o) {
@@ -1875,16 +1914,16 @@ __device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, 
 }
 
 // eval_row at NA step sizes over every row (o: NA x 3 sums).  The row passes are latency bound, so
-// each thread loads RU rows (r0, r0 + BLK, ...: the same per-thread order as a plain strided loop,
+// each thread loads RU rows (r0, r0 + nthr(), ...: the same per-thread order as a plain strided loop,
 // hence the same sums) before evaluating any of them.
-constexpr int RU = 4;
+constexpr int RU = 4;  // 8 and 16 rows in flight per thread measured 14 % and 73 % slower on aloha_cloth
 template <int NA>
 __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas, float* o) {
-  for (int r0 = c.ne + tid(); r0 < c.nefc; r0 += RU * BLK) {  // equality rows: folded into the quadratic
+  for (int r0 = c.ne + tid(); r0 < c.nefc; r0 += RU * nthr()) {  // equality rows: folded into the quadratic
     float D[RU], ja[RU], jv[RU];
 #pragma unroll
     for (int u = 0; u < RU; u++) {
-      const int r = r0 + u * BLK;
+      const int r = r0 + u * nthr();
       const bool ok = r < c.nefc;
       D[u] = ok ? c.D[r] : 0.0f;
       ja[u] = ok ? c.Jaref[r] : 0.0f;
@@ -1892,7 +1931,7 @@ __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas
     }
 #pragma unroll
     for (int u = 0; u < RU; u++) {
-      const int r = r0 + u * BLK;
+      const int r = r0 + u * nthr();
       if (r < c.nefc) {
 #pragma unroll
         for (int a = 0; a < NA; a++) eval_row_v(c, r, D[u], ja[u], jv[u], alphas[a], o + 3 * a);
@@ -1904,11 +1943,11 @@ __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas
 // `alpha`: the linesearch step still to be applied to Jaref (fused here: Jaref += alpha * jv)
 __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   float cost = 0.0f;
-  for (int r0 = tid(); r0 < c.nefc; r0 += RU * BLK) {
+  for (int r0 = tid(); r0 < c.nefc; r0 += RU * nthr()) {
   float Du[RU], jau[RU];
 #pragma unroll
   for (int u = 0; u < RU; u++) {
-    const int r = r0 + u * BLK;
+    const int r = r0 + u * nthr();
     const bool ok = r < c.nefc;
     Du[u] = ok ? c.D[r] : 0.0f;
     jau[u] = ok ? c.Jaref[r] : 0.0f;
@@ -1916,7 +1955,7 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   }
 #pragma unroll
   for (int u = 0; u < RU; u++) {
-    const int r = r0 + u * BLK;
+    const int r = r0 + u * nthr();
     if (r >= c.nefc) break;
     const float D = Du[u];
     const float jaref = jau[u];
@@ -1942,7 +1981,7 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   }
   __syncthreads();
   float g = 0.0f;
-  for (int i = tid(); i < c.nv; i += BLK) {
+  for (int i = tid(); i < c.nv; i += nthr()) {
     float s = 0.0f;
     // 4 entries in flight (index loads, then the dependent force gathers), same summation order
     const int pa = c.JT_adr[i], pb = c.JT_adr[i + 1];
@@ -1961,7 +2000,7 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
     g += (c.Ma[i] - c.qfrc_s[i]) * (c.qacc[i] - c.qacc_s[i]);
   }
   float v[2] = {cost, g};
-  block_sum<2>(v, sm);
+  block_sum_db<2>(v, sm, c.rphase);
   c.prev_cost = c.cost;
   c.gauss = 0.5f * v[1];
   c.cost = v[0] + 0.5f * v[1];
@@ -1969,13 +2008,13 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
 
 __device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
   float gd = 0.0f;
-  for (int i = tid(); i < c.nv; i += BLK) {
+  for (int i = tid(); i < c.nv; i += nthr()) {
     const float g = c.Ma[i] - c.qfrc_s[i] - c.qfrc_c[i];
     c.grad[i] = g;
     c.Mgrad[i] = g;
     gd += g * g;
   }
-  c.grad_dot = block_sum1(gd, sm);  // syncs
+  c.grad_dot = block_sum1_db(gd, sm, c.rphase);  // syncs
   solve_trees(m, c.LD, c.Mgrad);
   __syncthreads();
 }
@@ -1991,13 +2030,13 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
   // equality rows are quadratic for every step size: their cost 0.5 D (Jaref + a jv)^2 is folded
   // into the Gauss quadratic once here (v5[5..7]), and the line-search passes skip them
   float v5[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r0 = tid(); r0 < c.nefc; r0 += RU * BLK) {
+  for (int r0 = tid(); r0 < c.nefc; r0 += RU * nthr()) {
     // RU rows interleaved so their (column -> search) gathers overlap; per-row order unchanged
     int nz[RU], kmax = 0;
     float acc[RU];
 #pragma unroll
     for (int u = 0; u < RU; u++) {
-      const int r = r0 + u * BLK;
+      const int r = r0 + u * nthr();
       nz[u] = r < c.nefc ? c.Jnnz[r] : 0;
       kmax = max(kmax, nz[u]);
       acc[u] = 0.0f;
@@ -2007,7 +2046,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
       int col[RU];
 #pragma unroll
       for (int u = 0; u < RU; u++) {
-        const long q = (long)k * c.P + r0 + u * BLK;
+        const long q = (long)k * c.P + r0 + u * nthr();
         v[u] = k < nz[u] ? c.J[q] : 0.0f;
         col[u] = k < nz[u] ? c.Jcol[q] : 0;
       }
@@ -2017,7 +2056,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
     }
 #pragma unroll
     for (int u = 0; u < RU; u++) {
-    const int r = r0 + u * BLK;
+    const int r = r0 + u * nthr();
     if (r >= c.nefc) break;
     const float s = acc[u];
     c.jv[r] = s;
@@ -2035,11 +2074,11 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
   const float snorm = sqrtf(c.search_dot);
   const float scale = MR_W(stat_meaninertia) * (float)c.nv;
   const float gtol = fmaxf(MR_W(opt_tolerance) * MR_W(opt_ls_tolerance) * snorm * scale, 1e-6f);
-  for (int i = tid(); i < c.nv; i += BLK) {
+  for (int i = tid(); i < c.nv; i += nthr()) {
     v5[3] += c.search[i] * (c.Ma[i] - c.qfrc_s[i]);
     v5[4] += 0.5f * c.search[i] * c.mv[i];
   }
-  block_sum<8>(v5, sm);
+  block_sum_db<8>(v5, sm, c.rphase);
   const float qg0 = c.gauss + v5[5], qg1 = v5[3] + v5[6], qg2 = v5[4] + v5[7];
   const float p0[3] = {qg0 + v5[0], qg1 + v5[1], 2.0f * qg2 + v5[2]};
   auto gauss_at = [&](float a, float* o) {
@@ -2050,7 +2089,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
   const float lo_alpha_in = -safe_div(p0[1], p0[2]);
   float lo_in[3] = {0, 0, 0};
   eval_rows<1>(c, &lo_alpha_in, lo_in);
-  block_sum<3>(lo_in, sm);
+  block_sum_db<3>(lo_in, sm, c.rphase);
   {
     float g[3];
     gauss_at(lo_alpha_in, g);
@@ -2076,7 +2115,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
       float v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       const float al[3] = {lo_next_alpha, hi_next_alpha, mid_alpha};
       eval_rows<3>(c, al, v9);
-      block_sum<9>(v9, sm);
+      block_sum_db<9>(v9, sm, c.rphase);
       float lo_next[3], hi_next[3], mid[3], g[3];
       gauss_at(lo_next_alpha, g);
       for (int k = 0; k < 3; k++) lo_next[k] = g[k] + v9[k];
@@ -2104,7 +2143,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
   } else {
     alpha = lo_alpha_in;
   }
-  for (int i = tid(); i < c.nv; i += BLK) {
+  for (int i = tid(); i < c.nv; i += nthr()) {
     c.qacc[i] += alpha * c.search[i];
     c.Ma[i] += alpha * c.mv[i];
   }
@@ -2114,9 +2153,12 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
 
 // PART 0: qacc from the warmstart, Jaref, and the transposed index of J; PART 1: the CG iterations.
 // Two launches so that the index build (register-resident segment sorts) and the solver loop each
-// get their own register budget.
+// get their own register budget.  PART 2 is PART 1 with the per-row line-search state (Jaref, jv)
+// in LDS and SOLVE_LDS_THREADS threads per world: the line-search passes, which re-read that state
+// several times per CG iteration, then stop streaming it through HBM (sparse_launch picks it when
+// 2 * njmax floats fit the LDS of a CU).
 template <int PART>
-__global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const mjw_data_t d) {
+__global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_kernel(const mjw_model_t m, const mjw_data_t d) {
   __shared__ Smem sm;
   const int wid = blockIdx.x;
   const int nv = m.nv, njmax = d.njmax;
@@ -2124,12 +2166,13 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   const float* qacc_s = d.qacc_smooth + (long)wid * nv;
   if (njmax == 0 || nv == 0) {
     if (PART == 0) return;
-    for (int i = tid(); i < nv; i += BLK) qacc[i] = qacc_s[i];
+    for (int i = tid(); i < nv; i += nthr()) qacc[i] = qacc_s[i];
     if (tid() == 0) d.solver_niter[wid] = 0;
     return;
   }
   SPROF_T0();
   SolveCtx c;
+  c.rphase = 0;
   c.nv = nv;
   c.nefc = min(d.nefc[wid], njmax);
   c.ne = d.ne[wid];
@@ -2156,6 +2199,13 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   c.state = d.efc_state + (long)wid * d.njmax_pad;
   c.Jaref = d.sp_row + (long)wid * njmax * 2;
   c.jv = c.Jaref + njmax;
+  if constexpr (PART == 2) {
+    float* rows = reinterpret_cast<float*>(s_cnt);
+    for (int r = tid(); r < c.nefc; r += nthr()) rows[r] = c.Jaref[r];
+    c.Jaref = rows;
+    c.jv = rows + njmax;
+    __syncthreads();
+  }
   c.qacc = qacc;
   c.Ma = d.efc_Ma + (long)wid * nv;
   c.qfrc_c = d.qfrc_constraint + (long)wid * nv;
@@ -2174,14 +2224,14 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   const bool ws = !(m.opt_disableflags & DSBL_WARMSTART);
   if constexpr (PART == 0) {
   // transposed index of J: counts, scan, fill, per-column sort (deterministic J'f)
-  for (int i = tid(); i <= nv; i += BLK) cnt[i] = 0;
-  for (int i = tid(); i < nv; i += BLK) qacc[i] = ws ? warm[i] : qacc_s[i];
+  for (int i = tid(); i <= nv; i += nthr()) cnt[i] = 0;
+  for (int i = tid(); i < nv; i += nthr()) qacc[i] = ws ? warm[i] : qacc_s[i];
   __syncthreads();
-  for (int r = tid(); r < c.nefc; r += BLK)
+  for (int r = tid(); r < c.nefc; r += nthr())
     for (int k = 0; k < c.Jnnz[r]; k++) atomicAdd(&cnt[c.Jcol[k * P + r]], 1);
   __syncthreads();
   int run = 0;
-  for (int c0 = 0; c0 < nv; c0 += BLK) {
+  for (int c0 = 0; c0 < nv; c0 += nthr()) {
     const int i = c0 + tid();
     const int n = i < nv ? cnt[i] : 0;
     int chunk;
@@ -2193,7 +2243,7 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   __syncthreads();
   // fill carries the values (and computes Jaref on the way); the per-column sort of the
   // (row * njrow + slot) codes then fixes the summation order of J'f whatever the atomics did
-  for (int r = tid(); r < c.nefc; r += BLK) {
+  for (int r = tid(); r < c.nefc; r += nthr()) {
     float s = 0.0f;
     for (int k = 0; k < c.Jnnz[r]; k++) {
       const float v = c.J[k * P + r];
@@ -2206,7 +2256,7 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
     c.Jaref[r] = s - c.aref[r];
   }
   __syncthreads();
-  for (int i = tid(); i < nv; i += BLK) {
+  for (int i = tid(); i < nv; i += nthr()) {
     const int a = JT_adr[i], b = JT_adr[i + 1];
     if (b - a <= SORTN) {
       // short segment: loaded at once, odd-even transposition network in registers
@@ -2257,11 +2307,11 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
   update_constraint(c, sm);
   update_gradient(m, c, sm);
   float sd = 0.0f;
-  for (int i = tid(); i < nv; i += BLK) {
+  for (int i = tid(); i < nv; i += nthr()) {
     c.search[i] = -c.Mgrad[i];
     sd += c.Mgrad[i] * c.Mgrad[i];
   }
-  c.search_dot = block_sum1(sd, sm);
+  c.search_dot = block_sum1_db(sd, sm, c.rphase);
   const float scale = 1.0f / (MR_W(stat_meaninertia) * (float)nv);
   const float tol = MR_W(opt_tolerance);
   int niter = 0;
@@ -2270,7 +2320,7 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
     for (;;) {
       const float alpha = linesearch(m, c, wid, sm);
       SPROF_MARK(SPH_SLS);
-      for (int i = tid(); i < nv; i += BLK) {
+      for (int i = tid(); i < nv; i += nthr()) {
         c.pgrad[i] = c.grad[i];
         c.pMgrad[i] = c.Mgrad[i];
       }
@@ -2279,19 +2329,19 @@ __global__ void __launch_bounds__(BLK) solve_kernel(const mjw_model_t m, const m
       update_gradient(m, c, sm);
       SPROF_MARK(SPH_SUPD);
       float nd[2] = {0.0f, 0.0f};
-      for (int i = tid(); i < nv; i += BLK) {
+      for (int i = tid(); i < nv; i += nthr()) {
         nd[0] += c.grad[i] * (c.Mgrad[i] - c.pMgrad[i]);
         nd[1] += c.pgrad[i] * c.pMgrad[i];
       }
-      block_sum<2>(nd, sm);
+      block_sum_db<2>(nd, sm, c.rphase);
       const float beta = fmaxf(0.0f, nd[0] / fmaxf(MJW_MINVAL, nd[1]));
       float s2 = 0.0f;
-      for (int i = tid(); i < nv; i += BLK) {
+      for (int i = tid(); i < nv; i += nthr()) {
         const float v = -c.Mgrad[i] + beta * c.search[i];
         c.search[i] = v;
         s2 += v * v;
       }
-      c.search_dot = block_sum1(s2, sm);
+      c.search_dot = block_sum1_db(s2, sm, c.rphase);
       niter++;
       SPROF_MARK(SPH_SCG);
       const float improvement = (c.prev_cost - c.cost) * scale;
@@ -2387,7 +2437,22 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
   if (stages & ST_SOLVE) {
     const size_t lds = (m->nv + 1) <= sp::SP_LDS_CNT_MAX ? (size_t)(m->nv + 1) * 4 : 0;
     hipLaunchKernelGGL(sp::solve_kernel<0>, dim3(nw), dim3(sp::BLK), lds, s, *m, *d);
-    hipLaunchKernelGGL(sp::solve_kernel<1>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
+    // CG iterations: with Jaref / jv of every row in LDS when 2 * njmax floats fit (MJW_SP_SOLVE_LDS=0
+    // keeps them in HBM)
+    const size_t row_lds = (size_t)2 * d->njmax * 4;
+    static const bool lds_ok = [] {
+      const char* e = getenv("MJW_SP_SOLVE_LDS");
+      return !(e && e[0] == '0');
+    }();
+    if (lds_ok && d->njmax > 0 && row_lds <= 150 * 1024) {
+      static std::once_flag once;
+      std::call_once(once, [] {
+        (void)hipFuncSetAttribute((const void*)sp::solve_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      });
+      hipLaunchKernelGGL(sp::solve_kernel<2>, dim3(nw), dim3(sp::SOLVE_LDS_THREADS), row_lds, s, *m, *d);
+    } else {
+      hipLaunchKernelGGL(sp::solve_kernel<1>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
+    }
   }
   if (stages & ST_EULER) hipLaunchKernelGGL(sp::euler_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
   return (int)hipGetLastError();
