@@ -1087,18 +1087,21 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
   }
   float v[2] = {(float)cnt, (float)passed};
   block_sum<2>(v, sm);
-  // every world keeps at most its share naconmax / nworld of the pool, in item order: the kept set
-  // is then the oracle's per-world nconmax cut and independent of the other worlds (and of sharding);
-  // the reference's global atomic pool drops an arbitrary overflow instead
+  // one global pool of naconmax contacts shared by all worlds, as the reference's (collision_core.py:
+  // 212-231: nacon counts every contact found, contacts past the pool are dropped): the world
+  // reserves its contiguous block with one atomic and keeps the part of it inside the pool, its
+  // contacts in item order.  Which world overflows depends on the atomics' order, as there.
   const int total = (int)v[0];
-  const int keep = min(total, d.naconmax / max(d.nworld, 1));
   if (tid() == 0) {
-    sm.ival[0] = keep ? atomicAdd(d.nacon, keep) : 0;
+    const int base = total ? atomicAdd(d.nacon, total) : 0;
+    sm.ival[0] = base;
+    sm.ival[1] = total ? max(0, min(total, d.naconmax - base)) : 0;
     if (v[1] > 0.0f) atomicAdd(d.ncollision, (int)v[1]);
-    ncw[0] = sm.ival[0];
-    ncw[1] = keep;
+    ncw[0] = base;
+    ncw[1] = sm.ival[1];
   }
   __syncthreads();
+  const int keep = sm.ival[1];
   const int start = sm.ival[0], lim = start + keep;
   int run = start;
   if (keep) {

@@ -241,7 +241,7 @@ def test_gpu_cloth_rollout_parity_and_determinism(which):
 def test_gpu_aloha_sharding_is_bitwise_invariant():
   """SURVEY §8(e) on the sparse path: two shards (world_offset 0 / 8) of a 16-world aloha_cloth
   rollout with the benchmark's control noise equal the single 16-world run bitwise -- worlds never
-  read each other, and each keeps its own share of the contact pool."""
+  read each other (the pool is large enough that none overflows)."""
   import torch
 
   import mujoco_warp_amd as mjw
@@ -266,3 +266,46 @@ def test_gpu_aloha_sharding_is_bitwise_invariant():
   np.testing.assert_array_equal(np.concatenate([q0, q1]), q_all)
   np.testing.assert_array_equal(np.concatenate([v0, v1]), v_all)
   assert np.isfinite(q_all).all()
+
+
+@pytest.mark.gpu
+def test_gpu_aloha_global_contact_pool_overflow():
+  """The sparse path shares one pool of naconmax contacts between worlds like the reference
+  (collision_core.py:212-231): nacon counts every contact found, each world's block is reserved with
+  one atomic, and contacts past the pool are dropped together with their rows."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+  from mujoco_warp_amd.types import ConstraintType
+
+  mjm = aloha_model()
+  nworld = 4
+  qpos, qvel, ctrl = aloha_states(mjm, nworld, seed=3)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=ALOHA_NJMAX, nconmax=ALOHA_NCONMAX)
+  mjw.fwd_position(m, d)
+  torch.cuda.synchronize()
+  per_world = d.ncon_world[:, 1].cpu().numpy().copy()
+  total = int(per_world.sum())
+  assert total > 1000
+  pool = total // 2 + 17
+  d2s = mjw.put_data(mjm, mjcf.MjData(mjm), nworld=nworld, nconmax=ALOHA_NCONMAX, njmax=ALOHA_NJMAX, naconmax=pool, device="cuda", m=m)
+  for f in ("qpos", "qvel", "ctrl"):
+    getattr(d2s, f).copy_(getattr(d, f))
+  m2 = m
+  mjw.fwd_position(m2, d2s)
+  torch.cuda.synchronize()
+  assert int(d2s.nacon[0]) == total  # every contact found is counted
+  ncw = d2s.ncon_world.cpu().numpy()
+  assert int(ncw[:, 1].sum()) == pool  # the pool is filled exactly
+  for w in range(nworld):
+    base, kept = int(ncw[w, 0]), int(ncw[w, 1])
+    assert kept == max(0, min(per_world[w], pool - base))
+    if kept:
+      assert (d2s.contact.worldid[base:base + kept].cpu().numpy() == w).all()
+    # contact rows only for the kept contacts
+    n = int(d2s.nefc[w])
+    typ = d2s.efc.type[w, :n].cpu().numpy()
+    ids = d2s.efc.id[w, :n].cpu().numpy()
+    con = typ == int(ConstraintType.CONTACT_PYRAMIDAL)
+    assert (ids[con] < pool).all()
