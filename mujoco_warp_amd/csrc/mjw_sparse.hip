@@ -40,7 +40,8 @@ namespace sp {
 // the solve, and 256 with a 64 VGPR cap were 12-25 % slower; so was capping the solve's residency
 // to fit the per-world row state in the 256 MB MALL: DESIGN 3.6)
 constexpr int BLK = 256;
-constexpr int SOLVE_LDS_THREADS = 1024;  // threads per world of the LDS-resident CG (solve_kernel<2>)
+constexpr int SOLVE_LDS_THREADS = 1024;
+constexpr int SP_LDS_SEARCH_MAX = 8192;  // the CG search direction lives in LDS up to this nv
 constexpr int SORTN = 32;  // J-transpose segments up to this length are sorted in registers
 constexpr int SP_LDS_CNT_MAX = 8192;  // column counters of the J transpose live in LDS up to this nv + 1
 constexpr int SP_LDS_ITEMS_MAX = 48 * 1024;  // per-item contact counts of the collision pass in LDS up to this
@@ -2221,6 +2222,10 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
   c.mv = vec + 3 * nv;
   c.pgrad = vec + 4 * nv;
   c.pMgrad = vec + 5 * nv;
+  if constexpr (PART != 0) {
+    // the search direction in LDS when it fits: the jv pass gathers it by column every CG iteration
+    if (nv <= SP_LDS_SEARCH_MAX) c.search = reinterpret_cast<float*>(s_cnt) + (PART == 2 ? 2 * njmax : 0);
+  }
   c.M = d.qM + (long)wid * m.nM;
   c.LD = d.qLD + (long)wid * m.nM;
   const float* warm = d.qacc_warmstart + (long)wid * nv;
@@ -2440,12 +2445,14 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
   if (stages & ST_SOLVE) {
     const size_t lds = (m->nv + 1) <= sp::SP_LDS_CNT_MAX ? (size_t)(m->nv + 1) * 4 : 0;
     hipLaunchKernelGGL(sp::solve_kernel<0>, dim3(nw), dim3(sp::BLK), lds, s, *m, *d);
-    // CG iterations: with Jaref / jv of every row in LDS when 2 * njmax floats fit (MJW_SP_SOLVE_LDS=0
-    // keeps them in HBM)
-    const size_t row_lds = (size_t)2 * d->njmax * 4;
+    // CG iterations, the search direction in LDS.  MJW_SP_SOLVE_LDS=1 also keeps Jaref / jv of every
+    // row in LDS (1024-thread worlds, when 2 * njmax floats fit): measured equal on aloha_cloth
+    // (22.75 vs 22.80 ms per step) and 4 % slower on cloth, so the rows stay in HBM by default
+    const size_t search_lds = m->nv <= sp::SP_LDS_SEARCH_MAX ? (size_t)m->nv * 4 : 0;
+    const size_t row_lds = (size_t)2 * d->njmax * 4 + search_lds;
     static const bool lds_ok = [] {
       const char* e = getenv("MJW_SP_SOLVE_LDS");
-      return !(e && e[0] == '0');
+      return e && e[0] == '1';
     }();
     if (lds_ok && d->njmax > 0 && row_lds <= 150 * 1024) {
       static std::once_flag once;
@@ -2454,7 +2461,7 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
       });
       hipLaunchKernelGGL(sp::solve_kernel<2>, dim3(nw), dim3(sp::SOLVE_LDS_THREADS), row_lds, s, *m, *d);
     } else {
-      hipLaunchKernelGGL(sp::solve_kernel<1>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
+      hipLaunchKernelGGL(sp::solve_kernel<1>, dim3(nw), dim3(sp::BLK), search_lds, s, *m, *d);
     }
   }
   if (stages & ST_EULER) hipLaunchKernelGGL(sp::euler_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
