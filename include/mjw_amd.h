@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 10
+#define MJW_ABI_VERSION 11
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -37,7 +37,7 @@
   X(nxn) X(nlevel) X(nlimited) X(nlimited_ball) X(nmaxcondim) X(nmaxpyramid) X(nv_pad) X(nJmom)    \
   X(neq) X(neq_cw)                                                                                 \
   X(nsensor) X(nsensordata) X(sensor_rne_postconstraint) X(nsensor_acc)                           \
-  X(nxn_ccd) X(opt_ccd_iterations) X(ccd_epa_iterations)                                           \
+  X(nxn_ccd) X(nxn_box) X(opt_ccd_iterations) X(ccd_epa_iterations)                                           \
   X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations) X(opt_ls_iterations)             \
   X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)                                  \
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \

@@ -608,6 +608,10 @@ __device__ __forceinline__ bool broadphase_filter(const mjw_model_t& m, const La
 }
 
 // narrowphase of one pair (collision_primitive.py:280-662); pair is type-sorted on the host
+// BOX = false compiles out the pairs with a box (sphere-box, capsule-box; plane-box and box-box are
+// handled by the caller): models without boxes then run a kernel with 118 instead of 128+ VGPRs and
+// no scratch spills
+template <bool BOX>
 __device__ __forceinline__ void narrowphase(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2, float margin, Con2& c) {
   const float* geom_size = MR(geom_size);
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
@@ -639,12 +643,12 @@ __device__ __forceinline__ void narrowphase(const mjw_model_t& m, const Lay& L, 
     c.n = 1;
   } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
     capsule_capsule(c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], margin);
-  } else if (t1 == GEOM_SPHERE && t2 == GEOM_BOX) {  // collision_primitive.py:1047-1114
+  } else if (BOX && t1 == GEOM_SPHERE && t2 == GEOM_BOX) {  // collision_primitive.py:1047-1114
     float nrm[3];
     c.dist[0] = sphere_box(c.pos[0], nrm, p1, s1[0], p2, r2, s2);
     make_frame(c.frame[0], nrm);
     c.n = 1;
-  } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {  // collision_primitive.py:1117-1199
+  } else if (BOX && t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {  // collision_primitive.py:1117-1199
     capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
   }
 }
@@ -810,6 +814,7 @@ __device__ __forceinline__ void eq_connect_weld(const mjw_model_t& m, const mjw_
 }
 
 // collision_driver.py:754-789 + constraint.py:2209-2779 (friction-dof, limits, pyramidal contacts)
+template <bool BOX>
 __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -1027,8 +1032,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           g2 = m.nxn_geom_pair[2 * p + 1];
           pairid0 = m.nxn_pairid[2 * p];
           margin = geom_margin[g1] + geom_margin[g2];
-          pbox = m.geom_type[g1] == GEOM_PLANE && m.geom_type[g2] == GEOM_BOX;
-          ccd = m.geom_type[g1] == GEOM_BOX && m.geom_type[g2] == GEOM_BOX;
+          pbox = BOX && m.geom_type[g1] == GEOM_PLANE && m.geom_type[g2] == GEOM_BOX;
+          ccd = BOX && m.geom_type[g1] == GEOM_BOX && m.geom_type[g2] == GEOM_BOX;
           if (ccd) {
           } else if (pbox) {
             const float* r1 = s + L.gxmat + 9 * g1;
@@ -1039,7 +1044,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
               if (dist < margin && pairid0 >= -1) bmask |= 1u << q;
             }
           } else {
-            narrowphase(m, L, s, wid, g1, g2, margin, c);
+            narrowphase<BOX>(m, L, s, wid, g1, g2, margin, c);
           }
         }
         // convex pairs: results of the CCD pre-pass (ccd_kernel), c.n contacts at distance c.dist[0]
@@ -2079,7 +2084,7 @@ __device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data
 }
 
 // the stages in STAGES of world w.wid by the calling wavefront
-template <int STAGES>
+template <int STAGES, bool BOX>
 __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   PROF_T0();
   load_state(m, d, L, w);
@@ -2095,7 +2100,7 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
     PROF_MARK(PH_CAM);
     crb_qM(m, d, L, w);
     PROF_MARK(PH_CRB);
-    collision_and_constraints(m, d, L, w);
+    collision_and_constraints<BOX>(m, d, L, w);
     PROF_MARK(PH_COLL);
     transmission(m, d, L, w);
     PROF_MARK(PH_TRN);
@@ -2117,7 +2122,7 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
 // 4 waves per SIMD (<= 128 VGPRs): with the direct-mode LDS layout (9.8 KB per humanoid world)
 // this is 16 worlds per CU; the collision narrowphase spills ~40 registers to scratch for it
 // (measured: forward kernel 0.326 -> 0.303 ms at nworld 8192 against the unconstrained 160 VGPRs)
-template <int STAGES>
+template <int STAGES, bool BOX = true>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   WS w;
@@ -2126,7 +2131,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mj
   w.wid = w0 + (int)blockIdx.x;
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
-  run_stages<STAGES>(m, d, L, w);
+  run_stages<STAGES, BOX>(m, d, L, w);
 }
 
 // -------------------------------------------------------------------------------------------
@@ -2245,9 +2250,18 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   }
   static std::once_flag once;
   std::call_once(once, [] {
-    (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if constexpr ((STAGES & mjw::ST_POS) != 0)
+      (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
-  hipLaunchKernelGGL(mjw::mjw_kernel<STAGES>, dim3(count), dim3(64), lds, s, *m, *d, L, w0);
+  // position-stage kernels without the box narrowphase paths for models that have no box pairs
+  if constexpr ((STAGES & mjw::ST_POS) != 0) {
+    if (m->nxn_box == 0) {
+      hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
+      return set_err(hipGetLastError(), name);
+    }
+  }
+  hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, true>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
   return set_err(hipGetLastError(), name);
 }
 

@@ -221,6 +221,7 @@ def put_model(mjm, device=None) -> types.Model:
   kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in pairs]
   ccd_set = _SPARSE_CCD_PAIRS if sparse else _CCD_PAIRS
   m.nxn_ccd = int(sum(k in ccd_set for k in kinds))
+  m.nxn_box = int(sum(6 in k for k in kinds))  # pairs with a box: the forward kernel's box narrowphase paths
   ccdid = np.cumsum([k in ccd_set for k in kinds]) - 1
   m.nxn_ccdid = _i32(np.where([k in ccd_set for k in kinds], ccdid, -1) if kinds else np.zeros(0), dev)
   m.nmesh, m.nmeshvert = int(getattr(mjm, "nmesh", 0)), int(getattr(mjm, "nmeshvert", 0))
@@ -329,7 +330,7 @@ DERIVED_INT_ARRAYS = {
   "tree_dofadr": "tree_dofadr", "flex_cgeomadr": "flex_cgeomadr", "flex_cgeom": "flex_cgeom", "plane_geom": "plane_geom",
   "flexvert_incadr": "flexvert_incadr", "flexvert_inc": "flexvert_inc",
 }
-DERIVED_SCALARS = ("nxn", "nxn_ccd", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow",
+DERIVED_SCALARS = ("nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow",
                    "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane")
 
 
