@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-KERNELS = {"forward": "mjw_kernel<79>", "dense": "dense_kernel<7, false>"}
+KERNELS = {"forward": "mjw_kernel<79", "dense": "dense_kernel<7, false>"}
 SPARSE_KERNELS = {"forward": "sp::forward_kernel", "solve": "sp::solve_kernel", "ccd": "sp::ccd_kernel", "euler": "sp::euler_kernel"}
 
 
