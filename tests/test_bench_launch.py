@@ -77,3 +77,23 @@ def test_gpu_bench_two_ranks_strong_and_graph(tmp_path):
   got = [np.load(tmp_path / "s" / f"qpos_rank{r}.npz") for r in range(2)]
   assert [int(z["offset"]) for z in got] == [0, 151]
   np.testing.assert_array_equal(np.concatenate([z["qpos"] for z in got]), qg)
+
+
+def test_pmc_traffic_is_bound_to_the_kernel_sources(tmp_path):
+  """bench.py reports `roofline.traffic` only from a PMC summary of the same workload taken on a build of
+  the current kernel sources (csrc_sha == build.sources_hash())."""
+  sys.path.insert(0, ROOT)
+  import bench
+  from mujoco_warp_amd import build
+
+  pmc = {"nworld": 8192, "solver": "CG", "model": "humanoid", "csrc_sha": build.sources_hash(),
+         "kernels": {"forward": {"hbm_bytes_per_launch": 123.0}}}
+  f = tmp_path / "pmc_humanoid_r99.json"
+  f.write_text(json.dumps(pmc))
+  assert bench.pmc_traffic(str(f), "humanoid", 8192, "CG", False)[0] == 123.0
+  assert bench.pmc_traffic(str(f), "humanoid", 4096, "CG", False)[0] is None  # other workload
+  pmc["csrc_sha"] = "0" * 16
+  f.write_text(json.dumps(pmc))
+  traffic, why = bench.pmc_traffic(str(f), "humanoid", 8192, "CG", False)
+  assert traffic is None and "predates" in why
+  assert bench.pmc_traffic(str(tmp_path / "missing.json"), "humanoid", 8192, "CG", False)[0] is None
