@@ -435,7 +435,7 @@ def main():
         "traffic": traffic,
         "traffic_source": traffic_src,
         "kernel": ("mjw::sp::forward_kernel + mjw::sp::solve_kernel (sparse path: forward + CG)" if m.is_sparse else
-                   "mjw::mjw_kernel<79> (forward: position/velocity/actuation/qfrc_smooth)"
+                   f"mjw::mjw_kernel<79, {'false' if m.nxn_box == 0 else 'true'}> (forward: position/velocity/actuation/qfrc_smooth)"
                    + (" + mjw::ccd_kernel (convex pre-pass)" if m.nxn_ccd else "")),
         "kernel_ms": kernel_ms,
         "worlds_per_launch": nlaunch,
