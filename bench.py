@@ -320,16 +320,21 @@ def main():
   for i in range(args.warmup):
     one_step(i)
   torch.cuda.synchronize()
+  graph_error = None
   if args.graph:
-    # capture after warmup (benchmark.py:123-155 captures fn(m, d) once and replays it every step)
-    graphs = []
-    for dk in shards:
-      cs = torch.cuda.Stream(device=dev)
-      cs.wait_stream(torch.cuda.current_stream(dev))
-      g = torch.cuda.CUDAGraph()
-      with torch.cuda.graph(g, stream=cs):
-        mjw.step(m, dk)
-      graphs.append(g)
+    # capture after warmup (benchmark.py:123-155 captures fn(m, d) once and replays it every step);
+    # should the capture fail, the steps run eagerly and the record says why
+    try:
+      graphs = []
+      for dk in shards:
+        cs = torch.cuda.Stream(device=dev)
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cs):
+          mjw.step(m, dk)
+        graphs.append(g)
+    except RuntimeError as e:
+      graphs, graph_error = None, str(e)[:200]
     # capture does not execute: the state is unchanged, the replays below advance it
     torch.cuda.synchronize()
 
@@ -418,7 +423,8 @@ def main():
         "njmax": args.njmax,
         "solver": solver_name,
         "parallelism": parallelism,
-        "graph": bool(args.graph),
+        "graph": graphs is not None,
+        **({"graph_error": graph_error} if graph_error else {}),
         "timed_kernel_launches": len(events),
         "converged_worlds": converged,
         "nefc_mean": nefc_mean,
