@@ -5,8 +5,11 @@
 
 namespace mjw {
 
+// 3 waves/SIMD (up to 168 VGPRs, 12 worlds/CU): at 4 (128 VGPRs, 16 worlds/CU, which the 9.7 KB of
+// LDS would also allow) the Euler+CG instance spilled 6-11 registers; measured humanoid dense kernel
+// 0.295 -> 0.288 ms at 3, 0.287 ms at 2
 template <int FLAGS, bool NEWTON>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON>()];
   const int wid = w0 + (int)blockIdx.x;
