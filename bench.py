@@ -21,14 +21,17 @@ transmission, velocity, rne, actuation, qfrc_smooth) and the dense kernel
 mjw::dense_kernel<7,false> (Cholesky + M^-1, CG solve, Euler).  As in the
 reference's benchmark (benchmark.py:123-155) the step is captured once as a
 hipGraph and replayed every step, the control noise launched before each replay;
-every 10th timed step instead runs eagerly with HIP events recorded on that stream
-around each kernel (mjw_step_events), which gives the per-kernel durations.
+every 10th timed step instead runs eagerly through mjw_step_trace, which records a
+HIP event on that stream after every kernel launch and so times each kernel.
 
-Also reported: `roofline` for the dominant (forward) kernel: its algorithmic
-bytes per env-step (SURVEY.md 8(d)'s B_alg split by kernel) x nworld
-over its HIP-event duration vs 8 TB/s HBM peak, traffic from the committed
-rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, KB -> B); and `cpu_baseline`
-(the fp64 C oracle, OpenMP over worlds on the host cores, bounded sample, rank 0).
+Also reported: `roofline` for the dominant kernel group -- the one with the most
+time per step (the dense kernel on the humanoid, the CG solve on the sparse path):
+its algorithmic bytes per env-step (SURVEY.md 8(d)'s B_alg split by the kernel that
+writes each output) x worlds per launch over its HIP-event time vs
+the 8 TB/s HBM peak, and its traffic from the committed rocprofv3 PMC passes
+((2 FETCH_SIZE + WRITE_SIZE) KB -> B, summed per step over the group's launches);
+every group's figures side by side in `roofline.kernels`; and `cpu_baseline` (the
+fp64 C oracle, OpenMP over worlds on the host cores, bounded sample, rank 0).
 """
 
 import argparse
@@ -101,9 +104,37 @@ def b_alg_parts(words, nefc_mean, ncon_mean, nv_pad):
   return fwd, dense
 
 
+def b_alg_groups(mjm, words, nefc_mean, ncon_mean, row_words, sparse):
+  """Algorithmic bytes per env-step by kernel group (the kernels that write those outputs).  Dense path:
+  forward (mjw_kernel, the convex pre-pass) and dense (factor / solve / Euler, the sensor kernel).  Sparse
+  path: forward (the four stage kernels + the mesh pre-pass; they also write qLD and qacc_smooth), solve
+  (transposed index + CG: qacc, qfrc_constraint, efc_Ma, solver scalars, efc force / state) and euler."""
+  fwd, dense = b_alg_parts(words, nefc_mean, ncon_mean, row_words)
+  if not sparse:
+    return {"forward": fwd, "dense": dense}
+  solve = 4.0 * (3 * mjm.nv + 5 + 2.0 * nefc_mean)
+  euler = 4.0 * (mjm.nq + 2 * mjm.nv + 1)
+  return {"forward": fwd + dense - solve - euler, "solve": solve, "euler": euler}
+
+
+def kernel_group(name, sparse):
+  """Kernel group of a traced launch (see b_alg_groups); 'other' = the pool-counter reset."""
+  if "reset_counters" in name or "ctrl_noise" in name:
+    return "other"
+  if sparse:
+    if "solve_kernel" in name:
+      return "solve"
+    if "euler_kernel" in name:
+      return "euler"
+    return "forward"
+  if "dense_kernel" in name or "sensor_acc" in name:
+    return "dense"
+  return "forward"
+
+
 def parse():
   p = argparse.ArgumentParser()
-  p.add_argument("--gpus", type=int, default=1)
+  p.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default: WORLD_SIZE when launched by torchrun, else 1")
   p.add_argument("--steps", type=int, default=None, help="timed steps (default: the config's, 1000 unless stated)")
   p.add_argument("--warmup", type=int, default=20)
   p.add_argument("--model", default="humanoid", choices=sorted(MODELS), help="benchmark config (default: the headline C2)")
@@ -118,8 +149,8 @@ def parse():
   p.add_argument("--graph", type=int, default=1, help="capture mjw.step once as a hipGraph and replay it every step "
                  "(benchmark.py:123-155: ctrl noise is launched outside the graph); 0 = launch the step eagerly")
   p.add_argument("--event-every", type=int, default=10,
-                 help="every E-th timed step runs eagerly with HIP events around its kernels (the per-kernel "
-                 "durations of `roofline`); the others replay the graph (events on every step cost ~6%%)")
+                 help="every E-th timed step runs eagerly with a HIP event after each kernel launch (mjw_step_trace: "
+                 "the per-kernel durations of `roofline`); the others replay the graph (events on every step cost ~6%%)")
   p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                  help="weak: --nworld worlds per rank; strong: --nworld worlds in total, split over the ranks")
   p.add_argument("--streams", type=int, default=1,
@@ -127,6 +158,8 @@ def parse():
                  "than one batch on the humanoid: 12.2 vs 13.9 M env-steps/s)")
   p.add_argument("--dump-qpos", default=None, help="directory: each rank writes its final qpos + world offset (tests)")
   a = p.parse_args()
+  if a.gpus is None:  # torchrun without --gpus: one rank per process of the launch
+    a.gpus = int(os.environ.get("WORLD_SIZE", "1"))
   cfg = MODELS[a.model]
   for k in ("nworld", "nconmax", "njmax", "solver"):
     if getattr(a, k) is None:
@@ -203,13 +236,14 @@ def cpu_baseline(mjm, nworld, nsteps, key, njmax, nconmax, model):
   )
 
 
-def pmc_traffic(path, model, nworld, solver_name, sparse):
-  """HBM bytes per launch from a committed rocprofv3 PMC summary, only when that summary was taken on the
-  same workload (`nworld` = worlds per launch) AND on a kernel build from the current sources (its
-  `csrc_sha` equals build.sources_hash())."""
+def pmc_traffic(path, model, nworld, solver_name):
+  """Per-kernel HBM bytes from a committed rocprofv3 PMC summary (tools/pmc_traffic.py): {kernel name:
+  {bytes_per_launch, bytes_per_step, launches_per_step}}, only when that summary was taken on the same
+  workload (`nworld` = worlds per launch) AND on a kernel build from the current sources (its `csrc_sha`
+  equals build.sources_hash()); else (None, reason)."""
   from mujoco_warp_amd import build as _build
 
-  if not os.path.exists(path):
+  if not path or not os.path.exists(path):
     return None, "no PMC summary"
   with open(path) as f:
     pmc = json.load(f)
@@ -217,10 +251,76 @@ def pmc_traffic(path, model, nworld, solver_name, sparse):
     return None, f"PMC summary {os.path.basename(path)} is for another workload"
   if pmc.get("csrc_sha") != _build.sources_hash():
     return None, f"PMC summary {os.path.basename(path)} predates the current kernel sources"
-  fk = pmc.get("kernels", {}).get("forward", {})
-  # sparse path: the timed region is forward (x2 around the convex pre-pass) + solve
-  key = "hbm_bytes_per_step_forward_plus_solve" if sparse else "hbm_bytes_per_launch"
-  return fk.get(key), os.path.basename(path)
+  out = {}
+  for k, v in pmc.get("kernels", {}).items():
+    if v.get("hbm_bytes_per_launch") is None:
+      continue
+    out[k] = {"bytes_per_launch": v["hbm_bytes_per_launch"], "bytes_per_step": v.get("hbm_bytes_per_step"),
+              "launches_per_step": v.get("launches_per_step")}
+  return out, os.path.basename(path)
+
+
+def kernel_table(durations, sparse):
+  """Per kernel: mean time and launches per step over the traced steps (mjw_step_trace durations)."""
+  tab = {}
+  nstep = max(1, len(durations))
+  for launches in durations:
+    for name, ms in launches:
+      e = tab.setdefault(name, {"ms_per_step": 0.0, "launches_per_step": 0.0, "group": kernel_group(name, sparse)})
+      e["ms_per_step"] += ms / nstep
+      e["launches_per_step"] += 1.0 / nstep
+  return tab
+
+
+def roofline_record(tab, groups_alg, nworld, pmc, pmc_src):
+  """`roofline` of the dominant kernel group (most time per step) and the per-group / per-kernel figures."""
+  groups = {}
+  for name, e in tab.items():
+    g = groups.setdefault(e["group"], {"kernels": [], "ms_per_step": 0.0, "traffic_per_step": 0.0, "traffic_known": True})
+    g["kernels"].append(name)
+    g["ms_per_step"] += e["ms_per_step"]
+    t = (pmc or {}).get(name)
+    e["alg_group"] = e["group"]
+    if t is not None:
+      e["traffic_per_launch"] = t["bytes_per_launch"]
+      e["traffic_per_step"] = t["bytes_per_launch"] * e["launches_per_step"]
+      g["traffic_per_step"] += e["traffic_per_step"]
+    else:
+      e["traffic_per_launch"] = None
+      g["traffic_known"] = False
+  rec = {}
+  for gname, g in groups.items():
+    alg = groups_alg.get(gname)
+    ach = alg * nworld / (g["ms_per_step"] * 1e-3) / 1e9 if alg and g["ms_per_step"] > 0 else None
+    rec[gname] = {
+      "kernels": sorted(g["kernels"]), "ms_per_step": g["ms_per_step"],
+      "alg_bytes_per_env_step": alg, "alg_bytes_per_step": alg * nworld if alg else None,
+      "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS if ach else None,
+      "traffic_per_step": g["traffic_per_step"] if g["traffic_known"] else None,
+      "traffic_over_alg": (g["traffic_per_step"] / (alg * nworld)) if g["traffic_known"] and alg else None,
+    }
+  cand = {k: v for k, v in rec.items() if v["alg_bytes_per_env_step"]}
+  dom = max(cand, key=lambda k: cand[k]["ms_per_step"])
+  d = rec[dom]
+  return {
+    "bound": "hbm",
+    "achieved": d["achieved_GBs"],
+    "peak": HBM_PEAK_GBS,
+    "unit": "GB/s",
+    "frac": d["frac"],
+    "traffic": d["traffic_per_step"],
+    "traffic_source": pmc_src,
+    "traffic_note": "HBM bytes per step of the group's launches ((2 FETCH_SIZE + WRITE_SIZE) KB, rocprofv3 PMC); "
+                    "= per launch when the group is one kernel launched once per step",
+    "kernel": " + ".join(d["kernels"]),
+    "group": dom,
+    "kernel_ms": d["ms_per_step"],
+    "worlds_per_launch": nworld,
+    "alg_bytes_per_env_step": d["alg_bytes_per_env_step"],
+    "groups": rec,
+    "kernels": tab,
+    "step_alg_bytes_per_env_step": sum(v for v in (x["alg_bytes_per_env_step"] for x in rec.values()) if v),
+  }
 
 
 def _free_port():
@@ -302,16 +402,17 @@ def main():
   # default stream, which would synchronise with the others)
   streams = [torch.cuda.current_stream(dev)] if nshard == 1 else [torch.cuda.Stream(device=dev) for _ in range(nshard)]
 
-  from mujoco_warp_amd.forward import step_timed
+  from mujoco_warp_amd.forward import StepTracer
 
   graphs = None
+  tracer = StepTracer()
 
-  def one_step(i, ev=None):
+  def one_step(i, traced=False):
     for k, (dk, st) in enumerate(zip(shards, streams)):
       with torch.cuda.stream(st):
         mjw.ctrl_noise(m, dk, i, center=center)
-        if ev is not None and k == 0:
-          step_timed(m, dk, *ev)  # shard 0's kernels are the timed launches
+        if traced and k == 0:
+          tracer.step(m, dk)  # shard 0's kernels are the timed launches
         elif graphs is not None:
           graphs[k].replay()
         else:
@@ -346,31 +447,28 @@ def main():
   # sizes for the algorithmic-bytes figure (untimed)
   nefc_mean, ncon_mean = sizes()
 
-  # per-kernel HIP events on every `event_every`-th timed step (every step without a graph)
+  # a launch trace (one HIP event after every kernel) on every `event_every`-th timed step (every step
+  # without a graph)
   every = 1 if graphs is None else max(1, args.event_every)
-  events = {i: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for i in range(0, args.steps, every)}
-  for ev in events.values():  # torch creates the HIP event on first record; mjw_step_events re-records it
-    for e in ev:
-      e.record()
+  traced = set(range(0, args.steps, every))
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   for i in range(args.steps):
-    one_step(args.warmup + i, events.get(i))
+    one_step(args.warmup + i, i in traced)
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   elapsed = time.perf_counter() - t0
-  fwd_ms = float(np.mean([a.elapsed_time(b) for a, b, c in events.values()]))
-  dense_ms = float(np.mean([b.elapsed_time(c) for a, b, c in events.values()]))
-  kernel_ms = fwd_ms
+  tab = kernel_table(tracer.durations(), bool(m.is_sparse))
   n2, c2 = sizes()
   nefc_mean, ncon_mean = 0.5 * (nefc_mean + n2), 0.5 * (ncon_mean + c2)
   qpos_all = torch.cat([dk.qpos for dk in shards])
   converged = int((~torch.isnan(qpos_all).any(dim=1)).sum())
   solver_niter_mean = float(torch.cat([dk.solver_niter for dk in shards]).float().mean())
+  solver_niter_max = int(torch.cat([dk.solver_niter for dk in shards]).max())
   if args.dump_qpos:
     os.makedirs(args.dump_qpos, exist_ok=True)
     np.savez(os.path.join(args.dump_qpos, f"qpos_rank{rank}.npz"), qpos=qpos_all.cpu().numpy(), offset=offset)
@@ -378,9 +476,12 @@ def main():
 
   total_worlds = nworld
   if world > 1:
-    t = torch.tensor([elapsed, kernel_ms, dense_ms], dtype=torch.float64)
+    names = sorted(tab)
+    t = torch.tensor([elapsed] + [tab[k]["ms_per_step"] for k in names], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms, dense_ms = (float(x) for x in t)
+    elapsed = float(t[0])
+    for k, v in zip(names, t[1:]):
+      tab[k]["ms_per_step"] = float(v)
     c = torch.tensor([converged, nworld], dtype=torch.int64)
     dist.all_reduce(c)
     converged, total_worlds = int(c[0]), int(c[1])
@@ -389,12 +490,11 @@ def main():
   if rank == 0:
     words = step_words(mjm, m.nv_pad, bool(m.is_sparse))
     # a sparse efc row carries njrow values + njrow column indices instead of an nv_pad dense row
-    fwd_b, dense_b = b_alg_parts(words, nefc_mean, ncon_mean, 2 * m.njrow if m.is_sparse else m.nv_pad)
-    # worlds per timed forward launch: shard 0's
+    groups_alg = b_alg_groups(mjm, words, nefc_mean, ncon_mean, 2 * m.njrow if m.is_sparse else m.nv_pad, bool(m.is_sparse))
+    # worlds per timed launch: shard 0's
     nlaunch = d.nworld
-    bytes_per_launch = fwd_b * nlaunch
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.pmc, args.model, nlaunch, solver_name, bool(m.is_sparse))
+    pmc, pmc_src = pmc_traffic(args.pmc, args.model, nlaunch, solver_name)
+    roof = roofline_record(tab, groups_alg, nlaunch, pmc, pmc_src)
     if args.scaling == "weak":
       parallelism = f"{args.nworld} worlds per rank on {world} GPU(s) (weak), no collective"
     else:
@@ -425,37 +525,15 @@ def main():
         "parallelism": parallelism,
         "graph": graphs is not None,
         **({"graph_error": graph_error} if graph_error else {}),
-        "timed_kernel_launches": len(events),
+        "timed_kernel_launches": len(traced),
         "converged_worlds": converged,
         "nefc_mean": nefc_mean,
         "ncon_mean": ncon_mean,
         "solver_niter_mean": solver_niter_mean,
+        "solver_niter_max": solver_niter_max,
         "streams": nshard,
       },
-      "roofline": {
-        "bound": "hbm",
-        "achieved": achieved,
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS,
-        "traffic": traffic,
-        "traffic_source": traffic_src,
-        "kernel": ("mjw::sp::forward_kernel + mjw::sp::solve_kernel (sparse path: forward + CG)" if m.is_sparse else
-                   f"mjw::mjw_kernel<79, {'false' if m.nxn_box == 0 else 'true'}> (forward: position/velocity/actuation/qfrc_smooth)"
-                   + (" + mjw::ccd_kernel (convex pre-pass)" if m.nxn_ccd else "")),
-        "kernel_ms": kernel_ms,
-        "worlds_per_launch": nlaunch,
-        "alg_bytes_per_env_step": fwd_b,
-        "other_kernels": {
-          ("mjw::sp::euler_kernel" if m.is_sparse else
-           "mjw::dense_kernel (factor/solve/Euler)" + (" + mjw::sensor_acc_kernel" if m.nsensor else "")): {
-            "ms": dense_ms,
-            "alg_bytes_per_env_step": dense_b,
-            "achieved_GBs": dense_b * nlaunch / (dense_ms * 1e-3) / 1e9,
-          }
-        },
-        "step_alg_bytes_per_env_step": fwd_b + dense_b,
-      },
+      "roofline": roof,
       "cpu_baseline": None,
     }
     if world == 1 and args.cpu_baseline:

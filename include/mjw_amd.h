@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 11
+#define MJW_ABI_VERSION 12
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -198,6 +198,15 @@ int mjw_step(const mjw_model_t* m, const mjw_data_t* d, void* stream);
  * this to time the dominant kernel live; on the generic path only ev_begin/ev_end bracket it).
  * No reference counterpart (the reference times with wp.ScopedTimer/event_trace, benchmark.py). */
 int mjw_step_events(const mjw_model_t* m, const mjw_data_t* d, void* stream, void* ev_begin, void* ev_mid, void* ev_end);
+
+/* mjw_step with a launch trace: events[0] is recorded on `stream` before the step and events[i + 1]
+ * right after the step's i-th kernel launch (i < nevents - 1), kernel_ids[i] names that kernel
+ * (mjw_kernel_name); *nlaunch = launches traced.  The events must exist (hipEventCreate).  bench.py
+ * times every kernel of the step with it on the stream they run on.  No reference counterpart (the
+ * reference's event_trace, benchmark.py, times its Warp kernels the same way). */
+int mjw_step_trace(const mjw_model_t* m, const mjw_data_t* d, void* stream, void** events, int nevents, int* kernel_ids,
+                   int* nlaunch);
+const char* mjw_kernel_name(int kernel_id);
 
 int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream);

@@ -124,13 +124,58 @@ static __device__ unsigned long long g_prof[PH_N];
     }                                                                                           \
     return (int)e;                                                                              \
   }
+// per-wave lifetime log (tools/wave_log.py): 4 x u64 per world, {start, end} s_memrealtime (100 MHz,
+// one clock for the whole chip), HW_ID | XCC_ID << 32, solver iterations; set with the TU's setter
+static __device__ unsigned long long* g_wlog = nullptr;
+#define WLOG_T0() const unsigned long long _wt0 = __builtin_amdgcn_s_memrealtime()
+#define WLOG_END(wid, niter)                                                                         \
+  do {                                                                                               \
+    if (g_wlog && (threadIdx.x & 63) == 0) {                                                         \
+      unsigned long long* r = g_wlog + 4 * (long)(wid);                                              \
+      r[0] = _wt0;                                                                                   \
+      r[1] = __builtin_amdgcn_s_memrealtime();                                                       \
+      r[2] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |                         \
+             ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);                 \
+      r[3] = (unsigned long long)(niter);                                                            \
+    }                                                                                                \
+  } while (0)
+#define MJW_WLOG_SETTER(fname)                                                                       \
+  extern "C" int fname(unsigned long long* buf) {                                                    \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(mjw::g_wlog), &buf, sizeof(buf));                         \
+  }
 #else
+#define WLOG_T0() (void)0
+#define WLOG_END(wid, niter) (void)0
+#define MJW_WLOG_SETTER(fname)
 #define MJW_PROF_READER(fname)
 #define PROF_T0() (void)0
 #define PROF_MARK(ph) (void)0
 #define PROF_T0_SUB() (void)0
 #define PROF_MARK_SUB(ph) (void)0
 #endif
+
+// ---- launch trace (mjw_step_trace): one HIP event recorded after every kernel launch of a step,
+// tagged with a kernel id (mjw_kernel_name gives its name), so that a host can time each kernel
+// of the step on the stream the kernels run on
+enum : int {
+  K_RESET = 0, K_CTRL_NOISE, K_CCD, K_SENSOR, K_RK4,
+  K_SP_POS, K_SP_CCD, K_SP_COLL, K_SP_CON, K_SP_VEL, K_SP_INDEX, K_SP_SOLVE, K_SP_SOLVE_LDS, K_SP_EULER,
+  K_DENSE = 32,  // + 2 * FLAGS + NEWTON  (dense_kernel<FLAGS, NEWTON>)
+  K_FWD = 256,   // + 2 * STAGES + box    (mjw_kernel<STAGES, box>)
+  K_END = 512
+};
+struct LaunchTrace {
+  hipEvent_t* ev;  // ev[0] recorded by the caller before the step; ev[i + 1] after launch i
+  int* ids;        // ids[i]: kernel id of launch i
+  int cap, n;
+};
+extern thread_local LaunchTrace* g_trace;
+__host__ inline void trace_launch(hipStream_t s, int id) {
+  LaunchTrace* t = g_trace;
+  if (!t || t->n >= t->cap) return;
+  (void)hipEventRecord(t->ev[t->n + 1], s);
+  t->ids[t->n++] = id;
+}
 
 // dense (register-resident) factor / solve / euler kernel launcher, mjw_dense.hip
 enum : int { DF_FACTOR = 1, DF_SOLVE = 2, DF_EULER = 4 };

@@ -14,7 +14,9 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON>()];
   const int wid = w0 + (int)blockIdx.x;
   if (wid >= d.nworld) return;
+  WLOG_T0();
   dense_world<FLAGS, NEWTON>(m, d, wid, sm);
+  WLOG_END(wid, (FLAGS & DF_SOLVE) ? d.solver_niter[wid] : 0);
 }
 
 // device self-checks of the primitives above (mjw_selftest): which = 0 -> per-wave dsum and
@@ -41,10 +43,12 @@ __global__ void __launch_bounds__(64) selftest_kernel(int which, const float* in
 
 template <int FLAGS>
 hipError_t launch_flags(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int w0, int count) {
-  if (m->opt_solver == SOLVER_NEWTON)
+  const bool newton = m->opt_solver == SOLVER_NEWTON;
+  if (newton)
     hipLaunchKernelGGL((dense_kernel<FLAGS, true>), dim3(count), dim3(64), 0, s, *m, *d, w0);
   else
     hipLaunchKernelGGL((dense_kernel<FLAGS, false>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+  trace_launch(s, K_DENSE + 2 * FLAGS + (newton ? 1 : 0));
   return hipGetLastError();
 }
 
@@ -72,6 +76,7 @@ int dense_launch(int flags, const mjw_model_t* m, const mjw_data_t* d, hipStream
 }  // namespace mjw
 
 MJW_PROF_READER(mjw_prof_read_dense)
+MJW_WLOG_SETTER(mjw_prof_wlog_dense)
 
 extern "C" int mjw_selftest(int which, const float* in, float* out, int n, void* stream) {
   if (n <= 0) return 0;

@@ -98,6 +98,7 @@ __global__ void __launch_bounds__(64) rk4_kernel(const mjw_model_t m, const mjw_
 int rk4_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int op, float scale) {
   if (d->nworld <= 0) return 0;
   hipLaunchKernelGGL(rk4_kernel, dim3(d->nworld), dim3(64), 0, s, *m, *d, op, scale);
+  trace_launch(s, K_RK4);
   return (int)hipGetLastError();
 }
 

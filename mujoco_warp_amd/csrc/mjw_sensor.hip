@@ -289,6 +289,7 @@ int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int 
   size_t lds = (size_t)L.total * 4;
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(sensor_acc_kernel, dim3(count), dim3(64), lds, s, *m, *d, L, stages, w0);
+  trace_launch(s, K_SENSOR);
   return (int)hipGetLastError();
 }
 

@@ -1778,6 +1778,8 @@ __device__ void fwd_acceleration(const mjw_model_t& m, const mjw_data_t& d, int 
 // all stages (248 VGPRs, 3.4 KB scratch per lane, 2 waves / SIMD).  POS_A: frames to qM; COLL:
 // collision; CON: constraint rows + transmission; the convex pre-pass runs between POS_A and COLL.
 enum : int { SP_POS_A = 1 << 8, SP_POS_B = 1 << 9, SP_COLL = 1 << 10, SP_CON = 1 << 11 };
+// mjw_kernel_name (mjw_step.hip) spells these launches with the numeric template arguments
+static_assert(SP_POS_A == 256 && SP_COLL == 1024 && SP_CON == 2048 && ST_VEL == 2, "kernel names");
 
 template <int S>
 __global__ void __launch_bounds__(BLK, 4) forward_kernel(const mjw_model_t m, const mjw_data_t d, int stages) {
@@ -2430,21 +2432,28 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
   if (fwd & ST_POS) {
     // frames, [the convex pre-pass,] collision, constraint rows
     hipLaunchKernelGGL(sp::forward_kernel<sp::SP_POS_A>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
+    trace_launch(s, K_SP_POS);
     if (ccd) {
       const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations).total + 64) * 4;
       hipLaunchKernelGGL(sp::ccd_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
+      trace_launch(s, K_SP_CCD);
     }
     // collision items (upper bound of ncollide_items): one LDS byte each when they fit
     const long nitem = (long)m->nxn + (long)m->nflexvert * m->nplane + (long)m->nflexelem * m->nflexcg;
     const size_t lds = nitem <= sp::SP_LDS_ITEMS_MAX ? (size_t)((nitem + 3) & ~3L) : 0;
     hipLaunchKernelGGL(sp::forward_kernel<sp::SP_COLL>, dim3(nw), dim3(sp::BLK), lds, s, *m, *d, fwd);
+    trace_launch(s, K_SP_COLL);
     hipLaunchKernelGGL(sp::forward_kernel<sp::SP_CON>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
+    trace_launch(s, K_SP_CON);
   }
-  if (fwd & (ST_VEL | ST_ACT | ST_ACC))
+  if (fwd & (ST_VEL | ST_ACT | ST_ACC)) {
     hipLaunchKernelGGL(sp::forward_kernel<ST_VEL>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
+    trace_launch(s, K_SP_VEL);
+  }
   if (stages & ST_SOLVE) {
     const size_t lds = (m->nv + 1) <= sp::SP_LDS_CNT_MAX ? (size_t)(m->nv + 1) * 4 : 0;
     hipLaunchKernelGGL(sp::solve_kernel<0>, dim3(nw), dim3(sp::BLK), lds, s, *m, *d);
+    trace_launch(s, K_SP_INDEX);
     // CG iterations, the search direction in LDS.  MJW_SP_SOLVE_LDS=1 also keeps Jaref / jv of every
     // row in LDS (1024-thread worlds, when 2 * njmax floats fit): measured equal on aloha_cloth
     // (22.75 vs 22.80 ms per step) and 4 % slower on cloth, so the rows stay in HBM by default
@@ -2460,11 +2469,16 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
         (void)hipFuncSetAttribute((const void*)sp::solve_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
       });
       hipLaunchKernelGGL(sp::solve_kernel<2>, dim3(nw), dim3(sp::SOLVE_LDS_THREADS), row_lds, s, *m, *d);
+      trace_launch(s, K_SP_SOLVE_LDS);
     } else {
       hipLaunchKernelGGL(sp::solve_kernel<1>, dim3(nw), dim3(sp::BLK), search_lds, s, *m, *d);
+      trace_launch(s, K_SP_SOLVE);
     }
   }
-  if (stages & ST_EULER) hipLaunchKernelGGL(sp::euler_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
+  if (stages & ST_EULER) {
+    hipLaunchKernelGGL(sp::euler_kernel, dim3(nw), dim3(sp::BLK), 0, s, *m, *d);
+    trace_launch(s, K_SP_EULER);
+  }
   return (int)hipGetLastError();
 }
 

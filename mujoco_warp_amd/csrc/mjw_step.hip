@@ -2131,7 +2131,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mj
   w.wid = w0 + (int)blockIdx.x;
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
+  WLOG_T0();
   run_stages<STAGES, BOX>(m, d, L, w);
+  WLOG_END(w.wid, 0);
 }
 
 // -------------------------------------------------------------------------------------------
@@ -2207,6 +2209,10 @@ __global__ void ctrl_noise_kernel(const mjw_model_t m, const mjw_data_t d, const
 // =============================================================================================
 // C ABI
 // =============================================================================================
+namespace mjw {
+thread_local LaunchTrace* g_trace = nullptr;
+}
+
 namespace {
 thread_local std::string g_err;
 
@@ -2218,6 +2224,7 @@ int set_err(hipError_t e, const char* where) {
 
 hipError_t reset_counters(const mjw_data_t* d, hipStream_t s) {
   hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision);
+  mjw::trace_launch(s, mjw::K_RESET);
   return hipGetLastError();
 }
 
@@ -2244,6 +2251,7 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
       });
       const mjw::Lay LC = mjw::make_layout(*m, d->njmax, nofactor, true);
       hipLaunchKernelGGL(mjw::ccd_kernel, dim3(count), dim3(64), (size_t)LC.total * 4, s, *m, *d, LC, w0);
+      mjw::trace_launch(s, mjw::K_CCD);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return set_err(e, name);
     }
@@ -2258,10 +2266,12 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   if constexpr ((STAGES & mjw::ST_POS) != 0) {
     if (m->nxn_box == 0) {
       hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
+      mjw::trace_launch(s, mjw::K_FWD + 2 * STAGES);
       return set_err(hipGetLastError(), name);
     }
   }
   hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, true>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
+  mjw::trace_launch(s, mjw::K_FWD + 2 * STAGES + 1);
   return set_err(hipGetLastError(), name);
 }
 
@@ -2281,8 +2291,7 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     // workgroup-per-world sparse / flex pipeline (mjw_sparse.hip); no sensors on this path
     hipStream_t s = (hipStream_t)stream;
     if (stages & ST_POS) {
-      hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision);
-      hipError_t e = hipGetLastError();
+      hipError_t e = reset_counters(d, s);
       if (e != hipSuccess) return set_err(e, name);
     }
     if (g_ev[0]) (void)hipEventRecord(g_ev[0], s);
@@ -2385,6 +2394,7 @@ int step(const mjw_model_t* m, const mjw_data_t* d, void* stream, const char* na
 }  // namespace
 
 MJW_PROF_READER(mjw_prof_read)
+MJW_WLOG_SETTER(mjw_prof_wlog_fwd)
 
 extern "C" {
 
@@ -2416,6 +2426,36 @@ int mjw_step_events(const mjw_model_t* m, const mjw_data_t* d, void* stream, voi
   g_ev[0] = g_ev[1] = g_ev[2] = nullptr;
   return rc;
 }
+int mjw_step_trace(const mjw_model_t* m, const mjw_data_t* d, void* stream, void** events, int nevents, int* kernel_ids,
+                   int* nlaunch) {
+  if (!events || nevents < 1 || !kernel_ids || !nlaunch) { g_err = "mjw_step_trace: need events[>=1], kernel_ids, nlaunch"; return -1; }
+  mjw::LaunchTrace t{(hipEvent_t*)events, kernel_ids, nevents - 1, 0};
+  (void)hipEventRecord((hipEvent_t)events[0], (hipStream_t)stream);
+  mjw::g_trace = &t;
+  int rc = step(m, d, stream, "mjw_step_trace");
+  mjw::g_trace = nullptr;
+  *nlaunch = t.n;
+  return rc;
+}
+// names as rocprofv3 demangles them (numeric template arguments: SP_POS_A = 256, SP_COLL = 1024,
+// SP_CON = 2048, ST_VEL = 2), so that traced launches and PMC summaries key on the same string
+const char* mjw_kernel_name(int id) {
+  static const char* misc[] = {"mjw::reset_counters_kernel", "mjw::ctrl_noise_kernel", "mjw::ccd_kernel", "mjw::sensor_acc_kernel",
+                               "mjw::rk4_kernel", "mjw::sp::forward_kernel<256>", "mjw::sp::ccd_kernel",
+                               "mjw::sp::forward_kernel<1024>", "mjw::sp::forward_kernel<2048>", "mjw::sp::forward_kernel<2>",
+                               "mjw::sp::solve_kernel<0>", "mjw::sp::solve_kernel<1>", "mjw::sp::solve_kernel<2>", "mjw::sp::euler_kernel"};
+  static thread_local char buf[64];
+  if (id >= 0 && id < (int)(sizeof(misc) / sizeof(misc[0]))) return misc[id];
+  if (id >= mjw::K_DENSE && id < mjw::K_DENSE + 16) {
+    snprintf(buf, sizeof(buf), "mjw::dense_kernel<%d, %s>", (id - mjw::K_DENSE) >> 1, (id & 1) ? "true" : "false");
+    return buf;
+  }
+  if (id >= mjw::K_FWD && id < mjw::K_END) {
+    snprintf(buf, sizeof(buf), "mjw::mjw_kernel<%d, %s>", (id - mjw::K_FWD) >> 1, (id & 1) ? "true" : "false");
+    return buf;
+  }
+  return "unknown";
+}
 int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE, "mjw_forward");
 }
@@ -2442,6 +2482,7 @@ int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* cente
   int n = d->nworld * m->nu;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(mjw::ctrl_noise_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, *m, *d, center, step, std, rate);
+  mjw::trace_launch((hipStream_t)stream, mjw::K_CTRL_NOISE);
   return set_err(hipGetLastError(), "mjw_ctrl_noise");
 }
 

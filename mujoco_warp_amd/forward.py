@@ -44,6 +44,37 @@ def step_timed(m: Model, d: Data, ev_begin, ev_mid, ev_end):
   _lib.check(rc, "mjw_step_events")
 
 
+class StepTracer:
+  """Times every kernel launch of `step` with HIP events on the stream the kernels run on
+  (mjw_step_trace).  `step(m, d)` runs one traced step; `durations()` then gives, per traced step, the
+  list of (kernel name, ms) in launch order (call after the work has finished)."""
+
+  def __init__(self, max_launch: int = 32):
+    import ctypes
+
+    self._ct = ctypes
+    self.max_launch = max_launch
+    self.records = []  # (events, ids, n) per traced step
+
+  def step(self, m: Model, d: Data):
+    ct = self._ct
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(self.max_launch + 1)]
+    for e in evs:  # torch creates the HIP event on its first record
+      e.record()
+    arr = (ct.c_void_p * len(evs))(*[e.cuda_event for e in evs])
+    ids = (ct.c_int * self.max_launch)()
+    n = ct.c_int(0)
+    _lib.check(_lib.lib().mjw_step_trace(cmodel(m), cdata(d), _stream(d), arr, len(evs), ids, ct.byref(n)), "mjw_step_trace")
+    self.records.append((evs, [ids[i] for i in range(n.value)], n.value))
+
+  def durations(self):
+    L = _lib.lib()
+    out = []
+    for evs, ids, n in self.records:
+      out.append([(L.mjw_kernel_name(ids[i]).decode(), evs[i].elapsed_time(evs[i + 1])) for i in range(n)])
+    return out
+
+
 # callbacks whose reference call sites fall inside one fused launch of this path: act_dyn / act_gain /
 # act_bias run between _actuator_force and the moment map (forward.py:876-881), contactfilter between
 # the narrowphase and make_constraint (collision_driver.py:788); they are refused instead of being run

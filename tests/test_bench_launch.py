@@ -87,13 +87,13 @@ def test_pmc_traffic_is_bound_to_the_kernel_sources(tmp_path):
   from mujoco_warp_amd import build
 
   pmc = {"nworld": 8192, "solver": "CG", "model": "humanoid", "csrc_sha": build.sources_hash(),
-         "kernels": {"forward": {"hbm_bytes_per_launch": 123.0}}}
+         "kernels": {"mjw::dense_kernel<7, false>": {"hbm_bytes_per_launch": 123.0, "hbm_bytes_per_step": 123.0, "launches_per_step": 1.0}}}
   f = tmp_path / "pmc_humanoid_r99.json"
   f.write_text(json.dumps(pmc))
-  assert bench.pmc_traffic(str(f), "humanoid", 8192, "CG", False)[0] == 123.0
-  assert bench.pmc_traffic(str(f), "humanoid", 4096, "CG", False)[0] is None  # other workload
+  assert bench.pmc_traffic(str(f), "humanoid", 8192, "CG")[0]["mjw::dense_kernel<7, false>"]["bytes_per_launch"] == 123.0
+  assert bench.pmc_traffic(str(f), "humanoid", 4096, "CG")[0] is None  # other workload
   pmc["csrc_sha"] = "0" * 16
   f.write_text(json.dumps(pmc))
-  traffic, why = bench.pmc_traffic(str(f), "humanoid", 8192, "CG", False)
+  traffic, why = bench.pmc_traffic(str(f), "humanoid", 8192, "CG")
   assert traffic is None and "predates" in why
-  assert bench.pmc_traffic(str(tmp_path / "missing.json"), "humanoid", 8192, "CG", False)[0] is None
+  assert bench.pmc_traffic(str(tmp_path / "missing.json"), "humanoid", 8192, "CG")[0] is None

@@ -1,22 +1,44 @@
-"""Summarise rocprofv3 CSV output into profiles/: kernel-trace stats + per-kernel HBM traffic.
+"""Summarise rocprofv3 CSV output into profiles/: per-kernel HBM traffic and time, per launch and per step.
 
 usage: python tools/pmc_traffic.py <stats_dir> <fetch_dir> <write_dir> <out.json> [worlds per launch] [solver] [model]
-  model     : humanoid (default: the dense path's kernels) or a sparse-path model (cloth, aloha_cloth)
   stats_dir : rocprofv3 --kernel-trace --stats --output-format csv output directory
   fetch_dir : rocprofv3 --pmc FETCH_SIZE --output-format csv output directory
   write_dir : rocprofv3 --pmc WRITE_SIZE --output-format csv output directory
-Traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes (MI355X_MICROARCH.md HBM section:
-FETCH_SIZE counts half the bytes of wide streaming reads on gfx950; units are KB), averaged over
-the dispatches of each kernel.
+
+Traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes (MI355X_MICROARCH.md HBM section: units
+are KB; FETCH_SIZE counts half the bytes of wide streaming reads on gfx950), averaged over the dispatches of
+each kernel (keyed by its demangled name without arguments, e.g. `mjw::sp::solve_kernel<1>`; the template
+instances stay separate).
+
+Per step: the number of steps in a PMC run is the dispatch count of `mjw::reset_counters_kernel`, which the
+step launches exactly once; each kernel contributes dispatches / steps launches per step, and the step's
+traffic is the sum over kernels of launches_per_step * bytes_per_launch.  Each kernel keeps its own
+rocprof average duration (`avg_ns`, from the kernel-trace pass of the same command).
 """
+import collections
 import csv
 import glob
 import json
 import os
 import sys
 
-KERNELS = {"forward": "mjw_kernel<79", "dense": "dense_kernel<7, false>"}
-SPARSE_KERNELS = {"forward": "sp::forward_kernel", "solve": "sp::solve_kernel", "ccd": "sp::ccd_kernel", "euler": "sp::euler_kernel"}
+STEP_KERNEL = "mjw::reset_counters_kernel"
+
+
+def kname(full):
+  """'void mjw::dense_kernel<7, false>(mjw_model_t, mjw_data_t, int)' -> 'mjw::dense_kernel<7, false>'."""
+  s = full.strip()
+  if s.startswith("void "):
+    s = s[5:]
+  depth = 0
+  for i, ch in enumerate(s):
+    if ch == "<":
+      depth += 1
+    elif ch == ">":
+      depth -= 1
+    elif ch == "(" and depth == 0:
+      return s[:i]
+  return s
 
 
 def rows(d, pattern):
@@ -27,51 +49,56 @@ def rows(d, pattern):
   return out
 
 
-def counter_avg(d, counter):
-  vals = {k: [] for k in KERNELS}
+def counter(d, name):
+  """{kernel: [values per dispatch]} of one PMC counter."""
+  vals = collections.defaultdict(list)
   for r in rows(d, "*counter_collection.csv"):
-    name = r.get("Kernel_Name", "")
-    if r.get("Counter_Name") != counter:
+    if r.get("Counter_Name") != name:
       continue
-    for k, pat in KERNELS.items():
-      if pat in name.replace("mjw::", ""):
-        vals[k].append(float(r["Counter_Value"]))
-  return {k: (sum(v) / len(v) if v else None, len(v)) for k, v in vals.items()}
+    k = kname(r.get("Kernel_Name", ""))
+    if "mjw" in k:
+      vals[k].append(float(r["Counter_Value"]))
+  return vals
+
+
+def summarise(stats_dir, fetch_dir, write_dir, nworld, solver, model, csrc_sha):
+  fetch = counter(fetch_dir, "FETCH_SIZE")
+  write = counter(write_dir, "WRITE_SIZE")
+  stats = {kname(r["Name"]): r for r in rows(stats_dir, "*kernel_stats.csv")}
+  steps_f = len(fetch.get(STEP_KERNEL, []))
+  steps_w = len(write.get(STEP_KERNEL, []))
+  res = {"nworld": nworld, "solver": solver, "model": model, "csrc_sha": csrc_sha,
+         "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024; per step = "
+                      "sum over kernels of (dispatches / steps) * bytes per launch, steps = dispatches of " + STEP_KERNEL,
+         "steps": [steps_f, steps_w], "kernels": {}}
+  total = 0.0
+  for k in sorted(set(fetch) | set(write)):
+    f, w = fetch.get(k, []), write.get(k, [])
+    fa = sum(f) / len(f) if f else None
+    wa = sum(w) / len(w) if w else None
+    per_launch = (2 * fa + wa) * 1024 if fa is not None and wa is not None else None
+    lps = len(f) / steps_f if steps_f else None
+    st = stats.get(k)
+    ent = {"fetch_size_kb": fa, "write_size_kb": wa, "dispatches": [len(f), len(w)], "hbm_bytes_per_launch": per_launch,
+           "launches_per_step": lps,
+           "hbm_bytes_per_step": per_launch * lps if per_launch is not None and lps is not None else None,
+           "avg_ns": float(st["AverageNs"]) if st else None, "calls_in_stats_pass": int(st["Calls"]) if st else None}
+    res["kernels"][k] = ent
+    if ent["hbm_bytes_per_step"] is not None and k != STEP_KERNEL:
+      total += ent["hbm_bytes_per_step"]
+  res["hbm_bytes_per_step_total"] = total
+  return res
 
 
 def main():
-  global KERNELS
   stats_dir, fetch_dir, write_dir, out = sys.argv[1:5]
   nworld = int(sys.argv[5]) if len(sys.argv) > 5 else 8192
   solver = sys.argv[6] if len(sys.argv) > 6 else "CG"
   model = sys.argv[7] if len(sys.argv) > 7 else "humanoid"
-  if model != "humanoid" and model in ("cloth", "aloha_cloth"):
-    KERNELS = SPARSE_KERNELS
-  fetch = counter_avg(fetch_dir, "FETCH_SIZE")
-  write = counter_avg(write_dir, "WRITE_SIZE")
-  stats = rows(stats_dir, "*kernel_stats.csv")
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
   from mujoco_warp_amd import build as _build
 
-  res = {"nworld": nworld, "solver": solver, "model": model, "csrc_sha": _build.sources_hash(), "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024",
-         "kernels": {}}
-  for k, pat in KERNELS.items():
-    f, nf = fetch[k]
-    w, nw = write[k]
-    st = [r for r in stats if pat in r.get("Name", "").replace("mjw::", "")]
-    res["kernels"][k] = {
-      "pattern": pat,
-      "fetch_size_kb": f, "write_size_kb": w, "dispatches": [nf, nw],
-      "hbm_bytes_per_launch": (2 * f + w) * 1024 if f is not None and w is not None else None,
-      "avg_ns_rocprof": float(st[0]["AverageNs"]) if st else None,
-    }
-  if KERNELS is SPARSE_KERNELS:
-    # per step: every forward-stage launch (frames / collision / rows / velocity) and one solve
-    k = res["kernels"]
-    nfwd = k["forward"]["dispatches"][0] / max(1, k["solve"]["dispatches"][0])
-    parts = [k["forward"]["hbm_bytes_per_launch"], k["solve"]["hbm_bytes_per_launch"]]
-    if None not in parts:
-      k["forward"]["hbm_bytes_per_step_forward_plus_solve"] = nfwd * parts[0] + parts[1]
+  res = summarise(stats_dir, fetch_dir, write_dir, nworld, solver, model, _build.sources_hash())
   with open(out, "w") as fh:
     json.dump(res, fh, indent=1)
   print(json.dumps(res, indent=1))
