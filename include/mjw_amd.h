@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 12
+#define MJW_ABI_VERSION 13
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -110,7 +110,9 @@
  * Sparse models (is_sparse, the reference's io.py:67-74 switch) store qM / qLD as (nworld, nM) rows of
  * ancestors ascending then the diagonal (M_rowadr / M_colind), and efc_J as (nworld, njmax_pad, njrow)
  * stored slot-major (slot k of row r at [k * njmax_pad + r]) with efc_J_colind / efc_J_rownnz; dense models keep qM (nv_pad, nv_pad), qLD (nv, nv), efc_J
- * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt / ncon_world are sparse-path workspace (size 0 when dense). */
+ * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt / ncon_world are sparse-path workspace (size 0 when dense).
+ * world_order / world_key: the dense path's longest-first world order (a permutation of the worlds, rebuilt
+ * every step from the previous step's solver iterations) and each world's iteration bucket. */
 #define MJW_DATA_REAL_ARRAYS(X)                                                                    \
   X(time, 1) X(qpos, nq) X(qvel, nv) X(act, na) X(ctrl, nu) X(qacc_warmstart, nv)                 \
   X(qfrc_applied, nv) X(xfrc_applied, nbody * 6) X(mocap_pos, nmocap * 3) X(mocap_quat, nmocap * 4) \
@@ -141,7 +143,8 @@
   X(moment_rownnz, nu) X(moment_rowadr, nu) X(moment_colind, nJmom)                                \
   X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax_pad) X(eq_active, neq)                   \
   X(efc_J_colind, njmax_pad * njrow) X(efc_J_rownnz, njmax) X(efc_JT_rowind, njmax_pad * njrow)   \
-  X(efc_JT_adr, nv + 1) X(sp_cnt, nv + 1) X(ncon_world, 2)
+  X(efc_JT_adr, nv + 1) X(sp_cnt, nv + 1) X(ncon_world, 2)                                        \
+  X(world_order, 1) X(world_key, 1)
 
 /* ---- contact pool: float arrays, (naconmax, count) ---- */
 #define MJW_CONTACT_REAL_ARRAYS(X)                                                                 \
@@ -162,6 +165,10 @@ typedef struct mjw_model_t {
   MJW_MODEL_INT_ARRAYS(MJW_DECL_IA)
 } mjw_model_t;
 
+/* world-order workspace (mjw_data_t.sched): MJW_SCHED_BUCKETS histogram words, as many cursors, a flag */
+#define MJW_SCHED_BUCKETS 32
+#define MJW_SCHED_WORDS (2 * MJW_SCHED_BUCKETS + 2)
+
 typedef struct mjw_data_t {
   int32_t nworld;     /* worlds held by these buffers */
   int32_t njmax;      /* max constraint rows per world */
@@ -171,6 +178,8 @@ typedef struct mjw_data_t {
   int32_t pad_;
   int32_t* nacon;      /* (1,) contacts written this step (may exceed naconmax) */
   int32_t* ncollision; /* (1,) broadphase pairs this step */
+  int32_t* sched;      /* (MJW_SCHED_WORDS,) world-order workspace of the dense path: histogram of
+                        * the previous step's solver-iteration buckets, bucket cursors, valid flag */
 #define MJW_DECL_DRA(name, n) float* name;
 #define MJW_DECL_DIA(name, n) int32_t* name;
   MJW_DATA_REAL_ARRAYS(MJW_DECL_DRA)

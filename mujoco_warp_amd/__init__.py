@@ -36,6 +36,7 @@ from .mjcf import load_model_from_string
 from .mjcf import reset_data_keyframe
 from .support import contact_force
 from .support import get_state
+from .support import efc_J_csr
 from .support import mul_m
 from .support import set_state
 from .support import state_size

@@ -12,10 +12,18 @@ template <int FLAGS, bool NEWTON>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON>()];
-  const int wid = w0 + (int)blockIdx.x;
-  if (wid >= d.nworld) return;
+  const int b = w0 + (int)blockIdx.x;
+  if (b >= d.nworld) return;
+  // d.sched set: worlds in the forward kernel's longest-first order (world_order is a permutation)
+  const int wid = d.sched ? d.world_order[b] : b;
   WLOG_T0();
   dense_world<FLAGS, NEWTON>(m, d, wid, sm);
+  if ((FLAGS & DF_SOLVE) && d.sched && (threadIdx.x & 63) == 0) {
+    // the next step's order: bucket by this step's iterations, most iterations first
+    const int key = MJW_SCHED_BUCKETS - 1 - min(d.solver_niter[wid] >> 1, MJW_SCHED_BUCKETS - 1);
+    d.world_key[wid] = key;
+    atomicAdd(d.sched + key, 1);
+  }
   WLOG_END(wid, (FLAGS & DF_SOLVE) ? d.solver_niter[wid] : 0);
 }
 

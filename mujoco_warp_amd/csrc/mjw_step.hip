@@ -2132,7 +2132,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mj
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
   WLOG_T0();
+  // longest-first world order for the dense kernel that follows (d.sched is set only for full-range
+  // forward + dense launches, run() below): this world's slot in its iteration bucket, reserved now so
+  // that the atomic's latency overlaps the stages, written at the end
+  int order_pos = -1;
+  if constexpr ((STAGES & ST_POS) != 0) {
+    if (d.sched && w.lane == 0)
+      order_pos = d.sched[2 * MJW_SCHED_BUCKETS] ? atomicAdd(d.sched + MJW_SCHED_BUCKETS + d.world_key[w.wid], 1) : w.wid;
+  }
   run_stages<STAGES, BOX>(m, d, L, w);
+  if (order_pos >= 0 && order_pos < d.nworld) d.world_order[order_pos] = w.wid;
   WLOG_END(w.wid, 0);
 }
 
@@ -2181,8 +2190,31 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
 // clears the contact pool counters at the start of the position stage.  A kernel, not
 // hipMemsetAsync: in a captured hipGraph the 4-byte memset node was observed to race the
 // forward kernel (stale counts, contacts dropped past the pool), kernel nodes stay ordered
-__global__ void reset_counters_kernel(int* nacon, int* ncollision) {
-  if (threadIdx.x == 0) { nacon[0] = 0; ncollision[0] = 0; }
+//
+// It also turns the dense kernel's histogram of the last step's solver-iteration buckets (sched[0, NB))
+// into bucket cursors (sched[NB, 2 NB), exclusive prefix sums) and clears it; the order is valid
+// (sched[2 NB] = 1) only when the histogram counts every world exactly once, i.e. when the last dense
+// pass covered all worlds with the order enabled; otherwise the next step runs in identity order.
+__global__ void reset_counters_kernel(int* nacon, int* ncollision, int* sched, int nworld) {
+  const int t = threadIdx.x;
+  if (t == 0) { nacon[0] = 0; ncollision[0] = 0; }
+  if (sched) {
+    constexpr int NB = MJW_SCHED_BUCKETS;
+    static_assert(NB <= 64, "one wave scans the buckets");
+    const int h = t < NB ? sched[t] : 0;
+    int x = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (t >= o) x += y;
+    }
+    const int total = __shfl(x, 63);
+    if (t < NB) {
+      sched[NB + t] = x - h;
+      sched[t] = 0;
+    }
+    if (t == 0) sched[2 * NB] = total == nworld ? 1 : 0;
+  }
 }
 
 __global__ void ctrl_noise_kernel(const mjw_model_t m, const mjw_data_t d, const float* center, int step, float std, float rate_) {
@@ -2223,7 +2255,7 @@ int set_err(hipError_t e, const char* where) {
 }
 
 hipError_t reset_counters(const mjw_data_t* d, hipStream_t s) {
-  hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision);
+  hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision, d->sched, d->nworld);
   mjw::trace_launch(s, mjw::K_RESET);
   return hipGetLastError();
 }
@@ -2313,6 +2345,17 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   const bool full = (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE)) == (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE);
   const bool acc_sensors = full && m->nsensor > 0 && !(m->opt_disableflags & DSBL_SENSOR);
   if (dense_ok(m, d)) {
+    // longest-first order (forward kernel writes world_order, the dense kernels read it, the solving
+    // dense kernel histograms the iteration buckets for the next step): full forward + solve only;
+    // every other launch sees sched = nullptr and runs worlds in identity order.  MJW_WORLD_ORDER=0
+    // disables it (A/B measurements).
+    static const bool order_on = [] {
+      const char* e = getenv("MJW_WORLD_ORDER");
+      return !(e && e[0] == '0');
+    }();
+    mjw_data_t dv = *d;
+    if (!(order_on && full && d->sched)) dv.sched = nullptr;
+    d = &dv;
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel, for the
     // world range [w0, w0 + cnt) on stream st; `timed` records the optional bench events.
     // (Measured and dropped, DESIGN 4: a two-stream split of one batch inside the step -- the join

@@ -427,6 +427,8 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     efc_type=(njmax,), efc_id=(njmax,), efc_state=(njmax_pad,), eq_active=(m.neq,),
     efc_J_colind=(m.njrow * sp, njmax_pad), efc_J_rownnz=(njmax * sp,), efc_JT_rowind=(njmax_pad * m.njrow * sp,),
     efc_JT_adr=((nv + 1) * sp,), sp_cnt=((nv + 1) * sp,), ncon_world=(2,),
+    # the dense path's longest-first world order (mjw_step.hip) and each world's iteration bucket
+    world_order=(), world_key=(),
   )
   creal = dict(
     contact_dist=(), contact_pos=(3,), contact_frame=(3, 3), contact_includemargin=(), contact_friction=(5,),
@@ -519,6 +521,7 @@ def _alloc_data(m, nworld, nconmax, njmax, naconmax, device, nccdmax=None, njmax
   d.contact.efc_address.fill_(-1)
   d.nacon = torch.zeros(1, dtype=torch.int32, device=device)
   d.ncollision = torch.zeros(1, dtype=torch.int32, device=device)
+  d.sched = torch.zeros(_lib.SCHED_WORDS, dtype=torch.int32, device=device)
   d.efc.J_rowadr = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
   d.mocap_quat[..., 0] = 1.0
   d.xquat[..., 0] = 1.0
@@ -547,7 +550,7 @@ def _get_data_field(d, name):
 def cdata(d: types.Data) -> _lib.CData:
   """Builds (and caches) the C data view holding the device pointers of `d`."""
   names = [n for n, _ in _lib.DATA_REAL_ARRAYS + _lib.DATA_INT_ARRAYS + _lib.CONTACT_REAL_ARRAYS + _lib.CONTACT_INT_ARRAYS]
-  tensors = [_get_data_field(d, n) for n in names] + [d.nacon, d.ncollision]
+  tensors = [_get_data_field(d, n) for n in names] + [d.nacon, d.ncollision, d.sched]
   cache = getattr(d, "_cdata_cache", None)
   key = (d.nworld, d.njmax, d.njmax_pad, d.naconmax, d.world_offset)
   if cache is not None and cache[1] == key and all(a is b for a, b in zip(cache[2], tensors)):
@@ -560,6 +563,7 @@ def cdata(d: types.Data) -> _lib.CData:
     setattr(c, n, t.data_ptr())
   c.nacon = d.nacon.data_ptr()
   c.ncollision = d.ncollision.data_ptr()
+  c.sched = d.sched.data_ptr()
   d._cdata_cache = (c, key, tensors)
   return c
 

@@ -115,14 +115,91 @@ def contact_force(m: Model, d: Data, contact_ids: torch.Tensor, to_world_frame: 
   force[:] = out
 
 
+def _mulm_index(m: Model):
+  """Gather lists of the symmetric product with the sparse ancestor-row qM (support.py:67-101's
+  qM_mulm_rowadr / _col / _madr, padded to the longest row): for dof i, the entries of row i (its
+  ancestors and the diagonal) and the entries M[k, i] of every descendant k.  Padding points at a zero
+  column appended to vec.  Built once per Model on the host, kept on the device."""
+  idx = getattr(m, "_mulm_idx", None)
+  if idx is not None:
+    return idx
+  nv = int(m.nv)
+  rowadr = m.M_rowadr.reshape(-1).cpu().tolist()
+  rownnz = m.M_rownnz.reshape(-1).cpu().tolist()
+  colind = m.M_colind.reshape(-1).cpu().tolist()
+  ent = [[] for _ in range(nv)]
+  for i in range(nv):
+    for k in range(rownnz[i]):
+      a = rowadr[i] + k
+      j = colind[a]
+      ent[i].append((j, a))
+      if j != i:
+        ent[j].append((i, a))
+  K = max(1, max(len(e) for e in ent))
+  nM = int(m.nM)
+  col = torch.full((nv, K), nv, dtype=torch.long)
+  madr = torch.full((nv, K), nM, dtype=torch.long)
+  for i, e in enumerate(ent):
+    for k, (j, a) in enumerate(sorted(e)):
+      col[i, k], madr[i, k] = j, a
+  dev = m.M_rowadr.device
+  idx = (col.to(dev), madr.to(dev))
+  m._mulm_idx = idx
+  return idx
+
+
 def mul_m(m: Model, d: Data, res: torch.Tensor, vec: torch.Tensor, skip: Optional[torch.Tensor] = None, M: Optional[torch.Tensor] = None):
-  """res = qM @ vec per world (support.py:132-171, dense qM)."""
+  """res = qM @ vec per world (support.py:132-171): dense qM (nworld, nv_pad, nv_pad) as a batched
+  matvec; sparse qM (nworld, nM) in the ancestor-row layout as a gather over each dof's row and column
+  entries (mul_m_sparse, support.py:67-101), summed in a fixed order."""
   if M is None:
     M = d.qM
   nv = m.nv
-  out = torch.bmm(M[:, :nv, :nv], vec.unsqueeze(-1)).squeeze(-1)
+  if m.is_sparse:
+    col, madr = _mulm_index(m)
+    nw = M.shape[0]
+    Mz = torch.cat([M.reshape(nw, -1), M.new_zeros((nw, 1))], dim=1)
+    vz = torch.cat([vec.reshape(nw, -1)[:, :nv], vec.new_zeros((nw, 1))], dim=1)
+    out = (Mz[:, madr] * vz[:, col]).sum(dim=2)
+  else:
+    out = torch.bmm(M[:, :nv, :nv], vec.unsqueeze(-1)).squeeze(-1)
   if skip is None:
     res[:] = out
   else:
     keep = ~skip.to(torch.bool)
     res[keep] = out[keep]
+
+
+def efc_J_csr(m: Model, d: Data, njmax_nnz: Optional[int] = None):
+  """The sparse constraint Jacobian in the reference's CSR layout (io.py:940-943: `efc.J_rownnz`,
+  `efc.J_rowadr` (nworld, njmax), `efc.J_colind` / `efc.J` (nworld, 1, njmax_nnz)), converted from this
+  build's slot-major ELL rows (slot k of row r at `efc_J[w, k, r]`).  Rows are packed in
+  row order; columns ascend within a row.  Rows past nefc have rownnz 0.  Returns
+  (J_rownnz, J_rowadr, J_colind, J); a device-side conversion (torch ops), no host round trip."""
+  if not m.is_sparse:
+    raise ValueError("efc_J_csr: dense models keep efc.J as (nworld, njmax_pad, nv_pad), as the reference does")
+  nw, njmax = d.nworld, d.njmax
+  dev = d.efc.J.device
+  nnz = (njmax_nnz or getattr(d, "njmax_nnz", None) or njmax * int(m.nv))
+  nrow = torch.minimum(d.nefc.reshape(nw), torch.tensor(njmax, device=dev)).to(torch.long)
+  rows = torch.arange(njmax, device=dev)
+  rownnz = torch.where(rows[None, :] < nrow[:, None], d.efc.J_rownnz.reshape(nw, -1)[:, :njmax].to(torch.long), torch.zeros((), dtype=torch.long, device=dev))
+  rowadr = torch.cumsum(rownnz, dim=1) - rownnz
+  if int((rowadr[:, -1] + rownnz[:, -1]).max()) > nnz:
+    raise ValueError(f"efc_J_csr: more than njmax_nnz = {nnz} non-zeros")
+  njrow = d.efc.J.shape[1]
+  vals = d.efc.J.reshape(nw, njrow, -1)[:, :, :njmax].transpose(1, 2)  # (nw, njmax, njrow)
+  cols = d.efc.J_colind.reshape(nw, njrow, -1)[:, :, :njmax].transpose(1, 2).to(torch.long)
+  slot = torch.arange(njrow, device=dev)
+  valid = slot[None, None, :] < rownnz[:, :, None]
+  big = int(m.nv) + 1
+  key = torch.where(valid, cols, torch.full_like(cols, big))
+  key, order = torch.sort(key, dim=2, stable=True)
+  vals = torch.gather(vals, 2, order)
+  pos = rowadr[:, :, None] + slot[None, None, :]
+  wid = torch.arange(nw, device=dev)[:, None, None].expand_as(pos)
+  J = torch.zeros((nw, 1, nnz), dtype=vals.dtype, device=dev)
+  colind = torch.zeros((nw, 1, nnz), dtype=torch.int32, device=dev)
+  J[wid[valid], 0, pos[valid]] = vals[valid]
+  colind[wid[valid], 0, pos[valid]] = key[valid].to(torch.int32)
+  return rownnz.to(torch.int32), rowadr.to(torch.int32), colind, J

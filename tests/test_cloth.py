@@ -309,3 +309,97 @@ def test_gpu_aloha_global_contact_pool_overflow():
     ids = d2s.efc.id[w, :n].cpu().numpy()
     con = typ == int(ConstraintType.CONTACT_PYRAMIDAL)
     assert (ids[con] < pool).all()
+
+
+def _mul_m_check(mjm, device):
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  m = mjw.put_model(mjm, device=device)
+  d = mjw.make_data(mjm, nworld=3, nconmax=8, njmax=8, device=device, m=m)
+  rng = np.random.default_rng(5)
+  qm = rng.normal(size=(3, int(m.nM)))
+  vec = rng.normal(size=(3, mjm.nv))
+  d.qM[:] = torch.as_tensor(qm, dtype=torch.float32, device=device)
+  res = torch.zeros((3, mjm.nv), dtype=torch.float32, device=device)
+  v = torch.as_tensor(vec, dtype=torch.float32, device=device)
+  mjw.mul_m(m, d, res, v)
+  skip = torch.tensor([False, True, False], device=device)
+  res2 = torch.full((3, mjm.nv), 7.0, dtype=torch.float32, device=device)
+  mjw.mul_m(m, d, res2, v, skip=skip)
+  qm32 = qm.astype(np.float32).astype(np.float64)
+  for w in range(3):
+    want = dense_qM(mjm, qm32[w]) @ vec[w].astype(np.float32)
+    assert_close(f"mul_m[w{w}]", res[w].cpu().numpy(), want, rtol=1e-5, atol=1e-5 * np.abs(want).max())
+  assert (res2[1] == 7.0).all() and torch.equal(res2[0], res[0])
+
+
+def test_mul_m_sparse_layout(mjm):
+  """support.mul_m on the sparse ancestor-row qM (support.py:67-101 gather): equal to the densified
+  matrix times the vector, on the CPU device (torch ops only, no kernel)."""
+  _mul_m_check(mjm, "cpu")
+
+
+@pytest.mark.gpu
+def test_gpu_mul_m_sparse_layout(mjm):
+  _mul_m_check(mjm, "cuda")
+
+
+def _csr_dense(rownnz, rowadr, colind, J, w, n, nv):
+  out = np.zeros((n, nv))
+  for r in range(n):
+    a, k = int(rowadr[w, r]), int(rownnz[w, r])
+    c = colind[w, 0, a:a + k]
+    assert (np.diff(c) > 0).all()
+    out[r, c] = J[w, 0, a:a + k]
+  return out
+
+
+def test_efc_J_csr_converter(mjm):
+  """The ELL -> reference-CSR converter (io.py:940-943 layout) on synthetic slot-major rows (CPU)."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  m = mjw.put_model(mjm, device="cpu")
+  d = mjw.make_data(mjm, nworld=2, nconmax=8, njmax=16, device="cpu", m=m)
+  rng = np.random.default_rng(9)
+  nv, njrow = mjm.nv, d.efc.J.shape[1]
+  dense = np.zeros((2, 16, nv))
+  nefc = [5, 11]
+  for w in range(2):
+    d.nefc[w] = nefc[w]
+    for r in range(nefc[w]):
+      k = int(rng.integers(1, njrow + 1))
+      cols = rng.choice(nv, size=k, replace=False)
+      vals = rng.normal(size=k)
+      d.efc.J_rownnz[w, r] = k
+      for s in range(k):  # unsorted slots, as a tree walk may emit them
+        d.efc.J[w, s, r] = vals[s]
+        d.efc.J_colind[w, s, r] = int(cols[s])
+        dense[w, r, cols[s]] = np.float32(vals[s])
+    d.efc.J_rownnz[w, nefc[w]:] = 3  # stale counts past nefc are ignored
+  rownnz, rowadr, colind, J = mjw.efc_J_csr(m, d, njmax_nnz=16 * njrow)
+  assert J.shape == (2, 1, 16 * njrow) and rownnz.shape == (2, 16)
+  for w in range(2):
+    assert int(rownnz[w, nefc[w]:].sum()) == 0
+    got = _csr_dense(rownnz.numpy(), rowadr.numpy(), colind.numpy(), J.numpy(), w, nefc[w], nv)
+    np.testing.assert_array_equal(got, dense[w, :nefc[w]])
+
+
+@pytest.mark.gpu
+def test_gpu_efc_J_csr_matches_rows(mjm):
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  qpos, qvel, ctrl = cloth_states(mjm, 2, seed=1)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=NJMAX, nconmax=NCONMAX)
+  mjw.fwd_position(m, d)
+  rownnz, rowadr, colind, J = mjw.efc_J_csr(m, d)
+  torch.cuda.synchronize()
+  for w in range(2):
+    n = int(d.nefc[w])
+    got = _csr_dense(rownnz.cpu().numpy(), rowadr.cpu().numpy(), colind.cpu().numpy(), J.cpu().numpy(), w, n, mjm.nv)
+    np.testing.assert_array_equal(got, dense_J(d, w, n, mjm.nv))
