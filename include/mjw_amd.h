@@ -249,6 +249,11 @@ int mjw_selftest(int which, const float* in, float* out, int n, void* stream);
  *            16 out per case, aux unused. */
 int mjw_kat(int which, const float* in, const float* aux, float* out, int n, void* stream);
 
+/* qfrc_actuator from the Data's actuator_force and moment rows (forward.py:899-927), for hosts that run
+ * the act_dyn / act_gain / act_bias callbacks (forward.py:876-881) between mjw_fwd_actuation and the
+ * moment map; dense path only */
+int mjw_actuator_map(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+
 int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* center, int step, float std, float rate,
                    void* stream);
 

@@ -2217,6 +2217,35 @@ __global__ void reset_counters_kernel(int* nacon, int* ncollision, int* sched, i
   }
 }
 
+// forward.py:899-927 (_qfrc_actuator, _qfrc_actuator_gravcomp_limits): qfrc_actuator = moment' force
+// from the Data's actuator_force and sparse moment rows, clamped by the joint actuator force range;
+// one wave per world, lanes over dofs.  The staged fwd_actuation runs it after the act_dyn / act_gain /
+// act_bias callbacks (forward.py:876-881), which may rewrite actuator_force.
+__global__ void __launch_bounds__(64) actuator_map_kernel(const mjw_model_t m, const mjw_data_t d) {
+  const int wid = blockIdx.x, lane = threadIdx.x;
+  if (wid >= d.nworld) return;
+  const int nv = m.nv, nu = m.nu;
+  const bool off = !nu || (m.opt_disableflags & DSBL_ACTUATION);
+  const float* jnt_actfrcrange = MR(jnt_actfrcrange);
+  for (int i = lane; i < nv; i += 64) {
+    float q = 0.0f;
+    if (!off) {
+      for (int a = 0; a < nu; a++) {
+        const long ga = (long)wid * nu + a;
+        const int nnz = d.moment_rownnz[ga], adr = d.moment_rowadr[ga];
+        const float f = d.actuator_force[ga];
+        for (int k = 0; k < nnz; k++) {
+          const long e = (long)wid * m.nJmom + adr + k;
+          if (d.moment_colind[e] == i) q += d.actuator_moment[e] * f;
+        }
+      }
+      const int j = m.dof_jntid[i];
+      if (m.jnt_actfrclimited[j]) q = clampf(q, jnt_actfrcrange[2 * j], jnt_actfrcrange[2 * j + 1]);
+    }
+    d.qfrc_actuator[(long)wid * nv + i] = q;
+  }
+}
+
 __global__ void ctrl_noise_kernel(const mjw_model_t m, const mjw_data_t d, const float* center, int step, float std, float rate_) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.nworld * m.nu) return;
@@ -2519,6 +2548,14 @@ int mjw_solve(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
 }
 int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_EULER, "mjw_euler");
+}
+
+int mjw_actuator_map(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  if (!m || !d) { g_err = "mjw_actuator_map: null model/data"; return -1; }
+  if (d->nworld <= 0) return 0;
+  if (m->is_sparse) { g_err = "mjw_actuator_map: sparse models keep the moment map inside the velocity-stage kernel"; return -2; }
+  hipLaunchKernelGGL(mjw::actuator_map_kernel, dim3(d->nworld), dim3(64), 0, (hipStream_t)stream, *m, *d);
+  return set_err(hipGetLastError(), "mjw_actuator_map");
 }
 
 int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* center, int step, float std, float rate, void* stream) {

@@ -75,13 +75,11 @@ class StepTracer:
     return out
 
 
-# callbacks whose reference call sites fall inside one fused launch of this path: act_dyn / act_gain /
-# act_bias run between _actuator_force and the moment map (forward.py:876-881), contactfilter between
-# the narrowphase and make_constraint (collision_driver.py:788); they are refused instead of being run
-# where they could no longer change the step
-_UNSUPPORTED_CALLBACKS = {
-  "act_dyn": "forward.py:876", "act_gain": "forward.py:878", "act_bias": "forward.py:880", "contactfilter": "collision_driver.py:788",
-}
+# callbacks whose reference call sites fall inside one fused launch of this path: contactfilter runs
+# between the narrowphase and make_constraint (collision_driver.py:788), which share the position-stage
+# kernel; it is refused instead of being run where it could no longer change the step
+_UNSUPPORTED_CALLBACKS = {"contactfilter": "collision_driver.py:788"}
+_STAGED_CALLBACKS = ("control", "passive", "act_dyn", "act_gain", "act_bias")
 
 
 def _has_callbacks(m: Model) -> bool:
@@ -89,7 +87,7 @@ def _has_callbacks(m: Model) -> bool:
   for f, where in _UNSUPPORTED_CALLBACKS.items():
     if getattr(cb, f) is not None:
       raise NotImplementedError(f"callback.{f} (called at reference {where}) is not supported: the stage it hooks into is one fused HIP launch")
-  return any(getattr(cb, f) is not None for f in ("control", "passive"))
+  return any(getattr(cb, f) is not None for f in _STAGED_CALLBACKS)
 
 
 def fwd_position(m: Model, d: Data):
@@ -106,9 +104,20 @@ def fwd_velocity(m: Model, d: Data):
 
 
 def fwd_actuation(m: Model, d: Data):
-  """Actuation-dependent computations (forward.py:836-927)."""
+  """Actuation-dependent computations (forward.py:836-927).  With act_dyn / act_gain / act_bias
+  callbacks: actuator force and act_dot first, then the callbacks in the reference's order
+  (forward.py:876-881), then the moment map qfrc_actuator = moment' actuator_force from the forces the
+  callbacks left (mjw_actuator_map)."""
   _has_callbacks(m)
   _call("mjw_fwd_actuation", m, d)
+  cb = m.callback
+  act_cbs = [f for f in (cb.act_dyn, cb.act_gain, cb.act_bias) if f is not None]
+  if act_cbs and m.nu and not (m.opt.disableflags & DisableBit.ACTUATION):
+    if m.is_sparse:
+      raise NotImplementedError("act_* callbacks on the sparse path: its moment map is fused into the velocity-stage kernel")
+    for f in act_cbs:
+      f(m, d)
+    _call("mjw_actuator_map", m, d)
 
 
 def fwd_acceleration(m: Model, d: Data, factorize: bool = True):

@@ -149,3 +149,47 @@ def test_gpu_get_set_state_roundtrip():
   mjw.step(m2, d2)
   torch.cuda.synchronize()
   np.testing.assert_array_equal(np_(d.qpos), np_(d2.qpos))
+
+
+def _humanoid_gpu(seed, gain_scale=1.0):
+  import mujoco_warp_amd as mjw
+  from tests.common import gpu_from_state, humanoid_model, random_states
+
+  mjm = humanoid_model("CG")
+  mjm.actuator_gainprm = np.array(mjm.actuator_gainprm, dtype=np.float64) * gain_scale
+  qpos, qvel, ctrl = random_states(mjm, 8, seed=seed)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl)
+  return mjm, m, d
+
+
+@pytest.mark.gpu
+def test_gpu_act_callbacks_run_between_force_and_moment_map():
+  """act_dyn / act_gain / act_bias (forward.py:876-881) run in that order after the actuator forces and
+  before the moment map: a gain callback that doubles every humanoid motor force (FIXED gain, no bias,
+  no force limit) steps bitwise like a model whose gains are doubled (x2 is exact in fp32), and the
+  callbacks see the forces _actuator_force computed."""
+  import mujoco_warp_amd as mjw
+
+  mjm, m, d = _humanoid_gpu(seed=90)
+  assert not np.asarray(mjm.actuator_forcelimited).any() and (np.asarray(mjm.actuator_biastype) == 0).all()
+  _, m2, d2 = _humanoid_gpu(seed=90, gain_scale=2.0)
+  order, seen = [], []
+
+  def gain(mm, dd):
+    order.append("gain")
+    seen.append(dd.actuator_force.clone())
+    dd.actuator_force.mul_(2.0)
+
+  m.callback.act_dyn = lambda mm, dd: order.append("dyn")
+  m.callback.act_gain = gain
+  m.callback.act_bias = lambda mm, dd: order.append("bias")
+  for _ in range(3):
+    mjw.step(m, d)
+    mjw.step(m2, d2)
+  torch.cuda.synchronize()
+  assert order == ["dyn", "gain", "bias"] * 3
+  assert float(seen[0].abs().max()) > 0
+  np.testing.assert_array_equal(np_(d.actuator_force), np_(d2.actuator_force))
+  np.testing.assert_array_equal(np_(d.qfrc_actuator), np_(d2.qfrc_actuator))
+  np.testing.assert_array_equal(np_(d.qpos), np_(d2.qpos))
+  np.testing.assert_array_equal(np_(d.qvel), np_(d2.qvel))
