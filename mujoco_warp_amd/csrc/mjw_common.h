@@ -42,8 +42,10 @@ enum : int {
   SENS_FRAMELINACC = 33, SENS_FRAMEANGACC = 34, SENS_SUBTREECOM = 35, SENS_CLOCK = 45
 };
 enum : int { ENBL_ENERGY = 2 };
-enum : int { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
-enum : int { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3 };
+enum : int { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6,
+             CNSTR_CONTACT_ELLIPTIC = 7 };
+enum : int { CONE_PYRAMIDAL = 0, CONE_ELLIPTIC = 1 };
+enum : int { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3, STATE_CONE = 4 };
 enum : int { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
 enum : int { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
 enum : int { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
@@ -124,8 +126,18 @@ static __device__ unsigned long long g_prof[PH_N];
     }                                                                                           \
     return (int)e;                                                                              \
   }
-// per-wave lifetime log (tools/wave_log.py): 4 x u64 per world, {start, end} s_memrealtime (100 MHz,
-// one clock for the whole chip), HW_ID | XCC_ID << 32, solver iterations; set with the TU's setter
+#else
+#define MJW_PROF_READER(fname)
+#define PROF_T0() (void)0
+#define PROF_MARK(ph) (void)0
+#define PROF_T0_SUB() (void)0
+#define PROF_MARK_SUB(ph) (void)0
+#endif
+
+// per-wave lifetime log (tools/wave_log.py; -DMJW_WAVELOG alone, or with MJW_PROFILE): 4 x u64 per
+// world, {start, end} s_memrealtime (100 MHz, one clock for the whole chip), HW_ID | XCC_ID << 32,
+// solver iterations; set with the translation unit's setter
+#if defined(MJW_PROFILE) || defined(MJW_WAVELOG)
 static __device__ unsigned long long* g_wlog = nullptr;
 #define WLOG_T0() const unsigned long long _wt0 = __builtin_amdgcn_s_memrealtime()
 #define WLOG_END(wid, niter)                                                                         \
@@ -147,11 +159,6 @@ static __device__ unsigned long long* g_wlog = nullptr;
 #define WLOG_T0() (void)0
 #define WLOG_END(wid, niter) (void)0
 #define MJW_WLOG_SETTER(fname)
-#define MJW_PROF_READER(fname)
-#define PROF_T0() (void)0
-#define PROF_MARK(ph) (void)0
-#define PROF_T0_SUB() (void)0
-#define PROF_MARK_SUB(ph) (void)0
 #endif
 
 // ---- launch trace (mjw_step_trace): one HIP event recorded after every kernel launch of a step,
@@ -160,7 +167,7 @@ static __device__ unsigned long long* g_wlog = nullptr;
 enum : int {
   K_RESET = 0, K_CTRL_NOISE, K_CCD, K_SENSOR, K_RK4,
   K_SP_POS, K_SP_CCD, K_SP_COLL, K_SP_CON, K_SP_VEL, K_SP_INDEX, K_SP_SOLVE, K_SP_SOLVE_LDS, K_SP_EULER,
-  K_DENSE = 32,  // + 2 * FLAGS + NEWTON  (dense_kernel<FLAGS, NEWTON>)
+  K_DENSE = 32,  // + 4 * FLAGS + 2 * ELL + NEWTON  (dense_kernel<FLAGS, NEWTON, ELL>)
   K_FWD = 256,   // + 2 * STAGES + box    (mjw_kernel<STAGES, box>)
   K_END = 512
 };

@@ -279,6 +279,59 @@ __device__ __forceinline__ Pt ls_point(const Row& w, float alpha, float q1, floa
   return p;
 }
 
+// ---- elliptic cones (solver.py:263-323 _eval_elliptic, 1550-1611 quad, 1886-1942 update) ----------
+// quad / quad1 / quad2 of one contact, held by the lane of its first row for one line search
+struct Ell {
+  float q0, q1, q2, u0, v0, uu, uv, vv, dm, mu;
+};
+
+__device__ __forceinline__ void eval_elliptic(const Ell& e, float alpha, float& c, float& g, float& hh) {
+  c = g = hh = 0.0f;
+  const float N = e.u0 + alpha * e.v0;
+  const float Tsqr = e.uu + alpha * (2.0f * e.uv + alpha * e.vv);
+  bool bottom = false;
+  if (Tsqr <= 0.0f) {
+    bottom = N < 0.0f;
+  } else {
+    const float T = sqrtf(Tsqr);
+    if (N >= e.mu * T) return;
+    if (e.mu * N + T <= 0.0f) {
+      bottom = true;
+    } else {
+      const float N1 = e.v0, T1 = (e.uv + alpha * e.vv) / T;
+      const float T2 = e.vv / T - (e.uv + alpha * e.vv) * T1 / (T * T);
+      const float nmt = N - e.mu * T, d1 = N1 - e.mu * T1;
+      c = 0.5f * e.dm * nmt * nmt;
+      g = e.dm * nmt * d1;
+      hh = e.dm * (d1 * d1 + nmt * (-e.mu * T2));
+      return;
+    }
+  }
+  if (bottom) {
+    const float aq2 = alpha * e.q2;
+    c = alpha * aq2 + alpha * e.q1 + e.q0;
+    g = 2.0f * aq2 + e.q1;
+    hh = 2.0f * e.q2;
+  }
+}
+
+// ls_point with elliptic rows (cls 3): the contact's first row evaluates the cone, the others add 0
+__device__ __forceinline__ Pt ls_point_e(const Row& w, const Ell& e, bool first, float alpha, float q1, float q2, float qg0) {
+  float c, g, hh;
+  if (w.cls == 3) {
+    if (first) eval_elliptic(e, alpha, c, g, hh);
+    else c = g = hh = 0.0f;
+  } else {
+    row_eval(w, alpha, c, g, hh);
+  }
+  Pt p;
+  p.alpha = alpha;
+  p.c = dsum(c) + alpha * alpha * q2 + alpha * q1 + qg0;
+  p.g = dsum(g) + 2.0f * alpha * q2 + q1;
+  p.h = dsum(hh) + 2.0f * q2;
+  return p;
+}
+
 __device__ __forceinline__ bool bracket(const Pt& x, const Pt& y) { return (x.g < y.g && y.g < 0.0f) || (x.g > y.g && y.g > 0.0f); }
 
 // force / state / cost of one row at its current jaref
@@ -299,17 +352,22 @@ __device__ __forceinline__ float row_force(const Row& w, int& state, float& cost
 
 // ---- the kernel ---------------------------------------------------------------------------
 // LDS words of one world of the dense path
-template <int FLAGS, bool NEWTON>
+// elliptic-cone workspace (ELL): per row D, cone coefficient, two scratch rows, first row / dim of its
+// contact, and the 6 cone-Hessian coefficients of the row (Newton)
+constexpr int DE_WORDS = 6 * 64 + 6 * 64;
+template <int FLAGS, bool NEWTON, bool ELL = false>
 __host__ __device__ constexpr int dense_lds_words() {
-  return ((NEWTON && (FLAGS & DF_SOLVE)) ? DJ_WORDS + DS_WORDS : DJ_WORDS) + 5 * 64;
+  return ((NEWTON && (FLAGS & DF_SOLVE)) ? DJ_WORDS + DS_WORDS : DJ_WORDS) + 5 * 64 + (ELL && (FLAGS & DF_SOLVE) ? DE_WORDS : 0);
 }
+
 
 // factor / solve / integrate of world `wid` by the calling wavefront; sm: dense_lds_words() floats of
 // LDS, 16-B aligned (the dense kernel's own, or the fused step kernel's dynamic LDS once the
 // forward stages are done with it)
-template <int FLAGS, bool NEWTON>
+template <int FLAGS, bool NEWTON, bool ELL = false>
 __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data_t& d, const int wid, float* sm) {
   constexpr bool NT = NEWTON && (FLAGS & DF_SOLVE);
+  constexpr bool EL = ELL && (FLAGS & DF_SOLVE);
   constexpr int S_OFF = NT ? DJ_WORDS : 0;  // CG: the 32x32 scratch aliases J (used before J is staged)
   constexpr int V_OFF = NT ? DJ_WORDS + DS_WORDS : DJ_WORDS;
   float* Jl = sm;
@@ -319,6 +377,15 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
   float* vr = vd + 128;          // row vector buffer (64)
   float* vr2 = vd + 192;         // second row buffer (Newton weights)
   float* vq = vd + 256;          // qpos (Euler)
+  // elliptic workspace (EL only): per row D, cone coefficient (mu for the first row of a contact, its
+  // friction coefficient for the others), scratch A / B, first row and dim of the contact, cone Hessian
+  float* eD = vd + 320;
+  float* eF = eD + 64;
+  float* eA = eD + 128;
+  float* eB = eD + 192;
+  int* eR0 = reinterpret_cast<int*>(eD + 256);
+  int* eDim = reinterpret_cast<int*>(eD + 320);
+  float* eC = eD + 384;  // 6 per row
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
   const int nv = m.nv, np = m.nv_pad;
   const bool dof = c < nv;      // lane holds a dof value (both halves)
@@ -416,6 +483,34 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       w.rf = safe_div(w.fl, w.D);
       w.cls = lane < ne ? 0 : (lane < ne + nf ? 1 : 2);
       w.jv = 0.0f;
+      // elliptic contacts (cls 3): the rows of one contact are consecutive (constraint rows are emitted
+      // per contact); e_r0 = its first row (segment start of equal efc_id), e_dim its rows, e_fr this
+      // row's cone coefficient; a contact cut by njmax (e_r0 + e_dim > nefc) contributes nothing
+      int e_r0 = lane, e_dim = 1;
+      float e_fr = 0.0f, e_mu = 0.0f;
+      bool e_cut = false;
+      if (EL) {
+        const int typ = row ? d.efc_type[(long)wid * njmax + lane] : -1;
+        const bool ell = typ == CNSTR_CONTACT_ELLIPTIC;
+        const int cid = ell ? d.efc_id[(long)wid * njmax + lane] : -1;
+        const int prev = __shfl_up(cid, 1, 64);
+        const unsigned long long starts = __ballot(ell && (lane == 0 || prev != cid));
+        if (ell) {
+          e_r0 = 63 - __clzll(starts & ((2ull << lane) - 1ull));
+          e_dim = d.contact_dim[cid];
+          const float* fr = d.contact_friction + 5L * cid;
+          e_mu = fr[0] * MR(opt_impratio_invsqrt)[0];
+          const int k = lane - e_r0;
+          e_fr = k == 0 ? e_mu : fr[k - 1];
+          e_cut = e_r0 + e_dim > nefc;
+          w.cls = 3;
+        }
+        eD[lane] = w.D;
+        eF[lane] = e_fr;
+        eR0[lane] = e_r0;
+        eDim[lane] = (ell && !e_cut) ? e_dim : 1;
+      }
+      Ell ecoef = {};
       const float tolerance = MR(opt_tolerance)[0];
       const float ls_tolerance = MR(opt_ls_tolerance)[0];
       const float meaninertia = MR(stat_meaninertia)[0];
@@ -433,6 +528,33 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       auto update_constraint = [&]() {
         float rc;
         force = row_force(w, state, rc);
+        if (EL) {
+          // elliptic cone zones (solver.py:1886-1942): N from the first row, T from the friction rows
+          eA[lane] = w.jaref * e_fr;
+          __syncthreads();
+          if (w.cls == 3) {
+            float TT = 0.0f;
+            for (int j = 1; j < e_dim && !e_cut; j++) {
+              const float u = eA[e_r0 + j];
+              TT += u * u;
+            }
+            const float N = eA[e_r0], mu = e_mu;
+            const float T = TT <= 0.0f ? 0.0f : sqrtf(TT);
+            rc = 0.0f;
+            if (e_cut || N >= mu * T || (T <= 0.0f && N >= 0.0f)) {
+              force = 0.0f; state = STATE_SATISFIED;
+            } else if (mu * N + T <= 0.0f || (T <= 0.0f && N < 0.0f)) {
+              force = -w.D * w.jaref; state = STATE_QUADRATIC; rc = 0.5f * w.D * w.jaref * w.jaref;
+            } else {
+              const float dm = safe_div(eD[e_r0], mu * mu * (1.0f + mu * mu));
+              const float nmt = N - mu * T;
+              const float f0 = -dm * nmt * mu;
+              if (lane == e_r0) { force = f0; rc = 0.5f * dm * nmt * nmt; }
+              else force = -safe_div(f0, T) * (eA[lane] * e_fr);
+              state = STATE_CONE;
+            }
+          }
+        }
         if (!row) { force = 0.0f; rc = 0.0f; }
         vr[lane] = force;
         __syncthreads();
@@ -447,13 +569,55 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         if (NEWTON) {
           // H = M + J' diag(D * quadratic) J (solver.py:2896-3008): 32x32x2 MFMA over row pairs
           vr2[lane] = (row && state == STATE_QUADRATIC) ? w.D : 0.0f;
+          if (EL) {
+            // + J_c' C J_c for elliptic contacts in the cone state (solver.py:2430-2585): row a's MFMA
+            // operand becomes sum_k C[a][k] J[r0 + k] (C = D on the diagonal for quadratic rows)
+            const int ea = lane - e_r0;
+            const bool quad = row && state == STATE_QUADRATIC;
+            const bool cone = w.cls == 3 && state == STATE_CONE;
+            float dm = 0.0f, mu = e_mu, mu_over_t = 0.0f, mu_n_over_ttt = 0.0f, diag = 0.0f, ua = 0.0f;
+            if (cone) {
+              const float mu2 = mu * mu;
+              dm = safe_div(eD[e_r0], mu2 * (1.0f + mu2));
+              const float n = eA[e_r0];
+              float tt = 0.0f;
+              for (int j = 1; j < e_dim; j++) tt += eA[e_r0 + j] * eA[e_r0 + j];
+              float t = tt <= 0.0f ? 0.0f : sqrtf(tt);
+              t = fmaxf(t, MJW_MINVAL);
+              const float ttt = fmaxf(t * t * t, MJW_MINVAL);
+              mu_over_t = safe_div(mu, t);
+              mu_n_over_ttt = mu * safe_div(n, ttt);
+              diag = mu2 - mu * safe_div(n, t);
+              ua = eA[lane];
+            }
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+              float ck = (quad && k == ea) ? w.D : 0.0f;
+              if (cone && k < e_dim) {
+                const float ub = eA[e_r0 + k];
+                float hc;
+                if (ea == 0 && k == 0) hc = 1.0f;
+                else if (ea == 0) hc = -mu_over_t * ub;
+                else if (k == 0) hc = -mu_over_t * ua;
+                else hc = mu_n_over_ttt * ua * ub + (ea == k ? diag : 0.0f);
+                ck = hc * dm * e_fr * eF[e_r0 + k];
+              }
+              eC[6 * lane + k] = ck;
+            }
+          }
           __syncthreads();
           f32x16 H = Mm;
           const int npair = (nefc + 1) >> 1;
           for (int t = 0; t < npair; t++) {
             int r = 2 * t + h;
             float jrc = Jl[r * DJS + c];
-            H = __builtin_amdgcn_mfma_f32_32x32x2f32(jrc, vr2[r] * jrc, H, 0, 0, 0);
+            float wrc = vr2[r] * jrc;
+            if (EL) {
+              wrc = 0.0f;
+              const int r0 = eR0[r], dm_ = eDim[r];
+              for (int k = 0; k < dm_; k++) wrc = fmaf(eC[6 * r + k], Jl[(r0 + k) * DJS + c], wrc);
+            }
+            H = __builtin_amdgcn_mfma_f32_32x32x2f32(jrc, wrc, H, 0, 0, 0);
           }
           // identity-pad rows/cols >= nv, then rows into lanes through S
 #pragma unroll
@@ -497,9 +661,31 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         const float q1 = dsum(lo ? search * (ma - qfrc_smooth) : 0.0f);
         const float q2 = dsum(lo ? 0.5f * search * mv : 0.0f);
         const float qg0 = gauss;
-        Pt p0 = ls_point(w, 0.0f, q1, q2, qg0);
+        const bool e_first = EL && w.cls == 3 && lane == e_r0 && !e_cut;
+        if (EL) {
+          // per-contact quad / quad1 / quad2 at the first row (solver.py:1550-1611)
+          eA[lane] = w.jaref;
+          eB[lane] = w.jv;
+          __syncthreads();
+          ecoef = Ell{};
+          if (e_first) {
+            const float D0 = w.D, ja = w.jaref, jv = w.jv, mu = e_mu;
+            ecoef.q0 = 0.5f * ja * ja * D0; ecoef.q1 = jv * ja * D0; ecoef.q2 = 0.5f * jv * jv * D0;
+            ecoef.u0 = ja * mu; ecoef.v0 = jv * mu; ecoef.mu = mu;
+            for (int j = 1; j < e_dim; j++) {
+              const int rj = lane + j;
+              const float jaj = eA[rj], jvj = eB[rj], dj = eD[rj], fj = eF[rj], DJj = dj * jaj;
+              ecoef.q0 += 0.5f * jaj * DJj; ecoef.q1 += jvj * DJj; ecoef.q2 += 0.5f * jvj * dj * jvj;
+              const float uj = jaj * fj, vj = jvj * fj;
+              ecoef.uu += uj * uj; ecoef.uv += uj * vj; ecoef.vv += vj * vj;
+            }
+            ecoef.dm = D0 / (mu * mu * (1.0f + mu * mu));
+          }
+        }
+        auto lsp = [&](float al) -> Pt { return EL ? ls_point_e(w, ecoef, e_first, al, q1, q2, qg0) : ls_point(w, al, q1, q2, qg0); };
+        Pt p0 = lsp(0.0f);
         float lo_alpha_in = -safe_div(p0.g, p0.h);
-        Pt lo_in = ls_point(w, lo_alpha_in, q1, q2, qg0);
+        Pt lo_in = lsp(lo_alpha_in);
         float alpha;
         if (fabsf(lo_in.g) < gtol && lo_in.c < p0.c) {
           alpha = lo_alpha_in;
@@ -509,9 +695,9 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
           Pt plo = lo_less ? lo_in : p0;
           Pt phi = lo_less ? p0 : lo_in;
           for (int it = 0; it < m.opt_ls_iterations; it++) {
-            Pt ln = ls_point(w, plo.alpha - safe_div(plo.g, plo.h), q1, q2, qg0);
-            Pt hn = ls_point(w, phi.alpha - safe_div(phi.g, phi.h), q1, q2, qg0);
-            Pt md = ls_point(w, 0.5f * (plo.alpha + phi.alpha), q1, q2, qg0);
+            Pt ln = lsp(plo.alpha - safe_div(plo.g, plo.h));
+            Pt hn = lsp(phi.alpha - safe_div(phi.g, phi.h));
+            Pt md = lsp(0.5f * (plo.alpha + phi.alpha));
             bool s1 = bracket(plo, ln);
             if (s1) plo = ln;
             bool s2 = bracket(plo, md);

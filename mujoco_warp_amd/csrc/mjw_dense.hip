@@ -8,16 +8,18 @@ namespace mjw {
 // 3 waves/SIMD (up to 168 VGPRs, 12 worlds/CU): at 4 (128 VGPRs, 16 worlds/CU, which the 9.7 KB of
 // LDS would also allow) the Euler+CG instance spilled 6-11 registers; measured humanoid dense kernel
 // 0.295 -> 0.288 ms at 3, 0.287 ms at 2
-template <int FLAGS, bool NEWTON>
+// ELL: elliptic friction cones (opt.cone = ELLIPTIC), a separate instantiation so that the pyramidal
+// kernels keep their registers
+template <int FLAGS, bool NEWTON, bool ELL>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
-  __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON>()];
+  __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON, ELL>()];
   const int b = w0 + (int)blockIdx.x;
   if (b >= d.nworld) return;
-  // d.sched set: worlds in the forward kernel's longest-first order (world_order is a permutation)
+  // d.sched set: worlds in the counter-reset kernel's longest-first order (world_order is a permutation)
   const int wid = d.sched ? d.world_order[b] : b;
   WLOG_T0();
-  dense_world<FLAGS, NEWTON>(m, d, wid, sm);
+  dense_world<FLAGS, NEWTON, ELL>(m, d, wid, sm);
   if ((FLAGS & DF_SOLVE) && d.sched && (threadIdx.x & 63) == 0) {
     // the next step's order: bucket by this step's iterations, most iterations first
     const int key = MJW_SCHED_BUCKETS - 1 - min(d.solver_niter[wid] >> 1, MJW_SCHED_BUCKETS - 1);
@@ -52,11 +54,16 @@ __global__ void __launch_bounds__(64) selftest_kernel(int which, const float* in
 template <int FLAGS>
 hipError_t launch_flags(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int w0, int count) {
   const bool newton = m->opt_solver == SOLVER_NEWTON;
-  if (newton)
-    hipLaunchKernelGGL((dense_kernel<FLAGS, true>), dim3(count), dim3(64), 0, s, *m, *d, w0);
-  else
-    hipLaunchKernelGGL((dense_kernel<FLAGS, false>), dim3(count), dim3(64), 0, s, *m, *d, w0);
-  trace_launch(s, K_DENSE + 2 * FLAGS + (newton ? 1 : 0));
+  // the cone only matters to the solve; Euler-only / factor-only launches use the pyramidal kernels
+  const bool ell = (FLAGS & DF_SOLVE) && m->opt_cone == CONE_ELLIPTIC;
+  if (ell) {
+    if (newton) hipLaunchKernelGGL((dense_kernel<FLAGS, true, true>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+    else hipLaunchKernelGGL((dense_kernel<FLAGS, false, true>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+  } else {
+    if (newton) hipLaunchKernelGGL((dense_kernel<FLAGS, true, false>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+    else hipLaunchKernelGGL((dense_kernel<FLAGS, false, false>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+  }
+  trace_launch(s, K_DENSE + 4 * FLAGS + (ell ? 2 : 0) + (newton ? 1 : 0));
   return hipGetLastError();
 }
 

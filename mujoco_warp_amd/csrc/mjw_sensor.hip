@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
     // constraint-row order (each contact at its first row), lane = body
     for (int r = 0; r < nefc; r++) {
       const int type = d.efc_type[wr + r];
-      if (type != CNSTR_CONTACT_FRICTIONLESS && type != CNSTR_CONTACT_PYRAMIDAL) continue;
+      if (type != CNSTR_CONTACT_FRICTIONLESS && type != CNSTR_CONTACT_PYRAMIDAL && type != CNSTR_CONTACT_ELLIPTIC) continue;
       const int cid = d.efc_id[wr + r];
       if (cid < 0 || cid >= d.naconmax || d.contact_efc_address[(long)cid * m.nmaxpyramid] != r) continue;
       const int id1 = m.geom_bodyid[d.contact_geom[2L * cid]], id2 = m.geom_bodyid[d.contact_geom[2L * cid + 1]];
@@ -124,6 +124,12 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
       float f[6] = {0, 0, 0, 0, 0, 0};
       if (condim == 1) {
         f[0] = d.efc_force[wr + r];
+      } else if (type == CNSTR_CONTACT_ELLIPTIC) {
+        // elliptic rows are the contact-frame force components (support.py:296-299)
+        for (int i = 0; i < condim; i++) {
+          const int a = d.contact_efc_address[(long)cid * m.nmaxpyramid + i];
+          f[i] = (a >= 0 && a < d.njmax) ? d.efc_force[wr + a] : 0.0f;
+        }
       } else {
         for (int i = 0; i < condim - 1; i++) {
           int a = 2 * i + r;

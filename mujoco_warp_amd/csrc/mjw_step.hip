@@ -1164,14 +1164,15 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       if (lane == 0) gbase = atomicAdd(d.nacon, nstage);
       gbase = __shfl(gbase, 0, 64);
       WSYNC();
-      // rows per staged contact (pyramidal: 1 or 2*(condim-1)), prefix over contacts
+      // rows per staged contact (pyramidal: 1 or 2*(condim-1); elliptic: condim), prefix over contacts
+      const bool ell = m.opt_cone == CONE_ELLIPTIC;
       int nrow = 0;
       if (lane < nstage) {
         const float* rec = s + L.con + lane * CREC;
         int condim = reinterpret_cast<const int*>(rec)[28];
         float pos = rec[0] - rec[1];
         // a contact past the global pool is dropped with its rows (collision_core.py:212-231)
-        nrow = (pos < 0.0f && gbase + lane < d.naconmax) ? (condim == 1 ? 1 : 2 * (condim - 1)) : 0;
+        nrow = (pos < 0.0f && gbase + lane < d.naconmax) ? (condim == 1 ? 1 : (ell ? condim : 2 * (condim - 1))) : 0;
         reinterpret_cast<int*>(s + L.con + lane * CREC)[31] = gbase + lane;
       }
       int rincl = wave_scan_incl(nrow);
@@ -1214,7 +1215,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         int r0 = si[L.iscratch + cc];
         float pos = rec[0] - rec[1];
         if (!(pos < 0.0f) || gbase + cc >= d.naconmax) continue;
-        int nr = condim == 1 ? 1 : 2 * (condim - 1);
+        int nr = condim == 1 ? 1 : (ell ? condim : 2 * (condim - 1));
         const int b1 = reci[21] & 0xffff, b2 = reci[21] >> 16;
         const float* cpos = rec + 2;
         const float* frame = rec + 5;
@@ -1232,7 +1233,15 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           int r = r0 + dimid;
           if (r >= njmax) break;
           float Jval = Jn;
-          if (condim > 1) {
+          if (ell && condim > 1) {
+            // elliptic (constraint.py:2151-2160): row dimid is frame row dimid applied to the relative
+            // translational (dimid < 3) or rotational jacobian
+            if (dimid > 0) {
+              const float* fr = dimid < 3 ? frame + 3 * dimid : frame + 3 * (dimid - 3);
+              const float* jd = dimid < 3 ? jdp : jdr;
+              Jval = fr[0] * jd[0] + fr[1] * jd[1] + fr[2] * jd[2];
+            }
+          } else if (condim > 1) {
             int dimid2 = dimid / 2 + 1;
             float frii = rec[14 + dimid2 - 1];
             float Ji;
@@ -1260,16 +1269,30 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         int dimid = r - si[L.iscratch + cc];
         const int body1 = reci[22] & 0xffff, body2 = reci[22] >> 16;
         float invweight = body_invweight0[2 * body1] + body_invweight0[2 * body2];
+        float Jqvel = s[L.jqvel + r];
+        float pos = rec[0] - rec[1];
+        if (ell && condim > 1) {
+          // constraint.py:2168-2195: friction rows scale invweight by impratio^-1 (fri0 / frii)^2 and have
+          // no position term (solreffriction is zero: no explicit <pair>, so solref applies)
+          float pos_aref = pos;
+          if (dimid > 0) {
+            invweight = invweight * impratio_invsqrt * impratio_invsqrt;
+            if (dimid > 1) {
+              const float fri0 = rec[14], frii = rec[14 + dimid - 1];
+              invweight *= fri0 * fri0 / (frii * frii);
+            }
+            pos_aref = 0.0f;
+          }
+          efc_row(m, d, L, s, wid, r, pos_aref, pos, invweight, rec + 19, rec + 23, rec[1], Jqvel, 0.0f, CNSTR_CONTACT_ELLIPTIC, reci[31]);
+          continue;
+        }
         if (condim > 1) {
           float fri0 = rec[14];
           invweight = invweight + fri0 * fri0 * invweight;
           invweight = invweight * 2.0f * fri0 * fri0 * impratio_invsqrt * impratio_invsqrt;
         }
-        float Jqvel = s[L.jqvel + r];
-        float pos = rec[0] - rec[1];
         int type = condim == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
         efc_row(m, d, L, s, wid, r, pos, pos, invweight, rec + 19, rec + 23, rec[1], Jqvel, 0.0f, type, reci[31]);
-        (void)dimid;
       }
       nefc += nrow_total;
       WSYNC();
@@ -2132,16 +2155,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mj
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
   WLOG_T0();
-  // longest-first world order for the dense kernel that follows (d.sched is set only for full-range
-  // forward + dense launches, run() below): this world's slot in its iteration bucket, reserved now so
-  // that the atomic's latency overlaps the stages, written at the end
-  int order_pos = -1;
-  if constexpr ((STAGES & ST_POS) != 0) {
-    if (d.sched && w.lane == 0)
-      order_pos = d.sched[2 * MJW_SCHED_BUCKETS] ? atomicAdd(d.sched + MJW_SCHED_BUCKETS + d.world_key[w.wid], 1) : w.wid;
-  }
   run_stages<STAGES, BOX>(m, d, L, w);
-  if (order_pos >= 0 && order_pos < d.nworld) d.world_order[order_pos] = w.wid;
   WLOG_END(w.wid, 0);
 }
 
@@ -2191,16 +2205,24 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
 // hipMemsetAsync: in a captured hipGraph the 4-byte memset node was observed to race the
 // forward kernel (stale counts, contacts dropped past the pool), kernel nodes stay ordered
 //
-// It also turns the dense kernel's histogram of the last step's solver-iteration buckets (sched[0, NB))
-// into bucket cursors (sched[NB, 2 NB), exclusive prefix sums) and clears it; the order is valid
-// (sched[2 NB] = 1) only when the histogram counts every world exactly once, i.e. when the last dense
-// pass covered all worlds with the order enabled; otherwise the next step runs in identity order.
-__global__ void reset_counters_kernel(int* nacon, int* ncollision, int* sched, int nworld) {
+// It also builds the dense kernel's longest-first world order for this step: the dense kernel of the
+// previous step histogrammed each world's solver-iteration bucket (sched[0, NB), world_key); a counting
+// sort over the buckets in this one workgroup (LDS cursors) writes world_order, a permutation of the
+// worlds with the most iterations first.  The order is built only when the histogram counts every world
+// exactly once (the last dense pass covered all worlds with the order enabled); otherwise world_order is
+// the identity.  Measured: the same scatter done with global atomics inside the forward kernel serialised
+// on the 32 bucket counters and cost the forward kernel what it saved the dense kernel.
+constexpr int RESET_THREADS = 1024;
+__global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* nacon, int* ncollision, int* sched, int* world_order,
+                                                                       const int* world_key, int nworld) {
   const int t = threadIdx.x;
   if (t == 0) { nacon[0] = 0; ncollision[0] = 0; }
-  if (sched) {
-    constexpr int NB = MJW_SCHED_BUCKETS;
-    static_assert(NB <= 64, "one wave scans the buckets");
+  if (!sched) return;
+  constexpr int NB = MJW_SCHED_BUCKETS;
+  static_assert(NB <= 64, "one wave scans the buckets");
+  __shared__ int cursor[NB];
+  __shared__ int valid;
+  if (t < 64) {
     const int h = t < NB ? sched[t] : 0;
     int x = h;
 #pragma unroll
@@ -2210,10 +2232,20 @@ __global__ void reset_counters_kernel(int* nacon, int* ncollision, int* sched, i
     }
     const int total = __shfl(x, 63);
     if (t < NB) {
-      sched[NB + t] = x - h;
+      cursor[t] = x - h;
       sched[t] = 0;
     }
-    if (t == 0) sched[2 * NB] = total == nworld ? 1 : 0;
+    if (t == 0) valid = total == nworld;
+  }
+  __syncthreads();
+  if (valid) {
+    for (int w = t; w < nworld; w += RESET_THREADS) {
+      const int k = min(max(world_key[w], 0), NB - 1);
+      const int pos = atomicAdd(&cursor[k], 1);
+      if (pos < nworld) world_order[pos] = w;
+    }
+  } else {
+    for (int w = t; w < nworld; w += RESET_THREADS) world_order[w] = w;
   }
 }
 
@@ -2283,8 +2315,10 @@ int set_err(hipError_t e, const char* where) {
   return (int)e;
 }
 
-hipError_t reset_counters(const mjw_data_t* d, hipStream_t s) {
-  hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(64), 0, s, d->nacon, d->ncollision, d->sched, d->nworld);
+hipError_t reset_counters(const mjw_data_t* d, hipStream_t s, bool order = false) {
+  // the order is built only for the dense path's full forward + solve (run() passes order = true)
+  hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(order ? mjw::RESET_THREADS : 64), 0, s, d->nacon, d->ncollision,
+                     order ? d->sched : nullptr, d->world_order, d->world_key, d->nworld);
   mjw::trace_launch(s, mjw::K_RESET);
   return hipGetLastError();
 }
@@ -2365,25 +2399,31 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   if (m->nv > 64 || m->nbody > 4096) { g_err = std::string(name) + ": model too large for the dense world-per-wave path"; return -2; }
   hipStream_t s = (hipStream_t)stream;
   int rc = 0;
-  if (stages & ST_POS) {
-    rc = set_err(reset_counters(d, s), name);
-    if (rc) return rc;
-  }
   // sensors (all stages, one kernel after the solver and before the integrator): only the fused
   // forward / step (the stage entry points, like the reference's fwd_* functions, compute none)
   const bool full = (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE)) == (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE);
   const bool acc_sensors = full && m->nsensor > 0 && !(m->opt_disableflags & DSBL_SENSOR);
+  // longest-first world order of the dense kernels (the counter-reset kernel sorts the worlds by the
+  // iteration bucket the previous step's solving dense kernel recorded; the dense kernels read
+  // world_order; the solving one records this step's buckets): full forward + solve on the dense path
+  // only; every other launch sees sched = nullptr and runs worlds in identity order.
+  // MJW_WORLD_ORDER=0 disables it (A/B measurements).
+  static const bool order_on = [] {
+    const char* e = getenv("MJW_WORLD_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  const bool order = order_on && full && d->sched && dense_ok(m, d);
+  if (m->opt_cone == CONE_ELLIPTIC && (stages & ST_SOLVE) && !dense_ok(m, d)) {
+    g_err = std::string(name) + ": elliptic cones need the register-resident dense solve (nv <= 32, njmax <= 64)";
+    return -5;
+  }
+  if (stages & ST_POS) {
+    rc = set_err(reset_counters(d, s, order), name);
+    if (rc) return rc;
+  }
   if (dense_ok(m, d)) {
-    // longest-first order (forward kernel writes world_order, the dense kernels read it, the solving
-    // dense kernel histograms the iteration buckets for the next step): full forward + solve only;
-    // every other launch sees sched = nullptr and runs worlds in identity order.  MJW_WORLD_ORDER=0
-    // disables it (A/B measurements).
-    static const bool order_on = [] {
-      const char* e = getenv("MJW_WORLD_ORDER");
-      return !(e && e[0] == '0');
-    }();
     mjw_data_t dv = *d;
-    if (!(order_on && full && d->sched)) dv.sched = nullptr;
+    if (!order) dv.sched = nullptr;
     d = &dv;
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel, for the
     // world range [w0, w0 + cnt) on stream st; `timed` records the optional bench events.
@@ -2518,8 +2558,9 @@ const char* mjw_kernel_name(int id) {
                                "mjw::sp::solve_kernel<0>", "mjw::sp::solve_kernel<1>", "mjw::sp::solve_kernel<2>", "mjw::sp::euler_kernel"};
   static thread_local char buf[64];
   if (id >= 0 && id < (int)(sizeof(misc) / sizeof(misc[0]))) return misc[id];
-  if (id >= mjw::K_DENSE && id < mjw::K_DENSE + 16) {
-    snprintf(buf, sizeof(buf), "mjw::dense_kernel<%d, %s>", (id - mjw::K_DENSE) >> 1, (id & 1) ? "true" : "false");
+  if (id >= mjw::K_DENSE && id < mjw::K_DENSE + 32) {
+    const int k = id - mjw::K_DENSE;
+    snprintf(buf, sizeof(buf), "mjw::dense_kernel<%d, %s, %s>", k >> 2, (k & 1) ? "true" : "false", (k & 2) ? "true" : "false");
     return buf;
   }
   if (id >= mjw::K_FWD && id < mjw::K_END) {

@@ -110,8 +110,8 @@ def put_model(mjm, device=None) -> types.Model:
       raise NotImplementedError(f"geom type {types.GeomType(int(g)).name} not supported.")
   if mjm.opt.integrator not in (types.IntegratorType.EULER, types.IntegratorType.RK4, types.IntegratorType.IMPLICITFAST):
     raise NotImplementedError(f"{types.IntegratorType(mjm.opt.integrator).name} is unsupported.")
-  if mjm.opt.cone != types.ConeType.PYRAMIDAL:
-    raise NotImplementedError("ELLIPTIC is unsupported.")
+  if mjm.opt.cone not in (types.ConeType.PYRAMIDAL, types.ConeType.ELLIPTIC):
+    raise NotImplementedError(f"cone {int(mjm.opt.cone)} is unsupported.")
   if mjm.opt.solver not in (types.SolverType.CG, types.SolverType.NEWTON):
     raise NotImplementedError(f"{types.SolverType(mjm.opt.solver).name} is unsupported.")
   if getattr(mjm.opt, "noslip_iterations", 0) > 0:
@@ -123,6 +123,8 @@ def put_model(mjm, device=None) -> types.Model:
     # the workgroup-per-world sparse / flex pipeline (csrc/mjw_sparse.hip) covers this subset
     if mjm.opt.solver != types.SolverType.CG:
       raise NotImplementedError("sparse / flex models: only the CG solver is supported by this build yet.")
+    if mjm.opt.cone != types.ConeType.PYRAMIDAL:
+      raise NotImplementedError("sparse / flex models: elliptic cones are not supported by this build yet.")
     if mjm.opt.integrator != types.IntegratorType.EULER:
       raise NotImplementedError("sparse / flex models: only the Euler integrator is supported by this build yet.")
     if getattr(mjm, "nsensor", 0):

@@ -83,9 +83,8 @@ def set_state(m: Model, d: Data, state: torch.Tensor, sig: int, active: Optional
 
 
 def contact_force(m: Model, d: Data, contact_ids: torch.Tensor, to_world_frame: bool, force: torch.Tensor):
-  """6D force:torque of contacts (support.py:241-351), pyramidal decoding, optional world frame."""
-  if m.opt.cone != ConeType.PYRAMIDAL:
-    raise NotImplementedError("elliptic cones are not supported by this build")
+  """6D force:torque of contacts (support.py:241-351): pyramidal decoding, or the elliptic rows directly
+  (support.py:296-299); optional world frame."""
   ids = contact_ids.to(torch.long)
   nacon = int(d.nacon[0])
   valid = (ids >= 0) & (ids < min(nacon, d.naconmax))
@@ -102,6 +101,17 @@ def contact_force(m: Model, d: Data, contact_ids: torch.Tensor, to_world_frame: 
     inb = ok & (a < d.njmax)
     return torch.where(inb, efc[wid, a.clamp(0, d.njmax - 1)], torch.zeros_like(out[:, 0]))
 
+  if m.opt.cone != ConeType.PYRAMIDAL:
+    for i in range(int(m.nmaxcondim)):
+      a = d.contact.efc_address[ids_c, i].to(torch.long) if i < d.contact.efc_address.shape[1] else adr
+      use = ok & (i < dim) & (a >= 0)
+      out[:, i] = torch.where(use, f_at(a.clamp(min=0)), out[:, i])
+    out[~ok] = 0
+    if to_world_frame:
+      frame = d.contact.frame[ids_c]
+      out = torch.cat([torch.einsum("ni,nij->nj", out[:, :3], frame), torch.einsum("ni,nij->nj", out[:, 3:], frame)], dim=1)
+    force[:] = out
+    return
   out[:, 0] = torch.where(dim == 1, f_at(adr), out[:, 0])
   for i in range(int(m.nmaxcondim) - 1 if m.nmaxcondim > 1 else 0):
     use = ok & (dim > 1) & (i < dim - 1)

@@ -26,8 +26,10 @@ enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_
 enum { DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16,
        DSBL_SPRING = 32, DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512,
        DSBL_FILTERPARENT = 1024, DSBL_ACTUATION = 2048, DSBL_REFSAFE = 4096, DSBL_SENSOR = 8192, DSBL_EULERDAMP = 1 << 15 };
-enum { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6 };
-enum { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3 };
+enum { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6,
+       CNSTR_CONTACT_ELLIPTIC = 7 };
+enum { CONE_PYRAMIDAL = 0, CONE_ELLIPTIC = 1 };
+enum { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3, STATE_CONE = 4 };
 enum { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
 enum { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICITFAST = 3 };
 enum { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
@@ -2097,12 +2099,13 @@ static void make_constraint(const orc_model* m, orc_data* d) {
               Jv * d->qvel[da], 0, CNSTR_LIMIT_JOINT, j);
     }
   }
-  /* contact pyramidal constraint.py:1668-1936 */
+  /* contact pyramidal constraint.py:1668-1936, elliptic :1940-2200 */
   if (!(m->opt_disableflags & DSBL_CONTACT)) {
     int ncon = *d->ncon < d->nconmax ? *d->ncon : d->nconmax;
     for (int c = 0; c < ncon; c++) {
       int condim = d->con_dim[c];
-      int nrow = condim == 1 ? 1 : 2 * (condim - 1);
+      int elliptic = m->opt_cone == CONE_ELLIPTIC && condim > 1;
+      int nrow = condim == 1 ? 1 : (elliptic ? condim : 2 * (condim - 1));
       real includemargin = d->con_includemargin[c];
       real pos = d->con_dist[c] - includemargin;
       if (!(pos < 0)) continue;
@@ -2118,6 +2121,37 @@ static void make_constraint(const orc_model* m, orc_data* d) {
         int efcid = (*d->nefc)++;
         if (efcid >= njmax) { d->con_efc_address[10 * c + dimid] = -1; continue; }
         d->con_efc_address[10 * c + dimid] = efcid;
+        if (elliptic) {
+          /* constraint.py:2107-2195: row dimid projects the relative jacobian on frame row dimid
+           * (translational for dimid < 3, rotational after); friction rows scale invweight by
+           * impratio^-1 and (fri0 / frii)^2, use solreffriction when set, and have no position term */
+          real invw = iw_base, pos_aref = pos;
+          const real* sr = d->con_solref + 2 * c;
+          if (dimid > 0) {
+            const real* srf = d->con_solreffriction + 2 * c;
+            if (srf[0] != 0 || srf[1] != 0) sr = srf;
+            invw = invw * m->opt_impratio_invsqrt * m->opt_impratio_invsqrt;
+            if (dimid > 1) {
+              real fri0 = d->con_friction[5 * c], frii = d->con_friction[5 * c + dimid - 1];
+              invw *= fri0 * fri0 / (frii * frii);
+            }
+            pos_aref = 0;
+          }
+          real* J = d->efc_J + (size_t)efcid * nv;
+          real Jqvel = 0;
+          for (int i = nv - 1; i >= 0; i--) {
+            real j1p[3], j1r[3], j2p[3], j2r[3];
+            jac_dof(m, d, cpos, w1, i, j1p, j1r);
+            jac_dof(m, d, cpos, w2, i, j2p, j2r);
+            real Jval = 0;
+            for (int x = 0; x < 3; x++)
+              Jval += dimid < 3 ? frame[3 * dimid + x] * (j2p[x] - j1p[x]) : frame[3 * (dimid - 3) + x] * (j2r[x] - j1r[x]);
+            J[i] = Jval;
+            Jqvel += Jval * d->qvel[i];
+          }
+          efc_row(m, d, efcid, pos_aref, pos, invw, sr, d->con_solimp + 5 * c, includemargin, Jqvel, 0, CNSTR_CONTACT_ELLIPTIC, c);
+          continue;
+        }
         real invweight = iw_base;
         real frii = 0;
         int dimid2 = dimid / 2 + 1;
@@ -2277,6 +2311,7 @@ static void fwd_acceleration(const orc_model* m, orc_data* d) {
  * ============================================================================================= */
 typedef struct {
   real* Jaref; real* jv;
+  real* quad;  /* 9 per row: the elliptic primary row's quad, quad1, quad2 (solver.py:1550-1611) */
   real* grad; real* Mgrad; real* search; real* mv; real* prev_grad; real* prev_Mgrad;
   real* H; real* HL;
   real cost, prev_cost, gauss, search_dot, grad_dot;
@@ -2308,9 +2343,38 @@ static void update_constraint(const orc_model* m, orc_data* d, solver_ctx* c) {
       if (Jaref <= -rf) { d->efc_force[r] = f; state = STATE_LINEARNEG; c->cost += -f * ((real)0.5 * rf + Jaref); }
       else if (Jaref >= rf) { d->efc_force[r] = -f; state = STATE_LINEARPOS; c->cost += -f * ((real)0.5 * rf - Jaref); }
       else { d->efc_force[r] = -D * Jaref; state = STATE_QUADRATIC; c->cost += (real)0.5 * D * Jaref * Jaref; }
-    } else {
+    } else if (d->efc_type[r] != CNSTR_CONTACT_ELLIPTIC) {
       if (Jaref >= 0) { d->efc_force[r] = 0; state = STATE_SATISFIED; }
       else { d->efc_force[r] = -D * Jaref; state = STATE_QUADRATIC; c->cost += (real)0.5 * D * Jaref * Jaref; }
+    } else {
+      /* elliptic friction cone, solver.py:1886-1942 */
+      int con = d->efc_id[r], dim = d->con_dim[con];
+      const real* fr = d->con_friction + 5 * con;
+      real mu = fr[0] * m->opt_impratio_invsqrt;
+      int r0 = d->con_efc_address[10 * con];
+      real N = c->Jaref[r0] * mu, uf = 0, TT = 0;
+      int cut = r0 < 0;
+      for (int j = 1; j < dim && !cut; j++) {
+        int rj = d->con_efc_address[10 * con + j];
+        if (rj < 0) { cut = 1; break; }  /* rows past njmax: the reference leaves the row untouched */
+        real uj = c->Jaref[rj] * fr[j - 1];
+        TT += uj * uj;
+        if (rj == r) uf = uj * fr[j - 1];
+      }
+      if (cut) { d->efc_force[r] = 0; d->efc_state[r] = STATE_SATISFIED; continue; }
+      real T = TT <= 0 ? 0 : sqrt(TT);
+      if (N >= mu * T || (T <= 0 && N >= 0)) {
+        d->efc_force[r] = 0; state = STATE_SATISFIED;
+      } else if (mu * N + T <= 0 || (T <= 0 && N < 0)) {
+        d->efc_force[r] = -D * Jaref; state = STATE_QUADRATIC; c->cost += (real)0.5 * D * Jaref * Jaref;
+      } else {
+        real dm = safe_div(d->efc_D[r0], mu * mu * (1 + mu * mu));
+        real nmt = N - mu * T;
+        real force = -dm * nmt * mu;
+        if (r == r0) { d->efc_force[r] = force; c->cost += (real)0.5 * dm * nmt * nmt; }
+        else d->efc_force[r] = -safe_div(force, T) * uf;
+        state = STATE_CONE;
+      }
     }
     d->efc_state[r] = state;
   }
@@ -2347,15 +2411,101 @@ static void update_gradient(const orc_model* m, orc_data* d, solver_ctx* c) {
         for (int j = 0; j < nv; j++) c->H[i * nv + j] += D * J[i] * J[j];
       }
     }
+    /* elliptic cones in the CONE state: H += J_c' C J_c with the cone Hessian C of the contact
+     * (update_gradient_JTCJ, solver.py:2430-2585) */
+    for (int r0 = 0; r0 < nefc; r0++) {
+      if (d->efc_type[r0] != CNSTR_CONTACT_ELLIPTIC || d->efc_state[r0] != STATE_CONE) continue;
+      int con = d->efc_id[r0];
+      if (d->con_efc_address[10 * con] != r0) continue;
+      int dim = d->con_dim[con];
+      const real* fr = d->con_friction + 5 * con;
+      real mu = fr[0] * m->opt_impratio_invsqrt, mu2 = mu * mu;
+      real dm = safe_div(d->efc_D[r0], mu2 * (1 + mu2));
+      if (dm == 0) continue;
+      real u[6], fri[6];
+      int rows[6];
+      u[0] = c->Jaref[r0] * mu;
+      fri[0] = mu;
+      rows[0] = r0;
+      real tt = 0;
+      int cut = 0;
+      for (int j = 1; j < dim; j++) {
+        rows[j] = d->con_efc_address[10 * con + j];
+        if (rows[j] < 0) { cut = 1; break; }
+        u[j] = c->Jaref[rows[j]] * fr[j - 1];
+        fri[j] = fr[j - 1];
+        tt += u[j] * u[j];
+      }
+      if (cut) continue;
+      real t = tt <= 0 ? 0 : sqrt(tt);
+      t = maxr(t, MINVAL);
+      real ttt = maxr(t * t * t, MINVAL);
+      real mu_over_t = safe_div(mu, t), mu_n_over_ttt = mu * safe_div(u[0], ttt), diag = mu2 - mu * safe_div(u[0], t);
+      for (int a = 0; a < dim; a++) {
+        for (int b = 0; b < dim; b++) {
+          real h;
+          if (a == 0 && b == 0) h = 1;
+          else if (a == 0) h = -mu_over_t * u[b];
+          else if (b == 0) h = -mu_over_t * u[a];
+          else h = mu_n_over_ttt * u[a] * u[b] + (a == b ? diag : 0);
+          h *= dm * fri[a] * fri[b];
+          if (h == 0) continue;
+          const real* Ja = d->efc_J + (size_t)rows[a] * nv;
+          const real* Jb = d->efc_J + (size_t)rows[b] * nv;
+          for (int i = 0; i < nv; i++) {
+            if (Ja[i] == 0) continue;
+            for (int j = 0; j < nv; j++) c->H[i * nv + j] += h * Ja[i] * Jb[j];
+          }
+        }
+      }
+    }
     cholesky(nv, c->H, c->HL);
     cholesky_solve(nv, c->HL, c->grad, c->Mgrad);
   }
 }
 
-/* per-row (cost, grad, hess) for pyramidal cones, solver.py:570-598 */
-static void eval_row(const orc_data* d, const solver_ctx* c, int r, int ne, int nf, real alpha, real* out) {
+/* elliptic cone (cost, grad, hess) of one contact at alpha, solver.py:263-323 (_eval_elliptic) */
+static void eval_elliptic(real mu, const real* quad, const real* quad1, const real* quad2, real alpha, real* out) {
+  real u0 = quad1[0], v0 = quad1[1], uu = quad1[2], uv = quad2[0], vv = quad2[1], dm = quad2[2];
+  real N = u0 + alpha * v0;
+  real Tsqr = uu + alpha * (2 * uv + alpha * vv);
+  int bottom = 0;
+  if (Tsqr <= 0) {
+    if (N < 0) bottom = 1;
+    else return;
+  } else {
+    real T = sqrt(Tsqr);
+    if (N >= mu * T) return;
+    if (mu * N + T <= 0) bottom = 1;
+    else {
+      real N1 = v0, T1 = (uv + alpha * vv) / T;
+      real T2 = vv / T - (uv + alpha * vv) * T1 / (T * T);
+      out[0] += (real)0.5 * dm * (N - mu * T) * (N - mu * T);
+      out[1] += dm * (N - mu * T) * (N1 - mu * T1);
+      out[2] += dm * ((N1 - mu * T1) * (N1 - mu * T1) + (N - mu * T) * (-mu * T2));
+      return;
+    }
+  }
+  if (bottom) {
+    real aq2 = alpha * quad[2];
+    out[0] += alpha * aq2 + alpha * quad[1] + quad[0];
+    out[1] += 2 * aq2 + quad[1];
+    out[2] += 2 * quad[2];
+  }
+}
+
+/* per-row (cost, grad, hess), solver.py:570-640; an elliptic contact is evaluated once, at its first
+ * row, from the quad coefficients linesearch() prepared */
+static void eval_row(const orc_model* m, const orc_data* d, const solver_ctx* c, int r, int ne, int nf, real alpha, real* out) {
   real D = d->efc_D[r], jaref = c->Jaref[r], jv = c->jv[r];
   real x = jaref + alpha * jv;
+  if (r >= ne + nf && d->efc_type[r] == CNSTR_CONTACT_ELLIPTIC) {
+    int con = d->efc_id[r];
+    if (d->con_efc_address[10 * con] != r) return;
+    const real* q = c->quad + 9 * (size_t)r;
+    eval_elliptic(d->con_friction[5 * con] * m->opt_impratio_invsqrt, q, q + 3, q + 6, alpha, out);
+    return;
+  }
   if (r >= ne + nf) {
     if (x < 0) { real jvD = jv * D; out[0] += (real)0.5 * D * x * x; out[1] += jvD * x; out[2] += jv * jvD; }
     return;
@@ -2384,11 +2534,38 @@ static void linesearch(const orc_model* m, orc_data* d, solver_ctx* c) {
     for (int i = 0; i < nv; i++) s += J[i] * c->search[i];
     c->jv[r] = s;
   }
+  /* elliptic contacts: quad / quad1 / quad2 at the first row (solver.py:1550-1611) */
+  if (m->opt_cone == CONE_ELLIPTIC) {
+    for (int r = ne + nf; r < nefc; r++) {
+      if (d->efc_type[r] != CNSTR_CONTACT_ELLIPTIC) continue;
+      int con = d->efc_id[r];
+      if (d->con_efc_address[10 * con] != r) continue;
+      int dim = d->con_dim[con];
+      const real* fr = d->con_friction + 5 * con;
+      real mu = fr[0] * m->opt_impratio_invsqrt;
+      real Jaref = c->Jaref[r], jv = c->jv[r], D = d->efc_D[r];
+      real* q = c->quad + 9 * (size_t)r;
+      q[0] = (real)0.5 * Jaref * Jaref * D; q[1] = jv * Jaref * D; q[2] = (real)0.5 * jv * jv * D;
+      real uu = 0, uv = 0, vv = 0;
+      int cut = 0;
+      for (int j = 1; j < dim; j++) {
+        int rj = d->con_efc_address[10 * con + j];
+        if (rj < 0) { cut = 1; break; }
+        real jvj = c->jv[rj], jarefj = c->Jaref[rj], dj = d->efc_D[rj], DJj = dj * jarefj;
+        q[0] += (real)0.5 * jarefj * DJj; q[1] += jvj * DJj; q[2] += (real)0.5 * jvj * dj * jvj;
+        real uj = jarefj * fr[j - 1], vj = jvj * fr[j - 1];
+        uu += uj * uj; uv += uj * vj; vv += vj * vj;
+      }
+      q[3] = Jaref * mu; q[4] = jv * mu; q[5] = uu;
+      q[6] = uv; q[7] = vv; q[8] = D / (mu * mu * (1 + mu * mu));
+      if (cut) memset(q, 0, 9 * sizeof(real));  /* a contact cut by njmax contributes nothing */
+    }
+  }
   real snorm = sqrt(c->search_dot);
   real scale = m->stat_meaninertia * (real)nv;
   real gtol = maxr(m->opt_tolerance * m->opt_ls_tolerance * snorm * scale, (real)1e-6);
   real p0s[3] = {0, 0, 0};
-  for (int r = 0; r < nefc; r++) eval_row(d, c, r, ne, nf, 0, p0s);
+  for (int r = 0; r < nefc; r++) eval_row(m, d, c, r, ne, nf, 0, p0s);
   real qg1 = 0, qg2 = 0;
   for (int i = 0; i < nv; i++) {
     qg1 += c->search[i] * (d->efc_Ma[i] - d->qfrc_smooth[i]);
@@ -2400,7 +2577,7 @@ static void linesearch(const orc_model* m, orc_data* d, solver_ctx* c) {
   real lo_alpha_in = -safe_div(p0[1], p0[2]);
   real lo_in[3];
   EVAL_GAUSS(lo_in, lo_alpha_in);
-  for (int r = 0; r < nefc; r++) eval_row(d, c, r, ne, nf, lo_alpha_in, lo_in);
+  for (int r = 0; r < nefc; r++) eval_row(m, d, c, r, ne, nf, lo_alpha_in, lo_in);
   real alpha;
   int initial_converged = fabs(lo_in[1]) < gtol && lo_in[0] < p0[0];
   if (!initial_converged) {
@@ -2418,9 +2595,9 @@ static void linesearch(const orc_model* m, orc_data* d, solver_ctx* c) {
       EVAL_GAUSS(hi_next, hi_next_alpha);
       EVAL_GAUSS(mid, mid_alpha);
       for (int r = 0; r < nefc; r++) {
-        eval_row(d, c, r, ne, nf, lo_next_alpha, lo_next);
-        eval_row(d, c, r, ne, nf, hi_next_alpha, hi_next);
-        eval_row(d, c, r, ne, nf, mid_alpha, mid);
+        eval_row(m, d, c, r, ne, nf, lo_next_alpha, lo_next);
+        eval_row(m, d, c, r, ne, nf, hi_next_alpha, hi_next);
+        eval_row(m, d, c, r, ne, nf, mid_alpha, mid);
       }
       int s1 = in_bracket(lo, lo_next);
       if (s1) { memcpy(lo, lo_next, sizeof(lo)); lo_alpha = lo_next_alpha; }
@@ -2459,9 +2636,9 @@ static void solve(const orc_model* m, orc_data* d) {
     *d->solver_niter = 0;
     return;
   }
-  real* buf = (real*)calloc((size_t)2 * njmax + 8 * (size_t)nv + 2 * (size_t)nv * nv, sizeof(real));
+  real* buf = (real*)calloc((size_t)11 * njmax + 8 * (size_t)nv + 2 * (size_t)nv * nv, sizeof(real));
   solver_ctx c;
-  c.Jaref = buf; c.jv = buf + njmax;
+  c.Jaref = buf; c.jv = buf + njmax; c.quad = buf + 2 * (size_t)nv * nv + 8 * (size_t)nv + 2 * njmax;
   c.grad = buf + 2 * njmax; c.Mgrad = c.grad + nv; c.search = c.Mgrad + nv; c.mv = c.search + nv;
   c.prev_grad = c.mv + nv; c.prev_Mgrad = c.prev_grad + nv; c.H = c.prev_Mgrad + 2 * nv; c.HL = c.H + nv * nv;
   if (!(m->opt_disableflags & DSBL_WARMSTART)) memcpy(d->qacc, d->qacc_warmstart, nv * sizeof(real));
@@ -2828,13 +3005,18 @@ static void sensor_vel(const orc_model* m, orc_data* d) {
   }
 }
 
-/* support.py:241-308 contact force (pyramidal decode, to world frame) */
-static void contact_force_world(const orc_data* d, int c, real* f6) {
+/* support.py:241-308 contact force (pyramidal decode or the elliptic rows directly, to world frame) */
+static void contact_force_world(const orc_model* m, const orc_data* d, int c, real* f6) {
   real f[6] = {0, 0, 0, 0, 0, 0};
   int condim = d->con_dim[c];
   int adr = d->con_efc_address[10 * c];
   if (adr >= 0) {
-    if (condim == 1) f[0] = d->efc_force[adr];
+    if (m->opt_cone == CONE_ELLIPTIC) {
+      for (int i = 0; i < condim; i++) {
+        int a = d->con_efc_address[10 * c + i];
+        if (a >= 0 && a < d->njmax) f[i] = d->efc_force[a];
+      }
+    } else if (condim == 1) f[0] = d->efc_force[adr];
     else {
       for (int i = 0; i < condim - 1; i++) {
         int a = 2 * i + adr;
@@ -2897,7 +3079,7 @@ static void rne_postconstraint(const orc_model* m, orc_data* d) {
     int id1 = m->geom_bodyid[d->con_geom[2 * c]], id2 = m->geom_bodyid[d->con_geom[2 * c + 1]];
     if (id1 == 0 && id2 == 0) continue;
     real f6[6];
-    contact_force_world(d, c, f6);
+    contact_force_world(m, d, c, f6);
     const real* pos = d->con_pos + 3 * c;
     for (int k = 0; k < 2; k++) {
       int b = k == 0 ? id1 : id2;

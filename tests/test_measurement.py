@@ -59,11 +59,11 @@ def test_roofline_names_the_dominant_group():
   import bench
 
   # humanoid-like trace: dense kernel slower than the forward kernel
-  dur = [[("mjw::reset_counters_kernel", 0.004), ("mjw::mjw_kernel<79, false>", 0.280), ("mjw::dense_kernel<7, false>", 0.290)]] * 3
+  dur = [[("mjw::reset_counters_kernel", 0.004), ("mjw::mjw_kernel<79, false>", 0.280), ("mjw::dense_kernel<7, false, false>", 0.290)]] * 3
   tab = bench.kernel_table(dur, False)
-  pmc = {"mjw::dense_kernel<7, false>": {"bytes_per_launch": 95e6}, "mjw::mjw_kernel<79, false>": {"bytes_per_launch": 157e6}}
+  pmc = {"mjw::dense_kernel<7, false, false>": {"bytes_per_launch": 95e6}, "mjw::mjw_kernel<79, false>": {"bytes_per_launch": 157e6}}
   r = bench.roofline_record(tab, {"forward": 18170.0, "dense": 3930.0}, 8192, pmc, "pmc_x.json")
-  assert r["kernel"] == "mjw::dense_kernel<7, false>" and r["group"] == "dense"
+  assert r["kernel"] == "mjw::dense_kernel<7, false, false>" and r["group"] == "dense"
   assert abs(r["kernel_ms"] - 0.290) < 1e-12
   assert abs(r["achieved"] - 3930.0 * 8192 / 0.290e-3 / 1e9) < 1e-9
   assert r["traffic"] == 95e6 and abs(r["groups"]["dense"]["traffic_over_alg"] - 95e6 / (3930.0 * 8192)) < 1e-12

@@ -86,7 +86,7 @@ def rows_of(mjm, d, od, w, sparse, njmax):
   """(gpu row ids, oracle row ids, dense gpu J rows): identical order on the dense path; through the
   matched contacts on the sparse path (tests/test_cloth.py)."""
   nv = mjm.nv
-  n = int(od.nefc[w, 0])
+  n = min(int(od.nefc[w, 0]), njmax)
   if not sparse:
     return np.arange(n), np.arange(n), np_(d.efc.J[w, :n, :nv])
   from tests.cloth_common import dense_J, gpu_contacts, oracle_contacts
@@ -184,7 +184,7 @@ def report(name):
   torch.cuda.synchronize()
   ratio, qn = 0.0, 0.0
   for w in range(nworld):
-    n = int(od.nefc[w, 0])
+    n = min(int(od.nefc[w, 0]), njmax)
     Mg, Mo = dense_M(mjm, d, od, w)
     J = od.efc_J[w].reshape(njmax, nv)[:n]
     args = (J, od.efc_D[w, :n], od.efc_aref[w, :n], od.efc_type[w, :n], Mo, od.qacc_smooth[w])

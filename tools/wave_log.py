@@ -1,4 +1,5 @@
-"""Per-wave lifetimes of the humanoid step's two kernels (profile build, -DMJW_PROFILE).
+"""Per-wave lifetimes of the humanoid step's two kernels (wave-log build, -DMJW_WAVELOG: no other
+instrumentation, so the kernels keep their timing).
 
 Each world's wave logs {start, end} s_memrealtime (100 MHz, chip-wide), its HW_ID / XCC_ID and, for the
 dense kernel, its CG iterations (mjw_common.h WLOG_*).  For the last of `nsteps` steps this prints, per
@@ -17,11 +18,11 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-PROF = os.path.join(ROOT, "mujoco_warp_amd", "libmjw_amd_prof.so")
+PROF = os.path.join(ROOT, "mujoco_warp_amd", "libmjw_amd_wlog.so")
 if not os.path.exists(PROF):
   from mujoco_warp_amd import build
 
-  build.build(out=PROF, defines=("MJW_PROFILE",))
+  build.build(out=PROF, defines=("MJW_WAVELOG",))
 os.environ["MJW_LIB_PATH"] = PROF
 
 import torch  # noqa: E402
