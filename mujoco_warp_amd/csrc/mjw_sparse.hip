@@ -150,7 +150,7 @@ __device__ __forceinline__ int block_scan(int v, int& total, Smem& sm) {
   __syncthreads();
   int off = 0;
   total = 0;
-  for (int w = 0; w < NWAVE; w++) {
+  for (int w = 0; w < (nthr() >> 6); w++) {  // every wave of the block (1024-thread solve blocks too)
     if (w < wv) off += sm.iscan[w];
     total += sm.iscan[w];
   }
@@ -1071,7 +1071,7 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
       __syncthreads();
       if (tid() < 6) {
         float r = sm.red[0][tid()];
-        for (int w = 1; w < NWAVE; w++) r = fminf(r, sm.red[w][tid()]);
+        for (int w = 1; w < (nthr() >> 6); w++) r = fminf(r, sm.red[w][tid()]);
         sm.fbox[f][tid()] = tid() < 3 ? r : -r;
       }
       __syncthreads();

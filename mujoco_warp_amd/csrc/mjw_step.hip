@@ -2145,8 +2145,13 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
 // 4 waves per SIMD (<= 128 VGPRs): with the direct-mode LDS layout (9.8 KB per humanoid world)
 // this is 16 worlds per CU; the collision narrowphase spills ~40 registers to scratch for it
 // (measured: forward kernel 0.326 -> 0.303 ms at nworld 8192 against the unconstrained 160 VGPRs)
+// The cap applies to the direct-mode (ST_NOFACTOR) instantiations the dense path launches and to the
+// single-stage ones; the generic kernels that factor and solve in-kernel (nv 33-64 or njmax > 64) keep
+// their registers (at the cap they spilled 80 B/lane).
+template <int STAGES>
+constexpr int fwd_waves_per_eu() { return ((STAGES & ST_SOLVE) && !(STAGES & ST_NOFACTOR)) ? 1 : 4; }
 template <int STAGES, bool BOX = true>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu<STAGES>()))) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   WS w;
   w.s = smem;

@@ -1924,8 +1924,12 @@ def set_const(m: MjModel):
 
 
 def _hull_faces(v):
-  """Outward-oriented triangles of the convex hull of `v` (inline meshes without faces)."""
-  from scipy.spatial import ConvexHull
+  """Outward-oriented triangles of the convex hull of `v` (inline meshes without faces).  Needs scipy
+  (an optional dependency of the compiler, used only for this case)."""
+  try:
+    from scipy.spatial import ConvexHull
+  except ImportError as e:  # pragma: no cover - scipy is installed in this image
+    raise ImportError("an inline <mesh vertex=...> without faces needs scipy.spatial.ConvexHull") from e
 
   h = ConvexHull(v)
   c = v.mean(axis=0)

@@ -217,3 +217,26 @@ def test_gpu_mesh_contacts_and_rollout_match_oracle(tmp_path):
     od2.step()
   torch.cuda.synchronize()
   assert_close("qpos", np_(d2.qpos), od2.qpos, rtol=5e-3, atol=5e-3)
+
+
+def test_inline_vertex_only_mesh_hull():
+  """An inline <mesh vertex=...> without faces compiles to its convex hull (mjcf._hull_faces): a cube's
+  8 corners give 12 outward triangles and the box's volume-integral mass; a tetrahedron 4 faces and
+  volume 1/6."""
+  from mujoco_warp_amd import mjcf
+
+  cube = " ".join(f"{x} {y} {z}" for x in (-0.5, 0.5) for y in (-0.5, 0.5) for z in (-0.5, 0.5))
+  tet = "0 0 0 1 0 0 0 1 0 0 0 1"
+  xml = f"""<mujoco><asset><mesh name="c" vertex="{cube}"/><mesh name="t" vertex="{tet}"/></asset><worldbody>
+<body><freejoint/><geom type="mesh" mesh="c" density="1000"/></body>
+<body pos="2 0 0"><freejoint/><geom type="mesh" mesh="t" density="600"/></body></worldbody></mujoco>"""
+  m = mjcf.load_model_from_string(xml)
+  np.testing.assert_allclose(m.body_mass[1], 1000.0, rtol=1e-9)
+  np.testing.assert_allclose(m.body_mass[2], 600.0 / 6.0, rtol=1e-9)
+  np.testing.assert_allclose(m.body_inertia[1], [1000.0 / 6.0] * 3, rtol=1e-9)  # m (a^2 + b^2) / 12, a = b = 1
+  v = np.array([float(x) for x in cube.split()]).reshape(-1, 3)
+  f = mjcf._hull_faces(v)
+  assert len(f) == 12
+  c = v.mean(axis=0)
+  for i, j, k in f:
+    assert np.dot(np.cross(v[j] - v[i], v[k] - v[i]), v[i] - c) > 0
