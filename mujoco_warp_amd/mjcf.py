@@ -908,13 +908,13 @@ class _Compiler:
     self._build_geoms()
     self._build_inertia()
     self._build_sites_cams_lights()
+    self._build_tendons(root)
     self._build_actuators(root)
     self._build_contact(root)
     self._build_keys(root)
     self._build_flex()
     self._build_equality(root)
     self._build_sensors(root)
-    m.ntendon = 0
     m.nhfield = 0
     m.body_subtreemass = self._subtreemass()
     set_const(m)
@@ -1321,6 +1321,78 @@ class _Compiler:
     m.light_pos = np.array([r["pos"] for r in lrows]).reshape(-1, 3)
     m.light_dir = np.array([r["dir"] for r in lrows]).reshape(-1, 3)
 
+  def _build_tendons(self, root):
+    """<tendon><fixed>: fixed (joint) tendons, length = sum coef * qpos (smooth.py:3085-3121).  The
+    sparse Jacobian structure ten_J_rownnz / _rowadr / _colind lists each tendon's dofs ascending, as
+    MuJoCo's compiler does; spatial tendons are not supported."""
+    m = self.m
+    name2jnt = {n: i for i, n in enumerate(m.jnt_names) if n}
+    rows, wraps = [], []
+    for ten in root.findall("tendon"):
+      for el in ten:
+        if el.tag != "fixed":
+          raise NotImplementedError(f"<tendon><{el.tag}> is not supported (fixed tendons only)")
+        a = dict(self.defaults[el.get("class", "main")].attrs.get("tendon", {}))
+        a.update(el.attrib)
+
+        def limited(key, rkey):
+          v = a.get(key, "auto")
+          if v == "auto":
+            return bool(self.autolimits and rkey in a)
+          return v == "true"
+
+        adr = len(wraps)
+        for j in el:
+          if j.tag != "joint":
+            raise NotImplementedError(f"<fixed><{j.tag}> is not supported")
+          jid = name2jnt[j.get("joint")]
+          if m.jnt_type[jid] not in (JointType.HINGE, JointType.SLIDE):
+            raise ValueError("fixed tendon joints must be hinge or slide joints")
+          wraps.append((jid, float(j.get("coef", 1.0))))
+        sl = _floats(a.get("springlength", "-1 -1"))
+        rows.append(dict(
+          name=a.get("name", ""), adr=adr, num=len(wraps) - adr,
+          stiffness=float(a.get("stiffness", 0.0)), damping=float(a.get("damping", 0.0)),
+          frictionloss=float(a.get("frictionloss", 0.0)), armature=float(a.get("armature", 0.0)),
+          limited=limited("limited", "range"), range=_floats(a.get("range", "0 0"), 2), margin=float(a.get("margin", 0.0)),
+          springlength=sl if len(sl) == 2 else [sl[0], sl[0]],
+          solref_lim=_merge_vec([0.02, 1.0], _floats(a.get("solreflimit", "0.02 1"))),
+          solimp_lim=_merge_vec([0.9, 0.95, 0.001, 0.5, 2.0], _floats(a.get("solimplimit", "0.9 0.95 0.001 0.5 2"))),
+          solref_fri=_merge_vec([0.02, 1.0], _floats(a.get("solreffriction", "0.02 1"))),
+          solimp_fri=_merge_vec([0.9, 0.95, 0.001, 0.5, 2.0], _floats(a.get("solimpfriction", "0.9 0.95 0.001 0.5 2"))),
+          actfrclimited=limited("actuatorfrclimited", "actuatorfrcrange"),
+          actfrcrange=_floats(a.get("actuatorfrcrange", "0 0"), 2),
+        ))
+    nt = len(rows)
+    m.ntendon, m.nwrap = nt, len(wraps)
+    m.tendon_names = [r["name"] for r in rows]
+    m.tendon_adr = np.array([r["adr"] for r in rows], dtype=np.int32)
+    m.tendon_num = np.array([r["num"] for r in rows], dtype=np.int32)
+    for k in ("stiffness", "damping", "frictionloss", "armature", "margin"):
+      setattr(m, "tendon_" + k, np.array([r[k] for r in rows], dtype=np.float64))
+    m.tendon_limited = np.array([r["limited"] for r in rows], dtype=bool)
+    m.tendon_actfrclimited = np.array([r["actfrclimited"] for r in rows], dtype=bool)
+    m.tendon_range = np.array([r["range"] for r in rows]).reshape(nt, 2)
+    m.tendon_actfrcrange = np.array([r["actfrcrange"] for r in rows]).reshape(nt, 2)
+    m.tendon_lengthspring = np.array([r["springlength"] for r in rows], dtype=np.float64).reshape(nt, 2)
+    m.tendon_solref_lim = np.array([r["solref_lim"] for r in rows]).reshape(nt, 2)
+    m.tendon_solimp_lim = np.array([r["solimp_lim"] for r in rows]).reshape(nt, 5)
+    m.tendon_solref_fri = np.array([r["solref_fri"] for r in rows]).reshape(nt, 2)
+    m.tendon_solimp_fri = np.array([r["solimp_fri"] for r in rows]).reshape(nt, 5)
+    m.wrap_type = np.full(len(wraps), 1, dtype=np.int32)  # mjWRAP_JOINT
+    m.wrap_objid = np.array([w[0] for w in wraps], dtype=np.int32)
+    m.wrap_prm = np.array([w[1] for w in wraps], dtype=np.float64)
+    rownnz, rowadr, colind = [], [], []
+    for r in rows:
+      dofs = sorted({int(m.jnt_dofadr[m.wrap_objid[k]]) for k in range(r["adr"], r["adr"] + r["num"])})
+      rowadr.append(len(colind))
+      rownnz.append(len(dofs))
+      colind += dofs
+    m.ten_J_rownnz = np.array(rownnz, dtype=np.int32)
+    m.ten_J_rowadr = np.array(rowadr, dtype=np.int32)
+    m.ten_J_colind = np.array(colind, dtype=np.int32)
+    m.nJten = len(colind)
+
   def _build_actuators(self, root):
     m = self.m
     name2jnt = {n: i for i, n in enumerate(m.jnt_names) if n}
@@ -1387,8 +1459,10 @@ class _Compiler:
           trntype, trnid = TrnType.JOINT, [name2jnt[a["joint"]], -1]
         elif "jointinparent" in a:
           trntype, trnid = TrnType.JOINTINPARENT, [name2jnt[a["jointinparent"]], -1]
+        elif "tendon" in a:
+          trntype, trnid = TrnType.TENDON, [m.tendon_names.index(a["tendon"]), -1]
         else:
-          raise NotImplementedError("only joint transmissions are supported by the MJCF compiler")
+          raise NotImplementedError("only joint and tendon transmissions are supported by the MJCF compiler")
         rows.append(
           dict(
             name=a.get("name", ""),
@@ -1824,6 +1898,23 @@ def set_const(m: MjModel):
   nv, nb = m.nv, m.nbody
   k = _kinematics_qpos0(m)
   M = k["M"]
+  # fixed tendons at qpos0: length0, the dense Jacobians, armature in M (smooth.py:916-1000)
+  nt = getattr(m, "ntendon", 0)
+  tenJ = np.zeros((nt, nv))
+  m.tendon_length0 = np.zeros(nt)
+  for t in range(nt):
+    for w in range(m.tendon_adr[t], m.tendon_adr[t] + m.tendon_num[t]):
+      j = m.wrap_objid[w]
+      m.tendon_length0[t] += m.wrap_prm[w] * m.qpos0[m.jnt_qposadr[j]]
+      tenJ[t, m.jnt_dofadr[j]] += m.wrap_prm[w]
+    if m.tendon_armature[t]:
+      M = M + m.tendon_armature[t] * np.outer(tenJ[t], tenJ[t])
+  if nt:
+    # springlength -1: the spring rests at the qpos0 length (MuJoCo's compiler)
+    ls = m.tendon_lengthspring
+    for t in range(nt):
+      if ls[t, 0] == -1 and ls[t, 1] == -1:
+        ls[t] = m.tendon_length0[t]
   m.stat.meaninertia = float(np.trace(M) / nv) if nv else 1.0
   Minv = np.linalg.inv(M) if nv else np.zeros((0, 0))
   # dof_invweight0 (io.py:1802-1843)
@@ -1839,6 +1930,8 @@ def set_const(m: MjModel):
     else:
       inv[i] = diag[i]
   m.dof_invweight0 = inv
+  # tendon_invweight0 = J M^-1 J' at qpos0
+  m.tendon_invweight0 = np.array([tenJ[t] @ Minv @ tenJ[t] for t in range(nt)]) if nt else np.zeros(0)
   # body_invweight0 (io.py:1846-1956)
   biw = np.zeros((nb, 2))
   for b in range(1, nb):
@@ -1911,6 +2004,9 @@ def set_const(m: MjModel):
   for a in range(m.nu):
     vec = np.zeros(nv)
     j = m.actuator_trnid[a, 0]
+    if m.actuator_trntype[a] == TrnType.TENDON:
+      acc0[a] = np.linalg.norm(Minv @ (m.actuator_gear[a, 0] * tenJ[j]))
+      continue
     t = m.jnt_type[j]
     da = m.jnt_dofadr[j]
     if t == JointType.FREE:

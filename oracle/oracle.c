@@ -39,7 +39,8 @@ enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2, EQ_FLEX = 4 };
 enum { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum { INTEGRATOR_EULER = 0, INTEGRATOR_RK4 = 1, INTEGRATOR_IMPLICIT = 2, INTEGRATOR_IMPLICITFAST = 3 };
 enum { BIAS_NONE = 0, BIAS_AFFINE = 1 };
-enum { TRN_JOINT = 0, TRN_JOINTINPARENT = 1 };
+enum { TRN_JOINT = 0, TRN_JOINTINPARENT = 1, TRN_TENDON = 3 };
+enum { CNSTR_FRICTION_TENDON = 2, CNSTR_LIMIT_TENDON = 4 };
 enum { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
 
 /* =============================================================================================
@@ -274,8 +275,8 @@ static void world_view(const orc_model* m, const orc_data* b, int w, orc_data* o
   int nq = m->nq, nv = m->nv, nu = m->nu, na = m->na, nbody = m->nbody, njnt = m->njnt;
   int ngeom = m->ngeom, nsite = m->nsite, ncam = m->ncam, nlight = m->nlight, nmocap = m->nmocap, neq = m->neq;
   int njmax = b->njmax, nconmax = b->nconmax, nsensordata = m->nsensordata;
-  int nflexvert = m->nflexvert, nflexedge = m->nflexedge;
-  (void)nflexvert; (void)nflexedge;
+  int nflexvert = m->nflexvert, nflexedge = m->nflexedge, ntendon = m->ntendon, nJten = m->nJten;
+  (void)nflexvert; (void)nflexedge; (void)ntendon; (void)nJten;
   (void)nsensordata;
   (void)nq; (void)nv; (void)nu; (void)na; (void)nbody; (void)njnt; (void)ngeom; (void)nsite; (void)ncam;
   (void)nlight; (void)nmocap; (void)njmax; (void)nconmax; (void)neq;
@@ -742,6 +743,54 @@ static void solve_m(const orc_model* m, int n, const real* L, const real* y, rea
 }
 
 /* smooth.py:2041-2147 (_transmission, joint transmissions; dense moment rows) */
+/* smooth.py:3085-3121 (_joint_tendon): fixed tendon length sum coef * qpos, Jacobian coef at the joint's
+ * dof, stored in the sparse ten_J layout (ten_J_rowadr / _rownnz / _colind, dofs ascending) */
+static void tendon(const orc_model* m, orc_data* d) {
+  for (int t = 0; t < m->ntendon; t++) {
+    real L = 0;
+    const int ra = m->ten_J_rowadr[t], rn = m->ten_J_rownnz[t];
+    for (int k = 0; k < rn; k++) d->ten_J[ra + k] = 0;
+    for (int w = m->tendon_adr[t]; w < m->tendon_adr[t] + m->tendon_num[t]; w++) {
+      const int j = m->wrap_objid[w];
+      const real prm = m->wrap_prm[w];
+      L += prm * d->qpos[m->jnt_qposadr[j]];
+      for (int k = 0; k < rn; k++)
+        if (m->ten_J_colind[ra + k] == m->jnt_dofadr[j]) { d->ten_J[ra + k] = prm; break; }
+    }
+    d->ten_length[t] = L;
+  }
+}
+
+/* dense row of tendon t's Jacobian */
+static void ten_J_dense(const orc_model* m, const orc_data* d, int t, real* J) {
+  memset(J, 0, (size_t)m->nv * sizeof(real));
+  for (int k = 0; k < m->ten_J_rownnz[t]; k++) J[m->ten_J_colind[m->ten_J_rowadr[t] + k]] = d->ten_J[m->ten_J_rowadr[t] + k];
+}
+
+/* smooth.py:916-1000 (_tendon_armature): qM[i][j] += armature J_i J_j for j = i and every ancestor j of i
+ * (the ancestor pattern of qM) */
+static void tendon_armature(const orc_model* m, orc_data* d) {
+  int nv = m->nv;
+  for (int t = 0; t < m->ntendon; t++) {
+    const real arm = m->tendon_armature[t];
+    if (arm == 0) continue;
+    const int ra = m->ten_J_rowadr[t], rn = m->ten_J_rownnz[t];
+    for (int k = 0; k < rn; k++) {
+      const int i = m->ten_J_colind[ra + k];
+      const real Ji = d->ten_J[ra + k];
+      if (Ji == 0) continue;
+      for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+        real Jj = 0;
+        for (int q = 0; q < rn; q++)
+          if (m->ten_J_colind[ra + q] == j) Jj = d->ten_J[ra + q];
+        const real v = arm * Jj * Ji;
+        d->qM[(size_t)i * nv + j] += v;
+        if (i != j) d->qM[(size_t)j * nv + i] += v;
+      }
+    }
+  }
+}
+
 static void transmission(const orc_model* m, orc_data* d) {
   int nv = m->nv;
   memset(d->actuator_moment, 0, (size_t)m->nu * nv * sizeof(real));
@@ -749,6 +798,14 @@ static void transmission(const orc_model* m, orc_data* d) {
     const real* gear = m->actuator_gear + 6 * a;
     int trn = m->actuator_trntype[a];
     real* mom = d->actuator_moment + (size_t)a * nv;
+    if (trn == TRN_TENDON) {
+      /* smooth.py:2244-2260: length = ten_length gear0, moment = gear0 ten_J */
+      const int t = m->actuator_trnid[2 * a];
+      d->actuator_length[a] = d->ten_length[t] * gear[0];
+      for (int k = 0; k < m->ten_J_rownnz[t]; k++)
+        mom[m->ten_J_colind[m->ten_J_rowadr[t] + k]] = d->ten_J[m->ten_J_rowadr[t] + k] * gear[0];
+      continue;
+    }
     if (trn == TRN_JOINT || trn == TRN_JOINTINPARENT) {
       int j = m->actuator_trnid[2 * a];
       int jt = m->jnt_type[j], qa = m->jnt_qposadr[j], va = m->jnt_dofadr[j];
@@ -887,6 +944,20 @@ static void passive(const orc_model* m, orc_data* d) {
     } else {
       if (has_s) d->qfrc_spring[da] = -stiff * (d->qpos[qa] - m->qpos_spring[qa]);
       if (has_d) d->qfrc_damper[da] = -damp * d->qvel[da];
+    }
+  }
+  /* passive.py:183-252: tendon spring (dead band between lengthspring[0] and [1]) and damper */
+  for (int t = 0; t < m->ntendon; t++) {
+    const real k = m->tendon_stiffness[t], b = m->tendon_damping[t];
+    const int has_s = k != 0 && !dsbl_spring, has_d = b != 0 && !dsbl_damper;
+    if (!has_s && !has_d) continue;
+    const real L = d->ten_length[t], lo = m->tendon_lengthspring[2 * t], hi = m->tendon_lengthspring[2 * t + 1];
+    const real fs = L > hi ? k * (hi - L) : (L < lo ? k * (lo - L) : 0);
+    const real fd = -b * d->ten_velocity[t];
+    for (int q = 0; q < m->ten_J_rownnz[t]; q++) {
+      const int e = m->ten_J_rowadr[t] + q, i = m->ten_J_colind[e];
+      if (has_s) d->qfrc_spring[i] += d->ten_J[e] * fs;
+      if (has_d) d->qfrc_damper[i] += d->ten_J[e] * fd;
     }
   }
   if (!dsbl_spring) flex_passive(m, d);
@@ -2051,6 +2122,20 @@ static void make_constraint(const orc_model* m, orc_data* d) {
       efc_row(m, d, efcid, 0, 0, m->dof_invweight0[i], m->dof_solref + 2 * i, m->dof_solimp + 5 * i, 0, d->qvel[i], fl,
               CNSTR_FRICTION_DOF, i);
     }
+    /* friction tendon constraint.py:1204-1313 */
+    for (int t = 0; t < m->ntendon; t++) {
+      real fl = m->tendon_frictionloss[t];
+      if (fl <= 0) continue;
+      (*d->nf)++;
+      int efcid = (*d->nefc)++;
+      if (efcid >= njmax) continue;
+      real* J = d->efc_J + (size_t)efcid * nv;
+      ten_J_dense(m, d, t, J);
+      real Jqvel = 0;
+      for (int i = 0; i < nv; i++) Jqvel += J[i] * d->qvel[i];
+      efc_row(m, d, efcid, 0, 0, m->tendon_invweight0[t], m->tendon_solref_fri + 2 * t, m->tendon_solimp_fri + 5 * t, 0, Jqvel, fl,
+              CNSTR_FRICTION_TENDON, t);
+    }
   }
   /* limit ball constraint.py:1421-1543 */
   if (!(m->opt_disableflags & DSBL_LIMIT)) {
@@ -2097,6 +2182,24 @@ static void make_constraint(const orc_model* m, orc_data* d) {
       J[da] = Jv;
       efc_row(m, d, efcid, pos, pos, m->dof_invweight0[da], m->jnt_solref + 2 * j, m->jnt_solimp + 5 * j, m->jnt_margin[j],
               Jv * d->qvel[da], 0, CNSTR_LIMIT_JOINT, j);
+    }
+    /* limit tendon constraint.py:1547-1665 */
+    for (int t = 0; t < m->ntendon; t++) {
+      if (!m->tendon_limited[t]) continue;
+      const real* rng = m->tendon_range + 2 * t;
+      real L = d->ten_length[t], dmn = L - rng[0], dmx = rng[1] - L;
+      real pos = minr(dmn, dmx) - m->tendon_margin[t];
+      if (!(pos < 0)) continue;
+      (*d->nl)++;
+      int efcid = (*d->nefc)++;
+      if (efcid >= njmax) continue;
+      real scl = (real)(dmn < dmx) * 2 - 1;
+      real* J = d->efc_J + (size_t)efcid * nv;
+      ten_J_dense(m, d, t, J);
+      real Jqvel = 0;
+      for (int i = 0; i < nv; i++) { J[i] *= scl; Jqvel += J[i] * d->qvel[i]; }
+      efc_row(m, d, efcid, pos, pos, m->tendon_invweight0[t], m->tendon_solref_lim + 2 * t, m->tendon_solimp_lim + 5 * t,
+              m->tendon_margin[t], Jqvel, 0, CNSTR_LIMIT_TENDON, t);
     }
   }
   /* contact pyramidal constraint.py:1668-1936, elliptic :1940-2200 */
@@ -2200,7 +2303,9 @@ static void fwd_position(const orc_model* m, orc_data* d) {
   com_pos(m, d);
   camlight(m, d);
   flex_kinematics(m, d);
+  tendon(m, d);
   crb(m, d);
+  tendon_armature(m, d);
   collision(m, d);
   make_constraint(m, d);
   transmission(m, d);
@@ -2213,9 +2318,16 @@ static void fwd_velocity(const orc_model* m, orc_data* d) {
     for (int i = 0; i < m->nv; i++) v += d->actuator_moment[(size_t)a * m->nv + i] * d->qvel[i];
     d->actuator_velocity[a] = v;
   }
+  /* forward.py:604-609 _tendon_velocity */
+  for (int t = 0; t < m->ntendon; t++) {
+    real v = 0;
+    for (int q = 0; q < m->ten_J_rownnz[t]; q++) v += d->ten_J[m->ten_J_rowadr[t] + q] * d->qvel[m->ten_J_colind[m->ten_J_rowadr[t] + q]];
+    d->ten_velocity[t] = v;
+  }
   com_vel(m, d);
   passive(m, d);
   rne(m, d);
+  /* tendon_bias (smooth.py:1810-1905): armature * J * (dJ/dt qvel) vanishes for fixed tendons */
 }
 
 /* support.py:38-64 next_act */
@@ -2265,6 +2377,19 @@ static void fwd_actuation(const orc_model* m, orc_data* d) {
     real force = gain * ctrl_act + bias;
     if (m->actuator_forcelimited[a]) force = clampr(force, m->actuator_forcerange[2 * a], m->actuator_forcerange[2 * a + 1]);
     d->actuator_force[a] = force;
+  }
+  /* forward.py:739-779: total actuator force per tendon clamped to its actuatorfrcrange by scaling */
+  for (int t = 0; t < m->ntendon; t++) {
+    if (!m->tendon_actfrclimited[t]) continue;
+    real tot = 0;
+    for (int a = 0; a < m->nu; a++)
+      if (m->actuator_trntype[a] == TRN_TENDON && m->actuator_trnid[2 * a] == t) tot += d->actuator_force[a];
+    const real lo = m->tendon_actfrcrange[2 * t], hi = m->tendon_actfrcrange[2 * t + 1];
+    for (int a = 0; a < m->nu; a++) {
+      if (m->actuator_trntype[a] != TRN_TENDON || m->actuator_trnid[2 * a] != t) continue;
+      if (tot < lo) d->actuator_force[a] *= lo / tot;
+      else if (tot > hi) d->actuator_force[a] *= hi / tot;
+    }
   }
   memset(d->qfrc_actuator, 0, nv * sizeof(real));
   for (int a = 0; a < m->nu; a++)

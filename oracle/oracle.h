@@ -29,7 +29,8 @@ typedef ORC_REAL real;
   X(nxn) X(nmaxpyramid) X(neq) X(nsensor) X(nsensordata) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)             \
   X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
-  X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)
+  X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)   \
+  X(ntendon) X(nwrap) X(nJten)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
@@ -61,7 +62,12 @@ typedef ORC_REAL real;
   X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)                               \
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flex_vert, nflexvert * 3) X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)    \
-  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17) X(mesh_vert, nmeshvert * 3)
+  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17) X(mesh_vert, nmeshvert * 3)      \
+  X(tendon_stiffness, ntendon) X(tendon_damping, ntendon) X(tendon_frictionloss, ntendon)          \
+  X(tendon_armature, ntendon) X(tendon_margin, ntendon) X(tendon_range, ntendon * 2)               \
+  X(tendon_lengthspring, ntendon * 2) X(tendon_solref_lim, ntendon * 2) X(tendon_solimp_lim, ntendon * 5) \
+  X(tendon_solref_fri, ntendon * 2) X(tendon_solimp_fri, ntendon * 5) X(tendon_invweight0, ntendon)  \
+  X(tendon_actfrcrange, ntendon * 2) X(wrap_prm, nwrap)
 
 /* ---- model: int arrays (name, element count) ---- */
 #define ORC_MODEL_INT_ARRAYS(X)                                                                    \
@@ -89,7 +95,9 @@ typedef ORC_REAL real;
   X(flex_elemedgeadr, nflex) X(flex_contype, nflex) X(flex_conaffinity, nflex) X(flex_condim, nflex) \
   X(flex_centered, nflex) X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert)              \
   X(flex_edge, nflexedge * 2) X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata)          \
-  X(flex_elemedge, nflexelem * 3) X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)
+  X(flex_elemedge, nflexelem * 3) X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom) \
+  X(tendon_adr, ntendon) X(tendon_num, ntendon) X(tendon_limited, ntendon) X(tendon_actfrclimited, ntendon) \
+  X(wrap_objid, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)
 
 /* ---- per-world data: real arrays (name, element count per world) ---- */
 #define ORC_DATA_REAL_ARRAYS(X)                                                                    \
@@ -113,7 +121,7 @@ typedef ORC_REAL real;
   X(con_includemargin, nconmax) X(con_friction, nconmax * 5) X(con_solref, nconmax * 2)           \
   X(con_solreffriction, nconmax * 2) X(con_solimp, nconmax * 5) X(solver_cost, 1)                 \
   X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
-  X(flexedge_J, nflexedge * 6)
+  X(flexedge_J, nflexedge * 6) X(ten_length, ntendon) X(ten_velocity, ntendon) X(ten_J, nJten)
 
 /* ---- per-world data: int arrays ---- */
 #define ORC_DATA_INT_ARRAYS(X)                                                                     \

@@ -131,6 +131,7 @@ class OracleModel:
       nflex=getattr(mjm, "nflex", 0), nflexvert=getattr(mjm, "nflexvert", 0), nflexedge=getattr(mjm, "nflexedge", 0),
       nflexelem=getattr(mjm, "nflexelem", 0), nflexelemdata=getattr(mjm, "nflexelemdata", 0),
       nmesh=getattr(mjm, "nmesh", 0), nmeshvert=getattr(mjm, "nmeshvert", 0),
+      ntendon=getattr(mjm, "ntendon", 0), nwrap=getattr(mjm, "nwrap", 0), nJten=getattr(mjm, "nJten", 0),
     )
     if overrides:
       vals.update(overrides)
