@@ -2923,6 +2923,19 @@ static void implicit(const orc_model* m, orc_data* d) {
       for (int a = 0; a < m->nu; a++)
         if (vel[a] != 0) qd += d->actuator_moment[a * nv + i] * d->actuator_moment[a * nv + j] * vel[a];
       if (!(flags & DSBL_DAMPER) && i == j) qd -= m->dof_damping[i];
+      /* derivative.py:267-320 _qderiv_tendon_damping: - sum_t damping_t J_ti J_tj on the qM pattern */
+      if (!(flags & DSBL_DAMPER)) {
+        for (int t = 0; t < m->ntendon; t++) {
+          if (m->tendon_damping[t] == 0) continue;
+          real Ji = 0, Jj = 0;
+          for (int k = 0; k < m->ten_J_rownnz[t]; k++) {
+            const int e = m->ten_J_rowadr[t] + k;
+            if (m->ten_J_colind[e] == i) Ji = d->ten_J[e];
+            if (m->ten_J_colind[e] == j) Jj = d->ten_J[e];
+          }
+          qd -= Ji * Jj * m->tendon_damping[t];
+        }
+      }
       qd *= dt;
       A[i * nv + j] = d->qM[i * nv + j] - qd;
       A[j * nv + i] = A[i * nv + j];

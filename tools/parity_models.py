@@ -54,7 +54,9 @@ def setup(name):
 
   if name == "franka":
     mjm = franka_model()
-    return (mjm,) + franka_states(mjm, 16, seed=22) + (16, 4, 16)
+    # pools sized so that neither side drops rows or contacts (the device pool is global, the
+    # oracle's per world): fingertip pads and the hand can make up to 10 floor contacts
+    return (mjm,) + franka_states(mjm, 16, seed=22) + (64, 16, 16)
   if name == "apollo":
     mjm = mjw.load_model(os.path.join(ROOT, "models", "apptronik_apollo", "scene_flat.xml"))
     nworld = 32
