@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 13
+#define MJW_ABI_VERSION 14
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -42,7 +42,7 @@
   X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)                                  \
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
-  X(nmesh) X(nmeshvert)
+  X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -73,7 +73,12 @@
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)                                \
   X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)                              \
-  X(mesh_vert, nmeshvert * 3)
+  X(mesh_vert, nmeshvert * 3)                                                                      \
+  X(tendon_stiffness, ntendon) X(tendon_damping, ntendon) X(tendon_frictionloss, ntendon)          \
+  X(tendon_armature, ntendon) X(tendon_margin, ntendon) X(tendon_range, ntendon * 2)               \
+  X(tendon_lengthspring, ntendon * 2) X(tendon_solref_lim, ntendon * 2) X(tendon_solimp_lim, ntendon * 5) \
+  X(tendon_solref_fri, ntendon * 2) X(tendon_solimp_fri, ntendon * 5) X(tendon_invweight0, ntendon)  \
+  X(tendon_actfrcrange, ntendon * 2) X(wrap_prm, nwrap)
 
 /* ---- model: int arrays (never batched) ---- */
 #define MJW_MODEL_INT_ARRAYS(X)                                                                    \
@@ -104,7 +109,9 @@
   X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert) X(flex_edge, nflexedge * 2)          \
   X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata) X(flex_elemedge, nflexelem * 3)      \
   X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)                                     \
-  X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)
+  X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)                            \
+  X(tendon_adr, ntendon) X(tendon_num, ntendon) X(tendon_limited, ntendon) X(tendon_actfrclimited, ntendon) \
+  X(wrap_objid, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)
 
 /* ---- data: float arrays, (nworld, count) world-major like mujoco_warp types.Data ----
  * Sparse models (is_sparse, the reference's io.py:67-74 switch) store qM / qLD as (nworld, nM) rows of
@@ -135,7 +142,8 @@
   X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
   X(flexedge_J, nflexedge * 6) X(flex_frc, nflexelem * 9 + nflexedge * 12)                        \
   X(sp_body, nbody * 6) X(sp_vec, nv * 10) X(sp_row, njmax * 2) X(sp_LD, nM)                     \
-  X(efc_JT_val, njmax_pad * njrow)
+  X(efc_JT_val, njmax_pad * njrow)                                                                 \
+  X(ten_length, ntendon) X(ten_velocity, ntendon) X(ten_J, nJten)
 
 /* ---- data: int arrays, (nworld, count) ---- */
 #define MJW_DATA_INT_ARRAYS(X)                                                                     \

@@ -31,6 +31,7 @@ enum : int {
   DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512, DSBL_ACTUATION = 2048,
   DSBL_REFSAFE = 4096, DSBL_SENSOR = 8192, DSBL_EULERDAMP = 1 << 15
 };
+enum : int { TRN_JOINT = 0, TRN_JOINTINPARENT = 1, TRN_TENDON = 3 };
 enum : int { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum : int { DATATYPE_REAL = 0, DATATYPE_POSITIVE = 1 };
 enum : int { STAGE_POS = 1, STAGE_VEL = 2, STAGE_ACC = 3 };
@@ -42,7 +43,7 @@ enum : int {
   SENS_FRAMELINACC = 33, SENS_FRAMEANGACC = 34, SENS_SUBTREECOM = 35, SENS_CLOCK = 45
 };
 enum : int { ENBL_ENERGY = 2 };
-enum : int { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6,
+enum : int { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_FRICTION_TENDON = 2, CNSTR_LIMIT_JOINT = 3, CNSTR_LIMIT_TENDON = 4, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6,
              CNSTR_CONTACT_ELLIPTIC = 7 };
 enum : int { CONE_PYRAMIDAL = 0, CONE_ELLIPTIC = 1 };
 enum : int { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINEARPOS = 3, STATE_CONE = 4 };

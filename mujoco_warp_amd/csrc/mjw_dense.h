@@ -20,6 +20,7 @@
 
 #pragma once
 #include "mjw_common.h"
+#include "mjw_tendon.h"
 
 namespace mjw {
 
@@ -790,6 +791,26 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
               S[i * DSS + j] -= v;
               if (i != j) S[j * DSS + i] -= v;
             }
+          }
+          __syncthreads();
+        }
+      }
+      if (implicitfast && m.ntendon && !(fl & DSBL_DAMPER)) {
+        // derivative.py:267-320: tendon damping enters qDeriv as -damping J_i J_j on the qM pattern
+        const float* tdamp = MR(tendon_damping);
+        for (int t = 0; t < m.ntendon; t++) {
+          if (tdamp[t] == 0.0f) continue;
+          const int rn = m.ten_J_rownnz[t], ra = m.ten_J_rowadr[t];
+          for (int p = lane; p < rn * rn; p += 64) {
+            const int k1 = p / rn, k2 = p - k1 * rn;
+            if (k2 > k1) continue;
+            const int i = m.ten_J_colind[ra + k1], j = m.ten_J_colind[ra + k2];
+            int q = i;
+            while (q > j) q = m.dof_parentid[q];
+            if (q != j || i >= 32) continue;
+            const float v = dt * tdamp[t] * ten_coef(m, wid, t, i) * ten_coef(m, wid, t, j);
+            S[i * DSS + j] += v;
+            if (i != j) S[j * DSS + i] += v;
           }
           __syncthreads();
         }

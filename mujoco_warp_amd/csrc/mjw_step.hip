@@ -15,6 +15,7 @@
 #include "mjw_common.h"
 #include "mjw_ccd.h"
 #include "mjw_narrow.h"
+#include "mjw_tendon.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -92,7 +93,7 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
   L.rowcon = -1;
   // moment slots per actuator: 1 when every transmission has one non-zero (nJmom == nu: hinge / slide
   // joints), else 6 (free / ball joints)
-  L.amax = m.nJmom == nu ? 1 : 6;
+  L.amax = m.nJmom == nu ? 1 : (m.ten_maxnnz > 6 ? m.ten_maxnnz : 6);
   L.act_len = take(nu); L.act_vel = take(nu); L.act_force = take(nu); L.act_mom = take(nu * L.amax); L.act_momdof = take(nu * L.amax);
   L.act_nnz = take(nu);
   L.scratch = take(64);
@@ -475,6 +476,7 @@ __device__ __forceinline__ void camlight(const mjw_model_t& m, const mjw_data_t&
 }
 
 // smooth.py:806-912: composite inertia (subtree ranges) and dense qM
+template <bool TEN>
 __device__ __forceinline__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -518,6 +520,7 @@ __device__ __forceinline__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d
     }
   }
   WSYNC();
+  if (TEN && m.ntendon) tendon_armature(m, M, nvs, wid, lane);  // smooth.py:916-1000
   const int np = m.nv_pad;
   float* gM = d.qM + (long)wid * np * np;
   for (int e = lane; e < np * np; e += LPW) {
@@ -814,7 +817,58 @@ __device__ __forceinline__ void eq_connect_weld(const mjw_model_t& m, const mjw_
 }
 
 // collision_driver.py:754-789 + constraint.py:2209-2779 (friction-dof, limits, pyramidal contacts)
-template <bool BOX>
+// friction (limit = false, constraint.py:1204-1313) or limit (limit = true, :1547-1665) rows of the
+// fixed tendons from row nefc on; returns the rows added.  collision_and_constraints counts these rows
+// where the reference emits them (after the dof friction / joint limit rows) and fills them in here
+// once the contact rows are done, so that the tendon code does not overlap the narrowphase's
+// register peak (inline there it pushed the forward kernel into 16 B/lane of scratch).
+__device__ __forceinline__ int tendon_rows(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, float* s, int wid, int lane, int nefc,
+                                        int kJ, bool limit) {
+  const int nv = m.nv, np = m.nv_pad, njmax = d.njmax;
+  const float* qvel = s + L.qvel;
+  const float* tiw = MR(tendon_invweight0);
+  const float* tfl = MR(tendon_frictionloss);
+  const float* trng = MR(tendon_range);
+  const float* tmar = MR(tendon_margin);
+  const float* tsr = limit ? MR(tendon_solref_lim) : MR(tendon_solref_fri);
+  const float* tsi = limit ? MR(tendon_solimp_lim) : MR(tendon_solimp_fri);
+  int added = 0;
+  for (int base = 0; base < m.ntendon; base += LPW) {
+    const int t = base + lane;
+    bool act = false;
+    float pos = 0.0f, scl = 1.0f, tm = 0.0f;
+    if (t < m.ntendon) {
+      if (limit) {
+        if (m.tendon_limited[t]) {
+          const float len = ten_len(m, wid, s + L.qpos, t);
+          const float dmn = len - trng[2 * t], dmx = trng[2 * t + 1] - len;
+          tm = tmar[t];
+          pos = fminf(dmn, dmx) - tm;
+          scl = (float)(dmn < dmx) * 2.0f - 1.0f;
+          act = pos < 0.0f;
+        }
+      } else {
+        act = tfl[t] > 0.0f;
+      }
+    }
+    unsigned long long bal = __ballot(act);
+    int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
+    int r = nefc + added + rank;
+    if (act && r < njmax) {
+      for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, k < nv ? scl * ten_coef(m, wid, t, k) : 0.0f);
+      if (limit)
+        efc_row(m, d, L, s, wid, r, pos, pos, tiw[t], tsr + 2 * t, tsi + 5 * t, tm, scl * ten_vel(m, wid, qvel, t), 0.0f,
+                CNSTR_LIMIT_TENDON, t);
+      else
+        efc_row(m, d, L, s, wid, r, 0.0f, 0.0f, tiw[t], tsr + 2 * t, tsi + 5 * t, 0.0f, ten_vel(m, wid, qvel, t), tfl[t],
+                CNSTR_FRICTION_TENDON, t);
+    }
+    added += __popcll(bal);
+  }
+  return added;
+}
+
+template <bool BOX, bool TEN>
 __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -908,6 +962,15 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       nefc += cnt;
       nf += cnt;
     }
+    // --- friction tendon rows (constraint.py:1204-1313): counted here, filled after the contacts
+    if (TEN && m.ntendon) {
+      const float* tfl = MR(tendon_frictionloss);
+      int cnt = 0;
+      for (int base = 0; base < m.ntendon; base += LPW) cnt += __popcll(__ballot(base + lane < m.ntendon && tfl[base + lane] > 0.0f));
+      if (lane == 0) si[L.iscratch + 56] = nefc;  // first friction tendon row (filled after the contacts)
+      nefc += cnt;
+      nf += cnt;
+    }
   }
   // --- ball joint limits (constraint.py:1421-1543): one row on the joint's 3 dofs along -axis
   if (!dsbl_constraint && !(m.opt_disableflags & DSBL_LIMIT) && m.nlimited_ball > 0) {
@@ -982,6 +1045,24 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
                 CNSTR_LIMIT_JOINT, j);
       }
       int cnt = __popcll(bal);
+      nefc += cnt;
+      nl += cnt;
+    }
+    // --- tendon limits (constraint.py:1547-1665): counted here, filled after the contacts
+    if (TEN && m.ntendon) {
+      const float* trng = MR(tendon_range);
+      const float* tmar = MR(tendon_margin);
+      int cnt = 0;
+      for (int base = 0; base < m.ntendon; base += LPW) {
+        const int t = base + lane;
+        bool act = false;
+        if (t < m.ntendon && m.tendon_limited[t]) {
+          const float len = ten_len(m, wid, s + L.qpos, t);
+          act = fminf(len - trng[2 * t], trng[2 * t + 1] - len) - tmar[t] < 0.0f;
+        }
+        cnt += __popcll(__ballot(act));
+      }
+      if (lane == 0) si[L.iscratch + 57] = nefc;  // first limit tendon row
       nefc += cnt;
       nl += cnt;
     }
@@ -1302,6 +1383,11 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
     }
   }
   (void)ncon_total;
+  if (TEN && m.ntendon && !dsbl_constraint) {
+    WSYNC();
+    if (!(m.opt_disableflags & DSBL_FRICTIONLOSS)) tendon_rows(m, d, L, s, wid, lane, si[L.iscratch + 56], kJ, false);
+    if (!(m.opt_disableflags & DSBL_LIMIT)) tendon_rows(m, d, L, s, wid, lane, si[L.iscratch + 57], kJ, true);
+  }
   WSYNC();
   // write rows to global (efc arrays are (nworld, njmax[_pad]))
   const int nrows = min(nefc, njmax);
@@ -1326,6 +1412,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
 }
 
 // smooth.py:2041-2147 (joint transmissions; moment rows packed in actuator order)
+template <bool TEN>
 __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -1336,8 +1423,12 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
     const int a = a0 + lane;
     int my_nnz = 0;
     if (a < m.nu) {
-      const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
-      my_nnz = jt0 == JNT_FREE ? 6 : (jt0 == JNT_BALL ? 3 : 1);
+      if (TEN && m.actuator_trntype[a] == TRN_TENDON) {
+        my_nnz = m.ten_J_rownnz[m.actuator_trnid[2 * a]];
+      } else {
+        const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
+        my_nnz = jt0 == JNT_FREE ? 6 : (jt0 == JNT_BALL ? 3 : 1);
+      }
     }
     const int incl = wave_scan_incl(my_nnz);
     const int rowadr = carry + incl - my_nnz;
@@ -1345,6 +1436,29 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
     if (a >= m.nu) continue;
     const float* gear = gear_all + 6 * a;
     int trn = m.actuator_trntype[a];
+    if (TEN && trn == TRN_TENDON) {
+      // smooth.py:2244-2260: length = ten_length gear0, moment row = gear0 ten_J (the tendon's dofs)
+      const int t = m.actuator_trnid[2 * a];
+      const float length = ten_len(m, wid, s + L.qpos, t) * gear[0];
+      const int nnz = my_nnz;
+      s[L.act_len + a] = length;
+      si[L.act_nnz + a] = nnz;
+      const long gu = (long)wid * m.nu + a;
+      d.actuator_length[gu] = length;
+      d.moment_rownnz[gu] = nnz;
+      d.moment_rowadr[gu] = rowadr;
+      for (int k = 0; k < L.amax; k++) {
+        const int dof = k < nnz ? m.ten_J_colind[m.ten_J_rowadr[t] + k] : 0;
+        const float mk = k < nnz ? gear[0] * ten_coef(m, wid, t, dof) : 0.0f;
+        s[L.act_mom + L.amax * a + k] = mk;
+        si[L.act_momdof + L.amax * a + k] = dof;
+        if (k < nnz) {
+          d.actuator_moment[(long)wid * m.nJmom + rowadr + k] = mk;
+          d.moment_colind[(long)wid * m.nJmom + rowadr + k] = dof;
+        }
+      }
+      continue;
+    }
     int j = m.actuator_trnid[2 * a];
     int jt = m.jnt_type[j], qa = m.jnt_qposadr[j], va = m.jnt_dofadr[j];
     const float* qpos = s + L.qpos;
@@ -1404,6 +1518,7 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
 // -------------------------------------------------------------------------------------------
 // velocity (forward.py:592-613): actuator velocity, com_vel, passive, rne
 // -------------------------------------------------------------------------------------------
+template <bool TEN>
 __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -1504,6 +1619,7 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
     }
   }
   WSYNC();
+  if (TEN && m.ntendon) tendon_passive(m, d, qpos, qvel, spring, damper, wid, lane);  // passive.py:183-252
   for (int i = lane; i < nv; i += LPW) {
     float p = spring[i] + damper[i];
     qfrc_passive[i] = p;
@@ -1575,6 +1691,7 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
 }
 
 // forward.py:616-927 (actuator force, qfrc_actuator)
+template <bool TEN>
 __device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -1625,6 +1742,12 @@ __device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_da
     d.actuator_force[(long)wid * m.nu + a] = force;
   }
   WSYNC();
+  if (TEN && m.ntendon) {
+    tendon_actuator_clamp(m, s + L.act_force, wid, lane);  // forward.py:739-779
+    for (int a = lane; a < m.nu; a += LPW)
+      if (m.actuator_trntype[a] == TRN_TENDON) d.actuator_force[(long)wid * m.nu + a] = s[L.act_force + a];
+    WSYNC();
+  }
   const float* jnt_actfrcrange = MR(jnt_actfrcrange);
   for (int i = lane; i < nv; i += LPW) {
     float q = 0.0f;
@@ -2107,7 +2230,9 @@ __device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data
 }
 
 // the stages in STAGES of world w.wid by the calling wavefront
-template <int STAGES, bool BOX>
+// FULL: the box narrowphase and the tendon paths (the lean instantiation, FULL = false, serves
+// models with neither: it keeps the humanoid-class kernel free of their register pressure)
+template <int STAGES, bool FULL>
 __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   PROF_T0();
   load_state(m, d, L, w);
@@ -2121,18 +2246,19 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
     PROF_MARK(PH_COM);
     camlight(m, d, L, w);
     PROF_MARK(PH_CAM);
-    crb_qM(m, d, L, w);
+    if (FULL && m.ntendon) tendon_pos(m, d, w.s + L.qpos, w.wid, w.lane);  // smooth.py:3085-3121 (fwd_position: before crb)
+    crb_qM<FULL>(m, d, L, w);
     PROF_MARK(PH_CRB);
-    collision_and_constraints<BOX>(m, d, L, w);
+    collision_and_constraints<FULL, FULL>(m, d, L, w);
     PROF_MARK(PH_COLL);
-    transmission(m, d, L, w);
+    transmission<FULL>(m, d, L, w);
     PROF_MARK(PH_TRN);
   }
-  if (STAGES & ST_VEL) fwd_velocity(m, d, L, w);
+  if (STAGES & ST_VEL) fwd_velocity<FULL>(m, d, L, w);
   if ((STAGES & ST_POS) && (STAGES & ST_VEL) && w.lane < 2 && !(m.opt_enableflags & ENBL_ENERGY))
     d.energy[(long)w.wid * 2 + w.lane] = 0.0f;
   PROF_MARK(PH_VEL);
-  if (STAGES & ST_ACT) fwd_actuation(m, d, L, w);
+  if (STAGES & ST_ACT) fwd_actuation<FULL>(m, d, L, w);
   PROF_MARK(PH_ACT);
   if (STAGES & ST_ACC) fwd_acceleration(m, d, L, w);
   PROF_MARK(PH_ACC);
@@ -2150,7 +2276,7 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
 // their registers (at the cap they spilled 80 B/lane).
 template <int STAGES>
 constexpr int fwd_waves_per_eu() { return ((STAGES & ST_SOLVE) && !(STAGES & ST_NOFACTOR)) ? 1 : 4; }
-template <int STAGES, bool BOX = true>
+template <int STAGES, bool FULL = true>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu<STAGES>()))) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   WS w;
@@ -2160,7 +2286,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
   WLOG_T0();
-  run_stages<STAGES, BOX>(m, d, L, w);
+  run_stages<STAGES, FULL>(m, d, L, w);
   WLOG_END(w.wid, 0);
 }
 
@@ -2362,9 +2488,9 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
     if constexpr ((STAGES & mjw::ST_POS) != 0)
       (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
-  // position-stage kernels without the box narrowphase paths for models that have no box pairs
+  // position-stage kernels without the box narrowphase and tendon paths for models that have neither
   if constexpr ((STAGES & mjw::ST_POS) != 0) {
-    if (m->nxn_box == 0) {
+    if (m->nxn_box == 0 && m->ntendon == 0) {
       hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
       mjw::trace_launch(s, mjw::K_FWD + 2 * STAGES);
       return set_err(hipGetLastError(), name);

@@ -152,8 +152,13 @@ def put_model(mjm, device=None) -> types.Model:
   if mjm.nu and (np.any(mjm.actuator_dyntype == types.DynType.MUSCLE) or np.any(mjm.actuator_gaintype == types.GainType.MUSCLE)
                  or np.any(mjm.actuator_biastype == types.BiasType.MUSCLE)):
     raise NotImplementedError("muscle actuators are not supported by this build yet.")
-  if np.any(mjm.actuator_trntype > types.TrnType.JOINTINPARENT):
-    raise NotImplementedError("only joint transmissions are supported.")
+  if np.any((mjm.actuator_trntype > types.TrnType.JOINTINPARENT) & (mjm.actuator_trntype != types.TrnType.TENDON)):
+    raise NotImplementedError("only joint and tendon transmissions are supported.")
+  ntendon = int(getattr(mjm, "ntendon", 0))
+  if ntendon and sparse:
+    raise NotImplementedError("sparse / flex models: tendons are not supported by this build yet.")
+  if ntendon and np.any(np.asarray(mjm.wrap_type) != 1):
+    raise NotImplementedError("only fixed (joint) tendons are supported by this build yet.")
 
   nv = mjm.nv
   opt = types.Option()
@@ -181,7 +186,9 @@ def put_model(mjm, device=None) -> types.Model:
   m.device = dev
   for n in ("nq", "nv", "nu", "na", "nbody", "njnt", "ngeom", "nsite", "ncam", "nlight", "nmocap", "nM", "nC"):
     setattr(m, n, int(getattr(mjm, n)))
-  m.ntendon = 0
+  m.ntendon = int(getattr(mjm, "ntendon", 0))
+  m.nwrap, m.nJten = int(getattr(mjm, "nwrap", 0)), int(getattr(mjm, "nJten", 0))
+  m.ten_maxnnz = int(np.max(mjm.ten_J_rownnz)) if m.ntendon else 0  # the reference's max_ten_J_rownnz (io.py:232)
   m.neq = int(getattr(mjm, "neq", 0))
   m.nsensor = int(getattr(mjm, "nsensor", 0))
   m.nsensordata = int(getattr(mjm, "nsensordata", 0))
@@ -234,7 +241,12 @@ def put_model(mjm, device=None) -> types.Model:
   m.nlimited = len(jnt_limited_sh)
   m.nlimited_ball = len(jnt_limited_ball)
   m.neq_cw = int(np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD)).sum()) if mjm.neq else 0
-  m.nJmom = int(sum({JointType.FREE: 6, JointType.BALL: 3}.get(int(mjm.jnt_type[mjm.actuator_trnid[a, 0]]), 1) for a in range(mjm.nu)))
+  def _mom_nnz(a):
+    if int(mjm.actuator_trntype[a]) == types.TrnType.TENDON:
+      return int(mjm.ten_J_rownnz[mjm.actuator_trnid[a, 0]])
+    return {JointType.FREE: 6, JointType.BALL: 3}.get(int(mjm.jnt_type[mjm.actuator_trnid[a, 0]]), 1)
+
+  m.nJmom = int(sum(_mom_nnz(a) for a in range(mjm.nu)))
 
   # sparse path: kinematic trees as dof ranges (a tree starts at every dof without a parent dof),
   # J row width = the longest union of two dof chains (+ the 6 dofs of a flex edge)
@@ -332,7 +344,7 @@ DERIVED_INT_ARRAYS = {
   "tree_dofadr": "tree_dofadr", "flex_cgeomadr": "flex_cgeomadr", "flex_cgeom": "flex_cgeom", "plane_geom": "plane_geom",
   "flexvert_incadr": "flexvert_incadr", "flexvert_inc": "flexvert_inc",
 }
-DERIVED_SCALARS = ("nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow",
+DERIVED_SCALARS = ("nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz",
                    "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane")
 
 
@@ -423,6 +435,8 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     flexedge_J=(m.nflexedge, 6), flex_frc=(m.nflexelem * 9 + m.nflexedge * 12,),
     sp_body=(nb * 6 * sp,), sp_vec=(nv * 10 * sp,), sp_row=(njmax * 2 * sp,), sp_LD=(m.nM * sp,),
     efc_JT_val=(njmax_pad * m.njrow * sp,),
+    # fixed tendons (smooth.py:3085-3121): lengths, velocities, sparse Jacobian (ten_J_rowadr / _colind)
+    ten_length=(m.ntendon,), ten_velocity=(m.ntendon,), ten_J=(m.nJten,),
   )
   ints = dict(
     ne=(), nf=(), nl=(), nefc=(), solver_niter=(), moment_rownnz=(nu,), moment_rowadr=(nu,), moment_colind=(m.nJmom,),
