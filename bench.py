@@ -164,15 +164,14 @@ def parse():
   for k in ("nworld", "nconmax", "njmax", "solver"):
     if getattr(a, k) is None:
       setattr(a, k, cfg[k])
-  if a.pmc is None:  # the committed summary for this model taken on the current kernel sources, else the latest
-    import glob
+  if a.pmc is None:  # the committed summaries for this model (pmc_<model>[_<solver>]_rNN.json), newest first;
+    import glob    # main() takes the first one that matches the workload and the current kernel sources
 
-    from mujoco_warp_amd import build as _build
-
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{a.model}_r[0-9]*.json")), key=os.path.getmtime)
-    sha = _build.sources_hash()
-    same = [f for f in found if json.load(open(f)).get("csrc_sha") == sha]
-    a.pmc = (same or found or [""])[-1]
+    found = glob.glob(os.path.join(ROOT, "profiles", f"pmc_{a.model}_r[0-9]*.json"))
+    found += glob.glob(os.path.join(ROOT, "profiles", f"pmc_{a.model}_[a-z]*_r[0-9]*.json"))
+    a.pmc = sorted(set(found), key=lambda f: (os.path.basename(f).rsplit("_r", 1)[-1], os.path.getmtime(f)), reverse=True)
+  else:
+    a.pmc = [a.pmc]
   for k, dflt in (("steps", 1000), ("cpu_worlds", 1024), ("cpu_steps", 1000)):
     if getattr(a, k) is None:
       setattr(a, k, cfg.get(k, dflt))
@@ -493,7 +492,11 @@ def main():
     groups_alg = b_alg_groups(mjm, words, nefc_mean, ncon_mean, 2 * m.njrow if m.is_sparse else m.nv_pad, bool(m.is_sparse))
     # worlds per timed launch: shard 0's
     nlaunch = d.nworld
-    pmc, pmc_src = pmc_traffic(args.pmc, args.model, nlaunch, solver_name)
+    pmc, pmc_src = None, "no PMC summary"
+    for path in args.pmc:
+      pmc, pmc_src = pmc_traffic(path, args.model, nlaunch, solver_name)
+      if pmc is not None:
+        break
     roof = roofline_record(tab, groups_alg, nlaunch, pmc, pmc_src)
     if args.scaling == "weak":
       parallelism = f"{args.nworld} worlds per rank on {world} GPU(s) (weak), no collective"

@@ -416,14 +416,12 @@ __device__ void camlight(const mjw_model_t& m, const mjw_data_t& d, int wid) {
   for (int l = tid(); l < m.nlight; l += BLK) {
     const int mode = m.light_mode[l], b = m.light_bodyid[l], tgt = m.light_targetbodyid[l];
     const bool is_target = mode == CAM_TARGETBODY || mode == CAM_TARGETBODYCOM;
-    float* lx = d.light_xpos + ((long)wid * m.nlight + l) * 3;
-    float* ld = d.light_xdir + ((long)wid * m.nlight + l) * 3;
+    float lx[3], ld[3];  // built in registers, stored once (smooth.py:703-758)
     if ((is_target && tgt < 0) || mode == CAM_FIXED) {
       float t[3];
       rot_vec_quat(t, light_pos + 3 * l, xquat + 4 * b);
       for (int i = 0; i < 3; i++) lx[i] = xpos[3 * b + i] + t[i];
       rot_vec_quat(ld, light_dir + 3 * l, xquat + 4 * b);
-      if (is_target && tgt < 0) continue;
     } else if (mode == CAM_TRACK) {
       for (int i = 0; i < 3; i++) {
         ld[i] = light_dir0[3 * l + i];
@@ -442,6 +440,12 @@ __device__ void camlight(const mjw_model_t& m, const mjw_data_t& d, int wid) {
       for (int i = 0; i < 3; i++) ld[i] = tp[i] - lx[i];
     }
     normalize3(ld);
+    float* gx = d.light_xpos + ((long)wid * m.nlight + l) * 3;
+    float* gd = d.light_xdir + ((long)wid * m.nlight + l) * 3;
+    for (int i = 0; i < 3; i++) {
+      gx[i] = lx[i];
+      gd[i] = ld[i];
+    }
   }
 }
 

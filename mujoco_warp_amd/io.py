@@ -117,8 +117,6 @@ def put_model(mjm, device=None) -> types.Model:
   if getattr(mjm.opt, "noslip_iterations", 0) > 0:
     raise NotImplementedError("noslip solver not implemented.")
   sparse = is_sparse(mjm) or getattr(mjm, "nflex", 0) > 0
-  if getattr(mjm, "ntendon", 0):
-    raise NotImplementedError("tendons are not supported by this build yet.")
   if sparse:
     # the workgroup-per-world sparse / flex pipeline (csrc/mjw_sparse.hip) covers this subset
     if mjm.opt.solver != types.SolverType.CG:

@@ -231,5 +231,10 @@ def test_gpu_apollo_step_matches_oracle():
   torch.cuda.synchronize()
   assert np.isfinite(np_(d.qpos)).all()
   np.testing.assert_array_equal(d.nefc.cpu().numpy().reshape(-1), od.nefc.reshape(-1))
-  assert_close("qpos", np_(d.qpos), od.qpos, rtol=2e-3, atol=2e-3)
-  assert_close("sensordata[quat]", np_(d.sensordata)[:, :4], od.sensordata[:, :4], rtol=2e-3, atol=2e-3)
+  from tests.test_gpu_parity_strict import normwise_close
+
+  # normwise per world: qpos and the orientation sensor at the strict 1e-5, qvel at the reference's
+  # Newton qacc bar carried through 3 steps (solver_test.py:32)
+  normwise_close("qpos", np_(d.qpos), od.qpos)
+  normwise_close("sensordata[quat]", np_(d.sensordata)[:, :4], od.sensordata[:, :4])
+  normwise_close("qvel", np_(d.qvel), od.qvel, tol=5e-3)

@@ -131,18 +131,21 @@ def test_gpu_franka_forward():
   torch.cuda.synchronize()
   od.forward()
   nw, nv = 16, 9
+  from tests.test_gpu_parity_strict import normwise_close, strict_close
+
+  # the strict bar (tests/test_gpu_parity_strict.py): smooth outputs elementwise rtol 1e-5 with a
+  # 1e-6 * scale floor; rows J strict, aref through the impedance curve at 3e-4; qacc at the
+  # reference solver bar (solver_test.py:32)
   for name in ("xpos", "xquat", "cinert", "cdof", "actuator_force", "qfrc_actuator", "qfrc_passive", "qfrc_bias", "qfrc_smooth"):
-    got = np_(getattr(d, name)).reshape(nw, -1)
-    want = getattr(od, name)
-    assert_close(name, got, want, rtol=1e-3, atol=1e-4 * (np.abs(want).max() + 1e-9))
+    strict_close(name, np_(getattr(d, name)).reshape(nw, -1), getattr(od, name))
   assert np.array_equal(np_(d.ne).astype(int), od.ne[:, 0]) and np.array_equal(np_(d.nefc).astype(int), od.nefc[:, 0])
   for w in range(nw):
     n = int(d.nefc[w])
-    assert_close(f"J[w{w}]", np_(d.efc.J[w, :n, :nv]), od.efc_J[w].reshape(16, nv)[:n], rtol=1e-3, atol=1e-4)
-    assert_close(f"aref[w{w}]", np_(d.efc.aref[w, :n]), od.efc_aref[w, :n], rtol=2e-3, atol=2e-3)
-  qo = od.qacc
-  err = np.abs(np_(d.qacc) - qo) / (np.abs(qo).max(axis=1, keepdims=True) + 1.0)
-  assert np.median(err) < 5e-3
+    if n == 0:
+      continue
+    strict_close(f"J[w{w}]", np_(d.efc.J[w, :n, :nv]).reshape(1, -1), od.efc_J[w].reshape(16, nv)[:n].reshape(1, -1))
+    normwise_close(f"aref[w{w}]", np_(d.efc.aref[w, :n])[None], od.efc_aref[w, :n][None], tol=3e-4)
+  normwise_close("qacc", np_(d.qacc), od.qacc, tol=5e-3)
 
 
 @pytest.mark.gpu
@@ -158,8 +161,11 @@ def test_gpu_franka_implicitfast_rollout():
     mjw.step(m, d)
     od.step()
   torch.cuda.synchronize()
-  assert_close("qpos", np_(d.qpos), od.qpos, rtol=2e-3, atol=2e-3)
-  assert_close("qvel", np_(d.qvel), od.qvel, rtol=1e-2, atol=1e-2)
+  from tests.test_gpu_parity_strict import normwise_close
+
+  # normwise per world: qpos at the strict 1e-5, qvel at the solver bar (it carries 10 solves)
+  normwise_close("qpos", np_(d.qpos), od.qpos)
+  normwise_close("qvel", np_(d.qvel), od.qvel, tol=5e-3)
 
 
 @pytest.mark.gpu

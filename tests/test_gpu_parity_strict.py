@@ -281,3 +281,50 @@ def test_constraint_rows_strict():
     for f in ("D", "aref"):
       strict_close(f"efc.{f}[w{w}]", np_(getattr(d.efc, f)[w, :n])[None], getattr(od, "efc_" + f)[w, :n][None], rtol=3e-4)
   assert total > 10 * nworld
+
+
+@pytest.mark.parametrize("solver", ["CG", "NEWTON"])
+def test_step_with_contacts_nworld1(solver):
+  """C1 (humanoid, nworld = 1) through a contact step: the rows agree (count, type, order), the solve
+  from the same smooth state reaches the oracle's optimum (fp64 primal cost of the oracle's rows:
+  relative excess <= 1e-5, the reference's bar being 2.5 %, solver_test.py:308-322) with qacc
+  normwise 5e-3 (solver_test.py:32), and one full step gives qpos normwise 1e-5 and qvel 5e-3."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from tests.parity_models import efc_cost
+
+  mjm = humanoid_model(solver)
+  nv = mjm.nv
+  for seed in range(80, 120):  # the first state whose feet touch the floor
+    qpos, qvel, ctrl = random_states(mjm, 1, seed=seed)
+    om, od = oracle_from_state(mjm, qpos, qvel, ctrl)
+    od.fwd_position()
+    if int(od.nefc[0, 0]) >= 8:
+      break
+  n = int(od.nefc[0, 0])
+  assert n >= 8
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl)
+  om, od = oracle_from_state(mjm, qpos, qvel, ctrl)
+  for st in SMOOTH:
+    getattr(mjw, st)(m, d)
+    getattr(od, st)()
+  mjw.solve(m, d)
+  od.solve()
+  torch.cuda.synchronize()
+  assert int(d.nefc[0]) == n
+  assert np.array_equal(d.efc.type[0, :n].cpu().numpy(), od.efc_type[0, :n])
+  J = od.efc_J[0].reshape(od.njmax, nv)[:n]
+  M = od.qM[0].reshape(nv, nv)
+  args = (J, od.efc_D[0, :n], od.efc_aref[0, :n], od.efc_type[0, :n], M, od.qacc_smooth[0])
+  c_or = efc_cost(*args, od.qacc[0], fl=od.efc_frictionloss[0, :n])
+  c_gpu = efc_cost(*args, np_(d.qacc[0]), fl=od.efc_frictionloss[0, :n])
+  assert (c_gpu - c_or) / abs(c_or) <= 1e-5, (c_gpu, c_or)
+  normwise_close("qacc", np_(d.qacc), od.qacc, tol=5e-3)
+  m2, d2 = gpu_from_state(mjm, qpos, qvel, ctrl)
+  om2, od2 = oracle_from_state(mjm, qpos, qvel, ctrl)
+  mjw.step(m2, d2)
+  od2.step()
+  torch.cuda.synchronize()
+  normwise_close("qpos", np_(d2.qpos), od2.qpos)
+  normwise_close("qvel", np_(d2.qvel), od2.qvel, tol=5e-3)

@@ -1,217 +1,14 @@
-"""Per-field error report of the HIP path against the fp64 oracle on the C3 / C4 / C5 models (GPU box).
-
-For franka (scene.xml), apollo (scene_flat.xml, keyframe "stand"), cloth and aloha_cloth: every smooth
-stage's outputs, qM, qacc_smooth (normwise + fp64 backward error), the constraint rows (same count /
-order / type; J, pos, vel, D, aref), the solve from the oracle's own rows (fp64 cost ratio, qacc
-normwise) and one full step (qpos, qvel).  `norm` = max |got - want| / max |want| per world (worst
-world), `elem` = the smallest elementwise rtol passing with an absolute floor of 1e-6 * scale (the
-north-star rung of tests/test_gpu_parity_strict.py).  The strict model tests take their tolerances
-from this report (profiles/r03_parity_models.json).
+"""Per-field error report of the HIP path against the fp64 oracle on the C3 / C4 / C5 models (GPU box);
+the report itself lives in tests/parity_models.py.
 usage: python tools/parity_models.py [out.json] [model ...]
 """
 import json
 import os
 import sys
 
-import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
-
-from tests.common import franka_model, franka_states, gpu_from_state, np_, oracle_from_state  # noqa: E402
-
-SMOOTH = {
-  "fwd_position": ("xpos", "xquat", "xmat", "xipos", "ximat", "xanchor", "xaxis", "geom_xpos", "geom_xmat", "site_xpos", "site_xmat",
-                   "subtree_com", "cinert", "cdof", "crb", "cam_xpos", "cam_xmat", "light_xpos", "light_xdir", "actuator_length",
-                   "flexvert_xpos", "flexedge_length"),
-  "fwd_velocity": ("actuator_velocity", "cvel", "cdof_dot", "qfrc_spring", "qfrc_damper", "qfrc_passive", "qfrc_bias", "flexedge_velocity"),
-  "fwd_actuation": ("actuator_force", "qfrc_actuator"),
-  "fwd_acceleration": ("qfrc_smooth",),
-}
-
-
-def err(got, want):
-  got = np.asarray(got, np.float64).reshape(len(want), -1)
-  want = np.asarray(want, np.float64).reshape(len(want), -1)
-  if want.size == 0:
-    return None
-  scale = np.abs(want).max(axis=1, keepdims=True) + 1e-30
-  e = np.abs(got - want)
-  return dict(norm=float((e / scale).max()), elem=float((np.maximum(e - 1e-6 * scale, 0) / np.maximum(np.abs(want), 1e-30)).max()))
-
-
-def merge(a, b):
-  if a is None:
-    return b
-  if b is None:
-    return a
-  return dict(norm=max(a["norm"], b["norm"]), elem=max(a["elem"], b["elem"]))
-
-
-def setup(name):
-  """(mjm, qpos, qvel, ctrl, njmax, nconmax, nworld) of a C3-C5 parity workload."""
-  import mujoco_warp_amd as mjw
-
-  if name == "franka":
-    mjm = franka_model()
-    # pools sized so that neither side drops rows or contacts (the device pool is global, the
-    # oracle's per world): fingertip pads and the hand can make up to 10 floor contacts
-    return (mjm,) + franka_states(mjm, 16, seed=22) + (64, 16, 16)
-  if name == "apollo":
-    mjm = mjw.load_model(os.path.join(ROOT, "models", "apptronik_apollo", "scene_flat.xml"))
-    nworld = 32
-    rng = np.random.default_rng(7)
-    qpos = np.tile(mjm.key_qpos[0], (nworld, 1))
-    qpos[:, 7:] += rng.normal(0, 0.05, (nworld, mjm.nq - 7))
-    qvel = rng.normal(0, 0.2, (nworld, mjm.nv))
-    ctrl = np.tile(mjm.key_ctrl[0], (nworld, 1))
-    return mjm, qpos, qvel, ctrl, 64, 16, nworld
-  from tests.cloth_common import aloha_model, aloha_states, cloth_model, cloth_states
-
-  if name == "cloth":
-    mjm = cloth_model()
-    return (mjm,) + cloth_states(mjm, 2, seed=1) + (3000, 200, 2)
-  mjm = aloha_model()
-  return (mjm,) + aloha_states(mjm, 2, seed=1) + (16384, 4096, 2)
-
-
-def dense_M(mjm, d, od, w):
-  nv = mjm.nv
-  if int(np.asarray(mjm.opt.jacobian)) == 1 or d.qM.dim() == 2:
-    from tests.cloth_common import dense_qM
-
-    return dense_qM(mjm, np_(d.qM[w])), od.qM[w].reshape(nv, nv)
-  return np_(d.qM[w])[:nv, :nv], od.qM[w].reshape(nv, nv)
-
-
-def rows_of(mjm, d, od, w, sparse, njmax):
-  """(gpu row ids, oracle row ids, dense gpu J rows): identical order on the dense path; through the
-  matched contacts on the sparse path (tests/test_cloth.py)."""
-  nv = mjm.nv
-  n = min(int(od.nefc[w, 0]), njmax)
-  if not sparse:
-    return np.arange(n), np.arange(n), np_(d.efc.J[w, :n, :nv])
-  from tests.cloth_common import dense_J, gpu_contacts, oracle_contacts
-  from tests.test_cloth import _match_rows
-
-  pairs = _match_rows(d, od, w, gpu_contacts(d, w), oracle_contacts(od, w))
-  g = np.array([p[0] for p in pairs], dtype=int)
-  o = np.array([p[1] for p in pairs], dtype=int)
-  return g, o, dense_J(d, w, n, nv)[g]
-
-
-def efc_cost(J, D, aref, types_, M, qacc_smooth, qacc, fl=None, nf=0):
-  """fp64 primal cost (solver.py): Gauss term + rows; equality always quadratic, friction loss
-  Huber, limits / contacts quadratic while J qacc - aref < 0."""
-  dq = qacc - qacc_smooth
-  jar = J @ qacc - aref
-  c = 0.5 * dq @ M @ dq
-  for i in range(len(jar)):
-    t = types_[i]
-    if t == 0:
-      c += 0.5 * D[i] * jar[i] ** 2
-    elif t == 1:
-      f = fl[i]
-      rf = f / D[i] if D[i] > 0 else 0.0
-      if jar[i] <= -rf:
-        c += -f * (0.5 * rf + jar[i])
-      elif jar[i] >= rf:
-        c += -f * (0.5 * rf - jar[i])
-      else:
-        c += 0.5 * D[i] * jar[i] ** 2
-    elif jar[i] < 0:
-      c += 0.5 * D[i] * jar[i] ** 2
-  return c
-
-
-def report(name):
-  import torch
-
-  import mujoco_warp_amd as mjw
-
-  mjm, qpos, qvel, ctrl, njmax, nconmax, nworld = setup(name)
-  sparse = bool(mjw.put_model(mjm, device="cpu").is_sparse)
-  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=nconmax)
-  om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=nconmax)
-  out = {"nworld": nworld, "sparse": sparse, "fields": {}}
-  for st, fields in SMOOTH.items():
-    getattr(mjw, st)(m, d)
-    getattr(od, st)()
-    torch.cuda.synchronize()
-    for f in fields:
-      g = getattr(d, f, None)
-      if g is None or g.numel() == 0:
-        continue
-      try:
-        want = getattr(od, f)
-      except AttributeError:
-        continue
-      e = err(np_(g).reshape(nworld, -1), want)
-      if e is not None:
-        out["fields"][f] = e
-  nv = mjm.nv
-  eM = None
-  bw = 0.0
-  for w in range(nworld):
-    Mg, Mo = dense_M(mjm, d, od, w)
-    eM = merge(eM, err(Mg[None], Mo[None]))
-    r = Mo @ np_(d.qacc_smooth[w]) - od.qfrc_smooth[w]
-    bw = max(bw, float(np.abs(r).max() / (np.abs(od.qfrc_smooth[w]).max() + 1e-300)))
-  out["fields"]["qM"] = eM
-  out["fields"]["qacc_smooth"] = err(np_(d.qacc_smooth), od.qacc_smooth)
-  out["qacc_smooth_backward"] = bw
-  # rows
-  counts_equal = all(int(d.nefc[w]) == int(od.nefc[w, 0]) for w in range(nworld))
-  out["rows_counts_equal"] = bool(counts_equal)
-  rowerr = {}
-  types_equal = True
-  nrows = 0
-  for w in range(nworld):
-    g, o, Jg = rows_of(mjm, d, od, w, sparse, njmax)
-    nrows += len(o)
-    Jo = od.efc_J[w].reshape(njmax, nv)[o]
-    types_equal &= bool(np.array_equal(d.efc.type[w].cpu().numpy()[g], od.efc_type[w][o]))
-    if len(o) == 0:
-      continue
-    rowerr["J"] = merge(rowerr.get("J"), err(Jg.reshape(1, -1), Jo.reshape(1, -1)))
-    for f in ("pos", "vel", "D", "aref"):
-      rowerr[f] = merge(rowerr.get(f), err(np_(getattr(d.efc, f)[w])[g][None], getattr(od, "efc_" + f)[w][o][None]))
-    rowerr["pos_abs"] = max(rowerr.get("pos_abs", 0.0), float(np.abs(np_(d.efc.pos[w])[g] - od.efc_pos[w][o]).max()))
-  out["rows"] = rowerr
-  out["rows_types_equal"] = types_equal
-  out["rows_total"] = nrows
-  # solve from the same smooth state: the oracle's rows define the fp64 cost
-  mjw.solve(m, d)
-  od.solve()
-  torch.cuda.synchronize()
-  ratio, qn = 0.0, 0.0
-  for w in range(nworld):
-    n = min(int(od.nefc[w, 0]), njmax)
-    Mg, Mo = dense_M(mjm, d, od, w)
-    J = od.efc_J[w].reshape(njmax, nv)[:n]
-    args = (J, od.efc_D[w, :n], od.efc_aref[w, :n], od.efc_type[w, :n], Mo, od.qacc_smooth[w])
-    c_or = efc_cost(*args, od.qacc[w], fl=od.efc_frictionloss[w, :n])
-    c_gpu = efc_cost(*args, np_(d.qacc[w]), fl=od.efc_frictionloss[w, :n])
-    c_0 = efc_cost(*args, od.qacc_smooth[w], fl=od.efc_frictionloss[w, :n])
-    # relative excess over the oracle optimum, in units of the cost reduction the solve achieved
-    ratio = max(ratio, (c_gpu - c_or) / max(abs(c_or), 1e-300))
-    qn = max(qn, float(np.abs(np_(d.qacc[w]) - od.qacc[w]).max() / (np.abs(od.qacc[w]).max() + 1e-300)))
-    _ = c_0
-  out["solve_cost_excess"] = ratio
-  out["solve_qacc_norm"] = qn
-  out["solver_niter_gpu"] = np_(d.solver_niter).ravel().tolist()
-  out["solver_niter_oracle"] = np.asarray(od.solver_niter).ravel().tolist()
-  # one full step from the initial state
-  m2, d2 = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=nconmax)
-  om2, od2 = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=nconmax)
-  mjw.step(m2, d2)
-  od2.step()
-  torch.cuda.synchronize()
-  for f in ("qpos", "qvel", "qacc"):
-    out["step_" + f] = err(np_(getattr(d2, f)), getattr(od2, f))
-  if mjm.nsensordata:
-    out["step_sensordata"] = err(np_(d2.sensordata), od2.sensordata)
-  return out
+from tests.parity_models import report  # noqa: E402
 
 
 def main():
