@@ -50,19 +50,22 @@ def test_launcher_command_without_gpu(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_gpu_bench_two_ranks_weak_equals_single(tmp_path):
-  common = ["--steps", "5", "--warmup", "2", "--cpu-baseline", "0", "--graph", "0"]
-  two = _run(["--gpus", "2", "--nworld", "256", "--dump-qpos", str(tmp_path / "two")] + common)
+@pytest.mark.parametrize("model,per_rank", [("humanoid", 256), ("apollo", 64)])
+def test_gpu_bench_two_ranks_weak_equals_single(tmp_path, model, per_rank):
+  """C2 and C4 (apollo: Newton, sensors, box-box CCD) sharded over two ranks: each rank's worlds
+  bitwise equal to the same global worlds of one 2 x per_rank run."""
+  common = ["--model", model, "--steps", "5", "--warmup", "2", "--cpu-baseline", "0", "--graph", "0"]
+  two = _run(["--gpus", "2", "--nworld", str(per_rank), "--dump-qpos", str(tmp_path / "two")] + common)
   assert two["n_gpus"] == 2 and two["scaling"] == "weak"
-  assert two["config"]["nworld_total"] == 512 and two["config"]["converged_worlds"] == 512
-  one = _run(["--gpus", "1", "--nworld", "512", "--dump-qpos", str(tmp_path / "one")] + common)
+  assert two["config"]["nworld_total"] == 2 * per_rank and two["config"]["converged_worlds"] == 2 * per_rank
+  one = _run(["--gpus", "1", "--nworld", str(2 * per_rank), "--dump-qpos", str(tmp_path / "one")] + common)
   assert one["n_gpus"] == 1
   q1 = np.load(tmp_path / "one" / "qpos_rank0.npz")["qpos"]
   for r in range(2):
     z = np.load(tmp_path / "two" / f"qpos_rank{r}.npz")
     off = int(z["offset"])
-    assert off == 256 * r
-    np.testing.assert_array_equal(z["qpos"], q1[off:off + 256])
+    assert off == per_rank * r
+    np.testing.assert_array_equal(z["qpos"], q1[off:off + per_rank])
 
 
 @pytest.mark.gpu
