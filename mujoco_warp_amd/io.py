@@ -577,7 +577,8 @@ def cdata(d: types.Data) -> _lib.CData:
     setattr(c, n, t.data_ptr())
   c.nacon = d.nacon.data_ptr()
   c.ncollision = d.ncollision.data_ptr()
-  c.sched = d.sched.data_ptr()
+  # world-order workspace; None -> the dense kernels run the worlds in identity order
+  c.sched = d.sched.data_ptr() if d.sched is not None else None
   d._cdata_cache = (c, key, tensors)
   return c
 

@@ -193,3 +193,36 @@ def test_gpu_act_callbacks_run_between_force_and_moment_map():
   np.testing.assert_array_equal(np_(d.qfrc_actuator), np_(d2.qfrc_actuator))
   np.testing.assert_array_equal(np_(d.qpos), np_(d2.qpos))
   np.testing.assert_array_equal(np_(d.qvel), np_(d2.qvel))
+
+
+@pytest.mark.gpu
+def test_gpu_world_order_does_not_change_results():
+  """The dense path's longest-first world order (d.sched, mjw_step.hip reset_counters_kernel): after a
+  step, world_order is a permutation of the worlds ordered by the recorded iteration buckets, and 5
+  steps give bitwise the same state as with d.sched = None (identity order)."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from tests.common import gpu_from_state, humanoid_model, np_, random_states
+
+  mjm = humanoid_model("CG")
+  nworld = 257
+  qpos, qvel, ctrl = random_states(mjm, nworld, seed=90)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl)
+  m2, d2 = gpu_from_state(mjm, qpos, qvel, ctrl)
+  d2.sched = None
+  for i in range(5):
+    if i == 4:
+      torch.cuda.synchronize()
+      key4 = d.world_key.cpu().numpy().copy()  # the buckets step 4 recorded
+    mjw.step(m, d)
+    mjw.step(m2, d2)
+  torch.cuda.synchronize()
+  for f in ("qpos", "qvel", "qacc", "act", "solver_niter"):
+    assert np.array_equal(np_(getattr(d, f)), np_(getattr(d2, f))), f
+  # step 5 walked the permutation its counter-reset kernel built from step 4's buckets: most
+  # iterations (smallest key) first
+  order = d.world_order.cpu().numpy()
+  assert sorted(order.tolist()) == list(range(nworld))
+  assert np.all(np.diff(key4[order]) >= 0)
+  assert len(np.unique(key4)) > 1
