@@ -61,18 +61,22 @@ __device__ __forceinline__ float symv(const f32x16& A, const float* vec, int h) 
 // On return a[] holds row (lane&31) of L (A = L L^T, upper part zero); the result is
 // A^-1 in accumulator layout.  All broadcasts are v_readlane into SGPRs, so the only
 // live VGPR arrays are a[32], x[32] and the accumulator.
-template <bool STORE_L = false>
+// NB (>= n, compile time): the factor and substitution loops stop there -- rows and columns past n
+// are the identity, which the skipped steps would leave unchanged (exact), so a model with nv <= 16
+// does a quarter of the readlane / FMA work of the full 32 (the unrolled schedule is kept: no
+// runtime early-outs, which measured slower)
+template <bool STORE_L = false, int NB = 32>
 __device__ __forceinline__ f32x16 spd_inverse(float (&a)[32], int lane, float* S = nullptr) {
   const int c = lane & 31;
   // right-looking Cholesky, rows in lanes (wp.tile_cholesky, smooth.py:2860-2928);
   // 1/L[j][j] by v_rsq_f32 keeps the per-column critical path short
 #pragma unroll
-  for (int j = 0; j < 32; j++) {
+  for (int j = 0; j < NB; j++) {
     float piv = rdlane(a[j], j);
     float inv = __builtin_amdgcn_rsqf(piv);
     a[j] = (c > j) ? a[j] * inv : (c == j ? piv * inv : 0.0f);
 #pragma unroll
-    for (int k = j + 1; k < 32; k++) a[k] = fmaf(-a[j], rdlane(a[j], k), a[k]);
+    for (int k = j + 1; k < NB; k++) a[k] = fmaf(-a[j], rdlane(a[j], k), a[k]);
   }
   if (STORE_L && lane < 32) {
     f32x4* rw = reinterpret_cast<f32x4*>(S + c * DSS);
@@ -85,10 +89,10 @@ __device__ __forceinline__ f32x16 spd_inverse(float (&a)[32], int lane, float* S
 #pragma unroll
   for (int j = 0; j < 32; j++) x[j] = (c == j) ? 1.0f : 0.0f;
 #pragma unroll
-  for (int k = 0; k < 32; k++) {
+  for (int k = 0; k < NB; k++) {
     x[k] *= __builtin_amdgcn_rcpf(rdlane(a[k], k));
 #pragma unroll
-    for (int j = k + 1; j < 32; j++) x[j] = fmaf(-rdlane(a[k], j), x[k], x[j]);
+    for (int j = k + 1; j < NB; j++) x[j] = fmaf(-rdlane(a[k], j), x[k], x[j]);
   }
   // A^-1 = X^T X : 16 x (32x32x2) f32 MFMA in two independent chains, operand X[2t + h][c]
   const bool hi = lane >= 32;
@@ -103,16 +107,17 @@ __device__ __forceinline__ f32x16 spd_inverse(float (&a)[32], int lane, float* S
   return r0 + r1;
 }
 
-// Cholesky in place (rows in lanes) and L rows -> S; no inverse
+// Cholesky in place (rows in lanes) and L rows -> S; no inverse (NB as in spd_inverse)
+template <int NB = 32>
 __device__ __forceinline__ void chol_factor(float (&a)[32], int lane, float* S) {
   const int c = lane & 31;
 #pragma unroll
-  for (int j = 0; j < 32; j++) {
+  for (int j = 0; j < NB; j++) {
     float piv = rdlane(a[j], j);
     float inv = __builtin_amdgcn_rsqf(piv);
     a[j] = (c > j) ? a[j] * inv : (c == j ? piv * inv : 0.0f);
 #pragma unroll
-    for (int k = j + 1; k < 32; k++) a[k] = fmaf(-a[j], rdlane(a[j], k), a[k]);
+    for (int k = j + 1; k < NB; k++) a[k] = fmaf(-a[j], rdlane(a[j], k), a[k]);
   }
   __syncthreads();
   if (lane < 32) {
@@ -124,16 +129,17 @@ __device__ __forceinline__ void chol_factor(float (&a)[32], int lane, float* S) 
 }
 
 // (L L^T) x = b for a dof vector b (lane c, both halves): forward sweep with L rows in
-// registers, backward sweep with L columns read from S (wp.tile_cholesky_solve)
+// registers, backward sweep with L columns read from S (wp.tile_cholesky_solve); b = 0 past NB
+template <int NB = 32>
 __device__ __forceinline__ float chol_solve(const float (&a)[32], const float* S, int lane, float b) {
   const int c = lane & 31;
 #pragma unroll
-  for (int k = 0; k < 32; k++) {
+  for (int k = 0; k < NB; k++) {
     float yk = rdlane(b, k) * __builtin_amdgcn_rcpf(rdlane(a[k], k));
     b = (c > k) ? fmaf(-a[k], yk, b) : (c == k ? yk : b);
   }
 #pragma unroll
-  for (int k = 31; k >= 0; k--) {
+  for (int k = NB - 1; k >= 0; k--) {
     float xk = rdlane(b, k) * __builtin_amdgcn_rcpf(S[k * DSS + k]);
     b = (c < k) ? fmaf(-S[k * DSS + c], xk, b) : (c == k ? xk : b);
   }
@@ -211,10 +217,11 @@ __device__ __forceinline__ float actuator_vel_deriv(const mjw_model_t& m, const 
   return vel;
 }
 
-// lane r: sum_k J[r][k] v[k] over k < 4*nq
+// lane r: sum_k J[r][k] v[k] over k < 4*nq (JS: the LDS row stride of J)
+template <int JS = DJS>
 __device__ __forceinline__ float gemv_rows(const float* Jl, const float* vec, int lane, int nq) {
   const f32x4* v4 = reinterpret_cast<const f32x4*>(vec);
-  const float* jr = Jl + lane * DJS;
+  const float* jr = Jl + lane * JS;
   float p0 = 0.0f, p1 = 0.0f;
   for (int q = 0; q < nq; q++) {
     f32x4 v = v4[q];
@@ -226,20 +233,23 @@ __device__ __forceinline__ float gemv_rows(const float* Jl, const float* vec, in
   return p0 + p1;
 }
 
-// lane c (both halves): sum_r J[r][c] f[r]; half h sums rows 32h + [0, 4*nq)
+// lane c (both halves): sum_r J[r][c] f[r]; half h sums rows 32h + [0, 4*nq); J holds JS - 1 columns
+// (lanes past them return 0)
+template <int JS = DJS>
 __device__ __forceinline__ float gemv_cols(const float* Jl, const float* fvec, int lane, int nq) {
   const int c = lane & 31, h = lane >> 5;
+  const bool in = c < JS - 1;
   const f32x4* f4 = reinterpret_cast<const f32x4*>(fvec + 32 * h);
-  const float* jc = Jl + 32 * h * DJS + c;
+  const float* jc = Jl + 32 * h * JS + (in ? c : 0);
   float p0 = 0.0f, p1 = 0.0f;
   for (int q = 0; q < nq; q++) {
     f32x4 f = f4[q];
-    p0 = fmaf(jc[(4 * q + 0) * DJS], f.x, p0);
-    p1 = fmaf(jc[(4 * q + 1) * DJS], f.y, p1);
-    p0 = fmaf(jc[(4 * q + 2) * DJS], f.z, p0);
-    p1 = fmaf(jc[(4 * q + 3) * DJS], f.w, p1);
+    p0 = fmaf(jc[(4 * q + 0) * JS], f.x, p0);
+    p1 = fmaf(jc[(4 * q + 1) * JS], f.y, p1);
+    p0 = fmaf(jc[(4 * q + 2) * JS], f.z, p0);
+    p1 = fmaf(jc[(4 * q + 3) * JS], f.w, p1);
   }
-  return xhalf_add(p0 + p1);
+  return xhalf_add(in ? p0 + p1 : 0.0f);
 }
 
 // ---- solver row math (solver.py:886-1341 linesearch, 2154-2219 update_constraint) -----------
@@ -356,21 +366,35 @@ __device__ __forceinline__ float row_force(const Row& w, int& state, float& cost
 // elliptic-cone workspace (ELL): per row D, cone coefficient, two scratch rows, first row / dim of its
 // contact, and the 6 cone-Hessian coefficients of the row (Newton)
 constexpr int DE_WORDS = 6 * 64 + 6 * 64;
-template <int FLAGS, bool NEWTON, bool ELL = false>
+// LDS row stride of the staged J: 33 (32 columns), 17 for the NB = 16 kernels (16 columns)
+template <int NB>
+__host__ __device__ constexpr int dense_js() { return NB <= 16 ? 17 : DJS; }
+template <int FLAGS, bool NEWTON, bool ELL = false, int NB = 32>
+__host__ __device__ constexpr int dense_j_words() {
+  // CG: the 32x32 scratch aliases J, so the region is the larger of the two
+  return (NEWTON && (FLAGS & DF_SOLVE)) ? 64 * dense_js<NB>() : (64 * dense_js<NB>() > DS_WORDS ? 64 * dense_js<NB>() : DS_WORDS);
+}
+template <int FLAGS, bool NEWTON, bool ELL = false, int NB = 32>
 __host__ __device__ constexpr int dense_lds_words() {
-  return ((NEWTON && (FLAGS & DF_SOLVE)) ? DJ_WORDS + DS_WORDS : DJ_WORDS) + 5 * 64 + (ELL && (FLAGS & DF_SOLVE) ? DE_WORDS : 0);
+  // launches without the solve stage no J, only the 32x32 scratch (the Euler-only kernel: 5.9 KB)
+  return ((NEWTON && (FLAGS & DF_SOLVE)) ? dense_j_words<FLAGS, NEWTON, ELL, NB>() + DS_WORDS
+          : (FLAGS & DF_SOLVE)           ? dense_j_words<FLAGS, NEWTON, ELL, NB>()
+                                         : DS_WORDS) +
+         5 * 64 + (ELL && (FLAGS & DF_SOLVE) ? DE_WORDS : 0);
 }
 
 
 // factor / solve / integrate of world `wid` by the calling wavefront; sm: dense_lds_words() floats of
 // LDS, 16-B aligned (the dense kernel's own, or the fused step kernel's dynamic LDS once the
 // forward stages are done with it)
-template <int FLAGS, bool NEWTON, bool ELL = false>
+template <int FLAGS, bool NEWTON, bool ELL = false, int NB = 32>
 __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data_t& d, const int wid, float* sm) {
   constexpr bool NT = NEWTON && (FLAGS & DF_SOLVE);
   constexpr bool EL = ELL && (FLAGS & DF_SOLVE);
-  constexpr int S_OFF = NT ? DJ_WORDS : 0;  // CG: the 32x32 scratch aliases J (used before J is staged)
-  constexpr int V_OFF = NT ? DJ_WORDS + DS_WORDS : DJ_WORDS;
+  constexpr int JS = dense_js<NB>(), JC = JS - 1;  // J row stride and staged columns
+  constexpr int JW = dense_j_words<FLAGS, NEWTON, ELL, NB>();
+  constexpr int S_OFF = NT ? JW : 0;  // CG: the 32x32 scratch aliases J (used before J is staged)
+  constexpr int V_OFF = NT ? JW + DS_WORDS : (FLAGS & DF_SOLVE) ? JW : DS_WORDS;
   float* Jl = sm;
   float* S = sm + S_OFF;
   float* vd = sm + V_OFF;        // dof vector broadcast buffer (32)
@@ -425,7 +449,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
     // ---- factor M, form M^-1, qacc_smooth (smooth.py:2860-2928 factor_solve_i)
     float a[32];
     stage_spd(d.qM + (long)wid * np * np, np, nv, nullptr, 0.0f, S, lane, a, Mm);
-    Mi = spd_inverse<(FLAGS & DF_FACTOR) != 0>(a, lane, S);
+    Mi = spd_inverse<(FLAGS & DF_FACTOR) != 0, NB>(a, lane, S);
     if (FLAGS & DF_FACTOR) {
       // L rows -> qLD (nv x nv) through S for coalesced stores
       __syncthreads();
@@ -460,20 +484,20 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       }
       if (lane == 0) d.solver_niter[wid] = 0;
     } else {
-      // stage J (zero padded to 64 x 32), 16 loads in flight per lane and batch
+      // stage J (zero padded to 64 x JC), 16 loads in flight per lane and batch
       const float* gJ = d.efc_J + (long)wid * d.njmax_pad * np;
 #pragma unroll
-      for (int half = 0; half < 2; half++) {
+      for (int half = 0; half < JC / 16; half++) {
         float v[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-          const int e = lane + 64 * (16 * half + q), r = e >> 5, k = e & 31;
+          const int e = lane + 64 * (16 * half + q), r = e / JC, k = e % JC;
           v[q] = gJ[(r < nefc && k < nv) ? r * np + k : 0];
         }
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-          const int e = lane + 64 * (16 * half + q), r = e >> 5, k = e & 31;
-          Jl[r * DJS + k] = (r < nefc && k < nv) ? v[q] : 0.0f;
+          const int e = lane + 64 * (16 * half + q), r = e / JC, k = e % JC;
+          Jl[r * JS + k] = (r < nefc && k < nv) ? v[q] : 0.0f;
         }
       }
       Row w;
@@ -520,7 +544,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       if (lo) vd[c] = qacc;
       __syncthreads();
       ma = symv(Mm, vd, h);
-      w.jaref = gemv_rows(Jl, vd, lane, nvq) - aref;
+      w.jaref = gemv_rows<JS>(Jl, vd, lane, nvq) - aref;
       const int nrq = (min(nefc, 32) + 3) >> 2;
 
       float cost, gauss, qfrc_c, grad, Mgrad, grad_dot;
@@ -559,7 +583,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         if (!row) { force = 0.0f; rc = 0.0f; }
         vr[lane] = force;
         __syncthreads();
-        qfrc_c = gemv_cols(Jl, vr, lane, nrq);
+        qfrc_c = gemv_cols<JS>(Jl, vr, lane, nrq);
         gauss = 0.5f * dsum(lo ? (ma - qfrc_smooth) * (qacc - qacc_smooth) : 0.0f);
         cost = dsum(rc) + gauss;
       };
@@ -611,12 +635,12 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
           const int npair = (nefc + 1) >> 1;
           for (int t = 0; t < npair; t++) {
             int r = 2 * t + h;
-            float jrc = Jl[r * DJS + c];
+            float jrc = c < JC ? Jl[r * JS + c] : 0.0f;
             float wrc = vr2[r] * jrc;
             if (EL) {
               wrc = 0.0f;
               const int r0 = eR0[r], dm_ = eDim[r];
-              for (int k = 0; k < dm_; k++) wrc = fmaf(eC[6 * r + k], Jl[(r0 + k) * DJS + c], wrc);
+              for (int k = 0; k < dm_; k++) wrc = fmaf(eC[6 * r + k], c < JC ? Jl[(r0 + k) * JS + c] : 0.0f, wrc);
             }
             H = __builtin_amdgcn_mfma_f32_32x32x2f32(jrc, wrc, H, 0, 0, 0);
           }
@@ -634,8 +658,8 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
             f32x4 v = rw[q];
             a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
           }
-          chol_factor(a, lane, S);
-          Mgrad = chol_solve(a, S, lane, grad);
+          chol_factor<NB>(a, lane, S);
+          Mgrad = chol_solve<NB>(a, S, lane, grad);
         } else {
           __syncthreads();
           Mgrad = symv(Mi, vd2, h);
@@ -656,7 +680,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         if (lo) vd[c] = search;
         __syncthreads();
         float mv = symv(Mm, vd, h);
-        w.jv = gemv_rows(Jl, vd, lane, nvq);
+        w.jv = gemv_rows<JS>(Jl, vd, lane, nvq);
         const float snorm = sqrtf(search_dot);
         const float gtol = fmaxf(tolerance * ls_tolerance * snorm * meaninertia * (float)nv, 1e-6f);
         const float q1 = dsum(lo ? search * (ma - qfrc_smooth) : 0.0f);
@@ -817,10 +841,9 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       }
       stage_rows(nv, S, lane, a, Md);
       __syncthreads();
-      f32x16 Mdi = spd_inverse(a, lane);
-      if (lo) vd[c] = ma;
-      __syncthreads();
-      qacc_adv = symv(Mdi, vd, h);
+      // one solve with the factor (forward + backward sweep), no explicit inverse
+      chol_factor<NB>(a, lane, S);
+      qacc_adv = chol_solve<NB>(a, S, lane, dof ? ma : 0.0f);
       if (!dof) qacc_adv = 0.0f;
     }
     // activations (forward.py:132-168)

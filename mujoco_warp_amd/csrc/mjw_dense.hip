@@ -10,16 +10,21 @@ namespace mjw {
 // 0.295 -> 0.288 ms at 3, 0.287 ms at 2
 // ELL: elliptic friction cones (opt.cone = ELLIPTIC), a separate instantiation so that the pyramidal
 // kernels keep their registers
-template <int FLAGS, bool NEWTON, bool ELL>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+// NB: the compile-time bound of the factor / substitution loops (>= nv; 16, 28 or 32, mjw_dense.h).
+// The NB = 16 instances fit 128 VGPRs (4 waves/SIMD, 16 worlds/CU); the Euler-only one (5.9 KB of LDS,
+// 27 worlds/CU) fits 64.
+template <int FLAGS, int NB>
+constexpr int dense_waves_per_eu() { return FLAGS == DF_EULER ? 6 : (NB <= 16 ? 4 : 3); }
+template <int FLAGS, bool NEWTON, bool ELL, int NB>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(dense_waves_per_eu<FLAGS, NB>())))
 dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
-  __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON, ELL>()];
+  __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON, ELL, NB>()];
   const int b = w0 + (int)blockIdx.x;
   if (b >= d.nworld) return;
   // d.sched set: worlds in the counter-reset kernel's longest-first order (world_order is a permutation)
   const int wid = d.sched ? d.world_order[b] : b;
   WLOG_T0();
-  dense_world<FLAGS, NEWTON, ELL>(m, d, wid, sm);
+  dense_world<FLAGS, NEWTON, ELL, NB>(m, d, wid, sm);
   if ((FLAGS & DF_SOLVE) && d.sched && (threadIdx.x & 63) == 0) {
     // the next step's order: bucket by this step's iterations, most iterations first
     const int key = MJW_SCHED_BUCKETS - 1 - min(d.solver_niter[wid] >> 1, MJW_SCHED_BUCKETS - 1);
@@ -30,7 +35,8 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
 }
 
 // device self-checks of the primitives above (mjw_selftest): which = 0 -> per-wave dsum and
-// xhalf_add of 64-lane chunks; which = 1 -> spd_inverse of 32x32 row-major SPD matrices
+// xhalf_add of 64-lane chunks; which = 1 -> spd_inverse of 32x32 row-major SPD matrices; which = 2 ->
+// the same with the factor bound NB = 16 (matrices that are the identity past row / column 16)
 __global__ void __launch_bounds__(64) selftest_kernel(int which, const float* in, float* out, int n) {
   __shared__ __attribute__((aligned(16))) float S[DS_WORDS];
   const int w = blockIdx.x, lane = threadIdx.x;
@@ -44,11 +50,18 @@ __global__ void __launch_bounds__(64) selftest_kernel(int which, const float* in
     float a[32];
     f32x16 M;
     stage_spd(in + (long)w * 1024, 32, 32, nullptr, 0.0f, S, lane, a, M);
-    f32x16 Mi = spd_inverse(a, lane);
+    // which = 2: the NB = 16 bound (input identity past 16)
+    f32x16 Mi = which == 2 ? spd_inverse<false, 16>(a, lane) : spd_inverse(a, lane);
     const int c = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int r = 0; r < 16; r++) out[(long)w * 1024 + acc_row(r, h) * 32 + c] = Mi[r];
   }
+}
+
+template <int FLAGS, int NB>
+void launch_nb(bool newton, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int w0, int count) {
+  if (newton) hipLaunchKernelGGL((dense_kernel<FLAGS, true, false, NB>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+  else hipLaunchKernelGGL((dense_kernel<FLAGS, false, false, NB>), dim3(count), dim3(64), 0, s, *m, *d, w0);
 }
 
 template <int FLAGS>
@@ -56,14 +69,20 @@ hipError_t launch_flags(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s
   const bool newton = m->opt_solver == SOLVER_NEWTON;
   // the cone only matters to the solve; Euler-only / factor-only launches use the pyramidal kernels
   const bool ell = (FLAGS & DF_SOLVE) && m->opt_cone == CONE_ELLIPTIC;
+  int nbi = 0;  // factor bound: 0 -> 32, 1 -> 16, 2 -> 28 (the kernel id and name carry it)
   if (ell) {
-    if (newton) hipLaunchKernelGGL((dense_kernel<FLAGS, true, true>), dim3(count), dim3(64), 0, s, *m, *d, w0);
-    else hipLaunchKernelGGL((dense_kernel<FLAGS, false, true>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+    if (newton) hipLaunchKernelGGL((dense_kernel<FLAGS, true, true, 32>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+    else hipLaunchKernelGGL((dense_kernel<FLAGS, false, true, 32>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+  } else if (m->nv <= 16) {
+    launch_nb<FLAGS, 16>(newton, m, d, s, w0, count);
+    nbi = 1;
+  } else if (m->nv <= 28) {
+    launch_nb<FLAGS, 28>(newton, m, d, s, w0, count);
+    nbi = 2;
   } else {
-    if (newton) hipLaunchKernelGGL((dense_kernel<FLAGS, true, false>), dim3(count), dim3(64), 0, s, *m, *d, w0);
-    else hipLaunchKernelGGL((dense_kernel<FLAGS, false, false>), dim3(count), dim3(64), 0, s, *m, *d, w0);
+    launch_nb<FLAGS, 32>(newton, m, d, s, w0, count);
   }
-  trace_launch(s, K_DENSE + 4 * FLAGS + (ell ? 2 : 0) + (newton ? 1 : 0));
+  trace_launch(s, K_DENSE + 32 * nbi + 4 * FLAGS + (ell ? 2 : 0) + (newton ? 1 : 0));
   return hipGetLastError();
 }
 

@@ -417,11 +417,13 @@ __device__ void camlight(const mjw_model_t& m, const mjw_data_t& d, int wid) {
     const int mode = m.light_mode[l], b = m.light_bodyid[l], tgt = m.light_targetbodyid[l];
     const bool is_target = mode == CAM_TARGETBODY || mode == CAM_TARGETBODYCOM;
     float lx[3], ld[3];  // built in registers, stored once (smooth.py:703-758)
+    bool norm = true;
     if ((is_target && tgt < 0) || mode == CAM_FIXED) {
       float t[3];
       rot_vec_quat(t, light_pos + 3 * l, xquat + 4 * b);
       for (int i = 0; i < 3; i++) lx[i] = xpos[3 * b + i] + t[i];
       rot_vec_quat(ld, light_dir + 3 * l, xquat + 4 * b);
+      norm = !(is_target && tgt < 0);  // smooth.py:726-732 returns before normalize
     } else if (mode == CAM_TRACK) {
       for (int i = 0; i < 3; i++) {
         ld[i] = light_dir0[3 * l + i];
@@ -439,7 +441,7 @@ __device__ void camlight(const mjw_model_t& m, const mjw_data_t& d, int wid) {
       const float* tp = mode == CAM_TARGETBODYCOM ? sc + 3 * tgt : xpos + 3 * tgt;
       for (int i = 0; i < 3; i++) ld[i] = tp[i] - lx[i];
     }
-    normalize3(ld);
+    if (norm) normalize3(ld);
     float* gx = d.light_xpos + ((long)wid * m.nlight + l) * 3;
     float* gd = d.light_xdir + ((long)wid * m.nlight + l) * 3;
     for (int i = 0; i < 3; i++) {

@@ -2689,9 +2689,10 @@ const char* mjw_kernel_name(int id) {
                                "mjw::sp::solve_kernel<0>", "mjw::sp::solve_kernel<1>", "mjw::sp::solve_kernel<2>", "mjw::sp::euler_kernel"};
   static thread_local char buf[64];
   if (id >= 0 && id < (int)(sizeof(misc) / sizeof(misc[0]))) return misc[id];
-  if (id >= mjw::K_DENSE && id < mjw::K_DENSE + 32) {
-    const int k = id - mjw::K_DENSE;
-    snprintf(buf, sizeof(buf), "mjw::dense_kernel<%d, %s, %s>", k >> 2, (k & 1) ? "true" : "false", (k & 2) ? "true" : "false");
+  if (id >= mjw::K_DENSE && id < mjw::K_DENSE + 96) {
+    const int k = (id - mjw::K_DENSE) & 31, nb[3] = {32, 16, 28};
+    snprintf(buf, sizeof(buf), "mjw::dense_kernel<%d, %s, %s, %d>", k >> 2, (k & 1) ? "true" : "false", (k & 2) ? "true" : "false",
+             nb[(id - mjw::K_DENSE) >> 5]);
     return buf;
   }
   if (id >= mjw::K_FWD && id < mjw::K_END) {

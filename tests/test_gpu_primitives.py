@@ -56,3 +56,23 @@ def test_spd_inverse_mfma_layout():
   err = np.abs(out - want).max(axis=(1, 2)) / np.abs(want).max(axis=(1, 2))
   assert err.max() < 1e-4, err.max()
   assert np.array_equal(out, out.transpose(0, 2, 1))  # X^T X is bitwise symmetric
+
+
+def test_spd_inverse_factor_bound_16():
+  """spd_inverse with the compile-time factor bound NB = 16 (the nv <= 16 dense kernels, e.g. franka):
+  matrices that are the identity past row / column 16 invert exactly as with the full 32 steps."""
+  rng = np.random.default_rng(2)
+  n = 64
+  M = np.tile(np.eye(32), (n, 1, 1))
+  for i in range(n):
+    k = 1 + i % 16  # every size 1..16
+    A = rng.normal(size=(k, k))
+    M[i, :k, :k] = A @ A.T / k + np.eye(k) * 0.5
+  x = M.astype(np.float32).reshape(n, -1)
+  out16 = _run(2, x, n * 1024).reshape(n, 32, 32)
+  out32 = _run(1, x, n * 1024).reshape(n, 32, 32)
+  want = np.linalg.inv(M)
+  err = np.abs(out16 - want).max(axis=(1, 2)) / np.abs(want).max(axis=(1, 2))
+  assert err.max() < 1e-4, err.max()
+  np.testing.assert_array_equal(out16[:, 16:, 16:], np.tile(np.eye(16), (n, 1, 1)))
+  np.testing.assert_array_equal(out16, out32)  # the skipped steps are exact no-ops
