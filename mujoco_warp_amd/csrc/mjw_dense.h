@@ -191,32 +191,6 @@ __device__ __forceinline__ void stage_spd(const float* g, int gs, int n, const f
   stage_rows(n, S, lane, a, Macc);
 }
 
-// derivative.py:36-107 (_qderiv_actuator_passive_vel): d force / d velocity scale of actuator a
-__device__ __forceinline__ float actuator_vel_deriv(const mjw_model_t& m, const mjw_data_t& d, int wid, int a) {
-  const float* gainprm = MR(actuator_gainprm) + 10 * a;
-  const float* biasprm = MR(actuator_biasprm) + 10 * a;
-  float gain = m.actuator_gaintype[a] == GAIN_AFFINE ? gainprm[2] : 0.0f;
-  float bias = m.actuator_biastype[a] == BIAS_AFFINE ? biasprm[2] : 0.0f;
-  if (bias == 0.0f && gain == 0.0f) return 0.0f;
-  if (m.actuator_forcelimited[a]) {
-    float f = d.actuator_force[(long)wid * m.nu + a];
-    const float* fr = MR(actuator_forcerange) + 2 * a;
-    if (f <= fr[0] || f >= fr[1]) return 0.0f;
-  }
-  float vel = bias;
-  if (m.actuator_dyntype[a] != DYN_NONE) {
-    if (gain != 0.0f) {  // derivative.py:86-101: actearly differentiates at the next activation
-      const long ga = (long)wid * m.na + m.actuator_actadr[a] + m.actuator_actnum[a] - 1;
-      vel += gain * (m.actuator_actearly[a] ? next_act(MR(opt_timestep)[0], m.actuator_dyntype[a], MR(actuator_dynprm)[10 * a], MR(actuator_actrange) + 2 * a,
-                                                       d.act[ga], d.act_dot[ga], 1.0f, m.actuator_actlimited[a] != 0)
-                                            : d.act[ga]);
-    }
-  } else if (gain != 0.0f) {
-    vel += gain * d.ctrl[(long)wid * m.nu + a];
-  }
-  return vel;
-}
-
 // lane r: sum_k J[r][k] v[k] over k < 4*nq (JS: the LDS row stride of J)
 template <int JS = DJS>
 __device__ __forceinline__ float gemv_rows(const float* Jl, const float* vec, int lane, int nq) {

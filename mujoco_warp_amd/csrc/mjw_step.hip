@@ -2080,7 +2080,9 @@ __device__ __forceinline__ void solve(const mjw_model_t& m, const mjw_data_t& d,
   WSYNC();
 }
 
-// forward.py:51-354 (_advance + euler; implicit damping when EULERDAMP is enabled)
+// forward.py:51-354 (_advance + euler; implicit damping when EULERDAMP is enabled) and implicitfast
+// (forward.py:494-510: (M - dt qDeriv) qacc_adv = M qacc, qDeriv = sum_a vel_a m_a m_a' - diag(damping)
+// - tendon damping, on the ancestor pattern of qM; derivative.py:320-416), as in the dense kernel
 __device__ __forceinline__ void euler(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -2088,14 +2090,58 @@ __device__ __forceinline__ void euler(const mjw_model_t& m, const mjw_data_t& d,
   const float dt = MR(opt_timestep)[0];
   float qacc = lane < nv ? s[L.qacc + lane] : 0.0f;
   float qacc_adv = qacc;
-  if (!(m.opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER))) {
+  const int fl = m.opt_disableflags;
+  const bool implicitfast = m.opt_integrator == INT_IMPLICITFAST;
+  const bool need_implicit = implicitfast ? (fl & (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) != (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)
+                                          : !(fl & (DSBL_EULERDAMP | DSBL_DAMPER));
+  if (need_implicit) {
     const float* dof_damping = MR(dof_damping);
+    const bool damp = !(fl & DSBL_DAMPER);
     float* Lm = s + L.L;
     for (int e = lane; e < nv * nvs; e += LPW) {
       int r = e / nvs, c = e - r * nvs;
-      Lm[e] = s[L.qM + e] + ((r == c && r < nv) ? dt * dof_damping[r] : 0.0f);
+      Lm[e] = s[L.qM + e] + ((damp && r == c && r < nv) ? dt * dof_damping[r] : 0.0f);
     }
     WSYNC();
+    if (implicitfast && m.nu > 0 && !(fl & DSBL_ACTUATION)) {
+      for (int u = 0; u < m.nu; u++) {
+        const float vel = actuator_vel_deriv(m, d, wid, u);
+        if (vel == 0.0f) continue;
+        const long gu = (long)wid * m.nu + u;
+        const int nnz = d.moment_rownnz[gu], adr = d.moment_rowadr[gu];
+        const long base = (long)wid * m.nJmom + adr;
+        for (int p = lane; p < nnz * nnz; p += LPW) {
+          const int k1 = p / nnz, k2 = p - k1 * nnz;
+          const int i = d.moment_colind[base + k1], j = d.moment_colind[base + k2];
+          int a = i;
+          while (a > j) a = m.dof_parentid[a];
+          if (a != j) continue;
+          const float v = dt * vel * d.actuator_moment[base + k1] * d.actuator_moment[base + k2];
+          Lm[i * nvs + j] -= v;
+          if (i != j) Lm[j * nvs + i] -= v;
+        }
+        WSYNC();
+      }
+    }
+    if (implicitfast && m.ntendon && !(fl & DSBL_DAMPER)) {
+      const float* tdamp = MR(tendon_damping);
+      for (int t = 0; t < m.ntendon; t++) {
+        if (tdamp[t] == 0.0f) continue;
+        const int rn = m.ten_J_rownnz[t], ra = m.ten_J_rowadr[t];
+        for (int p = lane; p < rn * rn; p += LPW) {
+          const int k1 = p / rn, k2 = p - k1 * rn;
+          if (k2 > k1) continue;
+          const int i = m.ten_J_colind[ra + k1], j = m.ten_J_colind[ra + k2];
+          int a = i;
+          while (a > j) a = m.dof_parentid[a];
+          if (a != j) continue;
+          const float v = dt * tdamp[t] * ten_coef(m, wid, t, i) * ten_coef(m, wid, t, j);
+          Lm[i * nvs + j] += v;
+          if (i != j) Lm[j * nvs + i] += v;
+        }
+        WSYNC();
+      }
+    }
     cholesky(Lm, nv, nvs, lane);
     qacc_adv = cholesky_solve(Lm, nv, nvs, lane, lane < nv ? s[L.Ma + lane] : 0.0f);
   }

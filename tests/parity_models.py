@@ -58,7 +58,15 @@ def setup(name):
     mjm = franka_model()
     # pools sized so that neither side drops rows or contacts (the device pool is global, the
     # oracle's per world): the random poses drive the hand up to 0.2 m into the floor, 18 contacts
+    # (73 rows > 64: the generic LDS-solver kernel, mjw_step.hip, runs this workload)
     return (mjm,) + franka_states(mjm, 16, seed=22) + (96, 24, 16)
+  if name == "franka_dense":
+    # the same states without the two buried-hand worlds: every world within the register-resident
+    # dense kernel's njmax <= 64 (mjw_dense.h), the path the C3 benchmark runs
+    mjm = franka_model()
+    q, v, c = franka_states(mjm, 16, seed=22)
+    keep = np.array([w for w in range(16) if w not in (2, 6)])
+    return mjm, q[keep], v[keep], c[keep], 64, 16, len(keep)
   if name == "apollo":
     mjm = mjw.load_model(os.path.join(ROOT, "models", "apptronik_apollo", "scene_flat.xml"))
     nworld = 32

@@ -13,7 +13,7 @@ from tests.parity_models import report  # noqa: E402
 
 def main():
   path = sys.argv[1] if len(sys.argv) > 1 else None
-  names = sys.argv[2:] or ["franka", "apollo", "cloth", "aloha"]
+  names = sys.argv[2:] or ["franka", "franka_dense", "apollo", "cloth", "aloha"]
   res = {}
   for n in names:
     res[n] = report(n)
