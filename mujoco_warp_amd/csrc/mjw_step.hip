@@ -2331,6 +2331,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
   w.wid = w0 + (int)blockIdx.x;
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
+  // the full step on the dense path: worlds in the counter-reset kernel's most-rows-first order
+  if ((STAGES & ST_POS) && d.sched && d.fwd_order) w.wid = d.fwd_order[w.wid];
   WLOG_T0();
   run_stages<STAGES, FULL>(m, d, L, w);
   WLOG_END(w.wid, 0);
@@ -2389,16 +2391,40 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
 // exactly once (the last dense pass covered all worlds with the order enabled); otherwise world_order is
 // the identity.  Measured: the same scatter done with global atomics inside the forward kernel serialised
 // on the 32 bucket counters and cost the forward kernel what it saved the dense kernel.
+// fwd_order (when non-null): the forward kernel's order, by the previous step's constraint-row count
+// (nefc, 2 rows per bucket, most first), sorted here the same way from an LDS histogram.
 constexpr int RESET_THREADS = 1024;
 __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* nacon, int* ncollision, int* sched, int* world_order,
-                                                                       const int* world_key, int nworld) {
+                                                                       const int* world_key, const int* nefc, int* fwd_order, int nworld) {
   const int t = threadIdx.x;
   if (t == 0) { nacon[0] = 0; ncollision[0] = 0; }
   if (!sched) return;
   constexpr int NB = MJW_SCHED_BUCKETS;
   static_assert(NB <= 64, "one wave scans the buckets");
   __shared__ int cursor[NB];
+  __shared__ int fcount[NB];
   __shared__ int valid;
+  if (fwd_order) {
+    if (t < NB) fcount[t] = 0;
+    __syncthreads();
+    for (int w = t; w < nworld; w += RESET_THREADS) atomicAdd(&fcount[NB - 1 - min(max(nefc[w], 0) >> 1, NB - 1)], 1);
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the row-count histogram: fcount becomes the cursors
+      const int h = t < NB ? fcount[t] : 0;
+      int x = h;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (t >= o) x += y;
+      }
+      if (t < NB) fcount[t] = x - h;
+    }
+    __syncthreads();
+    for (int w = t; w < nworld; w += RESET_THREADS) {
+      const int pos = atomicAdd(&fcount[NB - 1 - min(max(nefc[w], 0) >> 1, NB - 1)], 1);
+      fwd_order[pos] = w;
+    }
+  }
   if (t < 64) {
     const int h = t < NB ? sched[t] : 0;
     int x = h;
@@ -2492,10 +2518,10 @@ int set_err(hipError_t e, const char* where) {
   return (int)e;
 }
 
-hipError_t reset_counters(const mjw_data_t* d, hipStream_t s, bool order = false) {
+hipError_t reset_counters(const mjw_data_t* d, hipStream_t s, bool order = false, bool fwd = false) {
   // the order is built only for the dense path's full forward + solve (run() passes order = true)
   hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(order ? mjw::RESET_THREADS : 64), 0, s, d->nacon, d->ncollision,
-                     order ? d->sched : nullptr, d->world_order, d->world_key, d->nworld);
+                     order ? d->sched : nullptr, d->world_order, d->world_key, d->nefc, fwd ? d->fwd_order : nullptr, d->nworld);
   mjw::trace_launch(s, mjw::K_RESET);
   return hipGetLastError();
 }
@@ -2590,17 +2616,24 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     return !(e && e[0] == '0');
   }();
   const bool order = order_on && full && d->sched && dense_ok(m, d);
+  // the forward kernel's order by the previous step's row count (MJW_FWD_ORDER=0 disables it)
+  static const bool fwd_on = [] {
+    const char* e = getenv("MJW_FWD_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  const bool fwd = order && fwd_on && d->fwd_order;
   if (m->opt_cone == CONE_ELLIPTIC && (stages & ST_SOLVE) && !dense_ok(m, d)) {
     g_err = std::string(name) + ": elliptic cones need the register-resident dense solve (nv <= 32, njmax <= 64)";
     return -5;
   }
   if (stages & ST_POS) {
-    rc = set_err(reset_counters(d, s, order), name);
+    rc = set_err(reset_counters(d, s, order, fwd), name);
     if (rc) return rc;
   }
   if (dense_ok(m, d)) {
     mjw_data_t dv = *d;
     if (!order) dv.sched = nullptr;
+    if (!fwd) dv.fwd_order = nullptr;
     d = &dv;
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel, for the
     // world range [w0, w0 + cnt) on stream st; `timed` records the optional bench events.
