@@ -2276,9 +2276,10 @@ __device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data
 }
 
 // the stages in STAGES of world w.wid by the calling wavefront
-// FULL: the box narrowphase and the tendon paths (the lean instantiation, FULL = false, serves
-// models with neither: it keeps the humanoid-class kernel free of their register pressure)
-template <int STAGES, bool FULL>
+// BOX: the box narrowphase paths; TEN: the tendon paths.  The lean instantiations keep the
+// humanoid-class kernel (neither) and the box models' kernel (no tendons) free of the register
+// pressure of code they never run.
+template <int STAGES, bool BOX, bool TEN>
 __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   PROF_T0();
   load_state(m, d, L, w);
@@ -2292,19 +2293,19 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
     PROF_MARK(PH_COM);
     camlight(m, d, L, w);
     PROF_MARK(PH_CAM);
-    if (FULL && m.ntendon) tendon_pos(m, d, w.s + L.qpos, w.wid, w.lane);  // smooth.py:3085-3121 (fwd_position: before crb)
-    crb_qM<FULL>(m, d, L, w);
+    if (TEN && m.ntendon) tendon_pos(m, d, w.s + L.qpos, w.wid, w.lane);  // smooth.py:3085-3121 (fwd_position: before crb)
+    crb_qM<TEN>(m, d, L, w);
     PROF_MARK(PH_CRB);
-    collision_and_constraints<FULL, FULL>(m, d, L, w);
+    collision_and_constraints<BOX, TEN>(m, d, L, w);
     PROF_MARK(PH_COLL);
-    transmission<FULL>(m, d, L, w);
+    transmission<TEN>(m, d, L, w);
     PROF_MARK(PH_TRN);
   }
-  if (STAGES & ST_VEL) fwd_velocity<FULL>(m, d, L, w);
+  if (STAGES & ST_VEL) fwd_velocity<TEN>(m, d, L, w);
   if ((STAGES & ST_POS) && (STAGES & ST_VEL) && w.lane < 2 && !(m.opt_enableflags & ENBL_ENERGY))
     d.energy[(long)w.wid * 2 + w.lane] = 0.0f;
   PROF_MARK(PH_VEL);
-  if (STAGES & ST_ACT) fwd_actuation<FULL>(m, d, L, w);
+  if (STAGES & ST_ACT) fwd_actuation<TEN>(m, d, L, w);
   PROF_MARK(PH_ACT);
   if (STAGES & ST_ACC) fwd_acceleration(m, d, L, w);
   PROF_MARK(PH_ACC);
@@ -2322,7 +2323,7 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
 // their registers (at the cap they spilled 80 B/lane).
 template <int STAGES>
 constexpr int fwd_waves_per_eu() { return ((STAGES & ST_SOLVE) && !(STAGES & ST_NOFACTOR)) ? 1 : 4; }
-template <int STAGES, bool FULL = true>
+template <int STAGES, bool BOX = true, bool TEN = true>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu<STAGES>()))) mjw_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   WS w;
@@ -2334,7 +2335,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
   // the full step on the dense path: worlds in the counter-reset kernel's most-rows-first order
   if ((STAGES & ST_POS) && d.sched && d.fwd_order) w.wid = d.fwd_order[w.wid];
   WLOG_T0();
-  run_stages<STAGES, FULL>(m, d, L, w);
+  run_stages<STAGES, BOX, TEN>(m, d, L, w);
   WLOG_END(w.wid, 0);
 }
 
@@ -2556,20 +2557,28 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   }
   static std::once_flag once;
   std::call_once(once, [] {
-    (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if constexpr ((STAGES & mjw::ST_POS) != 0)
-      (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if constexpr ((STAGES & mjw::ST_POS) != 0) {
+      (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    }
   });
-  // position-stage kernels without the box narrowphase and tendon paths for models that have neither
+  // position-stage kernels without the tendon paths, and without the box narrowphase, for models
+  // that have none (kernel id: K_FWD + 4 STAGES + 2 BOX + TEN)
   if constexpr ((STAGES & mjw::ST_POS) != 0) {
-    if (m->nxn_box == 0 && m->ntendon == 0) {
-      hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
-      mjw::trace_launch(s, mjw::K_FWD + 2 * STAGES);
+    if (m->ntendon == 0) {
+      if (m->nxn_box == 0) {
+        hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, false, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
+        mjw::trace_launch(s, mjw::K_FWD + 4 * STAGES);
+      } else {
+        hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, true, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
+        mjw::trace_launch(s, mjw::K_FWD + 4 * STAGES + 2);
+      }
       return set_err(hipGetLastError(), name);
     }
   }
-  hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, true>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
-  mjw::trace_launch(s, mjw::K_FWD + 2 * STAGES + 1);
+  hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, true, true>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
+  mjw::trace_launch(s, mjw::K_FWD + 4 * STAGES + 3);
   return set_err(hipGetLastError(), name);
 }
 
@@ -2775,7 +2784,7 @@ const char* mjw_kernel_name(int id) {
     return buf;
   }
   if (id >= mjw::K_FWD && id < mjw::K_END) {
-    snprintf(buf, sizeof(buf), "mjw::mjw_kernel<%d, %s>", (id - mjw::K_FWD) >> 1, (id & 1) ? "true" : "false");
+    snprintf(buf, sizeof(buf), "mjw::mjw_kernel<%d, %s, %s>", (id - mjw::K_FWD) >> 2, (id & 2) ? "true" : "false", (id & 1) ? "true" : "false");
     return buf;
   }
   return "unknown";
