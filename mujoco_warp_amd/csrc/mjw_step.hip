@@ -2639,11 +2639,13 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     rc = set_err(reset_counters(d, s, order, fwd), name);
     if (rc) return rc;
   }
+  // every launch below sees the world orders only when this call built them (the generic path and
+  // the stage launches run the worlds in identity order)
+  mjw_data_t dv = *d;
+  if (!order) dv.sched = nullptr;
+  if (!fwd) dv.fwd_order = nullptr;
+  d = &dv;
   if (dense_ok(m, d)) {
-    mjw_data_t dv = *d;
-    if (!order) dv.sched = nullptr;
-    if (!fwd) dv.fwd_order = nullptr;
-    d = &dv;
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel, for the
     // world range [w0, w0 + cnt) on stream st; `timed` records the optional bench events.
     // (Measured and dropped, DESIGN 4: a two-stream split of one batch inside the step -- the join
