@@ -3,6 +3,8 @@
 
 #include "mjw_dense.h"
 
+#include <cstdlib>
+
 namespace mjw {
 
 // 3 waves/SIMD (up to 168 VGPRs, 12 worlds/CU): at 4 (128 VGPRs, 16 worlds/CU, which the 9.7 KB of
@@ -70,10 +72,16 @@ hipError_t launch_flags(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s
   // the cone only matters to the solve; Euler-only / factor-only launches use the pyramidal kernels
   const bool ell = (FLAGS & DF_SOLVE) && m->opt_cone == CONE_ELLIPTIC;
   int nbi = 0;  // factor bound: 0 -> 32, 1 -> 16, 2 -> 28 (the kernel id and name carry it)
+  static const int nb_max = [] {  // MJW_DENSE_NB=32 / 28: never use the smaller bounds (A/B runs)
+    const char* e = getenv("MJW_DENSE_NB");
+    return e ? atoi(e) : 0;
+  }();
   if (ell) {
     if (newton) hipLaunchKernelGGL((dense_kernel<FLAGS, true, true, 32>), dim3(count), dim3(64), 0, s, *m, *d, w0);
     else hipLaunchKernelGGL((dense_kernel<FLAGS, false, true, 32>), dim3(count), dim3(64), 0, s, *m, *d, w0);
-  } else if (m->nv <= 16) {
+  } else if (nb_max == 32) {
+    launch_nb<FLAGS, 32>(newton, m, d, s, w0, count);
+  } else if (m->nv <= 16 && nb_max != 28) {
     launch_nb<FLAGS, 16>(newton, m, d, s, w0, count);
     nbi = 1;
   } else if (m->nv <= 28) {

@@ -2395,6 +2395,26 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
 // fwd_order (when non-null): the forward kernel's order, by the previous step's constraint-row count
 // (nefc, 2 rows per bucket, most first), sorted here the same way from an LDS histogram.
 constexpr int RESET_THREADS = 1024;
+// atomicAdd(&ctr[key], 1) for every active lane, aggregated per distinct key of the wave (one LDS atomic
+// per key and wave instead of one per lane: a batch whose worlds share one bucket -- franka, 1 row and
+// 1 iteration per world -- serialised 16k same-address atomics, 46 us); returns each lane's old value
+__device__ __forceinline__ int wave_aggregated_add(int* ctr, int key, bool active) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long todo = __ballot(active);
+  int pos = 0;
+  while (todo) {
+    const int leader = __ffsll((long long)todo) - 1;
+    const int k = __shfl(key, leader);
+    const unsigned long long mk = __ballot(active && key == k) & todo;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&ctr[k], __popcll(mk));
+    base = __shfl(base, leader);
+    if ((mk >> lane) & 1ull) pos = base + __popcll(mk & ((1ull << lane) - 1ull));
+    todo &= ~mk;
+  }
+  return pos;
+}
+
 __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* nacon, int* ncollision, int* sched, int* world_order,
                                                                        const int* world_key, const int* nefc, int* fwd_order, int nworld) {
   const int t = threadIdx.x;
@@ -2408,7 +2428,10 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
   if (fwd_order) {
     if (t < NB) fcount[t] = 0;
     __syncthreads();
-    for (int w = t; w < nworld; w += RESET_THREADS) atomicAdd(&fcount[NB - 1 - min(max(nefc[w], 0) >> 1, NB - 1)], 1);
+    for (int w0 = 0; w0 < nworld; w0 += RESET_THREADS) {  // uniform trip count: whole waves in the loop
+      const int w = w0 + t;
+      (void)wave_aggregated_add(fcount, w < nworld ? NB - 1 - min(max(nefc[w], 0) >> 1, NB - 1) : 0, w < nworld);
+    }
     __syncthreads();
     if (t < 64) {  // exclusive scan of the row-count histogram: fcount becomes the cursors
       const int h = t < NB ? fcount[t] : 0;
@@ -2421,9 +2444,10 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
       if (t < NB) fcount[t] = x - h;
     }
     __syncthreads();
-    for (int w = t; w < nworld; w += RESET_THREADS) {
-      const int pos = atomicAdd(&fcount[NB - 1 - min(max(nefc[w], 0) >> 1, NB - 1)], 1);
-      fwd_order[pos] = w;
+    for (int w0 = 0; w0 < nworld; w0 += RESET_THREADS) {
+      const int w = w0 + t;
+      const int pos = wave_aggregated_add(fcount, w < nworld ? NB - 1 - min(max(nefc[w], 0) >> 1, NB - 1) : 0, w < nworld);
+      if (w < nworld) fwd_order[pos] = w;
     }
   }
   if (t < 64) {
@@ -2443,10 +2467,10 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
   }
   __syncthreads();
   if (valid) {
-    for (int w = t; w < nworld; w += RESET_THREADS) {
-      const int k = min(max(world_key[w], 0), NB - 1);
-      const int pos = atomicAdd(&cursor[k], 1);
-      if (pos < nworld) world_order[pos] = w;
+    for (int w0 = 0; w0 < nworld; w0 += RESET_THREADS) {
+      const int w = w0 + t;
+      const int pos = wave_aggregated_add(cursor, w < nworld ? min(max(world_key[w], 0), NB - 1) : 0, w < nworld);
+      if (w < nworld && pos < nworld) world_order[pos] = w;
     }
   } else {
     for (int w = t; w < nworld; w += RESET_THREADS) world_order[w] = w;
