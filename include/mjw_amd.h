@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 15
+#define MJW_ABI_VERSION 16
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -119,8 +119,7 @@
  * stored slot-major (slot k of row r at [k * njmax_pad + r]) with efc_J_colind / efc_J_rownnz; dense models keep qM (nv_pad, nv_pad), qLD (nv, nv), efc_J
  * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt / ncon_world are sparse-path workspace (size 0 when dense).
  * world_order / world_key: the dense path's longest-first world order (a permutation of the worlds, rebuilt
- * every step from the previous step's solver iterations) and each world's iteration bucket; fwd_order: the
- * forward kernel's order, most constraint rows (previous step's nefc) first. */
+ * every step from the previous step's solver iterations) and each world's iteration bucket. */
 #define MJW_DATA_REAL_ARRAYS(X)                                                                    \
   X(time, 1) X(qpos, nq) X(qvel, nv) X(act, na) X(ctrl, nu) X(qacc_warmstart, nv)                 \
   X(qfrc_applied, nv) X(xfrc_applied, nbody * 6) X(mocap_pos, nmocap * 3) X(mocap_quat, nmocap * 4) \
@@ -153,7 +152,7 @@
   X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax_pad) X(eq_active, neq)                   \
   X(efc_J_colind, njmax_pad * njrow) X(efc_J_rownnz, njmax) X(efc_JT_rowind, njmax_pad * njrow)   \
   X(efc_JT_adr, nv + 1) X(sp_cnt, nv + 1) X(ncon_world, 2)                                        \
-  X(world_order, 1) X(world_key, 1) X(fwd_order, 1)
+  X(world_order, 1) X(world_key, 1)
 
 /* ---- contact pool: float arrays, (naconmax, count) ---- */
 #define MJW_CONTACT_REAL_ARRAYS(X)                                                                 \

@@ -2332,8 +2332,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
   w.wid = w0 + (int)blockIdx.x;
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
-  // the full step on the dense path: worlds in the counter-reset kernel's most-rows-first order
-  if ((STAGES & ST_POS) && d.sched && d.fwd_order) w.wid = d.fwd_order[w.wid];
   WLOG_T0();
   run_stages<STAGES, BOX, TEN>(m, d, L, w);
   WLOG_END(w.wid, 0);
@@ -2389,67 +2387,19 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
 // previous step histogrammed each world's solver-iteration bucket (sched[0, NB), world_key); a counting
 // sort over the buckets in this one workgroup (LDS cursors) writes world_order, a permutation of the
 // worlds with the most iterations first.  The order is built only when the histogram counts every world
-// exactly once (the last dense pass covered all worlds with the order enabled); otherwise world_order is
-// the identity.  Measured: the same scatter done with global atomics inside the forward kernel serialised
+// exactly once (the last dense pass covered all worlds with the order enabled) in more than one bucket;
+// otherwise world_order is the identity.  Measured: the same scatter done with global atomics inside the forward kernel serialised
 // on the 32 bucket counters and cost the forward kernel what it saved the dense kernel.
-// fwd_order (when non-null): the forward kernel's order, by the previous step's constraint-row count
-// (nefc, 2 rows per bucket, most first), sorted here the same way from an LDS histogram.
 constexpr int RESET_THREADS = 1024;
-// atomicAdd(&ctr[key], 1) for every active lane, aggregated per distinct key of the wave (one LDS atomic
-// per key and wave instead of one per lane: a batch whose worlds share one bucket -- franka, 1 row and
-// 1 iteration per world -- serialised 16k same-address atomics, 46 us); returns each lane's old value
-__device__ __forceinline__ int wave_aggregated_add(int* ctr, int key, bool active) {
-  const int lane = threadIdx.x & 63;
-  unsigned long long todo = __ballot(active);
-  int pos = 0;
-  while (todo) {
-    const int leader = __ffsll((long long)todo) - 1;
-    const int k = __shfl(key, leader);
-    const unsigned long long mk = __ballot(active && key == k) & todo;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&ctr[k], __popcll(mk));
-    base = __shfl(base, leader);
-    if ((mk >> lane) & 1ull) pos = base + __popcll(mk & ((1ull << lane) - 1ull));
-    todo &= ~mk;
-  }
-  return pos;
-}
-
 __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* nacon, int* ncollision, int* sched, int* world_order,
-                                                                       const int* world_key, const int* nefc, int* fwd_order, int nworld) {
+                                                                       const int* world_key, int nworld) {
   const int t = threadIdx.x;
   if (t == 0) { nacon[0] = 0; ncollision[0] = 0; }
   if (!sched) return;
   constexpr int NB = MJW_SCHED_BUCKETS;
   static_assert(NB <= 64, "one wave scans the buckets");
   __shared__ int cursor[NB];
-  __shared__ int fcount[NB];
   __shared__ int valid;
-  if (fwd_order) {
-    if (t < NB) fcount[t] = 0;
-    __syncthreads();
-    for (int w0 = 0; w0 < nworld; w0 += RESET_THREADS) {  // uniform trip count: whole waves in the loop
-      const int w = w0 + t;
-      (void)wave_aggregated_add(fcount, w < nworld ? NB - 1 - min(max(nefc[w], 0) >> 1, NB - 1) : 0, w < nworld);
-    }
-    __syncthreads();
-    if (t < 64) {  // exclusive scan of the row-count histogram: fcount becomes the cursors
-      const int h = t < NB ? fcount[t] : 0;
-      int x = h;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (t >= o) x += y;
-      }
-      if (t < NB) fcount[t] = x - h;
-    }
-    __syncthreads();
-    for (int w0 = 0; w0 < nworld; w0 += RESET_THREADS) {
-      const int w = w0 + t;
-      const int pos = wave_aggregated_add(fcount, w < nworld ? NB - 1 - min(max(nefc[w], 0) >> 1, NB - 1) : 0, w < nworld);
-      if (w < nworld) fwd_order[pos] = w;
-    }
-  }
   if (t < 64) {
     const int h = t < NB ? sched[t] : 0;
     int x = h;
@@ -2459,18 +2409,23 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
       if (t >= o) x += y;
     }
     const int total = __shfl(x, 63);
+    int hmax = h;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hmax = max(hmax, __shfl_xor(hmax, o));
     if (t < NB) {
       cursor[t] = x - h;
       sched[t] = 0;
     }
-    if (t == 0) valid = total == nworld;
+    // one bucket holding every world (franka: 1 iteration each) orders nothing and would serialise
+    // all the LDS atomics on one address: identity order then
+    if (t == 0) valid = total == nworld && hmax < nworld;
   }
   __syncthreads();
   if (valid) {
-    for (int w0 = 0; w0 < nworld; w0 += RESET_THREADS) {
-      const int w = w0 + t;
-      const int pos = wave_aggregated_add(cursor, w < nworld ? min(max(world_key[w], 0), NB - 1) : 0, w < nworld);
-      if (w < nworld && pos < nworld) world_order[pos] = w;
+    for (int w = t; w < nworld; w += RESET_THREADS) {
+      const int k = min(max(world_key[w], 0), NB - 1);
+      const int pos = atomicAdd(&cursor[k], 1);
+      if (pos < nworld) world_order[pos] = w;
     }
   } else {
     for (int w = t; w < nworld; w += RESET_THREADS) world_order[w] = w;
@@ -2543,10 +2498,10 @@ int set_err(hipError_t e, const char* where) {
   return (int)e;
 }
 
-hipError_t reset_counters(const mjw_data_t* d, hipStream_t s, bool order = false, bool fwd = false) {
+hipError_t reset_counters(const mjw_data_t* d, hipStream_t s, bool order = false) {
   // the order is built only for the dense path's full forward + solve (run() passes order = true)
   hipLaunchKernelGGL(mjw::reset_counters_kernel, dim3(1), dim3(order ? mjw::RESET_THREADS : 64), 0, s, d->nacon, d->ncollision,
-                     order ? d->sched : nullptr, d->world_order, d->world_key, d->nefc, fwd ? d->fwd_order : nullptr, d->nworld);
+                     order ? d->sched : nullptr, d->world_order, d->world_key, d->nworld);
   mjw::trace_launch(s, mjw::K_RESET);
   return hipGetLastError();
 }
@@ -2649,25 +2604,18 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     return !(e && e[0] == '0');
   }();
   const bool order = order_on && full && d->sched && dense_ok(m, d);
-  // the forward kernel's order by the previous step's row count (MJW_FWD_ORDER=0 disables it)
-  static const bool fwd_on = [] {
-    const char* e = getenv("MJW_FWD_ORDER");
-    return !(e && e[0] == '0');
-  }();
-  const bool fwd = order && fwd_on && d->fwd_order;
   if (m->opt_cone == CONE_ELLIPTIC && (stages & ST_SOLVE) && !dense_ok(m, d)) {
     g_err = std::string(name) + ": elliptic cones need the register-resident dense solve (nv <= 32, njmax <= 64)";
     return -5;
   }
   if (stages & ST_POS) {
-    rc = set_err(reset_counters(d, s, order, fwd), name);
+    rc = set_err(reset_counters(d, s, order), name);
     if (rc) return rc;
   }
   // every launch below sees the world orders only when this call built them (the generic path and
   // the stage launches run the worlds in identity order)
   mjw_data_t dv = *d;
   if (!order) dv.sched = nullptr;
-  if (!fwd) dv.fwd_order = nullptr;
   d = &dv;
   if (dense_ok(m, d)) {
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel, for the

@@ -442,7 +442,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     efc_J_colind=(m.njrow * sp, njmax_pad), efc_J_rownnz=(njmax * sp,), efc_JT_rowind=(njmax_pad * m.njrow * sp,),
     efc_JT_adr=((nv + 1) * sp,), sp_cnt=((nv + 1) * sp,), ncon_world=(2,),
     # the dense path's longest-first world order (mjw_step.hip) and each world's iteration bucket
-    world_order=(), world_key=(), fwd_order=(),
+    world_order=(), world_key=(),
   )
   creal = dict(
     contact_dist=(), contact_pos=(3,), contact_frame=(3, 3), contact_includemargin=(), contact_friction=(5,),
