@@ -2,7 +2,7 @@
 
 Builds mujoco_warp_amd/libmjw_amd_prof.so with -DMJW_PROFILE (unless present), loads it via
 MJW_LIB_PATH, runs `nsteps` steps of the benchmark workload and prints each phase's share.
-usage: python tools/phase_prof.py [nworld] [nsteps] [CG|NEWTON]
+usage: python tools/phase_prof.py [nworld] [nsteps] [CG|NEWTON|default] [model]
 """
 import ctypes
 import json
@@ -30,13 +30,19 @@ SUB = ["c:eq_friction_limits", "c:broadphase", "c:narrowphase_staging", "c:pool_
 nworld = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 solver = sys.argv[3] if len(sys.argv) > 3 else "CG"
-mjm = mjcf.load_model(os.path.join(ROOT, "models", "humanoid.xml"))
-mjw.override_model(mjm, [f"opt.solver={solver}"])
+model = sys.argv[4] if len(sys.argv) > 4 else "humanoid"  # a bench.py config (dense-path models)
+from bench import MODELS  # noqa: E402
+
+cfg = MODELS[model]
+mjm = mjcf.load_model(os.path.join(ROOT, cfg["path"]))
+if solver != "default":
+  mjw.override_model(mjm, [f"opt.solver={solver}"])
 mjd = mjcf.MjData(mjm)
-mjcf.reset_data_keyframe(mjm, mjd, 0)
+if cfg["key"] is not None:
+  mjcf.reset_data_keyframe(mjm, mjd, cfg["key"])
 m = mjw.put_model(mjm, device="cuda")
-d = mjw.put_data(mjm, mjd, nworld=nworld, nconmax=24, njmax=64, device="cuda", m=m)
-center = torch.zeros(mjm.nu, device="cuda")
+d = mjw.put_data(mjm, mjd, nworld=nworld, nconmax=cfg["nconmax"], njmax=cfg["njmax"], device="cuda", m=m)
+center = None if cfg["key"] is None else torch.zeros(mjm.nu, device="cuda")
 L = _lib.lib()
 buf = (ctypes.c_ulonglong * (len(PHASES) + len(SUB)))()
 for i in range(20):
