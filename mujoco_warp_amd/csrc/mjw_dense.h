@@ -423,7 +423,11 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
     // ---- factor M, form M^-1, qacc_smooth (smooth.py:2860-2928 factor_solve_i)
     float a[32];
     stage_spd(d.qM + (long)wid * np * np, np, nv, nullptr, 0.0f, S, lane, a, Mm);
-    Mi = spd_inverse<(FLAGS & DF_FACTOR) != 0, NB>(a, lane, S);
+    // CG preconditions with M^-1 every iteration, so it forms the inverse; Newton (its own Hessian
+    // factor) and the factor-only launch need L and one solve only
+    constexpr bool NEED_INV = (FLAGS & DF_SOLVE) && !NEWTON;
+    if (NEED_INV) Mi = spd_inverse<(FLAGS & DF_FACTOR) != 0, NB>(a, lane, S);
+    else chol_factor<NB>(a, lane, S);  // L rows -> S
     if (FLAGS & DF_FACTOR) {
       // L rows -> qLD (nv x nv) through S for coalesced stores
       __syncthreads();
@@ -434,9 +438,13 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       }
     }
     qfrc_smooth = pf_qfrc_smooth;
-    if (lo) vd[c] = qfrc_smooth;
-    __syncthreads();
-    qacc_smooth = symv(Mi, vd, h);
+    if (NEED_INV) {
+      if (lo) vd[c] = qfrc_smooth;
+      __syncthreads();
+      qacc_smooth = symv(Mi, vd, h);
+    } else {
+      qacc_smooth = chol_solve<NB>(a, S, lane, dof ? qfrc_smooth : 0.0f);
+    }
     if (!dof) qacc_smooth = 0.0f;
     if ((FLAGS & DF_FACTOR) && lo && dof) d.qacc_smooth[gi] = qacc_smooth;
   }
