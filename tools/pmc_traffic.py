@@ -1,6 +1,7 @@
 """Summarise rocprofv3 CSV output into profiles/: per-kernel HBM traffic and time, per launch and per step.
 
-usage: python tools/pmc_traffic.py <stats_dir> <fetch_dir> <write_dir> <out.json> [worlds per launch] [solver] [model]
+usage: python tools/pmc_traffic.py <stats_dir> <fetch_dir> <write_dir> <out.json> [worlds per launch] [solver] [model] [tail steps]
+  tail steps: average the counters over the last N steps only (the passes warm up first)
   stats_dir : rocprofv3 --kernel-trace --stats --output-format csv output directory
   fetch_dir : rocprofv3 --pmc FETCH_SIZE --output-format csv output directory
   write_dir : rocprofv3 --pmc WRITE_SIZE --output-format csv output directory
@@ -50,9 +51,9 @@ def rows(d, pattern):
 
 
 def counter(d, name):
-  """{kernel: [values per dispatch]} of one PMC counter."""
+  """{kernel: [values per dispatch, in dispatch order]} of one PMC counter."""
   vals = collections.defaultdict(list)
-  for r in rows(d, "*counter_collection.csv"):
+  for r in sorted(rows(d, "*counter_collection.csv"), key=lambda r: int(r.get("Dispatch_Id", 0) or 0)):
     if r.get("Counter_Name") != name:
       continue
     k = kname(r.get("Kernel_Name", ""))
@@ -61,16 +62,25 @@ def counter(d, name):
   return vals
 
 
-def summarise(stats_dir, fetch_dir, write_dir, nworld, solver, model, csrc_sha):
+def tail(vals, steps, tail_steps):
+  """The dispatches of the last `tail_steps` of `steps` steps (all when tail_steps is 0)."""
+  if not tail_steps or not steps or tail_steps >= steps:
+    return vals
+  return {k: v[len(v) - max(1, round(len(v) * tail_steps / steps)):] for k, v in vals.items()}
+
+
+def summarise(stats_dir, fetch_dir, write_dir, nworld, solver, model, csrc_sha, tail_steps=0):
   fetch = counter(fetch_dir, "FETCH_SIZE")
   write = counter(write_dir, "WRITE_SIZE")
   stats = {kname(r["Name"]): r for r in rows(stats_dir, "*kernel_stats.csv")}
+  fetch = tail(fetch, len(fetch.get(STEP_KERNEL, [])), tail_steps)
+  write = tail(write, len(write.get(STEP_KERNEL, [])), tail_steps)
   steps_f = len(fetch.get(STEP_KERNEL, []))
   steps_w = len(write.get(STEP_KERNEL, []))
   res = {"nworld": nworld, "solver": solver, "model": model, "csrc_sha": csrc_sha,
          "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024; per step = "
                       "sum over kernels of (dispatches / steps) * bytes per launch, steps = dispatches of " + STEP_KERNEL,
-         "steps": [steps_f, steps_w], "kernels": {}}
+         "steps": [steps_f, steps_w], "tail_steps": tail_steps, "kernels": {}}
   total = 0.0
   for k in sorted(set(fetch) | set(write)):
     f, w = fetch.get(k, []), write.get(k, [])
@@ -95,10 +105,11 @@ def main():
   nworld = int(sys.argv[5]) if len(sys.argv) > 5 else 8192
   solver = sys.argv[6] if len(sys.argv) > 6 else "CG"
   model = sys.argv[7] if len(sys.argv) > 7 else "humanoid"
+  tail_steps = int(sys.argv[8]) if len(sys.argv) > 8 else 0
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
   from mujoco_warp_amd import build as _build
 
-  res = summarise(stats_dir, fetch_dir, write_dir, nworld, solver, model, _build.sources_hash())
+  res = summarise(stats_dir, fetch_dir, write_dir, nworld, solver, model, _build.sources_hash(), tail_steps)
   with open(out, "w") as fh:
     json.dump(res, fh, indent=1)
   print(json.dumps(res, indent=1))
