@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 16
+#define MJW_ABI_VERSION 17
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -117,7 +117,8 @@
  * Sparse models (is_sparse, the reference's io.py:67-74 switch) store qM / qLD as (nworld, nM) rows of
  * ancestors ascending then the diagonal (M_rowadr / M_colind), and efc_J as (nworld, njmax_pad, njrow)
  * stored slot-major (slot k of row r at [k * njmax_pad + r]) with efc_J_colind / efc_J_rownnz; dense models keep qM (nv_pad, nv_pad), qLD (nv, nv), efc_J
- * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt / ncon_world are sparse-path workspace (size 0 when dense).
+ * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt / ncon_world are sparse-path workspace (size 0 when dense);
+ * sp_idx16 holds the CG's 16-bit copies of efc_J_colind and of the transposed index's rows (two uint16 per int).
  * world_order / world_key: the dense path's longest-first world order (a permutation of the worlds, rebuilt
  * every step from the previous step's solver iterations) and each world's iteration bucket. */
 #define MJW_DATA_REAL_ARRAYS(X)                                                                    \
@@ -152,6 +153,7 @@
   X(efc_type, njmax) X(efc_id, njmax) X(efc_state, njmax_pad) X(eq_active, neq)                   \
   X(efc_J_colind, njmax_pad * njrow) X(efc_J_rownnz, njmax) X(efc_JT_rowind, njmax_pad * njrow)   \
   X(efc_JT_adr, nv + 1) X(sp_cnt, nv + 1) X(ncon_world, 2)                                        \
+  X(sp_idx16, njmax_pad * njrow)                                                                   \
   X(world_order, 1) X(world_key, 1)
 
 /* ---- contact pool: float arrays, (naconmax, count) ---- */

@@ -290,9 +290,16 @@ __device__ void com_pos(const mjw_model_t& m, const mjw_data_t& d, int wid) {
   const float* body_subtreemass = MR(body_subtreemass);
   float* sc = d.subtree_com + (long)wid * nb * 3;
   for (int b = tid(); b < nb; b += BLK) {
-    float s[3] = {0.0f, 0.0f, 0.0f};
+    // compensated (Kahan) sums: the world body's subtree spans every body (~900 flex vertices on the
+    // cloth), where a plain fp32 running sum drifted to 1.5e-5 of the oracle's fp64 value
+    float s[3] = {0.0f, 0.0f, 0.0f}, comp[3] = {0.0f, 0.0f, 0.0f};
     for (int c = b; c < m.body_subtree_end[b]; c++)
-      for (int i = 0; i < 3; i++) s[i] += xipos[3 * c + i] * body_mass[c];
+      for (int i = 0; i < 3; i++) {
+        const float y = fmaf(xipos[3 * c + i], body_mass[c], -comp[i]);
+        const float t = s[i] + y;
+        comp[i] = (t - s[i]) - y;
+        s[i] = t;
+      }
     const float mass = body_subtreemass[b];
     for (int i = 0; i < 3; i++) sc[3 * b + i] = mass != 0.0f ? s[i] / mass : s[i];
   }
@@ -1870,9 +1877,10 @@ struct SolveCtx {
   int nv, nefc, ne, nf, njrow, P;
   const float* J;     // slot-major: slot k of row r at J[k * P + r]
   const int* Jcol;
+  const unsigned short* Jcol16;  // 16-bit copy of Jcol for the CG passes (solve_kernel<0> writes it)
   const int* Jnnz;
-  const int* JT_adr;  // J transposed (CSR by dof): rows JT_ind[p], values JT_val[p]
-  const int* JT_ind;
+  const int* JT_adr;  // J transposed (CSR by dof): rows JT16[p] (16 bit), values JT_val[p]
+  const unsigned short* JT16;
   const float* JT_val;
   const float* D;
   const float* fl;
@@ -1973,22 +1981,19 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
     const float jaref = jau[u];
     if (alpha != 0.0f) c.Jaref[r] = jaref;
     float f;
-    int st;
     if (r < c.ne) {
       f = -D * jaref;
-      st = STATE_QUADRATIC;
       cost += 0.5f * D * jaref * jaref;
     } else if (r < c.ne + c.nf) {
       const float fl = c.fl[r], rf = safe_div(fl, D);
-      if (jaref <= -rf) { f = fl; st = STATE_LINEARNEG; cost += -fl * (0.5f * rf + jaref); }
-      else if (jaref >= rf) { f = -fl; st = STATE_LINEARPOS; cost += -fl * (0.5f * rf - jaref); }
-      else { f = -D * jaref; st = STATE_QUADRATIC; cost += 0.5f * D * jaref * jaref; }
+      if (jaref <= -rf) { f = fl; cost += -fl * (0.5f * rf + jaref); }
+      else if (jaref >= rf) { f = -fl; cost += -fl * (0.5f * rf - jaref); }
+      else { f = -D * jaref; cost += 0.5f * D * jaref * jaref; }
     } else {
-      if (jaref >= 0.0f) { f = 0.0f; st = STATE_SATISFIED; }
-      else { f = -D * jaref; st = STATE_QUADRATIC; cost += 0.5f * D * jaref * jaref; }
+      if (jaref >= 0.0f) { f = 0.0f; }
+      else { f = -D * jaref; cost += 0.5f * D * jaref * jaref; }
     }
     c.force[r] = f;
-    c.state[r] = st;
   }
   }
   __syncthreads();
@@ -1999,7 +2004,7 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
     const int pa = c.JT_adr[i], pb = c.JT_adr[i + 1];
     int p = pa;
     for (; p + 4 <= pb; p += 4) {
-      const int r0 = c.JT_ind[p], r1 = c.JT_ind[p + 1], r2 = c.JT_ind[p + 2], r3 = c.JT_ind[p + 3];
+      const int r0 = c.JT16[p], r1 = c.JT16[p + 1], r2 = c.JT16[p + 2], r3 = c.JT16[p + 3];
       const float v0 = c.JT_val[p], v1 = c.JT_val[p + 1], v2 = c.JT_val[p + 2], v3 = c.JT_val[p + 3];
       const float f0 = c.force[r0], f1 = c.force[r1], f2 = c.force[r2], f3 = c.force[r3];
       s += v0 * f0;
@@ -2007,7 +2012,7 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
       s += v2 * f2;
       s += v3 * f3;
     }
-    for (; p < pb; p++) s += c.JT_val[p] * c.force[c.JT_ind[p]];
+    for (; p < pb; p++) s += c.JT_val[p] * c.force[c.JT16[p]];
     c.qfrc_c[i] = s;
     g += (c.Ma[i] - c.qfrc_s[i]) * (c.qacc[i] - c.qacc_s[i]);
   }
@@ -2016,6 +2021,22 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   c.prev_cost = c.cost;
   c.gauss = 0.5f * v[1];
   c.cost = v[0] + 0.5f * v[1];
+}
+
+// efc_state of the final Jaref (solver.py:2154-2219), written once after the iterations: the CG itself
+// never reads it, so update_constraint does not store it every iteration
+__device__ void write_states(const SolveCtx& c) {
+  for (int r = tid(); r < c.nefc; r += nthr()) {
+    const float D = c.D[r], jaref = c.Jaref[r];
+    int st = STATE_QUADRATIC;
+    if (r >= c.ne && r < c.ne + c.nf) {
+      const float fl = c.fl[r], rf = safe_div(fl, D);
+      st = jaref <= -rf ? STATE_LINEARNEG : (jaref >= rf ? STATE_LINEARPOS : STATE_QUADRATIC);
+    } else if (r >= c.ne + c.nf) {
+      st = jaref >= 0.0f ? STATE_SATISFIED : STATE_QUADRATIC;
+    }
+    c.state[r] = st;
+  }
 }
 
 __device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
@@ -2060,7 +2081,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
       for (int u = 0; u < RU; u++) {
         const long q = (long)k * c.P + r0 + u * nthr();
         v[u] = k < nz[u] ? c.J[q] : 0.0f;
-        col[u] = k < nz[u] ? c.Jcol[q] : 0;
+        col[u] = k < nz[u] ? c.Jcol16[q] : 0;
       }
 #pragma unroll
       for (int u = 0; u < RU; u++)
@@ -2202,8 +2223,14 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
   int* cnt = (nv + 1) <= SP_LDS_CNT_MAX ? s_cnt : d.sp_cnt + (long)wid * (nv + 1);
   float* JT_val = d.efc_JT_val + (long)wid * d.njmax_pad * m.njrow;
   c.JT_adr = JT_adr;
-  c.JT_ind = JT_ind;
   c.JT_val = JT_val;
+  // 16-bit indices (rows < 65536 and dofs < 65535, io.make_data checks): half the index bytes that every
+  // CG iteration streams twice (the jv pass's columns, the J'f gathers' rows)
+  unsigned short* idx16 = reinterpret_cast<unsigned short*>(d.sp_idx16 + (long)wid * d.njmax_pad * m.njrow);
+  unsigned short* Jcol16 = idx16;
+  unsigned short* JT16 = idx16 + P * m.njrow;
+  c.Jcol16 = Jcol16;
+  c.JT16 = JT16;
   c.D = d.efc_D + (long)wid * d.njmax_pad;
   c.fl = d.efc_frictionloss + (long)wid * njmax;
   c.aref = d.efc_aref + (long)wid * njmax;
@@ -2264,6 +2291,7 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
     for (int k = 0; k < c.Jnnz[r]; k++) {
       const float v = c.J[k * P + r];
       const int col = c.Jcol[k * P + r];
+      Jcol16[k * P + r] = (unsigned short)col;
       const int pos = atomicAdd(&cnt[col], 1);
       JT_ind[pos] = r * m.njrow + k;
       JT_val[pos] = v;
@@ -2300,7 +2328,7 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
 #pragma unroll
       for (int j = 0; j < SORTN; j++)
         if (j < n) {
-          JT_ind[a + j] = key[j] / m.njrow;  // code -> row
+          JT16[a + j] = (unsigned short)(key[j] / m.njrow);  // code -> row
           JT_val[a + j] = val[j];
         }
       continue;
@@ -2313,7 +2341,7 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
       JT_ind[q + 1] = key;
       JT_val[q + 1] = kv;
     }
-    for (int p = a; p < b; p++) JT_ind[p] /= m.njrow;  // code -> row
+    for (int p = a; p < b; p++) JT16[p] = (unsigned short)(JT_ind[p] / m.njrow);  // code -> row
   }
   return;
   }
@@ -2365,6 +2393,7 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
       if (improvement < tol || gradient < tol || niter == m.opt_iterations) break;
     }
   }
+  write_states(c);
   if (tid() == 0) d.solver_niter[wid] = niter;
 }
 

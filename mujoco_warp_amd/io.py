@@ -440,7 +440,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     ne=(), nf=(), nl=(), nefc=(), solver_niter=(), moment_rownnz=(nu,), moment_rowadr=(nu,), moment_colind=(m.nJmom,),
     efc_type=(njmax,), efc_id=(njmax,), efc_state=(njmax_pad,), eq_active=(m.neq,),
     efc_J_colind=(m.njrow * sp, njmax_pad), efc_J_rownnz=(njmax * sp,), efc_JT_rowind=(njmax_pad * m.njrow * sp,),
-    efc_JT_adr=((nv + 1) * sp,), sp_cnt=((nv + 1) * sp,), ncon_world=(2,),
+    efc_JT_adr=((nv + 1) * sp,), sp_cnt=((nv + 1) * sp,), ncon_world=(2,), sp_idx16=(njmax_pad * m.njrow * sp,),
     # the dense path's longest-first world order (mjw_step.hip) and each world's iteration bucket
     world_order=(), world_key=(),
   )
@@ -514,6 +514,9 @@ def _alloc_data(m, nworld, nconmax, njmax, naconmax, device, nccdmax=None, njmax
   if njmax_nnz is None:
     njmax_nnz = njmax * m.nv
   njmax_pad, _ = _padded_sizes(m.nv, njmax, False)
+  if m.is_sparse and (njmax_pad > 65536 or m.nv > 65535):
+    # the sparse CG keeps its row / dof indices in 16 bits (sp_idx16, csrc/mjw_sparse.hip)
+    raise NotImplementedError(f"sparse / flex models: njmax ({njmax}) must be <= 65536 and nv ({m.nv}) <= 65535 in this build.")
   real, ints, creal, cint = _data_shapes(m, nworld, njmax, njmax_pad, naconmax)
   d = types.Data()
   d.nworld, d.njmax, d.njmax_pad, d.naconmax, d.nconmax = nworld, njmax, njmax_pad, naconmax, nconmax
