@@ -283,25 +283,45 @@ __device__ void kinematics(const mjw_model_t& m, const mjw_data_t& d, int wid) {
 // ---------------------------------------------------------------------------------------------
 // smooth.py:463-632 com_pos: subtree com (DFS subtree-range sums), cinert, cdof
 // ---------------------------------------------------------------------------------------------
-__device__ void com_pos(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+__device__ void com_pos(const mjw_model_t& m, const mjw_data_t& d, int wid, Smem& sm) {
   const int nb = m.nbody;
   const float* xipos = d.xipos + (long)wid * nb * 3;
   const float* body_mass = MR(body_mass);
   const float* body_subtreemass = MR(body_subtreemass);
   float* sc = d.subtree_com + (long)wid * nb * 3;
+  // subtrees of up to BIG bodies: one thread each, serial; larger ones (the world body's spans every
+  // flex vertex, ~900 on the cloth) as block-wide sums: a serial fp32 running sum over them drifted to
+  // 1.5e-5 of the oracle's fp64 value and sat on the critical path of the whole block
+  constexpr int BIG = 64, NBIG = 16;
+  __shared__ int big[NBIG];
+  __shared__ int nbig;
+  if (tid() == 0) nbig = 0;
+  __syncthreads();
   for (int b = tid(); b < nb; b += BLK) {
-    // compensated (Kahan) sums: the world body's subtree spans every body (~900 flex vertices on the
-    // cloth), where a plain fp32 running sum drifted to 1.5e-5 of the oracle's fp64 value
-    float s[3] = {0.0f, 0.0f, 0.0f}, comp[3] = {0.0f, 0.0f, 0.0f};
-    for (int c = b; c < m.body_subtree_end[b]; c++)
-      for (int i = 0; i < 3; i++) {
-        const float y = fmaf(xipos[3 * c + i], body_mass[c], -comp[i]);
-        const float t = s[i] + y;
-        comp[i] = (t - s[i]) - y;
-        s[i] = t;
+    if (m.body_subtree_end[b] - b > BIG) {  // (past NBIG of them: serial here after all)
+      const int k = atomicAdd(&nbig, 1);
+      if (k < NBIG) {
+        big[k] = b;
+        continue;
       }
+    }
+    float s[3] = {0.0f, 0.0f, 0.0f};
+    for (int c = b; c < m.body_subtree_end[b]; c++)
+      for (int i = 0; i < 3; i++) s[i] += xipos[3 * c + i] * body_mass[c];
     const float mass = body_subtreemass[b];
     for (int i = 0; i < 3; i++) sc[3 * b + i] = mass != 0.0f ? s[i] / mass : s[i];
+  }
+  __syncthreads();
+  const int nbg = min(nbig, NBIG);
+  for (int j = 0; j < nbg; j++) {  // uniform: the big subtrees, one block sum each
+    const int b = big[j], e = m.body_subtree_end[b];
+    float v[3] = {0.0f, 0.0f, 0.0f};
+    for (int c = b + tid(); c < e; c += BLK)
+      for (int i = 0; i < 3; i++) v[i] += xipos[3 * c + i] * body_mass[c];
+    block_sum<3>(v, sm);
+    const float mass = body_subtreemass[b];
+    if (tid() == 0)
+      for (int i = 0; i < 3; i++) sc[3 * b + i] = mass != 0.0f ? v[i] / mass : v[i];
   }
   __syncthreads();
   const float* body_inertia = MR(body_inertia);
@@ -1801,7 +1821,7 @@ __global__ void __launch_bounds__(BLK, 4) forward_kernel(const mjw_model_t m, co
   SPROF_T0();
   if constexpr ((S & SP_POS_A) != 0) {
     kinematics(m, d, wid);
-    com_pos(m, d, wid);
+    com_pos(m, d, wid, sm);
     camlight(m, d, wid);
     SPROF_MARK(SPH_KIN);
     flex_edges(m, d, wid);

@@ -12,7 +12,6 @@ report (profiles/r03_parity_models.json holds one); the bars, per quantity:
       - qfrc_spring / qfrc_passive on the flex models: a flex spring force is stiffness x (length -
         length0) and length0 cancels to ~1e-7 m in fp32, so the floor is 1e-6 * max |qfrc_smooth|
         (the force scale of the step), normwise;
-      - subtree_com on the cloth: the world subtree sums ~900 vertex bodies; normwise 3e-5.
   * qacc_smooth (behind a Cholesky solve with M): normwise 1e-5 plus the fp64 backward error
     |M qacc_smooth - qfrc_smooth| <= 1e-5 |qfrc_smooth|.
   * constraint rows: identical counts and types (same order on the dense path; on the sparse path
@@ -58,10 +57,9 @@ def test_smooth_stages(reports, name):
       if e["abs"] > 1e-6 * r["force_scale"]:
         bad.append((f, "abs", e["abs"], r["force_scale"]))
       continue
-    tol = 3e-5 if (name == "cloth" and f == "subtree_com") else SMOOTH_TOL
-    if e["norm"] > tol:
+    if e["norm"] > SMOOTH_TOL:
       bad.append((f, "norm", e["norm"]))
-    if not (name == "cloth" and f == "subtree_com") and e["elem"] > SMOOTH_TOL:
+    if e["elem"] > SMOOTH_TOL:
       bad.append((f, "elem", e["elem"]))
   assert not bad, f"{name}: {bad}"
   assert r["fields"]["qacc_smooth"]["norm"] <= SMOOTH_TOL
