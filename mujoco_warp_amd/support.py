@@ -59,10 +59,13 @@ def get_state(m: Model, d: Data, state: torch.Tensor, sig: int, active: Optional
 def set_state(m: Model, d: Data, state: torch.Tensor, sig: int, active: Optional[torch.Tensor] = None):
   """Copy the state components selected by `sig` from `state` into `d` (support.py:711-830).
 
-  Follows mj_setState's layout.  Two quirks of the reference kernel are not reproduced: it advances
-  the read address by neq - 1 after EQ_ACTIVE (support.py:801, `adr += j`) and swaps the x / y
-  components of MOCAP_POS (support.py:806-808); here every element is read at its mj_stateSize
-  offset, so get_state / set_state round-trip exactly."""
+  Follows mj_setState's layout, which is what the reference's own test asserts (support_test.py:144-180:
+  set_state of mj_getState's vector reproduces every MjData field, eq_active and mocap_pos included).
+  Two quirks of the reference kernel that this test does not reach (its model has no mocap bodies) are
+  therefore not reproduced: it advances the read address by neq - 1 after EQ_ACTIVE (support.py:801,
+  `adr += j`), which shifts the mocap elements that follow, and swaps the x / y components of
+  MOCAP_POS (support.py:806-808).  Here every element is read at its mj_stateSize offset, so
+  get_state / set_state round-trip exactly."""
   if sig >= (1 << State.NSTATE):
     raise ValueError(f"invalid state signature {sig} >= 2^mjNSTATE")
   sel = None if active is None else active.to(torch.bool)
