@@ -2417,7 +2417,9 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
   if (tid() == 0) d.solver_niter[wid] = niter;
 }
 
-// forward.py:326-354 euler with implicit damping (sparse: factor M + dt*diag(damping) per tree)
+// forward.py:326-354 euler with implicit damping (sparse: factor M + dt*diag(damping) per tree), and
+// implicitfast (forward.py:494-510): M - dt qDeriv with qDeriv = sum_a vel_a m_a m_a' - diag(damping)
+// (derivative.py:320-416) on the ancestor rows of the sparse M, which hold exactly that pattern
 __global__ void __launch_bounds__(BLK) euler_kernel(const mjw_model_t m, const mjw_data_t d) {
   const int wid = blockIdx.x;
   const int nv = m.nv;
@@ -2426,10 +2428,45 @@ __global__ void __launch_bounds__(BLK) euler_kernel(const mjw_model_t m, const m
   float* qpos = d.qpos + (long)wid * m.nq;
   const float* qacc = d.qacc + (long)wid * nv;
   const float* adv = qacc;
-  if (!(m.opt_disableflags & (DSBL_EULERDAMP | DSBL_DAMPER))) {
+  const int fl = m.opt_disableflags;
+  const bool implicitfast = m.opt_integrator == INT_IMPLICITFAST;
+  const bool need_implicit = implicitfast ? (fl & (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) != (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)
+                                          : !(fl & (DSBL_EULERDAMP | DSBL_DAMPER));
+  if (need_implicit) {
     float* LD2 = d.sp_LD + (long)wid * m.nM;
     float* q = d.sp_vec + (long)wid * nv * 10 + 6 * nv;
-    factor_trees(m, d.qM + (long)wid * m.nM, LD2, MR(dof_damping), dt);
+    const float* M = d.qM + (long)wid * m.nM;
+    const float* damping = MR(dof_damping);
+    const bool damp = !(fl & DSBL_DAMPER);
+    for (int i = tid(); i < nv; i += BLK) {
+      const int adr = m.M_rowadr[i], nnz = m.M_rownnz[i];
+      for (int p = 0; p < nnz; p++) LD2[adr + p] = M[adr + p];
+      if (damp) LD2[adr + nnz - 1] += dt * damping[i];
+    }
+    __syncthreads();
+    if (implicitfast && m.nu > 0 && !(fl & DSBL_ACTUATION)) {
+      for (int u = 0; u < m.nu; u++) {  // uniform: one actuator's (i >= j) moment pairs per round
+        const float vel = actuator_vel_deriv(m, d, wid, u);
+        if (vel == 0.0f) continue;
+        const long gu = (long)wid * m.nu + u;
+        const int nnz = d.moment_rownnz[gu];
+        const long base = (long)wid * m.nJmom + d.moment_rowadr[gu];
+        for (int p = tid(); p < nnz * nnz; p += BLK) {
+          const int k1 = p / nnz, k2 = p - k1 * nnz;
+          const int i = d.moment_colind[base + k1], j = d.moment_colind[base + k2];
+          if (i < j) continue;
+          const int adr = m.M_rowadr[i], rn = m.M_rownnz[i];
+          int pos = -1;
+          if (i == j) pos = adr + rn - 1;
+          else
+            for (int q2 = 0; q2 < rn - 1; q2++)
+              if (m.M_colind[adr + q2] == j) pos = adr + q2;
+          if (pos >= 0) LD2[pos] -= dt * vel * d.actuator_moment[base + k1] * d.actuator_moment[base + k2];
+        }
+        __syncthreads();
+      }
+    }
+    factor_trees(m, LD2, LD2, nullptr, 0.0f);
     for (int i = tid(); i < nv; i += BLK) q[i] = d.efc_Ma[(long)wid * nv + i];
     __syncthreads();
     solve_trees(m, LD2, q);

@@ -123,8 +123,8 @@ def put_model(mjm, device=None) -> types.Model:
       raise NotImplementedError("sparse / flex models: only the CG solver is supported by this build yet.")
     if mjm.opt.cone != types.ConeType.PYRAMIDAL:
       raise NotImplementedError("sparse / flex models: elliptic cones are not supported by this build yet.")
-    if mjm.opt.integrator != types.IntegratorType.EULER:
-      raise NotImplementedError("sparse / flex models: only the Euler integrator is supported by this build yet.")
+    if mjm.opt.integrator not in (types.IntegratorType.EULER, types.IntegratorType.IMPLICITFAST):
+      raise NotImplementedError("sparse / flex models: only the Euler and implicitfast integrators are supported by this build yet.")
     if getattr(mjm, "nsensor", 0):
       raise NotImplementedError("sparse / flex models: sensors are not supported by this build yet.")
     if getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.JOINT, types.EqType.FLEX))):

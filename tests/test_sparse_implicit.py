@@ -1,0 +1,103 @@
+"""implicitfast on the sparse / flex path (csrc/mjw_sparse.hip euler_kernel): M - dt qDeriv assembled on
+the sparse ancestor rows (forward.py:494-510, derivative.py:320-416), factored per tree.
+
+A 3-link hinge chain with position actuators (kv enters qDeriv off the diagonal through the chain's
+ancestor pattern) and dof damping, forced onto the sparse path with jacobian="sparse", against the
+fp64 oracle and against the same model on the dense path; then aloha_cloth (flex towel, mesh arms,
+position actuators) stepped with implicitfast against the oracle at the solver bar."""
+
+import numpy as np
+import pytest
+
+from tests.common import gpu_from_state, np_, oracle_from_state
+
+CHAIN = """<mujoco><option timestep="0.01" integrator="implicitfast" solver="CG" gravity="0 0 -9.81" jacobian="{jac}"/>
+<worldbody>
+  <body pos="0 0 1"><joint name="j0" type="hinge" axis="0 1 0" damping="0.3"/>
+    <geom type="capsule" fromto="0 0 0 0 0 -0.4" size="0.04" contype="0" conaffinity="0"/>
+    <body pos="0 0 -0.4"><joint name="j1" type="hinge" axis="0 1 0" damping="0.2"/>
+      <geom type="capsule" fromto="0 0 0 0 0 -0.4" size="0.04" contype="0" conaffinity="0"/>
+      <body pos="0 0 -0.4"><joint name="j2" type="hinge" axis="1 0 0" damping="0.1"/>
+        <geom type="capsule" fromto="0 0 0 0 0 -0.3" size="0.03" contype="0" conaffinity="0"/>
+      </body>
+    </body>
+  </body>
+</worldbody>
+<actuator>
+  <position joint="j0" kp="40" kv="3"/>
+  <position joint="j1" kp="30" kv="2"/>
+  <position joint="j2" kp="20" kv="1"/>
+</actuator></mujoco>"""
+
+
+def _chain(jac):
+  from mujoco_warp_amd import mjcf
+
+  return mjcf.load_model_from_string(CHAIN.format(jac=jac))
+
+
+def test_chain_compiles_sparse():
+  import mujoco_warp_amd as mjw
+
+  m = mjw.put_model(_chain("sparse"), device="cpu")
+  assert m.is_sparse and int(m.opt.integrator) == 3
+
+
+@pytest.mark.gpu
+def test_gpu_sparse_implicitfast_matches_oracle_and_dense():
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  nworld = 8
+  rng = np.random.default_rng(3)
+  ms = _chain("sparse")
+  qpos = rng.normal(0, 0.3, (nworld, ms.nq))
+  qvel = rng.normal(0, 2.0, (nworld, ms.nv))
+  ctrl = rng.uniform(-0.5, 0.5, (nworld, ms.nu))
+  m, d = gpu_from_state(ms, qpos, qvel, ctrl, njmax=8, nconmax=4)
+  m2, d2 = gpu_from_state(_chain("dense"), qpos, qvel, ctrl, njmax=8, nconmax=4)
+  om, od = oracle_from_state(ms, qpos, qvel, ctrl, njmax=8, nconmax=4)
+  assert m.is_sparse and not m2.is_sparse
+  for _ in range(3):
+    mjw.step(m, d)
+    mjw.step(m2, d2)
+    od.step()
+  torch.cuda.synchronize()
+  from tests.test_gpu_parity_strict import normwise_close
+
+  # no constraint rows: the step is the smooth dynamics and the implicit solve only
+  normwise_close("qvel", np_(d.qvel), od.qvel)
+  normwise_close("qpos", np_(d.qpos), od.qpos)
+  normwise_close("qvel sparse vs dense", np_(d.qvel), np_(d2.qvel))
+  # the implicit terms matter: the same steps with semi-implicit Euler land far outside the tolerance
+  from mujoco_warp_amd import mjcf
+
+  me = mjcf.load_model_from_string(CHAIN.format(jac="sparse").replace('integrator="implicitfast"', 'integrator="Euler"'))
+  m3, d3 = gpu_from_state(me, qpos, qvel, ctrl, njmax=8, nconmax=4)
+  for _ in range(3):
+    mjw.step(m3, d3)
+  torch.cuda.synchronize()
+  e = np.abs(np_(d3.qvel) - od.qvel).max() / np.abs(od.qvel).max()
+  assert e > 1e-3, e
+
+
+@pytest.mark.gpu
+def test_gpu_aloha_cloth_implicitfast_step():
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from tests.cloth_common import aloha_model, aloha_states
+  from tests.test_gpu_parity_strict import normwise_close
+
+  mjm = aloha_model()
+  mjw.override_model(mjm, ["opt.integrator=implicitfast"])
+  qpos, qvel, ctrl = aloha_states(mjm, 2, seed=5)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=16384, nconmax=4096)
+  om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=16384, nconmax=4096)
+  assert m.is_sparse
+  mjw.step(m, d)
+  od.step()
+  torch.cuda.synchronize()
+  normwise_close("qpos", np_(d.qpos), od.qpos)
+  normwise_close("qvel", np_(d.qvel), od.qvel, tol=5e-3)  # carries the CG solve (solver_test.py:32)
