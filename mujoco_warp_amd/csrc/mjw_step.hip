@@ -2573,8 +2573,12 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   using namespace mjw;
   if (!m || !d) { g_err = std::string(name) + ": null model/data"; return -1; }
   if (d->nworld <= 0) return 0;
+  // sensors (all stages, one kernel after the solver and before the integrator): only the fused
+  // forward / step (the stage entry points, like the reference's fwd_* functions, compute none)
+  const bool full = (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE)) == (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE);
+  const bool acc_sensors = full && m->nsensor > 0 && !(m->opt_disableflags & DSBL_SENSOR);
   if (m->is_sparse) {
-    // workgroup-per-world sparse / flex pipeline (mjw_sparse.hip); no sensors on this path
+    // workgroup-per-world sparse / flex pipeline (mjw_sparse.hip), the same sensor kernel after the solve
     hipStream_t s = (hipStream_t)stream;
     if (stages & ST_POS) {
       hipError_t e = reset_counters(d, s);
@@ -2582,6 +2586,7 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     }
     if (g_ev[0]) (void)hipEventRecord(g_ev[0], s);
     int rc = set_err((hipError_t)sparse_launch(stages & ~ST_EULER, m, d, s), name);
+    if (!rc && acc_sensors) rc = set_err((hipError_t)sensor_launch(m, d, s, 7), name);
     if (g_ev[1]) (void)hipEventRecord(g_ev[1], s);
     if (!rc && (stages & ST_EULER)) rc = set_err((hipError_t)sparse_launch(ST_EULER, m, d, s), name);
     if (g_ev[2]) (void)hipEventRecord(g_ev[2], s);
@@ -2590,10 +2595,6 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   if (m->nv > 64 || m->nbody > 4096) { g_err = std::string(name) + ": model too large for the dense world-per-wave path"; return -2; }
   hipStream_t s = (hipStream_t)stream;
   int rc = 0;
-  // sensors (all stages, one kernel after the solver and before the integrator): only the fused
-  // forward / step (the stage entry points, like the reference's fwd_* functions, compute none)
-  const bool full = (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE)) == (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE);
-  const bool acc_sensors = full && m->nsensor > 0 && !(m->opt_disableflags & DSBL_SENSOR);
   // longest-first world order of the dense kernels (the counter-reset kernel sorts the worlds by the
   // iteration bucket the previous step's solving dense kernel recorded; the dense kernels read
   // world_order; the solving one records this step's buckets): full forward + solve on the dense path

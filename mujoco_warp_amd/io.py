@@ -126,7 +126,9 @@ def put_model(mjm, device=None) -> types.Model:
     if mjm.opt.integrator not in (types.IntegratorType.EULER, types.IntegratorType.IMPLICITFAST):
       raise NotImplementedError("sparse / flex models: only the Euler and implicitfast integrators are supported by this build yet.")
     if getattr(mjm, "nsensor", 0):
-      raise NotImplementedError("sparse / flex models: sensors are not supported by this build yet.")
+      # the sensor kernel (csrc/mjw_sensor.hip) stages a world's body / dof state in 64 KB of LDS
+      if 37 * mjm.nbody + 14 * mjm.nv > 16384:
+        raise NotImplementedError("sparse / flex models: sensors need 37 nbody + 14 nv <= 16384 in this build (the flex bodies exceed it).")
     if getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.JOINT, types.EqType.FLEX))):
       raise NotImplementedError("sparse / flex models: only joint and flex equality constraints are supported by this build yet.")
     if np.any(mjm.jnt_limited & (mjm.jnt_type == JointType.BALL)):

@@ -101,3 +101,47 @@ def test_gpu_aloha_cloth_implicitfast_step():
   torch.cuda.synchronize()
   normwise_close("qpos", np_(d.qpos), od.qpos)
   normwise_close("qvel", np_(d.qvel), od.qvel, tol=5e-3)  # carries the CG solve (solver_test.py:32)
+
+
+SENSED = CHAIN.replace('<geom type="capsule" fromto="0 0 0 0 0 -0.3" size="0.03" contype="0" conaffinity="0"/>',
+                       '<geom type="capsule" fromto="0 0 0 0 0 -0.3" size="0.03" contype="0" conaffinity="0"/>'
+                       '<site name="tip" pos="0 0 -0.3"/>').replace('<position joint="j0"', '<position name="a0" joint="j0"').replace(
+  '</actuator></mujoco>', '''</actuator>
+<sensor>
+  <jointpos joint="j1"/> <jointvel joint="j2"/> <actuatorfrc actuator="a0"/>
+  <accelerometer site="tip"/> <gyro site="tip"/> <velocimeter site="tip"/>
+  <framepos objtype="site" objname="tip"/> <framequat objtype="site" objname="tip"/> <subtreecom body="world"/>
+</sensor></mujoco>''')
+
+
+@pytest.mark.gpu
+def test_gpu_sparse_sensors_match_oracle():
+  """Sensors on the sparse path (the sensor kernel runs after the sparse solve, mjw_step.hip run()):
+  position, velocity and acceleration sensors of the chain against the oracle (no constraint rows, so
+  qacc is the smooth solve and the acceleration sensors are held to the strict bar too)."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+  from tests.test_gpu_parity_strict import normwise_close
+
+  mjm = mjcf.load_model_from_string(SENSED.format(jac="sparse"))
+  assert mjm.nsensor == 9
+  nworld = 6
+  rng = np.random.default_rng(4)
+  qpos = rng.normal(0, 0.3, (nworld, mjm.nq))
+  qvel = rng.normal(0, 2.0, (nworld, mjm.nv))
+  ctrl = rng.uniform(-0.5, 0.5, (nworld, mjm.nu))
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=8, nconmax=4)
+  om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=8, nconmax=4)
+  assert m.is_sparse
+  mjw.forward(m, d)
+  od.forward()
+  torch.cuda.synchronize()
+  normwise_close("sensordata", np_(d.sensordata), od.sensordata)
+  m2, d2 = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=8, nconmax=4)
+  mjw.step(m2, d2)
+  od2 = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=8, nconmax=4)[1]
+  od2.step()
+  torch.cuda.synchronize()
+  normwise_close("sensordata after step", np_(d2.sensordata), od2.sensordata)
