@@ -23,8 +23,8 @@ enum : int { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
 enum : int { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6, GEOM_MESH = 7 };
 enum : int { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
 enum : int { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICIT = 2, INT_IMPLICITFAST = 3 };
-enum : int { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
-enum : int { BIAS_NONE = 0, BIAS_AFFINE = 1 };
+enum : int { GAIN_FIXED = 0, GAIN_AFFINE = 1, GAIN_MUSCLE = 2 };
+enum : int { BIAS_NONE = 0, BIAS_AFFINE = 1, BIAS_MUSCLE = 2 };
 enum : int { DYN_NONE = 0, DYN_INTEGRATOR = 1, DYN_FILTER = 2, DYN_FILTEREXACT = 3, DYN_MUSCLE = 4, DYN_USER = 5 };
 enum : int {
   DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16, DSBL_SPRING = 32,
@@ -71,6 +71,73 @@ __device__ __forceinline__ float next_act(float dt, int dyntype, float tau_prm, 
     a = act + scale * act_dot * dt;
   }
   return clamp ? clampf(a, actrange[0], actrange[1]) : a;
+}
+
+// ---- muscles (util_misc.py:454-600): prm = (range[2], force, scale, lmin, lmax, vmax, fpmax, fvmax),
+// dynprm = (tau_act, tau_deact, tausmooth); acc0 / lengthrange are the actuator's model constants
+__device__ __forceinline__ float muscle_gain_length(float L, float lmin, float lmax) {
+  if (lmin > L || L > lmax) return 0.0f;
+  const float a = 0.5f * (lmin + 1.0f), b = 0.5f * (1.0f + lmax);
+  if (L <= a) {
+    const float x = (L - lmin) / fmaxf(MJW_MINVAL, a - lmin);
+    return 0.5f * x * x;
+  }
+  if (L <= 1.0f) {
+    const float x = (1.0f - L) / fmaxf(MJW_MINVAL, 1.0f - a);
+    return 1.0f - 0.5f * x * x;
+  }
+  if (L <= b) {
+    const float x = (L - 1.0f) / fmaxf(MJW_MINVAL, b - 1.0f);
+    return 1.0f - 0.5f * x * x;
+  }
+  const float x = (lmax - L) / fmaxf(MJW_MINVAL, lmax - b);
+  return 0.5f * x * x;
+}
+
+__device__ __forceinline__ float muscle_gain(float len, float vel, const float* lr, float acc0, const float* prm) {
+  float force = prm[2];
+  if (force < 0.0f) force = prm[3] / fmaxf(MJW_MINVAL, acc0);
+  const float L0 = (lr[1] - lr[0]) / fmaxf(MJW_MINVAL, prm[1] - prm[0]);
+  const float L = prm[0] + (len - lr[0]) / fmaxf(MJW_MINVAL, L0);
+  const float V = vel / fmaxf(MJW_MINVAL, L0 * prm[6]);
+  const float FL = muscle_gain_length(L, prm[4], prm[5]);
+  const float fvmax = prm[8], y = fvmax - 1.0f;
+  float FV;
+  if (V <= -1.0f) FV = 0.0f;
+  else if (V <= 0.0f) FV = (V + 1.0f) * (V + 1.0f);
+  else if (V <= y) FV = fvmax - (y - V) * (y - V) / fmaxf(MJW_MINVAL, y);
+  else FV = fvmax;
+  return -force * FL * FV;
+}
+
+__device__ __forceinline__ float muscle_bias(float len, const float* lr, float acc0, const float* prm) {
+  float force = prm[2];
+  if (force < 0.0f) force = prm[3] / fmaxf(MJW_MINVAL, acc0);
+  const float L0 = (lr[1] - lr[0]) / fmaxf(MJW_MINVAL, prm[1] - prm[0]);
+  const float L = prm[0] + (len - lr[0]) / fmaxf(MJW_MINVAL, L0);
+  const float b = 0.5f * (1.0f + prm[5]), fpmax = prm[7];
+  if (L <= 1.0f) return 0.0f;
+  if (L <= b) {
+    const float x = (L - 1.0f) / fmaxf(MJW_MINVAL, b - 1.0f);
+    return -force * fpmax * 0.5f * x * x;
+  }
+  const float x = (L - b) / fmaxf(MJW_MINVAL, b - 1.0f);
+  return -force * fpmax * (0.5f + x);
+}
+
+__device__ __forceinline__ float muscle_dynamics(float ctrl, float act, const float* prm) {
+  const float ctrlclamp = fminf(fmaxf(ctrl, 0.0f), 1.0f), actclamp = fminf(fmaxf(act, 0.0f), 1.0f);
+  const float tau_act = prm[0] * (0.5f + 1.5f * actclamp), tau_deact = prm[1] / (0.5f + 1.5f * actclamp);
+  const float smooth = prm[2], dctrl = ctrlclamp - act;
+  float tau;
+  if (smooth < MJW_MINVAL) {
+    tau = dctrl > 0.0f ? tau_act : tau_deact;
+  } else {
+    const float x = dctrl / smooth + 0.5f;
+    const float sig = x <= 0.0f ? 0.0f : (x >= 1.0f ? 1.0f : x * x * x * (3.0f * x * (2.0f * x - 5.0f) + 10.0f));
+    tau = tau_deact + (tau_act - tau_deact) * sig;
+  }
+  return dctrl / fmaxf(MJW_MINVAL, tau);
 }
 
 // derivative.py:36-107 (_qderiv_actuator_passive_vel): d force / d velocity scale of actuator a

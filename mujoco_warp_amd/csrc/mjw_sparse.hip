@@ -1742,6 +1742,7 @@ __device__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, int wid
       float act_dot = 0.0f;
       if (dt == DYN_INTEGRATOR) act_dot = ctrl;
       else if (dt == DYN_FILTER || dt == DYN_FILTEREXACT) act_dot = (ctrl - act) / fmaxf(dynprm[10 * a], MJW_MINVAL);
+      else if (dt == DYN_MUSCLE) act_dot = muscle_dynamics(ctrl, act, dynprm + 10 * a);
       d.act_dot[(long)wid * m.na + last] = act_dot;
       ctrl_act = m.actuator_actearly[a]
                    ? next_act(MR(opt_timestep)[0], dt, dynprm[10 * a], MR(actuator_actrange) + 2 * a, act, act_dot, 1.0f, m.actuator_actlimited[a] != 0)
@@ -1754,6 +1755,8 @@ __device__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, int wid
     if (m.actuator_gaintype[a] == GAIN_FIXED) gain = gp[0];
     else if (m.actuator_gaintype[a] == GAIN_AFFINE) gain = gp[0] + gp[1] * len + gp[2] * vel;
     if (m.actuator_biastype[a] == BIAS_AFFINE) bias = bp[0] + bp[1] * len + bp[2] * vel;
+    if (m.actuator_gaintype[a] == GAIN_MUSCLE) gain = muscle_gain(len, vel, MR(actuator_lengthrange) + 2 * a, MR(actuator_acc0)[a], gp);
+    if (m.actuator_biastype[a] == BIAS_MUSCLE) bias = muscle_bias(len, MR(actuator_lengthrange) + 2 * a, MR(actuator_acc0)[a], bp);
     float force = gain * ctrl_act + bias;
     if (m.actuator_forcelimited[a]) force = clampf(force, forcerange[2 * a], forcerange[2 * a + 1]);
     d.actuator_force[gu] = force;

@@ -1722,6 +1722,7 @@ __device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_da
       float act_dot = 0.0f;
       if (dt == DYN_INTEGRATOR) act_dot = ctrl;
       else if (dt == DYN_FILTER || dt == DYN_FILTEREXACT) act_dot = (ctrl - act) / fmaxf(dynprm[10 * a], MJW_MINVAL);
+      else if (TEN && dt == DYN_MUSCLE) act_dot = muscle_dynamics(ctrl, act, dynprm + 10 * a);  // forward.py:671-674
       d.act_dot[(long)wid * m.na + act_last] = act_dot;
       // actearly (forward.py:682-697): the force sees the activation of the next step
       ctrl_act = m.actuator_actearly[a] ? next_act(MR(opt_timestep)[0], dt, dynprm[10 * a], MR(actuator_actrange) + 2 * a, act, act_dot, 1.0f,
@@ -1736,6 +1737,12 @@ __device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_da
     if (gt == 0) gain = gp[0];
     else if (gt == 1) gain = gp[0] + gp[1] * len + gp[2] * vel;
     if (bt == 1) bias = bp[0] + bp[1] * len + bp[2] * vel;
+    if (TEN && (gt == GAIN_MUSCLE || bt == BIAS_MUSCLE)) {  // forward.py:711-727 (the extended instantiation)
+      const float* lr = MR(actuator_lengthrange) + 2 * a;
+      const float acc0 = MR(actuator_acc0)[a];
+      if (gt == GAIN_MUSCLE) gain = muscle_gain(len, vel, lr, acc0, gp);
+      if (bt == BIAS_MUSCLE) bias = muscle_bias(len, lr, acc0, bp);
+    }
     float force = gain * ctrl_act + bias;
     if (m.actuator_forcelimited[a]) force = clampf(force, forcerange[2 * a], forcerange[2 * a + 1]);
     s[L.act_force + a] = force;
@@ -2542,10 +2549,10 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
       (void)hipFuncSetAttribute((const void*)mjw::mjw_kernel<STAGES, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
   });
-  // position-stage kernels without the tendon paths, and without the box narrowphase, for models
-  // that have none (kernel id: K_FWD + 4 STAGES + 2 BOX + TEN)
+  // position-stage kernels without the tendon / muscle paths, and without the box narrowphase, for
+  // models that have none (kernel id: K_FWD + 4 STAGES + 2 BOX + TEN)
   if constexpr ((STAGES & mjw::ST_POS) != 0) {
-    if (m->ntendon == 0) {
+    if (m->ntendon == 0 && m->nmuscle == 0) {
       if (m->nxn_box == 0) {
         hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, false, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
         mjw::trace_launch(s, mjw::K_FWD + 4 * STAGES);

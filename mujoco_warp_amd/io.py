@@ -33,6 +33,14 @@ def _padded_sizes(nv: int, njmax: int, is_sparse: bool):
   return njmax_pad, nv_pad
 
 
+def _muscle_mask(mjm):
+  """Actuators with a muscle gain, bias or activation (forward.py:671-727)."""
+  if not mjm.nu:
+    return np.zeros(0, dtype=bool)
+  return ((np.asarray(mjm.actuator_dyntype) == types.DynType.MUSCLE) | (np.asarray(mjm.actuator_gaintype) == types.GainType.MUSCLE)
+          | (np.asarray(mjm.actuator_biastype) == types.BiasType.MUSCLE))
+
+
 def is_sparse(mjm) -> bool:
   """io.py:67-74."""
   if mjm.opt.jacobian == types.JacobianType.AUTO:
@@ -149,9 +157,11 @@ def put_model(mjm, device=None) -> types.Model:
   if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
       tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) == (6, 6) for a, b in pairs_chk):
     raise NotImplementedError("box-box with NATIVECCD disabled (primitive box_box) is not supported by this build yet.")
-  if mjm.nu and (np.any(mjm.actuator_dyntype == types.DynType.MUSCLE) or np.any(mjm.actuator_gaintype == types.GainType.MUSCLE)
-                 or np.any(mjm.actuator_biastype == types.BiasType.MUSCLE)):
-    raise NotImplementedError("muscle actuators are not supported by this build yet.")
+  muscle = _muscle_mask(mjm)
+  if np.any(muscle):
+    lr = np.asarray(mjm.actuator_lengthrange, np.float64).reshape(-1, 2)[muscle]
+    if np.any(lr[:, 0] >= lr[:, 1]):
+      raise NotImplementedError("muscle actuators need an actuator_lengthrange (lengthrange attribute, or a limited joint / tendon transmission).")
   if np.any((mjm.actuator_trntype > types.TrnType.JOINTINPARENT) & (mjm.actuator_trntype != types.TrnType.TENDON)):
     raise NotImplementedError("only joint and tendon transmissions are supported.")
   ntendon = int(getattr(mjm, "ntendon", 0))
@@ -189,6 +199,7 @@ def put_model(mjm, device=None) -> types.Model:
   m.ntendon = int(getattr(mjm, "ntendon", 0))
   m.nwrap, m.nJten = int(getattr(mjm, "nwrap", 0)), int(getattr(mjm, "nJten", 0))
   m.ten_maxnnz = int(np.max(mjm.ten_J_rownnz)) if m.ntendon else 0  # the reference's max_ten_J_rownnz (io.py:232)
+  m.nmuscle = int(np.sum(_muscle_mask(mjm)))  # > 0 selects the forward kernel compiled with the muscle paths
   m.neq = int(getattr(mjm, "neq", 0))
   m.nsensor = int(getattr(mjm, "nsensor", 0))
   m.nsensordata = int(getattr(mjm, "nsensordata", 0))
@@ -344,7 +355,7 @@ DERIVED_INT_ARRAYS = {
   "tree_dofadr": "tree_dofadr", "flex_cgeomadr": "flex_cgeomadr", "flex_cgeom": "flex_cgeom", "plane_geom": "plane_geom",
   "flexvert_incadr": "flexvert_incadr", "flexvert_inc": "flexvert_inc",
 }
-DERIVED_SCALARS = ("nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz",
+DERIVED_SCALARS = ("nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle",
                    "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane")
 
 

@@ -108,7 +108,7 @@ _INTEGRATORS = {
 _SOLVERS = {"pgs": SolverType.PGS, "cg": SolverType.CG, "newton": SolverType.NEWTON}
 _CONES = {"pyramidal": ConeType.PYRAMIDAL, "elliptic": ConeType.ELLIPTIC}
 _JACOBIANS = {"dense": JacobianType.DENSE, "sparse": JacobianType.SPARSE, "auto": JacobianType.AUTO}
-_ACTUATOR_TAGS = ("motor", "position", "velocity", "general", "intvelocity", "damper")
+_ACTUATOR_TAGS = ("motor", "position", "velocity", "general", "intvelocity", "damper", "muscle")
 
 # MuJoCo default element attribute values (MJCF reference defaults).
 _GEOM_DEFAULTS = dict(
@@ -1448,6 +1448,18 @@ class _Compiler:
           biastype = BiasType.AFFINE
           biasprm[:3] = [0.0, -kp, 0.0]
           dyntype = DynType.INTEGRATOR
+        elif tag == "muscle":
+          # MuJoCo's <muscle> shortcut: muscle gain / bias / activation with its default curve
+          # parameters, gainprm = biasprm = (range[2], force, scale, lmin, lmax, vmax, fpmax, fvmax) and
+          # dynprm = (timeconst[2], tausmooth) (util_misc.py:478-600 unpacks them in this order)
+          gaintype, biastype, dyntype = GainType.MUSCLE, BiasType.MUSCLE, DynType.MUSCLE
+          tc = _floats(a.get("timeconst", "0.01 0.04"), 2)
+          dynprm[:3] = [tc[0], tc[1], float(a.get("tausmooth", 0.0))]
+          rng = _floats(a.get("range", "0.75 1.05"), 2)
+          prm = [rng[0], rng[1], float(a.get("force", -1.0)), float(a.get("scale", 200.0)), float(a.get("lmin", 0.5)),
+                 float(a.get("lmax", 1.6)), float(a.get("vmax", 1.5)), float(a.get("fpmax", 1.3)), float(a.get("fvmax", 1.2))]
+          gainprm[:9] = prm
+          biasprm[:9] = prm
         else:  # general
           gaintype = {"fixed": GainType.FIXED, "affine": GainType.AFFINE, "muscle": GainType.MUSCLE, "user": GainType.USER}[a.get("gaintype", "fixed")]
           biastype = {"none": BiasType.NONE, "affine": BiasType.AFFINE, "muscle": BiasType.MUSCLE, "user": BiasType.USER}[a.get("biastype", "none")]
@@ -1482,6 +1494,7 @@ class _Compiler:
             forcerange=forcerange,
             actrange=actrange,
             actearly=a.get("actearly", "false") == "true",
+            lengthrange=_floats(a.get("lengthrange", "0 0"), 2),
           )
         )
     nu = len(rows)
@@ -1504,7 +1517,22 @@ class _Compiler:
     m.actuator_actrange = np.array([r["actrange"] for r in rows]).reshape(nu, 2)
     m.actuator_actearly = np.array([r["actearly"] for r in rows], dtype=bool)
     m.actuator_cranklength = np.zeros(nu)
-    m.actuator_lengthrange = np.zeros((nu, 2))
+    m.actuator_lengthrange = np.array([r["lengthrange"] for r in rows], dtype=np.float64).reshape(nu, 2)
+    # muscles need the actuator length range (mj_setLengthRange).  MuJoCo finds it at compile time by
+    # simulation; here it is the transmission's limited range times the gear (MuJoCo's `uselimit`
+    # path), unless the element gives lengthrange itself
+    for i, r in enumerate(rows):
+      is_muscle = r["dyntype"] == DynType.MUSCLE or r["gaintype"] == GainType.MUSCLE or r["biastype"] == BiasType.MUSCLE
+      if not is_muscle or m.actuator_lengthrange[i, 0] < m.actuator_lengthrange[i, 1]:
+        continue
+      g = r["gear"][0]
+      rng = None
+      if r["trntype"] in (TrnType.JOINT, TrnType.JOINTINPARENT) and m.jnt_limited[r["trnid"][0]]:
+        rng = m.jnt_range[r["trnid"][0]]
+      elif r["trntype"] == TrnType.TENDON and m.tendon_limited[r["trnid"][0]]:
+        rng = m.tendon_range[r["trnid"][0]]
+      if rng is not None:
+        m.actuator_lengthrange[i] = sorted((g * rng[0], g * rng[1]))
     actadr = -np.ones(nu, dtype=np.int32)
     actnum = np.zeros(nu, dtype=np.int32)
     na = 0

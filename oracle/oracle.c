@@ -33,12 +33,12 @@ enum { STATE_SATISFIED = 0, STATE_QUADRATIC = 1, STATE_LINEARNEG = 2, STATE_LINE
 enum { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
 enum { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICITFAST = 3 };
 enum { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
-enum { GAIN_FIXED = 0, GAIN_AFFINE = 1 };
+enum { GAIN_FIXED = 0, GAIN_AFFINE = 1, GAIN_MUSCLE = 2 };
 enum { DYN_NONE = 0, DYN_INTEGRATOR = 1, DYN_FILTER = 2, DYN_FILTEREXACT = 3, DYN_MUSCLE = 4, DYN_USER = 5 };
 enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2, EQ_FLEX = 4 };
 enum { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum { INTEGRATOR_EULER = 0, INTEGRATOR_RK4 = 1, INTEGRATOR_IMPLICIT = 2, INTEGRATOR_IMPLICITFAST = 3 };
-enum { BIAS_NONE = 0, BIAS_AFFINE = 1 };
+enum { BIAS_NONE = 0, BIAS_AFFINE = 1, BIAS_MUSCLE = 2 };
 enum { TRN_JOINT = 0, TRN_JOINTINPARENT = 1, TRN_TENDON = 3 };
 enum { CNSTR_FRICTION_TENDON = 2, CNSTR_LIMIT_TENDON = 4 };
 enum { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
@@ -2345,6 +2345,55 @@ static real next_act(const orc_model* m, int a, real act, real act_dot, real sca
   return clamp ? clampr(r, m->actuator_actrange[2 * a], m->actuator_actrange[2 * a + 1]) : r;
 }
 
+/* util_misc.py:454-600: muscle length / velocity curves, passive force and activation dynamics;
+   prm = (range[2], force, scale, lmin, lmax, vmax, fpmax, fvmax), dynprm = (tau_act, tau_deact, tausmooth) */
+static real muscle_gain_length(real L, real lmin, real lmax) {
+  if (lmin > L || L > lmax) return 0;
+  real a = 0.5 * (lmin + 1), b = 0.5 * (1 + lmax), x;
+  if (L <= a) { x = (L - lmin) / maxr(MINVAL, a - lmin); return 0.5 * x * x; }
+  if (L <= 1) { x = (1 - L) / maxr(MINVAL, 1 - a); return 1 - 0.5 * x * x; }
+  if (L <= b) { x = (L - 1) / maxr(MINVAL, b - 1); return 1 - 0.5 * x * x; }
+  x = (lmax - L) / maxr(MINVAL, lmax - b);
+  return 0.5 * x * x;
+}
+
+static real muscle_force_scale(const real* prm, real acc0) { return prm[2] < 0 ? prm[3] / maxr(MINVAL, acc0) : prm[2]; }
+
+static real muscle_gain(real len, real vel, const real* lr, real acc0, const real* prm) {
+  real force = muscle_force_scale(prm, acc0);
+  real L0 = (lr[1] - lr[0]) / maxr(MINVAL, prm[1] - prm[0]);
+  real L = prm[0] + (len - lr[0]) / maxr(MINVAL, L0), V = vel / maxr(MINVAL, L0 * prm[6]);
+  real FL = muscle_gain_length(L, prm[4], prm[5]), fvmax = prm[8], y = fvmax - 1, FV;
+  if (V <= -1) FV = 0;
+  else if (V <= 0) FV = (V + 1) * (V + 1);
+  else if (V <= y) FV = fvmax - (y - V) * (y - V) / maxr(MINVAL, y);
+  else FV = fvmax;
+  return -force * FL * FV;
+}
+
+static real muscle_bias(real len, const real* lr, real acc0, const real* prm) {
+  real force = muscle_force_scale(prm, acc0);
+  real L0 = (lr[1] - lr[0]) / maxr(MINVAL, prm[1] - prm[0]);
+  real L = prm[0] + (len - lr[0]) / maxr(MINVAL, L0), b = 0.5 * (1 + prm[5]), x;
+  if (L <= 1) return 0;
+  if (L <= b) { x = (L - 1) / maxr(MINVAL, b - 1); return -force * prm[7] * 0.5 * x * x; }
+  x = (L - b) / maxr(MINVAL, b - 1);
+  return -force * prm[7] * (0.5 + x);
+}
+
+static real muscle_dynamics(real ctrl, real act, const real* prm) {
+  real cc = clampr(ctrl, 0, 1), ac = clampr(act, 0, 1);
+  real tau_act = prm[0] * (0.5 + 1.5 * ac), tau_deact = prm[1] / (0.5 + 1.5 * ac), dctrl = cc - act, tau;
+  if (prm[2] < MINVAL) {
+    tau = dctrl > 0 ? tau_act : tau_deact;
+  } else {
+    real x = dctrl / prm[2] + 0.5;
+    real sig = x <= 0 ? 0 : (x >= 1 ? 1 : x * x * x * (3 * x * (2 * x - 5) + 10));
+    tau = tau_deact + (tau_act - tau_deact) * sig;
+  }
+  return dctrl / maxr(MINVAL, tau);
+}
+
 /* forward.py:616-927: activation dynamics (integrator / filter / filterexact), actearly, gain/bias */
 static void fwd_actuation(const orc_model* m, orc_data* d) {
   int nv = m->nv;
@@ -2364,6 +2413,7 @@ static void fwd_actuation(const orc_model* m, orc_data* d) {
       real act = d->act[last], act_dot = 0;
       if (dyn == DYN_INTEGRATOR) act_dot = ctrl;
       else if (dyn == DYN_FILTER || dyn == DYN_FILTEREXACT) act_dot = (ctrl - act) / maxr(m->actuator_dynprm[10 * a], MINVAL);
+      else if (dyn == DYN_MUSCLE) act_dot = muscle_dynamics(ctrl, act, m->actuator_dynprm + 10 * a);  /* forward.py:671-674 */
       d->act_dot[last] = act_dot;
       ctrl_act = m->actuator_actearly[a] ? next_act(m, a, act, act_dot, 1, m->actuator_actlimited[a]) : act;
     }
@@ -2374,6 +2424,8 @@ static void fwd_actuation(const orc_model* m, orc_data* d) {
     if (m->actuator_gaintype[a] == GAIN_FIXED) gain = gp[0];
     else if (m->actuator_gaintype[a] == GAIN_AFFINE) gain = gp[0] + gp[1] * len + gp[2] * vel;
     if (m->actuator_biastype[a] == BIAS_AFFINE) bias = bp[0] + bp[1] * len + bp[2] * vel;
+    if (m->actuator_gaintype[a] == GAIN_MUSCLE) gain = muscle_gain(len, vel, m->actuator_lengthrange + 2 * a, m->actuator_acc0[a], gp);
+    if (m->actuator_biastype[a] == BIAS_MUSCLE) bias = muscle_bias(len, m->actuator_lengthrange + 2 * a, m->actuator_acc0[a], bp);
     real force = gain * ctrl_act + bias;
     if (m->actuator_forcelimited[a]) force = clampr(force, m->actuator_forcerange[2 * a], m->actuator_forcerange[2 * a + 1]);
     d->actuator_force[a] = force;

@@ -129,7 +129,9 @@ def test_oracle_rk4_free_and_ball_quaternions_stay_unit():
   assert np.isfinite(od.qpos).all()
 
 
-def test_put_model_accepts_rk4_rejects_muscle():
+def test_put_model_accepts_rk4_rejects_muscle_without_lengthrange():
+  """RK4 is accepted; a muscle activation on an actuator whose length range is unknown (no lengthrange
+  attribute, unlimited joint) is refused rather than run with a degenerate range."""
   import mujoco_warp_amd as mjw
 
   mjm = _load(ACT_XML.format(integrator="RK4"))
