@@ -29,7 +29,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 18
+#define MJW_ABI_VERSION 19
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -42,7 +42,7 @@
   X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)                                  \
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
-  X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle)
+  X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -142,7 +142,7 @@
   X(qpos_t0, nq) X(qvel_t0, nv) X(act_t0, na) X(qvel_rk, nv) X(qacc_rk, nv) X(act_dot_rk, na)     \
   X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
   X(flexedge_J, nflexedge * 6) X(flex_frc, nflexelem * 9 + nflexedge * 12)                        \
-  X(sp_body, nbody * 6) X(sp_vec, nv * 10) X(sp_row, njmax * 2) X(sp_LD, nM)                     \
+  X(sp_body, nbody * 6) X(sp_vec, nv * 10) X(sp_row, njmax * 3) X(sp_LD, nM) X(sp_H, sp_nH * sp_nH) \
   X(efc_JT_val, njmax_pad * njrow)                                                                 \
   X(ten_length, ntendon) X(ten_velocity, ntendon) X(ten_J, nJten)
 

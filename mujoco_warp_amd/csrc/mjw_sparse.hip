@@ -1911,6 +1911,9 @@ struct SolveCtx {
   float* force;
   int* state;
   float *Jaref, *jv;
+  float* Dq;   // Newton: D of the rows in the quadratic state, 0 for the others (sp_row's third block)
+  float* H;    // Newton: the dense nv x nv Hessian / its Cholesky factor (sp_H), null for CG
+  bool newton;
   float *qacc, *Ma, *qfrc_c;
   const float *qfrc_s, *qacc_s;
   float *grad, *Mgrad, *search, *mv, *pgrad, *pMgrad;
@@ -2062,6 +2065,85 @@ __device__ void write_states(const SolveCtx& c) {
   }
 }
 
+// Newton direction (solver.py:2879-3008): H = M + J' diag(D quadratic) J (dense, nv x nv, lower
+// triangle, row-major; solver.py:2367-2425 builds the same H for the reference's sparse models),
+// factored in place (right-looking Cholesky, one column per round) and solved for Mgrad = H^-1 grad.
+// J'DJ entries come from the transposed index: rows common to columns i and j, merged in ascending
+// row order -- a fixed summation order, so replicas stay bitwise equal
+__device__ void newton_direction(const mjw_model_t& m, SolveCtx& c) {
+  const int nv = c.nv;
+  float* H = c.H;
+  for (int r = c.ne + tid(); r < c.nefc; r += nthr()) {  // equality rows are always quadratic
+    const float D = c.D[r], ja = c.Jaref[r];
+    bool quad = true;
+    if (r < c.ne + c.nf) {
+      const float rf = safe_div(c.fl[r], D);
+      quad = -rf < ja && ja < rf;
+    } else {
+      quad = ja < 0.0f;
+    }
+    c.Dq[r] = quad ? D : 0.0f;
+  }
+  for (int r = tid(); r < min(c.ne, c.nefc); r += nthr()) c.Dq[r] = c.D[r];
+  __syncthreads();
+  for (int i = tid(); i < nv; i += nthr()) {
+    const int ai = c.JT_adr[i], bi = c.JT_adr[i + 1];
+    for (int j = 0; j <= i; j++) {
+      float s = 0.0f;
+      int p = ai, q = c.JT_adr[j];
+      const int bj = c.JT_adr[j + 1];
+      while (p < bi && q < bj) {
+        const int rp = c.JT16[p], rq = c.JT16[q];
+        if (rp == rq) {
+          s += c.Dq[rp] * c.JT_val[p] * c.JT_val[q];
+          p++;
+          q++;
+        } else if (rp < rq) {
+          p++;
+        } else {
+          q++;
+        }
+      }
+      H[i * nv + j] = s;
+    }
+  }
+  __syncthreads();
+  for (int i = tid(); i < nv; i += nthr()) {  // + M on its ancestor rows (diagonal last)
+    const int adr = m.M_rowadr[i], nnz = m.M_rownnz[i];
+    for (int p = 0; p < nnz - 1; p++) H[i * nv + m.M_colind[adr + p]] += c.M[adr + p];
+    H[i * nv + i] += c.M[adr + nnz - 1];
+  }
+  for (int k = 0; k < nv; k++) {
+    __syncthreads();
+    const float piv = sqrtf(fmaxf(H[k * nv + k], MJW_MINVAL));
+    __syncthreads();
+    if (tid() == 0) H[k * nv + k] = piv;
+    for (int i = k + 1 + tid(); i < nv; i += nthr()) H[i * nv + k] /= piv;
+    __syncthreads();
+    for (int i = k + 1 + tid(); i < nv; i += nthr()) {
+      const float lik = H[i * nv + k];
+      for (int j = k + 1; j <= i; j++) H[i * nv + j] -= lik * H[j * nv + k];
+    }
+  }
+  __syncthreads();
+  // L y = grad, then L' x = y, in Mgrad (one pivot per round, the updates in parallel)
+  float* x = c.Mgrad;
+  for (int k = 0; k < nv; k++) {
+    const float yk = x[k] / H[k * nv + k];
+    __syncthreads();
+    if (tid() == 0) x[k] = yk;
+    for (int i = k + 1 + tid(); i < nv; i += nthr()) x[i] -= H[i * nv + k] * yk;
+    __syncthreads();
+  }
+  for (int k = nv - 1; k >= 0; k--) {
+    const float xk = x[k] / H[k * nv + k];
+    __syncthreads();
+    if (tid() == 0) x[k] = xk;
+    for (int i = tid(); i < k; i += nthr()) x[i] -= H[k * nv + i] * xk;
+    __syncthreads();
+  }
+}
+
 __device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
   float gd = 0.0f;
   for (int i = tid(); i < c.nv; i += nthr()) {
@@ -2071,7 +2153,8 @@ __device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
     gd += g * g;
   }
   c.grad_dot = block_sum1_db(gd, sm, c.rphase);  // syncs
-  solve_trees(m, c.LD, c.Mgrad);
+  if (c.newton) newton_direction(m, c);
+  else solve_trees(m, c.LD, c.Mgrad);
   __syncthreads();
 }
 
@@ -2259,8 +2342,11 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
   c.aref = d.efc_aref + (long)wid * njmax;
   c.force = d.efc_force + (long)wid * njmax;
   c.state = d.efc_state + (long)wid * d.njmax_pad;
-  c.Jaref = d.sp_row + (long)wid * njmax * 2;
+  c.Jaref = d.sp_row + (long)wid * njmax * 3;
   c.jv = c.Jaref + njmax;
+  c.Dq = c.Jaref + 2 * njmax;
+  c.newton = m.opt_solver == SOLVER_NEWTON && m.sp_nH == nv;
+  c.H = c.newton ? d.sp_H + (long)wid * nv * nv : nullptr;
   if constexpr (PART == 2) {
     float* rows = reinterpret_cast<float*>(s_cnt);
     for (int r = tid(); r < c.nefc; r += nthr()) rows[r] = c.Jaref[r];
@@ -2401,7 +2487,8 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
         nd[1] += c.pgrad[i] * c.pMgrad[i];
       }
       block_sum_db<2>(nd, sm, c.rphase);
-      const float beta = fmaxf(0.0f, nd[0] / fmaxf(MJW_MINVAL, nd[1]));
+      // Polak-Ribiere for CG; Newton steps along -H^-1 grad (solver.py:3141-3144)
+      const float beta = c.newton ? 0.0f : fmaxf(0.0f, nd[0] / fmaxf(MJW_MINVAL, nd[1]));
       float s2 = 0.0f;
       for (int i = tid(); i < nv; i += nthr()) {
         const float v = -c.Mgrad[i] + beta * c.search[i];

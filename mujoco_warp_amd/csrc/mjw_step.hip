@@ -2586,6 +2586,10 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   const bool acc_sensors = full && m->nsensor > 0 && !(m->opt_disableflags & DSBL_SENSOR);
   if (m->is_sparse) {
     // workgroup-per-world sparse / flex pipeline (mjw_sparse.hip), the same sensor kernel after the solve
+    if ((stages & ST_SOLVE) && m->opt_solver == SOLVER_NEWTON && m->sp_nH != m->nv) {
+      g_err = std::string(name) + ": sparse Newton needs the Hessian workspace (put_model with opt.solver = NEWTON, nv <= 256)";
+      return -5;
+    }
     hipStream_t s = (hipStream_t)stream;
     if (stages & ST_POS) {
       hipError_t e = reset_counters(d, s);

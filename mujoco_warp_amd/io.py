@@ -33,6 +33,9 @@ def _padded_sizes(nv: int, njmax: int, is_sparse: bool):
   return njmax_pad, nv_pad
 
 
+SPARSE_NEWTON_NVMAX = 256
+
+
 def _muscle_mask(mjm):
   """Actuators with a muscle gain, bias or activation (forward.py:671-727)."""
   if not mjm.nu:
@@ -127,8 +130,9 @@ def put_model(mjm, device=None) -> types.Model:
   sparse = is_sparse(mjm) or getattr(mjm, "nflex", 0) > 0
   if sparse:
     # the workgroup-per-world sparse / flex pipeline (csrc/mjw_sparse.hip) covers this subset
-    if mjm.opt.solver != types.SolverType.CG:
-      raise NotImplementedError("sparse / flex models: only the CG solver is supported by this build yet.")
+    if mjm.opt.solver == types.SolverType.NEWTON and mjm.nv > SPARSE_NEWTON_NVMAX:
+      # Newton's Hessian is dense (nv x nv per world, as the reference's H), so the flex models stay on CG
+      raise NotImplementedError(f"sparse / flex models: Newton needs nv <= {SPARSE_NEWTON_NVMAX} in this build (nv = {mjm.nv}); use CG.")
     if mjm.opt.cone != types.ConeType.PYRAMIDAL:
       raise NotImplementedError("sparse / flex models: elliptic cones are not supported by this build yet.")
     if mjm.opt.integrator not in (types.IntegratorType.EULER, types.IntegratorType.IMPLICITFAST):
@@ -200,6 +204,8 @@ def put_model(mjm, device=None) -> types.Model:
   m.nwrap, m.nJten = int(getattr(mjm, "nwrap", 0)), int(getattr(mjm, "nJten", 0))
   m.ten_maxnnz = int(np.max(mjm.ten_J_rownnz)) if m.ntendon else 0  # the reference's max_ten_J_rownnz (io.py:232)
   m.nmuscle = int(np.sum(_muscle_mask(mjm)))  # > 0 selects the forward kernel compiled with the muscle paths
+  # the sparse path's dense Newton Hessian (nv x nv per world), zero-sized otherwise
+  m.sp_nH = int(mjm.nv) if (is_sparse(mjm) or getattr(mjm, "nflex", 0) > 0) and mjm.opt.solver == types.SolverType.NEWTON else 0
   m.neq = int(getattr(mjm, "neq", 0))
   m.nsensor = int(getattr(mjm, "nsensor", 0))
   m.nsensordata = int(getattr(mjm, "nsensordata", 0))
@@ -355,7 +361,7 @@ DERIVED_INT_ARRAYS = {
   "tree_dofadr": "tree_dofadr", "flex_cgeomadr": "flex_cgeomadr", "flex_cgeom": "flex_cgeom", "plane_geom": "plane_geom",
   "flexvert_incadr": "flexvert_incadr", "flexvert_inc": "flexvert_inc",
 }
-DERIVED_SCALARS = ("nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle",
+DERIVED_SCALARS = ("nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle", "sp_nH",
                    "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane")
 
 
@@ -444,7 +450,8 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     # flex (smooth.py:228-355) and the sparse path's workspace (size 0 on the dense path)
     flexvert_xpos=(m.nflexvert, 3), flexedge_length=(m.nflexedge,), flexedge_velocity=(m.nflexedge,),
     flexedge_J=(m.nflexedge, 6), flex_frc=(m.nflexelem * 9 + m.nflexedge * 12,),
-    sp_body=(nb * 6 * sp,), sp_vec=(nv * 10 * sp,), sp_row=(njmax * 2 * sp,), sp_LD=(m.nM * sp,),
+    sp_body=(nb * 6 * sp,), sp_vec=(nv * 10 * sp,), sp_row=(njmax * 3 * sp,), sp_LD=(m.nM * sp,),
+    sp_H=(m.sp_nH * m.sp_nH,),
     efc_JT_val=(njmax_pad * m.njrow * sp,),
     # fixed tendons (smooth.py:3085-3121): lengths, velocities, sparse Jacobian (ten_J_rowadr / _colind)
     ten_length=(m.ntendon,), ten_velocity=(m.ntendon,), ten_J=(m.nJten,),

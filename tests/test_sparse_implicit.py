@@ -145,3 +145,51 @@ def test_gpu_sparse_sensors_match_oracle():
   od2.step()
   torch.cuda.synchronize()
   normwise_close("sensordata after step", np_(d2.sensordata), od2.sensordata)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("integrator", ["Euler", "implicitfast"])
+def test_gpu_sparse_newton_humanoid_matches_oracle(integrator):
+  """Newton on the sparse path (dense H = M + J'DJ per world, solver.py:2879-3008, as the reference
+  builds for its sparse models): the humanoid forced onto the sparse path (jacobian="sparse") in
+  contact, against the fp64 oracle at the solver bar (cost excess, qacc 5e-3), and one step."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from tests.common import humanoid_model, random_states
+  from tests.parity_models import efc_cost
+  from tests.test_gpu_parity_strict import normwise_close
+
+  mjm = humanoid_model("NEWTON")
+  mjw.override_model(mjm, ["opt.jacobian=sparse", f"opt.integrator={integrator}"])
+  nworld = 16
+  qpos, qvel, ctrl = random_states(mjm, nworld, seed=12)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl)
+  om, od = oracle_from_state(mjm, qpos, qvel, ctrl)
+  assert m.is_sparse and m.sp_nH == mjm.nv
+  for st in ("fwd_position", "fwd_velocity", "fwd_actuation", "fwd_acceleration"):
+    getattr(mjw, st)(m, d)
+    getattr(od, st)()
+  mjw.solve(m, d)
+  od.solve()
+  torch.cuda.synchronize()
+  nv = mjm.nv
+  worst = 0.0
+  for w in range(nworld):
+    n = int(od.nefc[w, 0])
+    assert n > 0 and int(d.nefc[w]) == n
+    J = od.efc_J[w].reshape(od.njmax, nv)[:n]
+    args = (J, od.efc_D[w, :n], od.efc_aref[w, :n], od.efc_type[w, :n], od.qM[w].reshape(nv, nv), od.qacc_smooth[w])
+    c_or = efc_cost(*args, od.qacc[w], fl=od.efc_frictionloss[w, :n])
+    c_gpu = efc_cost(*args, np_(d.qacc[w]), fl=od.efc_frictionloss[w, :n])
+    worst = max(worst, (c_gpu - c_or) / abs(c_or))
+  assert worst <= 1e-5, worst
+  normwise_close("qacc", np_(d.qacc), od.qacc, tol=5e-3)
+  assert int(np_(d.solver_niter).max()) <= 10  # Newton converges in a few iterations (CG takes tens)
+  m2, d2 = gpu_from_state(mjm, qpos, qvel, ctrl)
+  od2 = oracle_from_state(mjm, qpos, qvel, ctrl)[1]
+  mjw.step(m2, d2)
+  od2.step()
+  torch.cuda.synchronize()
+  normwise_close("qpos", np_(d2.qpos), od2.qpos)
+  normwise_close("qvel", np_(d2.qvel), od2.qvel, tol=5e-3)
