@@ -363,9 +363,24 @@ __device__ __forceinline__ bool aabb_filter(const float* c1, const float* c2, co
   return true;
 }
 
-// collision_core.py:235-341 (geom mixing; explicit <pair> entries are not produced by this build's compiler)
-__device__ __forceinline__ void contact_params(const mjw_model_t& m, int wid, int g1, int g2, float* margin, float* gap, int* condim,
-                               float* friction, float* solref, float* solimp) {
+// collision_core.py:235-341: an explicit <pair> (pairid > -1, nxn_pairid[.][0]) supplies every parameter
+// (:270-277); otherwise the geoms' parameters are mixed.  solreffriction (elliptic friction rows) is
+// non-zero for explicit pairs only; `solreffriction` may be null where the caller reads it from the pair.
+__device__ __forceinline__ void contact_params(const mjw_model_t& m, int wid, int g1, int g2, int pairid, float* margin, float* gap,
+                                               int* condim, float* friction, float* solref, float* solimp,
+                                               float* solreffriction = nullptr) {
+  if (pairid > -1) {
+    *margin = MR(pair_margin)[pairid];
+    *gap = MR(pair_gap)[pairid];
+    *condim = m.pair_dim[pairid];
+    for (int i = 0; i < 5; i++) friction[i] = fmaxf(MJW_MINMU, MR(pair_friction)[5 * pairid + i]);
+    for (int i = 0; i < 2; i++) solref[i] = MR(pair_solref)[2 * pairid + i];
+    for (int i = 0; i < 5; i++) solimp[i] = MR(pair_solimp)[5 * pairid + i];
+    if (solreffriction)
+      for (int i = 0; i < 2; i++) solreffriction[i] = MR(pair_solreffriction)[2 * pairid + i];
+    return;
+  }
+  if (solreffriction) solreffriction[0] = solreffriction[1] = 0.0f;
   const float* geom_solmix = MR(geom_solmix);
   const float* geom_friction = MR(geom_friction);
   const float* geom_solref = MR(geom_solref);

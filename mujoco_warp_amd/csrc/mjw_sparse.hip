@@ -889,9 +889,8 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
     if (npassed) (*npassed)++;
     ConOut o;
     float gap;
-    contact_params(m, wid, g1, g2, &o.margin, &gap, &o.condim, o.friction, o.solref, o.solimp);
+    contact_params(m, wid, g1, g2, m.nxn_pairid[2 * item], &o.margin, &gap, &o.condim, o.friction, o.solref, o.solimp, o.solreffriction);
     o.includemargin = o.margin - gap;
-    o.solreffriction[0] = o.solreffriction[1] = 0.0f;
     o.g1 = g1;
     o.g2 = g2;
     o.flex = o.vert = -1;
@@ -1884,7 +1883,9 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
       put_cgeom(W + CL.geoms + CGEOM_WORDS, gx + 3 * g2, gm + 9 * g2, gsize + 3 * g2, t2, md2 >= 0 ? m.mesh_vertadr[md2] : 0,
                 md2 >= 0 ? m.mesh_vertnum[md2] : 0);
       __syncthreads();
-      const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, gmargin[g1] + gmargin[g2], mesh_vert);
+      const int pid = m.nxn_pairid[2 * q];  // explicit <pair>: its own margin (collision_core.py:271)
+      const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations,
+                              pid > -1 ? MR(pair_margin)[pid] : gmargin[g1] + gmargin[g2], mesh_vert);
       float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[q]) * CCD_OUT;
       if (lane < CCD_OUT) out[lane] = lane == 0 ? (float)nc : (nc > 0 ? W[CL.out + lane - 1] : 0.0f);
       __syncthreads();

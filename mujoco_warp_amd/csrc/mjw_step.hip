@@ -1112,7 +1112,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           g1 = m.nxn_geom_pair[2 * p];
           g2 = m.nxn_geom_pair[2 * p + 1];
           pairid0 = m.nxn_pairid[2 * p];
-          margin = geom_margin[g1] + geom_margin[g2];
+          margin = pairid0 > -1 ? MR(pair_margin)[pairid0] : geom_margin[g1] + geom_margin[g2];
           pbox = BOX && m.geom_type[g1] == GEOM_PLANE && m.geom_type[g2] == GEOM_BOX;
           ccd = BOX && m.geom_type[g1] == GEOM_BOX && m.geom_type[g2] == GEOM_BOX;
           if (ccd) {
@@ -1154,7 +1154,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         if (stage0 || stage1 || stagebox) {
           float gap, friction[5], solref[2], solimp[5];
           int condim;
-          contact_params(m, wid, g1, g2, &margin, &gap, &condim, friction, solref, solimp);
+          contact_params(m, wid, g1, g2, pairid0, &margin, &gap, &condim, friction, solref, solimp);
           // body and weld-body ids, packed: resolved here for all staged pairs at once instead of
           // per contact inside the serial row loops below
           const int cb1 = m.geom_bodyid[g1], cb2 = m.geom_bodyid[g2];
@@ -1183,7 +1183,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
               reinterpret_cast<int*>(rec)[32] = croots;
               for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
               int* reci = reinterpret_cast<int*>(rec);
-              reci[28] = condim;
+              reci[28] = condim | ((pairid0 + 1) << 8);  // + the explicit <pair> id
               reci[29] = g1;
               reci[30] = g2;
             }
@@ -1204,7 +1204,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
               reinterpret_cast<int*>(rec)[32] = croots;
               for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
               int* reci = reinterpret_cast<int*>(rec);
-              reci[28] = condim;
+              reci[28] = condim | ((pairid0 + 1) << 8);  // + the explicit <pair> id
               reci[29] = g1;
               reci[30] = g2;
             }
@@ -1228,7 +1228,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
               reinterpret_cast<int*>(rec)[32] = croots;
               for (int i = 0; i < 5; i++) rec[23 + i] = solimp[i];
               int* reci = reinterpret_cast<int*>(rec);
-              reci[28] = condim;
+              reci[28] = condim | ((pairid0 + 1) << 8);  // + the explicit <pair> id
               reci[29] = g1;
               reci[30] = g2;
             }
@@ -1250,7 +1250,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       int nrow = 0;
       if (lane < nstage) {
         const float* rec = s + L.con + lane * CREC;
-        int condim = reinterpret_cast<const int*>(rec)[28];
+        int condim = reinterpret_cast<const int*>(rec)[28] & 0xff;
         float pos = rec[0] - rec[1];
         // a contact past the global pool is dropped with its rows (collision_core.py:212-231)
         nrow = (pos < 0.0f && gbase + lane < d.naconmax) ? (condim == 1 ? 1 : (ell ? condim : 2 * (condim - 1))) : 0;
@@ -1272,9 +1272,13 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           for (int i = 0; i < 9; i++) d.contact_frame[9L * cid + i] = rec[5 + i];
           d.contact_includemargin[cid] = rec[1];
           for (int i = 0; i < 5; i++) d.contact_friction[5L * cid + i] = rec[14 + i];
-          for (int i = 0; i < 2; i++) { d.contact_solref[2L * cid + i] = rec[19 + i]; d.contact_solreffriction[2L * cid + i] = 0.0f; }
+          const int pid = (reci[28] >> 8) - 1;
+          for (int i = 0; i < 2; i++) {
+            d.contact_solref[2L * cid + i] = rec[19 + i];
+            d.contact_solreffriction[2L * cid + i] = pid > -1 ? MR(pair_solreffriction)[2 * pid + i] : 0.0f;
+          }
           for (int i = 0; i < 5; i++) d.contact_solimp[5L * cid + i] = rec[23 + i];
-          d.contact_dim[cid] = reci[28];
+          d.contact_dim[cid] = reci[28] & 0xff;
           d.contact_geom[2L * cid] = reci[29];
           d.contact_geom[2L * cid + 1] = reci[30];
           d.contact_worldid[cid] = wid;
@@ -1292,7 +1296,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       for (int cc = 0; cc < nstage; cc++) {
         const float* rec = s + L.con + cc * CREC;
         const int* reci = reinterpret_cast<const int*>(rec);
-        int condim = reci[28];
+        int condim = reci[28] & 0xff;
         int r0 = si[L.iscratch + cc];
         float pos = rec[0] - rec[1];
         if (!(pos < 0.0f) || gbase + cc >= d.naconmax) continue;
@@ -1346,7 +1350,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         while (cc + 1 < nstage && si[L.iscratch + cc + 1] <= r) cc++;
         const float* rec = s + L.con + cc * CREC;
         const int* reci = reinterpret_cast<const int*>(rec);
-        int condim = reci[28];
+        int condim = reci[28] & 0xff;
         int dimid = r - si[L.iscratch + cc];
         const int body1 = reci[22] & 0xffff, body2 = reci[22] >> 16;
         float invweight = body_invweight0[2 * body1] + body_invweight0[2 * body2];
@@ -1354,9 +1358,15 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         float pos = rec[0] - rec[1];
         if (ell && condim > 1) {
           // constraint.py:2168-2195: friction rows scale invweight by impratio^-1 (fri0 / frii)^2 and have
-          // no position term (solreffriction is zero: no explicit <pair>, so solref applies)
+          // no position term; they use solreffriction when an explicit <pair> sets it (:2160-2165)
           float pos_aref = pos;
+          const float* sref = rec + 19;
           if (dimid > 0) {
+            const int pid = (reci[28] >> 8) - 1;
+            if (pid > -1) {
+              const float* srf = MR(pair_solreffriction) + 2 * pid;
+              if (srf[0] != 0.0f || srf[1] != 0.0f) sref = srf;
+            }
             invweight = invweight * impratio_invsqrt * impratio_invsqrt;
             if (dimid > 1) {
               const float fri0 = rec[14], frii = rec[14 + dimid - 1];
@@ -1364,7 +1374,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
             }
             pos_aref = 0.0f;
           }
-          efc_row(m, d, L, s, wid, r, pos_aref, pos, invweight, rec + 19, rec + 23, rec[1], Jqvel, 0.0f, CNSTR_CONTACT_ELLIPTIC, reci[31]);
+          efc_row(m, d, L, s, wid, r, pos_aref, pos, invweight, sref, rec + 23, rec[1], Jqvel, 0.0f, CNSTR_CONTACT_ELLIPTIC, reci[31]);
           continue;
         }
         if (condim > 1) {
@@ -2377,7 +2387,9 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
     if (pass) {
       put_cgeom(W + CL.geoms, s + L.gxpos + 3 * g1, s + L.gxmat + 9 * g1, gsize + 3 * g1, m.geom_type[g1]);
       put_cgeom(W + CL.geoms + CGEOM_WORDS, s + L.gxpos + 3 * g2, s + L.gxmat + 9 * g2, gsize + 3 * g2, m.geom_type[g2]);
-      nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, geom_margin[g1] + geom_margin[g2]);
+      const int pid = m.nxn_pairid[2 * p];  // explicit <pair>: its own margin (collision_core.py:271)
+      nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations,
+                    pid > -1 ? MR(pair_margin)[pid] : geom_margin[g1] + geom_margin[g2]);
     }
     float* out = d.ccd_out + ((long)wid * m.nxn_ccd + slot) * CCD_OUT;
     const int lane = w.lane;

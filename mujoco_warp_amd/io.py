@@ -65,8 +65,9 @@ def _i32(a, device):
   return torch.as_tensor(np.ascontiguousarray(np.asarray(a).astype(np.int32)), device=device)
 
 
-def nxn_geom_pairs(mjm):
-  """Filtered NXN candidate pairs and pair ids (io.py:269-358)."""
+def nxn_geom_pairs(mjm, unfiltered=False):
+  """Filtered NXN candidate pairs and pair ids (io.py:269-358); `unfiltered` returns every upper-triangle
+  pair with its ids instead (the reference's m.nxn_geom_pair / m.nxn_pairid, -2 = never a contact)."""
   filterparent = not (mjm.opt.disableflags & DisableBit.FILTERPARENT)
   g1, g2 = np.triu_indices(mjm.ngeom, k=1)
   bodyid1, bodyid2 = mjm.geom_bodyid[g1], mjm.geom_bodyid[g2]
@@ -79,9 +80,14 @@ def nxn_geom_pairs(mjm):
   exclude = np.isin((bodyid1 << 16) + bodyid2, getattr(mjm, "exclude_signature", np.zeros(0, dtype=np.int32)))
   pairid_contact = -np.ones(len(g1), dtype=np.int32)
   pairid_contact[~(mask & ~self_collision & ~parent_child & ~exclude)] = -2
-  if getattr(mjm, "npair", 0):
-    raise NotImplementedError("explicit <contact><pair> entries are not supported yet")
+  # explicit <contact><pair> entries (io.py:296-302): always candidates, parameters from the pair
+  n = mjm.ngeom
+  for i in range(getattr(mjm, "npair", 0)):
+    a, b = sorted((int(mjm.pair_geom1[i]), int(mjm.pair_geom2[i])))
+    pairid_contact[(a * (2 * n - a - 3)) // 2 + b - 1] = i
   pairid_collision = -np.ones(len(g1), dtype=np.int32)
+  if unfiltered:
+    return np.stack([g1, g2], axis=1).astype(np.int32), np.stack([pairid_contact, pairid_collision], axis=1).astype(np.int32)
   include = pairid_contact > -2
   pairs = np.stack([g1, g2], axis=1)[include].astype(np.int32)
   pairid = np.stack([pairid_contact, pairid_collision], axis=1)[include].astype(np.int32)
@@ -161,6 +167,10 @@ def put_model(mjm, device=None) -> types.Model:
   if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
       tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) == (6, 6) for a, b in pairs_chk):
     raise NotImplementedError("box-box with NATIVECCD disabled (primitive box_box) is not supported by this build yet.")
+  for pid in range(int(getattr(mjm, "npair", 0))):  # io.py:405-410: margins on box / mesh pairs
+    t1, t2 = int(mjm.geom_type[mjm.pair_geom1[pid]]), int(mjm.geom_type[mjm.pair_geom2[pid]])
+    if mjm.pair_margin[pid] and t1 in (types.GeomType.BOX, types.GeomType.MESH) and t2 in (types.GeomType.BOX, types.GeomType.MESH):
+      raise NotImplementedError(f"pair {pid} has non-zero margin ({mjm.pair_margin[pid]}) with NATIVECCD enabled. Set margin to 0 or disable NATIVECCD.")
   muscle = _muscle_mask(mjm)
   if np.any(muscle):
     lr = np.asarray(mjm.actuator_lengthrange, np.float64).reshape(-1, 2)[muscle]
@@ -201,6 +211,7 @@ def put_model(mjm, device=None) -> types.Model:
   for n in ("nq", "nv", "nu", "na", "nbody", "njnt", "ngeom", "nsite", "ncam", "nlight", "nmocap", "nM", "nC"):
     setattr(m, n, int(getattr(mjm, n)))
   m.ntendon = int(getattr(mjm, "ntendon", 0))
+  m.npair = int(getattr(mjm, "npair", 0))
   m.nwrap, m.nJten = int(getattr(mjm, "nwrap", 0)), int(getattr(mjm, "nJten", 0))
   m.ten_maxnnz = int(np.max(mjm.ten_J_rownnz)) if m.ntendon else 0  # the reference's max_ten_J_rownnz (io.py:232)
   m.nmuscle = int(np.sum(_muscle_mask(mjm)))  # > 0 selects the forward kernel compiled with the muscle paths
@@ -214,7 +225,7 @@ def put_model(mjm, device=None) -> types.Model:
   m.nsensor_acc = int((np.asarray(getattr(mjm, "sensor_needstage", np.zeros(0))) == types.Stage.ACC).sum())
   m.is_sparse = bool(sparse)
   njmax_pad_unused, m.nv_pad = _padded_sizes(nv, 0, False)
-  m.nmaxcondim = int(np.concatenate(([0], mjm.geom_condim)).max())
+  m.nmaxcondim = int(np.concatenate(([0], mjm.geom_condim, getattr(mjm, "pair_dim", []))).max())
   m.nmaxpyramid = int(max(1, 2 * (m.nmaxcondim - 1)))
   m.block_dim = None
 
@@ -242,6 +253,8 @@ def put_model(mjm, device=None) -> types.Model:
   typed[swap] = typed[swap][:, ::-1]
   m.nxn_geom_pair_filtered = _i32(pairs, dev)
   m.nxn_pairid_filtered = _i32(pairid, dev)
+  pairs_all, pairid_all = nxn_geom_pairs(mjm, unfiltered=True)  # the reference's unfiltered fields (API parity)
+  m.nxn_geom_pair, m.nxn_pairid = _i32(pairs_all, dev), _i32(pairid_all, dev)
   m.nxn_geom_pair_typed = _i32(typed, dev)
   m.nxn = len(pairs)
   kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in pairs]

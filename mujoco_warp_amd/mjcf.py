@@ -1675,8 +1675,8 @@ class _Compiler:
   def _build_contact(self, root):
     m = self.m
     name2body = {b.name: i for i, b in enumerate(self.bodies)}
-    sigs = []
-    m.npair = 0
+    name2geom = {n: i for i, n in enumerate(m.geom_names) if n}
+    sigs, pairs = [], []
     for c in root.findall("contact"):
       for el in c:
         if el.tag == "exclude":
@@ -1684,9 +1684,55 @@ class _Compiler:
           b1, b2 = min(b1, b2), max(b1, b2)
           sigs.append((b1 << 16) + b2)
         elif el.tag == "pair":
-          raise NotImplementedError("<contact><pair> is not supported by the MJCF compiler yet")
+          pairs.append(self._pair(self._resolve("pair", el, None), name2geom))
     m.exclude_signature = np.array(sigs, dtype=np.int32)
     m.nexclude = len(sigs)
+    m.npair = len(pairs)
+    m.pair_geom1 = np.array([p["geom1"] for p in pairs], dtype=np.int32)
+    m.pair_geom2 = np.array([p["geom2"] for p in pairs], dtype=np.int32)
+    m.pair_dim = np.array([p["dim"] for p in pairs], dtype=np.int32)
+    for f, n in (("friction", 5), ("solref", 2), ("solreffriction", 2), ("solimp", 5)):
+      setattr(m, "pair_" + f, np.array([p[f] for p in pairs], dtype=np.float64).reshape(len(pairs), n))
+    m.pair_margin = np.array([p["margin"] for p in pairs], dtype=np.float64)
+    m.pair_gap = np.array([p["gap"] for p in pairs], dtype=np.float64)
+
+  def _pair(self, a, name2geom):
+    """One explicit <contact><pair>: attributes it leaves unset are derived from its two geoms the way
+    MuJoCo's compiler does (mjCPair::Compile): margin / gap = max, condim / friction / solref / solimp
+    from the higher-priority geom, or at equal priority max condim and friction and solmix-weighted
+    solref / solimp (min solref when either is a direct (negative) reference); solreffriction = 0 0.
+    The compiled values feed contact_params' pair branch (collision_core.py:270-277)."""
+    m = self.m
+    g1, g2 = name2geom[a["geom1"]], name2geom[a["geom2"]]
+    out = dict(geom1=g1, geom2=g2)
+    out["margin"] = float(a["margin"]) if "margin" in a else max(m.geom_margin[g1], m.geom_margin[g2])
+    out["gap"] = float(a["gap"]) if "gap" in a else max(m.geom_gap[g1], m.geom_gap[g2])
+    p1, p2 = m.geom_priority[g1], m.geom_priority[g2]
+    if p1 != p2:
+      gh = g1 if p1 > p2 else g2
+      dim = m.geom_condim[gh]
+      fr = m.geom_friction[gh]
+      sref, simp = m.geom_solref[gh], m.geom_solimp[gh]
+    else:
+      dim = max(m.geom_condim[g1], m.geom_condim[g2])
+      fr = np.maximum(m.geom_friction[g1], m.geom_friction[g2])
+      s1, s2 = m.geom_solmix[g1], m.geom_solmix[g2]
+      if s1 >= MJ_MINVAL and s2 >= MJ_MINVAL:
+        mix = s1 / (s1 + s2)
+      elif s1 < MJ_MINVAL and s2 < MJ_MINVAL:
+        mix = 0.5
+      else:
+        mix = 0.0 if s1 < MJ_MINVAL else 1.0
+      r1, r2 = m.geom_solref[g1], m.geom_solref[g2]
+      sref = mix * r1 + (1 - mix) * r2 if (r1[0] > 0 and r2[0] > 0) else np.minimum(r1, r2)
+      simp = mix * m.geom_solimp[g1] + (1 - mix) * m.geom_solimp[g2]
+    out["dim"] = int(a["condim"]) if "condim" in a else int(dim)
+    out["friction"] = _merge_vec([fr[0], fr[0], fr[1], fr[2], fr[2]], _floats(a["friction"])) if "friction" in a else \
+      [fr[0], fr[0], fr[1], fr[2], fr[2]]
+    out["solref"] = _merge_vec([0.02, 1.0], _floats(a["solref"])) if "solref" in a else list(sref)
+    out["solimp"] = _merge_vec([0.9, 0.95, 0.001, 0.5, 2.0], _floats(a["solimp"])) if "solimp" in a else list(simp)
+    out["solreffriction"] = _merge_vec([0.0, 0.0], _floats(a["solreffriction"])) if "solreffriction" in a else [0.0, 0.0]
+    return out
 
   def _build_keys(self, root):
     m = self.m

@@ -1173,9 +1173,19 @@ static void plane_capsule(contacts2* out, const real* n, const real* ppos, const
   out->n = 2;
 }
 
-/* collision_core.py:235-341 (geom-geom mixing; explicit <pair> not supported here) */
-static void contact_params(const orc_model* m, int g1, int g2, real* margin, real* gap, int* condim, real* friction,
-                           real* solref, real* solreffriction, real* solimp) {
+/* collision_core.py:235-341: an explicit <pair> (pairid > -1) supplies every parameter (:270-277),
+   otherwise the two geoms' parameters are mixed */
+static void contact_params(const orc_model* m, int g1, int g2, int pairid, real* margin, real* gap, int* condim,
+                           real* friction, real* solref, real* solreffriction, real* solimp) {
+  if (pairid > -1) {
+    *margin = m->pair_margin[pairid];
+    *gap = m->pair_gap[pairid];
+    *condim = m->pair_dim[pairid];
+    for (int i = 0; i < 5; i++) friction[i] = maxr(MINMU, m->pair_friction[5 * pairid + i]);
+    for (int i = 0; i < 2; i++) { solref[i] = m->pair_solref[2 * pairid + i]; solreffriction[i] = m->pair_solreffriction[2 * pairid + i]; }
+    for (int i = 0; i < 5; i++) solimp[i] = m->pair_solimp[5 * pairid + i];
+    return;
+  }
   real s1 = m->geom_solmix[g1], s2 = m->geom_solmix[g2];
   int c1 = m->geom_condim[g1], c2 = m->geom_condim[g2];
   int p1 = m->geom_priority[g1], p2 = m->geom_priority[g2];
@@ -1509,7 +1519,7 @@ static void collision(const orc_model* m, orc_data* d) {
     if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
     real margin, gap, friction[5], solref[2], solreffriction[2], solimp[5];
     int condim;
-    contact_params(m, g1, g2, &margin, &gap, &condim, friction, solref, solreffriction, solimp);
+    contact_params(m, g1, g2, pairid0, &margin, &gap, &condim, friction, solref, solreffriction, solimp);
     int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
     const real *p1 = d->geom_xpos + 3 * g1, *p2 = d->geom_xpos + 3 * g2;
     const real *r1 = d->geom_xmat + 9 * g1, *r2 = d->geom_xmat + 9 * g2;

@@ -30,7 +30,7 @@ typedef ORC_REAL real;
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)             \
   X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
   X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)   \
-  X(ntendon) X(nwrap) X(nJten)
+  X(ntendon) X(nwrap) X(nJten) X(npair)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
@@ -67,7 +67,9 @@ typedef ORC_REAL real;
   X(tendon_armature, ntendon) X(tendon_margin, ntendon) X(tendon_range, ntendon * 2)               \
   X(tendon_lengthspring, ntendon * 2) X(tendon_solref_lim, ntendon * 2) X(tendon_solimp_lim, ntendon * 5) \
   X(tendon_solref_fri, ntendon * 2) X(tendon_solimp_fri, ntendon * 5) X(tendon_invweight0, ntendon)  \
-  X(tendon_actfrcrange, ntendon * 2) X(wrap_prm, nwrap)
+  X(tendon_actfrcrange, ntendon * 2) X(wrap_prm, nwrap)                                            \
+  X(pair_solref, npair * 2) X(pair_solreffriction, npair * 2) X(pair_solimp, npair * 5)           \
+  X(pair_margin, npair) X(pair_gap, npair) X(pair_friction, npair * 5)
 
 /* ---- model: int arrays (name, element count) ---- */
 #define ORC_MODEL_INT_ARRAYS(X)                                                                    \
@@ -84,7 +86,7 @@ typedef ORC_REAL real;
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
   X(actuator_ctrllimited, nu) X(actuator_forcelimited, nu) X(actuator_actlimited, nu)             \
   X(actuator_actearly, nu)                                                                         \
-  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2)                                                 \
+  X(nxn_geom_pair, nxn * 2) X(nxn_pairid, nxn * 2) X(pair_dim, npair)                              \
   X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq) X(eq_objtype, neq)                           \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \

@@ -88,8 +88,14 @@ def nxn_pairs(mjm):
   mask = ((mjm.geom_contype[g1] & mjm.geom_conaffinity[g2]) | (mjm.geom_contype[g2] & mjm.geom_conaffinity[g1])).astype(bool)
   excl = np.isin((b1 << 16) + b2, getattr(mjm, "exclude_signature", np.zeros(0, dtype=np.int32)))
   keep = mask & ~self_col & ~parent_child & ~excl
+  pid = -np.ones(len(g1), dtype=np.int32)
+  for i in range(getattr(mjm, "npair", 0)):  # explicit pairs (io.py:301-302): kept whatever the filters say
+    a, b = sorted((int(mjm.pair_geom1[i]), int(mjm.pair_geom2[i])))
+    k = int(np.nonzero((g1 == a) & (g2 == b))[0][0])
+    keep[k] = True
+    pid[k] = i
   pairs = np.stack([g1[keep], g2[keep]], axis=1).astype(np.int32)
-  pairid = np.stack([-np.ones(keep.sum()), -np.ones(keep.sum())], axis=1).astype(np.int32)
+  pairid = np.stack([pid[keep], -np.ones(keep.sum(), dtype=np.int32)], axis=1).astype(np.int32)
   return pairs, pairid
 
 
@@ -119,7 +125,7 @@ class OracleModel:
       nq=mjm.nq, nv=mjm.nv, nu=mjm.nu, na=mjm.na, nbody=mjm.nbody, njnt=mjm.njnt, ngeom=mjm.ngeom, nsite=mjm.nsite,
       ncam=mjm.ncam, nlight=mjm.nlight, nmocap=mjm.nmocap, nxn=len(pairs), neq=mjm.neq,
       nsensor=getattr(mjm, "nsensor", 0), nsensordata=getattr(mjm, "nsensordata", 0),
-      nmaxpyramid=max(1, 2 * (int(np.concatenate(([0], mjm.geom_condim)).max()) - 1)),
+      nmaxpyramid=max(1, 2 * (int(np.concatenate(([0], mjm.geom_condim, getattr(mjm, "pair_dim", []))).max()) - 1)),
       opt_integrator=o.integrator, opt_cone=o.cone, opt_solver=o.solver, opt_iterations=o.iterations,
       opt_ls_iterations=o.ls_iterations, opt_disableflags=o.disableflags, opt_enableflags=o.enableflags,
       opt_broadphase_filter=int(getattr(o, "broadphase_filter", 1 | 2 | 8)),
@@ -132,6 +138,7 @@ class OracleModel:
       nflexelem=getattr(mjm, "nflexelem", 0), nflexelemdata=getattr(mjm, "nflexelemdata", 0),
       nmesh=getattr(mjm, "nmesh", 0), nmeshvert=getattr(mjm, "nmeshvert", 0),
       ntendon=getattr(mjm, "ntendon", 0), nwrap=getattr(mjm, "nwrap", 0), nJten=getattr(mjm, "nJten", 0),
+      npair=getattr(mjm, "npair", 0),
     )
     if overrides:
       vals.update(overrides)
