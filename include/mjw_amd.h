@@ -7,6 +7,8 @@
  *   mjw_step              <- forward.step                 forward.py:1003-1018
  *   mjw_forward           <- forward.forward              forward.py:972-1000
  *   mjw_fwd_position      <- forward.fwd_position         forward.py:513-537
+ *   mjw_contact_rows      <- constraint.make_constraint   constraint.py:2718-2779 (contact rows again from
+ *                            d.contact after a contactfilter callback, collision_driver.py:788-789)
  *   mjw_fwd_velocity      <- forward.fwd_velocity         forward.py:592-613
  *   mjw_fwd_actuation     <- forward.fwd_actuation        forward.py:836-927
  *   mjw_fwd_acceleration  <- forward.fwd_acceleration     forward.py:949-969
@@ -29,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 20
+#define MJW_ABI_VERSION 21
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -232,6 +234,7 @@ const char* mjw_kernel_name(int kernel_id);
 
 int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+int mjw_contact_rows(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_velocity(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_actuation(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_acceleration(const mjw_model_t* m, const mjw_data_t* d, void* stream);

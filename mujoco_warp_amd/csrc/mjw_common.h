@@ -18,7 +18,9 @@ constexpr int LPW = 64;   // lanes per world (one wavefront)
 constexpr int CREC = 33;  // words per staged contact record (odd: lane-per-record access is bank-conflict free)
 constexpr int CMAX = 32;  // staged contacts per collision round
 
-enum : int { ST_POS = 1, ST_VEL = 2, ST_ACT = 4, ST_ACC = 8, ST_SOLVE = 16, ST_EULER = 32, ST_NOFACTOR = 64 };
+// ST_POOL (with ST_POS): the position stage with the contacts read back from the pool instead of the
+// narrowphase -- the constraint rows after a contactfilter callback edited d.contact (mjw_contact_rows)
+enum : int { ST_POS = 1, ST_VEL = 2, ST_ACT = 4, ST_ACC = 8, ST_SOLVE = 16, ST_EULER = 32, ST_NOFACTOR = 64, ST_POOL = 128 };
 enum : int { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
 enum : int { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6, GEOM_MESH = 7 };
 enum : int { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
@@ -263,7 +265,7 @@ enum : int {
   K_SP_POS, K_SP_CCD, K_SP_COLL, K_SP_CON, K_SP_VEL, K_SP_INDEX, K_SP_SOLVE, K_SP_SOLVE_LDS, K_SP_EULER,
   K_DENSE = 32,  // + 32 * nbi + 4 * FLAGS + 2 * ELL + NEWTON  (dense_kernel<FLAGS, NEWTON, ELL, NB>, NB = 32 / 16 / 28 for nbi 0 / 1 / 2)
   K_FWD = 256,   // + 4 * STAGES + 2 * box + tendon    (mjw_kernel<STAGES, box, tendon>)
-  K_END = 256 + 4 * 128
+  K_END = 256 + 4 * 256
 };
 struct LaunchTrace {
   hipEvent_t* ev;  // ev[0] recorded by the caller before the step; ev[i + 1] after launch i

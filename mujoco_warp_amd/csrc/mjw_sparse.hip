@@ -1275,7 +1275,13 @@ __device__ int make_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int
             CNSTR_LIMIT_JOINT, i);
     return 1;
   }
-  // cat 4: contact pyramidal (constraint.py:1668-1936); i = pool slot
+  // cat 4: contact pyramidal (constraint.py:1668-1936); i = pool slot; contacts a contactfilter took the
+  // CONSTRAINT bit from get no rows (constraint.py:1731)
+  if (!(d.contact_type[i] & 1)) {
+    if (r0 < 0)  // the counting pass visits every contact once
+      for (int k = 0; k < m.nmaxpyramid; k++) d.contact_efc_address[(long)i * m.nmaxpyramid + k] = -1;
+    return 0;
+  }
   const int condim = d.contact_dim[i];
   const int nrow = condim == 1 ? 1 : 2 * (condim - 1);
   const float includemargin = d.contact_includemargin[i];
@@ -2610,6 +2616,12 @@ extern "C" int mjw_prof_read_sparse(unsigned long long* out, int reset) {
 int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s) {
   const int nw = d->nworld;
   if (nw <= 0) return 0;
+  if (stages & ST_POOL) {
+    // constraint rows (and transmission) again from the contact pool as a contactfilter left it
+    hipLaunchKernelGGL(sp::forward_kernel<sp::SP_CON>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, (int)ST_POS);
+    trace_launch(s, K_SP_CON);
+    return (int)hipGetLastError();
+  }
   const int fwd = stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC);
   const bool ccd = (stages & ST_POS) && m->nxn_ccd > 0 && d->naconmax > 0 && !(m->opt_disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT));
   if (fwd & ST_POS) {

@@ -868,7 +868,7 @@ __device__ __forceinline__ int tendon_rows(const mjw_model_t& m, const mjw_data_
   return added;
 }
 
-template <bool BOX, bool TEN>
+template <bool BOX, bool TEN, bool POOL = false>
 __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -1078,7 +1078,10 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
     // broadphase over all pairs once; survivors (in pair order) -> plist
     int npass = 0;
     int* plist = si + L.plist;
-    for (int base = 0; base < m.nxn; base += LPW) {
+    // POOL: the candidates are this world's contacts in the pool (a contactfilter callback may have
+    // edited them), in slot order = the pair order the narrowphase wrote them in
+    const int npool = POOL ? min(d.nacon[0], d.naconmax) : 0;
+    for (int base = 0; base < (POOL ? 0 : m.nxn); base += LPW) {
       int p = base + lane;
       bool pass = false;
       if (p < m.nxn) {
@@ -1090,7 +1093,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       if (pass) plist[npass + rank] = p;
       npass += __popcll(bal);
     }
-    if (lane == 0 && npass > 0) atomicAdd(d.ncollision, npass);
+    if (!POOL && lane == 0 && npass > 0) atomicAdd(d.ncollision, npass);
     WSYNC();
     PROF_MARK_SUB(PH_C_BROAD);
     const float* geom_margin = MR(geom_margin);
@@ -1098,8 +1101,39 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
     while (true) {
       const int rbeg = round * CM, rend = rbeg + CM;
       int running = 0;  // contacts found so far (world-local, in pair order)
-      for (int base = 0; base < npass; base += LPW) {
+      for (int base = 0; base < (POOL ? npool : npass); base += LPW) {
         int k = base + lane;
+        if constexpr (POOL) {
+          // constraint.py:1731: contacts without the CONSTRAINT type bit get no rows (and no row address)
+          const bool mine = k < npool && d.contact_worldid[k] == wid;
+          const bool sel = mine && (d.contact_type[k] & 1);
+          if (mine && !sel)
+            for (int i = 0; i < m.nmaxpyramid; i++) d.contact_efc_address[(long)k * m.nmaxpyramid + i] = -1;
+          const int incl = wave_scan_incl((int)sel);
+          const int idx = running + incl - (int)sel;
+          if (sel && idx >= rbeg && idx < rend) {
+            float* rec = s + L.con + (idx - rbeg) * CREC;
+            int* reci = reinterpret_cast<int*>(rec);
+            const int g1 = d.contact_geom[2L * k], g2 = d.contact_geom[2L * k + 1];
+            const int cb1 = m.geom_bodyid[g1], cb2 = m.geom_bodyid[g2];
+            rec[0] = d.contact_dist[k];
+            rec[1] = d.contact_includemargin[k];
+            for (int i = 0; i < 3; i++) rec[2 + i] = d.contact_pos[3L * k + i];
+            for (int i = 0; i < 9; i++) rec[5 + i] = d.contact_frame[9L * k + i];
+            for (int i = 0; i < 5; i++) rec[14 + i] = d.contact_friction[5L * k + i];
+            rec[19] = d.contact_solref[2L * k]; rec[20] = d.contact_solref[2L * k + 1];
+            reci[21] = m.body_weldid[cb1] | (m.body_weldid[cb2] << 16);
+            reci[22] = cb1 | (cb2 << 16);
+            reci[32] = m.body_rootid[cb1] | (m.body_rootid[cb2] << 16);
+            for (int i = 0; i < 5; i++) rec[23 + i] = d.contact_solimp[5L * k + i];
+            reci[28] = d.contact_dim[k];
+            reci[29] = g1;
+            reci[30] = g2;
+            reci[31] = k;  // the pool slot (set from the reserved range in the narrowphase mode)
+          }
+          running += __shfl(incl, 63, 64);
+          continue;
+        }
         Con2 c;
         c.n = 0;
         int g1 = 0, g2 = 0, pairid0 = -2;
@@ -1242,7 +1276,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       if (nstage <= 0) break;
       // global pool slot for this round (one atomic per world per round)
       int gbase = 0;
-      if (lane == 0) gbase = atomicAdd(d.nacon, nstage);
+      if (!POOL && lane == 0) gbase = atomicAdd(d.nacon, nstage);
       gbase = __shfl(gbase, 0, 64);
       WSYNC();
       // rows per staged contact (pyramidal: 1 or 2*(condim-1); elliptic: condim), prefix over contacts
@@ -1253,8 +1287,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         int condim = reinterpret_cast<const int*>(rec)[28] & 0xff;
         float pos = rec[0] - rec[1];
         // a contact past the global pool is dropped with its rows (collision_core.py:212-231)
-        nrow = (pos < 0.0f && gbase + lane < d.naconmax) ? (condim == 1 ? 1 : (ell ? condim : 2 * (condim - 1))) : 0;
-        reinterpret_cast<int*>(s + L.con + lane * CREC)[31] = gbase + lane;
+        nrow = (pos < 0.0f && (POOL || gbase + lane < d.naconmax)) ? (condim == 1 ? 1 : (ell ? condim : 2 * (condim - 1))) : 0;
+        if (!POOL) reinterpret_cast<int*>(s + L.con + lane * CREC)[31] = gbase + lane;
       }
       int rincl = wave_scan_incl(nrow);
       int rfirst = nefc + rincl - nrow;
@@ -1265,8 +1299,13 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       if (lane < nstage) {
         const float* rec = s + L.con + lane * CREC;
         const int* reci = reinterpret_cast<const int*>(rec);
-        int cid = gbase + lane;
-        if (cid < d.naconmax) {
+        int cid = POOL ? reci[31] : gbase + lane;
+        if (POOL) {
+          for (int i = 0; i < m.nmaxpyramid; i++) {
+            int r = rfirst + i;
+            d.contact_efc_address[(long)cid * m.nmaxpyramid + i] = (i < nrow && r < njmax) ? r : -1;
+          }
+        } else if (cid < d.naconmax) {
           d.contact_dist[cid] = rec[0];
           for (int i = 0; i < 3; i++) d.contact_pos[3L * cid + i] = rec[2 + i];
           for (int i = 0; i < 9; i++) d.contact_frame[9L * cid + i] = rec[5 + i];
@@ -1299,7 +1338,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         int condim = reci[28] & 0xff;
         int r0 = si[L.iscratch + cc];
         float pos = rec[0] - rec[1];
-        if (!(pos < 0.0f) || gbase + cc >= d.naconmax) continue;
+        if (!(pos < 0.0f) || (!POOL && gbase + cc >= d.naconmax)) continue;
         int nr = condim == 1 ? 1 : (ell ? condim : 2 * (condim - 1));
         const int b1 = reci[21] & 0xffff, b2 = reci[21] >> 16;
         const float* cpos = rec + 2;
@@ -1363,10 +1402,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           const float* sref = rec + 19;
           if (dimid > 0) {
             const int pid = (reci[28] >> 8) - 1;
-            if (pid > -1) {
-              const float* srf = MR(pair_solreffriction) + 2 * pid;
-              if (srf[0] != 0.0f || srf[1] != 0.0f) sref = srf;
-            }
+            const float* srf = POOL ? d.contact_solreffriction + 2L * reci[31] : (pid > -1 ? MR(pair_solreffriction) + 2 * pid : nullptr);
+            if (srf && (srf[0] != 0.0f || srf[1] != 0.0f)) sref = srf;
             invweight = invweight * impratio_invsqrt * impratio_invsqrt;
             if (dimid > 1) {
               const float fri0 = rec[14], frii = rec[14 + dimid - 1];
@@ -2313,7 +2350,7 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
     if (TEN && m.ntendon) tendon_pos(m, d, w.s + L.qpos, w.wid, w.lane);  // smooth.py:3085-3121 (fwd_position: before crb)
     crb_qM<TEN>(m, d, L, w);
     PROF_MARK(PH_CRB);
-    collision_and_constraints<BOX, TEN>(m, d, L, w);
+    collision_and_constraints<BOX, TEN, (STAGES & ST_POOL) != 0>(m, d, L, w);
     PROF_MARK(PH_COLL);
     transmission<TEN>(m, d, L, w);
     PROF_MARK(PH_TRN);
@@ -2540,7 +2577,7 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   }();
   lds += lds_pad;
   if (lds > 160 * 1024) { g_err = std::string(name) + ": per-world LDS working set exceeds 160 KiB"; return -3; }
-  if (STAGES & mjw::ST_POS) {
+  if ((STAGES & mjw::ST_POS) && !(STAGES & mjw::ST_POOL)) {
     if (m->nxn_ccd > 0 && d->naconmax > 0 && !(m->opt_disableflags & (mjw::DSBL_CONSTRAINT | mjw::DSBL_CONTACT))) {
       static std::once_flag once_ccd;
       std::call_once(once_ccd, [] {
@@ -2603,7 +2640,7 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
       return -5;
     }
     hipStream_t s = (hipStream_t)stream;
-    if (stages & ST_POS) {
+    if ((stages & ST_POS) && !(stages & ST_POOL)) {
       hipError_t e = reset_counters(d, s);
       if (e != hipSuccess) return set_err(e, name);
     }
@@ -2632,7 +2669,7 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     g_err = std::string(name) + ": elliptic cones need the register-resident dense solve (nv <= 32, njmax <= 64)";
     return -5;
   }
-  if (stages & ST_POS) {
+  if ((stages & ST_POS) && !(stages & ST_POOL)) {
     rc = set_err(reset_counters(d, s, order), name);
     if (rc) return rc;
   }
@@ -2653,7 +2690,9 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
       switch (stages & (ST_POS | ST_VEL | ST_ACT | ST_ACC)) {
         case 0: break;
         case ST_POS | ST_VEL | ST_ACT | ST_ACC: r = launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_NOFACTOR>(m, d, st, name, w0, cnt); break;
-        case ST_POS: r = launch_generic<ST_POS>(m, d, st, name, w0, cnt); break;
+        case ST_POS:
+          r = (stages & ST_POOL) ? launch_generic<ST_POS | ST_POOL>(m, d, st, name, w0, cnt) : launch_generic<ST_POS>(m, d, st, name, w0, cnt);
+          break;
         case ST_VEL: r = launch_generic<ST_VEL>(m, d, st, name, w0, cnt); break;
         case ST_ACT: r = launch_generic<ST_ACT>(m, d, st, name, w0, cnt); break;
         case ST_ACC: r = launch_generic<ST_ACC | ST_NOFACTOR>(m, d, st, name, w0, cnt); break;
@@ -2685,6 +2724,7 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     case ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE | ST_EULER: return launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE | ST_EULER>(m, d, s, name);
     case ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE: return launch_generic<ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE>(m, d, s, name);
     case ST_POS: return launch_generic<ST_POS>(m, d, s, name);
+    case ST_POS | ST_POOL: return launch_generic<ST_POS | ST_POOL>(m, d, s, name);
     case ST_VEL: return launch_generic<ST_VEL>(m, d, s, name);
     case ST_ACT: return launch_generic<ST_ACT>(m, d, s, name);
     case ST_ACC: return launch_generic<ST_ACC>(m, d, s, name);
@@ -2792,6 +2832,9 @@ int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
 }
 int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_POS, "mjw_fwd_position");
+}
+int mjw_contact_rows(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  return run(m, d, stream, mjw::ST_POS | mjw::ST_POOL, "mjw_contact_rows");
 }
 int mjw_fwd_velocity(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_VEL, "mjw_fwd_velocity");

@@ -75,11 +75,11 @@ class StepTracer:
     return out
 
 
-# callbacks whose reference call sites fall inside one fused launch of this path: contactfilter runs
-# between the narrowphase and make_constraint (collision_driver.py:788), which share the position-stage
-# kernel; it is refused instead of being run where it could no longer change the step
-_UNSUPPORTED_CALLBACKS = {"contactfilter": "collision_driver.py:788"}
-_STAGED_CALLBACKS = ("control", "passive", "act_dyn", "act_gain", "act_bias")
+# callbacks whose reference call sites fall inside one fused launch of this path (none left: contactfilter,
+# between the narrowphase and make_constraint, runs after the position stage, which then rebuilds the
+# constraint rows from the contact pool it edited -- mjw_contact_rows)
+_UNSUPPORTED_CALLBACKS: dict = {}
+_STAGED_CALLBACKS = ("control", "passive", "act_dyn", "act_gain", "act_bias", "contactfilter")
 
 
 def _has_callbacks(m: Model) -> bool:
@@ -91,9 +91,16 @@ def _has_callbacks(m: Model) -> bool:
 
 
 def fwd_position(m: Model, d: Data):
-  """Position-dependent computations (forward.py:513-537)."""
+  """Position-dependent computations (forward.py:513-537).  A contactfilter callback runs after the
+  narrowphase wrote d.contact (collision_driver.py:788-789); the constraint rows (make_constraint, which
+  the reference runs after it) are then rebuilt from the contacts as the callback left them
+  (mjw_contact_rows: contacts whose `type` lost the CONSTRAINT bit get no rows)."""
   _has_callbacks(m)
   _call("mjw_fwd_position", m, d)
+  if m.callback.contactfilter is not None:
+    if d.naconmax > 0 and not (m.opt.disableflags & (DisableBit.CONSTRAINT | DisableBit.CONTACT)):
+      m.callback.contactfilter(m, d)
+      _call("mjw_contact_rows", m, d)
 
 
 def fwd_velocity(m: Model, d: Data):

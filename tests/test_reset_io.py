@@ -126,22 +126,6 @@ def test_get_data_into_world_selection():
     mjw.get_data_into(res, mjm, d, world_id=3)
 
 
-def test_unsupported_callbacks_are_refused():
-  import mujoco_warp_amd as mjw
-  from tests.common import humanoid_model
-
-  mjm = humanoid_model()
-  m = mjw.put_model(mjm, device="cpu")
-  d = mjw.make_data(mjm, nworld=1, device="cpu", m=m)
-  # contactfilter hooks between the narrowphase and make_constraint, inside the position-stage kernel
-  # (collision_driver.py:788); the act_* callbacks run on the staged path (tests/test_api.py)
-  for name in ("contactfilter",):
-    setattr(m.callback, name, lambda mm, dd: None)
-    with pytest.raises(NotImplementedError, match=name):
-      mjw.step(m, d)
-    setattr(m.callback, name, None)
-
-
 @pytest.mark.gpu
 def test_gpu_reset_then_step_equals_fresh_worlds():
   """Step humanoid worlds into contact, reset a mask, step again: reset worlds equal fresh ones bitwise."""
