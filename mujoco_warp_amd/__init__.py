@@ -34,6 +34,26 @@ from .mjcf import MjModel
 from .mjcf import load_model
 from .mjcf import load_model_from_string
 from .mjcf import reset_data_keyframe
+from .stages import camlight
+from .stages import collision
+from .stages import com_pos
+from .stages import com_vel
+from .stages import crb
+from .stages import energy_pos
+from .stages import energy_vel
+from .stages import factor_m
+from .stages import flex
+from .stages import jac
+from .stages import kinematics
+from .stages import make_constraint
+from .stages import passive
+from .stages import rne
+from .stages import rne_postconstraint
+from .stages import solve_m
+from .stages import subtree_vel
+from .stages import tendon
+from .stages import transmission
+from .stages import xfrc_accumulate
 from .support import contact_force
 from .support import get_state
 from .support import efc_J_csr
@@ -41,6 +61,7 @@ from .support import mul_m
 from .support import set_state
 from .support import state_size
 from .types import BiasType
+from .types import Callback
 from .types import BroadphaseFilter
 from .types import BroadphaseType
 from .types import CamLightType

@@ -1,0 +1,295 @@
+"""The reference's finer-grained stage and support functions, on this build's fused launches.
+
+`mujoco_warp` exposes every pipeline stage as its own function (mujoco_warp/__init__.py:26-112:
+`kinematics`, `com_pos`, `crb`, `collision`, `make_constraint`, `rne`, ...).  Here a stage group runs as
+one HIP launch, so each of these functions runs the launch that contains it:
+
+* position stage (`mjw_fwd_position`): kinematics, com_pos, camlight, flex, tendon, crb, collision,
+  make_constraint, transmission -- each computes its reference outputs from `qpos` / `mocap_*` (and the
+  stage's other outputs along with them; an input the reference would read from an earlier stage's output,
+  e.g. a hand-edited `d.xipos` before `com_pos`, is recomputed from `qpos`, not taken from `d`);
+* velocity stage (`mjw_fwd_velocity`): com_vel, passive, rne (flg_acc = False);
+* `factor_m`: the acceleration stage launch, whose dense kernel factors qM into qLD
+  (it also refreshes qfrc_smooth / qacc_smooth from the current force inputs);
+* `rne_postconstraint`: the sensor kernel's acceleration stage (cacc, cfrc_int, cfrc_ext).
+
+The support functions that take caller arrays -- `jac`, `xfrc_accumulate`, `solve_m`, `subtree_vel`,
+`energy_pos`, `energy_vel` -- are torch ops on the Data tensors in HBM, on the device and stream of the
+HIP launches (restatements of support.py / smooth.py / sensor.py, cited per function).  None of them is on
+the `step` path.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import forward as _fwd
+from .types import Data, DisableBit, JointType, Model
+
+
+# -- stage-group aliases --------------------------------------------------------------------------
+def _position(m: Model, d: Data):
+  _fwd._call("mjw_fwd_position", m, d)
+
+
+def kinematics(m: Model, d: Data):
+  """Forward kinematics (smooth.py:357-415): the position-stage launch."""
+  _position(m, d)
+
+
+def com_pos(m: Model, d: Data):
+  """subtree_com, cinert, cdof (smooth.py:463-632): the position-stage launch."""
+  _position(m, d)
+
+
+def camlight(m: Model, d: Data):
+  """Camera / light frames (smooth.py:635-803): the position-stage launch."""
+  _position(m, d)
+
+
+def flex(m: Model, d: Data):
+  """Flex vertex positions and edge lengths / Jacobians (smooth.py:419-460): the position-stage launch."""
+  _position(m, d)
+
+
+def tendon(m: Model, d: Data):
+  """Tendon lengths and Jacobians (smooth.py:3627-3700): the position-stage launch."""
+  _position(m, d)
+
+
+def crb(m: Model, d: Data):
+  """Composite rigid-body inertia and qM (smooth.py:806-912): the position-stage launch."""
+  _position(m, d)
+
+
+def collision(m: Model, d: Data):
+  """Broadphase + narrowphase into d.contact (collision_driver.py:757-789), with the contactfilter callback
+  after it: the position-stage launch (fwd_position)."""
+  _fwd.fwd_position(m, d)
+
+
+def make_constraint(m: Model, d: Data):
+  """Constraint rows d.efc (constraint.py:2718-2779): the position-stage launch, whose rows come from the
+  contacts it collides; after a caller edited d.contact, `mjw_contact_rows` rebuilds them from the pool."""
+  _position(m, d)
+
+
+def transmission(m: Model, d: Data):
+  """Actuator lengths and moments (smooth.py:2605-2700): the position-stage launch."""
+  _position(m, d)
+
+
+def com_vel(m: Model, d: Data):
+  """cvel, cdof_dot (smooth.py:1935-2038): the velocity-stage launch."""
+  _fwd._call("mjw_fwd_velocity", m, d)
+
+
+def passive(m: Model, d: Data):
+  """qfrc_spring / damper / passive (passive.py:535-563): the velocity-stage launch (then the passive
+  callback, as fwd_velocity)."""
+  _fwd.fwd_velocity(m, d)
+
+
+def rne(m: Model, d: Data, flg_acc: bool = False):
+  """qfrc_bias = RNE with zero acceleration (smooth.py:1276-1300, flg_acc = False): the velocity-stage
+  launch.  flg_acc = True (the inverse-dynamics use, out of this build's scope) is refused."""
+  if flg_acc:
+    raise NotImplementedError("rne(flg_acc=True) (inverse dynamics) is not part of this build")
+  _fwd._call("mjw_fwd_velocity", m, d)
+
+
+def factor_m(m: Model, d: Data):
+  """qLD = factor(qM) (smooth.py:1104-1112): the acceleration-stage launch (dense: Cholesky L, row-major
+  nv x nv; sparse: L'DL on the ancestor rows, mj_factorM order)."""
+  _fwd._call("mjw_fwd_acceleration", m, d)
+
+
+def rne_postconstraint(m: Model, d: Data):
+  """cacc, cfrc_int, cfrc_ext after the solver (smooth.py:1501-1600): the sensor kernel's acceleration
+  stage (it also evaluates the acceleration sensors)."""
+  _fwd._sensor(m, d, 4)
+
+
+# -- support functions on caller arrays -------------------------------------------------------------
+def _path_mask(m: Model) -> torch.Tensor:
+  """(nbody, nbody) bool, [b, a]: body a lies on the path from b up to (not including) the world body."""
+  mask = getattr(m, "_path_mask", None)
+  if mask is None:
+    par = m.body_parentid.cpu().numpy()
+    nb = len(par)
+    out = np.zeros((nb, nb), dtype=bool)
+    for b in range(nb):
+      p = b
+      while p != 0:
+        out[b, p] = True
+        p = par[p]
+    mask = torch.as_tensor(out, device=m.body_parentid.device)
+    m._path_mask = mask
+  return mask
+
+
+def _cdof(m: Model, d: Data):
+  c = d.cdof.reshape(d.nworld, m.nv, 6)
+  return c[..., :3], c[..., 3:]  # angular (spatial top), linear (spatial bottom)
+
+
+def jac(m: Model, d: Data, jacp: Optional[torch.Tensor], jacr: Optional[torch.Tensor], point: torch.Tensor, body: torch.Tensor):
+  """Translational / rotational Jacobian of a point on a body, per world (support.py:397-503): dof i
+  contributes when its body is on the path from `body` to the root (or is the world body), with
+  jacp = cdof_lin + cdof_ang x (point - subtree_com[rootid[body]]) and jacr = cdof_ang.
+  point: (nworld, 3); body: (nworld,) int; jacp / jacr: (nworld, 3, nv) outputs, either may be None."""
+  body = body.to(torch.long).reshape(-1)
+  ang, lin = _cdof(m, d)
+  dof_body = m.dof_bodyid.to(torch.long)
+  in_tree = (dof_body == 0).unsqueeze(0) | _path_mask(m)[body][:, dof_body]  # (nworld, nv)
+  root = m.body_rootid.to(torch.long)[body]
+  sc = d.subtree_com.reshape(d.nworld, m.nbody, 3)
+  offset = point.reshape(-1, 3) - sc[torch.arange(d.nworld, device=sc.device), root]
+  w = in_tree.to(ang.dtype).unsqueeze(-1)
+  if jacp is not None:
+    jp = (lin + torch.cross(ang, offset.unsqueeze(1).expand_as(ang), dim=-1)) * w
+    jacp[:] = jp.transpose(1, 2)
+  if jacr is not None:
+    jacr[:] = (ang * w).transpose(1, 2)
+
+
+def xfrc_accumulate(m: Model, d: Data, qfrc: torch.Tensor):
+  """qfrc += J' xfrc_applied over every body (support.py:175-237 apply_ft): the body's force (xfrc[:3]) acts
+  at xipos, its torque (xfrc[3:]) on the rotational Jacobian; dof i sees the bodies of its body's subtree."""
+  ang, lin = _cdof(m, d)
+  ft = d.xfrc_applied.reshape(d.nworld, m.nbody, 6)
+  f, t = ft[..., :3], ft[..., 3:]
+  sc = d.subtree_com.reshape(d.nworld, m.nbody, 3)
+  off = d.xipos.reshape(d.nworld, m.nbody, 3) - sc[:, m.body_rootid.to(torch.long)]
+  mask = _path_mask(m)[:, m.dof_bodyid.to(torch.long)].to(ang.dtype)  # (nbody, nv): dof's body on b's path
+  # lin . f + ang . t + (ang x off) . f  =  lin . f + ang . (t + off x f)
+  tq = t + torch.cross(off, f, dim=-1)
+  qfrc += torch.einsum("wik,wbk,bi->wi", lin, f, mask) + torch.einsum("wik,wbk,bi->wi", ang, tq, mask)
+
+
+def solve_m(m: Model, d: Data, x: torch.Tensor, y: torch.Tensor):
+  """x = M^-1 y with the factor in d.qLD (smooth.py:2848-2858).  Dense: qLD holds the Cholesky factor L
+  (M = L L'); sparse: L'DL on the ancestor rows (the sparse path's solve_trees order,
+  smooth.py:2813-2846)."""
+  nv = m.nv
+  if not m.is_sparse:
+    L = torch.tril(d.qLD.reshape(d.nworld, nv, nv))
+    x[:] = torch.cholesky_solve(y.reshape(d.nworld, nv, 1), L).reshape(d.nworld, nv)
+    return
+  LD = d.qLD.reshape(d.nworld, -1)
+  rowadr = m.M_rowadr.cpu().numpy()
+  rownnz = m.M_rownnz.cpu().numpy()
+  colind = m.M_colind.cpu().numpy()
+  v = y.reshape(d.nworld, nv).clone()
+  for k in range(nv - 1, -1, -1):
+    a, n = int(rowadr[k]), int(rownnz[k])
+    if n > 1:
+      cols = torch.as_tensor(colind[a : a + n - 1], device=v.device, dtype=torch.long)
+      v[:, cols] -= LD[:, a : a + n - 1] * v[:, k : k + 1]
+  diag = torch.as_tensor(rowadr + rownnz - 1, device=v.device, dtype=torch.long)
+  v /= LD[:, diag]
+  for k in range(nv):
+    a, n = int(rowadr[k]), int(rownnz[k])
+    if n > 1:
+      cols = torch.as_tensor(colind[a : a + n - 1], device=v.device, dtype=torch.long)
+      v[:, k] -= (LD[:, a : a + n - 1] * v[:, cols]).sum(dim=1)
+  x[:] = v
+
+
+def subtree_vel(m: Model, d: Data):
+  """subtree_linvel and subtree_angmom (smooth.py:2932-3083), stored on d as (nworld, nbody, 3) tensors and
+  returned: each body's COM velocity and spin momentum, then linear momenta summed up the tree (deepest
+  bodies first; DFS pre-order puts every descendant after its ancestors) and divided by the subtree mass,
+  then angular momenta about the subtree COMs summed up the tree."""
+  nw, nb = d.nworld, m.nbody
+  mass = m.body_mass.reshape(-1, nb)[0]
+  stm = m.body_subtreemass.reshape(-1, nb)[0]
+  inertia = m.body_inertia.reshape(-1, nb, 3)[0]
+  cvel = d.cvel.reshape(nw, nb, 6)
+  xipos = d.xipos.reshape(nw, nb, 3)
+  ximat = d.ximat.reshape(nw, nb, 3, 3)
+  sc = d.subtree_com.reshape(nw, nb, 3)
+  ang = cvel[..., :3]
+  lin = cvel[..., 3:] - torch.cross(xipos - sc[:, m.body_rootid.to(torch.long)], ang, dim=-1)  # :2960
+  linvel = mass.unsqueeze(-1) * lin
+  dv = torch.einsum("wbji,wbj->wbi", ximat, ang) * inertia  # ximat' ang, scaled by the principal inertia
+  angmom = torch.einsum("wbij,wbj->wbi", ximat, dv)
+  par = m.body_parentid.cpu().numpy()
+  stm_h = stm.cpu().numpy()
+  for b in range(nb - 1, -1, -1):  # _linear_momentum (:2972-2988)
+    if b:
+      linvel[:, par[b]] += linvel[:, b]
+    linvel[:, b] /= max(float(stm_h[b]), 1e-15)
+  for b in range(nb - 1, 0, -1):  # _angular_momentum (:2992-3041)
+    p = par[b]
+    angmom[:, b] += torch.cross(xipos[:, b] - sc[:, b], (lin[:, b] - linvel[:, b]) * mass[b], dim=-1)
+    angmom[:, p] += angmom[:, b]
+    angmom[:, p] += torch.cross(sc[:, b] - sc[:, p], (linvel[:, b] - linvel[:, p]) * stm[b], dim=-1)
+  d.subtree_linvel = linvel
+  d.subtree_angmom = angmom
+  return linvel, angmom
+
+
+def _quat_sub(qa: torch.Tensor, qb: torch.Tensor) -> torch.Tensor:
+  """math.py:162-185: qb * quat(res) = qa, as a 3D rotation vector."""
+  w1, v1 = qb[..., :1], -qb[..., 1:]
+  w2, v2 = qa[..., :1], qa[..., 1:]
+  w = w1 * w2 - (v1 * v2).sum(-1, keepdim=True)
+  v = w1 * v2 + w2 * v1 + torch.cross(v1, v2, dim=-1)
+  s = torch.linalg.norm(v, dim=-1, keepdim=True)
+  speed = 2.0 * torch.atan2(s, w)
+  speed = torch.where(speed > np.pi, speed - 2.0 * np.pi, speed)
+  return torch.where(s > 0, v * speed / torch.where(s > 0, s, torch.ones_like(s)), torch.zeros_like(v))
+
+
+def energy_pos(m: Model, d: Data):
+  """d.energy[:, 0] = potential energy (sensor.py:2854-2890): gravity -sum mass g . xipos over the bodies
+  and joint / tendon springs 0.5 k dif^2 (free joints: translation and rotation, ball joints: rotation)."""
+  nw, nb = d.nworld, m.nbody
+  e = torch.zeros(nw, dtype=d.energy.dtype, device=d.energy.device)
+  if not (m.opt.disableflags & DisableBit.GRAVITY):
+    g = m.opt.gravity.reshape(-1, 3)[0]
+    mass = m.body_mass.reshape(-1, nb)[0]
+    xipos = d.xipos.reshape(nw, nb, 3)
+    e -= (mass[1:] * (xipos[:, 1:] @ g)).sum(dim=1)
+  if not (m.opt.disableflags & DisableBit.SPRING):
+    stiff = m.jnt_stiffness.reshape(-1, m.njnt)[0].cpu().numpy()
+    jt = m.jnt_type.cpu().numpy()
+    qa_all = m.jnt_qposadr.cpu().numpy()
+    qs = m.qpos_spring.reshape(-1, m.nq)[0]
+    qpos = d.qpos.reshape(nw, m.nq)
+    for j in np.nonzero(stiff)[0]:
+      k, qa = float(stiff[j]), int(qa_all[j])
+      if jt[j] == JointType.FREE:
+        d0 = qpos[:, qa : qa + 3] - qs[qa : qa + 3]
+        q1 = torch.nn.functional.normalize(qpos[:, qa + 3 : qa + 7], dim=-1)
+        d1 = _quat_sub(q1, qs[qa + 3 : qa + 7].expand_as(q1))
+        e += 0.5 * k * ((d0 * d0).sum(-1) + (d1 * d1).sum(-1))
+      elif jt[j] == JointType.BALL:
+        q = torch.nn.functional.normalize(qpos[:, qa : qa + 4], dim=-1)
+        dq = _quat_sub(q, qs[qa : qa + 4].expand_as(q))
+        e += 0.5 * k * (dq * dq).sum(-1)
+      else:
+        dq = qpos[:, qa] - qs[qa]
+        e += 0.5 * k * dq * dq
+    for t in range(getattr(m, "ntendon", 0)):
+      k = float(m.tendon_stiffness.reshape(-1, m.ntendon)[0, t])
+      if k == 0.0:
+        continue
+      lo, hi = (float(x) for x in m.tendon_lengthspring.reshape(-1, m.ntendon, 2)[0, t])
+      length = d.ten_length.reshape(nw, m.ntendon)[:, t]
+      disp = torch.where(length > hi, hi - length, torch.where(length < lo, lo - length, torch.zeros_like(length)))
+      e += 0.5 * k * disp * disp
+  d.energy.reshape(nw, 2)[:, 0] = e
+
+
+def energy_vel(m: Model, d: Data):
+  """d.energy[:, 1] = kinetic energy 0.5 qvel' M qvel (sensor.py:2922-2940, mul_m on qM)."""
+  from .support import mul_m
+
+  mv = torch.zeros_like(d.qvel)
+  mul_m(m, d, mv, d.qvel)
+  d.energy.reshape(d.nworld, 2)[:, 1] = 0.5 * (d.qvel * mv).sum(dim=1)
