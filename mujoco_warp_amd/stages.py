@@ -26,13 +26,13 @@ from typing import Optional
 import numpy as np
 import torch
 
-from . import forward as _fwd
+from .forward import _call, _sensor, fwd_position, fwd_velocity
 from .types import Data, DisableBit, JointType, Model
 
 
 # -- stage-group aliases --------------------------------------------------------------------------
 def _position(m: Model, d: Data):
-  _fwd._call("mjw_fwd_position", m, d)
+  _call("mjw_fwd_position", m, d)
 
 
 def kinematics(m: Model, d: Data):
@@ -68,7 +68,7 @@ def crb(m: Model, d: Data):
 def collision(m: Model, d: Data):
   """Broadphase + narrowphase into d.contact (collision_driver.py:757-789), with the contactfilter callback
   after it: the position-stage launch (fwd_position)."""
-  _fwd.fwd_position(m, d)
+  fwd_position(m, d)
 
 
 def make_constraint(m: Model, d: Data):
@@ -84,13 +84,13 @@ def transmission(m: Model, d: Data):
 
 def com_vel(m: Model, d: Data):
   """cvel, cdof_dot (smooth.py:1935-2038): the velocity-stage launch."""
-  _fwd._call("mjw_fwd_velocity", m, d)
+  _call("mjw_fwd_velocity", m, d)
 
 
 def passive(m: Model, d: Data):
   """qfrc_spring / damper / passive (passive.py:535-563): the velocity-stage launch (then the passive
   callback, as fwd_velocity)."""
-  _fwd.fwd_velocity(m, d)
+  fwd_velocity(m, d)
 
 
 def rne(m: Model, d: Data, flg_acc: bool = False):
@@ -98,19 +98,19 @@ def rne(m: Model, d: Data, flg_acc: bool = False):
   launch.  flg_acc = True (the inverse-dynamics use, out of this build's scope) is refused."""
   if flg_acc:
     raise NotImplementedError("rne(flg_acc=True) (inverse dynamics) is not part of this build")
-  _fwd._call("mjw_fwd_velocity", m, d)
+  _call("mjw_fwd_velocity", m, d)
 
 
 def factor_m(m: Model, d: Data):
   """qLD = factor(qM) (smooth.py:1104-1112): the acceleration-stage launch (dense: Cholesky L, row-major
   nv x nv; sparse: L'DL on the ancestor rows, mj_factorM order)."""
-  _fwd._call("mjw_fwd_acceleration", m, d)
+  _call("mjw_fwd_acceleration", m, d)
 
 
 def rne_postconstraint(m: Model, d: Data):
   """cacc, cfrc_int, cfrc_ext after the solver (smooth.py:1501-1600): the sensor kernel's acceleration
   stage (it also evaluates the acceleration sensors)."""
-  _fwd._sensor(m, d, 4)
+  _sensor(m, d, 4)
 
 
 # -- support functions on caller arrays -------------------------------------------------------------
