@@ -114,6 +114,13 @@ def rne_postconstraint(m: Model, d: Data):
 
 
 # -- support functions on caller arrays -------------------------------------------------------------
+def _per_world(t: torch.Tensor, nworld: int, *shape) -> torch.Tensor:
+  """A batched model field (leading dim 1 or nworld) as one row per world: types.py's `*` fields are read
+  at worldid % nb."""
+  t = t.reshape((-1,) + shape)
+  return t[torch.arange(nworld, device=t.device) % t.shape[0]]
+
+
 def _path_mask(m: Model) -> torch.Tensor:
   """(nbody, nbody) bool, [b, a]: body a lies on the path from b up to (not including) the world body."""
   mask = getattr(m, "_path_mask", None)
@@ -205,9 +212,9 @@ def subtree_vel(m: Model, d: Data):
   bodies first; DFS pre-order puts every descendant after its ancestors) and divided by the subtree mass,
   then angular momenta about the subtree COMs summed up the tree."""
   nw, nb = d.nworld, m.nbody
-  mass = m.body_mass.reshape(-1, nb)[0]
-  stm = m.body_subtreemass.reshape(-1, nb)[0]
-  inertia = m.body_inertia.reshape(-1, nb, 3)[0]
+  mass = _per_world(m.body_mass, nw, nb)
+  stm = _per_world(m.body_subtreemass, nw, nb)
+  inertia = _per_world(m.body_inertia, nw, nb, 3)
   cvel = d.cvel.reshape(nw, nb, 6)
   xipos = d.xipos.reshape(nw, nb, 3)
   ximat = d.ximat.reshape(nw, nb, 3, 3)
@@ -218,16 +225,15 @@ def subtree_vel(m: Model, d: Data):
   dv = torch.einsum("wbji,wbj->wbi", ximat, ang) * inertia  # ximat' ang, scaled by the principal inertia
   angmom = torch.einsum("wbij,wbj->wbi", ximat, dv)
   par = m.body_parentid.cpu().numpy()
-  stm_h = stm.cpu().numpy()
   for b in range(nb - 1, -1, -1):  # _linear_momentum (:2972-2988)
     if b:
       linvel[:, par[b]] += linvel[:, b]
-    linvel[:, b] /= max(float(stm_h[b]), 1e-15)
+    linvel[:, b] /= torch.clamp(stm[:, b : b + 1], min=1e-15)
   for b in range(nb - 1, 0, -1):  # _angular_momentum (:2992-3041)
     p = par[b]
-    angmom[:, b] += torch.cross(xipos[:, b] - sc[:, b], (lin[:, b] - linvel[:, b]) * mass[b], dim=-1)
+    angmom[:, b] += torch.cross(xipos[:, b] - sc[:, b], (lin[:, b] - linvel[:, b]) * mass[:, b : b + 1], dim=-1)
     angmom[:, p] += angmom[:, b]
-    angmom[:, p] += torch.cross(sc[:, b] - sc[:, p], (linvel[:, b] - linvel[:, p]) * stm[b], dim=-1)
+    angmom[:, p] += torch.cross(sc[:, b] - sc[:, p], (linvel[:, b] - linvel[:, p]) * stm[:, b : b + 1], dim=-1)
   d.subtree_linvel = linvel
   d.subtree_angmom = angmom
   return linvel, angmom
@@ -251,10 +257,10 @@ def energy_pos(m: Model, d: Data):
   nw, nb = d.nworld, m.nbody
   e = torch.zeros(nw, dtype=d.energy.dtype, device=d.energy.device)
   if not (m.opt.disableflags & DisableBit.GRAVITY):
-    g = m.opt.gravity.reshape(-1, 3)[0]
-    mass = m.body_mass.reshape(-1, nb)[0]
+    g = _per_world(m.opt.gravity, nw, 3)
+    mass = _per_world(m.body_mass, nw, nb)
     xipos = d.xipos.reshape(nw, nb, 3)
-    e -= (mass[1:] * (xipos[:, 1:] @ g)).sum(dim=1)
+    e -= (mass[:, 1:] * (xipos[:, 1:] * g[:, None, :]).sum(-1)).sum(dim=1)
   if not (m.opt.disableflags & DisableBit.SPRING):
     stiff = m.jnt_stiffness.reshape(-1, m.njnt)[0].cpu().numpy()
     jt = m.jnt_type.cpu().numpy()
