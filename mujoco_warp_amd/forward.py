@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from .io import cdata, cmodel
-from .types import Data, DisableBit, IntegratorType, Model
+from .types import Data, DisableBit, EnableBit, IntegratorType, Model
 
 
 def _stream(d: Data):
@@ -179,7 +179,7 @@ def rungekutta4(m: Model, d: Data):
   Without Python callbacks the three inner forward passes and the bookkeeping run inside the
   library (mjw_rungekutta4); with callbacks the inner passes go through `forward` here so the
   callbacks see every stage, and the bookkeeping launches the same device ops one by one."""
-  if not _has_callbacks(m):
+  if not (_has_callbacks(m) or _energy(m)):
     _call("mjw_rungekutta4", m, d)
     return
   A = (0.5, 0.5, 1.0)
@@ -217,9 +217,21 @@ def step2(m: Model, d: Data):
   _integrate(m, d)
 
 
+def _energy(m: Model) -> bool:
+  """opt.enableflags ENERGY: potential / kinetic energy into d.energy (forward.py:975-991), computed on the
+  staged path right after the position and velocity stages, as the reference does."""
+  return bool(m.opt.enableflags & EnableBit.ENERGY)
+
+
 def _forward_staged(m: Model, d: Data):
+  from .stages import energy_pos, energy_vel
+
   fwd_position(m, d)
+  if _energy(m):
+    energy_pos(m, d)
   fwd_velocity(m, d)
+  if _energy(m):
+    energy_vel(m, d)
   if not (m.opt.disableflags & DisableBit.ACTUATION) and m.callback.control is not None:
     m.callback.control(m, d)
   fwd_actuation(m, d)
@@ -230,7 +242,7 @@ def _forward_staged(m: Model, d: Data):
 
 def forward(m: Model, d: Data):
   """Forward dynamics (forward.py:972-1000)."""
-  if _has_callbacks(m):
+  if _has_callbacks(m) or _energy(m):
     _forward_staged(m, d)
   else:
     _call("mjw_forward", m, d)
@@ -238,7 +250,7 @@ def forward(m: Model, d: Data):
 
 def step(m: Model, d: Data):
   """Advance simulation (forward.py:1003-1018)."""
-  if _has_callbacks(m):
+  if _has_callbacks(m) or _energy(m):
     _forward_staged(m, d)
     _integrate(m, d)
   else:

@@ -196,3 +196,28 @@ def test_gpu_energy_conserved_on_pendulum():
     mjw.step(m, d)
   e1 = energy()
   assert np.all(np.abs(e1 - e0) <= 1e-2 * np.abs(e0) + 1e-3), (e0, e1)
+
+
+@pytest.mark.gpu
+def test_gpu_energy_flag_fills_d_energy():
+  """opt.enableflags ENERGY: step fills d.energy like energy_pos / energy_vel on the pre-step state
+  (forward.py:975-991); without the flag the step leaves it zero."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import types
+
+  mjm, m, d = _humanoid(4, seed=8)
+  _, m2, d2 = _humanoid(4, seed=8)
+  m.opt.enableflags |= types.EnableBit.ENERGY
+  mjw.step(m, d)
+  mjw.forward(m2, d2)
+  mjw.energy_pos(m2, d2)
+  mjw.energy_vel(m2, d2)
+  torch.cuda.synchronize()
+  assert float(np.abs(np_(d.energy)).max()) > 0
+  np.testing.assert_allclose(np_(d.energy), np_(d2.energy), rtol=1e-5, atol=1e-5)
+  _, m3, d3 = _humanoid(4, seed=8)
+  mjw.step(m3, d3)
+  torch.cuda.synchronize()
+  assert float(np.abs(np_(d3.energy)).max()) == 0.0
