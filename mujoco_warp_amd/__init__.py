@@ -49,6 +49,7 @@ from .stages import make_constraint
 from .stages import passive
 from .stages import rne
 from .stages import rne_postconstraint
+from .stages import set_const_fixed
 from .stages import solve_m
 from .stages import subtree_vel
 from .stages import tendon

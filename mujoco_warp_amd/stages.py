@@ -299,3 +299,17 @@ def energy_vel(m: Model, d: Data):
   mv = torch.zeros_like(d.qvel)
   mul_m(m, d, mv, d.qvel)
   d.energy.reshape(d.nworld, 2)[:, 1] = 0.5 * (d.qvel * mv).sum(dim=1)
+
+
+def set_const_fixed(m: Model, d: Data):
+  """The qpos0-independent derived constants (io.py:2197-2219): body_subtreemass = the body's mass plus
+  its descendants', per model row (a body_mass batched per world gives a per-world body_subtreemass, which
+  the kernels then read at worldid % nb).  The rest of the set_const family (qpos0-dependent invweights,
+  acc0, camera / light references) is derived by put_model and not recomputed on the device."""
+  nb = m.nbody
+  mass = m.body_mass.reshape(-1, nb)
+  sub = mass.clone()
+  par = m.body_parentid.cpu().numpy()
+  for b in range(nb - 1, 0, -1):  # DFS pre-order: descendants follow their ancestors
+    sub[:, par[b]] += sub[:, b]
+  m.body_subtreemass = sub.to(m.body_subtreemass.dtype).contiguous()

@@ -21,7 +21,7 @@ from tests.common import HUMANOID, np_, random_states
 OUT_OF_SCOPE = {
   "RenderContext", "create_render_context", "get_depth", "get_rgb", "get_segmentation", "render", "ray", "rays", "refit_bvh",
   "inverse", "island", "sap_broadphase", "nxn_broadphase", "primitive_narrowphase", "sdf_narrowphase", "set_const",
-  "set_const_0", "set_const_fixed", "set_length_range", "deriv_smooth_vel",
+  "set_const_0", "set_length_range", "deriv_smooth_vel",
 }
 
 
@@ -221,3 +221,44 @@ def test_gpu_energy_flag_fills_d_energy():
   mjw.step(m3, d3)
   torch.cuda.synchronize()
   assert float(np.abs(np_(d3.energy)).max()) == 0.0
+
+
+def test_set_const_fixed_subtreemass():
+  """set_const_fixed (io.py:2197-2219) on the CPU tensors: the compiler's body_subtreemass, and a per-world
+  batched body_mass giving per-world subtree masses."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+
+  mjm = mjcf.load_model(HUMANOID)
+  m = mjw.put_model(mjm, device="cpu")
+  d = mjw.make_data(mjm, nworld=3, device="cpu", m=m)
+  mjw.set_const_fixed(m, d)
+  np.testing.assert_allclose(m.body_subtreemass.numpy()[0], mjm.body_subtreemass, rtol=1e-6)
+  m.body_mass = m.body_mass.repeat(3, 1) * torch.tensor([[1.0], [2.0], [0.5]])
+  mjw.set_const_fixed(m, d)
+  assert m.body_subtreemass.shape == (3, mjm.nbody)
+  np.testing.assert_allclose(m.body_subtreemass.numpy()[1], 2.0 * mjm.body_subtreemass, rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_set_const_fixed_per_world_mass():
+  """Scaling every body mass of world 1 by 2 (batched body_mass + set_const_fixed) leaves its subtree COMs
+  equal to world 0's and doubles its composite inertia."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  mjm, m, d = _humanoid(2, seed=9)
+  d.qpos[1] = d.qpos[0]
+  d.qvel[1] = d.qvel[0]
+  m.body_mass = m.body_mass.repeat(2, 1) * torch.tensor([[1.0], [2.0]], device="cuda")
+  m.body_inertia = m.body_inertia.repeat(2, 1, 1) * torch.tensor([1.0, 2.0], device="cuda").reshape(2, 1, 1)
+  mjw.set_const_fixed(m, d)
+  mjw.fwd_position(m, d)
+  torch.cuda.synchronize()
+  sc = np_(d.subtree_com)
+  np.testing.assert_allclose(sc[1], sc[0], rtol=1e-5, atol=1e-6)
+  crb = np_(d.crb)
+  np.testing.assert_allclose(crb[1], 2.0 * crb[0], rtol=1e-5, atol=1e-5)
