@@ -49,6 +49,8 @@ from .stages import make_constraint
 from .stages import passive
 from .stages import rne
 from .stages import rne_postconstraint
+from .stages import set_const
+from .stages import set_const_0
 from .stages import set_const_fixed
 from .stages import solve_m
 from .stages import subtree_vel

@@ -313,3 +313,88 @@ def set_const_fixed(m: Model, d: Data):
   for b in range(nb - 1, 0, -1):  # DFS pre-order: descendants follow their ancestors
     sub[:, par[b]] += sub[:, b]
   m.body_subtreemass = sub.to(m.body_subtreemass.dtype).contiguous()
+
+
+def set_const_0(m: Model, d: Data):
+  """The qpos0-dependent derived constants (io.py:2222-2407) on the device, per world: the position stage at
+  qpos0 (then qpos is restored), then from qM and its inverse stat.meaninertia (trace / nv),
+  dof_invweight0 (diag M^-1, averaged per free-joint translation / rotation and per ball joint),
+  body_invweight0 (mean translational / rotational diagonal of J M^-1 J' at the body COM; zero for the world
+  and static bodies), tendon_invweight0 (J M^-1 J') and actuator_acc0 (||M^-1 moment||, joint and tendon
+  transmissions) -- the same definitions mjcf.py's compiler applies on the host.  Dense models; the camera /
+  light references and the dampratio resolution keep put_model's values."""
+  if m.is_sparse:
+    raise NotImplementedError("set_const_0 on sparse models is not part of this build")
+  nw, nv, nb = d.nworld, m.nv, m.nbody
+  saved = d.qpos.clone()
+  d.qpos[:] = _per_world(m.qpos0, nw, m.nq)
+  _call("mjw_fwd_position", m, d)
+  M = d.qM.reshape(nw, m.nv_pad, m.nv_pad)[:, :nv, :nv].double()
+  Minv = torch.linalg.inv(M)
+  f32 = m.dof_invweight0.dtype
+  m.stat.meaninertia = (M.diagonal(dim1=1, dim2=2).sum(1) / max(nv, 1)).to(f32)
+  diag = Minv.diagonal(dim1=1, dim2=2)
+  jt, jda = m.jnt_type.cpu().numpy(), m.jnt_dofadr.cpu().numpy()
+  inv = torch.zeros_like(diag)
+  for i, j in enumerate(m.dof_jntid.cpu().numpy()):
+    da = int(jda[j])
+    if jt[j] == JointType.FREE:
+      inv[:, i] = diag[:, da : da + 3].mean(1) if i < da + 3 else diag[:, da + 3 : da + 6].mean(1)
+    elif jt[j] == JointType.BALL:
+      inv[:, i] = diag[:, da : da + 3].mean(1)
+    else:
+      inv[:, i] = diag[:, i]
+  m.dof_invweight0 = inv.to(f32)
+  # body_invweight0 at the body COMs
+  biw = torch.zeros(nw, nb, 2, dtype=torch.float64, device=M.device)
+  weld = m.body_weldid.cpu().numpy()
+  jacp = torch.zeros(nw, 3, nv, device=M.device)
+  jacr = torch.zeros(nw, 3, nv, device=M.device)
+  xipos = d.xipos.reshape(nw, nb, 3)
+  for b in range(1, nb):
+    if weld[b] == 0 or nv == 0:
+      continue
+    jac(m, d, jacp, jacr, xipos[:, b], torch.full((nw,), b, device=M.device))
+    J = torch.cat([jacp, jacr], dim=1).double()
+    A = J @ Minv @ J.transpose(1, 2)
+    ad = A.diagonal(dim1=1, dim2=2)
+    tr, rot = ad[:, :3].mean(1), ad[:, 3:].mean(1)
+    tr2 = torch.where((tr < 1e-15) & (rot > 1e-15), rot, tr)
+    rot2 = torch.where((rot < 1e-15) & (tr > 1e-15), tr, rot)
+    biw[:, b, 0], biw[:, b, 1] = tr2, rot2
+  m.body_invweight0 = biw.to(f32)
+  # tendons: dense Jacobian rows from the sparse ten_J pattern
+  nt = int(getattr(m, "ntendon", 0))
+  tenJ = torch.zeros(nw, nt, nv, dtype=torch.float64, device=M.device)
+  if nt:
+    rownnz, rowadr, colind = (getattr(m, f).cpu().numpy() for f in ("ten_J_rownnz", "ten_J_rowadr", "ten_J_colind"))
+    vals = d.ten_J.reshape(nw, -1).double()
+    for t in range(nt):
+      for k in range(int(rownnz[t])):
+        tenJ[:, t, int(colind[rowadr[t] + k])] = vals[:, rowadr[t] + k]
+    m.tendon_invweight0 = torch.einsum("wti,wij,wtj->wt", tenJ, Minv, tenJ).to(f32)
+  # actuator_acc0
+  if m.nu:
+    gear = _per_world(m.actuator_gear, nw, m.nu, 6).double()
+    trn, trnid = m.actuator_trntype.cpu().numpy(), m.actuator_trnid.reshape(-1, 2).cpu().numpy()
+    vec = torch.zeros(nw, m.nu, nv, dtype=torch.float64, device=M.device)
+    for a in range(m.nu):
+      j = int(trnid[a, 0])
+      if trn[a] == 3:  # TrnType.TENDON
+        vec[:, a] = gear[:, a, :1] * tenJ[:, j]
+        continue
+      da = int(jda[j])
+      if jt[j] == JointType.FREE:
+        vec[:, a, da : da + 6] = gear[:, a]
+      elif jt[j] == JointType.BALL:
+        vec[:, a, da : da + 3] = gear[:, a, :3]
+      else:
+        vec[:, a, da] = gear[:, a, 0]
+    m.actuator_acc0 = torch.linalg.norm(torch.einsum("wij,waj->wai", Minv, vec), dim=-1).to(f32)
+  d.qpos[:] = saved
+
+
+def set_const(m: Model, d: Data):
+  """set_const_fixed then set_const_0 (io.py:2410-2470)."""
+  set_const_fixed(m, d)
+  set_const_0(m, d)

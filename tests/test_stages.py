@@ -20,8 +20,8 @@ from tests.common import HUMANOID, np_, random_states
 # velocity derivative, which runs inside the integrator kernel
 OUT_OF_SCOPE = {
   "RenderContext", "create_render_context", "get_depth", "get_rgb", "get_segmentation", "render", "ray", "rays", "refit_bvh",
-  "inverse", "island", "sap_broadphase", "nxn_broadphase", "primitive_narrowphase", "sdf_narrowphase", "set_const",
-  "set_const_0", "set_length_range", "deriv_smooth_vel",
+  "inverse", "island", "sap_broadphase", "nxn_broadphase", "primitive_narrowphase", "sdf_narrowphase",
+  "set_length_range", "deriv_smooth_vel",
 }
 
 
@@ -262,3 +262,38 @@ def test_gpu_set_const_fixed_per_world_mass():
   np.testing.assert_allclose(sc[1], sc[0], rtol=1e-5, atol=1e-6)
   crb = np_(d.crb)
   np.testing.assert_allclose(crb[1], 2.0 * crb[0], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["humanoid", "franka", "tendon"])
+def test_gpu_set_const_0_reproduces_put_model(model):
+  """set_const_0 on the device (qpos0 position stage, M^-1 in fp64 from the fp32 qM) reproduces the
+  constants put_model took from the compiler (mjcf.py, the same definitions in fp64 on the host)."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+  from tests.common import franka_model
+
+  if model == "humanoid":
+    mjm = mjcf.load_model(HUMANOID)
+  elif model == "franka":
+    mjm = franka_model()
+  else:
+    mjm = mjcf.load_model_from_string("""<mujoco><worldbody><body><joint name="a" axis="0 1 0"/><geom size=".1" pos=".2 0 0"/>
+      <body pos=".4 0 0"><joint name="b" axis="0 1 0"/><geom size=".1" pos=".2 0 0"/></body></body></worldbody>
+      <tendon><fixed name="t"><joint joint="a" coef="1"/><joint joint="b" coef="-.5"/></fixed></tendon>
+      <actuator><motor tendon="t" gear="2"/><motor joint="b"/></actuator></mujoco>""")
+  m = mjw.put_model(mjm, device="cuda")
+  d = mjw.make_data(mjm, nworld=2, device="cuda", m=m)
+  want = {f: np_(getattr(m, f))[0] for f in ("dof_invweight0", "body_invweight0", "actuator_acc0")}
+  want_mi = float(np_(m.stat.meaninertia).reshape(-1)[0])
+  q = d.qpos.clone()
+  mjw.set_const_0(m, d)
+  torch.cuda.synchronize()
+  assert torch.equal(d.qpos, q)
+  np.testing.assert_allclose(np_(m.stat.meaninertia), want_mi, rtol=1e-5)
+  for f, w in want.items():
+    got = np_(getattr(m, f))
+    assert got.shape[0] == 2
+    np.testing.assert_allclose(got[1], w, rtol=2e-4, atol=1e-6, err_msg=f)
