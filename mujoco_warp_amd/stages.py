@@ -321,8 +321,8 @@ def set_const_0(m: Model, d: Data):
   dof_invweight0 (diag M^-1, averaged per free-joint translation / rotation and per ball joint),
   body_invweight0 (mean translational / rotational diagonal of J M^-1 J' at the body COM; zero for the world
   and static bodies), tendon_invweight0 (J M^-1 J') and actuator_acc0 (||M^-1 moment||, joint and tendon
-  transmissions) -- the same definitions mjcf.py's compiler applies on the host.  Dense models; the camera /
-  light references and the dampratio resolution keep put_model's values."""
+  transmissions), the camera / light references -- the same definitions mjcf.py's compiler applies on
+  the host.  Dense models; the dampratio resolution keeps put_model's values."""
   if m.is_sparse:
     raise NotImplementedError("set_const_0 on sparse models is not part of this build")
   nw, nv, nb = d.nworld, m.nv, m.nbody
@@ -391,7 +391,40 @@ def set_const_0(m: Model, d: Data):
       else:
         vec[:, a, da] = gear[:, a, 0]
     m.actuator_acc0 = torch.linalg.norm(torch.einsum("wij,waj->wai", Minv, vec), dim=-1).to(f32)
+  # camera / light references at qpos0 (io.py:2330-2345): the fixed-frame placement relative to the body
+  # and to the target's (or own) subtree COM
+  xpos = d.xpos.reshape(nw, nb, 3)
+  xmat = d.xmat.reshape(nw, nb, 3, 3)
+  sc = d.subtree_com.reshape(nw, nb, 3)
+  if m.ncam:
+    b = m.cam_bodyid.to(torch.long)
+    tgt = m.cam_targetbodyid.to(torch.long)
+    ref = torch.where(tgt >= 0, tgt, b)
+    cpos = _per_world(m.cam_pos, nw, m.ncam, 3)
+    cq = torch.nn.functional.normalize(_per_world(m.cam_quat, nw, m.ncam, 4), dim=-1)
+    cx = xpos[:, b] + torch.einsum("wcij,wcj->wci", xmat[:, b], cpos)
+    m.cam_pos0 = (cx - xpos[:, b]).to(f32)
+    m.cam_poscom0 = (cx - sc[:, ref]).to(f32)
+    m.cam_mat0 = torch.einsum("wcij,wcjk->wcik", xmat[:, b], _quat_to_mat(cq)).reshape(nw, m.ncam, 9).to(f32)
+  if m.nlight:
+    b = m.light_bodyid.to(torch.long)
+    tgt = m.light_targetbodyid.to(torch.long)
+    ref = torch.where(tgt >= 0, tgt, b)
+    lx = xpos[:, b] + torch.einsum("wlij,wlj->wli", xmat[:, b], _per_world(m.light_pos, nw, m.nlight, 3))
+    m.light_pos0 = (lx - xpos[:, b]).to(f32)
+    m.light_poscom0 = (lx - sc[:, ref]).to(f32)
+    m.light_dir0 = torch.einsum("wlij,wlj->wli", xmat[:, b], _per_world(m.light_dir, nw, m.nlight, 3)).to(f32)
   d.qpos[:] = saved
+
+
+def _quat_to_mat(q: torch.Tensor) -> torch.Tensor:
+  """math.py quat_to_mat for unit quaternions (..., 4) -> (..., 3, 3)."""
+  w, x, y, z = q.unbind(-1)
+  r = torch.stack([
+    1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+    2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+    2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], dim=-1)
+  return r.reshape(q.shape[:-1] + (3, 3))
 
 
 def set_const(m: Model, d: Data):
