@@ -16,22 +16,24 @@ collective on the data path: a gloo (host) barrier + max-over-ranks of the
 elapsed time brackets the timed region.
 
 A step is a counter reset and two kernels on the torch stream: the forward kernel
-mjw::mjw_kernel<79> (kinematics, com, crb/qM, collision, constraint rows,
+mjw::mjw_kernel<79, ...> (kinematics, com, crb/qM, collision, constraint rows,
 transmission, velocity, rne, actuation, qfrc_smooth) and the dense kernel
-mjw::dense_kernel<7,false> (Cholesky + M^-1, CG solve, Euler).  As in the
+mjw::dense_kernel<7, ...> (Cholesky + M^-1, CG solve, Euler).  As in the
 reference's benchmark (benchmark.py:123-155) the step is captured once as a
-hipGraph and replayed every step, the control noise launched before each replay;
-every 10th timed step instead runs eagerly through mjw_step_trace, which records a
-HIP event on that stream after every kernel launch and so times each kernel.
+hipGraph (after the first warmup step) and replayed every step, the control noise
+launched before each replay; the timed region holds graph replays only.  After it,
+an untimed pass of --trace-steps steps runs eagerly through mjw_step_trace, which
+records a HIP event on that stream after every kernel launch and so times each kernel.
 
 Also reported: `roofline` for the dominant kernel group -- the one with the most
-time per step (the dense kernel on the humanoid, the CG solve on the sparse path):
+time per step (the forward kernel on the humanoid, the CG solve on the sparse path):
 its algorithmic bytes per env-step (SURVEY.md 8(d)'s B_alg split by the kernel that
-writes each output) x worlds per launch over its HIP-event time vs
-the 8 TB/s HBM peak, and its traffic from the committed rocprofv3 PMC passes
-((2 FETCH_SIZE + WRITE_SIZE) KB -> B, summed per step over the group's launches);
-every group's figures side by side in `roofline.kernels`; and `cpu_baseline` (the
-fp64 C oracle, OpenMP over worlds on the host cores, bounded sample, rank 0).
+writes each output, DESIGN.md 3.5, at the trace pass's nefc / ncon) x worlds per
+launch over its HIP-event time vs the 8 TB/s HBM peak, and its traffic from the
+committed rocprofv3 PMC passes ((2 FETCH_SIZE + WRITE_SIZE) KB -> B, summed per step
+over the group's launches, with the PMC window's own algorithmic bytes for the
+ratio); every group's figures side by side in `roofline.kernels`; and `cpu_baseline`
+(the fp64 C oracle, OpenMP over worlds on the box's CPU share, bounded sample, rank 0).
 """
 
 import argparse
@@ -148,9 +150,9 @@ def parse():
   p.add_argument("--pmc", default=None, help="PMC traffic summary (default: the newest profiles/pmc_<model>_rNN.json)")
   p.add_argument("--graph", type=int, default=1, help="capture mjw.step once as a hipGraph and replay it every step "
                  "(benchmark.py:123-155: ctrl noise is launched outside the graph); 0 = launch the step eagerly")
-  p.add_argument("--event-every", type=int, default=10,
-                 help="every E-th timed step runs eagerly with a HIP event after each kernel launch (mjw_step_trace: "
-                 "the per-kernel durations of `roofline`); the others replay the graph (events on every step cost ~6%%)")
+  p.add_argument("--trace-steps", type=int, default=10,
+                 help="untimed steps after the timed region that run eagerly with a HIP event after each kernel launch "
+                 "(mjw_step_trace): the per-kernel durations of `roofline`; every timed step is a graph replay")
   p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                  help="weak: --nworld worlds per rank; strong: --nworld worlds in total, split over the ranks")
   p.add_argument("--streams", type=int, default=1,
@@ -203,8 +205,9 @@ def cpu_baseline(mjm, nworld, nsteps, key, njmax, nconmax, model):
   from oracle import orc
 
   nproc, allowed, cpu_model = _host_cpu()
-  # the box grants its share through OMP_NUM_THREADS / the affinity mask; use all of it
-  nthread = int(os.environ.get("OMP_NUM_THREADS", "0")) or allowed
+  # the GPU box grants a 1-GPU job its CPU share through OMP_NUM_THREADS (16) while the affinity mask shows
+  # the whole host; the baseline uses that share, all of it (MJW_CPU_BASELINE_THREADS overrides)
+  nthread = int(os.environ.get("MJW_CPU_BASELINE_THREADS", "0")) or int(os.environ.get("OMP_NUM_THREADS", "0")) or allowed
   nthread = max(1, min(nthread, allowed))
   rates = {}
   for bits in (64, 32):
@@ -226,11 +229,16 @@ def cpu_baseline(mjm, nworld, nsteps, key, njmax, nconmax, model):
     cores=nthread,
     kind="port",
     value_fp32=rates[32][0],
+    value_per_thread=rates[64][0] / nthread,
+    # worlds are independent, so the OpenMP loop scales with threads up to the memory bandwidth; this is
+    # the linear extrapolation to every CPU the affinity mask shows, not a measurement
+    value_all_cpus_linear_estimate=rates[64][0] / nthread * allowed,
     host_nproc=nproc,
     host_cpus_allowed=allowed,
     cpu_model=cpu_model,
     sample=f"C oracle (oracle/oracle.c), {model}, {nworld} worlds x {nsteps} steps with ctrl noise, {nthread} OpenMP "
-    f"threads (host: {nproc} logical CPUs, {allowed} allowed), fp64 {rates[64][1]:.1f} s (value), fp32 "
+    f"threads = the box's CPU share for one GPU (host: {nproc} logical CPUs, {allowed} in the affinity mask), "
+    f"fp64 {rates[64][1]:.1f} s (value), fp32 "
     f"{rates[32][1]:.1f} s (value_fp32); the reference's Warp-CPU path is not runnable here (no warp/mujoco)",
   )
 
@@ -256,6 +264,10 @@ def pmc_traffic(path, model, nworld, solver_name):
       continue
     out[k] = {"bytes_per_launch": v["hbm_bytes_per_launch"], "bytes_per_step": v.get("hbm_bytes_per_step"),
               "launches_per_step": v.get("launches_per_step")}
+  # the counted window's nefc / ncon (tools/pmc_traffic.py records the PMC passes' own bench lines)
+  win = (pmc.get("window") or {}).get("fetch")
+  if win is not None:
+    out["_window"] = {"nefc_mean": float(win["nefc_mean"]), "ncon_mean": float(win["ncon_mean"])}
   return out, os.path.basename(path)
 
 
@@ -271,8 +283,13 @@ def kernel_table(durations, sparse):
   return tab
 
 
-def roofline_record(tab, groups_alg, nworld, pmc, pmc_src):
-  """`roofline` of the dominant kernel group (most time per step) and the per-group / per-kernel figures."""
+def roofline_record(tab, groups_alg, nworld, pmc, pmc_src, groups_alg_at=None):
+  """`roofline` of the dominant kernel group (most time per step) and the per-group / per-kernel figures.
+  `groups_alg_at(nefc, ncon)` prices the algorithmic bytes at the PMC window's sizes for traffic_over_alg
+  (the counters were taken on other steps than the trace pass; without a recorded window the trace pass's
+  bytes are used and the record says so)."""
+  win = (pmc or {}).get("_window")
+  alg_pmc = groups_alg_at(win["nefc_mean"], win["ncon_mean"]) if (win and groups_alg_at) else groups_alg
   groups = {}
   for name, e in tab.items():
     g = groups.setdefault(e["group"], {"kernels": [], "ms_per_step": 0.0, "traffic_per_step": 0.0, "traffic_known": True})
@@ -296,7 +313,7 @@ def roofline_record(tab, groups_alg, nworld, pmc, pmc_src):
       "alg_bytes_per_env_step": alg, "alg_bytes_per_step": alg * nworld if alg else None,
       "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS if ach else None,
       "traffic_per_step": g["traffic_per_step"] if g["traffic_known"] else None,
-      "traffic_over_alg": (g["traffic_per_step"] / (alg * nworld)) if g["traffic_known"] and alg else None,
+      "traffic_over_alg": (g["traffic_per_step"] / (alg_pmc[gname] * nworld)) if g["traffic_known"] and alg_pmc.get(gname) else None,
     }
   cand = {k: v for k, v in rec.items() if v["alg_bytes_per_env_step"]}
   dom = max(cand, key=lambda k: cand[k]["ms_per_step"])
@@ -310,7 +327,9 @@ def roofline_record(tab, groups_alg, nworld, pmc, pmc_src):
     "traffic": d["traffic_per_step"],
     "traffic_source": pmc_src,
     "traffic_note": "HBM bytes per step of the group's launches ((2 FETCH_SIZE + WRITE_SIZE) KB, rocprofv3 PMC); "
-                    "= per launch when the group is one kernel launched once per step",
+                    "= per launch when the group is one kernel launched once per step; traffic_over_alg divides by the "
+                    + (f"algorithmic bytes at the PMC window's own nefc {win['nefc_mean']:.2f} / ncon {win['ncon_mean']:.2f}"
+                       if win else "trace pass's algorithmic bytes (the PMC summary records no window)"),
     "kernel": " + ".join(d["kernels"]),
     "group": dom,
     "kernel_ms": d["ms_per_step"],
@@ -417,13 +436,12 @@ def main():
         else:
           mjw.step(m, dk)
 
-  for i in range(args.warmup):
-    one_step(i)
-  torch.cuda.synchronize()
   graph_error = None
-  if args.graph:
-    # capture after warmup (benchmark.py:123-155 captures fn(m, d) once and replays it every step);
-    # should the capture fail, the steps run eagerly and the record says why
+
+  def capture():
+    # benchmark.py:123-155 captures fn(m, d) once and replays it every step; should the capture fail,
+    # the steps run eagerly and the record says why.  Capture does not execute: the state is unchanged.
+    nonlocal graphs, graph_error
     try:
       graphs = []
       for dk in shards:
@@ -435,32 +453,45 @@ def main():
         graphs.append(g)
     except RuntimeError as e:
       graphs, graph_error = None, str(e)[:200]
-    # capture does not execute: the state is unchanged, the replays below advance it
     torch.cuda.synchronize()
+
+  # warmup: the first step eagerly (loads the kernels), then the graph is captured and the remaining
+  # warmup steps already replay it, so the timed region starts on a warm graph
+  for i in range(args.warmup):
+    if i == 1 and args.graph:
+      capture()
+    one_step(i)
+  torch.cuda.synchronize()
+  if args.graph and graphs is None and graph_error is None:
+    capture()
 
   def sizes():
     nefc = sum(float(dk.nefc.float().sum()) for dk in shards) / nworld
     ncon = sum(float(dk.nacon[0]) for dk in shards) / nworld
     return nefc, ncon
 
-  # sizes for the algorithmic-bytes figure (untimed)
-  nefc_mean, ncon_mean = sizes()
-
-  # a launch trace (one HIP event after every kernel) on every `event_every`-th timed step (every step
-  # without a graph)
-  every = 1 if graphs is None else max(1, args.event_every)
-  traced = set(range(0, args.steps, every))
+  # the timed region: K graph replays (or K eager steps when capture failed), nothing else
+  nefc_t0, ncon_t0 = sizes()
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   for i in range(args.steps):
-    one_step(args.warmup + i, i in traced)
+    one_step(args.warmup + i)
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
   elapsed = time.perf_counter() - t0
+  # per-kernel durations: an untimed pass of `trace_steps` eager steps right after the timed region, one
+  # HIP event after every kernel launch (mjw_step_trace); the algorithmic bytes of `roofline` use this
+  # window's own constraint / contact counts (mean of its first and last step)
+  ntrace = max(1, args.trace_steps)
+  nefc_mean, ncon_mean = sizes()
+  nefc_t1, ncon_t1 = nefc_mean, ncon_mean
+  for i in range(ntrace):
+    one_step(args.warmup + args.steps + i, traced=True)
+  torch.cuda.synchronize()
   tab = kernel_table(tracer.durations(), bool(m.is_sparse))
   n2, c2 = sizes()
   nefc_mean, ncon_mean = 0.5 * (nefc_mean + n2), 0.5 * (ncon_mean + c2)
@@ -497,7 +528,9 @@ def main():
       pmc, pmc_src = pmc_traffic(path, args.model, nlaunch, solver_name)
       if pmc is not None:
         break
-    roof = roofline_record(tab, groups_alg, nlaunch, pmc, pmc_src)
+    row_w = 2 * m.njrow if m.is_sparse else m.nv_pad
+    roof = roofline_record(tab, groups_alg, nlaunch, pmc, pmc_src,
+                           lambda ne, nc: b_alg_groups(mjm, words, ne, nc, row_w, bool(m.is_sparse)))
     if args.scaling == "weak":
       parallelism = f"{args.nworld} worlds per rank on {world} GPU(s) (weak), no collective"
     else:
@@ -528,10 +561,13 @@ def main():
         "parallelism": parallelism,
         "graph": graphs is not None,
         **({"graph_error": graph_error} if graph_error else {}),
-        "timed_kernel_launches": len(traced),
+        "timed_region": "graph replays only" if graphs is not None else "eager steps (no graph)",
+        "trace_steps": ntrace,
         "converged_worlds": converged,
         "nefc_mean": nefc_mean,
         "ncon_mean": ncon_mean,
+        "nefc_ncon_window": "trace pass (mean of its first and last step); timed region start / end: "
+                            f"nefc {nefc_t0:.2f} / {nefc_t1:.2f}, ncon {ncon_t0:.2f} / {ncon_t1:.2f}",
         "solver_niter_mean": solver_niter_mean,
         "solver_niter_max": solver_niter_max,
         "streams": nshard,

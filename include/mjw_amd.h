@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 21
+#define MJW_ABI_VERSION 22
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -45,24 +45,25 @@
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
-  X(npair)
+  X(npair) X(ngravcomp) X(has_fluid)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
   X(opt_timestep, 1) X(opt_tolerance, 1) X(opt_ls_tolerance, 1) X(opt_impratio_invsqrt, 1)        \
   X(opt_ccd_tolerance, 1)                                                                          \
   X(opt_gravity, 3) X(opt_magnetic, 3) X(stat_meaninertia, 1)                                      \
+  X(opt_wind, 3) X(opt_density, 1) X(opt_viscosity, 1)                                             \
   X(qpos0, nq) X(qpos_spring, nq)                                                                  \
   X(body_pos, nbody * 3) X(body_quat, nbody * 4) X(body_ipos, nbody * 3) X(body_iquat, nbody * 4) \
   X(body_mass, nbody) X(body_subtreemass, nbody) X(body_inertia, nbody * 3)                       \
-  X(body_invweight0, nbody * 2)                                                                    \
+  X(body_invweight0, nbody * 2) X(body_gravcomp, nbody)                                            \
   X(jnt_solref, njnt * 2) X(jnt_solimp, njnt * 5) X(jnt_pos, njnt * 3) X(jnt_axis, njnt * 3)      \
   X(jnt_stiffness, njnt) X(jnt_range, njnt * 2) X(jnt_actfrcrange, njnt * 2) X(jnt_margin, njnt)  \
   X(dof_solref, nv * 2) X(dof_solimp, nv * 5) X(dof_frictionloss, nv) X(dof_armature, nv)         \
   X(dof_damping, nv) X(dof_invweight0, nv)                                                         \
   X(geom_solmix, ngeom) X(geom_solref, ngeom * 2) X(geom_solimp, ngeom * 5) X(geom_size, ngeom * 3) \
   X(geom_aabb, ngeom * 6) X(geom_rbound, ngeom) X(geom_pos, ngeom * 3) X(geom_quat, ngeom * 4)    \
-  X(geom_friction, ngeom * 3) X(geom_margin, ngeom) X(geom_gap, ngeom)                             \
+  X(geom_friction, ngeom * 3) X(geom_margin, ngeom) X(geom_gap, ngeom) X(geom_fluid, ngeom * 12)  \
   X(site_pos, nsite * 3) X(site_quat, nsite * 4)                                                   \
   X(cam_pos, ncam * 3) X(cam_quat, ncam * 4) X(cam_poscom0, ncam * 3) X(cam_pos0, ncam * 3)       \
   X(cam_mat0, ncam * 9)                                                                            \
@@ -92,7 +93,8 @@
   X(body_subtree_end, nbody) X(body_level, nbody) X(level_body, nbody) X(level_adr, nlevel + 1)    \
   X(jnt_type, njnt) X(jnt_qposadr, njnt) X(jnt_dofadr, njnt) X(jnt_bodyid, njnt)                  \
   X(jnt_limited, njnt) X(jnt_actfrclimited, njnt) X(jnt_limited_slide_hinge_adr, nlimited)        \
-  X(jnt_limited_ball_adr, nlimited_ball)                                                           \
+  X(jnt_limited_ball_adr, nlimited_ball) X(jnt_actgravcomp, njnt)                                 \
+  X(body_geomadr, nbody) X(body_geomnum, nbody) X(body_fluid_ellipsoid, nbody)                    \
   X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \
   X(geom_type, ngeom) X(geom_condim, ngeom) X(geom_bodyid, ngeom) X(geom_priority, ngeom)         \
   X(site_bodyid, nsite)                                                                            \
@@ -138,7 +140,7 @@
   X(qM, nv_pad * nv_pad) X(qLD, nv * nv)                                                           \
   X(actuator_length, nu) X(actuator_moment, nJmom) X(actuator_velocity, nu) X(actuator_force, nu) \
   X(cvel, nbody * 6) X(cdof_dot, nv * 6) X(qfrc_bias, nv) X(qfrc_spring, nv) X(qfrc_damper, nv)   \
-  X(qfrc_gravcomp, nv) X(qfrc_passive, nv) X(qfrc_actuator, nv) X(qfrc_smooth, nv)                \
+  X(qfrc_gravcomp, nv) X(qfrc_fluid, nv) X(qfrc_passive, nv) X(qfrc_actuator, nv) X(qfrc_smooth, nv) \
   X(qacc_smooth, nv) X(qfrc_constraint, nv) X(cacc, nbody * 6) X(cfrc_int, nbody * 6)             \
   X(cfrc_ext, nbody * 6)                                                                           \
   X(efc_J, njmax_pad * nv_pad) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax_pad)         \

@@ -30,6 +30,7 @@
 #include "mjw_ccd.h"
 #include "mjw_narrow.h"
 #include "mjw_flexcol.h"
+#include "mjw_passive.h"
 
 namespace mjw {
 namespace sp {
@@ -1675,8 +1676,57 @@ __device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, int wid)
     }
   }
   __syncthreads();
+  // passive.py:829-869: gravity compensation and fluid forces (mjw_passive.h), per-body wrenches in the
+  // sp_body / cacc scratch (rne fills both afterwards), then per dof over its body's subtree
   float* qp = d.qfrc_passive + (long)wid * nv;
-  for (int i = tid(); i < nv; i += BLK) qp[i] = qs[i] + qd[i];
+  float* qg = d.qfrc_gravcomp + (long)wid * nv;
+  float* qf = d.qfrc_fluid + (long)wid * nv;
+  const bool gc_on = m.ngravcomp && !(m.opt_disableflags & DSBL_GRAVITY) && !(dsbl_spring && dsbl_damper);
+  const bool fl_on = m.has_fluid && !(dsbl_spring && dsbl_damper);
+  if (gc_on || fl_on) {
+    float* Wg = d.sp_body + (long)wid * nb * 6;
+    float* Wf = d.cacc + (long)wid * nb * 6;
+    const float* xipos = d.xipos + (long)wid * nb * 3;
+    const float* ximat = d.ximat + (long)wid * nb * 9;
+    const float* sc = d.subtree_com + (long)wid * nb * 3;
+    const float* gxpos = d.geom_xpos + (long)wid * m.ngeom * 3;
+    const float* gxmat = d.geom_xmat + (long)wid * m.ngeom * 9;
+    const float zero3[3] = {0.0f, 0.0f, 0.0f};
+    for (int b = tid(); b < nb; b += BLK) {
+      const float* sr = sc + 3 * m.body_rootid[b];
+      float f[3], t[3];
+      if (gc_on) {
+        gravcomp_force(m, wid, b, f);
+        body_wrench(Wg + 6 * b, f, zero3, xipos + 3 * b, sr);
+      }
+      if (fl_on) {
+        fluid_force(m, wid, b, xipos + 3 * b, ximat + 9 * b, cvel_all + 6 * b, sr, gxpos, gxmat, f, t);
+        body_wrench(Wf + 6 * b, f, t, xipos + 3 * b, sr);
+      }
+    }
+    __syncthreads();
+    for (int i = tid(); i < nv; i += BLK) {
+      const float* cd = cdof + 6 * i;
+      const int db = m.dof_bodyid[i], end = m.body_subtree_end[db];
+      float g = 0.0f, fl = 0.0f;
+      for (int b = db; b < end; b++) {
+        if (gc_on) g += cd[0] * Wg[6 * b] + cd[1] * Wg[6 * b + 1] + cd[2] * Wg[6 * b + 2] + cd[3] * Wg[6 * b + 3] + cd[4] * Wg[6 * b + 4] + cd[5] * Wg[6 * b + 5];
+        if (fl_on) fl += cd[0] * Wf[6 * b] + cd[1] * Wf[6 * b + 1] + cd[2] * Wf[6 * b + 2] + cd[3] * Wf[6 * b + 3] + cd[4] * Wf[6 * b + 4] + cd[5] * Wf[6 * b + 5];
+      }
+      qg[i] = g;
+      qf[i] = fl;
+    }
+  } else {
+    for (int i = tid(); i < nv; i += BLK) qg[i] = qf[i] = 0.0f;
+  }
+  __syncthreads();
+  // passive.py:555-561: gravcomp unless routed to the actuators (forward.py:824-826), then the fluid force
+  for (int i = tid(); i < nv; i += BLK) {
+    float p = qs[i] + qd[i];
+    if (gc_on && !m.jnt_actgravcomp[m.dof_jntid[i]]) p += qg[i];
+    if (fl_on) p += qf[i];
+    qp[i] = p;
+  }
   // rne: cacc by ancestor walk, body forces into scratch, subtree sums, projection on cdof
   float* cacc = d.cacc + (long)wid * nb * 6;
   float* body_f = d.sp_body + (long)wid * nb * 6;
@@ -1777,6 +1827,7 @@ __device__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, int wid
         if (d.moment_colind[(long)wid * m.nJmom + adr + k] == i) q += d.actuator_moment[(long)wid * m.nJmom + adr + k] * d.actuator_force[gu];
     }
     const int j = m.dof_jntid[i];
+    if (m.ngravcomp && m.jnt_actgravcomp[j]) q += d.qfrc_gravcomp[(long)wid * nv + i];  // forward.py:824-826
     if (m.jnt_actfrclimited[j]) q = clampf(q, jfr[2 * j], jfr[2 * j + 1]);
     qa[i] = q;
   }

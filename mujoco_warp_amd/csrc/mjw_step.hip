@@ -15,6 +15,7 @@
 #include "mjw_common.h"
 #include "mjw_ccd.h"
 #include "mjw_narrow.h"
+#include "mjw_passive.h"
 #include "mjw_tendon.h"
 
 #include <algorithm>
@@ -1565,7 +1566,9 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
 // -------------------------------------------------------------------------------------------
 // velocity (forward.py:592-613): actuator velocity, com_vel, passive, rne
 // -------------------------------------------------------------------------------------------
-template <bool TEN>
+// POS_LDS: the position stage ran in this launch, so the body / geom frames are in LDS (else they are read
+// from the Data)
+template <bool TEN, bool POS_LDS>
 __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -1667,14 +1670,64 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
   }
   WSYNC();
   if (TEN && m.ntendon) tendon_passive(m, d, qpos, qvel, spring, damper, wid, lane);  // passive.py:183-252
+  // passive.py:829-869: gravity compensation (unless gravity is off) and fluid forces, both body forces at
+  // xipos mapped through the body Jacobian (mjw_passive.h); in the extended instantiation only.  The cacc /
+  // cfrc LDS slots hold the two per-body wrenches (rne fills them afterwards).  nv <= 64: dof i is lane i.
+  float gcomp = 0.0f, fluid = 0.0f;
+  const bool gc_on = TEN && m.ngravcomp && !(m.opt_disableflags & DSBL_GRAVITY) && !(dsbl_spring && dsbl_damper);
+  const bool fl_on = TEN && m.has_fluid && !(dsbl_spring && dsbl_damper);
+  if (gc_on || fl_on) {
+    float* Wg = s + L.cacc;
+    float* Wf = s + L.cfrc;
+    const float* xipos = s + L.xipos;
+    const float* gxpos = POS_LDS ? s + L.gxpos : d.geom_xpos + (long)wid * m.ngeom * 3;
+    const float* gxmat = POS_LDS ? s + L.gxmat : d.geom_xmat + (long)wid * m.ngeom * 9;
+    const float zero3[3] = {0.0f, 0.0f, 0.0f};
+    for (int b = lane; b < m.nbody; b += LPW) {
+      const float* sr = s + L.subtree_com + 3 * m.body_rootid[b];
+      float f[3], t[3];
+      if (gc_on) {
+        gravcomp_force(m, wid, b, f);
+        body_wrench(Wg + 6 * b, f, zero3, xipos + 3 * b, sr);
+      }
+      if (fl_on) {
+        float xm[9];
+        if (POS_LDS) {  // the inertial frame as kinematics() computes it (its LDS copy is gone in direct mode)
+          const float q[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+          float qi[4];
+          mul_quat(qi, q, MR(body_iquat) + 4 * b);
+          quat_to_mat(xm, qi);
+        } else {
+          for (int k = 0; k < 9; k++) xm[k] = d.ximat[((long)wid * m.nbody + b) * 9 + k];
+        }
+        fluid_force(m, wid, b, xipos + 3 * b, xm, cvel + 6 * b, sr, gxpos, gxmat, f, t);
+        body_wrench(Wf + 6 * b, f, t, xipos + 3 * b, sr);
+      }
+    }
+    WSYNC();
+    for (int i = lane; i < nv; i += LPW) {
+      const float* cd = s + L.cdof + 6 * i;
+      const int db = m.dof_bodyid[i], end = m.body_subtree_end[db];
+      for (int b = db; b < end; b++) {
+        if (gc_on) gcomp += cd[0] * Wg[6 * b] + cd[1] * Wg[6 * b + 1] + cd[2] * Wg[6 * b + 2] + cd[3] * Wg[6 * b + 3] + cd[4] * Wg[6 * b + 4] + cd[5] * Wg[6 * b + 5];
+        if (fl_on) fluid += cd[0] * Wf[6 * b] + cd[1] * Wf[6 * b + 1] + cd[2] * Wf[6 * b + 2] + cd[3] * Wf[6 * b + 3] + cd[4] * Wf[6 * b + 4] + cd[5] * Wf[6 * b + 5];
+      }
+    }
+    WSYNC();
+  }
   for (int i = lane; i < nv; i += LPW) {
     float p = spring[i] + damper[i];
+    // passive.py:555-561: gravcomp unless the joint routes it to the actuators, then the fluid force
+    if (gc_on && !m.jnt_actgravcomp[m.dof_jntid[i]]) p += gcomp;
+    if (fl_on) p += fluid;
     qfrc_passive[i] = p;
     long gi = (long)wid * nv + i;
     d.qfrc_spring[gi] = spring[i];
     d.qfrc_damper[gi] = damper[i];
-    d.qfrc_gravcomp[gi] = 0.0f;
+    d.qfrc_gravcomp[gi] = gcomp;
+    d.qfrc_fluid[gi] = fluid;
     d.qfrc_passive[gi] = p;
+    if (TEN) spring[i] = gcomp;  // kept for the actuation stage of this launch (L.vec is free until the solver)
   }
   // rne (smooth.py:1112-1274, flg_acc = False): cacc[b] = cacc[parent] + sum cdof_dot qvel
   for (int b = lane; b < m.nbody; b += LPW) {
@@ -1737,8 +1790,9 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
   WSYNC();
 }
 
-// forward.py:616-927 (actuator force, qfrc_actuator)
-template <bool TEN>
+// forward.py:616-927 (actuator force, qfrc_actuator); VEL_LDS: the velocity stage ran in this launch and
+// left qfrc_gravcomp in L.vec (else it is read from the Data)
+template <bool TEN, bool VEL_LDS>
 __device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -1809,6 +1863,8 @@ __device__ __forceinline__ void fwd_actuation(const mjw_model_t& m, const mjw_da
       for (int k = 0; k < si[L.act_nnz + a]; k++)
         if (si[L.act_momdof + L.amax * a + k] == i) q += s[L.act_mom + L.amax * a + k] * s[L.act_force + a];
     int j = m.dof_jntid[i];
+    // forward.py:824-826: actuator-level gravity compensation
+    if (TEN && m.ngravcomp && m.jnt_actgravcomp[j]) q += VEL_LDS ? s[L.vec + i] : d.qfrc_gravcomp[(long)wid * nv + i];
     if (m.jnt_actfrclimited[j]) q = clampf(q, jnt_actfrcrange[2 * j], jnt_actfrcrange[2 * j + 1]);
     qfrc_act[i] = q;
     d.qfrc_actuator[(long)wid * nv + i] = q;
@@ -2355,11 +2411,11 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
     transmission<TEN>(m, d, L, w);
     PROF_MARK(PH_TRN);
   }
-  if (STAGES & ST_VEL) fwd_velocity<TEN>(m, d, L, w);
+  if (STAGES & ST_VEL) fwd_velocity<TEN, (STAGES & ST_POS) != 0>(m, d, L, w);
   if ((STAGES & ST_POS) && (STAGES & ST_VEL) && w.lane < 2 && !(m.opt_enableflags & ENBL_ENERGY))
     d.energy[(long)w.wid * 2 + w.lane] = 0.0f;
   PROF_MARK(PH_VEL);
-  if (STAGES & ST_ACT) fwd_actuation<TEN>(m, d, L, w);
+  if (STAGES & ST_ACT) fwd_actuation<TEN, (STAGES & ST_VEL) != 0>(m, d, L, w);
   PROF_MARK(PH_ACT);
   if (STAGES & ST_ACC) fwd_acceleration(m, d, L, w);
   PROF_MARK(PH_ACC);
@@ -2488,15 +2544,19 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
   }
 }
 
-// forward.py:899-927 (_qfrc_actuator, _qfrc_actuator_gravcomp_limits): qfrc_actuator = moment' force
-// from the Data's actuator_force and sparse moment rows, clamped by the joint actuator force range;
-// one wave per world, lanes over dofs.  The staged fwd_actuation runs it after the act_dyn / act_gain /
-// act_bias callbacks (forward.py:876-881), which may rewrite actuator_force.
+// forward.py:883-927 (_tendon_actuator_force_clamp, _qfrc_actuator, _qfrc_actuator_gravcomp_limits): the
+// tendon actuator force range applied to the Data's actuator_force (written back), then qfrc_actuator =
+// moment' force from the sparse moment rows, plus the actuator-level gravity compensation, clamped by the
+// joint actuator force range; one wave per world, lanes over dofs.  The staged fwd_actuation runs it after
+// the act_dyn / act_gain / act_bias callbacks (forward.py:876-881), which may rewrite actuator_force.  (The
+// stage launch before the callbacks applied the tendon range already; forces it left in range pass unchanged.)
 __global__ void __launch_bounds__(64) actuator_map_kernel(const mjw_model_t m, const mjw_data_t d) {
   const int wid = blockIdx.x, lane = threadIdx.x;
   if (wid >= d.nworld) return;
   const int nv = m.nv, nu = m.nu;
   const bool off = !nu || (m.opt_disableflags & DSBL_ACTUATION);
+  // each actuator drives one tendon, so a lane rescales only forces no other tendon's sum reads
+  if (!off && m.ntendon) tendon_actuator_clamp(m, d.actuator_force + (long)wid * nu, wid, lane);
   const float* jnt_actfrcrange = MR(jnt_actfrcrange);
   for (int i = lane; i < nv; i += 64) {
     float q = 0.0f;
@@ -2511,6 +2571,7 @@ __global__ void __launch_bounds__(64) actuator_map_kernel(const mjw_model_t m, c
         }
       }
       const int j = m.dof_jntid[i];
+      if (m.ngravcomp && m.jnt_actgravcomp[j]) q += d.qfrc_gravcomp[(long)wid * nv + i];
       if (m.jnt_actfrclimited[j]) q = clampf(q, jnt_actfrcrange[2 * j], jnt_actfrcrange[2 * j + 1]);
     }
     d.qfrc_actuator[(long)wid * nv + i] = q;
@@ -2601,7 +2662,7 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   // position-stage kernels without the tendon / muscle paths, and without the box narrowphase, for
   // models that have none (kernel id: K_FWD + 4 STAGES + 2 BOX + TEN)
   if constexpr ((STAGES & mjw::ST_POS) != 0) {
-    if (m->ntendon == 0 && m->nmuscle == 0) {
+    if (m->ntendon == 0 && m->nmuscle == 0 && m->ngravcomp == 0 && !m->has_fluid) {
       if (m->nxn_box == 0) {
         hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, false, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
         mjw::trace_launch(s, mjw::K_FWD + 4 * STAGES);

@@ -200,21 +200,34 @@ def _integrate(m: Model, d: Data):
 
 
 def step1(m: Model, d: Data):
-  """First half of `step` (forward.py:1022-1047): position and velocity stages with their sensors."""
+  """First half of `step` (forward.py:1022-1047): position and velocity stages with their sensors, the
+  potential / kinetic energy after each when ENERGY is enabled (else d.energy is cleared), then the
+  control callback."""
+  from .stages import energy_pos, energy_vel
+
   fwd_position(m, d)
   sensor_pos(m, d)
+  if _energy(m):
+    energy_pos(m, d)
+  else:
+    d.energy.zero_()
   fwd_velocity(m, d)
   sensor_vel(m, d)
+  if _energy(m):
+    energy_vel(m, d)
+  if not (m.opt.disableflags & DisableBit.ACTUATION) and m.callback.control is not None:
+    m.callback.control(m, d)
 
 
 def step2(m: Model, d: Data):
   """Second half of `step` after the user has set its inputs (forward.py:1050-1064): actuation,
-  acceleration, solver, acceleration sensors, integration."""
+  acceleration, solver, acceleration sensors, integration -- implicitfast for implicitfast models, Euler
+  otherwise (the reference's step2 integrates RK4 models with Euler, forward.py:1063)."""
   fwd_actuation(m, d)
   fwd_acceleration(m, d)
   solve(m, d)
   sensor_acc(m, d)
-  _integrate(m, d)
+  euler(m, d)  # mjw_euler dispatches on opt.integrator: implicitfast, else Euler (RK4 included)
 
 
 def _energy(m: Model) -> bool:

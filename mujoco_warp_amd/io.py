@@ -183,6 +183,8 @@ def put_model(mjm, device=None) -> types.Model:
     raise NotImplementedError("sparse / flex models: tendons are not supported by this build yet.")
   if ntendon and np.any(np.asarray(mjm.wrap_type) != 1):
     raise NotImplementedError("only fixed (joint) tendons are supported by this build yet.")
+  if (mjm.opt.viscosity > 0 or mjm.opt.density > 0) and mjm.opt.integrator in (types.IntegratorType.IMPLICITFAST, types.IntegratorType.IMPLICIT):
+    raise NotImplementedError("Implicit integrators and fluid model not implemented.")  # io.py:126-130
 
   nv = mjm.nv
   opt = types.Option()
@@ -215,6 +217,14 @@ def put_model(mjm, device=None) -> types.Model:
   m.nwrap, m.nJten = int(getattr(mjm, "nwrap", 0)), int(getattr(mjm, "nJten", 0))
   m.ten_maxnnz = int(np.max(mjm.ten_J_rownnz)) if m.ntendon else 0  # the reference's max_ten_J_rownnz (io.py:232)
   m.nmuscle = int(np.sum(_muscle_mask(mjm)))  # > 0 selects the forward kernel compiled with the muscle paths
+  # gravity compensation and fluid forces (passive.py:246-533; io.py:230, :2218-2219); either selects the
+  # forward kernel's extended instantiation, as tendons and muscles do
+  body_gravcomp = np.asarray(getattr(mjm, "body_gravcomp", np.zeros(mjm.nbody)), dtype=np.float64).reshape(-1, mjm.nbody)
+  m.ngravcomp = int((body_gravcomp > 0.0).any(axis=0).sum())
+  m.has_fluid = bool(np.any(np.asarray(o.wind) != 0) or o.density > 0 or o.viscosity > 0)
+  geom_fluid = np.asarray(getattr(mjm, "geom_fluid", np.zeros((mjm.ngeom, 12))), dtype=np.float64).reshape(mjm.ngeom, 12)
+  body_fluid_ellipsoid = np.zeros(mjm.nbody, dtype=np.int32)  # io.py:262-263
+  body_fluid_ellipsoid[np.asarray(mjm.geom_bodyid)[geom_fluid[:, 0] > 0]] = 1
   # the sparse path's dense Newton Hessian (nv x nv per world), zero-sized otherwise
   m.sp_nH = int(mjm.nv) if (is_sparse(mjm) or getattr(mjm, "nflex", 0) > 0) and mjm.opt.solver == types.SolverType.NEWTON else 0
   m.neq = int(getattr(mjm, "neq", 0))
@@ -324,6 +334,7 @@ def put_model(mjm, device=None) -> types.Model:
   m.nflexinc, m.nflexcg, m.nplane = len(inc_flat), len(cg), len(planes)
   derived_int = dict(
     tree_dofadr=tree_dofadr,
+    body_fluid_ellipsoid=body_fluid_ellipsoid,
     flex_cgeomadr=np.array(cg_adr, dtype=np.int32),
     flex_cgeom=np.array(cg, dtype=np.int32),
     plane_geom=planes.astype(np.int32),
@@ -337,7 +348,7 @@ def put_model(mjm, device=None) -> types.Model:
     jnt_limited_ball_adr=jnt_limited_ball,
   )
   for k_, v_ in derived_int.items():
-    if k_ in ("tree_dofadr", "flex_cgeomadr", "flex_cgeom", "plane_geom", "flexvert_incadr", "flexvert_inc"):
+    if k_ in ("tree_dofadr", "flex_cgeomadr", "flex_cgeom", "plane_geom", "flexvert_incadr", "flexvert_inc", "body_fluid_ellipsoid"):
       setattr(m, k_, _i32(v_, dev))
   m.body_subtree_end = _i32(subtree_end, dev)
   m.body_level = _i32(depth, dev)
@@ -453,7 +464,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     subtree_com=(nb, 3), cdof=(nv, 6), cinert=(nb, 10), crb=(nb, 10),
     qM=(m.nM,) if sp else (np_, np_), qLD=(m.nM,) if sp else (nv, nv),
     actuator_length=(nu,), actuator_moment=(m.nJmom,), actuator_velocity=(nu,), actuator_force=(nu,),
-    cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,),
+    cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,), qfrc_fluid=(nv,),
     qfrc_passive=(nv,), qfrc_actuator=(nv,), qfrc_smooth=(nv,), qacc_smooth=(nv,), qfrc_constraint=(nv,),
     cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 17,),
     efc_J=(m.njrow, njmax_pad) if sp else (njmax_pad, m.njrow), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
@@ -691,7 +702,7 @@ def get_data_into(result, mjm, d: types.Data, world_id: int = 0):
   for name in ("qpos", "qvel", "act", "ctrl", "qacc_warmstart", "qfrc_applied", "qacc", "act_dot", "xpos", "xquat", "xipos", "xanchor",
                "xaxis", "geom_xpos", "site_xpos", "cam_xpos", "light_xpos", "light_xdir", "subtree_com", "cdof", "cinert", "crb",
                "actuator_length", "actuator_velocity", "actuator_force", "cvel", "cdof_dot", "qfrc_bias", "qfrc_spring", "qfrc_damper",
-               "qfrc_gravcomp", "qfrc_passive", "qfrc_actuator", "qfrc_smooth", "qacc_smooth", "qfrc_constraint", "cacc", "cfrc_int",
+               "qfrc_gravcomp", "qfrc_fluid", "qfrc_passive", "qfrc_actuator", "qfrc_smooth", "qacc_smooth", "qfrc_constraint", "cacc", "cfrc_int",
                "cfrc_ext", "xfrc_applied", "mocap_pos", "mocap_quat", "energy", "sensordata"):
     if hasattr(result, name) or isinstance(result, object):
       val = getattr(d, name)[world_id].detach().cpu().numpy().astype(np.float64)

@@ -703,6 +703,7 @@ class _Compiler:
     m.body_pos = np.array([b.pos for b in bodies])
     m.body_quat = np.array([b.quat for b in bodies])
     m.body_gravcomp = np.array([b.gravcomp for b in bodies])
+    m.ngravcomp = int((m.body_gravcomp > 0.0).sum())  # bodies with gravity compensation (io.py:2218-2219)
 
     # mocap
     mocapid = -np.ones(nbody, dtype=np.int32)
@@ -1078,6 +1079,7 @@ class _Compiler:
     m.geom_rbound = np.array([r["rbound"] for r in rows])
     m.geom_aabb = np.array([r["aabb"] for r in rows]).reshape(ng, 6)
     m.geom_dataid = np.array([r["dataid"] for r in rows], dtype=np.int32)
+    m.geom_fluid = np.array([r["fluid"] for r in rows]).reshape(ng, NFLUID)
     self.geom_mesh_props = [(r["mesh_com"], r["mesh_I"]) for r in rows]
     m.geom_mass_ = np.array([r["mass"] for r in rows])
     m.geom_inertia_ = np.array([r["inertia"] for r in rows]).reshape(ng, 3)
@@ -1158,6 +1160,7 @@ class _Compiler:
       raise NotImplementedError(gtype)
     density = float(ga.get("density", _GEOM_DEFAULTS["density"]))
     mass = float(ga["mass"]) if "mass" in ga else density * vol
+    fluid = _geom_fluid(ga, gtype, size)
     if gtype == GeomType.MESH:
       inertia = np.zeros(3)
       # full inertia about the mesh COM in the geom frame (unit-density integrals scaled to mass)
@@ -1187,6 +1190,7 @@ class _Compiler:
       mass=mass if gtype != GeomType.PLANE else 0.0,
       inertia=inertia,
       dataid=dataid if gtype == GeomType.MESH else -1,
+      fluid=fluid,
       mesh_com=mesh_com if gtype == GeomType.MESH else None,
       mesh_I=mesh_I if gtype == GeomType.MESH else None,
     )
@@ -1819,6 +1823,52 @@ def _mesh_mass_props(v, f):
   I = np.trace(C) * np.eye(3) - C
   sign = 1.0 if vol > 0 else -1.0
   return abs(vol), com, sign * I
+
+
+NFLUID = 12  # mjNFLUID: (interaction coef, blunt / slender / angular drag, Kutta / Magnus lift, virtual mass x3, virtual inertia x3)
+
+
+def fluid_semiaxes(gtype, size):
+  """Semi-axes of the ellipsoid that stands in for a geom in the fluid model (passive.py:42-59)."""
+  if gtype == GeomType.SPHERE:
+    return np.array([size[0]] * 3)
+  if gtype == GeomType.CAPSULE:
+    return np.array([size[0], size[0], size[1] + size[0]])
+  if gtype == GeomType.CYLINDER:
+    return np.array([size[0], size[0], size[1]])
+  return np.asarray(size[:3], dtype=float)
+
+
+def added_mass_kappa(dx, dy, dz):
+  """kappa_x = dx dy dz * int_0^inf dl / ((dx^2 + l)^1.5 sqrt((dy^2 + l)(dz^2 + l))) of an ellipsoid (the
+  potential-flow added-mass integral MuJoCo's compiler evaluates for fluidshape="ellipsoid"), here in closed
+  form through Carlson's symmetric integral: (2/3) dx dy dz R_D(dy^2, dz^2, dx^2).  kx + ky + kz = 2."""
+  from scipy.special import elliprd
+
+  return 2.0 / 3.0 * dx * dy * dz * float(elliprd(dy * dy, dz * dz, dx * dx))
+
+
+def _geom_fluid(ga, gtype, size):
+  """geom_fluid row (types.py:961, read by passive.py:335-450): zero unless fluidshape="ellipsoid"; then
+  (1, fluidcoef[5], virtual mass[3], virtual inertia[3]) per unit fluid density.  Virtual mass
+  m_i = V k_i / (2 - k_i) and inertia I_x = V / 5 (dy^2 - dz^2)^2 |kz - ky| / |2 (dy^2 - dz^2) + (dy^2 + dz^2)(ky - kz)|
+  (cyclic), the ellipsoid's potential-flow added mass (MuJoCo's fluid model documentation)."""
+  out = np.zeros(NFLUID)
+  if ga.get("fluidshape", "none") != "ellipsoid":
+    return out
+  out[0] = 1.0
+  out[1:6] = _merge_vec([0.5, 0.25, 1.5, 1.0, 1.0], _floats(ga["fluidcoef"]) if "fluidcoef" in ga else [])
+  d = fluid_semiaxes(gtype, size)
+  k = [added_mass_kappa(d[i], d[(i + 1) % 3], d[(i + 2) % 3]) for i in range(3)]
+  vol = 4.0 / 3.0 * math.pi * d[0] * d[1] * d[2]
+  for i in range(3):
+    out[6 + i] = vol * k[i] / max(MJ_MINVAL, 2.0 - k[i])
+    j, l = (i + 1) % 3, (i + 2) % 3
+    dj2, dl2 = d[j] ** 2, d[l] ** 2
+    num = (dj2 - dl2) ** 2 * abs(k[l] - k[j])
+    den = abs(2.0 * (dj2 - dl2) + (dj2 + dl2) * (k[j] - k[l]))
+    out[9 + i] = vol / 5.0 * num / max(MJ_MINVAL, den)
+  return out
 
 
 def _geom_inertia(gtype, size, mass):

@@ -262,33 +262,36 @@ def energy_pos(m: Model, d: Data):
     xipos = d.xipos.reshape(nw, nb, 3)
     e -= (mass[:, 1:] * (xipos[:, 1:] * g[:, None, :]).sum(-1)).sum(dim=1)
   if not (m.opt.disableflags & DisableBit.SPRING):
-    stiff = m.jnt_stiffness.reshape(-1, m.njnt)[0].cpu().numpy()
+    # batched (*) stiffness, spring reference and tendon spring lengths are read per world at worldid % nb,
+    # as sensor.py's _energy_pos_* kernels do; a joint / tendon counts when any world's stiffness is non-zero
+    stiff = _per_world(m.jnt_stiffness, nw, m.njnt)
     jt = m.jnt_type.cpu().numpy()
     qa_all = m.jnt_qposadr.cpu().numpy()
-    qs = m.qpos_spring.reshape(-1, m.nq)[0]
+    qs = _per_world(m.qpos_spring, nw, m.nq)
     qpos = d.qpos.reshape(nw, m.nq)
-    for j in np.nonzero(stiff)[0]:
-      k, qa = float(stiff[j]), int(qa_all[j])
+    for j in np.nonzero((m.jnt_stiffness.reshape(-1, m.njnt) != 0).any(dim=0).cpu().numpy())[0]:
+      k, qa = stiff[:, j], int(qa_all[j])
       if jt[j] == JointType.FREE:
-        d0 = qpos[:, qa : qa + 3] - qs[qa : qa + 3]
+        d0 = qpos[:, qa : qa + 3] - qs[:, qa : qa + 3]
         q1 = torch.nn.functional.normalize(qpos[:, qa + 3 : qa + 7], dim=-1)
-        d1 = _quat_sub(q1, qs[qa + 3 : qa + 7].expand_as(q1))
+        d1 = _quat_sub(q1, qs[:, qa + 3 : qa + 7])
         e += 0.5 * k * ((d0 * d0).sum(-1) + (d1 * d1).sum(-1))
       elif jt[j] == JointType.BALL:
         q = torch.nn.functional.normalize(qpos[:, qa : qa + 4], dim=-1)
-        dq = _quat_sub(q, qs[qa : qa + 4].expand_as(q))
+        dq = _quat_sub(q, qs[:, qa : qa + 4])
         e += 0.5 * k * (dq * dq).sum(-1)
       else:
-        dq = qpos[:, qa] - qs[qa]
+        dq = qpos[:, qa] - qs[:, qa]
         e += 0.5 * k * dq * dq
-    for t in range(getattr(m, "ntendon", 0)):
-      k = float(m.tendon_stiffness.reshape(-1, m.ntendon)[0, t])
-      if k == 0.0:
-        continue
-      lo, hi = (float(x) for x in m.tendon_lengthspring.reshape(-1, m.ntendon, 2)[0, t])
-      length = d.ten_length.reshape(nw, m.ntendon)[:, t]
-      disp = torch.where(length > hi, hi - length, torch.where(length < lo, lo - length, torch.zeros_like(length)))
-      e += 0.5 * k * disp * disp
+    nten = getattr(m, "ntendon", 0)
+    if nten:
+      tstiff = _per_world(m.tendon_stiffness, nw, nten)
+      tls = _per_world(m.tendon_lengthspring, nw, nten, 2)
+      for t in np.nonzero((m.tendon_stiffness.reshape(-1, nten) != 0).any(dim=0).cpu().numpy())[0]:
+        k, lo, hi = tstiff[:, t], tls[:, t, 0], tls[:, t, 1]
+        length = d.ten_length.reshape(nw, nten)[:, t]
+        disp = torch.where(length > hi, hi - length, torch.where(length < lo, lo - length, torch.zeros_like(length)))
+        e += 0.5 * k * disp * disp
   d.energy.reshape(nw, 2)[:, 0] = e
 
 

@@ -911,12 +911,180 @@ static void rne(const orc_model* m, orc_data* d) {
   }
 }
 
-/* passive.py:70-179 (+ _qfrc_passive :535-563) */
+/* support.py:174-216 apply_ft (flg_add = False): qfrc = sum over bodies of J(xipos_b)^T (f_b, t_b);
+   ft: (nbody, 6) = (force, torque) per body */
+static void apply_ft(const orc_model* m, const orc_data* d, const real* ft, real* qfrc) {
+  for (int i = 0; i < m->nv; i++) {
+    const real* cd = d->cdof + 6 * i;
+    const int db = m->dof_bodyid[i];
+    real acc = 0;
+    for (int b = db; b < m->nbody; b++) {
+      const real* f = ft + 6 * b;
+      if (f[0] == 0 && f[1] == 0 && f[2] == 0 && f[3] == 0 && f[4] == 0 && f[5] == 0) continue;
+      int p = b;
+      while (p != 0 && p != db) p = m->body_parentid[p];
+      if (p == 0) continue;
+      real off[3], c[3];
+      for (int k = 0; k < 3; k++) off[k] = d->xipos[3 * b + k] - d->subtree_com[3 * m->body_rootid[b] + k];
+      cross3(c, cd, off);
+      acc += cd[3] * f[0] + cd[4] * f[1] + cd[5] * f[2] + cd[0] * f[3] + cd[1] * f[4] + cd[2] * f[5] + dot3(c, f);
+    }
+    qfrc[i] = acc;
+  }
+}
+
+/* passive.py:246-272 _gravity_force: f_b = -gravity * mass_b * gravcomp_b at xipos_b */
+static void gravcomp(const orc_model* m, orc_data* d, real* ft) {
+  memset(ft, 0, 6 * m->nbody * sizeof(real));
+  for (int b = 1; b < m->nbody; b++) {
+    const real gc = m->body_gravcomp[b];
+    if (gc == 0) continue;
+    for (int k = 0; k < 3; k++) ft[6 * b + k] = -m->opt_gravity[k] * m->body_mass[b] * gc;
+  }
+  apply_ft(m, d, ft, d->qfrc_gravcomp);
+}
+
+/* R^T v and R v for a row-major R (world from local) */
+static void rt_vec(real* r, const real* R, const real* v) {
+  for (int i = 0; i < 3; i++) r[i] = R[i] * v[0] + R[3 + i] * v[1] + R[6 + i] * v[2];
+}
+static void r_vec(real* r, const real* R, const real* v) {
+  for (int i = 0; i < 3; i++) r[i] = R[3 * i] * v[0] + R[3 * i + 1] * v[1] + R[3 * i + 2] * v[2];
+}
+static real pow4r(real x) { return x * x * x * x; }
+
+/* passive.py:42-59 */
+static void fluid_semiaxes(int type, const real* size, real* s) {
+  if (type == GEOM_SPHERE) { s[0] = s[1] = s[2] = size[0]; }
+  else if (type == GEOM_CAPSULE) { s[0] = s[1] = size[0]; s[2] = size[1] + size[0]; }
+  else if (type == GEOM_CYLINDER) { s[0] = s[1] = size[0]; s[2] = size[1]; }
+  else { s[0] = size[0]; s[1] = size[1]; s[2] = size[2]; }
+}
+
+/* passive.py:276-500 _fluid_force (ellipsoid model per geom with geom_fluid[0] > 0, else the body's
+   equivalent inertia box), then support.apply_ft into qfrc_fluid (passive.py:503-532) */
+static void fluid(const orc_model* m, orc_data* d, real* ft) {
+  const real PI = 3.14159265358979323846;
+  const real rho = m->opt_density, mu = m->opt_viscosity;
+  const real* wind = m->opt_wind;
+  memset(ft, 0, 6 * m->nbody * sizeof(real));
+  for (int b = 1; b < m->nbody; b++) {
+    const real mass = m->body_mass[b];
+    if (mass < MINVAL) continue;
+    const real* xipos = d->xipos + 3 * b;
+    const real* R = d->ximat + 9 * b;
+    const real* ang = d->cvel + 6 * b;
+    const real* root = d->subtree_com + 3 * m->body_rootid[b];
+    real off[3] = {xipos[0] - root[0], xipos[1] - root[1], xipos[2] - root[2]}, c[3], lin_com[3];
+    cross3(c, off, ang);
+    for (int k = 0; k < 3; k++) lin_com[k] = d->cvel[6 * b + 3 + k] - c[k];
+    real F[3] = {0, 0, 0}, T[3] = {0, 0, 0};
+    if (m->body_fluid_ellipsoid[b]) {
+      for (int g = m->body_geomadr[b]; g < m->body_geomadr[b] + m->body_geomnum[b]; g++) {
+        const real* fl = m->geom_fluid + 12 * g;
+        if (fl[0] <= 0) continue;
+        real s[3];
+        fluid_semiaxes(m->geom_type[g], m->geom_size + 3 * g, s);
+        const real* G = d->geom_xmat + 9 * g;
+        real dp[3], lp[3], w[3], la[3], ll[3];
+        for (int k = 0; k < 3; k++) dp[k] = d->geom_xpos[3 * g + k] - xipos[k];
+        cross3(c, ang, dp);
+        for (int k = 0; k < 3; k++) lp[k] = lin_com[k] + c[k];
+        rt_vec(la, G, ang);
+        rt_vec(ll, G, lp);
+        rt_vec(w, G, wind);
+        for (int k = 0; k < 3; k++) ll[k] -= w[k];
+        real tq[3] = {0, 0, 0}, fo[3] = {0, 0, 0};
+        if (rho > 0) {  /* added mass */
+          real vl[3], va[3], a[3];
+          for (int k = 0; k < 3; k++) { vl[k] = rho * fl[6 + k] * ll[k]; va[k] = rho * fl[9 + k] * la[k]; }
+          cross3(a, vl, la);
+          for (int k = 0; k < 3; k++) fo[k] += a[k];
+          cross3(a, vl, ll);
+          for (int k = 0; k < 3; k++) tq[k] += a[k];
+          cross3(a, va, la);
+          for (int k = 0; k < 3; k++) tq[k] += a[k];
+        }
+        const real vol = 4.0 / 3.0 * PI * s[0] * s[1] * s[2];
+        const real dmax = maxr(maxr(s[0], s[1]), s[2]), dmin = minr(minr(s[0], s[1]), s[2]);
+        const real dmid = s[0] + s[1] + s[2] - dmax - dmin, Amax = PI * dmax * dmid;
+        const real speed = sqrt(dot3(ll, ll));
+        real magnus[3];
+        cross3(magnus, la, ll);
+        for (int k = 0; k < 3; k++) magnus[k] *= fl[5] * rho * vol;
+        const real s12 = s[1] * s[2], s20 = s[2] * s[0], s01 = s[0] * s[1];
+        const real den = pow4r(s12) * ll[0] * ll[0] + pow4r(s20) * ll[1] * ll[1] + pow4r(s01) * ll[2] * ll[2];
+        const real num = s12 * ll[0] * s12 * ll[0] + s20 * ll[1] * s20 * ll[1] + s01 * ll[2] * s01 * ll[2];
+        real Aproj = 0, cosa = 0;
+        if (num > MINVAL && den > MINVAL) {
+          Aproj = PI * sqrt(den / maxr(MINVAL, num));
+          if (speed > MINVAL) cosa = num / maxr(MINVAL, speed * den);
+        }
+        const real nrm[3] = {s12 * s12 * ll[0], s20 * s20 * ll[1], s01 * s01 * ll[2]};
+        real kutta[3] = {0, 0, 0};
+        if (rho > 0 && fl[4] != 0 && speed > MINVAL) {
+          real circ[3];
+          cross3(circ, nrm, ll);
+          for (int k = 0; k < 3; k++) circ[k] *= fl[4] * rho * cosa * Aproj;
+          cross3(kutta, circ, ll);
+        }
+        const real D = 2.0 / 3.0 * (s[0] + s[1] + s[2]);
+        const real Imax = 8.0 / 15.0 * PI * dmid * pow4r(dmax);
+        real mv[3];
+        for (int k = 0; k < 3; k++) {
+          const real II = 8.0 / 15.0 * PI * s[k] * pow4r(maxr(s[(k + 1) % 3], s[(k + 2) % 3]));
+          mv[k] = la[k] * (fl[3] * II + fl[2] * (Imax - II));
+        }
+        const real dlin = mu * 3.0 * PI * D + rho * speed * (Aproj * fl[1] + fl[2] * (Amax - Aproj));
+        const real dang = mu * PI * D * D * D + rho * sqrt(dot3(mv, mv));
+        for (int k = 0; k < 3; k++) {
+          tq[k] = (tq[k] - dang * la[k]) * fl[0];
+          fo[k] = (fo[k] + magnus[k] + kutta[k] - dlin * ll[k]) * fl[0];
+        }
+        real wt[3], wf[3];
+        r_vec(wt, G, tq);
+        r_vec(wf, G, fo);
+        for (int k = 0; k < 3; k++) { T[k] += wt[k]; F[k] += wf[k]; }
+      }
+    } else {
+      real la[3], ll[3], w[3];
+      rt_vec(la, R, ang);
+      rt_vec(ll, R, lin_com);
+      rt_vec(w, R, wind);
+      for (int k = 0; k < 3; k++) ll[k] -= w[k];
+      real tq[3] = {0, 0, 0}, fo[3] = {0, 0, 0};
+      if (mu > 0 || rho > 0) {
+        const real* I = m->body_inertia + 3 * b;
+        const real box[3] = {sqrt(maxr(MINVAL, I[1] + I[2] - I[0]) * 6 / mass), sqrt(maxr(MINVAL, I[0] + I[2] - I[1]) * 6 / mass),
+                             sqrt(maxr(MINVAL, I[0] + I[1] - I[2]) * 6 / mass)};
+        if (mu > 0) {
+          const real diam = (box[0] + box[1] + box[2]) / 3;
+          for (int k = 0; k < 3; k++) { tq[k] = -la[k] * diam * diam * diam * PI * mu; fo[k] = -3 * ll[k] * diam * PI * mu; }
+        }
+        if (rho > 0) {
+          for (int k = 0; k < 3; k++) {
+            const int i1 = (k + 1) % 3, i2 = (k + 2) % 3;
+            fo[k] -= 0.5 * rho * box[i1] * box[i2] * fabs(ll[k]) * ll[k];
+            tq[k] -= box[k] * (pow4r(box[i1]) + pow4r(box[i2])) * fabs(la[k]) * la[k] * rho / 64;
+          }
+        }
+      }
+      r_vec(T, R, tq);
+      r_vec(F, R, fo);
+    }
+    for (int k = 0; k < 3; k++) { ft[6 * b + k] = F[k]; ft[6 * b + 3 + k] = T[k]; }
+  }
+  apply_ft(m, d, ft, d->qfrc_fluid);
+}
+
+/* passive.py:728-872 (spring / damper :70-179, tendons :183-252, flex, gravcomp, fluid, _qfrc_passive :535-563) */
 static void passive(const orc_model* m, orc_data* d) {
   int nv = m->nv;
   int dsbl_spring = m->opt_disableflags & DSBL_SPRING, dsbl_damper = m->opt_disableflags & DSBL_DAMPER;
   memset(d->qfrc_spring, 0, nv * sizeof(real));
   memset(d->qfrc_damper, 0, nv * sizeof(real));
+  memset(d->qfrc_gravcomp, 0, nv * sizeof(real));
+  memset(d->qfrc_fluid, 0, nv * sizeof(real));
   if (dsbl_spring && dsbl_damper) { memset(d->qfrc_passive, 0, nv * sizeof(real)); return; }
   for (int j = 0; j < m->njnt; j++) {
     int da = m->jnt_dofadr[j], qa = m->jnt_qposadr[j], jt = m->jnt_type[j];
@@ -961,7 +1129,18 @@ static void passive(const orc_model* m, orc_data* d) {
     }
   }
   if (!dsbl_spring) flex_passive(m, d);
-  for (int i = 0; i < nv; i++) d->qfrc_passive[i] = d->qfrc_spring[i] + d->qfrc_damper[i];
+  const int gc = m->ngravcomp && !(m->opt_disableflags & DSBL_GRAVITY);
+  if (gc || m->has_fluid) {
+    real* ft = (real*)malloc(6 * m->nbody * sizeof(real));
+    if (gc) gravcomp(m, d, ft);
+    if (m->has_fluid) fluid(m, d, ft);
+    free(ft);
+  }
+  for (int i = 0; i < nv; i++) {
+    d->qfrc_passive[i] = d->qfrc_spring[i] + d->qfrc_damper[i];
+    if (gc && !m->jnt_actgravcomp[m->dof_jntid[i]]) d->qfrc_passive[i] += d->qfrc_gravcomp[i];
+    if (m->has_fluid) d->qfrc_passive[i] += d->qfrc_fluid[i];
+  }
 }
 
 /* =============================================================================================
@@ -2458,6 +2637,7 @@ static void fwd_actuation(const orc_model* m, orc_data* d) {
     for (int i = 0; i < nv; i++) d->qfrc_actuator[i] += d->actuator_moment[(size_t)a * nv + i] * d->actuator_force[a];
   for (int i = 0; i < nv; i++) {
     int j = m->dof_jntid[i];
+    if (m->ngravcomp && m->jnt_actgravcomp[j]) d->qfrc_actuator[i] += d->qfrc_gravcomp[i];  /* forward.py:824-826 */
     if (m->jnt_actfrclimited[j]) d->qfrc_actuator[i] = clampr(d->qfrc_actuator[i], m->jnt_actfrcrange[2 * j], m->jnt_actfrcrange[2 * j + 1]);
   }
 }

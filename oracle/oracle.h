@@ -30,20 +30,20 @@ typedef ORC_REAL real;
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)             \
   X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
   X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)   \
-  X(ntendon) X(nwrap) X(nJten) X(npair)
+  X(ntendon) X(nwrap) X(nJten) X(npair) X(ngravcomp) X(has_fluid)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
   X(opt_timestep) X(opt_tolerance) X(opt_ls_tolerance) X(opt_impratio_invsqrt) X(stat_meaninertia)         \
-  X(opt_ccd_tolerance)
+  X(opt_ccd_tolerance) X(opt_density) X(opt_viscosity)
 
 /* ---- model: real arrays (name, element count) ---- */
 #define ORC_MODEL_REAL_ARRAYS(X)                                                                   \
-  X(opt_gravity, 3) X(opt_magnetic, 3) X(sensor_cutoff, nsensor)                                   \
+  X(opt_gravity, 3) X(opt_magnetic, 3) X(opt_wind, 3) X(sensor_cutoff, nsensor)                    \
   X(qpos0, nq) X(qpos_spring, nq)                                                                  \
   X(body_pos, nbody * 3) X(body_quat, nbody * 4) X(body_ipos, nbody * 3) X(body_iquat, nbody * 4) \
   X(body_mass, nbody) X(body_subtreemass, nbody) X(body_inertia, nbody * 3)                       \
-  X(body_invweight0, nbody * 2)                                                                    \
+  X(body_invweight0, nbody * 2) X(body_gravcomp, nbody) X(geom_fluid, ngeom * 12)                  \
   X(jnt_solref, njnt * 2) X(jnt_solimp, njnt * 5) X(jnt_pos, njnt * 3) X(jnt_axis, njnt * 3)      \
   X(jnt_stiffness, njnt) X(jnt_range, njnt * 2) X(jnt_actfrcrange, njnt * 2) X(jnt_margin, njnt)  \
   X(dof_solref, nv * 2) X(dof_solimp, nv * 5) X(dof_frictionloss, nv) X(dof_armature, nv)         \
@@ -76,7 +76,8 @@ typedef ORC_REAL real;
   X(body_parentid, nbody) X(body_rootid, nbody) X(body_weldid, nbody) X(body_mocapid, nbody)      \
   X(body_jntnum, nbody) X(body_jntadr, nbody) X(body_dofnum, nbody) X(body_dofadr, nbody)         \
   X(jnt_type, njnt) X(jnt_qposadr, njnt) X(jnt_dofadr, njnt) X(jnt_bodyid, njnt)                  \
-  X(jnt_limited, njnt) X(jnt_actfrclimited, njnt)                                                  \
+  X(jnt_limited, njnt) X(jnt_actfrclimited, njnt) X(jnt_actgravcomp, njnt)                         \
+  X(body_geomadr, nbody) X(body_geomnum, nbody) X(body_fluid_ellipsoid, nbody)                    \
   X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \
   X(geom_type, ngeom) X(geom_condim, ngeom) X(geom_bodyid, ngeom) X(geom_priority, ngeom)         \
   X(site_bodyid, nsite)                                                                            \
@@ -114,6 +115,7 @@ typedef ORC_REAL real;
   X(qM, nv * nv) X(qLD, nv * nv)                                                                   \
   X(actuator_length, nu) X(actuator_moment, nu * nv) X(actuator_velocity, nu) X(actuator_force, nu) \
   X(cvel, nbody * 6) X(cdof_dot, nv * 6) X(qfrc_bias, nv) X(qfrc_spring, nv) X(qfrc_damper, nv)   \
+  X(qfrc_gravcomp, nv) X(qfrc_fluid, nv)                                                           \
   X(qfrc_passive, nv) X(qfrc_actuator, nv) X(qfrc_smooth, nv) X(qacc_smooth, nv)                  \
   X(qfrc_constraint, nv) X(cacc, nbody * 6) X(cfrc_int, nbody * 6) X(cfrc_ext, nbody * 6)         \
   X(sensordata, nsensordata)                                                                       \

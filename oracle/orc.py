@@ -139,12 +139,20 @@ class OracleModel:
       nmesh=getattr(mjm, "nmesh", 0), nmeshvert=getattr(mjm, "nmeshvert", 0),
       ntendon=getattr(mjm, "ntendon", 0), nwrap=getattr(mjm, "nwrap", 0), nJten=getattr(mjm, "nJten", 0),
       npair=getattr(mjm, "npair", 0),
+      # passive.py:829-851: gravity compensation / fluid switches (io.py:230, :2218-2219)
+      ngravcomp=int((np.asarray(getattr(mjm, "body_gravcomp", np.zeros(mjm.nbody))) > 0).sum()),
+      has_fluid=int(bool(np.any(np.asarray(o.wind) != 0) or o.density > 0 or o.viscosity > 0)),
+      opt_density=o.density, opt_viscosity=o.viscosity,
     )
     if overrides:
       vals.update(overrides)
     self.sizes = {k: int(v) for k, v in vals.items() if k in MODEL_INT_SCALARS}
+    geom_fluid = np.asarray(getattr(mjm, "geom_fluid", np.zeros((mjm.ngeom, 12))), dtype=np.float64).reshape(mjm.ngeom, 12)
+    fluid_ellipsoid = np.zeros(mjm.nbody, dtype=np.int32)  # io.py:262-263
+    fluid_ellipsoid[np.asarray(mjm.geom_bodyid)[geom_fluid[:, 0] > 0]] = 1
     arrays = dict(
-      opt_gravity=o.gravity, opt_magnetic=o.magnetic, nxn_geom_pair=pairs, nxn_pairid=pairid,
+      opt_gravity=o.gravity, opt_magnetic=o.magnetic, opt_wind=o.wind, nxn_geom_pair=pairs, nxn_pairid=pairid,
+      body_gravcomp=getattr(mjm, "body_gravcomp", np.zeros(mjm.nbody)), geom_fluid=geom_fluid, body_fluid_ellipsoid=fluid_ellipsoid,
       cam_mat0=getattr(mjm, "cam_mat0", np.zeros((mjm.ncam, 9))),
     )
     self._keep = []
@@ -190,8 +198,12 @@ class OracleData:
     self.struct = s
     m = om.mjm
     self.arrays["qpos"][:] = m.qpos0
-    if m.nmocap:
+    if m.nmocap:  # make_data (io.py:859-1013): mocap poses start at the mocap bodies' body_pos / body_quat
       self.arrays["mocap_quat"][:] = np.tile([1.0, 0, 0, 0], m.nmocap)
+      for b in np.nonzero(np.asarray(m.body_mocapid) >= 0)[0]:
+        k = int(m.body_mocapid[b])
+        self.arrays["mocap_pos"][:, 3 * k:3 * k + 3] = m.body_pos[b]
+        self.arrays["mocap_quat"][:, 4 * k:4 * k + 4] = m.body_quat[b]
     if m.neq:
       self.arrays["eq_active"][:] = np.asarray(m.eq_active0, dtype=np.int32)
 

@@ -70,12 +70,14 @@ def test_gpu_bench_two_ranks_weak_equals_single(tmp_path, model, per_rank):
 
 @pytest.mark.gpu
 def test_gpu_bench_two_ranks_strong_and_graph(tmp_path):
-  common = ["--steps", "5", "--warmup", "2", "--cpu-baseline", "0", "--nworld", "301"]
+  common = ["--steps", "5", "--warmup", "2", "--cpu-baseline", "0", "--nworld", "301", "--trace-steps", "2"]
   strong = _run(["--gpus", "2", "--scaling", "strong", "--graph", "0", "--dump-qpos", str(tmp_path / "s")] + common)
   assert strong["scaling"] == "strong" and strong["config"]["nworld_total"] == 301
-  # graph replay (eager steps with events every 2nd step) over two stream shards of one rank
-  graph = _run(["--gpus", "1", "--graph", "1", "--event-every", "2", "--streams", "2", "--dump-qpos", str(tmp_path / "g")] + common)
-  assert graph["config"]["graph"] is True and graph["config"]["streams"] == 2 and graph["config"]["timed_kernel_launches"] == 3
+  # graph replay over two stream shards of one rank: the timed region is replays only, the kernel times
+  # come from the 2-step eager trace pass after it (same number of steps as the strong run's)
+  graph = _run(["--gpus", "1", "--graph", "1", "--streams", "2", "--dump-qpos", str(tmp_path / "g")] + common)
+  assert graph["config"]["graph"] is True and graph["config"]["streams"] == 2
+  assert graph["config"]["timed_region"] == "graph replays only" and graph["config"]["trace_steps"] == 2
   qg = np.load(tmp_path / "g" / "qpos_rank0.npz")["qpos"]
   got = [np.load(tmp_path / "s" / f"qpos_rank{r}.npz") for r in range(2)]
   assert [int(z["offset"]) for z in got] == [0, 151]
@@ -100,3 +102,24 @@ def test_pmc_traffic_is_bound_to_the_kernel_sources(tmp_path):
   traffic, why = bench.pmc_traffic(str(f), "humanoid", 8192, "CG")
   assert traffic is None and "predates" in why
   assert bench.pmc_traffic(str(tmp_path / "missing.json"), "humanoid", 8192, "CG")[0] is None
+
+
+def test_pmc_traffic_ratio_uses_the_pmc_window(tmp_path):
+  """traffic_over_alg divides the PMC bytes by the algorithmic bytes at the counted window's own nefc / ncon
+  (tools/pmc_traffic.py records them from the PMC passes' bench lines), not at the trace pass's."""
+  sys.path.insert(0, ROOT)
+  import bench
+  from mujoco_warp_amd import build
+
+  k = "mjw::mjw_kernel<79, false, false>"
+  pmc = {"nworld": 8, "solver": "CG", "model": "humanoid", "csrc_sha": build.sources_hash(),
+         "window": {"fetch": {"nefc_mean": 10.0, "ncon_mean": 2.0}},
+         "kernels": {k: {"hbm_bytes_per_launch": 8000.0, "hbm_bytes_per_step": 8000.0, "launches_per_step": 1.0}}}
+  f = tmp_path / "pmc_humanoid_r99.json"
+  f.write_text(json.dumps(pmc))
+  traffic, src = bench.pmc_traffic(str(f), "humanoid", 8, "CG")
+  tab = {k: {"ms_per_step": 1.0, "launches_per_step": 1.0, "group": "forward"}}
+  alg_at = lambda ne, nc: {"forward": 100.0 * ne + nc}
+  rec = bench.roofline_record(tab, alg_at(30.0, 5.0), 8, traffic, src, alg_at)
+  assert rec["groups"]["forward"]["traffic_over_alg"] == 8000.0 / (8 * 1002.0)
+  assert rec["groups"]["forward"]["alg_bytes_per_env_step"] == 3005.0

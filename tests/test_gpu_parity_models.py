@@ -2,7 +2,10 @@
 configs[2..4]): franka (scene.xml, implicitfast; 16 worlds of which two bury the hand in the floor, 73
 rows, so the generic LDS-solver kernel runs them, and `franka_dense`, the other 14 through the
 register-resident dense kernel), apollo (scene_flat.xml, Newton, dense
-path), cloth and aloha_cloth (flex, sparse path).  The measurements are tests/parity_models.py's
+path), cloth and aloha_cloth (flex, sparse path); and the reference's passive-force test models:
+test_data/pendula.xml (gravcomp bodies, an actuatorgravcomp joint; with and without gravity), the
+gravcomp model of passive_test.py:160-205 on the dense and the sparse path, and two fluid models
+(inertia-box and ellipsoid, wind on).  The measurements are tests/parity_models.py's
 report (profiles/r03_parity_models.json holds one); the bars, per quantity:
 
   * smooth-stage outputs (kinematics, com, cinert / crb / qM, cdof, camera and light frames, actuator
@@ -46,7 +49,13 @@ def _report(reports, name):
   return reports[name]
 
 
-@pytest.mark.parametrize("name", ["franka", "franka_dense", "apollo", "cloth", "aloha"])
+ALL = ["franka", "franka_dense", "apollo", "cloth", "aloha", "pendula", "pendula_nograv", "gravcomp", "gravcomp_sparse", "fluid_box",
+       "fluid_ellipsoid"]
+# models with constraint rows (pendula: joint / tendon limits; the gravcomp and fluid models have none)
+ROWS = ["franka", "franka_dense", "apollo", "cloth", "aloha", "pendula", "pendula_nograv"]
+
+
+@pytest.mark.parametrize("name", ALL)
 def test_smooth_stages(reports, name):
   r = _report(reports, name)
   bad = []
@@ -66,7 +75,7 @@ def test_smooth_stages(reports, name):
   assert r["qacc_smooth_backward"] <= SMOOTH_TOL
 
 
-@pytest.mark.parametrize("name", ["franka", "franka_dense", "apollo", "cloth", "aloha"])
+@pytest.mark.parametrize("name", ROWS)
 def test_constraint_rows(reports, name):
   r = _report(reports, name)
   assert r["rows_counts_equal"] and r["rows_types_equal"]
@@ -77,7 +86,7 @@ def test_constraint_rows(reports, name):
   assert rows["D"]["norm"] <= 3e-4 and rows["aref"]["norm"] <= 3e-4, rows
 
 
-@pytest.mark.parametrize("name", ["franka", "franka_dense", "apollo", "cloth", "aloha"])
+@pytest.mark.parametrize("name", ALL)
 def test_solve_and_step(reports, name):
   r = _report(reports, name)
   assert r["solve_cost_excess"] <= 1e-5, r["solve_cost_excess"]

@@ -16,8 +16,8 @@ import pytest
 from tests.common import HUMANOID, np_, random_states
 
 # out of scope: rendering / rays, inverse dynamics, islands, BVH / SAP / SDF collision
-# front ends, the set_const family (this build derives model constants in put_model), and the smooth
-# velocity derivative, which runs inside the integrator kernel
+# front ends, MuJoCo's simulation-based muscle length range, and the smooth velocity derivative, which
+# runs inside the integrator kernel (the set_const family is implemented, stages.py)
 OUT_OF_SCOPE = {
   "RenderContext", "create_render_context", "get_depth", "get_rgb", "get_segmentation", "render", "ray", "rays", "refit_bvh",
   "inverse", "island", "sap_broadphase", "nxn_broadphase", "primitive_narrowphase", "sdf_narrowphase",
@@ -240,6 +240,45 @@ def test_set_const_fixed_subtreemass():
   mjw.set_const_fixed(m, d)
   assert m.body_subtreemass.shape == (3, mjm.nbody)
   np.testing.assert_allclose(m.body_subtreemass.numpy()[1], 2.0 * mjm.body_subtreemass, rtol=1e-6)
+
+
+def test_energy_pos_reads_batched_springs_per_world():
+  """energy_pos (sensor.py:2854-2890) on CPU tensors with per-world (batched *) joint stiffness, qpos_spring
+  and tendon spring fields: each world's potential is its own 0.5 k dif^2, including a world whose only
+  non-zero stiffness is on a joint that world 0 leaves at zero."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+
+  mjm = mjcf.load_model_from_string("""<mujoco><option gravity="0 0 0"/><worldbody>
+  <body><joint name="a" type="hinge"/><geom size=".1"/><body pos="1 0 0"><joint name="b" type="slide"/><geom size=".1"/></body></body>
+  <body pos="0 2 0"><joint type="ball"/><geom size=".1"/></body></worldbody>
+  <tendon><fixed stiffness="1" springlength="0 .1"><joint joint="a" coef="1"/><joint joint="b" coef="2"/></fixed></tendon></mujoco>""")
+  m = mjw.put_model(mjm, device="cpu")
+  d = mjw.make_data(mjm, nworld=3, device="cpu", m=m)
+  rng = np.random.default_rng(0)
+  d.qpos[:, :2] = torch.as_tensor(rng.normal(0, 0.5, (3, 2)), dtype=torch.float32)
+  d.qpos[:, 2:] = torch.nn.functional.normalize(torch.as_tensor(rng.normal(size=(3, 4)), dtype=torch.float32), dim=-1)
+  m.jnt_stiffness = torch.tensor([[2.0, 0.0, 0.0], [0.0, 3.0, 0.0], [1.0, 1.0, 4.0]])
+  m.qpos_spring = m.qpos_spring.repeat(3, 1)
+  m.qpos_spring[1, 1] = 0.25
+  m.tendon_stiffness = torch.tensor([[1.0], [0.0], [5.0]])
+  m.tendon_lengthspring = torch.tensor([[[0.0, 0.1]], [[0.0, 0.1]], [[-1.0, -0.5]]])
+  L = (d.qpos[:, 0] + 2 * d.qpos[:, 1]).double()
+  d.ten_length[:] = L.float().reshape(3, 1)
+  mjw.energy_pos(m, d)
+  q = d.qpos.double()
+  from mujoco_warp_amd.stages import _quat_sub
+
+  ball = _quat_sub(q[:, 2:6], torch.tensor([[1.0, 0, 0, 0]], dtype=torch.float64).expand(3, 4))
+  k, qs = m.jnt_stiffness.double(), m.qpos_spring.double()
+  want = 0.5 * (k[:, 0] * (q[:, 0] - qs[:, 0]) ** 2 + k[:, 1] * (q[:, 1] - qs[:, 1]) ** 2 + k[:, 2] * (ball * ball).sum(-1))
+  lo, hi = m.tendon_lengthspring[:, 0, 0].double(), m.tendon_lengthspring[:, 0, 1].double()
+  disp = torch.where(L > hi, hi - L, torch.where(L < lo, lo - L, torch.zeros_like(L)))
+  want += 0.5 * m.tendon_stiffness[:, 0].double() * disp * disp
+  np.testing.assert_allclose(d.energy[:, 0].numpy(), want.numpy(), rtol=1e-5)
+  assert float(d.energy[1, 0]) > 0  # world 1: stiffness only on the slide, with its own spring reference
 
 
 @pytest.mark.gpu

@@ -69,6 +69,19 @@ def tail(vals, steps, tail_steps):
   return {k: v[len(v) - max(1, round(len(v) * tail_steps / steps)):] for k, v in vals.items()}
 
 
+def bench_window(d):
+  """nefc / ncon means of the bench line a PMC pass ran (its trace pass = the tail window the counters are
+  averaged over, profile_model.sh), from the JSON line in <pass dir>.log."""
+  try:
+    with open(d.rstrip("/") + ".log") as fh:
+      lines = [ln for ln in fh if ln.startswith("{")]
+    rec = json.loads(lines[-1])
+    c = rec["config"]
+    return {"nefc_mean": c["nefc_mean"], "ncon_mean": c["ncon_mean"], "trace_steps": c.get("trace_steps")}
+  except (OSError, IndexError, KeyError, ValueError):
+    return None
+
+
 def summarise(stats_dir, fetch_dir, write_dir, nworld, solver, model, csrc_sha, tail_steps=0):
   fetch = counter(fetch_dir, "FETCH_SIZE")
   write = counter(write_dir, "WRITE_SIZE")
@@ -80,7 +93,10 @@ def summarise(stats_dir, fetch_dir, write_dir, nworld, solver, model, csrc_sha, 
   res = {"nworld": nworld, "solver": solver, "model": model, "csrc_sha": csrc_sha,
          "unit_note": "FETCH/WRITE_SIZE in KB per dispatch; hbm bytes = (2*FETCH + WRITE)*1024; per step = "
                       "sum over kernels of (dispatches / steps) * bytes per launch, steps = dispatches of " + STEP_KERNEL,
-         "steps": [steps_f, steps_w], "tail_steps": tail_steps, "kernels": {}}
+         "steps": [steps_f, steps_w], "tail_steps": tail_steps,
+         # the counted window's constraint / contact sizes (the FETCH and WRITE passes run the same
+         # deterministic steps): bench.py prices the window's algorithmic bytes with them
+         "window": {"fetch": bench_window(fetch_dir), "write": bench_window(write_dir)}, "kernels": {}}
   total = 0.0
   for k in sorted(set(fetch) | set(write)):
     f, w = fetch.get(k, []), write.get(k, [])
