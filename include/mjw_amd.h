@@ -41,7 +41,7 @@
   X(nsensor) X(nsensordata) X(sensor_rne_postconstraint) X(nsensor_acc)                           \
   X(nxn_ccd) X(nxn_box) X(opt_ccd_iterations) X(ccd_epa_iterations)                                           \
   X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations) X(opt_ls_iterations)             \
-  X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)                                  \
+  X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter) X(opt_ls_parallel)               \
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
@@ -52,7 +52,7 @@
   X(opt_timestep, 1) X(opt_tolerance, 1) X(opt_ls_tolerance, 1) X(opt_impratio_invsqrt, 1)        \
   X(opt_ccd_tolerance, 1)                                                                          \
   X(opt_gravity, 3) X(opt_magnetic, 3) X(stat_meaninertia, 1)                                      \
-  X(opt_wind, 3) X(opt_density, 1) X(opt_viscosity, 1)                                             \
+  X(opt_wind, 3) X(opt_density, 1) X(opt_viscosity, 1) X(opt_ls_parallel_min_step, 1)             \
   X(qpos0, nq) X(qpos_spring, nq)                                                                  \
   X(body_pos, nbody * 3) X(body_quat, nbody * 4) X(body_ipos, nbody * 3) X(body_iquat, nbody * 4) \
   X(body_mass, nbody) X(body_subtreemass, nbody) X(body_inertia, nbody * 3)                       \

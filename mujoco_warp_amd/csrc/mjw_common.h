@@ -59,6 +59,13 @@ __device__ __forceinline__ const float* mb(const float* p, int nb, int cnt, int 
 }
 #define MR(name) mb(m.name, m.name##_nb, m.name##_cnt, wid)
 
+// solver.py:325-327 _log_scale: step size i of the parallel linesearch, log-spaced in [min_step, 1]
+__device__ __forceinline__ float ls_parallel_alpha(float min_step, int n, int i) {
+  const float lmin = logf(min_step);
+  const float step = (logf(1.0f) - lmin) / fmaxf(1.0f, (float)(n - 1));
+  return expf(lmin + (float)i * step);
+}
+
 // support.py:38-64 next_act: one activation advanced by scale * act_dot over the timestep dt
 // (FILTEREXACT integrates the first-order filter exactly; USER activations are left to the user)
 __device__ __forceinline__ float next_act(float dt, int dyntype, float tau_prm, const float* actrange, float act, float act_dot,

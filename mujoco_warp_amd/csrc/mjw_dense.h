@@ -690,10 +690,21 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
           }
         }
         auto lsp = [&](float al) -> Pt { return EL ? ls_point_e(w, ecoef, e_first, al, q1, q2, qg0) : ls_point(w, al, q1, q2, qg0); };
+        float alpha;
+        if (m.opt_ls_parallel) {
+          // solver.py:325-478 parallel linesearch: the cheapest of ls_iterations log-spaced step sizes
+          // in [ls_parallel_min_step, 1] (the first one on ties)
+          alpha = 0.0f;
+          float best = MJW_MAXVAL;
+          for (int i = 0; i < m.opt_ls_iterations; i++) {
+            const float al = ls_parallel_alpha(MR(opt_ls_parallel_min_step)[0], m.opt_ls_iterations, i);
+            const float cst = lsp(al).c;
+            if (cst < best) { best = cst; alpha = al; }
+          }
+        } else {
         Pt p0 = lsp(0.0f);
         float lo_alpha_in = -safe_div(p0.g, p0.h);
         Pt lo_in = lsp(lo_alpha_in);
-        float alpha;
         if (fabsf(lo_in.g) < gtol && lo_in.c < p0.c) {
           alpha = lo_alpha_in;
         } else {
@@ -723,6 +734,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
             if (improved) alpha = plo.c < phi.c ? plo.alpha : phi.alpha;
             if (ls_done) break;
           }
+        }
         }
         qacc = fmaf(alpha, search, qacc);
         ma = fmaf(alpha, mv, ma);

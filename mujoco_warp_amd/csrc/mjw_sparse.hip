@@ -2283,6 +2283,26 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
     o[1] = 2.0f * a * qg2 + qg1;
     o[2] = 2.0f * qg2;
   };
+  float alpha;
+  if (m.opt_ls_parallel) {
+    // solver.py:325-478 parallel linesearch: the cheapest of ls_iterations log-spaced step sizes in
+    // [ls_parallel_min_step, 1] (the first one on ties), three per row pass
+    alpha = 0.0f;
+    float best = MJW_MAXVAL;
+    const int n = m.opt_ls_iterations;
+    for (int i0 = 0; i0 < n; i0 += 3) {
+      float al[3], v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < 3; k++) al[k] = ls_parallel_alpha(MR_W(opt_ls_parallel_min_step), n, min(i0 + k, n - 1));
+      eval_rows<3>(c, al, v9);
+      block_sum_db<9>(v9, sm, c.rphase);
+      for (int k = 0; k < 3 && i0 + k < n; k++) {
+        float g[3];
+        gauss_at(al[k], g);
+        const float cst = v9[3 * k] + g[0];
+        if (cst < best) { best = cst; alpha = al[k]; }
+      }
+    }
+  } else {
   const float lo_alpha_in = -safe_div(p0[1], p0[2]);
   float lo_in[3] = {0, 0, 0};
   eval_rows<1>(c, &lo_alpha_in, lo_in);
@@ -2292,7 +2312,6 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
     gauss_at(lo_alpha_in, g);
     for (int k = 0; k < 3; k++) lo_in[k] += g[k];
   }
-  float alpha;
   if (!(fabsf(lo_in[1]) < gtol && lo_in[0] < p0[0])) {
     alpha = 0.0f;
     float lo[3], hi[3], lo_alpha, hi_alpha;
@@ -2339,6 +2358,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
     }
   } else {
     alpha = lo_alpha_in;
+  }
   }
   for (int i = tid(); i < c.nv; i += nthr()) {
     c.qacc[i] += alpha * c.search[i];

@@ -2094,15 +2094,31 @@ __device__ __forceinline__ void solve(const mjw_model_t& m, const mjw_data_t& d,
         o.c = wave_sum(o.c); o.g = wave_sum(o.g); o.h = wave_sum(o.h);
         return o;
       };
-      Vec3 p0 = eval_all(0.0f);
-      p0.c += qg0; p0.g += q1; p0.h += 2.0f * q2;
-      float lo_alpha_in = -safe_div(p0.g, p0.h);
-      Vec3 lo_in = eval_all(lo_alpha_in);
-      lo_in.c += lo_alpha_in * lo_alpha_in * q2 + lo_alpha_in * q1 + qg0;
-      lo_in.g += 2.0f * lo_alpha_in * q2 + q1;
-      lo_in.h += 2.0f * q2;
       float alpha;
-      bool initial_converged = fabsf(lo_in.g) < gtol && lo_in.c < p0.c;
+      Vec3 p0 = {0.0f, 0.0f, 0.0f}, lo_in = {0.0f, 0.0f, 0.0f};
+      float lo_alpha_in = 0.0f;
+      bool initial_converged = false;
+      if (m.opt_ls_parallel) {
+        // solver.py:325-478 parallel linesearch: the cheapest of ls_iterations log-spaced step sizes
+        alpha = 0.0f;
+        float best = MJW_MAXVAL;
+        for (int i = 0; i < m.opt_ls_iterations; i++) {
+          const float al = ls_parallel_alpha(MR(opt_ls_parallel_min_step)[0], m.opt_ls_iterations, i);
+          const float cst = eval_all(al).c + al * al * q2 + al * q1 + qg0;
+          if (cst < best) { best = cst; alpha = al; }
+        }
+        initial_converged = true;  // skip the iterative search below
+        lo_alpha_in = alpha;
+      } else {
+        p0 = eval_all(0.0f);
+        p0.c += qg0; p0.g += q1; p0.h += 2.0f * q2;
+        lo_alpha_in = -safe_div(p0.g, p0.h);
+        lo_in = eval_all(lo_alpha_in);
+        lo_in.c += lo_alpha_in * lo_alpha_in * q2 + lo_alpha_in * q1 + qg0;
+        lo_in.g += 2.0f * lo_alpha_in * q2 + q1;
+        lo_in.h += 2.0f * q2;
+        initial_converged = fabsf(lo_in.g) < gtol && lo_in.c < p0.c;
+      }
       if (!initial_converged) {
         alpha = 0.0f;
         bool lo_less = lo_in.g < p0.g;

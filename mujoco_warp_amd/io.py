@@ -19,7 +19,7 @@ import torch
 
 from . import _lib
 from . import types
-from .types import BroadphaseFilter, DisableBit, JointType
+from .types import BroadphaseFilter, DisableBit, EnableBit, JointType
 
 # reference io.py:650-661
 def _round_up(x, k):
@@ -133,6 +133,13 @@ def put_model(mjm, device=None) -> types.Model:
     raise NotImplementedError(f"{types.SolverType(mjm.opt.solver).name} is unsupported.")
   if getattr(mjm.opt, "noslip_iterations", 0) > 0:
     raise NotImplementedError("noslip solver not implemented.")
+  # io.py:114-121: flags outside the reference's DisableBit / EnableBit sets (types.py:166-221)
+  unsupported = int(mjm.opt.disableflags) & int(DisableBit.MIDPHASE | DisableBit.AUTORESET)
+  if unsupported:
+    raise NotImplementedError(f"{DisableBit(unsupported).name} is unsupported.")
+  unsupported = int(mjm.opt.enableflags) & int(EnableBit.OVERRIDE | EnableBit.FWDINV)
+  if unsupported:
+    raise NotImplementedError(f"{EnableBit(unsupported).name} is unsupported.")
   sparse = is_sparse(mjm) or getattr(mjm, "nflex", 0) > 0
   if sparse:
     # the workgroup-per-world sparse / flex pipeline (csrc/mjw_sparse.hip) covers this subset
@@ -164,6 +171,10 @@ def put_model(mjm, device=None) -> types.Model:
     if t not in (_SUPPORTED_PAIRS | _SPARSE_PAIRS | _SPARSE_CCD_PAIRS if sparse else _SUPPORTED_PAIRS):
       names = tuple(types.GeomType(x).name for x in t)
       raise NotImplementedError(f"collision between {names[0]} and {names[1]} is not supported by this build yet.")
+  if mjm.opt.enableflags & EnableBit.MULTICCD and any(
+      tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) in _CONVEX_TABLE - {(6, 6)} for a, b in pairs_chk):
+    # collision_convex.py:1130-1137: multi-contact of convex pairs other than box-box needs the mesh polygon data
+    raise NotImplementedError("MULTICCD for convex pairs other than box-box (mesh multi-contact) is not supported by this build yet.")
   if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
       tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) == (6, 6) for a, b in pairs_chk):
     raise NotImplementedError("box-box with NATIVECCD disabled (primitive box_box) is not supported by this build yet.")
@@ -203,6 +214,9 @@ def put_model(mjm, device=None) -> types.Model:
   opt.integrator, opt.cone, opt.solver, opt.jacobian = int(o.integrator), int(o.cone), int(o.solver), int(o.jacobian)
   opt.iterations, opt.ls_iterations = int(o.iterations), int(o.ls_iterations)
   opt.disableflags, opt.enableflags = int(o.disableflags), int(o.enableflags)
+  # io.py:188-190: the parallel linesearch switch (a <numeric name="ls_parallel"> of 1) and its smallest step
+  opt.ls_parallel = bool(getattr(o, "ls_parallel", False))
+  opt.ls_parallel_min_step = _f32([1.0e-6], dev)
   stat = types.Statistic(meaninertia=_f32([mjm.stat.meaninertia], dev))
 
   m = types.Model()
@@ -410,6 +424,9 @@ def cmodel(m: types.Model) -> _lib.CModel:
   for name, _ in _lib.MODEL_REAL_ARRAYS:
     grp, attr = _model_attr(name)
     t = getattr(getattr(m, grp), attr) if grp else getattr(m, attr)
+    if not isinstance(t, torch.Tensor):  # an Option scalar set as a Python number (e.g. ls_parallel_min_step)
+      t = torch.tensor([float(t)], dtype=torch.float32, device=m.device)
+      setattr(getattr(m, grp) if grp else m, attr, t)
     tensors.append(t)
   for name, _ in _lib.MODEL_INT_ARRAYS:
     attr = {"nxn_geom_pair": "nxn_geom_pair_typed", "nxn_pairid": "nxn_pairid_filtered"}.get(name, name)

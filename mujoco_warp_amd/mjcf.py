@@ -254,6 +254,7 @@ class MjOption:
     self.iterations = 100
     self.ls_iterations = 50
     self.noslip_iterations = 0
+    self.ls_parallel = False  # Warp-only option from <custom><numeric name="ls_parallel" data="1"/>
     self.ccd_iterations = 35
     self.disableflags = 0
     self.enableflags = 0
@@ -619,6 +620,16 @@ class _Compiler:
 
     for opt in root.findall("option"):
       self._parse_option(opt)
+    # <custom><numeric>: the reference's Warp-only options (io.py:188-199): ls_parallel = 1 selects the
+    # parallel linesearch, contact_sensor_maxmatch sizes the contact sensor's match list
+    m.numeric = {}
+    for cust in root.findall("custom"):
+      for num in cust.findall("numeric"):
+        m.numeric[num.get("name", "")] = _floats(num.get("data", "0"))
+    if "ls_parallel" in m.numeric:
+      m.opt.ls_parallel = m.numeric["ls_parallel"][0] == 1
+    if "contact_sensor_maxmatch" in m.numeric:
+      m.opt.contact_sensor_maxmatch = int(m.numeric["contact_sensor_maxmatch"][0])
 
     # defaults (top-level <default> is class 'main')
     top = _Default("main")

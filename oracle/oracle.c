@@ -2941,12 +2941,29 @@ static void linesearch(const orc_model* m, orc_data* d, solver_ctx* c) {
   real qg[3] = {c->gauss, qg1, qg2};
   real p0[3] = {qg[0] + p0s[0], qg[1] + p0s[1], 2 * qg[2] + p0s[2]};
 #define EVAL_GAUSS(out, a) { out[0] = (a) * (a) * qg[2] + (a) * qg[1] + qg[0]; out[1] = 2 * (a) * qg[2] + qg[1]; out[2] = 2 * qg[2]; }
-  real lo_alpha_in = -safe_div(p0[1], p0[2]);
-  real lo_in[3];
-  EVAL_GAUSS(lo_in, lo_alpha_in);
-  for (int r = 0; r < nefc; r++) eval_row(m, d, c, r, ne, nf, lo_alpha_in, lo_in);
   real alpha;
-  int initial_converged = fabs(lo_in[1]) < gtol && lo_in[0] < p0[0];
+  real lo_alpha_in = 0, lo_in[3] = {0, 0, 0};
+  int initial_converged;
+  if (m->opt_ls_parallel) {
+    /* solver.py:325-478 linesearch_parallel: the cheapest of ls_iterations step sizes log-spaced over
+       [ls_parallel_min_step, 1] (_log_scale :325-327), the first on ties */
+    int n = m->opt_ls_iterations;
+    real step = (log((real)1) - log(m->opt_ls_parallel_min_step)) / maxr(1, (real)(n - 1)), best = (real)1e10;
+    alpha = 0;
+    for (int i = 0; i < n; i++) {
+      real al = exp(log(m->opt_ls_parallel_min_step) + (real)i * step), v[3];
+      EVAL_GAUSS(v, al);
+      for (int r = 0; r < nefc; r++) eval_row(m, d, c, r, ne, nf, al, v);
+      if (v[0] < best) { best = v[0]; alpha = al; }
+    }
+    lo_alpha_in = alpha;
+    initial_converged = 1;
+  } else {
+    lo_alpha_in = -safe_div(p0[1], p0[2]);
+    EVAL_GAUSS(lo_in, lo_alpha_in);
+    for (int r = 0; r < nefc; r++) eval_row(m, d, c, r, ne, nf, lo_alpha_in, lo_in);
+    initial_converged = fabs(lo_in[1]) < gtol && lo_in[0] < p0[0];
+  }
   if (!initial_converged) {
     alpha = 0;
     int lo_less = lo_in[1] < p0[1];

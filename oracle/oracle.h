@@ -27,7 +27,7 @@ typedef ORC_REAL real;
 #define ORC_MODEL_INT_SCALARS(X)                                                                   \
   X(nq) X(nv) X(nu) X(na) X(nbody) X(njnt) X(ngeom) X(nsite) X(ncam) X(nlight) X(nmocap)          \
   X(nxn) X(nmaxpyramid) X(neq) X(nsensor) X(nsensordata) X(opt_integrator) X(opt_cone) X(opt_solver) X(opt_iterations)             \
-  X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter)             \
+  X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter) X(opt_ls_parallel) \
   X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
   X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)   \
   X(ntendon) X(nwrap) X(nJten) X(npair) X(ngravcomp) X(has_fluid)
@@ -35,7 +35,7 @@ typedef ORC_REAL real;
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
   X(opt_timestep) X(opt_tolerance) X(opt_ls_tolerance) X(opt_impratio_invsqrt) X(stat_meaninertia)         \
-  X(opt_ccd_tolerance) X(opt_density) X(opt_viscosity)
+  X(opt_ccd_tolerance) X(opt_density) X(opt_viscosity) X(opt_ls_parallel_min_step)
 
 /* ---- model: real arrays (name, element count) ---- */
 #define ORC_MODEL_REAL_ARRAYS(X)                                                                   \

@@ -143,6 +143,7 @@ class OracleModel:
       ngravcomp=int((np.asarray(getattr(mjm, "body_gravcomp", np.zeros(mjm.nbody))) > 0).sum()),
       has_fluid=int(bool(np.any(np.asarray(o.wind) != 0) or o.density > 0 or o.viscosity > 0)),
       opt_density=o.density, opt_viscosity=o.viscosity,
+      opt_ls_parallel=int(bool(getattr(o, "ls_parallel", False))), opt_ls_parallel_min_step=getattr(o, "ls_parallel_min_step", 1e-6),
     )
     if overrides:
       vals.update(overrides)
