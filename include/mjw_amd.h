@@ -145,7 +145,7 @@
   X(cfrc_ext, nbody * 6)                                                                           \
   X(efc_J, njmax_pad * nv_pad) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax_pad)         \
   X(efc_vel, njmax) X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax)             \
-  X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 17)                                 \
+  X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 20)                                 \
   X(qpos_t0, nq) X(qvel_t0, nv) X(act_t0, na) X(qvel_rk, nv) X(qacc_rk, nv) X(act_dot_rk, na)     \
   X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
   X(flexedge_J, nflexedge * 6) X(flex_frc, nflexelem * 9 + nflexedge * 12)                        \

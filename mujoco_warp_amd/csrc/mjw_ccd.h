@@ -23,8 +23,10 @@ constexpr unsigned CCD_FACE_INVALID = 0x40000000u;
 
 // one geom in the workspace: pos[3] rot[9] size[3] margin type mesh_vertadr mesh_vertnum
 constexpr int CGEOM_WORDS = 19;
-// per-pair result record in HBM (d.ccd_out): count, dist, normal[3], points[4][3]
-constexpr int CCD_OUT = 17;
+// per-pair result record in HBM (d.ccd_out): count, normal[3], then per point (dist, pos[3]) x 4.  The
+// convex pairs (GJK / EPA / box multi-contact) give every point the pair's distance; the multi-point
+// primitives the pre-passes also run (plane-cylinder, plane-mesh) give each point its own.
+constexpr int CCD_OUT = 20;
 
 // LDS workspace layout (offsets in words) for epa_iterations = it
 struct CcdLay {
@@ -925,6 +927,16 @@ __device__ __forceinline__ void put_cgeom(float* dst, const float* pos, const fl
   dst[16] = __int_as_float(type);
   dst[17] = __int_as_float(vertadr);
   dst[18] = __int_as_float(nvert);
+}
+
+// lane `lane` (< CCD_OUT) of the record of a convex pair from the lockstep workspace's result
+// (Wout: dist, normal[3], points[4][3]) and its contact count nc
+__device__ __forceinline__ float ccd_record_word(int lane, int nc, const float* Wout) {
+  if (lane == 0) return (float)nc;
+  if (nc <= 0) return 0.0f;
+  if (lane < 4) return Wout[lane];
+  const int q = (lane - 4) >> 2, j = (lane - 4) & 3;
+  return j == 0 ? Wout[0] : Wout[4 + 3 * q + j - 1];
 }
 
 __device__ __forceinline__ CGeom get_cgeom(const float* src, const float* mesh_vert) {

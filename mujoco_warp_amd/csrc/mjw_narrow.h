@@ -415,4 +415,160 @@ __device__ __forceinline__ void contact_params(const mjw_model_t& m, int wid, in
   for (int i = 0; i < 5; i++) friction[i] = fmaxf(MJW_MINMU, friction[i]);
 }
 
+// collision_primitive_core.py:519-613 plane_cylinder candidate k
+__device__ __forceinline__ void plane_cylinder_k(int k, const float* n, const float* pp, const float* cc, const float* cax, float r, float hh, float* dist,
+                                 float* pos) {
+  float axis[3] = {cax[0], cax[1], cax[2]};
+  float prjaxis = dot3(n, axis);
+  if (prjaxis > 0.0f) {
+    for (int i = 0; i < 3; i++) axis[i] = -axis[i];
+    prjaxis = -prjaxis;
+  }
+  const float df[3] = {cc[0] - pp[0], cc[1] - pp[1], cc[2] - pp[2]};
+  const float dist0 = dot3(df, n);
+  float vec[3];
+  for (int i = 0; i < 3; i++) vec[i] = axis[i] * prjaxis - n[i];
+  const float len2 = dot3(vec, vec);
+  if (len2 >= 1e-12f) {
+    const float s = safe_div(r, sqrtf(len2));
+    for (int i = 0; i < 3; i++) vec[i] *= s;
+  } else {
+    vec[0] = r;
+    vec[1] = vec[2] = 0.0f;
+  }
+  const float prjvec = dot3(vec, n);
+  for (int i = 0; i < 3; i++) axis[i] *= hh;
+  prjaxis *= hh;
+  if (k == 0) {
+    *dist = dist0 + prjaxis + prjvec;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + vec[i] + axis[i] - n[i] * (*dist * 0.5f);
+  } else if (k == 1) {
+    *dist = dist0 - prjaxis + prjvec;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + vec[i] - axis[i] - n[i] * (*dist * 0.5f);
+  } else {
+    *dist = dist0 + prjaxis - prjvec * 0.5f;
+    float v1[3];
+    cross3(v1, vec, axis);
+    normalize3(v1);
+    const float s = r * sqrtf(3.0f) * 0.5f, sg = k == 2 ? 1.0f : -1.0f;
+    for (int i = 0; i < 3; i++) pos[i] = cc[i] + sg * v1[i] * s + axis[i] - vec[i] * 0.5f - n[i] * (*dist * 0.5f);
+  }
+}
+
+// collision_primitive.py:52-139, 257-277 plane_convex, exhaustive-search branch (the reference takes it
+// for meshes without a hull graph; with one it hill-climbs the hull, which reaches the same deepest
+// vertex a): the deepest vertex a, then among vertices within 1e-3 of its depth the one farthest from
+// a (b), farthest from line ab (c) and from the triangle's other edges (d); each distinct vertex is a
+// contact at its own depth.  One thread, serial over the vertices.
+static __device__ __noinline__ int plane_mesh(const float* nw, const float* ppos, const float* gpos, const float* R, const float* mv, int nvert, float* dist,
+                          float (*pos)[3]) {
+  constexpr float HUGE_ = 1e6f;
+  const float d0[3] = {ppos[0] - gpos[0], ppos[1] - gpos[1], ppos[2] - gpos[2]};
+  float pl[3], n[3];
+  for (int i = 0; i < 3; i++) {
+    pl[i] = R[i] * d0[0] + R[3 + i] * d0[1] + R[6 + i] * d0[2];
+    n[i] = R[i] * nw[0] + R[3 + i] * nw[1] + R[6 + i] * nw[2];
+  }
+  auto sup = [&](const float* v) { return (pl[0] - v[0]) * n[0] + (pl[1] - v[1]) * n[1] + (pl[2] - v[2]) * n[2]; };
+  int idx[4] = {-1, -1, -1, -1};
+  float maxs = -HUGE_, a[3] = {0, 0, 0}, b[3] = {0, 0, 0}, c[3] = {0, 0, 0};
+  for (int i = 0; i < nvert; i++) {
+    const float s = sup(mv + 3 * i);
+    if (s > maxs) { maxs = s; idx[0] = i; a[0] = mv[3 * i]; a[1] = mv[3 * i + 1]; a[2] = mv[3 * i + 2]; }
+  }
+  if (maxs < 0.0f) return 0;
+  const float thr = maxs - 1e-3f;
+  float best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const float* v = mv + 3 * i;
+    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
+    const float dv[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]};
+    const float dd = dot3(dv, dv) + mask;
+    if (dd > best) { idx[1] = i; best = dd; b[0] = v[0]; b[1] = v[1]; b[2] = v[2]; }
+  }
+  float ab[3], t[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+  cross3(ab, n, t);
+  best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const float* v = mv + 3 * i;
+    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
+    const float ap[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]};
+    const float dd = fabsf(dot3(ap, ab)) + mask;
+    if (dd > best) { idx[2] = i; best = dd; c[0] = v[0]; c[1] = v[1]; c[2] = v[2]; }
+  }
+  float ac[3], bc[3], t1[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]}, t2[3] = {b[0] - c[0], b[1] - c[1], b[2] - c[2]};
+  cross3(ac, n, t1);
+  cross3(bc, n, t2);
+  best = -HUGE_;
+  for (int i = 0; i < nvert; i++) {
+    const float* v = mv + 3 * i;
+    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
+    const float ap[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]}, bp[3] = {b[0] - v[0], b[1] - v[1], b[2] - v[2]};
+    const float dd = (fabsf(dot3(ap, ac)) + mask) + (fabsf(dot3(bp, bc)) + mask);
+    if (dd > best) { idx[3] = i; best = dd; }
+  }
+  int cnt = 0;
+  for (int i = 3; i >= 0; i--) {
+    int count = 0;
+    for (int j = 0; j <= i; j++) count += idx[j] == idx[i];
+    if (count != 1) continue;
+    const float* v = mv + 3 * idx[i];
+    const float dd = -sup(v);
+    for (int k = 0; k < 3; k++) pos[cnt][k] = gpos[k] + R[3 * k] * v[0] + R[3 * k + 1] * v[1] + R[3 * k + 2] * v[2] - 0.5f * dd * nw[k];
+    dist[cnt] = dd;
+    cnt++;
+  }
+  return cnt;
+}
+
+// collision_primitive_core.py:364-392 plane_ellipsoid: the ellipsoid's support point against the plane
+// normal (in the unit-sphere frame of the ellipsoid), the contact at the middle of the penetration
+__device__ __forceinline__ float plane_ellipsoid(float* pos, const float* n, const float* ppos, const float* epos, const float* R,
+                                                 const float* size) {
+  float l[3];
+  mat_t_vec3(l, R, n);
+  for (int i = 0; i < 3; i++) l[i] *= size[i];
+  normalize3(l);
+  float sl[3] = {-l[0] * size[0], -l[1] * size[1], -l[2] * size[2]}, w[3];
+  matvec3(w, R, sl);
+  for (int i = 0; i < 3; i++) pos[i] = epos[i] + w[i];
+  const float d[3] = {pos[0] - ppos[0], pos[1] - ppos[1], pos[2] - ppos[2]};
+  const float dist = dot3(n, d);
+  for (int i = 0; i < 3; i++) pos[i] -= n[i] * dist * 0.5f;
+  return dist;
+}
+
+// collision_primitive_core.py:446-515 sphere_cylinder: side (sphere vs the axis point at the sphere's
+// height), cap (plane of the nearer cap, normal flipped) or rim corner, whichever the sphere centre lies in
+__device__ __forceinline__ float sphere_cylinder(float* pos, float* nrm, const float* sp, float sr, const float* cp, const float* ax, float cr,
+                                                 float hh) {
+  const float vec[3] = {sp[0] - cp[0], sp[1] - cp[1], sp[2] - cp[2]};
+  const float x = dot3(vec, ax);
+  const float a_proj[3] = {ax[0] * x, ax[1] * x, ax[2] * x};
+  float p_proj[3] = {vec[0] - a_proj[0], vec[1] - a_proj[1], vec[2] - a_proj[2]};
+  const float p2 = dot3(p_proj, p_proj);
+  bool side = fabsf(x) < hh, cap = p2 < cr * cr;
+  if (side && cap) {
+    if (hh - fabsf(x) < cr - sqrtf(p2)) side = false;
+    else cap = false;
+  }
+  if (side) {
+    const float tgt[3] = {cp[0] + a_proj[0], cp[1] + a_proj[1], cp[2] + a_proj[2]};
+    return sphere_sphere(pos, nrm, sp, sr, tgt, cr);
+  }
+  if (cap) {
+    const float sg = x > 0.0f ? 1.0f : -1.0f;
+    const float pc[3] = {cp[0] + sg * ax[0] * hh, cp[1] + sg * ax[1] * hh, cp[2] + sg * ax[2] * hh};
+    const float pn[3] = {sg * ax[0], sg * ax[1], sg * ax[2]};
+    const float dist = plane_sphere(pos, pn, pc, sp, sr);
+    for (int i = 0; i < 3; i++) nrm[i] = -pn[i];
+    return dist;
+  }
+  const float inv = safe_div(1.0f, sqrtf(p2));
+  for (int i = 0; i < 3; i++) p_proj[i] *= cr * inv;
+  const float sg = x < 0.0f ? -1.0f : 1.0f;  // wp.sign
+  const float corner[3] = {cp[0] + ax[0] * sg * hh + p_proj[0], cp[1] + ax[1] * sg * hh + p_proj[1], cp[2] + ax[2] * sg * hh + p_proj[2]};
+  return sphere_sphere(pos, nrm, sp, sr, corner, 0.0f);
+}
+
 }  // namespace mjw

@@ -680,112 +680,6 @@ __device__ void mul_m_trees(const mjw_model_t& m, const float* M, const float* x
 // collision: geom pairs (collision_driver.py:697-789 + primitive narrowphase), flex triangles vs
 // geoms (collision_flex.py:381-529) and flex vertices vs planes (:261-378)
 // ---------------------------------------------------------------------------------------------
-// collision_primitive_core.py:519-613 plane_cylinder candidate k
-__device__ void plane_cylinder_k(int k, const float* n, const float* pp, const float* cc, const float* cax, float r, float hh, float* dist,
-                                 float* pos) {
-  float axis[3] = {cax[0], cax[1], cax[2]};
-  float prjaxis = dot3(n, axis);
-  if (prjaxis > 0.0f) {
-    for (int i = 0; i < 3; i++) axis[i] = -axis[i];
-    prjaxis = -prjaxis;
-  }
-  const float df[3] = {cc[0] - pp[0], cc[1] - pp[1], cc[2] - pp[2]};
-  const float dist0 = dot3(df, n);
-  float vec[3];
-  for (int i = 0; i < 3; i++) vec[i] = axis[i] * prjaxis - n[i];
-  const float len2 = dot3(vec, vec);
-  if (len2 >= 1e-12f) {
-    const float s = safe_div(r, sqrtf(len2));
-    for (int i = 0; i < 3; i++) vec[i] *= s;
-  } else {
-    vec[0] = r;
-    vec[1] = vec[2] = 0.0f;
-  }
-  const float prjvec = dot3(vec, n);
-  for (int i = 0; i < 3; i++) axis[i] *= hh;
-  prjaxis *= hh;
-  if (k == 0) {
-    *dist = dist0 + prjaxis + prjvec;
-    for (int i = 0; i < 3; i++) pos[i] = cc[i] + vec[i] + axis[i] - n[i] * (*dist * 0.5f);
-  } else if (k == 1) {
-    *dist = dist0 - prjaxis + prjvec;
-    for (int i = 0; i < 3; i++) pos[i] = cc[i] + vec[i] - axis[i] - n[i] * (*dist * 0.5f);
-  } else {
-    *dist = dist0 + prjaxis - prjvec * 0.5f;
-    float v1[3];
-    cross3(v1, vec, axis);
-    normalize3(v1);
-    const float s = r * sqrtf(3.0f) * 0.5f, sg = k == 2 ? 1.0f : -1.0f;
-    for (int i = 0; i < 3; i++) pos[i] = cc[i] + sg * v1[i] * s + axis[i] - vec[i] * 0.5f - n[i] * (*dist * 0.5f);
-  }
-}
-
-// collision_primitive.py:52-139, 257-277 plane_convex, exhaustive-search branch (the reference takes it
-// for meshes without a hull graph; with one it hill-climbs the hull, which reaches the same deepest
-// vertex a): the deepest vertex a, then among vertices within 1e-3 of its depth the one farthest from
-// a (b), farthest from line ab (c) and from the triangle's other edges (d); each distinct vertex is a
-// contact at its own depth.  One thread, serial over the vertices (rare: plane-near meshes only).
-__device__ __noinline__ int plane_mesh(const float* nw, const float* ppos, const float* gpos, const float* R, const float* mv, int nvert, float* dist,
-                          float (*pos)[3]) {
-  constexpr float HUGE_ = 1e6f;
-  const float d0[3] = {ppos[0] - gpos[0], ppos[1] - gpos[1], ppos[2] - gpos[2]};
-  float pl[3], n[3];
-  for (int i = 0; i < 3; i++) {
-    pl[i] = R[i] * d0[0] + R[3 + i] * d0[1] + R[6 + i] * d0[2];
-    n[i] = R[i] * nw[0] + R[3 + i] * nw[1] + R[6 + i] * nw[2];
-  }
-  auto sup = [&](const float* v) { return (pl[0] - v[0]) * n[0] + (pl[1] - v[1]) * n[1] + (pl[2] - v[2]) * n[2]; };
-  int idx[4] = {-1, -1, -1, -1};
-  float maxs = -HUGE_, a[3] = {0, 0, 0}, b[3] = {0, 0, 0}, c[3] = {0, 0, 0};
-  for (int i = 0; i < nvert; i++) {
-    const float s = sup(mv + 3 * i);
-    if (s > maxs) { maxs = s; idx[0] = i; a[0] = mv[3 * i]; a[1] = mv[3 * i + 1]; a[2] = mv[3 * i + 2]; }
-  }
-  if (maxs < 0.0f) return 0;
-  const float thr = maxs - 1e-3f;
-  float best = -HUGE_;
-  for (int i = 0; i < nvert; i++) {
-    const float* v = mv + 3 * i;
-    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
-    const float dv[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]};
-    const float dd = dot3(dv, dv) + mask;
-    if (dd > best) { idx[1] = i; best = dd; b[0] = v[0]; b[1] = v[1]; b[2] = v[2]; }
-  }
-  float ab[3], t[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
-  cross3(ab, n, t);
-  best = -HUGE_;
-  for (int i = 0; i < nvert; i++) {
-    const float* v = mv + 3 * i;
-    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
-    const float ap[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]};
-    const float dd = fabsf(dot3(ap, ab)) + mask;
-    if (dd > best) { idx[2] = i; best = dd; c[0] = v[0]; c[1] = v[1]; c[2] = v[2]; }
-  }
-  float ac[3], bc[3], t1[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]}, t2[3] = {b[0] - c[0], b[1] - c[1], b[2] - c[2]};
-  cross3(ac, n, t1);
-  cross3(bc, n, t2);
-  best = -HUGE_;
-  for (int i = 0; i < nvert; i++) {
-    const float* v = mv + 3 * i;
-    const float mask = sup(v) > thr ? 0.0f : -HUGE_;
-    const float ap[3] = {a[0] - v[0], a[1] - v[1], a[2] - v[2]}, bp[3] = {b[0] - v[0], b[1] - v[1], b[2] - v[2]};
-    const float dd = (fabsf(dot3(ap, ac)) + mask) + (fabsf(dot3(bp, bc)) + mask);
-    if (dd > best) { idx[3] = i; best = dd; }
-  }
-  int cnt = 0;
-  for (int i = 3; i >= 0; i--) {
-    int count = 0;
-    for (int j = 0; j <= i; j++) count += idx[j] == idx[i];
-    if (count != 1) continue;
-    const float* v = mv + 3 * idx[i];
-    const float dd = -sup(v);
-    for (int k = 0; k < 3; k++) pos[cnt][k] = gpos[k] + R[3 * k] * v[0] + R[3 * k + 1] * v[1] + R[3 * k + 2] * v[2] - 0.5f * dd * nw[k];
-    dist[cnt] = dd;
-    cnt++;
-  }
-  return cnt;
-}
-
 // collision_driver.py:274-321 on global frames
 __device__ bool broadphase(const mjw_model_t& m, int wid, const float* gx, const float* gm, int g1, int g2) {
   const float* geom_aabb = MR(geom_aabb);
@@ -905,10 +799,13 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
       // frame make_frame(normal) (collision_convex.py:763-852)
       const float* out = d.ccd_out + ((long)wid * m.nxn_ccd + ccdslot) * CCD_OUT;
       const int n = (int)out[0];
-      const float dist = out[1];
-      if (!(dist < o.margin) || m.nxn_pairid[2 * item] < -1) return 0;
-      for (int k = 0; k < n && base >= 0; k++) write_contact(m, d, wid, base + k, lim, o, dist, out + 5 + 3 * k, out + 2);
-      return n;
+      if (m.nxn_pairid[2 * item] < -1) return 0;
+      for (int k = 0; k < n; k++) {
+        if (!(out[4 + 4 * k] < o.margin)) continue;
+        if (base >= 0) write_contact(m, d, wid, base + cnt, lim, o, out[4 + 4 * k], out + 5 + 4 * k, out + 1);
+        cnt++;
+      }
+      return cnt;
     }
     if (t1 == GEOM_PLANE && t2 == GEOM_MESH) {
       float pd[4], pp[4][3];
@@ -951,6 +848,15 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
       c.n = 1;
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {
       nl_capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_ELLIPSOID) {  // collision_primitive.py:665-733
+      c.dist[0] = plane_ellipsoid(c.pos[0], n1, p1, p2, r2, s2);
+      make_frame(c.frame[0], n1);
+      c.n = 1;
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_CYLINDER) {  // collision_primitive.py:882-960
+      float nrm[3];
+      c.dist[0] = sphere_cylinder(c.pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]);
+      make_frame(c.frame[0], nrm);
+      c.n = 1;
     }
     const int nk = ncand == 2 ? c.n : ncand;
     for (int k = 0; k < nk; k++) {
@@ -1944,7 +1850,7 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
       const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations,
                               pid > -1 ? MR(pair_margin)[pid] : gmargin[g1] + gmargin[g2], mesh_vert);
       float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[q]) * CCD_OUT;
-      if (lane < CCD_OUT) out[lane] = lane == 0 ? (float)nc : (nc > 0 ? W[CL.out + lane - 1] : 0.0f);
+      if (lane < CCD_OUT) out[lane] = ccd_record_word(lane, nc, W + CL.out);
       __syncthreads();
     }
   }

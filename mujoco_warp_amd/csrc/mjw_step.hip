@@ -1149,8 +1149,13 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           pairid0 = m.nxn_pairid[2 * p];
           margin = pairid0 > -1 ? MR(pair_margin)[pairid0] : geom_margin[g1] + geom_margin[g2];
           pbox = BOX && m.geom_type[g1] == GEOM_PLANE && m.geom_type[g2] == GEOM_BOX;
-          ccd = BOX && m.geom_type[g1] == GEOM_BOX && m.geom_type[g2] == GEOM_BOX;
+          ccd = BOX && m.nxn_ccdid[p] >= 0;
           if (ccd) {
+            // pre-pass record (ccd_kernel): up to 4 points, each with its own distance
+            const float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[p]) * CCD_OUT;
+            const int n = (int)out[0];
+            for (int q = 0; q < 4; q++)
+              if (q < n && out[4 + 4 * q] < margin && pairid0 >= -1) bmask |= 1u << q;
           } else if (pbox) {
             const float* r1 = s + L.gxmat + 9 * g1;
             float n1[3] = {r1[2], r1[5], r1[8]}, cp[3];
@@ -1163,24 +1168,11 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
             narrowphase<BOX>(m, L, s, wid, g1, g2, margin, c);
           }
         }
-        // convex pairs: results of the CCD pre-pass (ccd_kernel), c.n contacts at distance c.dist[0]
-        // with frame c.frame[0], points in c.pos[0], c.pos[1], c.frame[1][0..2], c.frame[1][3..5]
-        if (ccd) {
-          const float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[plist[k]]) * CCD_OUT;
-          c.n = (int)out[0];
-          c.dist[0] = out[1];
-          make_frame(c.frame[0], out + 2);
-          for (int i = 0; i < 3; i++) {
-            c.pos[0][i] = out[5 + i];
-            c.pos[1][i] = out[8 + i];
-            c.frame[1][i] = out[11 + i];
-            c.frame[1][3 + i] = out[14 + i];
-          }
-        }
-        // active contacts (write_contact collision_core.py:199-213)
+        // active contacts (write_contact collision_core.py:199-213); plane-box corners and pre-pass points
+        // (convex pairs, multi-point primitives) by their bit masks
         bool a0 = !ccd && c.n > 0 && c.dist[0] < margin && pairid0 >= -1;
         bool a1 = !ccd && c.n > 1 && c.dist[1] < margin && pairid0 >= -1;
-        int cnt = pbox ? __popc(bmask) : (ccd ? (pairid0 >= -1 && c.dist[0] < margin ? c.n : 0) : (int)a0 + (int)a1);
+        int cnt = (pbox || ccd) ? __popc(bmask) : (int)a0 + (int)a1;
         int incl = wave_scan_incl(cnt);
         int first = running + incl - cnt;
         bool stage0 = a0 && first >= rbeg && first < rend;
@@ -1224,15 +1216,20 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
             }
           }
           if (ccd) {
-            for (int q = 0; q < c.n; q++) {
-              int idx = first + q;
+            const float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[plist[k]]) * CCD_OUT;
+            float frame[9];
+            make_frame(frame, out + 1);
+            int kk = 0;
+            for (int q = 0; q < 4; q++) {
+              if (!(bmask & (1u << q))) continue;
+              int idx = first + kk;
+              kk++;
               if (idx < rbeg || idx >= rend) continue;
               float* rec = s + L.con + (idx - rbeg) * CREC;
-              rec[0] = c.dist[0];
+              rec[0] = out[4 + 4 * q];
               rec[1] = margin - gap;
-              for (int i = 0; i < 3; i++)
-                rec[2 + i] = q == 0 ? c.pos[0][i] : (q == 1 ? c.pos[1][i] : (q == 2 ? c.frame[1][i] : c.frame[1][3 + i]));
-              for (int i = 0; i < 9; i++) rec[5 + i] = c.frame[0][i];
+              for (int i = 0; i < 3; i++) rec[2 + i] = out[5 + 4 * q + i];
+              for (int i = 0; i < 9; i++) rec[5 + i] = frame[i];
               for (int i = 0; i < 5; i++) rec[14 + i] = friction[i];
               rec[19] = solref[0]; rec[20] = solref[1];
               reinterpret_cast<int*>(rec)[21] = cwelds; reinterpret_cast<int*>(rec)[22] = cbodies;
@@ -2464,12 +2461,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
 }
 
 // -------------------------------------------------------------------------------------------
-// convex collision pre-pass (collision_convex.py:701-890): one wave per world recomputes the
-// geom frames (same kinematics code as the forward kernel), applies the broadphase filter to the
-// convex pairs and runs GJK / EPA / multi-contact on the survivors, one pair at a time with the
-// whole wave in lockstep over an LDS workspace.  Results go to d.ccd_out, which the forward
-// kernel's narrowphase reads, so the (large) CCD code never shares a kernel with the hot path.
+// collision pre-pass: one wave per world recomputes the geom frames (the forward kernel's own
+// kinematics()) and, for the pairs with a pre-pass slot (nxn_ccdid >= 0), applies the broadphase
+// filter and writes each survivor's contact record to d.ccd_out, which the forward kernel's
+// narrowphase reads in pair order.  Two kinds of pairs:
+//  * multi-point and rare primitives (plane-ellipsoid, plane-cylinder, sphere-cylinder, plane-mesh;
+//    collision_primitive.py:665-1040, 810-880 plane_convex), one pair per lane;
+//  * convex pairs (collision_driver.py:43-77 CONVEX: GJK / EPA, box-box multi-contact;
+//    collision_convex.py:701-890), one pair at a time with the whole wave in lockstep over an LDS
+//    workspace (mesh support points by a wave-parallel vertex scan).
+// So the long, branchy CCD and the 4-point primitives never share a kernel (or registers) with the
+// hot path.
 // -------------------------------------------------------------------------------------------
+// pre-pass kind of a type-sorted pair: 1 = lane-parallel primitive, 0 = convex (lockstep)
+__device__ __forceinline__ int prepass_prim(int t1, int t2) {
+  return (t1 == GEOM_PLANE && (t2 == GEOM_ELLIPSOID || t2 == GEOM_CYLINDER || t2 == GEOM_MESH)) || (t1 == GEOM_SPHERE && t2 == GEOM_CYLINDER);
+}
+
 __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   WS w;
@@ -2478,31 +2486,70 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
   w.wid = w0 + (int)blockIdx.x;
   w.lane = lane_id();
   if (w.wid >= d.nworld) return;
-  const int wid = w.wid;
+  const int wid = w.wid, lane = w.lane;
   load_state(m, d, L, w);
   WSYNC();
   kinematics(m, d, L, w);
   float* s = w.s;
   const float* geom_margin = MR(geom_margin);
   const float* gsize = MR(geom_size);
+  const float* mesh_vert = MR(mesh_vert);
+  for (int p = lane; p < m.nxn; p += LPW) {
+    const int slot = m.nxn_ccdid[p];
+    if (slot < 0) continue;
+    const int g1 = m.nxn_geom_pair[2 * p], g2 = m.nxn_geom_pair[2 * p + 1];
+    const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+    if (!prepass_prim(t1, t2)) continue;
+    if (!(m.nxn_pairid[2 * p + 1] >= 0 || broadphase_filter(m, L, s, wid, g1, g2))) continue;
+    const float *p1 = s + L.gxpos + 3 * g1, *p2 = s + L.gxpos + 3 * g2, *r1 = s + L.gxmat + 9 * g1, *r2 = s + L.gxmat + 9 * g2;
+    const float *s1 = gsize + 3 * g1, *s2 = gsize + 3 * g2;
+    const float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
+    float dist[4], pos[4][3], nrm[3] = {n1[0], n1[1], n1[2]};
+    int n = 0;
+    if (t1 == GEOM_PLANE && t2 == GEOM_ELLIPSOID) {
+      dist[0] = plane_ellipsoid(pos[0], n1, p1, p2, r2, s2);
+      n = 1;
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_CYLINDER) {
+      for (int k = 0; k < 4; k++) plane_cylinder_k(k, n1, p1, p2, n2, s2[0], s2[1], &dist[k], pos[k]);
+      n = 4;
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_CYLINDER) {
+      dist[0] = sphere_cylinder(pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]);
+      n = 1;
+    } else {  // plane-mesh
+      const int md = m.geom_dataid[g2];
+      n = plane_mesh(n1, p1, p2, r2, mesh_vert + 3 * (long)m.mesh_vertadr[md], m.mesh_vertnum[md], dist, pos);
+    }
+    float* out = d.ccd_out + ((long)wid * m.nxn_ccd + slot) * CCD_OUT;
+    out[0] = (float)n;
+    for (int i = 0; i < 3; i++) out[1 + i] = nrm[i];
+    for (int q = 0; q < 4; q++) {
+      out[4 + 4 * q] = q < n ? dist[q] : 0.0f;
+      for (int i = 0; i < 3; i++) out[5 + 4 * q + i] = q < n ? pos[q][i] : 0.0f;
+    }
+  }
+  if (L.ccd < 0) return;  // no convex pair (the lockstep workspace is not allocated)
   const CcdLay CL = ccd_layout(m.ccd_epa_iterations);
   float* W = s + L.ccd;
   for (int p = 0; p < m.nxn; p++) {
     const int slot = m.nxn_ccdid[p];
     if (slot < 0) continue;
     const int g1 = m.nxn_geom_pair[2 * p], g2 = m.nxn_geom_pair[2 * p + 1];
+    const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+    if (prepass_prim(t1, t2)) continue;
     const bool pass = m.nxn_pairid[2 * p + 1] >= 0 || broadphase_filter(m, L, s, wid, g1, g2);
     int nc = 0;
     if (pass) {
-      put_cgeom(W + CL.geoms, s + L.gxpos + 3 * g1, s + L.gxmat + 9 * g1, gsize + 3 * g1, m.geom_type[g1]);
-      put_cgeom(W + CL.geoms + CGEOM_WORDS, s + L.gxpos + 3 * g2, s + L.gxmat + 9 * g2, gsize + 3 * g2, m.geom_type[g2]);
+      const int md1 = t1 == GEOM_MESH ? m.geom_dataid[g1] : -1, md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
+      put_cgeom(W + CL.geoms, s + L.gxpos + 3 * g1, s + L.gxmat + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0,
+                md1 >= 0 ? m.mesh_vertnum[md1] : 0);
+      put_cgeom(W + CL.geoms + CGEOM_WORDS, s + L.gxpos + 3 * g2, s + L.gxmat + 9 * g2, gsize + 3 * g2, t2,
+                md2 >= 0 ? m.mesh_vertadr[md2] : 0, md2 >= 0 ? m.mesh_vertnum[md2] : 0);
       const int pid = m.nxn_pairid[2 * p];  // explicit <pair>: its own margin (collision_core.py:271)
       nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations,
-                    pid > -1 ? MR(pair_margin)[pid] : geom_margin[g1] + geom_margin[g2]);
+                    pid > -1 ? MR(pair_margin)[pid] : geom_margin[g1] + geom_margin[g2], mesh_vert);
     }
     float* out = d.ccd_out + ((long)wid * m.nxn_ccd + slot) * CCD_OUT;
-    const int lane = w.lane;
-    if (lane < CCD_OUT) out[lane] = lane == 0 ? (float)nc : (nc > 0 ? W[CL.out + lane - 1] : 0.0f);
+    if (lane < CCD_OUT) out[lane] = ccd_record_word(lane, nc, W + CL.out);
   }
 }
 

@@ -103,19 +103,22 @@ def _model_attr(name):
   return (None, name)
 
 
-_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.BOX, types.GeomType.MESH,
-                    types.GeomType.CYLINDER}
-# narrowphase pairs built on the device (type-sorted): collision_primitive.py:1280-1300 subset
-_SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6), (6, 6)}
-# extra pairs of the sparse path (plane-cylinder, collision_primitive.py:964-1040; plane-mesh
-# plane_convex, :52-300)
-_SPARSE_PAIRS = {(0, 5), (0, 7)}
-# pairs routed through GJK/EPA (the CONVEX entries of collision_driver.py:42-76 built here)
-_CCD_PAIRS = {(6, 6)}
-# ... and on the sparse path, which also runs the mesh pairs (sphere / capsule / box / mesh vs mesh)
-_SPARSE_CCD_PAIRS = {(6, 6), (2, 7), (3, 7), (6, 7), (7, 7)}
-# every CONVEX entry of the reference table (heightfields excluded), for the EPA iteration cap
+_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.ELLIPSOID, types.GeomType.CYLINDER,
+                    types.GeomType.BOX, types.GeomType.MESH}
+# every CONVEX entry of the reference table (collision_driver.py:43-77; heightfields excluded): GJK / EPA
 _CONVEX_TABLE = {(2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
+# PRIMITIVE entries (type-sorted), collision_primitive.py:1280-1300: in the forward kernel's narrowphase ...
+_PRIMITIVE_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6)}
+# ... and in the dense path's pre-pass (ccd_kernel, one pair per lane): plane-ellipsoid, plane-cylinder,
+# sphere-cylinder and plane-mesh (plane_convex) -- the multi-point or rare ones kept out of the hot kernel
+_PREPASS_PRIMITIVES = {(0, 4), (0, 5), (2, 5), (0, 7)}
+_SUPPORTED_PAIRS = _PRIMITIVE_PAIRS | _PREPASS_PRIMITIVES | _CONVEX_TABLE
+# pairs with a pre-pass record slot on the dense path (nxn_ccdid)
+_CCD_PAIRS = _PREPASS_PRIMITIVES | _CONVEX_TABLE
+# the sparse path computes every primitive in its collision kernel and runs the convex pairs in its own
+# CCD pre-pass (mjw_sparse.hip)
+_SPARSE_PAIRS = _PREPASS_PRIMITIVES
+_SPARSE_CCD_PAIRS = _CONVEX_TABLE
 
 
 def put_model(mjm, device=None) -> types.Model:
@@ -284,7 +287,8 @@ def put_model(mjm, device=None) -> types.Model:
   kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in pairs]
   ccd_set = _SPARSE_CCD_PAIRS if sparse else _CCD_PAIRS
   m.nxn_ccd = int(sum(k in ccd_set for k in kinds))
-  m.nxn_box = int(sum(6 in k for k in kinds))  # pairs with a box: the forward kernel's box narrowphase paths
+  # pairs that need the forward kernel's box / pre-pass narrowphase paths (the BOX instantiation)
+  m.nxn_box = int(sum((6 in k) or (k in ccd_set) for k in kinds))
   ccdid = np.cumsum([k in ccd_set for k in kinds]) - 1
   m.nxn_ccdid = _i32(np.where([k in ccd_set for k in kinds], ccdid, -1) if kinds else np.zeros(0), dev)
   m.nmesh, m.nmeshvert = int(getattr(mjm, "nmesh", 0)), int(getattr(mjm, "nmeshvert", 0))
@@ -483,7 +487,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     actuator_length=(nu,), actuator_moment=(m.nJmom,), actuator_velocity=(nu,), actuator_force=(nu,),
     cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,), qfrc_fluid=(nv,),
     qfrc_passive=(nv,), qfrc_actuator=(nv,), qfrc_smooth=(nv,), qacc_smooth=(nv,), qfrc_constraint=(nv,),
-    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 17,),
+    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 20,),
     efc_J=(m.njrow, njmax_pad) if sp else (njmax_pad, m.njrow), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
     efc_aref=(njmax,), efc_frictionloss=(njmax,), efc_force=(njmax,), efc_Ma=(nv,),
     # RK4 workspace (forward.py:462-472 temporaries; kept resident so a step allocates nothing)

@@ -1686,6 +1686,58 @@ static int plane_mesh(const real* nw, const real* ppos, const real* gpos, const 
   return cnt;
 }
 
+/* collision_primitive_core.py:364-392 plane_ellipsoid */
+static real plane_ellipsoid(real* pos, const real* n, const real* ppos, const real* epos, const real* R, const real* size) {
+  real l[3], w[3];
+  for (int i = 0; i < 3; i++) l[i] = (R[i] * n[0] + R[3 + i] * n[1] + R[6 + i] * n[2]) * size[i];
+  normalize3(l);
+  for (int i = 0; i < 3; i++) l[i] = -l[i] * size[i];
+  for (int i = 0; i < 3; i++) w[i] = R[3 * i] * l[0] + R[3 * i + 1] * l[1] + R[3 * i + 2] * l[2];
+  for (int i = 0; i < 3; i++) pos[i] = epos[i] + w[i];
+  real df[3] = {pos[0] - ppos[0], pos[1] - ppos[1], pos[2] - ppos[2]};
+  real dist = dot3(n, df);
+  for (int i = 0; i < 3; i++) pos[i] -= n[i] * dist * (real)0.5;
+  return dist;
+}
+
+/* collision_primitive_core.py:446-515 sphere_cylinder */
+static real sphere_cylinder(real* pos, real* nrm, const real* sp, real sr, const real* cp, const real* ax, real cr, real hh) {
+  real v[3] = {sp[0] - cp[0], sp[1] - cp[1], sp[2] - cp[2]};
+  real x = dot3(v, ax);
+  real ap[3] = {ax[0] * x, ax[1] * x, ax[2] * x}, pp[3] = {v[0] - ap[0], v[1] - ap[1], v[2] - ap[2]};
+  real p2 = dot3(pp, pp);
+  int side = fabs(x) < hh, cap = p2 < cr * cr;
+  if (side && cap) {
+    if (hh - fabs(x) < cr - sqrt(p2)) side = 0;
+    else cap = 0;
+  }
+  if (side) {
+    real t[3] = {cp[0] + ap[0], cp[1] + ap[1], cp[2] + ap[2]};
+    return sphere_sphere(pos, nrm, sp, sr, t, cr);
+  }
+  if (cap) {
+    real sg = x > 0 ? 1 : -1;
+    real pc[3] = {cp[0] + sg * ax[0] * hh, cp[1] + sg * ax[1] * hh, cp[2] + sg * ax[2] * hh}, pn[3] = {sg * ax[0], sg * ax[1], sg * ax[2]};
+    real dist = plane_sphere(pos, pn, pc, sp, sr);
+    for (int i = 0; i < 3; i++) nrm[i] = -pn[i];
+    return dist;
+  }
+  real inv = safe_div(1, sqrt(p2)), sg = x < 0 ? -1 : 1;
+  real c[3];
+  for (int i = 0; i < 3; i++) c[i] = cp[i] + ax[i] * sg * hh + pp[i] * cr * inv;
+  return sphere_sphere(pos, nrm, sp, sr, c, 0);
+}
+
+/* collision_driver.py:43-77 CONVEX entries (heightfields excluded), type-sorted */
+static int convex_pair(int t1, int t2) {
+  if (t1 == GEOM_PLANE || t1 == GEOM_HFIELD || t2 == GEOM_HFIELD) return 0;
+  if (t2 == GEOM_MESH || t2 == GEOM_ELLIPSOID) return 1;
+  if (t1 == GEOM_ELLIPSOID) return 1;
+  if (t2 == GEOM_CYLINDER) return t1 == GEOM_CAPSULE || t1 == GEOM_CYLINDER;
+  if (t1 == GEOM_CYLINDER && t2 == GEOM_BOX) return 1;
+  return t1 == GEOM_BOX && t2 == GEOM_BOX;
+}
+
 static void collision(const orc_model* m, orc_data* d) {
   *d->ncon = 0;
   *d->ncollision = 0;
@@ -1731,6 +1783,15 @@ static void collision(const orc_model* m, orc_data* d) {
       c.n = 1;
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) { /* collision_primitive.py:1117-1199 */
       capsule_box(&c, p1, n1, s1[0], s1[1], p2, r2, s2);
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_ELLIPSOID) { /* collision_primitive.py:665-733 */
+      c.dist[0] = plane_ellipsoid(c.pos[0], n1, p1, p2, r2, s2);
+      make_frame(c.frame[0], n1);
+      c.n = 1;
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_CYLINDER) { /* collision_primitive.py:882-960 */
+      real nrm[3];
+      c.dist[0] = sphere_cylinder(c.pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]);
+      make_frame(c.frame[0], nrm);
+      c.n = 1;
     } else if (t1 == GEOM_PLANE && t2 == GEOM_MESH) { /* collision_primitive.py:52-277, 810-870 plane_convex */
       real pd[4], pp[4][3], fr[9];
       int md = m->geom_dataid[g2];
@@ -1756,7 +1817,7 @@ static void collision(const orc_model* m, orc_data* d) {
         (*d->ncon)++;
       }
       continue;
-    } else if ((t1 == GEOM_BOX && t2 == GEOM_BOX) || (t2 == GEOM_MESH && (t1 == GEOM_SPHERE || t1 == GEOM_CAPSULE || t1 == GEOM_BOX || t1 == GEOM_MESH))) {
+    } else if (convex_pair(t1, t2)) {
       /* convex (GJK/EPA) pair, collision_convex.py:701-890 */
       ccd_geom cg1, cg2;
       cg1.type = t1; cg2.type = t2;
