@@ -113,16 +113,26 @@ def test_batched_model_fields_accepted():
 
 
 def test_unsupported_features_raise():
+  """Features outside this build raise NotImplementedError at put_model / the compiler, as the reference's
+  io.py:89-144 does (every collision-table pair except heightfields is supported since round 4)."""
   import mujoco_warp_amd as mjw
   from mujoco_warp_amd import mjcf
 
-  ell = mjcf.load_model_from_string('<mujoco><worldbody><body><freejoint/><geom type="ellipsoid" size=".1 .1 .2"/></body></worldbody></mujoco>')
-  with pytest.raises(NotImplementedError):
-    mjw.put_model(ell, device="cpu")
-  # cylinders collide only on the sparse path (plane-cylinder); a dense model with a cylinder pair raises
-  cyl = mjcf.load_model_from_string('<mujoco><worldbody><geom type="plane" size="1 1 .1"/><body><freejoint/><geom type="cylinder" size=".1 .1"/></body></worldbody></mujoco>')
-  with pytest.raises(NotImplementedError):
-    mjw.put_model(cyl, device="cpu")
+  with pytest.raises(NotImplementedError):  # heightfields: not compiled
+    mjcf.load_model_from_string('<mujoco><asset><hfield name="h" nrow="2" ncol="2" size="1 1 .1 .1"/></asset>'
+                                '<worldbody><geom type="hfield" hfield="h"/></worldbody></mujoco>')
+  for flags in ("<flag override=\"enable\"/>", "<flag fwdinv=\"enable\"/>", "<flag midphase=\"disable\"/>"):
+    try:
+      m = mjcf.load_model_from_string(f'<mujoco><option>{flags}</option><worldbody><body><freejoint/><geom size=".1"/></body></worldbody></mujoco>')
+    except (KeyError, ValueError):
+      continue  # the compiler does not know the flag name
+    with pytest.raises(NotImplementedError):
+      mjw.put_model(m, device="cpu")
+  # ellipsoids and cylinders collide with everything of the table now (tests/test_collision_types.py)
+  ell = mjcf.load_model_from_string('<mujoco><worldbody><geom type="plane" size="1 1 .1"/><body><freejoint/><geom type="ellipsoid" size=".1 .1 .2"/></body>'
+                                    '<body pos=".3 0 0"><freejoint/><geom type="cylinder" size=".1 .1"/></body></worldbody></mujoco>')
+  m = mjw.put_model(ell, device="cpu")
+  assert m.nxn_ccd == 3  # plane-ellipsoid, plane-cylinder (pre-pass primitives) and ellipsoid-cylinder (convex)
 
 
 # ---- C ABI ------------------------------------------------------------------------------------
