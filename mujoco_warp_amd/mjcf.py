@@ -48,6 +48,7 @@ from .types import (
   SolverType,
   Stage,
   TrnType,
+  WrapType,
 )
 
 MJ_MINVAL = 1e-15
@@ -1337,16 +1338,20 @@ class _Compiler:
     m.light_dir = np.array([r["dir"] for r in lrows]).reshape(-1, 3)
 
   def _build_tendons(self, root):
-    """<tendon><fixed>: fixed (joint) tendons, length = sum coef * qpos (smooth.py:3085-3121).  The
-    sparse Jacobian structure ten_J_rownnz / _rowadr / _colind lists each tendon's dofs ascending, as
-    MuJoCo's compiler does; spatial tendons are not supported."""
+    """<tendon><fixed>: fixed (joint) tendons, length = sum coef * qpos (smooth.py:3085-3121); <tendon><spatial>:
+    paths through sites, wrapping around sphere / cylinder geoms (optional sidesite) and split by pulleys
+    (smooth.py:3172-3465).  The sparse Jacobian structure ten_J_rownnz / _rowadr / _colind lists each
+    tendon's dofs ascending: the wrap joints' dofs (fixed), every dof on the kinematic chains of the path's
+    bodies (spatial)."""
     m = self.m
     name2jnt = {n: i for i, n in enumerate(m.jnt_names) if n}
+    name2site = {n: i for i, n in enumerate(m.site_names) if n}
+    name2geom = {n: i for i, n in enumerate(m.geom_names) if n}
     rows, wraps = [], []
     for ten in root.findall("tendon"):
       for el in ten:
-        if el.tag != "fixed":
-          raise NotImplementedError(f"<tendon><{el.tag}> is not supported (fixed tendons only)")
+        if el.tag not in ("fixed", "spatial"):
+          raise NotImplementedError(f"<tendon><{el.tag}> is not supported")
         a = dict(self.defaults[el.get("class", "main")].attrs.get("tendon", {}))
         a.update(el.attrib)
 
@@ -1358,12 +1363,35 @@ class _Compiler:
 
         adr = len(wraps)
         for j in el:
-          if j.tag != "joint":
-            raise NotImplementedError(f"<fixed><{j.tag}> is not supported")
-          jid = name2jnt[j.get("joint")]
-          if m.jnt_type[jid] not in (JointType.HINGE, JointType.SLIDE):
-            raise ValueError("fixed tendon joints must be hinge or slide joints")
-          wraps.append((jid, float(j.get("coef", 1.0))))
+          if el.tag == "fixed":
+            if j.tag != "joint":
+              raise NotImplementedError(f"<fixed><{j.tag}> is not supported")
+            jid = name2jnt[j.get("joint")]
+            if m.jnt_type[jid] not in (JointType.HINGE, JointType.SLIDE):
+              raise ValueError("fixed tendon joints must be hinge or slide joints")
+            wraps.append((WrapType.JOINT, jid, float(j.get("coef", 1.0))))
+          elif j.tag == "site":  # spatial tendon path (smooth.py:3172-3465): sites, wrap geoms, pulleys
+            wraps.append((WrapType.SITE, name2site[j.get("site")], 0.0))
+          elif j.tag == "geom":
+            g = name2geom[j.get("geom")]
+            gt = {GeomType.SPHERE: WrapType.SPHERE, GeomType.CYLINDER: WrapType.CYLINDER}.get(int(m.geom_type[g]))
+            if gt is None:
+              raise ValueError("spatial tendons wrap spheres and cylinders only")
+            wraps.append((gt, g, float(name2site[j.get("sidesite")]) if j.get("sidesite") else -1.0))
+          elif j.tag == "pulley":
+            wraps.append((WrapType.PULLEY, -1, float(j.get("divisor", 1.0))))
+          else:
+            raise NotImplementedError(f"<spatial><{j.tag}> is not supported")
+        if el.tag == "spatial":
+          # every pulley-delimited branch runs site ... site, a wrap geom always between two sites
+          kinds = [w[0] for w in wraps[adr:]]
+          for i, k in enumerate(kinds):
+            prv = kinds[i - 1] if i > 0 else WrapType.PULLEY
+            nxt = kinds[i + 1] if i + 1 < len(kinds) else WrapType.PULLEY
+            if k in (WrapType.SPHERE, WrapType.CYLINDER) and not (prv == WrapType.SITE and nxt == WrapType.SITE):
+              raise ValueError("a spatial tendon's wrap geom sits between two sites")
+            if k == WrapType.SITE and prv == WrapType.PULLEY and nxt == WrapType.PULLEY:
+              raise ValueError("a spatial tendon branch needs two sites")
         sl = _floats(a.get("springlength", "-1 -1"))
         rows.append(dict(
           name=a.get("name", ""), adr=adr, num=len(wraps) - adr,
@@ -1394,12 +1422,23 @@ class _Compiler:
     m.tendon_solimp_lim = np.array([r["solimp_lim"] for r in rows]).reshape(nt, 5)
     m.tendon_solref_fri = np.array([r["solref_fri"] for r in rows]).reshape(nt, 2)
     m.tendon_solimp_fri = np.array([r["solimp_fri"] for r in rows]).reshape(nt, 5)
-    m.wrap_type = np.full(len(wraps), 1, dtype=np.int32)  # mjWRAP_JOINT
-    m.wrap_objid = np.array([w[0] for w in wraps], dtype=np.int32)
-    m.wrap_prm = np.array([w[1] for w in wraps], dtype=np.float64)
+    m.wrap_type = np.array([w[0] for w in wraps], dtype=np.int32)
+    m.wrap_objid = np.array([w[1] for w in wraps], dtype=np.int32)
+    m.wrap_prm = np.array([w[2] for w in wraps], dtype=np.float64)
     rownnz, rowadr, colind = [], [], []
     for r in rows:
-      dofs = sorted({int(m.jnt_dofadr[m.wrap_objid[k]]) for k in range(r["adr"], r["adr"] + r["num"])})
+      dofs = set()
+      for k in range(r["adr"], r["adr"] + r["num"]):
+        wt, obj = int(m.wrap_type[k]), int(m.wrap_objid[k])
+        if wt == WrapType.JOINT:
+          dofs.add(int(m.jnt_dofadr[obj]))
+          continue
+        # a spatial tendon moves with every dof on the chains of its sites' and wrap geoms' bodies
+        b = -1 if wt == WrapType.PULLEY else int(m.site_bodyid[obj] if wt == WrapType.SITE else m.geom_bodyid[obj])
+        while b > 0:
+          dofs.update(range(int(m.body_dofadr[b]), int(m.body_dofadr[b]) + int(m.body_dofnum[b])))
+          b = int(m.body_parentid[b])
+      dofs = sorted(dofs)
       rowadr.append(len(colind))
       rownnz.append(len(dofs))
       colind += dofs
@@ -1926,10 +1965,10 @@ def _eig3(I):
 # ---------------------------------------------------------------------------------------------
 
 
-def _kinematics_qpos0(m: MjModel):
+def _kinematics_qpos0(m: MjModel, qpos=None):
   """Forward kinematics + subtree com + cdof + composite inertia + dense qM at qpos0 (fp64)."""
   nb, nv = m.nbody, m.nv
-  qpos = m.qpos0
+  qpos = m.qpos0 if qpos is None else np.asarray(qpos, float)
   xpos = np.zeros((nb, 3))
   xquat = np.tile([1.0, 0, 0, 0], (nb, 1)).astype(float)
   xanchor = np.zeros((m.njnt, 3))
@@ -2024,6 +2063,27 @@ def _kinematics_qpos0(m: MjModel):
   return dict(xpos=xpos, xquat=xquat, xmat=xmat, xipos=xipos, subtree_com=subtree_com, cdof=cdof, M=M)
 
 
+def _spatial_tendon_qpos0(m: MjModel, k: dict, t: int):
+  """Length and Jacobian of spatial tendon t at qpos0 (tendon_geom.py restates smooth.py:3172-3465)."""
+  from .tendon_geom import tendon_length_jac
+
+  xpos, xquat = k["xpos"], k["xquat"]
+  site_xpos = np.array([xpos[b] + rot_vec(xquat[b], m.site_pos[s]) for s, b in enumerate(m.site_bodyid)]).reshape(-1, 3)
+  geom_xpos = np.array([xpos[b] + rot_vec(xquat[b], m.geom_pos[g]) for g, b in enumerate(m.geom_bodyid)]).reshape(-1, 3)
+  geom_xmat = np.array([quat_to_mat(quat_mul(xquat[b], m.geom_quat[g])) for g, b in enumerate(m.geom_bodyid)]).reshape(-1, 3, 3)
+
+  def jac_point(p, b):
+    J = np.zeros((3, m.nv))
+    off = p - k["subtree_com"][m.body_rootid[b]]
+    while b > 0:
+      for d in range(m.body_dofadr[b], m.body_dofadr[b] + m.body_dofnum[b]):
+        J[:, d] = k["cdof"][d, 3:] + np.cross(k["cdof"][d, :3], off)
+      b = m.body_parentid[b]
+    return J
+
+  return tendon_length_jac(m, t, site_xpos, m.site_bodyid, geom_xpos, geom_xmat, jac_point)
+
+
 def _skew(v):
   return np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
 
@@ -2038,10 +2098,13 @@ def set_const(m: MjModel):
   tenJ = np.zeros((nt, nv))
   m.tendon_length0 = np.zeros(nt)
   for t in range(nt):
-    for w in range(m.tendon_adr[t], m.tendon_adr[t] + m.tendon_num[t]):
-      j = m.wrap_objid[w]
-      m.tendon_length0[t] += m.wrap_prm[w] * m.qpos0[m.jnt_qposadr[j]]
-      tenJ[t, m.jnt_dofadr[j]] += m.wrap_prm[w]
+    if m.wrap_type[m.tendon_adr[t]] != WrapType.JOINT:
+      m.tendon_length0[t], tenJ[t] = _spatial_tendon_qpos0(m, k, t)
+    else:
+      for w in range(m.tendon_adr[t], m.tendon_adr[t] + m.tendon_num[t]):
+        j = m.wrap_objid[w]
+        m.tendon_length0[t] += m.wrap_prm[w] * m.qpos0[m.jnt_qposadr[j]]
+        tenJ[t, m.jnt_dofadr[j]] += m.wrap_prm[w]
     if m.tendon_armature[t]:
       M = M + m.tendon_armature[t] * np.outer(tenJ[t], tenJ[t])
   if nt:

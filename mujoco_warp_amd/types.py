@@ -109,6 +109,16 @@ class BiasType(enum.IntEnum):
   USER = 3
 
 
+class WrapType(enum.IntEnum):
+  """Tendon wrap object (types.py:580-595, MuJoCo mjtWrap)."""
+  NONE = 0
+  JOINT = 1
+  PULLEY = 2
+  SITE = 3
+  SPHERE = 4
+  CYLINDER = 5
+
+
 class JointType(enum.IntEnum):
   FREE = 0
   BALL = 1

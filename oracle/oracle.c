@@ -745,11 +745,17 @@ static void solve_m(const orc_model* m, int n, const real* L, const real* y, rea
 /* smooth.py:2041-2147 (_transmission, joint transmissions; dense moment rows) */
 /* smooth.py:3085-3121 (_joint_tendon): fixed tendon length sum coef * qpos, Jacobian coef at the joint's
  * dof, stored in the sparse ten_J layout (ten_J_rowadr / _rownnz / _colind, dofs ascending) */
+static real spatial_tendon(const orc_model* m, orc_data* d, int t);
+
 static void tendon(const orc_model* m, orc_data* d) {
   for (int t = 0; t < m->ntendon; t++) {
     real L = 0;
     const int ra = m->ten_J_rowadr[t], rn = m->ten_J_rownnz[t];
     for (int k = 0; k < rn; k++) d->ten_J[ra + k] = 0;
+    if (m->wrap_type[m->tendon_adr[t]] != 1) { /* spatial: oracle_tendon.h */
+      d->ten_length[t] = spatial_tendon(m, d, t);
+      continue;
+    }
     for (int w = m->tendon_adr[t]; w < m->tendon_adr[t] + m->tendon_num[t]; w++) {
       const int j = m->wrap_objid[w];
       const real prm = m->wrap_prm[w];
@@ -952,6 +958,8 @@ static void r_vec(real* r, const real* R, const real* v) {
   for (int i = 0; i < 3; i++) r[i] = R[3 * i] * v[0] + R[3 * i + 1] * v[1] + R[3 * i + 2] * v[2];
 }
 static real pow4r(real x) { return x * x * x * x; }
+
+#include "oracle_tendon.h"
 
 /* passive.py:42-59 */
 static void fluid_semiaxes(int type, const real* size, real* s) {
@@ -2577,7 +2585,7 @@ static void fwd_velocity(const orc_model* m, orc_data* d) {
   com_vel(m, d);
   passive(m, d);
   rne(m, d);
-  /* tendon_bias (smooth.py:1810-1905): armature * J * (dJ/dt qvel) vanishes for fixed tendons */
+  tendon_bias(m, d, d->qfrc_bias); /* smooth.py:1878-1932; zero for fixed tendons */
 }
 
 /* support.py:38-64 next_act */

@@ -100,7 +100,7 @@ typedef ORC_REAL real;
   X(flex_edge, nflexedge * 2) X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata)          \
   X(flex_elemedge, nflexelem * 3) X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom) \
   X(tendon_adr, ntendon) X(tendon_num, ntendon) X(tendon_limited, ntendon) X(tendon_actfrclimited, ntendon) \
-  X(wrap_objid, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)
+  X(wrap_objid, nwrap) X(wrap_type, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)
 
 /* ---- per-world data: real arrays (name, element count per world) ---- */
 #define ORC_DATA_REAL_ARRAYS(X)                                                                    \

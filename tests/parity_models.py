@@ -227,6 +227,12 @@ def report(name):
   out["fields"]["qacc_smooth"] = err(np_(d.qacc_smooth), od.qacc_smooth)
   out["qacc_smooth_backward"] = bw
   out["force_scale"] = float(np.abs(od.qfrc_smooth).max())
+  # qfrc_smooth = passive - bias + actuator: when the summands cancel (gravity compensation against the gravity
+  # bias) fp32 rounding of the summands, not of the result, bounds its error
+  summ = max(float(np.abs(od.qfrc_bias).max()), float(np.abs(od.qfrc_passive).max()), out["force_scale"])
+  out["cancel_scale"] = max(1.0, summ / (out["force_scale"] + 1e-300))
+  # qacc_smooth = M^-1 qfrc_smooth: its forward error carries cond(M) times the (checked) residual
+  out["cond_M"] = max(float(np.linalg.cond(od.qM[w].reshape(nv, nv))) for w in range(nworld))
   # rows
   counts_equal = all(int(d.nefc[w]) == int(od.nefc[w, 0]) for w in range(nworld))
   out["rows_counts_equal"] = bool(counts_equal)

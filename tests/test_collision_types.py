@@ -137,7 +137,7 @@ def _match(mjm, d, od, w, tol_d, tol_p, tol_n):
     og = sorted(od.con_geom[w, 2 * i:2 * i + 2])
     ok = [j for j in range(len(sel)) if j not in used and sorted(gg[j]) == og and abs(gd[j] - od.con_dist[w, i]) <= tol_d
           and np.abs(gp[j] - od.con_pos[w, 3 * i:3 * i + 3]).max() <= tol_p and np.abs(gf[j, :3] - od.con_frame[w, 9 * i:9 * i + 3]).max() <= tol_n]
-    assert ok, (i, od.con_dist[w, i], od.con_pos[w, 3 * i:3 * i + 3], gd, gp)
+    assert ok, (i, od.con_dist[w, i], od.con_pos[w, 3 * i:3 * i + 3], od.con_frame[w, 9 * i:9 * i + 3], gd, gp, gf[:, :3])
     used.add(ok[0])
 
 
@@ -181,4 +181,8 @@ def test_gpu_convex_pairs_match_oracle(pair, sparse):
     qpos[:, 7 * b + 3:7 * b + 7] = q / np.linalg.norm(q, axis=1, keepdims=True)
   od = _oracle_contacts(mjm, qpos)
   assert int(od.ncon.sum()) > 0  # some orientations collide
-  _gpu_vs_oracle(mjm, qpos, sparse, (2e-5, 2e-4, 2e-3))
+  # smooth supports (ellipsoid, cylinder): EPA's witness point / normal come off a polytope face whose choice
+  # differs between fp32 and fp64 once depth has converged; the depth still agrees to ~1e-6.  The reference
+  # accepts rtol 5e-2 / atol 1e-2 against MuJoCo C for these (collision_driver_test.py:567-569).
+  tol = (2e-5, 2e-3, 5e-2) if (4 in pair or 5 in pair) else (2e-5, 2e-4, 2e-3)
+  _gpu_vs_oracle(mjm, qpos, sparse, tol)
