@@ -3806,6 +3806,21 @@ int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* s
 /* collision_primitive_core_test.py: sphere_triangle (gt = SPHERE), box_triangle, capsule_triangle and
  * cylinder_triangle (collision_primitive_core.py:1518-1990); capsule / cylinder take their axis from column
  * 2 of `gr`.  out = 2 x (dist, pos[3], normal[3]); returns the number of candidates. */
+/* util_misc.py:30-450 known-answer entry: fn 0 is_intersect(a[0:2], a[2:4], a[4:6], a[6:8]) -> out[0];
+ * 1 length_circle(a[0:2], a[2:4], ind, radius) -> out[0]; 2 wrap_circle(end a[0:4], side a[4:6], radius);
+ * 3 wrap_inside(end a[0:4], radius); 4 wrap(x0 a[0:3], x1 a[3:6], pos a[6:9], mat a[9:18], radius, ind = type,
+ * side a[18:21]).  2-4 write (length, point0, point1) to out. */
+int orc_kat_wrap(int fn, const real* a, int ind, real radius, real* out) {
+  switch (fn) {
+    case 0: out[0] = wrap_is_intersect(a, a + 2, a + 4, a + 6); return 0;
+    case 1: out[0] = wrap_length_circle(a, a + 2, ind, radius); return 0;
+    case 2: out[0] = wrap_circle(a, a + 4, radius, out + 1, out + 3); return 0;
+    case 3: out[0] = wrap_inside(a, radius, out + 1, out + 3); return 0;
+    case 4: out[0] = wrap_geom(a, a + 3, a + 6, a + 9, radius, ind, a + 18, out + 1, out + 4); return 0;
+  }
+  return -1;
+}
+
 int orc_kat_geom_triangle(int gt, const real* gp, const real* gr, const real* gs, const real* tri, real tr, real* out) {
   const real* t[3] = {tri, tri + 3, tri + 6};
   real ax[3] = {gr[2], gr[5], gr[8]};

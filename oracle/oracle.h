@@ -178,6 +178,7 @@ real orc_halton(int index, int base);
 /* collision KATs (collision_gjk_test.py, collision_primitive_core_test.py) */
 int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* size, const real* mesh_vert, const int* vertadr,
                 const int* vertnum, real margin, real tolerance, int iterations, int multiccd, real* out);
+int orc_kat_wrap(int fn, const real* a, int ind, real radius, real* out);
 int orc_kat_geom_triangle(int gt, const real* gp, const real* gr, const real* gs, const real* tri, real tr, real* out);
 void orc_ctrl_noise(const orc_model* m, real* ctrl, const real* center, int ncenter, int step, real std,
                     real rate, int nworld, int world_offset);

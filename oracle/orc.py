@@ -295,6 +295,24 @@ def kat_ccd(types, pos, mat, size, margin, tolerance, iterations, multiccd, mesh
   return n, float(out[0]), out[1:4].copy(), out[4:7].copy()
 
 
+def kat_wrap(fn, args, ind=0, radius=0.0, real_bits=64):
+  """util_misc_test.py on the oracle: fn 'is_intersect' | 'length_circle' | 'wrap_circle' | 'wrap_inside' | 'wrap'."""
+  lib = _lib(real_bits)
+  creal = ctypes.c_double if real_bits == 64 else ctypes.c_float
+  dt = np.float64 if real_bits == 64 else np.float32
+  k = ["is_intersect", "length_circle", "wrap_circle", "wrap_inside", "wrap"].index(fn)
+  a = np.ascontiguousarray(np.concatenate([np.ravel(x) for x in args]), dtype=dt)
+  out = np.zeros(7, dt)
+  f = lib.orc_kat_wrap
+  f.restype = ctypes.c_int
+  assert f(ctypes.c_int(k), a.ctypes.data_as(ctypes.POINTER(creal)), ctypes.c_int(int(ind)), creal(radius),
+           out.ctypes.data_as(ctypes.POINTER(creal))) == 0
+  if k < 2:
+    return float(out[0])
+  n = 2 if k < 4 else 3
+  return float(out[0]), out[1:1 + n].copy(), out[1 + n:1 + 2 * n].copy()
+
+
 def kat_geom_triangle(gt, gp, gr, gs, tri, tr, real_bits=64):
   """collision_primitive_core_test.py on the oracle: (n, out[2, 7] = dist, pos, normal)."""
   lib = _lib(real_bits)
