@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 22
+#define MJW_ABI_VERSION 23
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -45,7 +45,7 @@
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
-  X(npair) X(ngravcomp) X(has_fluid)
+  X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -71,7 +71,7 @@
   X(light_pos0, nlight * 3) X(light_dir0, nlight * 3)                                              \
   X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
   X(actuator_ctrlrange, nu * 2) X(actuator_forcerange, nu * 2) X(actuator_actrange, nu * 2)       \
-  X(actuator_gear, nu * 6) X(actuator_acc0, nu) X(actuator_lengthrange, nu * 2)                   \
+  X(actuator_gear, nu * 6) X(actuator_acc0, nu) X(actuator_lengthrange, nu * 2) X(actuator_cranklength, nu)                   \
   X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)                               \
   X(sensor_cutoff, nsensor)                                                                        \
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
@@ -82,7 +82,7 @@
   X(tendon_armature, ntendon) X(tendon_margin, ntendon) X(tendon_range, ntendon * 2)               \
   X(tendon_lengthspring, ntendon * 2) X(tendon_solref_lim, ntendon * 2) X(tendon_solimp_lim, ntendon * 5) \
   X(tendon_solref_fri, ntendon * 2) X(tendon_solimp_fri, ntendon * 5) X(tendon_invweight0, ntendon)  \
-  X(tendon_actfrcrange, ntendon * 2) X(wrap_prm, nwrap)                                            \
+  X(tendon_actfrcrange, ntendon * 2) X(wrap_prm, nwrap) X(wrap_pulley_scale, nwrap)                                          \
   X(pair_solref, npair * 2) X(pair_solreffriction, npair * 2) X(pair_solimp, npair * 5)           \
   X(pair_margin, npair) X(pair_gap, npair) X(pair_friction, npair * 5)
 
@@ -118,7 +118,7 @@
   X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)                                     \
   X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)                            \
   X(tendon_adr, ntendon) X(tendon_num, ntendon) X(tendon_limited, ntendon) X(tendon_actfrclimited, ntendon) \
-  X(wrap_objid, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)
+  X(wrap_objid, nwrap) X(wrap_type, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)
 
 /* ---- data: float arrays, (nworld, count) world-major like mujoco_warp types.Data ----
  * Sparse models (is_sparse, the reference's io.py:67-74 switch) store qM / qLD as (nworld, nM) rows of

@@ -33,7 +33,7 @@ enum : int {
   DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512, DSBL_ACTUATION = 2048,
   DSBL_REFSAFE = 4096, DSBL_SENSOR = 8192, DSBL_EULERDAMP = 1 << 15
 };
-enum : int { TRN_JOINT = 0, TRN_JOINTINPARENT = 1, TRN_TENDON = 3 };
+enum : int { TRN_JOINT = 0, TRN_JOINTINPARENT = 1, TRN_SLIDERCRANK = 2, TRN_TENDON = 3, TRN_SITE = 4, TRN_BODY = 5 };
 enum : int { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum : int { DATATYPE_REAL = 0, DATATYPE_POSITIVE = 1 };
 enum : int { STAGE_POS = 1, STAGE_VEL = 2, STAGE_ACC = 3 };

@@ -826,7 +826,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
             int q = i;
             while (q > j) q = m.dof_parentid[q];
             if (q != j || i >= 32) continue;
-            const float v = dt * tdamp[t] * ten_coef(m, wid, t, i) * ten_coef(m, wid, t, j);
+            const float v = dt * tdamp[t] * ten_coef(m, d, wid, t, i) * ten_coef(m, d, wid, t, j);
             S[i * DSS + j] += v;
             if (i != j) S[j * DSS + i] += v;
           }

@@ -17,6 +17,7 @@
 #include "mjw_narrow.h"
 #include "mjw_passive.h"
 #include "mjw_tendon.h"
+#include "mjw_trn.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -94,7 +95,7 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
   L.rowcon = -1;
   // moment slots per actuator: 1 when every transmission has one non-zero (nJmom == nu: hinge / slide
   // joints), else 6 (free / ball joints)
-  L.amax = m.nJmom == nu ? 1 : (m.ten_maxnnz > 6 ? m.ten_maxnnz : 6);
+  L.amax = m.nJmom == nu ? 1 : (m.act_maxnnz > 6 ? m.act_maxnnz : 6);
   L.act_len = take(nu); L.act_vel = take(nu); L.act_force = take(nu); L.act_mom = take(nu * L.amax); L.act_momdof = take(nu * L.amax);
   L.act_nnz = take(nu);
   L.scratch = take(64);
@@ -521,7 +522,7 @@ __device__ __forceinline__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d
     }
   }
   WSYNC();
-  if (TEN && m.ntendon) tendon_armature(m, M, nvs, wid, lane);  // smooth.py:916-1000
+  if (TEN && m.ntendon) tendon_armature(m, d, M, nvs, wid, lane);  // smooth.py:916-1000
   const int np = m.nv_pad;
   float* gM = d.qM + (long)wid * np * np;
   for (int e = lane; e < np * np; e += LPW) {
@@ -841,7 +842,7 @@ __device__ __forceinline__ int tendon_rows(const mjw_model_t& m, const mjw_data_
     if (t < m.ntendon) {
       if (limit) {
         if (m.tendon_limited[t]) {
-          const float len = ten_len(m, wid, s + L.qpos, t);
+          const float len = ten_len(m, d, wid, s + L.qpos, t);
           const float dmn = len - trng[2 * t], dmx = trng[2 * t + 1] - len;
           tm = tmar[t];
           pos = fminf(dmn, dmx) - tm;
@@ -856,12 +857,12 @@ __device__ __forceinline__ int tendon_rows(const mjw_model_t& m, const mjw_data_
     int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
     int r = nefc + added + rank;
     if (act && r < njmax) {
-      for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, k < nv ? scl * ten_coef(m, wid, t, k) : 0.0f);
+      for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, k < nv ? scl * ten_coef(m, d, wid, t, k) : 0.0f);
       if (limit)
-        efc_row(m, d, L, s, wid, r, pos, pos, tiw[t], tsr + 2 * t, tsi + 5 * t, tm, scl * ten_vel(m, wid, qvel, t), 0.0f,
+        efc_row(m, d, L, s, wid, r, pos, pos, tiw[t], tsr + 2 * t, tsi + 5 * t, tm, scl * ten_vel(m, d, wid, qvel, t), 0.0f,
                 CNSTR_LIMIT_TENDON, t);
       else
-        efc_row(m, d, L, s, wid, r, 0.0f, 0.0f, tiw[t], tsr + 2 * t, tsi + 5 * t, 0.0f, ten_vel(m, wid, qvel, t), tfl[t],
+        efc_row(m, d, L, s, wid, r, 0.0f, 0.0f, tiw[t], tsr + 2 * t, tsi + 5 * t, 0.0f, ten_vel(m, d, wid, qvel, t), tfl[t],
                 CNSTR_FRICTION_TENDON, t);
     }
     added += __popcll(bal);
@@ -1058,7 +1059,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         const int t = base + lane;
         bool act = false;
         if (t < m.ntendon && m.tendon_limited[t]) {
-          const float len = ten_len(m, wid, s + L.qpos, t);
+          const float len = ten_len(m, d, wid, s + L.qpos, t);
           act = fminf(len - trng[2 * t], trng[2 * t + 1] - len) - tmar[t] < 0.0f;
         }
         cnt += __popcll(__ballot(act));
@@ -1336,6 +1337,9 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
         int condim = reci[28] & 0xff;
         int r0 = si[L.iscratch + cc];
         float pos = rec[0] - rec[1];
+        if (TEN && m.nbodytrn && (POOL || gbase + cc < d.naconmax) && reci[29] >= 0 && reci[30] >= 0)  // smooth.py:2448-2602
+          body_trn_contact(m, s + L.subtree_com, s + L.cdof, rec + 2, rec + 5, reci[22] & 0xffff, reci[22] >> 16, s + L.act_mom, si + L.act_nnz,
+                           L.amax, lane);
         if (!(pos < 0.0f) || (!POOL && gbase + cc >= d.naconmax)) continue;
         int nr = condim == 1 ? 1 : (ell ? condim : 2 * (condim - 1));
         const int b1 = reci[21] & 0xffff, b2 = reci[21] >> 16;
@@ -1468,8 +1472,11 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
     const int a = a0 + lane;
     int my_nnz = 0;
     if (a < m.nu) {
-      if (TEN && m.actuator_trntype[a] == TRN_TENDON) {
+      const int tt = m.actuator_trntype[a];
+      if (TEN && tt == TRN_TENDON) {
         my_nnz = m.ten_J_rownnz[m.actuator_trnid[2 * a]];
+      } else if (TEN && (tt == TRN_SITE || tt == TRN_SLIDERCRANK || tt == TRN_BODY)) {
+        my_nnz = trn_site_nnz(m, a);
       } else {
         const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
         my_nnz = jt0 == JNT_FREE ? 6 : (jt0 == JNT_BALL ? 3 : 1);
@@ -1484,7 +1491,7 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
     if (TEN && trn == TRN_TENDON) {
       // smooth.py:2244-2260: length = ten_length gear0, moment row = gear0 ten_J (the tendon's dofs)
       const int t = m.actuator_trnid[2 * a];
-      const float length = ten_len(m, wid, s + L.qpos, t) * gear[0];
+      const float length = ten_len(m, d, wid, s + L.qpos, t) * gear[0];
       const int nnz = my_nnz;
       s[L.act_len + a] = length;
       si[L.act_nnz + a] = nnz;
@@ -1494,7 +1501,7 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
       d.moment_rowadr[gu] = rowadr;
       for (int k = 0; k < L.amax; k++) {
         const int dof = k < nnz ? m.ten_J_colind[m.ten_J_rowadr[t] + k] : 0;
-        const float mk = k < nnz ? gear[0] * ten_coef(m, wid, t, dof) : 0.0f;
+        const float mk = k < nnz ? gear[0] * ten_coef(m, d, wid, t, dof) : 0.0f;
         s[L.act_mom + L.amax * a + k] = mk;
         si[L.act_momdof + L.amax * a + k] = dof;
         if (k < nnz) {
@@ -1502,6 +1509,35 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
           d.moment_colind[(long)wid * m.nJmom + rowadr + k] = dof;
         }
       }
+      continue;
+    }
+    if (TEN && (trn == TRN_SITE || trn == TRN_SLIDERCRANK || trn == TRN_BODY)) {
+      const long gu = (long)wid * m.nu + a;
+      float* mom = s + L.act_mom + L.amax * a;
+      int* momdof = si + L.act_momdof + L.amax * a;
+      float* gm = d.actuator_moment + (long)wid * m.nJmom + rowadr;
+      int* gc = d.moment_colind + (long)wid * m.nJmom + rowadr;
+      float length = 0.0f;
+      if (trn == TRN_BODY) {  // smooth.py:2597-2602: the contact sum (collision stage) over -ncon
+        const int ncon = si[L.act_nnz + a];
+        const float sc = ncon > 0 ? -1.0f / (float)ncon : 0.0f;
+        for (int i = 0; i < my_nnz; i++) {
+          const float v = ncon > 0 ? mom[i] * sc : 0.0f;
+          mom[i] = v;
+          momdof[i] = i;
+          gm[i] = v;
+          gc[i] = i;
+        }
+      } else {
+        length = trn_site(m, wid, a, my_nnz, d.site_xpos + (long)wid * m.nsite * 3, d.site_xmat + (long)wid * m.nsite * 9, s + L.xquat,
+                          s + L.subtree_com, s + L.cdof, mom, momdof, gm, gc);
+      }
+      for (int k = my_nnz; k < L.amax; k++) { mom[k] = 0.0f; momdof[k] = 0; }
+      s[L.act_len + a] = length;
+      si[L.act_nnz + a] = my_nnz;
+      d.actuator_length[gu] = length;
+      d.moment_rownnz[gu] = my_nnz;
+      d.moment_rowadr[gu] = rowadr;
       continue;
     }
     int j = m.actuator_trnid[2 * a];
@@ -1726,6 +1762,13 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
     d.qfrc_passive[gi] = p;
     if (TEN) spring[i] = gcomp;  // kept for the actuation stage of this launch (L.vec is free until the solver)
   }
+  // smooth.py:1878-1932 tendon_bias: armature J (Jdot qvel) of the spatial tendons, kept in damper[] (free
+  // after the passive forces) until qfrc_bias is written; needs cvel before rne reuses its slot
+  const bool ten_bias = TEN && m.nten_spatial;
+  if (ten_bias) {
+    const TenFrames f{d.site_xpos + (long)wid * m.nsite * 3, nullptr, nullptr, s + L.subtree_com, s + L.cdof};
+    tendon_bias(m, d, wid, lane, qvel, f, cvel, cdof_dot, s + L.scratch, damper);
+  }
   // rne (smooth.py:1112-1274, flg_acc = False): cacc[b] = cacc[parent] + sum cdof_dot qvel
   for (int b = lane; b < m.nbody; b += LPW) {
     float acc[6] = {0, 0, 0, 0, 0, 0};
@@ -1781,6 +1824,7 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
     const float* cd = s + L.cdof + 6 * i;
     const float* ci = s + L.cvel + 6 * b;
     float v = cd[0] * ci[0] + cd[1] * ci[1] + cd[2] * ci[2] + cd[3] * ci[3] + cd[4] * ci[4] + cd[5] * ci[5];
+    if (ten_bias) v += damper[i];
     s[L.qfrc_bias + i] = v;
     d.qfrc_bias[(long)wid * nv + i] = v;
   }
@@ -2258,7 +2302,7 @@ __device__ __forceinline__ void euler(const mjw_model_t& m, const mjw_data_t& d,
           int a = i;
           while (a > j) a = m.dof_parentid[a];
           if (a != j) continue;
-          const float v = dt * tdamp[t] * ten_coef(m, wid, t, i) * ten_coef(m, wid, t, j);
+          const float v = dt * tdamp[t] * ten_coef(m, d, wid, t, i) * ten_coef(m, d, wid, t, j);
           Lm[i * nvs + j] += v;
           if (i != j) Lm[j * nvs + i] += v;
         }
@@ -2416,9 +2460,17 @@ __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_
     PROF_MARK(PH_COM);
     camlight(m, d, L, w);
     PROF_MARK(PH_CAM);
-    if (TEN && m.ntendon) tendon_pos(m, d, w.s + L.qpos, w.wid, w.lane);  // smooth.py:3085-3121 (fwd_position: before crb)
+    if (TEN && m.ntendon) {  // smooth.py:3085-3465 (fwd_position: before crb)
+      const TenFrames f{d.site_xpos + (long)w.wid * m.nsite * 3, w.s + L.gxpos, w.s + L.gxmat, w.s + L.subtree_com, w.s + L.cdof};
+      tendon_pos(m, d, w.s + L.qpos, f, w.wid, w.lane);
+      WSYNC();  // spatial rows are read back by other lanes from here on
+    }
     crb_qM<TEN>(m, d, L, w);
     PROF_MARK(PH_CRB);
+    if (TEN && m.nbodytrn) {  // BODY transmissions accumulate over the contacts as they are staged
+      body_trn_init(m, w.s + L.act_mom, w.si + L.act_nnz, L.amax, w.lane);
+      WSYNC();
+    }
     collision_and_constraints<BOX, TEN, (STAGES & ST_POOL) != 0>(m, d, L, w);
     PROF_MARK(PH_COLL);
     transmission<TEN>(m, d, L, w);
@@ -2725,7 +2777,7 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
   // position-stage kernels without the tendon / muscle paths, and without the box narrowphase, for
   // models that have none (kernel id: K_FWD + 4 STAGES + 2 BOX + TEN)
   if constexpr ((STAGES & mjw::ST_POS) != 0) {
-    if (m->ntendon == 0 && m->nmuscle == 0 && m->ngravcomp == 0 && !m->has_fluid) {
+    if (m->ntendon == 0 && m->nmuscle == 0 && m->ngravcomp == 0 && !m->has_fluid && m->nbodytrn == 0 && m->nsitetrn == 0) {
       if (m->nxn_box == 0) {
         hipLaunchKernelGGL((mjw::mjw_kernel<STAGES, false, false>), dim3(count), dim3(64), lds, s, *m, *d, L, w0);
         mjw::trace_launch(s, mjw::K_FWD + 4 * STAGES);

@@ -190,13 +190,11 @@ def put_model(mjm, device=None) -> types.Model:
     lr = np.asarray(mjm.actuator_lengthrange, np.float64).reshape(-1, 2)[muscle]
     if np.any(lr[:, 0] >= lr[:, 1]):
       raise NotImplementedError("muscle actuators need an actuator_lengthrange (lengthrange attribute, or a limited joint / tendon transmission).")
-  if np.any((mjm.actuator_trntype > types.TrnType.JOINTINPARENT) & (mjm.actuator_trntype != types.TrnType.TENDON)):
-    raise NotImplementedError("only joint and tendon transmissions are supported.")
+  if sparse and np.any((mjm.actuator_trntype > types.TrnType.JOINTINPARENT) & (mjm.actuator_trntype != types.TrnType.TENDON)):
+    raise NotImplementedError("sparse / flex models: only joint and tendon transmissions are supported by this build yet.")
   ntendon = int(getattr(mjm, "ntendon", 0))
   if ntendon and sparse:
     raise NotImplementedError("sparse / flex models: tendons are not supported by this build yet.")
-  if ntendon and np.any(np.asarray(mjm.wrap_type) != 1):
-    raise NotImplementedError("only fixed (joint) tendons are supported by this build yet.")
   if (mjm.opt.viscosity > 0 or mjm.opt.density > 0) and mjm.opt.integrator in (types.IntegratorType.IMPLICITFAST, types.IntegratorType.IMPLICIT):
     raise NotImplementedError("Implicit integrators and fluid model not implemented.")  # io.py:126-130
 
@@ -233,6 +231,13 @@ def put_model(mjm, device=None) -> types.Model:
   m.npair = int(getattr(mjm, "npair", 0))
   m.nwrap, m.nJten = int(getattr(mjm, "nwrap", 0)), int(getattr(mjm, "nJten", 0))
   m.ten_maxnnz = int(np.max(mjm.ten_J_rownnz)) if m.ntendon else 0  # the reference's max_ten_J_rownnz (io.py:232)
+  # spatial tendons (smooth.py:3172-3465): their count selects the per-world length / Jacobian path; the
+  # pulley divisor of each wrap (io.py:491-497)
+  wrap_type = np.asarray(getattr(mjm, "wrap_type", np.zeros(0)), dtype=np.int32)
+  m.nten_spatial = int(sum(wrap_type[mjm.tendon_adr[t]] != types.WrapType.JOINT for t in range(m.ntendon)))
+  from .tendon_geom import pulley_scale
+
+  wrap_pulley_scale = pulley_scale(mjm) if m.nwrap else np.zeros(0)
   m.nmuscle = int(np.sum(_muscle_mask(mjm)))  # > 0 selects the forward kernel compiled with the muscle paths
   # gravity compensation and fluid forces (passive.py:246-533; io.py:230, :2218-2219); either selects the
   # forward kernel's extended instantiation, as tendons and muscles do
@@ -299,12 +304,11 @@ def put_model(mjm, device=None) -> types.Model:
   m.nlimited = len(jnt_limited_sh)
   m.nlimited_ball = len(jnt_limited_ball)
   m.neq_cw = int(np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD)).sum()) if mjm.neq else 0
-  def _mom_nnz(a):
-    if int(mjm.actuator_trntype[a]) == types.TrnType.TENDON:
-      return int(mjm.ten_J_rownnz[mjm.actuator_trnid[a, 0]])
-    return {JointType.FREE: 6, JointType.BALL: 3}.get(int(mjm.jnt_type[mjm.actuator_trnid[a, 0]]), 1)
+  m.act_maxnnz = max([_mom_nnz(mjm, a) for a in range(mjm.nu)] + [0])
+  m.nbodytrn = int(np.sum(np.asarray(mjm.actuator_trntype) == types.TrnType.BODY)) if mjm.nu else 0  # the reference's nacttrnbody
+  m.nsitetrn = int(np.isin(np.asarray(mjm.actuator_trntype), (types.TrnType.SITE, types.TrnType.SLIDERCRANK)).sum()) if mjm.nu else 0
 
-  m.nJmom = int(sum(_mom_nnz(a) for a in range(mjm.nu)))
+  m.nJmom = int(sum(_mom_nnz(mjm, a) for a in range(mjm.nu)))
 
   # sparse path: kinematic trees as dof ranges (a tree starts at every dof without a parent dof),
   # J row width = the longest union of two dof chains (+ the 6 dofs of a flex edge)
@@ -380,7 +384,7 @@ def put_model(mjm, device=None) -> types.Model:
     grp, attr = _model_attr(name)
     if grp is not None:
       continue
-    val = np.asarray(getattr(mjm, attr), dtype=np.float64)
+    val = np.asarray(wrap_pulley_scale if name == "wrap_pulley_scale" else getattr(mjm, attr), dtype=np.float64)
     setattr(m, attr, _f32(val.reshape((1,) + val.shape), dev))
   for name, cnt in _lib.MODEL_INT_ARRAYS:
     if name in derived_int or name in ("nxn_geom_pair", "nxn_pairid", "nxn_ccdid"):
@@ -395,6 +399,33 @@ def put_model(mjm, device=None) -> types.Model:
   return m
 
 
+def _mom_nnz(mjm, a) -> int:
+  """Non-zeros of actuator a's moment row, as smooth.py:2042-2442 counts them: the joint's dofs, the tendon's
+  Jacobian row, the union of the two sites' weld-body dof chains (SLIDERCRANK; SITE with a reference site stops
+  at their common ancestor dof), one site's chain (SITE), or every dof (BODY)."""
+  trn, (i1, i2) = int(mjm.actuator_trntype[a]), mjm.actuator_trnid[a]
+  if trn == types.TrnType.TENDON:
+    return int(mjm.ten_J_rownnz[i1])
+  if trn == types.TrnType.BODY:
+    return int(mjm.nv)
+  if trn in (types.TrnType.SITE, types.TrnType.SLIDERCRANK):
+    last = lambda s_: (lambda b: mjm.body_dofadr[b] + mjm.body_dofnum[b] - 1 if b > 0 else -1)(mjm.body_weldid[mjm.site_bodyid[s_]])
+    d1 = last(i1)
+    d2 = last(i2) if i2 >= 0 else -1
+    n = 0
+    while d1 >= 0 or d2 >= 0:
+      da = max(d1, d2)
+      if trn == types.TrnType.SITE and i2 >= 0 and d1 == da and d2 == da:
+        break
+      n += 1
+      if d1 == da:
+        d1 = mjm.dof_parentid[d1]
+      if d2 == da:
+        d2 = mjm.dof_parentid[d2]
+    return n
+  return {JointType.FREE: 6, JointType.BALL: 3}.get(int(mjm.jnt_type[i1]), 1)
+
+
 # derived topology the C views carry beyond the reference Model fields (INTEGRATION.md section 2)
 DERIVED_INT_ARRAYS = {
   "body_subtree_end": "body_subtree_end", "body_level": "body_level", "level_body": "level_body", "level_adr": "level_adr",
@@ -403,7 +434,7 @@ DERIVED_INT_ARRAYS = {
   "tree_dofadr": "tree_dofadr", "flex_cgeomadr": "flex_cgeomadr", "flex_cgeom": "flex_cgeom", "plane_geom": "plane_geom",
   "flexvert_incadr": "flexvert_incadr", "flexvert_inc": "flexvert_inc",
 }
-DERIVED_SCALARS = ("nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle", "sp_nH",
+DERIVED_SCALARS = ("act_maxnnz", "nbodytrn", "nsitetrn", "nten_spatial", "nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle", "sp_nH",
                    "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane")
 
 

@@ -109,7 +109,7 @@ _INTEGRATORS = {
 _SOLVERS = {"pgs": SolverType.PGS, "cg": SolverType.CG, "newton": SolverType.NEWTON}
 _CONES = {"pyramidal": ConeType.PYRAMIDAL, "elliptic": ConeType.ELLIPTIC}
 _JACOBIANS = {"dense": JacobianType.DENSE, "sparse": JacobianType.SPARSE, "auto": JacobianType.AUTO}
-_ACTUATOR_TAGS = ("motor", "position", "velocity", "general", "intvelocity", "damper", "muscle")
+_ACTUATOR_TAGS = ("motor", "position", "velocity", "general", "intvelocity", "damper", "muscle", "adhesion")
 
 # MuJoCo default element attribute values (MJCF reference defaults).
 _GEOM_DEFAULTS = dict(
@@ -1450,6 +1450,7 @@ class _Compiler:
   def _build_actuators(self, root):
     m = self.m
     name2jnt = {n: i for i, n in enumerate(m.jnt_names) if n}
+    name2site = {n: i for i, n in enumerate(getattr(m, "site_names", [])) if n}
     rows = []
     for act in root.findall("actuator"):
       for el in act:
@@ -1502,6 +1503,10 @@ class _Compiler:
           biastype = BiasType.AFFINE
           biasprm[:3] = [0.0, -kp, 0.0]
           dyntype = DynType.INTEGRATOR
+        elif tag == "adhesion":
+          # MuJoCo's <adhesion> shortcut: gain * ctrl through a BODY transmission (smooth.py:2260-2273,
+          # 2448-2602), ctrl limited to [0, ctrlrange[1]]
+          gainprm[0] = float(a.get("gain", 1.0))
         elif tag == "muscle":
           # MuJoCo's <muscle> shortcut: muscle gain / bias / activation with its default curve
           # parameters, gainprm = biasprm = (range[2], force, scale, lmin, lmax, vmax, fpmax, fvmax) and
@@ -1527,8 +1532,14 @@ class _Compiler:
           trntype, trnid = TrnType.JOINTINPARENT, [name2jnt[a["jointinparent"]], -1]
         elif "tendon" in a:
           trntype, trnid = TrnType.TENDON, [m.tendon_names.index(a["tendon"]), -1]
+        elif "cranksite" in a:  # smooth.py:2150-2241
+          trntype, trnid = TrnType.SLIDERCRANK, [name2site[a["cranksite"]], name2site[a["slidersite"]]]
+        elif "site" in a:  # smooth.py:2274-2442
+          trntype, trnid = TrnType.SITE, [name2site[a["site"]], name2site[a["refsite"]] if "refsite" in a else -1]
+        elif "body" in a:  # smooth.py:2260-2273
+          trntype, trnid = TrnType.BODY, [m.body_names.index(a["body"]), -1]
         else:
-          raise NotImplementedError("only joint and tendon transmissions are supported by the MJCF compiler")
+          raise ValueError(f"actuator <{tag}> names no transmission target")
         rows.append(
           dict(
             name=a.get("name", ""),
@@ -1549,6 +1560,7 @@ class _Compiler:
             actrange=actrange,
             actearly=a.get("actearly", "false") == "true",
             lengthrange=_floats(a.get("lengthrange", "0 0"), 2),
+            cranklength=float(a.get("cranklength", 0.0)),
           )
         )
     nu = len(rows)
@@ -1570,7 +1582,7 @@ class _Compiler:
     m.actuator_forcerange = np.array([r["forcerange"] for r in rows]).reshape(nu, 2)
     m.actuator_actrange = np.array([r["actrange"] for r in rows]).reshape(nu, 2)
     m.actuator_actearly = np.array([r["actearly"] for r in rows], dtype=bool)
-    m.actuator_cranklength = np.zeros(nu)
+    m.actuator_cranklength = np.array([r["cranklength"] for r in rows], dtype=np.float64)
     m.actuator_lengthrange = np.array([r["lengthrange"] for r in rows], dtype=np.float64).reshape(nu, 2)
     # muscles need the actuator length range (mj_setLengthRange).  MuJoCo finds it at compile time by
     # simulation; here it is the transmission's limited range times the gear (MuJoCo's `uselimit`
@@ -2084,6 +2096,77 @@ def _spatial_tendon_qpos0(m: MjModel, k: dict, t: int):
   return tendon_length_jac(m, t, site_xpos, m.site_bodyid, geom_xpos, geom_xmat, jac_point)
 
 
+def _site_moment(m: MjModel, k: dict, a: int):
+  """Moment row of a SITE / SLIDERCRANK transmission at the pose of `k` (smooth.py:2150-2241, 2274-2442; the
+  oracle's site_transmission restates the same)."""
+  xpos, xquat = k["xpos"], k["xquat"]
+  sx = lambda s_: xpos[m.site_bodyid[s_]] + rot_vec(xquat[m.site_bodyid[s_]], m.site_pos[s_])
+  sm = lambda s_: quat_to_mat(quat_mul(xquat[m.site_bodyid[s_]], m.site_quat[s_]))
+
+  def jac(p, b, dof):
+    db = m.dof_bodyid[dof]
+    bb, ok = b, db == 0
+    while bb != 0 and not ok:
+      ok = bb == db
+      bb = m.body_parentid[bb]
+    if not ok:
+      return np.zeros(3), np.zeros(3)
+    cd = k["cdof"][dof]
+    return cd[3:] + np.cross(cd[:3], p - k["subtree_com"][m.body_rootid[b]]), cd[:3].copy()
+
+  def last(b):
+    return m.body_dofadr[b] + m.body_dofnum[b] - 1 if b > 0 else -1
+
+  gear = m.actuator_gear[a]
+  i1, i2 = m.actuator_trnid[a]
+  mom = np.zeros(m.nv)
+  if m.actuator_trntype[a] == TrnType.SLIDERCRANK:
+    rod = m.actuator_cranklength[a]
+    axis = sm(i2)[:, 2]
+    vec = sx(i1) - sx(i2)
+    av = vec @ axis
+    det = av * av + rod * rod - vec @ vec
+    if det > 0:
+      sdet = np.sqrt(det)
+      sc = 1 - av / sdet
+      dldv, dlda = axis * sc + vec / sdet, vec * sc
+    else:
+      dldv, dlda = axis, vec
+    d1, d2 = last(m.body_weldid[m.site_bodyid[i1]]), last(m.body_weldid[m.site_bodyid[i2]])
+    while d1 >= 0 or d2 >= 0:
+      da = max(d1, d2)
+      jp2, jr2 = jac(sx(i2), m.site_bodyid[i2], da)
+      jp1, _ = jac(sx(i1), m.site_bodyid[i1], da)
+      mom[da] = (dlda @ np.cross(jr2, axis) + dldv @ (jp1 - jp2)) * gear[0]
+      if d1 == da:
+        d1 = m.dof_parentid[d1]
+      if d2 == da:
+        d2 = m.dof_parentid[d2]
+    return mom
+  if i2 < 0:
+    R = sm(i1)
+    da = last(m.body_weldid[m.site_bodyid[i1]])
+    while da >= 0:
+      jp, jr = jac(sx(i1), m.site_bodyid[i1], da)
+      mom[da] = jp @ (R @ gear[:3]) + jr @ (R @ gear[3:])
+      da = m.dof_parentid[da]
+    return mom
+  R = sm(i2)
+  d1, d2 = last(m.body_weldid[m.site_bodyid[i1]]), last(m.body_weldid[m.site_bodyid[i2]])
+  while d1 >= 0 or d2 >= 0:
+    da = max(d1, d2)
+    if d1 == da and d2 == da:
+      break
+    jp, jr = jac(sx(i1), m.site_bodyid[i1], da)
+    jq, jqr = jac(sx(i2), m.site_bodyid[i2], da)
+    mom[da] = (jp - jq) @ (R @ gear[:3]) + (jr - jqr) @ (R @ gear[3:])
+    if d1 == da:
+      d1 = m.dof_parentid[d1]
+    if d2 == da:
+      d2 = m.dof_parentid[d2]
+  return mom
+
+
 def _skew(v):
   return np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
 
@@ -2204,6 +2287,9 @@ def set_const(m: MjModel):
     j = m.actuator_trnid[a, 0]
     if m.actuator_trntype[a] == TrnType.TENDON:
       acc0[a] = np.linalg.norm(Minv @ (m.actuator_gear[a, 0] * tenJ[j]))
+      continue
+    if m.actuator_trntype[a] in (TrnType.SITE, TrnType.SLIDERCRANK, TrnType.BODY):
+      acc0[a] = np.linalg.norm(Minv @ _site_moment(m, k, a)) if m.actuator_trntype[a] != TrnType.BODY else 0.0
       continue
     t = m.jnt_type[j]
     da = m.jnt_dofadr[j]

@@ -39,7 +39,7 @@ enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2, EQ_FLEX = 4 };
 enum { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum { INTEGRATOR_EULER = 0, INTEGRATOR_RK4 = 1, INTEGRATOR_IMPLICIT = 2, INTEGRATOR_IMPLICITFAST = 3 };
 enum { BIAS_NONE = 0, BIAS_AFFINE = 1, BIAS_MUSCLE = 2 };
-enum { TRN_JOINT = 0, TRN_JOINTINPARENT = 1, TRN_TENDON = 3 };
+enum { TRN_JOINT = 0, TRN_JOINTINPARENT = 1, TRN_SLIDERCRANK = 2, TRN_TENDON = 3, TRN_SITE = 4, TRN_BODY = 5 };
 enum { CNSTR_FRICTION_TENDON = 2, CNSTR_LIMIT_TENDON = 4 };
 enum { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
 
@@ -797,6 +797,140 @@ static void tendon_armature(const orc_model* m, orc_data* d) {
   }
 }
 
+static void rt_vec(real* r, const real* R, const real* v);
+static void r_vec(real* r, const real* R, const real* v);
+
+static int jac_dof(const orc_model* m, const orc_data* d, const real* point, int bodyid, int dofid, real* jacp, real* jacr);
+
+static int last_dof(const orc_model* m, int body) { return body > 0 ? m->body_dofadr[body] + m->body_dofnum[body] - 1 : -1; }
+
+/* smooth.py:2150-2241 (SLIDERCRANK) and 2274-2442 (SITE): moments over the union of the two bodies' dof
+ * chains (SITE with a reference site: above their common ancestor dof only) */
+static void site_transmission(const orc_model* m, orc_data* d, int a, real* mom) {
+  const real* gear = m->actuator_gear + 6 * a;
+  const int trn = m->actuator_trntype[a], id = m->actuator_trnid[2 * a], id2 = m->actuator_trnid[2 * a + 1];
+  const real* sx = d->site_xpos + 3 * id;
+  real jp[3], jr[3], jp2[3], jr2[3];
+  if (trn == TRN_SLIDERCRANK) {
+    const real rod = m->actuator_cranklength[a];
+    const real* sm = d->site_xmat + 9 * id2;
+    const real* sx2 = d->site_xpos + 3 * id2;
+    real axis[3] = {sm[2], sm[5], sm[8]}, vec[3] = {sx[0] - sx2[0], sx[1] - sx2[1], sx[2] - sx2[2]};
+    real av = dot3(vec, axis), det = av * av + rod * rod - dot3(vec, vec), sdet = 0, length = av;
+    const int ok = det > 0;
+    if (ok) { sdet = sqrt(det); length = av - sdet; }
+    d->actuator_length[a] = length * gear[0];
+    real dldv[3], dlda[3];
+    for (int i = 0; i < 3; i++) {
+      if (ok) {
+        const real sc = 1 - safe_div(av, sdet);
+        dldv[i] = axis[i] * sc + safe_div(vec[i], sdet);
+        dlda[i] = vec[i] * sc;
+      } else {
+        dldv[i] = axis[i];
+        dlda[i] = vec[i];
+      }
+    }
+    int da1 = last_dof(m, m->body_weldid[m->site_bodyid[id]]), da2 = last_dof(m, m->body_weldid[m->site_bodyid[id2]]);
+    while (da1 >= 0 || da2 >= 0) {
+      const int da = da1 > da2 ? da1 : da2;
+      real jacA[3], jac[3];
+      jac_dof(m, d, sx2, m->site_bodyid[id2], da, jp2, jr2);
+      cross3(jacA, jr2, axis);
+      jac_dof(m, d, sx, m->site_bodyid[id], da, jp, jr);
+      for (int i = 0; i < 3; i++) jac[i] = jp[i] - jp2[i];
+      mom[da] = (dot3(dlda, jacA) + dot3(dldv, jac)) * gear[0];
+      if (da1 == da) da1 = m->dof_parentid[da1];
+      if (da2 == da) da2 = m->dof_parentid[da2];
+    }
+    return;
+  }
+  if (id2 < 0) { /* wrench in the global frame */
+    const real* sm = d->site_xmat + 9 * id;
+    real wt[3], wr[3];
+    r_vec(wt, sm, gear);
+    r_vec(wr, sm, gear + 3);
+    d->actuator_length[a] = 0;
+    for (int da = last_dof(m, m->body_weldid[m->site_bodyid[id]]); da >= 0; da = m->dof_parentid[da]) {
+      jac_dof(m, d, sx, m->site_bodyid[id], da, jp, jr);
+      mom[da] = dot3(jp, wt) + dot3(jr, wr);
+    }
+    return;
+  }
+  const int body = m->site_bodyid[id], bref = m->site_bodyid[id2];
+  const real *rx = d->site_xpos + 3 * id2, *rm = d->site_xmat + 9 * id2;
+  const int tr = gear[0] != 0 || gear[1] != 0 || gear[2] != 0, rot = gear[3] != 0 || gear[4] != 0 || gear[5] != 0;
+  real length = 0, wt[3] = {0, 0, 0}, wr[3] = {0, 0, 0};
+  if (tr) {
+    real dx[3] = {sx[0] - rx[0], sx[1] - rx[1], sx[2] - rx[2]}, vec[3];
+    rt_vec(vec, rm, dx);
+    length += dot3(vec, gear);
+    r_vec(wt, rm, gear);
+  }
+  if (rot) {
+    real q[4], qr[4], vec[3];
+    mul_quat(q, m->site_quat + 4 * id, d->xquat + 4 * body); /* smooth.py:2375-2376 multiplies in this order */
+    mul_quat(qr, m->site_quat + 4 * id2, d->xquat + 4 * bref);
+    quat_sub(vec, q, qr);
+    length += dot3(vec, gear + 3);
+    r_vec(wr, rm, gear + 3);
+  }
+  d->actuator_length[a] = length;
+  int da1 = last_dof(m, m->body_weldid[body]), da2 = last_dof(m, m->body_weldid[bref]);
+  while (da1 >= 0 || da2 >= 0) {
+    const int da = da1 > da2 ? da1 : da2;
+    if (da1 == da && da2 == da) break;
+    jac_dof(m, d, sx, body, da, jp, jr);
+    jac_dof(m, d, rx, bref, da, jp2, jr2);
+    real v = 0;
+    for (int i = 0; i < 3; i++) {
+      if (tr) v += (jp[i] - jp2[i]) * wt[i];
+      if (rot) v += (jr[i] - jr2[i]) * wr[i];
+    }
+    mom[da] = v;
+    if (da1 == da) da1 = m->dof_parentid[da1];
+    if (da2 == da) da2 = m->dof_parentid[da2];
+  }
+}
+
+/* smooth.py:2260-2273, 2448-2602 (BODY, adhesion): minus the mean over the body's contacts of the normal
+ * direction's Jacobian -- the contact's constraint rows when it is active (pyramid rows weighted 1/(2 npyr)
+ * each, i.e. their mean), else normal . (J(pos, b2) - J(pos, b1)) -- zero without contacts */
+static void body_transmission(const orc_model* m, orc_data* d, int a, real* mom) {
+  const int body = m->actuator_trnid[2 * a], nv = m->nv;
+  int ncon = 0;
+  d->actuator_length[a] = 0;
+  for (int c = 0; c < d->ncon[0]; c++) {
+    const int g1 = d->con_geom[2 * c], g2 = d->con_geom[2 * c + 1];
+    if (g1 < 0 || g2 < 0) continue;
+    const int b1 = m->geom_bodyid[g1], b2 = m->geom_bodyid[g2];
+    if (b1 != body && b2 != body) continue;
+    ncon++;
+    if (d->con_dist[c] < d->con_includemargin[c]) {
+      const int dim = d->con_dim[c];
+      const int* adr = d->con_efc_address + (size_t)c * 10;
+      if (dim == 1 || m->opt_cone == 1) {
+        for (int i = 0; i < nv; i++) mom[i] += d->efc_J[(size_t)adr[0] * nv + i];
+      } else {
+        const int np = dim - 1;
+        for (int j = 0; j < 2 * np; j++)
+          for (int i = 0; i < nv; i++) mom[i] += d->efc_J[(size_t)adr[j] * nv + i] * (0.5 / np);
+      }
+    } else {
+      const real* pos = d->con_pos + 3 * c;
+      const real* n = d->con_frame + 9 * c;
+      for (int i = 0; i < nv; i++) {
+        real j1[3], j2[3], r[3];
+        jac_dof(m, d, pos, b1, i, j1, r);
+        jac_dof(m, d, pos, b2, i, j2, r);
+        mom[i] += n[0] * (j2[0] - j1[0]) + n[1] * (j2[1] - j1[1]) + n[2] * (j2[2] - j1[2]);
+      }
+    }
+  }
+  if (ncon > 0)
+    for (int i = 0; i < nv; i++) mom[i] /= -(real)ncon;
+}
+
 static void transmission(const orc_model* m, orc_data* d) {
   int nv = m->nv;
   memset(d->actuator_moment, 0, (size_t)m->nu * nv * sizeof(real));
@@ -810,6 +944,14 @@ static void transmission(const orc_model* m, orc_data* d) {
       d->actuator_length[a] = d->ten_length[t] * gear[0];
       for (int k = 0; k < m->ten_J_rownnz[t]; k++)
         mom[m->ten_J_colind[m->ten_J_rowadr[t] + k]] = d->ten_J[m->ten_J_rowadr[t] + k] * gear[0];
+      continue;
+    }
+    if (trn == TRN_SITE || trn == TRN_SLIDERCRANK) {
+      site_transmission(m, d, a, mom);
+      continue;
+    }
+    if (trn == TRN_BODY) {
+      body_transmission(m, d, a, mom);
       continue;
     }
     if (trn == TRN_JOINT || trn == TRN_JOINTINPARENT) {

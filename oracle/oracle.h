@@ -58,7 +58,7 @@ typedef ORC_REAL real;
   X(light_pos0, nlight * 3) X(light_dir0, nlight * 3)                                              \
   X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
   X(actuator_ctrlrange, nu * 2) X(actuator_forcerange, nu * 2) X(actuator_actrange, nu * 2)       \
-  X(actuator_gear, nu * 6) X(actuator_acc0, nu) X(actuator_lengthrange, nu * 2)                   \
+  X(actuator_gear, nu * 6) X(actuator_cranklength, nu) X(actuator_acc0, nu) X(actuator_lengthrange, nu * 2)                   \
   X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)                               \
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flex_vert, nflexvert * 3) X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)    \
