@@ -23,7 +23,7 @@ constexpr int CMAX = 32;  // staged contacts per collision round
 enum : int { ST_POS = 1, ST_VEL = 2, ST_ACT = 4, ST_ACC = 8, ST_SOLVE = 16, ST_EULER = 32, ST_NOFACTOR = 64, ST_POOL = 128 };
 enum : int { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
 enum : int { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6, GEOM_MESH = 7 };
-enum : int { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2 };
+enum : int { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2, EQ_TENDON = 3 };
 enum : int { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICIT = 2, INT_IMPLICITFAST = 3 };
 enum : int { GAIN_FIXED = 0, GAIN_AFFINE = 1, GAIN_MUSCLE = 2 };
 enum : int { BIAS_NONE = 0, BIAS_AFFINE = 1, BIAS_MUSCLE = 2 };

@@ -943,6 +943,42 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       ne += cnt;
     }
   }
+  // --- tendon equality rows (constraint.py:498-674), in equality index order: L1 - L1_0 = poly(L2 - L2_0),
+  // J = J1 - poly'(L2 - L2_0) J2 (lane = dof)
+  if (TEN && !dsbl_constraint && !(m.opt_disableflags & DSBL_EQUALITY) && m.neq > 0 && m.ntendon > 0) {
+    const float* eq_data = MR(eq_data);
+    const float* len0 = MR(tendon_length0);
+    const float* tiw = MR(tendon_invweight0);
+    const float* qpos = s + L.qpos;
+    for (int e = 0; e < m.neq; e++) {
+      if (m.eq_type[e] != EQ_TENDON || !d.eq_active[(long)wid * m.neq + e]) continue;
+      const int r = nefc;
+      nefc++;
+      ne++;
+      if (r >= njmax) continue;
+      const float* data = eq_data + 11 * e;
+      const int t1 = m.eq_obj1id[e], t2 = m.eq_obj2id[e];
+      const float pos1 = ten_len(m, d, wid, qpos, t1) - len0[t1];
+      float pos, deriv = 0.0f, invweight = tiw[t1];
+      if (t2 > -1) {
+        invweight += tiw[t2];
+        const float dif = ten_len(m, d, wid, qpos, t2) - len0[t2];
+        pos = pos1 - (data[0] + data[1] * dif + data[2] * dif * dif + data[3] * dif * dif * dif + data[4] * dif * dif * dif * dif);
+        deriv = data[1] + 2.0f * data[2] * dif + 3.0f * data[3] * dif * dif + 4.0f * data[4] * dif * dif * dif;
+      } else {
+        pos = pos1 - data[0];
+      }
+      float Jk = 0.0f;
+      if (lane < nv) {
+        Jk = ten_coef(m, d, wid, t1, lane);
+        if (deriv != 0.0f) Jk += ten_coef(m, d, wid, t2, lane) * -deriv;
+      }
+      for (int k = lane; k < kJ; k += LPW) put_J(d, L, s, wid, np, r, k, k == lane ? Jk : 0.0f);
+      const float Jqvel = dsum(lane < nv ? Jk * qvel[lane] : 0.0f);
+      if (lane == 0)
+        efc_row(m, d, L, s, wid, r, pos, pos, invweight, MR(eq_solref) + 2 * e, MR(eq_solimp) + 5 * e, 0.0f, Jqvel, 0.0f, CNSTR_EQUALITY, e);
+    }
+  }
   // --- friction dof rows (constraint.py:1113-1190)
   if (!dsbl_constraint && !(m.opt_disableflags & DSBL_FRICTIONLOSS)) {
     const float* dof_frictionloss = MR(dof_frictionloss);

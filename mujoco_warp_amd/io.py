@@ -166,8 +166,8 @@ def put_model(mjm, device=None) -> types.Model:
   for st in np.unique(getattr(mjm, "sensor_type", np.zeros(0, dtype=np.int32))):
     if int(st) not in types.SUPPORTED_SENSORS:
       raise NotImplementedError(f"sensor type {int(st)} is not supported by this build yet.")
-  if not sparse and getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD, types.EqType.JOINT))):
-    raise NotImplementedError("only connect, weld and joint equality constraints are supported by this build yet.")
+  if not sparse and getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD, types.EqType.JOINT, types.EqType.TENDON))):
+    raise NotImplementedError("only connect, weld, joint and tendon equality constraints are supported by this build yet.")
   pairs_chk, _ = nxn_geom_pairs(mjm)
   for g1, g2 in pairs_chk:
     t = tuple(sorted((int(mjm.geom_type[g1]), int(mjm.geom_type[g2]))))

@@ -1636,6 +1636,11 @@ class _Compiler:
           etype, obj1 = EqType.JOINT, name2jnt[a["joint1"]]
           obj2 = name2jnt[a["joint2"]] if "joint2" in a else -1
           data[:5] = _merge_vec([0, 1, 0, 0, 0], _floats(a.get("polycoef", "0 1 0 0 0")))
+        elif el.tag == "tendon":  # constraint.py:498-674: length1 - length0_1 = poly(length2 - length0_2)
+          etype, objtype = EqType.TENDON, int(ObjType.TENDON)
+          obj1 = m.tendon_names.index(a["tendon1"])
+          obj2 = m.tendon_names.index(a["tendon2"]) if "tendon2" in a else -1
+          data[:5] = _merge_vec([0, 1, 0, 0, 0], _floats(a.get("polycoef", "0 1 0 0 0")))
         elif el.tag in ("connect", "weld"):
           etype = EqType.CONNECT if el.tag == "connect" else EqType.WELD
           if "site1" in a:

@@ -196,6 +196,8 @@ class ObjType(enum.IntEnum):
   SITE = 6
   CAMERA = 7
   LIGHT = 8
+  FLEX = 9
+  TENDON = 18
   ACTUATOR = 19
 
 

@@ -35,7 +35,7 @@ enum { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICITFAST = 3 };
 enum { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
 enum { GAIN_FIXED = 0, GAIN_AFFINE = 1, GAIN_MUSCLE = 2 };
 enum { DYN_NONE = 0, DYN_INTEGRATOR = 1, DYN_FILTER = 2, DYN_FILTEREXACT = 3, DYN_MUSCLE = 4, DYN_USER = 5 };
-enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2, EQ_FLEX = 4 };
+enum { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2, EQ_TENDON = 3, EQ_FLEX = 4 };
 enum { OBJ_UNKNOWN = 0, OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum { INTEGRATOR_EULER = 0, INTEGRATOR_RK4 = 1, INTEGRATOR_IMPLICIT = 2, INTEGRATOR_IMPLICITFAST = 3 };
 enum { BIAS_NONE = 0, BIAS_AFFINE = 1, BIAS_MUSCLE = 2 };
@@ -2476,6 +2476,37 @@ static void make_constraint(const orc_model* m, orc_data* d) {
         Jqvel = d->qvel[da1];
         invweight = m->dof_invweight0[da1];
       }
+      efc_row(m, d, efcid, pos, pos, invweight, m->eq_solref + 2 * e, m->eq_solimp + 5 * e, 0, Jqvel, 0, CNSTR_EQUALITY, e);
+    }
+  }
+  /* equality tendon constraint.py:498-674: L1 - L1_0 = poly(L2 - L2_0), J = J1 - poly'(L2 - L2_0) J2 */
+  if (!(m->opt_disableflags & DSBL_EQUALITY)) {
+    for (int e = 0; e < m->neq; e++) {
+      if (m->eq_type[e] != EQ_TENDON || !d->eq_active[e]) continue;
+      (*d->ne)++;
+      int efcid = (*d->nefc)++;
+      if (efcid >= njmax) continue;
+      const int t1 = m->eq_obj1id[e], t2 = m->eq_obj2id[e];
+      const real* data = m->eq_data + 11 * e;
+      real pos1 = d->ten_length[t1] - m->tendon_length0[t1], pos, deriv = 0, invweight = m->tendon_invweight0[t1];
+      if (t2 > -1) {
+        invweight += m->tendon_invweight0[t2];
+        const real dif = d->ten_length[t2] - m->tendon_length0[t2];
+        pos = pos1 - (data[0] + data[1] * dif + data[2] * dif * dif + data[3] * dif * dif * dif + data[4] * dif * dif * dif * dif);
+        deriv = data[1] + 2 * data[2] * dif + 3 * data[3] * dif * dif + 4 * data[4] * dif * dif * dif;
+      } else {
+        pos = pos1 - data[0];
+      }
+      real* J = d->efc_J + (size_t)efcid * nv;
+      ten_J_dense(m, d, t1, J);
+      if (deriv != 0) {
+        real* J2 = (real*)malloc(nv * sizeof(real));
+        ten_J_dense(m, d, t2, J2);
+        for (int i = 0; i < nv; i++) J[i] += J2[i] * -deriv;
+        free(J2);
+      }
+      real Jqvel = 0;
+      for (int i = 0; i < nv; i++) Jqvel += J[i] * d->qvel[i];
       efc_row(m, d, efcid, pos, pos, invweight, m->eq_solref + 2 * e, m->eq_solimp + 5 * e, 0, Jqvel, 0, CNSTR_EQUALITY, e);
     }
   }

@@ -66,7 +66,7 @@ typedef ORC_REAL real;
   X(tendon_stiffness, ntendon) X(tendon_damping, ntendon) X(tendon_frictionloss, ntendon)          \
   X(tendon_armature, ntendon) X(tendon_margin, ntendon) X(tendon_range, ntendon * 2)               \
   X(tendon_lengthspring, ntendon * 2) X(tendon_solref_lim, ntendon * 2) X(tendon_solimp_lim, ntendon * 5) \
-  X(tendon_solref_fri, ntendon * 2) X(tendon_solimp_fri, ntendon * 5) X(tendon_invweight0, ntendon)  \
+  X(tendon_solref_fri, ntendon * 2) X(tendon_solimp_fri, ntendon * 5) X(tendon_invweight0, ntendon) X(tendon_length0, ntendon) \
   X(tendon_actfrcrange, ntendon * 2) X(wrap_prm, nwrap)                                            \
   X(pair_solref, npair * 2) X(pair_solreffriction, npair * 2) X(pair_solimp, npair * 5)           \
   X(pair_margin, npair) X(pair_gap, npair) X(pair_friction, npair * 5)

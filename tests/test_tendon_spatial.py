@@ -252,3 +252,58 @@ def test_gpu_tendon_models_match_oracle(path):
     np.testing.assert_allclose(g, o, atol=tol * scale, err_msg=f)
   err = np.abs(np_(d.qacc) - od.qacc).max() / max(1.0, float(np.abs(od.qacc).max()))
   assert err < 5e-3, err
+
+
+TENDON_EQ = """<mujoco><worldbody><site name="s0" pos="0 0 .5"/>
+<body pos="0 0 0"><joint name="j0" type="hinge" axis="0 1 0"/><geom type="capsule" size=".05" fromto="0 0 0 .3 0 0"/><site name="s1" pos=".3 0 0"/>
+<body pos=".3 0 0"><joint name="j1" type="hinge" axis="0 1 0"/><geom type="capsule" size=".05" fromto="0 0 0 .3 0 0"/><site name="s2" pos=".3 0 0"/></body></body>
+<body pos="0 .5 0"><joint name="j2" type="slide" axis="1 0 0"/><geom type="sphere" size=".05"/></body></worldbody>
+<tendon><spatial name="sp"><site site="s0"/><site site="s1"/><site site="s2"/></spatial>
+<fixed name="fx"><joint joint="j2" coef="1"/><joint joint="j0" coef=".5"/></fixed><fixed name="f1"><joint joint="j1" coef="1"/></fixed></tendon>
+<equality><tendon tendon1="sp" tendon2="fx" polycoef="0 .7 .2 0 0"/><tendon tendon1="f1" polycoef=".1 0 0 0 0"/></equality></mujoco>"""
+
+
+def test_oracle_tendon_equality_rows():
+  """constraint.py:498-674: one row per active tendon equality, pos = (L1 - L1_0) - poly(L2 - L2_0), J = J1 -
+  poly'(L2 - L2_0) J2, after the joint equality rows."""
+  from mujoco_warp_amd import mjcf
+
+  mjm = mjcf.load_model_from_string(TENDON_EQ)
+  assert mjm.neq == 2 and list(mjm.eq_type) == [3, 3]
+  qpos, qvel, ctrl = _key_state(mjm, nworld=3, seed=7)
+  _, od = oracle_from_state(mjm, qpos, qvel, ctrl)
+  od.fwd_position()
+  for w in range(3):
+    assert int(od.ne[w, 0]) == 2
+    J = _dense_J(mjm, od, w)
+    L = od.ten_length[w]
+    dif = L[1] - mjm.tendon_length0[1]
+    c = mjm.eq_data[0]
+    pos0 = (L[0] - mjm.tendon_length0[0]) - (c[0] + c[1] * dif + c[2] * dif ** 2)
+    np.testing.assert_allclose(od.efc_pos[w, 0], pos0, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(od.efc_J[w].reshape(od.njmax, mjm.nv)[0], J[0] - (c[1] + 2 * c[2] * dif) * J[1], atol=1e-12)
+    np.testing.assert_allclose(od.efc_pos[w, 1], (L[2] - mjm.tendon_length0[2]) - 0.1, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_tendon_equality_matches_oracle():
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+  from tests.parity_models import efc_cost
+
+  mjm = mjcf.load_model_from_string(TENDON_EQ)
+  qpos, qvel, ctrl = _key_state(mjm, nworld=8, seed=8)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=16, nconmax=4)
+  _, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=16, nconmax=4)
+  mjw.forward(m, d)
+  od.forward()
+  torch.cuda.synchronize()
+  for w in range(8):
+    n = int(od.nefc[w, 0])
+    assert int(d.nefc[w]) == n == 2
+    np.testing.assert_allclose(np_(d.efc.pos[w, :n]), od.efc_pos[w, :n], atol=2e-6)
+    np.testing.assert_allclose(np_(d.efc.J[w, :n, :mjm.nv]), od.efc_J[w].reshape(16, mjm.nv)[:n], atol=2e-5)
+  err = np.abs(np_(d.qacc) - od.qacc).max() / max(1.0, float(np.abs(od.qacc).max()))
+  assert err < 5e-3, err
