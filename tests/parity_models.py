@@ -229,8 +229,8 @@ def report(name):
   out["force_scale"] = float(np.abs(od.qfrc_smooth).max())
   # qfrc_smooth = passive - bias + actuator: when the summands cancel (gravity compensation against the gravity
   # bias) fp32 rounding of the summands, not of the result, bounds its error
-  summ = max(float(np.abs(od.qfrc_bias).max()), float(np.abs(od.qfrc_passive).max()), out["force_scale"])
-  out["cancel_scale"] = max(1.0, summ / (out["force_scale"] + 1e-300))
+  summ = np.maximum(np.maximum(np.abs(od.qfrc_bias).max(axis=1), np.abs(od.qfrc_passive).max(axis=1)), np.abs(od.qfrc_actuator).max(axis=1))
+  out["cancel_scale"] = max(1.0, float((summ / (np.abs(od.qfrc_smooth).max(axis=1) + 1e-300)).max()))
   # qacc_smooth = M^-1 qfrc_smooth: its forward error carries cond(M) times the (checked) residual
   out["cond_M"] = max(float(np.linalg.cond(od.qM[w].reshape(nv, nv))) for w in range(nworld))
   # rows
