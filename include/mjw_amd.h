@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 23
+#define MJW_ABI_VERSION 24
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -64,7 +64,7 @@
   X(geom_solmix, ngeom) X(geom_solref, ngeom * 2) X(geom_solimp, ngeom * 5) X(geom_size, ngeom * 3) \
   X(geom_aabb, ngeom * 6) X(geom_rbound, ngeom) X(geom_pos, ngeom * 3) X(geom_quat, ngeom * 4)    \
   X(geom_friction, ngeom * 3) X(geom_margin, ngeom) X(geom_gap, ngeom) X(geom_fluid, ngeom * 12)  \
-  X(site_pos, nsite * 3) X(site_quat, nsite * 4)                                                   \
+  X(site_pos, nsite * 3) X(site_quat, nsite * 4) X(site_size, nsite * 3)                                                \
   X(cam_pos, ncam * 3) X(cam_quat, ncam * 4) X(cam_poscom0, ncam * 3) X(cam_pos0, ncam * 3)       \
   X(cam_mat0, ncam * 9)                                                                            \
   X(light_pos, nlight * 3) X(light_dir, nlight * 3) X(light_poscom0, nlight * 3)                  \
@@ -97,7 +97,7 @@
   X(body_geomadr, nbody) X(body_geomnum, nbody) X(body_fluid_ellipsoid, nbody)                    \
   X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \
   X(geom_type, ngeom) X(geom_condim, ngeom) X(geom_bodyid, ngeom) X(geom_priority, ngeom)         \
-  X(site_bodyid, nsite)                                                                            \
+  X(site_bodyid, nsite) X(site_type, nsite)                                                                      \
   X(cam_mode, ncam) X(cam_bodyid, ncam) X(cam_targetbodyid, ncam)                                 \
   X(light_mode, nlight) X(light_bodyid, nlight) X(light_targetbodyid, nlight)                     \
   X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
@@ -136,7 +136,7 @@
   X(xanchor, njnt * 3) X(xaxis, njnt * 3) X(geom_xpos, ngeom * 3) X(geom_xmat, ngeom * 9)         \
   X(site_xpos, nsite * 3) X(site_xmat, nsite * 9) X(cam_xpos, ncam * 3) X(cam_xmat, ncam * 9)     \
   X(light_xpos, nlight * 3) X(light_xdir, nlight * 3)                                              \
-  X(subtree_com, nbody * 3) X(cdof, nv * 6) X(cinert, nbody * 10) X(crb, nbody * 10)              \
+  X(subtree_com, nbody * 3) X(subtree_linvel, nbody * 3) X(subtree_angmom, nbody * 3) X(cdof, nv * 6) X(cinert, nbody * 10) X(crb, nbody * 10)              \
   X(qM, nv_pad * nv_pad) X(qLD, nv * nv)                                                           \
   X(actuator_length, nu) X(actuator_moment, nJmom) X(actuator_velocity, nu) X(actuator_force, nu) \
   X(cvel, nbody * 6) X(cdof_dot, nv * 6) X(qfrc_bias, nv) X(qfrc_spring, nv) X(qfrc_damper, nv)   \

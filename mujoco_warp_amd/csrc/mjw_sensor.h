@@ -85,6 +85,248 @@ __device__ __forceinline__ const float* cvel_offset(const mjw_model_t& m, int wi
   return F.cvel + 6 * b;
 }
 
+// ---- ray-zone intersection of the touch sensor (ray.py:105-450, distances only) ---------------------------
+__device__ __forceinline__ float ray_quad(float a, float b, float c, float* x) {
+  float det = b * b - a * c;
+  x[0] = x[1] = -1.0f;
+  if (det < MJW_MINVAL) return -1.0f;
+  det = sqrtf(det);
+  const float den = 1.0f / (a != 0.0f ? a : MJW_MINVAL);
+  x[0] = (-b - det) * den;
+  x[1] = (-b + det) * den;
+  return x[0] >= 0.0f ? x[0] : (x[1] >= 0.0f ? x[1] : -1.0f);
+}
+
+__device__ __forceinline__ float ray_sphere0(float r2, const float* p, const float* v) {
+  float x[2];
+  return ray_quad(dot3(v, v), dot3(v, p), dot3(p, p) - r2, x);
+}
+
+// the ray lp + t lv in the geom's frame against a sphere / capsule / ellipsoid / cylinder / box of `size`
+__device__ float ray_geom_local(int type, const float* size, const float* lp, const float* lv) {
+  float x[2];
+  if (type == GEOM_SPHERE) return ray_sphere0(size[0] * size[0], lp, lv);
+  if (type == GEOM_CAPSULE) {
+    const float ssz = size[0] + size[1];
+    if (ray_sphere0(ssz * ssz, lp, lv) < 0.0f) return -1.0f;
+    const float sq = size[0] * size[0];
+    float a = lv[0] * lv[0] + lv[1] * lv[1];
+    float best = -1.0f;
+    const float sol = ray_quad(a, lv[0] * lp[0] + lv[1] * lp[1], lp[0] * lp[0] + lp[1] * lp[1] - sq, x);
+    if (sol >= 0.0f && fabsf(lp[2] + sol * lv[2]) <= size[1]) best = sol;
+    a += lv[2] * lv[2];
+    for (int side = 1; side >= -1; side -= 2) {
+      const float ld[3] = {lp[0], lp[1], lp[2] - side * size[1]};
+      ray_quad(a, dot3(lv, ld), dot3(ld, ld) - sq, x);
+      for (int i = 0; i < 2; i++)
+        if (x[i] >= 0.0f && (side > 0 ? lp[2] + x[i] * lv[2] >= size[1] : lp[2] + x[i] * lv[2] <= -size[1]) && (best < 0.0f || x[i] < best))
+          best = x[i];
+    }
+    return best;
+  }
+  if (type == GEOM_ELLIPSOID) {
+    float s[3], sv[3], sp[3];
+    for (int i = 0; i < 3; i++) {
+      const float q = size[i] * size[i];
+      s[i] = 1.0f / (q != 0.0f ? q : MJW_MINVAL);
+      sv[i] = s[i] * lv[i];
+      sp[i] = s[i] * lp[i];
+    }
+    return ray_quad(dot3(sv, lv), dot3(sv, lp), dot3(sp, lp) - 1.0f, x);
+  }
+  if (type == GEOM_CYLINDER) {
+    if (ray_sphere0(size[0] * size[0] + size[1] * size[1], lp, lv) < 0.0f) return -1.0f;
+    float best = -1.0f;
+    if (fabsf(lv[2]) > MJW_MINVAL)
+      for (int side = -1; side <= 1; side += 2) {
+        const float sol = (side * size[1] - lp[2]) / lv[2];
+        const float p0 = lp[0] + sol * lv[0], p1 = lp[1] + sol * lv[1];
+        if (sol >= 0.0f && p0 * p0 + p1 * p1 <= size[0] * size[0] && (best < 0.0f || sol < best)) best = sol;
+      }
+    const float sol = ray_quad(lv[0] * lv[0] + lv[1] * lv[1], lv[0] * lp[0] + lv[1] * lp[1], lp[0] * lp[0] + lp[1] * lp[1] - size[0] * size[0], x);
+    if (sol >= 0.0f && fabsf(lp[2] + sol * lv[2]) <= size[1] && (best < 0.0f || sol < best)) best = sol;
+    return best;
+  }
+  if (type == GEOM_BOX) {
+    if (ray_sphere0(dot3(size, size), lp, lv) < 0.0f) return -1.0f;
+    float best = -1.0f;
+    for (int i = 0; i < 3; i++) {
+      if (fabsf(lv[i]) <= MJW_MINVAL) continue;
+      const int i0 = i == 0 ? 1 : 0, i1 = i == 2 ? 1 : 2;
+      for (int side = -1; side <= 1; side += 2) {
+        const float sol = (side * size[i] - lp[i]) / lv[i];
+        if (sol >= 0.0f && fabsf(lp[i0] + sol * lv[i0]) <= size[i0] && fabsf(lp[i1] + sol * lv[i1]) <= size[i1] && (best < 0.0f || sol < best))
+          best = sol;
+      }
+    }
+    return best;
+  }
+  return -1.0f;
+}
+
+// sensor.py:2001-2076 touch: normal forces of the site body's contacts whose ray along the contact normal
+// (away from the body) meets the site's zone.  Contacts are visited at their first constraint row.
+__device__ float touch_sensor(const mjw_model_t& m, const mjw_data_t& d, int wid, int site, const float* sxpos, const float* sxmat) {
+  const int body = m.site_bodyid[site];
+  const float* ssize = MR(site_size) + 3 * site;
+  const int nefc = min(d.nefc[wid], d.njmax);
+  const long wr = (long)wid * d.njmax;
+  float total = 0.0f;
+  for (int r = 0; r < nefc; r++) {
+    const int type = d.efc_type[wr + r];
+    if (type != CNSTR_CONTACT_FRICTIONLESS && type != CNSTR_CONTACT_PYRAMIDAL && type != CNSTR_CONTACT_ELLIPTIC) continue;
+    const int cid = d.efc_id[wr + r];
+    if (cid < 0 || cid >= d.naconmax || d.contact_efc_address[(long)cid * m.nmaxpyramid] != r) continue;
+    const int g1 = d.contact_geom[2L * cid], g2 = d.contact_geom[2L * cid + 1];
+    if (g1 < 0 || g2 < 0) continue;
+    const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+    if (body != b1 && body != b2) continue;
+    float f = d.efc_force[wr + r];
+    if (m.opt_cone == CONE_PYRAMIDAL)
+      for (int i = 1; i < 2 * (d.contact_dim[cid] - 1); i++) {
+        const int a = d.contact_efc_address[(long)cid * m.nmaxpyramid + i];
+        if (a >= 0 && a < d.njmax) f += d.efc_force[wr + a];
+      }
+    if (f <= 0.0f) continue;
+    const float* n = d.contact_frame + 9L * cid;
+    const float nn = sqrtf(dot3(n, n)) * f;
+    const float sg = body == b2 ? -1.0f : 1.0f;
+    float dir[3], dif[3], lp[3], lv[3];
+    for (int i = 0; i < 3; i++) {
+      dir[i] = nn > 0.0f ? sg * n[i] * f / nn : 0.0f;
+      dif[i] = d.contact_pos[3L * cid + i] - sxpos[i];
+    }
+    mat_t_vec(lp, sxmat, dif);
+    mat_t_vec(lv, sxmat, dir);
+    if (ray_geom_local(m.site_type[site], ssize, lp, lv) >= 0.0f) total += f;
+  }
+  return total;
+}
+
+// the efc row of the limit on joint / tendon `id` (sensor.py:243-278: any limit row with that id) or -1
+__device__ __forceinline__ int limit_row(const mjw_data_t& d, int wid, int id) {
+  const int lo = d.ne[wid] + d.nf[wid], hi = min(lo + d.nl[wid], d.njmax);
+  const long wr = (long)wid * d.njmax;
+  int r = -1;
+  for (int e = lo; e < hi; e++)
+    if (d.efc_id[wr + e] == id && (d.efc_type[wr + e] == CNSTR_LIMIT_JOINT || d.efc_type[wr + e] == CNSTR_LIMIT_TENDON)) r = e;
+  return r;
+}
+
+// sensor.py:2700-2890 energy_pos: -sum m g . xipos over the bodies, joint and tendon springs
+__device__ float energy_potential(const mjw_model_t& m, const mjw_data_t& d, int wid, const float* qpos, const float* xipos) {
+  float e = 0.0f;
+  const float* grav = MR(opt_gravity);
+  const float* mass = MR(body_mass);
+  if (!(m.opt_disableflags & DSBL_GRAVITY))
+    for (int b = 1; b < m.nbody; b++) e -= mass[b] * dot3(grav, xipos + 3 * b);
+  if (m.opt_disableflags & DSBL_SPRING) return e;
+  const float* stiff = MR(jnt_stiffness);
+  const float* qs = MR(qpos_spring);
+  for (int j = 0; j < m.njnt; j++) {
+    const float k = stiff[j];
+    if (k == 0.0f) continue;
+    const int a = m.jnt_qposadr[j], t = m.jnt_type[j];
+    if (t == JNT_FREE || t == JNT_BALL) {
+      float lin = 0.0f;
+      int q0 = a;
+      if (t == JNT_FREE) {
+        for (int i = 0; i < 3; i++) lin += (qpos[a + i] - qs[a + i]) * (qpos[a + i] - qs[a + i]);
+        q0 = a + 3;
+      }
+      float q[4] = {qpos[q0], qpos[q0 + 1], qpos[q0 + 2], qpos[q0 + 3]}, dif[3];
+      normalize4(q);
+      quat_sub(dif, q, qs + q0);
+      e += 0.5f * k * (lin + dot3(dif, dif));
+    } else {
+      const float dq = qpos[a] - qs[a];
+      e += 0.5f * k * dq * dq;
+    }
+  }
+  const float* tst = MR(tendon_stiffness);
+  const float* tls = MR(tendon_lengthspring);
+  for (int t = 0; t < m.ntendon; t++) {
+    if (tst[t] == 0.0f) continue;
+    const float L = d.ten_length[(long)wid * m.ntendon + t], lo = tls[2 * t], hi = tls[2 * t + 1];
+    const float disp = L > hi ? hi - L : (L < lo ? lo - L : 0.0f);
+    e += 0.5f * tst[t] * disp * disp;
+  }
+  return e;
+}
+
+// sensor.py:2893-2940 energy_vel: 0.5 qvel' M qvel (dense qM rows of nv_pad, or the sparse ancestor rows)
+__device__ float energy_kinetic(const mjw_model_t& m, const mjw_data_t& d, int wid, const float* qvel) {
+  float e = 0.0f;
+  if (m.is_sparse) {
+    const float* M = d.qM + (long)wid * m.nM;
+    for (int i = 0; i < m.nv; i++)
+      for (int k = 0; k < m.M_rownnz[i]; k++) {
+        const int j = m.M_colind[m.M_rowadr[i] + k];
+        e += (j == i ? 1.0f : 2.0f) * qvel[i] * M[m.M_rowadr[i] + k] * qvel[j];
+      }
+  } else {
+    const int np = m.nv_pad;
+    const float* M = d.qM + (long)wid * np * np;
+    for (int i = 0; i < m.nv; i++) {
+      float row = 0.0f;
+      for (int j = 0; j < m.nv; j++) row += M[i * np + j] * qvel[j];
+      e += qvel[i] * row;
+    }
+  }
+  return 0.5f * e;
+}
+
+// smooth.py:2932-3084 subtree_vel, by one lane (sensor models only): subtree linear velocity and angular
+// momentum into the Data, children before parents (bodies are in DFS pre-order)
+__device__ void subtree_vel(const mjw_model_t& m, const mjw_data_t& d, int wid, const float* cvel, const float* com) {
+  const long wb = (long)wid * m.nbody;
+  float* lv = d.subtree_linvel + wb * 3;
+  float* am = d.subtree_angmom + wb * 3;
+  const float* xipos = d.xipos + wb * 3;
+  const float* ximat = d.ximat + wb * 9;
+  const float* mass = MR(body_mass);
+  const float* smass = MR(body_subtreemass);
+  const float* inertia = MR(body_inertia);
+  for (int b = 0; b < m.nbody; b++) {
+    const float* cv = cvel + 6 * b;
+    const float* sc = com + 3 * m.body_rootid[b];
+    float dif[3], c[3], dv[3];
+    for (int i = 0; i < 3; i++) dif[i] = xipos[3 * b + i] - sc[i];
+    cross3(c, dif, cv);
+    for (int i = 0; i < 3; i++) lv[3 * b + i] = mass[b] * (cv[3 + i] - c[i]);
+    mat_t_vec(dv, ximat + 9 * b, cv);
+    for (int i = 0; i < 3; i++) dv[i] *= inertia[3 * b + i];
+    matvec3(am + 3 * b, ximat + 9 * b, dv);
+  }
+  for (int b = m.nbody - 1; b >= 0; b--) {
+    if (b > 0)
+      for (int i = 0; i < 3; i++) lv[3 * m.body_parentid[b] + i] += lv[3 * b + i];
+    const float sm = fmaxf(MJW_MINVAL, smass[b]);
+    for (int i = 0; i < 3; i++) lv[3 * b + i] /= sm;
+  }
+  for (int b = m.nbody - 1; b > 0; b--) {
+    const int p = m.body_parentid[b];
+    const float* cv = cvel + 6 * b;
+    const float* sc = com + 3 * m.body_rootid[b];
+    float dif[3], c[3], dx[3], dp[3], dL[3];
+    for (int i = 0; i < 3; i++) dif[i] = xipos[3 * b + i] - sc[i];
+    cross3(c, dif, cv);
+    for (int i = 0; i < 3; i++) {
+      dx[i] = xipos[3 * b + i] - com[3 * b + i];
+      dp[i] = (cv[3 + i] - c[i] - lv[3 * b + i]) * mass[b];
+    }
+    cross3(dL, dx, dp);
+    for (int i = 0; i < 3; i++) am[3 * b + i] += dL[i];
+    for (int i = 0; i < 3; i++) am[3 * p + i] += am[3 * b + i];
+    for (int i = 0; i < 3; i++) {
+      dx[i] = com[3 * b + i] - com[3 * p + i];
+      dp[i] = (lv[3 * b + i] - lv[3 * p + i]) * smass[b];
+    }
+    cross3(dL, dx, dp);
+    for (int i = 0; i < 3; i++) am[3 * p + i] += dL[i];
+  }
+}
+
 // one position- or velocity-stage sensor (sensor.py:459-706 / 1251-1373, supported types)
 __device__ void sensor_posvel_one(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s, const float* qpos,
                                   const float* qvel, const float* act_len, const float* act_vel, float time) {
@@ -145,6 +387,23 @@ __device__ void sensor_posvel_one(const mjw_model_t& m, const mjw_data_t& d, int
     for (int i = 0; i < 3; i++) v[i] = F.subtree_com[3 * id + i];
   } else if (t == SENS_CLOCK) {
     v[0] = time; dim = 1;
+  } else if (t == SENS_TENDONPOS) {  // sensor.py:222-224
+    v[0] = d.ten_length[(long)wid * m.ntendon + id]; dim = 1;
+  } else if (t == SENS_TENDONVEL) {  // sensor.py:957-959
+    v[0] = d.ten_velocity[(long)wid * m.ntendon + id]; dim = 1;
+  } else if (t == SENS_JOINTLIMITPOS || t == SENS_TENDONLIMITPOS || t == SENS_JOINTLIMITVEL || t == SENS_TENDONLIMITVEL) {
+    const int r = limit_row(d, wid, id);  // sensor.py:243-278, 972-1007 (no row: the zeroed sensordata)
+    const long e = (long)wid * d.njmax + r;
+    const bool pos = t == SENS_JOINTLIMITPOS || t == SENS_TENDONLIMITPOS;
+    v[0] = r < 0 ? 0.0f : (pos ? d.efc_pos[e] - d.efc_margin[e] : d.efc_vel[e]);
+    dim = 1;
+  } else if (t == SENS_SUBTREELINVEL || t == SENS_SUBTREEANGMOM) {  // sensor.py:1240-1248 (subtree_vel ran first)
+    const float* src = (t == SENS_SUBTREELINVEL ? d.subtree_linvel : d.subtree_angmom) + ((long)wid * m.nbody + id) * 3;
+    for (int i = 0; i < 3; i++) v[i] = src[i];
+  } else if (t == SENS_E_POTENTIAL) {  // sensor.py:698-700
+    v[0] = energy_potential(m, d, wid, qpos, F.xipos); dim = 1;
+  } else if (t == SENS_E_KINETIC) {  // sensor.py:701-703
+    v[0] = energy_kinetic(m, d, wid, qvel); dim = 1;
   } else if (t == SENS_GYRO || t == SENS_VELOCIMETER) {  // sensor.py:909-949
     float p[3], R[9];
     site_pose(m, wid, F, id, p, R);

@@ -222,6 +222,15 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   F.ximat = d.ximat + wb * 9; F.gxpos = d.geom_xpos + (long)wid * m.ngeom * 3; F.gxmat = d.geom_xmat + (long)wid * m.ngeom * 9;
   F.cxpos = d.cam_xpos + (long)wid * m.ncam * 3; F.cxmat = d.cam_xmat + (long)wid * m.ncam * 9;
   F.subtree_com = s + L.com; F.cvel = cvel;
+  // smooth.py:3044-3084 subtree_vel for the subtree velocity / momentum sensors (sensor.py:1383-1384)
+  if (stages & 2) {
+    bool sub = false;
+    for (int k = 0; k < m.nsensor; k++) sub |= m.sensor_type[k] == SENS_SUBTREELINVEL || m.sensor_type[k] == SENS_SUBTREEANGMOM;
+    if (sub) {
+      if (lane == 0) subtree_vel(m, d, wid, cvel, s + L.com);
+      __syncthreads();
+    }
+  }
   // position / velocity sensors (sensor.py:459-706, 1251-1373), lane = sensor
   const float time = d.time[wid];
   for (int k = lane; k < m.nsensor; k += LPW) {
@@ -281,6 +290,19 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
       float p[3], R[9];
       const int b = obj_frame(m, wid, F, ot == OBJ_BODY ? OBJ_XBODY : ot, id, p, R);
       for (int i = 0; i < 3; i++) v[i] = cacc[6 * b + i];
+    } else if (t == SENS_TENDONACTFRC) {  // sensor.py:1538-1577
+      for (int a = 0; a < m.nu; a++)
+        if (m.actuator_trntype[a] == TRN_TENDON && m.actuator_trnid[2 * a] == id) v[0] += d.actuator_force[(long)wid * m.nu + a];
+      dim = 1;
+    } else if (t == SENS_JOINTLIMITFRC || t == SENS_TENDONLIMITFRC) {  // sensor.py:1580-1615
+      const int r = limit_row(d, wid, id);
+      v[0] = r < 0 ? 0.0f : d.efc_force[(long)wid * d.njmax + r];
+      dim = 1;
+    } else if (t == SENS_TOUCH) {  // sensor.py:2001-2076
+      float p[3], R[9];
+      site_pose(m, wid, F, id, p, R);
+      v[0] = touch_sensor(m, d, wid, id, p, R);
+      dim = 1;
     } else {
       continue;
     }

@@ -513,7 +513,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     xpos=(nb, 3), xquat=(nb, 4), xmat=(nb, 3, 3), xipos=(nb, 3), ximat=(nb, 3, 3), xanchor=(nj, 3), xaxis=(nj, 3),
     geom_xpos=(ng, 3), geom_xmat=(ng, 3, 3), site_xpos=(m.nsite, 3), site_xmat=(m.nsite, 3, 3),
     cam_xpos=(m.ncam, 3), cam_xmat=(m.ncam, 3, 3), light_xpos=(m.nlight, 3), light_xdir=(m.nlight, 3),
-    subtree_com=(nb, 3), cdof=(nv, 6), cinert=(nb, 10), crb=(nb, 10),
+    subtree_com=(nb, 3), subtree_linvel=(nb, 3), subtree_angmom=(nb, 3), cdof=(nv, 6), cinert=(nb, 10), crb=(nb, 10),
     qM=(m.nM,) if sp else (np_, np_), qLD=(m.nM,) if sp else (nv, nv),
     actuator_length=(nu,), actuator_moment=(m.nJmom,), actuator_velocity=(nu,), actuator_force=(nu,),
     cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,), qfrc_fluid=(nv,),

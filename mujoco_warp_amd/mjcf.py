@@ -1288,7 +1288,11 @@ class _Compiler:
     for i, b in enumerate(self.bodies):
       for sa in b.sites:
         q = _orientation(sa, self.angle_scale, self.eulerseq)
-        srows.append(dict(bodyid=i, pos=_floats(sa.get("pos", "0 0 0"), 3), quat=q if q is not None else [1, 0, 0, 0], name=sa.get("name", "")))
+        stype = {"sphere": GeomType.SPHERE, "capsule": GeomType.CAPSULE, "ellipsoid": GeomType.ELLIPSOID, "cylinder": GeomType.CYLINDER,
+                 "box": GeomType.BOX}[sa.get("type", "sphere")]
+        size = _merge_vec([0.005, 0.005, 0.005], _floats(sa.get("size", "0.005")))
+        srows.append(dict(bodyid=i, pos=_floats(sa.get("pos", "0 0 0"), 3), quat=q if q is not None else [1, 0, 0, 0], name=sa.get("name", ""),
+                          type=int(stype), size=size))
       for ca in b.cams:
         q = _orientation(ca, self.angle_scale, self.eulerseq)
         crows.append(
@@ -1321,6 +1325,8 @@ class _Compiler:
     m.site_bodyid = np.array([r["bodyid"] for r in srows], dtype=np.int32)
     m.site_pos = np.array([r["pos"] for r in srows]).reshape(-1, 3)
     m.site_quat = np.array([r["quat"] for r in srows]).reshape(-1, 4)
+    m.site_type = np.array([r["type"] for r in srows], dtype=np.int32)  # the touch sensor's zone (sensor.py:2001-2076)
+    m.site_size = np.array([r["size"] for r in srows], dtype=np.float64).reshape(-1, 3)
     m.ncam = len(crows)
     m.cam_names = [r["name"] for r in crows]
     m.cam_bodyid = np.array([r["bodyid"] for r in crows], dtype=np.int32)
@@ -1698,6 +1704,20 @@ class _Compiler:
     "frameangacc": (SensorType.FRAMEANGACC, 3, DataType.REAL, Stage.ACC, None, None),
     "subtreecom": (SensorType.SUBTREECOM, 3, DataType.REAL, Stage.POS, "body", ObjType.BODY),
     "clock": (SensorType.CLOCK, 1, DataType.REAL, Stage.POS, None, ObjType.UNKNOWN),
+    "touch": (SensorType.TOUCH, 1, DataType.POSITIVE, Stage.ACC, "site", ObjType.SITE),
+    "tendonpos": (SensorType.TENDONPOS, 1, DataType.REAL, Stage.POS, "tendon", ObjType.TENDON),
+    "tendonvel": (SensorType.TENDONVEL, 1, DataType.REAL, Stage.VEL, "tendon", ObjType.TENDON),
+    "tendonactuatorfrc": (SensorType.TENDONACTFRC, 1, DataType.REAL, Stage.ACC, "tendon", ObjType.TENDON),
+    "jointlimitpos": (SensorType.JOINTLIMITPOS, 1, DataType.REAL, Stage.POS, "joint", ObjType.JOINT),
+    "jointlimitvel": (SensorType.JOINTLIMITVEL, 1, DataType.REAL, Stage.VEL, "joint", ObjType.JOINT),
+    "jointlimitfrc": (SensorType.JOINTLIMITFRC, 1, DataType.POSITIVE, Stage.ACC, "joint", ObjType.JOINT),
+    "tendonlimitpos": (SensorType.TENDONLIMITPOS, 1, DataType.REAL, Stage.POS, "tendon", ObjType.TENDON),
+    "tendonlimitvel": (SensorType.TENDONLIMITVEL, 1, DataType.REAL, Stage.VEL, "tendon", ObjType.TENDON),
+    "tendonlimitfrc": (SensorType.TENDONLIMITFRC, 1, DataType.POSITIVE, Stage.ACC, "tendon", ObjType.TENDON),
+    "subtreelinvel": (SensorType.SUBTREELINVEL, 3, DataType.REAL, Stage.VEL, "body", ObjType.BODY),
+    "subtreeangmom": (SensorType.SUBTREEANGMOM, 3, DataType.REAL, Stage.VEL, "body", ObjType.BODY),
+    "e_potential": (SensorType.E_POTENTIAL, 1, DataType.REAL, Stage.POS, None, ObjType.UNKNOWN),
+    "e_kinetic": (SensorType.E_KINETIC, 1, DataType.REAL, Stage.VEL, None, ObjType.UNKNOWN),
   }
   _OBJTYPES = {"body": ObjType.BODY, "xbody": ObjType.XBODY, "geom": ObjType.GEOM, "site": ObjType.SITE, "camera": ObjType.CAMERA}
 
@@ -1712,6 +1732,7 @@ class _Compiler:
       ObjType.CAMERA: {n: i for i, n in enumerate(m.cam_names) if n},
       ObjType.JOINT: {n: i for i, n in enumerate(m.jnt_names) if n},
       ObjType.ACTUATOR: {n: i for i, n in enumerate(m.actuator_names) if n},
+      ObjType.TENDON: {n: i for i, n in enumerate(getattr(m, "tendon_names", [])) if n},
     }
     rows = []
     adr = 0

@@ -243,6 +243,13 @@ class SensorType(enum.IntEnum):
   SUBTREECOM = 35
   SUBTREELINVEL = 36
   SUBTREEANGMOM = 37
+  INSIDESITE = 38
+  GEOMDIST = 39
+  GEOMNORMAL = 40
+  GEOMFROMTO = 41
+  CONTACT = 42
+  E_POTENTIAL = 43
+  E_KINETIC = 44
   CLOCK = 45  # after INSIDESITE, GEOMDIST, GEOMNORMAL, GEOMFROMTO, CONTACT, E_POTENTIAL, E_KINETIC
 
 
@@ -271,6 +278,9 @@ SUPPORTED_SENSORS = {
   SensorType.ACTUATORFRC, SensorType.JOINTACTFRC, SensorType.BALLQUAT, SensorType.BALLANGVEL, SensorType.FRAMEPOS,
   SensorType.FRAMEQUAT, SensorType.FRAMEXAXIS, SensorType.FRAMEYAXIS, SensorType.FRAMEZAXIS, SensorType.FRAMELINVEL,
   SensorType.FRAMEANGVEL, SensorType.FRAMELINACC, SensorType.FRAMEANGACC, SensorType.SUBTREECOM, SensorType.CLOCK,
+  SensorType.TOUCH, SensorType.TENDONPOS, SensorType.TENDONVEL, SensorType.TENDONACTFRC, SensorType.JOINTLIMITPOS,
+  SensorType.JOINTLIMITVEL, SensorType.JOINTLIMITFRC, SensorType.TENDONLIMITPOS, SensorType.TENDONLIMITVEL,
+  SensorType.TENDONLIMITFRC, SensorType.SUBTREELINVEL, SensorType.SUBTREEANGMOM, SensorType.E_POTENTIAL, SensorType.E_KINETIC,
 }
 # sensors that need rne_postconstraint (io.py:542-551)
 RNE_POSTCONSTRAINT_SENSORS = {

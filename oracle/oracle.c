@@ -3502,8 +3502,11 @@ static void frame_quat(const orc_model* m, const orc_data* d, int type, int id, 
   else if (type == OBJ_CAMERA) mul_quat(q, d->xquat + 4 * m->cam_bodyid[id], m->cam_quat + 4 * id);
 }
 
+#include "oracle_sensor.h"
+
 /* sensor.py:459-706 (_sensor_pos, supported types) */
 static void sensor_pos(const orc_model* m, orc_data* d) {
+  sensor_extra(m, d, STAGE_POS);
   for (int s = 0; s < m->nsensor; s++) {
     if (m->sensor_needstage[s] != STAGE_POS) continue;
     int t = m->sensor_type[s], id = m->sensor_objid[s], ot = m->sensor_objtype[s];
@@ -3581,6 +3584,7 @@ static void cvel_offset(const orc_model* m, const orc_data* d, int type, int id,
 
 /* sensor.py:1251-1373 (_sensor_vel, supported types) */
 static void sensor_vel(const orc_model* m, orc_data* d) {
+  sensor_extra(m, d, STAGE_VEL);
   for (int s = 0; s < m->nsensor; s++) {
     if (m->sensor_needstage[s] != STAGE_VEL) continue;
     int t = m->sensor_type[s], id = m->sensor_objid[s], ot = m->sensor_objtype[s];
@@ -3771,6 +3775,7 @@ static void sensor_acc(const orc_model* m, orc_data* d) {
     post |= t == SENS_ACCELEROMETER || t == SENS_FORCE || t == SENS_TORQUE || t == SENS_FRAMELINACC || t == SENS_FRAMEANGACC;
   }
   if (post) rne_postconstraint(m, d);
+  sensor_extra(m, d, STAGE_ACC);
   for (int s = 0; s < m->nsensor; s++) {
     if (m->sensor_needstage[s] != STAGE_ACC) continue;
     int t = m->sensor_type[s], id = m->sensor_objid[s], ot = m->sensor_objtype[s];
