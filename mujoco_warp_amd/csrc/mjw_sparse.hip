@@ -31,6 +31,7 @@
 #include "mjw_narrow.h"
 #include "mjw_flexcol.h"
 #include "mjw_passive.h"
+#include "mjw_tendon.h"
 
 namespace mjw {
 namespace sp {
@@ -551,6 +552,43 @@ __device__ void crb_qM(const mjw_model_t& m, const mjw_data_t& d, int wid) {
   __syncthreads();
 }
 
+// ---------------------------------------------------------------------------------------------
+// tendons (fixed and spatial; mjw_tendon.h restates smooth.py:3085-3465 for both paths): lengths and
+// Jacobian rows into the Data, then armature into the sparse M rows (smooth.py:916-1000)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ TenFrames ten_frames(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  return TenFrames{d.site_xpos + (long)wid * m.nsite * 3, d.geom_xpos + (long)wid * m.ngeom * 3, d.geom_xmat + (long)wid * m.ngeom * 9,
+                   d.subtree_com + (long)wid * m.nbody * 3, d.cdof + (long)wid * m.nv * 6};
+}
+
+// position of M[i][j] (j = i or an ancestor dof of i) in the ancestor-row layout, or -1
+__device__ __forceinline__ int m_pos(const mjw_model_t& m, int i, int j) {
+  const int adr = m.M_rowadr[i], rn = m.M_rownnz[i];
+  if (i == j) return adr + rn - 1;
+  for (int q = 0; q < rn - 1; q++)
+    if (m.M_colind[adr + q] == j) return adr + q;
+  return -1;
+}
+
+__device__ void tendons(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  tendon_pos(m, d, d.qpos + (long)wid * m.nq, ten_frames(m, d, wid), wid, tid(), BLK);
+  __syncthreads();
+  const float* arm = MR(tendon_armature);
+  float* qM = d.qM + (long)wid * m.nM;
+  for (int t = 0; t < m.ntendon; t++) {  // uniform: one tendon's (i >= j) pairs per round
+    if (arm[t] == 0.0f) continue;
+    const int rn = m.ten_J_rownnz[t], ra = m.ten_J_rowadr[t];
+    const float* J = d.ten_J + (long)wid * m.nJten + ra;
+    for (int p = tid(); p < rn * rn; p += BLK) {
+      const int k1 = p / rn, k2 = p - k1 * rn;
+      if (k2 > k1) continue;
+      const int pos = m_pos(m, m.ten_J_colind[ra + k1], m.ten_J_colind[ra + k2]);
+      if (pos >= 0) qM[pos] += arm[t] * J[k1] * J[k2];
+    }
+    __syncthreads();
+  }
+}
+
 // M = L' D L per kinematic tree (smooth.py:1003-1064, mj_factorM order): LD = factor(M + diag(add))
 __device__ void factor_trees(const mjw_model_t& m, const float* M, float* LD, const float* add, float add_scale) {
   for (int t = tid(); t < m.ntree; t += BLK) {
@@ -1060,6 +1098,10 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
 // ---------------------------------------------------------------------------------------------
 // constraint.py make_constraint (joint / flex equality, friction, limits, pyramidal contacts)
 // ---------------------------------------------------------------------------------------------
+__device__ void put_row_scalars(const mjw_model_t& m, const mjw_data_t& d, int wid, int r, float vel, float pos_aref, float pos_imp,
+                                float invweight, const float* solref, const float* solimp, float margin, float frictionloss, int type,
+                                int id);
+
 // constraint.py:52-121 _efc_row (scalars) + the sparse J row
 __device__ void put_row(const mjw_model_t& m, const mjw_data_t& d, int wid, int r, int nnz, const int* cols, const float* vals, float pos_aref,
                         float pos_imp, float invweight, const float* solref, const float* solimp, float margin, float frictionloss, int type,
@@ -1073,6 +1115,13 @@ __device__ void put_row(const mjw_model_t& m, const mjw_data_t& d, int wid, int 
     vel += vals[k] * qvel[cols[k]];
   }
   d.efc_J_rownnz[(long)wid * d.njmax + r] = nnz;
+  put_row_scalars(m, d, wid, r, vel, pos_aref, pos_imp, invweight, solref, solimp, margin, frictionloss, type, id);
+}
+
+// constraint.py:52-121 _efc_row: the row scalars for a J row already written (its J qvel in vel)
+__device__ void put_row_scalars(const mjw_model_t& m, const mjw_data_t& d, int wid, int r, float vel, float pos_aref, float pos_imp,
+                                float invweight, const float* solref, const float* solimp, float margin, float frictionloss, int type,
+                                int id) {
   const float timestep = MR(opt_timestep)[0];
   float timeconst = solref[0], dampratio = solref[1];
   float dmin = solimp[0], dmax = solimp[1], width = solimp[2], mid = solimp[3], power = solimp[4];
@@ -1180,6 +1229,80 @@ __device__ int make_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int
     const float Jv = (float)(dmn < dmx) * 2.0f - 1.0f;
     put_row(m, d, wid, r0, 1, &da, &Jv, pos, pos, dof_invweight0[da], MR(jnt_solref) + 2 * i, MR(jnt_solimp) + 5 * i, margin, 0.0f,
             CNSTR_LIMIT_JOINT, i);
+    return 1;
+  }
+  if (cat >= 5) {  // tendon rows: 5 equality (constraint.py:498-674), 6 friction (:1204-1313), 7 limit (:1547-1665)
+    const float* qv = d.qvel + (long)wid * m.nv;
+    const float* tiw = MR(tendon_invweight0);
+    int t1 = i, t2 = -1;
+    float pos = 0.0f, deriv = 0.0f, scl = 1.0f, margin = 0.0f, fl = 0.0f, iw;
+    const float *sref, *simp;
+    int type;
+    if (cat == 5) {
+      if (m.eq_type[i] != EQ_TENDON || !d.eq_active[(long)wid * m.neq + i]) return 0;
+      if (r0 < 0 || r0 >= njmax) return 1;
+      const float* data = MR(eq_data) + 11 * i;
+      const float* len0 = MR(tendon_length0);
+      t1 = m.eq_obj1id[i];
+      t2 = m.eq_obj2id[i];
+      pos = ten_len(m, d, wid, qpos, t1) - len0[t1];
+      iw = tiw[t1];
+      if (t2 > -1) {
+        iw += tiw[t2];
+        const float dif = ten_len(m, d, wid, qpos, t2) - len0[t2];
+        pos -= data[0] + data[1] * dif + data[2] * dif * dif + data[3] * dif * dif * dif + data[4] * dif * dif * dif * dif;
+        deriv = data[1] + 2.0f * data[2] * dif + 3.0f * data[3] * dif * dif + 4.0f * data[4] * dif * dif * dif;
+      } else {
+        pos -= data[0];
+      }
+      if (deriv == 0.0f) t2 = -1;
+      sref = MR(eq_solref) + 2 * i;
+      simp = MR(eq_solimp) + 5 * i;
+      type = CNSTR_EQUALITY;
+    } else if (cat == 6) {
+      fl = MR(tendon_frictionloss)[i];
+      if (fl <= 0.0f) return 0;
+      if (r0 < 0 || r0 >= njmax) return 1;
+      iw = tiw[i];
+      sref = MR(tendon_solref_fri) + 2 * i;
+      simp = MR(tendon_solimp_fri) + 5 * i;
+      type = CNSTR_FRICTION_TENDON;
+    } else {
+      if (!m.tendon_limited[i]) return 0;
+      const float* rng = MR(tendon_range) + 2 * i;
+      const float L = ten_len(m, d, wid, qpos, i);
+      const float dmn = L - rng[0], dmx = rng[1] - L;
+      margin = MR(tendon_margin)[i];
+      pos = fminf(dmn, dmx) - margin;
+      if (!(pos < 0.0f)) return 0;
+      if (r0 < 0 || r0 >= njmax) return 1;
+      scl = (float)(dmn < dmx) * 2.0f - 1.0f;
+      iw = tiw[i];
+      sref = MR(tendon_solref_lim) + 2 * i;
+      simp = MR(tendon_solimp_lim) + 5 * i;
+      type = CNSTR_LIMIT_TENDON;
+    }
+    // J = scl J1 - deriv J2 over the merged (ascending) columns of the two tendon rows
+    const long jb = (long)wid * m.njrow * d.njmax_pad + r0, P = d.njmax_pad;
+    const int n1 = m.ten_J_rownnz[t1], a1 = m.ten_J_rowadr[t1];
+    const int n2 = t2 >= 0 ? m.ten_J_rownnz[t2] : 0, a2 = t2 >= 0 ? m.ten_J_rowadr[t2] : 0;
+    const float* J1 = d.ten_J + (long)wid * m.nJten + a1;
+    const float* J2 = d.ten_J + (long)wid * m.nJten + a2;
+    int p1 = 0, p2 = 0, nnz = 0;
+    float vel = 0.0f;
+    while ((p1 < n1 || p2 < n2) && nnz < m.njrow) {
+      const int c1 = p1 < n1 ? m.ten_J_colind[a1 + p1] : 0x7fffffff, c2 = p2 < n2 ? m.ten_J_colind[a2 + p2] : 0x7fffffff;
+      const int col = min(c1, c2);
+      float v = 0.0f;
+      if (c1 == col) v += scl * J1[p1++];
+      if (c2 == col) v -= deriv * J2[p2++];
+      d.efc_J[jb + nnz * P] = v;
+      d.efc_J_colind[jb + nnz * P] = col;
+      vel += v * qv[col];
+      nnz++;
+    }
+    d.efc_J_rownnz[(long)wid * njmax + r0] = nnz;
+    put_row_scalars(m, d, wid, r0, vel, pos, pos, iw, sref, simp, margin, fl, type, i);
     return 1;
   }
   // cat 4: contact pyramidal (constraint.py:1668-1936); i = pool slot; contacts a contactfilter took the
@@ -1308,11 +1431,16 @@ __device__ void make_constraint(const mjw_model_t& m, const mjw_data_t& d, int w
   const int dsbl = m.opt_disableflags;
   if (!(dsbl & DSBL_CONSTRAINT)) {
     const int ncon_base = d.ncon_world[2 * (long)wid], ncon = d.ncon_world[2 * (long)wid + 1];
-    for (int cat = 0; cat < 5; cat++) {
-      if (cat <= 1 && (dsbl & DSBL_EQUALITY)) continue;
-      if (cat == 2 && (dsbl & DSBL_FRICTIONLOSS)) continue;
-      if (cat == 3 && (dsbl & DSBL_LIMIT)) continue;
+    // the reference's row order: equality (joint, tendon, flex), friction (dof, tendon), limits (joint,
+    // tendon), contacts
+    const int order[8] = {0, 5, 1, 2, 6, 3, 7, 4};
+    for (int oi = 0; oi < 8; oi++) {
+      const int cat = order[oi];
+      if ((cat <= 1 || cat == 5) && (dsbl & DSBL_EQUALITY)) continue;
+      if ((cat == 2 || cat == 6) && (dsbl & DSBL_FRICTIONLOSS)) continue;
+      if ((cat == 3 || cat == 7) && (dsbl & DSBL_LIMIT)) continue;
       if (cat == 4 && (dsbl & DSBL_CONTACT)) continue;
+      if (cat >= 5 && m.ntendon == 0) continue;
       const int start = run;
       const int neqs = cat == 1 ? m.neq : 1;
       for (int e = 0; e < neqs; e++) {
@@ -1325,6 +1453,8 @@ __device__ void make_constraint(const mjw_model_t& m, const mjw_data_t& d, int w
           n_items = m.flex_edgenum[f];
         } else if (cat == 2) n_items = m.nv;
         else if (cat == 3) n_items = m.njnt;
+        else if (cat == 5) n_items = m.neq;
+        else if (cat >= 6) n_items = m.ntendon;
         else {
           i0 = ncon_base;
           n_items = min(ncon, max(d.naconmax - ncon_base, 0));
@@ -1338,9 +1468,9 @@ __device__ void make_constraint(const mjw_model_t& m, const mjw_data_t& d, int w
           run += chunk;
         }
       }
-      if (cat <= 1) ne += run - start;
-      else if (cat == 2) nf += run - start;
-      else if (cat == 3) nl += run - start;
+      if (cat <= 1 || cat == 5) ne += run - start;
+      else if (cat == 2 || cat == 6) nf += run - start;
+      else if (cat == 3 || cat == 7) nl += run - start;
     }
   }
   if (tid() == 0) {
@@ -1361,8 +1491,12 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid,
     const int a = a0 + tid();
     int nnz = 0;
     if (a < m.nu) {
-      const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
-      nnz = jt0 == JNT_FREE ? 6 : (jt0 == JNT_BALL ? 3 : 1);
+      if (m.actuator_trntype[a] == TRN_TENDON) {
+        nnz = m.ten_J_rownnz[m.actuator_trnid[2 * a]];
+      } else {
+        const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
+        nnz = jt0 == JNT_FREE ? 6 : (jt0 == JNT_BALL ? 3 : 1);
+      }
     }
     int chunk;
     const int rowadr = carry + block_scan(nnz, chunk, sm);
@@ -1370,6 +1504,18 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid,
     if (a >= m.nu) continue;
     const float* gear = gear_all + 6 * a;
     const int trn = m.actuator_trntype[a], j = m.actuator_trnid[2 * a];
+    if (trn == TRN_TENDON) {  // smooth.py:2242-2259: length = ten_length gear0, moment row = gear0 ten_J
+      const long gu = (long)wid * m.nu + a;
+      const float* J = d.ten_J + (long)wid * m.nJten + m.ten_J_rowadr[j];
+      d.actuator_length[gu] = ten_len(m, d, wid, qpos, j) * gear[0];
+      d.moment_rownnz[gu] = nnz;
+      d.moment_rowadr[gu] = rowadr;
+      for (int k = 0; k < nnz; k++) {
+        d.actuator_moment[(long)wid * m.nJmom + rowadr + k] = gear[0] * J[k];
+        d.moment_colind[(long)wid * m.nJmom + rowadr + k] = m.ten_J_colind[m.ten_J_rowadr[j] + k];
+      }
+      continue;
+    }
     const int jt = m.jnt_type[j], qa = m.jnt_qposadr[j], va = m.jnt_dofadr[j];
     float mom[6] = {0, 0, 0, 0, 0, 0}, length;
     if (jt == JNT_FREE) {
@@ -1582,6 +1728,30 @@ __device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, int wid)
     }
   }
   __syncthreads();
+  // passive.py:183-252: tendon velocity, spring (dead band between lengthspring[0] and [1]) and damper; one
+  // tendon per round (rows may share dofs), threads over its Jacobian row
+  if (m.ntendon) {
+    __syncthreads();
+    const float* tst = MR(tendon_stiffness);
+    const float* tdp = MR(tendon_damping);
+    const float* tls = MR(tendon_lengthspring);
+    for (int t = tid(); t < m.ntendon; t += BLK) d.ten_velocity[(long)wid * m.ntendon + t] = ten_vel(m, d, wid, qvel, t);
+    for (int t = 0; t < m.ntendon; t++) {
+      const bool hs = tst[t] != 0.0f && !dsbl_spring, hd = tdp[t] != 0.0f && !dsbl_damper;
+      if (!hs && !hd) continue;
+      const float L = ten_len(m, d, wid, qpos, t), v = ten_vel(m, d, wid, qvel, t);
+      const float lo = tls[2 * t], hi = tls[2 * t + 1];
+      const float fs = L > hi ? tst[t] * (hi - L) : (L < lo ? tst[t] * (lo - L) : 0.0f);
+      const float fd = -tdp[t] * v;
+      const float* J = d.ten_J + (long)wid * m.nJten + m.ten_J_rowadr[t];
+      for (int k = tid(); k < m.ten_J_rownnz[t]; k += BLK) {
+        const int dof = m.ten_J_colind[m.ten_J_rowadr[t] + k];
+        if (hs) qs[dof] += J[k] * fs;
+        if (hd) qd[dof] += J[k] * fd;
+      }
+      __syncthreads();
+    }
+  }
   // passive.py:829-869: gravity compensation and fluid forces (mjw_passive.h), per-body wrenches in the
   // sp_body / cacc scratch (rne fills both afterwards), then per dof over its body's subtree
   float* qp = d.qfrc_passive + (long)wid * nv;
@@ -1675,6 +1845,23 @@ __device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, int wid)
     bias[i] = s;
   }
   __syncthreads();
+  // smooth.py:1878-1932 tendon_bias: armature J (Jdot qvel) of the spatial tendons, BLK tendons per round
+  if (m.nten_spatial) {
+    __shared__ float coef[BLK];
+    const TenFrames f = ten_frames(m, d, wid);
+    for (int base = 0; base < m.ntendon; base += BLK) {
+      const int t = base + tid();
+      coef[tid()] = t < m.ntendon ? tendon_bias_coef(m, wid, t, qvel, f, cvel_all, cdot) : 0.0f;
+      __syncthreads();
+      for (int q = 0; q < BLK && base + q < m.ntendon; q++) {
+        if (coef[q] == 0.0f) continue;
+        const int tq = base + q, ra = m.ten_J_rowadr[tq];
+        for (int k = tid(); k < m.ten_J_rownnz[tq]; k += BLK)
+          bias[m.ten_J_colind[ra + k]] += coef[q] * d.ten_J[(long)wid * m.nJten + ra + k];
+        __syncthreads();
+      }
+    }
+  }
 }
 
 // forward.py:616-927 actuation (gain / bias / activation dynamics, joint actuator force limits)
@@ -1723,6 +1910,22 @@ __device__ void fwd_actuation(const mjw_model_t& m, const mjw_data_t& d, int wid
     d.actuator_force[gu] = force;
   }
   __syncthreads();
+  // forward.py:739-779: the total force of the actuators on a force-limited tendon scaled into its range
+  if (m.ntendon) {
+    const float* rng = MR(tendon_actfrcrange);
+    float* force = d.actuator_force + (long)wid * m.nu;
+    for (int t = tid(); t < m.ntendon; t += BLK) {
+      if (!m.tendon_actfrclimited[t]) continue;
+      float tot = 0.0f;
+      for (int a = 0; a < m.nu; a++)
+        if (m.actuator_trntype[a] == TRN_TENDON && m.actuator_trnid[2 * a] == t) tot += force[a];
+      const float sc = tot < rng[2 * t] ? rng[2 * t] / tot : (tot > rng[2 * t + 1] ? rng[2 * t + 1] / tot : 1.0f);
+      if (sc != 1.0f)
+        for (int a = 0; a < m.nu; a++)
+          if (m.actuator_trntype[a] == TRN_TENDON && m.actuator_trnid[2 * a] == t) force[a] *= sc;
+    }
+    __syncthreads();
+  }
   const float* jfr = MR(jnt_actfrcrange);
   for (int i = tid(); i < nv; i += BLK) {
     float q = 0.0f;
@@ -1792,6 +1995,7 @@ __global__ void __launch_bounds__(BLK, 4) forward_kernel(const mjw_model_t m, co
     flex_edges(m, d, wid);
     SPROF_MARK(SPH_FLEX);
     crb_qM(m, d, wid);
+    if (m.ntendon) tendons(m, d, wid);
     SPROF_MARK(SPH_CRB);
   }
   if constexpr ((S & SP_COLL) != 0) {
@@ -2536,6 +2740,22 @@ __global__ void __launch_bounds__(BLK) euler_kernel(const mjw_model_t m, const m
             for (int q2 = 0; q2 < rn - 1; q2++)
               if (m.M_colind[adr + q2] == j) pos = adr + q2;
           if (pos >= 0) LD2[pos] -= dt * vel * d.actuator_moment[base + k1] * d.actuator_moment[base + k2];
+        }
+        __syncthreads();
+      }
+    }
+    if (implicitfast && m.ntendon && !(fl & DSBL_DAMPER)) {
+      // derivative.py:267-320: tendon damping enters qDeriv as -damping J_i J_j on the ancestor pattern of M
+      const float* tdamp = MR(tendon_damping);
+      for (int t = 0; t < m.ntendon; t++) {
+        if (tdamp[t] == 0.0f) continue;
+        const int rn = m.ten_J_rownnz[t], ra = m.ten_J_rowadr[t];
+        const float* J = d.ten_J + (long)wid * m.nJten + ra;
+        for (int p = tid(); p < rn * rn; p += BLK) {
+          const int k1 = p / rn, k2 = p - k1 * rn;
+          if (k2 > k1) continue;
+          const int pos = m_pos(m, m.ten_J_colind[ra + k1], m.ten_J_colind[ra + k2]);
+          if (pos >= 0) LD2[pos] += dt * tdamp[t] * J[k1] * J[k2];
         }
         __syncthreads();
       }

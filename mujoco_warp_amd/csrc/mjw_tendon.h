@@ -319,8 +319,9 @@ __device__ float spatial_tendon(const mjw_model_t& m, int wid, float* J, int t, 
 // position stage: ten_length, ten_J (Data contract).  Spatial tendons: one lane per tendon accumulates
 // its row in registers-then-global (the row's owner is the only writer); the caller syncs the wave
 // before any reader.
-__device__ __forceinline__ void tendon_pos(const mjw_model_t& m, const mjw_data_t& d, const float* qpos, const TenFrames& f, int wid, int lane) {
-  for (int t = lane; t < m.ntendon; t += 64) {
+__device__ __forceinline__ void tendon_pos(const mjw_model_t& m, const mjw_data_t& d, const float* qpos, const TenFrames& f, int wid, int lane,
+                                           int stride = 64) {
+  for (int t = lane; t < m.ntendon; t += stride) {
     float* J = d.ten_J + (long)wid * m.nJten + m.ten_J_rowadr[t];
     if (ten_spatial(m, t)) {
       for (int k = 0; k < m.ten_J_rownnz[t]; k++) J[k] = 0.0f;
@@ -356,49 +357,53 @@ __device__ __forceinline__ float ten_jacdot_chain(const mjw_model_t& m, int body
   return acc;
 }
 
-// smooth.py:1656-1932 (_tendon_dot, tendon_bias): qfrc_bias += armature J (Jdot qvel) for the spatial tendons
-// with armature; as the reference, a site-geom-site wrap ends its tendon's Jdot (segments before it count).
-// out[nv]: the bias added per dof (LDS); coef[64]: LDS scratch.
+// smooth.py:1656-1840 (_tendon_dot, _tendon_bias_coef): armature_t (dJ_t/dt qvel) of spatial tendon t (0 for fixed
+// tendons and tendons without armature); as the reference, a site-geom-site wrap ends the tendon's Jdot
+// (segments before it count)
+__device__ float tendon_bias_coef(const mjw_model_t& m, int wid, int t, const float* qvel, const TenFrames& f, const float* cvel,
+                                  const float* cdof_dot) {
+  const float* arm = MR(tendon_armature);
+  if (arm[t] == 0.0f || !ten_spatial(m, t)) return 0.0f;
+  const int a = m.tendon_adr[t], n = m.tendon_num[t];
+  float divisor = 1.0f, c = 0.0f;
+  for (int j = 0; j < n - 1; j++) {
+    const int t0 = m.wrap_type[a + j], t1 = m.wrap_type[a + j + 1];
+    if (t0 == WRAP_PULLEY || t1 == WRAP_PULLEY) {
+      if (t0 == WRAP_PULLEY) divisor = MR(wrap_prm)[a + j];
+      continue;
+    }
+    if (t1 == WRAP_SPHERE || t1 == WRAP_CYLINDER) break;
+    const int s0 = m.wrap_objid[a + j], s1 = m.wrap_objid[a + j + 1];
+    const int b0 = m.site_bodyid[s0], b1 = m.site_bodyid[s1];
+    if (b0 == b1) continue;
+    const float *p0 = f.site_xpos + 3 * s0, *p1 = f.site_xpos + 3 * s1;
+    const float *sc0 = f.subtree_com + 3 * m.body_rootid[b0], *sc1 = f.subtree_com + 3 * m.body_rootid[b1];
+    float off0[3], off1[3], v0[3], v1[3], dif[3], c0[3], c1[3];
+    for (int i = 0; i < 3; i++) { off0[i] = p0[i] - sc0[i]; off1[i] = p1[i] - sc1[i]; dif[i] = p1[i] - p0[i]; }
+    cross3(c0, off0, cvel + 6 * b0);
+    cross3(c1, off1, cvel + 6 * b1);
+    for (int i = 0; i < 3; i++) { v0[i] = cvel[6 * b0 + 3 + i] - c0[i]; v1[i] = cvel[6 * b1 + 3 + i] - c1[i]; }
+    const float nrm = sqrtf(dot3(dif, dif));
+    float dpnt[3], dvel[3];
+    for (int i = 0; i < 3; i++) dpnt[i] = nrm > 0.0f ? dif[i] / nrm : 0.0f;
+    for (int i = 0; i < 3; i++) dvel[i] = v1[i] - v0[i];
+    const float dt = dot3(dpnt, dvel);
+    for (int i = 0; i < 3; i++) dvel[i] = nrm > MJW_MINVAL ? (dvel[i] - dpnt[i] * dt) / nrm : 0.0f;
+    const float inv = ten_safe_div(1.0f, divisor);
+    c += inv * (ten_jacdot_chain(m, b1, off1, v1, dpnt, dvel, f.cdof, cdof_dot, cvel, qvel) -
+                ten_jacdot_chain(m, b0, off0, v0, dpnt, dvel, f.cdof, cdof_dot, cvel, qvel));
+  }
+  return c * arm[t];
+}
+
+// smooth.py:1843-1932 (_tendon_bias_qfrc): out[i] = sum_t coef_t J_ti for the wave's world (lane stride 64;
+// coef: 64 floats of LDS scratch)
 __device__ __forceinline__ void tendon_bias(const mjw_model_t& m, const mjw_data_t& d, int wid, int lane, const float* qvel, const TenFrames& f,
                                             const float* cvel, const float* cdof_dot, float* coef, float* out) {
-  const float* arm = MR(tendon_armature);
   for (int i = lane; i < m.nv; i += 64) out[i] = 0.0f;
   for (int base = 0; base < m.ntendon; base += 64) {
     const int t = base + lane;
-    float c = 0.0f;
-    if (t < m.ntendon && arm[t] != 0.0f && ten_spatial(m, t)) {
-      const int a = m.tendon_adr[t], n = m.tendon_num[t];
-      float divisor = 1.0f;
-      for (int j = 0; j < n - 1; j++) {
-        const int t0 = m.wrap_type[a + j], t1 = m.wrap_type[a + j + 1];
-        if (t0 == WRAP_PULLEY || t1 == WRAP_PULLEY) {
-          if (t0 == WRAP_PULLEY) divisor = MR(wrap_prm)[a + j];
-          continue;
-        }
-        if (t1 == WRAP_SPHERE || t1 == WRAP_CYLINDER) break;
-        const int s0 = m.wrap_objid[a + j], s1 = m.wrap_objid[a + j + 1];
-        const int b0 = m.site_bodyid[s0], b1 = m.site_bodyid[s1];
-        if (b0 == b1) continue;
-        const float *p0 = f.site_xpos + 3 * s0, *p1 = f.site_xpos + 3 * s1;
-        const float *sc0 = f.subtree_com + 3 * m.body_rootid[b0], *sc1 = f.subtree_com + 3 * m.body_rootid[b1];
-        float off0[3], off1[3], v0[3], v1[3], dif[3], c0[3], c1[3];
-        for (int i = 0; i < 3; i++) { off0[i] = p0[i] - sc0[i]; off1[i] = p1[i] - sc1[i]; dif[i] = p1[i] - p0[i]; }
-        cross3(c0, off0, cvel + 6 * b0);
-        cross3(c1, off1, cvel + 6 * b1);
-        for (int i = 0; i < 3; i++) { v0[i] = cvel[6 * b0 + 3 + i] - c0[i]; v1[i] = cvel[6 * b1 + 3 + i] - c1[i]; }
-        const float nrm = sqrtf(dot3(dif, dif));
-        float dpnt[3], dvel[3];
-        for (int i = 0; i < 3; i++) dpnt[i] = nrm > 0.0f ? dif[i] / nrm : 0.0f;
-        for (int i = 0; i < 3; i++) dvel[i] = v1[i] - v0[i];
-        const float dt = dot3(dpnt, dvel);
-        for (int i = 0; i < 3; i++) dvel[i] = nrm > MJW_MINVAL ? (dvel[i] - dpnt[i] * dt) / nrm : 0.0f;
-        const float inv = ten_safe_div(1.0f, divisor);
-        c += inv * (ten_jacdot_chain(m, b1, off1, v1, dpnt, dvel, f.cdof, cdof_dot, cvel, qvel) -
-                    ten_jacdot_chain(m, b0, off0, v0, dpnt, dvel, f.cdof, cdof_dot, cvel, qvel));
-      }
-      c *= arm[t];
-    }
-    coef[lane] = c;
+    coef[lane] = t < m.ntendon ? tendon_bias_coef(m, wid, t, qvel, f, cvel, cdof_dot) : 0.0f;
     __syncthreads();
     for (int i = lane; i < m.nv; i += 64) {
       float acc = 0.0f;

@@ -157,8 +157,8 @@ def put_model(mjm, device=None) -> types.Model:
       # the sensor kernel (csrc/mjw_sensor.hip) stages a world's body / dof state in 64 KB of LDS
       if 37 * mjm.nbody + 14 * mjm.nv > 16384:
         raise NotImplementedError("sparse / flex models: sensors need 37 nbody + 14 nv <= 16384 in this build (the flex bodies exceed it).")
-    if getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.JOINT, types.EqType.FLEX))):
-      raise NotImplementedError("sparse / flex models: only joint and flex equality constraints are supported by this build yet.")
+    if getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.JOINT, types.EqType.FLEX, types.EqType.TENDON))):
+      raise NotImplementedError("sparse / flex models: only joint, tendon and flex equality constraints are supported by this build yet.")
     if np.any(mjm.jnt_limited & (mjm.jnt_type == JointType.BALL)):
       raise NotImplementedError("sparse / flex models: ball joint limits are not supported by this build yet.")
     if getattr(mjm, "nflex", 0) and np.any(mjm.flex_dim != 2):
@@ -192,9 +192,6 @@ def put_model(mjm, device=None) -> types.Model:
       raise NotImplementedError("muscle actuators need an actuator_lengthrange (lengthrange attribute, or a limited joint / tendon transmission).")
   if sparse and np.any((mjm.actuator_trntype > types.TrnType.JOINTINPARENT) & (mjm.actuator_trntype != types.TrnType.TENDON)):
     raise NotImplementedError("sparse / flex models: only joint and tendon transmissions are supported by this build yet.")
-  ntendon = int(getattr(mjm, "ntendon", 0))
-  if ntendon and sparse:
-    raise NotImplementedError("sparse / flex models: tendons are not supported by this build yet.")
   if (mjm.opt.viscosity > 0 or mjm.opt.density > 0) and mjm.opt.integrator in (types.IntegratorType.IMPLICITFAST, types.IntegratorType.IMPLICIT):
     raise NotImplementedError("Implicit integrators and fluid model not implemented.")  # io.py:126-130
 
@@ -321,7 +318,12 @@ def put_model(mjm, device=None) -> types.Model:
   maxchain = int(chain.max()) if nv else 0
   m.ntree = len(starts)
   nflex = int(getattr(mjm, "nflex", 0))
-  m.njrow = max(2 * maxchain, 6 if nflex else 0, 2) if sparse else m.nv_pad
+  # tendon rows (friction, limit: one tendon's Jacobian row; equality: the union of two) fit a J row too
+  ten_w = int(max(mjm.ten_J_rownnz)) if getattr(mjm, "ntendon", 0) else 0
+  for e in range(int(getattr(mjm, "neq", 0))):
+    if mjm.eq_type[e] == types.EqType.TENDON and mjm.eq_obj2id[e] >= 0:
+      ten_w = max(ten_w, int(mjm.ten_J_rownnz[mjm.eq_obj1id[e]] + mjm.ten_J_rownnz[mjm.eq_obj2id[e]]))
+  m.njrow = max(2 * maxchain, 6 if nflex else 0, 2, ten_w) if sparse else m.nv_pad
   # flex collision candidates (collision_flex.py:381-529 tests every sphere / capsule / box / cylinder
   # geom whose contype / conaffinity matches) and planes (:261-378)
   cg_adr, cg = [0], []

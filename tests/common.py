@@ -158,3 +158,13 @@ def oracle_rows(od, w, nv):
     margin=od.efc_margin[w, :n],
     type=od.efc_type[w, :n],
   )
+
+
+def dense_efc_J(m, d, w):
+  """The first nefc constraint Jacobian rows of world w as a dense (n, nv) array, from either layout."""
+  n = min(int(d.nefc[w]), d.njmax)
+  if not m.is_sparse:
+    return np_(d.efc.J[w, :n, :m.nv])
+  from tests.cloth_common import dense_J
+
+  return dense_J(d, w, n, m.nv)

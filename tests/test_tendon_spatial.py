@@ -229,15 +229,19 @@ def test_wrap_model_wraps():
 
 # ---- GPU ------------------------------------------------------------------------------------------
 @pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
 @pytest.mark.parametrize("path", TENDON_XML, ids=[os.path.basename(p)[:-4] for p in TENDON_XML])
-def test_gpu_tendon_models_match_oracle(path):
+def test_gpu_tendon_models_match_oracle(path, sparse):
   """Forward on the device against the oracle: ten_length / ten_J / ten_velocity, qfrc_bias (armature bias),
-  qfrc_passive and qacc, on 8 worlds around the keyframe."""
+  qfrc_passive and qacc, on 8 worlds around the keyframe; dense (world-per-wave) and sparse
+  (workgroup-per-world, jacobian = sparse) paths."""
   import torch
 
   import mujoco_warp_amd as mjw
 
   mjm = _load(path)
+  if sparse:
+    mjm.opt.jacobian = 1
   if mjm.ntendon:
     mjm.tendon_armature = np.where(np.arange(mjm.ntendon) % 2 == 0, 0.3, 0.0)
   qpos, qvel, ctrl = _key_state(mjm, nworld=8, seed=5)
@@ -286,7 +290,8 @@ def test_oracle_tendon_equality_rows():
 
 
 @pytest.mark.gpu
-def test_gpu_tendon_equality_matches_oracle():
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gpu_tendon_equality_matches_oracle(sparse):
   import torch
 
   import mujoco_warp_amd as mjw
@@ -294,16 +299,21 @@ def test_gpu_tendon_equality_matches_oracle():
   from tests.parity_models import efc_cost
 
   mjm = mjcf.load_model_from_string(TENDON_EQ)
+  if sparse:
+    mjm.opt.jacobian = 1
   qpos, qvel, ctrl = _key_state(mjm, nworld=8, seed=8)
   m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=16, nconmax=4)
+  assert bool(m.is_sparse) == sparse
   _, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=16, nconmax=4)
   mjw.forward(m, d)
   od.forward()
   torch.cuda.synchronize()
+  from tests.common import dense_efc_J
+
   for w in range(8):
     n = int(od.nefc[w, 0])
     assert int(d.nefc[w]) == n == 2
     np.testing.assert_allclose(np_(d.efc.pos[w, :n]), od.efc_pos[w, :n], atol=2e-6)
-    np.testing.assert_allclose(np_(d.efc.J[w, :n, :mjm.nv]), od.efc_J[w].reshape(16, mjm.nv)[:n], atol=2e-5)
+    np.testing.assert_allclose(dense_efc_J(m, d, w)[:n], od.efc_J[w].reshape(16, mjm.nv)[:n], atol=2e-5)
   err = np.abs(np_(d.qacc) - od.qacc).max() / max(1.0, float(np.abs(od.qacc).max()))
   assert err < 5e-3, err
