@@ -31,15 +31,16 @@ def needs_build():
   return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
 
 
-def build(force=False, verbose=False, out=None, defines=()):
-  """Compile SOURCES into `out` (default libmjw_amd.so); `defines` e.g. ("MJW_PROFILE",)."""
+def build(force=False, verbose=False, out=None, defines=(), extra_flags=()):
+  """Compile SOURCES into `out` (default libmjw_amd.so); `defines` e.g. ("MJW_PROFILE",); `extra_flags`
+  e.g. ("-gline-tables-only",) for a PC-sampling build (same code, source line tables)."""
   OUT_ = out or OUT
   if out is None and not force and not needs_build():
     return OUT
   # one object per translation unit, compiled in parallel, then linked
   flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=on", "-fPIC", "-I", os.path.join(_ROOT, "include")]
-  flags += [f"-D{x}" for x in defines]
-  tag = "_".join(defines).lower()
+  flags += [f"-D{x}" for x in defines] + list(extra_flags)
+  tag = "_".join(defines).lower() + ("_x" if extra_flags else "")
   objs, procs = [], []
   for src in SOURCES:
     obj = os.path.join(_PKG, "csrc", os.path.basename(src) + tag + ".o")

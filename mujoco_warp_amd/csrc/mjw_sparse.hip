@@ -32,6 +32,7 @@
 #include "mjw_flexcol.h"
 #include "mjw_passive.h"
 #include "mjw_tendon.h"
+#include "mjw_trn.h"
 
 namespace mjw {
 namespace sp {
@@ -1153,13 +1154,227 @@ __device__ void put_row_scalars(const mjw_model_t& m, const mjw_data_t& d, int w
   d.efc_id[gr] = id;
 }
 
+// constraint.py:124-365 (_equality_connect) and :792-1110 (_equality_weld), equality e: 3 (6) rows from
+// r0 on, J over the union of the two bodies' dof chains (descending, as the contact rows), one thread
+__device__ void eq_connect_weld_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int e, int r0, bool weld) {
+  const float* data = MR(eq_data) + 11 * e;
+  const int o1 = m.eq_obj1id[e], o2 = m.eq_obj2id[e];
+  const bool site = m.eq_objtype[e] == OBJ_SITE && m.nsite > 0;
+  const long wb = (long)wid * m.nbody;
+  const float* xpos = d.xpos + wb * 3;
+  const float* xquat = d.xquat + wb * 4;
+  const float* xmat = d.xmat + wb * 9;
+  int b1, b2;
+  float p1[3], p2[3], q[4] = {1, 0, 0, 0}, q1[4] = {1, 0, 0, 0};
+  if (site) {
+    const float* site_quat = MR(site_quat);
+    const float* sx = d.site_xpos + (long)wid * m.nsite * 3;
+    b1 = m.site_bodyid[o1];
+    b2 = m.site_bodyid[o2];
+    for (int k = 0; k < 3; k++) { p1[k] = sx[3 * o1 + k]; p2[k] = sx[3 * o2 + k]; }
+    if (weld) {
+      float t[4];
+      mul_quat(q, xquat + 4 * b1, site_quat + 4 * o1);
+      mul_quat(t, xquat + 4 * b2, site_quat + 4 * o2);
+      q1[0] = t[0]; q1[1] = -t[1]; q1[2] = -t[2]; q1[3] = -t[3];
+    }
+  } else {
+    b1 = o1;
+    b2 = o2;
+    const float* a1 = weld ? data + 3 : data;  // the weld reads its anchors swapped (constraint.py:855-856)
+    const float* a2 = weld ? data : data + 3;
+    matvec3(p1, xmat + 9 * b1, a1);
+    matvec3(p2, xmat + 9 * b2, a2);
+    for (int k = 0; k < 3; k++) { p1[k] += xpos[3 * b1 + k]; p2[k] += xpos[3 * b2 + k]; }
+    if (weld) {
+      mul_quat(q, xquat + 4 * b1, data + 6);
+      q1[0] = xquat[4 * b2]; q1[1] = -xquat[4 * b2 + 1]; q1[2] = -xquat[4 * b2 + 2]; q1[3] = -xquat[4 * b2 + 3];
+    }
+  }
+  const float ts = data[10];
+  const int nrow = weld ? 6 : 3;
+  const float* sc = d.subtree_com + wb * 3;
+  const float* cdof = d.cdof + (long)wid * m.nv * 6;
+  const float* qvel = d.qvel + (long)wid * m.nv;
+  float off1[3], off2[3];
+  for (int x = 0; x < 3; x++) {
+    off1[x] = p1[x] - sc[3 * m.body_rootid[b1] + x];
+    off2[x] = p2[x] - sc[3 * m.body_rootid[b2] + x];
+  }
+  const int w1 = m.body_weldid[b1], w2 = m.body_weldid[b2];
+  const long P = d.njmax_pad;
+  float jq[6] = {0, 0, 0, 0, 0, 0};
+  int i1 = w1 > 0 ? m.body_dofadr[w1] + m.body_dofnum[w1] - 1 : -1;
+  int i2 = w2 > 0 ? m.body_dofadr[w2] + m.body_dofnum[w2] - 1 : -1;
+  int nnz = 0;
+  while ((i1 >= 0 || i2 >= 0) && nnz < m.njrow) {
+    const int dof = max(i1, i2);
+    const float* c = cdof + 6 * dof;
+    float v[6] = {0, 0, 0, 0, 0, 0}, dr[3] = {0, 0, 0}, cr[3];
+    if (dof == i1) {
+      cross3(cr, c, off1);
+      for (int x = 0; x < 3; x++) { v[x] += c[3 + x] + cr[x]; dr[x] += c[x]; }
+      i1 = m.dof_parentid[i1];
+    }
+    if (dof == i2) {
+      cross3(cr, c, off2);
+      for (int x = 0; x < 3; x++) { v[x] -= c[3 + x] + cr[x]; dr[x] -= c[x]; }
+      i2 = m.dof_parentid[i2];
+    }
+    if (weld) {
+      float t[4], u[4];
+      for (int x = 0; x < 3; x++) dr[x] *= ts;
+      quat_mul_axis(t, q1, dr);
+      mul_quat(u, t, q);
+      for (int x = 0; x < 3; x++) v[3 + x] = 0.5f * u[1 + x];
+    }
+    for (int k = 0; k < nrow; k++) {
+      if (r0 + k >= d.njmax) break;
+      const long jb = (long)wid * m.njrow * P + r0 + k;
+      d.efc_J[jb + nnz * P] = v[k];
+      d.efc_J_colind[jb + nnz * P] = dof;
+      jq[k] += v[k] * qvel[dof];
+    }
+    nnz++;
+  }
+  float cpos[6], pos_imp;
+  for (int k = 0; k < 3; k++) cpos[k] = p1[k] - p2[k];
+  if (weld) {
+    float cq[4];
+    mul_quat(cq, q1, q);
+    for (int k = 0; k < 3; k++) cpos[3 + k] = cq[1 + k] * ts;
+    pos_imp = sqrtf(dot3(cpos, cpos) + dot3(cpos + 3, cpos + 3));
+  } else {
+    pos_imp = sqrtf(dot3(cpos, cpos));
+  }
+  const float* biw = MR(body_invweight0);
+  for (int k = 0; k < nrow && r0 + k < d.njmax; k++) {
+    const int cc = k < 3 ? 0 : 1;
+    d.efc_J_rownnz[(long)wid * d.njmax + r0 + k] = nnz;
+    put_row_scalars(m, d, wid, r0 + k, jq[k], cpos[k], pos_imp, biw[2 * b1 + cc] + biw[2 * b2 + cc], MR(eq_solref) + 2 * e,
+                    MR(eq_solimp) + 5 * e, 0.0f, 0.0f, CNSTR_EQUALITY, e);
+  }
+}
+
+// constraint.py:1940-2207 (_contact_elliptic): contact i's condim rows from r0 on -- row dimid projects
+// the relative Jacobian on frame row dimid (translational below 3, rotational after); the friction rows
+// scale invweight by impratio^-1 and (fri0 / frii)^2, use solreffriction when set, and have no position
+// term.  J over the union of the two weld bodies' dof chains, as the pyramidal rows.
+__device__ void contact_elliptic_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int i, int r0, int condim, float pos,
+                                      float includemargin) {
+  const int g1 = d.contact_geom[2 * (long)i], g2 = d.contact_geom[2 * (long)i + 1];
+  const int body1 = g1 >= 0 ? m.geom_bodyid[g1] : m.flex_vertbodyid[m.flex_vertadr[d.contact_flex[2 * (long)i]] + d.contact_vert[2 * (long)i]];
+  const int body2 =
+    g2 >= 0 ? m.geom_bodyid[g2] : m.flex_vertbodyid[m.flex_vertadr[d.contact_flex[2 * (long)i + 1]] + d.contact_vert[2 * (long)i + 1]];
+  const float* biw = MR(body_invweight0);
+  const float iw_base = biw[2 * body1] + biw[2 * body2];
+  const int w1 = m.body_weldid[body1], w2 = m.body_weldid[body2];
+  const float* frame = d.contact_frame + 9 * (long)i;
+  const float* cpos = d.contact_pos + 3 * (long)i;
+  const float* sc = d.subtree_com + (long)wid * m.nbody * 3;
+  const float* cdof = d.cdof + (long)wid * m.nv * 6;
+  const float* qvel = d.qvel + (long)wid * m.nv;
+  const float* fr = d.contact_friction + 5 * (long)i;
+  const float iri = MR(opt_impratio_invsqrt)[0];
+  float off1[3], off2[3];
+  for (int x = 0; x < 3; x++) {
+    off1[x] = cpos[x] - sc[3 * m.body_rootid[w1] + x];
+    off2[x] = cpos[x] - sc[3 * m.body_rootid[w2] + x];
+  }
+  const long P = d.njmax_pad;
+  for (int dimid = 0; dimid < condim; dimid++) {
+    const int r = r0 + dimid;
+    if (r >= d.njmax) {
+      d.contact_efc_address[(long)i * m.nmaxpyramid + dimid] = -1;
+      continue;
+    }
+    d.contact_efc_address[(long)i * m.nmaxpyramid + dimid] = r;
+    const long jb = (long)wid * m.njrow * P + r;
+    int i1 = w1 > 0 ? m.body_dofadr[w1] + m.body_dofnum[w1] - 1 : -1;
+    int i2 = w2 > 0 ? m.body_dofadr[w2] + m.body_dofnum[w2] - 1 : -1;
+    int nnz = 0;
+    float vel = 0.0f;
+    const float* fv = frame + 3 * (dimid < 3 ? dimid : dimid - 3);
+    while ((i1 >= 0 || i2 >= 0) && nnz < m.njrow) {
+      const int dof = max(i1, i2);
+      const float* c = cdof + 6 * dof;
+      float jd[3] = {0, 0, 0}, cr[3];
+      if (dof == i1) {
+        if (dimid < 3) {
+          cross3(cr, c, off1);
+          for (int x = 0; x < 3; x++) jd[x] -= c[3 + x] + cr[x];
+        } else {
+          for (int x = 0; x < 3; x++) jd[x] -= c[x];
+        }
+        i1 = m.dof_parentid[i1];
+      }
+      if (dof == i2) {
+        if (dimid < 3) {
+          cross3(cr, c, off2);
+          for (int x = 0; x < 3; x++) jd[x] += c[3 + x] + cr[x];
+        } else {
+          for (int x = 0; x < 3; x++) jd[x] += c[x];
+        }
+        i2 = m.dof_parentid[i2];
+      }
+      const float Jval = fv[0] * jd[0] + fv[1] * jd[1] + fv[2] * jd[2];
+      d.efc_J[jb + nnz * P] = Jval;
+      d.efc_J_colind[jb + nnz * P] = dof;
+      vel += Jval * qvel[dof];
+      nnz++;
+    }
+    d.efc_J_rownnz[(long)wid * d.njmax + r] = nnz;
+    float invw = iw_base, pos_aref = pos;
+    const float* sr = d.contact_solref + 2 * (long)i;
+    if (dimid > 0) {
+      const float* srf = d.contact_solreffriction + 2 * (long)i;
+      if (srf[0] != 0.0f || srf[1] != 0.0f) sr = srf;
+      invw = invw * iri * iri;
+      if (dimid > 1) {
+        const float fri0 = fr[0], frii = fr[dimid - 1];
+        invw *= fri0 * fri0 / (frii * frii);
+      }
+      pos_aref = 0.0f;
+    }
+    put_row_scalars(m, d, wid, r, vel, pos_aref, pos, invw, sr, d.contact_solimp + 5 * (long)i, includemargin, 0.0f, CNSTR_CONTACT_ELLIPTIC, i);
+  }
+}
+
 // rows contributed by item i of a category (cat: 0 eq joint, 1 flex edge of eq e, 2 friction dof,
-// 3 limit joint, 4 contact); writes them from row r0 when r0 >= 0
+// 3 limit joint, 4 contact, 5-7 tendon equality / friction / limit, 8 eq connect, 9 eq weld, 10 ball
+// joint limit); writes them from row r0 when r0 >= 0
 __device__ int make_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int cat, int i, int e, int r0) {
   const float* qpos = d.qpos + (long)wid * m.nq;
   const float* qpos0 = MR(qpos0);
   const float* dof_invweight0 = MR(dof_invweight0);
   const int njmax = d.njmax;
+  if (cat == 8 || cat == 9) {
+    if (m.eq_type[i] != (cat == 9 ? EQ_WELD : EQ_CONNECT) || !d.eq_active[(long)wid * m.neq + i]) return 0;
+    const int nrow = cat == 9 ? 6 : 3;
+    if (r0 < 0) return nrow;
+    if (r0 < njmax) eq_connect_weld_rows(m, d, wid, i, r0, cat == 9);
+    return nrow;
+  }
+  if (cat == 10) {  // constraint.py:1421-1543: one row on the ball joint's 3 dofs along -axis
+    if (!m.jnt_limited[i] || m.jnt_type[i] != JNT_BALL) return 0;
+    const float* qp = qpos + m.jnt_qposadr[i];
+    float q[4] = {qp[0], qp[1], qp[2], qp[3]}, aa[3], axis[3];
+    normalize4(q);
+    quat_to_vel(aa, q);
+    const float angle = sqrtf(dot3(aa, aa));  // math.py:261-265 normalize_with_norm
+    for (int k = 0; k < 3; k++) axis[k] = angle == 0.0f ? aa[k] : aa[k] / angle;
+    const float* rng = MR(jnt_range) + 2 * i;
+    const float margin = MR(jnt_margin)[i];
+    const float pos = fmaxf(rng[0], rng[1]) - angle - margin;
+    if (!(pos < 0.0f)) return 0;
+    if (r0 < 0 || r0 >= njmax) return 1;
+    const int da = m.jnt_dofadr[i];
+    const int cols[3] = {da + 2, da + 1, da};  // descending, as the chain rows
+    const float vals[3] = {-axis[2], -axis[1], -axis[0]};
+    put_row(m, d, wid, r0, 3, cols, vals, pos, pos, dof_invweight0[da], MR(jnt_solref) + 2 * i, MR(jnt_solimp) + 5 * i, margin, 0.0f,
+            CNSTR_LIMIT_JOINT, i);
+    return 1;
+  }
   if (cat == 0) {
     if (m.eq_type[i] != EQ_JOINT || !d.eq_active[(long)wid * m.neq + i]) return 0;
     if (r0 < 0 || r0 >= njmax) return 1;
@@ -1313,11 +1528,16 @@ __device__ int make_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int
     return 0;
   }
   const int condim = d.contact_dim[i];
-  const int nrow = condim == 1 ? 1 : 2 * (condim - 1);
+  const bool ell = m.opt_cone == CONE_ELLIPTIC && condim > 1;
+  const int nrow = condim == 1 ? 1 : (ell ? condim : 2 * (condim - 1));
   const float includemargin = d.contact_includemargin[i];
   const float pos = d.contact_dist[i] - includemargin;
   if (!(pos < 0.0f)) return 0;
   if (r0 < 0) return nrow;
+  if (ell) {
+    contact_elliptic_rows(m, d, wid, i, r0, condim, pos, includemargin);
+    return nrow;
+  }
   const int g1 = d.contact_geom[2 * (long)i], g2 = d.contact_geom[2 * (long)i + 1];
   const int body1 = g1 >= 0 ? m.geom_bodyid[g1] : m.flex_vertbodyid[m.flex_vertadr[d.contact_flex[2 * (long)i]] + d.contact_vert[2 * (long)i]];
   const int body2 =
@@ -1431,21 +1651,25 @@ __device__ void make_constraint(const mjw_model_t& m, const mjw_data_t& d, int w
   const int dsbl = m.opt_disableflags;
   if (!(dsbl & DSBL_CONSTRAINT)) {
     const int ncon_base = d.ncon_world[2 * (long)wid], ncon = d.ncon_world[2 * (long)wid + 1];
-    // the reference's row order: equality (joint, tendon, flex), friction (dof, tendon), limits (joint,
-    // tendon), contacts
-    const int order[8] = {0, 5, 1, 2, 6, 3, 7, 4};
-    for (int oi = 0; oi < 8; oi++) {
+    // the reference's row order (constraint.py:2209-2779 launch order): equality (connect, weld, joint,
+    // tendon, flex), friction (dof, tendon), limits (ball, slide / hinge, tendon), contacts
+    const int order[11] = {8, 9, 0, 5, 1, 2, 6, 10, 3, 7, 4};
+    for (int oi = 0; oi < 11; oi++) {
       const int cat = order[oi];
-      if ((cat <= 1 || cat == 5) && (dsbl & DSBL_EQUALITY)) continue;
+      const bool eq = cat <= 1 || cat == 5 || cat == 8 || cat == 9, lim = cat == 3 || cat == 7 || cat == 10;
+      if (eq && (dsbl & DSBL_EQUALITY)) continue;
       if ((cat == 2 || cat == 6) && (dsbl & DSBL_FRICTIONLOSS)) continue;
-      if ((cat == 3 || cat == 7) && (dsbl & DSBL_LIMIT)) continue;
+      if (lim && (dsbl & DSBL_LIMIT)) continue;
       if (cat == 4 && (dsbl & DSBL_CONTACT)) continue;
-      if (cat >= 5 && m.ntendon == 0) continue;
+      if (cat >= 5 && cat <= 7 && m.ntendon == 0) continue;
+      if ((cat == 8 || cat == 9) && m.neq_cw == 0) continue;
+      if (cat == 10 && m.nlimited_ball == 0) continue;
       const int start = run;
       const int neqs = cat == 1 ? m.neq : 1;
       for (int e = 0; e < neqs; e++) {
         int n_items, i0 = 0;
-        if (cat == 0) n_items = m.neq;
+        if (cat == 0 || cat == 8 || cat == 9) n_items = m.neq;
+        else if (cat == 10) n_items = m.njnt;
         else if (cat == 1) {
           if (m.eq_type[e] != EQ_FLEX || !d.eq_active[(long)wid * m.neq + e]) continue;
           const int f = m.eq_obj1id[e];
@@ -1468,9 +1692,9 @@ __device__ void make_constraint(const mjw_model_t& m, const mjw_data_t& d, int w
           run += chunk;
         }
       }
-      if (cat <= 1 || cat == 5) ne += run - start;
+      if (eq) ne += run - start;
       else if (cat == 2 || cat == 6) nf += run - start;
-      else if (cat == 3 || cat == 7) nl += run - start;
+      else if (lim) nl += run - start;
     }
   }
   if (tid() == 0) {
@@ -1493,6 +1717,8 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid,
     if (a < m.nu) {
       if (m.actuator_trntype[a] == TRN_TENDON) {
         nnz = m.ten_J_rownnz[m.actuator_trnid[2 * a]];
+      } else if (m.actuator_trntype[a] == TRN_SITE || m.actuator_trntype[a] == TRN_SLIDERCRANK) {
+        nnz = trn_site_nnz(m, a);
       } else {
         const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
         nnz = jt0 == JNT_FREE ? 6 : (jt0 == JNT_BALL ? 3 : 1);
@@ -1514,6 +1740,17 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid,
         d.actuator_moment[(long)wid * m.nJmom + rowadr + k] = gear[0] * J[k];
         d.moment_colind[(long)wid * m.nJmom + rowadr + k] = m.ten_J_colind[m.ten_J_rowadr[j] + k];
       }
+      continue;
+    }
+    if (trn == TRN_SITE || trn == TRN_SLIDERCRANK) {  // smooth.py:2150-2241, 2274-2442 (mjw_trn.h)
+      const long gu = (long)wid * m.nu + a;
+      float* gm = d.actuator_moment + (long)wid * m.nJmom + rowadr;
+      int* gc = d.moment_colind + (long)wid * m.nJmom + rowadr;
+      d.actuator_length[gu] = trn_site(m, wid, a, nnz, d.site_xpos + (long)wid * m.nsite * 3, d.site_xmat + (long)wid * m.nsite * 9,
+                                       d.xquat + (long)wid * m.nbody * 4, d.subtree_com + (long)wid * m.nbody * 3,
+                                       d.cdof + (long)wid * m.nv * 6, gm, gc, gm, gc);
+      d.moment_rownnz[gu] = nnz;
+      d.moment_rowadr[gu] = rowadr;
       continue;
     }
     const int jt = m.jnt_type[j], qa = m.jnt_qposadr[j], va = m.jnt_dofadr[j];
@@ -2088,7 +2325,121 @@ struct SolveCtx {
   const float *M, *LD;
   float cost, prev_cost, gauss, search_dot, grad_dot;
   int rphase;  // block_sum_db buffer parity (uniform)
+  const struct EllCtx* ell;  // elliptic cones (solve_kernel<3> only)
 };
+
+// row types / ids, and the contacts' first rows, dims and frictions, for the cone rows
+struct EllCtx {
+  const int* type;
+  const int* id;
+  const int* con_adr;  // contact_efc_address (nmaxpyramid per contact)
+  const int* con_dim;
+  const float* con_fr;
+  int nmaxpyr;
+  float iri;  // opt.impratio_invsqrt
+};
+
+// ---- elliptic cones (solver.py:263-323 _eval_elliptic, 1550-1611 quad, 1886-1942 update) ----------
+// the contact of elliptic row r: its first row, dim, friction and mu; false when its rows run past
+// njmax (the oracle and the reference then leave the contact out)
+struct ConeRow {
+  int r0, dim, con;
+  float mu;
+  const float* fr;
+};
+__device__ __forceinline__ bool cone_of(const SolveCtx& c, int r, ConeRow& k) {
+  const EllCtx& e = *c.ell;
+  k.con = e.id[r];
+  k.r0 = e.con_adr[(long)k.con * e.nmaxpyr];
+  k.dim = e.con_dim[k.con];
+  k.fr = e.con_fr + 5 * (long)k.con;
+  k.mu = k.fr[0] * e.iri;
+  return k.r0 >= 0 && k.r0 + k.dim <= c.nefc;
+}
+
+// quad, quad1, quad2 of the contact whose first row is r (solver.py:1550-1611), at the current Jaref / jv
+__device__ __forceinline__ void ell_quad(const SolveCtx& c, const ConeRow& k, float* q) {
+  const int r = k.r0;
+  const float D0 = c.D[r], ja = c.Jaref[r], jv = c.jv[r];
+  q[0] = 0.5f * ja * ja * D0; q[1] = jv * ja * D0; q[2] = 0.5f * jv * jv * D0;
+  float uu = 0.0f, uv = 0.0f, vv = 0.0f;
+  for (int j = 1; j < k.dim; j++) {
+    const int rj = r + j;
+    const float jaj = c.Jaref[rj], jvj = c.jv[rj], dj = c.D[rj], DJj = dj * jaj;
+    q[0] += 0.5f * jaj * DJj; q[1] += jvj * DJj; q[2] += 0.5f * jvj * dj * jvj;
+    const float uj = jaj * k.fr[j - 1], vj = jvj * k.fr[j - 1];
+    uu += uj * uj; uv += uj * vj; vv += vj * vj;
+  }
+  q[3] = ja * k.mu; q[4] = jv * k.mu; q[5] = uu;
+  q[6] = uv; q[7] = vv; q[8] = D0 / (k.mu * k.mu * (1.0f + k.mu * k.mu));
+}
+
+// (cost, grad, hess) of one contact's cone at alpha (solver.py:263-323), added into o
+__device__ __forceinline__ void ell_eval(const float* q, float mu, float alpha, float* o) {
+  const float u0 = q[3], v0 = q[4], uu = q[5], uv = q[6], vv = q[7], dm = q[8];
+  const float N = u0 + alpha * v0;
+  const float Tsqr = uu + alpha * (2.0f * uv + alpha * vv);
+  bool bottom = false;
+  if (Tsqr <= 0.0f) {
+    if (!(N < 0.0f)) return;
+    bottom = true;
+  } else {
+    const float T = sqrtf(Tsqr);
+    if (N >= mu * T) return;
+    if (mu * N + T <= 0.0f) {
+      bottom = true;
+    } else {
+      const float N1 = v0, T1 = (uv + alpha * vv) / T;
+      const float T2 = vv / T - (uv + alpha * vv) * T1 / (T * T);
+      const float nmt = N - mu * T, d1 = N1 - mu * T1;
+      o[0] += 0.5f * dm * nmt * nmt;
+      o[1] += dm * nmt * d1;
+      o[2] += dm * (d1 * d1 + nmt * (-mu * T2));
+      return;
+    }
+  }
+  if (bottom) {
+    const float aq2 = alpha * q[2];
+    o[0] += alpha * aq2 + alpha * q[1] + q[0];
+    o[1] += 2.0f * aq2 + q[1];
+    o[2] += 2.0f * q[2];
+  }
+}
+
+// force / cost / state of elliptic row r at the current Jaref (solver.py:1886-1942); every row of the
+// contact must be current
+__device__ __forceinline__ float ell_force(const SolveCtx& c, int r, float jaref, float& cost, int& state) {
+  ConeRow k;
+  cost = 0.0f;
+  if (!cone_of(c, r, k)) { state = STATE_SATISFIED; return 0.0f; }
+  const float N = c.Jaref[k.r0] * k.mu;
+  float TT = 0.0f, uf = 0.0f;
+  for (int j = 1; j < k.dim; j++) {
+    const float uj = c.Jaref[k.r0 + j] * k.fr[j - 1];
+    TT += uj * uj;
+    if (k.r0 + j == r) uf = uj * k.fr[j - 1];
+  }
+  const float T = TT <= 0.0f ? 0.0f : sqrtf(TT);
+  const float D = c.D[r];
+  if (N >= k.mu * T || (T <= 0.0f && N >= 0.0f)) {
+    state = STATE_SATISFIED;
+    return 0.0f;
+  }
+  if (k.mu * N + T <= 0.0f || (T <= 0.0f && N < 0.0f)) {
+    state = STATE_QUADRATIC;
+    cost = 0.5f * D * jaref * jaref;
+    return -D * jaref;
+  }
+  const float dm = safe_div(c.D[k.r0], k.mu * k.mu * (1.0f + k.mu * k.mu));
+  const float nmt = N - k.mu * T;
+  const float f0 = -dm * nmt * k.mu;
+  state = STATE_CONE;
+  if (r == k.r0) {
+    cost = 0.5f * dm * nmt * nmt;
+    return f0;
+  }
+  return -safe_div(f0, T) * uf;
+}
 
 __device__ __forceinline__ void eval_row_v(const SolveCtx& c, int r, float D, float jaref, float jv, float alpha, float* o) {
   const float x = jaref + alpha * jv;
@@ -2131,8 +2482,25 @@ __device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, 
 // each thread loads RU rows (r0, r0 + nthr(), ...: the same per-thread order as a plain strided loop,
 // hence the same sums) before evaluating any of them.
 constexpr int RU = 4;  // 8 and 16 rows in flight per thread measured 14 % and 73 % slower on aloha_cloth
-template <int NA>
+template <int NA, bool ELL = false>
 __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas, float* o) {
+  if (ELL) {
+    // elliptic models: contact rows of the cone type are evaluated per contact, at its first row
+    for (int r = c.ne + tid(); r < c.nefc; r += nthr()) {
+      if (r >= c.ne + c.nf && c.ell->type[r] == CNSTR_CONTACT_ELLIPTIC) {
+        ConeRow k;
+        if (!cone_of(c, r, k) || k.r0 != r) continue;
+        float q[9];
+        ell_quad(c, k, q);
+#pragma unroll
+        for (int a = 0; a < NA; a++) ell_eval(q, k.mu, alphas[a], o + 3 * a);
+        continue;
+      }
+#pragma unroll
+      for (int a = 0; a < NA; a++) eval_row(c, r, alphas[a], o + 3 * a);
+    }
+    return;
+  }
   for (int r0 = c.ne + tid(); r0 < c.nefc; r0 += RU * nthr()) {  // equality rows: folded into the quadratic
     float D[RU], ja[RU], jv[RU];
 #pragma unroll
@@ -2155,9 +2523,40 @@ __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas
 }
 
 // `alpha`: the linesearch step still to be applied to Jaref (fused here: Jaref += alpha * jv)
+template <bool ELL = false>
 __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   float cost = 0.0f;
-  for (int r0 = tid(); r0 < c.nefc; r0 += RU * nthr()) {
+  if (ELL) {
+    // a cone row reads its contact's other rows: Jaref is advanced for every row first
+    if (alpha != 0.0f) {
+      for (int r = tid(); r < c.nefc; r += nthr()) c.Jaref[r] += alpha * c.jv[r];
+      __syncthreads();
+    }
+    for (int r = tid(); r < c.nefc; r += nthr()) {
+      const float D = c.D[r], jaref = c.Jaref[r];
+      float f;
+      if (r < c.ne) {
+        f = -D * jaref;
+        cost += 0.5f * D * jaref * jaref;
+      } else if (r < c.ne + c.nf) {
+        const float fl = c.fl[r], rf = safe_div(fl, D);
+        if (jaref <= -rf) { f = fl; cost += -fl * (0.5f * rf + jaref); }
+        else if (jaref >= rf) { f = -fl; cost += -fl * (0.5f * rf - jaref); }
+        else { f = -D * jaref; cost += 0.5f * D * jaref * jaref; }
+      } else if (c.ell->type[r] == CNSTR_CONTACT_ELLIPTIC) {
+        float rc;
+        int st;
+        f = ell_force(c, r, jaref, rc, st);
+        cost += rc;
+      } else {
+        if (jaref >= 0.0f) { f = 0.0f; }
+        else { f = -D * jaref; cost += 0.5f * D * jaref * jaref; }
+      }
+      c.force[r] = f;
+    }
+    alpha = 0.0f;
+  }
+  for (int r0 = ELL ? c.nefc : tid(); r0 < c.nefc; r0 += RU * nthr()) {
   float Du[RU], jau[RU];
 #pragma unroll
   for (int u = 0; u < RU; u++) {
@@ -2219,11 +2618,15 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
 
 // efc_state of the final Jaref (solver.py:2154-2219), written once after the iterations: the CG itself
 // never reads it, so update_constraint does not store it every iteration
+template <bool ELL = false>
 __device__ void write_states(const SolveCtx& c) {
   for (int r = tid(); r < c.nefc; r += nthr()) {
     const float D = c.D[r], jaref = c.Jaref[r];
     int st = STATE_QUADRATIC;
-    if (r >= c.ne && r < c.ne + c.nf) {
+    if (ELL && r >= c.ne + c.nf && c.ell->type[r] == CNSTR_CONTACT_ELLIPTIC) {
+      float rc;
+      (void)ell_force(c, r, jaref, rc, st);
+    } else if (r >= c.ne && r < c.ne + c.nf) {
       const float fl = c.fl[r], rf = safe_div(fl, D);
       st = jaref <= -rf ? STATE_LINEARNEG : (jaref >= rf ? STATE_LINEARPOS : STATE_QUADRATIC);
     } else if (r >= c.ne + c.nf) {
@@ -2238,13 +2641,19 @@ __device__ void write_states(const SolveCtx& c) {
 // factored in place (right-looking Cholesky, one column per round) and solved for Mgrad = H^-1 grad.
 // J'DJ entries come from the transposed index: rows common to columns i and j, merged in ascending
 // row order -- a fixed summation order, so replicas stay bitwise equal
+template <bool ELL = false>
 __device__ void newton_direction(const mjw_model_t& m, SolveCtx& c) {
   const int nv = c.nv;
   float* H = c.H;
   for (int r = c.ne + tid(); r < c.nefc; r += nthr()) {  // equality rows are always quadratic
     const float D = c.D[r], ja = c.Jaref[r];
     bool quad = true;
-    if (r < c.ne + c.nf) {
+    if (ELL && r >= c.ne + c.nf && c.ell->type[r] == CNSTR_CONTACT_ELLIPTIC) {
+      float rc;
+      int st;
+      (void)ell_force(c, r, ja, rc, st);
+      quad = st == STATE_QUADRATIC;
+    } else if (r < c.ne + c.nf) {
       const float rf = safe_div(c.fl[r], D);
       quad = -rf < ja && ja < rf;
     } else {
@@ -2273,6 +2682,52 @@ __device__ void newton_direction(const mjw_model_t& m, SolveCtx& c) {
         }
       }
       H[i * nv + j] = s;
+    }
+    if (ELL) {
+      // + J_c' C J_c of every contact in the cone state (solver.py:2430-2585), row i of H by this thread:
+      // C[a][b] J[ra][i] J[rb][j] over the contact's rows a, b and the columns j <= i of row rb
+      for (int r = c.ne + c.nf; r < c.nefc; r++) {
+        if (c.ell->type[r] != CNSTR_CONTACT_ELLIPTIC) continue;
+        ConeRow k;
+        if (!cone_of(c, r, k) || k.r0 != r) continue;
+        const float mu2 = k.mu * k.mu;
+        const float dm = safe_div(c.D[r], mu2 * (1.0f + mu2));
+        float u[6], fri[6], tt = 0.0f;
+        u[0] = c.Jaref[r] * k.mu;
+        fri[0] = k.mu;
+        for (int j = 1; j < k.dim; j++) {
+          u[j] = c.Jaref[r + j] * k.fr[j - 1];
+          fri[j] = k.fr[j - 1];
+          tt += u[j] * u[j];
+        }
+        const float T = tt <= 0.0f ? 0.0f : sqrtf(tt), N = u[0];
+        // the cone state of the contact (ell_force's zones)
+        if (N >= k.mu * T || (T <= 0.0f && N >= 0.0f) || k.mu * N + T <= 0.0f || (T <= 0.0f && N < 0.0f) || dm == 0.0f) continue;
+        const float t = fmaxf(T, MJW_MINVAL), ttt = fmaxf(t * t * t, MJW_MINVAL);
+        const float mu_over_t = safe_div(k.mu, t), mu_n_over_ttt = k.mu * safe_div(N, ttt), diag = mu2 - k.mu * safe_div(N, t);
+        for (int a = 0; a < k.dim; a++) {
+          // J[r + a][i]
+          const int ra = r + a;
+          float jai = 0.0f;
+          for (int q = 0; q < c.Jnnz[ra]; q++)
+            if (c.Jcol[(long)q * c.P + ra] == i) jai = c.J[(long)q * c.P + ra];
+          if (jai == 0.0f) continue;
+          for (int b = 0; b < k.dim; b++) {
+            float h;
+            if (a == 0 && b == 0) h = 1.0f;
+            else if (a == 0) h = -mu_over_t * u[b];
+            else if (b == 0) h = -mu_over_t * u[a];
+            else h = mu_n_over_ttt * u[a] * u[b] + (a == b ? diag : 0.0f);
+            h *= dm * fri[a] * fri[b];
+            if (h == 0.0f) continue;
+            const int rb = r + b;
+            for (int q = 0; q < c.Jnnz[rb]; q++) {
+              const int j = c.Jcol[(long)q * c.P + rb];
+              if (j <= i) H[i * nv + j] += h * jai * c.J[(long)q * c.P + rb];
+            }
+          }
+        }
+      }
     }
   }
   __syncthreads();
@@ -2312,6 +2767,7 @@ __device__ void newton_direction(const mjw_model_t& m, SolveCtx& c) {
   }
 }
 
+template <bool ELL = false>
 __device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
   float gd = 0.0f;
   for (int i = tid(); i < c.nv; i += nthr()) {
@@ -2321,7 +2777,7 @@ __device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
     gd += g * g;
   }
   c.grad_dot = block_sum1_db(gd, sm, c.rphase);  // syncs
-  if (c.newton) newton_direction(m, c);
+  if (c.newton) newton_direction<ELL>(m, c);
   else solve_trees(m, c.LD, c.Mgrad);
   __syncthreads();
 }
@@ -2331,6 +2787,7 @@ __device__ __forceinline__ bool in_bracket(const float* x, const float* y) {
 }
 
 // returns the step; qacc / Ma are updated here, Jaref by update_constraint
+template <bool ELL = false>
 __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm) {
   mul_m_trees(m, c.M, c.search, c.mv);
   // jv = J search, fused with the alpha = 0 evaluation of each row (same thread)
@@ -2372,12 +2829,22 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
       v5[5] += 0.5f * D * ja * ja;
       v5[6] += D * ja * s;
       v5[7] += 0.5f * D * s * s;
-    } else {
+    } else if (!ELL || r < c.ne + c.nf || c.ell->type[r] != CNSTR_CONTACT_ELLIPTIC) {
       eval_row(c, r, 0.0f, v5);
     }
     }
   }
   __syncthreads();
+  if (ELL) {  // the cones at alpha = 0, once every row's jv is in
+    for (int r = c.ne + c.nf + tid(); r < c.nefc; r += nthr()) {
+      if (c.ell->type[r] != CNSTR_CONTACT_ELLIPTIC) continue;
+      ConeRow k;
+      if (!cone_of(c, r, k) || k.r0 != r) continue;
+      float q[9];
+      ell_quad(c, k, q);
+      ell_eval(q, k.mu, 0.0f, v5);
+    }
+  }
   const float snorm = sqrtf(c.search_dot);
   const float scale = MR_W(stat_meaninertia) * (float)c.nv;
   const float gtol = fmaxf(MR_W(opt_tolerance) * MR_W(opt_ls_tolerance) * snorm * scale, 1e-6f);
@@ -2403,7 +2870,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
     for (int i0 = 0; i0 < n; i0 += 3) {
       float al[3], v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       for (int k = 0; k < 3; k++) al[k] = ls_parallel_alpha(MR_W(opt_ls_parallel_min_step), n, min(i0 + k, n - 1));
-      eval_rows<3>(c, al, v9);
+      eval_rows<3, ELL>(c, al, v9);
       block_sum_db<9>(v9, sm, c.rphase);
       for (int k = 0; k < 3 && i0 + k < n; k++) {
         float g[3];
@@ -2415,7 +2882,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
   } else {
   const float lo_alpha_in = -safe_div(p0[1], p0[2]);
   float lo_in[3] = {0, 0, 0};
-  eval_rows<1>(c, &lo_alpha_in, lo_in);
+  eval_rows<1, ELL>(c, &lo_alpha_in, lo_in);
   block_sum_db<3>(lo_in, sm, c.rphase);
   {
     float g[3];
@@ -2440,7 +2907,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
       const float mid_alpha = 0.5f * (lo_alpha + hi_alpha);
       float v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       const float al[3] = {lo_next_alpha, hi_next_alpha, mid_alpha};
-      eval_rows<3>(c, al, v9);
+      eval_rows<3, ELL>(c, al, v9);
       block_sum_db<9>(v9, sm, c.rphase);
       float lo_next[3], hi_next[3], mid[3], g[3];
       gauss_at(lo_next_alpha, g);
@@ -2486,6 +2953,8 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
 // 2 * njmax floats fit the LDS of a CU).
 template <int PART>
 __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_kernel(const mjw_model_t m, const mjw_data_t d) {
+  // PART 3: PART 1 for elliptic-cone models (the cone rows of a contact are evaluated together)
+  constexpr bool ELL = PART == 3;
   __shared__ Smem sm;
   const int wid = blockIdx.x;
   const int nv = m.nv, njmax = d.njmax;
@@ -2533,6 +3002,17 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
   c.Jaref = d.sp_row + (long)wid * njmax * 3;
   c.jv = c.Jaref + njmax;
   c.Dq = c.Jaref + 2 * njmax;
+  EllCtx ell;
+  if (ELL) {
+    ell.type = d.efc_type + (long)wid * njmax;
+    ell.id = d.efc_id + (long)wid * njmax;
+    ell.con_adr = d.contact_efc_address;
+    ell.con_dim = d.contact_dim;
+    ell.con_fr = d.contact_friction;
+    ell.nmaxpyr = m.nmaxpyramid;
+    ell.iri = MR_W(opt_impratio_invsqrt);
+  }
+  c.ell = ELL ? &ell : nullptr;
   c.newton = m.opt_solver == SOLVER_NEWTON && m.sp_nH == nv;
   c.H = c.newton ? d.sp_H + (long)wid * nv * nv : nullptr;
   if constexpr (PART == 2) {
@@ -2645,8 +3125,8 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
   mul_m_trees(m, c.M, qacc, c.Ma);
   __syncthreads();
   c.cost = MJW_MAXVAL;
-  update_constraint(c, sm);
-  update_gradient(m, c, sm);
+  update_constraint<ELL>(c, sm);
+  update_gradient<ELL>(m, c, sm);
   float sd = 0.0f;
   for (int i = tid(); i < nv; i += nthr()) {
     c.search[i] = -c.Mgrad[i];
@@ -2659,15 +3139,15 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
   SPROF_MARK(SPH_SINIT);
   if (m.opt_iterations != 0) {
     for (;;) {
-      const float alpha = linesearch(m, c, wid, sm);
+      const float alpha = linesearch<ELL>(m, c, wid, sm);
       SPROF_MARK(SPH_SLS);
       for (int i = tid(); i < nv; i += nthr()) {
         c.pgrad[i] = c.grad[i];
         c.pMgrad[i] = c.Mgrad[i];
       }
       __syncthreads();
-      update_constraint(c, sm, alpha);
-      update_gradient(m, c, sm);
+      update_constraint<ELL>(c, sm, alpha);
+      update_gradient<ELL>(m, c, sm);
       SPROF_MARK(SPH_SUPD);
       float nd[2] = {0.0f, 0.0f};
       for (int i = tid(); i < nv; i += nthr()) {
@@ -2691,7 +3171,7 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
       if (improvement < tol || gradient < tol || niter == m.opt_iterations) break;
     }
   }
-  write_states(c);
+  write_states<ELL>(c);
   if (tid() == 0) d.solver_niter[wid] = niter;
 }
 
@@ -2855,7 +3335,10 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
       const char* e = getenv("MJW_SP_SOLVE_LDS");
       return e && e[0] == '1';
     }();
-    if (lds_ok && d->njmax > 0 && row_lds <= 150 * 1024) {
+    if (m->opt_cone == CONE_ELLIPTIC) {
+      hipLaunchKernelGGL(sp::solve_kernel<3>, dim3(nw), dim3(sp::BLK), search_lds, s, *m, *d);
+      trace_launch(s, K_SP_SOLVE);
+    } else if (lds_ok && d->njmax > 0 && row_lds <= 150 * 1024) {
       static std::once_flag once;
       std::call_once(once, [] {
         (void)hipFuncSetAttribute((const void*)sp::solve_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);

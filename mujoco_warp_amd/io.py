@@ -149,18 +149,10 @@ def put_model(mjm, device=None) -> types.Model:
     if mjm.opt.solver == types.SolverType.NEWTON and mjm.nv > SPARSE_NEWTON_NVMAX:
       # Newton's Hessian is dense (nv x nv per world, as the reference's H), so the flex models stay on CG
       raise NotImplementedError(f"sparse / flex models: Newton needs nv <= {SPARSE_NEWTON_NVMAX} in this build (nv = {mjm.nv}); use CG.")
-    if mjm.opt.cone != types.ConeType.PYRAMIDAL:
-      raise NotImplementedError("sparse / flex models: elliptic cones are not supported by this build yet.")
-    if mjm.opt.integrator not in (types.IntegratorType.EULER, types.IntegratorType.IMPLICITFAST):
-      raise NotImplementedError("sparse / flex models: only the Euler and implicitfast integrators are supported by this build yet.")
     if getattr(mjm, "nsensor", 0):
       # the sensor kernel (csrc/mjw_sensor.hip) stages a world's body / dof state in 64 KB of LDS
       if 37 * mjm.nbody + 14 * mjm.nv > 16384:
         raise NotImplementedError("sparse / flex models: sensors need 37 nbody + 14 nv <= 16384 in this build (the flex bodies exceed it).")
-    if getattr(mjm, "neq", 0) and np.any(~np.isin(mjm.eq_type, (types.EqType.JOINT, types.EqType.FLEX, types.EqType.TENDON))):
-      raise NotImplementedError("sparse / flex models: only joint, tendon and flex equality constraints are supported by this build yet.")
-    if np.any(mjm.jnt_limited & (mjm.jnt_type == JointType.BALL)):
-      raise NotImplementedError("sparse / flex models: ball joint limits are not supported by this build yet.")
     if getattr(mjm, "nflex", 0) and np.any(mjm.flex_dim != 2):
       raise NotImplementedError("only dim-2 flexes are supported by this build yet.")
   for st in np.unique(getattr(mjm, "sensor_type", np.zeros(0, dtype=np.int32))):
@@ -190,8 +182,8 @@ def put_model(mjm, device=None) -> types.Model:
     lr = np.asarray(mjm.actuator_lengthrange, np.float64).reshape(-1, 2)[muscle]
     if np.any(lr[:, 0] >= lr[:, 1]):
       raise NotImplementedError("muscle actuators need an actuator_lengthrange (lengthrange attribute, or a limited joint / tendon transmission).")
-  if sparse and np.any((mjm.actuator_trntype > types.TrnType.JOINTINPARENT) & (mjm.actuator_trntype != types.TrnType.TENDON)):
-    raise NotImplementedError("sparse / flex models: only joint and tendon transmissions are supported by this build yet.")
+  if sparse and np.any(mjm.actuator_trntype == types.TrnType.BODY):
+    raise NotImplementedError("sparse / flex models: BODY (adhesion) transmissions are not supported by this build yet.")
   if (mjm.opt.viscosity > 0 or mjm.opt.density > 0) and mjm.opt.integrator in (types.IntegratorType.IMPLICITFAST, types.IntegratorType.IMPLICIT):
     raise NotImplementedError("Implicit integrators and fluid model not implemented.")  # io.py:126-130
 

@@ -172,17 +172,22 @@ def _dense_moment(mjm, d, w):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["site", "slidercrank", "adhesion", "adhesion_elliptic", "site_translational"])
+@pytest.mark.parametrize("name", ["site", "slidercrank", "adhesion", "adhesion_elliptic", "site_translational", "site_sparse",
+                                  "slidercrank_sparse", "site_translational_sparse"])
 def test_gpu_transmissions_match_oracle(name):
   """The device computes the BODY moment from the contact normals; the oracle from the constraint rows as
-  the reference does (pyramidal and elliptic cones)."""
+  the reference does (pyramidal and elliptic cones).  `_sparse`: the same models forced onto the sparse
+  path (jacobian="sparse"), whose transmission stage runs the same site / slider-crank rows (mjw_trn.h)."""
   import torch
 
   import mujoco_warp_amd as mjw
 
-  mjm = _load(SITE_TRANSLATIONAL if name == "site_translational" else name.replace("_elliptic", ""))
+  base = name.replace("_elliptic", "").replace("_sparse", "")
+  mjm = _load(SITE_TRANSLATIONAL if base == "site_translational" else base)
   if name == "adhesion_elliptic":
     mjm.opt.cone = 1
+  if name.endswith("_sparse"):
+    mjw.override_model(mjm, ["opt.jacobian=sparse"])
   nworld = 8
   if name.startswith("adhesion"):
     qpos = np.stack([mjm.key_qpos[i % 4] for i in range(nworld)])
@@ -193,6 +198,7 @@ def test_gpu_transmissions_match_oracle(name):
   ctrl = rng.uniform(0, 1, size=(nworld, mjm.nu))
   m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=32, nconmax=8)
   _, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=32, nconmax=8)
+  assert m.is_sparse == name.endswith("_sparse")
   mjw.forward(m, d)
   od.forward()
   torch.cuda.synchronize()
