@@ -56,6 +56,20 @@ enum : int { SOLVER_CG = 1, SOLVER_NEWTON = 2 };
 enum : int { CAM_FIXED = 0, CAM_TRACK = 1, CAM_TRACKCOM = 2, CAM_TARGETBODY = 3, CAM_TARGETBODYCOM = 4 };
 enum : int { FILTER_PLANE = 1, FILTER_SPHERE = 2, FILTER_AABB = 4, FILTER_OBB = 8 };
 
+// The kernel arguments as a struct `A` mirroring the kernel's parameter list (same order, so the same
+// layout as the kernarg segment), seen through an opaque copy of the segment pointer: loads of its
+// fields after this point cannot be merged with loads before it, so a field is re-read (s_load from the
+// kernarg segment, scalar cache) in each stage that uses it instead of being held in an SGPR across the
+// whole kernel.  Without it the forward kernel kept ~1000 field values live and spilled 946 SGPRs into
+// VGPR lanes (v_writelane / v_readlane: VALU work in every stage).
+template <class A>
+__device__ __forceinline__ const A& fresh_args() {
+  typedef const __attribute__((address_space(4))) char* kptr;
+  kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const A*)p;
+}
+
 // batched model field base pointer for world w (types.py "*" semantics: worldid % nb)
 __device__ __forceinline__ const float* mb(const float* p, int nb, int cnt, int w) {
   return nb <= 1 ? p : p + (long)(w % nb) * cnt;

@@ -2482,47 +2482,56 @@ __device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data
 // BOX: the box narrowphase paths; TEN: the tendon paths.  The lean instantiations keep the
 // humanoid-class kernel (neither) and the box models' kernel (no tendons) free of the register
 // pressure of code they never run.
+// the forward kernel's arguments (mjw_kernel's parameter list), re-read per stage through fresh_args
+struct FwdArgs {
+  mjw_model_t m;
+  mjw_data_t d;
+  Lay L;
+  int w0;
+};
+#define FA (fresh_args<FwdArgs>())
+
 template <int STAGES, bool BOX, bool TEN>
 __device__ __forceinline__ void run_stages(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   PROF_T0();
-  load_state(m, d, L, w);
-  load_smooth(m, d, L, w, STAGES);
+  load_state(FA.m, FA.d, FA.L, w);
+  load_smooth(FA.m, FA.d, FA.L, w, STAGES);
   WSYNC();
   PROF_MARK(PH_LOAD);
   if (STAGES & ST_POS) {
-    kinematics(m, d, L, w);
+    kinematics(FA.m, FA.d, FA.L, w);
     PROF_MARK(PH_KIN);
-    com_pos(m, d, L, w);
+    com_pos(FA.m, FA.d, FA.L, w);
     PROF_MARK(PH_COM);
-    camlight(m, d, L, w);
+    camlight(FA.m, FA.d, FA.L, w);
     PROF_MARK(PH_CAM);
     if (TEN && m.ntendon) {  // smooth.py:3085-3465 (fwd_position: before crb)
       const TenFrames f{d.site_xpos + (long)w.wid * m.nsite * 3, w.s + L.gxpos, w.s + L.gxmat, w.s + L.subtree_com, w.s + L.cdof};
       tendon_pos(m, d, w.s + L.qpos, f, w.wid, w.lane);
       WSYNC();  // spatial rows are read back by other lanes from here on
     }
-    crb_qM<TEN>(m, d, L, w);
+    crb_qM<TEN>(FA.m, FA.d, FA.L, w);
     PROF_MARK(PH_CRB);
     if (TEN && m.nbodytrn) {  // BODY transmissions accumulate over the contacts as they are staged
       body_trn_init(m, w.s + L.act_mom, w.si + L.act_nnz, L.amax, w.lane);
       WSYNC();
     }
-    collision_and_constraints<BOX, TEN, (STAGES & ST_POOL) != 0>(m, d, L, w);
+    collision_and_constraints<BOX, TEN, (STAGES & ST_POOL) != 0>(FA.m, FA.d, FA.L, w);
     PROF_MARK(PH_COLL);
-    transmission<TEN>(m, d, L, w);
+    transmission<TEN>(FA.m, FA.d, FA.L, w);
     PROF_MARK(PH_TRN);
   }
-  if (STAGES & ST_VEL) fwd_velocity<TEN, (STAGES & ST_POS) != 0>(m, d, L, w);
+  if (STAGES & ST_VEL) fwd_velocity<TEN, (STAGES & ST_POS) != 0>(FA.m, FA.d, FA.L, w);
   if ((STAGES & ST_POS) && (STAGES & ST_VEL) && w.lane < 2 && !(m.opt_enableflags & ENBL_ENERGY))
     d.energy[(long)w.wid * 2 + w.lane] = 0.0f;
   PROF_MARK(PH_VEL);
-  if (STAGES & ST_ACT) fwd_actuation<TEN, (STAGES & ST_VEL) != 0>(m, d, L, w);
+  if (STAGES & ST_ACT) fwd_actuation<TEN, (STAGES & ST_VEL) != 0>(FA.m, FA.d, FA.L, w);
   PROF_MARK(PH_ACT);
-  if (STAGES & ST_ACC) fwd_acceleration(m, d, L, w);
+  if (STAGES & ST_ACC) fwd_acceleration(FA.m, FA.d, FA.L, w);
   PROF_MARK(PH_ACC);
-  if (STAGES & ST_SOLVE) solve(m, d, L, w);
+  if (STAGES & ST_SOLVE) solve(FA.m, FA.d, FA.L, w);
   PROF_MARK(PH_GSOLVE);
-  if (STAGES & ST_EULER) euler(m, d, L, w);
+  if (STAGES & ST_EULER) euler(FA.m, FA.d, FA.L, w);
   PROF_MARK(PH_GEULER);
 }
 
