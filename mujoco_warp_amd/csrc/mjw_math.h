@@ -24,6 +24,20 @@ __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fm
 // math.py:317-319
 __device__ __forceinline__ float safe_div(float x, float y) { return x / (y != 0.0f ? y : MJW_MINVAL); }
 
+// constraint.py:91-100 (_efc_row): the impedance shape of solimp's (mid, power) at imp_x, with the
+// integer powers (solimp's default is 2) as products instead of powf, which costs ~100 VALU
+// instructions per call and was a quarter of the forward kernel's code
+__device__ __forceinline__ float imp_pow(float x, float p) {
+  if (p == 1.0f) return x;
+  if (p == 2.0f) return x * x;
+  if (p == 3.0f) return x * x * x;
+  return powf(x, p);
+}
+__device__ __forceinline__ float imp_shape(float imp_x, float mid, float power) {
+  if (imp_x < mid) return (1.0f / imp_pow(mid, power - 1.0f)) * imp_pow(imp_x, power);
+  return 1.0f - (1.0f / imp_pow(1.0f - mid, power - 1.0f)) * imp_pow(1.0f - imp_x, power);
+}
+
 // wp.normalize semantics: zero stays zero
 __device__ __forceinline__ void normalize3(float* v) {
   float n = sqrtf(dot3(v, v));

@@ -1138,9 +1138,7 @@ __device__ void put_row_scalars(const mjw_model_t& m, const mjw_data_t& d, int w
   if (solref[0] <= 0.0f) k = -solref[0] / dmax_sq;
   if (solref[1] <= 0.0f) b = -solref[1] / dmax;
   const float imp_x = fabsf(pos_imp) / width;
-  const float imp_a = (1.0f / powf(mid, power - 1.0f)) * powf(imp_x, power);
-  const float imp_b = 1.0f - (1.0f / powf(1.0f - mid, power - 1.0f)) * powf(1.0f - imp_x, power);
-  float imp = dmin + (imp_x < mid ? imp_a : imp_b) * (dmax - dmin);
+  float imp = dmin + imp_shape(imp_x, mid, power) * (dmax - dmin);
   imp = clampf(imp, dmin, dmax);
   if (imp_x > 1.0f) imp = dmax;
   const long gr = (long)wid * d.njmax + r;
@@ -1628,9 +1626,7 @@ __device__ int make_rows(const mjw_model_t& m, const mjw_data_t& d, int wid, int
     if (sr[0] <= 0.0f) kk = -sr[0] / dmax_sq;
     if (sr[1] <= 0.0f) bb = -sr[1] / dmax;
     const float imp_x = fabsf(pos) / width;
-    const float imp_a = (1.0f / powf(mid, power - 1.0f)) * powf(imp_x, power);
-    const float imp_b = 1.0f - (1.0f / powf(1.0f - mid, power - 1.0f)) * powf(1.0f - imp_x, power);
-    float imp = dmin + (imp_x < mid ? imp_a : imp_b) * (dmax - dmin);
+    float imp = dmin + imp_shape(imp_x, mid, power) * (dmax - dmin);
     imp = clampf(imp, dmin, dmax);
     if (imp_x > 1.0f) imp = dmax;
     const long gr = (long)wid * njmax + r;

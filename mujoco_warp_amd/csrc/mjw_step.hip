@@ -681,9 +681,7 @@ __device__ __forceinline__ void efc_row(const mjw_model_t& m, const mjw_data_t& 
   if (solref[0] <= 0.0f) k = -solref[0] / dmax_sq;
   if (solref[1] <= 0.0f) b = -solref[1] / dmax;
   float imp_x = fabsf(pos_imp) / width;
-  float imp_a = (1.0f / powf(mid, power - 1.0f)) * powf(imp_x, power);
-  float imp_b = 1.0f - (1.0f / powf(1.0f - mid, power - 1.0f)) * powf(1.0f - imp_x, power);
-  float imp_y = imp_x < mid ? imp_a : imp_b;
+  float imp_y = imp_shape(imp_x, mid, power);
   float imp = dmin + imp_y * (dmax - dmin);
   imp = clampf(imp, dmin, dmax);
   if (imp_x > 1.0f) imp = dmax;
