@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 24
+#define MJW_ABI_VERSION 25
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -45,7 +45,8 @@
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
-  X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)
+  X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)             \
+  X(nsensorcollision)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -109,6 +110,7 @@
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
   X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)                     \
+  X(sensor_collision_adr, nsensor) X(sensor_collision_num, nsensor) X(sensor_collision_pair, nsensorcollision * 4) \
   X(M_rownnz, nv) X(M_rowadr, nv) X(M_colind, nM) X(tree_dofadr, ntree + 1)                        \
   X(flex_dim, nflex) X(flex_vertadr, nflex) X(flex_edgeadr, nflex) X(flex_edgenum, nflex)          \
   X(flex_elemadr, nflex) X(flex_elemnum, nflex) X(flex_elemdataadr, nflex) X(flex_elemedgeadr, nflex) \

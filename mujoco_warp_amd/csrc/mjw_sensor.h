@@ -5,6 +5,7 @@
 #pragma once
 
 #include "mjw_common.h"
+#include "mjw_narrow.h"
 
 namespace mjw {
 
@@ -59,8 +60,9 @@ __device__ __forceinline__ void sensor_write(const mjw_model_t& m, const mjw_dat
   float* out = d.sensordata + (long)wid * m.nsensordata + m.sensor_adr[s];
   for (int i = 0; i < dim; i++) {
     float x = v[i];
-    if (cutoff > 0.0f && dt == DATATYPE_REAL) x = clampf(x, -cutoff, cutoff);
-    else if (cutoff > 0.0f && dt == DATATYPE_POSITIVE) x = fminf(x, cutoff);
+    const bool clip = cutoff > 0.0f && m.sensor_type[s] != SENS_GEOMFROMTO;  // sensor.py:69, 98
+    if (clip && dt == DATATYPE_REAL) x = clampf(x, -cutoff, cutoff);
+    else if (clip && dt == DATATYPE_POSITIVE) x = fminf(x, cutoff);
     out[i] = x;
   }
 }
@@ -327,6 +329,149 @@ __device__ void subtree_vel(const mjw_model_t& m, const mjw_data_t& d, int wid, 
   }
 }
 
+// ---- collision sensors (sensor.py:604-680, 710-757): the smallest-distance contact over a sensor's geom
+// pairs, each pair's contacts from the primitive narrowphase (collision_primitive.py) -----------------
+struct CollBest {
+  float dist;
+  float p1[3], p2[3];
+  bool flip;
+};
+
+// sensor.py:744-757 (_sensor_collision): contact points pos -+ dist / 2 along the normal
+__device__ __forceinline__ void coll_offer(CollBest& b, float dist, const float* pos, const float* nrm, bool flip) {
+  if (!(dist < b.dist)) return;
+  b.dist = dist;
+  b.flip = flip;
+  for (int i = 0; i < 3; i++) {
+    b.p1[i] = pos[i] - 0.5f * dist * nrm[i];
+    b.p2[i] = pos[i] + 0.5f * dist * nrm[i];
+  }
+}
+
+// every contact collision_primitive.py writes for the type-sorted pair (g1, g2) -- inside or outside the
+// margin, as write_contact keeps sensor contacts (collision_core.py:199-213) -- offered to b
+__device__ void coll_pair(const mjw_model_t& m, int wid, const Frames& F, int g1, int g2, int pairid, bool flip, CollBest& b) {
+  const float* geom_size = MR(geom_size);
+  const float* gmargin = MR(geom_margin);
+  const float margin = pairid > -1 ? MR(pair_margin)[pairid] : gmargin[g1] + gmargin[g2];
+  const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  const float* p1 = F.gxpos + 3 * g1;
+  const float* p2 = F.gxpos + 3 * g2;
+  const float* r1 = F.gxmat + 9 * g1;
+  const float* r2 = F.gxmat + 9 * g2;
+  const float* s1 = geom_size + 3 * g1;
+  const float* s2 = geom_size + 3 * g2;
+  const float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
+  float pos[3], nrm[3];
+  if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {  // collision_primitive.py:737-790: all 8 corners
+    for (int k = 0; k < 8; k++) {
+      const float dist = plane_box_corner(k, n1, p1, p2, r2, s2, pos);
+      coll_offer(b, dist, pos, n1, flip);
+    }
+    return;
+  }
+  if (t1 == GEOM_PLANE && t2 == GEOM_CYLINDER) {  // collision_primitive.py:964-1040: 4 candidates
+    for (int k = 0; k < 4; k++) {
+      float dist;
+      plane_cylinder_k(k, n1, p1, p2, n2, s2[0], s2[1], &dist, pos);
+      coll_offer(b, dist, pos, n1, flip);
+    }
+    return;
+  }
+  Con2 c;
+  c.n = 0;
+  if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) {
+    c.dist[0] = plane_sphere(c.pos[0], n1, p1, p2, s2[0]);
+    make_frame(c.frame[0], n1);
+    c.n = 1;
+  } else if (t1 == GEOM_PLANE && t2 == GEOM_CAPSULE) {
+    plane_capsule(c, n1, p1, p2, n2, s2[0], s2[1]);
+  } else if (t1 == GEOM_PLANE && t2 == GEOM_ELLIPSOID) {
+    c.dist[0] = plane_ellipsoid(c.pos[0], n1, p1, p2, r2, s2);
+    make_frame(c.frame[0], n1);
+    c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
+    c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], p2, s2[0]);
+    make_frame(c.frame[0], nrm);
+    c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
+    float a[3], bb[3], pt[3];
+    for (int i = 0; i < 3; i++) { a[i] = p2[i] - n2[i] * s2[1]; bb[i] = p2[i] + n2[i] * s2[1]; }
+    closest_segment_point(pt, a, bb, p1);
+    c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], pt, s2[0]);
+    make_frame(c.frame[0], nrm);
+    c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_CYLINDER) {
+    c.dist[0] = sphere_cylinder(c.pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]);
+    make_frame(c.frame[0], nrm);
+    c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_BOX) {
+    c.dist[0] = sphere_box(c.pos[0], nrm, p1, s1[0], p2, r2, s2);
+    make_frame(c.frame[0], nrm);
+    c.n = 1;
+  } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
+    capsule_capsule(c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], margin);
+  } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {
+    capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
+  }
+  for (int i = 0; i < c.n && i < 2; i++) coll_offer(b, c.dist[i], c.pos[i], c.frame[i], flip);
+}
+
+// sensor.py:604-680: GEOMDIST (dim 1), GEOMNORMAL (3) or GEOMFROMTO (6) of sensor s
+__device__ void collision_sensor(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s) {
+  const int t = m.sensor_type[s];
+  const float cutoff = MR(sensor_cutoff)[s];
+  CollBest b;
+  b.dist = cutoff;
+  b.flip = false;
+  for (int i = 0; i < 3; i++) b.p1[i] = b.p2[i] = 0.0f;
+  const int adr = m.sensor_collision_adr[s];
+  for (int e = 0; e < m.sensor_collision_num[s]; e++) {
+    const int* r = m.sensor_collision_pair + 4 * (adr + e);
+    coll_pair(m, wid, F, r[0], r[1], r[2], r[3] != 0, b);
+  }
+  float v[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  int dim = 1;
+  if (t == SENS_GEOMDIST) {
+    v[0] = b.dist;
+  } else if (t == SENS_GEOMNORMAL) {
+    dim = 3;
+    if (b.dist <= cutoff) {
+      float nn[3] = {b.p2[0] - b.p1[0], b.p2[1] - b.p1[1], b.p2[2] - b.p1[2]};
+      normalize3(nn);
+      for (int i = 0; i < 3; i++) v[i] = b.flip ? -nn[i] : nn[i];
+    }
+  } else {
+    dim = 6;
+    if (b.dist <= cutoff)
+      for (int i = 0; i < 3; i++) {
+        v[i] = b.flip ? b.p2[i] : b.p1[i];
+        v[3 + i] = b.flip ? b.p1[i] : b.p2[i];
+      }
+  }
+  sensor_write(m, d, wid, s, v, dim);
+}
+
+// util_misc.py:603-632 inside_geom
+__device__ __forceinline__ bool inside_geom(const float* pos, const float* mat, const float* size, int type, const float* pt) {
+  const float vec[3] = {pt[0] - pos[0], pt[1] - pos[1], pt[2] - pos[2]};
+  if (type == GEOM_SPHERE) return dot3(vec, vec) < size[0] * size[0];
+  float pl[3];
+  mat_t_vec(pl, mat, vec);
+  if (type == GEOM_CAPSULE) {
+    const float z = pl[2], zd = z - clampf(z, -size[1], size[1]);
+    return pl[0] * pl[0] + pl[1] * pl[1] + zd * zd < size[0] * size[0];
+  }
+  if (type == GEOM_ELLIPSOID) {
+    const float q[3] = {pl[0] / size[0], pl[1] / size[1], pl[2] / size[2]};
+    return dot3(q, q) < 1.0f;
+  }
+  if (type == GEOM_CYLINDER) return fabsf(pl[2]) < size[1] && pl[0] * pl[0] + pl[1] * pl[1] < size[0] * size[0];
+  if (type == GEOM_BOX) return fabsf(pl[0]) < size[0] && fabsf(pl[1]) < size[1] && fabsf(pl[2]) < size[2];
+  if (type == GEOM_PLANE) return pl[2] < 0.0f;
+  return false;
+}
+
 // one position- or velocity-stage sensor (sensor.py:459-706 / 1251-1373, supported types)
 __device__ void sensor_posvel_one(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s, const float* qpos,
                                   const float* qvel, const float* act_len, const float* act_vel, float time) {
@@ -400,6 +545,15 @@ __device__ void sensor_posvel_one(const mjw_model_t& m, const mjw_data_t& d, int
   } else if (t == SENS_SUBTREELINVEL || t == SENS_SUBTREEANGMOM) {  // sensor.py:1240-1248 (subtree_vel ran first)
     const float* src = (t == SENS_SUBTREELINVEL ? d.subtree_linvel : d.subtree_angmom) + ((long)wid * m.nbody + id) * 3;
     for (int i = 0; i < 3; i++) v[i] = src[i];
+  } else if (t == SENS_GEOMDIST || t == SENS_GEOMNORMAL || t == SENS_GEOMFROMTO) {
+    collision_sensor(m, d, wid, F, s);
+    return;
+  } else if (t == SENS_INSIDESITE) {  // sensor.py:681-697
+    float p[3], R[9], sp[3], sR[9];
+    obj_frame(m, wid, F, ot, id, p, R);
+    site_pose(m, wid, F, rid, sp, sR);
+    v[0] = inside_geom(sp, sR, MR(site_size) + 3 * rid, m.site_type[rid], p) ? 1.0f : 0.0f;
+    dim = 1;
   } else if (t == SENS_E_POTENTIAL) {  // sensor.py:698-700
     v[0] = energy_potential(m, d, wid, qpos, F.xipos); dim = 1;
   } else if (t == SENS_E_KINETIC) {  // sensor.py:701-703

@@ -709,6 +709,21 @@ __device__ __forceinline__ void put_J(const mjw_data_t& d, const Lay& L, float* 
   else d.efc_J[((long)wid * d.njmax_pad + r) * np + k] = v;
 }
 
+// the rows of the ballot `bal` (row nefc + rank for each set lane, in lane order) whose Jacobian has up
+// to three non-zeros (columns c0 < c1 < c2 of the source lane, -1 = none): one coalesced row store per
+// row with the lanes over columns, instead of kJ scattered stores by each row's own lane
+__device__ __forceinline__ void put_J_rows(const mjw_data_t& d, const Lay& L, float* s, int wid, int np, int kJ, int njmax, int lane,
+                                           unsigned long long bal, int nefc, int c0, float v0, int c1 = -1, float v1 = 0.0f, int c2 = -1,
+                                           float v2 = 0.0f) {
+  for (int rr = nefc; bal && rr < njmax; rr++) {
+    const int src = __builtin_ctzll(bal);
+    bal &= bal - 1;
+    const int a0 = __builtin_amdgcn_readlane(c0, src), a1 = __builtin_amdgcn_readlane(c1, src), a2 = __builtin_amdgcn_readlane(c2, src);
+    const float w0 = rdlane(v0, src), w1 = rdlane(v1, src), w2 = rdlane(v2, src);
+    if (lane < kJ) put_J(d, L, s, wid, np, rr, lane, lane == a0 ? w0 : (lane == a1 ? w1 : (lane == a2 ? w2 : 0.0f)));
+  }
+}
+
 // support.py:396-432 restricted to one dof; returns jacp, jacr (zero when not in tree).  The
 // reference walks bodyid's ancestors looking for the dof's body; with bodies in DFS pre-order that
 // is the range test db <= bodyid < subtree_end(db), so the per-lane (db, dend) pair is loaded once
@@ -912,12 +927,14 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       unsigned long long bal = __ballot(act);
       int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
       int r = nefc + rank;
+      int da1 = -1, da2 = -1;
+      float d2 = 0.0f;
       if (act && r < njmax) {
         const float* data = eq_data + 11 * e;
         int j1 = m.eq_obj1id[e], j2 = m.eq_obj2id[e];
-        int da1 = m.jnt_dofadr[j1], qa1 = m.jnt_qposadr[j1];
-        int da2 = -1;
-        float pos, Jqvel, invweight, d2 = 0.0f;
+        da1 = m.jnt_dofadr[j1];
+        int qa1 = m.jnt_qposadr[j1];
+        float pos, Jqvel, invweight;
         if (j2 > -1) {
           int qa2 = m.jnt_qposadr[j2];
           da2 = m.jnt_dofadr[j2];
@@ -932,10 +949,10 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           Jqvel = qvel[da1];
           invweight = dof_invweight0[da1];
         }
-        for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, k == da1 ? 1.0f : (k == da2 ? -d2 : 0.0f));
         efc_row(m, d, L, s, wid, r, pos, pos, invweight, eq_solref + 2 * e, eq_solimp + 5 * e, 0.0f, Jqvel, 0.0f,
                 CNSTR_EQUALITY, e);
       }
+      put_J_rows(d, L, s, wid, np, kJ, njmax, lane, bal, nefc, da1, 1.0f, da2, -d2);
       int cnt = __popcll(bal);
       nefc += cnt;
       ne += cnt;
@@ -989,11 +1006,10 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       unsigned long long bal = __ballot(act);
       int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
       int r = nefc + rank;
-      if (act && r < njmax) {
-        for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, (k == i) ? 1.0f : 0.0f);
+      if (act && r < njmax)
         efc_row(m, d, L, s, wid, r, 0.0f, 0.0f, dof_invweight0[i], dof_solref + 2 * i, dof_solimp + 5 * i, 0.0f, qvel[i],
                 dof_frictionloss[i], CNSTR_FRICTION_DOF, i);
-      }
+      put_J_rows(d, L, s, wid, np, kJ, njmax, lane, bal, nefc, i, 1.0f);
       int cnt = __popcll(bal);
       nefc += cnt;
       nf += cnt;
@@ -1035,9 +1051,10 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       unsigned long long bal = __ballot(act);
       int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
       int r = nefc + rank;
+      const int dab = act ? m.jnt_dofadr[j] : -3;
+      put_J_rows(d, L, s, wid, np, kJ, njmax, lane, bal, nefc, dab, -axis[0], dab + 1, -axis[1], dab + 2, -axis[2]);
       if (act && r < njmax) {
-        const int da = m.jnt_dofadr[j];
-        for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, (k >= da && k < da + 3) ? -sel3(axis, k - da) : 0.0f);
+        const int da = dab;
         float Jqvel = -axis[0] * qvel[da];
         Jqvel -= axis[1] * qvel[da + 1];
         Jqvel -= axis[2] * qvel[da + 2];
@@ -1073,13 +1090,12 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       unsigned long long bal = __ballot(act);
       int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
       int r = nefc + rank;
-      if (act && r < njmax) {
-        int da = m.jnt_dofadr[j];
-        float Jv = (float)(dmn < dmx) * 2.0f - 1.0f;
-        for (int k = 0; k < kJ; k++) put_J(d, L, s, wid, np, r, k, (k == da) ? Jv : 0.0f);
+      const int da = act ? m.jnt_dofadr[j] : -1;
+      const float Jv = (float)(dmn < dmx) * 2.0f - 1.0f;
+      if (act && r < njmax)
         efc_row(m, d, L, s, wid, r, pos, pos, dof_invweight0[da], jnt_solref + 2 * j, jnt_solimp + 5 * j, jm, Jv * qvel[da], 0.0f,
                 CNSTR_LIMIT_JOINT, j);
-      }
+      put_J_rows(d, L, s, wid, np, kJ, njmax, lane, bal, nefc, da, Jv);
       int cnt = __popcll(bal);
       nefc += cnt;
       nl += cnt;

@@ -298,6 +298,8 @@ def put_model(mjm, device=None) -> types.Model:
   m.nsitetrn = int(np.isin(np.asarray(mjm.actuator_trntype), (types.TrnType.SITE, types.TrnType.SLIDERCRANK)).sum()) if mjm.nu else 0
 
   m.nJmom = int(sum(_mom_nnz(mjm, a) for a in range(mjm.nu)))
+  sc_adr, sc_num, sc_pair = _sensor_collision_pairs(mjm, pairid_all)
+  m.nsensorcollision = len(sc_pair) // 4
 
   # sparse path: kinematic trees as dof ranges (a tree starts at every dof without a parent dof),
   # J row width = the longest union of two dof chains (+ the 6 dofs of a flex edge)
@@ -362,9 +364,13 @@ def put_model(mjm, device=None) -> types.Model:
     level_adr=level_adr,
     jnt_limited_slide_hinge_adr=jnt_limited_sh,
     jnt_limited_ball_adr=jnt_limited_ball,
+    sensor_collision_adr=sc_adr,
+    sensor_collision_num=sc_num,
+    sensor_collision_pair=sc_pair,
   )
   for k_, v_ in derived_int.items():
-    if k_ in ("tree_dofadr", "flex_cgeomadr", "flex_cgeom", "plane_geom", "flexvert_incadr", "flexvert_inc", "body_fluid_ellipsoid"):
+    if k_ in ("tree_dofadr", "flex_cgeomadr", "flex_cgeom", "plane_geom", "flexvert_incadr", "flexvert_inc", "body_fluid_ellipsoid",
+              "sensor_collision_adr", "sensor_collision_num", "sensor_collision_pair"):
       setattr(m, k_, _i32(v_, dev))
   m.body_subtree_end = _i32(subtree_end, dev)
   m.body_level = _i32(depth, dev)
@@ -391,6 +397,49 @@ def put_model(mjm, device=None) -> types.Model:
       setattr(m, name, _i32(np.asarray(getattr(mjm, name)), dev))
   m._mjm_sizes = dict(nq=mjm.nq, nv=nv)
   return m
+
+
+# collision sensors (GEOMDIST / GEOMNORMAL / GEOMFROMTO) and the primitive pairs they can evaluate: the
+# type-sorted pairs of collision_driver.py:43-77's PRIMITIVE entries (the convex entries need the GJK
+# distance with an unbounded cutoff, collision_convex.py:772-776, which this build does not evaluate)
+_COLLISION_SENSORS = (types.SensorType.GEOMDIST, types.SensorType.GEOMNORMAL, types.SensorType.GEOMFROMTO)
+_SENSOR_PAIRS = _PRIMITIVE_PAIRS | {(0, 4), (0, 5), (2, 5)}
+
+
+def _sensor_collision_pairs(mjm, pairid_all):
+  """Per collision sensor, the geom pairs it collides (io.py:304-346: every geom of obj (a geom, or a body's
+  geoms) against every geom of ref, in that loop order) as (g1, g2, pairid, flip) records with (g1, g2)
+  in the narrowphase's type-then-index order, pairid the explicit <pair> that sets the margin (-1: the geoms'
+  margins), and flip = the record's order is (ref, obj) (sensor.py:656-661).  Returns (adr, num, flat
+  records); adr = -1 for the other sensors."""
+  ns = int(getattr(mjm, "nsensor", 0))
+  adr, num, recs = np.full(ns, -1, np.int32), np.zeros(ns, np.int32), []
+  n = mjm.ngeom
+  for s_ in range(ns):
+    if int(mjm.sensor_type[s_]) not in _COLLISION_SENSORS:
+      continue
+    geoms = []
+    for ot, oid in ((mjm.sensor_objtype[s_], mjm.sensor_objid[s_]), (mjm.sensor_reftype[s_], mjm.sensor_refid[s_])):
+      if int(ot) == types.ObjType.BODY:
+        geoms.append(range(mjm.body_geomadr[oid], mjm.body_geomadr[oid] + mjm.body_geomnum[oid]))
+      else:
+        geoms.append([int(oid)])
+    adr[s_] = len(recs)
+    for a in geoms[0]:
+      for b in geoms[1]:
+        if a == b:
+          raise NotImplementedError(f"collision sensor {s_}: a geom against itself")
+        ta, tb = int(mjm.geom_type[a]), int(mjm.geom_type[b])
+        if tuple(sorted((ta, tb))) not in _SENSOR_PAIRS:
+          names = tuple(types.GeomType(x).name for x in sorted((ta, tb)))
+          raise NotImplementedError(f"collision sensor {s_}: {names[0]}-{names[1]} needs the convex (GJK distance) path, not supported by this build yet")
+        flip = ta > tb or (ta == tb and a > b)
+        g1, g2 = (b, a) if flip else (a, b)
+        lo, hi = min(a, b), max(a, b)
+        pid = int(pairid_all[(lo * (2 * n - lo - 3)) // 2 + hi - 1, 0])
+        recs.append((g1, g2, max(pid, -1), int(flip)))
+        num[s_] += 1
+  return adr, num, np.array(recs, dtype=np.int32).reshape(-1)
 
 
 def _mom_nnz(mjm, a) -> int:
@@ -427,9 +476,11 @@ DERIVED_INT_ARRAYS = {
   "nxn_geom_pair": "nxn_geom_pair_typed", "nxn_pairid": "nxn_pairid_filtered", "nxn_ccdid": "nxn_ccdid",
   "tree_dofadr": "tree_dofadr", "flex_cgeomadr": "flex_cgeomadr", "flex_cgeom": "flex_cgeom", "plane_geom": "plane_geom",
   "flexvert_incadr": "flexvert_incadr", "flexvert_inc": "flexvert_inc",
+  "sensor_collision_adr": "sensor_collision_adr", "sensor_collision_num": "sensor_collision_num", "sensor_collision_pair": "sensor_collision_pair",
 }
 DERIVED_SCALARS = ("act_maxnnz", "nbodytrn", "nsitetrn", "nten_spatial", "nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle", "sp_nH",
-                   "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane")
+                   "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane",
+                   "nsensorcollision")
 
 
 def derive_model_fields(mjm) -> dict:

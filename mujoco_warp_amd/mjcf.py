@@ -1718,6 +1718,12 @@ class _Compiler:
     "subtreeangmom": (SensorType.SUBTREEANGMOM, 3, DataType.REAL, Stage.VEL, "body", ObjType.BODY),
     "e_potential": (SensorType.E_POTENTIAL, 1, DataType.REAL, Stage.POS, None, ObjType.UNKNOWN),
     "e_kinetic": (SensorType.E_KINETIC, 1, DataType.REAL, Stage.VEL, None, ObjType.UNKNOWN),
+    # collision sensors: geom1 | body1 against geom2 | body2 (MuJoCo's mjSENS_GEOMDIST / GEOMNORMAL / GEOMFROMTO)
+    "distance": (SensorType.GEOMDIST, 1, DataType.REAL, Stage.POS, "collision", None),
+    "normal": (SensorType.GEOMNORMAL, 3, DataType.AXIS, Stage.POS, "collision", None),
+    "fromto": (SensorType.GEOMFROMTO, 6, DataType.REAL, Stage.POS, "collision", None),
+    # insidesite: objtype / objname inside the geometry of `site`
+    "insidesite": (SensorType.INSIDESITE, 1, DataType.REAL, Stage.POS, "insidesite", None),
   }
   _OBJTYPES = {"body": ObjType.BODY, "xbody": ObjType.XBODY, "geom": ObjType.GEOM, "site": ObjType.SITE, "camera": ObjType.CAMERA}
 
@@ -1744,7 +1750,14 @@ class _Compiler:
         a.update(el.attrib)
         stype, dim, dtype, stage, key, otype = self._SENSORS[el.tag]
         objid, reftype, refid = -1, ObjType.UNKNOWN, -1
-        if key is not None:
+        if key == "collision":
+          otype, objid = (ObjType.GEOM, names[ObjType.GEOM][a["geom1"]]) if "geom1" in a else (ObjType.BODY, names[ObjType.BODY][a["body1"]])
+          reftype, refid = (ObjType.GEOM, names[ObjType.GEOM][a["geom2"]]) if "geom2" in a else (ObjType.BODY, names[ObjType.BODY][a["body2"]])
+        elif key == "insidesite":
+          otype = self._OBJTYPES[a["objtype"]]
+          objid = names[otype][a["objname"]]
+          reftype, refid = ObjType.SITE, names[ObjType.SITE][a["site"]]
+        elif key is not None:
           objid = names[otype][a[key]]
         elif otype is None:  # frame sensors: objtype / objname (+ optional reftype / refname)
           otype = self._OBJTYPES[a["objtype"]]

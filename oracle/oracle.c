@@ -3469,8 +3469,9 @@ static void sensor_write(const orc_model* m, orc_data* d, int s, const real* v, 
   real* out = d->sensordata + m->sensor_adr[s];
   for (int i = 0; i < dim; i++) {
     real x = v[i];
-    if (cutoff > 0 && dt == DATATYPE_REAL) x = clampr(x, -cutoff, cutoff);
-    else if (cutoff > 0 && dt == DATATYPE_POSITIVE) x = minr(x, cutoff);
+    int clip = cutoff > 0 && m->sensor_type[s] != 41; /* sensor.py:69, 98: never GEOMFROMTO */
+    if (clip && dt == DATATYPE_REAL) x = clampr(x, -cutoff, cutoff);
+    else if (clip && dt == DATATYPE_POSITIVE) x = minr(x, cutoff);
     out[i] = x;
   }
 }

@@ -3,14 +3,135 @@
  * touch (sensor.py:2001-2076, with ray.py:105-450's ray-geom intersections for the site zone), tendon
  * position / velocity / actuator force (sensor.py:222, 957, 1538-1577), joint and tendon limit position /
  * velocity / force (sensor.py:243-278, 972-1007, 1580-1615), subtree linear velocity and angular momentum
- * (smooth.py:2932-3084), potential and kinetic energy (sensor.py:2700-2940).  Included by oracle.c after its
- * sensor helpers. */
+ * (smooth.py:2932-3084), potential and kinetic energy (sensor.py:2700-2940), the collision sensors distance /
+ * normal / fromto over primitive geom pairs (sensor.py:604-680, 710-757) and insidesite (sensor.py:681-697,
+ * util_misc.py:603-632).  Included by oracle.c after its sensor helpers. */
 
 enum {
   SENS_TOUCH = 0, SENS_TENDONPOS = 11, SENS_TENDONVEL = 12, SENS_TENDONACTFRC = 17, SENS_JOINTLIMITPOS = 20,
   SENS_JOINTLIMITVEL = 21, SENS_JOINTLIMITFRC = 22, SENS_TENDONLIMITPOS = 23, SENS_TENDONLIMITVEL = 24,
-  SENS_TENDONLIMITFRC = 25, SENS_SUBTREELINVEL = 36, SENS_SUBTREEANGMOM = 37, SENS_E_POTENTIAL = 43, SENS_E_KINETIC = 44
+  SENS_TENDONLIMITFRC = 25, SENS_SUBTREELINVEL = 36, SENS_SUBTREEANGMOM = 37, SENS_E_POTENTIAL = 43, SENS_E_KINETIC = 44,
+  SENS_INSIDESITE = 38, SENS_GEOMDIST = 39, SENS_GEOMNORMAL = 40, SENS_GEOMFROMTO = 41
 };
+
+/* ---- collision sensors: the smallest-distance contact over the sensor's geom pairs ---- */
+typedef struct {
+  real dist, p1[3], p2[3];
+  int flip;
+} coll_best;
+
+/* sensor.py:744-757: contact points pos -+ dist / 2 along the contact normal */
+static void coll_offer(coll_best* b, real dist, const real* pos, const real* nrm, int flip) {
+  if (!(dist < b->dist)) return;
+  b->dist = dist;
+  b->flip = flip;
+  for (int i = 0; i < 3; i++) {
+    b->p1[i] = pos[i] - 0.5 * dist * nrm[i];
+    b->p2[i] = pos[i] + 0.5 * dist * nrm[i];
+  }
+}
+
+/* every contact collision_primitive.py writes for the type-sorted pair (g1, g2), inside or outside the margin
+ * (write_contact keeps sensor contacts, collision_core.py:199-213) */
+static void coll_pair(const orc_model* m, const orc_data* d, int g1, int g2, int flip, coll_best* b) {
+  int pairid = -1;
+  for (int p = 0; p < m->nxn; p++) {
+    int a = m->nxn_geom_pair[2 * p], c = m->nxn_geom_pair[2 * p + 1];
+    if ((a == g1 && c == g2) || (a == g2 && c == g1)) { pairid = m->nxn_pairid[2 * p] > -1 ? m->nxn_pairid[2 * p] : -1; break; }
+  }
+  real margin = pairid > -1 ? m->pair_margin[pairid] : m->geom_margin[g1] + m->geom_margin[g2];
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const real *p1 = d->geom_xpos + 3 * g1, *p2 = d->geom_xpos + 3 * g2;
+  const real *r1 = d->geom_xmat + 9 * g1, *r2 = d->geom_xmat + 9 * g2;
+  const real *s1 = m->geom_size + 3 * g1, *s2 = m->geom_size + 3 * g2;
+  real n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]}, nrm[3], pos[3], dist;
+  contacts2 c;
+  c.n = 0;
+  if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {
+    for (int k = 0; k < 8; k++) { plane_box_corner(k, n1, p1, p2, r2, s2, &dist, pos); coll_offer(b, dist, pos, n1, flip); }
+    return;
+  }
+  if (t1 == GEOM_PLANE && t2 == GEOM_CYLINDER) {
+    for (int k = 0; k < 4; k++) { plane_cylinder_k(k, n1, p1, p2, n2, s2[0], s2[1], &dist, pos); coll_offer(b, dist, pos, n1, flip); }
+    return;
+  }
+  if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) {
+    c.dist[0] = plane_sphere(c.pos[0], n1, p1, p2, s2[0]); make_frame(c.frame[0], n1); c.n = 1;
+  } else if (t1 == GEOM_PLANE && t2 == GEOM_CAPSULE) {
+    plane_capsule(&c, n1, p1, p2, n2, s2[0], s2[1]);
+  } else if (t1 == GEOM_PLANE && t2 == GEOM_ELLIPSOID) {
+    c.dist[0] = plane_ellipsoid(c.pos[0], n1, p1, p2, r2, s2); make_frame(c.frame[0], n1); c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
+    c.dist[0] = sphere_sphere(c.pos[0], nrm, p1, s1[0], p2, s2[0]); make_frame(c.frame[0], nrm); c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
+    c.dist[0] = sphere_capsule(c.pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]); make_frame(c.frame[0], nrm); c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_CYLINDER) {
+    c.dist[0] = sphere_cylinder(c.pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]); make_frame(c.frame[0], nrm); c.n = 1;
+  } else if (t1 == GEOM_SPHERE && t2 == GEOM_BOX) {
+    c.dist[0] = sphere_box(c.pos[0], nrm, p1, s1[0], p2, r2, s2); make_frame(c.frame[0], nrm); c.n = 1;
+  } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
+    capsule_capsule(&c, p1, n1, s1[0], s1[1], p2, n2, s2[0], s2[1], margin);
+  } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {
+    capsule_box(&c, p1, n1, s1[0], s1[1], p2, r2, s2);
+  }
+  for (int i = 0; i < c.n && i < 2; i++) coll_offer(b, c.dist[i], c.pos[i], c.frame[i], flip);
+}
+
+/* sensor.py:604-680: GEOMDIST / GEOMNORMAL / GEOMFROMTO; obj (a geom, or a body's geoms) against ref, pairs
+ * in type-then-index order with flip = the pair runs (ref, obj) */
+static void collision_sensor(const orc_model* m, orc_data* d, int s) {
+  const int t = m->sensor_type[s];
+  const real cutoff = m->sensor_cutoff[s];
+  coll_best b = {cutoff, {0, 0, 0}, {0, 0, 0}, 0};
+  int ids[2], nums[2];
+  const int types[2] = {m->sensor_objtype[s], m->sensor_reftype[s]}, objs[2] = {m->sensor_objid[s], m->sensor_refid[s]};
+  for (int k = 0; k < 2; k++) {
+    if (types[k] == OBJ_BODY) { ids[k] = m->body_geomadr[objs[k]]; nums[k] = m->body_geomnum[objs[k]]; }
+    else { ids[k] = objs[k]; nums[k] = 1; }
+  }
+  for (int a = ids[0]; a < ids[0] + nums[0]; a++)
+    for (int c = ids[1]; c < ids[1] + nums[1]; c++) {
+      int ta = m->geom_type[a], tc = m->geom_type[c];
+      int flip = ta > tc || (ta == tc && a > c);
+      coll_pair(m, d, flip ? c : a, flip ? a : c, flip, &b);
+    }
+  real v[6] = {0, 0, 0, 0, 0, 0};
+  int dim = 1;
+  if (t == SENS_GEOMDIST) {
+    v[0] = b.dist;
+  } else if (t == SENS_GEOMNORMAL) {
+    dim = 3;
+    if (b.dist <= cutoff) {
+      real nn[3] = {b.p2[0] - b.p1[0], b.p2[1] - b.p1[1], b.p2[2] - b.p1[2]};
+      normalize3(nn);
+      for (int i = 0; i < 3; i++) v[i] = b.flip ? -nn[i] : nn[i];
+    }
+  } else {
+    dim = 6;
+    if (b.dist <= cutoff)
+      for (int i = 0; i < 3; i++) { v[i] = b.flip ? b.p2[i] : b.p1[i]; v[3 + i] = b.flip ? b.p1[i] : b.p2[i]; }
+  }
+  sensor_write(m, d, s, v, dim);
+}
+
+/* util_misc.py:603-632 inside_geom */
+static int inside_geom(const real* pos, const real* mat, const real* size, int type, const real* pt) {
+  real vec[3] = {pt[0] - pos[0], pt[1] - pos[1], pt[2] - pos[2]}, pl[3];
+  if (type == GEOM_SPHERE) return dot3(vec, vec) < size[0] * size[0];
+  mat_t_vec(pl, mat, vec);
+  if (type == GEOM_CAPSULE) {
+    real z = pl[2], zc = z < -size[1] ? -size[1] : (z > size[1] ? size[1] : z), zd = z - zc;
+    return pl[0] * pl[0] + pl[1] * pl[1] + zd * zd < size[0] * size[0];
+  }
+  if (type == GEOM_ELLIPSOID) {
+    real q[3] = {pl[0] / size[0], pl[1] / size[1], pl[2] / size[2]};
+    return dot3(q, q) < 1;
+  }
+  if (type == GEOM_CYLINDER) return fabs(pl[2]) < size[1] && pl[0] * pl[0] + pl[1] * pl[1] < size[0] * size[0];
+  if (type == GEOM_BOX) return fabs(pl[0]) < size[0] && fabs(pl[1]) < size[1] && fabs(pl[2]) < size[2];
+  if (type == GEOM_PLANE) return pl[2] < 0;
+  return 0;
+}
 
 /* ray.py:105-125: smallest non-negative root of a x^2 + 2 b x + c = 0 (else -1); both roots in x */
 static real ray_quad(real a, real b, real c, real* x) {
@@ -262,6 +383,15 @@ static void sensor_extra(const orc_model* m, orc_data* d, int stage) {
       case SENS_SUBTREEANGMOM: memcpy(v, d->subtree_angmom + 3 * id, sizeof(v)); dim = 3; break;
       case SENS_E_POTENTIAL: v[0] = energy_potential(m, d); break;
       case SENS_E_KINETIC: v[0] = energy_kinetic(m, d); break;
+      case SENS_GEOMDIST: case SENS_GEOMNORMAL: case SENS_GEOMFROMTO: collision_sensor(m, d, s); continue;
+      case SENS_INSIDESITE: {
+        const real *p, *R;
+        int body;
+        obj_frame(m, d, m->sensor_objtype[s], id, &p, &R, &body);
+        const int site = m->sensor_refid[s];
+        v[0] = inside_geom(d->site_xpos + 3 * site, d->site_xmat + 9 * site, m->site_size + 3 * site, m->site_type[site], p);
+        break;
+      }
       default: continue;
     }
     sensor_write(m, d, s, v, dim);
