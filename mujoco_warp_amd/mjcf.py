@@ -475,35 +475,44 @@ class _Compiler:
     spacing * (i - (count-1)/2) (MuJoCo user_flexcomp.cc, restated: parity unpinned, no MuJoCo here)."""
     a = el.attrib
     ftype = a.get("type", "grid")
-    if ftype != "grid":
-      raise NotImplementedError(f"flexcomp type '{ftype}' is not supported (grid only)")
+    if ftype not in ("grid", "direct"):
+      raise NotImplementedError(f"flexcomp type '{ftype}' is not supported (grid and direct only)")
     dim = int(a.get("dim", 2))
     if dim != 2:
-      raise NotImplementedError("only dim=2 flexcomp grids are supported")
+      raise NotImplementedError("only dim=2 flexcomps are supported")
     if a.get("dof", "full") != "full":
       raise NotImplementedError("only flexcomp dof='full' is supported")
-    count = [int(x) for x in _floats(a.get("count", "10 10 1"), 3)]
-    if count[2] != 1:
-      raise NotImplementedError("dim=2 grid needs count[2] == 1")
-    spacing = np.array(_floats(a.get("spacing", "0.02 0.02 0.02"), 3))
     pos = np.array(_floats(a.get("pos", "0 0 0"), 3))
     q = _orientation(a, self.angle_scale, self.eulerseq)
     R = quat_to_mat(np.array([1.0, 0, 0, 0]) if q is None else np.asarray(q, dtype=float))
     name = a.get("name", f"flex{len(self.flexcomps)}")
-    npnt = count[0] * count[1] * count[2]
     mass = float(a.get("mass", 1.0))
-    pts = []
-    for ix in range(count[0]):
-      for iy in range(count[1]):
-        for iz in range(count[2]):
-          loc = spacing * (np.array([ix, iy, iz]) - 0.5 * (np.array(count) - 1))
-          pts.append(R @ loc + pos)
-    elems = []
-    cy = count[1]
-    for ix in range(count[0] - 1):
-      for iy in range(count[1] - 1):
-        v00, v10, v11, v01 = ix * cy + iy, (ix + 1) * cy + iy, (ix + 1) * cy + iy + 1, ix * cy + iy + 1
-        elems += [(v00, v10, v11), (v00, v11, v01)]
+    pts, elems = [], []
+    if ftype == "direct":
+      # type="direct": the points (flexcomp frame) and the triangles (vertex index triples) as given
+      loc = np.array(_floats(a["point"]), dtype=float).reshape(-1, 3)
+      pts = [R @ p_ + pos for p_ in loc]
+      tri = np.array([int(x) for x in a["element"].split()], dtype=np.int64).reshape(-1, 3)
+      if tri.size and (tri.min() < 0 or tri.max() >= len(pts)):
+        raise ValueError(f"flexcomp '{name}': element index out of range")
+      elems = [tuple(int(v) for v in t) for t in tri]
+      npnt = len(pts)
+    else:
+      count = [int(x) for x in _floats(a.get("count", "10 10 1"), 3)]
+      if count[2] != 1:
+        raise NotImplementedError("dim=2 grid needs count[2] == 1")
+      spacing = np.array(_floats(a.get("spacing", "0.02 0.02 0.02"), 3))
+      npnt = count[0] * count[1] * count[2]
+      for ix in range(count[0]):
+        for iy in range(count[1]):
+          for iz in range(count[2]):
+            loc = spacing * (np.array([ix, iy, iz]) - 0.5 * (np.array(count) - 1))
+            pts.append(R @ loc + pos)
+      cy = count[1]
+      for ix in range(count[0] - 1):
+        for iy in range(count[1] - 1):
+          v00, v10, v11, v01 = ix * cy + iy, (ix + 1) * cy + iy, (ix + 1) * cy + iy + 1, ix * cy + iy + 1
+          elems += [(v00, v10, v11), (v00, v11, v01)]
     bodies = []
     for i, p in enumerate(pts):
       b = _Body(f"{name}_{i}", parent, childclass)
@@ -553,8 +562,9 @@ class _Compiler:
 
   def _flatten_frame(self, frame):
     """<frame pos quat/euler/...>: compose the frame transform into each child (MJCF frame semantics)."""
-    if frame.get("childclass") is not None and len(frame):
-      raise NotImplementedError("<frame childclass=...> is not supported by the MJCF compiler")
+    # childclass: the frame's children (and, for bodies, their subtrees) default to it unless they name a
+    # class (bodies: a childclass) of their own; an inner frame's childclass was applied first
+    fcls = frame.get("childclass")
     fpos = np.array(_floats(frame.get("pos", "0 0 0"), 3))
     fq = _orientation(frame.attrib, self.angle_scale, self.eulerseq)
     fq = np.array([1.0, 0, 0, 0]) if fq is None else np.asarray(fq, dtype=float)
@@ -568,6 +578,10 @@ class _Compiler:
       for c in subs:
         c = copy.deepcopy(c)
         a = c.attrib
+        if fcls is not None:
+          key = "childclass" if c.tag == "body" else "class"
+          if key not in a:
+            a[key] = fcls
         if c.tag == "geom" and "fromto" in a:
           ft = np.array(_floats(a["fromto"], 6))
           p0, p1 = R @ ft[:3] + fpos, R @ ft[3:] + fpos

@@ -135,6 +135,45 @@ def test_unsupported_features_raise():
   assert m.nxn_ccd == 3  # plane-ellipsoid, plane-cylinder (pre-pass primitives) and ellipsoid-cylinder (convex)
 
 
+def test_frame_childclass():
+  """<frame childclass>: the frame's elements default to the class (an explicit class wins), bodies inside take
+  it as their childclass, and an inner frame's childclass overrides the outer one (MJCF frame semantics)."""
+  from mujoco_warp_amd import mjcf
+
+  m = mjcf.load_model_from_string("""<mujoco><default><default class="big"><geom size=".3"/><joint damping="2"/></default>
+  <default class="small"><geom size=".05"/></default></default>
+  <worldbody><frame childclass="big" pos="1 0 0"><geom name="a" type="sphere"/><geom name="b" type="sphere" class="small" pos="0 1 0"/>
+  <body><joint type="hinge"/><geom name="c" type="sphere" pos="0 0 1"/><frame childclass="small"><geom name="d" type="sphere" pos="0 0 2"/></frame>
+  </body></frame><geom name="e" type="sphere" size=".7" pos="5 0 0"/></worldbody></mujoco>""")
+  size = {n: m.geom_size[i, 0] for i, n in enumerate(m.geom_names)}
+  assert (size["a"], size["b"], size["c"], size["d"], size["e"]) == (0.3, 0.05, 0.3, 0.05, 0.7)
+  np.testing.assert_allclose(m.dof_damping, [2.0])
+  np.testing.assert_allclose(m.geom_pos[list(m.geom_names).index("a")], [1, 0, 0])
+
+
+def test_flexcomp_direct_equals_grid():
+  """flexcomp type="direct" (explicit points and triangles) compiles to the same flex tables, vertex bodies
+  and bending coefficients as the grid it lists (the grid's own point / triangle order)."""
+  from mujoco_warp_amd import mjcf
+
+  body = ('<edge equality="true"/><elasticity young="1e3" poisson="0.2" thickness="0.01" elastic2d="bend"/>'
+          '<contact condim="3"/></flexcomp></worldbody></mujoco>')
+  grid = mjcf.load_model_from_string('<mujoco><worldbody><geom type="plane" size="1 1 .1"/>'
+                                     '<flexcomp name="c" type="grid" count="3 4 1" spacing=".1 .1 .1" pos="0 0 .5" mass=".6" radius=".01" dim="2">'
+                                     + body)
+  pts = grid.body_pos[grid.flex_vertbodyid] - np.array([0, 0, 0.5])
+  tri = grid.flex_elem.reshape(-1, 3)
+  direct = mjcf.load_model_from_string('<mujoco><worldbody><geom type="plane" size="1 1 .1"/>'
+                                       f'<flexcomp name="c" type="direct" pos="0 0 .5" mass=".6" radius=".01" dim="2" '
+                                       f'point="{" ".join(repr(float(x)) for x in pts.reshape(-1))}" element="{" ".join(str(int(x)) for x in tri.reshape(-1))}">'
+                                       + body)
+  for f in ("flex_edge", "flex_edgeflap", "flex_elem", "flex_elemedge", "body_pos", "body_mass"):
+    np.testing.assert_array_equal(getattr(direct, f), getattr(grid, f), err_msg=f)
+  for f in ("flexedge_length0", "flex_bending", "flexedge_invweight0"):
+    np.testing.assert_allclose(getattr(direct, f), getattr(grid, f), rtol=1e-12, atol=1e-15, err_msg=f)
+  assert direct.nflexelem == 2 * 2 * 3 and direct.neq == grid.neq
+
+
 # ---- C ABI ------------------------------------------------------------------------------------
 def test_header_declares_and_library_exports_every_entry_point():
   from mujoco_warp_amd import _lib
