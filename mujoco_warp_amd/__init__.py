@@ -52,6 +52,8 @@ from .stages import rne_postconstraint
 from .stages import set_const
 from .stages import set_const_0
 from .stages import set_const_fixed
+from .stages import set_length_range
+from .stages import deriv_smooth_vel
 from .stages import solve_m
 from .stages import subtree_vel
 from .stages import tendon

@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from .forward import _call, _sensor, fwd_position, fwd_velocity
+from . import types
 from .types import Data, DisableBit, JointType, Model
 
 
@@ -428,6 +429,160 @@ def _quat_to_mat(q: torch.Tensor) -> torch.Tensor:
     2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
     2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], dim=-1)
   return r.reshape(q.shape[:-1] + (3, 3))
+
+
+def set_length_range(m: Model, d: Data, index: int = -1):
+  """io.py:2465-2495 (with _set_length_range :2158-2194): the actuator length ranges from the limits of joint
+  and tendon transmissions scaled by gear[0] (swapped for a negative gear); every other actuator gets (0, 0),
+  as the reference writes them.  One row per world (actuator_gear / jnt_range / tendon_range are read at
+  worldid % nb).  `index` is accepted for API parity and, as in the reference, does not restrict the update."""
+  del index
+  nu, nw = m.nu, d.nworld
+  if nu == 0:
+    return
+  dev = m.actuator_gear.device
+  trn = m.actuator_trntype.long()
+  id0 = m.actuator_trnid.reshape(nu, 2)[:, 0].long()
+  gear0 = _per_world(m.actuator_gear, nw, nu, 6)[:, :, 0].double()
+  lr = torch.zeros(nw, nu, 2, dtype=torch.float64, device=dev)
+  joint = (trn == int(types.TrnType.JOINT)) | (trn == int(types.TrnType.JOINTINPARENT))
+  if m.njnt:
+    jl = m.jnt_limited.long()[id0.clamp(0, m.njnt - 1)] != 0
+    rng = _per_world(m.jnt_range, nw, m.njnt, 2).double()[:, id0.clamp(0, m.njnt - 1)]
+    sel = (joint & jl)[None, :, None].expand(nw, nu, 2)
+    lr = torch.where(sel, rng * gear0[:, :, None], lr)
+  nten = int(getattr(m, "ntendon", 0))
+  if nten:
+    ten = trn == int(types.TrnType.TENDON)
+    tl = m.tendon_limited.long()[id0.clamp(0, nten - 1)] != 0
+    rng = _per_world(m.tendon_range, nw, nten, 2).double()[:, id0.clamp(0, nten - 1)]
+    sel = (ten & tl)[None, :, None].expand(nw, nu, 2)
+    lr = torch.where(sel, rng * gear0[:, :, None], lr)
+  neg = (gear0 <= 0.0)[:, :, None].expand(nw, nu, 2)
+  lr = torch.where(neg, lr.flip(-1), lr)  # gear <= 0: (rng[1] gear, rng[0] gear)
+  m.actuator_lengthrange = lr.to(m.actuator_lengthrange.dtype).contiguous()
+
+
+def deriv_smooth_vel(m: Model, d: Data, out: torch.Tensor):
+  """derivative.py:321-416: out = qM - dt qDeriv, the derivative of the smooth forces with respect to qvel on
+  the qM pattern: qDeriv = sum_a vel_a m_a m_a' (_qderiv_actuator_passive_vel: affine gain / bias slope, with
+  the activation or control and the force-range cut) - diag(dof_damping) - sum_t damping_t J_t' J_t.  `out` has
+  qM's shape: (nworld, nv_pad, nv_pad) dense, (nworld, nM) sparse.  The device implicitfast integrator forms
+  the same matrix inside its Euler launch; this is the reference's stand-alone entry point."""
+  nw, nv, nu = d.nworld, m.nv, m.nu
+  dev = d.qM.device
+  fl = int(m.opt.disableflags)
+  dt = _per_world(m.opt.timestep, nw, 1)[:, 0].double()
+  qd = torch.zeros(nw, nv, nv, dtype=torch.float64, device=dev)
+  if nu and not (fl & int(DisableBit.ACTUATION)):
+    gt, bt, dyn = m.actuator_gaintype.long(), m.actuator_biastype.long(), m.actuator_dyntype.long()
+    gain = torch.where(gt == int(types.GainType.AFFINE), _per_world(m.actuator_gainprm, nw, nu, 10)[:, :, 2].double(), 0.0)
+    bias = torch.where(bt == int(types.BiasType.AFFINE), _per_world(m.actuator_biasprm, nw, nu, 10)[:, :, 2].double(), 0.0)
+    force = d.actuator_force.reshape(nw, nu).double()
+    frng = _per_world(m.actuator_forcerange, nw, nu, 2).double()
+    clamped = (m.actuator_forcelimited.bool())[None] & ((force <= frng[:, :, 0]) | (force >= frng[:, :, 1]))
+    vel = bias.clone()
+    na = int(m.na)
+    if na:
+      adr = (m.actuator_actadr.long() + m.actuator_actnum.long() - 1).clamp(0, na - 1)
+      act = d.act.reshape(nw, na).double()[:, adr]
+      act_dot = d.act_dot.reshape(nw, na).double()[:, adr]
+      tau = _per_world(m.actuator_dynprm, nw, nu, 10)[:, :, 0].double().clamp_min(1e-15)
+      nxt = torch.where(dyn == int(types.DynType.FILTEREXACT), act + act_dot * tau * (1 - torch.exp(-dt[:, None] / tau)), act + act_dot * dt[:, None])
+      nxt = torch.where(dyn == int(types.DynType.USER), act, nxt)
+      arng = _per_world(m.actuator_actrange, nw, nu, 2).double()
+      nxt = torch.where(m.actuator_actlimited.bool()[None], torch.minimum(torch.maximum(nxt, arng[:, :, 0]), arng[:, :, 1]), nxt)
+      act_use = torch.where(m.actuator_actearly.bool()[None], nxt, act)
+    else:
+      act_use = torch.zeros(nw, nu, dtype=torch.float64, device=dev)
+    ctrl = d.ctrl.reshape(nw, nu).double()
+    vel = vel + torch.where(dyn != int(types.DynType.NONE), gain * act_use, gain * ctrl)
+    vel = torch.where(((gain == 0) & (bias == 0)) | clamped, 0.0, vel)
+    mom = _moment_dense(m, d)  # (nw, nu, nv)
+    qd += torch.einsum("wa,wai,waj->wij", vel, mom, mom)
+  if not (fl & int(DisableBit.DAMPER)):
+    qd -= torch.diag_embed(_per_world(m.dof_damping, nw, nv).double())
+    nten = int(getattr(m, "ntendon", 0))
+    if nten:
+      J = _ten_J_dense(m, d)  # (nw, nten, nv)
+      qd -= torch.einsum("wt,wti,wtj->wij", _per_world(m.tendon_damping, nw, nten).double(), J, J)
+  res = _dense_qM(m, d).double() - dt[:, None, None] * qd
+  # the reference fills the qM pattern only (qM_fullm_i / j: a dof and its ancestors)
+  pat = _qM_pattern(m).to(dev)
+  res = torch.where(pat[None], res, 0.0)
+  if m.is_sparse:
+    rows, cols = _sparse_index(m)
+    out.reshape(nw, -1)[:, : m.nM] = res[:, rows, cols].to(out.dtype)
+  else:
+    out.zero_()
+    out[:, :nv, :nv] = res.to(out.dtype)
+
+
+def _moment_dense(m: Model, d: Data) -> torch.Tensor:
+  """actuator_moment as (nworld, nu, nv) fp64 from its per-world sparse rows (moment_rownnz / rowadr / colind)."""
+  nw, nu, nv = d.nworld, m.nu, m.nv
+  nJ = int(m.nJmom)
+  rnz = d.moment_rownnz.reshape(nw, nu).long()
+  radr = d.moment_rowadr.reshape(nw, nu).long()
+  col = d.moment_colind.reshape(nw, -1)[:, :nJ].long()
+  val = d.actuator_moment.reshape(nw, -1)[:, :nJ].double()
+  k = torch.arange(nJ, device=val.device)
+  # actuator of slot k: rowadr <= k < rowadr + rownnz
+  owner = ((k[None, None, :] >= radr[:, :, None]) & (k[None, None, :] < (radr + rnz)[:, :, None]))  # (nw, nu, nJ)
+  out = torch.zeros(nw, nu, nv, dtype=torch.float64, device=val.device)
+  out.scatter_add_(2, col[:, None, :].expand(nw, nu, nJ), torch.where(owner, val[:, None, :], 0.0))
+  return out
+
+
+def _ten_J_dense(m: Model, d: Data) -> torch.Tensor:
+  """ten_J as (nworld, ntendon, nv) fp64 (the model's fixed row pattern ten_J_rownnz / rowadr / colind)."""
+  nw, nten, nv = d.nworld, int(m.ntendon), m.nv
+  nJ = int(m.nJten)
+  rnz, radr, col = m.ten_J_rownnz.long(), m.ten_J_rowadr.long(), m.ten_J_colind.long()
+  val = d.ten_J.reshape(nw, -1)[:, :nJ].double()
+  out = torch.zeros(nw, nten, nv, dtype=torch.float64, device=val.device)
+  for t in range(nten):
+    a, n = int(radr[t]), int(rnz[t])
+    out[:, t].index_add_(1, col[a:a + n], val[:, a:a + n])
+  return out
+
+
+def _qM_pattern(m: Model) -> torch.Tensor:
+  """(nv, nv) bool: i, j in the same dof chain (the ancestor pattern qM stores, both triangles)."""
+  nv = m.nv
+  par = m.dof_parentid.cpu().numpy()
+  pat = np.zeros((nv, nv), dtype=bool)
+  for i in range(nv):
+    j = i
+    while j >= 0:
+      pat[i, j] = pat[j, i] = True
+      j = par[j]
+  return torch.as_tensor(pat)
+
+
+def _sparse_index(m: Model):
+  """Row / column of every entry of the sparse qM layout (M_rowadr / M_colind: ancestors ascending, then the
+  diagonal)."""
+  rowadr = m.M_rowadr.cpu().numpy()
+  rownnz = m.M_rownnz.cpu().numpy()
+  colind = m.M_colind.cpu().numpy()
+  rows = np.zeros(m.nM, dtype=np.int64)
+  for i in range(m.nv):
+    rows[rowadr[i]:rowadr[i] + rownnz[i]] = i
+  return torch.as_tensor(rows), torch.as_tensor(colind.astype(np.int64))
+
+
+def _dense_qM(m: Model, d: Data) -> torch.Tensor:
+  """qM of every world as (nworld, nv, nv), from either layout."""
+  nw, nv = d.nworld, m.nv
+  if not m.is_sparse:
+    return d.qM[:, :nv, :nv]
+  rows, cols = _sparse_index(m)
+  q = d.qM.reshape(nw, -1)[:, : m.nM]
+  full = torch.zeros(nw, nv, nv, dtype=q.dtype, device=q.device)
+  full[:, rows.to(q.device), cols.to(q.device)] = q
+  full[:, cols.to(q.device), rows.to(q.device)] = q
+  return full
 
 
 def set_const(m: Model, d: Data):
