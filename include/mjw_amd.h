@@ -126,7 +126,8 @@
  * Sparse models (is_sparse, the reference's io.py:67-74 switch) store qM / qLD as (nworld, nM) rows of
  * ancestors ascending then the diagonal (M_rowadr / M_colind), and efc_J as (nworld, njmax_pad, njrow)
  * stored slot-major (slot k of row r at [k * njmax_pad + r]) with efc_J_colind / efc_J_rownnz; dense models keep qM (nv_pad, nv_pad), qLD (nv, nv), efc_J
- * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt / ncon_world are sparse-path workspace (size 0 when dense);
+ * (njmax_pad, nv_pad).  sp_* / efc_JT_* / sp_cnt are sparse-path workspace (size 0 when dense); ncon_world holds a
+ * world's contact-pool range (first slot, count / span): the sparse path's, and the dense contact-rows pass's;
  * sp_idx16 holds the CG's 16-bit copies of efc_J_colind and of the transposed index's rows (two uint16 per int).
  * world_order / world_key: the dense path's longest-first world order (a permutation of the worlds, rebuilt
  * every step from the previous step's solver iterations) and each world's iteration bucket. */

@@ -1132,7 +1132,11 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
     int* plist = si + L.plist;
     // POOL: the candidates are this world's contacts in the pool (a contactfilter callback may have
     // edited them), in slot order = the pair order the narrowphase wrote them in
+    // the world's slot range [pool_k0, pool_k1) from pool_ranges_kernel (ncon_world: first slot, span), so a
+    // world scans its own contacts instead of the whole pool
     const int npool = POOL ? min(d.nacon[0], d.naconmax) : 0;
+    const int pool_k0 = POOL ? d.ncon_world[2L * wid] : 0;
+    const int pool_k1 = POOL ? min(npool, pool_k0 + d.ncon_world[2L * wid + 1]) : 0;
     for (int base = 0; base < (POOL ? 0 : m.nxn); base += LPW) {
       int p = base + lane;
       bool pass = false;
@@ -1153,11 +1157,11 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
     while (true) {
       const int rbeg = round * CM, rend = rbeg + CM;
       int running = 0;  // contacts found so far (world-local, in pair order)
-      for (int base = 0; base < (POOL ? npool : npass); base += LPW) {
+      for (int base = POOL ? pool_k0 : 0; base < (POOL ? pool_k1 : npass); base += LPW) {
         int k = base + lane;
         if constexpr (POOL) {
           // constraint.py:1731: contacts without the CONSTRAINT type bit get no rows (and no row address)
-          const bool mine = k < npool && d.contact_worldid[k] == wid;
+          const bool mine = k < pool_k1 && d.contact_worldid[k] == wid;
           const bool sel = mine && (d.contact_type[k] & 1);
           if (mine && !sel)
             for (int i = 0; i < m.nmaxpyramid; i++) d.contact_efc_address[(long)k * m.nmaxpyramid + i] = -1;
@@ -2724,6 +2728,32 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
 // joint actuator force range; one wave per world, lanes over dofs.  The staged fwd_actuation runs it after
 // the act_dyn / act_gain / act_bias callbacks (forward.py:876-881), which may rewrite actuator_force.  (The
 // stage launch before the callbacks applied the tendon range already; forces it left in range pass unchanged.)
+// per-world slot range of the contact pool for the POOL row pass (mjw_contact_rows): ncon_world[2w] = first
+// slot of world w, ncon_world[2w + 1] = span to its last slot (0 when it has none); the narrowphase reserves
+// one block per world and staging round, so the span is the world's own contacts unless it took several rounds
+__global__ void pool_ranges_init_kernel(const mjw_data_t d) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= d.nworld) return;
+  d.ncon_world[2L * w] = 0x7fffffff;
+  d.ncon_world[2L * w + 1] = -1;  // last slot, turned into the span below
+}
+__global__ void pool_ranges_kernel(const mjw_data_t d) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = min(d.nacon[0], d.naconmax);
+  if (k >= n) return;
+  const int w = d.contact_worldid[k];
+  if (w < 0 || w >= d.nworld) return;
+  atomicMin(d.ncon_world + 2L * w, k);
+  atomicMax(d.ncon_world + 2L * w + 1, k);
+}
+__global__ void pool_ranges_finish_kernel(const mjw_data_t d) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= d.nworld) return;
+  const int k0 = d.ncon_world[2L * w], k1 = d.ncon_world[2L * w + 1];
+  d.ncon_world[2L * w] = k1 < 0 ? 0 : k0;
+  d.ncon_world[2L * w + 1] = k1 < 0 ? 0 : k1 - k0 + 1;
+}
+
 __global__ void __launch_bounds__(64) actuator_map_kernel(const mjw_model_t m, const mjw_data_t d) {
   const int wid = blockIdx.x, lane = threadIdx.x;
   if (wid >= d.nworld) return;
@@ -3069,6 +3099,16 @@ int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_POS, "mjw_fwd_position");
 }
 int mjw_contact_rows(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
+  if (m && d && !m->is_sparse && d->nworld > 0) {
+    hipStream_t s = (hipStream_t)stream;
+    const int nw = d->nworld, nb = (d->nworld + 255) / 256, nk = (d->naconmax + 255) / 256;
+    hipLaunchKernelGGL(mjw::pool_ranges_init_kernel, dim3(nb), dim3(256), 0, s, *d);
+    if (nk > 0) hipLaunchKernelGGL(mjw::pool_ranges_kernel, dim3(nk), dim3(256), 0, s, *d);
+    hipLaunchKernelGGL(mjw::pool_ranges_finish_kernel, dim3(nb), dim3(256), 0, s, *d);
+    (void)nw;
+    const int rc = set_err(hipGetLastError(), "mjw_contact_rows");
+    if (rc) return rc;
+  }
   return run(m, d, stream, mjw::ST_POS | mjw::ST_POOL, "mjw_contact_rows");
 }
 int mjw_fwd_velocity(const mjw_model_t* m, const mjw_data_t* d, void* stream) {

@@ -33,9 +33,6 @@ def _padded_sizes(nv: int, njmax: int, is_sparse: bool):
   return njmax_pad, nv_pad
 
 
-SPARSE_NEWTON_NVMAX = 256
-
-
 def _muscle_mask(mjm):
   """Actuators with a muscle gain, bias or activation (forward.py:671-727)."""
   if not mjm.nu:
@@ -146,9 +143,6 @@ def put_model(mjm, device=None) -> types.Model:
   sparse = is_sparse(mjm) or getattr(mjm, "nflex", 0) > 0
   if sparse:
     # the workgroup-per-world sparse / flex pipeline (csrc/mjw_sparse.hip) covers this subset
-    if mjm.opt.solver == types.SolverType.NEWTON and mjm.nv > SPARSE_NEWTON_NVMAX:
-      # Newton's Hessian is dense (nv x nv per world, as the reference's H), so the flex models stay on CG
-      raise NotImplementedError(f"sparse / flex models: Newton needs nv <= {SPARSE_NEWTON_NVMAX} in this build (nv = {mjm.nv}); use CG.")
     if getattr(mjm, "nsensor", 0):
       # the sensor kernel (csrc/mjw_sensor.hip) stages a world's body / dof state in 64 KB of LDS
       if 37 * mjm.nbody + 14 * mjm.nv > 16384:

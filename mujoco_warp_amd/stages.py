@@ -331,8 +331,14 @@ def set_const_0(m: Model, d: Data):
     raise NotImplementedError("set_const_0 on sparse models is not part of this build")
   nw, nv, nb = d.nworld, m.nv, m.nbody
   saved = d.qpos.clone()
+  # the position launch also runs collision and make_constraint, which the reference's set_const_0 does not
+  # (io.py:2245-2253 runs the smooth stages only): the contact pool and the constraint rows are restored
+  kept = {k: getattr(d, k).clone() for k in ("nacon", "ncollision", "ne", "nf", "nl", "nefc") if torch.is_tensor(getattr(d, k, None))}
+  kept_sub = {(g, k): v.clone() for g in ("contact", "efc") for k, v in vars(getattr(d, g)).items() if torch.is_tensor(v)}
   d.qpos[:] = _per_world(m.qpos0, nw, m.nq)
   _call("mjw_fwd_position", m, d)
+  if int(getattr(m, "ntendon", 0)):  # io.py:2263 tendon_length0 from ten_length at qpos0
+    m.tendon_length0 = d.ten_length.reshape(nw, m.ntendon).to(m.tendon_length0.dtype).clone()
   M = d.qM.reshape(nw, m.nv_pad, m.nv_pad)[:, :nv, :nv].double()
   Minv = torch.linalg.inv(M)
   f32 = m.dof_invweight0.dtype
@@ -419,6 +425,10 @@ def set_const_0(m: Model, d: Data):
     m.light_poscom0 = (lx - sc[:, ref]).to(f32)
     m.light_dir0 = torch.einsum("wlij,wlj->wli", xmat[:, b], _per_world(m.light_dir, nw, m.nlight, 3)).to(f32)
   d.qpos[:] = saved
+  for k, v in kept.items():
+    getattr(d, k).copy_(v)
+  for (g, k), v in kept_sub.items():
+    getattr(getattr(d, g), k).copy_(v)
 
 
 def _quat_to_mat(q: torch.Tensor) -> torch.Tensor:

@@ -215,3 +215,63 @@ def test_gpu_sparse_elliptic_rollout_and_sliding_box():
   v1 = np_(db.qvel[:, 0])
   assert ncone > 50
   np.testing.assert_allclose((v1 - v0) / (100 * 0.002), mu * g, rtol=0.03)
+
+
+# ---- Newton on flex models past nv = 256 (the dense H of solver.py:2879-3008, nv x nv per world) ------
+BIG_CLOTH = """<mujoco><option timestep="0.002" solver="Newton" iterations="20"/><worldbody>
+<geom type="plane" size="2 2 .1"/><geom type="sphere" size=".15" pos="0 0 .15"/>
+<flexcomp name="c" type="grid" count="10 10 1" spacing=".05 .05 .05" pos="0 0 .32" mass=".2" radius=".005" dim="2">
+<edge equality="true"/><contact condim="3"/></flexcomp></worldbody></mujoco>"""
+
+
+def test_put_model_accepts_big_flex_newton():
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+
+  mjm = mjcf.load_model_from_string(BIG_CLOTH)
+  m = mjw.put_model(mjm, device="cpu")
+  assert m.is_sparse and mjm.nv == 300 and m.sp_nH == 300
+
+
+@pytest.mark.gpu
+def test_gpu_big_flex_newton_matches_oracle():
+  """A 10 x 10 towel (nv = 300) draped on a sphere, solved with Newton on the device: the fp64 cost of the
+  device qacc on the oracle's rows within the reference's 1.025x of the oracle optimum (solver_test.py:317),
+  and a 3-step rollout at the solver bar."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf
+  from tests.parity_models import efc_cost
+  from tests.test_gpu_parity_strict import normwise_close
+
+  mjm = mjcf.load_model_from_string(BIG_CLOTH)
+  nworld = 2
+  rng = np.random.default_rng(2)
+  qpos = np.tile(mjm.qpos0, (nworld, 1)) + rng.normal(0, 0.002, (nworld, mjm.nq))
+  qpos[:, 2::3] -= 0.03  # lower the towel into the sphere
+  qvel = rng.normal(0, 0.05, (nworld, mjm.nv))
+  ctrl = np.zeros((nworld, mjm.nu))
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=2048, nconmax=512)
+  om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=2048, nconmax=512)
+  mjw.forward(m, d)
+  od.forward()
+  torch.cuda.synchronize()
+  nv = mjm.nv
+  for w in range(nworld):
+    n = int(od.nefc[w, 0])
+    assert n > 0 and int(d.nefc[w]) == n and int(od.ncon[w, 0]) > 0
+    J = od.efc_J[w].reshape(od.njmax, nv)[:n]
+    args = (J, od.efc_D[w, :n], od.efc_aref[w, :n], od.efc_type[w, :n], od.qM[w].reshape(nv, nv), od.qacc_smooth[w])
+    c_or = efc_cost(*args, od.qacc[w], fl=od.efc_frictionloss[w, :n])
+    c_gpu = efc_cost(*args, np_(d.qacc[w]), fl=od.efc_frictionloss[w, :n])
+    assert c_gpu <= c_or + 0.025 * abs(c_or), (w, c_gpu, c_or)
+  normwise_close("qacc", np_(d.qacc), od.qacc, tol=5e-3)
+  m2, d2 = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=2048, nconmax=512)
+  om2, od2 = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=2048, nconmax=512)
+  for _ in range(3):
+    mjw.step(m2, d2)
+    od2.step()
+  torch.cuda.synchronize()
+  normwise_close("qpos", np_(d2.qpos), od2.qpos)
+  normwise_close("qvel", np_(d2.qvel), od2.qvel, tol=5e-3)

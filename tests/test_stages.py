@@ -331,9 +331,19 @@ def test_gpu_set_const_0_reproduces_put_model(model):
   want = {f: np_(getattr(m, f))[0] for f in fields}
   want_mi = float(np_(m.stat.meaninertia).reshape(-1)[0])
   q = d.qpos.clone()
+  mjw.forward(m, d)
+  before = {k: getattr(d, k).clone() for k in ("nacon", "nefc")}
+  J0 = d.efc.J.clone()
+  len0 = np.asarray(getattr(mjm, "tendon_length0", np.zeros(0)), dtype=np.float64)
   mjw.set_const_0(m, d)
   torch.cuda.synchronize()
   assert torch.equal(d.qpos, q)
+  # the contact pool and the constraint rows are the forward's, not the qpos0 position stage's
+  for k, v in before.items():
+    assert torch.equal(getattr(d, k), v), k
+  assert torch.equal(d.efc.J, J0)
+  if len0.size:  # io.py:2263: tendon_length0 = ten_length at qpos0, per world
+    np.testing.assert_allclose(np_(m.tendon_length0).reshape(2, -1), np.tile(len0, (2, 1)), rtol=1e-5, atol=1e-6)
   np.testing.assert_allclose(np_(m.stat.meaninertia), want_mi, rtol=1e-5)
   for f, w in want.items():
     got = np_(getattr(m, f))
