@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 25
+#define MJW_ABI_VERSION 26
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -46,7 +46,7 @@
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
   X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)             \
-  X(nsensorcollision)
+  X(nsensorcollision) X(nhfield) X(nhfielddata)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -78,7 +78,7 @@
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)                                \
   X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)                              \
-  X(mesh_vert, nmeshvert * 3)                                                                      \
+  X(mesh_vert, nmeshvert * 3) X(hfield_size, nhfield * 4) X(hfield_data, nhfielddata)             \
   X(tendon_stiffness, ntendon) X(tendon_damping, ntendon) X(tendon_frictionloss, ntendon)          \
   X(tendon_armature, ntendon) X(tendon_margin, ntendon) X(tendon_range, ntendon * 2)               \
   X(tendon_lengthspring, ntendon * 2) X(tendon_solref_lim, ntendon * 2) X(tendon_solimp_lim, ntendon * 5) \
@@ -119,6 +119,7 @@
   X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata) X(flex_elemedge, nflexelem * 3)      \
   X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)                                     \
   X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)                            \
+  X(hfield_nrow, nhfield) X(hfield_ncol, nhfield) X(hfield_adr, nhfield)                          \
   X(tendon_adr, ntendon) X(tendon_num, ntendon) X(tendon_limited, ntendon) X(tendon_actfrclimited, ntendon) \
   X(wrap_objid, nwrap) X(wrap_type, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)
 
@@ -148,7 +149,7 @@
   X(cfrc_ext, nbody * 6)                                                                           \
   X(efc_J, njmax_pad * nv_pad) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax_pad)         \
   X(efc_vel, njmax) X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax)             \
-  X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 20)                                 \
+  X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 32)                                 \
   X(qpos_t0, nq) X(qvel_t0, nv) X(act_t0, na) X(qvel_rk, nv) X(qacc_rk, nv) X(act_dot_rk, na)     \
   X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
   X(flexedge_J, nflexedge * 6) X(flex_frc, nflexelem * 9 + nflexedge * 12)                        \

@@ -23,19 +23,25 @@ constexpr unsigned CCD_FACE_INVALID = 0x40000000u;
 
 // one geom in the workspace: pos[3] rot[9] size[3] margin type mesh_vertadr mesh_vertnum
 constexpr int CGEOM_WORDS = 19;
-// per-pair result record in HBM (d.ccd_out): count, normal[3], then per point (dist, pos[3]) x 4.  The
-// convex pairs (GJK / EPA / box multi-contact) give every point the pair's distance; the multi-point
-// primitives the pre-passes also run (plane-cylinder, plane-mesh) give each point its own.
-constexpr int CCD_OUT = 20;
+// per-pair result record in HBM (d.ccd_out): count, normal[3], then per point (dist, pos[3]) x 4, then per
+// point normal[3] x 4 (words 20-31).  The convex pairs (GJK / EPA / box multi-contact) give every point the
+// pair's distance and normal; the multi-point primitives the pre-passes also run (plane-cylinder,
+// plane-mesh) give each point its own distance, and heightfield pairs each point its own distance and normal.
+constexpr int CCD_OUT = 32;
+// heightfield pairs (collision_convex.py:158-697): at most mjMAXCONPAIR prism contacts per pair
+constexpr int HF_MAXCON = 50;
+// heightfield scratch: the prism (6 x 3), then per prism contact dist, pos[3], normal[3]
+constexpr int HF_WORDS = 18 + 7 * HF_MAXCON;
 
 // LDS workspace layout (offsets in words) for epa_iterations = it
 struct CcdLay {
   int vert, vidx, face, pr, norm2, horizon, simplex, sidx, coords, nrm, idx, endvert, f1, f2, pn, pd, poly, clip, w1, w2;
-  int geoms, out;
+  int geoms, out, hf;
   int cap_vert, cap_face, total;
 };
 
-__host__ __device__ inline CcdLay ccd_layout(int it) {
+// hf: reserve the heightfield scratch (models with heightfield geoms)
+__host__ __device__ inline CcdLay ccd_layout(int it, bool hf = false) {
   CcdLay L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += n; return r; };
@@ -48,7 +54,8 @@ __host__ __device__ inline CcdLay ccd_layout(int it) {
   L.nrm = take(2 * 3 * 3); L.idx = take(2 * 3); L.endvert = take(3 * 3);
   L.f1 = take(4 * 3); L.f2 = take(4 * 3); L.pn = take(8 * 3); L.pd = take(8);
   L.poly = take(16 * 3); L.clip = take(16 * 3); L.w1 = take(4 * 3); L.w2 = take(4 * 3);
-  L.geoms = take(2 * CGEOM_WORDS); L.out = take(16);
+  L.geoms = take(2 * CGEOM_WORDS); L.out = take(CCD_OUT);
+  L.hf = take(hf ? HF_WORDS : 0);
   L.total = o;
   return L;
 }
@@ -58,6 +65,7 @@ struct CGeom {
   int type;
   const float* mv;  // mesh vertices (geom frame), GEOM_MESH only
   int nvert;
+  const float* prism;  // GEOM_HFIELD: the 6 prism vertices (heightfield frame, LDS); pos = the prism center
 };
 
 __device__ __forceinline__ float ccd_sign(float x) { return x < 0.0f ? -1.0f : 1.0f; }  // wp.sign
@@ -68,6 +76,21 @@ __device__ __forceinline__ void rot_apply(float* r, const float* R, float x, flo
 
 // collision_gjk.py:97-190 (primitive geoms)
 __device__ __forceinline__ void ccd_support(const CGeom& g, const float* dir, float* pt, int* vidx) {
+  if (g.type == GEOM_HFIELD) {
+    // collision_gjk.py:178-187: first strict maximum over the prism's vertices, already in the
+    // heightfield frame (no pose); the index only tells the top (-3) from the bottom (-2) direction
+    *vidx = dir[2] < 0.0f ? -2 : -3;
+    float best = -CCD_FLOAT_MAX;
+    pt[0] = pt[1] = pt[2] = 0.0f;
+    for (int i = 0; i < 6; i++) {
+      const float* v = g.prism + 3 * i;
+      const float dd = v[0] * dir[0] + v[1] * dir[1] + v[2] * dir[2];
+      if (dd > best) { best = dd; pt[0] = v[0]; pt[1] = v[1]; pt[2] = v[2]; }
+    }
+    if (g.margin > 0.0f)
+      for (int i = 0; i < 3; i++) pt[i] += dir[i] * (0.5f * g.margin);
+    return;
+  }
   *vidx = -1;
   float ld[3], res[3] = {0.0f, 0.0f, 0.0f};
   for (int i = 0; i < 3; i++) ld[i] = g.rot[i] * dir[0] + g.rot[3 + i] * dir[1] + g.rot[6 + i] * dir[2];
@@ -278,6 +301,9 @@ struct GjkOut {
 // collision_gjk.py:562-685 (simplex kept in the workspace)
 __device__ __forceinline__ GjkOut gjk(const CcdWS& w, float tolerance, int iterations, const CGeom& g1, const CGeom& g2, float cutoff, int discrete) {
   GjkOut r;
+  // a zero-initialised result (warp structs are): an early exit past the cutoff reports x1 = x2 = 0, which the
+  // heightfield path caches as a (never active) prism contact at the heightfield's origin
+  for (int i = 0; i < 3; i++) r.x1[i] = r.x2[i] = 0.0f;
   const float cutoff2 = cutoff * cutoff, tol2 = tolerance * tolerance;
   const float epsilon = discrete ? 0.0f : 0.5f * tol2;
   float* coords = w.coords();
@@ -542,6 +568,23 @@ __device__ __forceinline__ int add_edge(const CcdWS& w, int n, int e1, int e2) {
   return n + 1;
 }
 
+// collision_gjk.py:2173-2186 / 914-921: the heightfield-side witness below x2 on the prism's top triangle
+// (its vertical projection when inside, else onto the plane through the nearest corner); returns -|x1 - x2|
+__device__ __forceinline__ float hfield_top_witness(const CGeom& g1, const float* x2, float* x1) {
+  const float *a = g1.prism + 9, *b = g1.prism + 12, *c = g1.prism + 15;
+  float co[3];
+  tri_affine_coord(co, a, b, c, x2);
+  if (co[0] > 0.0f && co[1] > 0.0f && co[2] > 0.0f) {
+    for (int i = 0; i < 3; i++) x1[i] = co[0] * a[i] + co[1] * b[i] + co[2] * c[i];
+  } else {
+    const float* p = co[0] > 0.0f ? a : (co[1] > 0.0f ? b : c);
+    const float dz = x2[2] - p[2];  // dot(x2 - p, n), n = +z
+    x1[0] = x2[0]; x1[1] = x2[1]; x1[2] = x2[2] - dz;
+  }
+  float dd[3] = {x1[0] - x2[0], x1[1] - x2[1], x1[2] - x2[2]};
+  return -sqrtf(dot3(dd, dd));
+}
+
 // collision_gjk.py:1201-1328 + witness :861-933; returns the face index or -1
 __device__ __forceinline__ int epa(const CcdWS& w, int nvert, int nface, float tolerance, int iterations, const CGeom& g1, const CGeom& g2, int discrete,
                    float* dist, float* x1, float* x2) {
@@ -618,6 +661,27 @@ __device__ __forceinline__ int epa(const CcdWS& w, int nvert, int nface, float t
   for (int i = 0; i < 3; i++) {
     x2[i] = w.vert(2 * f[0] + 1)[i] * c[0] + w.vert(2 * f[1] + 1)[i] * c[1] + w.vert(2 * f[2] + 1)[i] * c[2];
     x1[i] = w.vert(2 * f[0])[i] * c[0] + w.vert(2 * f[1])[i] * c[1] + w.vert(2 * f[2])[i] * c[2];
+  }
+  const int* vi = w.vidx();
+  if (g1.type == GEOM_HFIELD && (vi[2 * f[0]] != vi[2 * f[1]] || vi[2 * f[0]] != vi[2 * f[2]])) {
+    // collision_gjk.py:886-922: a face spanning the prism's top and bottom -- geom2's support point
+    // against the top triangle instead
+    float sp[3];
+    int si;
+    if (g2.type == GEOM_CAPSULE || g2.type == GEOM_SPHERE) {
+      CGeom g = g2;
+      g.margin = 0.0f;
+      g.size[0] = 0.0f;
+      ccd_support(g, x2, sp, &si);
+      for (int i = 0; i < 3; i++) x2[i] = sp[i];
+      x2[2] -= 0.5f * g2.margin + g2.size[0];
+    } else {
+      normalize3(x2);
+      ccd_support(g2, x2, sp, &si);
+      for (int i = 0; i < 3; i++) x2[i] = sp[i];
+    }
+    *dist = hfield_top_witness(g1, x2, x1);
+    return idx;
   }
   *dist = -sqrtf(norm2[idx]);
   return idx;
@@ -935,6 +999,7 @@ __device__ __forceinline__ float ccd_record_word(int lane, int nc, const float* 
   if (lane == 0) return (float)nc;
   if (nc <= 0) return 0.0f;
   if (lane < 4) return Wout[lane];
+  if (lane >= 20) return Wout[1 + (lane - 20) % 3];  // every point's normal = the pair's
   const int q = (lane - 4) >> 2, j = (lane - 4) & 3;
   return j == 0 ? Wout[0] : Wout[4 + 3 * q + j - 1];
 }
@@ -947,6 +1012,7 @@ __device__ __forceinline__ CGeom get_cgeom(const float* src, const float* mesh_v
   g.type = __float_as_int(src[16]);
   g.mv = mesh_vert ? mesh_vert + 3 * (long)__float_as_int(src[17]) : nullptr;
   g.nvert = mesh_vert ? __float_as_int(src[18]) : 0;
+  g.prism = nullptr;
   return g;
 }
 
@@ -958,8 +1024,8 @@ __device__ __forceinline__ int ccd_raw(const CcdWS& w, int epa_it, float toleran
                                        float* x1, float* x2, int* idx) {
   *idx = -1;
   // collision_gjk.py:91-94 _discrete_geoms: boxes and meshes (polytopes)
-  const int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH) && (g2.type == GEOM_BOX || g2.type == GEOM_MESH) &&
-                       g1.margin == 0.0f && g2.margin == 0.0f;
+  const int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH || g1.type == GEOM_HFIELD) &&
+                       (g2.type == GEOM_BOX || g2.type == GEOM_MESH || g2.type == GEOM_HFIELD) && g1.margin == 0.0f && g2.margin == 0.0f;
   float full1 = 0.0f, full2 = 0.0f, size1 = 0.0f, size2 = 0.0f;
   if (g1.type == GEOM_SPHERE || g1.type == GEOM_CAPSULE) { size1 = g1.size[0]; full1 = size1 + 0.5f * g1.margin; g1.margin = 0.0f; g1.size[0] = 0.0f; }
   if (g2.type == GEOM_SPHERE || g2.type == GEOM_CAPSULE) { size2 = g2.size[0]; full2 = size2 + 0.5f * g2.margin; g2.margin = 0.0f; g2.size[0] = 0.0f; }
@@ -969,6 +1035,20 @@ __device__ __forceinline__ int ccd_raw(const CcdWS& w, int epa_it, float toleran
     r = gjk(w, tolerance, gjk_it, g1, g2, cutoff, discrete);
     if (r.dist > tolerance) {  // shallow: inflate (collision_gjk.py:194-213)
       if (r.dist == CCD_FLOAT_MAX) { *dist = r.dist; st3(x1, r.x1); st3(x2, r.x2); return 1; }
+      if (g1.type == GEOM_HFIELD) {
+        // collision_gjk.py:2160-2187: a simplex touching both the prism's top and bottom
+        bool side = false;
+        for (int i = 1; i < r.dim; i++) side |= w.sidx(0)[i] != w.sidx(0)[0];
+        if (side) {
+          float sp[3];
+          int si;
+          ccd_support(g2, r.x2, sp, &si);  // geom2 still shrunk to its point / segment
+          st3(x2, sp);
+          x2[2] -= full2;
+          *dist = hfield_top_witness(g1, x2, x1);
+          return 1;
+        }
+      }
       float n[3] = {r.x2[0] - r.x1[0], r.x2[1] - r.x1[1], r.x2[2] - r.x1[2]};
       normalize3(n);
       for (int i = 0; i < 3; i++) { x1[i] = r.x1[i] + (full1 > 0.0f ? full1 * n[i] : 0.0f); x2[i] = r.x2[i] - (full2 > 0.0f ? full2 * n[i] : 0.0f); }
@@ -1035,6 +1115,170 @@ __device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, i
   for (int i = 0; i < n; i++)
     for (int k = 0; k < 3; k++) pts[3 * i + k] = 0.5f * (W1[3 * i + k] + W2[3 * i + k]);
   for (int k = 0; k < 3; k++) normal[k] = W1[k] - W2[k];
+  return n;
+}
+
+
+// ---- heightfields (collision_convex.py:55-154 _hfield_filter, 158-697 ccd_hfield_kernel) ------------
+// One heightfield-convex pair, the whole wave in lockstep: the filter, then GJK / EPA of geom2 against
+// each triangular prism of the grid cells under geom2's bounding box (the heightfield frame; the prism
+// holds the cell triangle raised by the margin and the base at -size[3]), every result cached, then up
+// to four of them kept -- the deepest, the farthest from it, the farthest from their line, and the
+// farthest from the triangle's other edges.  `rec` (LDS, CCD_OUT words) receives the record: every
+// point with its own distance and normal.  Returns the number of points.
+//   hpos / hmat: the heightfield geom's frame; hsize: hfield_size (x, y half-extents, top, base);
+//   fmargin: geom_margin sum (the filter's); margin: the contact margin (contact_params).
+__device__ __forceinline__ int hfield_pair(const CcdWS& w, int epa_it, float tolerance, int gjk_it, float fmargin, float margin,
+                                           const float* hpos, const float* hmat, const float* hsize, int nrow, int ncol,
+                                           const float* hdata, const float* gpos, const float* gmat, const float* gsize,
+                                           float grbound, int t2, const float* mv, int nvert, float* rec) {
+  rec[0] = 0.0f;
+  float dp[3] = {gpos[0] - hpos[0], gpos[1] - hpos[1], gpos[2] - hpos[2]}, pos[3], rot[9];
+  for (int i = 0; i < 3; i++) pos[i] = hmat[i] * dp[0] + hmat[3 + i] * dp[1] + hmat[6 + i] * dp[2];
+  // box-sphere tests: horizontal, up, down
+  for (int i = 0; i < 2; i++)
+    if (hsize[i] < pos[i] - grbound - fmargin || -hsize[i] > pos[i] + grbound + fmargin) return 0;
+  if (hsize[2] < pos[2] - grbound - fmargin) return 0;
+  if (-hsize[3] > pos[2] + grbound + fmargin) return 0;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) rot[3 * i + j] = hmat[i] * gmat[j] + hmat[3 + i] * gmat[3 + j] + hmat[6 + i] * gmat[6 + j];
+  CGeom g2;
+  for (int i = 0; i < 3; i++) { g2.pos[i] = pos[i]; g2.size[i] = gsize[i]; }
+  for (int i = 0; i < 9; i++) g2.rot[i] = rot[i];
+  g2.margin = 0.0f;
+  g2.type = t2;
+  g2.mv = mv;
+  g2.nvert = nvert;
+  g2.prism = nullptr;
+  // tight bounds from the support function (box-box test)
+  float ext[6], sp[3];
+  int si;
+  for (int k = 0; k < 6; k++) {
+    float dir[3] = {0.0f, 0.0f, 0.0f};
+    dir[k >> 1] = (k & 1) ? -1.0f : 1.0f;
+    ccd_support(g2, dir, sp, &si);
+    ext[k] = sp[k >> 1];
+  }
+  const float xmax = ext[0], xmin = ext[1], ymax = ext[2], ymin = ext[3], zmax = ext[4], zmin = ext[5];
+  if (xmin - fmargin > hsize[0] || xmax + fmargin < -hsize[0] || ymin - fmargin > hsize[1] || ymax + fmargin < -hsize[1] ||
+      zmin - fmargin > hsize[2] || zmax + fmargin < -hsize[3])
+    return 0;
+  // the subgrid under geom2
+  const float x_scale = 0.5f * (float)(ncol - 1) / hsize[0], y_scale = 0.5f * (float)(nrow - 1) / hsize[1];
+  const int cmin = max(0, (int)floorf((xmin + hsize[0]) * x_scale));
+  const int cmax = min(ncol - 1, (int)ceilf((xmax + hsize[0]) * x_scale));
+  const int rmin = max(0, (int)floorf((ymin + hsize[1]) * y_scale));
+  const int rmax = min(nrow - 1, (int)ceilf((ymax + hsize[1]) * y_scale));
+  const float dx = (2.0f * hsize[0]) / (float)(ncol - 1), dy = (2.0f * hsize[1]) / (float)(nrow - 1);
+  float* prism = w.W + w.L.hf;
+  float* cd = prism + 18;               // per cached contact: dist
+  float* cp = cd + HF_MAXCON;           // pos[3]
+  float* cn = cp + 3 * HF_MAXCON;       // normal[3]
+  for (int i = 0; i < 3; i++) prism[3 * i + 2] = -hsize[3];
+  g2.margin = margin;
+  CGeom g1;
+  for (int i = 0; i < 9; i++) g1.rot[i] = (i % 4 == 0) ? 1.0f : 0.0f;
+  g1.size[0] = g1.size[1] = g1.size[2] = 0.0f;
+  g1.margin = 0.0f;
+  g1.type = GEOM_HFIELD;
+  g1.mv = nullptr;
+  g1.nvert = 0;
+  g1.prism = prism;
+  auto push = [&](float x, float y, float z) {  // prism[0] = prism[1], prism[1] = prism[2], ...; new vertex 2 / 5
+    for (int i = 0; i < 3; i++) {
+      prism[i] = prism[3 + i]; prism[3 + i] = prism[6 + i];
+      prism[9 + i] = prism[12 + i]; prism[12 + i] = prism[15 + i];
+    }
+    prism[6] = x; prism[15] = x;
+    prism[7] = y; prism[16] = y;
+    prism[17] = z;
+  };
+  int count = 0, min_id = -1;
+  float min_dist = MJW_MAXVAL;
+  for (int r = rmin; r < rmax; r++) {
+    for (int i = 0; i < 2; i++)
+      push(dx * (float)cmin - hsize[0], dy * (float)(r + i) - hsize[1], hdata[(r + i) * ncol + cmin] * hsize[2] + margin);
+    for (int c = cmin + 1; c <= cmax; c++) {
+      for (int i = 0; i < 2; i++) {
+        if (count >= HF_MAXCON) continue;  // the reference reports the overflow and drops the prism
+        push(dx * (float)c - hsize[0], dy * (float)(r + i) - hsize[1], hdata[(r + i) * ncol + c] * hsize[2] + margin);
+        if (prism[11] < zmin && prism[14] < zmin && prism[17] < zmin) continue;  // prism height test
+        for (int k = 0; k < 3; k++)
+          g1.pos[k] = (prism[k] + prism[3 + k] + prism[6 + k] + prism[9 + k] + prism[12 + k] + prism[15 + k]) * (1.0f / 6.0f);
+        CGeom a = g1, b = g2;
+        float d, x1[3], x2[3];
+        int idx;
+        if (!ccd_raw(w, epa_it, tolerance, gjk_it, 0.0f, a, b, &d, x1, x2, &idx)) continue;
+        float pl[3] = {0.5f * (x1[0] + x2[0]), 0.5f * (x1[1] + x2[1]), 0.5f * (x1[2] + x2[2])};
+        float nl[3] = {x1[0] - x2[0], x1[1] - x2[1], x1[2] - x2[2]}, pg[3], ng[3];
+        normalize3(nl);  // make_frame(w1 - w2)'s first row
+        matvec3(pg, hmat, pl);
+        matvec3(ng, hmat, nl);
+        cd[count] = d;
+        for (int k = 0; k < 3; k++) { cp[3 * count + k] = pg[k] + hpos[k]; cn[3 * count + k] = ng[k]; }
+        if (d < min_dist) { min_dist = d; min_id = count; }
+        count++;
+      }
+    }
+  }
+  // contact 0: the minimum distance
+  float min_pos[3] = {MJW_MAXVAL, MJW_MAXVAL, MJW_MAXVAL}, min_nrm[3] = {MJW_MAXVAL, MJW_MAXVAL, MJW_MAXVAL};
+  if (min_id >= 0)
+    for (int k = 0; k < 3; k++) { min_pos[k] = cp[3 * min_id + k]; min_nrm[k] = cn[3 * min_id + k]; }
+  auto put = [&](int q, float d, const float* p, const float* n) {
+    rec[4 + 4 * q] = d;
+    for (int k = 0; k < 3; k++) { rec[5 + 4 * q + k] = p[k]; rec[20 + 3 * q + k] = n[k]; }
+  };
+  put(0, min_dist, min_pos, min_nrm);
+  for (int k = 0; k < 3; k++) rec[1 + k] = min_nrm[k];
+  int n = 1;
+  constexpr float MIN_DIST_TO_NEXT = 1.0e-3f;
+  // contact 1: the farthest from contact 0
+  int id1 = -1;
+  float dist1 = -MJW_MAXVAL;
+  for (int i = 0; i < count; i++) {
+    if (i == min_id) continue;
+    float t[3] = {cp[3 * i] - min_pos[0], cp[3 * i + 1] - min_pos[1], cp[3 * i + 2] - min_pos[2]};
+    const float dd = sqrtf(dot3(t, t));
+    if (dd > dist1) { id1 = i; dist1 = dd; }
+  }
+  if (!(id1 == -1 || (0.0f < dist1 && dist1 < MIN_DIST_TO_NEXT))) {
+    const float* pos1 = cp + 3 * id1;
+    put(n++, cd[id1], pos1, cn + 3 * id1);
+    // contact 2: the farthest from the line through contacts 0 and 1
+    float t[3] = {min_pos[0] - pos1[0], min_pos[1] - pos1[1], min_pos[2] - pos1[2]}, dmin1[3];
+    cross3(dmin1, min_nrm, t);
+    int id2 = -1;
+    float dist12 = -MJW_MAXVAL;
+    for (int i = 0; i < count; i++) {
+      if (i == min_id || i == id1) continue;
+      float u[3] = {cp[3 * i] - min_pos[0], cp[3 * i + 1] - min_pos[1], cp[3 * i + 2] - min_pos[2]};
+      const float dd = fabsf(dot3(u, dmin1));
+      if (dd > dist12) { id2 = i; dist12 = dd; }
+    }
+    if (!(id2 == -1 || (0.0f < dist12 && dist12 < MIN_DIST_TO_NEXT))) {
+      const float* pos2 = cp + 3 * id2;
+      put(n++, cd[id2], pos2, cn + 3 * id2);
+      // contact 3: the farthest from the triangle's other two edges
+      float a0[3] = {min_pos[0] - pos2[0], min_pos[1] - pos2[1], min_pos[2] - pos2[2]};
+      float a1[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]}, vmin2[3], v12[3];
+      cross3(vmin2, min_nrm, a0);
+      cross3(v12, min_nrm, a1);
+      int id3 = -1;
+      float dist3 = -MJW_MAXVAL;
+      for (int i = 0; i < count; i++) {
+        if (i == min_id || i == id1 || i == id2) continue;
+        const float* pi = cp + 3 * i;
+        float u[3] = {pi[0] - min_pos[0], pi[1] - min_pos[1], pi[2] - min_pos[2]};
+        float v[3] = {pos1[0] - pi[0], pos1[1] - pi[1], pos1[2] - pi[2]};
+        const float dd = fabsf(dot3(u, vmin2)) + fabsf(dot3(v, v12));
+        if (dd > dist3) { id3 = i; dist3 = dd; }
+      }
+      if (!(id3 == -1 || (0.0f < dist3 && dist3 < MIN_DIST_TO_NEXT))) put(n++, cd[id3], cp + 3 * id3, cn + 3 * id3);
+    }
+  }
+  rec[0] = (float)n;
+  for (int q = n; q < 4; q++) put(q, 0.0f, min_pos, min_nrm);
   return n;
 }
 

@@ -22,7 +22,7 @@ constexpr int CMAX = 32;  // staged contacts per collision round
 // narrowphase -- the constraint rows after a contactfilter callback edited d.contact (mjw_contact_rows)
 enum : int { ST_POS = 1, ST_VEL = 2, ST_ACT = 4, ST_ACC = 8, ST_SOLVE = 16, ST_EULER = 32, ST_NOFACTOR = 64, ST_POOL = 128 };
 enum : int { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
-enum : int { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6, GEOM_MESH = 7 };
+enum : int { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_ELLIPSOID = 4, GEOM_CYLINDER = 5, GEOM_BOX = 6, GEOM_MESH = 7 };
 enum : int { EQ_CONNECT = 0, EQ_WELD = 1, EQ_JOINT = 2, EQ_TENDON = 3 };
 enum : int { INT_EULER = 0, INT_RK4 = 1, INT_IMPLICIT = 2, INT_IMPLICITFAST = 3 };
 enum : int { GAIN_FIXED = 0, GAIN_AFFINE = 1, GAIN_MUSCLE = 2 };
@@ -211,6 +211,25 @@ __device__ __forceinline__ float dsum(float x) {
   x += dpp_src<0x142, 0xa>(x);  // row_bcast:15 into rows 1,3
   x += dpp_src<0x143, 0xc>(x);  // row_bcast:31 into rows 2,3 -> lane 63 holds the total
   return rdlane(x, 63);
+}
+
+// the sums of x over lanes 0-31 and over lanes 32-63, wave-uniform (all lanes active): dsum without its
+// last (cross-half) step, so two 32-lane sums cost one reduction
+__device__ __forceinline__ void dsum_halves(float x, float& lo, float& hi) {
+  x += dpp_src<0xb1>(x);        // quad_perm [1,0,3,2]
+  x += dpp_src<0x4e>(x);        // quad_perm [2,3,0,1]
+  x += dpp_src<0x124>(x);       // row_ror:4
+  x += dpp_src<0x128>(x);       // row_ror:8            -> row (16-lane) sums
+  x += dpp_src<0x142, 0xa>(x);  // row_bcast:15 into rows 1,3 -> lanes 31 / 63 hold the half sums
+  lo = rdlane(x, 31);
+  hi = rdlane(x, 63);
+}
+
+// the full 64-lane sums of a and b in one reduction: v_permlane32_swap leaves a's two halves in
+// lanes 0-31 and b's in lanes 32-63 of the two results (their sum pairs the halves), then dsum_halves
+__device__ __forceinline__ void dsum2(float a, float b, float& sa, float& sb) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  dsum_halves(__uint_as_float(r[0]) + __uint_as_float(r[1]), sa, sb);
 }
 
 // opt-in phase timers (build with -DMJW_PROFILE): per-phase s_memtime deltas summed over

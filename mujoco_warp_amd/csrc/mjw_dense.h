@@ -22,6 +22,12 @@
 #include "mjw_common.h"
 #include "mjw_tendon.h"
 
+// pair independent wave reductions (two 32-lane sums in one reduction, mjw_common.h dsum_halves / dsum2);
+// 0 builds the one-reduction-per-sum variant for A/B runs
+#ifndef MJW_DENSE_PAIRED
+#define MJW_DENSE_PAIRED 1
+#endif
+
 namespace mjw {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -258,8 +264,14 @@ __device__ __forceinline__ Pt ls_point(const Row& w, float alpha, float q1, floa
   row_eval(w, alpha, c, g, hh);
   Pt p;
   p.alpha = alpha;
-  p.c = dsum(c) + alpha * alpha * q2 + alpha * q1 + qg0;
-  p.g = dsum(g) + 2.0f * alpha * q2 + q1;
+#if MJW_DENSE_PAIRED
+  float sc, sg;
+  dsum2(c, g, sc, sg);
+#else
+  const float sc = dsum(c), sg = dsum(g);
+#endif
+  p.c = sc + alpha * alpha * q2 + alpha * q1 + qg0;
+  p.g = sg + 2.0f * alpha * q2 + q1;
   p.h = dsum(hh) + 2.0f * q2;
   return p;
 }
@@ -311,8 +323,14 @@ __device__ __forceinline__ Pt ls_point_e(const Row& w, const Ell& e, bool first,
   }
   Pt p;
   p.alpha = alpha;
-  p.c = dsum(c) + alpha * alpha * q2 + alpha * q1 + qg0;
-  p.g = dsum(g) + 2.0f * alpha * q2 + q1;
+#if MJW_DENSE_PAIRED
+  float sc, sg;
+  dsum2(c, g, sc, sg);
+#else
+  const float sc = dsum(c), sg = dsum(g);
+#endif
+  p.c = sc + alpha * alpha * q2 + alpha * q1 + qg0;
+  p.g = sg + 2.0f * alpha * q2 + q1;
   p.h = dsum(hh) + 2.0f * q2;
   return p;
 }
@@ -566,12 +584,20 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         vr[lane] = force;
         __syncthreads();
         qfrc_c = gemv_cols<JS>(Jl, vr, lane, nrq);
+        // update_gradient's grad (solver.py:2879-2890) here, so that the Gauss term and |grad|^2 -- both
+        // sums over the dofs -- share one reduction (dofs in lanes 0-31, replicated in 32-63)
+        grad = dof ? ma - qfrc_smooth - qfrc_c : 0.0f;
+#if MJW_DENSE_PAIRED
+        float g2;
+        dsum_halves(lo ? (ma - qfrc_smooth) * (qacc - qacc_smooth) : grad * grad, g2, grad_dot);
+        gauss = 0.5f * g2;
+#else
         gauss = 0.5f * dsum(lo ? (ma - qfrc_smooth) * (qacc - qacc_smooth) : 0.0f);
+        grad_dot = dsum(lo ? grad * grad : 0.0f);
+#endif
         cost = dsum(rc) + gauss;
       };
       auto update_gradient = [&]() {
-        grad = dof ? ma - qfrc_smooth - qfrc_c : 0.0f;
-        grad_dot = dsum(lo ? grad * grad : 0.0f);
         if (lo) vd2[c] = grad;
         if (NEWTON) {
           // H = M + J' diag(D * quadratic) J (solver.py:2896-3008): 32x32x2 MFMA over row pairs
@@ -665,8 +691,13 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         w.jv = gemv_rows<JS>(Jl, vd, lane, nvq);
         const float snorm = sqrtf(search_dot);
         const float gtol = fmaxf(tolerance * ls_tolerance * snorm * meaninertia * (float)nv, 1e-6f);
+#if MJW_DENSE_PAIRED
+        float q1, q2;
+        dsum_halves(lo ? search * (ma - qfrc_smooth) : 0.5f * search * mv, q1, q2);
+#else
         const float q1 = dsum(lo ? search * (ma - qfrc_smooth) : 0.0f);
         const float q2 = dsum(lo ? 0.5f * search * mv : 0.0f);
+#endif
         const float qg0 = gauss;
         const bool e_first = EL && w.cls == 3 && lane == e_r0 && !e_cut;
         if (EL) {
@@ -746,8 +777,13 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         update_gradient();
         float beta = 0.0f;
         if (!NEWTON) {
+#if MJW_DENSE_PAIRED
+          float num, den;
+          dsum_halves(lo ? grad * (Mgrad - prev_Mgrad) : prev_grad * prev_Mgrad, num, den);
+#else
           float num = dsum(lo ? grad * (Mgrad - prev_Mgrad) : 0.0f);
           float den = dsum(lo ? prev_grad * prev_Mgrad : 0.0f);
+#endif
           beta = fmaxf(0.0f, num / fmaxf(MJW_MINVAL, den));
         }
         search = dof ? (-Mgrad + beta * search) : 0.0f;

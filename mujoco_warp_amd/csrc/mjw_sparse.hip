@@ -834,14 +834,14 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
     const float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
     const int ccdslot = m.nxn_ccdid[item];
     if (ccdslot >= 0) {
-      // convex pair: results of the CCD pre-pass (ccd_kernel below), n contacts at one distance with
-      // frame make_frame(normal) (collision_convex.py:763-852)
+      // convex pair: results of the CCD pre-pass (ccd_kernel below), n contacts, each with its distance and
+      // frame make_frame(normal) (collision_convex.py:763-852; heightfields :495-695)
       const float* out = d.ccd_out + ((long)wid * m.nxn_ccd + ccdslot) * CCD_OUT;
       const int n = (int)out[0];
       if (m.nxn_pairid[2 * item] < -1) return 0;
       for (int k = 0; k < n; k++) {
         if (!(out[4 + 4 * k] < o.margin)) continue;
-        if (base >= 0) write_contact(m, d, wid, base + cnt, lim, o, out[4 + 4 * k], out + 5 + 4 * k, out + 1);
+        if (base >= 0) write_contact(m, d, wid, base + cnt, lim, o, out[4 + 4 * k], out + 5 + 4 * k, out + 20 + 3 * k);
         cnt++;
       }
       return cnt;
@@ -2257,7 +2257,7 @@ __global__ void __launch_bounds__(BLK, 4) forward_kernel(const mjw_model_t m, co
 __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wid = blockIdx.x, lane = (int)threadIdx.x;
-  const CcdLay CL = ccd_layout(m.ccd_epa_iterations);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0);
   float* W = smem;
   int* list = reinterpret_cast<int*>(smem + CL.total);
   const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
@@ -2279,6 +2279,22 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
       const int g1 = m.nxn_geom_pair[2 * q], g2 = m.nxn_geom_pair[2 * q + 1];
       const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
       const int md1 = t1 == GEOM_MESH ? m.geom_dataid[g1] : -1, md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
+      if (t1 == GEOM_HFIELD) {
+        // heightfield-convex pair (collision_convex.py:158-697): the record is built whole in the workspace
+        const int hid = m.geom_dataid[g1], pid = m.nxn_pairid[2 * q];
+        CcdWS cw;
+        cw.W = W;
+        cw.L = CL;
+        hfield_pair(cw, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, gmargin[g1] + gmargin[g2],
+                    pid > -1 ? MR(pair_margin)[pid] : gmargin[g1] + gmargin[g2], gx + 3 * g1, gm + 9 * g1, MR(hfield_size) + 4 * hid,
+                    m.hfield_nrow[hid], m.hfield_ncol[hid], MR(hfield_data) + m.hfield_adr[hid], gx + 3 * g2, gm + 9 * g2, gsize + 3 * g2,
+                    MR(geom_rbound)[g2], t2, md2 >= 0 ? mesh_vert + 3 * (long)m.mesh_vertadr[md2] : nullptr,
+                    md2 >= 0 ? m.mesh_vertnum[md2] : 0, W + CL.out);
+        float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[q]) * CCD_OUT;
+        if (lane < CCD_OUT) out[lane] = W[CL.out + lane];
+        __syncthreads();
+        continue;
+      }
       put_cgeom(W + CL.geoms, gx + 3 * g1, gm + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0, md1 >= 0 ? m.mesh_vertnum[md1] : 0);
       put_cgeom(W + CL.geoms + CGEOM_WORDS, gx + 3 * g2, gm + 9 * g2, gsize + 3 * g2, t2, md2 >= 0 ? m.mesh_vertadr[md2] : 0,
                 md2 >= 0 ? m.mesh_vertnum[md2] : 0);
@@ -3302,7 +3318,7 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
     hipLaunchKernelGGL(sp::forward_kernel<sp::SP_POS_A>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
     trace_launch(s, K_SP_POS);
     if (ccd) {
-      const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations).total + 64) * 4;
+      const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations, m->nhfield > 0).total + 64) * 4;
       hipLaunchKernelGGL(sp::ccd_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
       trace_launch(s, K_SP_CCD);
     }

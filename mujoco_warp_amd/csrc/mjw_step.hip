@@ -105,7 +105,7 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
   // otherwise the workspace gets its own LDS
   L.ccd = -1;
   if (ccd && m.nxn_ccd > 0) {
-    const int need = ccd_layout(m.ccd_epa_iterations).total;
+    const int need = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0).total;
     if (nofactor) L.ccd = (usz >= need) ? L.ximat : take(need);
     else L.ccd = (L.qM - L.cdof_dot >= need) ? L.cdof_dot : take(need);
   }
@@ -1272,8 +1272,6 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
           }
           if (ccd) {
             const float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[plist[k]]) * CCD_OUT;
-            float frame[9];
-            make_frame(frame, out + 1);
             int kk = 0;
             for (int q = 0; q < 4; q++) {
               if (!(bmask & (1u << q))) continue;
@@ -1281,6 +1279,8 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
               kk++;
               if (idx < rbeg || idx >= rend) continue;
               float* rec = s + L.con + (idx - rbeg) * CREC;
+              float frame[9];
+              make_frame(frame, out + 20 + 3 * q);  // each point's own normal (heightfield pairs)
               rec[0] = out[4 + 4 * q];
               rec[1] = margin - gap;
               for (int i = 0; i < 3; i++) rec[2 + i] = out[5 + 4 * q + i];
@@ -2640,10 +2640,11 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
     for (int q = 0; q < 4; q++) {
       out[4 + 4 * q] = q < n ? dist[q] : 0.0f;
       for (int i = 0; i < 3; i++) out[5 + 4 * q + i] = q < n ? pos[q][i] : 0.0f;
+      for (int i = 0; i < 3; i++) out[20 + 3 * q + i] = nrm[i];
     }
   }
   if (L.ccd < 0) return;  // no convex pair (the lockstep workspace is not allocated)
-  const CcdLay CL = ccd_layout(m.ccd_epa_iterations);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0);
   float* W = s + L.ccd;
   for (int p = 0; p < m.nxn; p++) {
     const int slot = m.nxn_ccdid[p];
@@ -2653,6 +2654,22 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
     if (prepass_prim(t1, t2)) continue;
     const bool pass = m.nxn_pairid[2 * p + 1] >= 0 || broadphase_filter(m, L, s, wid, g1, g2);
     int nc = 0;
+    if (pass && t1 == GEOM_HFIELD) {
+      // heightfield-convex pair (collision_convex.py:158-697): its record is built whole in the workspace
+      const int hid = m.geom_dataid[g1], md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
+      const int pid = m.nxn_pairid[2 * p];
+      CcdWS cw;
+      cw.W = W;
+      cw.L = CL;
+      hfield_pair(cw, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, geom_margin[g1] + geom_margin[g2],
+                  pid > -1 ? MR(pair_margin)[pid] : geom_margin[g1] + geom_margin[g2], s + L.gxpos + 3 * g1, s + L.gxmat + 9 * g1,
+                  MR(hfield_size) + 4 * hid, m.hfield_nrow[hid], m.hfield_ncol[hid], MR(hfield_data) + m.hfield_adr[hid],
+                  s + L.gxpos + 3 * g2, s + L.gxmat + 9 * g2, gsize + 3 * g2, MR(geom_rbound)[g2], t2,
+                  md2 >= 0 ? mesh_vert + 3 * (long)m.mesh_vertadr[md2] : nullptr, md2 >= 0 ? m.mesh_vertnum[md2] : 0, W + CL.out);
+      float* out = d.ccd_out + ((long)wid * m.nxn_ccd + slot) * CCD_OUT;
+      if (lane < CCD_OUT) out[lane] = W[CL.out + lane];
+      continue;
+    }
     if (pass) {
       const int md1 = t1 == GEOM_MESH ? m.geom_dataid[g1] : -1, md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
       put_cgeom(W + CL.geoms, s + L.gxpos + 3 * g1, s + L.gxmat + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0,

@@ -100,10 +100,11 @@ def _model_attr(name):
   return (None, name)
 
 
-_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.ELLIPSOID, types.GeomType.CYLINDER,
+_SUPPORTED_GEOMS = {types.GeomType.PLANE, types.GeomType.HFIELD, types.GeomType.SPHERE, types.GeomType.CAPSULE, types.GeomType.ELLIPSOID, types.GeomType.CYLINDER,
                     types.GeomType.BOX, types.GeomType.MESH}
-# every CONVEX entry of the reference table (collision_driver.py:43-77; heightfields excluded): GJK / EPA
-_CONVEX_TABLE = {(2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
+# every CONVEX entry of the reference table (collision_driver.py:43-77): GJK / EPA (heightfield pairs: per
+# grid prism, collision_convex.py:158-697)
+_CONVEX_TABLE = {(1, 2), (1, 3), (1, 4), (1, 5), (1, 6), (1, 7), (2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
 # PRIMITIVE entries (type-sorted), collision_primitive.py:1280-1300: in the forward kernel's narrowphase ...
 _PRIMITIVE_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6)}
 # ... and in the dense path's pre-pass (ccd_kernel, one pair per lane): plane-ellipsoid, plane-cylinder,
@@ -161,7 +162,7 @@ def put_model(mjm, device=None) -> types.Model:
       names = tuple(types.GeomType(x).name for x in t)
       raise NotImplementedError(f"collision between {names[0]} and {names[1]} is not supported by this build yet.")
   if mjm.opt.enableflags & EnableBit.MULTICCD and any(
-      tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) in _CONVEX_TABLE - {(6, 6)} for a, b in pairs_chk):
+      tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) in _CONVEX_TABLE - {(6, 6)} and 1 not in (int(mjm.geom_type[a]), int(mjm.geom_type[b])) for a, b in pairs_chk):
     # collision_convex.py:1130-1137: multi-contact of convex pairs other than box-box needs the mesh polygon data
     raise NotImplementedError("MULTICCD for convex pairs other than box-box (mesh multi-contact) is not supported by this build yet.")
   if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
@@ -280,6 +281,7 @@ def put_model(mjm, device=None) -> types.Model:
   ccdid = np.cumsum([k in ccd_set for k in kinds]) - 1
   m.nxn_ccdid = _i32(np.where([k in ccd_set for k in kinds], ccdid, -1) if kinds else np.zeros(0), dev)
   m.nmesh, m.nmeshvert = int(getattr(mjm, "nmesh", 0)), int(getattr(mjm, "nmeshvert", 0))
+  m.nhfield, m.nhfielddata = int(getattr(mjm, "nhfield", 0)), int(getattr(mjm, "nhfielddata", 0))
   nconvex = sum(k in _CONVEX_TABLE for k in kinds)
   nboxbox = sum(k == (6, 6) for k in kinds)
   # collision_convex.py:1127: EPA iteration cap
@@ -557,7 +559,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     actuator_length=(nu,), actuator_moment=(m.nJmom,), actuator_velocity=(nu,), actuator_force=(nu,),
     cvel=(nb, 6), cdof_dot=(nv, 6), qfrc_bias=(nv,), qfrc_spring=(nv,), qfrc_damper=(nv,), qfrc_gravcomp=(nv,), qfrc_fluid=(nv,),
     qfrc_passive=(nv,), qfrc_actuator=(nv,), qfrc_smooth=(nv,), qacc_smooth=(nv,), qfrc_constraint=(nv,),
-    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 20,),
+    cacc=(nb, 6), cfrc_int=(nb, 6), cfrc_ext=(nb, 6), sensordata=(m.nsensordata,), ccd_out=(m.nxn_ccd * 32,),
     efc_J=(m.njrow, njmax_pad) if sp else (njmax_pad, m.njrow), efc_pos=(njmax,), efc_margin=(njmax,), efc_D=(njmax_pad,), efc_vel=(njmax,),
     efc_aref=(njmax,), efc_frictionloss=(njmax,), efc_force=(njmax,), efc_Ma=(nv,),
     # RK4 workspace (forward.py:462-472 temporaries; kept resident so a step allocates nothing)

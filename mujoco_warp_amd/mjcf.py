@@ -932,6 +932,7 @@ class _Compiler:
     m.nC = nM
 
     self._load_meshes(root)
+    self._load_hfields(root)
     self._build_geoms()
     self._build_inertia()
     self._build_sites_cams_lights()
@@ -942,7 +943,6 @@ class _Compiler:
     self._build_flex()
     self._build_equality(root)
     self._build_sensors(root)
-    m.nhfield = 0
     m.body_subtreemass = self._subtreemass()
     set_const(m)
 
@@ -981,6 +981,46 @@ class _Compiler:
     m.mesh_vertadr = np.concatenate([[0], np.cumsum(m.mesh_vertnum)[:-1]]).astype(np.int32) if m.nmesh else np.zeros(0, np.int32)
     m.mesh_vert = np.concatenate([v for v, _ in self.mesh_data]) if m.nmesh else np.zeros((0, 3))
     m.nmeshvert = int(m.mesh_vertnum.sum())
+
+  def _load_hfields(self, root):
+    """<asset><hfield>: nrow x ncol elevation grid (row 0 at -y, MuJoCo's mjModel.hfield_data order), size =
+    (x half-extent, y half-extent, top, base).  `elevation` values are normalised to [0, 1] by subtracting
+    the minimum and dividing by the range when it is non-zero (MuJoCo user_hfield); without it the grid is
+    flat.  PNG / binary `file` data is not read (parity unpinned: no MuJoCo here)."""
+    m = self.m
+    self.hfield_id = {}
+    sizes, nrows, ncols, datas = [], [], [], []
+    for asset in root.findall("asset"):
+      for he in asset.findall("hfield"):
+        a = self._resolve("hfield", he, None)
+        if "file" in a:
+          raise NotImplementedError("<hfield file=...>: image / binary heightfield files are not read by this compiler")
+        nrow, ncol = int(a.get("nrow", 0)), int(a.get("ncol", 0))
+        if nrow < 2 or ncol < 2:
+          raise ValueError("<hfield> needs nrow >= 2 and ncol >= 2")
+        size = _floats(a.get("size", "0 0 0 0"), 4)
+        if min(size) <= 0:
+          raise ValueError("<hfield> size must be positive")
+        if "elevation" in a:
+          e = np.array(_floats(a["elevation"]), dtype=np.float64)
+          if e.size != nrow * ncol:
+            raise ValueError(f"<hfield> elevation has {e.size} values, nrow * ncol = {nrow * ncol}")
+          lo, hi = e.min(), e.max()
+          e = (e - lo) / (hi - lo) if hi > lo else e - lo
+        else:
+          e = np.zeros(nrow * ncol)
+        self.hfield_id[a.get("name", "")] = len(sizes)
+        sizes.append(size)
+        nrows.append(nrow)
+        ncols.append(ncol)
+        datas.append(e)
+    m.nhfield = len(sizes)
+    m.hfield_size = np.array(sizes, dtype=np.float64).reshape(-1, 4)
+    m.hfield_nrow = np.array(nrows, dtype=np.int32)
+    m.hfield_ncol = np.array(ncols, dtype=np.int32)
+    m.hfield_adr = np.concatenate([[0], np.cumsum(m.hfield_nrow * m.hfield_ncol)[:-1]]).astype(np.int32) if m.nhfield else np.zeros(0, np.int32)
+    m.hfield_data = np.concatenate(datas) if datas else np.zeros(0)
+    m.nhfielddata = int(m.hfield_data.size)
 
   def _build_flex(self):
     """mjModel flex_* tables of the flexcomps (MuJoCo user_flex.cc semantics, restated).
@@ -1121,8 +1161,10 @@ class _Compiler:
 
   def _geom(self, ga, bodyid):
     gtype = _GEOM_TYPES[ga.get("type", _GEOM_DEFAULTS["type"])]
-    if gtype in (GeomType.HFIELD, GeomType.SDF):
+    if gtype == GeomType.SDF:
       raise NotImplementedError(f"geom type {gtype.name} not supported by the MJCF compiler")
+    if gtype == GeomType.HFIELD and bodyid != 0:
+      raise NotImplementedError("heightfield geoms on moving bodies are not supported by this compiler (attach them to the worldbody)")
     # mesh geoms: the mesh file is not read (no mesh collision or mesh-derived inertia here), so
     # the geom keeps its declared frame; put_model rejects meshes that can collide and bodies
     # whose inertia would come from a mesh.
@@ -1172,6 +1214,15 @@ class _Compiler:
       vol = 0.0
       rbound = 0.0
       aabb = [0, 0, 0, size[0], size[1], 0.0]
+    elif gtype == GeomType.HFIELD:
+      if ga.get("hfield") not in self.hfield_id:
+        raise ValueError(f"geom {ga.get('name', '')}: unknown hfield '{ga.get('hfield')}'")
+      dataid = self.hfield_id[ga["hfield"]]
+      hs = self.m.hfield_size[dataid]
+      vol = 0.0
+      size = np.array([hs[0], hs[1], 0.5 * (hs[2] + hs[3])])
+      rbound = float(math.sqrt(hs[0] ** 2 + hs[1] ** 2 + max(hs[2], hs[3]) ** 2))
+      aabb = [0, 0, 0.5 * (hs[2] - hs[3]), hs[0], hs[1], 0.5 * (hs[2] + hs[3])]
     elif gtype == GeomType.MESH:
       if ga.get("mesh") not in self.mesh_id:
         raise ValueError(f"geom {ga.get('name', '')}: unknown mesh '{ga.get('mesh')}'")
@@ -1213,9 +1264,9 @@ class _Compiler:
       gap=float(ga.get("gap", 0.0)),
       rbound=rbound,
       aabb=aabb,
-      mass=mass if gtype != GeomType.PLANE else 0.0,
+      mass=mass if gtype not in (GeomType.PLANE, GeomType.HFIELD) else 0.0,
       inertia=inertia,
-      dataid=dataid if gtype == GeomType.MESH else -1,
+      dataid=dataid if gtype in (GeomType.MESH, GeomType.HFIELD) else -1,
       fluid=fluid,
       mesh_com=mesh_com if gtype == GeomType.MESH else None,
       mesh_I=mesh_I if gtype == GeomType.MESH else None,

@@ -1967,9 +1967,45 @@ static void collision(const orc_model* m, orc_data* d) {
         (*d->ncon)++;
       }
       continue;
+    } else if (t1 == GEOM_HFIELD) {
+      /* heightfield-convex pair, collision_convex.py:158-697: up to 4 points, each with its own normal */
+      ccd_geom cg2;
+      memset(&cg2, 0, sizeof(cg2));
+      cg2.type = t2;
+      memcpy(cg2.pos, p2, sizeof(cg2.pos)); memcpy(cg2.rot, r2, sizeof(cg2.rot)); memcpy(cg2.size, s2, sizeof(cg2.size));
+      cg2.vert = t2 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g2]] : NULL;
+      cg2.nvert = t2 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g2]] : 0;
+      int hid = m->geom_dataid[g1];
+      real hd[4], hp[4][3], hn[4][3], fr[9];
+      int n = hfield_pair(p1, r1, m->hfield_size + 4 * hid, m->hfield_nrow[hid], m->hfield_ncol[hid], m->hfield_data + m->hfield_adr[hid],
+                          &cg2, m->geom_rbound[g2], m->geom_margin[g1] + m->geom_margin[g2], margin, m->opt_ccd_tolerance,
+                          m->opt_ccd_iterations, m->ccd_epa_iterations, hd, hp, hn);
+      for (int k = 0; k < n; k++) {
+        if (!(hd[k] < margin) || pairid0 < -1) continue;
+        int cid = *d->ncon;
+        if (cid >= d->nconmax) { (*d->ncon)++; continue; }
+        make_frame(fr, hn[k]);
+        d->con_dist[cid] = hd[k];
+        memcpy(d->con_pos + 3 * cid, hp[k], 3 * sizeof(real));
+        memcpy(d->con_frame + 9 * cid, fr, 9 * sizeof(real));
+        d->con_includemargin[cid] = margin - gap;
+        memcpy(d->con_friction + 5 * cid, friction, 5 * sizeof(real));
+        memcpy(d->con_solref + 2 * cid, solref, 2 * sizeof(real));
+        memcpy(d->con_solreffriction + 2 * cid, solreffriction, 2 * sizeof(real));
+        memcpy(d->con_solimp + 5 * cid, solimp, 5 * sizeof(real));
+        d->con_dim[cid] = condim;
+        d->con_geom[2 * cid] = g1;
+        d->con_geom[2 * cid + 1] = g2;
+        d->con_flex[2 * cid] = d->con_flex[2 * cid + 1] = d->con_vert[2 * cid] = d->con_vert[2 * cid + 1] = -1;
+        for (int i = 0; i < 10; i++) d->con_efc_address[10 * cid + i] = -1;
+        (*d->ncon)++;
+      }
+      continue;
     } else if (convex_pair(t1, t2)) {
       /* convex (GJK/EPA) pair, collision_convex.py:701-890 */
       ccd_geom cg1, cg2;
+      memset(&cg1, 0, sizeof(cg1));
+      memset(&cg2, 0, sizeof(cg2));
       cg1.type = t1; cg2.type = t2;
       memcpy(cg1.pos, p1, sizeof(cg1.pos)); memcpy(cg1.rot, r1, sizeof(cg1.rot)); memcpy(cg1.size, s1, sizeof(cg1.size));
       memcpy(cg2.pos, p2, sizeof(cg2.pos)); memcpy(cg2.rot, r2, sizeof(cg2.rot)); memcpy(cg2.size, s2, sizeof(cg2.size));
@@ -3956,6 +3992,19 @@ void orc_forward(const orc_model* m, const orc_data* b, int nworld, int nthread)
 /* collision_gjk_test.py:34-265 _geom_dist: ccd(tolerance, cutoff 1e30, iterations, iterations) of two geoms
  * carrying `margin`, then (multiccd) multicontact.  out = dist, x1[3], x2[3]; returns ncon, or -1 for a
  * multi-contact request this build does not restate (mesh polygons). */
+/* collision_gjk_test.py:811-880 test_hfield_support: the support point of a heightfield prism
+ * (6 x 3 vertices) with margin `margin` along dir */
+int orc_kat_hfield_support(const real* prism, const real* dir, real margin, real* out) {
+  ccd_geom g;
+  memset(&g, 0, sizeof(g));
+  g.type = GEOM_HFIELD;
+  g.prism = prism;
+  g.margin = margin;
+  ccd_sp sp = ccd_support(&g, dir);
+  memcpy(out, sp.point, 3 * sizeof(real));
+  return sp.vertex_index;
+}
+
 int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* size, const real* mesh_vert, const int* vertadr,
                 const int* vertnum, real margin, real tolerance, int iterations, int multiccd, real* out) {
   ccd_geom g[2], h1, h2;

@@ -2,9 +2,9 @@
  * ORACLE -- TEST INFRASTRUCTURE ONLY (included by oracle.c).
  *
  * Convex collision (GJK distance, EPA penetration, box multi-contact) restated from
- * mujoco_warp/_src/collision_gjk.py and the ccd kernel of collision_convex.py:701-890, for
- * the convex pair types this build routes through CCD (box-box, the reference's default
- * collision table collision_driver.py:74).  Serial, one pair at a time.
+ * mujoco_warp/_src/collision_gjk.py and the ccd kernels of collision_convex.py:158-890 (heightfield
+ * prisms and the convex pairs of the reference's collision table, collision_driver.py:43-77).
+ * Serial, one pair at a time.
  */
 #include <stdint.h>
 
@@ -27,6 +27,7 @@ typedef struct {
   int type;
   const real* vert; /* mesh vertices in the geom frame (GEOM_MESH) */
   int nvert;
+  const real* prism; /* GEOM_HFIELD: the 6 prism vertices (heightfield frame); pos = the prism center */
 } ccd_geom;
 
 typedef struct {
@@ -39,6 +40,19 @@ static inline real ccd_sign(real x) { return x < 0 ? -1 : 1; } /* wp.sign */
 /* collision_gjk.py:97-190 support (primitive types) */
 static ccd_sp ccd_support(const ccd_geom* g, const real* dir) {
   ccd_sp sp;
+  if (g->type == GEOM_HFIELD) { /* collision_gjk.py:178-187: first strict maximum over the prism, no pose */
+    real best = -CCD_FLOAT_MAX;
+    sp.vertex_index = dir[2] < 0 ? -2 : -3;
+    sp.point[0] = sp.point[1] = sp.point[2] = 0;
+    for (int i = 0; i < 6; i++) {
+      const real* v = g->prism + 3 * i;
+      real dd = v[0] * dir[0] + v[1] * dir[1] + v[2] * dir[2];
+      if (dd > best) { best = dd; sp.point[0] = v[0]; sp.point[1] = v[1]; sp.point[2] = v[2]; }
+    }
+    if (g->margin > 0)
+      for (int i = 0; i < 3; i++) sp.point[i] += dir[i] * (0.5 * g->margin);
+    return sp;
+  }
   sp.vertex_index = -1;
   real ld[3], res[3] = {0, 0, 0};
   for (int i = 0; i < 3; i++) ld[i] = g->rot[i] * dir[0] + g->rot[3 + i] * dir[1] + g->rot[6 + i] * dir[2];
@@ -501,8 +515,27 @@ static int polytope4(polytope* pt, gjk_result* r) {
   return 0;
 }
 
-/* collision_gjk.py:861-933 (primitive geoms) */
-static real epa_witness(const polytope* pt, int fidx, real* x1, real* x2) {
+/* collision_gjk.py:2173-2186 / 914-921: the heightfield-side witness under x2 on the prism's top triangle
+ * (vertical projection inside it, else onto the horizontal plane through the nearest corner) */
+static real hfield_top_witness(const ccd_geom* g1, const real* x2, real* x1) {
+  const real *a = g1->prism + 9, *b = g1->prism + 12, *c = g1->prism + 15;
+  real co[3];
+  tri_affine_coord(co, a, b, c, x2);
+  if (co[0] > 0 && co[1] > 0 && co[2] > 0) {
+    for (int i = 0; i < 3; i++) x1[i] = co[0] * a[i] + co[1] * b[i] + co[2] * c[i];
+  } else {
+    const real* p = c;
+    if (co[1] > 0) p = b;
+    if (co[0] > 0) p = a;
+    real dz = x2[2] - p[2];
+    x1[0] = x2[0]; x1[1] = x2[1]; x1[2] = x2[2] - dz;
+  }
+  real dd[3] = {x1[0] - x2[0], x1[1] - x2[1], x1[2] - x2[2]};
+  return -sqrt(dot3(dd, dd));
+}
+
+/* collision_gjk.py:861-933 */
+static real epa_witness(const polytope* pt, int fidx, const ccd_geom* g1, const ccd_geom* g2, real* x1, real* x2) {
   int f[3];
   face_verts(pt->face[fidx], f);
   real v1[3], v2[3], v3[3], c[3];
@@ -511,6 +544,23 @@ static real epa_witness(const polytope* pt, int fidx, real* x1, real* x2) {
   for (int i = 0; i < 3; i++) {
     x2[i] = pt->vert[2 * f[0] + 1][i] * c[0] + pt->vert[2 * f[1] + 1][i] * c[1] + pt->vert[2 * f[2] + 1][i] * c[2];
     x1[i] = pt->vert[2 * f[0]][i] * c[0] + pt->vert[2 * f[1]][i] * c[1] + pt->vert[2 * f[2]][i] * c[2];
+  }
+  int i1 = pt->vert_index[2 * f[0]], i2 = pt->vert_index[2 * f[1]], i3 = pt->vert_index[2 * f[2]];
+  if (g1->type == GEOM_HFIELD && (i1 != i2 || i1 != i3)) { /* :886-922 a face across the prism's top and bottom */
+    ccd_sp sp;
+    if (g2->type == GEOM_CAPSULE || g2->type == GEOM_SPHERE) {
+      ccd_geom g = *g2;
+      g.margin = 0;
+      g.size[0] = 0;
+      sp = ccd_support(&g, x2);
+      for (int i = 0; i < 3; i++) x2[i] = sp.point[i];
+      x2[2] -= 0.5 * g2->margin + g2->size[0];
+    } else {
+      normalize3(x2);
+      sp = ccd_support(g2, x2);
+      for (int i = 0; i < 3; i++) x2[i] = sp.point[i];
+    }
+    return hfield_top_witness(g1, x2, x1);
   }
   return -sqrt(pt->face_norm2[fidx]);
 }
@@ -579,7 +629,7 @@ static int epa(real tolerance, int iterations, polytope* pt, const ccd_geom* g1,
     pt->nhorizon = 0;
   }
   if (idx > -1) {
-    *dist = epa_witness(pt, idx, x1, x2);
+    *dist = epa_witness(pt, idx, g1, g2, x1, x2);
     return idx;
   }
   *dist = 0;
@@ -868,8 +918,8 @@ static int ccd_raw(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, r
   ccd_geom g1 = *g1in, g2 = *g2in;
   *idx = -1;
   /* collision_gjk.py:91-94, 2226: boxes and meshes are discrete */
-  int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH) && (g2.type == GEOM_BOX || g2.type == GEOM_MESH) && g1.margin == 0 &&
-                 g2.margin == 0;
+  int discrete = (g1.type == GEOM_BOX || g1.type == GEOM_MESH || g1.type == GEOM_HFIELD) &&
+                 (g2.type == GEOM_BOX || g2.type == GEOM_MESH || g2.type == GEOM_HFIELD) && g1.margin == 0 && g2.margin == 0;
   real full1 = 0, full2 = 0, size1 = 0, size2 = 0;
   if (g1.type == GEOM_SPHERE || g1.type == GEOM_CAPSULE) {
     size1 = g1.size[0]; full1 = size1 + 0.5 * g1.margin; g1.margin = 0; g1.size[0] = 0;
@@ -889,6 +939,17 @@ static int ccd_raw(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, r
         memcpy(x1, r.x1, 3 * sizeof(real));
         memcpy(x2, r.x2, 3 * sizeof(real));
         return 1;
+      }
+      if (g1.type == GEOM_HFIELD) { /* collision_gjk.py:2160-2187: a simplex touching the prism's top and bottom */
+        int side = 0;
+        for (int i = 1; i < r.dim; i++) side |= r.index1[i] != r.index1[0];
+        if (side) {
+          ccd_sp sp = ccd_support(&g2, r.x2); /* geom2 still shrunk to its point / segment */
+          memcpy(x2, sp.point, 3 * sizeof(real));
+          x2[2] -= full2;
+          *dist = hfield_top_witness(&g1, x2, x1);
+          return 1;
+        }
       }
       real n[3] = {r.x2[0] - r.x1[0], r.x2[1] - r.x1[1], r.x2[2] - r.x1[2]};
       normalize3(n);
@@ -965,5 +1026,133 @@ static int ccd_pair(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, 
   for (int i = 0; i < n; i++)
     for (int k = 0; k < 3; k++) pts[i][k] = 0.5 * (w1[i][k] + w2[i][k]);
   for (int k = 0; k < 3; k++) normal[k] = w1[0][k] - w2[0][k];
+  return n;
+}
+
+/* ---- heightfields: collision_convex.py:55-154 _hfield_filter and 158-697 ccd_hfield_kernel ----
+ * One heightfield (g1, frame hpos / hmat) against a convex geom2 (world frame).  Every triangular prism
+ * of the grid cells under geom2's bounds goes through ccd() (cached: distance, world position, world
+ * normal); then contact 0 = the minimum distance, 1 = the farthest from it, 2 = the farthest from their
+ * line, 3 = the farthest from the triangle's other edges (each only while the previous one exists and lies
+ * at least 1e-3 away).  Returns the number of points written to dist / pos / nrm. */
+#define HF_MAXCON 50 /* mjMAXCONPAIR */
+static int hfield_pair(const real* hpos, const real* hmat, const real* hsize, int nrow, int ncol, const real* hdata,
+                       const ccd_geom* g2w, real grbound, real fmargin, real margin, real tolerance, int gjk_iter, int epa_iter,
+                       real dist[4], real pos[4][3], real nrm[4][3]) {
+  real dp[3] = {g2w->pos[0] - hpos[0], g2w->pos[1] - hpos[1], g2w->pos[2] - hpos[2]}, lp[3];
+  for (int i = 0; i < 3; i++) lp[i] = hmat[i] * dp[0] + hmat[3 + i] * dp[1] + hmat[6 + i] * dp[2];
+  for (int i = 0; i < 2; i++)
+    if (hsize[i] < lp[i] - grbound - fmargin || -hsize[i] > lp[i] + grbound + fmargin) return 0;
+  if (hsize[2] < lp[2] - grbound - fmargin) return 0;
+  if (-hsize[3] > lp[2] + grbound + fmargin) return 0;
+  ccd_geom g2 = *g2w;
+  memcpy(g2.pos, lp, sizeof(lp));
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) g2.rot[3 * i + j] = hmat[i] * g2w->rot[j] + hmat[3 + i] * g2w->rot[3 + j] + hmat[6 + i] * g2w->rot[6 + j];
+  g2.margin = 0;
+  real ext[6];
+  for (int k = 0; k < 6; k++) {
+    real dir[3] = {0, 0, 0};
+    dir[k >> 1] = (k & 1) ? -1 : 1;
+    ext[k] = ccd_support(&g2, dir).point[k >> 1];
+  }
+  real xmax = ext[0], xmin = ext[1], ymax = ext[2], ymin = ext[3], zmax = ext[4], zmin = ext[5];
+  if (xmin - fmargin > hsize[0] || xmax + fmargin < -hsize[0] || ymin - fmargin > hsize[1] || ymax + fmargin < -hsize[1] ||
+      zmin - fmargin > hsize[2] || zmax + fmargin < -hsize[3])
+    return 0;
+  real x_scale = 0.5 * (real)(ncol - 1) / hsize[0], y_scale = 0.5 * (real)(nrow - 1) / hsize[1];
+  int cmin = (int)floor((xmin + hsize[0]) * x_scale), cmax = (int)ceil((xmax + hsize[0]) * x_scale);
+  int rmin = (int)floor((ymin + hsize[1]) * y_scale), rmax = (int)ceil((ymax + hsize[1]) * y_scale);
+  if (cmin < 0) cmin = 0;
+  if (cmax > ncol - 1) cmax = ncol - 1;
+  if (rmin < 0) rmin = 0;
+  if (rmax > nrow - 1) rmax = nrow - 1;
+  real dx = (2 * hsize[0]) / (real)(ncol - 1), dy = (2 * hsize[1]) / (real)(nrow - 1);
+  real prism[6][3];
+  memset(prism, 0, sizeof(prism));
+  for (int i = 0; i < 3; i++) prism[i][2] = -hsize[3];
+  g2.margin = margin;
+  ccd_geom g1;
+  memset(&g1, 0, sizeof(g1));
+  for (int i = 0; i < 3; i++) g1.rot[4 * i] = 1;
+  g1.type = GEOM_HFIELD;
+  g1.prism = &prism[0][0];
+  real cd[HF_MAXCON], cp[HF_MAXCON][3], cn[HF_MAXCON][3];
+  int count = 0, min_id = -1;
+  real min_dist = 1e10; /* MJ_MAXVAL */
+  polytope* pt = ccd_polytope();
+  for (int r = rmin; r < rmax; r++) {
+    for (int c = cmin; c <= cmax; c++) {
+      for (int i = 0; i < 2; i++) {
+        if (c > cmin && count >= HF_MAXCON) continue; /* overflow: the reference drops the prism */
+        memmove(prism[0], prism[1], 2 * sizeof(prism[0]));
+        memmove(prism[3], prism[4], 2 * sizeof(prism[0]));
+        real x = dx * (real)c - hsize[0], y = dy * (real)(r + i) - hsize[1];
+        prism[2][0] = prism[5][0] = x;
+        prism[2][1] = prism[5][1] = y;
+        prism[5][2] = hdata[(r + i) * ncol + c] * hsize[2] + margin;
+        if (c == cmin) continue; /* the first column only seeds the prism */
+        if (prism[3][2] < zmin && prism[4][2] < zmin && prism[5][2] < zmin) continue;
+        for (int k = 0; k < 3; k++)
+          g1.pos[k] = (prism[0][k] + prism[1][k] + prism[2][k] + prism[3][k] + prism[4][k] + prism[5][k]) * (1.0 / 6.0);
+        real d, x1[3], x2[3];
+        int idx;
+        ccd_geom h1, h2;
+        if (!ccd_raw(&g1, &g2, tolerance, 0, gjk_iter, epa_iter, pt, &d, x1, x2, &idx, &h1, &h2)) continue;
+        real pl[3] = {0.5 * (x1[0] + x2[0]), 0.5 * (x1[1] + x2[1]), 0.5 * (x1[2] + x2[2])};
+        real nl[3] = {x1[0] - x2[0], x1[1] - x2[1], x1[2] - x2[2]};
+        normalize3(nl);
+        cd[count] = d;
+        for (int k = 0; k < 3; k++) {
+          cp[count][k] = hmat[3 * k] * pl[0] + hmat[3 * k + 1] * pl[1] + hmat[3 * k + 2] * pl[2] + hpos[k];
+          cn[count][k] = hmat[3 * k] * nl[0] + hmat[3 * k + 1] * nl[1] + hmat[3 * k + 2] * nl[2];
+        }
+        if (d < min_dist) { min_dist = d; min_id = count; }
+        count++;
+      }
+    }
+  }
+  real mpos[3] = {1e10, 1e10, 1e10}, mnrm[3] = {1e10, 1e10, 1e10};
+  if (min_id >= 0) { memcpy(mpos, cp[min_id], sizeof(mpos)); memcpy(mnrm, cn[min_id], sizeof(mnrm)); }
+  int n = 0;
+  dist[n] = min_dist; memcpy(pos[n], mpos, sizeof(mpos)); memcpy(nrm[n], mnrm, sizeof(mnrm)); n++;
+  const real min_next = 1.0e-3;
+  int id1 = -1;
+  real dist1 = -1e10;
+  for (int i = 0; i < count; i++) {
+    if (i == min_id) continue;
+    real t[3] = {cp[i][0] - mpos[0], cp[i][1] - mpos[1], cp[i][2] - mpos[2]};
+    real dd = sqrt(dot3(t, t));
+    if (dd > dist1) { id1 = i; dist1 = dd; }
+  }
+  if (id1 == -1 || (0 < dist1 && dist1 < min_next)) return n;
+  dist[n] = cd[id1]; memcpy(pos[n], cp[id1], sizeof(mpos)); memcpy(nrm[n], cn[id1], sizeof(mnrm)); n++;
+  real t1[3] = {mpos[0] - cp[id1][0], mpos[1] - cp[id1][1], mpos[2] - cp[id1][2]}, dmin1[3];
+  cross3(dmin1, mnrm, t1);
+  int id2 = -1;
+  real dist12 = -1e10;
+  for (int i = 0; i < count; i++) {
+    if (i == min_id || i == id1) continue;
+    real u[3] = {cp[i][0] - mpos[0], cp[i][1] - mpos[1], cp[i][2] - mpos[2]};
+    real dd = fabs(dot3(u, dmin1));
+    if (dd > dist12) { id2 = i; dist12 = dd; }
+  }
+  if (id2 == -1 || (0 < dist12 && dist12 < min_next)) return n;
+  dist[n] = cd[id2]; memcpy(pos[n], cp[id2], sizeof(mpos)); memcpy(nrm[n], cn[id2], sizeof(mnrm)); n++;
+  real a0[3] = {mpos[0] - cp[id2][0], mpos[1] - cp[id2][1], mpos[2] - cp[id2][2]};
+  real a1[3] = {cp[id1][0] - cp[id2][0], cp[id1][1] - cp[id2][1], cp[id1][2] - cp[id2][2]}, vmin2[3], v12[3];
+  cross3(vmin2, mnrm, a0);
+  cross3(v12, mnrm, a1);
+  int id3 = -1;
+  real dist3 = -1e10;
+  for (int i = 0; i < count; i++) {
+    if (i == min_id || i == id1 || i == id2) continue;
+    real u[3] = {cp[i][0] - mpos[0], cp[i][1] - mpos[1], cp[i][2] - mpos[2]};
+    real v[3] = {cp[id1][0] - cp[i][0], cp[id1][1] - cp[i][1], cp[id1][2] - cp[i][2]};
+    real dd = fabs(dot3(u, vmin2)) + fabs(dot3(v, v12));
+    if (dd > dist3) { id3 = i; dist3 = dd; }
+  }
+  if (id3 == -1 || (0 < dist3 && dist3 < min_next)) return n;
+  dist[n] = cd[id3]; memcpy(pos[n], cp[id3], sizeof(mpos)); memcpy(nrm[n], cn[id3], sizeof(mnrm)); n++;
   return n;
 }

@@ -99,8 +99,9 @@ def nxn_pairs(mjm):
   return pairs, pairid
 
 
-# convex (GJK/EPA) entries of MJ_COLLISION_TABLE without heightfields (collision_driver.py:42-76)
-CONVEX_PAIRS = {(2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
+# convex (GJK/EPA) entries of MJ_COLLISION_TABLE (collision_driver.py:42-76), heightfield pairs included
+CONVEX_PAIRS = {(1, 2), (1, 3), (1, 4), (1, 5), (1, 6), (1, 7),
+                (2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
 
 
 def ccd_epa_iterations(mjm, pairs):
@@ -139,6 +140,7 @@ class OracleModel:
       nmesh=getattr(mjm, "nmesh", 0), nmeshvert=getattr(mjm, "nmeshvert", 0),
       ntendon=getattr(mjm, "ntendon", 0), nwrap=getattr(mjm, "nwrap", 0), nJten=getattr(mjm, "nJten", 0),
       npair=getattr(mjm, "npair", 0),
+      nhfield=getattr(mjm, "nhfield", 0), nhfielddata=getattr(mjm, "nhfielddata", 0),
       # passive.py:829-851: gravity compensation / fluid switches (io.py:230, :2218-2219)
       ngravcomp=int((np.asarray(getattr(mjm, "body_gravcomp", np.zeros(mjm.nbody))) > 0).sum()),
       has_fluid=int(bool(np.any(np.asarray(o.wind) != 0) or o.density > 0 or o.viscosity > 0)),
@@ -293,6 +295,21 @@ def kat_ccd(types, pos, mat, size, margin, tolerance, iterations, multiccd, mesh
   n = f(I(t), P(pos), P(mat), P(size), P(mv), I(va), I(vn), creal(margin), creal(tolerance), ctypes.c_int(iterations),
         ctypes.c_int(int(multiccd)), P(out))
   return n, float(out[0]), out[1:4].copy(), out[4:7].copy()
+
+
+def kat_hfield_support(prism, direction, margin=0.0, real_bits=64):
+  """collision_gjk_test.py:811-880 on the oracle: (support point, vertex index) of a heightfield prism."""
+  lib = _lib(real_bits)
+  creal = ctypes.c_double if real_bits == 64 else ctypes.c_float
+  dt = np.float64 if real_bits == 64 else np.float32
+  P = lambda a: a.ctypes.data_as(ctypes.POINTER(creal))
+  pr = np.ascontiguousarray(prism, dtype=dt).reshape(-1)
+  dr = np.ascontiguousarray(direction, dtype=dt).reshape(-1)
+  out = np.zeros(3, dt)
+  f = lib.orc_kat_hfield_support
+  f.restype = ctypes.c_int
+  vi = f(P(pr), P(dr), creal(margin), P(out))
+  return out, int(vi)
 
 
 def kat_wrap(fn, args, ind=0, radius=0.0, real_bits=64):

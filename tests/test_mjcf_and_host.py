@@ -114,13 +114,14 @@ def test_batched_model_fields_accepted():
 
 def test_unsupported_features_raise():
   """Features outside this build raise NotImplementedError at put_model / the compiler, as the reference's
-  io.py:89-144 does (every collision-table pair except heightfields is supported since round 4)."""
+  io.py:89-144 does (every pair of the collision table is supported since round 4, heightfields included:
+  tests/test_hfield.py)."""
   import mujoco_warp_amd as mjw
   from mujoco_warp_amd import mjcf
 
-  with pytest.raises(NotImplementedError):  # heightfields: not compiled
+  with pytest.raises(NotImplementedError):  # heightfields on a moving body: not compiled
     mjcf.load_model_from_string('<mujoco><asset><hfield name="h" nrow="2" ncol="2" size="1 1 .1 .1"/></asset>'
-                                '<worldbody><geom type="hfield" hfield="h"/></worldbody></mujoco>')
+                                '<worldbody><body><freejoint/><geom type="hfield" hfield="h"/></body></worldbody></mujoco>')
   for flags in ("<flag override=\"enable\"/>", "<flag fwdinv=\"enable\"/>", "<flag midphase=\"disable\"/>"):
     try:
       m = mjcf.load_model_from_string(f'<mujoco><option>{flags}</option><worldbody><body><freejoint/><geom size=".1"/></body></worldbody></mujoco>')

@@ -16,12 +16,11 @@ import pytest
 from tests.common import HUMANOID, np_, random_states
 
 # out of scope: rendering / rays, inverse dynamics, islands, BVH / SAP / SDF collision
-# front ends, MuJoCo's simulation-based muscle length range, and the smooth velocity derivative, which
-# runs inside the integrator kernel (the set_const family is implemented, stages.py)
+# front ends and the broad- / narrowphase sub-stages of `collision` (one fused stage here); the set_const
+# family, set_length_range and deriv_smooth_vel are implemented (stages.py)
 OUT_OF_SCOPE = {
   "RenderContext", "create_render_context", "get_depth", "get_rgb", "get_segmentation", "render", "ray", "rays", "refit_bvh",
   "inverse", "island", "sap_broadphase", "nxn_broadphase", "primitive_narrowphase", "sdf_narrowphase",
-  "set_length_range", "deriv_smooth_vel",
 }
 
 
