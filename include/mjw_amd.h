@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 26
+#define MJW_ABI_VERSION 27
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -46,7 +46,7 @@
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
   X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)             \
-  X(nsensorcollision) X(nhfield) X(nhfielddata)
+  X(nsensorcollision) X(nsensorccd) X(nhfield) X(nhfielddata)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \

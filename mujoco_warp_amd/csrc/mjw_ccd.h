@@ -1091,7 +1091,9 @@ __device__ __forceinline__ int ccd_raw(const CcdWS& w, int epa_it, float toleran
 // (corrected by +margin), [1..3] normal (unnormalized; frame = make_frame(normal)), [4..15] up to 4
 // points.  Returns the contact count (0: not penetrating).  Only scalars and the LDS base cross the
 // call, so the CCD code does not touch the caller's register budget.
-__device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, int gjk_it, float margin, const float* mesh_vert = nullptr) {
+// cutoff > 0 (collision sensors, collision_convex.py:772-776): separated pairs are reported too
+__device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, int gjk_it, float margin, const float* mesh_vert = nullptr,
+                                       float cutoff = 0.0f) {
   CcdWS w;
   w.W = W;
   w.L = ccd_layout(epa_it);
@@ -1103,8 +1105,8 @@ __device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, i
   g2.margin = margin;
   float d, x1[3], x2[3];
   int idx;
-  if (!ccd_raw(w, epa_it, tolerance, gjk_it, 0.0f, g1, g2, &d, x1, x2, &idx)) return 0;
-  if (d >= 0.0f) return 0;
+  if (!ccd_raw(w, epa_it, tolerance, gjk_it, cutoff, g1, g2, &d, x1, x2, &idx)) return 0;
+  if (d >= 0.0f && cutoff == 0.0f) return 0;
   *dist_out = d + margin;
   int n = 1;
   float* W1 = w.W + w.L.w1;

@@ -6,13 +6,23 @@
 
 #include "mjw_common.h"
 #include "mjw_narrow.h"
+#include "mjw_ccd.h"
 
 namespace mjw {
 
 // per-world frame sources (each a per-world base pointer)
 struct Frames {
   const float *xpos, *xquat, *xmat, *xipos, *ximat, *gxpos, *gxmat, *cxpos, *cxmat, *subtree_com, *cvel;
+  const float* scc;  // convex collision-sensor records' results (dist, pos[3], normal[3]; LDS), or null
 };
+
+// type-sorted pairs of collision_driver.py:43-77's CONVEX entries without heightfields (GJK / EPA)
+__device__ __forceinline__ bool sensor_convex(int t1, int t2) {
+  if (t1 == GEOM_PLANE || t1 == GEOM_HFIELD) return false;
+  if (t2 == GEOM_MESH || t2 == GEOM_ELLIPSOID || t1 == GEOM_ELLIPSOID) return true;
+  if (t2 == GEOM_CYLINDER) return t1 == GEOM_CAPSULE || t1 == GEOM_CYLINDER;
+  return t2 == GEOM_BOX && (t1 == GEOM_CYLINDER || t1 == GEOM_BOX);
+}
 
 // site pose from the body pose (smooth.py:205-224, same operations as kinematics)
 __device__ __forceinline__ void site_pose(const mjw_model_t& m, int wid, const Frames& F, int id, float* pos, float* mat) {
@@ -350,11 +360,17 @@ __device__ __forceinline__ void coll_offer(CollBest& b, float dist, const float*
 
 // every contact collision_primitive.py writes for the type-sorted pair (g1, g2) -- inside or outside the
 // margin, as write_contact keeps sensor contacts (collision_core.py:199-213) -- offered to b
-__device__ void coll_pair(const mjw_model_t& m, int wid, const Frames& F, int g1, int g2, int pairid, bool flip, CollBest& b) {
+// (record e: convex pairs read the result the wave computed in lockstep, sensor_convex_records)
+__device__ void coll_pair(const mjw_model_t& m, int wid, const Frames& F, int g1, int g2, int pairid, bool flip, CollBest& b, int e) {
   const float* geom_size = MR(geom_size);
   const float* gmargin = MR(geom_margin);
   const float margin = pairid > -1 ? MR(pair_margin)[pairid] : gmargin[g1] + gmargin[g2];
   const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  if (sensor_convex(t1, t2)) {
+    const float* q = F.scc + 8 * e;
+    if (q[7] != 0.0f) coll_offer(b, q[0], q + 1, q + 4, flip);
+    return;
+  }
   const float* p1 = F.gxpos + 3 * g1;
   const float* p2 = F.gxpos + 3 * g2;
   const float* r1 = F.gxmat + 9 * g1;
@@ -417,6 +433,47 @@ __device__ void coll_pair(const mjw_model_t& m, int wid, const Frames& F, int g1
   for (int i = 0; i < c.n && i < 2; i++) coll_offer(b, c.dist[i], c.pos[i], c.frame[i], flip);
 }
 
+// collision_convex.py:763-852 for collision-sensor pairs (pairid[1] >= 0): GJK / EPA with an unbounded
+// cutoff (1e32), so separated pairs report their distance too; dist += margin; the first witness pair's
+// midpoint and the flipped frame's normal (frame *= -1, :849-852).  The whole wave runs each convex record
+// of the position-stage collision sensors in lockstep over the LDS workspace W (mjw_ccd.h) and stores
+// (dist, pos[3], normal[3], valid) at out + 8 * record.  Separate from the lane-per-sensor loop.
+__device__ void sensor_convex_records(const mjw_model_t& m, const Frames& F, int wid, float* W, float* out) {
+  const float* gsize = MR(geom_size);
+  const float* gmargin = MR(geom_margin);
+  const float* mesh_vert = MR(mesh_vert);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations);
+  const int lane = (int)(threadIdx.x & 63);
+  for (int k = 0; k < m.nsensor; k++) {
+    const int t = m.sensor_type[k];
+    if (t != SENS_GEOMDIST && t != SENS_GEOMNORMAL && t != SENS_GEOMFROMTO) continue;
+    const int adr = m.sensor_collision_adr[k];
+    for (int e = adr; e < adr + m.sensor_collision_num[k]; e++) {
+      const int* r = m.sensor_collision_pair + 4 * e;
+      const int g1 = r[0], g2 = r[1], t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+      if (!sensor_convex(t1, t2)) continue;
+      const int md1 = t1 == GEOM_MESH ? m.geom_dataid[g1] : -1, md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
+      put_cgeom(W + CL.geoms, F.gxpos + 3 * g1, F.gxmat + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0,
+                md1 >= 0 ? m.mesh_vertnum[md1] : 0);
+      put_cgeom(W + CL.geoms + CGEOM_WORDS, F.gxpos + 3 * g2, F.gxmat + 9 * g2, gsize + 3 * g2, t2, md2 >= 0 ? m.mesh_vertadr[md2] : 0,
+                md2 >= 0 ? m.mesh_vertnum[md2] : 0);
+      __syncthreads();
+      const float margin = r[2] > -1 ? MR(pair_margin)[r[2]] : gmargin[g1] + gmargin[g2];
+      const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, margin, mesh_vert, 1.0e32f);
+      if (lane == 0) {
+        const float* o = W + CL.out;
+        float nrm[3] = {o[1], o[2], o[3]};
+        normalize3(nrm);
+        float* q = out + 8 * e;
+        q[0] = o[0];
+        for (int i = 0; i < 3; i++) { q[1 + i] = o[4 + i]; q[4 + i] = -nrm[i]; }
+        q[7] = nc > 0 ? 1.0f : 0.0f;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // sensor.py:604-680: GEOMDIST (dim 1), GEOMNORMAL (3) or GEOMFROMTO (6) of sensor s
 __device__ void collision_sensor(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s) {
   const int t = m.sensor_type[s];
@@ -428,7 +485,7 @@ __device__ void collision_sensor(const mjw_model_t& m, const mjw_data_t& d, int 
   const int adr = m.sensor_collision_adr[s];
   for (int e = 0; e < m.sensor_collision_num[s]; e++) {
     const int* r = m.sensor_collision_pair + 4 * (adr + e);
-    coll_pair(m, wid, F, r[0], r[1], r[2], r[3] != 0, b);
+    coll_pair(m, wid, F, r[0], r[1], r[2], r[3] != 0, b, adr + e);
   }
   float v[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   int dim = 1;

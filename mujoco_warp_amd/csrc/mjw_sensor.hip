@@ -16,7 +16,7 @@
 namespace mjw {
 
 struct SLay {
-  int cacc, cfrc, cext, cvel, cinert, com, cdof, cdofdot, qvel, qacc, total;
+  int cacc, cfrc, cext, cvel, cinert, com, cdof, cdofdot, qvel, qacc, ccd, scc, total;
 };
 
 __host__ inline SLay make_slayout(const mjw_model_t& m) {
@@ -26,6 +26,12 @@ __host__ inline SLay make_slayout(const mjw_model_t& m) {
   const int nb = m.nbody, nv = m.nv;
   L.cacc = take(nb * 6); L.cfrc = take(nb * 6); L.cext = take(nb * 6); L.cvel = take(nb * 6); L.cinert = take(nb * 10);
   L.com = take(nb * 3); L.cdof = take(nv * 6); L.cdofdot = take(nv * 6); L.qvel = take(nv); L.qacc = take(nv);
+  // collision sensors on convex pairs: the lockstep GJK / EPA workspace and the per-record results
+  L.ccd = L.scc = -1;
+  if (m.nsensorccd > 0) {
+    L.ccd = take(ccd_layout(m.ccd_epa_iterations).total);
+    L.scc = take(8 * m.nsensorcollision);
+  }
   L.total = o;
   return L;
 }
@@ -222,6 +228,8 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   F.ximat = d.ximat + wb * 9; F.gxpos = d.geom_xpos + (long)wid * m.ngeom * 3; F.gxmat = d.geom_xmat + (long)wid * m.ngeom * 9;
   F.cxpos = d.cam_xpos + (long)wid * m.ncam * 3; F.cxmat = d.cam_xmat + (long)wid * m.ncam * 9;
   F.subtree_com = s + L.com; F.cvel = cvel;
+  F.scc = L.scc >= 0 ? s + L.scc : nullptr;
+  if ((stages & 1) && L.ccd >= 0) sensor_convex_records(m, F, wid, s + L.ccd, s + L.scc);
   // smooth.py:3044-3084 subtree_vel for the subtree velocity / momentum sensors (sensor.py:1383-1384)
   if (stages & 2) {
     bool sub = false;

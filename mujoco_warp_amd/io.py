@@ -282,10 +282,6 @@ def put_model(mjm, device=None) -> types.Model:
   m.nxn_ccdid = _i32(np.where([k in ccd_set for k in kinds], ccdid, -1) if kinds else np.zeros(0), dev)
   m.nmesh, m.nmeshvert = int(getattr(mjm, "nmesh", 0)), int(getattr(mjm, "nmeshvert", 0))
   m.nhfield, m.nhfielddata = int(getattr(mjm, "nhfield", 0)), int(getattr(mjm, "nhfielddata", 0))
-  nconvex = sum(k in _CONVEX_TABLE for k in kinds)
-  nboxbox = sum(k == (6, 6) for k in kinds)
-  # collision_convex.py:1127: EPA iteration cap
-  m.ccd_epa_iterations = 16 if nconvex and nboxbox == nconvex else int(getattr(mjm.opt, "ccd_iterations", 35))
   m.nlimited = len(jnt_limited_sh)
   m.nlimited_ball = len(jnt_limited_ball)
   m.neq_cw = int(np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD)).sum()) if mjm.neq else 0
@@ -296,6 +292,16 @@ def put_model(mjm, device=None) -> types.Model:
   m.nJmom = int(sum(_mom_nnz(mjm, a) for a in range(mjm.nu)))
   sc_adr, sc_num, sc_pair = _sensor_collision_pairs(mjm, pairid_all)
   m.nsensorcollision = len(sc_pair) // 4
+  sc_kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in sc_pair.reshape(-1, 4)[:, :2]]
+  m.nsensorccd = int(sum(k in _SENSOR_CONVEX for k in sc_kinds))  # convex sensor records (GJK in the sensor kernel)
+  # collision_convex.py:1127: EPA iteration cap over the convex pairs of the collision and sensor pair lists
+  geom_pairs = {tuple(sorted(map(int, p_))) for p_ in pairs} | {tuple(sorted(map(int, r_[:2]))) for r_ in sc_pair.reshape(-1, 4)}
+  gkinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in geom_pairs]
+  nconvex = sum(k in _CONVEX_TABLE for k in gkinds)
+  nboxbox = sum(k == (6, 6) for k in gkinds)
+  m.ccd_epa_iterations = 16 if nconvex and nboxbox == nconvex else int(getattr(mjm.opt, "ccd_iterations", 35))
+  if m.nsensorccd and 37 * mjm.nbody + 14 * mjm.nv + _ccd_words(m.ccd_epa_iterations) + 8 * m.nsensorcollision > 16384:
+    raise NotImplementedError("collision sensors on convex pairs: the sensor kernel's 64 KB of LDS is exceeded by this model.")
 
   # sparse path: kinematic trees as dof ranges (a tree starts at every dof without a parent dof),
   # J row width = the longest union of two dof chains (+ the 6 dofs of a flex edge)
@@ -395,11 +401,18 @@ def put_model(mjm, device=None) -> types.Model:
   return m
 
 
-# collision sensors (GEOMDIST / GEOMNORMAL / GEOMFROMTO) and the primitive pairs they can evaluate: the
-# type-sorted pairs of collision_driver.py:43-77's PRIMITIVE entries (the convex entries need the GJK
-# distance with an unbounded cutoff, collision_convex.py:772-776, which this build does not evaluate)
+# collision sensors (GEOMDIST / GEOMNORMAL / GEOMFROMTO) and the pairs they can evaluate: the type-sorted
+# pairs of collision_driver.py:43-77's PRIMITIVE entries, in the sensor kernel's primitive narrowphase ...
 _COLLISION_SENSORS = (types.SensorType.GEOMDIST, types.SensorType.GEOMNORMAL, types.SensorType.GEOMFROMTO)
-_SENSOR_PAIRS = _PRIMITIVE_PAIRS | {(0, 4), (0, 5), (2, 5)}
+# ... and the convex entries (heightfields aside), GJK / EPA with an unbounded cutoff in the sensor kernel
+_SENSOR_CONVEX = {k for k in _CONVEX_TABLE if k[0] != 1}
+_SENSOR_PAIRS = _PRIMITIVE_PAIRS | {(0, 4), (0, 5), (2, 5)} | _SENSOR_CONVEX
+
+
+def _ccd_words(it):
+  """Words of mjw_ccd.h's lockstep GJK / EPA workspace (ccd_layout, no heightfield scratch)."""
+  cv, cf = 10 + 2 * it, 6 + 5 * it
+  return cv * 4 + cf * 5 + 24 + 36 + 8 + 4 + 18 + 6 + 9 + 12 + 12 + 24 + 8 + 48 + 48 + 12 + 12 + 38 + 32
 
 
 def _sensor_collision_pairs(mjm, pairid_all):
@@ -428,7 +441,7 @@ def _sensor_collision_pairs(mjm, pairid_all):
         ta, tb = int(mjm.geom_type[a]), int(mjm.geom_type[b])
         if tuple(sorted((ta, tb))) not in _SENSOR_PAIRS:
           names = tuple(types.GeomType(x).name for x in sorted((ta, tb)))
-          raise NotImplementedError(f"collision sensor {s_}: {names[0]}-{names[1]} needs the convex (GJK distance) path, not supported by this build yet")
+          raise NotImplementedError(f"collision sensor {s_}: {names[0]}-{names[1]} (heightfield distance) is not supported by this build yet")
         flip = ta > tb or (ta == tb and a > b)
         g1, g2 = (b, a) if flip else (a, b)
         lo, hi = min(a, b), max(a, b)
@@ -476,7 +489,7 @@ DERIVED_INT_ARRAYS = {
 }
 DERIVED_SCALARS = ("act_maxnnz", "nbodytrn", "nsitetrn", "nten_spatial", "nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle", "sp_nH",
                    "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane",
-                   "nsensorcollision")
+                   "nsensorcollision", "nsensorccd")
 
 
 def derive_model_fields(mjm) -> dict:

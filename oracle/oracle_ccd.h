@@ -1006,16 +1006,24 @@ static polytope* ccd_polytope(void) {
 /* collision_convex.py:763-852 (eval_ccd_write_contact): contacts of one convex pair.  Returns the number
  * of contacts (0 when not penetrating), all at distance *dist (already corrected by +margin) with normal
  * `normal` (unnormalized; the frame is make_frame(normal)). */
+static int ccd_pair_cut(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, int gjk_iter, int epa_iter, real margin,
+                        real cutoff, real* dist_out, real* normal, real pts[4][3]);
 static int ccd_pair(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, int gjk_iter, int epa_iter, real margin,
                     real* dist_out, real* normal, real pts[4][3]) {
+  return ccd_pair_cut(g1in, g2in, tolerance, gjk_iter, epa_iter, margin, 0, dist_out, normal, pts);
+}
+
+/* cutoff > 0: collision sensors (collision_convex.py:772-776, cutoff 1e32), separated pairs reported too */
+static int ccd_pair_cut(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, int gjk_iter, int epa_iter, real margin,
+                        real cutoff, real* dist_out, real* normal, real pts[4][3]) {
   polytope* pt = ccd_polytope();
   ccd_geom g1 = *g1in, g2 = *g2in, h1, h2;
   g1.margin = margin;
   g2.margin = margin;
   real d, x1[3], x2[3];
   int idx;
-  if (!ccd_raw(&g1, &g2, tolerance, 0, gjk_iter, epa_iter, pt, &d, x1, x2, &idx, &h1, &h2)) return 0;
-  if (d >= 0) return 0;
+  if (!ccd_raw(&g1, &g2, tolerance, cutoff, gjk_iter, epa_iter, pt, &d, x1, x2, &idx, &h1, &h2)) return 0;
+  if (d >= 0 && cutoff == 0) return 0;
   d += margin;
   *dist_out = d;
   real w1[4][3], w2[4][3];

@@ -4,7 +4,7 @@
  * position / velocity / actuator force (sensor.py:222, 957, 1538-1577), joint and tendon limit position /
  * velocity / force (sensor.py:243-278, 972-1007, 1580-1615), subtree linear velocity and angular momentum
  * (smooth.py:2932-3084), potential and kinetic energy (sensor.py:2700-2940), the collision sensors distance /
- * normal / fromto over primitive geom pairs (sensor.py:604-680, 710-757) and insidesite (sensor.py:681-697,
+ * normal / fromto over primitive and convex geom pairs (sensor.py:604-680, 710-757; collision_convex.py:763-852) and insidesite (sensor.py:681-697,
  * util_misc.py:603-632).  Included by oracle.c after its sensor helpers. */
 
 enum {
@@ -45,6 +45,28 @@ static void coll_pair(const orc_model* m, const orc_data* d, int g1, int g2, int
   const real *r1 = d->geom_xmat + 9 * g1, *r2 = d->geom_xmat + 9 * g2;
   const real *s1 = m->geom_size + 3 * g1, *s2 = m->geom_size + 3 * g2;
   real n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]}, nrm[3], pos[3], dist;
+  if (convex_pair(t1, t2)) {
+    /* collision_convex.py:763-852 for a sensor pair: GJK / EPA with cutoff 1e32 (separated pairs keep their
+     * distance), dist += margin, the first point, and the frame flipped (:849-852) */
+    ccd_geom cg1, cg2;
+    memset(&cg1, 0, sizeof(cg1));
+    memset(&cg2, 0, sizeof(cg2));
+    cg1.type = t1; cg2.type = t2;
+    memcpy(cg1.pos, p1, sizeof(cg1.pos)); memcpy(cg1.rot, r1, sizeof(cg1.rot)); memcpy(cg1.size, s1, sizeof(cg1.size));
+    memcpy(cg2.pos, p2, sizeof(cg2.pos)); memcpy(cg2.rot, r2, sizeof(cg2.rot)); memcpy(cg2.size, s2, sizeof(cg2.size));
+    cg1.vert = t1 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g1]] : NULL;
+    cg1.nvert = t1 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g1]] : 0;
+    cg2.vert = t2 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g2]] : NULL;
+    cg2.nvert = t2 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g2]] : 0;
+    real cdist, cnrm[3], cpts[4][3];
+    int nc = ccd_pair_cut(&cg1, &cg2, m->opt_ccd_tolerance, m->opt_ccd_iterations, m->ccd_epa_iterations, margin, 1e32, &cdist, cnrm, cpts);
+    if (nc > 0) {
+      normalize3(cnrm);
+      for (int i = 0; i < 3; i++) cnrm[i] = -cnrm[i];
+      coll_offer(b, cdist, cpts[0], cnrm, flip);
+    }
+    return;
+  }
   contacts2 c;
   c.n = 0;
   if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {

@@ -104,9 +104,24 @@ CONVEX_PAIRS = {(1, 2), (1, 3), (1, 4), (1, 5), (1, 6), (1, 7),
                 (2, 4), (2, 7), (3, 4), (3, 5), (3, 7), (4, 4), (4, 5), (4, 6), (4, 7), (5, 5), (5, 6), (5, 7), (6, 6), (6, 7), (7, 7)}
 
 
+def _sensor_geom_pairs(mjm):
+  """The geom pairs of the collision sensors (GEOMDIST / GEOMNORMAL / GEOMFROMTO: obj geoms x ref geoms)."""
+  out = set()
+  for s_ in range(int(getattr(mjm, "nsensor", 0))):
+    if int(mjm.sensor_type[s_]) not in (39, 40, 41):
+      continue
+    sides = []
+    for ot, oid in ((mjm.sensor_objtype[s_], mjm.sensor_objid[s_]), (mjm.sensor_reftype[s_], mjm.sensor_refid[s_])):
+      sides.append(range(mjm.body_geomadr[oid], mjm.body_geomadr[oid] + mjm.body_geomnum[oid]) if int(ot) == 1 else [int(oid)])
+    out |= {tuple(sorted((int(a), int(b)))) for a in sides[0] for b in sides[1]}
+  return out
+
+
 def ccd_epa_iterations(mjm, pairs):
-  """EPA iteration cap: 16 when every convex pair is box-box, else opt.ccd_iterations (collision_convex.py:1127)."""
-  convex = [t for t in (tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in pairs) if t in CONVEX_PAIRS]
+  """EPA iteration cap: 16 when every convex pair -- of the collision and the collision-sensor pair lists --
+  is box-box, else opt.ccd_iterations (collision_convex.py:1127)."""
+  allpairs = {tuple(sorted((int(a), int(b)))) for a, b in pairs} | _sensor_geom_pairs(mjm)
+  convex = [t for t in (tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in allpairs) if t in CONVEX_PAIRS]
   nboxbox = sum(t == (6, 6) for t in convex)
   return 16 if convex and nboxbox == len(convex) else int(getattr(mjm.opt, "ccd_iterations", 35))
 

@@ -6,8 +6,11 @@ MuJoCo C at run time and store no values, so the oracle is pinned here by analyt
 surface distance, normal and nearest points; a body's distance is the minimum over its geoms; swapping
 obj and ref flips the normal and the fromto segment; a cutoff of 0 reports 0 (and a zero normal / segment)
 for separated geoms and clamps nothing for fromto; a box over a plane reports its lowest corner's height.
-`-m gpu`: the sensor kernel against the oracle on the reference's collision-sensor layouts, restricted to the
-primitive pairs this build evaluates (the convex pairs need GJK distance and are refused at put_model)."""
+Convex pairs (collision_convex.py:763-852 with the sensor cutoff 1e32: GJK distance when separated, EPA depth
+when overlapping, the frame flipped) are pinned by boxes: the gap between two aligned boxes and their facing
+points, the overlap depth of two interpenetrating ones.  `-m gpu`: the sensor kernel against the oracle on the
+reference's collision-sensor layouts (sensor_test.py:689-777), primitive and convex type sets, and on
+overlapping box pairs."""
 
 import numpy as np
 import pytest
@@ -82,14 +85,47 @@ def test_oracle_plane_box_lowest_corner():
   np.testing.assert_allclose(sd[4:7], [low[0], low[1], 0.0], atol=1e-12)  # ... to the plane
 
 
-def test_put_model_refuses_convex_collision_sensors():
+def test_put_model_refuses_heightfield_collision_sensors():
   import mujoco_warp_amd as mjw
 
-  mjm = _load("""<mujoco><worldbody><body><geom name="a" type="box" size=".1 .1 .1"/></body>
-  <body pos="0 0 1"><geom name="b" type="box" size=".1 .1 .1"/></body></worldbody>
+  mjm = _load("""<mujoco><asset><hfield name="h" nrow="2" ncol="2" size="1 1 .1 .1"/></asset><worldbody>
+  <geom name="a" type="hfield" hfield="h"/><body pos="0 0 1"><freejoint/><geom name="b" type="box" size=".1 .1 .1"/></body></worldbody>
   <sensor><distance geom1="a" geom2="b" cutoff="1"/></sensor></mujoco>""")
-  with pytest.raises(NotImplementedError, match="GJK distance"):
+  with pytest.raises(NotImplementedError, match="heightfield"):
     mjw.put_model(mjm, device="cpu")
+
+
+BOXES = """<mujoco><worldbody><body name="a"><geom name="a" type="box" size=".1 .2 .3"/></body>
+<body name="b" pos="0.02 -0.03 {z}"><freejoint/><geom name="b" type="box" size=".15 .1 .05"/></body></worldbody>
+<sensor><distance geom1="a" geom2="b" cutoff="10"/><normal geom1="a" geom2="b" cutoff="10"/>
+<fromto geom1="a" geom2="b" cutoff="10"/><distance geom1="b" geom2="a" cutoff="10"/><normal geom1="b" geom2="a" cutoff="10"/>
+<distance geom1="a" geom2="b" cutoff="0"/></sensor></mujoco>"""
+
+
+def test_put_model_accepts_convex_collision_sensors():
+  import mujoco_warp_amd as mjw
+
+  mjm = _load(BOXES.format(z=1))
+  m = mjw.put_model(mjm, device="cpu")
+  assert m.nsensorccd == 6 and m.nsensorcollision == 6
+  assert m.ccd_epa_iterations == 16  # every convex pair (the sensors') is box-box (collision_convex.py:1127)
+
+
+@pytest.mark.parametrize("z", [1.0, 0.33])
+def test_oracle_convex_sensor_boxes(z):
+  """Aligned boxes along z: separated by z - 0.35 (GJK distance), or overlapping by 0.35 - z (EPA depth); the
+  normal from a to b is +z, the fromto ends lie on the facing faces (the overlap's points on b's bottom / a's
+  top face), and swapping the geoms negates the normal."""
+  mjm = _load(BOXES.format(z=z))
+  sd = _oracle_sensors(mjm)[0]
+  gap = z - 0.35
+  np.testing.assert_allclose(sd[0], gap, atol=1e-6)
+  np.testing.assert_allclose(sd[1:4], [0, 0, 1], atol=1e-6)
+  np.testing.assert_allclose([sd[6], sd[9]], [0.3, z - 0.05] if gap > 0 else [z - 0.05, 0.3], atol=1e-6)
+  np.testing.assert_allclose(np.linalg.norm(sd[7:10] - sd[4:7]), abs(gap), atol=1e-6)
+  np.testing.assert_allclose(sd[10], gap, atol=1e-6)
+  np.testing.assert_allclose(sd[11:14], [0, 0, -1], atol=1e-6)
+  np.testing.assert_allclose(sd[14], 0.0 if gap > 0 else gap, atol=1e-6)  # cutoff 0 clamps positive distances
 
 
 # the reference's collision-sensor layout (sensor_test.py:689-777) over primitive pairs
@@ -122,6 +158,9 @@ def _layout(types_):
 
 PRIMITIVE_SETS = [("sphere", "capsule", "capsule", "sphere"), ("capsule", "sphere", "box", "capsule"), ("sphere", "sphere", "box", "cylinder"),
                   ("capsule", "capsule", "sphere", "box")]
+# sets with convex (GJK) pairs: box-box, ellipsoid / cylinder against the rest
+CONVEX_SETS = [("box", "box", "box", "box"), ("ellipsoid", "cylinder", "box", "sphere"), ("cylinder", "box", "capsule", "ellipsoid"),
+               ("box", "ellipsoid", "cylinder", "cylinder")]
 
 
 def test_oracle_layout_invariants():
@@ -137,8 +176,20 @@ def test_oracle_layout_invariants():
   assert dist[0] == 0.0 and np.all(nrm[0] == 0) and np.all(ft[0] == 0)  # cutoff 0, separated
 
 
+def test_oracle_convex_layout_invariants():
+  """The layout's invariants hold on the convex path too (GJK witness points, flipped frame)."""
+  mjm = _layout(CONVEX_SETS[1])
+  sd = _oracle_sensors(mjm)[0]
+  n = 12
+  dist, nrm, ft = sd[:n], sd[n:n + 3 * n].reshape(n, 3), sd[4 * n:4 * n + 6 * n].reshape(n, 6)
+  np.testing.assert_allclose(dist[1], dist[3], atol=1e-9)
+  np.testing.assert_allclose(nrm[1], -nrm[3], atol=1e-6)
+  np.testing.assert_allclose(np.linalg.norm(ft[1][3:] - ft[1][:3]), abs(dist[1]), atol=1e-6)
+  np.testing.assert_allclose((ft[1][3:] - ft[1][:3]) / dist[1], nrm[1], atol=1e-6)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("types_", PRIMITIVE_SETS)
+@pytest.mark.parametrize("types_", PRIMITIVE_SETS + CONVEX_SETS)
 def test_gpu_collision_sensors_match_oracle(types_):
   import torch
 
@@ -161,8 +212,40 @@ def test_gpu_collision_sensors_match_oracle(types_):
   od.forward()
   torch.cuda.synchronize()
   got, want = np_(d.sensordata), od.sensordata
-  np.testing.assert_allclose(got, want, rtol=1e-5, atol=2e-6)
+  if types_ in PRIMITIVE_SETS:
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=2e-6)
+  else:
+    # GJK distance of separated convex geoms: the distance converges to the ccd tolerance (1e-6); the witness
+    # points of smooth supports (ellipsoid, cylinder) to its square root
+    n = 12
+    np.testing.assert_allclose(got[:, :n], want[:, :n], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(got[:, n:], want[:, n:], atol=2e-3)
   assert np.abs(want[:, 1:12:2]).max() > 0.05  # cutoff-10 distances are real distances
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("z", [1.0, 0.33, 0.3])
+def test_gpu_convex_sensor_boxes(z):
+  """BOXES on the device (GJK when separated, EPA + box multi-contact's first point when overlapping),
+  turned a little per world, against the oracle."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  mjm = _load(BOXES.format(z=z))
+  nworld = 6
+  rng = np.random.default_rng(4)
+  qpos = np.tile(mjm.qpos0, (nworld, 1))
+  q = qpos[1:, 3:7] + rng.normal(0, 0.05, (nworld - 1, 4))
+  qpos[1:, 3:7] = q / np.linalg.norm(q, axis=1, keepdims=True)
+  m, d = gpu_from_state(mjm, qpos, np.zeros((nworld, mjm.nv)), np.zeros((nworld, mjm.nu)))
+  _, od = oracle_from_state(mjm, qpos, np.zeros((nworld, mjm.nv)), np.zeros((nworld, mjm.nu)))
+  mjw.forward(m, d)
+  od.forward()
+  torch.cuda.synchronize()
+  got, want = np_(d.sensordata), od.sensordata
+  np.testing.assert_allclose(got[:, [0, 10, 14]], want[:, [0, 10, 14]], atol=2e-5)
+  np.testing.assert_allclose(got, want, atol=5e-4)
 
 
 @pytest.mark.gpu
