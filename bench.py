@@ -129,7 +129,7 @@ def kernel_group(name, sparse):
     if "euler_kernel" in name:
       return "euler"
     return "forward"
-  if "dense_kernel" in name or "sensor_acc" in name:
+  if "dense_kernel" in name or "sensor_acc" in name or "sensor_coll" in name:
     return "dense"
   return "forward"
 

@@ -307,6 +307,7 @@ static __device__ unsigned long long* g_wlog = nullptr;
 enum : int {
   K_RESET = 0, K_CTRL_NOISE, K_CCD, K_SENSOR, K_RK4,
   K_SP_POS, K_SP_CCD, K_SP_COLL, K_SP_CON, K_SP_VEL, K_SP_INDEX, K_SP_SOLVE, K_SP_SOLVE_LDS, K_SP_EULER,
+  K_CCD_HF, K_SENSOR_COLL, K_SP_CCD_HF,
   K_DENSE = 32,  // + 32 * nbi + 4 * FLAGS + 2 * ELL + NEWTON  (dense_kernel<FLAGS, NEWTON, ELL, NB>, NB = 32 / 16 / 28 for nbi 0 / 1 / 2)
   K_FWD = 256,   // + 4 * STAGES + 2 * box + tendon    (mjw_kernel<STAGES, box, tendon>)
   K_END = 256 + 4 * 256

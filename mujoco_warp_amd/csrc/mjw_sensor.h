@@ -529,7 +529,9 @@ __device__ __forceinline__ bool inside_geom(const float* pos, const float* mat, 
   return false;
 }
 
-// one position- or velocity-stage sensor (sensor.py:459-706 / 1251-1373, supported types)
+// one position- or velocity-stage sensor (sensor.py:459-706 / 1251-1373, supported types); COLL: with the
+// collision sensors (their narrowphase is compiled into the models' kernel that has them only)
+template <bool COLL>
 __device__ void sensor_posvel_one(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s, const float* qpos,
                                   const float* qvel, const float* act_len, const float* act_vel, float time) {
   const int t = m.sensor_type[s], id = m.sensor_objid[s], ot = m.sensor_objtype[s];
@@ -602,7 +604,7 @@ __device__ void sensor_posvel_one(const mjw_model_t& m, const mjw_data_t& d, int
   } else if (t == SENS_SUBTREELINVEL || t == SENS_SUBTREEANGMOM) {  // sensor.py:1240-1248 (subtree_vel ran first)
     const float* src = (t == SENS_SUBTREELINVEL ? d.subtree_linvel : d.subtree_angmom) + ((long)wid * m.nbody + id) * 3;
     for (int i = 0; i < 3; i++) v[i] = src[i];
-  } else if (t == SENS_GEOMDIST || t == SENS_GEOMNORMAL || t == SENS_GEOMFROMTO) {
+  } else if (COLL && (t == SENS_GEOMDIST || t == SENS_GEOMNORMAL || t == SENS_GEOMFROMTO)) {
     collision_sensor(m, d, wid, F, s);
     return;
   } else if (t == SENS_INSIDESITE) {  // sensor.py:681-697

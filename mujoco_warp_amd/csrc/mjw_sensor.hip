@@ -36,8 +36,12 @@ __host__ inline SLay make_slayout(const mjw_model_t& m) {
   return L;
 }
 
-// stages: bit 0 position, bit 1 velocity, bit 2 acceleration sensors (+ rne_postconstraint)
-__global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L, int stages, int w0) {
+// stages: bit 0 position, bit 1 velocity, bit 2 acceleration sensors (+ rne_postconstraint).  COLL: the
+// instantiation with the collision sensors (primitive narrowphase + the lockstep GJK / EPA), launched as
+// sensor_coll_kernel for models that have them; compiled into every model's kernel they pushed it to
+// 256 VGPRs with 3.2 KB of scratch per lane (apollo's IMU-only sensor kernel 0.306 ms)
+template <bool COLL>
+__device__ __forceinline__ void sensor_body(const mjw_model_t& m, const mjw_data_t& d, const SLay& L, int stages, int w0) {
   extern __shared__ __attribute__((aligned(16))) float s[];
   const int wid = w0 + (int)blockIdx.x, lane = threadIdx.x & 63;
   if (wid >= d.nworld) return;
@@ -229,7 +233,7 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   F.cxpos = d.cam_xpos + (long)wid * m.ncam * 3; F.cxmat = d.cam_xmat + (long)wid * m.ncam * 9;
   F.subtree_com = s + L.com; F.cvel = cvel;
   F.scc = L.scc >= 0 ? s + L.scc : nullptr;
-  if ((stages & 1) && L.ccd >= 0) sensor_convex_records(m, F, wid, s + L.ccd, s + L.scc);
+  if (COLL && (stages & 1) && L.ccd >= 0) sensor_convex_records(m, F, wid, s + L.ccd, s + L.scc);
   // smooth.py:3044-3084 subtree_vel for the subtree velocity / momentum sensors (sensor.py:1383-1384)
   if (stages & 2) {
     bool sub = false;
@@ -244,7 +248,7 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   for (int k = lane; k < m.nsensor; k += LPW) {
     const int st = m.sensor_needstage[k];
     if ((st == STAGE_POS && (stages & 1)) || (st == STAGE_VEL && (stages & 2)))
-      sensor_posvel_one(m, d, wid, F, k, d.qpos + (long)wid * m.nq, s + L.qvel, d.actuator_length + (long)wid * m.nu,
+      sensor_posvel_one<COLL>(m, d, wid, F, k, d.qpos + (long)wid * m.nq, s + L.qvel, d.actuator_length + (long)wid * m.nu,
                         d.actuator_velocity + (long)wid * m.nu, time);
   }
   // acceleration sensors (sensor.py:1697-1997, supported types), lane = sensor
@@ -318,14 +322,26 @@ __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, con
   }
 }
 
+__global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L, int stages, int w0) {
+  sensor_body<false>(m, d, L, stages, w0);
+}
+__global__ void __launch_bounds__(64) sensor_coll_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L, int stages, int w0) {
+  sensor_body<true>(m, d, L, stages, w0);
+}
+
 int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages, int w0, int count) {
   if (count < 0) count = d->nworld - w0;
   if (count <= 0 || m->nsensor == 0 || (m->opt_disableflags & DSBL_SENSOR) || !stages) return 0;
   SLay L = make_slayout(*m);
   size_t lds = (size_t)L.total * 4;
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(sensor_acc_kernel, dim3(count), dim3(64), lds, s, *m, *d, L, stages, w0);
-  trace_launch(s, K_SENSOR);
+  if (m->nsensorcollision > 0) {
+    hipLaunchKernelGGL(sensor_coll_kernel, dim3(count), dim3(64), lds, s, *m, *d, L, stages, w0);
+    trace_launch(s, K_SENSOR_COLL);
+  } else {
+    hipLaunchKernelGGL(sensor_acc_kernel, dim3(count), dim3(64), lds, s, *m, *d, L, stages, w0);
+    trace_launch(s, K_SENSOR);
+  }
   return (int)hipGetLastError();
 }
 

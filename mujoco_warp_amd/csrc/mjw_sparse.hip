@@ -2254,10 +2254,11 @@ __global__ void __launch_bounds__(BLK, 4) forward_kernel(const mjw_model_t m, co
 // convex pairs 64 at a time, then runs GJK / EPA (mjw_ccd.h) on each survivor with the whole wave in
 // lockstep over an LDS workspace; mesh supports are wave-parallel vertex scans.  Results go to
 // d.ccd_out, which collide_item reads for the same (broadphase-passing) pairs.
-__global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d) {
+template <bool HF>  // HF: with the heightfield pairs (see the dense pre-pass)
+__device__ __forceinline__ void ccd_body(const mjw_model_t& m, const mjw_data_t& d) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wid = blockIdx.x, lane = (int)threadIdx.x;
-  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, HF && m.nhfield > 0);
   float* W = smem;
   int* list = reinterpret_cast<int*>(smem + CL.total);
   const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
@@ -2279,7 +2280,7 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
       const int g1 = m.nxn_geom_pair[2 * q], g2 = m.nxn_geom_pair[2 * q + 1];
       const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
       const int md1 = t1 == GEOM_MESH ? m.geom_dataid[g1] : -1, md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
-      if (t1 == GEOM_HFIELD) {
+      if (HF && t1 == GEOM_HFIELD) {
         // heightfield-convex pair (collision_convex.py:158-697): the record is built whole in the workspace
         const int hid = m.geom_dataid[g1], pid = m.nxn_pairid[2 * q];
         CcdWS cw;
@@ -2308,6 +2309,8 @@ __global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_
     }
   }
 }
+__global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d) { ccd_body<false>(m, d); }
+__global__ void __launch_bounds__(64) ccd_hf_kernel(const mjw_model_t m, const mjw_data_t d) { ccd_body<true>(m, d); }
 
 // ---------------------------------------------------------------------------------------------
 // solver.py CG (primal, pyramidal): init_context :3257-3293, iteration :3187-3254, exact
@@ -3319,8 +3322,13 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
     trace_launch(s, K_SP_POS);
     if (ccd) {
       const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations, m->nhfield > 0).total + 64) * 4;
-      hipLaunchKernelGGL(sp::ccd_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
-      trace_launch(s, K_SP_CCD);
+      if (m->nhfield > 0) {
+        hipLaunchKernelGGL(sp::ccd_hf_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
+        trace_launch(s, K_SP_CCD_HF);
+      } else {
+        hipLaunchKernelGGL(sp::ccd_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
+        trace_launch(s, K_SP_CCD);
+      }
     }
     // collision items (upper bound of ncollide_items): one LDS byte each when they fit
     const long nitem = (long)m->nxn + (long)m->nflexvert * m->nplane + (long)m->nflexelem * m->nflexcg;
