@@ -251,7 +251,7 @@ def test_gpu_convex_sensor_boxes(z):
   # polygon flips with rounding at these ties, so the device's segment is held to the sensor's invariants
   seg = got[:, 7:10] - got[:, 4:7]
   np.testing.assert_allclose(np.linalg.norm(seg, axis=1), np.abs(got[:, 0]), atol=2e-5)
-  np.testing.assert_allclose(seg / got[:, :1], got[:, 1:4], atol=1e-3)
+  np.testing.assert_allclose(seg / np.abs(got[:, :1]), got[:, 1:4], atol=1e-3)  # normal = normalize(to - from)
   if z > 0.35:
     np.testing.assert_allclose(got[:, 4:10], want[:, 4:10], atol=5e-4)
 
