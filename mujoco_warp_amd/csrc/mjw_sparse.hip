@@ -809,6 +809,19 @@ __device__ __noinline__ float nl_sphere_box(float* pos, float* nrm, const float*
   return sphere_box(pos, nrm, p1, r, p2, r2, s2);
 }
 
+__device__ __noinline__ float nl_plane_ellipsoid(float* pos, const float* n1, const float* p1, const float* p2, const float* r2,
+                                                 const float* s2) {
+  return plane_ellipsoid(pos, n1, p1, p2, r2, s2);
+}
+__device__ __noinline__ float nl_sphere_cylinder(float* pos, float* nrm, const float* p1, float r, const float* p2, const float* n2,
+                                                 float rc, float hc) {
+  return sphere_cylinder(pos, nrm, p1, r, p2, n2, rc, hc);
+}
+__device__ __noinline__ void nl_plane_cylinder_k(int k, const float* n1, const float* p1, const float* p2, const float* n2, float r,
+                                                 float h, float* dist, float* pos) {
+  plane_cylinder_k(k, n1, p1, p2, n2, r, h, dist, pos);
+}
+
 // one collision item: a geom pair, a (flex element, collidable geom) pair or a (flex vertex, plane)
 // pair.  Returns the number of contacts; writes them from pool slot `base` when base >= 0.
 __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data_t& d, int wid, int item, int base, int* npassed, int lim = 0x7fffffff,
@@ -888,12 +901,12 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
     } else if (t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {
       nl_capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
     } else if (t1 == GEOM_PLANE && t2 == GEOM_ELLIPSOID) {  // collision_primitive.py:665-733
-      c.dist[0] = plane_ellipsoid(c.pos[0], n1, p1, p2, r2, s2);
+      c.dist[0] = nl_plane_ellipsoid(c.pos[0], n1, p1, p2, r2, s2);
       make_frame(c.frame[0], n1);
       c.n = 1;
     } else if (t1 == GEOM_SPHERE && t2 == GEOM_CYLINDER) {  // collision_primitive.py:882-960
       float nrm[3];
-      c.dist[0] = sphere_cylinder(c.pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]);
+      c.dist[0] = nl_sphere_cylinder(c.pos[0], nrm, p1, s1[0], p2, n2, s2[0], s2[1]);
       make_frame(c.frame[0], nrm);
       c.n = 1;
     }
@@ -904,7 +917,7 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
         dist = plane_box_corner(k, n1, p1, p2, r2, s2, pos);
         for (int i = 0; i < 3; i++) nrm[i] = n1[i];
       } else if (ncand == 4) {
-        plane_cylinder_k(k, n1, p1, p2, n2, s2[0], s2[1], &dist, pos);
+        nl_plane_cylinder_k(k, n1, p1, p2, n2, s2[0], s2[1], &dist, pos);
         for (int i = 0; i < 3; i++) nrm[i] = n1[i];
       } else {
         dist = c.dist[k];
