@@ -13,8 +13,11 @@ namespace mjw {
 // per-world frame sources (each a per-world base pointer)
 struct Frames {
   const float *xpos, *xquat, *xmat, *xipos, *ximat, *gxpos, *gxmat, *cxpos, *cxmat, *subtree_com, *cvel;
-  const float* scc;  // convex collision-sensor records' results (dist, pos[3], normal[3]; LDS), or null
+  const float* scc;  // convex / heightfield collision-sensor records' results (SCC_WORDS each, LDS), or null
 };
+
+// a lockstep-evaluated sensor record: count, then per point (dist, pos[3], normal[3]) x 4
+constexpr int SCC_WORDS = 32;
 
 // type-sorted pairs of collision_driver.py:43-77's CONVEX entries without heightfields (GJK / EPA)
 __device__ __forceinline__ bool sensor_convex(int t1, int t2) {
@@ -366,9 +369,9 @@ __device__ void coll_pair(const mjw_model_t& m, int wid, const Frames& F, int g1
   const float* gmargin = MR(geom_margin);
   const float margin = pairid > -1 ? MR(pair_margin)[pairid] : gmargin[g1] + gmargin[g2];
   const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
-  if (sensor_convex(t1, t2)) {
-    const float* q = F.scc + 8 * e;
-    if (q[7] != 0.0f) coll_offer(b, q[0], q + 1, q + 4, flip);
+  if (sensor_convex(t1, t2) || t1 == GEOM_HFIELD) {
+    const float* q = F.scc + SCC_WORDS * e;
+    for (int i = 0; i < (int)q[0]; i++) coll_offer(b, q[1 + 7 * i], q + 2 + 7 * i, q + 5 + 7 * i, flip);
     return;
   }
   const float* p1 = F.gxpos + 3 * g1;
@@ -437,12 +440,14 @@ __device__ void coll_pair(const mjw_model_t& m, int wid, const Frames& F, int g1
 // cutoff (1e32), so separated pairs report their distance too; dist += margin; the first witness pair's
 // midpoint and the flipped frame's normal (frame *= -1, :849-852).  The whole wave runs each convex record
 // of the position-stage collision sensors in lockstep over the LDS workspace W (mjw_ccd.h) and stores
-// (dist, pos[3], normal[3], valid) at out + 8 * record.  Separate from the lane-per-sensor loop.
+// (count, dist, pos[3], normal[3]) at out + SCC_WORDS * record.  Heightfield records run the heightfield
+// routine (collision_convex.py:158-697: every kept prism contact, frames unflipped) with their contacts'
+// margins.  Separate from the lane-per-sensor loop.
 __device__ void sensor_convex_records(const mjw_model_t& m, const Frames& F, int wid, float* W, float* out) {
   const float* gsize = MR(geom_size);
   const float* gmargin = MR(geom_margin);
   const float* mesh_vert = MR(mesh_vert);
-  const CcdLay CL = ccd_layout(m.ccd_epa_iterations);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0);
   const int lane = (int)(threadIdx.x & 63);
   for (int k = 0; k < m.nsensor; k++) {
     const int t = m.sensor_type[k];
@@ -451,23 +456,45 @@ __device__ void sensor_convex_records(const mjw_model_t& m, const Frames& F, int
     for (int e = adr; e < adr + m.sensor_collision_num[k]; e++) {
       const int* r = m.sensor_collision_pair + 4 * e;
       const int g1 = r[0], g2 = r[1], t1 = m.geom_type[g1], t2 = m.geom_type[g2];
-      if (!sensor_convex(t1, t2)) continue;
+      if (!sensor_convex(t1, t2) && t1 != GEOM_HFIELD) continue;
       const int md1 = t1 == GEOM_MESH ? m.geom_dataid[g1] : -1, md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
+      const float margin = r[2] > -1 ? MR(pair_margin)[r[2]] : gmargin[g1] + gmargin[g2];
+      if (t1 == GEOM_HFIELD) {
+        const int hid = m.geom_dataid[g1];
+        CcdWS cw;
+        cw.W = W;
+        cw.L = CL;
+        const int n = hfield_pair(cw, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, gmargin[g1] + gmargin[g2],
+                                  margin, F.gxpos + 3 * g1, F.gxmat + 9 * g1, MR(hfield_size) + 4 * hid, m.hfield_nrow[hid],
+                                  m.hfield_ncol[hid], MR(hfield_data) + m.hfield_adr[hid], F.gxpos + 3 * g2, F.gxmat + 9 * g2,
+                                  gsize + 3 * g2, MR(geom_rbound)[g2], t2, md2 >= 0 ? mesh_vert + 3 * (long)m.mesh_vertadr[md2] : nullptr,
+                                  md2 >= 0 ? m.mesh_vertnum[md2] : 0, W + CL.out);
+        if (lane == 0) {
+          const float* o = W + CL.out;
+          float* q = out + SCC_WORDS * e;
+          q[0] = (float)n;
+          for (int i = 0; i < n; i++) {
+            q[1 + 7 * i] = o[4 + 4 * i];
+            for (int k = 0; k < 3; k++) { q[2 + 7 * i + k] = o[5 + 4 * i + k]; q[5 + 7 * i + k] = o[20 + 3 * i + k]; }
+          }
+        }
+        __syncthreads();
+        continue;
+      }
       put_cgeom(W + CL.geoms, F.gxpos + 3 * g1, F.gxmat + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0,
                 md1 >= 0 ? m.mesh_vertnum[md1] : 0);
       put_cgeom(W + CL.geoms + CGEOM_WORDS, F.gxpos + 3 * g2, F.gxmat + 9 * g2, gsize + 3 * g2, t2, md2 >= 0 ? m.mesh_vertadr[md2] : 0,
                 md2 >= 0 ? m.mesh_vertnum[md2] : 0);
       __syncthreads();
-      const float margin = r[2] > -1 ? MR(pair_margin)[r[2]] : gmargin[g1] + gmargin[g2];
       const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, margin, mesh_vert, 1.0e32f);
       if (lane == 0) {
         const float* o = W + CL.out;
         float nrm[3] = {o[1], o[2], o[3]};
         normalize3(nrm);
-        float* q = out + 8 * e;
-        q[0] = o[0];
-        for (int i = 0; i < 3; i++) { q[1 + i] = o[4 + i]; q[4 + i] = -nrm[i]; }
-        q[7] = nc > 0 ? 1.0f : 0.0f;
+        float* q = out + SCC_WORDS * e;
+        q[0] = nc > 0 ? 1.0f : 0.0f;
+        q[1] = o[0];
+        for (int i = 0; i < 3; i++) { q[2 + i] = o[4 + i]; q[5 + i] = -nrm[i]; }
       }
       __syncthreads();
     }

@@ -293,14 +293,14 @@ def put_model(mjm, device=None) -> types.Model:
   sc_adr, sc_num, sc_pair = _sensor_collision_pairs(mjm, pairid_all)
   m.nsensorcollision = len(sc_pair) // 4
   sc_kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in sc_pair.reshape(-1, 4)[:, :2]]
-  m.nsensorccd = int(sum(k in _SENSOR_CONVEX for k in sc_kinds))  # convex sensor records (GJK in the sensor kernel)
+  m.nsensorccd = int(sum(k in _SENSOR_CONVEX or k in _SENSOR_HFIELD for k in sc_kinds))  # records the sensor kernel runs in lockstep
   # collision_convex.py:1127: EPA iteration cap over the convex pairs of the collision and sensor pair lists
   geom_pairs = {tuple(sorted(map(int, p_))) for p_ in pairs} | {tuple(sorted(map(int, r_[:2]))) for r_ in sc_pair.reshape(-1, 4)}
   gkinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in geom_pairs]
   nconvex = sum(k in _CONVEX_TABLE for k in gkinds)
   nboxbox = sum(k == (6, 6) for k in gkinds)
   m.ccd_epa_iterations = 16 if nconvex and nboxbox == nconvex else int(getattr(mjm.opt, "ccd_iterations", 35))
-  if m.nsensorccd and 37 * mjm.nbody + 14 * mjm.nv + _ccd_words(m.ccd_epa_iterations) + 8 * m.nsensorcollision > 16384:
+  if m.nsensorccd and 37 * mjm.nbody + 14 * mjm.nv + _ccd_words(m.ccd_epa_iterations) + 368 * (m.nhfield > 0) + 32 * m.nsensorcollision > 16384:
     raise NotImplementedError("collision sensors on convex pairs: the sensor kernel's 64 KB of LDS is exceeded by this model.")
 
   # sparse path: kinematic trees as dof ranges (a tree starts at every dof without a parent dof),
@@ -406,7 +406,8 @@ def put_model(mjm, device=None) -> types.Model:
 _COLLISION_SENSORS = (types.SensorType.GEOMDIST, types.SensorType.GEOMNORMAL, types.SensorType.GEOMFROMTO)
 # ... and the convex entries (heightfields aside), GJK / EPA with an unbounded cutoff in the sensor kernel
 _SENSOR_CONVEX = {k for k in _CONVEX_TABLE if k[0] != 1}
-_SENSOR_PAIRS = _PRIMITIVE_PAIRS | {(0, 4), (0, 5), (2, 5)} | _SENSOR_CONVEX
+_SENSOR_HFIELD = {k for k in _CONVEX_TABLE if k[0] == 1}  # ... and heightfields (the prism routine)
+_SENSOR_PAIRS = _PRIMITIVE_PAIRS | {(0, 4), (0, 5), (2, 5)} | _SENSOR_CONVEX | _SENSOR_HFIELD
 
 
 def _ccd_words(it):
@@ -441,7 +442,7 @@ def _sensor_collision_pairs(mjm, pairid_all):
         ta, tb = int(mjm.geom_type[a]), int(mjm.geom_type[b])
         if tuple(sorted((ta, tb))) not in _SENSOR_PAIRS:
           names = tuple(types.GeomType(x).name for x in sorted((ta, tb)))
-          raise NotImplementedError(f"collision sensor {s_}: {names[0]}-{names[1]} (heightfield distance) is not supported by this build yet")
+          raise NotImplementedError(f"collision sensor {s_}: {names[0]}-{names[1]} is not in the collision table")
         flip = ta > tb or (ta == tb and a > b)
         g1, g2 = (b, a) if flip else (a, b)
         lo, hi = min(a, b), max(a, b)

@@ -45,6 +45,26 @@ static void coll_pair(const orc_model* m, const orc_data* d, int g1, int g2, int
   const real *r1 = d->geom_xmat + 9 * g1, *r2 = d->geom_xmat + 9 * g2;
   const real *s1 = m->geom_size + 3 * g1, *s2 = m->geom_size + 3 * g2;
   real n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]}, nrm[3], pos[3], dist;
+  if (t1 == GEOM_HFIELD) {
+    /* collision_convex.py:158-697 for a sensor pair: every kept prism contact, its own normal, unflipped */
+    ccd_geom cg2;
+    memset(&cg2, 0, sizeof(cg2));
+    cg2.type = t2;
+    memcpy(cg2.pos, p2, sizeof(cg2.pos)); memcpy(cg2.rot, r2, sizeof(cg2.rot)); memcpy(cg2.size, s2, sizeof(cg2.size));
+    cg2.vert = t2 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g2]] : NULL;
+    cg2.nvert = t2 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g2]] : 0;
+    int hid = m->geom_dataid[g1];
+    real hd[4], hp[4][3], hn[4][3];
+    int n = hfield_pair(p1, r1, m->hfield_size + 4 * hid, m->hfield_nrow[hid], m->hfield_ncol[hid], m->hfield_data + m->hfield_adr[hid],
+                        &cg2, m->geom_rbound[g2], m->geom_margin[g1] + m->geom_margin[g2], margin, m->opt_ccd_tolerance,
+                        m->opt_ccd_iterations, m->ccd_epa_iterations, hd, hp, hn);
+    for (int k = 0; k < n; k++) {
+      real fr[9];
+      make_frame(fr, hn[k]);
+      coll_offer(b, hd[k], hp[k], fr, flip);
+    }
+    return;
+  }
   if (convex_pair(t1, t2)) {
     /* collision_convex.py:763-852 for a sensor pair: GJK / EPA with cutoff 1e32 (separated pairs keep their
      * distance), dist += margin, the first point, and the frame flipped (:849-852) */

@@ -85,14 +85,31 @@ def test_oracle_plane_box_lowest_corner():
   np.testing.assert_allclose(sd[4:7], [low[0], low[1], 0.0], atol=1e-12)  # ... to the plane
 
 
-def test_put_model_refuses_heightfield_collision_sensors():
+HFSENS = """<mujoco><asset><hfield name="h" nrow="3" ncol="4" size=".6 .5 .2 .1" elevation="0 0 0 0 0 0 0 0 0 0 0 0"/></asset>
+<worldbody><geom name="hf" type="hfield" hfield="h" margin=".05"/>
+<body name="s" pos=".1 .05 {z}"><freejoint/><geom name="s" type="{kind}" size=".1 .08 .06"/></body></worldbody>
+<sensor><distance geom1="hf" geom2="s" cutoff="10"/><normal geom1="hf" geom2="s" cutoff="10"/>
+<fromto geom1="s" geom2="hf" cutoff="10"/></sensor></mujoco>"""
+
+
+@pytest.mark.parametrize("z", [0.09, 0.13, 0.5])
+def test_oracle_hfield_sensor_sphere(z):
+  """A sphere over a flat heightfield (collision_convex.py:158-697 for a sensor pair): the prism contacts'
+  smallest distance while the pair passes the heightfield filter (within the 0.05 margin); beyond it the pair
+  yields no contact and the sensor reports its cutoff.  The heightfield path reports distances of the
+  margin-inflated shapes with no correction -- the prism top raised by the margin (:399, :425) and geom2
+  inflated by half of it in support() -- so the distance is z - r - 1.5 margin."""
   import mujoco_warp_amd as mjw
 
-  mjm = _load("""<mujoco><asset><hfield name="h" nrow="2" ncol="2" size="1 1 .1 .1"/></asset><worldbody>
-  <geom name="a" type="hfield" hfield="h"/><body pos="0 0 1"><freejoint/><geom name="b" type="box" size=".1 .1 .1"/></body></worldbody>
-  <sensor><distance geom1="a" geom2="b" cutoff="1"/></sensor></mujoco>""")
-  with pytest.raises(NotImplementedError, match="heightfield"):
-    mjw.put_model(mjm, device="cpu")
+  mjm = _load(HFSENS.format(z=z, kind="sphere"))
+  assert mjw.put_model(mjm, device="cpu").nsensorccd == 3
+  sd = _oracle_sensors(mjm)[0]
+  if z < 0.2:
+    np.testing.assert_allclose(sd[0], z - 0.1 - 0.075, atol=1e-6)
+    np.testing.assert_allclose(np.abs(sd[3]), 1.0, atol=1e-6)
+    np.testing.assert_allclose(np.linalg.norm(sd[7:10] - sd[4:7]), abs(z - 0.175), atol=1e-6)
+  else:
+    assert sd[0] == 10.0 and np.all(sd[1:] == 0)
 
 
 BOXES = """<mujoco><worldbody><body name="a"><geom name="a" type="box" size=".1 .2 .3"/></body>
@@ -221,6 +238,31 @@ def test_gpu_collision_sensors_match_oracle(types_):
     np.testing.assert_allclose(got[:, :n], want[:, :n], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(got[:, n:], want[:, n:], atol=2e-3)
   assert np.abs(want[:, 1:12:2]).max() > 0.05  # cutoff-10 distances are real distances
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["sphere", "box", "capsule"])
+def test_gpu_hfield_sensors_match_oracle(kind):
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  mjm = _load(HFSENS.format(z=0.1, kind=kind))
+  nworld = 6
+  rng = np.random.default_rng(8)
+  qpos = np.tile(mjm.qpos0, (nworld, 1))
+  qpos[:, 2] = rng.uniform(0.02, 0.16, nworld)
+  q = qpos[:, 3:7] + rng.normal(0, 0.3, (nworld, 4))
+  qpos[:, 3:7] = q / np.linalg.norm(q, axis=1, keepdims=True)
+  m, d = gpu_from_state(mjm, qpos, np.zeros((nworld, mjm.nv)), np.zeros((nworld, mjm.nu)))
+  _, od = oracle_from_state(mjm, qpos, np.zeros((nworld, mjm.nv)), np.zeros((nworld, mjm.nu)))
+  mjw.forward(m, d)
+  od.forward()
+  torch.cuda.synchronize()
+  got, want = np_(d.sensordata), od.sensordata
+  np.testing.assert_allclose(got[:, 0], want[:, 0], atol=5e-5)  # the smallest prism-contact distance
+  seg = got[:, 7:10] - got[:, 4:7]
+  np.testing.assert_allclose(np.linalg.norm(seg, axis=1), np.minimum(np.abs(got[:, 0]), 10.0) * (got[:, 0] < 10), atol=5e-5)
 
 
 @pytest.mark.gpu
