@@ -21,9 +21,12 @@ transmission, velocity, rne, actuation, qfrc_smooth) and the dense kernel
 mjw::dense_kernel<7, ...> (Cholesky + M^-1, CG solve, Euler).  As in the
 reference's benchmark (benchmark.py:123-155) the step is captured once as a
 hipGraph (after the first warmup step) and replayed every step, the control noise
-launched before each replay; the timed region holds graph replays only.  After it,
-an untimed pass of --trace-steps steps runs eagerly through mjw_step_trace, which
-records a HIP event on that stream after every kernel launch and so times each kernel.
+launched before each replay; the timed region holds graph replays only.  The whole
+Data state is saved right before it; after it the state is restored and the same
+steps (same state, same control-noise indices, so bitwise the same work) run again
+eagerly through mjw_step_trace, which records a HIP event on that stream after every
+kernel launch and so times each kernel over exactly the timed window.  The record
+checks that the traced kernel sum per step is <= 1.03 x the timed ms/step.
 
 Also reported: `roofline` for the dominant kernel group -- the one with the most
 time per step (the forward kernel on the humanoid, the CG solve on the sparse path):
@@ -150,9 +153,10 @@ def parse():
   p.add_argument("--pmc", default=None, help="PMC traffic summary (default: the newest profiles/pmc_<model>_rNN.json)")
   p.add_argument("--graph", type=int, default=1, help="capture mjw.step once as a hipGraph and replay it every step "
                  "(benchmark.py:123-155: ctrl noise is launched outside the graph); 0 = launch the step eagerly")
-  p.add_argument("--trace-steps", type=int, default=10,
-                 help="untimed steps after the timed region that run eagerly with a HIP event after each kernel launch "
-                 "(mjw_step_trace): the per-kernel durations of `roofline`; every timed step is a graph replay")
+  p.add_argument("--trace-steps", type=int, default=0,
+                 help="after the timed region the Data state saved before it is restored and the first --trace-steps "
+                 "of the same timed steps (0 = all of them) run again eagerly with a HIP event after each kernel "
+                 "launch (mjw_step_trace): the per-kernel durations of `roofline`; every timed step is a graph replay")
   p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                  help="weak: --nworld worlds per rank; strong: --nworld worlds in total, split over the ranks")
   p.add_argument("--streams", type=int, default=1,
@@ -341,6 +345,28 @@ def roofline_record(tab, groups_alg, nworld, pmc, pmc_src, groups_alg_at=None):
   }
 
 
+def _tensors(obj, prefix=""):
+  """(name, tensor) of every torch tensor reachable from a Data container (Contact / Constraint nested)."""
+  import torch
+
+  for k, v in vars(obj).items():
+    if isinstance(v, torch.Tensor):
+      yield prefix + k, v
+    elif hasattr(v, "__dict__") and type(v).__name__ in ("Contact", "Constraint"):
+      yield from _tensors(v, prefix + k + ".")
+
+
+def snapshot(d):
+  """Copy of every Data tensor (state, pools, solver warmstart, the world-order histogram ...)."""
+  return {k: v.clone() for k, v in _tensors(d)}
+
+
+def restore(d, saved):
+  """Write a snapshot back in place (the captured graph keeps its pointers)."""
+  for k, v in _tensors(d):
+    v.copy_(saved[k])
+
+
 def _free_port():
   import socket
 
@@ -472,6 +498,7 @@ def main():
 
   # the timed region: K graph replays (or K eager steps when capture failed), nothing else
   nefc_t0, ncon_t0 = sizes()
+  saved = [snapshot(dk) for dk in shards]  # the state the timed window starts from (restored for the trace)
   torch.cuda.synchronize()
   if world > 1:
     dist.barrier()
@@ -483,19 +510,28 @@ def main():
   if world > 1:
     dist.barrier()
   elapsed = time.perf_counter() - t0
-  # per-kernel durations: an untimed pass of `trace_steps` eager steps right after the timed region, one
-  # HIP event after every kernel launch (mjw_step_trace); the algorithmic bytes of `roofline` use this
-  # window's own constraint / contact counts (mean of its first and last step)
-  ntrace = max(1, args.trace_steps)
-  nefc_mean, ncon_mean = sizes()
-  nefc_t1, ncon_t1 = nefc_mean, ncon_mean
+  nefc_t1, ncon_t1 = sizes()
+  qpos_all = torch.cat([dk.qpos for dk in shards])
+  qpos_timed = qpos_all.clone()
+  # per-kernel durations over the timed window itself: restore the saved state and run the first `ntrace`
+  # timed steps again eagerly with one HIP event after every kernel launch (mjw_step_trace); every world is
+  # computed by one wave from its own data, so these are the timed steps' kernels, with the same nefc /
+  # ncon, which the algorithmic bytes of `roofline` are priced at (mean over the traced steps)
+  ntrace = args.steps if args.trace_steps <= 0 else min(args.trace_steps, args.steps)
+  for dk, sv in zip(shards, saved):
+    restore(dk, sv)
+  del saved
+  acc = torch.zeros(2, dtype=torch.float64, device=dev)
   for i in range(ntrace):
-    one_step(args.warmup + args.steps + i, traced=True)
+    one_step(args.warmup + i, traced=True)
+    acc[0] += shards[0].nefc.sum()
+    acc[1] += shards[0].nacon[0]
   torch.cuda.synchronize()
   tab = kernel_table(tracer.durations(), bool(m.is_sparse))
-  n2, c2 = sizes()
-  nefc_mean, ncon_mean = 0.5 * (nefc_mean + n2), 0.5 * (ncon_mean + c2)
-  qpos_all = torch.cat([dk.qpos for dk in shards])
+  nefc_mean, ncon_mean = (float(x) / (ntrace * shards[0].nworld) for x in acc.cpu())
+  trace_sum = sum(e["ms_per_step"] for e in tab.values())
+  # a full re-run of the window ends in the timed run's state, bitwise (the replay of the same work)
+  replay_bitwise = bool(torch.equal(shards[0].qpos, qpos_timed[: shards[0].nworld])) if ntrace == args.steps else None
   converged = int((~torch.isnan(qpos_all).any(dim=1)).sum())
   solver_niter_mean = float(torch.cat([dk.solver_niter for dk in shards]).float().mean())
   solver_niter_max = int(torch.cat([dk.solver_niter for dk in shards]).max())
@@ -563,10 +599,16 @@ def main():
         **({"graph_error": graph_error} if graph_error else {}),
         "timed_region": "graph replays only" if graphs is not None else "eager steps (no graph)",
         "trace_steps": ntrace,
+        "trace_window": "the timed steps themselves: state restored to the timed region's start, steps "
+                        f"{args.warmup}..{args.warmup + ntrace - 1} re-run eagerly with HIP events per launch",
+        "trace_kernel_sum_ms_per_step": trace_sum,
+        "trace_over_timed": trace_sum / (elapsed / args.steps * 1e3),
+        "trace_consistent": trace_sum <= 1.03 * (elapsed / args.steps * 1e3),
+        "trace_replay_bitwise": replay_bitwise,
         "converged_worlds": converged,
         "nefc_mean": nefc_mean,
         "ncon_mean": ncon_mean,
-        "nefc_ncon_window": "trace pass (mean of its first and last step); timed region start / end: "
+        "nefc_ncon_window": "mean over the traced (= timed) steps; timed region start / end: "
                             f"nefc {nefc_t0:.2f} / {nefc_t1:.2f}, ncon {ncon_t0:.2f} / {ncon_t1:.2f}",
         "solver_niter_mean": solver_niter_mean,
         "solver_niter_max": solver_niter_max,

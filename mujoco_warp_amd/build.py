@@ -7,7 +7,10 @@ import sys
 _PKG = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_PKG)
 SOURCES = [os.path.join(_PKG, "csrc", n) for n in ("mjw_step.hip", "mjw_dense.hip", "mjw_sensor.hip", "mjw_rk4.hip", "mjw_sparse.hip", "mjw_kat.hip")]
-HEADERS = [os.path.join(_PKG, "csrc", n) for n in ("mjw_math.h", "mjw_common.h", "mjw_sensor.h", "mjw_ccd.h", "mjw_narrow.h", "mjw_flexcol.h", "mjw_dense.h", "mjw_tendon.h", "mjw_passive.h")] + [os.path.join(_ROOT, "include", "mjw_amd.h")]
+# every header next to the sources (a hand-kept list once missed mjw_trn.h, so sources_hash() and
+# needs_build() did not see edits to the transmission code)
+HEADERS = sorted(os.path.join(_PKG, "csrc", n) for n in os.listdir(os.path.join(_PKG, "csrc")) if n.endswith(".h"))
+HEADERS += [os.path.join(_ROOT, "include", "mjw_amd.h")]
 OUT = os.path.join(_PKG, "libmjw_amd.so")
 ARCH = os.environ.get("MJW_OFFLOAD_ARCH", "gfx950")
 
