@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 27
+#define MJW_ABI_VERSION 29
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -46,7 +46,7 @@
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
   X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)             \
-  X(nsensorcollision) X(nsensorccd) X(nhfield) X(nhfielddata)
+  X(nsensorcollision) X(nsensorccd) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -67,7 +67,7 @@
   X(geom_friction, ngeom * 3) X(geom_margin, ngeom) X(geom_gap, ngeom) X(geom_fluid, ngeom * 12)  \
   X(site_pos, nsite * 3) X(site_quat, nsite * 4) X(site_size, nsite * 3)                                                \
   X(cam_pos, ncam * 3) X(cam_quat, ncam * 4) X(cam_poscom0, ncam * 3) X(cam_pos0, ncam * 3)       \
-  X(cam_mat0, ncam * 9)                                                                            \
+  X(cam_mat0, ncam * 9) X(cam_fovy, ncam) X(cam_sensorsize, ncam * 2) X(cam_intrinsic, ncam * 4)    \
   X(light_pos, nlight * 3) X(light_dir, nlight * 3) X(light_poscom0, nlight * 3)                  \
   X(light_pos0, nlight * 3) X(light_dir0, nlight * 3)                                              \
   X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
@@ -99,7 +99,7 @@
   X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \
   X(geom_type, ngeom) X(geom_condim, ngeom) X(geom_bodyid, ngeom) X(geom_priority, ngeom)         \
   X(site_bodyid, nsite) X(site_type, nsite)                                                                      \
-  X(cam_mode, ncam) X(cam_bodyid, ncam) X(cam_targetbodyid, ncam)                                 \
+  X(cam_mode, ncam) X(cam_bodyid, ncam) X(cam_targetbodyid, ncam) X(cam_resolution, ncam * 2)     \
   X(light_mode, nlight) X(light_bodyid, nlight) X(light_targetbodyid, nlight)                     \
   X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
@@ -109,7 +109,7 @@
   X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq) X(eq_objtype, neq)                                             \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
-  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)                     \
+  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor) X(sensor_intprm, nsensor * 3) \
   X(sensor_collision_adr, nsensor) X(sensor_collision_num, nsensor) X(sensor_collision_pair, nsensorcollision * 4) \
   X(M_rownnz, nv) X(M_rowadr, nv) X(M_colind, nM) X(tree_dofadr, ntree + 1)                        \
   X(flex_dim, nflex) X(flex_vertadr, nflex) X(flex_edgeadr, nflex) X(flex_edgenum, nflex)          \

@@ -23,7 +23,9 @@ from .forward import step
 from .forward import rungekutta4
 from .forward import step1
 from .forward import step2
+from .io import find_keys
 from .io import get_data_into
+from .io import make_trajectory
 from .io import make_data
 from .io import override_model
 from .io import put_data

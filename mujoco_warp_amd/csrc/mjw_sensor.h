@@ -556,6 +556,179 @@ __device__ __forceinline__ bool inside_geom(const float* pos, const float* mat, 
   return false;
 }
 
+// ---- contact sensor (sensor.py:1750-1940 output, 2275-2430 matching) ---------------------------------
+// support.py:241-308 contact_force_fn: the contact's 6D force in its own frame (pyramid decoded)
+__device__ void contact_force_local(const mjw_model_t& m, const mjw_data_t& d, int wid, int cid, float* f) {
+  for (int i = 0; i < 6; i++) f[i] = 0.0f;
+  const int condim = d.contact_dim[cid];
+  const int adr = d.contact_efc_address[(long)cid * m.nmaxpyramid];
+  if (adr < 0) return;
+  const float* ef = d.efc_force + (long)wid * d.njmax;
+  if (m.opt_cone == CONE_PYRAMIDAL) {
+    if (condim == 1) { f[0] = ef[adr]; return; }
+    const float* mu = d.contact_friction + 5L * cid;
+    for (int i = 0; i < condim - 1; i++) {
+      const int a = 2 * i + adr;
+      const float d1 = a < d.njmax ? ef[a] : 0.0f, d2 = a + 1 < d.njmax ? ef[a + 1] : 0.0f;
+      f[0] += d1 + d2;
+      f[i + 1] = (d1 - d2) * mu[i];
+    }
+  } else {
+    for (int i = 0; i < condim; i++) {
+      const int a = d.contact_efc_address[(long)cid * m.nmaxpyramid + i];
+      if (a >= 0 && a < d.njmax) f[i] = ef[a];
+    }
+  }
+}
+
+// sensor.py:2258-2272 _check_match (XBODY: the contact body's ancestors, i.e. the subtree of objid)
+__device__ __forceinline__ bool contact_obj_match(const mjw_model_t& m, int body, int geom, int type, int id) {
+  if (type == OBJ_UNKNOWN || type == OBJ_SITE) return true;  // no object / the site zone was tested already
+  if (type == OBJ_GEOM) return id == geom;
+  if (type == OBJ_BODY) return id == body;
+  if (type == OBJ_XBODY) {
+    while (body > id) body = m.body_parentid[body];
+    return body == id;
+  }
+  return false;
+}
+
+// the world's contacts in pool (= narrowphase) order: each contact at its first constraint row; returns the
+// contact id of row r or -1
+__device__ __forceinline__ int contact_at_row(const mjw_model_t& m, const mjw_data_t& d, int wid, int r) {
+  const long wr = (long)wid * d.njmax;
+  const int type = d.efc_type[wr + r];
+  if (type != CNSTR_CONTACT_FRICTIONLESS && type != CNSTR_CONTACT_PYRAMIDAL && type != CNSTR_CONTACT_ELLIPTIC) return -1;
+  const int cid = d.efc_id[wr + r];
+  if (cid < 0 || cid >= d.naconmax || d.contact_efc_address[(long)cid * m.nmaxpyramid] != r) return -1;
+  return cid;
+}
+
+// sensor.py:2330-2375: does contact cid match sensor s, and in which direction (+-1; 0: no match)
+__device__ float contact_match(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s, int cid) {
+  const int ot = m.sensor_objtype[s], oid = m.sensor_objid[s], rt = m.sensor_reftype[s], rid = m.sensor_refid[s];
+  if (ot == OBJ_SITE) {
+    float sp[3], sR[9];
+    site_pose(m, wid, F, oid, sp, sR);
+    if (!inside_geom(sp, sR, MR(site_size) + 3 * oid, m.site_type[oid], d.contact_pos + 3L * cid)) return 0.0f;
+  }
+  if (ot == OBJ_UNKNOWN && rt == OBJ_UNKNOWN) return 1.0f;
+  const int g1 = d.contact_geom[2L * cid], g2 = d.contact_geom[2L * cid + 1];
+  const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+  const bool m11 = contact_obj_match(m, b1, g1, ot, oid), m12 = contact_obj_match(m, b2, g2, ot, oid);
+  const bool m21 = contact_obj_match(m, b1, g1, rt, rid), m22 = contact_obj_match(m, b2, g2, rt, rid);
+  if (!m11 && !m12) return 0.0f;
+  if (!m21 && !m22) return 0.0f;
+  if (ot != OBJ_UNKNOWN && rt != OBJ_UNKNOWN) {
+    const bool reg = m11 && m22, rev = m12 && m21;
+    if (!reg && !rev) return 0.0f;
+    return (rev && !reg) ? -1.0f : 1.0f;
+  }
+  if (ot != OBJ_UNKNOWN) return m11 ? 1.0f : -1.0f;
+  return m22 ? 1.0f : -1.0f;
+}
+
+// one contact sensor of world wid by the calling lane.  Matches are taken in the world's contact order (as
+// MuJoCo's mj_sensorAcc does; the reference's atomic match order is arbitrary), at most opt
+// contact_sensor_maxmatch of them; reduce mindist / maxforce pick the `num` smallest criteria (ties by that
+// order, a stable sort) by repeated selection, netforce sums them about the force-weighted centroid
+__device__ void contact_sensor(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s) {
+  const int spec = m.sensor_intprm[3 * s], reduce = m.sensor_intprm[3 * s + 1];
+  int size = 0;
+  const int fsz[7] = {1, 3, 3, 1, 3, 3, 3};
+  for (int i = 0; i < 7; i++)
+    if (spec & (1 << i)) size += fsz[i];
+  if (size == 0) return;
+  const int dim = m.sensor_dim[s], num = dim / size;
+  float* out = d.sensordata + (long)wid * m.nsensordata + m.sensor_adr[s];
+  const int nefc = min(d.nefc[wid], d.njmax);
+  const int maxmatch = m.opt_contact_sensor_maxmatch;
+  auto criteria = [&](int cid) -> float {
+    if (reduce == 1) return d.contact_dist[cid];
+    float f[6];
+    contact_force_local(m, d, wid, cid, f);
+    return -(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+  };
+  // pass 1: the match count (all matches: `found`) and, for netforce, the sums
+  int nmatch = 0;
+  float np[3] = {0, 0, 0}, nf[3] = {0, 0, 0}, nt[3] = {0, 0, 0}, wsum = 0.0f;
+  for (int r = 0; r < nefc; r++) {
+    const int cid = contact_at_row(m, d, wid, r);
+    if (cid < 0) continue;
+    const float dir = contact_match(m, d, wid, F, s, cid);
+    if (dir == 0.0f) continue;
+    const int k = nmatch++;
+    if (reduce != 3 || k >= maxmatch) continue;
+    float f[6];
+    contact_force_local(m, d, wid, cid, f);
+    const float w = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+    const float* cp = d.contact_pos + 3L * cid;
+    const float* fr = d.contact_frame + 9L * cid;
+    for (int i = 0; i < 3; i++) np[i] += w * cp[i];
+    wsum += w;
+    float fg[3], tg[3], c[3];
+    for (int i = 0; i < 3; i++) {
+      fg[i] = dir * (fr[i] * f[0] + fr[3 + i] * f[1] + fr[6 + i] * f[2]);  // frame^T @ (dir f)
+      tg[i] = dir * (fr[i] * f[3] + fr[3 + i] * f[4] + fr[6 + i] * f[5]);
+    }
+    cross3(c, cp, fg);
+    for (int i = 0; i < 3; i++) { nf[i] += fg[i]; nt[i] += tg[i] + c[i]; }
+  }
+  if (reduce == 3) {
+    float c[3];
+    for (int i = 0; i < 3; i++) np[i] /= fmaxf(wsum, MJW_MINVAL);
+    cross3(c, np, nf);
+    for (int i = 0; i < 3; i++) nt[i] -= c[i];
+    int a = 0;
+    if (spec & 1) out[a++] = (float)nmatch;
+    if (spec & 2) for (int i = 0; i < 3; i++) out[a++] = nf[i];
+    if (spec & 4) for (int i = 0; i < 3; i++) out[a++] = nt[i];
+    if (spec & 8) out[a++] = 0.0f;
+    if (spec & 16) for (int i = 0; i < 3; i++) out[a++] = np[i];
+    if (spec & 32) { out[a++] = 1.0f; out[a++] = 0.0f; out[a++] = 0.0f; }
+    if (spec & 64) { out[a++] = 0.0f; out[a++] = 1.0f; out[a++] = 0.0f; }
+    return;
+  }
+  const int nslots = min(min(nmatch, maxmatch), num);
+  float last_c = -MJW_MAXVAL;
+  int last_k = -1;
+  for (int i = 0; i < nslots; i++) {
+    // slot i: the i-th match in order (none) or the next (criteria, order) after the previous slot's
+    int cid = -1, k = 0, best_k = -1;
+    float dir = 0.0f, best_c = MJW_MAXVAL;
+    for (int r = 0; r < nefc && k < maxmatch; r++) {
+      const int c_ = contact_at_row(m, d, wid, r);
+      if (c_ < 0) continue;
+      const float dr = contact_match(m, d, wid, F, s, c_);
+      if (dr == 0.0f) continue;
+      if (reduce == 0) {
+        if (k == i) { cid = c_; dir = dr; break; }
+      } else {
+        const float cr = criteria(c_);
+        const bool after = cr > last_c || (cr == last_c && k > last_k);
+        if (after && (cr < best_c || best_k < 0)) { best_c = cr; best_k = k; cid = c_; dir = dr; }
+      }
+      k++;
+    }
+    if (reduce != 0) { last_c = best_c; last_k = best_k; }
+    if (cid < 0) break;
+    float* o = out + i * size;
+    int a = 0;
+    float f[6] = {0, 0, 0, 0, 0, 0};
+    if (spec & 6) contact_force_local(m, d, wid, cid, f);
+    const float* fr = d.contact_frame + 9L * cid;
+    if (spec & 1) o[a++] = (float)nmatch;
+    if (spec & 2) { o[a++] = f[0]; o[a++] = f[1]; o[a++] = dir * f[2]; }
+    if (spec & 4) { o[a++] = f[3]; o[a++] = f[4]; o[a++] = dir * f[5]; }
+    if (spec & 8) o[a++] = d.contact_dist[cid];
+    if (spec & 16) for (int j = 0; j < 3; j++) o[a++] = d.contact_pos[3L * cid + j];
+    if (spec & 32) for (int j = 0; j < 3; j++) o[a++] = dir * fr[j];
+    if (spec & 64) for (int j = 0; j < 3; j++) o[a++] = dir * fr[3 + j];
+  }
+  for (int i = max(nslots, 0); i < num; i++)
+    for (int j = 0; j < size; j++) out[i * size + j] = 0.0f;
+}
+
 // one position- or velocity-stage sensor (sensor.py:459-706 / 1251-1373, supported types); COLL: with the
 // collision sensors (their narrowphase is compiled into the models' kernel that has them only)
 template <bool COLL>
@@ -614,6 +787,27 @@ __device__ void sensor_posvel_one(const mjw_model_t& m, const mjw_data_t& d, int
       mul_quat(v, qi, q);
     }
     dim = 4;
+  } else if (t == SENS_CAMPROJECTION) {  // sensor.py:128-190: pixel coordinates of site `id` in camera `rid`
+    float sp[3], sR[9], cp[3], cR[9], dif[3], pc[3];
+    site_pose(m, wid, F, id, sp, sR);
+    obj_frame(m, wid, F, OBJ_CAMERA, rid, cp, cR);
+    for (int i = 0; i < 3; i++) dif[i] = sp[i] - cp[i];
+    mat_t_vec(pc, cR, dif);  // rotation @ translation @ [x; 1]: the point in the camera frame
+    const int rx = m.cam_resolution[2 * rid], ry = m.cam_resolution[2 * rid + 1];
+    const float* ss = MR(cam_sensorsize) + 2 * rid;
+    const float* in = MR(cam_intrinsic) + 4 * rid;
+    float fx, fy;
+    if (ss[0] != 0.0f && ss[1] != 0.0f) {
+      fx = in[0] / (ss[0] + MJW_MINVAL) * (float)rx;
+      fy = in[1] / (ss[1] + MJW_MINVAL) * (float)ry;
+    } else {
+      fx = fy = 0.5f / tanf(MR(cam_fovy)[rid] * (3.14159265358979f / 360.0f)) * (float)ry;
+    }
+    // image @ focal: (-fx x + rx/2 z, fy y + ry/2 z, z), divided by z clamped away from 0
+    const float u = -fx * pc[0] + 0.5f * (float)rx * pc[2], w = fy * pc[1] + 0.5f * (float)ry * pc[2];
+    float den = pc[2];
+    if (fabsf(den) < MJW_MINVAL) den = clampf(den, -MJW_MINVAL, MJW_MINVAL);
+    v[0] = u / den; v[1] = w / den; dim = 2;
   } else if (t == SENS_SUBTREECOM) {
     for (int i = 0; i < 3; i++) v[i] = F.subtree_com[3 * id + i];
   } else if (t == SENS_CLOCK) {

@@ -310,6 +310,9 @@ __device__ __forceinline__ void sensor_body(const mjw_model_t& m, const mjw_data
       const int r = limit_row(d, wid, id);
       v[0] = r < 0 ? 0.0f : d.efc_force[(long)wid * d.njmax + r];
       dim = 1;
+    } else if (t == SENS_CONTACT) {  // sensor.py:1750-1940
+      contact_sensor(m, d, wid, F, k);
+      continue;
     } else if (t == SENS_TOUCH) {  // sensor.py:2001-2076
       float p[3], R[9];
       site_pose(m, wid, F, id, p, R);

@@ -202,6 +202,7 @@ def put_model(mjm, device=None) -> types.Model:
   # io.py:188-190: the parallel linesearch switch (a <numeric name="ls_parallel"> of 1) and its smallest step
   opt.ls_parallel = bool(getattr(o, "ls_parallel", False))
   opt.ls_parallel_min_step = _f32([1.0e-6], dev)
+  opt.contact_sensor_maxmatch = int(getattr(o, "contact_sensor_maxmatch", 64))  # io.py:195-199
   stat = types.Statistic(meaninertia=_f32([mjm.stat.meaninertia], dev))
 
   m = types.Model()
@@ -951,3 +952,32 @@ def override_model(model, overrides: Sequence[str] | dict):
     else:
       setattr(obj, leaf, v)
   return model
+
+
+def find_keys(model, keyname_prefix: str) -> list:
+  """Ids of the keyframes whose name starts with `keyname_prefix`, in key order (io.py:2591-2600)."""
+  return [k for k, name in enumerate(model.key_names) if name.startswith(keyname_prefix)]
+
+
+def make_trajectory(model, keys: list) -> np.ndarray:
+  """Control trajectory through the keys' ctrl values, linearly interpolated in time at opt.timestep
+  (io.py:2603-2626): one row per step, the first key at time 0, keys in time order."""
+  ctrls = []
+  prev_ctrl = np.zeros(model.nu, dtype=np.float64)
+  prev_time, time = 0.0, 0.0
+  dt = float(model.opt.timestep)
+  for key in keys:
+    ctrl_key, ctrl_time = np.asarray(model.key_ctrl[key], dtype=np.float64), float(model.key_time[key])
+    if not ctrls and ctrl_time != 0.0:
+      raise ValueError("first keyframe must have time 0.0")
+    if ctrls and ctrl_time <= prev_time:
+      raise ValueError("keyframes must be in time order")
+    while time < ctrl_time:
+      frac = (time - prev_time) / (ctrl_time - prev_time)
+      ctrls.append(prev_ctrl * (1 - frac) + ctrl_key * frac)
+      time += dt
+    ctrls.append(ctrl_key)
+    time += dt
+    prev_ctrl = ctrl_key
+    prev_time = time
+  return np.array(ctrls)

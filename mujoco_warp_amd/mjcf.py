@@ -256,6 +256,7 @@ class MjOption:
     self.ls_iterations = 50
     self.noslip_iterations = 0
     self.ls_parallel = False  # Warp-only option from <custom><numeric name="ls_parallel" data="1"/>
+    self.contact_sensor_maxmatch = 64  # Warp-only option (io.py:195-199), <custom><numeric>
     self.ccd_iterations = 35
     self.disableflags = 0
     self.enableflags = 0
@@ -1369,6 +1370,10 @@ class _Compiler:
             pos=_floats(ca.get("pos", "0 0 0"), 3),
             quat=q if q is not None else [1, 0, 0, 0],
             fovy=float(ca.get("fovy", 45.0)),
+            # camera intrinsics (mjsCamera: resolution 1 x 1, sensorsize 0 0, focal 0.01 m, principal 0; the
+            # pixel forms convert through sensorsize / resolution): cam_resolution / cam_sensorsize /
+            # cam_intrinsic, which the camprojection sensor reads (sensor.py:128-190)
+            **_cam_intrinsics(ca),
           )
         )
       for la in b.lights:
@@ -1400,6 +1405,9 @@ class _Compiler:
     m.cam_pos = np.array([r["pos"] for r in crows]).reshape(-1, 3)
     m.cam_quat = np.array([r["quat"] for r in crows]).reshape(-1, 4)
     m.cam_fovy = np.array([r["fovy"] for r in crows])
+    m.cam_resolution = np.array([r["resolution"] for r in crows], dtype=np.int32).reshape(-1, 2)
+    m.cam_sensorsize = np.array([r["sensorsize"] for r in crows], dtype=np.float64).reshape(-1, 2)
+    m.cam_intrinsic = np.array([r["intrinsic"] for r in crows], dtype=np.float64).reshape(-1, 4)
     m.nlight = len(lrows)
     m.light_names = [r["name"] for r in lrows]
     m.light_bodyid = np.array([r["bodyid"] for r in lrows], dtype=np.int32)
@@ -1789,6 +1797,10 @@ class _Compiler:
     "fromto": (SensorType.GEOMFROMTO, 6, DataType.REAL, Stage.POS, "collision", None),
     # insidesite: objtype / objname inside the geometry of `site`
     "insidesite": (SensorType.INSIDESITE, 1, DataType.REAL, Stage.POS, "insidesite", None),
+    # contact: matched contacts' data (sensor.py:1750-1940, 2275-2430); dim from num x the data fields
+    "contact": (SensorType.CONTACT, 0, DataType.REAL, Stage.ACC, "contact", None),
+    # camprojection: pixel coordinates of `site` in `camera`'s image (sensor.py:128-190)
+    "camprojection": (SensorType.CAMPROJECTION, 2, DataType.REAL, Stage.POS, "camprojection", ObjType.SITE),
   }
   _OBJTYPES = {"body": ObjType.BODY, "xbody": ObjType.XBODY, "geom": ObjType.GEOM, "site": ObjType.SITE, "camera": ObjType.CAMERA}
 
@@ -1815,9 +1827,36 @@ class _Compiler:
         a.update(el.attrib)
         stype, dim, dtype, stage, key, otype = self._SENSORS[el.tag]
         objid, reftype, refid = -1, ObjType.UNKNOWN, -1
+        intprm = [0, 0, 0]
         if key == "collision":
           otype, objid = (ObjType.GEOM, names[ObjType.GEOM][a["geom1"]]) if "geom1" in a else (ObjType.BODY, names[ObjType.BODY][a["body1"]])
           reftype, refid = (ObjType.GEOM, names[ObjType.GEOM][a["geom2"]]) if "geom2" in a else (ObjType.BODY, names[ObjType.BODY][a["body2"]])
+        elif key == "contact":
+          # obj: geom1 | body1 | subtree1 | site, ref: geom2 | body2 | subtree2 (either may be absent: UNKNOWN);
+          # intprm = (data field bits: found force torque dist pos normal tangent, reduce: none mindist
+          # maxforce netforce, 0) -- MuJoCo's mjtConDataField / mjtConReduce
+          otype, objid = ObjType.UNKNOWN, -1
+          for k_, t_ in (("geom1", ObjType.GEOM), ("body1", ObjType.BODY), ("subtree1", ObjType.XBODY), ("site", ObjType.SITE)):
+            if k_ in a:
+              otype, objid = t_, names[ObjType.BODY if t_ == ObjType.XBODY else t_][a[k_]]
+          for k_, t_ in (("geom2", ObjType.GEOM), ("body2", ObjType.BODY), ("subtree2", ObjType.XBODY)):
+            if k_ in a:
+              reftype, refid = t_, names[ObjType.BODY if t_ == ObjType.XBODY else t_][a[k_]]
+          fields = a.get("data", "found").split()
+          order = ["found", "force", "torque", "dist", "pos", "normal", "tangent"]
+          if any(f_ not in order for f_ in fields) or [order.index(f_) for f_ in fields] != sorted(order.index(f_) for f_ in fields):
+            raise ValueError(f"contact sensor data {fields}: fields must be among {order}, in that order")
+          spec = sum(1 << order.index(f_) for f_ in fields)
+          size = sum((1, 3, 3, 1, 3, 3, 3)[order.index(f_)] for f_ in fields)
+          reduce = ["none", "mindist", "maxforce", "netforce"].index(a.get("reduce", "none"))
+          num = int(a.get("num", 1))
+          if reduce == 3 and num != 1:
+            raise ValueError("contact sensor: reduce='netforce' takes num = 1")
+          dim = num * size
+          intprm = [spec, reduce, 0]
+        elif key == "camprojection":
+          objid = names[ObjType.SITE][a["site"]]
+          reftype, refid = ObjType.CAMERA, names[ObjType.CAMERA][a["camera"]]
         elif key == "insidesite":
           otype = self._OBJTYPES[a["objtype"]]
           objid = names[otype][a["objname"]]
@@ -1832,13 +1871,14 @@ class _Compiler:
             refid = names[reftype][a["refname"]]
         rows.append(dict(name=a.get("name", ""), type=int(stype), datatype=int(dtype), needstage=int(stage), objtype=int(otype),
                          objid=objid, reftype=int(reftype), refid=refid, dim=dim, adr=adr, cutoff=float(a.get("cutoff", 0.0)),
-                         noise=float(a.get("noise", 0.0))))
+                         noise=float(a.get("noise", 0.0)), intprm=intprm))
         adr += dim
     m.nsensor = len(rows)
     m.nsensordata = adr
     m.sensor_names = [r["name"] for r in rows]
     for f in ("type", "datatype", "needstage", "objtype", "objid", "reftype", "refid", "dim", "adr"):
       setattr(m, "sensor_" + f, np.array([r[f] for r in rows], dtype=np.int32))
+    m.sensor_intprm = np.array([r["intprm"] for r in rows], dtype=np.int32).reshape(-1, 3)
     m.sensor_cutoff = np.array([r["cutoff"] for r in rows], dtype=np.float64)
     m.sensor_noise = np.array([r["noise"] for r in rows], dtype=np.float64)
 
@@ -1916,11 +1956,36 @@ class _Compiler:
     # a key shorter than nq (flexcomp dofs are appended after the keyed joints) is completed with qpos0
     m.key_qpos = np.array([np.concatenate([_floats(k.get("qpos")), m.qpos0[len(_floats(k.get("qpos"))):]]) if k.get("qpos") else m.qpos0
                            for k in keys]).reshape(m.nkey, m.nq)
+    # a (near-)zero free / ball joint quaternion in a key is the identity, as MuJoCo's mju_normalize4 makes
+    # it (the reference's aloha_pot keys store 0 0 0 0 for the pot's free joint, which the MuJoCo-C fixture
+    # state of unroll_test.py:42 reads as the identity); other key quaternions are kept as written
+    for j in range(m.njnt):
+      if int(m.jnt_type[j]) in (0, 1):  # FREE, BALL
+        a = int(m.jnt_qposadr[j]) + (3 if int(m.jnt_type[j]) == 0 else 0)
+        for kq in m.key_qpos:
+          if float(np.linalg.norm(kq[a:a + 4])) < MJ_MINVAL:
+            kq[a:a + 4] = (1.0, 0.0, 0.0, 0.0)
     m.key_qvel = np.array([_floats(k.get("qvel")) if k.get("qvel") else np.zeros(m.nv) for k in keys]).reshape(m.nkey, m.nv)
     m.key_act = np.array([_floats(k.get("act")) if k.get("act") else np.zeros(m.na) for k in keys]).reshape(m.nkey, m.na)
     m.key_ctrl = np.array([_floats(k.get("ctrl")) if k.get("ctrl") else np.zeros(m.nu) for k in keys]).reshape(m.nkey, m.nu)
     m.key_mpos = np.zeros((m.nkey, 3 * m.nmocap))
     m.key_mquat = np.tile(np.tile([1.0, 0, 0, 0], m.nmocap), (m.nkey, 1))
+
+
+def _cam_intrinsics(ca):
+  """resolution / sensorsize / intrinsic = [focal x, focal y, principal x, principal y] (length units) of a
+  <camera>: focal / principal in length, or focalpixel / principalpixel converted by sensorsize / resolution."""
+  res = [int(round(x)) for x in _floats(ca.get("resolution", "1 1"), 2)]
+  ss = _floats(ca.get("sensorsize", "0 0"), 2)
+  focal = _floats(ca.get("focal", "0.01 0.01"), 2)
+  principal = _floats(ca.get("principal", "0 0"), 2)
+  if "focalpixel" in ca:
+    fp = _floats(ca["focalpixel"], 2)
+    focal = [fp[i] / max(res[i], 1) * ss[i] for i in range(2)]
+  if "principalpixel" in ca:
+    pp = _floats(ca["principalpixel"], 2)
+    principal = [pp[i] / max(res[i], 1) * ss[i] for i in range(2)]
+  return dict(resolution=res, sensorsize=ss, intrinsic=list(focal) + list(principal))
 
 
 def _bending_coef(x, mu, thickness):

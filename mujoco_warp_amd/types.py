@@ -281,7 +281,8 @@ SUPPORTED_SENSORS = {
   SensorType.TOUCH, SensorType.TENDONPOS, SensorType.TENDONVEL, SensorType.TENDONACTFRC, SensorType.JOINTLIMITPOS,
   SensorType.JOINTLIMITVEL, SensorType.JOINTLIMITFRC, SensorType.TENDONLIMITPOS, SensorType.TENDONLIMITVEL,
   SensorType.TENDONLIMITFRC, SensorType.SUBTREELINVEL, SensorType.SUBTREEANGMOM, SensorType.E_POTENTIAL, SensorType.E_KINETIC,
-  SensorType.GEOMDIST, SensorType.GEOMNORMAL, SensorType.GEOMFROMTO, SensorType.INSIDESITE,
+  SensorType.GEOMDIST, SensorType.GEOMNORMAL, SensorType.GEOMFROMTO, SensorType.INSIDESITE, SensorType.CAMPROJECTION,
+  SensorType.CONTACT,
 }
 # sensors that need rne_postconstraint (io.py:542-551)
 RNE_POSTCONSTRAINT_SENSORS = {

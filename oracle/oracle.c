@@ -2344,12 +2344,12 @@ static void flex_collision(const orc_model* m, orc_data* d) {
  * constraint.py
  * ============================================================================================= */
 
-/* constraint.py:52-121 */
-static void efc_row(const orc_model* m, orc_data* d, int efcid, real pos_aref, real pos_imp, real invweight, const real* solref,
-                    const real* solimp, real margin, real vel, real frictionloss, int type, int id) {
+/* constraint.py:52-121: D and aref of one row from its impedance / reference inputs */
+static void efc_params(int disableflags, real timestep, real pos_aref, real pos_imp, real invweight, const real* solref,
+                       const real* solimp, real vel, real* D, real* aref) {
   real timeconst = solref[0], dampratio = solref[1];
   real dmin = solimp[0], dmax = solimp[1], width = solimp[2], mid = solimp[3], power = solimp[4];
-  if (!(m->opt_disableflags & DSBL_REFSAFE)) timeconst = maxr(timeconst, 2 * m->opt_timestep);
+  if (!(disableflags & DSBL_REFSAFE)) timeconst = maxr(timeconst, 2 * timestep);
   dmin = clampr(dmin, MINIMP, MAXIMP);
   dmax = clampr(dmax, MINIMP, MAXIMP);
   width = maxr(MINVAL, width);
@@ -2367,14 +2367,31 @@ static void efc_row(const orc_model* m, orc_data* d, int efcid, real pos_aref, r
   real imp = dmin + imp_y * (dmax - dmin);
   imp = clampr(imp, dmin, dmax);
   if (imp_x > 1) imp = dmax;
-  d->efc_D[efcid] = 1 / maxr(invweight * (1 - imp) / imp, MINVAL);
+  *D = 1 / maxr(invweight * (1 - imp) / imp, MINVAL);
+  *aref = -k * imp * pos_aref - b * vel;
+}
+
+void orc_kat_efc_row(int disableflags, real timestep, real pos_aref, real pos_imp, real invweight, const real* solref,
+                     const real* solimp, real vel, real* out) {
+  efc_params(disableflags, timestep, pos_aref, pos_imp, invweight, solref, solimp, vel, out, out + 1);
+}
+
+static void efc_row(const orc_model* m, orc_data* d, int efcid, real pos_aref, real pos_imp, real invweight, const real* solref,
+                    const real* solimp, real margin, real vel, real frictionloss, int type, int id) {
+  efc_params(m->opt_disableflags, m->opt_timestep, pos_aref, pos_imp, invweight, solref, solimp, vel, d->efc_D + efcid,
+             d->efc_aref + efcid);
   d->efc_vel[efcid] = vel;
-  d->efc_aref[efcid] = -k * imp * pos_aref - b * vel;
   d->efc_pos[efcid] = pos_aref + margin;
   d->efc_margin[efcid] = margin;
   d->efc_frictionloss[efcid] = frictionloss;
   d->efc_type[efcid] = type;
   d->efc_id[efcid] = id;
+  real* prm = d->efc_prm + 9 * efcid;
+  prm[0] = pos_imp;
+  prm[1] = invweight;
+  prm[2] = solref[0];
+  prm[3] = solref[1];
+  for (int i = 0; i < 5; i++) prm[4 + i] = solimp[i];
 }
 
 /* support.py:396-432 */
@@ -3495,7 +3512,7 @@ enum {
   SENS_JOINTPOS = 9, SENS_JOINTVEL = 10, SENS_ACTUATORPOS = 13, SENS_ACTUATORVEL = 14, SENS_ACTUATORFRC = 15,
   SENS_JOINTACTFRC = 16, SENS_BALLQUAT = 18, SENS_BALLANGVEL = 19, SENS_FRAMEPOS = 26, SENS_FRAMEQUAT = 27,
   SENS_FRAMEXAXIS = 28, SENS_FRAMEYAXIS = 29, SENS_FRAMEZAXIS = 30, SENS_FRAMELINVEL = 31, SENS_FRAMEANGVEL = 32,
-  SENS_FRAMELINACC = 33, SENS_FRAMEANGACC = 34, SENS_SUBTREECOM = 35, SENS_CLOCK = 45
+  SENS_FRAMELINACC = 33, SENS_FRAMEANGACC = 34, SENS_SUBTREECOM = 35, SENS_CLOCK = 45, SENS_CAMPROJECTION = 8
 };
 
 /* sensor.py:54-110 _write_scalar / _write_vector: cutoff clamps REAL, caps POSITIVE */
@@ -3600,6 +3617,46 @@ static void sensor_pos(const orc_model* m, orc_data* d) {
         mul_quat(v, qi, q);
       }
       sensor_write(m, d, s, v, 4);
+    } else if (t == SENS_CAMPROJECTION) {
+      /* sensor.py:128-190: proj = image @ focal @ rotation @ translation applied to [site_xpos; 1] */
+      const real* sp = d->site_xpos + 3 * id;
+      const real* cp = d->cam_xpos + 3 * rid;
+      const real* R = d->cam_xmat + 9 * rid;
+      real T[16] = {1, 0, 0, -cp[0], 0, 1, 0, -cp[1], 0, 0, 1, -cp[2], 0, 0, 0, 1};
+      real Rot[16] = {R[0], R[3], R[6], 0, R[1], R[4], R[7], 0, R[2], R[5], R[8], 0, 0, 0, 0, 1};
+      int rx = m->cam_resolution[2 * rid], ry = m->cam_resolution[2 * rid + 1];
+      const real* ss = m->cam_sensorsize + 2 * rid;
+      const real* in = m->cam_intrinsic + 4 * rid;
+      real fx, fy;
+      if (ss[0] != 0 && ss[1] != 0) {
+        fx = in[0] / (ss[0] + MINVAL) * (real)rx;
+        fy = in[1] / (ss[1] + MINVAL) * (real)ry;
+      } else {
+        fx = fy = 0.5 / tan(m->cam_fovy[rid] * (3.14159265358979323846 / 360.0)) * (real)ry;
+      }
+      real Fo[16] = {-fx, 0, 0, 0, 0, fy, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0};
+      real Im[16] = {1, 0, 0.5 * rx, 0, 0, 1, 0.5 * ry, 0, 0, 0, 1, 0, 0, 0, 0, 0};
+      real A[16], B[16], P[16];
+      for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+          A[4 * i + j] = B[4 * i + j] = 0;
+          for (int k = 0; k < 4; k++) A[4 * i + j] += Im[4 * i + k] * Fo[4 * k + j];
+        }
+      for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++)
+          for (int k = 0; k < 4; k++) B[4 * i + j] += A[4 * i + k] * Rot[4 * k + j];
+      for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+          P[4 * i + j] = 0;
+          for (int k = 0; k < 4; k++) P[4 * i + j] += B[4 * i + k] * T[4 * k + j];
+        }
+      real ph[3];
+      for (int i = 0; i < 3; i++) ph[i] = P[4 * i] * sp[0] + P[4 * i + 1] * sp[1] + P[4 * i + 2] * sp[2] + P[4 * i + 3];
+      real den = ph[2];
+      if (fabs(den) < MINVAL) den = clampr(den, -MINVAL, MINVAL);
+      v[0] = ph[0] / den;
+      v[1] = ph[1] / den;
+      sensor_write(m, d, s, v, 2);
     } else if (t == SENS_SUBTREECOM) {
       memcpy(v, d->subtree_com + 3 * id, 3 * sizeof(real));
       sensor_write(m, d, s, v, 3);

@@ -30,7 +30,7 @@ typedef ORC_REAL real;
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter) X(opt_ls_parallel) \
   X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
   X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)   \
-  X(ntendon) X(nwrap) X(nJten) X(npair) X(ngravcomp) X(has_fluid) X(nhfield) X(nhfielddata)
+  X(ntendon) X(nwrap) X(nJten) X(npair) X(ngravcomp) X(has_fluid) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
@@ -53,7 +53,7 @@ typedef ORC_REAL real;
   X(geom_friction, ngeom * 3) X(geom_margin, ngeom) X(geom_gap, ngeom)                             \
   X(site_pos, nsite * 3) X(site_quat, nsite * 4) X(site_size, nsite * 3)                                                \
   X(cam_pos, ncam * 3) X(cam_quat, ncam * 4) X(cam_poscom0, ncam * 3) X(cam_pos0, ncam * 3)       \
-  X(cam_mat0, ncam * 9)                                                                            \
+  X(cam_mat0, ncam * 9) X(cam_fovy, ncam) X(cam_sensorsize, ncam * 2) X(cam_intrinsic, ncam * 4)    \
   X(light_pos, nlight * 3) X(light_dir, nlight * 3) X(light_poscom0, nlight * 3)                  \
   X(light_pos0, nlight * 3) X(light_dir0, nlight * 3)                                              \
   X(actuator_dynprm, nu * 10) X(actuator_gainprm, nu * 10) X(actuator_biasprm, nu * 10)           \
@@ -82,7 +82,7 @@ typedef ORC_REAL real;
   X(dof_bodyid, nv) X(dof_jntid, nv) X(dof_parentid, nv)                                           \
   X(geom_type, ngeom) X(geom_condim, ngeom) X(geom_bodyid, ngeom) X(geom_priority, ngeom)         \
   X(site_bodyid, nsite) X(site_type, nsite)                                                                      \
-  X(cam_mode, ncam) X(cam_bodyid, ncam) X(cam_targetbodyid, ncam)                                 \
+  X(cam_mode, ncam) X(cam_bodyid, ncam) X(cam_targetbodyid, ncam) X(cam_resolution, ncam * 2)     \
   X(light_mode, nlight) X(light_bodyid, nlight) X(light_targetbodyid, nlight)                     \
   X(actuator_trntype, nu) X(actuator_dyntype, nu) X(actuator_gaintype, nu)                        \
   X(actuator_biastype, nu) X(actuator_trnid, nu * 2) X(actuator_actadr, nu) X(actuator_actnum, nu) \
@@ -92,7 +92,7 @@ typedef ORC_REAL real;
   X(eq_type, neq) X(eq_obj1id, neq) X(eq_obj2id, neq) X(eq_objtype, neq)                           \
   X(sensor_type, nsensor) X(sensor_datatype, nsensor) X(sensor_objtype, nsensor)                   \
   X(sensor_objid, nsensor) X(sensor_reftype, nsensor) X(sensor_refid, nsensor)                     \
-  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor)                     \
+  X(sensor_adr, nsensor) X(sensor_dim, nsensor) X(sensor_needstage, nsensor) X(sensor_intprm, nsensor * 3) \
   X(geom_contype, ngeom) X(geom_conaffinity, ngeom)                                                \
   X(flex_dim, nflex) X(flex_vertadr, nflex) X(flex_vertnum, nflex) X(flex_edgeadr, nflex)          \
   X(flex_edgenum, nflex) X(flex_elemadr, nflex) X(flex_elemnum, nflex) X(flex_elemdataadr, nflex)  \
@@ -123,6 +123,7 @@ typedef ORC_REAL real;
   X(sensordata, nsensordata)                                                                       \
   X(efc_J, njmax * nv) X(efc_pos, njmax) X(efc_margin, njmax) X(efc_D, njmax) X(efc_vel, njmax)   \
   X(efc_aref, njmax) X(efc_frictionloss, njmax) X(efc_force, njmax) X(efc_Ma, nv)                 \
+  X(efc_prm, njmax * 9) /* per row, the inputs of efc_row besides pos_aref / vel (tests only) */     \
   X(con_dist, nconmax) X(con_pos, nconmax * 3) X(con_frame, nconmax * 9)                          \
   X(con_includemargin, nconmax) X(con_friction, nconmax * 5) X(con_solref, nconmax * 2)           \
   X(con_solreffriction, nconmax * 2) X(con_solimp, nconmax * 5) X(solver_cost, 1)                 \
@@ -181,6 +182,8 @@ real orc_halton(int index, int base);
 int orc_kat_hfield_support(const real* prism, const real* dir, real margin, real* out);
 int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* size, const real* mesh_vert, const int* vertadr,
                 const int* vertnum, real margin, real tolerance, int iterations, int multiccd, real* out);
+void orc_kat_efc_row(int disableflags, real timestep, real pos_aref, real pos_imp, real invweight, const real* solref,
+                     const real* solimp, real vel, real* out);
 int orc_kat_wrap(int fn, const real* a, int ind, real radius, real* out);
 int orc_kat_geom_triangle(int gt, const real* gp, const real* gr, const real* gs, const real* tri, real tr, real* out);
 void orc_ctrl_noise(const orc_model* m, real* ctrl, const real* center, int ncenter, int step, real std,

@@ -11,7 +11,7 @@ enum {
   SENS_TOUCH = 0, SENS_TENDONPOS = 11, SENS_TENDONVEL = 12, SENS_TENDONACTFRC = 17, SENS_JOINTLIMITPOS = 20,
   SENS_JOINTLIMITVEL = 21, SENS_JOINTLIMITFRC = 22, SENS_TENDONLIMITPOS = 23, SENS_TENDONLIMITVEL = 24,
   SENS_TENDONLIMITFRC = 25, SENS_SUBTREELINVEL = 36, SENS_SUBTREEANGMOM = 37, SENS_E_POTENTIAL = 43, SENS_E_KINETIC = 44,
-  SENS_INSIDESITE = 38, SENS_GEOMDIST = 39, SENS_GEOMNORMAL = 40, SENS_GEOMFROMTO = 41
+  SENS_INSIDESITE = 38, SENS_GEOMDIST = 39, SENS_GEOMNORMAL = 40, SENS_GEOMFROMTO = 41, SENS_CONTACT = 42
 };
 
 /* ---- collision sensors: the smallest-distance contact over the sensor's geom pairs ---- */
@@ -393,6 +393,151 @@ static real touch_sensor(const orc_model* m, const orc_data* d, int site) {
   return total;
 }
 
+/* ---- contact sensor (sensor.py:1750-1940 output, 2258-2430 matching) ---- */
+/* support.py:241-308: the contact's 6D force in its own frame */
+static void contact_force_local(const orc_model* m, const orc_data* d, int c, real* f) {
+  for (int i = 0; i < 6; i++) f[i] = 0;
+  const int condim = d->con_dim[c], adr = d->con_efc_address[10 * c];
+  if (adr < 0) return;
+  if (m->opt_cone == 0) {
+    if (condim == 1) { f[0] = d->efc_force[adr]; return; }
+    for (int i = 0; i < condim - 1; i++) {
+      const int a = 2 * i + adr;
+      const real d1 = a < d->njmax ? d->efc_force[a] : 0, d2 = a + 1 < d->njmax ? d->efc_force[a + 1] : 0;
+      f[0] += d1 + d2;
+      f[i + 1] = (d1 - d2) * d->con_friction[5 * c + i];
+    }
+  } else {
+    for (int i = 0; i < condim; i++) {
+      const int a = d->con_efc_address[10 * c + i];
+      if (a >= 0 && a < d->njmax) f[i] = d->efc_force[a];
+    }
+  }
+}
+
+/* sensor.py:2258-2272 _check_match */
+static int contact_obj_match(const orc_model* m, int body, int geom, int type, int id) {
+  if (type == OBJ_UNKNOWN || type == OBJ_SITE) return 1; /* no object / the site zone was tested already */
+  if (type == OBJ_GEOM) return id == geom;
+  if (type == OBJ_BODY) return id == body;
+  if (type == OBJ_XBODY) {
+    while (body > id) body = m->body_parentid[body];
+    return body == id;
+  }
+  return 0;
+}
+
+/* sensor.py:2330-2375: direction (+-1) of a matched contact, 0 when it does not match */
+static real contact_match(const orc_model* m, const orc_data* d, int s, int c) {
+  const int ot = m->sensor_objtype[s], oid = m->sensor_objid[s], rt = m->sensor_reftype[s], rid = m->sensor_refid[s];
+  if (ot == OBJ_SITE &&
+      !inside_geom(d->site_xpos + 3 * oid, d->site_xmat + 9 * oid, m->site_size + 3 * oid, m->site_type[oid], d->con_pos + 3 * c))
+    return 0;
+  if (ot == OBJ_UNKNOWN && rt == OBJ_UNKNOWN) return 1;
+  const int g1 = d->con_geom[2 * c], g2 = d->con_geom[2 * c + 1];
+  const int b1 = m->geom_bodyid[g1], b2 = m->geom_bodyid[g2];
+  const int m11 = contact_obj_match(m, b1, g1, ot, oid), m12 = contact_obj_match(m, b2, g2, ot, oid);
+  const int m21 = contact_obj_match(m, b1, g1, rt, rid), m22 = contact_obj_match(m, b2, g2, rt, rid);
+  if ((!m11 && !m12) || (!m21 && !m22)) return 0;
+  if (ot != OBJ_UNKNOWN && rt != OBJ_UNKNOWN) {
+    const int reg = m11 && m22, rev = m12 && m21;
+    if (!reg && !rev) return 0;
+    return (rev && !reg) ? -1 : 1;
+  }
+  if (ot != OBJ_UNKNOWN) return m11 ? 1 : -1;
+  return m22 ? 1 : -1;
+}
+
+/* one contact sensor: matches in the world's contact order (MuJoCo's mj_sensorAcc order), at most
+ * contact_sensor_maxmatch of them; mindist / maxforce sort the matches stably by their criteria (insertion
+ * sort of the match list); netforce sums about the force-weighted centroid */
+static void contact_sensor(const orc_model* m, orc_data* d, int s) {
+  const int spec = m->sensor_intprm[3 * s], reduce = m->sensor_intprm[3 * s + 1];
+  static const int fsz[7] = {1, 3, 3, 1, 3, 3, 3};
+  int size = 0;
+  for (int i = 0; i < 7; i++)
+    if (spec & (1 << i)) size += fsz[i];
+  if (!size) return;
+  const int num = m->sensor_dim[s] / size;
+  real* out = d->sensordata + m->sensor_adr[s];
+  const int maxm = m->opt_contact_sensor_maxmatch;
+  int ids[256];
+  real dirs[256], crit[256];
+  int nmatch = 0;
+  for (int c = 0; c < d->ncon[0]; c++) {
+    if (d->con_efc_address[10 * c] < 0) continue;
+    const real dir = contact_match(m, d, s, c);
+    if (dir == 0) continue;
+    const int k = nmatch++;
+    if (k >= maxm || k >= 256) continue;
+    ids[k] = c;
+    dirs[k] = dir;
+    if (reduce == 1) crit[k] = d->con_dist[c];
+    else if (reduce == 2) {
+      real f[6];
+      contact_force_local(m, d, c, f);
+      crit[k] = -(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+    }
+  }
+  const int nkept = nmatch < maxm ? (nmatch < 256 ? nmatch : 256) : (maxm < 256 ? maxm : 256);
+  if (reduce == 3) {
+    real np[3] = {0, 0, 0}, nf[3] = {0, 0, 0}, nt[3] = {0, 0, 0}, w = 0, c3[3];
+    for (int k = 0; k < nkept; k++) {
+      const int c = ids[k];
+      real f[6], fg[3], tg[3];
+      contact_force_local(m, d, c, f);
+      const real wk = sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+      for (int i = 0; i < 3; i++) np[i] += wk * d->con_pos[3 * c + i];
+      w += wk;
+      const real* F = d->con_frame + 9 * c;
+      for (int i = 0; i < 3; i++) {
+        fg[i] = dirs[k] * (F[i] * f[0] + F[3 + i] * f[1] + F[6 + i] * f[2]);
+        tg[i] = dirs[k] * (F[i] * f[3] + F[3 + i] * f[4] + F[6 + i] * f[5]);
+      }
+      cross3(c3, d->con_pos + 3 * c, fg);
+      for (int i = 0; i < 3; i++) { nf[i] += fg[i]; nt[i] += tg[i] + c3[i]; }
+    }
+    for (int i = 0; i < 3; i++) np[i] /= (w > MINVAL ? w : MINVAL);
+    cross3(c3, np, nf);
+    for (int i = 0; i < 3; i++) nt[i] -= c3[i];
+    int a = 0;
+    if (spec & 1) out[a++] = nmatch;
+    if (spec & 2) for (int i = 0; i < 3; i++) out[a++] = nf[i];
+    if (spec & 4) for (int i = 0; i < 3; i++) out[a++] = nt[i];
+    if (spec & 8) out[a++] = 0;
+    if (spec & 16) for (int i = 0; i < 3; i++) out[a++] = np[i];
+    if (spec & 32) { out[a++] = 1; out[a++] = 0; out[a++] = 0; }
+    if (spec & 64) { out[a++] = 0; out[a++] = 1; out[a++] = 0; }
+    return;
+  }
+  if (reduce == 1 || reduce == 2)
+    for (int i = 1; i < nkept; i++) /* stable insertion sort by criteria */
+      for (int j = i; j > 0 && crit[j] < crit[j - 1]; j--) {
+        real tc = crit[j]; crit[j] = crit[j - 1]; crit[j - 1] = tc;
+        real td = dirs[j]; dirs[j] = dirs[j - 1]; dirs[j - 1] = td;
+        int ti = ids[j]; ids[j] = ids[j - 1]; ids[j - 1] = ti;
+      }
+  const int nslots = nkept < num ? nkept : num;
+  for (int i = 0; i < nslots; i++) {
+    const int c = ids[i];
+    const real dir = dirs[i];
+    real* o = out + i * size;
+    int a = 0;
+    real f[6];
+    contact_force_local(m, d, c, f);
+    const real* F = d->con_frame + 9 * c;
+    if (spec & 1) o[a++] = nmatch;
+    if (spec & 2) { o[a++] = f[0]; o[a++] = f[1]; o[a++] = dir * f[2]; }
+    if (spec & 4) { o[a++] = f[3]; o[a++] = f[4]; o[a++] = dir * f[5]; }
+    if (spec & 8) o[a++] = d->con_dist[c];
+    if (spec & 16) for (int j = 0; j < 3; j++) o[a++] = d->con_pos[3 * c + j];
+    if (spec & 32) for (int j = 0; j < 3; j++) o[a++] = dir * F[j];
+    if (spec & 64) for (int j = 0; j < 3; j++) o[a++] = dir * F[3 + j];
+  }
+  for (int i = nslots; i < num; i++)
+    for (int j = 0; j < size; j++) out[i * size + j] = 0;
+}
+
 /* the sensors above for one stage (1 position, 2 velocity, 3 acceleration) */
 static void sensor_extra(const orc_model* m, orc_data* d, int stage) {
   int subtree = 0;
@@ -426,6 +571,7 @@ static void sensor_extra(const orc_model* m, orc_data* d, int stage) {
       case SENS_E_POTENTIAL: v[0] = energy_potential(m, d); break;
       case SENS_E_KINETIC: v[0] = energy_kinetic(m, d); break;
       case SENS_GEOMDIST: case SENS_GEOMNORMAL: case SENS_GEOMFROMTO: collision_sensor(m, d, s); continue;
+      case SENS_CONTACT: contact_sensor(m, d, s); continue;
       case SENS_INSIDESITE: {
         const real *p, *R;
         int body;

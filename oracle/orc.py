@@ -160,7 +160,7 @@ class OracleModel:
       ngravcomp=int((np.asarray(getattr(mjm, "body_gravcomp", np.zeros(mjm.nbody))) > 0).sum()),
       has_fluid=int(bool(np.any(np.asarray(o.wind) != 0) or o.density > 0 or o.viscosity > 0)),
       opt_density=o.density, opt_viscosity=o.viscosity,
-      opt_ls_parallel=int(bool(getattr(o, "ls_parallel", False))), opt_ls_parallel_min_step=getattr(o, "ls_parallel_min_step", 1e-6),
+      opt_ls_parallel=int(bool(getattr(o, "ls_parallel", False))), opt_contact_sensor_maxmatch=int(getattr(o, "contact_sensor_maxmatch", 64)), opt_ls_parallel_min_step=getattr(o, "ls_parallel_min_step", 1e-6),
     )
     if overrides:
       vals.update(overrides)
@@ -172,6 +172,7 @@ class OracleModel:
       opt_gravity=o.gravity, opt_magnetic=o.magnetic, opt_wind=o.wind, nxn_geom_pair=pairs, nxn_pairid=pairid,
       body_gravcomp=getattr(mjm, "body_gravcomp", np.zeros(mjm.nbody)), geom_fluid=geom_fluid, body_fluid_ellipsoid=fluid_ellipsoid,
       cam_mat0=getattr(mjm, "cam_mat0", np.zeros((mjm.ncam, 9))),
+      sensor_intprm=getattr(mjm, "sensor_intprm", np.zeros((getattr(mjm, "nsensor", 0), 3))),
     )
     self._keep = []
     s = self.StructM()
@@ -343,6 +344,23 @@ def kat_wrap(fn, args, ind=0, radius=0.0, real_bits=64):
     return float(out[0])
   n = 2 if k < 4 else 3
   return float(out[0]), out[1:1 + n].copy(), out[1 + n:1 + 2 * n].copy()
+
+
+def efc_row_params(disableflags, timestep, pos_aref, pos_imp, invweight, solref, solimp, vel):
+  """(D, aref) of constraint rows from their inputs (constraint.py:52-121, fp64 oracle), vectorised over rows:
+  pos_aref / pos_imp / invweight / vel of shape (n,), solref (n, 2), solimp (n, 5)."""
+  lib = _lib(64)
+  P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+  n = len(pos_aref)
+  out = np.zeros((n, 2))
+  sr = np.ascontiguousarray(solref, dtype=np.float64).reshape(n, 2)
+  si = np.ascontiguousarray(solimp, dtype=np.float64).reshape(n, 5)
+  o = np.zeros(2)
+  for i in range(n):
+    lib.orc_kat_efc_row(ctypes.c_int(int(disableflags)), ctypes.c_double(timestep), ctypes.c_double(pos_aref[i]),
+                        ctypes.c_double(pos_imp[i]), ctypes.c_double(invweight[i]), P(sr[i]), P(si[i]), ctypes.c_double(vel[i]), P(o))
+    out[i] = o
+  return out[:, 0], out[:, 1]
 
 
 def kat_geom_triangle(gt, gp, gr, gs, tri, tr, real_bits=64):

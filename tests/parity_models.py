@@ -166,6 +166,39 @@ def rows_of(mjm, d, od, w, sparse, njmax):
   return g, o, dense_J(d, w, n, nv)[g]
 
 
+def rows_at_gpu_pos(mjm, d, od, w, g, o, njmax):
+  """Errors of the GPU's efc D / aref against the reference's row formula evaluated in fp64 at the GPU's own
+  pos_aref (= efc_pos - efc_margin), pos_imp and efc_vel: the row's remaining inputs (invweight, solref,
+  solimp) are model / contact parameters, taken from the oracle (efc_prm).  pos_imp is pos_aref for most
+  rows; for connect / weld rows it is the norm of the group's pos_aref, for elliptic friction rows the
+  normal row's (the group: rows with the same type and id).  Returns ({D, aref: err}, rows covered)."""
+  from oracle import orc
+
+  g, o = np.asarray(g, int), np.asarray(o, int)
+  if len(o) == 0:
+    return {"D": None, "aref": None}, 0
+  prm = np.asarray(od.efc_prm[w], np.float64).reshape(njmax, 9)[o]
+  pa_o = (od.efc_pos[w] - od.efc_margin[w])[o]
+  pa_g = (np_(d.efc.pos[w]).astype(np.float64) - np_(d.efc.margin[w]).astype(np.float64))[g]
+  typ, ids = od.efc_type[w][o], od.efc_id[w][o]
+  pi_g = pa_g.copy()
+  keep = np.ones(len(o), bool)
+  for i in np.nonzero(prm[:, 0] != pa_o)[0]:
+    grp = np.nonzero((typ == typ[i]) & (ids == ids[i]))[0]
+    nrm_o = float(np.linalg.norm(pa_o[grp]))
+    if abs(prm[i, 0] - nrm_o) <= 1e-12 * max(1.0, abs(nrm_o)):
+      pi_g[i] = float(np.linalg.norm(pa_g[grp]))
+    elif abs(prm[i, 0] - pa_o[grp[0]]) <= 1e-12 * max(1.0, abs(pa_o[grp[0]])):
+      pi_g[i] = pa_g[grp[0]]
+    else:
+      keep[i] = False
+  vel_g = np_(d.efc.vel[w]).astype(np.float64)[g]
+  D_ref, aref_ref = orc.efc_row_params(int(mjm.opt.disableflags), float(mjm.opt.timestep), pa_g[keep], pi_g[keep], prm[keep, 1],
+                                       prm[keep, 2:4], prm[keep, 4:9], vel_g[keep])
+  out = {"D": err(np_(d.efc.D[w])[g][keep][None], D_ref[None]), "aref": err(np_(d.efc.aref[w])[g][keep][None], aref_ref[None])}
+  return out, int(keep.sum())
+
+
 def efc_cost(J, D, aref, types_, M, qacc_smooth, qacc, fl=None, nf=0):
   """fp64 primal cost (solver.py): Gauss term + rows; equality always quadratic, friction loss
   Huber, limits / contacts quadratic while J qacc - aref < 0."""
@@ -231,6 +264,17 @@ def report(name):
   # bias) fp32 rounding of the summands, not of the result, bounds its error
   summ = np.maximum(np.maximum(np.abs(od.qfrc_bias).max(axis=1), np.abs(od.qfrc_passive).max(axis=1)), np.abs(od.qfrc_actuator).max(axis=1))
   out["cancel_scale"] = max(1.0, float((summ / (np.abs(od.qfrc_smooth).max(axis=1) + 1e-300)).max()))
+  # the same quantities from the fp32 build of the oracle (the reference's arithmetic type, sequential
+  # order): what fp32 evaluation of the formulas achieves on this state, against the same fp64 oracle
+  _, o32 = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=nconmax, real_bits=32)
+  o32.forward()
+  bw32 = 0.0
+  for w in range(nworld):
+    Mo = dense_M(mjm, d, od, w)[1]
+    r32 = Mo @ np.asarray(o32.qacc_smooth[w], np.float64) - od.qfrc_smooth[w]
+    bw32 = max(bw32, float(np.abs(r32).max() / (np.abs(od.qfrc_smooth[w]).max() + 1e-300)))
+  out["fp32_oracle"] = {"qfrc_smooth": err(np.asarray(o32.qfrc_smooth, np.float64), od.qfrc_smooth), "qacc_smooth_backward": bw32,
+                        "qacc_smooth": err(np.asarray(o32.qacc_smooth, np.float64), od.qacc_smooth)}
   # qacc_smooth = M^-1 qfrc_smooth: its forward error carries cond(M) times the (checked) residual
   out["cond_M"] = max(float(np.linalg.cond(od.qM[w].reshape(nv, nv))) for w in range(nworld))
   # rows
@@ -255,6 +299,12 @@ def report(name):
     for f in ("pos", "vel", "D", "aref"):
       rowerr[f] = merge(rowerr.get(f), err(np_(getattr(d.efc, f)[w])[g][None], getattr(od, "efc_" + f)[w][o][None]))
     rowerr["pos_abs"] = max(rowerr.get("pos_abs", 0.0), float(np.abs(np_(d.efc.pos[w])[g] - od.efc_pos[w][o]).max()))
+    # D / aref as functions of the GPU's own row positions (constraint.py:52-121 in fp64, the oracle's
+    # orc_kat_efc_row), with the row's other inputs (invweight, solref, solimp) from the oracle
+    e_at, n_at = rows_at_gpu_pos(mjm, d, od, w, g, o, njmax)
+    for f in ("D", "aref"):
+      rowerr[f + "_at_gpu_pos"] = merge(rowerr.get(f + "_at_gpu_pos"), e_at[f])
+    rowerr["rows_at_gpu_pos"] = rowerr.get("rows_at_gpu_pos", 0) + n_at
   out["rows"] = rowerr
   out["rows_types_equal"] = types_equal
   out["rows_total"] = nrows
