@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 29
+#define MJW_ABI_VERSION 30
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -46,7 +46,8 @@
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
   X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)             \
-  X(nsensorcollision) X(nsensorccd) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)
+  X(nsensorcollision) X(nsensorccd) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)           \
+  X(nmeshpoly) X(nmeshpolyvert) X(nmeshpolymap) X(nmaxpolygon) X(nmaxmeshdeg)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -79,6 +80,7 @@
   X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)                                \
   X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)                              \
   X(mesh_vert, nmeshvert * 3) X(hfield_size, nhfield * 4) X(hfield_data, nhfielddata)             \
+  X(mesh_polynormal, nmeshpoly * 3)                                                                \
   X(tendon_stiffness, ntendon) X(tendon_damping, ntendon) X(tendon_frictionloss, ntendon)          \
   X(tendon_armature, ntendon) X(tendon_margin, ntendon) X(tendon_range, ntendon * 2)               \
   X(tendon_lengthspring, ntendon * 2) X(tendon_solref_lim, ntendon * 2) X(tendon_solimp_lim, ntendon * 5) \
@@ -119,6 +121,8 @@
   X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata) X(flex_elemedge, nflexelem * 3)      \
   X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)                                     \
   X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)                            \
+  X(mesh_polyadr, nmesh) X(mesh_polynum, nmesh) X(mesh_polyvertadr, nmeshpoly) X(mesh_polyvertnum, nmeshpoly) \
+  X(mesh_polyvert, nmeshpolyvert) X(mesh_polymapadr, nmeshvert) X(mesh_polymapnum, nmeshvert) X(mesh_polymap, nmeshpolymap) \
   X(hfield_nrow, nhfield) X(hfield_ncol, nhfield) X(hfield_adr, nhfield)                          \
   X(tendon_adr, ntendon) X(tendon_num, ntendon) X(tendon_limited, ntendon) X(tendon_actfrclimited, ntendon) \
   X(wrap_objid, nwrap) X(wrap_type, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)

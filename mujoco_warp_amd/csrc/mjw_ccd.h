@@ -21,8 +21,8 @@ constexpr float CCD_INTERSECT_TOL = 0.0000003f;
 constexpr unsigned CCD_FACE_DELETED = 0x80000000u;
 constexpr unsigned CCD_FACE_INVALID = 0x40000000u;
 
-// one geom in the workspace: pos[3] rot[9] size[3] margin type mesh_vertadr mesh_vertnum
-constexpr int CGEOM_WORDS = 19;
+// one geom in the workspace: pos[3] rot[9] size[3] margin type mesh_vertadr mesh_vertnum mesh id
+constexpr int CGEOM_WORDS = 20;
 // per-pair result record in HBM (d.ccd_out): count, normal[3], then per point (dist, pos[3]) x 4, then per
 // point normal[3] x 4 (words 20-31).  The convex pairs (GJK / EPA / box multi-contact) give every point the
 // pair's distance and normal; the multi-point primitives the pre-passes also run (plane-cylinder,
@@ -37,28 +37,42 @@ constexpr int HF_WORDS = 18 + 7 * HF_MAXCON;
 struct CcdLay {
   int vert, vidx, face, pr, norm2, horizon, simplex, sidx, coords, nrm, idx, endvert, f1, f2, pn, pd, poly, clip, w1, w2;
   int geoms, out, hf;
-  int cap_vert, cap_face, total;
+  int cap_vert, cap_face, npoly, ndeg, total;
 };
 
-// hf: reserve the heightfield scratch (models with heightfield geoms)
-__host__ __device__ inline CcdLay ccd_layout(int it, bool hf = false) {
+// hf: reserve the heightfield scratch (models with heightfield geoms).  npoly / ndeg: the multi-contact
+// buffers' bounds (collision_convex.py:1120-1140: a box face has 4 corners and a corner 3 faces; with
+// MULTICCD on mesh pairs the model's largest polygon and vertex degree, m.nmaxpolygon / m.nmaxmeshdeg).
+// The multi-contact buffers follow the fixed part, and the heightfield scratch comes last, so every
+// offset but hf is the same with or without it.
+__host__ __device__ inline CcdLay ccd_layout(int it, bool hf = false, int npoly = 4, int ndeg = 3) {
   CcdLay L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += n; return r; };
   L.cap_vert = 10 + 2 * it;  // vec3 slots, two per polytope vertex (collision_convex.py:1146)
   L.cap_face = 6 + CCD_MAX_EPAFACES * it;
+  L.npoly = npoly < 4 ? 4 : npoly;
+  L.ndeg = ndeg < 3 ? 3 : ndeg;
   L.vert = take(L.cap_vert * 3); L.vidx = take(L.cap_vert);
   L.face = take(L.cap_face); L.pr = take(L.cap_face * 3); L.norm2 = take(L.cap_face);
   L.horizon = take(CCD_MAX_EPAHORIZON);
   L.simplex = take(3 * 4 * 3); L.sidx = take(2 * 4); L.coords = take(4);
-  L.nrm = take(2 * 3 * 3); L.idx = take(2 * 3); L.endvert = take(3 * 3);
-  L.f1 = take(4 * 3); L.f2 = take(4 * 3); L.pn = take(8 * 3); L.pd = take(8);
-  L.poly = take(16 * 3); L.clip = take(16 * 3); L.w1 = take(4 * 3); L.w2 = take(4 * 3);
   L.geoms = take(2 * CGEOM_WORDS); L.out = take(CCD_OUT);
+  L.w1 = take(4 * 3); L.w2 = take(4 * 3);
+  const int nclip = 2 * L.npoly > 16 ? 2 * L.npoly : 16;
+  L.nrm = take(2 * L.ndeg * 3); L.idx = take(2 * L.ndeg); L.endvert = take(L.ndeg * 3);
+  L.f1 = take(L.npoly * 3); L.f2 = take(L.npoly * 3); L.pn = take(L.npoly * 3); L.pd = take(L.npoly);
+  L.poly = take(nclip * 3); L.clip = take(nclip * 3);
   L.hf = take(hf ? HF_WORDS : 0);
   L.total = o;
   return L;
 }
+
+// a mesh's polygon data (mesh_poly*: the model's arrays; collision_gjk.py:1403-1790 reads them)
+struct MeshPoly {
+  const float* polynormal;
+  const int *polyadr, *polynum, *polyvertadr, *polyvertnum, *polyvert, *polymapadr, *polymapnum, *polymap, *vertadr;
+};
 
 struct CGeom {
   float pos[3], rot[9], size[3], margin;
@@ -66,6 +80,10 @@ struct CGeom {
   const float* mv;  // mesh vertices (geom frame), GEOM_MESH only
   int nvert;
   const float* prism;  // GEOM_HFIELD: the 6 prism vertices (heightfield frame, LDS); pos = the prism center
+  // GEOM_MESH polygon data, offset to this mesh (pnormal / pvadr / pvnum by its polygon address, pmapadr /
+  // pmapnum by its vertex address; pvert / pmap hold mesh-local vertex / polygon ids); null: none
+  const float* pnormal;
+  const int *pvadr, *pvnum, *pvert, *pmapadr, *pmapnum, *pmap;
 };
 
 __device__ __forceinline__ float ccd_sign(float x) { return x < 0.0f ? -1.0f : 1.0f; }  // wp.sign
@@ -857,6 +875,7 @@ __device__ __forceinline__ int polygon_clip(const CcdWS& w, const float* face1, 
   }
   float* poly = w.W + w.L.poly;
   float* clip = w.W + w.L.clip;
+  const int ncap = 2 * w.L.npoly > 16 ? 2 * w.L.npoly : 16;
   int np = nface2, nc = 0;
   for (int i = 0; i < 3 * nface2; i++) poly[i] = face2[i];
   for (int e = 0; e < nface1; e++) {
@@ -870,7 +889,7 @@ __device__ __forceinline__ int polygon_clip(const CcdWS& w, const float* face1, 
       float dP[3] = {P[0] - fe[0], P[1] - fe[1], P[2] - fe[2]}, dQ[3] = {Q[0] - fe[0], Q[1] - fe[1], Q[2] - fe[2]};
       const bool in1 = dot3(dP, pne) > -1e-10f, in2 = dot3(dQ, pne) > -1e-10f;
       if (!in1 && !in2) continue;
-      if (nc >= 14) break;  // buffer guard (16 slots; a convex 4-gon clipped 4 times has <= 8)
+      if (nc >= ncap - 2) break;  // buffer guard (a convex n-gon clipped by an m-gon has <= n + m vertices)
       if (in1 && in2) { st3(clip + 3 * nc, Q); nc++; continue; }
       float PQ[3] = {Q[0] - P[0], Q[1] - P[1], Q[2] - P[2]};
       float dt = dot3(pne, PQ);
@@ -902,8 +921,103 @@ __device__ __forceinline__ int polygon_clip(const CcdWS& w, const float* face1, 
   return np;
 }
 
-// collision_gjk.py:1929-2150 (box-box); witnesses in the workspace (w1 / w2)
-__device__ __forceinline__ int multicontact_box(const CcdWS& w, int fidx, const float* x1, const float* x2, const CGeom& g1, const CGeom& g2) {
+// collision_gjk.py:1427-1456 _intersect1 / _intersect2: up to two common entries, in a1's order
+__device__ __forceinline__ int mesh_intersect(const int* a1, int n1, const int* a2, int n2, int* res) {
+  int count = 0;
+  for (int i = 0; i < n1; i++)
+    for (int j = 0; j < n2; j++)
+      if (a1[i] == a2[j]) {
+        res[count++] = a1[i];
+        if (count == 2) return 2;
+      }
+  return count;
+}
+
+// collision_gjk.py:1460-1527 _mesh_normals (nout: LDS, stride 3; iout: LDS)
+__device__ __forceinline__ int mesh_normals(int dim, const int* fi, const CGeom& g, float* nout, int* iout, int ndeg) {
+  const int v1 = fi[0], v2 = fi[1], v3 = fi[2];
+  int edge[2], face[2], n;
+  if (dim == 3) {
+    n = mesh_intersect(g.pmap + g.pmapadr[v1], g.pmapnum[v1], g.pmap + g.pmapadr[v2], g.pmapnum[v2], edge);
+    if (n == 0) return 0;
+    n = mesh_intersect(edge, n, g.pmap + g.pmapadr[v3], g.pmapnum[v3], face);
+    if (n == 0) return 0;
+    const float* pn = g.pnormal + 3 * face[0];
+    rot_apply(nout, g.rot, pn[0], pn[1], pn[2]);
+    iout[0] = face[0];
+    return 1;
+  }
+  if (dim == 2) {
+    n = mesh_intersect(g.pmap + g.pmapadr[v1], g.pmapnum[v1], g.pmap + g.pmapadr[v2], g.pmapnum[v2], edge);
+    for (int i = 0; i < n; i++) {
+      const float* pn = g.pnormal + 3 * edge[i];
+      rot_apply(nout + 3 * i, g.rot, pn[0], pn[1], pn[2]);
+      iout[i] = edge[i];
+    }
+    return n;
+  }
+  if (dim == 1) {
+    const int num = min(g.pmapnum[v1], ndeg);
+    for (int i = 0; i < num; i++) {
+      const int idx = g.pmap[g.pmapadr[v1] + i];
+      const float* pn = g.pnormal + 3 * idx;
+      rot_apply(nout + 3 * i, g.rot, pn[0], pn[1], pn[2]);
+      iout[i] = idx;
+    }
+    return num;
+  }
+  return 0;
+}
+
+// collision_gjk.py:1530-1574 _mesh_edge_normals
+__device__ __forceinline__ int mesh_edge_normals(int dim, const CGeom& g, const float* v1, const float* v2, int v1i, float* nout, float* endvert,
+                                                 int ndeg) {
+  if (dim == 2) {
+    st3(endvert, v2);
+    float t[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
+    normalize3(t);
+    st3(nout, t);
+    return 1;
+  }
+  if (dim == 1) {
+    const int num = min(g.pmapnum[v1i], ndeg);
+    for (int i = 0; i < num; i++) {
+      const int idx = g.pmap[g.pmapadr[v1i] + i];
+      const int adr = g.pvadr[idx], nv = g.pvnum[idx];
+      for (int j = 0; j < nv; j++) {
+        if (g.pvert[adr + j] != v1i) continue;
+        const int k = j == 0 ? nv - 1 : j - 1;
+        const float* vk = g.mv + 3 * g.pvert[adr + k];
+        float e[3];
+        rot_apply(e, g.rot, vk[0], vk[1], vk[2]);
+        for (int c = 0; c < 3; c++) e[c] += g.pos[c];
+        st3(endvert + 3 * i, e);
+        float t[3] = {e[0] - v1[0], e[1] - v1[1], e[2] - v1[2]};
+        normalize3(t);
+        st3(nout + 3 * i, t);
+      }
+    }
+    return num;
+  }
+  return 0;
+}
+
+// collision_gjk.py:1765-1787 _mesh_face: polygon idx in world coordinates, its loop reversed
+__device__ __forceinline__ int mesh_face(const CGeom& g, int idx, float* fo, int npoly) {
+  const int adr = g.pvadr[idx], nv = min(g.pvnum[idx], npoly);
+  int j = 0;
+  for (int i = nv - 1; i >= 0; i--, j++) {
+    const float* v = g.mv + 3 * g.pvert[adr + i];
+    float e[3];
+    rot_apply(e, g.rot, v[0], v[1], v[2]);
+    for (int c = 0; c < 3; c++) fo[3 * j + c] = e[c] + g.pos[c];
+  }
+  return nv;
+}
+
+// collision_gjk.py:1929-2150 multicontact (boxes, and meshes with polygon data); witnesses in the
+// workspace (w1 / w2)
+__device__ __forceinline__ int multicontact(const CcdWS& w, int fidx, const float* x1, const float* x2, const CGeom& g1, const CGeom& g2) {
   float* W1 = w.W + w.L.w1;
   float* W2 = w.W + w.L.w2;
   st3(W1, x1);
@@ -914,13 +1028,14 @@ __device__ __forceinline__ int multicontact_box(const CcdWS& w, int fidx, const 
   const int nface1 = feature_dim(w, face, 0, fi1, fs1);
   const int nface2 = feature_dim(w, face, 1, fi2, fs2);
   float dir[3] = {x2[0] - x1[0], x2[1] - x1[1], x2[2] - x1[2]}, dneg[3] = {-dir[0], -dir[1], -dir[2]};
+  const int ndeg = w.L.ndeg, npoly = w.L.npoly;
   float* n1 = w.W + w.L.nrm;
-  float* n2 = n1 + 9;
+  float* n2 = n1 + 3 * ndeg;
   int* idx1 = reinterpret_cast<int*>(w.W + w.L.idx);
-  int* idx2 = idx1 + 3;
+  int* idx2 = idx1 + ndeg;
   float* endvert = w.W + w.L.endvert;
-  int nn1 = box_normals(nface1, fi1, g1.rot, dneg, n1, idx1);
-  int nn2 = box_normals(nface2, fi2, g2.rot, dir, n2, idx2);
+  int nn1 = g1.type == GEOM_BOX ? box_normals(nface1, fi1, g1.rot, dneg, n1, idx1) : mesh_normals(nface1, fi1, g1, n1, idx1, ndeg);
+  int nn2 = g2.type == GEOM_BOX ? box_normals(nface2, fi2, g2.rot, dir, n2, idx2) : mesh_normals(nface2, fi2, g2, n2, idx2, ndeg);
   const float face_tol = cosf(0.0016f), edge_tol = sinf(0.0016f);
   int edge1 = 0, edge2 = 0, ri = 0, rj = 0;
   bool found = false;
@@ -929,14 +1044,16 @@ __device__ __forceinline__ int multicontact_box(const CcdWS& w, int fidx, const 
       if (dot3(n1 + 3 * i, n2 + 3 * j) < -face_tol) { ri = i; rj = j; found = true; break; }
   if (!found) {
     if (nface1 < 3 && nface1 <= nface2) {
-      nn1 = box_edge_normals(nface1, g1, w.vert(fs1[0]), w.vert(fs1[1]), fi1[0], n1, endvert);
+      nn1 = g1.type == GEOM_BOX ? box_edge_normals(nface1, g1, w.vert(fs1[0]), w.vert(fs1[1]), fi1[0], n1, endvert)
+                                : mesh_edge_normals(nface1, g1, w.vert(fs1[0]), w.vert(fs1[1]), fi1[0], n1, endvert, ndeg);
       for (int i = 0; i < nn2 && !found; i++)
         for (int j = 0; j < nn1; j++)
           if (fabsf(dot3(n1 + 3 * j, n2 + 3 * i)) < edge_tol) { ri = j; rj = i; found = true; break; }
       if (!found) return 1;
       edge1 = 1;
     } else if (nface2 < 3) {
-      nn2 = box_edge_normals(nface2, g2, w.vert(fs2[0]), w.vert(fs2[1]), fi2[0], n2, endvert);
+      nn2 = g2.type == GEOM_BOX ? box_edge_normals(nface2, g2, w.vert(fs2[0]), w.vert(fs2[1]), fi2[0], n2, endvert)
+                                : mesh_edge_normals(nface2, g2, w.vert(fs2[0]), w.vert(fs2[1]), fi2[0], n2, endvert, ndeg);
       for (int i = 0; i < nn1 && !found; i++)
         for (int j = 0; j < nn2; j++)
           if (fabsf(dot3(n2 + 3 * j, n1 + 3 * i)) < edge_tol) { ri = j; rj = i; found = true; break; }
@@ -954,14 +1071,15 @@ __device__ __forceinline__ int multicontact_box(const CcdWS& w, int fidx, const 
     st3(f1 + 3, endvert + 3 * ri);
     nf1 = 2;
   } else {
-    nf1 = box_face(g1, edge2 ? idx1[rj] : idx1[ri], f1);
+    const int ind = edge2 ? idx1[rj] : idx1[ri];
+    nf1 = g1.type == GEOM_BOX ? box_face(g1, ind, f1) : mesh_face(g1, ind, f1, npoly);
   }
   if (edge2) {
     st3(f2, w.vert(2 * face[0] + 1));
     st3(f2 + 3, endvert + 3 * ri);
     nf2 = 2;
   } else {
-    nf2 = box_face(g2, idx2[rj], f2);
+    nf2 = g2.type == GEOM_BOX ? box_face(g2, idx2[rj], f2) : mesh_face(g2, idx2[rj], f2, npoly);
   }
   const float dl = sqrtf(dot3(dir, dir));
   float ad[3], nrm[3];
@@ -980,17 +1098,23 @@ __device__ __forceinline__ int multicontact_box(const CcdWS& w, int fidx, const 
   return polygon_clip(w, f1, nf1, f2, nf2, nrm, ad, W1, W2);
 }
 
+// box-box (the KAT kernel's name for it)
+__device__ __forceinline__ int multicontact_box(const CcdWS& w, int fidx, const float* x1, const float* x2, const CGeom& g1, const CGeom& g2) {
+  return multicontact(w, fidx, x1, x2, g1, g2);
+}
+
 // collision_gjk.py:2200-2345 ccd + collision_convex.py:763-852: contacts of one convex pair.
 // Returns the contact count (0: not penetrating); *dist is corrected by +margin, `normal` is
 // unnormalized (frame = make_frame(normal)), points in pts (stride 3, up to 4).
 __device__ __forceinline__ void put_cgeom(float* dst, const float* pos, const float* rot, const float* size, int type, int vertadr = 0,
-                                          int nvert = 0) {
+                                          int nvert = 0, int meshid = -1) {
   for (int i = 0; i < 3; i++) { dst[i] = pos[i]; dst[12 + i] = size[i]; }
   for (int i = 0; i < 9; i++) dst[3 + i] = rot[i];
   dst[15] = 0.0f;
   dst[16] = __int_as_float(type);
   dst[17] = __int_as_float(vertadr);
   dst[18] = __int_as_float(nvert);
+  dst[19] = __int_as_float(meshid);
 }
 
 // lane `lane` (< CCD_OUT) of the record of a convex pair from the lockstep workspace's result
@@ -1004,7 +1128,7 @@ __device__ __forceinline__ float ccd_record_word(int lane, int nc, const float* 
   return j == 0 ? Wout[0] : Wout[4 + 3 * q + j - 1];
 }
 
-__device__ __forceinline__ CGeom get_cgeom(const float* src, const float* mesh_vert) {
+__device__ __forceinline__ CGeom get_cgeom(const float* src, const float* mesh_vert, const MeshPoly* P = nullptr) {
   CGeom g;
   for (int i = 0; i < 3; i++) { g.pos[i] = src[i]; g.size[i] = src[12 + i]; }
   for (int i = 0; i < 9; i++) g.rot[i] = src[3 + i];
@@ -1013,7 +1137,30 @@ __device__ __forceinline__ CGeom get_cgeom(const float* src, const float* mesh_v
   g.mv = mesh_vert ? mesh_vert + 3 * (long)__float_as_int(src[17]) : nullptr;
   g.nvert = mesh_vert ? __float_as_int(src[18]) : 0;
   g.prism = nullptr;
+  g.pnormal = nullptr;
+  g.pvadr = g.pvnum = g.pvert = g.pmapadr = g.pmapnum = g.pmap = nullptr;
+  const int mid = __float_as_int(src[19]);
+  if (P && g.type == GEOM_MESH && mid >= 0 && P->polynum[mid] > 0) {
+    const int pa = P->polyadr[mid], va = P->vertadr[mid];
+    g.pnormal = P->polynormal + 3 * pa;
+    g.pvadr = P->polyvertadr + pa;
+    g.pvnum = P->polyvertnum + pa;
+    g.pvert = P->polyvert;
+    g.pmapadr = P->polymapadr + va;
+    g.pmapnum = P->polymapnum + va;
+    g.pmap = P->polymap;
+  }
   return g;
+}
+
+// the model's mesh polygon arrays
+__device__ __forceinline__ MeshPoly mesh_poly(const mjw_model_t& m) {
+  MeshPoly P;
+  P.polynormal = m.mesh_polynormal;
+  P.polyadr = m.mesh_polyadr; P.polynum = m.mesh_polynum; P.polyvertadr = m.mesh_polyvertadr; P.polyvertnum = m.mesh_polyvertnum;
+  P.polyvert = m.mesh_polyvert; P.polymapadr = m.mesh_polymapadr; P.polymapnum = m.mesh_polymapnum; P.polymap = m.mesh_polymap;
+  P.vertadr = m.mesh_vertadr;
+  return P;
 }
 
 // collision_gjk.py:2200-2345 ccd: distance (or depth) of one convex pair and its first witness points.
@@ -1081,8 +1228,10 @@ __device__ __forceinline__ int ccd_raw(const CcdWS& w, int epa_it, float toleran
     for (int i = 0; i < 3; i++) x1[i] = x2[i] = 0.0f;
     return 0;
   }
-  // multi-contact: no margin, boxes only in this build (the reference also takes meshes with polygon data)
-  *idx = (g1.margin != 0.0f || g2.margin != 0.0f || !(g1.type == GEOM_BOX && g2.type == GEOM_BOX)) ? -1 : f;
+  // collision_gjk.py:2336-2345: multi-contact needs no margin and boxes or meshes (with polygon data,
+  // collision_convex.py:810-818); the caller applies MULTICCD (box-box always, collision_convex.py:809)
+  const bool bm1 = g1.type == GEOM_BOX || (g1.type == GEOM_MESH && g1.pnormal), bm2 = g2.type == GEOM_BOX || (g2.type == GEOM_MESH && g2.pnormal);
+  *idx = (g1.margin != 0.0f || g2.margin != 0.0f || !bm1 || !bm2) ? -1 : f;
   return 1;
 }
 
@@ -1092,12 +1241,14 @@ __device__ __forceinline__ int ccd_raw(const CcdWS& w, int epa_it, float toleran
 // points.  Returns the contact count (0: not penetrating).  Only scalars and the LDS base cross the
 // call, so the CCD code does not touch the caller's register budget.
 // cutoff > 0 (collision sensors, collision_convex.py:772-776): separated pairs are reported too
+// P / multiccd / npoly / ndeg: the mesh polygon data, opt MULTICCD and the layout's multi-contact bounds
 __device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, int gjk_it, float margin, const float* mesh_vert = nullptr,
-                                       float cutoff = 0.0f) {
+                                       float cutoff = 0.0f, const MeshPoly* P = nullptr, bool multiccd = false, int npoly = 4,
+                                       int ndeg = 3) {
   CcdWS w;
   w.W = W;
-  w.L = ccd_layout(epa_it);
-  CGeom g1 = get_cgeom(W + w.L.geoms, mesh_vert), g2 = get_cgeom(W + w.L.geoms + CGEOM_WORDS, mesh_vert);
+  w.L = ccd_layout(epa_it, false, npoly, ndeg);
+  CGeom g1 = get_cgeom(W + w.L.geoms, mesh_vert, P), g2 = get_cgeom(W + w.L.geoms + CGEOM_WORDS, mesh_vert, P);
   float* dist_out = W + w.L.out;
   float* normal = W + w.L.out + 1;
   float* pts = W + w.L.out + 4;
@@ -1113,7 +1264,8 @@ __device__ __forceinline__ int ccd_pair(float* W, int epa_it, float tolerance, i
   float* W2 = w.W + w.L.w2;
   st3(W1, x1);
   st3(W2, x2);
-  if (idx > -1) n = multicontact_box(w, idx, x1, x2, g1, g2);
+  // collision_convex.py:809: box-box always, box-mesh / mesh-mesh under MULTICCD
+  if (idx > -1 && (multiccd || (g1.type == GEOM_BOX && g2.type == GEOM_BOX))) n = multicontact(w, idx, x1, x2, g1, g2);
   for (int i = 0; i < n; i++)
     for (int k = 0; k < 3; k++) pts[3 * i + k] = 0.5f * (W1[3 * i + k] + W2[3 * i + k]);
   for (int k = 0; k < 3; k++) normal[k] = W1[k] - W2[k];

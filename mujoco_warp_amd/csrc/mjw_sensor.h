@@ -447,7 +447,8 @@ __device__ void sensor_convex_records(const mjw_model_t& m, const Frames& F, int
   const float* gsize = MR(geom_size);
   const float* gmargin = MR(geom_margin);
   const float* mesh_vert = MR(mesh_vert);
-  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0, m.nmaxpolygon, m.nmaxmeshdeg);
+  const MeshPoly MP = mesh_poly(m);
   const int lane = (int)(threadIdx.x & 63);
   for (int k = 0; k < m.nsensor; k++) {
     const int t = m.sensor_type[k];
@@ -482,11 +483,12 @@ __device__ void sensor_convex_records(const mjw_model_t& m, const Frames& F, int
         continue;
       }
       put_cgeom(W + CL.geoms, F.gxpos + 3 * g1, F.gxmat + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0,
-                md1 >= 0 ? m.mesh_vertnum[md1] : 0);
+                md1 >= 0 ? m.mesh_vertnum[md1] : 0, md1);
       put_cgeom(W + CL.geoms + CGEOM_WORDS, F.gxpos + 3 * g2, F.gxmat + 9 * g2, gsize + 3 * g2, t2, md2 >= 0 ? m.mesh_vertadr[md2] : 0,
-                md2 >= 0 ? m.mesh_vertnum[md2] : 0);
+                md2 >= 0 ? m.mesh_vertnum[md2] : 0, md2);
       __syncthreads();
-      const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, margin, mesh_vert, 1.0e32f);
+      const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations, margin, mesh_vert, 1.0e32f, &MP,
+                              (m.opt_enableflags & ENBL_MULTICCD) != 0, m.nmaxpolygon, m.nmaxmeshdeg);
       if (lane == 0) {
         const float* o = W + CL.out;
         float nrm[3] = {o[1], o[2], o[3]};

@@ -29,7 +29,7 @@ __host__ inline SLay make_slayout(const mjw_model_t& m) {
   // collision sensors on convex pairs: the lockstep GJK / EPA workspace and the per-record results
   L.ccd = L.scc = -1;
   if (m.nsensorccd > 0) {
-    L.ccd = take(ccd_layout(m.ccd_epa_iterations, m.nhfield > 0).total);
+    L.ccd = take(ccd_layout(m.ccd_epa_iterations, m.nhfield > 0, m.nmaxpolygon, m.nmaxmeshdeg).total);
     L.scc = take(SCC_WORDS * m.nsensorcollision);
   }
   L.total = o;

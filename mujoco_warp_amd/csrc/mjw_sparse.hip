@@ -2271,9 +2271,10 @@ template <bool HF>  // HF: with the heightfield pairs (see the dense pre-pass)
 __device__ __forceinline__ void ccd_body(const mjw_model_t& m, const mjw_data_t& d) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wid = blockIdx.x, lane = (int)threadIdx.x;
-  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, HF && m.nhfield > 0);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, HF && m.nhfield > 0, m.nmaxpolygon, m.nmaxmeshdeg);
   float* W = smem;
   int* list = reinterpret_cast<int*>(smem + CL.total);
+  const MeshPoly MP = mesh_poly(m);
   const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
   const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;
   const float* gsize = MR(geom_size);
@@ -2309,13 +2310,15 @@ __device__ __forceinline__ void ccd_body(const mjw_model_t& m, const mjw_data_t&
         __syncthreads();
         continue;
       }
-      put_cgeom(W + CL.geoms, gx + 3 * g1, gm + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0, md1 >= 0 ? m.mesh_vertnum[md1] : 0);
+      put_cgeom(W + CL.geoms, gx + 3 * g1, gm + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0, md1 >= 0 ? m.mesh_vertnum[md1] : 0,
+                md1);
       put_cgeom(W + CL.geoms + CGEOM_WORDS, gx + 3 * g2, gm + 9 * g2, gsize + 3 * g2, t2, md2 >= 0 ? m.mesh_vertadr[md2] : 0,
-                md2 >= 0 ? m.mesh_vertnum[md2] : 0);
+                md2 >= 0 ? m.mesh_vertnum[md2] : 0, md2);
       __syncthreads();
       const int pid = m.nxn_pairid[2 * q];  // explicit <pair>: its own margin (collision_core.py:271)
       const int nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations,
-                              pid > -1 ? MR(pair_margin)[pid] : gmargin[g1] + gmargin[g2], mesh_vert);
+                              pid > -1 ? MR(pair_margin)[pid] : gmargin[g1] + gmargin[g2], mesh_vert, 0.0f, &MP,
+                              (m.opt_enableflags & ENBL_MULTICCD) != 0, m.nmaxpolygon, m.nmaxmeshdeg);
       float* out = d.ccd_out + ((long)wid * m.nxn_ccd + m.nxn_ccdid[q]) * CCD_OUT;
       if (lane < CCD_OUT) out[lane] = ccd_record_word(lane, nc, W + CL.out);
       __syncthreads();
@@ -3334,7 +3337,7 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
     hipLaunchKernelGGL(sp::forward_kernel<sp::SP_POS_A>, dim3(nw), dim3(sp::BLK), 0, s, *m, *d, fwd);
     trace_launch(s, K_SP_POS);
     if (ccd) {
-      const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations, m->nhfield > 0).total + 64) * 4;
+      const size_t lds = ((size_t)ccd_layout(m->ccd_epa_iterations, m->nhfield > 0, m->nmaxpolygon, m->nmaxmeshdeg).total + 64) * 4;
       if (m->nhfield > 0) {
         hipLaunchKernelGGL(sp::ccd_hf_kernel, dim3(nw), dim3(64), lds, s, *m, *d);
         trace_launch(s, K_SP_CCD_HF);

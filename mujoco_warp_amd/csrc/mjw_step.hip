@@ -105,7 +105,7 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
   // otherwise the workspace gets its own LDS
   L.ccd = -1;
   if (ccd && m.nxn_ccd > 0) {
-    const int need = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0).total;
+    const int need = ccd_layout(m.ccd_epa_iterations, m.nhfield > 0, m.nmaxpolygon, m.nmaxmeshdeg).total;
     if (nofactor) L.ccd = (usz >= need) ? L.ximat : take(need);
     else L.ccd = (L.qM - L.cdof_dot >= need) ? L.cdof_dot : take(need);
   }
@@ -2647,8 +2647,9 @@ __device__ __forceinline__ void ccd_body(const mjw_model_t& m, const mjw_data_t&
     }
   }
   if (L.ccd < 0) return;  // no convex pair (the lockstep workspace is not allocated)
-  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, HF && m.nhfield > 0);
+  const CcdLay CL = ccd_layout(m.ccd_epa_iterations, HF && m.nhfield > 0, m.nmaxpolygon, m.nmaxmeshdeg);
   float* W = s + L.ccd;
+  const MeshPoly MP = mesh_poly(m);
   for (int p = 0; p < m.nxn; p++) {
     const int slot = m.nxn_ccdid[p];
     if (slot < 0) continue;
@@ -2676,12 +2677,13 @@ __device__ __forceinline__ void ccd_body(const mjw_model_t& m, const mjw_data_t&
     if (pass) {
       const int md1 = t1 == GEOM_MESH ? m.geom_dataid[g1] : -1, md2 = t2 == GEOM_MESH ? m.geom_dataid[g2] : -1;
       put_cgeom(W + CL.geoms, s + L.gxpos + 3 * g1, s + L.gxmat + 9 * g1, gsize + 3 * g1, t1, md1 >= 0 ? m.mesh_vertadr[md1] : 0,
-                md1 >= 0 ? m.mesh_vertnum[md1] : 0);
+                md1 >= 0 ? m.mesh_vertnum[md1] : 0, md1);
       put_cgeom(W + CL.geoms + CGEOM_WORDS, s + L.gxpos + 3 * g2, s + L.gxmat + 9 * g2, gsize + 3 * g2, t2,
-                md2 >= 0 ? m.mesh_vertadr[md2] : 0, md2 >= 0 ? m.mesh_vertnum[md2] : 0);
+                md2 >= 0 ? m.mesh_vertadr[md2] : 0, md2 >= 0 ? m.mesh_vertnum[md2] : 0, md2);
       const int pid = m.nxn_pairid[2 * p];  // explicit <pair>: its own margin (collision_core.py:271)
       nc = ccd_pair(W, m.ccd_epa_iterations, MR(opt_ccd_tolerance)[0], m.opt_ccd_iterations,
-                    pid > -1 ? MR(pair_margin)[pid] : geom_margin[g1] + geom_margin[g2], mesh_vert);
+                    pid > -1 ? MR(pair_margin)[pid] : geom_margin[g1] + geom_margin[g2], mesh_vert, 0.0f, &MP,
+                    (m.opt_enableflags & ENBL_MULTICCD) != 0, m.nmaxpolygon, m.nmaxmeshdeg);
     }
     float* out = d.ccd_out + ((long)wid * m.nxn_ccd + slot) * CCD_OUT;
     if (lane < CCD_OUT) out[lane] = ccd_record_word(lane, nc, W + CL.out);

@@ -161,17 +161,37 @@ def put_model(mjm, device=None) -> types.Model:
     if t not in (_SUPPORTED_PAIRS | _SPARSE_PAIRS | _SPARSE_CCD_PAIRS if sparse else _SUPPORTED_PAIRS):
       names = tuple(types.GeomType(x).name for x in t)
       raise NotImplementedError(f"collision between {names[0]} and {names[1]} is not supported by this build yet.")
-  if mjm.opt.enableflags & EnableBit.MULTICCD and any(
-      tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) in _CONVEX_TABLE - {(6, 6)} and 1 not in (int(mjm.geom_type[a]), int(mjm.geom_type[b])) for a, b in pairs_chk):
-    # collision_convex.py:1130-1137: multi-contact of convex pairs other than box-box needs the mesh polygon data
-    raise NotImplementedError("MULTICCD for convex pairs other than box-box (mesh multi-contact) is not supported by this build yet.")
   if mjm.opt.disableflags & DisableBit.NATIVECCD and any(
       tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) == (6, 6) for a, b in pairs_chk):
     raise NotImplementedError("box-box with NATIVECCD disabled (primitive box_box) is not supported by this build yet.")
-  for pid in range(int(getattr(mjm, "npair", 0))):  # io.py:405-410: margins on box / mesh pairs
-    t1, t2 = int(mjm.geom_type[mjm.pair_geom1[pid]]), int(mjm.geom_type[mjm.pair_geom2[pid]])
-    if mjm.pair_margin[pid] and t1 in (types.GeomType.BOX, types.GeomType.MESH) and t2 in (types.GeomType.BOX, types.GeomType.MESH):
-      raise NotImplementedError(f"pair {pid} has non-zero margin ({mjm.pair_margin[pid]}) with NATIVECCD enabled. Set margin to 0 or disable NATIVECCD.")
+  # io.py:372-409: margins on the multi-contact pairs (box-box always, box-mesh / mesh-mesh under MULTICCD).
+  # One deviation: the reference also rejects box-box *geom* margins under NATIVECCD, which rejects its own
+  # apollo benchmark (the hand plates, margin 5e-4, BASELINE.json configs[3]); here those pairs run, and
+  # ccd() takes them as it does every pair with a margin -- one EPA contact, no multi-contact
+  # (collision_gjk.py:2336-2338).  Explicit <pair> margins keep the reference's check.
+  multiccd = bool(mjm.opt.enableflags & EnableBit.MULTICCD)
+  nativeccd_off = bool(mjm.opt.disableflags & DisableBit.NATIVECCD)
+  kinds_chk = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in pairs_chk]
+  if (6, 6) in kinds_chk or (multiccd and ((6, 7) in kinds_chk or (7, 7) in kinds_chk)) or int(getattr(mjm, "npair", 0)):
+    def _check_margin(name, t1, t2, margin, explicit=False):
+      if multiccd:
+        raise NotImplementedError(f"{name} has non-zero margin ({margin}) with MULTICCD enabled. Set margin to 0 or disable MULTICCD.")
+      if explicit and t1 in boxmesh and t2 in boxmesh and not nativeccd_off:
+        raise NotImplementedError(f"{name} has non-zero margin ({margin}) with NATIVECCD enabled. Set margin to 0 or disable NATIVECCD.")
+
+    boxmesh = (types.GeomType.BOX, types.GeomType.MESH)
+    pair_set = {(int(a), int(b)) for a, b in zip(getattr(mjm, "pair_geom1", []), getattr(mjm, "pair_geom2", []))}
+    for g1, g2 in pairs_chk:
+      if (int(g1), int(g2)) in pair_set or (int(g2), int(g1)) in pair_set:
+        continue
+      t1, t2 = int(mjm.geom_type[g1]), int(mjm.geom_type[g2])
+      m1, m2 = float(mjm.geom_margin[g1]), float(mjm.geom_margin[g2])
+      if (m1 or m2) and t1 in boxmesh and t2 in boxmesh:
+        _check_margin(f"geom pair ({g1}, {g2})", t1, t2, (m1, m2))
+    for pid in range(int(getattr(mjm, "npair", 0))):
+      t1, t2 = int(mjm.geom_type[mjm.pair_geom1[pid]]), int(mjm.geom_type[mjm.pair_geom2[pid]])
+      if mjm.pair_margin[pid] and t1 in boxmesh and t2 in boxmesh:
+        _check_margin(f"pair {pid}", t1, t2, float(mjm.pair_margin[pid]), explicit=True)
   muscle = _muscle_mask(mjm)
   if np.any(muscle):
     lr = np.asarray(mjm.actuator_lengthrange, np.float64).reshape(-1, 2)[muscle]
@@ -283,6 +303,14 @@ def put_model(mjm, device=None) -> types.Model:
   m.nxn_ccdid = _i32(np.where([k in ccd_set for k in kinds], ccdid, -1) if kinds else np.zeros(0), dev)
   m.nmesh, m.nmeshvert = int(getattr(mjm, "nmesh", 0)), int(getattr(mjm, "nmeshvert", 0))
   m.nhfield, m.nhfielddata = int(getattr(mjm, "nhfield", 0)), int(getattr(mjm, "nhfielddata", 0))
+  m.nmeshpoly, m.nmeshpolyvert = int(getattr(mjm, "nmeshpoly", 0)), int(getattr(mjm, "nmeshpolyvert", 0))
+  m.nmeshpolymap = int(getattr(mjm, "nmeshpolymap", 0))
+  # multi-contact workspace (collision_convex.py:1120-1140): 4-gon faces / 3 normals per vertex for box-box;
+  # with MULTICCD and box-mesh / mesh-mesh pairs the meshes' largest polygon and vertex degree
+  mesh_multi = bool(mjm.opt.enableflags & EnableBit.MULTICCD) and any(
+    tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) in ((6, 7), (7, 7)) for a, b in nxn_geom_pairs(mjm)[0])
+  m.nmaxpolygon = max(4, int(np.max(mjm.mesh_polyvertnum))) if mesh_multi and m.nmeshpoly else 4
+  m.nmaxmeshdeg = max(3, int(np.max(mjm.mesh_polymapnum))) if mesh_multi and m.nmeshpoly else 3
   m.nlimited = len(jnt_limited_sh)
   m.nlimited_ball = len(jnt_limited_ball)
   m.neq_cw = int(np.isin(mjm.eq_type, (types.EqType.CONNECT, types.EqType.WELD)).sum()) if mjm.neq else 0
@@ -301,7 +329,7 @@ def put_model(mjm, device=None) -> types.Model:
   nconvex = sum(k in _CONVEX_TABLE for k in gkinds)
   nboxbox = sum(k == (6, 6) for k in gkinds)
   m.ccd_epa_iterations = 16 if nconvex and nboxbox == nconvex else int(getattr(mjm.opt, "ccd_iterations", 35))
-  if m.nsensorccd and 37 * mjm.nbody + 14 * mjm.nv + _ccd_words(m.ccd_epa_iterations) + 368 * (m.nhfield > 0) + 32 * m.nsensorcollision > 16384:
+  if m.nsensorccd and 37 * mjm.nbody + 14 * mjm.nv + _ccd_words(m.ccd_epa_iterations, m.nmaxpolygon, m.nmaxmeshdeg) + 368 * (m.nhfield > 0) + 32 * m.nsensorcollision > 16384:
     raise NotImplementedError("collision sensors on convex pairs: the sensor kernel's 64 KB of LDS is exceeded by this model.")
 
   # sparse path: kinematic trees as dof ranges (a tree starts at every dof without a parent dof),
@@ -411,10 +439,12 @@ _SENSOR_HFIELD = {k for k in _CONVEX_TABLE if k[0] == 1}  # ... and heightfields
 _SENSOR_PAIRS = _PRIMITIVE_PAIRS | {(0, 4), (0, 5), (2, 5)} | _SENSOR_CONVEX | _SENSOR_HFIELD
 
 
-def _ccd_words(it):
+def _ccd_words(it, npoly=4, ndeg=3):
   """Words of mjw_ccd.h's lockstep GJK / EPA workspace (ccd_layout, no heightfield scratch)."""
   cv, cf = 10 + 2 * it, 6 + 5 * it
-  return cv * 4 + cf * 5 + 24 + 36 + 8 + 4 + 18 + 6 + 9 + 12 + 12 + 24 + 8 + 48 + 48 + 12 + 12 + 38 + 32
+  npoly, ndeg = max(npoly, 4), max(ndeg, 3)
+  nclip = max(2 * npoly, 16)
+  return cv * 4 + cf * 5 + 24 + 36 + 8 + 4 + 2 * 20 + 32 + 12 + 12 + 6 * ndeg + 2 * ndeg + 3 * ndeg + 3 * npoly * 3 + npoly + 6 * nclip
 
 
 def _sensor_collision_pairs(mjm, pairid_all):

@@ -982,6 +982,20 @@ class _Compiler:
     m.mesh_vertadr = np.concatenate([[0], np.cumsum(m.mesh_vertnum)[:-1]]).astype(np.int32) if m.nmesh else np.zeros(0, np.int32)
     m.mesh_vert = np.concatenate([v for v, _ in self.mesh_data]) if m.nmesh else np.zeros((0, 3))
     m.nmeshvert = int(m.mesh_vertnum.sum())
+    # polygon data of each mesh's convex hull (MuJoCo's mesh_poly* fields; multi-contact, collision_gjk.py:1403-1790)
+    polys = [_mesh_polygons(v) for v, _ in self.mesh_data]
+    m.mesh_polynum = np.array([len(p[0]) for p in polys], dtype=np.int32)
+    m.mesh_polyadr = np.concatenate([[0], np.cumsum(m.mesh_polynum)[:-1]]).astype(np.int32) if m.nmesh else np.zeros(0, np.int32)
+    m.mesh_polynormal = np.concatenate([p[1] for p in polys]).reshape(-1, 3) if m.nmesh else np.zeros((0, 3))
+    loops = [lp for p in polys for lp in p[0]]
+    m.mesh_polyvertnum = np.array([len(lp) for lp in loops], dtype=np.int32)
+    m.mesh_polyvertadr = np.concatenate([[0], np.cumsum(m.mesh_polyvertnum)[:-1]]).astype(np.int32) if loops else np.zeros(0, np.int32)
+    m.mesh_polyvert = np.array([i for lp in loops for i in lp], dtype=np.int32)
+    pmaps = [mp for p in polys for mp in p[2]]  # per vertex (all meshes in order): its polygons
+    m.mesh_polymapnum = np.array([len(mp) for mp in pmaps], dtype=np.int32)
+    m.mesh_polymapadr = np.concatenate([[0], np.cumsum(m.mesh_polymapnum)[:-1]]).astype(np.int32) if pmaps else np.zeros(0, np.int32)
+    m.mesh_polymap = np.array([i for mp in pmaps for i in mp], dtype=np.int32)
+    m.nmeshpoly, m.nmeshpolyvert, m.nmeshpolymap = len(loops), len(m.mesh_polyvert), len(m.mesh_polymap)
 
   def _load_hfields(self, root):
     """<asset><hfield>: nrow x ncol elevation grid (row 0 at -y, MuJoCo's mjModel.hfield_data order), size =
@@ -2470,6 +2484,50 @@ def set_const(m: MjModel):
       vec[da] = m.actuator_gear[a, 0]
     acc0[a] = np.linalg.norm(Minv @ vec)
   m.actuator_acc0 = acc0
+
+
+def _mesh_polygons(v):
+  """Polygons of the convex hull of mesh vertices `v` (MuJoCo's mesh_poly* data): the hull's coplanar
+  triangles merged into one face each.  Returns (loops, normals, polymap): per polygon its vertex loop (mesh
+  vertex ids, counter-clockwise about the outward normal, starting at its smallest id), its outward unit
+  normal, and per vertex the polygons that contain it (ascending).  Polygons are ordered by their smallest
+  vertex id, then their loop.  Vertices off the hull map to no polygon."""
+  n = len(v)
+  if n < 4:
+    return [], np.zeros((0, 3)), [[] for _ in range(n)]
+  from scipy.spatial import ConvexHull
+
+  h = ConvexHull(v)
+  scale = max(float(np.abs(v).max()), 1e-12)
+  groups = []  # (normal, offset, triangles)
+  for tri, eq in zip(h.simplices, h.equations):
+    nrm, off = eq[:3], eq[3]
+    for g in groups:
+      if np.dot(g[0], nrm) > 1.0 - 1e-9 and abs(g[1] - off) < 1e-9 * scale:
+        g[2].append(tri)
+        break
+    else:
+      groups.append((nrm, off, [tri]))
+  polys = []
+  for nrm, _, tris in groups:
+    edges = {}
+    for a, b, c in tris:
+      if np.dot(np.cross(v[b] - v[a], v[c] - v[a]), nrm) < 0:
+        b, c = c, b
+      for e0, e1 in ((a, b), (b, c), (c, a)):
+        edges[(int(e0), int(e1))] = True
+    nxt = {e0: e1 for (e0, e1) in edges if (e1, e0) not in edges}  # boundary, counter-clockwise
+    start = min(nxt)
+    loop = [start]
+    while nxt[loop[-1]] != start and len(loop) <= len(nxt):
+      loop.append(nxt[loop[-1]])
+    polys.append((loop, nrm / np.linalg.norm(nrm)))
+  polys.sort(key=lambda p: (min(p[0]), p[0]))
+  pmap = [[] for _ in range(n)]
+  for k, (loop, _) in enumerate(polys):
+    for i in loop:
+      pmap[i].append(k)
+  return [p[0] for p in polys], np.array([p[1] for p in polys]).reshape(-1, 3), pmap
 
 
 def _hull_faces(v):

@@ -26,6 +26,7 @@ enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_
 enum { DSBL_CONSTRAINT = 1, DSBL_EQUALITY = 2, DSBL_FRICTIONLOSS = 4, DSBL_LIMIT = 8, DSBL_CONTACT = 16,
        DSBL_SPRING = 32, DSBL_DAMPER = 64, DSBL_GRAVITY = 128, DSBL_CLAMPCTRL = 256, DSBL_WARMSTART = 512,
        DSBL_FILTERPARENT = 1024, DSBL_ACTUATION = 2048, DSBL_REFSAFE = 4096, DSBL_SENSOR = 8192, DSBL_EULERDAMP = 1 << 15 };
+enum { ENBL_MULTICCD = 16 };
 enum { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF = 1, CNSTR_LIMIT_JOINT = 3, CNSTR_CONTACT_FRICTIONLESS = 5, CNSTR_CONTACT_PYRAMIDAL = 6,
        CNSTR_CONTACT_ELLIPTIC = 7 };
 enum { CONE_PYRAMIDAL = 0, CONE_ELLIPTIC = 1 };
@@ -1560,6 +1561,23 @@ static void plane_box_corner(int k, const real* n, const real* ppos, const real*
 
 #include "oracle_ccd.h"
 
+/* a mesh geom's vertices and polygon data (mesh_poly*) for the convex routines; meshid < 0: not a mesh */
+static void ccd_geom_mesh(const orc_model* m, int meshid, ccd_geom* g) {
+  if (meshid < 0) return;
+  const int va = m->mesh_vertadr[meshid], pa = m->mesh_polyadr[meshid];
+  g->vert = m->mesh_vert + 3 * va;
+  g->nvert = m->mesh_vertnum[meshid];
+  if (m->mesh_polynum[meshid] > 0) {
+    g->pnormal = m->mesh_polynormal + 3 * pa;
+    g->pvadr = m->mesh_polyvertadr + pa;
+    g->pvnum = m->mesh_polyvertnum + pa;
+    g->pvert = m->mesh_polyvert;
+    g->pmapadr = m->mesh_polymapadr + va;
+    g->pmapnum = m->mesh_polymapnum + va;
+    g->pmap = m->mesh_polymap;
+  }
+}
+
 /* collision_primitive_core.py:1103-1155 sphere_box */
 static real sphere_box(real* pos, real* nrm, const real* spos, real r, const real* bpos, const real* brot, const real* bsize) {
   real dif[3] = {spos[0] - bpos[0], spos[1] - bpos[1], spos[2] - bpos[2]}, center[3], clamped[3], cdir[3], tmp[3];
@@ -2009,11 +2027,10 @@ static void collision(const orc_model* m, orc_data* d) {
       cg1.type = t1; cg2.type = t2;
       memcpy(cg1.pos, p1, sizeof(cg1.pos)); memcpy(cg1.rot, r1, sizeof(cg1.rot)); memcpy(cg1.size, s1, sizeof(cg1.size));
       memcpy(cg2.pos, p2, sizeof(cg2.pos)); memcpy(cg2.rot, r2, sizeof(cg2.rot)); memcpy(cg2.size, s2, sizeof(cg2.size));
-      cg1.vert = t1 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g1]] : NULL;
-      cg1.nvert = t1 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g1]] : 0;
-      cg2.vert = t2 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g2]] : NULL;
-      cg2.nvert = t2 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g2]] : 0;
+      if (t1 == GEOM_MESH) ccd_geom_mesh(m, m->geom_dataid[g1], &cg1);
+      if (t2 == GEOM_MESH) ccd_geom_mesh(m, m->geom_dataid[g2], &cg2);
       real cdist, cnrm[3], cpts[4][3], cframe[9];
+      ccd_multiccd = (m->opt_enableflags & ENBL_MULTICCD) != 0;
       int nc = ccd_pair(&cg1, &cg2, m->opt_ccd_tolerance, m->opt_ccd_iterations, m->ccd_epa_iterations, margin, &cdist, cnrm, cpts);
       make_frame(cframe, cnrm);
       for (int k = 0; k < nc; k++) {
@@ -4064,7 +4081,15 @@ int orc_kat_hfield_support(const real* prism, const real* dir, real margin, real
 
 int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* size, const real* mesh_vert, const int* vertadr,
                 const int* vertnum, real margin, real tolerance, int iterations, int multiccd, real* out) {
+  return orc_kat_ccd_model(type, pos, mat, size, mesh_vert, vertadr, vertnum, margin, tolerance, iterations, multiccd, NULL, NULL, out);
+}
+
+/* orc_kat_ccd with the meshes' polygon data from model `pm` (meshid[k]: the geom's mesh, -1 for none) */
+int orc_kat_ccd_model(const int* type, const real* pos, const real* mat, const real* size, const real* mesh_vert, const int* vertadr,
+                      const int* vertnum, real margin, real tolerance, int iterations, int multiccd, const orc_model* pm,
+                      const int* meshid, real* out) {
   ccd_geom g[2], h1, h2;
+  memset(g, 0, sizeof(g));
   for (int k = 0; k < 2; k++) {
     memcpy(g[k].pos, pos + 3 * k, 3 * sizeof(real));
     memcpy(g[k].rot, mat + 9 * k, 9 * sizeof(real));
@@ -4073,15 +4098,16 @@ int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* s
     g[k].type = type[k];
     g[k].vert = type[k] == GEOM_MESH ? mesh_vert + 3 * vertadr[k] : NULL;
     g[k].nvert = type[k] == GEOM_MESH ? vertnum[k] : 0;
+    if (pm && meshid && type[k] == GEOM_MESH) ccd_geom_mesh(pm, meshid[k], &g[k]);
   }
   polytope* pt = ccd_polytope();
   real d, x1[3], x2[3];
   int idx;
   int ncon = ccd_raw(&g[0], &g[1], tolerance, (real)1e30, iterations, iterations, pt, &d, x1, x2, &idx, &h1, &h2);
-  if (multiccd && (type[0] == GEOM_MESH || type[1] == GEOM_MESH)) return -1;
+  if (multiccd && ((type[0] == GEOM_MESH && !g[0].pnormal) || (type[1] == GEOM_MESH && !g[1].pnormal))) return -1;
   if (multiccd && idx > -1) {
     real w1[4][3], w2[4][3];
-    ncon = multicontact_box(pt, idx, x1, x2, &h1, &h2, w1, w2);
+    ncon = multicontact(pt, idx, x1, x2, &h1, &h2, w1, w2);
   }
   out[0] = d;
   for (int i = 0; i < 3; i++) { out[1 + i] = x1[i]; out[4 + i] = x2[i]; }

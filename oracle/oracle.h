@@ -30,7 +30,8 @@ typedef ORC_REAL real;
   X(opt_ls_iterations) X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter) X(opt_ls_parallel) \
   X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
   X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)   \
-  X(ntendon) X(nwrap) X(nJten) X(npair) X(ngravcomp) X(has_fluid) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)
+  X(ntendon) X(nwrap) X(nJten) X(npair) X(ngravcomp) X(has_fluid) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)          \
+  X(nmeshpoly) X(nmeshpolyvert) X(nmeshpolymap)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
@@ -63,6 +64,7 @@ typedef ORC_REAL real;
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flex_vert, nflexvert * 3) X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)    \
   X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17) X(mesh_vert, nmeshvert * 3)      \
+  X(mesh_polynormal, nmeshpoly * 3)                                                                \
   X(hfield_size, nhfield * 4) X(hfield_data, nhfielddata)                                          \
   X(tendon_stiffness, ntendon) X(tendon_damping, ntendon) X(tendon_frictionloss, ntendon)          \
   X(tendon_armature, ntendon) X(tendon_margin, ntendon) X(tendon_range, ntendon * 2)               \
@@ -100,6 +102,8 @@ typedef ORC_REAL real;
   X(flex_centered, nflex) X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert)              \
   X(flex_edge, nflexedge * 2) X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata)          \
   X(flex_elemedge, nflexelem * 3) X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom) \
+  X(mesh_polyadr, nmesh) X(mesh_polynum, nmesh) X(mesh_polyvertadr, nmeshpoly) X(mesh_polyvertnum, nmeshpoly) \
+  X(mesh_polyvert, nmeshpolyvert) X(mesh_polymapadr, nmeshvert) X(mesh_polymapnum, nmeshvert) X(mesh_polymap, nmeshpolymap) \
   X(hfield_nrow, nhfield) X(hfield_ncol, nhfield) X(hfield_adr, nhfield)                          \
   X(tendon_adr, ntendon) X(tendon_num, ntendon) X(tendon_limited, ntendon) X(tendon_actfrclimited, ntendon) \
   X(wrap_objid, nwrap) X(wrap_type, nwrap) X(ten_J_rownnz, ntendon) X(ten_J_rowadr, ntendon) X(ten_J_colind, nJten)
@@ -184,6 +188,9 @@ int orc_kat_ccd(const int* type, const real* pos, const real* mat, const real* s
                 const int* vertnum, real margin, real tolerance, int iterations, int multiccd, real* out);
 void orc_kat_efc_row(int disableflags, real timestep, real pos_aref, real pos_imp, real invweight, const real* solref,
                      const real* solimp, real vel, real* out);
+int orc_kat_ccd_model(const int* type, const real* pos, const real* mat, const real* size, const real* mesh_vert, const int* vertadr,
+                      const int* vertnum, real margin, real tolerance, int iterations, int multiccd, const orc_model* pm,
+                      const int* meshid, real* out);
 int orc_kat_wrap(int fn, const real* a, int ind, real radius, real* out);
 int orc_kat_geom_triangle(int gt, const real* gp, const real* gr, const real* gs, const real* tri, real tr, real* out);
 void orc_ctrl_noise(const orc_model* m, real* ctrl, const real* center, int ncenter, int step, real std,

@@ -28,7 +28,16 @@ typedef struct {
   const real* vert; /* mesh vertices in the geom frame (GEOM_MESH) */
   int nvert;
   const real* prism; /* GEOM_HFIELD: the 6 prism vertices (heightfield frame); pos = the prism center */
+  /* GEOM_MESH polygon data (mesh_poly*, offset to this mesh: pnormal / pvadr / pvnum by its polygon address,
+   * pmapadr / pmapnum by its vertex address; pvert / pmap are the model's arrays, holding mesh-local vertex /
+   * polygon ids); pnormal == NULL: no polygon data (no mesh multi-contact) */
+  const real* pnormal;
+  const int *pvadr, *pvnum, *pvert, *pmapadr, *pmapnum, *pmap;
 } ccd_geom;
+
+/* multi-contact workspace bounds (the reference sizes its buffers by the model's nmaxpolygon / nmaxmeshdeg) */
+#define CCD_MAXPOLY 128
+#define CCD_MAXDEG 64
 
 typedef struct {
   int vertex_index;
@@ -790,7 +799,10 @@ static int box_face(const real* mat, const real* pos, const real* s, int idx, re
 static int polygon_clip(real face1[][3], int nface1, real face2[][3], int nface2, const real* n, const real* dir, real w1[4][3],
                         real w2[4][3]) {
   if (nface1 < 3) return 0;
-  real pn[8][3], pd[8], bufA[16][3], bufB[16][3];
+  static real pn[CCD_MAXPOLY][3], pd[CCD_MAXPOLY], bufA[2 * CCD_MAXPOLY][3], bufB[2 * CCD_MAXPOLY][3];
+#ifdef _OPENMP
+#pragma omp threadprivate(pn, pd, bufA, bufB)
+#endif
   real(*poly)[3] = bufA;
   real(*clip)[3] = bufB;
   for (int i = 0; i < nface1; i++) {
@@ -811,6 +823,7 @@ static int polygon_clip(real face1[][3], int nface1, real face2[][3], int nface2
       for (int k = 0; k < 3; k++) { dP[k] = P[k] - face1[e][k]; dQ[k] = Q[k] - face1[e][k]; }
       int in1 = dot3(dP, pn[e]) > -1e-10, in2 = dot3(dQ, pn[e]) > -1e-10;
       if (!in1 && !in2) continue;
+      if (nc >= 2 * CCD_MAXPOLY - 2) break;
       if (in1 && in2) { memcpy(clip[nc++], Q, 3 * sizeof(real)); continue; }
       real PQ[3] = {Q[0] - P[0], Q[1] - P[1], Q[2] - P[2]};
       real dt = dot3(pn[e], PQ);
@@ -841,9 +854,100 @@ static int polygon_clip(real face1[][3], int nface1, real face2[][3], int nface2
   return np;
 }
 
-/* collision_gjk.py:1929-2150 (box-box) */
-static int multicontact_box(const polytope* pt, int fidx, const real* x1, const real* x2, const ccd_geom* g1, const ccd_geom* g2,
-                            real w1[4][3], real w2[4][3]) {
+/* collision_gjk.py:1427-1456 _intersect1 / _intersect2: up to two common entries, in a1's order */
+static int mesh_intersect(const int* a1, int n1, const int* a2, int n2, int* res) {
+  int count = 0;
+  for (int i = 0; i < n1; i++)
+    for (int j = 0; j < n2; j++)
+      if (a1[i] == a2[j]) {
+        res[count++] = a1[i];
+        if (count == 2) return 2;
+      }
+  return count;
+}
+
+/* collision_gjk.py:1460-1527 _mesh_normals: the polygon normals a feature of up to 3 mesh vertices can lie on */
+static int mesh_normals(int dim, const int* fi, const ccd_geom* g, real nout[][3], int* iout) {
+  const int* mp = g->pmap;
+  const int v1 = fi[0], v2 = fi[1], v3 = fi[2];
+  int edge[2], face[2], n;
+  if (dim == 3) {
+    n = mesh_intersect(mp + g->pmapadr[v1], g->pmapnum[v1], mp + g->pmapadr[v2], g->pmapnum[v2], edge);
+    if (n == 0) return 0;
+    n = mesh_intersect(edge, n, mp + g->pmapadr[v3], g->pmapnum[v3], face);
+    if (n == 0) return 0;
+    const real* pn = g->pnormal + 3 * face[0];
+    matvec3r(nout[0], g->rot, pn[0], pn[1], pn[2]);
+    iout[0] = face[0];
+    return 1;
+  }
+  if (dim == 2) {
+    n = mesh_intersect(mp + g->pmapadr[v1], g->pmapnum[v1], mp + g->pmapadr[v2], g->pmapnum[v2], edge);
+    for (int i = 0; i < n; i++) {
+      const real* pn = g->pnormal + 3 * edge[i];
+      matvec3r(nout[i], g->rot, pn[0], pn[1], pn[2]);
+      iout[i] = edge[i];
+    }
+    return n;
+  }
+  if (dim == 1) {
+    const int num = g->pmapnum[v1];
+    for (int i = 0; i < num && i < CCD_MAXDEG; i++) {
+      const int idx = mp[g->pmapadr[v1] + i];
+      const real* pn = g->pnormal + 3 * idx;
+      matvec3r(nout[i], g->rot, pn[0], pn[1], pn[2]);
+      iout[i] = idx;
+    }
+    return num;
+  }
+  return 0;
+}
+
+/* collision_gjk.py:1530-1574 _mesh_edge_normals: directions of the edges along a feature's vertex v1 */
+static int mesh_edge_normals(int dim, const ccd_geom* g, const real* v1, const real* v2, int v1i, real nout[][3], real endvert[][3]) {
+  if (dim == 2) {
+    memcpy(endvert[0], v2, 3 * sizeof(real));
+    real t[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
+    normalize3(t);
+    memcpy(nout[0], t, sizeof(t));
+    return 1;
+  }
+  if (dim == 1) {
+    const int num = g->pmapnum[v1i];
+    for (int i = 0; i < num && i < CCD_MAXDEG; i++) {
+      const int idx = g->pmap[g->pmapadr[v1i] + i];
+      const int adr = g->pvadr[idx], nv = g->pvnum[idx];
+      for (int j = 0; j < nv; j++) {
+        if (g->pvert[adr + j] != v1i) continue;
+        const int k = j == 0 ? nv - 1 : j - 1;
+        const real* vk = g->vert + 3 * g->pvert[adr + k];
+        matvec3r(endvert[i], g->rot, vk[0], vk[1], vk[2]);
+        for (int c = 0; c < 3; c++) endvert[i][c] += g->pos[c];
+        real t[3] = {endvert[i][0] - v1[0], endvert[i][1] - v1[1], endvert[i][2] - v1[2]};
+        normalize3(t);
+        memcpy(nout[i], t, sizeof(t));
+      }
+    }
+    return num;
+  }
+  return 0;
+}
+
+/* collision_gjk.py:1765-1787 _mesh_face: polygon idx in world coordinates, its loop reversed */
+static int mesh_face(const ccd_geom* g, int idx, real fo[][3]) {
+  const int adr = g->pvadr[idx], nv = g->pvnum[idx];
+  int j = 0;
+  for (int i = nv - 1; i >= 0; i--, j++) {
+    const real* v = g->vert + 3 * g->pvert[adr + i];
+    matvec3r(fo[j], g->rot, v[0], v[1], v[2]);
+    for (int c = 0; c < 3; c++) fo[j][c] += g->pos[c];
+  }
+  return nv;
+}
+
+/* collision_gjk.py:1929-2150 multicontact (boxes and meshes with polygon data) */
+static int multicontact(const polytope* pt, int fidx, const real* x1, const real* x2, const ccd_geom* g1, const ccd_geom* g2,
+                        real w1[4][3], real w2[4][3]) {
   memcpy(w1[0], x1, 3 * sizeof(real));
   memcpy(w2[0], x2, 3 * sizeof(real));
   int face[3];
@@ -853,24 +957,29 @@ static int multicontact_box(const polytope* pt, int fidx, const real* x1, const 
   int nface1 = feature_dim(face, pt, 0, fi1, fv1);
   int nface2 = feature_dim(face, pt, 1, fi2, fv2);
   real dir[3] = {x2[0] - x1[0], x2[1] - x1[1], x2[2] - x1[2]}, dneg[3] = {-dir[0], -dir[1], -dir[2]};
-  real n1[3][3], n2[3][3], endvert[3][3];
-  int idx1[3] = {0, 0, 0}, idx2[3] = {0, 0, 0};
-  int nn1 = box_normals(nface1, fi1, g1->rot, dneg, n1, idx1);
-  int nn2 = box_normals(nface2, fi2, g2->rot, dir, n2, idx2);
+  static real n1[CCD_MAXDEG][3], n2[CCD_MAXDEG][3], endvert[CCD_MAXDEG][3], f1[CCD_MAXPOLY][3], f2[CCD_MAXPOLY][3];
+  static int idx1[CCD_MAXDEG], idx2[CCD_MAXDEG];
+#ifdef _OPENMP
+#pragma omp threadprivate(n1, n2, endvert, f1, f2, idx1, idx2)
+#endif
+  int nn1 = g1->type == GEOM_BOX ? box_normals(nface1, fi1, g1->rot, dneg, n1, idx1) : mesh_normals(nface1, fi1, g1, n1, idx1);
+  int nn2 = g2->type == GEOM_BOX ? box_normals(nface2, fi2, g2->rot, dir, n2, idx2) : mesh_normals(nface2, fi2, g2, n2, idx2);
   int edge1 = 0, edge2 = 0, ri = 0, rj = 0, found = 0;
   for (int i = 0; i < nn1 && !found; i++)
     for (int j = 0; j < nn2; j++)
       if (dot3(n1[i], n2[j]) < -ccd_face_tol()) { ri = i; rj = j; found = 1; break; }
   if (!found) {
     if (nface1 < 3 && nface1 <= nface2) {
-      nn1 = box_edge_normals(nface1, g1->rot, g1->pos, g1->size, fv1[0], fv1[1], fi1[0], n1, endvert);
+      nn1 = g1->type == GEOM_BOX ? box_edge_normals(nface1, g1->rot, g1->pos, g1->size, fv1[0], fv1[1], fi1[0], n1, endvert)
+                                 : mesh_edge_normals(nface1, g1, fv1[0], fv1[1], fi1[0], n1, endvert);
       for (int i = 0; i < nn2 && !found; i++) /* _aligned_face_edge(n1 edges, n2 faces) */
         for (int j = 0; j < nn1; j++)
           if (fabs(dot3(n1[j], n2[i])) < ccd_edge_tol()) { ri = j; rj = i; found = 1; break; }
       if (!found) return 1;
       edge1 = 1;
     } else if (nface2 < 3) {
-      nn2 = box_edge_normals(nface2, g2->rot, g2->pos, g2->size, fv2[0], fv2[1], fi2[0], n2, endvert);
+      nn2 = g2->type == GEOM_BOX ? box_edge_normals(nface2, g2->rot, g2->pos, g2->size, fv2[0], fv2[1], fi2[0], n2, endvert)
+                                 : mesh_edge_normals(nface2, g2, fv2[0], fv2[1], fi2[0], n2, endvert);
       for (int i = 0; i < nn1 && !found; i++) /* _aligned_face_edge(n2 edges, n1 faces) */
         for (int j = 0; j < nn2; j++)
           if (fabs(dot3(n2[j], n1[i])) < ccd_edge_tol()) { ri = j; rj = i; found = 1; break; }
@@ -880,21 +989,21 @@ static int multicontact_box(const polytope* pt, int fidx, const real* x1, const 
       return 1;
     }
   }
-  real f1[4][3], f2[4][3];
   int nf1, nf2;
   if (edge1) {
     memcpy(f1[0], pt->vert[2 * face[0]], 3 * sizeof(real));
     memcpy(f1[1], endvert[ri], 3 * sizeof(real));
     nf1 = 2;
   } else {
-    nf1 = box_face(g1->rot, g1->pos, g1->size, edge2 ? idx1[rj] : idx1[ri], f1);
+    const int ind = edge2 ? idx1[rj] : idx1[ri];
+    nf1 = g1->type == GEOM_BOX ? box_face(g1->rot, g1->pos, g1->size, ind, f1) : mesh_face(g1, ind, f1);
   }
   if (edge2) {
     memcpy(f2[0], pt->vert[2 * face[0] + 1], 3 * sizeof(real));
     memcpy(f2[1], endvert[ri], 3 * sizeof(real));
     nf2 = 2;
   } else {
-    nf2 = box_face(g2->rot, g2->pos, g2->size, idx2[rj], f2);
+    nf2 = g2->type == GEOM_BOX ? box_face(g2->rot, g2->pos, g2->size, idx2[rj], f2) : mesh_face(g2, idx2[rj], f2);
   }
   real dl = sqrt(dot3(dir, dir)), ad[3];
   if (edge1) {
@@ -988,12 +1097,20 @@ static int ccd_raw(const ccd_geom* g1in, const ccd_geom* g2in, real tolerance, r
     for (int i = 0; i < 3; i++) x1[i] = x2[i] = 0;
     return 0;
   }
-  /* multicontact: no margin, boxes only in this build (the reference also takes meshes with polygon data) */
+  /* collision_gjk.py:2336-2345: multicontact needs no margin and boxes or meshes (with polygon data,
+   * collision_convex.py:810-818); the caller applies MULTICCD (box-box always, collision_convex.py:809) */
   if (g1.margin != 0 || g2.margin != 0) f = -1;
-  if (!((g1.type == GEOM_BOX) && (g2.type == GEOM_BOX))) f = -1;
+  if (!((g1.type == GEOM_BOX || g1.type == GEOM_MESH) && (g2.type == GEOM_BOX || g2.type == GEOM_MESH))) f = -1;
+  if ((g1.type == GEOM_MESH && !g1.pnormal) || (g2.type == GEOM_MESH && !g2.pnormal)) f = -1;
   *idx = f;
   return 1;
 }
+
+/* MULTICCD of the model being collided (opt.enableflags), set by the caller around ccd_pair */
+static int ccd_multiccd = 0;
+#ifdef _OPENMP
+#pragma omp threadprivate(ccd_multiccd)
+#endif
 
 static polytope* ccd_polytope(void) {
   static polytope pt_store;
@@ -1030,7 +1147,9 @@ static int ccd_pair_cut(const ccd_geom* g1in, const ccd_geom* g2in, real toleran
   int n = 1;
   memcpy(w1[0], x1, sizeof(x1));
   memcpy(w2[0], x2, sizeof(x2));
-  if (idx > -1) n = multicontact_box(pt, idx, x1, x2, &h1, &h2, w1, w2);
+  /* collision_convex.py:809: box-box always, box-mesh / mesh-mesh under MULTICCD (g*->multiccd) */
+  const int boxbox = g1.type == GEOM_BOX && g2.type == GEOM_BOX;
+  if (idx > -1 && (boxbox || ccd_multiccd)) n = multicontact(pt, idx, x1, x2, &h1, &h2, w1, w2);
   for (int i = 0; i < n; i++)
     for (int k = 0; k < 3; k++) pts[i][k] = 0.5 * (w1[i][k] + w2[i][k]);
   for (int k = 0; k < 3; k++) normal[k] = w1[0][k] - w2[0][k];

@@ -74,10 +74,9 @@ static void coll_pair(const orc_model* m, const orc_data* d, int g1, int g2, int
     cg1.type = t1; cg2.type = t2;
     memcpy(cg1.pos, p1, sizeof(cg1.pos)); memcpy(cg1.rot, r1, sizeof(cg1.rot)); memcpy(cg1.size, s1, sizeof(cg1.size));
     memcpy(cg2.pos, p2, sizeof(cg2.pos)); memcpy(cg2.rot, r2, sizeof(cg2.rot)); memcpy(cg2.size, s2, sizeof(cg2.size));
-    cg1.vert = t1 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g1]] : NULL;
-    cg1.nvert = t1 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g1]] : 0;
-    cg2.vert = t2 == GEOM_MESH ? m->mesh_vert + 3 * m->mesh_vertadr[m->geom_dataid[g2]] : NULL;
-    cg2.nvert = t2 == GEOM_MESH ? m->mesh_vertnum[m->geom_dataid[g2]] : 0;
+    if (t1 == GEOM_MESH) ccd_geom_mesh(m, m->geom_dataid[g1], &cg1);
+    if (t2 == GEOM_MESH) ccd_geom_mesh(m, m->geom_dataid[g2], &cg2);
+    ccd_multiccd = (m->opt_enableflags & ENBL_MULTICCD) != 0;
     real cdist, cnrm[3], cpts[4][3];
     int nc = ccd_pair_cut(&cg1, &cg2, m->opt_ccd_tolerance, m->opt_ccd_iterations, m->ccd_epa_iterations, margin, 1e32, &cdist, cnrm, cpts);
     if (nc > 0) {

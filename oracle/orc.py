@@ -153,6 +153,7 @@ class OracleModel:
       nflex=getattr(mjm, "nflex", 0), nflexvert=getattr(mjm, "nflexvert", 0), nflexedge=getattr(mjm, "nflexedge", 0),
       nflexelem=getattr(mjm, "nflexelem", 0), nflexelemdata=getattr(mjm, "nflexelemdata", 0),
       nmesh=getattr(mjm, "nmesh", 0), nmeshvert=getattr(mjm, "nmeshvert", 0),
+      nmeshpoly=getattr(mjm, "nmeshpoly", 0), nmeshpolyvert=getattr(mjm, "nmeshpolyvert", 0), nmeshpolymap=getattr(mjm, "nmeshpolymap", 0),
       ntendon=getattr(mjm, "ntendon", 0), nwrap=getattr(mjm, "nwrap", 0), nJten=getattr(mjm, "nJten", 0),
       npair=getattr(mjm, "npair", 0),
       nhfield=getattr(mjm, "nhfield", 0), nhfielddata=getattr(mjm, "nhfielddata", 0),
@@ -294,8 +295,9 @@ def kat_upper_trid_index(n, i, j):
 
 
 def kat_ccd(types, pos, mat, size, margin, tolerance, iterations, multiccd, mesh_vert=None, vertadr=(0, 0), vertnum=(0, 0),
-            real_bits=64):
-  """collision_gjk_test.py _geom_dist on the oracle: (ncon, dist, x1, x2); ncon -1 = not restated."""
+            real_bits=64, mjm=None, meshid=None):
+  """collision_gjk_test.py _geom_dist on the oracle: (ncon, dist, x1, x2); ncon -1 = not restated.  With the
+  compiled model `mjm` and the geoms' mesh ids, mesh geoms carry their polygon data (mesh multi-contact)."""
   lib = _lib(real_bits)
   creal = ctypes.c_double if real_bits == 64 else ctypes.c_float
   dt = np.float64 if real_bits == 64 else np.float32
@@ -306,10 +308,18 @@ def kat_ccd(types, pos, mat, size, margin, tolerance, iterations, multiccd, mesh
   mv = np.ascontiguousarray(np.zeros(3) if mesh_vert is None else mesh_vert, dtype=dt).reshape(-1)
   va, vn = np.ascontiguousarray(vertadr, dtype=np.int32), np.ascontiguousarray(vertnum, dtype=np.int32)
   out = np.zeros(7, dt)
-  f = lib.orc_kat_ccd
-  f.restype = ctypes.c_int
-  n = f(I(t), P(pos), P(mat), P(size), P(mv), I(va), I(vn), creal(margin), creal(tolerance), ctypes.c_int(iterations),
-        ctypes.c_int(int(multiccd)), P(out))
+  if mjm is not None:
+    om = OracleModel(mjm, real_bits=real_bits)
+    mid = np.ascontiguousarray(meshid, dtype=np.int32)
+    f = lib.orc_kat_ccd_model
+    f.restype = ctypes.c_int
+    n = f(I(t), P(pos), P(mat), P(size), P(mv), I(va), I(vn), creal(margin), creal(tolerance), ctypes.c_int(iterations),
+          ctypes.c_int(int(multiccd)), ctypes.byref(om.struct), I(mid), P(out))
+  else:
+    f = lib.orc_kat_ccd
+    f.restype = ctypes.c_int
+    n = f(I(t), P(pos), P(mat), P(size), P(mv), I(va), I(vn), creal(margin), creal(tolerance), ctypes.c_int(iterations),
+          ctypes.c_int(int(multiccd)), P(out))
   return n, float(out[0]), out[1:4].copy(), out[4:7].copy()
 
 

@@ -17,9 +17,12 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 KAT = os.path.join(HERE, "golden", "collision_kat.json")
 
-# multi-contact for mesh geoms needs MuJoCo's mesh polygon data (mesh_polynum / polyvert / polymap),
-# which this build's compiler does not produce; the C5 model does not enable multiccd
-UNSUPPORTED = {"test_mesh_mesh_ccd": "mesh multi-contact (polygon data) not built"}
+# every case runs (mesh multi-contact: the compiler's mesh polygon data, mjcf._mesh_polygons); the device
+# KAT kernel replays the primitive / box cases, and tests/test_multiccd.py runs the mesh case through the
+# device pipeline
+UNSUPPORTED = {}
+# cases the device KAT kernel (csrc/mjw_kat.hip, no model: no mesh polygon data) leaves to the pipeline test
+DEVICE_PIPELINE_ONLY = {"test_mesh_mesh_ccd": "mesh multi-contact: run through the device pipeline (tests/test_multiccd.py)"}
 
 # cases whose expected value is the reference's own fp32 (Warp `float`) result rather than MuJoCo C's
 # fp64 one: the fp64 oracle lands elsewhere and is not held to them (fp32 oracle and HIP are).
@@ -57,9 +60,10 @@ def gjk_inputs(case):
       mid = mjm.geom_dataid[g]
       vertadr[k], vertnum[k] = mjm.mesh_vertadr[mid], mjm.mesh_vertnum[mid]
   mesh_vert = np.asarray(mjm.mesh_vert, np.float64).reshape(-1, 3) if mjm.nmesh else np.zeros((1, 3))
+  meshid = np.array([mjm.geom_dataid[g] if types[k] == 7 else -1 for k, g in enumerate(gids)], np.int32)
   return dict(types=types, pos=pos, mat=mat, size=size, mesh_vert=mesh_vert, vertadr=vertadr, vertnum=vertnum,
               margin=case["margin"], tolerance=float(mjm.opt.ccd_tolerance), iterations=int(mjm.opt.ccd_iterations),
-              multiccd=case["multiccd"])
+              multiccd=case["multiccd"], mjm=mjm, meshid=meshid)
 
 
 def triangle_inputs(case):

@@ -22,7 +22,8 @@ def test_oracle_gjk_kat(case, real_bits):
     pytest.skip("expected value is the reference's fp32 result (golden_kat.FP32_ONLY)")
   a = gk.gjk_inputs(case)
   ncon, dist, x1, x2 = orc.kat_ccd(a["types"], a["pos"], a["mat"], a["size"], a["margin"], a["tolerance"], a["iterations"],
-                                   a["multiccd"], a["mesh_vert"], a["vertadr"], a["vertnum"], real_bits=real_bits)
+                                   a["multiccd"], a["mesh_vert"], a["vertadr"], a["vertnum"], real_bits=real_bits, mjm=a["mjm"],
+                                   meshid=a["meshid"])
   assert ncon >= 0
   gk.check(case, dict(dist=dist, ncon=ncon, x1=x1, x2=x2))
 

@@ -45,7 +45,7 @@ def _ccd_record(a, vert_base):
 @pytest.fixture(scope="module")
 def gjk_results():
   """All GJK cases in one launch (one wavefront each); mesh vertices of every scene concatenated."""
-  cases = [c for c in KAT["gjk"] if c["name"] not in gk.UNSUPPORTED]
+  cases = [c for c in KAT["gjk"] if c["name"] not in gk.UNSUPPORTED and c["name"] not in gk.DEVICE_PIPELINE_ONLY]
   recs, verts, base = [], [], 0
   for c in cases:
     a = gk.gjk_inputs(c)
@@ -62,6 +62,8 @@ def gjk_results():
 def test_hip_gjk_kat(case, gjk_results):
   if case["name"] in gk.UNSUPPORTED:
     pytest.skip(gk.UNSUPPORTED[case["name"]])
+  if case["name"] in gk.DEVICE_PIPELINE_ONLY:
+    pytest.skip(gk.DEVICE_PIPELINE_ONLY[case["name"]])
   o = gjk_results[case["name"]]
   assert o[0] >= 0
   gk.check(case, dict(ncon=int(o[0]), dist=float(o[1]), x1=o[2:5].astype(np.float64), x2=o[5:8].astype(np.float64)))
@@ -96,7 +98,7 @@ def test_hip_matches_fp32_oracle_kat(gjk_results):
   from oracle import orc
 
   for c in KAT["gjk"]:
-    if c["name"] in gk.UNSUPPORTED:
+    if c["name"] in gk.UNSUPPORTED or c["name"] in gk.DEVICE_PIPELINE_ONLY:
       continue
     a = gk.gjk_inputs(c)
     n, d, _, _ = orc.kat_ccd(a["types"], a["pos"], a["mat"], a["size"], a["margin"], a["tolerance"], a["iterations"], a["multiccd"],
