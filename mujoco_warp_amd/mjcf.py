@@ -1001,23 +1001,26 @@ class _Compiler:
     """<asset><hfield>: nrow x ncol elevation grid (row 0 at -y, MuJoCo's mjModel.hfield_data order), size =
     (x half-extent, y half-extent, top, base).  `elevation` values are normalised to [0, 1] by subtracting
     the minimum and dividing by the range when it is non-zero (MuJoCo user_hfield); without it the grid is
-    flat.  PNG / binary `file` data is not read (parity unpinned: no MuJoCo here)."""
+    flat.  A `file` gives the grid instead (_read_hfield_file: a PNG image or MuJoCo's binary format), its
+    values normalised the same way.""" 
     m = self.m
     self.hfield_id = {}
     sizes, nrows, ncols, datas = [], [], [], []
     for asset in root.findall("asset"):
       for he in asset.findall("hfield"):
         a = self._resolve("hfield", he, None)
+        fdata = None
         if "file" in a:
-          raise NotImplementedError("<hfield file=...>: image / binary heightfield files are not read by this compiler")
+          nrow, ncol, fdata = _read_hfield_file(os.path.join(self.basedir, a.get("file")))
+          a = dict(a, nrow=str(nrow), ncol=str(ncol))
         nrow, ncol = int(a.get("nrow", 0)), int(a.get("ncol", 0))
         if nrow < 2 or ncol < 2:
           raise ValueError("<hfield> needs nrow >= 2 and ncol >= 2")
         size = _floats(a.get("size", "0 0 0 0"), 4)
         if min(size) <= 0:
           raise ValueError("<hfield> size must be positive")
-        if "elevation" in a:
-          e = np.array(_floats(a["elevation"]), dtype=np.float64)
+        if fdata is not None or "elevation" in a:
+          e = fdata if fdata is not None else np.array(_floats(a["elevation"]), dtype=np.float64)
           if e.size != nrow * ncol:
             raise ValueError(f"<hfield> elevation has {e.size} values, nrow * ncol = {nrow * ncol}")
           lo, hi = e.min(), e.max()
@@ -2000,6 +2003,81 @@ def _cam_intrinsics(ca):
     pp = _floats(ca["principalpixel"], 2)
     principal = [pp[i] / max(res[i], 1) * ss[i] for i in range(2)]
   return dict(resolution=res, sensorsize=ss, intrinsic=list(focal) + list(principal))
+
+
+def _read_png(path):
+  """(height, width, samples (h, w, channels), bit depth) of a PNG file: the chunk stream, zlib and the five
+  scanline filters (PNG spec 9.2), for 8 / 16-bit greyscale, grey + alpha, RGB and RGBA images."""
+  import struct
+  import zlib
+
+  with open(path, "rb") as f:
+    raw = f.read()
+  if raw[:8] != b"\x89PNG\r\n\x1a\n":
+    raise ValueError(f"{path}: not a PNG file")
+  pos, idat, hdr = 8, [], None
+  while pos < len(raw):
+    n = struct.unpack(">I", raw[pos:pos + 4])[0]
+    kind, body = raw[pos + 4:pos + 8], raw[pos + 8:pos + 8 + n]
+    pos += 12 + n
+    if kind == b"IHDR":
+      hdr = struct.unpack(">IIBBBBB", body)
+    elif kind == b"IDAT":
+      idat.append(body)
+    elif kind == b"IEND":
+      break
+  w, h, depth, ctype, _, _, interlace = hdr
+  chans = {0: 1, 2: 3, 4: 2, 6: 4}.get(ctype)
+  if chans is None or depth not in (8, 16) or interlace:
+    raise NotImplementedError(f"{path}: PNG color type {ctype}, bit depth {depth}, interlace {interlace} not supported")
+  bpp = chans * depth // 8
+  stride = w * bpp
+  data = zlib.decompress(b"".join(idat))
+  out = np.zeros((h, stride), dtype=np.int32)
+  prev = np.zeros(stride, dtype=np.int32)
+  for r in range(h):
+    ft = data[r * (stride + 1)]
+    line = np.frombuffer(data, dtype=np.uint8, count=stride, offset=r * (stride + 1) + 1).astype(np.int32)
+    cur = np.zeros(stride, dtype=np.int32)
+    if ft == 0:
+      cur = line
+    elif ft == 2:
+      cur = (line + prev) & 255
+    else:
+      for i in range(stride):  # sub / average / paeth depend on the reconstructed left byte
+        left = cur[i - bpp] if i >= bpp else 0
+        up, ul = prev[i], (prev[i - bpp] if i >= bpp else 0)
+        if ft == 1:
+          pr = left
+        elif ft == 3:
+          pr = (left + up) >> 1
+        else:
+          p = left + up - ul
+          pa, pb, pc = abs(p - left), abs(p - up), abs(p - ul)
+          pr = left if (pa <= pb and pa <= pc) else (up if pb <= pc else ul)
+        cur[i] = (line[i] + pr) & 255
+    out[r] = cur
+    prev = cur
+  px = out.reshape(h, w, bpp).astype(np.uint16)
+  if depth == 16:
+    px = (px[:, :, 0::2] << 8) | px[:, :, 1::2]
+  return h, w, px.reshape(h, w, chans), depth
+
+
+def _read_hfield_file(path):
+  """(nrow, ncol, elevation) of an <hfield file=...>, in hfield_data order (row 0 at -y).  PNG: decoded to
+  8-bit grey as MuJoCo's loader does (lodepng LCT_GREY: the red / grey channel, 16-bit samples by their
+  high byte), image row 0 -- the top -- becoming the last grid row, values / 255.  Any other extension:
+  MuJoCo's binary format, int32 nrow, int32 ncol, then nrow * ncol float32 values in grid order."""
+  if path.lower().endswith(".png"):
+    h, w, px, depth = _read_png(path)
+    grey = (px[:, :, 0] >> 8) if depth == 16 else px[:, :, 0]
+    return h, w, (grey[::-1].astype(np.float64) / 255.0).reshape(-1)
+  with open(path, "rb") as f:
+    raw = f.read()
+  nrow, ncol = np.frombuffer(raw[:8], dtype="<i4")
+  data = np.frombuffer(raw[8:8 + 4 * int(nrow) * int(ncol)], dtype="<f4").astype(np.float64)
+  return int(nrow), int(ncol), data
 
 
 def _bending_coef(x, mu, thickness):

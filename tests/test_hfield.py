@@ -50,9 +50,7 @@ def test_compile_hfield_refusals():
   with pytest.raises(NotImplementedError):
     _load("""<mujoco><asset><hfield name="t" nrow="2" ncol="2" size="1 1 .1 .1"/></asset>
     <worldbody><body><freejoint/><geom type="hfield" hfield="t"/></body></worldbody></mujoco>""")
-  with pytest.raises(NotImplementedError):
-    _load("""<mujoco><asset><hfield name="t" file="terrain.png" size="1 1 .1 .1"/></asset>
-    <worldbody><geom type="hfield" hfield="t"/></worldbody></mujoco>""")
+  # (image / binary heightfield files are read: tests/test_hfield_file.py)
 
 
 @pytest.mark.parametrize("margin", [0.0, 0.1])
