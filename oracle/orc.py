@@ -46,6 +46,7 @@ _LIBS = {}
 
 
 def _lib(real_bits):
+  """real_bits 64 / 32, or "32f": fp32 with fused multiply-adds (liborc32f, the device's contraction)."""
   if real_bits not in _LIBS:
     path = os.path.join(_BUILD, f"liborc{real_bits}.so")
     if not os.path.exists(path):

@@ -179,8 +179,17 @@ def test_gpu_multiccd_matches_oracle(pair):
     assert len(sel) == n2, (w, len(sel), n2)
     np.testing.assert_allclose(np.sort(np_(d.contact.dist)[sel]), np.sort(d2), atol=2e-5)
     gp = np_(d.contact.pos)[sel].astype(np.float64)
-    for p in p2:  # every oracle point has a device point within fp32 rounding
-      assert np.min(np.linalg.norm(gp - p, axis=1)) < 2e-4, (w, p)
+    # the first pair (a 4-corner overlap rectangle): every oracle point has a device point within fp32
+    # rounding.  The turned pair clips to an 8-gon, of which polygon_quad's greedy search keeps 4 -- a search
+    # whose moves compare near-equal areas, so fp32 / fp64 may keep different quads: there every
+    # device point must lie in the overlap of both cubes, at the oracle's depth
+    for p in p2[p2[:, 0] < 0.5]:
+      assert np.min(np.linalg.norm(gp[gp[:, 0] < 0.5] - p, axis=1)) < 2e-4, (w, p)
+    xpos, xmat = np_(d.xpos[w]).astype(np.float64), np_(d.xmat[w]).astype(np.float64).reshape(-1, 3, 3)
+    for k, p in enumerate(gp):
+      for b in ((1, 2) if p[0] < 0.5 else (3, 4)):
+        loc = xmat[b].T @ (p - xpos[b])
+        assert np.abs(loc).max() <= 0.1 + 0.02, (w, k, b, loc)
 
 
 @pytest.mark.gpu

@@ -289,13 +289,32 @@ def test_gpu_convex_sensor_boxes(z):
   np.testing.assert_allclose(got[:, [0, 10, 14]], want[:, [0, 10, 14]], atol=2e-5)
   cols = [c for c in range(got.shape[1]) if not 4 <= c < 10]
   np.testing.assert_allclose(got[:, cols], want[:, cols], atol=5e-4)
-  # fromto: overlapping face-face boxes give 4 multi-contact points at one depth; which one leads the clipped
-  # polygon flips with rounding at these ties, so the device's segment is held to the sensor's invariants
-  seg = got[:, 7:10] - got[:, 4:7]
-  np.testing.assert_allclose(np.linalg.norm(seg, axis=1), np.abs(got[:, 0]), atol=2e-5)
-  np.testing.assert_allclose(seg / np.abs(got[:, :1]), got[:, 1:4], atol=1e-3)  # normal = normalize(to - from)
-  if z > 0.35:
-    np.testing.assert_allclose(got[:, 4:10], want[:, 4:10], atol=5e-4)
+  # fromto against the fp32 oracle (liborc32) at 5e-4.  Overlapping boxes give several multi-contact points at
+  # one depth, and the sensor reports the first: where the clipped polygon's start is a rounding tie (two
+  # coplanar EPA faces, duplicate points of an edge-face clip), the fp32 oracle compiled with the device's
+  # fused multiply-adds (liborc32f) can pick another point than the sequential builds -- at z = 0.33, world 2,
+  # it picks the device's.  In a world with several equal-depth contacts whose builds disagree, the device's
+  # segment must be one of the oracle's contact points' segments (pos -+ dist / 2 along the normal).
+  _, o32 = oracle_from_state(mjm, qpos, np.zeros((nworld, mjm.nv)), np.zeros((nworld, mjm.nu)), real_bits=32)
+  _, o32f = oracle_from_state(mjm, qpos, np.zeros((nworld, mjm.nv)), np.zeros((nworld, mjm.nu)), real_bits="32f")
+  o32.forward()
+  o32f.forward()
+  w32, w32f = np.asarray(o32.sensordata, np.float64), np.asarray(o32f.sensordata, np.float64)
+  ties = 0
+  for w in range(nworld):
+    n = int(od.ncon[w, 0])
+    if n <= 1 or np.abs(w32[w, 4:10] - w32f[w, 4:10]).max() < 5e-4 and np.abs(got[w, 4:10] - w32[w, 4:10]).max() < 5e-4:
+      # one contact (no order to tie), or every build agrees: the strict comparison
+      np.testing.assert_allclose(got[w, 4:10], w32[w, 4:10], atol=5e-4, err_msg=f"world {w}")
+      continue
+    ties += 1
+    segs = []
+    for c in range(n):
+      p, dd, nn = od.con_pos[w, 3 * c:3 * c + 3], od.con_dist[w, c], od.con_frame[w, 9 * c:9 * c + 3]
+      segs.append(np.sort(np.stack([p - 0.5 * dd * nn, p + 0.5 * dd * nn]), axis=0))
+    mine = np.sort(np.stack([got[w, 4:7], got[w, 7:10]]).astype(np.float64), axis=0)
+    assert min(np.abs(s_ - mine).max() for s_ in segs) < 5e-4, (w, got[w, 4:10], segs)
+  assert ties <= 2  # world 2 at z = 0.33 and 0.3 (four contacts at one depth, two of them duplicated)
 
 
 @pytest.mark.gpu
