@@ -1715,6 +1715,46 @@ __device__ void make_constraint(const mjw_model_t& m, const mjw_data_t& d, int w
   __syncthreads();
 }
 
+// smooth.py:2448-2602: BODY (adhesion) transmissions.  Moment = minus the mean, over the world's
+// contacts touching the body (flex contacts excepted), of n . (J(pos, b2) - J(pos, b1)) -- what the
+// reference reads back from the contact's constraint rows or, outside the margin, from the Jacobian
+// difference (mjw_trn.h).  The block splits the dofs; each thread walks the world's contacts in order.
+__device__ void body_transmission(const mjw_model_t& m, const mjw_data_t& d, int wid) {
+  const int cbase = d.ncon_world[2 * (long)wid], nc = d.ncon_world[2 * (long)wid + 1];
+  const float* sc = d.subtree_com + (long)wid * m.nbody * 3;
+  const float* cdof = d.cdof + (long)wid * m.nv * 6;
+  for (int a = 0; a < m.nu; a++) {
+    if (m.actuator_trntype[a] != TRN_BODY) continue;
+    const int body = m.actuator_trnid[2 * a];
+    int ncon = 0;
+    for (int c = cbase; c < cbase + nc; c++) {
+      const int g1 = d.contact_geom[2 * (long)c], g2 = d.contact_geom[2 * (long)c + 1];
+      if (g1 >= 0 && g2 >= 0 && (m.geom_bodyid[g1] == body || m.geom_bodyid[g2] == body)) ncon++;
+    }
+    const long gu = (long)wid * m.nu + a;
+    float* gm = d.actuator_moment + (long)wid * m.nJmom + d.moment_rowadr[gu];
+    int* gc = d.moment_colind + (long)wid * m.nJmom + d.moment_rowadr[gu];
+    for (int i = tid(); i < m.nv; i += BLK) {
+      float q = 0.0f;
+      for (int c = cbase; c < cbase + nc && ncon > 0; c++) {
+        const int g1 = d.contact_geom[2 * (long)c], g2 = d.contact_geom[2 * (long)c + 1];
+        if (g1 < 0 || g2 < 0) continue;
+        const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+        if (b1 != body && b2 != body) continue;
+        const float* pos = d.contact_pos + 3 * (long)c;
+        const float* n = d.contact_frame + 9 * (long)c;
+        float j1[3], j2[3], r[3];
+        trn_jac_dof(m, sc, cdof, pos, b1, i, j1, r);
+        trn_jac_dof(m, sc, cdof, pos, b2, i, j2, r);
+        q += n[0] * (j2[0] - j1[0]) + n[1] * (j2[1] - j1[1]) + n[2] * (j2[2] - j1[2]);
+      }
+      gm[i] = ncon > 0 ? q * (-1.0f / (float)ncon) : 0.0f;
+      gc[i] = i;
+    }
+  }
+  __syncthreads();
+}
+
 // smooth.py:2041-2147 joint transmissions (packed moment rows, actuator order)
 __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid, Smem& sm) {
   const float* gear_all = MR(actuator_gear);
@@ -1726,7 +1766,7 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid,
     if (a < m.nu) {
       if (m.actuator_trntype[a] == TRN_TENDON) {
         nnz = m.ten_J_rownnz[m.actuator_trnid[2 * a]];
-      } else if (m.actuator_trntype[a] == TRN_SITE || m.actuator_trntype[a] == TRN_SLIDERCRANK) {
+      } else if (m.actuator_trntype[a] == TRN_SITE || m.actuator_trntype[a] == TRN_SLIDERCRANK || m.actuator_trntype[a] == TRN_BODY) {
         nnz = trn_site_nnz(m, a);
       } else {
         const int jt0 = m.jnt_type[m.actuator_trnid[2 * a]];
@@ -1749,6 +1789,13 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid,
         d.actuator_moment[(long)wid * m.nJmom + rowadr + k] = gear[0] * J[k];
         d.moment_colind[(long)wid * m.nJmom + rowadr + k] = m.ten_J_colind[m.ten_J_rowadr[j] + k];
       }
+      continue;
+    }
+    if (trn == TRN_BODY) {  // a dense row over every dof, filled below once all rows are placed
+      const long gu = (long)wid * m.nu + a;
+      d.actuator_length[gu] = 0.0f;
+      d.moment_rownnz[gu] = nnz;
+      d.moment_rowadr[gu] = rowadr;
       continue;
     }
     if (trn == TRN_SITE || trn == TRN_SLIDERCRANK) {  // smooth.py:2150-2241, 2274-2442 (mjw_trn.h)
@@ -1800,6 +1847,7 @@ __device__ void transmission(const mjw_model_t& m, const mjw_data_t& d, int wid,
     }
   }
   __syncthreads();
+  if (m.nbodytrn) body_transmission(m, d, wid);
 }
 
 // ---------------------------------------------------------------------------------------------

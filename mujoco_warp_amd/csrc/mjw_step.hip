@@ -3166,7 +3166,7 @@ int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
 int mjw_actuator_map(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   if (!m || !d) { g_err = "mjw_actuator_map: null model/data"; return -1; }
   if (d->nworld <= 0) return 0;
-  if (m->is_sparse) { g_err = "mjw_actuator_map: sparse models keep the moment map inside the velocity-stage kernel"; return -2; }
+  // layout-independent: the moment rows (rowadr / rownnz / colind) are the same on the sparse path
   hipLaunchKernelGGL(mjw::actuator_map_kernel, dim3(d->nworld), dim3(64), 0, (hipStream_t)stream, *m, *d);
   return set_err(hipGetLastError(), "mjw_actuator_map");
 }

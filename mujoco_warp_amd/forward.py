@@ -120,8 +120,6 @@ def fwd_actuation(m: Model, d: Data):
   cb = m.callback
   act_cbs = [f for f in (cb.act_dyn, cb.act_gain, cb.act_bias) if f is not None]
   if act_cbs and m.nu and not (m.opt.disableflags & DisableBit.ACTUATION):
-    if m.is_sparse:
-      raise NotImplementedError("act_* callbacks on the sparse path: its moment map is fused into the velocity-stage kernel")
     for f in act_cbs:
       f(m, d)
     _call("mjw_actuator_map", m, d)

@@ -197,8 +197,6 @@ def put_model(mjm, device=None) -> types.Model:
     lr = np.asarray(mjm.actuator_lengthrange, np.float64).reshape(-1, 2)[muscle]
     if np.any(lr[:, 0] >= lr[:, 1]):
       raise NotImplementedError("muscle actuators need an actuator_lengthrange (lengthrange attribute, or a limited joint / tendon transmission).")
-  if sparse and np.any(mjm.actuator_trntype == types.TrnType.BODY):
-    raise NotImplementedError("sparse / flex models: BODY (adhesion) transmissions are not supported by this build yet.")
   if (mjm.opt.viscosity > 0 or mjm.opt.density > 0) and mjm.opt.integrator in (types.IntegratorType.IMPLICITFAST, types.IntegratorType.IMPLICIT):
     raise NotImplementedError("Implicit integrators and fluid model not implemented.")  # io.py:126-130
 

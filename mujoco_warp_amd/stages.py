@@ -326,9 +326,8 @@ def set_const_0(m: Model, d: Data):
   body_invweight0 (mean translational / rotational diagonal of J M^-1 J' at the body COM; zero for the world
   and static bodies), tendon_invweight0 (J M^-1 J') and actuator_acc0 (||M^-1 moment||, joint and tendon
   transmissions), the camera / light references -- the same definitions mjcf.py's compiler applies on
-  the host.  Dense models; the dampratio resolution keeps put_model's values."""
-  if m.is_sparse:
-    raise NotImplementedError("set_const_0 on sparse models is not part of this build")
+  the host.  Sparse models expand their ancestor-row qM (M_rowadr / M_rownnz / M_colind) to the dense
+  symmetric matrix first.  The dampratio resolution keeps put_model's values."""
   nw, nv, nb = d.nworld, m.nv, m.nbody
   saved = d.qpos.clone()
   # the position launch also runs collision and make_constraint, which the reference's set_const_0 does not
@@ -339,7 +338,17 @@ def set_const_0(m: Model, d: Data):
   _call("mjw_fwd_position", m, d)
   if int(getattr(m, "ntendon", 0)):  # io.py:2263 tendon_length0 from ten_length at qpos0
     m.tendon_length0 = d.ten_length.reshape(nw, m.ntendon).to(m.tendon_length0.dtype).clone()
-  M = d.qM.reshape(nw, m.nv_pad, m.nv_pad)[:, :nv, :nv].double()
+  if m.is_sparse:
+    rownnz = m.M_rownnz.reshape(-1).to(torch.long)
+    rows = torch.repeat_interleave(torch.arange(nv, device=rownnz.device), rownnz)
+    adr = torch.cat([torch.arange(int(a), int(a) + int(n)) for a, n in zip(m.M_rowadr.reshape(-1).tolist(), rownnz.tolist())]).to(rows.device)
+    cols = m.M_colind.reshape(-1).to(torch.long)[adr]
+    vals = d.qM.reshape(nw, -1)[:, adr].double()
+    M = torch.zeros(nw, nv, nv, dtype=torch.float64, device=d.qM.device)
+    M[:, cols, rows] = vals
+    M[:, rows, cols] = vals
+  else:
+    M = d.qM.reshape(nw, m.nv_pad, m.nv_pad)[:, :nv, :nv].double()
   Minv = torch.linalg.inv(M)
   f32 = m.dof_invweight0.dtype
   m.stat.meaninertia = (M.diagonal(dim1=1, dim2=2).sum(1) / max(nv, 1)).to(f32)

@@ -230,17 +230,22 @@ def test_gpu_full_gravcomp_holds_still():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("staged", [False, True])
-def test_gpu_actuatorgravcomp_routing(staged):
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gpu_actuatorgravcomp_routing(staged, sparse):
   """qfrc_gravcomp / qfrc_passive / qfrc_actuator of the routed joint against the oracle, through the
-  fused forward and through the staged path with an act_bias callback (mjw_actuator_map)."""
+  fused forward and through the staged path with an act_bias callback (mjw_actuator_map), on the dense
+  and the sparse (workgroup-per-world) pipelines."""
   import torch
 
   import mujoco_warp_amd as mjw
 
   mjm = _load(GC_XML.format(rng='actuatorfrcrange="-1 1"'))
+  if sparse:
+    mjm.opt.jacobian = 1
   rng = np.random.default_rng(2)
   qpos, qvel, ctrl = rng.normal(0, 0.5, (4, mjm.nq)), rng.normal(0, 1, (4, mjm.nv)), rng.normal(0, 0.3, (4, mjm.nu))
   m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=16, nconmax=4)
+  assert m.is_sparse == sparse
   if staged:
     m.callback.act_bias = lambda m_, d_: None
   _, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=16, nconmax=4)

@@ -303,17 +303,18 @@ def test_gpu_set_const_fixed_per_world_mass():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model", ["humanoid", "franka", "tendon"])
+@pytest.mark.parametrize("model", ["humanoid", "franka", "tendon", "humanoid_sparse", "tendon_sparse"])
 def test_gpu_set_const_0_reproduces_put_model(model):
   """set_const_0 on the device (qpos0 position stage, M^-1 in fp64 from the fp32 qM) reproduces the
-  constants put_model took from the compiler (mjcf.py, the same definitions in fp64 on the host)."""
+  constants put_model took from the compiler (mjcf.py, the same definitions in fp64 on the host);
+  `_sparse`: the same models on the sparse path (ancestor-row qM expanded first)."""
   import torch
 
   import mujoco_warp_amd as mjw
   from mujoco_warp_amd import mjcf
   from tests.common import franka_model
 
-  if model == "humanoid":
+  if model.startswith("humanoid"):
     mjm = mjcf.load_model(HUMANOID)
   elif model == "franka":
     mjm = franka_model()
@@ -322,7 +323,10 @@ def test_gpu_set_const_0_reproduces_put_model(model):
       <body pos=".4 0 0"><joint name="b" axis="0 1 0"/><geom size=".1" pos=".2 0 0"/></body></body></worldbody>
       <tendon><fixed name="t"><joint joint="a" coef="1"/><joint joint="b" coef="-.5"/></fixed></tendon>
       <actuator><motor tendon="t" gear="2"/><motor joint="b"/></actuator></mujoco>""")
+  if model.endswith("_sparse"):
+    mjw.override_model(mjm, ["opt.jacobian=sparse"])
   m = mjw.put_model(mjm, device="cuda")
+  assert m.is_sparse == model.endswith("_sparse")
   d = mjw.make_data(mjm, nworld=2, device="cuda", m=m)
   fields = ["dof_invweight0", "body_invweight0", "actuator_acc0"]
   fields += ["cam_pos0", "cam_poscom0", "cam_mat0"] if mjm.ncam else []

@@ -173,18 +173,19 @@ def _dense_moment(mjm, d, w):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["site", "slidercrank", "adhesion", "adhesion_elliptic", "site_translational", "site_sparse",
-                                  "slidercrank_sparse", "site_translational_sparse"])
+                                  "slidercrank_sparse", "site_translational_sparse", "adhesion_sparse", "adhesion_elliptic_sparse"])
 def test_gpu_transmissions_match_oracle(name):
   """The device computes the BODY moment from the contact normals; the oracle from the constraint rows as
   the reference does (pyramidal and elliptic cones).  `_sparse`: the same models forced onto the sparse
-  path (jacobian="sparse"), whose transmission stage runs the same site / slider-crank rows (mjw_trn.h)."""
+  path (jacobian="sparse"), whose transmission stage runs the same site / slider-crank rows (mjw_trn.h) and
+  fills the BODY rows from the world's contact list after the constraint stage."""
   import torch
 
   import mujoco_warp_amd as mjw
 
   base = name.replace("_elliptic", "").replace("_sparse", "")
   mjm = _load(SITE_TRANSLATIONAL if base == "site_translational" else base)
-  if name == "adhesion_elliptic":
+  if name.startswith("adhesion_elliptic"):
     mjm.opt.cone = 1
   if name.endswith("_sparse"):
     mjw.override_model(mjm, ["opt.jacobian=sparse"])

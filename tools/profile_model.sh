@@ -6,7 +6,7 @@
 cd "$(dirname "$0")/.." || exit 1
 M=${1:-humanoid}
 S=${2:-}
-R=${ROUND:-r04}
+R=${ROUND:-r05}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 tag=$M
@@ -22,18 +22,19 @@ print(a.nworld, s)") || exit 1
 # the stats pass runs the bench's own step window (its defaults: 20 warm-up + 1000 timed steps, 100 for
 # the flex configs) followed by its trace pass, so that rocprof's average per kernel covers the states of
 # the bench line's HIP events (the humanoid's first 60 steps -- the fall from the squat key -- cost up to
-# 2x the long-run average in the dense kernel); the counter passes count a 20-step trace pass after 200
-# warm-up steps and one timed step: the summary averages exactly that trace pass (tail = its steps),
-# whose nefc / ncon the pass's bench line reports, so bench.py prices the same window's algorithmic bytes
+# 2x the long-run average in the dense kernel); the counter passes count 200 warm-up steps, a 20-step
+# timed window and bench.py's trace pass, which replays that window from the saved state: the summary
+# averages exactly the trace pass (tail = its steps), whose nefc / ncon the pass's bench line reports, so
+# bench.py prices the same window's algorithmic bytes
 steps_stats=1000; warm_stats=20; steps_pmc=20; warm_pmc=200
 case $M in aloha_cloth|cloth) steps_stats=100; steps_pmc=5; warm_pmc=20;; esac
 common="--model $M $sarg --cpu-baseline 0 --graph 0"
 d=gpurun_out/prof_$tag
 rm -rf $d && mkdir -p $d
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $d/stats -o run -- python3 bench.py $common --steps $steps_stats --warmup $warm_stats > $d/stats.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/fetch -o run -- python3 bench.py $common --steps 1 --trace-steps $steps_pmc --warmup $warm_pmc > $d/fetch.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/write -o run -- python3 bench.py $common --steps 1 --trace-steps $steps_pmc --warmup $warm_pmc > $d/write.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $d/sq -o run -- python3 bench.py $common --steps 1 --trace-steps $steps_pmc --warmup $warm_pmc > $d/sq.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/fetch -o run -- python3 bench.py $common --steps $steps_pmc --trace-steps $steps_pmc --warmup $warm_pmc > $d/fetch.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/write -o run -- python3 bench.py $common --steps $steps_pmc --trace-steps $steps_pmc --warmup $warm_pmc > $d/write.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $d/sq -o run -- python3 bench.py $common --steps $steps_pmc --trace-steps $steps_pmc --warmup $warm_pmc > $d/sq.log 2>&1 || exit $?
 python3 tools/sq_counters.py $d/sq > gpurun_out/${R}_${tag}_sq_counters.txt || exit $?
 python3 tools/pmc_traffic.py $d/stats $d/fetch $d/write gpurun_out/pmc_${tag}_$R.json $NW $SOLVER $M $steps_pmc > $d/pmc.log || exit $?
 find $d/stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${R}_${tag}_kernel_stats.csv \;
