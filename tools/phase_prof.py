@@ -31,6 +31,7 @@ nworld = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 solver = sys.argv[3] if len(sys.argv) > 3 else "CG"
 model = sys.argv[4] if len(sys.argv) > 4 else "humanoid"  # a bench.py config (dense-path models)
+warm = int(sys.argv[5]) if len(sys.argv) > 5 else 20  # 5: the driver's bench window (steps 5..5+nsteps)
 from bench import MODELS  # noqa: E402
 
 cfg = MODELS[model]
@@ -42,10 +43,10 @@ if cfg["key"] is not None:
   mjcf.reset_data_keyframe(mjm, mjd, cfg["key"])
 m = mjw.put_model(mjm, device="cuda")
 d = mjw.put_data(mjm, mjd, nworld=nworld, nconmax=cfg["nconmax"], njmax=cfg["njmax"], device="cuda", m=m)
-center = None if cfg["key"] is None else torch.zeros(mjm.nu, device="cuda")
+center = None if cfg["key"] is None else torch.as_tensor(mjm.key_ctrl[cfg["key"]], dtype=torch.float32, device="cuda")
 L = _lib.lib()
 buf = (ctypes.c_ulonglong * (len(PHASES) + len(SUB)))()
-for i in range(20):
+for i in range(warm):
   mjw.ctrl_noise(m, d, i, center=center)
   mjw.step(m, d)
 torch.cuda.synchronize()
@@ -54,7 +55,7 @@ L.mjw_prof_read_dense(buf, 1)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 for i in range(nsteps):
-  mjw.ctrl_noise(m, d, 20 + i, center=center)
+  mjw.ctrl_noise(m, d, warm + i, center=center)
   mjw.step(m, d)
 e1.record()
 torch.cuda.synchronize()
