@@ -33,6 +33,10 @@ namespace mjw {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef MJW_SCHED_EARLY
+#define MJW_SCHED_EARLY 1
+#endif
+
 constexpr int DJS = 33;             // LDS row stride of J (odd: conflict-free rows and columns)
 constexpr int DSS = 36;             // LDS row stride of the 32x32 scratch (16-B aligned rows)
 constexpr int DJ_WORDS = 64 * DJS;  // 2112
@@ -232,6 +236,50 @@ __device__ __forceinline__ float gemv_cols(const float* Jl, const float* fvec, i
   return xhalf_add(in ? p0 + p1 : 0.0f);
 }
 
+// The same two products with compile-time trip counts, fully unrolled, so that every LDS read is issued
+// before the first FMA instead of one LDS round trip per loop iteration.  The terms past the runtime
+// bound are exact zeros (J is staged zero-padded; the dof / row vectors are zero past nv / nefc), so the
+// sums are the loops' sums.
+template <int JS, int NQ>
+__device__ __forceinline__ float gemv_rows_u(const float* Jl, const float* vec, int lane) {
+  const f32x4* v4 = reinterpret_cast<const f32x4*>(vec);
+  const float* jr = Jl + lane * JS;
+  float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+  for (int q = 0; q < NQ; q++) {
+    f32x4 v = v4[q];
+    p0 = fmaf(jr[4 * q + 0], v.x, p0);
+    p1 = fmaf(jr[4 * q + 1], v.y, p1);
+    p0 = fmaf(jr[4 * q + 2], v.z, p0);
+    p1 = fmaf(jr[4 * q + 3], v.w, p1);
+  }
+  return p0 + p1;
+}
+template <int JS, int NQ>
+__device__ __forceinline__ float gemv_cols_u(const float* Jl, const float* fvec, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  const bool in = c < JS - 1;
+  const f32x4* f4 = reinterpret_cast<const f32x4*>(fvec + 32 * h);
+  const float* jc = Jl + 32 * h * JS + (in ? c : 0);
+  float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+  for (int q = 0; q < NQ; q++) {
+    f32x4 f = f4[q];
+    p0 = fmaf(jc[(4 * q + 0) * JS], f.x, p0);
+    p1 = fmaf(jc[(4 * q + 1) * JS], f.y, p1);
+    p0 = fmaf(jc[(4 * q + 2) * JS], f.z, p0);
+    p1 = fmaf(jc[(4 * q + 3) * JS], f.w, p1);
+  }
+  return xhalf_add(in ? p0 + p1 : 0.0f);
+}
+// J' f over the rows of each half up to 4 * nq (nq <= 8, wave-uniform): the smallest unrolled width
+template <int JS>
+__device__ __forceinline__ float gemv_cols_n(const float* Jl, const float* fvec, int lane, int nq) {
+  if (nq <= 2) return gemv_cols_u<JS, 2>(Jl, fvec, lane);
+  if (nq <= 4) return gemv_cols_u<JS, 4>(Jl, fvec, lane);
+  return gemv_cols_u<JS, 8>(Jl, fvec, lane);
+}
+
 // ---- solver row math (solver.py:886-1341 linesearch, 2154-2219 update_constraint) -----------
 // cls: 0 = equality (always quadratic), 1 = friction loss, 2 = one-sided (limit / contact)
 struct Row {
@@ -239,10 +287,27 @@ struct Row {
   int cls;
 };
 
+// MJW_DENSE_FASTLS (default 1): the line search's row evaluation and row_force as selects instead of
+// per-lane branches (same values; the branches cost exec-mask bookkeeping on every evaluation: the CG
+// loop is 9 % shorter); 0 builds the branchy form for A/B runs
+#ifndef MJW_DENSE_FASTLS
+#define MJW_DENSE_FASTLS 1
+#endif
 __device__ __forceinline__ void row_eval(const Row& w, float alpha, float& c, float& g, float& hh) {
   float x = fmaf(alpha, w.jv, w.jaref);
   bool quad = (w.cls == 0) || (w.cls == 2 && x < 0.0f) || (w.cls == 1 && -w.rf < x && x < w.rf);
   float jvD = w.jv * w.D;
+#if MJW_DENSE_FASTLS
+  // non-short-circuit form (the && / || above become exec-mask branches)
+  quad = (w.cls == 0) | ((w.cls == 2) & (x < 0.0f)) | ((w.cls == 1) & (-w.rf < x) & (x < w.rf));
+  const bool lin = (w.cls == 1) & !quad;
+  const bool neg = x <= -w.rf;
+  const float cq = 0.5f * w.D * x * x, gq = jvD * x, hq = w.jv * jvD;
+  const float cl = w.fl * (-0.5f * w.rf + (neg ? -x : x)), gl = neg ? -w.fl * w.jv : w.fl * w.jv;
+  c = quad ? cq : (lin ? cl : 0.0f);
+  g = quad ? gq : (lin ? gl : 0.0f);
+  hh = quad ? hq : 0.0f;
+#else
   if (quad) {
     c = 0.5f * w.D * x * x; g = jvD * x; hh = w.jv * jvD;
   } else if (w.cls == 1) {
@@ -253,7 +318,9 @@ __device__ __forceinline__ void row_eval(const Row& w, float alpha, float& c, fl
   } else {
     c = 0.0f; g = 0.0f; hh = 0.0f;
   }
+#endif
 }
+
 
 struct Pt {
   float alpha, c, g, h;
@@ -339,6 +406,17 @@ __device__ __forceinline__ bool bracket(const Pt& x, const Pt& y) { return (x.g 
 
 // force / state / cost of one row at its current jaref
 __device__ __forceinline__ float row_force(const Row& w, int& state, float& cost) {
+#if MJW_DENSE_FASTLS
+  // the same cases as selects (no per-lane branches)
+  const bool fr = w.cls == 1;
+  const bool lneg = fr & (w.jaref <= -w.rf), lpos = fr & !lneg & (w.jaref >= w.rf);
+  const bool sat = (w.cls == 2) & (w.jaref >= 0.0f);
+  const float fq = -w.D * w.jaref, cq = 0.5f * w.D * w.jaref * w.jaref;
+  const float cneg = -w.fl * (0.5f * w.rf + w.jaref), cpos = -w.fl * (0.5f * w.rf - w.jaref);
+  state = lneg ? STATE_LINEARNEG : (lpos ? STATE_LINEARPOS : (sat ? STATE_SATISFIED : STATE_QUADRATIC));
+  cost = lneg ? cneg : (lpos ? cpos : (sat ? 0.0f : cq));
+  return lneg ? w.fl : (lpos ? -w.fl : (sat ? 0.0f : fq));
+#endif
   float f;
   cost = 0.0f;
   if (w.cls == 1) {
@@ -408,7 +486,6 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
   const bool dof = c < nv;      // lane holds a dof value (both halves)
   const bool lo = lane < 32;
   const long gi = (long)wid * nv + c;
-  const int nvq = (nv + 3) >> 2;
 
   // per-world inputs of the later phases, loaded up front so that their global latency overlaps
   // the qM staging and the factorisation instead of stalling each phase
@@ -468,6 +545,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
   }
 
   PROF_MARK(PH_DFACTOR);
+  int niter_out = 0;  // CG / Newton iterations of this world (0 without rows)
   if (FLAGS & DF_SOLVE) {
     const int njmax = d.njmax;
     const int nefc = min(pf_nefc, njmax);
@@ -544,7 +622,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       if (lo) vd[c] = qacc;
       __syncthreads();
       ma = symv(Mm, vd, h);
-      w.jaref = gemv_rows<JS>(Jl, vd, lane, nvq) - aref;
+      w.jaref = gemv_rows_u<JS, NB / 4>(Jl, vd, lane) - aref;
       const int nrq = (min(nefc, 32) + 3) >> 2;
 
       float cost, gauss, qfrc_c, grad, Mgrad, grad_dot;
@@ -583,7 +661,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         if (!row) { force = 0.0f; rc = 0.0f; }
         vr[lane] = force;
         __syncthreads();
-        qfrc_c = gemv_cols<JS>(Jl, vr, lane, nrq);
+        qfrc_c = gemv_cols_n<JS>(Jl, vr, lane, nrq);
         // update_gradient's grad (solver.py:2879-2890) here, so that the Gauss term and |grad|^2 -- both
         // sums over the dofs -- share one reduction (dofs in lanes 0-31, replicated in 32-63)
         grad = dof ? ma - qfrc_smooth - qfrc_c : 0.0f;
@@ -688,7 +766,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         if (lo) vd[c] = search;
         __syncthreads();
         float mv = symv(Mm, vd, h);
-        w.jv = gemv_rows<JS>(Jl, vd, lane, nvq);
+        w.jv = gemv_rows_u<JS, NB / 4>(Jl, vd, lane);
         const float snorm = sqrtf(search_dot);
         const float gtol = fmaxf(tolerance * ls_tolerance * snorm * meaninertia * (float)nv, 1e-6f);
 #if MJW_DENSE_PAIRED
@@ -803,10 +881,21 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
         d.efc_state[(long)wid * d.njmax_pad + lane] = state;
       }
       if (lane == 0) d.solver_niter[wid] = niter;
+      niter_out = niter;
     }
   }
 
   PROF_MARK(PH_DSOLVE);
+#if MJW_SCHED_EARLY
+  // the next step's longest-first order (see dense_kernel): the bucket count is bumped here, before the
+  // integration, not as the wave's last instruction -- a wave leaves its slot only once its memory
+  // operations are done, and a same-address atomic issued last held every slot a while longer
+  if ((FLAGS & DF_SOLVE) && d.sched && lane == 0) {
+    const int key = MJW_SCHED_BUCKETS - 1 - min(niter_out >> 1, MJW_SCHED_BUCKETS - 1);
+    d.world_key[wid] = key;
+    atomicAdd(d.sched + key, 1);
+  }
+#endif
   if (FLAGS & DF_EULER) {
     // ---- forward.py:51-354 (_advance + euler)
     const float dt = MR(opt_timestep)[0];

@@ -7,16 +7,20 @@
 
 namespace mjw {
 
-// 3 waves/SIMD (up to 168 VGPRs, 12 worlds/CU): at 4 (128 VGPRs, 16 worlds/CU, which the 9.7 KB of
-// LDS would also allow) the Euler+CG instance spilled 6-11 registers; measured humanoid dense kernel
-// 0.295 -> 0.288 ms at 3, 0.287 ms at 2
+// NB = 32: 3 waves/SIMD (up to 168 VGPRs, 12 worlds/CU).  NB <= 28: 4 (128 VGPRs, 16 worlds/CU, which
+// the 9.7 KB of LDS also allows): since the unrolled J products (round 5) the NB = 28 instance spills
+// the same 20 B/lane at 128 VGPRs as at 166, and the humanoid dense kernel measured 0.313 -> 0.305 ms
+// (driver window) and 0.273 -> 0.264 ms (200 steps) at 4 (round 4: 0.295 -> 0.288 ms at 3, 0.287 at 2)
 // ELL: elliptic friction cones (opt.cone = ELLIPTIC), a separate instantiation so that the pyramidal
 // kernels keep their registers
 // NB: the compile-time bound of the factor / substitution loops (>= nv; 16, 28 or 32, mjw_dense.h).
 // The NB = 16 instances fit 128 VGPRs (4 waves/SIMD, 16 worlds/CU); the Euler-only one (5.9 KB of LDS,
 // 27 worlds/CU) fits 64.
+#ifndef MJW_DENSE_WPE
+#define MJW_DENSE_WPE 4  // NB = 28 (A/B builds: 3)
+#endif
 template <int FLAGS, int NB>
-constexpr int dense_waves_per_eu() { return FLAGS == DF_EULER ? 6 : (NB <= 16 ? 4 : 3); }
+constexpr int dense_waves_per_eu() { return FLAGS == DF_EULER ? 6 : (NB <= 16 ? 4 : (NB <= 28 ? MJW_DENSE_WPE : 3)); }
 template <int FLAGS, bool NEWTON, bool ELL, int NB>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(dense_waves_per_eu<FLAGS, NB>())))
 dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
@@ -27,7 +31,7 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   const int wid = d.sched ? d.world_order[b] : b;
   WLOG_T0();
   dense_world<FLAGS, NEWTON, ELL, NB>(m, d, wid, sm);
-  if ((FLAGS & DF_SOLVE) && d.sched && (threadIdx.x & 63) == 0) {
+  if (!MJW_SCHED_EARLY && (FLAGS & DF_SOLVE) && d.sched && (threadIdx.x & 63) == 0) {
     // the next step's order: bucket by this step's iterations, most iterations first
     const int key = MJW_SCHED_BUCKETS - 1 - min(d.solver_niter[wid] >> 1, MJW_SCHED_BUCKETS - 1);
     d.world_key[wid] = key;

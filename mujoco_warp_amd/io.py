@@ -14,6 +14,8 @@ import ctypes
 import dataclasses
 from typing import Optional, Sequence
 
+import os
+
 import numpy as np
 import torch
 
@@ -718,7 +720,8 @@ def _alloc_data(m, nworld, nconmax, njmax, naconmax, device, nccdmax=None, njmax
   d.contact.efc_address.fill_(-1)
   d.nacon = torch.zeros(1, dtype=torch.int32, device=device)
   d.ncollision = torch.zeros(1, dtype=torch.int32, device=device)
-  d.sched = torch.zeros(_lib.SCHED_WORDS, dtype=torch.int32, device=device)
+  # MJW_SCHED=0: no longest-first world order for the dense kernel (A/B runs)
+  d.sched = None if os.environ.get("MJW_SCHED") == "0" else torch.zeros(_lib.SCHED_WORDS, dtype=torch.int32, device=device)
   d.efc.J_rowadr = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
   d.mocap_quat[..., 0] = 1.0
   d.xquat[..., 0] = 1.0

@@ -19,6 +19,8 @@ cfg = bench.MODELS[model]
 sys.argv = ["bench.py", "--model", model]
 a = bench.parse()
 mjm = mjcf.load_model(os.path.join(bench.ROOT, cfg["path"]))
+if a.solver is not None:
+  mjw.override_model(mjm, [f"opt.solver={a.solver}"])
 mjd = mjcf.MjData(mjm)
 center = None
 if cfg["key"] is not None:
@@ -27,6 +29,7 @@ if cfg["key"] is not None:
 m = mjw.put_model(mjm, device="cuda")
 d = mjw.put_data(mjm, mjd, nworld=a.nworld, nconmax=a.nconmax, njmax=a.njmax, device="cuda", m=m)
 out = []
+prev_it = None
 for i in range(nsteps):
   mjw.ctrl_noise(m, d, i, center=center)
   e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -39,7 +42,14 @@ for i in range(nsteps):
   r = {"step": i, "ms": round(e0.elapsed_time(e1), 4), "niter_mean": round(float(it.mean()), 2), "niter_p50": int(np.percentile(it, 50)),
        "niter_p99": int(np.percentile(it, 99)), "niter_max": int(it.max()), "niter_sum": int(it.sum()),
        "nefc_mean": round(float(nefc.mean()), 2), "nefc_max": int(nefc.max()), "nworld_gt32rows": int((nefc > 32).sum())}
-  hist = np.bincount(np.minimum(it, 40), minlength=41)
+  # how well the previous step's iterations and this step's rows predict this step's iterations (the
+  # dense kernel's longest-first order uses the former)
+  if prev_it is not None and it.std() > 0 and prev_it.std() > 0:
+    r["corr_prev_niter"] = round(float(np.corrcoef(prev_it, it)[0, 1]), 3)
+  if it.std() > 0 and nefc.std() > 0:
+    r["corr_nefc"] = round(float(np.corrcoef(nefc, it)[0, 1]), 3)
+  prev_it = it
+  hist = np.bincount(np.minimum(it, 60), minlength=61)
   r["niter_hist"] = hist.tolist()
   out.append(r)
   print(json.dumps({k: v for k, v in r.items() if k != "niter_hist"}), flush=True)
