@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 30
+#define MJW_ABI_VERSION 31
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -44,6 +44,7 @@
   X(opt_disableflags) X(opt_enableflags) X(opt_broadphase_filter) X(opt_ls_parallel)               \
   X(is_sparse) X(nM) X(ntree) X(njrow)                                                             \
   X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nflexinc) X(nflexcg) X(nplane) \
+  X(nflexelemedge) X(nflexshelldata)                                                               \
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
   X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)             \
   X(nsensorcollision) X(nsensorccd) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)           \
@@ -118,7 +119,8 @@
   X(flex_elemadr, nflex) X(flex_elemnum, nflex) X(flex_elemdataadr, nflex) X(flex_elemedgeadr, nflex) \
   X(flex_condim, nflex) X(flex_cgeomadr, nflex + 1) X(flex_cgeom, nflexcg) X(plane_geom, nplane)   \
   X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert) X(flex_edge, nflexedge * 2)          \
-  X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata) X(flex_elemedge, nflexelem * 3)      \
+  X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata) X(flex_elemedge, nflexelemedge)      \
+  X(flex_shellnum, nflex) X(flex_shelldataadr, nflex) X(flex_shell, nflexshelldata)               \
   X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)                                     \
   X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)                            \
   X(mesh_polyadr, nmesh) X(mesh_polynum, nmesh) X(mesh_polyvertadr, nmeshpoly) X(mesh_polyvertnum, nmeshpoly) \
@@ -156,7 +158,7 @@
   X(efc_Ma, nv) X(sensordata, nsensordata) X(ccd_out, nxn_ccd * 32)                                 \
   X(qpos_t0, nq) X(qvel_t0, nv) X(act_t0, na) X(qvel_rk, nv) X(qacc_rk, nv) X(act_dot_rk, na)     \
   X(flexvert_xpos, nflexvert * 3) X(flexedge_length, nflexedge) X(flexedge_velocity, nflexedge)   \
-  X(flexedge_J, nflexedge * 6) X(flex_frc, nflexelem * 9 + nflexedge * 12)                        \
+  X(flexedge_J, nflexedge * 6) X(flex_frc, nflexelem * 12 + nflexedge * 12)                       \
   X(sp_body, nbody * 6) X(sp_vec, nv * 10) X(sp_row, njmax * 3) X(sp_LD, nM) X(sp_H, sp_nH * sp_nH) \
   X(efc_JT_val, njmax_pad * njrow)                                                                 \
   X(ten_length, ntendon) X(ten_velocity, ntendon) X(ten_J, nJten)

@@ -933,7 +933,9 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
   const float* fx = d.flexvert_xpos + (long)wid * m.nflexvert * 3;
   for (int f = 0; f < m.nflex; f++) {
     const int ncg = m.flex_cgeomadr[f + 1] - m.flex_cgeomadr[f];
-    const int nitem = m.flex_dim[f] == 2 ? m.flex_elemnum[f] * ncg : 0;
+    // dim 2: the elements; dim 3: the boundary (shell) triangles (collision_flex.py:531-683); dim 1: none
+    const bool shell = m.flex_dim[f] == 3;
+    const int nitem = (m.flex_dim[f] == 2 ? m.flex_elemnum[f] : (shell ? m.flex_shellnum[f] : 0)) * ncg;
     if (item >= nitem) {
       item -= nitem;
       continue;
@@ -949,7 +951,7 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
           gp[2] > b[5] + grow)
         return 0;
     }
-    const int* ev = m.flex_elem + m.flex_elemdataadr[f] + 3 * el;
+    const int* ev = shell ? m.flex_shell + m.flex_shelldataadr[f] + 3 * el : m.flex_elem + m.flex_elemdataadr[f] + 3 * el;
     const float* t[3];
     float cen[3] = {0.0f, 0.0f, 0.0f}, rad = 0.0f;
     for (int k = 0; k < 3; k++) {
@@ -1024,7 +1026,7 @@ __device__ __forceinline__ int collide_item(const mjw_model_t& m, const mjw_data
 __device__ int ncollide_items(const mjw_model_t& m) {
   int n = m.nxn + m.nflexvert * m.nplane;
   for (int f = 0; f < m.nflex; f++)
-    if (m.flex_dim[f] == 2) n += m.flex_elemnum[f] * (m.flex_cgeomadr[f + 1] - m.flex_cgeomadr[f]);
+    n += (m.flex_dim[f] == 2 ? m.flex_elemnum[f] : (m.flex_dim[f] == 3 ? m.flex_shellnum[f] : 0)) * (m.flex_cgeomadr[f + 1] - m.flex_cgeomadr[f]);
   return n;
 }
 
@@ -1070,7 +1072,7 @@ __device__ void collision(const mjw_model_t& m, const mjw_data_t& d, int wid, Sm
     fbox = &sm.fbox[0][0];
   }
   // the same bound sparse_launch sizes the LDS with (>= nitem)
-  const bool cached = (long)m.nxn + (long)m.nflexvert * m.nplane + (long)m.nflexelem * m.nflexcg <= SP_LDS_ITEMS_MAX;
+  const bool cached = (long)m.nxn + (long)m.nflexvert * m.nplane + ((long)m.nflexelem + m.nflexshelldata / 3) * m.nflexcg <= SP_LDS_ITEMS_MAX;
   int cnt = 0, passed = 0;
   for (int it = tid(); it < nitem; it += BLK) {
     const int n = collide_item(m, d, wid, it, -1, &passed, 0x7fffffff, fbox);
@@ -1941,43 +1943,44 @@ __device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, int wid)
     }
   }
   // flex elasticity (per element) and bending (per edge) into scratch, gathered per vertex below
-  float* frc = d.flex_frc + (long)wid * (m.nflexelem * 9 + m.nflexedge * 12);
+  float* frc = d.flex_frc + (long)wid * (m.nflexelem * 12 + m.nflexedge * 12);
   const float* fx = d.flexvert_xpos + (long)wid * m.nflexvert * 3;
   if (!(dsbl_spring && dsbl_damper) && !dsbl_spring) {
     const float dt = MR(opt_timestep)[0];
     const float* stiff = MR(flex_stiffness);
+    // the local edges of a segment / triangle / tetrahedron (passive.py:606-613)
+    const int le[4][6][2] = {{{0, 0}}, {{0, 1}}, {{1, 2}, {2, 0}, {0, 1}}, {{0, 1}, {1, 2}, {2, 0}, {2, 3}, {0, 3}, {1, 3}}};
     for (int f = 0; f < m.nflex; f++) {
-      if (m.flex_dim[f] != 2) continue;
+      const int dim = m.flex_dim[f], nve = dim + 1, ne = dim == 1 ? 1 : (dim == 2 ? 3 : 6);
       const float kD = (dt > 0.0f && !dsbl_damper) ? MR(flex_damping)[f] / dt : 0.0f;
       const int vb = m.flex_vertadr[f];
       for (int el = tid(); el < m.flex_elemnum[f]; el += BLK) {
         const int elemid = m.flex_elemadr[f] + el;
-        const int* ev = m.flex_elem + m.flex_elemdataadr[f] + 3 * el;
-        const int e2[3][2] = {{1, 2}, {2, 0}, {0, 1}};
-        float grad[3][6], elong[3], force[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-        for (int e = 0; e < 3; e++) {
-          const float* x0 = fx + 3 * (vb + ev[e2[e][0]]);
-          const float* x1 = fx + 3 * (vb + ev[e2[e][1]]);
+        const int* ev = m.flex_elem + m.flex_elemdataadr[f] + nve * el;
+        float grad[6][6], elong[6], force[4][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+        for (int e = 0; e < ne; e++) {
+          const float* x0 = fx + 3 * (vb + ev[le[dim][e][0]]);
+          const float* x1 = fx + 3 * (vb + ev[le[dim][e][1]]);
           for (int i = 0; i < 3; i++) { grad[e][i] = x0[i] - x1[i]; grad[e][3 + i] = x1[i] - x0[i]; }
-          const int idx = m.flex_edgeadr[f] + m.flex_elemedge[m.flex_elemedgeadr[f] + 3 * el + e];
+          const int idx = m.flex_edgeadr[f] + m.flex_elemedge[m.flex_elemedgeadr[f] + ne * el + e];
           const float vel = d.flexedge_velocity[(long)wid * m.nflexedge + idx];
           const float def = d.flexedge_length[(long)wid * m.nflexedge + idx], ref = MR(flexedge_length0)[idx];
           const float prev = def - vel * dt;
           elong[e] = def * def - ref * ref + (def * def - prev * prev) * kD;
         }
-        float metric[3][3];
+        float metric[6][6];
         int id = 0;
-        for (int a = 0; a < 3; a++)
-          for (int b = a; b < 3; b++) { metric[a][b] = metric[b][a] = stiff[21 * elemid + id]; id++; }
-        for (int a = 0; a < 3; a++)
-          for (int b = 0; b < 3; b++)
+        for (int a = 0; a < ne; a++)
+          for (int b = a; b < ne; b++) { metric[a][b] = metric[b][a] = stiff[21 * elemid + id]; id++; }
+        for (int a = 0; a < ne; a++)
+          for (int b = 0; b < ne; b++)
             for (int s2 = 0; s2 < 2; s2++)
-              for (int x = 0; x < 3; x++) force[e2[b][s2]][x] -= elong[a] * grad[b][3 * s2 + x] * metric[a][b];
-        for (int k = 0; k < 3; k++)
-          for (int x = 0; x < 3; x++) frc[9 * elemid + 3 * k + x] = force[k][x];
+              for (int x = 0; x < 3; x++) force[le[dim][b][s2]][x] -= elong[a] * grad[b][3 * s2 + x] * metric[a][b];
+        for (int k = 0; k < nve; k++)
+          for (int x = 0; x < 3; x++) frc[12 * elemid + 3 * k + x] = force[k][x];
       }
       for (int e = m.flex_edgeadr[f] + tid(); e < m.flex_edgeadr[f] + m.flex_edgenum[f]; e += BLK) {
-        float* out = frc + 9 * m.nflexelem + 12 * e;
+        float* out = frc + 12 * m.nflexelem + 12 * e;
         if (m.flex_edgeflap[2 * e + 1] == -1) {
           for (int k = 0; k < 12; k++) out[k] = 0.0f;
           continue;
@@ -2007,15 +2010,15 @@ __device__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, int wid)
     }
   }
   __syncthreads();
-  // per-vertex gather in a fixed order (flexvert_inc: 4*nflexelem... encoded contributions)
+  // per-vertex gather in a fixed order (flexvert_inc: encoded contributions)
   if (!(dsbl_spring && dsbl_damper) && !dsbl_spring) {
     for (int v = tid(); v < m.nflexvert; v += BLK) {
       const int b = m.flex_vertbodyid[v];
       if (m.body_dofnum[b] == 0) continue;
       float s[3] = {0.0f, 0.0f, 0.0f};
       for (int p = m.flexvert_incadr[v]; p < m.flexvert_incadr[v + 1]; p++) {
-        const int code = m.flexvert_inc[p];  // 3*elem + k (element vertex slot) or 3*nflexelem + 4*edge + k
-        const float* src = code < 3 * m.nflexelem ? frc + 3 * code : frc + 9 * m.nflexelem + 3 * (code - 3 * m.nflexelem);
+        const int code = m.flexvert_inc[p];  // 4*elem + k (element vertex slot) or 4*nflexelem + 4*edge + k
+        const float* src = code < 4 * m.nflexelem ? frc + 3 * code : frc + 12 * m.nflexelem + 3 * (code - 4 * m.nflexelem);
         for (int x = 0; x < 3; x++) s[x] += src[x];
       }
       for (int x = 0; x < 3; x++) qs[m.body_dofadr[b] + x] += s[x];
@@ -3395,7 +3398,7 @@ int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStre
       }
     }
     // collision items (upper bound of ncollide_items): one LDS byte each when they fit
-    const long nitem = (long)m->nxn + (long)m->nflexvert * m->nplane + (long)m->nflexelem * m->nflexcg;
+    const long nitem = (long)m->nxn + (long)m->nflexvert * m->nplane + ((long)m->nflexelem + m->nflexshelldata / 3) * m->nflexcg;
     const size_t lds = nitem <= sp::SP_LDS_ITEMS_MAX ? (size_t)((nitem + 3) & ~3L) : 0;
     hipLaunchKernelGGL(sp::forward_kernel<sp::SP_COLL>, dim3(nw), dim3(sp::BLK), lds, s, *m, *d, fwd);
     trace_launch(s, K_SP_COLL);

@@ -150,8 +150,6 @@ def put_model(mjm, device=None) -> types.Model:
       # the sensor kernel (csrc/mjw_sensor.hip) stages a world's body / dof state in 64 KB of LDS
       if 37 * mjm.nbody + 14 * mjm.nv > 16384:
         raise NotImplementedError("sparse / flex models: sensors need 37 nbody + 14 nv <= 16384 in this build (the flex bodies exceed it).")
-    if getattr(mjm, "nflex", 0) and np.any(mjm.flex_dim != 2):
-      raise NotImplementedError("only dim-2 flexes are supported by this build yet.")
   for st in np.unique(getattr(mjm, "sensor_type", np.zeros(0, dtype=np.int32))):
     if int(st) not in types.SUPPORTED_SENSORS:
       raise NotImplementedError(f"sensor type {int(st)} is not supported by this build yet.")
@@ -358,15 +356,17 @@ def put_model(mjm, device=None) -> types.Model:
         cg.append(g)
     cg_adr.append(len(cg))
   planes = np.nonzero(mjm.geom_type == 0)[0] if nflex else np.zeros(0, dtype=int)
-  # per-vertex contribution lists of the flex passive forces (element slots, then bending slots)
+  # per-vertex contribution lists of the flex passive forces: element vertex slots (4 per element, the
+  # first dim + 1 used), then bending slots (4 per edge)
   nfv = int(getattr(mjm, "nflexvert", 0))
   inc = [[] for _ in range(nfv)]
   for f in range(nflex):
     vb = mjm.flex_vertadr[f]
+    nve = int(mjm.flex_dim[f]) + 1
     for el in range(mjm.flex_elemnum[f]):
       eg = mjm.flex_elemadr[f] + el
-      for k in range(3):
-        inc[vb + mjm.flex_elem[mjm.flex_elemdataadr[f] + 3 * el + k]].append(3 * eg + k)
+      for k in range(nve):
+        inc[vb + mjm.flex_elem[mjm.flex_elemdataadr[f] + nve * el + k]].append(4 * eg + k)
   nelem = int(getattr(mjm, "nflexelem", 0))
   for f in range(nflex):
     vb = mjm.flex_vertadr[f]
@@ -375,11 +375,13 @@ def put_model(mjm, device=None) -> types.Model:
         continue
       vs = (mjm.flex_edge[e, 0], mjm.flex_edge[e, 1], mjm.flex_edgeflap[e, 0], mjm.flex_edgeflap[e, 1])
       for k, v in enumerate(vs):
-        inc[vb + v].append(3 * nelem + 4 * e + k)
+        inc[vb + v].append(4 * nelem + 4 * e + k)
   inc_adr = np.concatenate([[0], np.cumsum([len(x) for x in inc])]).astype(np.int32)
   inc_flat = np.array([c for x in inc for c in x], dtype=np.int32)
   m.nflex, m.nflexvert, m.nflexedge = nflex, nfv, int(getattr(mjm, "nflexedge", 0))
   m.nflexelem, m.nflexelemdata = nelem, int(getattr(mjm, "nflexelemdata", 0))
+  m.nflexelemedge = int(getattr(mjm, "nflexelemedge", 3 * nelem))
+  m.nflexshelldata = int(getattr(mjm, "nflexshelldata", 0))
   m.nflexinc, m.nflexcg, m.nplane = len(inc_flat), len(cg), len(planes)
   derived_int = dict(
     tree_dofadr=tree_dofadr,
@@ -611,7 +613,7 @@ def _data_shapes(m, nworld, njmax, njmax_pad, naconmax):
     qpos_t0=(nq,), qvel_t0=(nv,), act_t0=(na,), qvel_rk=(nv,), qacc_rk=(nv,), act_dot_rk=(na,),
     # flex (smooth.py:228-355) and the sparse path's workspace (size 0 on the dense path)
     flexvert_xpos=(m.nflexvert, 3), flexedge_length=(m.nflexedge,), flexedge_velocity=(m.nflexedge,),
-    flexedge_J=(m.nflexedge, 6), flex_frc=(m.nflexelem * 9 + m.nflexedge * 12,),
+    flexedge_J=(m.nflexedge, 6), flex_frc=(m.nflexelem * 12 + m.nflexedge * 12,),
     sp_body=(nb * 6 * sp,), sp_vec=(nv * 10 * sp,), sp_row=(njmax * 3 * sp,), sp_LD=(m.nM * sp,),
     sp_H=(m.sp_nH * m.sp_nH,),
     efc_JT_val=(njmax_pad * m.njrow * sp,),

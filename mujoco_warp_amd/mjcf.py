@@ -469,18 +469,21 @@ class _Compiler:
     return body
 
   def _flexcomp(self, el, parent, childclass):
-    """<flexcomp type="grid" dim="2">: one body per vertex, each a child of `parent` at the vertex
-    position with three slide joints (x, y, z) -- MuJoCo's flexcomp dof="full" -- and the vertex
-    mass mass/npoint.  Elements, edges and flaps are built after the body tree is indexed
+    """<flexcomp type="grid" | "direct" dim="1" | "2" | "3">: one body per vertex, each a child of
+    `parent` at the vertex position with three slide joints (x, y, z) -- MuJoCo's flexcomp dof="full"
+    -- and the vertex mass mass/npoint; <pin id="..."/> vertices get no joints (static).  Elements,
+    edges, flaps, shells and the elasticity constants are built after the body tree is indexed
     (`_build_flex`).  Grid ordering: point (ix, iy, iz) has index (ix*cy + iy)*cz + iz and sits at
-    spacing * (i - (count-1)/2) (MuJoCo user_flexcomp.cc, restated: parity unpinned, no MuJoCo here)."""
+    spacing * (i - (count-1)/2); dim 1 links consecutive points of its one long axis, dim 2 splits each
+    cell into two triangles, dim 3 each cube into six tetrahedra around its main diagonal (MuJoCo
+    user_flexcomp.cc, restated: parity unpinned, no MuJoCo here)."""
     a = el.attrib
     ftype = a.get("type", "grid")
     if ftype not in ("grid", "direct"):
       raise NotImplementedError(f"flexcomp type '{ftype}' is not supported (grid and direct only)")
     dim = int(a.get("dim", 2))
-    if dim != 2:
-      raise NotImplementedError("only dim=2 flexcomps are supported")
+    if dim not in (1, 2, 3):
+      raise ValueError(f"flexcomp dim must be 1, 2 or 3, got {dim}")
     if a.get("dof", "full") != "full":
       raise NotImplementedError("only flexcomp dof='full' is supported")
     pos = np.array(_floats(a.get("pos", "0 0 0"), 3))
@@ -493,15 +496,19 @@ class _Compiler:
       # type="direct": the points (flexcomp frame) and the triangles (vertex index triples) as given
       loc = np.array(_floats(a["point"]), dtype=float).reshape(-1, 3)
       pts = [R @ p_ + pos for p_ in loc]
-      tri = np.array([int(x) for x in a["element"].split()], dtype=np.int64).reshape(-1, 3)
+      tri = np.array([int(x) for x in a["element"].split()], dtype=np.int64).reshape(-1, dim + 1)
       if tri.size and (tri.min() < 0 or tri.max() >= len(pts)):
         raise ValueError(f"flexcomp '{name}': element index out of range")
       elems = [tuple(int(v) for v in t) for t in tri]
       npnt = len(pts)
     else:
       count = [int(x) for x in _floats(a.get("count", "10 10 1"), 3)]
-      if count[2] != 1:
+      if dim == 1 and sum(c > 1 for c in count) != 1:
+        raise NotImplementedError("dim=1 grid needs exactly one count > 1")
+      if dim == 2 and count[2] != 1:
         raise NotImplementedError("dim=2 grid needs count[2] == 1")
+      if dim == 3 and min(count) < 2:
+        raise NotImplementedError("dim=3 grid needs every count >= 2")
       spacing = np.array(_floats(a.get("spacing", "0.02 0.02 0.02"), 3))
       npnt = count[0] * count[1] * count[2]
       for ix in range(count[0]):
@@ -509,18 +516,42 @@ class _Compiler:
           for iz in range(count[2]):
             loc = spacing * (np.array([ix, iy, iz]) - 0.5 * (np.array(count) - 1))
             pts.append(R @ loc + pos)
-      cy = count[1]
-      for ix in range(count[0] - 1):
-        for iy in range(count[1] - 1):
-          v00, v10, v11, v01 = ix * cy + iy, (ix + 1) * cy + iy, (ix + 1) * cy + iy + 1, ix * cy + iy + 1
-          elems += [(v00, v10, v11), (v00, v11, v01)]
+      cy, cz = count[1], count[2]
+      if dim == 1:
+        elems = [(i, i + 1) for i in range(npnt - 1)]
+      elif dim == 2:
+        for ix in range(count[0] - 1):
+          for iy in range(count[1] - 1):
+            v00, v10, v11, v01 = ix * cy + iy, (ix + 1) * cy + iy, (ix + 1) * cy + iy + 1, ix * cy + iy + 1
+            elems += [(v00, v10, v11), (v00, v11, v01)]
+      else:
+        idx = lambda i, j, k: (i * cy + j) * cz + k  # noqa: E731
+        for ix in range(count[0] - 1):
+          for iy in range(count[1] - 1):
+            for iz in range(count[2] - 1):
+              c = [idx(ix + (q & 1), iy + ((q >> 1) & 1), iz + ((q >> 2) & 1)) for q in range(8)]
+              # Kuhn split: the six monotone paths 0 -> 7 through the cube (conforming across cells)
+              for p1, p2 in ((1, 3), (1, 5), (2, 3), (2, 6), (4, 5), (4, 6)):
+                t = [c[0], c[p1], c[p2], c[7]]
+                X = np.array([pts[v] for v in t])
+                if np.linalg.det(np.stack([X[1] - X[0], X[2] - X[0], X[3] - X[0]])) < 0:
+                  t[1], t[2] = t[2], t[1]  # positive orientation
+                elems.append(tuple(t))
+    pinned = set()
+    for pin in el.findall("pin"):
+      pinned |= {int(v) for v in pin.get("id", "").split()}
+    nfree = max(npnt - len(pinned), 1)
     bodies = []
     for i, p in enumerate(pts):
       b = _Body(f"{name}_{i}", parent, childclass)
       b.pos = np.asarray(p, dtype=float)
-      b.inertial = {"pos": "0 0 0", "mass": repr(mass / npnt), "diaginertia": "0 0 0"}
-      for ax in ("1 0 0", "0 1 0", "0 0 1"):
-        b.joints.append({"type": "slide", "axis": ax, "name": f"{name}_{i}_{'xyz'[len(b.joints)]}"})
+      if i in pinned:
+        # a pinned vertex is a static body at its rest position (no dofs, no mass)
+        b.inertial = {"pos": "0 0 0", "mass": "0", "diaginertia": "0 0 0"}
+      else:
+        b.inertial = {"pos": "0 0 0", "mass": repr(mass / nfree), "diaginertia": "0 0 0"}
+        for ax in ("1 0 0", "0 1 0", "0 0 1"):
+          b.joints.append({"type": "slide", "axis": ax, "name": f"{name}_{i}_{'xyz'[len(b.joints)]}"})
       parent.children.append(b)
       bodies.append(b)
     edge = el.find("edge")
@@ -530,7 +561,7 @@ class _Compiler:
     la = elast.attrib if elast is not None else {}
     ca = contact.attrib if contact is not None else {}
     self.flexcomps.append(dict(
-      name=name, dim=dim, bodies=bodies, elems=np.array(elems, dtype=np.int32).reshape(-1, 3),
+      name=name, dim=dim, bodies=bodies, elems=np.array(elems, dtype=np.int32).reshape(-1, dim + 1),
       radius=float(a.get("radius", 0.005)),
       edge_equality=ea.get("equality", "false") == "true",
       edge_solref=_merge_vec([0.02, 1.0], _floats(ea.get("solref", "0.02 1"))),
@@ -1043,67 +1074,111 @@ class _Compiler:
   def _build_flex(self):
     """mjModel flex_* tables of the flexcomps (MuJoCo user_flex.cc semantics, restated).
 
-    Edges are numbered in first-encounter order over the elements, each triangle contributing its
-    edges (1,2), (2,0), (0,1) -- the local edge order of passive.py:_flex_elasticity (:606-613).
-    flex_edgeflap holds the vertex opposite the edge in its first and second triangle (-1 on the
-    boundary).  flex_bending holds the 16 coefficients of the discrete quadratic bending energy of
-    the edge's two triangles (cotangent weights, Wardetzky et al. 2007 / Bergou et al. 2006) scaled
-    by mu*thickness^3 / (8*(A0 + A1)) with mu = young / (2*(1+poisson)), and a zero 17th (flat rest
-    shape); flex_stiffness (membrane) is zero unless elastic2d includes stretch, which is not
-    supported.  These compiler constants are parity unpinned: MuJoCo's compiler is not available."""
+    Edges are numbered in first-encounter order over the elements, each element contributing its local
+    edges in the order of passive.py:_flex_elasticity (:606-613): (0,1) for a segment; (1,2), (2,0),
+    (0,1) for a triangle; (0,1), (1,2), (2,0), (2,3), (0,3), (1,3) for a tetrahedron.  flex_edgeflap
+    holds the vertex opposite the edge in its first and second triangle (-1 on the boundary, and for
+    dims 1 / 3).  flex_bending holds the 16 coefficients of the discrete quadratic bending energy of a
+    triangle edge's two triangles (cotangent weights, Wardetzky et al. 2007 / Bergou et al. 2006)
+    scaled by mu*thickness^3 / (8*(A0 + A1)) with mu = young / (2*(1+poisson)), and a zero 17th (flat
+    rest shape).  flex_stiffness holds, per element, the upper triangle of the edge metric M of the
+    Saint Venant-Kirchhoff energy in the squared-edge-length strains s_e = L_e^2 - L0_e^2 that
+    passive.py:_flex_elasticity evaluates (energy = 1/4 s' M s; `_svk_metric`): volumetric for dim 3,
+    the membrane (elastic2d stretch / both) for dim 2, axial for dim 1.  flex_shell lists the boundary
+    triangles of a dim-3 flex (faces of one tetrahedron only, outward), the triangles
+    collision_flex.py:531-683 collides.  These compiler constants are parity unpinned: MuJoCo's
+    compiler is not available."""
     m = self.m
     bid = {id(b): i for i, b in enumerate(self.bodies)}
     fl = self.flexcomps
     m.nflex = len(fl)
     vertadr, vertnum, edgeadr, edgenum, elemadr, elemnum, elemdataadr, elemedgeadr = [], [], [], [], [], [], [], []
     vertbodyid, edges, flaps, elemdata, elemedge, bending, stiffness, length0, vertflexid = [], [], [], [], [], [], [], [], []
+    shellnum, shelladr, shell = [], [], []
+    nelem_tot = 0
     for f, fc in enumerate(fl):
-      if fc["elastic2d"] >= 2 and fc["young"] > 0:
-        raise NotImplementedError("flex membrane (stretch) elasticity is not supported by the MJCF compiler yet")
+      dim = fc["dim"]
       vb = [bid[id(b)] for b in fc["bodies"]]
-      x = np.array([b.pos for b in fc["bodies"]])  # vertex bodies are children of the world body
-      if any(m.body_parentid[b] != 0 for b in vb):
-        raise NotImplementedError("flexcomp vertex bodies must be children of the world body")
+      x = np.array([_body_world_pos(b) for b in fc["bodies"]])  # rest positions, world frame
       vertadr.append(len(vertbodyid))
       vertnum.append(len(vb))
       vertbodyid += vb
       vertflexid += [f] * len(vb)
       el = fc["elems"]
-      elemadr.append(len(elemedge) // 3)
+      ledges = _FLEX_LOCAL_EDGES[dim]
+      elemadr.append(nelem_tot)
       elemnum.append(len(el))
+      nelem_tot += len(el)
       elemdataadr.append(len(elemdata))
       elemedgeadr.append(len(elemedge))
       eid, fe, tri_of_edge = {}, [], []
       for t, tri in enumerate(el):
-        for a_, b_ in ((1, 2), (2, 0), (0, 1)):
+        for a_, b_ in ledges:
           key = (min(tri[a_], tri[b_]), max(tri[a_], tri[b_]))
           if key not in eid:
             eid[key] = len(fe)
             fe.append(key)
             tri_of_edge.append([])
-          tri_of_edge[eid[key]].append((t, 3 - a_ - b_))
+          if dim == 2:
+            tri_of_edge[eid[key]].append((t, 3 - a_ - b_))
           elemedge.append(eid[key])
         elemdata += [int(v) for v in tri]
       edgeadr.append(len(edges))
       edgenum.append(len(fe))
-      mu = fc["young"] / (2.0 * (1.0 + fc["poisson"]))
+      young, poisson = fc["young"], fc["poisson"]
+      mu = young / (2.0 * (1.0 + poisson))
       for e, (v0, v1) in enumerate(fe):
         edges.append((v0, v1))
-        fp = [int(el[t][k]) for t, k in tri_of_edge[e]][:2] + [-1]
+        fp = [int(el[t][k]) for t, k in tri_of_edge[e]][:2] + [-1, -1]
         flaps.append((fp[0], fp[1]))
         length0.append(float(np.linalg.norm(x[v1] - x[v0])))
         coef = np.zeros(17)
-        if fc["elastic2d"] in (1, 3) and fp[1] >= 0 and fc["thickness"] > 0 and mu > 0:
+        if dim == 2 and fc["elastic2d"] in (1, 3) and fp[1] >= 0 and fc["thickness"] > 0 and mu > 0:
           coef[:16] = _bending_coef(x[[v0, v1, fp[0], fp[1]]], mu, fc["thickness"])
         bending.append(coef)
-      stiffness += [np.zeros(21)] * len(el)
+      # element metrics: dim 3 always (young > 0), dim 2 with elastic2d stretch / both, dim 1 axial
+      use = young > 0 and (dim != 2 or fc["elastic2d"] >= 2)
+      if dim == 2 and use and not fc["thickness"] > 0:
+        raise ValueError(f"flexcomp '{fc['name']}': membrane elasticity needs a positive thickness")
+      for tri in el:
+        coef = np.zeros(21)
+        if use:
+          M = _svk_metric(x[list(tri)], young, poisson, dim, fc["thickness"], fc["radius"])
+          iu = np.triu_indices(len(ledges))
+          coef[:len(iu[0])] = M[iu]
+        stiffness.append(coef)
+      # dim 3: boundary faces (faces of exactly one tetrahedron), oriented away from the fourth vertex
+      shelladr.append(len(shell))
+      ns = 0
+      if dim == 3:
+        faces = {}
+        order = []
+        for t, tet in enumerate(el):
+          for skip in range(4):
+            face = [int(tet[k]) for k in range(4) if k != skip]
+            key = tuple(sorted(face))
+            if key not in faces:
+              faces[key] = [face, int(tet[skip]), 0]
+              order.append(key)
+            faces[key][2] += 1
+        for key in order:
+          face, opp, cnt = faces[key]
+          if cnt != 1:
+            continue
+          a_, b_, c_ = face
+          if np.dot(np.cross(x[b_] - x[a_], x[c_] - x[a_]), x[opp] - x[a_]) > 0:
+            b_, c_ = c_, b_
+          shell += [a_, b_, c_]
+          ns += 1
+      shellnum.append(ns)
     m.flex_dim = np.array([fc["dim"] for fc in fl], dtype=np.int32)
     m.flex_vertadr, m.flex_vertnum = np.array(vertadr, dtype=np.int32), np.array(vertnum, dtype=np.int32)
     m.flex_edgeadr, m.flex_edgenum = np.array(edgeadr, dtype=np.int32), np.array(edgenum, dtype=np.int32)
     m.flex_elemadr, m.flex_elemnum = np.array(elemadr, dtype=np.int32), np.array(elemnum, dtype=np.int32)
     m.flex_elemdataadr = np.array(elemdataadr, dtype=np.int32)
     m.flex_elemedgeadr = np.array(elemedgeadr, dtype=np.int32)
-    m.nflexvert, m.nflexedge, m.nflexelem, m.nflexelemdata = len(vertbodyid), len(edges), len(elemedge) // 3, len(elemdata)
+    m.nflexvert, m.nflexedge, m.nflexelem, m.nflexelemdata = len(vertbodyid), len(edges), nelem_tot, len(elemdata)
+    m.nflexelemedge = len(elemedge)
     m.flex_vertbodyid = np.array(vertbodyid, dtype=np.int32)
     m.flex_vertflexid = np.array(vertflexid, dtype=np.int32)
     m.flex_vert = np.zeros((m.nflexvert, 3))
@@ -1112,6 +1187,10 @@ class _Compiler:
     m.flex_edgeflap = np.array(flaps, dtype=np.int32).reshape(-1, 2)
     m.flex_elem = np.array(elemdata, dtype=np.int32)
     m.flex_elemedge = np.array(elemedge, dtype=np.int32)
+    m.flex_shellnum = np.array(shellnum, dtype=np.int32)
+    m.flex_shelldataadr = np.array(shelladr, dtype=np.int32)
+    m.flex_shell = np.array(shell, dtype=np.int32)
+    m.nflexshelldata = len(shell)
     m.flexedge_length0 = np.array(length0)
     m.flex_bending = np.array(bending).reshape(-1, 17)
     m.flex_stiffness = np.array(stiffness).reshape(-1, 21)
@@ -2078,6 +2157,54 @@ def _read_hfield_file(path):
   nrow, ncol = np.frombuffer(raw[:8], dtype="<i4")
   data = np.frombuffer(raw[8:8 + 4 * int(nrow) * int(ncol)], dtype="<f4").astype(np.float64)
   return int(nrow), int(ncol), data
+
+
+# the local edge order of one element (passive.py:606-613)
+_FLEX_LOCAL_EDGES = {1: ((0, 1),), 2: ((1, 2), (2, 0), (0, 1)), 3: ((0, 1), (1, 2), (2, 0), (2, 3), (0, 3), (1, 3))}
+
+
+def _body_world_pos(b):
+  """World position of a compiler body at qpos0 (its frame chain up to the world body)."""
+  p = np.zeros(3)
+  while b is not None and b.parent is not None:
+    p = quat_to_mat(np.asarray(b.quat, dtype=float)) @ p + np.asarray(b.pos, dtype=float)
+    b = b.parent
+  return p
+
+
+def _svk_metric(X, young, poisson, dim, thickness, radius):
+  """Edge metric M (nedge x nedge) of one flex element with rest vertices X ((dim+1) x 3) such that
+  its Saint Venant-Kirchhoff energy is 1/4 s' M s, s_e = L_e^2 - L0_e^2 over the local edges.
+
+  With g_i the barycentric gradients of the rest element (sum_i g_i = 0), the right Cauchy-Green
+  tensor is C = F'F = -sum_{i<j} L_ij^2 S_ij, S_ij = (g_i g_j' + g_j g_i') / 2, so the Green strain is
+  E = -1/2 sum_e s_e S_e and W = V (mu tr E^2 + lambda/2 (tr E)^2) gives
+  M[e1, e2] = V (mu tr(S_e1 S_e2) + lambda/2 tr(S_e1) tr(S_e2)).  dim 3: V the tetrahedron volume;
+  dim 2: V = area * thickness with the plane-stress lambda 2 lambda mu / (lambda + 2 mu) (the gradients
+  in the triangle's plane); dim 1: V = length * pi radius^2 and the axial modulus (M = young V tr(S)^2 / 2)."""
+  X = np.asarray(X, dtype=float)
+  D = (X[1:] - X[0]).T  # 3 x dim
+  G = np.linalg.pinv(D)  # dim x 3: rows = gradients of the barycentric coordinates 1..dim
+  g = np.vstack([-G.sum(axis=0), G])
+  lam = young * poisson / ((1.0 + poisson) * (1.0 - 2.0 * poisson)) if poisson < 0.5 else 0.0
+  mu = young / (2.0 * (1.0 + poisson))
+  if dim == 3:
+    vol = abs(np.linalg.det(D)) / 6.0
+  elif dim == 2:
+    vol = 0.5 * np.linalg.norm(np.cross(D[:, 0], D[:, 1])) * thickness
+    lam = 2.0 * lam * mu / (lam + 2.0 * mu)
+  else:
+    vol = np.linalg.norm(D[:, 0]) * np.pi * radius * radius
+  S = [0.5 * (np.outer(g[i], g[j]) + np.outer(g[j], g[i])) for i, j in _FLEX_LOCAL_EDGES[dim]]
+  n = len(S)
+  M = np.zeros((n, n))
+  for a in range(n):
+    for b in range(n):
+      if dim == 1:
+        M[a, b] = 0.5 * young * vol * np.trace(S[a]) * np.trace(S[b])
+      else:
+        M[a, b] = vol * (mu * np.trace(S[a] @ S[b]) + 0.5 * lam * np.trace(S[a]) * np.trace(S[b]))
+  return M
 
 
 def _bending_coef(x, mu, thickness):

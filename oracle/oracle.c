@@ -584,33 +584,40 @@ static void flex_kinematics(const orc_model* m, orc_data* d) {
 }
 
 /* passive.py:566-662 _flex_elasticity and :665-725 _flex_bending, accumulated into qfrc_spring */
+/* the local edges of a segment / triangle / tetrahedron, passive.py:606-613 */
+static const int flex_ledge[4][6][2] = {{{0}},
+                                        {{0, 1}},
+                                        {{1, 2}, {2, 0}, {0, 1}},
+                                        {{0, 1}, {1, 2}, {2, 0}, {2, 3}, {0, 3}, {1, 3}}};
+static const int flex_nledge[4] = {0, 1, 3, 6};
+
 static void flex_passive(const orc_model* m, orc_data* d) {
-  static const int edges2[3][2] = {{1, 2}, {2, 0}, {0, 1}};
   for (int f = 0; f < m->nflex; f++) {
-    if (m->flex_dim[f] != 2) continue;
+    const int dim = m->flex_dim[f], nve = dim + 1, ne = flex_nledge[dim];
+    const int(*edges2)[2] = flex_ledge[dim];
     real kD = (m->opt_timestep > 0 && !(m->opt_disableflags & DSBL_DAMPER)) ? m->flex_damping[f] / m->opt_timestep : 0;
     for (int el = 0; el < m->flex_elemnum[f]; el++) {
       int elemid = m->flex_elemadr[f] + el;
-      const int* ev = m->flex_elem + m->flex_elemdataadr[f] + 3 * el;
+      const int* ev = m->flex_elem + m->flex_elemdataadr[f] + nve * el;
       int vb = m->flex_vertadr[f];
-      real grad[3][6], elong[3], metric[3][3], force[3][3] = {{0}};
-      for (int e = 0; e < 3; e++) {
+      real grad[6][6], elong[6], metric[6][6], force[4][3] = {{0}};
+      for (int e = 0; e < ne; e++) {
         const real* x0 = d->flexvert_xpos + 3 * (vb + ev[edges2[e][0]]);
         const real* x1 = d->flexvert_xpos + 3 * (vb + ev[edges2[e][1]]);
         for (int i = 0; i < 3; i++) { grad[e][i] = x0[i] - x1[i]; grad[e][3 + i] = x1[i] - x0[i]; }
-        int idx = m->flex_edgeadr[f] + m->flex_elemedge[m->flex_elemedgeadr[f] + 3 * el + e];
+        int idx = m->flex_edgeadr[f] + m->flex_elemedge[m->flex_elemedgeadr[f] + ne * el + e];
         real vel = d->flexedge_velocity[idx], def = d->flexedge_length[idx], ref = m->flexedge_length0[idx];
         real prev = def - vel * m->opt_timestep;
         elong[e] = def * def - ref * ref + (def * def - prev * prev) * kD;
       }
       int id = 0;
-      for (int a = 0; a < 3; a++)
-        for (int b = a; b < 3; b++) { metric[a][b] = metric[b][a] = m->flex_stiffness[21 * elemid + id]; id++; }
-      for (int e1 = 0; e1 < 3; e1++)
-        for (int e2 = 0; e2 < 3; e2++)
+      for (int a = 0; a < ne; a++)
+        for (int b = a; b < ne; b++) { metric[a][b] = metric[b][a] = m->flex_stiffness[21 * elemid + id]; id++; }
+      for (int e1 = 0; e1 < ne; e1++)
+        for (int e2 = 0; e2 < ne; e2++)
           for (int i = 0; i < 2; i++)
             for (int x = 0; x < 3; x++) force[edges2[e2][i]][x] -= elong[e1] * grad[e2][3 * i + x] * metric[e1][e2];
-      for (int k = 0; k < 3; k++) {
+      for (int k = 0; k < nve; k++) {
         int b = m->flex_vertbodyid[vb + ev[k]];
         if (m->body_dofnum[b] == 0) continue;
         for (int x = 0; x < 3; x++) d->qfrc_spring[m->body_dofadr[b] + x] += force[k][x];
@@ -2296,14 +2303,18 @@ static void write_flex_contact(const orc_model* m, orc_data* d, real dist, const
   (void)m;
 }
 
-/* collision_flex.py:381-529 (dim-2 elements vs sphere / capsule / box / cylinder, every geom tested
- * -- the reference has no flex broadphase) and :261-378 (vertices vs planes) */
+/* collision_flex.py:381-529 (dim-2 elements and, :531-683, dim-3 shell triangles vs sphere / capsule /
+ * box / cylinder, every geom tested -- the reference has no flex broadphase) and :261-378 (vertices of
+ * every flex vs planes) */
 static void flex_collision(const orc_model* m, orc_data* d) {
   for (int f = 0; f < m->nflex; f++) {
-    if (m->flex_dim[f] != 2) continue;
+    /* dim 2: the elements; dim 3: the boundary (shell) triangles, collision_flex.py:531-683 */
+    if (m->flex_dim[f] != 2 && m->flex_dim[f] != 3) continue;
+    const int shell = m->flex_dim[f] == 3;
     real tr = m->flex_radius[f], tm = m->flex_margin[f];
-    for (int el = 0; el < m->flex_elemnum[f]; el++) {
-      const int* ev = m->flex_elem + m->flex_elemdataadr[f] + 3 * el;
+    const int ntri = shell ? m->flex_shellnum[f] : m->flex_elemnum[f];
+    for (int el = 0; el < ntri; el++) {
+      const int* ev = shell ? m->flex_shell + m->flex_shelldataadr[f] + 3 * el : m->flex_elem + m->flex_elemdataadr[f] + 3 * el;
       const real* t[3];
       for (int k = 0; k < 3; k++) t[k] = d->flexvert_xpos + 3 * (m->flex_vertadr[f] + ev[k]);
       for (int g = 0; g < m->ngeom; g++) {
