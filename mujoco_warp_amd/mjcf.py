@@ -464,8 +464,6 @@ class _Compiler:
           self._parse_frame_child(sub, body, childclass)
       elif tag == "flexcomp":
         self._flexcomp(child, body, childclass)
-      elif tag == "flex":
-        raise NotImplementedError("<flex> elements (explicit flex meshes) are not supported; use <flexcomp type='grid'>")
     return body
 
   def _flexcomp(self, el, parent, childclass):
@@ -554,13 +552,19 @@ class _Compiler:
           b.joints.append({"type": "slide", "axis": ax, "name": f"{name}_{i}_{'xyz'[len(b.joints)]}"})
       parent.children.append(b)
       bodies.append(b)
+    self.flexcomps.append(self._flex_params(el, name, dim, bodies, elems))
+
+  def _flex_params(self, el, name, dim, bodies, elems):
+    """The flex record of a <flexcomp> or an explicit <flex>: vertex bodies, elements and the
+    <edge> / <elasticity> / <contact> children's parameters (MuJoCo's defaults)."""
+    a = el.attrib
     edge = el.find("edge")
     elast = el.find("elasticity")
     contact = el.find("contact")
     ea = edge.attrib if edge is not None else {}
     la = elast.attrib if elast is not None else {}
     ca = contact.attrib if contact is not None else {}
-    self.flexcomps.append(dict(
+    return dict(
       name=name, dim=dim, bodies=bodies, elems=np.array(elems, dtype=np.int32).reshape(-1, dim + 1),
       radius=float(a.get("radius", 0.005)),
       edge_equality=ea.get("equality", "false") == "true",
@@ -574,7 +578,34 @@ class _Compiler:
       solref=_merge_vec([0.02, 1.0], _floats(ca.get("solref", "0.02 1"))),
       solimp=_merge_vec([0.9, 0.95, 0.001, 0.5, 2.0], _floats(ca.get("solimp", "0.9 0.95 0.001 0.5 2"))),
       margin=float(ca.get("margin", 0.0)), gap=float(ca.get("gap", 0.0)),
-    ))
+    )
+
+  def _deformable(self, root):
+    """<deformable><flex dim body="b0 b1 ..." element="..."/>: an explicit flex over existing bodies,
+    one vertex per listed body at the body's origin (MuJoCo's <flex> without `vertex`); its elements,
+    edges and elasticity are built like a flexcomp's (`_build_flex`)."""
+    by_name = {b.name: b for b in self.bodies}
+    for dfm in root.findall("deformable"):
+      for el in dfm:
+        if el.tag == "skin":
+          continue
+        if el.tag != "flex":
+          raise NotImplementedError(f"<deformable><{el.tag}> is not supported")
+        a = el.attrib
+        dim = int(a.get("dim", 2))
+        if dim not in (1, 2, 3):
+          raise ValueError(f"flex dim must be 1, 2 or 3, got {dim}")
+        if a.get("vertex", "").strip():
+          raise NotImplementedError("<flex vertex=...> (vertices in body-local coordinates) is not supported; list one body per vertex")
+        names = a.get("body", "").split()
+        missing = [n for n in names if n not in by_name]
+        if missing:
+          raise ValueError(f"flex '{a.get('name', '')}': unknown bodies {missing}")
+        elems = np.array([int(x) for x in a.get("element", "").split()], dtype=np.int64).reshape(-1, dim + 1)
+        if elems.size and (elems.min() < 0 or elems.max() >= len(names)):
+          raise ValueError(f"flex '{a.get('name', '')}': element index out of range")
+        name = a.get("name", f"flex{len(self.flexcomps)}")
+        self.flexcomps.append(self._flex_params(el, name, dim, [by_name[n] for n in names], [tuple(int(v) for v in t) for t in elems]))
 
   def _parse_frame_child(self, child, body, childclass):
     """A child of a <frame> whose pose has already been composed with the frame's."""
@@ -713,6 +744,7 @@ class _Compiler:
 
     visit(world)
     self.bodies = bodies
+    self._deformable(root)
     self._build_tables(root)
     return m
 

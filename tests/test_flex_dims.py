@@ -237,3 +237,35 @@ def test_gpu_flex_dims_match_oracle(scene):
     mjw.step(m, d)
   torch.cuda.synchronize()
   assert torch.isfinite(d.qpos).all()
+
+
+def test_explicit_flex_matches_the_flexcomp():
+  """<deformable><flex body=... element=...> over hand-made vertex bodies compiles to the flexcomp's
+  tables and dynamics (a 3 x 3 sheet with bending and membrane elasticity)."""
+  from mujoco_warp_amd import mjcf
+
+  opts = '<edge equality="true"/><contact contype="0" conaffinity="0"/><elasticity young="1e3" poisson=".2" thickness=".01" elastic2d="both"/>'
+  comp = mjcf.load_model_from_string(f"""<mujoco><worldbody><geom type="plane" size="0 0 1"/>
+    <flexcomp type="grid" count="3 3 1" spacing=".1 .1 .1" pos="0 0 .3" radius=".01" name="s" dim="2" mass=".9">{opts}</flexcomp>
+    </worldbody></mujoco>""")
+  bodies, names = [], []
+  for i in range(9):
+    ix, iy = divmod(i, 3)
+    x, y = 0.1 * (ix - 1), 0.1 * (iy - 1)
+    names.append(f"v{i}")
+    bodies.append(f'<body name="v{i}" pos="{x} {y} .3"><inertial pos="0 0 0" mass=".1" diaginertia="0 0 0"/>'
+                  + "".join(f'<joint type="slide" axis="{ax}"/>' for ax in ("1 0 0", "0 1 0", "0 0 1")) + "</body>")
+  elems = " ".join(" ".join(map(str, t)) for t in comp.flex_elem.reshape(-1, 3))
+  expl = mjcf.load_model_from_string(f"""<mujoco><worldbody><geom type="plane" size="0 0 1"/>{''.join(bodies)}</worldbody>
+    <deformable><flex name="s" dim="2" radius=".01" body="{' '.join(names)}" element="{elems}">{opts}</flex></deformable></mujoco>""")
+  for f in ("flex_edge", "flex_edgeflap", "flex_elemedge", "flexedge_length0", "flex_bending", "flex_stiffness", "flex_vertbodyid"):
+    np.testing.assert_allclose(np.asarray(getattr(expl, f), float), np.asarray(getattr(comp, f), float), rtol=1e-12, atol=1e-12, err_msg=f)
+  rng = np.random.default_rng(1)
+  q = comp.qpos0 + 0.01 * rng.normal(size=comp.nq)
+  v = 0.1 * rng.normal(size=comp.nv)
+  outs = []
+  for mjm in (comp, expl):
+    _, od = oracle_from_state(mjm, q[None], v[None], np.zeros((1, mjm.nu)), njmax=128, nconmax=32)
+    od.forward()
+    outs.append(od.qacc[0].copy())
+  np.testing.assert_allclose(outs[1], outs[0], rtol=1e-10, atol=1e-10)
