@@ -19,10 +19,12 @@ namespace mjw {
 #ifndef MJW_DENSE_WPE
 #define MJW_DENSE_WPE 4  // NB = 28 (A/B builds: 3)
 #endif
-template <int FLAGS, int NB>
-constexpr int dense_waves_per_eu() { return FLAGS == DF_EULER ? 6 : (NB <= 16 ? 4 : (NB <= 28 ? MJW_DENSE_WPE : 3)); }
+// (Newton keeps 3: at 4 its NB = 28 instances allocate more registers, not fewer -- apollo's dense
+// kernel measured 0.153 -> 0.173 ms)
+template <int FLAGS, bool NEWTON, int NB>
+constexpr int dense_waves_per_eu() { return FLAGS == DF_EULER ? 6 : (NB <= 16 ? 4 : (NB <= 28 && !NEWTON ? MJW_DENSE_WPE : 3)); }
 template <int FLAGS, bool NEWTON, bool ELL, int NB>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(dense_waves_per_eu<FLAGS, NB>())))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(dense_waves_per_eu<FLAGS, NEWTON, NB>())))
 dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   __shared__ __attribute__((aligned(16))) float sm[dense_lds_words<FLAGS, NEWTON, ELL, NB>()];
   const int b = w0 + (int)blockIdx.x;

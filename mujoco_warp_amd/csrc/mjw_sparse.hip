@@ -2376,7 +2376,7 @@ __device__ __forceinline__ void ccd_body(const mjw_model_t& m, const mjw_data_t&
     }
   }
 }
-__global__ void __launch_bounds__(64) ccd_kernel(const mjw_model_t m, const mjw_data_t d) { ccd_body<false>(m, d); }
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) ccd_kernel(const mjw_model_t m, const mjw_data_t d) { ccd_body<false>(m, d); }
 __global__ void __launch_bounds__(64) ccd_hf_kernel(const mjw_model_t m, const mjw_data_t d) { ccd_body<true>(m, d); }
 
 // ---------------------------------------------------------------------------------------------
