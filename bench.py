@@ -116,7 +116,8 @@ def b_alg_groups(mjm, words, nefc_mean, ncon_mean, row_words, sparse):
   (transposed index + CG: qacc, qfrc_constraint, efc_Ma, solver scalars, efc force / state) and euler."""
   fwd, dense = b_alg_parts(words, nefc_mean, ncon_mean, row_words)
   if not sparse:
-    return {"forward": fwd, "dense": dense}
+    # step: the fused whole-step kernel (mjw_step.hip step_kernel) writes both groups' outputs
+    return {"forward": fwd, "dense": dense, "step": fwd + dense}
   solve = 4.0 * (3 * mjm.nv + 5 + 2.0 * nefc_mean)
   euler = 4.0 * (mjm.nq + 2 * mjm.nv + 1)
   return {"forward": fwd + dense - solve - euler, "solve": solve, "euler": euler}
@@ -134,6 +135,8 @@ def kernel_group(name, sparse):
     return "forward"
   if "dense_kernel" in name or "sensor_acc" in name or "sensor_coll" in name:
     return "dense"
+  if "step_kernel" in name:
+    return "step"
   return "forward"
 
 

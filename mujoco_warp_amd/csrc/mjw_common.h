@@ -308,6 +308,7 @@ enum : int {
   K_RESET = 0, K_CTRL_NOISE, K_CCD, K_SENSOR, K_RK4,
   K_SP_POS, K_SP_CCD, K_SP_COLL, K_SP_CON, K_SP_VEL, K_SP_INDEX, K_SP_SOLVE, K_SP_SOLVE_LDS, K_SP_EULER,
   K_CCD_HF, K_SENSOR_COLL, K_SP_CCD_HF,
+  K_STEP = 17,  // + NEWTON + 2 * BOX + 4 * nbi  (step_kernel<79, BOX, 7, NEWTON, NB>, NB = 28 / 16 for nbi 0 / 1)
   K_DENSE = 32,  // + 32 * nbi + 4 * FLAGS + 2 * ELL + NEWTON  (dense_kernel<FLAGS, NEWTON, ELL, NB>, NB = 32 / 16 / 28 for nbi 0 / 1 / 2)
   K_FWD = 256,   // + 4 * STAGES + 2 * box + tendon    (mjw_kernel<STAGES, box, tendon>)
   K_END = 256 + 4 * 256

@@ -18,6 +18,7 @@
 #include "mjw_passive.h"
 #include "mjw_tendon.h"
 #include "mjw_trn.h"
+#include "mjw_dense.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -2575,6 +2576,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
   WLOG_END(w.wid, 0);
 }
 
+// One wave runs the whole step of one world: the forward stages (direct mode, run_stages) and then,
+// in the same LDS, the dense factor / CG-or-Newton solve / Euler of mjw_dense.h.  No kernel boundary
+// between the two halves, so the forward kernel's tail and the dense kernel's ramp-up do not serialise
+// and a world's qM / J hand-off is read back while still L2-resident.  4 waves / SIMD: the forward half
+// needs 113 VGPRs, the dense half (NB <= 28, CG) 128.  Launched for the full step when neither sensors
+// nor an implicit integration split the dense work (run(); MJW_FUSED=0 keeps the two kernels).
+template <int STAGES, bool BOX, int FLAGS, bool NEWTON, int NB>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) step_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int b = w0 + (int)blockIdx.x;
+  if (b >= d.nworld) return;
+  WS w;
+  w.s = smem;
+  w.si = reinterpret_cast<int*>(smem);
+  // the longest-first order of the previous step's solve (a permutation) when the step built it
+  w.wid = d.sched ? d.world_order[b] : b;
+  w.lane = lane_id();
+  run_stages<STAGES, BOX, false>(m, d, L, w);
+  __syncthreads();  // the forward outputs (global) and the LDS are the dense half's from here
+  dense_world<FLAGS, NEWTON, false, NB>(m, d, w.wid, smem);
+}
+
 // -------------------------------------------------------------------------------------------
 // collision pre-pass: one wave per world recomputes the geom frames (the forward kernel's own
 // kinematics()) and, for the pairs with a pre-pass slot (nxn_ccdid >= 0), applies the broadphase
@@ -2920,6 +2943,44 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
 // the register-resident path (mjw_dense.h) covers worlds with nv <= 32 and njmax <= 64
 bool dense_ok(const mjw_model_t* m, const mjw_data_t* d) { return m->nv <= 32 && d->njmax <= 64; }
 
+// the fused whole-step kernel (step_kernel): instantiated for models without tendons / muscles /
+// gravity compensation / fluid / site or body transmissions (the lean forward variant), without box
+// pairs, with the dense factor bound NB = 28; returns kNotFused when it does not apply (the caller then
+// launches the forward and dense kernels)
+constexpr int kNotFused = 0x7fffffff;
+template <bool NEWTON>
+int launch_step_fused(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, const char* name) {
+  constexpr int STAGES = mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_NOFACTOR;
+  mjw::Lay L = mjw::make_layout(*m, d->njmax, true);
+  const size_t lds = std::max((size_t)L.total * 4, (size_t)mjw::dense_lds_words<7, NEWTON, false, 28>() * 4);
+  if (lds > 160 * 1024) return kNotFused;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute((const void*)mjw::step_kernel<STAGES, false, 7, NEWTON, 28>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  hipLaunchKernelGGL((mjw::step_kernel<STAGES, false, 7, NEWTON, 28>), dim3(d->nworld), dim3(64), lds, s, *m, *d, L, 0);
+  mjw::trace_launch(s, mjw::K_STEP + (NEWTON ? 1 : 0));
+  return set_err(hipGetLastError(), name);
+}
+
+int step_fused(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, const char* name) {
+  using namespace mjw;
+  static const bool on = [] {
+    const char* e = getenv("MJW_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  if (!on) return kNotFused;
+  const int fl = m->opt_disableflags;
+  const bool implicit_int = m->opt_integrator == INT_IMPLICITFAST
+                                ? (fl & (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)) != (DSBL_ACTUATION | DSBL_SPRING | DSBL_DAMPER)
+                                : !(fl & (DSBL_EULERDAMP | DSBL_DAMPER));
+  const bool lean = m->ntendon == 0 && m->nmuscle == 0 && m->ngravcomp == 0 && !m->has_fluid && m->nbodytrn == 0 && m->nsitetrn == 0 && m->nxn_box == 0;
+  const bool ccd = m->nxn_ccd > 0 && d->naconmax > 0 && !(fl & (DSBL_CONSTRAINT | DSBL_CONTACT));
+  if (!lean || ccd || implicit_int || m->opt_cone == CONE_ELLIPTIC || m->opt_integrator == INT_RK4 || m->nv <= 16 || m->nv > 28)
+    return kNotFused;
+  return m->opt_solver == SOLVER_NEWTON ? launch_step_fused<true>(m, d, s, name) : launch_step_fused<false>(m, d, s, name);
+}
+
 // optional timing events for the next run(): before the forward kernel, between it and
 // the dense kernel, after the dense kernel (mjw_step_events)
 thread_local hipEvent_t g_ev[3] = {nullptr, nullptr, nullptr};
@@ -2978,6 +3039,10 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
   mjw_data_t dv = *d;
   if (!order) dv.sched = nullptr;
   d = &dv;
+  if (dense_ok(m, d) && !acc_sensors && stages == (ST_POS | ST_VEL | ST_ACT | ST_ACC | ST_SOLVE | ST_EULER) && !g_ev[0]) {
+    const int r = step_fused(m, d, s, name);
+    if (r != kNotFused) return r;
+  }
   if (dense_ok(m, d)) {
     // generic kernel up to qfrc_smooth, then the dense factor / solve / euler kernel, for the
     // world range [w0, w0 + cnt) on stream st; `timed` records the optional bench events.
@@ -3116,6 +3181,11 @@ const char* mjw_kernel_name(int id) {
                                "mjw::ccd_hf_kernel", "mjw::sensor_coll_kernel", "mjw::sp::ccd_hf_kernel"};
   static thread_local char buf[64];
   if (id >= 0 && id < (int)(sizeof(misc) / sizeof(misc[0]))) return misc[id];
+  if (id >= mjw::K_STEP && id < mjw::K_STEP + 8) {
+    const int k = id - mjw::K_STEP;
+    snprintf(buf, sizeof(buf), "mjw::step_kernel<79, %s, 7, %s, %d>", (k & 2) ? "true" : "false", (k & 1) ? "true" : "false", (k & 4) ? 16 : 28);
+    return buf;
+  }
   if (id >= mjw::K_DENSE && id < mjw::K_DENSE + 96) {
     const int k = (id - mjw::K_DENSE) & 31, nb[3] = {32, 16, 28};
     snprintf(buf, sizeof(buf), "mjw::dense_kernel<%d, %s, %s, %d>", k >> 2, (k & 1) ? "true" : "false", (k & 2) ? "true" : "false",
