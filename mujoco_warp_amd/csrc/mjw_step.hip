@@ -2943,7 +2943,7 @@ int launch_generic(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, con
 // the register-resident path (mjw_dense.h) covers worlds with nv <= 32 and njmax <= 64
 bool dense_ok(const mjw_model_t* m, const mjw_data_t* d) { return m->nv <= 32 && d->njmax <= 64; }
 
-// the fused whole-step kernel (step_kernel): instantiated for models without tendons / muscles /
+// the fused whole-step kernel (step_kernel): instantiated for CG models without tendons / muscles /
 // gravity compensation / fluid / site or body transmissions (the lean forward variant), without box
 // pairs, with the dense factor bound NB = 28; returns kNotFused when it does not apply (the caller then
 // launches the forward and dense kernels)
@@ -2978,7 +2978,10 @@ int step_fused(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, const c
   const bool ccd = m->nxn_ccd > 0 && d->naconmax > 0 && !(fl & (DSBL_CONSTRAINT | DSBL_CONTACT));
   if (!lean || ccd || implicit_int || m->opt_cone == CONE_ELLIPTIC || m->opt_integrator == INT_RK4 || m->nv <= 16 || m->nv > 28)
     return kNotFused;
-  return m->opt_solver == SOLVER_NEWTON ? launch_step_fused<true>(m, d, s, name) : launch_step_fused<false>(m, d, s, name);
+  // CG only: the Newton dense half needs 131-134 VGPRs and spills at the fused kernel's 128 (humanoid
+  // Newton measured 0.513 -> 0.558 ms fused)
+  if (m->opt_solver == SOLVER_NEWTON) return kNotFused;
+  return launch_step_fused<false>(m, d, s, name);
 }
 
 // optional timing events for the next run(): before the forward kernel, between it and
