@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 31
+#define MJW_ABI_VERSION 32
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -48,7 +48,7 @@
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
   X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)             \
   X(nsensorcollision) X(nsensorccd) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)           \
-  X(nmeshpoly) X(nmeshpolyvert) X(nmeshpolymap) X(nmaxpolygon) X(nmaxmeshdeg)
+  X(nmeshpoly) X(nmeshpolyvert) X(nmeshpolymap) X(nmaxpolygon) X(nmaxmeshdeg) X(nsensortaxel) X(nmeshnormal)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \
@@ -79,7 +79,7 @@
   X(sensor_cutoff, nsensor)                                                                        \
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)                                \
-  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17)                              \
+  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17) X(mesh_normal, nmeshnormal * 3) \
   X(mesh_vert, nmeshvert * 3) X(hfield_size, nhfield * 4) X(hfield_data, nhfielddata)             \
   X(mesh_polynormal, nmeshpoly * 3)                                                                \
   X(tendon_stiffness, ntendon) X(tendon_damping, ntendon) X(tendon_frictionloss, ntendon)          \
@@ -121,6 +121,7 @@
   X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert) X(flex_edge, nflexedge * 2)          \
   X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata) X(flex_elemedge, nflexelemedge)      \
   X(flex_shellnum, nflex) X(flex_shelldataadr, nflex) X(flex_shell, nflexshelldata)               \
+  X(taxel_vertadr, nsensortaxel) X(taxel_sensorid, nsensortaxel) X(mesh_normaladr, nmesh) X(mesh_normalnum, nmesh) \
   X(flexvert_incadr, nflexvert + 1) X(flexvert_inc, nflexinc)                                     \
   X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom)                            \
   X(mesh_polyadr, nmesh) X(mesh_polynum, nmesh) X(mesh_polyvertadr, nmeshpoly) X(mesh_polyvertnum, nmeshpoly) \

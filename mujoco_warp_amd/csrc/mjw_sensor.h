@@ -606,6 +606,96 @@ __device__ __forceinline__ int contact_at_row(const mjw_model_t& m, const mjw_da
   return cid;
 }
 
+// collision_sdf.py:157-183, 393-400: primitive signed distances in the geom frame (box: radial field inside);
+// other geom types have none here (0: no pressure)
+__device__ __forceinline__ float tactile_sdf(int type, const float* p, const float* size) {
+  if (type == GEOM_PLANE) return p[2];
+  if (type == GEOM_SPHERE) return sqrtf(dot3(p, p)) - size[0];
+  if (type == GEOM_BOX) {
+    float a[3];
+    for (int i = 0; i < 3; i++) a[i] = fabsf(p[i]) - size[i];
+    if (a[0] >= 0.0f || a[1] >= 0.0f || a[2] >= 0.0f) {
+      const float b0 = fmaxf(a[0], 0.0f), b1 = fmaxf(a[1], 0.0f), b2 = fmaxf(a[2], 0.0f);
+      return sqrtf(b0 * b0 + b1 * b1 + b2 * b2) + fminf(fmaxf(fmaxf(a[0], a[1]), a[2]), 0.0f);
+    }
+    float f[3];
+    for (int i = 0; i < 3; i++) f[i] = -size[i] / a[i];
+    const float fn = sqrtf(dot3(f, f));
+    float tmin = MJW_MAXVAL;
+    for (int i = 0; i < 3; i++) tmin = fminf(tmin, -a[i] / fabsf(f[i] / fn));
+    return -tmin;
+  }
+  if (type == GEOM_ELLIPSOID) {
+    float sp[3], s2[3];
+    for (int i = 0; i < 3; i++) { sp[i] = p[i] / size[i]; s2[i] = p[i] / (size[i] * size[i]); }
+    const float k0 = sqrtf(dot3(sp, sp)), k1 = sqrtf(dot3(s2, s2));
+    return k0 * (k0 - 1.0f) / (k1 != 0.0f ? k1 : 1e-12f);
+  }
+  return 0.0f;
+}
+
+// the geom on the other side of row r's contact when `side` of it is on weld body pw (-1: none)
+__device__ __forceinline__ int tactile_other(const mjw_model_t& m, const mjw_data_t& d, int wid, int pw, int r, int side) {
+  const int cid = contact_at_row(m, d, wid, r);
+  if (cid < 0) return -1;
+  const int g1 = d.contact_geom[2L * cid], g2 = d.contact_geom[2L * cid + 1];
+  if (g1 < 0 || g2 < 0) return -1;
+  const int g = side == 0 ? g1 : g2;
+  return m.body_weldid[m.geom_bodyid[g]] == pw ? (side == 0 ? g2 : g1) : -1;
+}
+
+// sensor.py:2085-2252 tactile, one sensor by the whole wave (lane = taxel): each vertex of the sensor's
+// mesh, placed with the sensor geom's pose, takes pressure depth / max(0.05 - depth, MINVAL) from every
+// distinct geom among the first MJ_MAXCONPAIR (50) contact partners of the sensor geom's weld body at which
+// the SDF is negative.  Partners come in the world's contact order (each contact at its first constraint
+// row; the reference's atomic order is arbitrary), deduplicated by rescanning the earlier ones instead of
+// an indexed list, so the kernel needs no scratch.  Layout [normal (nvt), tangent 1 (nvt), tangent 2
+// (nvt)]; the tangential slip terms need per-vertex tangent frames, which the compiler's meshes do not have
+// (mesh_normalnum = vertnum), so they are 0.
+__device__ void tactile_sensor(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s, int lane) {
+  const int mesh = m.sensor_objid[s], geom = m.sensor_refid[s];
+  const int nvt = m.mesh_vertnum[mesh];
+  float* out = d.sensordata + (long)wid * m.nsensordata + m.sensor_adr[s];
+  const int pw = m.body_weldid[m.geom_bodyid[geom]];
+  const int nefc = min(d.nefc[wid], d.njmax);
+  const float* gx = F.gxpos + 3 * geom;
+  const float* gm = F.gxmat + 9 * geom;
+  const float* vert = MR(mesh_vert) + 3 * (long)m.mesh_vertadr[mesh];
+  const float* nrm0 = MR(mesh_normal) + 3 * (long)m.mesh_normaladr[mesh];
+  const float* gsize = MR(geom_size);
+  for (int v = lane; v < nvt; v += 64) {
+    float x[3];
+    for (int i = 0; i < 3; i++) x[i] = gm[3 * i] * vert[3 * v] + gm[3 * i + 1] * vert[3 * v + 1] + gm[3 * i + 2] * vert[3 * v + 2] + gx[i];
+    const float* nrm = nrm0 + 3 * v;
+    const float nn = dot3(nrm, nrm);
+    float total = 0.0f;
+    int nadd = 0;
+    for (int r = 0; r < nefc && nadd < 50; r++) {
+      for (int side = 0; side < 2 && nadd < 50; side++) {
+        const int g = tactile_other(m, d, wid, pw, r, side);
+        if (g < 0) continue;
+        nadd++;
+        bool dup = false;
+        for (int r2 = 0; r2 <= r && !dup; r2++)
+          for (int s2 = 0; s2 < 2 && !dup; s2++)
+            if (r2 < r || s2 < side) dup = tactile_other(m, d, wid, pw, r2, s2) == g;
+        if (dup) continue;
+        const float* px = F.gxpos + 3 * g;
+        const float* pm = F.gxmat + 9 * g;
+        float dx[3], q[3];
+        for (int i = 0; i < 3; i++) dx[i] = x[i] - px[i];
+        mat_t_vec(q, pm, dx);
+        const float depth = fminf(tactile_sdf(m.geom_type[g], q, gsize + 3 * g), 0.0f);
+        if (depth >= 0.0f) continue;
+        total += depth / fmaxf(0.05f - depth, MJW_MINVAL) * nn;
+      }
+    }
+    out[v] = total;
+    out[nvt + v] = 0.0f;
+    out[2 * nvt + v] = 0.0f;
+  }
+}
+
 // sensor.py:2330-2375: does contact cid match sensor s, and in which direction (+-1; 0: no match)
 __device__ float contact_match(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s, int cid) {
   const int ot = m.sensor_objtype[s], oid = m.sensor_objid[s], rt = m.sensor_reftype[s], rid = m.sensor_refid[s];

@@ -323,6 +323,10 @@ __device__ __forceinline__ void sensor_body(const mjw_model_t& m, const mjw_data
     }
     sensor_write(m, d, wid, k, v, dim);
   }
+  // tactile sensors (sensor.py:2085-2252): one sensor at a time, lane = taxel
+  if ((stages & 4) && m.nsensortaxel > 0)
+    for (int k = 0; k < m.nsensor; k++)
+      if (m.sensor_type[k] == SENS_TACTILE) tactile_sensor(m, d, wid, F, k, lane);
 }
 
 __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L, int stages, int w0) {

@@ -302,6 +302,7 @@ def put_model(mjm, device=None) -> types.Model:
   m.nmesh, m.nmeshvert = int(getattr(mjm, "nmesh", 0)), int(getattr(mjm, "nmeshvert", 0))
   m.nhfield, m.nhfielddata = int(getattr(mjm, "nhfield", 0)), int(getattr(mjm, "nhfielddata", 0))
   m.nmeshpoly, m.nmeshpolyvert = int(getattr(mjm, "nmeshpoly", 0)), int(getattr(mjm, "nmeshpolyvert", 0))
+  m.nmeshnormal = int(getattr(mjm, "nmeshnormal", 0))
   m.nmeshpolymap = int(getattr(mjm, "nmeshpolymap", 0))
   # multi-contact workspace (collision_convex.py:1120-1140): 4-gon faces / 3 normals per vertex for box-box;
   # with MULTICCD and box-mesh / mesh-mesh pairs the meshes' largest polygon and vertex degree
@@ -318,6 +319,14 @@ def put_model(mjm, device=None) -> types.Model:
 
   m.nJmom = int(sum(_mom_nnz(mjm, a) for a in range(mjm.nu)))
   sc_adr, sc_num, sc_pair = _sensor_collision_pairs(mjm, pairid_all)
+  # io.py:556-567: one taxel per vertex of each tactile sensor's mesh (global vertex index, sensor id)
+  taxel_vertadr, taxel_sensorid = [], []
+  for s_ in range(int(getattr(mjm, "nsensor", 0))):
+    if int(mjm.sensor_type[s_]) == types.SensorType.TACTILE:
+      mid = int(mjm.sensor_objid[s_])
+      taxel_vertadr += [int(mjm.mesh_vertadr[mid]) + j for j in range(int(mjm.mesh_vertnum[mid]))]
+      taxel_sensorid += [s_] * int(mjm.mesh_vertnum[mid])
+  m.nsensortaxel = len(taxel_vertadr)
   m.nsensorcollision = len(sc_pair) // 4
   sc_kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in sc_pair.reshape(-1, 4)[:, :2]]
   m.nsensorccd = int(sum(k in _SENSOR_CONVEX or k in _SENSOR_HFIELD for k in sc_kinds))  # records the sensor kernel runs in lockstep
@@ -397,12 +406,15 @@ def put_model(mjm, device=None) -> types.Model:
     level_adr=level_adr,
     jnt_limited_slide_hinge_adr=jnt_limited_sh,
     jnt_limited_ball_adr=jnt_limited_ball,
+    taxel_vertadr=np.array(taxel_vertadr, dtype=np.int32),
+    taxel_sensorid=np.array(taxel_sensorid, dtype=np.int32),
     sensor_collision_adr=sc_adr,
     sensor_collision_num=sc_num,
     sensor_collision_pair=sc_pair,
   )
   for k_, v_ in derived_int.items():
     if k_ in ("tree_dofadr", "flex_cgeomadr", "flex_cgeom", "plane_geom", "flexvert_incadr", "flexvert_inc", "body_fluid_ellipsoid",
+              "taxel_vertadr", "taxel_sensorid",
               "sensor_collision_adr", "sensor_collision_num", "sensor_collision_pair"):
       setattr(m, k_, _i32(v_, dev))
   m.body_subtree_end = _i32(subtree_end, dev)
@@ -520,10 +532,11 @@ DERIVED_INT_ARRAYS = {
   "tree_dofadr": "tree_dofadr", "flex_cgeomadr": "flex_cgeomadr", "flex_cgeom": "flex_cgeom", "plane_geom": "plane_geom",
   "flexvert_incadr": "flexvert_incadr", "flexvert_inc": "flexvert_inc",
   "sensor_collision_adr": "sensor_collision_adr", "sensor_collision_num": "sensor_collision_num", "sensor_collision_pair": "sensor_collision_pair",
+  "taxel_vertadr": "taxel_vertadr", "taxel_sensorid": "taxel_sensorid",
 }
 DERIVED_SCALARS = ("act_maxnnz", "nbodytrn", "nsitetrn", "nten_spatial", "nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle", "sp_nH",
                    "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane",
-                   "nsensorcollision", "nsensorccd")
+                   "nsensorcollision", "nsensorccd", "nsensortaxel")
 
 
 def derive_model_fields(mjm) -> dict:

@@ -1045,6 +1045,14 @@ class _Compiler:
     m.mesh_vertadr = np.concatenate([[0], np.cumsum(m.mesh_vertnum)[:-1]]).astype(np.int32) if m.nmesh else np.zeros(0, np.int32)
     m.mesh_vert = np.concatenate([v for v, _ in self.mesh_data]) if m.nmesh else np.zeros((0, 3))
     m.nmeshvert = int(m.mesh_vertnum.sum())
+    # per-vertex normals (MuJoCo's mesh_normal without tangent frames: normalnum = vertnum): the
+    # area-weighted mean of the adjacent triangles' normals, in the mesh frame (mesh_quat identity: this
+    # compiler keeps mesh vertices in their file frame)
+    normals = [_vertex_normals(v, f) for v, f in self.mesh_data]
+    m.mesh_normal = np.concatenate(normals).reshape(-1, 3) if m.nmesh else np.zeros((0, 3))
+    m.mesh_normaladr = m.mesh_vertadr.copy()
+    m.mesh_normalnum = m.mesh_vertnum.copy()
+    m.nmeshnormal = int(m.mesh_normalnum.sum())
     # polygon data of each mesh's convex hull (MuJoCo's mesh_poly* fields; multi-contact, collision_gjk.py:1403-1790)
     polys = [_mesh_polygons(v) for v, _ in self.mesh_data]
     m.mesh_polynum = np.array([len(p[0]) for p in polys], dtype=np.int32)
@@ -1929,6 +1937,9 @@ class _Compiler:
     "contact": (SensorType.CONTACT, 0, DataType.REAL, Stage.ACC, "contact", None),
     # camprojection: pixel coordinates of `site` in `camera`'s image (sensor.py:128-190)
     "camprojection": (SensorType.CAMPROJECTION, 2, DataType.REAL, Stage.POS, "camprojection", ObjType.SITE),
+    # tactile: per vertex of `mesh` placed on `geom`, the penetration pressure and tangential slip of the
+    # geoms in contact with that geom's weld body (sensor.py:2085-2250); dim = 3 x vertices
+    "tactile": (SensorType.TACTILE, 0, DataType.REAL, Stage.ACC, "tactile", ObjType.MESH),
   }
   _OBJTYPES = {"body": ObjType.BODY, "xbody": ObjType.XBODY, "geom": ObjType.GEOM, "site": ObjType.SITE, "camera": ObjType.CAMERA}
 
@@ -1985,6 +1996,10 @@ class _Compiler:
         elif key == "camprojection":
           objid = names[ObjType.SITE][a["site"]]
           reftype, refid = ObjType.CAMERA, names[ObjType.CAMERA][a["camera"]]
+        elif key == "tactile":
+          objid = self.mesh_id[a["mesh"]]
+          reftype, refid = ObjType.GEOM, names[ObjType.GEOM][a["geom"]]
+          dim = 3 * int(m.mesh_vertnum[objid])
         elif key == "insidesite":
           otype = self._OBJTYPES[a["objtype"]]
           objid = names[otype][a["objname"]]
@@ -2237,6 +2252,18 @@ def _svk_metric(X, young, poisson, dim, thickness, radius):
       else:
         M[a, b] = vol * (mu * np.trace(S[a] @ S[b]) + 0.5 * lam * np.trace(S[a]) * np.trace(S[b]))
   return M
+
+
+def _vertex_normals(v, f):
+  """Unit vertex normals: the sum of the adjacent triangles' (area-weighted) normals."""
+  n = np.zeros((len(v), 3))
+  f = np.asarray(f, dtype=np.int64).reshape(-1, 3)
+  if len(f):
+    fn = np.cross(v[f[:, 1]] - v[f[:, 0]], v[f[:, 2]] - v[f[:, 0]])
+    for k in range(3):
+      np.add.at(n, f[:, k], fn)
+  ln = np.linalg.norm(n, axis=1, keepdims=True)
+  return np.where(ln > 0, n / np.maximum(ln, 1e-30), np.array([0.0, 0.0, 1.0]))
 
 
 def _bending_coef(x, mu, thickness):

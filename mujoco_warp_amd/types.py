@@ -197,6 +197,7 @@ class ObjType(enum.IntEnum):
   CAMERA = 7
   LIGHT = 8
   FLEX = 9
+  MESH = 10
   TENDON = 18
   ACTUATOR = 19
 
@@ -251,6 +252,7 @@ class SensorType(enum.IntEnum):
   E_POTENTIAL = 43
   E_KINETIC = 44
   CLOCK = 45  # after INSIDESITE, GEOMDIST, GEOMNORMAL, GEOMFROMTO, CONTACT, E_POTENTIAL, E_KINETIC
+  TACTILE = 46  # this build's value (MuJoCo's enum position unpinned: mujoco is not importable here)
 
 
 class DataType(enum.IntEnum):
@@ -282,7 +284,7 @@ SUPPORTED_SENSORS = {
   SensorType.JOINTLIMITVEL, SensorType.JOINTLIMITFRC, SensorType.TENDONLIMITPOS, SensorType.TENDONLIMITVEL,
   SensorType.TENDONLIMITFRC, SensorType.SUBTREELINVEL, SensorType.SUBTREEANGMOM, SensorType.E_POTENTIAL, SensorType.E_KINETIC,
   SensorType.GEOMDIST, SensorType.GEOMNORMAL, SensorType.GEOMFROMTO, SensorType.INSIDESITE, SensorType.CAMPROJECTION,
-  SensorType.CONTACT,
+  SensorType.CONTACT, SensorType.TACTILE,
 }
 # sensors that need rne_postconstraint (io.py:542-551)
 RNE_POSTCONSTRAINT_SENSORS = {

@@ -31,7 +31,7 @@ typedef ORC_REAL real;
   X(opt_ccd_iterations) X(ccd_epa_iterations)                                                      \
   X(is_sparse) X(nflex) X(nflexvert) X(nflexedge) X(nflexelem) X(nflexelemdata) X(nmesh) X(nmeshvert)   \
   X(ntendon) X(nwrap) X(nJten) X(npair) X(ngravcomp) X(has_fluid) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)          \
-  X(nmeshpoly) X(nmeshpolyvert) X(nmeshpolymap) X(nflexelemedge) X(nflexshelldata)
+  X(nmeshpoly) X(nmeshpolyvert) X(nmeshpolymap) X(nflexelemedge) X(nflexshelldata) X(nmeshnormal)
 
 /* ---- model: real scalars ---- */
 #define ORC_MODEL_REAL_SCALARS(X)                                                                  \
@@ -63,7 +63,7 @@ typedef ORC_REAL real;
   X(eq_solref, neq * 2) X(eq_solimp, neq * 5) X(eq_data, neq * 11)                               \
   X(flex_radius, nflex) X(flex_margin, nflex) X(flex_damping, nflex) X(flex_friction, nflex * 3)  \
   X(flex_vert, nflexvert * 3) X(flexedge_length0, nflexedge) X(flexedge_invweight0, nflexedge)    \
-  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17) X(mesh_vert, nmeshvert * 3)      \
+  X(flex_stiffness, nflexelem * 21) X(flex_bending, nflexedge * 17) X(mesh_vert, nmeshvert * 3) X(mesh_normal, nmeshnormal * 3)      \
   X(mesh_polynormal, nmeshpoly * 3)                                                                \
   X(hfield_size, nhfield * 4) X(hfield_data, nhfielddata)                                          \
   X(tendon_stiffness, ntendon) X(tendon_damping, ntendon) X(tendon_frictionloss, ntendon)          \
@@ -101,7 +101,7 @@ typedef ORC_REAL real;
   X(flex_elemedgeadr, nflex) X(flex_contype, nflex) X(flex_conaffinity, nflex) X(flex_condim, nflex) \
   X(flex_centered, nflex) X(flex_vertbodyid, nflexvert) X(flex_vertflexid, nflexvert)              \
   X(flex_edge, nflexedge * 2) X(flex_edgeflap, nflexedge * 2) X(flex_elem, nflexelemdata)          \
-  X(flex_elemedge, nflexelemedge) X(flex_shellnum, nflex) X(flex_shelldataadr, nflex) X(flex_shell, nflexshelldata) X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom) \
+  X(flex_elemedge, nflexelemedge) X(flex_shellnum, nflex) X(flex_shelldataadr, nflex) X(flex_shell, nflexshelldata) X(mesh_normaladr, nmesh) X(mesh_vertadr, nmesh) X(mesh_vertnum, nmesh) X(geom_dataid, ngeom) \
   X(mesh_polyadr, nmesh) X(mesh_polynum, nmesh) X(mesh_polyvertadr, nmeshpoly) X(mesh_polyvertnum, nmeshpoly) \
   X(mesh_polyvert, nmeshpolyvert) X(mesh_polymapadr, nmeshvert) X(mesh_polymapnum, nmeshvert) X(mesh_polymap, nmeshpolymap) \
   X(hfield_nrow, nhfield) X(hfield_ncol, nhfield) X(hfield_adr, nhfield)                          \

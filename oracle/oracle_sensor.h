@@ -11,7 +11,7 @@ enum {
   SENS_TOUCH = 0, SENS_TENDONPOS = 11, SENS_TENDONVEL = 12, SENS_TENDONACTFRC = 17, SENS_JOINTLIMITPOS = 20,
   SENS_JOINTLIMITVEL = 21, SENS_JOINTLIMITFRC = 22, SENS_TENDONLIMITPOS = 23, SENS_TENDONLIMITVEL = 24,
   SENS_TENDONLIMITFRC = 25, SENS_SUBTREELINVEL = 36, SENS_SUBTREEANGMOM = 37, SENS_E_POTENTIAL = 43, SENS_E_KINETIC = 44,
-  SENS_INSIDESITE = 38, SENS_GEOMDIST = 39, SENS_GEOMNORMAL = 40, SENS_GEOMFROMTO = 41, SENS_CONTACT = 42
+  SENS_INSIDESITE = 38, SENS_GEOMDIST = 39, SENS_GEOMNORMAL = 40, SENS_GEOMFROMTO = 41, SENS_CONTACT = 42, SENS_TACTILE = 46
 };
 
 /* ---- collision sensors: the smallest-distance contact over the sensor's geom pairs ---- */
@@ -450,6 +450,97 @@ static real contact_match(const orc_model* m, const orc_data* d, int s, int c) {
 /* one contact sensor: matches in the world's contact order (MuJoCo's mj_sensorAcc order), at most
  * contact_sensor_maxmatch of them; mindist / maxforce sort the matches stably by their criteria (insertion
  * sort of the match list); netforce sums about the force-weighted centroid */
+/* collision_sdf.py:148-183: signed distances of the primitive SDFs in the geom frame (plane, sphere,
+ * box with the radial field inside, ellipsoid); other types have none there (0: no pressure) */
+static real tactile_sdf(int type, const real* p, const real* size) {
+  if (type == GEOM_PLANE) return p[2];
+  if (type == GEOM_SPHERE) return sqrt(dot3(p, p)) - size[0];
+  if (type == GEOM_BOX) {
+    real a[3];
+    for (int i = 0; i < 3; i++) a[i] = fabs(p[i]) - size[i];
+    if (a[0] >= 0 || a[1] >= 0 || a[2] >= 0) {
+      real b[3], mx = a[0];
+      for (int i = 0; i < 3; i++) b[i] = a[i] > 0 ? a[i] : 0;
+      if (a[1] > mx) mx = a[1];
+      if (a[2] > mx) mx = a[2];
+      return sqrt(dot3(b, b)) + (mx < 0 ? mx : 0);
+    }
+    real f[3];
+    for (int i = 0; i < 3; i++) f[i] = -size[i] / a[i];
+    const real fn = sqrt(dot3(f, f));
+    /* radial field b = +-normalize(-size / a) (collision_sdf.py:148-154): |b| = 1, t = -a / |b| */
+    real tmin = 1e30;
+    for (int i = 0; i < 3; i++) {
+      const real t = -a[i] / fabs(f[i] / fn);
+      if (t < tmin) tmin = t;
+    }
+    return -tmin;
+  }
+  if (type == GEOM_ELLIPSOID) {
+    real sp[3], s2[3];
+    for (int i = 0; i < 3; i++) { sp[i] = p[i] / size[i]; s2[i] = p[i] / (size[i] * size[i]); }
+    const real k0 = sqrt(dot3(sp, sp)), k1 = sqrt(dot3(s2, s2));
+    return k0 * (k0 - 1) / (k1 != 0 ? k1 : (real)1e-12);
+  }
+  return 0;
+}
+
+/* sensor.py:2085-2250 tactile: for each vertex (taxel) of the sensor's mesh, placed with the sensor
+ * geom's frame, the geoms in contact with that geom's weld body (first MJ_MAXCONPAIR = 50 entries of
+ * the per-weld list, duplicates once) add pressure depth / max(0.05 - depth, MINVAL) for a negative
+ * SDF depth (slip components 0: no tangent frames).  The world's contacts are those with constraint
+ * rows, as the device enumerates them (the reference also counts contacts without rows, e.g. in the
+ * margin-gap zone).  Other geoms than plane / sphere / box / ellipsoid (mesh ray SDF, SDF plugins) give
+ * no pressure here. */
+static void tactile_sensor(const orc_model* m, orc_data* d, int s) {
+  const int mesh = m->sensor_objid[s], geom = m->sensor_refid[s];
+  const int nvt = m->mesh_vertnum[mesh];
+  real* out = d->sensordata + m->sensor_adr[s];
+  for (int i = 0; i < 3 * nvt; i++) out[i] = 0;
+  const int pw = m->body_weldid[m->geom_bodyid[geom]];
+  int list[50], n = 0, nadd = 0;
+  for (int c = 0; c < d->ncon[0]; c++) {
+    if (d->con_efc_address[10 * c] < 0) continue;
+    const int g1 = d->con_geom[2 * c], g2 = d->con_geom[2 * c + 1];
+    if (g1 < 0 || g2 < 0) continue;
+    const int w1 = m->body_weldid[m->geom_bodyid[g1]], w2 = m->body_weldid[m->geom_bodyid[g2]];
+    for (int side = 0; side < 2; side++) {
+      if ((side == 0 ? w1 : w2) != pw) continue;
+      const int g = side == 0 ? g2 : g1;
+      if (nadd++ >= 50) continue;
+      int dup = 0;
+      for (int j = 0; j < n; j++) dup |= list[j] == g;
+      if (!dup) list[n++] = g;
+    }
+  }
+  if (!n) return;
+  const real* gx = d->geom_xpos + 3 * geom;
+  const real* gm = d->geom_xmat + 9 * geom;
+  for (int v = 0; v < nvt; v++) {
+    const real* lp = m->mesh_vert + 3 * (m->mesh_vertadr[mesh] + v);
+    real x[3];
+    for (int i = 0; i < 3; i++) x[i] = gm[3 * i] * lp[0] + gm[3 * i + 1] * lp[1] + gm[3 * i + 2] * lp[2] + gx[i];
+    const real* nrm = m->mesh_normal + 3 * (m->mesh_normaladr[mesh] + v);
+    for (int k = 0; k < n; k++) {
+      const int g = list[k];
+      const real* px = d->geom_xpos + 3 * g;
+      const real* pm = d->geom_xmat + 9 * g;
+      real dx[3], q[3];
+      for (int i = 0; i < 3; i++) dx[i] = x[i] - px[i];
+      for (int i = 0; i < 3; i++) q[i] = pm[i] * dx[0] + pm[3 + i] * dx[1] + pm[6 + i] * dx[2];
+      real depth = tactile_sdf(m->geom_type[g], q, m->geom_size + 3 * g);
+      if (depth > 0) depth = 0;
+      if (depth >= 0) continue;
+      const real pressure = depth / (0.05 - depth > MINVAL ? 0.05 - depth : MINVAL);
+      real f[3];
+      for (int i = 0; i < 3; i++) f[i] = nrm[i] * pressure;
+      out[v] += dot3(f, nrm);
+      /* slip |v_rel . t1|, |v_rel . t2| (sensor.py:2233-2247) enters only with per-vertex tangent
+       * frames (mesh_normalnum = 3 vertnum), which this compiler's meshes do not have: 0 */
+    }
+  }
+}
+
 static void contact_sensor(const orc_model* m, orc_data* d, int s) {
   const int spec = m->sensor_intprm[3 * s], reduce = m->sensor_intprm[3 * s + 1];
   static const int fsz[7] = {1, 3, 3, 1, 3, 3, 3};
@@ -571,6 +662,7 @@ static void sensor_extra(const orc_model* m, orc_data* d, int stage) {
       case SENS_E_KINETIC: v[0] = energy_kinetic(m, d); break;
       case SENS_GEOMDIST: case SENS_GEOMNORMAL: case SENS_GEOMFROMTO: collision_sensor(m, d, s); continue;
       case SENS_CONTACT: contact_sensor(m, d, s); continue;
+      case SENS_TACTILE: tactile_sensor(m, d, s); continue;
       case SENS_INSIDESITE: {
         const real *p, *R;
         int body;

@@ -154,6 +154,7 @@ class OracleModel:
       nflex=getattr(mjm, "nflex", 0), nflexvert=getattr(mjm, "nflexvert", 0), nflexedge=getattr(mjm, "nflexedge", 0),
       nflexelem=getattr(mjm, "nflexelem", 0), nflexelemdata=getattr(mjm, "nflexelemdata", 0),
       nflexelemedge=getattr(mjm, "nflexelemedge", 3 * getattr(mjm, "nflexelem", 0)), nflexshelldata=getattr(mjm, "nflexshelldata", 0),
+      nmeshnormal=getattr(mjm, "nmeshnormal", 0),
       nmesh=getattr(mjm, "nmesh", 0), nmeshvert=getattr(mjm, "nmeshvert", 0),
       nmeshpoly=getattr(mjm, "nmeshpoly", 0), nmeshpolyvert=getattr(mjm, "nmeshpolyvert", 0), nmeshpolymap=getattr(mjm, "nmeshpolymap", 0),
       ntendon=getattr(mjm, "ntendon", 0), nwrap=getattr(mjm, "nwrap", 0), nJten=getattr(mjm, "nJten", 0),
