@@ -42,6 +42,10 @@ for i in range(nsteps):
   r = {"step": i, "ms": round(e0.elapsed_time(e1), 4), "niter_mean": round(float(it.mean()), 2), "niter_p50": int(np.percentile(it, 50)),
        "niter_p99": int(np.percentile(it, 99)), "niter_max": int(it.max()), "niter_sum": int(it.sum()),
        "nefc_mean": round(float(nefc.mean()), 2), "nefc_max": int(nefc.max()), "nworld_gt32rows": int((nefc > 32).sum())}
+  if getattr(d.efc, "J_rownnz", None) is not None and d.efc.J_rownnz.numel() >= nefc.size and m.nv > 64:
+    nnz = d.efc.J_rownnz.reshape(nefc.size, -1).cpu().numpy().astype(np.int64)
+    mask = np.arange(nnz.shape[1])[None, :] < nefc[:, None]
+    r["Jnnz_per_world_mean"] = round(float((nnz * mask).sum(1).mean()), 1)
   # how well the previous step's iterations and this step's rows predict this step's iterations (the
   # dense kernel's longest-first order uses the former)
   if prev_it is not None and it.std() > 0 and prev_it.std() > 0:
