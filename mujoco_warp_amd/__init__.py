@@ -38,6 +38,11 @@ from .mjcf import load_model_from_string
 from .mjcf import reset_data_keyframe
 from .stages import camlight
 from .stages import collision
+from .stages import CollisionContext
+from .stages import create_collision_context
+from .stages import nxn_broadphase
+from .stages import primitive_narrowphase
+from .stages import sap_broadphase
 from .stages import com_pos
 from .stages import com_vel
 from .stages import crb

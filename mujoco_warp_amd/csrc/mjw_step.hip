@@ -575,17 +575,18 @@ __device__ __forceinline__ float cholesky_solve(const float* Lm, int n, int nvs,
 }
 // collision primitives, AABB/OBB filters and contact_params: mjw_narrow.h
 
-// collision_driver.py:274-321
-__device__ __forceinline__ bool broadphase_filter(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2) {
+// collision_driver.py:274-321; gxpos / gxmat: the world's geom frames (LDS in the fused kernels, HBM in the
+// stand-alone broadphase entry point)
+__device__ __forceinline__ bool broadphase_filter_g(const mjw_model_t& m, const float* gxpos, const float* gxmat, int wid, int g1, int g2) {
   const float* geom_aabb = MR(geom_aabb);
   const float* geom_rbound = MR(geom_rbound);
   const float* geom_margin = MR(geom_margin);
   float rb1 = geom_rbound[g1], rb2 = geom_rbound[g2];
   float mg1 = geom_margin[g1], mg2 = geom_margin[g2];
-  const float* xp1 = s + L.gxpos + 3 * g1;
-  const float* xp2 = s + L.gxpos + 3 * g2;
-  const float* xm1 = s + L.gxmat + 9 * g1;
-  const float* xm2 = s + L.gxmat + 9 * g2;
+  const float* xp1 = gxpos + 3 * g1;
+  const float* xp2 = gxpos + 3 * g2;
+  const float* xm1 = gxmat + 9 * g1;
+  const float* xm2 = gxmat + 9 * g2;
   int filt = m.opt_broadphase_filter;
   if (rb1 == 0.0f || rb2 == 0.0f) {
     if (filt & FILTER_PLANE) {
@@ -612,19 +613,23 @@ __device__ __forceinline__ bool broadphase_filter(const mjw_model_t& m, const La
       return false;
   return true;
 }
+__device__ __forceinline__ bool broadphase_filter(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2) {
+  return broadphase_filter_g(m, s + L.gxpos, s + L.gxmat, wid, g1, g2);
+}
 
 // narrowphase of one pair (collision_primitive.py:280-662); pair is type-sorted on the host
 // BOX = false compiles out the pairs with a box (sphere-box, capsule-box; plane-box and box-box are
 // handled by the caller): models without boxes then run a kernel with 118 instead of 128+ VGPRs and
 // no scratch spills
 template <bool BOX>
-__device__ __forceinline__ void narrowphase(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2, float margin, Con2& c) {
+__device__ __forceinline__ void narrowphase_g(const mjw_model_t& m, const float* gxpos, const float* gxmat, int wid, int g1, int g2, float margin,
+                                              Con2& c) {
   const float* geom_size = MR(geom_size);
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
-  const float* p1 = s + L.gxpos + 3 * g1;
-  const float* p2 = s + L.gxpos + 3 * g2;
-  const float* r1 = s + L.gxmat + 9 * g1;
-  const float* r2 = s + L.gxmat + 9 * g2;
+  const float* p1 = gxpos + 3 * g1;
+  const float* p2 = gxpos + 3 * g2;
+  const float* r1 = gxmat + 9 * g1;
+  const float* r2 = gxmat + 9 * g2;
   const float* s1 = geom_size + 3 * g1;
   const float* s2 = geom_size + 3 * g2;
   float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
@@ -657,6 +662,10 @@ __device__ __forceinline__ void narrowphase(const mjw_model_t& m, const Lay& L, 
   } else if (BOX && t1 == GEOM_CAPSULE && t2 == GEOM_BOX) {  // collision_primitive.py:1117-1199
     capsule_box(c, p1, n1, s1[0], s1[1], p2, r2, s2);
   }
+}
+template <bool BOX>
+__device__ __forceinline__ void narrowphase(const mjw_model_t& m, const Lay& L, const float* s, int wid, int g1, int g2, float margin, Con2& c) {
+  narrowphase_g<BOX>(m, s + L.gxpos, s + L.gxmat, wid, g1, g2, margin, c);
 }
 
 
@@ -2720,6 +2729,118 @@ __global__ void __launch_bounds__(64) ccd_hf_kernel(const mjw_model_t m, const m
   ccd_body<true>(m, d, L, w0);
 }
 
+// -------------------------------------------------------------------------------------------
+// The collision sub-stages as entry points of their own (mujoco_warp/__init__.py:33-35).  The step runs
+// broad- and narrowphase fused in the forward kernel, one wave per world, without materialising the
+// candidate list; these two kernels expose the same computations over the reference's intermediate
+// arrays (collision_core.py:345-365 CollisionContext), reading the geom frames from HBM (d.geom_xpos /
+// d.geom_xmat, as left by the position stage).
+// -------------------------------------------------------------------------------------------
+// collision_driver.py:697-731 nxn_broadphase, :325-358 _add_geom_pair: one thread per (world, filtered
+// pair); survivors of opt.broadphase_filter (and pairs with a collision sensor) take an atomically
+// reserved slot, slots past naconmax only counted.  nxn_geom_pair is type-ordered on the host already.
+__global__ void __launch_bounds__(256) nxn_broadphase_kernel(const mjw_model_t m, const mjw_data_t d, int* cpair, int* cpairid, int* cworld) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)d.nworld * m.nxn) return;
+  const int wid = (int)(t / m.nxn), p = (int)(t - (long)wid * m.nxn);
+  const int g1 = m.nxn_geom_pair[2 * p], g2 = m.nxn_geom_pair[2 * p + 1];
+  const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
+  const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;
+  if (!(m.nxn_pairid[2 * p + 1] >= 0 || broadphase_filter_g(m, gx, gm, wid, g1, g2))) return;
+  const int k = atomicAdd(d.ncollision, 1);
+  if (k >= d.naconmax) return;
+  cpair[2 * k] = g1;
+  cpair[2 * k + 1] = g2;
+  cpairid[2 * k] = m.nxn_pairid[2 * p];
+  cpairid[2 * k + 1] = m.nxn_pairid[2 * p + 1];
+  cworld[k] = wid;
+}
+
+// collision_primitive.py:1461-1549 primitive_narrowphase (+ collision_core.py:160-232 write_contact): one
+// thread per candidate [0, min(ncollision, naconmax)) whose type pair is set in `typemask` (bit 8 t1 + t2 of
+// the type-ordered pair; the PRIMITIVE entries of collision_driver.py:43-77 by default).  Every point is
+// written at an atomically reserved pool slot unless it is inactive (dist >= margin) or its pair is
+// excluded (pairid -2) and no collision sensor asked for it; its type carries CONSTRAINT (active, not
+// excluded) and SENSOR bits, geomcollisionid the point's index within the pair, efc_address -1 (the rows
+// come from make_constraint).  Same geometry routines as the fused path: plane-sphere / capsule,
+// sphere-sphere / capsule / box, capsule-capsule / box (narrowphase), plane-box corners, plane-ellipsoid /
+// cylinder / mesh and sphere-cylinder (the pre-pass routines).
+__global__ void __launch_bounds__(256) primitive_narrowphase_kernel(const mjw_model_t m, const mjw_data_t d, const int* cpair, const int* cpairid,
+                                                                    const int* cworld, unsigned long long typemask) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= min(d.ncollision[0], d.naconmax)) return;
+  const int g1 = cpair[2 * k], g2 = cpair[2 * k + 1], wid = cworld[k];
+  const int pid0 = cpairid[2 * k], pid1 = cpairid[2 * k + 1];
+  if (g1 < 0 || g2 < 0 || wid < 0 || wid >= d.nworld) return;
+  const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  if (t1 > 7 || t2 > 7 || !((typemask >> (8 * t1 + t2)) & 1ull)) return;
+  const float* gx = d.geom_xpos + (long)wid * m.ngeom * 3;
+  const float* gm = d.geom_xmat + (long)wid * m.ngeom * 9;
+  float margin, gap, friction[5], solref[2], solimp[5], srf[2];
+  int condim;
+  contact_params(m, wid, g1, g2, pid0, &margin, &gap, &condim, friction, solref, solimp, srf);
+  const float* gsize = MR(geom_size);
+  const float *p1 = gx + 3 * g1, *p2 = gx + 3 * g2, *r1 = gm + 9 * g1, *r2 = gm + 9 * g2;
+  const float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
+  int id = 0;
+  auto write = [&](float dist, const float* pos, const float* frame) {
+    const bool active = dist < margin;
+    if ((pid0 == -2 || !active) && pid1 == -1) return;
+    const int type = ((pid0 >= -1 && active) ? 1 : 0) | (pid1 >= 0 ? 2 : 0);
+    const int cid = atomicAdd(d.nacon, 1);
+    const int gid = id++;
+    if (cid >= d.naconmax) return;
+    d.contact_dist[cid] = dist;
+    for (int i = 0; i < 3; i++) d.contact_pos[3L * cid + i] = pos[i];
+    for (int i = 0; i < 9; i++) d.contact_frame[9L * cid + i] = frame[i];
+    d.contact_includemargin[cid] = margin - gap;
+    for (int i = 0; i < 5; i++) d.contact_friction[5L * cid + i] = friction[i];
+    for (int i = 0; i < 2; i++) {
+      d.contact_solref[2L * cid + i] = solref[i];
+      d.contact_solreffriction[2L * cid + i] = srf[i];
+    }
+    for (int i = 0; i < 5; i++) d.contact_solimp[5L * cid + i] = solimp[i];
+    d.contact_dim[cid] = condim;
+    d.contact_geom[2L * cid] = g1;
+    d.contact_geom[2L * cid + 1] = g2;
+    d.contact_worldid[cid] = wid;
+    d.contact_type[cid] = type;
+    d.contact_geomcollisionid[cid] = gid;
+    for (int i = 0; i < m.nmaxpyramid; i++) d.contact_efc_address[(long)cid * m.nmaxpyramid + i] = -1;
+  };
+  float frame[9];
+  if (t1 == GEOM_PLANE && t2 == GEOM_BOX) {
+    make_frame(frame, n1);
+    for (int q = 0; q < 8; q++) {
+      float cp[3];
+      const float dist = plane_box_corner(q, n1, p1, p2, r2, gsize + 3 * g2, cp);
+      write(dist, cp, frame);
+    }
+  } else if (prepass_prim(t1, t2)) {
+    float dist[4], pos[4][3], nrm[3] = {n1[0], n1[1], n1[2]};
+    int n = 0;
+    if (t1 == GEOM_PLANE && t2 == GEOM_ELLIPSOID) {
+      dist[0] = plane_ellipsoid(pos[0], n1, p1, p2, r2, gsize + 3 * g2);
+      n = 1;
+    } else if (t1 == GEOM_PLANE && t2 == GEOM_CYLINDER) {
+      for (int q = 0; q < 4; q++) plane_cylinder_k(q, n1, p1, p2, n2, gsize[3 * g2], gsize[3 * g2 + 1], &dist[q], pos[q]);
+      n = 4;
+    } else if (t1 == GEOM_SPHERE && t2 == GEOM_CYLINDER) {
+      dist[0] = sphere_cylinder(pos[0], nrm, p1, gsize[3 * g1], p2, n2, gsize[3 * g2], gsize[3 * g2 + 1]);
+      n = 1;
+    } else {  // plane-mesh
+      const int md = m.geom_dataid[g2];
+      n = plane_mesh(n1, p1, p2, r2, MR(mesh_vert) + 3 * (long)m.mesh_vertadr[md], m.mesh_vertnum[md], dist, pos);
+    }
+    make_frame(frame, nrm);
+    for (int q = 0; q < n; q++) write(dist[q], pos[q], frame);
+  } else {
+    Con2 c;
+    narrowphase_g<true>(m, gx, gm, wid, g1, g2, margin, c);
+    for (int q = 0; q < c.n; q++) write(c.dist[q], c.pos[q], c.frame[q]);
+  }
+}
+
 // benchmark.py:41-83
 // clears the contact pool counters at the start of the position stage.  A kernel, not
 // hipMemsetAsync: in a captured hipGraph the 4-byte memset node was observed to race the
@@ -3242,6 +3363,25 @@ int mjw_actuator_map(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   // layout-independent: the moment rows (rowadr / rownnz / colind) are the same on the sparse path
   hipLaunchKernelGGL(mjw::actuator_map_kernel, dim3(d->nworld), dim3(64), 0, (hipStream_t)stream, *m, *d);
   return set_err(hipGetLastError(), "mjw_actuator_map");
+}
+
+int mjw_nxn_broadphase(const mjw_model_t* m, const mjw_data_t* d, int* collision_pair, int* collision_pairid, int* collision_worldid,
+                       void* stream) {
+  const long n = (long)d->nworld * m->nxn;
+  if (n <= 0) return 0;
+  if (!collision_pair || !collision_pairid || !collision_worldid) return set_err(hipErrorInvalidValue, "mjw_nxn_broadphase: null context array");
+  hipLaunchKernelGGL(mjw::nxn_broadphase_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *m, *d, collision_pair,
+                     collision_pairid, collision_worldid);
+  return set_err(hipGetLastError(), "mjw_nxn_broadphase");
+}
+
+int mjw_primitive_narrowphase(const mjw_model_t* m, const mjw_data_t* d, const int* collision_pair, const int* collision_pairid,
+                              const int* collision_worldid, unsigned long long typemask, void* stream) {
+  if (d->naconmax <= 0) return 0;
+  if (!collision_pair || !collision_pairid || !collision_worldid) return set_err(hipErrorInvalidValue, "mjw_primitive_narrowphase: null context array");
+  hipLaunchKernelGGL(mjw::primitive_narrowphase_kernel, dim3((d->naconmax + 255) / 256), dim3(256), 0, (hipStream_t)stream, *m, *d, collision_pair,
+                     collision_pairid, collision_worldid, typemask);
+  return set_err(hipGetLastError(), "mjw_primitive_narrowphase");
 }
 
 int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* center, int step, float std, float rate, void* stream) {

@@ -72,6 +72,88 @@ def collision(m: Model, d: Data):
   fwd_position(m, d)
 
 
+# -- collision sub-stages (mujoco_warp/__init__.py:33-35) ---------------------------------------------------
+class CollisionContext(types._Container):
+  """Broadphase output arrays (collision_core.py:345-357), each naconmax long: collision_pair (n, 2) int32
+  type-ordered geom ids, collision_pairid (n, 2) int32 (explicit <pair> id or -1 / -2 excluded, collision-
+  sensor id or -1), collision_worldid (n,) int32."""
+
+
+def create_collision_context(naconmax: int, device=None) -> CollisionContext:
+  """collision_core.py:359-365 (device: the Data's device when given as a Data, else cuda)."""
+  if isinstance(device, Data):
+    device = device.qpos.device
+  dev = torch.device(device) if device is not None else torch.device("cuda")
+  n = int(naconmax)
+  return CollisionContext(
+    collision_pair=torch.full((n, 2), -1, dtype=torch.int32, device=dev),
+    collision_pairid=torch.full((n, 2), -1, dtype=torch.int32, device=dev),
+    collision_worldid=torch.full((n,), -1, dtype=torch.int32, device=dev),
+  )
+
+
+def _ctx_ptrs(d: Data, ctx: CollisionContext):
+  for name in ("collision_pair", "collision_pairid", "collision_worldid"):
+    t = getattr(ctx, name)
+    if t.dtype != torch.int32 or not t.is_contiguous() or t.shape[0] < d.naconmax:
+      raise ValueError(f"CollisionContext.{name}: int32, contiguous, at least naconmax = {d.naconmax} rows")
+  return ctx.collision_pair.data_ptr(), ctx.collision_pairid.data_ptr(), ctx.collision_worldid.data_ptr()
+
+
+def nxn_broadphase(m: Model, d: Data, ctx: CollisionContext):
+  """collision_driver.py:697-731: the filtered NXN pairs that pass opt.broadphase_filter (plane / sphere /
+  AABB / OBB, :274-321) at the current d.geom_xpos / d.geom_xmat, appended to `ctx` with d.ncollision
+  counting them (the caller zeroes it, as `collision` does); pairs with a collision sensor always pass.
+  One thread per (world, pair) (mjw_nxn_broadphase); the order of the candidates is the atomics' order."""
+  from . import _lib
+  from .io import cdata, cmodel
+  from .forward import _stream
+
+  L = _lib.lib()
+  pp, pi, pw = _ctx_ptrs(d, ctx)
+  _lib.check(L.mjw_nxn_broadphase(cmodel(m), cdata(d), pp, pi, pw, _stream(d)), "mjw_nxn_broadphase")
+
+
+def sap_broadphase(m: Model, d: Data, ctx: CollisionContext):
+  """collision_driver.py:602-640: sweep-and-prune is the reference's device for large geom counts; it
+  yields the same candidate set as nxn_broadphase (the same filtered pairs through the same filters, order
+  aside), which is what this build computes for it."""
+  nxn_broadphase(m, d, ctx)
+
+
+# the PRIMITIVE entries of collision_driver.py:43-77 (type-ordered pairs)
+PRIMITIVE_PAIRS = (
+  (types.GeomType.PLANE, types.GeomType.SPHERE), (types.GeomType.PLANE, types.GeomType.CAPSULE),
+  (types.GeomType.PLANE, types.GeomType.ELLIPSOID), (types.GeomType.PLANE, types.GeomType.CYLINDER),
+  (types.GeomType.PLANE, types.GeomType.BOX), (types.GeomType.PLANE, types.GeomType.MESH),
+  (types.GeomType.SPHERE, types.GeomType.SPHERE), (types.GeomType.SPHERE, types.GeomType.CAPSULE),
+  (types.GeomType.SPHERE, types.GeomType.CYLINDER), (types.GeomType.SPHERE, types.GeomType.BOX),
+  (types.GeomType.CAPSULE, types.GeomType.CAPSULE), (types.GeomType.CAPSULE, types.GeomType.BOX),
+)
+
+
+def primitive_narrowphase(m: Model, d: Data, ctx: CollisionContext, collision_table=None):
+  """collision_primitive.py:1461-1549: contacts of the broadphase candidates whose (type-ordered) geom types
+  are in `collision_table` (default: every PRIMITIVE pair), appended to d.contact at d.nacon with
+  write_contact's rules (collision_core.py:160-232: inactive points are kept only for collision sensors;
+  type = CONSTRAINT | SENSOR bits; efc_address -1 until make_constraint).  One thread per candidate
+  (mjw_primitive_narrowphase), the fused path's geometry routines."""
+  from . import _lib
+  from .io import cdata, cmodel
+  from .forward import _stream
+
+  table = PRIMITIVE_PAIRS if collision_table is None else collision_table
+  mask = 0
+  for t1, t2 in table:
+    a, b = sorted((int(t1), int(t2)))
+    if (a, b) not in {(int(x), int(y)) for x, y in PRIMITIVE_PAIRS}:
+      raise NotImplementedError(f"primitive_narrowphase: ({types.GeomType(a).name}, {types.GeomType(b).name}) is not a primitive pair")
+    mask |= 1 << (8 * a + b)
+  L = _lib.lib()
+  pp, pi, pw = _ctx_ptrs(d, ctx)
+  _lib.check(L.mjw_primitive_narrowphase(cmodel(m), cdata(d), pp, pi, pw, mask, _stream(d)), "mjw_primitive_narrowphase")
+
+
 def make_constraint(m: Model, d: Data):
   """Constraint rows d.efc (constraint.py:2718-2779): the position-stage launch, whose rows come from the
   contacts it collides; after a caller edited d.contact, `mjw_contact_rows` rebuilds them from the pool."""

@@ -1,0 +1,178 @@
+"""The collision sub-stages as entry points (mujoco_warp/__init__.py:33-35): nxn_broadphase /
+sap_broadphase (collision_driver.py:602-731) and primitive_narrowphase (collision_primitive.py:1461-1549)
+over the reference's CollisionContext arrays (collision_core.py:345-365).
+
+The step runs broad- and narrowphase fused (one wave per world, no candidate list); these entry points run
+the same filters and geometry routines as separate launches.  Pinned by:
+* broadphase_test.py's own answers (tests/golden/collision_kat.json "broadphase": pair counts over the
+  filter combinations, margins, filterparent, contype) and its pair checks (broadphase_test.py:139-184: the
+  three candidate pairs of keyframe 2, the two-world world ids, the type-ordered (3, 2) pair of keyframe 3);
+* the fused collision of the forward kernel: on a scene of every primitive type pair, broadphase +
+  primitive_narrowphase give the contact set the position stage wrote (same points, dist, frame and
+  mixed parameters), world by world.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import golden_kat as gk
+
+KAT = gk.load()
+
+
+def test_api_and_primitive_table():
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import stages, types
+
+  for name in ("nxn_broadphase", "sap_broadphase", "primitive_narrowphase", "create_collision_context", "CollisionContext"):
+    assert hasattr(mjw, name), name
+  ctx = mjw.create_collision_context(7, device="cpu")
+  assert ctx.collision_pair.shape == (7, 2) and ctx.collision_pairid.shape == (7, 2) and ctx.collision_worldid.shape == (7,)
+  assert ctx.collision_pair.dtype == torch.int32
+  # collision_driver.py:43-77: 12 PRIMITIVE entries, all type-ordered
+  assert len(stages.PRIMITIVE_PAIRS) == 12 and all(int(a) <= int(b) for a, b in stages.PRIMITIVE_PAIRS)
+  assert (types.GeomType.BOX, types.GeomType.BOX) not in stages.PRIMITIVE_PAIRS  # CONVEX (GJK / EPA)
+
+
+_BP_CASES = [c for c in KAT["broadphase"]]
+
+
+def _broadphase(case, broadphase):
+  import mujoco_warp_amd as mjw
+
+  mjm, qpos = gk.broadphase_model(case)
+  m = mjw.put_model(mjm, device="cuda")
+  m.opt.broadphase_filter = int(case["filter"])
+  d = mjw.make_data(mjm, nworld=len(qpos), nconmax=16, njmax=64, device="cuda", m=m)
+  d.qpos[:] = torch.as_tensor(qpos, dtype=torch.float32, device="cuda")
+  mjw.kinematics(m, d)  # the position stage: geom frames
+  d.ncollision.zero_()
+  ctx = mjw.create_collision_context(d.naconmax, device=d)
+  broadphase(m, d, ctx)
+  torch.cuda.synchronize()
+  n = int(d.ncollision[0])
+  pairs = ctx.collision_pair.cpu().numpy()[:n]
+  worlds = ctx.collision_worldid.cpu().numpy()[:n]
+  return n, {(int(w), int(a), int(b)) for w, (a, b) in zip(worlds, pairs)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _BP_CASES, ids=[f"{c['source']}-f{c['filter']}-k{c['keys']}" for c in _BP_CASES])
+def test_gpu_broadphase_entry_points_kat(case):
+  import mujoco_warp_amd as mjw
+
+  for bp in (mjw.nxn_broadphase, mjw.sap_broadphase):
+    n, got = _broadphase(case, bp)
+    assert n == case["ncollision"], (case["source"], bp.__name__)
+    assert len(got) == n  # no candidate twice
+    src = case["source"]
+    if case["name"] == "test_broadphase" and n:
+      # broadphase_test.py:139-184 pair checks (keyframe 2: pairs among the first three geoms; the two-world
+      # case: world 0 holds (0, 1); keyframe 3: the sphere-capsule pair type-ordered as (3, 2))
+      if case["keys"] == [2]:
+        assert got <= {(0, 0, 1), (0, 0, 2), (0, 1, 2)}, (src, got)
+      elif case["keys"] == [1, 2]:
+        assert got == {(0, 0, 1), (1, 0, 1), (1, 0, 2), (1, 1, 2)}, (src, got)
+      elif case["keys"] == [3]:
+        assert got == {(0, 3, 2)}, (src, got)
+      elif case["keys"] == [1]:
+        assert got == {(0, 0, 1)}, (src, got)
+
+
+# every primitive type pair of collision_driver.py:43-77 in contact (or within margin) somewhere
+PRIM_XML = """<mujoco><option timestep="0.002"/>
+<asset><mesh name="tet" vertex="0 0 0  .2 0 0  0 .2 0  0 0 .2"/></asset>
+<worldbody>
+  <geom name="floor" type="plane" size="5 5 .1"/>
+  <body pos="0 0 .09"><freejoint/><geom type="sphere" size=".1"/></body>
+  <body pos=".5 0 .04"><freejoint/><geom type="capsule" size=".05 .1" euler="0 90 5"/></body>
+  <body pos="1 0 .09"><freejoint/><geom type="ellipsoid" size=".1 .07 .1" margin=".01"/></body>
+  <body pos="1.5 0 .09"><freejoint/><geom type="cylinder" size=".08 .1" euler="10 0 0"/></body>
+  <body pos="2 0 .09"><freejoint/><geom type="box" size=".1 .1 .1" euler="3 4 0"/></body>
+  <body pos="2.5 0 -.01"><freejoint/><geom type="mesh" mesh="tet"/></body>
+  <body pos="0 1 .3"><freejoint/><geom type="sphere" size=".1"/></body>
+  <body pos="0 1 .49"><freejoint/><geom type="sphere" size=".1" margin=".02"/></body>
+  <body pos=".5 1 .3"><freejoint/><geom type="capsule" size=".05 .1"/></body>
+  <body pos=".5 1 .5"><freejoint/><geom type="sphere" size=".06"/></body>
+  <body pos="1 1 .3"><freejoint/><geom type="cylinder" size=".08 .1"/></body>
+  <body pos="1 1 .47"><freejoint/><geom type="sphere" size=".08"/></body>
+  <body pos="1.5 1 .3"><freejoint/><geom type="box" size=".1 .1 .1"/></body>
+  <body pos="1.5 1 .47"><freejoint/><geom type="sphere" size=".08"/></body>
+  <body pos="2 1 .3"><freejoint/><geom type="capsule" size=".05 .2" euler="0 90 0"/></body>
+  <body pos="2 1 .39"><freejoint/><geom type="capsule" size=".05 .2" euler="90 0 0"/></body>
+  <body pos="2.5 1 .3"><freejoint/><geom type="box" size=".1 .1 .1"/></body>
+  <body pos="2.5 1 .44"><freejoint/><geom type="capsule" size=".05 .2" euler="0 90 20"/></body>
+</worldbody></mujoco>"""
+
+
+def _contact_set(d, nacon, constraint_only):
+  c = d.contact
+  g = c.geom.cpu().numpy()[:nacon]
+  w = c.worldid.cpu().numpy()[:nacon]
+  t = c.type.cpu().numpy()[:nacon]
+  dist = c.dist.cpu().numpy()[:nacon]
+  pos = c.pos.cpu().numpy()[:nacon]
+  frame = c.frame.cpu().numpy().reshape(-1, 9)[:nacon]
+  fr = c.friction.cpu().numpy()[:nacon]
+  sr = c.solref.cpu().numpy()[:nacon]
+  si = c.solimp.cpu().numpy()[:nacon]
+  im = c.includemargin.cpu().numpy()[:nacon]
+  dim = c.dim.cpu().numpy()[:nacon]
+  rows = []
+  for k in range(nacon):
+    if constraint_only and not (int(t[k]) & 1):
+      continue
+    rows.append((int(w[k]), int(g[k, 0]), int(g[k, 1]), np.round(pos[k], 5).tolist(), float(dist[k]), frame[k], fr[k], sr[k], si[k],
+                 float(im[k]), int(dim[k])))
+  rows.sort(key=lambda r: (r[0], r[1], r[2], r[3]))
+  return rows
+
+
+@pytest.mark.gpu
+def test_gpu_primitive_narrowphase_matches_fused_collision():
+  import mujoco_warp_amd as mjw
+  from mujoco_warp_amd import mjcf, stages
+
+  mjm = mjcf.load_model_from_string(PRIM_XML)
+  nworld = 4
+  rng = np.random.default_rng(5)
+  qpos = np.tile(np.asarray(mjm.qpos0, np.float64), (nworld, 1))
+  qpos[1:, 2::7] += rng.uniform(-0.01, 0.01, (nworld - 1, mjm.nbody - 1))  # heights
+  m = mjw.put_model(mjm, device="cuda")
+  d = mjw.make_data(mjm, nworld=nworld, nconmax=64, njmax=256, device="cuda", m=m)
+  d.qpos[:] = torch.as_tensor(qpos, dtype=torch.float32, device="cuda")
+  mjw.fwd_position(m, d)  # fused broad- + narrowphase, contacts in the pool
+  torch.cuda.synchronize()
+  n_fused = int(d.nacon[0])
+  ncol_fused = int(d.ncollision[0])
+  fused = _contact_set(d, n_fused, constraint_only=False)
+  types_present = {(int(mjm.geom_type[a]), int(mjm.geom_type[b])) for _, a, b, *_ in fused}
+  want_types = {(int(a), int(b)) for a, b in stages.PRIMITIVE_PAIRS}
+  assert want_types <= types_present, sorted(want_types - types_present)
+  # the sub-stages on the same geom frames
+  d.nacon.zero_()
+  d.ncollision.zero_()
+  ctx = mjw.create_collision_context(d.naconmax, device=d)
+  mjw.nxn_broadphase(m, d, ctx)
+  mjw.primitive_narrowphase(m, d, ctx)
+  torch.cuda.synchronize()
+  assert int(d.ncollision[0]) == ncol_fused
+  staged = _contact_set(d, int(d.nacon[0]), constraint_only=False)
+  assert all(int(t) == 1 for t in d.contact.type.cpu().numpy()[: int(d.nacon[0])])
+  assert np.all(d.contact.efc_address.cpu().numpy()[: int(d.nacon[0])] == -1)
+  assert len(staged) == len(fused), (len(staged), len(fused))
+  for a, b in zip(staged, fused):
+    assert a[:4] == b[:4], (a[:4], b[:4])
+    np.testing.assert_allclose(a[4], b[4], rtol=0, atol=1e-6)
+    for i in range(5, 10):
+      np.testing.assert_allclose(a[i], b[i], rtol=0, atol=1e-6)
+    assert a[10] == b[10]
+  # a table restricted to plane-sphere: only those contacts
+  d.nacon.zero_()
+  mjw.primitive_narrowphase(m, d, ctx, [(mjw.GeomType.PLANE, mjw.GeomType.SPHERE)])
+  torch.cuda.synchronize()
+  only = _contact_set(d, int(d.nacon[0]), constraint_only=False)
+  assert only and all((int(mjm.geom_type[r[1]]), int(mjm.geom_type[r[2]])) == (0, 2) for r in only)
+  with pytest.raises(NotImplementedError):
+    mjw.primitive_narrowphase(m, d, ctx, [(mjw.GeomType.BOX, mjw.GeomType.BOX)])

@@ -15,12 +15,12 @@ import pytest
 
 from tests.common import HUMANOID, np_, random_states
 
-# out of scope: rendering / rays, inverse dynamics, islands, BVH / SAP / SDF collision
-# front ends and the broad- / narrowphase sub-stages of `collision` (one fused stage here); the set_const
-# family, set_length_range and deriv_smooth_vel are implemented (stages.py)
+# out of scope: rendering / rays, inverse dynamics, islands, BVH and SDF collision; the
+# broad- / narrowphase sub-stages (tests/test_collision_stages.py), the set_const family,
+# set_length_range and deriv_smooth_vel are implemented (stages.py)
 OUT_OF_SCOPE = {
   "RenderContext", "create_render_context", "get_depth", "get_rgb", "get_segmentation", "render", "ray", "rays", "refit_bvh",
-  "inverse", "island", "sap_broadphase", "nxn_broadphase", "primitive_narrowphase", "sdf_narrowphase",
+  "inverse", "island", "sdf_narrowphase",
 }
 
 
