@@ -167,12 +167,18 @@ def test_oracle_tactile_fp32_tracks_fp64():
 
 
 @pytest.mark.gpu
-def test_gpu_tactile_matches_oracle():
+@pytest.mark.parametrize("sparse", [False, True], ids=["dense", "sparse"])
+def test_gpu_tactile_matches_oracle(sparse):
+  """The sensor kernel serves both pipelines: the dense world-per-wave one and (jacobian = sparse) the
+  workgroup-per-world sparse one, whose contacts reach it through the same constraint rows."""
   import torch
 
   import mujoco_warp_amd as mjw
 
   mjm, od = _oracle()
+  if sparse:
+    mjm = _load()
+    mjm.opt.jacobian = 1
   qpos = _qpos()
   n = len(POSES)
   m, d = gpu_from_state(mjm, qpos, np.zeros((n, mjm.nv)), np.zeros((n, mjm.nu)), njmax=128, nconmax=32)
