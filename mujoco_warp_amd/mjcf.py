@@ -1300,8 +1300,8 @@ class _Compiler:
     gtype = _GEOM_TYPES[ga.get("type", _GEOM_DEFAULTS["type"])]
     if gtype == GeomType.SDF:
       raise NotImplementedError(f"geom type {gtype.name} not supported by the MJCF compiler")
-    if gtype == GeomType.HFIELD and bodyid != 0:
-      raise NotImplementedError("heightfield geoms on moving bodies are not supported by this compiler (attach them to the worldbody)")
+    # heightfields may sit on moving bodies: the collision routines take the geom's frame; like planes they
+    # contribute no mass (the body's other geoms or an explicit <inertial> give it one)
     # mesh geoms: the mesh file is not read (no mesh collision or mesh-derived inertia here), so
     # the geom keeps its declared frame; put_model rejects meshes that can collide and bodies
     # whose inertia would come from a mesh.

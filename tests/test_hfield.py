@@ -46,11 +46,77 @@ def test_compile_hfield_asset_and_geom():
   assert m.nxn_ccd == 2  # both heightfields against the sphere take pre-pass slots
 
 
-def test_compile_hfield_refusals():
-  with pytest.raises(NotImplementedError):
-    _load("""<mujoco><asset><hfield name="t" nrow="2" ncol="2" size="1 1 .1 .1"/></asset>
-    <worldbody><body><freejoint/><geom type="hfield" hfield="t"/></body></worldbody></mujoco>""")
-  # (image / binary heightfield files are read: tests/test_hfield_file.py)
+def test_compile_hfield_on_moving_body():
+  """Heightfields may sit on moving bodies (the collision routines take the geom's frame); like planes they
+  contribute no mass, so the body's mass comes from its other geoms.  (Image / binary heightfield files:
+  tests/test_hfield_file.py.)"""
+  mjm = _load(MOVING.format(elev=" ".join(["0"] * 42)))
+  b = mjm.body_names.index("terrain")
+  np.testing.assert_allclose(mjm.body_mass[b], 5.0)
+  assert int(mjm.geom_type[mjm.body_geomadr[b]]) == 1
+
+
+# the bumpy heightfield of BUMPY on a free body of its own (plus a massive non-colliding box), a sphere on
+# a second free body
+MOVING = """<mujoco><option gravity="0 0 -9.81"/><asset>
+<hfield name="h" nrow="6" ncol="7" size=".6 .5 .15 .1" elevation="{elev}"/></asset>
+<worldbody>
+<body name="terrain" pos=".05 -.03 0" euler="0 0 20"><freejoint/><geom type="hfield" hfield="h"/>
+  <geom type="box" size=".1 .1 .02" pos="0 0 -.3" contype="0" conaffinity="0" mass="5"/></body>
+<body pos="0 0 .2"><freejoint/><geom type="sphere" size=".12"/></body></worldbody></mujoco>"""
+
+
+def _qmul(a, b):
+  w1, x1, y1, z1 = a
+  w2, x2, y2, z2 = b
+  return np.array([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                   w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2])
+
+
+def _qrot(q):
+  w, x, y, z = q
+  return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                   [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                   [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def _moving_worlds(mjm, nworld, seed=4):
+  """World 0: the terrain at its default pose, the sphere somewhere over it; world k: both bodies moved by
+  one rigid transform (R_k, t_k).  Returns qpos and the transforms."""
+  rng = np.random.default_rng(seed)
+  q0 = np.asarray(mjm.qpos0, np.float64).copy()
+  q0[7:10] = [0.1, -0.05, 0.13]
+  qpos, T = [q0], [(np.eye(3), np.zeros(3))]
+  for _ in range(nworld - 1):
+    qr = rng.normal(size=4)
+    qr /= np.linalg.norm(qr)
+    R, t = _qrot(qr), rng.uniform(-1, 1, 3)
+    q = q0.copy()
+    for a in (0, 7):
+      q[a:a + 3] = R @ q0[a:a + 3] + t
+      q[a + 3:a + 7] = _qmul(qr, q0[a + 3:a + 7])
+    qpos.append(q)
+    T.append((R, t))
+  return np.stack(qpos), T
+
+
+def test_oracle_moving_hfield_is_rigid_motion_invariant():
+  """The same terrain-sphere configuration under rigid motions of both bodies: the same contact depths,
+  the points and normals carried by the motion."""
+  rng = np.random.default_rng(5)
+  mjm = _load(MOVING.format(elev=" ".join(f"{v:.4f}" for v in rng.uniform(0, 1, 42))))
+  qpos, T = _moving_worlds(mjm, 6)
+  od = _oracle(mjm, qpos)
+  n0, d0, p0, f0 = _contacts(od, 0)
+  assert n0 >= 1
+  for w in range(1, len(qpos)):
+    n, d, p, f = _contacts(od, w)
+    R, t = T[w]
+    assert n == n0, w
+    order = np.argsort(d0), np.argsort(d)
+    np.testing.assert_allclose(d[order[1]], d0[order[0]], atol=1e-9)
+    np.testing.assert_allclose(p[order[1]], (p0 @ R.T + t)[order[0]], atol=1e-7)
+    np.testing.assert_allclose(f[order[1]], (f0 @ R.T)[order[0]], atol=1e-7)
 
 
 @pytest.mark.parametrize("margin", [0.0, 0.1])
@@ -256,6 +322,28 @@ def test_gpu_hfield_contacts_match_oracle(kind, sparse):
   torch.cuda.synchronize()
   for w in stable:
     _match(d, od, w, *tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gpu_moving_hfield_matches_oracle(sparse):
+  """The heightfield on a moving body: the device pre-pass reads its frame from the kinematics, as the oracle."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  rng = np.random.default_rng(5)
+  mjm = _load(MOVING.format(elev=" ".join(f"{v:.4f}" for v in rng.uniform(0, 1, 42))))
+  if sparse:
+    mjm.opt.jacobian = 1
+  qpos, _ = _moving_worlds(mjm, 8)
+  m, d = gpu_from_state(mjm, qpos, np.zeros((8, mjm.nv)), np.zeros((8, mjm.nu)), njmax=256, nconmax=16)
+  assert bool(m.is_sparse) == sparse
+  od = _oracle(mjm, qpos)
+  mjw.fwd_position(m, d)
+  torch.cuda.synchronize()
+  for w in range(8):
+    _match(d, od, w, 5e-5, 5e-4, 5e-3)
 
 
 @pytest.mark.gpu

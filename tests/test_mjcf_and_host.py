@@ -119,9 +119,6 @@ def test_unsupported_features_raise():
   import mujoco_warp_amd as mjw
   from mujoco_warp_amd import mjcf
 
-  with pytest.raises(NotImplementedError):  # heightfields on a moving body: not compiled
-    mjcf.load_model_from_string('<mujoco><asset><hfield name="h" nrow="2" ncol="2" size="1 1 .1 .1"/></asset>'
-                                '<worldbody><body><freejoint/><geom type="hfield" hfield="h"/></body></worldbody></mujoco>')
   for flags in ("<flag override=\"enable\"/>", "<flag fwdinv=\"enable\"/>", "<flag midphase=\"disable\"/>"):
     try:
       m = mjcf.load_model_from_string(f'<mujoco><option>{flags}</option><worldbody><body><freejoint/><geom size=".1"/></body></worldbody></mujoco>')
