@@ -31,7 +31,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 32
+#define MJW_ABI_VERSION 33
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -48,7 +48,7 @@
   X(nmesh) X(nmeshvert) X(ntendon) X(nwrap) X(nJten) X(ten_maxnnz) X(nmuscle) X(sp_nH)   \
   X(npair) X(ngravcomp) X(has_fluid) X(nten_spatial) X(act_maxnnz) X(nbodytrn) X(nsitetrn)             \
   X(nsensorcollision) X(nsensorccd) X(nhfield) X(nhfielddata) X(opt_contact_sensor_maxmatch)           \
-  X(nmeshpoly) X(nmeshpolyvert) X(nmeshpolymap) X(nmaxpolygon) X(nmaxmeshdeg) X(nsensortaxel) X(nmeshnormal)
+  X(nmeshpoly) X(nmeshpolyvert) X(nmeshpolymap) X(nmaxpolygon) X(nmaxmeshdeg) X(nsensortaxel) X(nmeshnormal) X(nsensorcontact)
 
 /* ---- model: float arrays, batchable (leading dim nb = 1 or nworld, indexed worldid % nb) ---- */
 #define MJW_MODEL_REAL_ARRAYS(X)                                                                   \

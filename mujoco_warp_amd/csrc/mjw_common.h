@@ -336,5 +336,7 @@ int rk4_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int op,
 int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int stages = 7, int w0 = 0, int count = -1);
 // workgroup-per-world pipeline of sparse / flex models (m->is_sparse), mjw_sparse.hip; ST_* stage bits
 int sparse_launch(int stages, const mjw_model_t* m, const mjw_data_t* d, hipStream_t s);
+// per-world slot ranges of the contact pool (d->ncon_world) on the dense path, mjw_step.hip
+int pool_ranges_launch(const mjw_data_t* d, hipStream_t s);
 
 }  // namespace mjw

@@ -595,15 +595,55 @@ __device__ __forceinline__ bool contact_obj_match(const mjw_model_t& m, int body
   return false;
 }
 
-// the world's contacts in pool (= narrowphase) order: each contact at its first constraint row; returns the
-// contact id of row r or -1
-__device__ __forceinline__ int contact_at_row(const mjw_model_t& m, const mjw_data_t& d, int wid, int r) {
-  const long wr = (long)wid * d.njmax;
-  const int type = d.efc_type[wr + r];
-  if (type != CNSTR_CONTACT_FRICTIONLESS && type != CNSTR_CONTACT_PYRAMIDAL && type != CNSTR_CONTACT_ELLIPTIC) return -1;
-  const int cid = d.efc_id[wr + r];
-  if (cid < 0 || cid >= d.naconmax || d.contact_efc_address[(long)cid * m.nmaxpyramid] != r) return -1;
-  return cid;
+// the world's slot range of the contact pool, [k0, k1): ncon_world (first slot, span), filled by the pool_ranges
+// launch before the sensor kernel on the dense path (sensor_launch) and by the collision kernel on the sparse
+// path.  The world's contacts are the slots of the range whose worldid is wid, in pool (= narrowphase) order;
+// other worlds' slots can interleave when a world staged its contacts over several rounds.
+__device__ __forceinline__ void world_pool_range(const mjw_data_t& d, int wid, int& k0, int& k1) {
+  k0 = d.ncon_world[2L * wid];
+  k1 = min(min(d.nacon[0], d.naconmax), k0 + d.ncon_world[2L * wid + 1]);
+}
+// contact k of the pool is a constraint contact of world wid (sensor.py:2313-2316: the contact sensor keeps
+// every CONSTRAINT-typed contact, with rows or not; contact_force_local gives zero force without rows)
+__device__ __forceinline__ bool world_constraint_contact(const mjw_data_t& d, int wid, int k) {
+  return d.contact_worldid[k] == wid && (d.contact_type[k] & 1);
+}
+
+// sensor.py:2085-2118 _preprocess_tactile_contacts for one weld body: the partner geoms of the world's
+// contacts on weld body pw -- geom2 for a contact whose geom1 is on it, then geom1 for one whose geom2 is --
+// in pool order, the first MJ_MAXCONPAIR (50) kept in `list` (LDS); every contact of the pool counts,
+// sensor-only ones included.  Whole wave, lane = contact; returns the count kept.
+__device__ int tactile_partners(const mjw_model_t& m, const mjw_data_t& d, int wid, int pw, int* list, int lane) {
+  int k0, k1;
+  world_pool_range(d, wid, k0, k1);
+  int cnt = 0;
+  for (int base = k0; base < k1 && cnt < 50; base += 64) {
+    const int k = base + lane;
+    int ga = -1, gb = -1;
+    if (k < k1 && d.contact_worldid[k] == wid) {
+      const int g1 = d.contact_geom[2L * k], g2 = d.contact_geom[2L * k + 1];
+      if (g1 >= 0 && g2 >= 0) {
+        if (m.body_weldid[m.geom_bodyid[g1]] == pw) ga = g2;
+        if (m.body_weldid[m.geom_bodyid[g2]] == pw) gb = g1;
+      }
+    }
+    const int n = (ga >= 0) + (gb >= 0);
+    int incl = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    int pos = cnt + incl - n;
+    if (ga >= 0) {
+      if (pos < 50) list[pos] = ga;
+      pos++;
+    }
+    if (gb >= 0 && pos < 50) list[pos] = gb;
+    cnt += __shfl(incl, 63, 64);
+  }
+  __syncthreads();
+  return min(cnt, 50);
 }
 
 // collision_sdf.py:157-183, 393-400: primitive signed distances in the geom frame (box: radial field inside);
@@ -634,30 +674,19 @@ __device__ __forceinline__ float tactile_sdf(int type, const float* p, const flo
   return 0.0f;
 }
 
-// the geom on the other side of row r's contact when `side` of it is on weld body pw (-1: none)
-__device__ __forceinline__ int tactile_other(const mjw_model_t& m, const mjw_data_t& d, int wid, int pw, int r, int side) {
-  const int cid = contact_at_row(m, d, wid, r);
-  if (cid < 0) return -1;
-  const int g1 = d.contact_geom[2L * cid], g2 = d.contact_geom[2L * cid + 1];
-  if (g1 < 0 || g2 < 0) return -1;
-  const int g = side == 0 ? g1 : g2;
-  return m.body_weldid[m.geom_bodyid[g]] == pw ? (side == 0 ? g2 : g1) : -1;
-}
-
-// sensor.py:2085-2252 tactile, one sensor by the whole wave (lane = taxel): each vertex of the sensor's
+// sensor.py:2121-2252 tactile, one sensor by the whole wave (lane = taxel): each vertex of the sensor's
 // mesh, placed with the sensor geom's pose, takes pressure depth / max(0.05 - depth, MINVAL) from every
 // distinct geom among the first MJ_MAXCONPAIR (50) contact partners of the sensor geom's weld body at which
-// the SDF is negative.  Partners come in the world's contact order (each contact at its first constraint
-// row; the reference's atomic order is arbitrary), deduplicated by rescanning the earlier ones instead of
-// an indexed list, so the kernel needs no scratch.  Layout [normal (nvt), tangent 1 (nvt), tangent 2
-// (nvt)]; the tangential slip terms need per-vertex tangent frames, which the compiler's meshes do not have
-// (mesh_normalnum = vertnum), so they are 0.
-__device__ void tactile_sensor(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s, int lane) {
+// the SDF is negative.  The partner list (tactile_partners, LDS `list`) is built once per sensor and world
+// in pool order (the reference's atomic order is arbitrary).  Layout [normal (nvt), tangent 1 (nvt),
+// tangent 2 (nvt)]; the tangential slip terms need per-vertex tangent frames, which the compiler's meshes
+// do not have (mesh_normalnum = vertnum), so they are 0.
+__device__ void tactile_sensor(const mjw_model_t& m, const mjw_data_t& d, int wid, const Frames& F, int s, int lane, int* list) {
   const int mesh = m.sensor_objid[s], geom = m.sensor_refid[s];
   const int nvt = m.mesh_vertnum[mesh];
   float* out = d.sensordata + (long)wid * m.nsensordata + m.sensor_adr[s];
   const int pw = m.body_weldid[m.geom_bodyid[geom]];
-  const int nefc = min(d.nefc[wid], d.njmax);
+  const int npart = tactile_partners(m, d, wid, pw, list, lane);
   const float* gx = F.gxpos + 3 * geom;
   const float* gm = F.gxmat + 9 * geom;
   const float* vert = MR(mesh_vert) + 3 * (long)m.mesh_vertadr[mesh];
@@ -669,26 +698,19 @@ __device__ void tactile_sensor(const mjw_model_t& m, const mjw_data_t& d, int wi
     const float* nrm = nrm0 + 3 * v;
     const float nn = dot3(nrm, nrm);
     float total = 0.0f;
-    int nadd = 0;
-    for (int r = 0; r < nefc && nadd < 50; r++) {
-      for (int side = 0; side < 2 && nadd < 50; side++) {
-        const int g = tactile_other(m, d, wid, pw, r, side);
-        if (g < 0) continue;
-        nadd++;
-        bool dup = false;
-        for (int r2 = 0; r2 <= r && !dup; r2++)
-          for (int s2 = 0; s2 < 2 && !dup; s2++)
-            if (r2 < r || s2 < side) dup = tactile_other(m, d, wid, pw, r2, s2) == g;
-        if (dup) continue;
-        const float* px = F.gxpos + 3 * g;
-        const float* pm = F.gxmat + 9 * g;
-        float dx[3], q[3];
-        for (int i = 0; i < 3; i++) dx[i] = x[i] - px[i];
-        mat_t_vec(q, pm, dx);
-        const float depth = fminf(tactile_sdf(m.geom_type[g], q, gsize + 3 * g), 0.0f);
-        if (depth >= 0.0f) continue;
-        total += depth / fmaxf(0.05f - depth, MJW_MINVAL) * nn;
-      }
+    for (int p = 0; p < npart; p++) {
+      const int g = list[p];
+      bool dup = false;
+      for (int p2 = 0; p2 < p && !dup; p2++) dup = list[p2] == g;
+      if (dup) continue;
+      const float* px = F.gxpos + 3 * g;
+      const float* pm = F.gxmat + 9 * g;
+      float dx[3], q[3];
+      for (int i = 0; i < 3; i++) dx[i] = x[i] - px[i];
+      mat_t_vec(q, pm, dx);
+      const float depth = fminf(tactile_sdf(m.geom_type[g], q, gsize + 3 * g), 0.0f);
+      if (depth >= 0.0f) continue;
+      total += depth / fmaxf(0.05f - depth, MJW_MINVAL) * nn;
     }
     out[v] = total;
     out[nvt + v] = 0.0f;
@@ -733,7 +755,8 @@ __device__ void contact_sensor(const mjw_model_t& m, const mjw_data_t& d, int wi
   if (size == 0) return;
   const int dim = m.sensor_dim[s], num = dim / size;
   float* out = d.sensordata + (long)wid * m.nsensordata + m.sensor_adr[s];
-  const int nefc = min(d.nefc[wid], d.njmax);
+  int k0, k1;
+  world_pool_range(d, wid, k0, k1);
   const int maxmatch = m.opt_contact_sensor_maxmatch;
   auto criteria = [&](int cid) -> float {
     if (reduce == 1) return d.contact_dist[cid];
@@ -744,9 +767,8 @@ __device__ void contact_sensor(const mjw_model_t& m, const mjw_data_t& d, int wi
   // pass 1: the match count (all matches: `found`) and, for netforce, the sums
   int nmatch = 0;
   float np[3] = {0, 0, 0}, nf[3] = {0, 0, 0}, nt[3] = {0, 0, 0}, wsum = 0.0f;
-  for (int r = 0; r < nefc; r++) {
-    const int cid = contact_at_row(m, d, wid, r);
-    if (cid < 0) continue;
+  for (int cid = k0; cid < k1; cid++) {
+    if (!world_constraint_contact(d, wid, cid)) continue;
     const float dir = contact_match(m, d, wid, F, s, cid);
     if (dir == 0.0f) continue;
     const int k = nmatch++;
@@ -788,9 +810,8 @@ __device__ void contact_sensor(const mjw_model_t& m, const mjw_data_t& d, int wi
     // slot i: the i-th match in order (none) or the next (criteria, order) after the previous slot's
     int cid = -1, k = 0, best_k = -1;
     float dir = 0.0f, best_c = MJW_MAXVAL;
-    for (int r = 0; r < nefc && k < maxmatch; r++) {
-      const int c_ = contact_at_row(m, d, wid, r);
-      if (c_ < 0) continue;
+    for (int c_ = k0; c_ < k1 && k < maxmatch; c_++) {
+      if (!world_constraint_contact(d, wid, c_)) continue;
       const float dr = contact_match(m, d, wid, F, s, c_);
       if (dr == 0.0f) continue;
       if (reduce == 0) {

@@ -16,7 +16,7 @@
 namespace mjw {
 
 struct SLay {
-  int cacc, cfrc, cext, cvel, cinert, com, cdof, cdofdot, qvel, qacc, ccd, scc, total;
+  int cacc, cfrc, cext, cvel, cinert, com, cdof, cdofdot, qvel, qacc, ccd, scc, tac, total;
 };
 
 __host__ inline SLay make_slayout(const mjw_model_t& m) {
@@ -27,6 +27,7 @@ __host__ inline SLay make_slayout(const mjw_model_t& m) {
   L.cacc = take(nb * 6); L.cfrc = take(nb * 6); L.cext = take(nb * 6); L.cvel = take(nb * 6); L.cinert = take(nb * 10);
   L.com = take(nb * 3); L.cdof = take(nv * 6); L.cdofdot = take(nv * 6); L.qvel = take(nv); L.qacc = take(nv);
   // collision sensors on convex pairs: the lockstep GJK / EPA workspace and the per-record results
+  L.tac = m.nsensortaxel > 0 ? take(64) : -1;  // tactile: a weld body's contact partners (tactile_partners)
   L.ccd = L.scc = -1;
   if (m.nsensorccd > 0) {
     L.ccd = take(ccd_layout(m.ccd_epa_iterations, m.nhfield > 0, m.nmaxpolygon, m.nmaxmeshdeg).total);
@@ -326,7 +327,7 @@ __device__ __forceinline__ void sensor_body(const mjw_model_t& m, const mjw_data
   // tactile sensors (sensor.py:2085-2252): one sensor at a time, lane = taxel
   if ((stages & 4) && m.nsensortaxel > 0)
     for (int k = 0; k < m.nsensor; k++)
-      if (m.sensor_type[k] == SENS_TACTILE) tactile_sensor(m, d, wid, F, k, lane);
+      if (m.sensor_type[k] == SENS_TACTILE) tactile_sensor(m, d, wid, F, k, lane, reinterpret_cast<int*>(s) + L.tac);
 }
 
 __global__ void __launch_bounds__(64) sensor_acc_kernel(const mjw_model_t m, const mjw_data_t d, const SLay L, int stages, int w0) {
@@ -342,6 +343,12 @@ int sensor_launch(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, int 
   SLay L = make_slayout(*m);
   size_t lds = (size_t)L.total * 4;
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+  // contact and tactile sensors walk each world's contacts in the pool: its slot range first (the sparse
+  // path's collision kernel records it itself)
+  if (!m->is_sparse && (stages & 4) && (m->nsensorcontact > 0 || m->nsensortaxel > 0)) {
+    const int rc = pool_ranges_launch(d, s);
+    if (rc) return rc;
+  }
   if (m->nsensorcollision > 0) {
     hipLaunchKernelGGL(sensor_coll_kernel, dim3(count), dim3(64), lds, s, *m, *d, L, stages, w0);
     trace_launch(s, K_SENSOR_COLL);

@@ -25,6 +25,9 @@
 
 namespace mjw {
 
+// words per elliptic contact of the generic solver's line-search coefficients (Ell, mjw_dense.h)
+constexpr int EC_WORDS = 10;
+
 // per-world LDS layout (offsets in 4-byte words)
 struct Lay {
   int qpos, qvel, xpos, xquat, xmat, xipos, ximat, xanchor, xaxis, gxpos, gxmat;
@@ -35,6 +38,7 @@ struct Lay {
   int Jaref, jv, rowcon;
   int act_len, act_vel, act_force, act_mom, act_momdof, act_nnz, amax;
   int con, cmax, jqvel, plist, scratch, iscratch, ccd;
+  int ecoef, econe;  // generic solver, elliptic cones: per-contact line-search coefficients, Newton cone blocks
   int nofactor;
   int total;
 };
@@ -93,6 +97,13 @@ __host__ inline Lay make_layout(const mjw_model_t& m, int njmax, bool nofactor =
     L.plist = take(m.nxn);
     L.con = take(L.cmax * CREC);
   }
+  // elliptic cones in the generic solver (solve below): the rows' unused efc_pos / efc_margin / efc_vel
+  // slots hold each row's cone coefficient, contact extent and u = Jaref * coefficient; ecoef the
+  // quad / quad1 / quad2 words of a contact's line search at its first row; econe the 6 cone-Hessian
+  // coefficients of a row (Newton)
+  const bool ell_generic = !nofactor && m.opt_cone == CONE_ELLIPTIC;
+  L.ecoef = ell_generic ? take(EC_WORDS * njmax) : -1;
+  L.econe = (ell_generic && m.opt_solver == SOLVER_NEWTON) ? take(6 * njmax) : -1;
   L.rowcon = -1;
   // moment slots per actuator: 1 when every transmission has one non-zero (nJmom == nu: hinge / slide
   // joints), else 6 (free / ball joints)
@@ -710,6 +721,7 @@ __device__ __forceinline__ void efc_row(const mjw_model_t& m, const mjw_data_t& 
     s[L.efc_D + r] = D;
     s[L.efc_aref + r] = aref;
     s[L.efc_frictionloss + r] = frictionloss;
+    reinterpret_cast<int*>(s)[L.efc_type + r] = type;
   }
 }
 
@@ -1478,6 +1490,10 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
             pos_aref = 0.0f;
           }
           efc_row(m, d, L, s, wid, r, pos_aref, pos, invweight, sref, rec + 23, rec[1], Jqvel, 0.0f, CNSTR_CONTACT_ELLIPTIC, reci[31]);
+          if (L.ecoef >= 0) {  // the generic solver's cone coefficient and contact extent of the row
+            s[L.efc_pos + r] = dimid == 0 ? rec[14] * impratio_invsqrt : rec[14 + dimid - 1];
+            si[L.efc_margin + r] = (r - dimid) | (condim << 16);
+          }
           continue;
         }
         if (condim > 1) {
@@ -2063,15 +2079,75 @@ __device__ __forceinline__ bool in_bracket(const Vec3& x, const Vec3& y) {
 }
 
 // update_constraint (solver.py:2154-2219): returns (cost, gauss); sets force/state; qfrc_constraint per lane
+// elliptic rows of the generic solver (L.ecoef >= 0): row r is an elliptic contact row; its contact's first
+// row and dimension (efc_margin slot), and whether all of the contact's rows fit in nefc
+__device__ __forceinline__ bool ell_row(const Lay& L, const int* si, int r, int ne, int nf) {
+  return L.ecoef >= 0 && r >= ne + nf && si[L.efc_type + r] == CNSTR_CONTACT_ELLIPTIC;
+}
+__device__ __forceinline__ void ell_extent(const Lay& L, const int* si, int r, int& r0, int& dim) {
+  const int x = si[L.efc_margin + r];
+  r0 = x & 0xffff;
+  dim = x >> 16;
+}
+
+// one row's line-search terms at alpha, elliptic rows through their contact's cone at the first row
+// (solver.py:263-323, the other rows of the contact add nothing)
+__device__ __forceinline__ void eval_row_g(const Lay& L, const float* s, int rr, int nefc, int ne, int nf, float alpha, Vec3& o) {
+  const int* si = reinterpret_cast<const int*>(s);
+  if (ell_row(L, si, rr, ne, nf)) {
+    int r0, dim;
+    ell_extent(L, si, rr, r0, dim);
+    if (rr != r0 || r0 + dim > nefc) return;
+    const float* q = s + L.ecoef + EC_WORDS * rr;
+    const Ell e = {q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8], q[9]};
+    float c, g, hh;
+    eval_elliptic(e, alpha, c, g, hh);
+    o.c += c; o.g += g; o.h += hh;
+    return;
+  }
+  eval_row(s[L.efc_D + rr], s[L.Jaref + rr], s[L.jv + rr], s[L.efc_frictionloss + rr], rr, ne, nf, alpha, o);
+}
+
 __device__ __forceinline__ void update_constraint(const Lay& L, float* s, int lane, int nv, int nvs, int nefc, int ne, int nf, float ma,
                                   float qfrc_smooth, float qacc, float qacc_smooth, float& cost, float& gauss, float& qfrc_c) {
   int* si = reinterpret_cast<int*>(s);
   float c = 0.0f;
+  float* u = s + L.efc_vel;        // elliptic: u = Jaref * cone coefficient
+  const float* ef = s + L.efc_pos;  // elliptic: cone coefficient
+  if (L.ecoef >= 0) {
+    for (int r = lane; r < nefc; r += LPW) u[r] = s[L.Jaref + r] * ef[r];
+    WSYNC();
+  }
   for (int r = lane; r < nefc; r += LPW) {
     float D = s[L.efc_D + r], Jaref = s[L.Jaref + r];
     float f;
     int st;
-    if (r < ne) { f = -D * Jaref; st = STATE_QUADRATIC; c += 0.5f * D * Jaref * Jaref; }
+    if (ell_row(L, si, r, ne, nf)) {
+      // elliptic cone zones (solver.py:1886-1942): N from the first row, T from the friction rows; a
+      // contact cut by njmax contributes nothing
+      int r0, dim;
+      ell_extent(L, si, r, r0, dim);
+      const float mu = ef[r0];
+      f = 0.0f;
+      st = STATE_SATISFIED;
+      if (r0 + dim <= nefc) {
+        float TT = 0.0f;
+        for (int j = 1; j < dim; j++) TT += u[r0 + j] * u[r0 + j];
+        const float N = u[r0];
+        const float T = TT <= 0.0f ? 0.0f : sqrtf(TT);
+        if (N >= mu * T || (T <= 0.0f && N >= 0.0f)) {
+        } else if (mu * N + T <= 0.0f || (T <= 0.0f && N < 0.0f)) {
+          f = -D * Jaref; st = STATE_QUADRATIC; c += 0.5f * D * Jaref * Jaref;
+        } else {
+          const float dm = safe_div(s[L.efc_D + r0], mu * mu * (1.0f + mu * mu));
+          const float nmt = N - mu * T;
+          const float f0 = -dm * nmt * mu;
+          if (r == r0) { f = f0; c += 0.5f * dm * nmt * nmt; }
+          else f = -safe_div(f0, T) * (u[r] * ef[r]);
+          st = STATE_CONE;
+        }
+      }
+    } else if (r < ne) { f = -D * Jaref; st = STATE_QUADRATIC; c += 0.5f * D * Jaref * Jaref; }
     else if (r < ne + nf) {
       float fl = s[L.efc_frictionloss + r], rf = safe_div(fl, D);
       if (Jaref <= -rf) { f = fl; st = STATE_LINEARNEG; c += -fl * (0.5f * rf + Jaref); }
@@ -2146,12 +2222,53 @@ __device__ __forceinline__ void solve(const mjw_model_t& m, const mjw_data_t& d,
       Mgrad = cholesky_solve(Lm, nv, nvs, lane, grad);
     } else {
       // H = M + J' diag(D * QUADRATIC) J, Cholesky, solve
+      float* C = s + L.econe;
+      if (L.econe >= 0) {
+        // cone-state contacts add J_c' C J_c (solver.py:2430-2585); C's row a, from u = Jaref * coefficient
+        // of update_constraint, as in mjw_dense.h
+        const float* u = s + L.efc_vel;
+        const float* ef = s + L.efc_pos;
+        for (int r = lane; r < nefc; r += LPW) {
+          if (si[L.efc_state + r] != STATE_CONE) continue;
+          int r0, dim;
+          ell_extent(L, si, r, r0, dim);
+          const int ea = r - r0;
+          const float mu = ef[r0], mu2 = mu * mu;
+          const float dm = safe_div(s[L.efc_D + r0], mu2 * (1.0f + mu2));
+          const float n = u[r0];
+          float tt = 0.0f;
+          for (int j = 1; j < dim; j++) tt += u[r0 + j] * u[r0 + j];
+          float t = tt <= 0.0f ? 0.0f : sqrtf(tt);
+          t = fmaxf(t, MJW_MINVAL);
+          const float ttt = fmaxf(t * t * t, MJW_MINVAL);
+          const float mu_over_t = safe_div(mu, t), mu_n_over_ttt = mu * safe_div(n, ttt), diag = mu2 - mu * safe_div(n, t);
+          const float ua = u[r];
+          for (int k = 0; k < dim; k++) {
+            const float ub = u[r0 + k];
+            float hc;
+            if (ea == 0 && k == 0) hc = 1.0f;
+            else if (ea == 0) hc = -mu_over_t * ub;
+            else if (k == 0) hc = -mu_over_t * ua;
+            else hc = mu_n_over_ttt * ua * ub + (ea == k ? diag : 0.0f);
+            C[6 * r + k] = hc * dm * ef[r] * ef[r0 + k];
+          }
+        }
+        WSYNC();
+      }
       if (inl)
         for (int k = 0; k < nv; k++) {
           float h = M[lane * nvs + k];
           for (int r = 0; r < nefc; r++) {
-            if (si[L.efc_state + r] != STATE_QUADRATIC) continue;
-            h += s[L.efc_D + r] * s[L.J + r * nvs + lane] * s[L.J + r * nvs + k];
+            const int st = si[L.efc_state + r];
+            if (st == STATE_QUADRATIC) {
+              h += s[L.efc_D + r] * s[L.J + r * nvs + lane] * s[L.J + r * nvs + k];
+            } else if (L.econe >= 0 && st == STATE_CONE) {
+              int r0, dim;
+              ell_extent(L, si, r, r0, dim);
+              float w = 0.0f;
+              for (int b = 0; b < dim; b++) w += C[6 * r + b] * s[L.J + (r0 + b) * nvs + k];
+              h += s[L.J + r * nvs + lane] * w;
+            }
           }
           H[lane * nvs + k] = h;
         }
@@ -2175,7 +2292,6 @@ __device__ __forceinline__ void solve(const mjw_model_t& m, const mjw_data_t& d,
       float mv = 0.0f;
       if (inl)
         for (int k = 0; k < nv; k++) mv += M[lane * nvs + k] * vec[k];
-      float jv = 0.0f, jaref = 0.0f, Dr = 0.0f, flr = 0.0f;
       const int r = lane;  // row per lane (njmax <= 64 handled below by rows loop)
       for (int rr = lane; rr < nefc; rr += LPW) {
         float acc = 0.0f;
@@ -2184,6 +2300,29 @@ __device__ __forceinline__ void solve(const mjw_model_t& m, const mjw_data_t& d,
       }
       WSYNC();
       (void)r;
+      if (L.ecoef >= 0) {
+        // per-contact quad / quad1 / quad2 at the first row, once per line search (solver.py:1550-1611)
+        for (int rr = lane; rr < nefc; rr += LPW) {
+          if (!ell_row(L, si, rr, ne, nf)) continue;
+          int r0, dim;
+          ell_extent(L, si, rr, r0, dim);
+          if (rr != r0 || r0 + dim > nefc) continue;
+          const float D0 = s[L.efc_D + rr], ja = s[L.Jaref + rr], jv0 = s[L.jv + rr], mu = s[L.efc_pos + rr];
+          float q0 = 0.5f * ja * ja * D0, q1 = jv0 * ja * D0, q2 = 0.5f * jv0 * jv0 * D0;
+          float uu = 0.0f, uv = 0.0f, vv = 0.0f;
+          for (int j = 1; j < dim; j++) {
+            const int rj = rr + j;
+            const float jaj = s[L.Jaref + rj], jvj = s[L.jv + rj], dj = s[L.efc_D + rj], fj = s[L.efc_pos + rj], DJj = dj * jaj;
+            q0 += 0.5f * jaj * DJj; q1 += jvj * DJj; q2 += 0.5f * jvj * dj * jvj;
+            const float uj = jaj * fj, vj = jvj * fj;
+            uu += uj * uj; uv += uj * vj; vv += vj * vj;
+          }
+          float* e = s + L.ecoef + EC_WORDS * rr;
+          e[0] = q0; e[1] = q1; e[2] = q2; e[3] = ja * mu; e[4] = jv0 * mu;
+          e[5] = uu; e[6] = uv; e[7] = vv; e[8] = D0 / (mu * mu * (1.0f + mu * mu)); e[9] = mu;
+        }
+        WSYNC();
+      }
       float snorm = sqrtf(search_dot);
       float gtol = fmaxf(tolerance * ls_tolerance * snorm * meaninertia * (float)nv, 1e-6f);
       // quad_gauss
@@ -2192,10 +2331,7 @@ __device__ __forceinline__ void solve(const mjw_model_t& m, const mjw_data_t& d,
       float qg0 = gauss;
       auto eval_all = [&](float alpha) {
         Vec3 o = {0.0f, 0.0f, 0.0f};
-        for (int rr = lane; rr < nefc; rr += LPW) {
-          Dr = s[L.efc_D + rr]; jaref = s[L.Jaref + rr]; jv = s[L.jv + rr]; flr = s[L.efc_frictionloss + rr];
-          eval_row(Dr, jaref, jv, flr, rr, ne, nf, alpha, o);
-        }
+        for (int rr = lane; rr < nefc; rr += LPW) eval_row_g(L, s, rr, nefc, ne, nf, alpha, o);
         o.c = wave_sum(o.c); o.g = wave_sum(o.g); o.h = wave_sum(o.h);
         return o;
       };
@@ -2237,10 +2373,9 @@ __device__ __forceinline__ void solve(const mjw_model_t& m, const mjw_data_t& d,
           float mid_alpha = 0.5f * (lo_alpha + hi_alpha);
           Vec3 ln = {0.0f, 0.0f, 0.0f}, hn = {0.0f, 0.0f, 0.0f}, md = {0.0f, 0.0f, 0.0f};
           for (int rr = lane; rr < nefc; rr += LPW) {
-            float D = s[L.efc_D + rr], ja = s[L.Jaref + rr], j = s[L.jv + rr], fl = s[L.efc_frictionloss + rr];
-            eval_row(D, ja, j, fl, rr, ne, nf, lo_next_alpha, ln);
-            eval_row(D, ja, j, fl, rr, ne, nf, hi_next_alpha, hn);
-            eval_row(D, ja, j, fl, rr, ne, nf, mid_alpha, md);
+            eval_row_g(L, s, rr, nefc, ne, nf, lo_next_alpha, ln);
+            eval_row_g(L, s, rr, nefc, ne, nf, hi_next_alpha, hn);
+            eval_row_g(L, s, rr, nefc, ne, nf, mid_alpha, md);
           }
           ln.c = wave_sum(ln.c); ln.g = wave_sum(ln.g); ln.h = wave_sum(ln.h);
           hn.c = wave_sum(hn.c); hn.g = wave_sum(hn.g); hn.h = wave_sum(hn.h);
@@ -2494,6 +2629,23 @@ __device__ __forceinline__ void load_smooth(const mjw_model_t& m, const mjw_data
       si[L.iscratch + 60] = d.ne[wid];
       si[L.iscratch + 61] = d.nf[wid];
       si[L.iscratch + 62] = nefc;
+    }
+    if (L.ecoef >= 0) {
+      // elliptic rows (the position stage ran in an earlier launch): each row's contact extent from the
+      // run of equal efc_id behind it, its cone coefficient from the contact (constraint.py:2151-2195)
+      for (int r = lane; r < nrows; r += LPW) {
+        const long gr = (long)wid * d.njmax + r;
+        const int typ = d.efc_type[gr];
+        si[L.efc_type + r] = typ;
+        if (typ != CNSTR_CONTACT_ELLIPTIC) continue;
+        const int cid = d.efc_id[gr];
+        int r0 = r;
+        while (r0 > 0 && d.efc_type[gr - (r - r0) - 1] == CNSTR_CONTACT_ELLIPTIC && d.efc_id[gr - (r - r0) - 1] == cid) r0--;
+        const float* fr = d.contact_friction + 5L * cid;
+        const int k = r - r0;
+        s[L.efc_pos + r] = k == 0 ? fr[0] * MR(opt_impratio_invsqrt)[0] : fr[k - 1];
+        si[L.efc_margin + r] = r0 | (d.contact_dim[cid] << 16);
+      }
     }
   }
   if ((stages & ST_EULER) && !(stages & ST_SOLVE)) {
@@ -2782,13 +2934,13 @@ __global__ void __launch_bounds__(256) primitive_narrowphase_kernel(const mjw_mo
   const float* gsize = MR(geom_size);
   const float *p1 = gx + 3 * g1, *p2 = gx + 3 * g2, *r1 = gm + 9 * g1, *r2 = gm + 9 * g2;
   const float n1[3] = {r1[2], r1[5], r1[8]}, n2[3] = {r2[2], r2[5], r2[8]};
-  int id = 0;
-  auto write = [&](float dist, const float* pos, const float* frame) {
+  // gid: the candidate point's index within the pair (the corner index for plane-box, collision_primitive.py:
+  // 774-778), whether or not earlier candidates were written
+  auto write = [&](int gid, float dist, const float* pos, const float* frame) {
     const bool active = dist < margin;
     if ((pid0 == -2 || !active) && pid1 == -1) return;
     const int type = ((pid0 >= -1 && active) ? 1 : 0) | (pid1 >= 0 ? 2 : 0);
     const int cid = atomicAdd(d.nacon, 1);
-    const int gid = id++;
     if (cid >= d.naconmax) return;
     d.contact_dist[cid] = dist;
     for (int i = 0; i < 3; i++) d.contact_pos[3L * cid + i] = pos[i];
@@ -2814,7 +2966,7 @@ __global__ void __launch_bounds__(256) primitive_narrowphase_kernel(const mjw_mo
     for (int q = 0; q < 8; q++) {
       float cp[3];
       const float dist = plane_box_corner(q, n1, p1, p2, r2, gsize + 3 * g2, cp);
-      write(dist, cp, frame);
+      write(q, dist, cp, frame);
     }
   } else if (prepass_prim(t1, t2)) {
     float dist[4], pos[4][3], nrm[3] = {n1[0], n1[1], n1[2]};
@@ -2833,11 +2985,11 @@ __global__ void __launch_bounds__(256) primitive_narrowphase_kernel(const mjw_mo
       n = plane_mesh(n1, p1, p2, r2, MR(mesh_vert) + 3 * (long)m.mesh_vertadr[md], m.mesh_vertnum[md], dist, pos);
     }
     make_frame(frame, nrm);
-    for (int q = 0; q < n; q++) write(dist[q], pos[q], frame);
+    for (int q = 0; q < n; q++) write(q, dist[q], pos[q], frame);
   } else {
     Con2 c;
     narrowphase_g<true>(m, gx, gm, wid, g1, g2, margin, c);
-    for (int q = 0; q < c.n; q++) write(c.dist[q], c.pos[q], c.frame[q]);
+    for (int q = 0; q < c.n; q++) write(q, c.dist[q], c.pos[q], c.frame[q]);
   }
 }
 
@@ -2925,6 +3077,17 @@ __global__ void pool_ranges_finish_kernel(const mjw_data_t d) {
   const int k0 = d.ncon_world[2L * w], k1 = d.ncon_world[2L * w + 1];
   d.ncon_world[2L * w] = k1 < 0 ? 0 : k0;
   d.ncon_world[2L * w + 1] = k1 < 0 ? 0 : k1 - k0 + 1;
+}
+
+// host: the ranges above for every world of d (mjw_contact_rows, and sensor_launch for the contact and
+// tactile sensors)
+int pool_ranges_launch(const mjw_data_t* d, hipStream_t s) {
+  if (d->nworld <= 0) return 0;
+  const int nb = (d->nworld + 255) / 256, nk = (d->naconmax + 255) / 256;
+  hipLaunchKernelGGL(pool_ranges_init_kernel, dim3(nb), dim3(256), 0, s, *d);
+  if (nk > 0) hipLaunchKernelGGL(pool_ranges_kernel, dim3(nk), dim3(256), 0, s, *d);
+  hipLaunchKernelGGL(pool_ranges_finish_kernel, dim3(nb), dim3(256), 0, s, *d);
+  return (int)hipGetLastError();
 }
 
 __global__ void __launch_bounds__(64) actuator_map_kernel(const mjw_model_t m, const mjw_data_t d) {
@@ -3150,10 +3313,6 @@ int run(const mjw_model_t* m, const mjw_data_t* d, void* stream, int stages, con
     return !(e && e[0] == '0');
   }();
   const bool order = order_on && full && d->sched && dense_ok(m, d);
-  if (m->opt_cone == CONE_ELLIPTIC && (stages & ST_SOLVE) && !dense_ok(m, d)) {
-    g_err = std::string(name) + ": elliptic cones need the register-resident dense solve (nv <= 32, njmax <= 64)";
-    return -5;
-  }
   if ((stages & ST_POS) && !(stages & ST_POOL)) {
     rc = set_err(reset_counters(d, s, order), name);
     if (rc) return rc;
@@ -3330,13 +3489,7 @@ int mjw_fwd_position(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
 }
 int mjw_contact_rows(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   if (m && d && !m->is_sparse && d->nworld > 0) {
-    hipStream_t s = (hipStream_t)stream;
-    const int nw = d->nworld, nb = (d->nworld + 255) / 256, nk = (d->naconmax + 255) / 256;
-    hipLaunchKernelGGL(mjw::pool_ranges_init_kernel, dim3(nb), dim3(256), 0, s, *d);
-    if (nk > 0) hipLaunchKernelGGL(mjw::pool_ranges_kernel, dim3(nk), dim3(256), 0, s, *d);
-    hipLaunchKernelGGL(mjw::pool_ranges_finish_kernel, dim3(nb), dim3(256), 0, s, *d);
-    (void)nw;
-    const int rc = set_err(hipGetLastError(), "mjw_contact_rows");
+    const int rc = set_err((hipError_t)mjw::pool_ranges_launch(d, (hipStream_t)stream), "mjw_contact_rows");
     if (rc) return rc;
   }
   return run(m, d, stream, mjw::ST_POS | mjw::ST_POOL, "mjw_contact_rows");

@@ -327,6 +327,7 @@ def put_model(mjm, device=None) -> types.Model:
       taxel_vertadr += [int(mjm.mesh_vertadr[mid]) + j for j in range(int(mjm.mesh_vertnum[mid]))]
       taxel_sensorid += [s_] * int(mjm.mesh_vertnum[mid])
   m.nsensortaxel = len(taxel_vertadr)
+  m.nsensorcontact = int(sum(int(mjm.sensor_type[s_]) == types.SensorType.CONTACT for s_ in range(int(getattr(mjm, "nsensor", 0)))))
   m.nsensorcollision = len(sc_pair) // 4
   sc_kinds = [tuple(sorted((int(mjm.geom_type[a]), int(mjm.geom_type[b])))) for a, b in sc_pair.reshape(-1, 4)[:, :2]]
   m.nsensorccd = int(sum(k in _SENSOR_CONVEX or k in _SENSOR_HFIELD for k in sc_kinds))  # records the sensor kernel runs in lockstep
@@ -536,7 +537,7 @@ DERIVED_INT_ARRAYS = {
 }
 DERIVED_SCALARS = ("act_maxnnz", "nbodytrn", "nsitetrn", "nten_spatial", "nxn", "nxn_ccd", "nxn_box", "ccd_epa_iterations", "nlevel", "nlimited", "nlimited_ball", "neq_cw", "nJmom", "ntree", "njrow", "ten_maxnnz", "nmuscle", "sp_nH",
                    "nv_pad", "nmaxcondim", "nmaxpyramid", "sensor_rne_postconstraint", "nsensor_acc", "nflexinc", "nflexcg", "nplane",
-                   "nsensorcollision", "nsensorccd", "nsensortaxel")
+                   "nsensorcollision", "nsensorccd", "nsensortaxel", "nsensorcontact")
 
 
 def derive_model_fields(mjm) -> dict:

@@ -1436,6 +1436,12 @@ class _Compiler:
           m.body_iquat[i] = q if q is not None else [1, 0, 0, 0]
           m.body_inertia[i] = _floats(ia["diaginertia"], 3)
         continue
+      # a heightfield geom's mass and inertia (MuJoCo's compiler prices it like a box from the heightfield
+      # asset) are not reproduced: a moving body with one needs an explicit <inertial> (parity unpinned
+      # otherwise; static bodies never use their inertia)
+      if m.body_weldid[i] != 0 and any(m.geom_bodyid[g] == i and m.geom_type[g] == GeomType.HFIELD for g in range(m.ngeom)):
+        raise NotImplementedError(f"body {i}: a heightfield geom on a moving body needs an explicit <inertial> (its "
+                                  "geom-derived mass / inertia is not built)")
       # massless geoms (e.g. density="0" visual meshes) do not shape the inertial frame
       geoms = [g for g in range(m.ngeom) if m.geom_bodyid[g] == i and m.geom_type[g] != GeomType.PLANE and m.geom_mass_[g] > 0]
       if not geoms:

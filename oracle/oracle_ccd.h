@@ -795,6 +795,21 @@ static int box_face(const real* mat, const real* pos, const real* s, int idx, re
   return 4;
 }
 
+/* test hook (tests/test_multiccd.py): when set, every clipped polygon of more than 4 vertices that
+   polygon_quad searches is appended to the log as (np, the quad it kept, np x 3 coordinates), ORC_POLYLOG_STRIDE
+   reals per record, so that a test can enumerate the quads the greedy search reaches when near-equal areas
+   compare either way.  Single-threaded callers only. */
+#define ORC_POLYLOG_STRIDE (5 + 3 * 2 * CCD_MAXPOLY)
+static real* g_polylog = NULL;
+static int g_polylog_cap = 0, g_polylog_n = 0;
+void orc_polylog(real* buf, int cap) {
+  g_polylog = buf;
+  g_polylog_cap = cap;
+  g_polylog_n = 0;
+}
+int orc_polylog_count(void) { return g_polylog_n; }
+int orc_polylog_stride(void) { return ORC_POLYLOG_STRIDE; }
+
 /* collision_gjk.py:1815-1909 */
 static int polygon_clip(real face1[][3], int nface1, real face2[][3], int nface2, const real* n, const real* dir, real w1[4][3],
                         real w2[4][3]) {
@@ -845,6 +860,13 @@ static int polygon_clip(real face1[][3], int nface1, real face2[][3], int nface2
   if (np > 4) {
     int q[4];
     polygon_quad(q, poly, np);
+    if (g_polylog && g_polylog_n < g_polylog_cap) {
+      real* rec = g_polylog + (long)ORC_POLYLOG_STRIDE * g_polylog_n++;
+      rec[0] = (real)np;
+      for (int i = 0; i < 4; i++) rec[1 + i] = (real)q[i];
+      for (int i = 0; i < np; i++)
+        for (int k = 0; k < 3; k++) rec[5 + 3 * i + k] = poly[i][k];
+    }
     for (int i = 0; i < 4; i++)
       for (int k = 0; k < 3; k++) { w2[i][k] = poly[q[i]][k]; w1[i][k] = w2[i][k] - dir[k]; }
     return 4;

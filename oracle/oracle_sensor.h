@@ -488,10 +488,9 @@ static real tactile_sdf(int type, const real* p, const real* size) {
 /* sensor.py:2085-2250 tactile: for each vertex (taxel) of the sensor's mesh, placed with the sensor
  * geom's frame, the geoms in contact with that geom's weld body (first MJ_MAXCONPAIR = 50 entries of
  * the per-weld list, duplicates once) add pressure depth / max(0.05 - depth, MINVAL) for a negative
- * SDF depth (slip components 0: no tangent frames).  The world's contacts are those with constraint
- * rows, as the device enumerates them (the reference also counts contacts without rows, e.g. in the
- * margin-gap zone).  Other geoms than plane / sphere / box / ellipsoid (mesh ray SDF, SDF plugins) give
- * no pressure here. */
+ * SDF depth (slip components 0: no tangent frames).  Every contact of the world counts, with constraint
+ * rows or not (sensor.py:2097-2118 takes all of nacon: the margin-gap zone, rows cut by njmax).  Other geoms
+ * than plane / sphere / box / ellipsoid (mesh ray SDF, SDF plugins) give no pressure here. */
 static void tactile_sensor(const orc_model* m, orc_data* d, int s) {
   const int mesh = m->sensor_objid[s], geom = m->sensor_refid[s];
   const int nvt = m->mesh_vertnum[mesh];
@@ -500,7 +499,6 @@ static void tactile_sensor(const orc_model* m, orc_data* d, int s) {
   const int pw = m->body_weldid[m->geom_bodyid[geom]];
   int list[50], n = 0, nadd = 0;
   for (int c = 0; c < d->ncon[0]; c++) {
-    if (d->con_efc_address[10 * c] < 0) continue;
     const int g1 = d->con_geom[2 * c], g2 = d->con_geom[2 * c + 1];
     if (g1 < 0 || g2 < 0) continue;
     const int w1 = m->body_weldid[m->geom_bodyid[g1]], w2 = m->body_weldid[m->geom_bodyid[g2]];
@@ -554,8 +552,9 @@ static void contact_sensor(const orc_model* m, orc_data* d, int s) {
   int ids[256];
   real dirs[256], crit[256];
   int nmatch = 0;
+  /* every constraint contact of the world, with rows or not (sensor.py:2313-2316; a contact without rows
+   * has zero force, contact_force_local) */
   for (int c = 0; c < d->ncon[0]; c++) {
-    if (d->con_efc_address[10 * c] < 0) continue;
     const real dir = contact_match(m, d, s, c);
     if (dir == 0) continue;
     const int k = nmatch++;

@@ -248,6 +248,22 @@ class OracleData:
   def fwd_position(self):
     self._call("orc_fwd_position")
 
+  def fwd_position_polygons(self, cap=64):
+    """fwd_position, returning the clipped polygons (> 4 vertices) polygon_quad searched: a list of
+    (kept quad indices, (np, 3) vertices), in the order the narrowphase clipped them."""
+    lib = self.om.lib
+    real = ctypes.c_double if self.om.real_bits == 64 else ctypes.c_float
+    stride = lib.orc_polylog_stride()
+    buf = (real * (stride * cap))()
+    lib.orc_polylog(buf, ctypes.c_int(cap))
+    try:
+      self.fwd_position()
+      n = lib.orc_polylog_count()
+    finally:
+      lib.orc_polylog(None, ctypes.c_int(0))
+    a = np.frombuffer(buf, dtype=np.float64 if self.om.real_bits == 64 else np.float32).reshape(cap, stride)[:n].astype(np.float64)
+    return [(a[i, 1:5].astype(int), a[i, 5:5 + 3 * int(a[i, 0])].reshape(-1, 3)) for i in range(n)]
+
   def fwd_velocity(self):
     self._call("orc_fwd_velocity")
 

@@ -17,6 +17,7 @@ import pytest
 import torch
 
 import golden_kat as gk
+from tests.common import np_
 
 KAT = gk.load()
 
@@ -162,6 +163,25 @@ def test_gpu_primitive_narrowphase_matches_fused_collision():
   assert all(int(t) == 1 for t in d.contact.type.cpu().numpy()[: int(d.nacon[0])])
   assert np.all(d.contact.efc_address.cpu().numpy()[: int(d.nacon[0])] == -1)
   assert len(staged) == len(fused), (len(staged), len(fused))
+  # geomcollisionid is the candidate's index within its pair: for plane-box the box corner (bit 0 / 1 / 2 =
+  # the +x / +y / +z half of the box frame, collision_primitive.py:774-778), recovered from the contact point
+  nst = int(d.nacon[0])
+  gcid = d.contact.geomcollisionid.cpu().numpy()[:nst]
+  cg, cw = d.contact.geom.cpu().numpy()[:nst], d.contact.worldid.cpu().numpy()[:nst]
+  cpos, cdist = np_(d.contact.pos)[:nst], np_(d.contact.dist)[:nst]
+  gxp, gxm = np_(d.geom_xpos), np_(d.geom_xmat)
+  nbox = 0
+  for k in range(nst):
+    g1, g2 = int(cg[k, 0]), int(cg[k, 1])
+    if (int(mjm.geom_type[g1]), int(mjm.geom_type[g2])) != (0, 6):
+      continue
+    w = int(cw[k])
+    R = gxm[w, g2].reshape(3, 3)
+    nrm = gxm[w, g1].reshape(3, 3)[:, 2]
+    loc = R.T @ (cpos[k] + 0.5 * nrm * cdist[k] - gxp[w, g2])
+    assert int(gcid[k]) == int(loc[0] > 0) | int(loc[1] > 0) << 1 | int(loc[2] > 0) << 2, (k, gcid[k], loc)
+    nbox += 1
+  assert nbox >= 4 * nworld
   for a, b in zip(staged, fused):
     assert a[:4] == b[:4], (a[:4], b[:4])
     np.testing.assert_allclose(a[4], b[4], rtol=0, atol=1e-6)

@@ -120,8 +120,30 @@ def test_oracle_contact_sensor_fp32_tracks_fp64():
   np.testing.assert_allclose(b, a, rtol=2e-3, atol=2e-3 * np.abs(a).max())
 
 
+def test_oracle_contact_sensor_counts_contacts_without_rows():
+  """sensor.py:2313-2316 keeps every CONSTRAINT contact, with rows or not: with njmax too small for the
+  contact rows (4 box corners x 4 pyramid rows + the other bodies' contacts > 10), the found counts do not
+  change, and a contact whose rows were cut reports zero force."""
+  mjm = _load()
+  od0 = _settled(mjm)
+  qpos, warm = od0.qpos[:1].copy(), od0.qacc[:1].copy()
+  _, od = oracle_from_state(mjm, qpos, np.zeros((1, mjm.nv)), np.zeros((1, mjm.nu)), njmax=10, nconmax=32, qacc_warmstart=warm)
+  od.forward()
+  assert int(od.nefc[0, 0]) > 10  # rows were requested past njmax and dropped
+  ncon = int(od.ncon[0, 0])
+  adr0 = od.con_efc_address[0].reshape(-1, 10)[:ncon, 0]
+  assert (adr0 < 0).any()
+  sd, sd0 = od.sensordata[0], od0.sensordata[0]
+  for name in ("box_found", "all"):
+    a, _ = _adr(mjm, name)
+    assert sd[a] == sd0[a] == (4 if name == "box_found" else ncon)
+  a, dim = _adr(mjm, "sub")
+  assert sd[a] == sd0[a]
+
+
 @pytest.mark.gpu
-def test_gpu_contact_sensor_matches_oracle():
+@pytest.mark.parametrize("njmax", [128, 10])
+def test_gpu_contact_sensor_matches_oracle(njmax):
   import torch
 
   import mujoco_warp_amd as mjw
@@ -135,8 +157,9 @@ def test_gpu_contact_sensor_matches_oracle():
   qvel = np.zeros((nworld, mjm.nv))
   ctrl = np.zeros((nworld, mjm.nu))
   warm = np.tile(od0.qacc[0], (nworld, 1))
-  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=128, nconmax=32, qacc_warmstart=warm)
-  _, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=128, nconmax=32, qacc_warmstart=warm)
+  # njmax 10: the rows of most contacts are dropped, the contacts stay in the pool (found counts them)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=32, qacc_warmstart=warm)
+  _, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=njmax, nconmax=32, qacc_warmstart=warm)
   mjw.forward(m, d)
   od.forward()
   torch.cuda.synchronize()

@@ -176,26 +176,28 @@ def test_contact_force_elliptic_rows_are_the_force(tmp_path):
 
 
 # ---- GPU ------------------------------------------------------------------------------------------
-def _gpu_pair(solver, nworld, seed):
+def _gpu_pair(solver, nworld, seed, njmax=64):
   mjm = _elliptic_humanoid(solver)
   qpos, qvel, ctrl = random_states(mjm, nworld, seed=seed)
-  m, d = gpu_from_state(mjm, qpos, qvel, ctrl)
-  om, od = oracle_from_state(mjm, qpos, qvel, ctrl)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl, njmax=njmax)
+  om, od = oracle_from_state(mjm, qpos, qvel, ctrl, njmax=njmax)
   return mjm, m, d, od
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("njmax", [64, 128])
 @pytest.mark.parametrize("solver", ["CG", "NEWTON"])
-def test_gpu_elliptic_rows_and_solve(solver):
+def test_gpu_elliptic_rows_and_solve(solver, njmax):
   """Elliptic rows (same count / order / type, J and scalars) and the device solve: fp64 cost within the
   reference's 1.025x of the oracle optimum (solver_test.py:317); Newton qacc at the reference's
-  solver bar (solver_test.py:32-38: 5e-3 * 20)."""
+  solver bar (solver_test.py:32-38: 5e-3 * 20).  njmax 64: the register-resident dense solve; njmax 128:
+  the generic LDS solver (rows past one wavefront, the cone at the first row of each contact)."""
   import torch
 
   import mujoco_warp_amd as mjw
 
   nworld = 32
-  mjm, m, d, od = _gpu_pair(solver, nworld, seed=80)
+  mjm, m, d, od = _gpu_pair(solver, nworld, seed=80, njmax=njmax)
   mjw.forward(m, d)
   od.forward()
   torch.cuda.synchronize()
@@ -278,13 +280,14 @@ def test_gpu_elliptic_step_rollout_and_sliding_box():
 
   import mujoco_warp_amd as mjw
 
-  mjm, m, d, od = _gpu_pair("NEWTON", 16, seed=81)
-  for _ in range(5):
-    mjw.step(m, d)
-    od.step()
-  torch.cuda.synchronize()
-  e = np.abs(np_(d.qpos) - od.qpos).max(axis=1) / np.abs(od.qpos).max(axis=1)
-  assert e.max() < 1e-3, e.max()
+  for njmax in (64, 128):  # register-resident and generic solves
+    mjm, m, d, od = _gpu_pair("NEWTON", 16, seed=81, njmax=njmax)
+    for _ in range(5):
+      mjw.step(m, d)
+      od.step()
+    torch.cuda.synchronize()
+    e = np.abs(np_(d.qpos) - od.qpos).max(axis=1) / np.abs(od.qpos).max(axis=1)
+    assert e.max() < 1e-3, (njmax, e.max())
 
   mu, g = 0.4, 9.81
   bm = _model(type="box", size="0.3 0.3 0.01", z=0.0099, mu=mu, condim=3)

@@ -47,23 +47,28 @@ def test_compile_hfield_asset_and_geom():
 
 
 def test_compile_hfield_on_moving_body():
-  """Heightfields may sit on moving bodies (the collision routines take the geom's frame); like planes they
-  contribute no mass, so the body's mass comes from its other geoms.  (Image / binary heightfield files:
-  tests/test_hfield_file.py.)"""
+  """Heightfields may sit on moving bodies (the collision routines take the geom's frame).  MuJoCo's compiler
+  gives a heightfield geom a box-like mass and inertia from its asset, which this compiler does not
+  reproduce, so a moving body with a heightfield needs an explicit <inertial> (without one the model is
+  refused).  (Image / binary heightfield files: tests/test_hfield_file.py.)"""
   mjm = _load(MOVING.format(elev=" ".join(["0"] * 42)))
   b = mjm.body_names.index("terrain")
   np.testing.assert_allclose(mjm.body_mass[b], 5.0)
+  np.testing.assert_allclose(mjm.body_ipos[b], [0, 0, -0.3])
   assert int(mjm.geom_type[mjm.body_geomadr[b]]) == 1
+  with pytest.raises(NotImplementedError, match="explicit <inertial>"):
+    _load(MOVING.format(elev=" ".join(["0"] * 42)).replace(INERTIAL, ""))
 
 
-# the bumpy heightfield of BUMPY on a free body of its own (plus a massive non-colliding box), a sphere on
-# a second free body
+# the bumpy heightfield of BUMPY on a free body of its own (plus a massive non-colliding box, whose mass and
+# inertia the explicit <inertial> restates), a sphere on a second free body
+INERTIAL = '<inertial pos="0 0 -.3" mass="5" diaginertia="0.0173333 0.0173333 0.0333333"/>'
 MOVING = """<mujoco><option gravity="0 0 -9.81"/><asset>
 <hfield name="h" nrow="6" ncol="7" size=".6 .5 .15 .1" elevation="{elev}"/></asset>
 <worldbody>
-<body name="terrain" pos=".05 -.03 0" euler="0 0 20"><freejoint/><geom type="hfield" hfield="h"/>
+<body name="terrain" pos=".05 -.03 0" euler="0 0 20"><freejoint/>{inertial}<geom type="hfield" hfield="h"/>
   <geom type="box" size=".1 .1 .02" pos="0 0 -.3" contype="0" conaffinity="0" mass="5"/></body>
-<body pos="0 0 .2"><freejoint/><geom type="sphere" size=".12"/></body></worldbody></mujoco>"""
+<body pos="0 0 .2"><freejoint/><geom type="sphere" size=".12"/></body></worldbody></mujoco>""".replace("{inertial}", INERTIAL)
 
 
 def _qmul(a, b):

@@ -121,8 +121,6 @@ def test_gpu_lifts_pot(cone, njmax):
   import mujoco_warp_amd as mjw
   from mujoco_warp_amd import mjcf
 
-  if cone == "ELLIPTIC" and njmax > 64:
-    pytest.skip("elliptic cones on dense models run in the register-resident solve only (njmax <= 64, DESIGN.md 3.2)")
   mjm = _model(cone)
   key = mjw.find_keys(mjm, "lift_pot0")[0]
   traj = mjw.make_trajectory(mjm, mjw.find_keys(mjm, "lift_pot"))

@@ -19,19 +19,19 @@ a = bench.parse()
 import mujoco_warp_amd as mjw
 s = a.solver or {1: 'CG', 2: 'NEWTON'}[int(mjw.load_model(bench.MODELS['$M']['path']).opt.solver)]
 print(a.nworld, s)") || exit 1
-# the stats pass runs the bench's own step window (its defaults: 20 warm-up + 1000 timed steps, 100 for
-# the flex configs) followed by its trace pass, so that rocprof's average per kernel covers the states of
-# the bench line's HIP events (the humanoid's first 60 steps -- the fall from the squat key -- cost up to
-# 2x the long-run average in the dense kernel); the counter passes count 200 warm-up steps, a 20-step
-# timed window and bench.py's trace pass, which replays that window from the saved state: the summary
-# averages exactly the trace pass (tail = its steps), whose nefc / ncon the pass's bench line reports, so
-# bench.py prices the same window's algorithmic bytes
-steps_stats=1000; warm_stats=20; steps_pmc=20; warm_pmc=200
-case $M in aloha_cloth|cloth) steps_stats=100; steps_pmc=5; warm_pmc=20;; esac
-common="--model $M $sarg --cpu-baseline 0 --graph 0"
+# The counter passes (FETCH_SIZE, WRITE_SIZE, SQ) run the driver's own command -- `bench.py --steps 20
+# --warmup 5`, the timed region replayed as a hipGraph -- followed by bench.py's trace pass, which replays
+# that window eagerly from the state saved at its start: the summary averages exactly the trace pass (tail =
+# its steps), whose nefc / ncon the pass's bench line reports, so bench.py prices the driver window's
+# algorithmic bytes (round 6; round 5 counted a later, contact-richer window after 200 eager warm-up steps).
+# The stats pass runs the same window (the kernel-time averages of the line's `achieved`).  The flex configs
+# count 5 steps after 20 (their steps take ~20 ms).
+steps_stats=20; warm_stats=5; steps_pmc=20; warm_pmc=5
+case $M in aloha_cloth|cloth) steps_stats=20; warm_stats=20; steps_pmc=5; warm_pmc=20;; esac
+common="--model $M $sarg --cpu-baseline 0"
 d=gpurun_out/prof_$tag
 rm -rf $d && mkdir -p $d
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $d/stats -o run -- python3 bench.py $common --steps $steps_stats --warmup $warm_stats > $d/stats.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $d/stats -o run -- python3 bench.py $common --steps $steps_stats --trace-steps $steps_stats --warmup $warm_stats > $d/stats.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/fetch -o run -- python3 bench.py $common --steps $steps_pmc --trace-steps $steps_pmc --warmup $warm_pmc > $d/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/write -o run -- python3 bench.py $common --steps $steps_pmc --trace-steps $steps_pmc --warmup $warm_pmc > $d/write.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $d/sq -o run -- python3 bench.py $common --steps $steps_pmc --trace-steps $steps_pmc --warmup $warm_pmc > $d/sq.log 2>&1 || exit $?
