@@ -14,6 +14,8 @@
  *   mjw_fwd_acceleration  <- forward.fwd_acceleration     forward.py:949-969
  *   mjw_solve             <- solver.solve                 solver.py:3296-3343
  *   mjw_euler             <- forward.euler                forward.py:326-354
+ *   mjw_stage             <- smooth.kinematics / com_pos / camlight / tendon / crb / transmission /
+ *                            com_vel / rne, passive.passive, constraint.make_constraint (one stage, below)
  *   mjw_sensor            <- sensor.sensor_pos/_vel/_acc  sensor.py:761,1377,2447
  *   mjw_ctrl_noise        <- benchmark.ctrl_noise         _src/benchmark.py:41-83
  *
@@ -253,6 +255,21 @@ int mjw_fwd_actuation(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_fwd_acceleration(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_solve(const mjw_model_t* m, const mjw_data_t* d, void* stream);
 int mjw_euler(const mjw_model_t* m, const mjw_data_t* d, void* stream);
+/* One stage of every world, its inputs the Data fields the earlier stages wrote and its outputs written
+ * back (dense-path models; round 6).  `stage` (MJW_STAGE_*) names the reference function it replaces:
+ *   1 kinematics          smooth.py:357-415   (qpos, mocap -> body / joint / geom / site frames)
+ *   2 com_pos             smooth.py:601-632   (frames -> subtree_com, cinert, cdof)
+ *   3 camlight            smooth.py:635-803   (frames, subtree_com -> camera / light frames)
+ *   4 tendon              smooth.py:3627-3700 (qpos, frames -> ten_length, ten_J)
+ *   5 crb                 smooth.py:888-912   (cinert, cdof -> crb, qM incl. armature)
+ *   6 make_constraint     constraint.py:2718-2779 (contacts in d.contact + frames -> efc rows)
+ *   7 transmission        smooth.py:2605-2700 (actuator_length / moment; not for BODY transmissions)
+ *   8 com_vel             smooth.py:1935-2038 (+ actuator_velocity, forward.py:540-562)
+ *   9 passive             passive.py:535-563
+ *  10 rne                 smooth.py:1276-1300 (flg_acc = False; + tendon_bias, :1878-1932) */
+enum { MJW_STAGE_KINEMATICS = 1, MJW_STAGE_COM_POS = 2, MJW_STAGE_CAMLIGHT = 3, MJW_STAGE_TENDON = 4, MJW_STAGE_CRB = 5,
+       MJW_STAGE_MAKE_CONSTRAINT = 6, MJW_STAGE_TRANSMISSION = 7, MJW_STAGE_COM_VEL = 8, MJW_STAGE_PASSIVE = 9, MJW_STAGE_RNE = 10 };
+int mjw_stage(const mjw_model_t* m, const mjw_data_t* d, int stage, void* stream);
 /* sensors of the stages in `stages` (bit 0: sensor_pos, sensor.py:761; bit 1: sensor_vel, :1377;
  * bit 2: sensor_acc with rne_postconstraint, :2447) from the Data of the current step; mjw_step /
  * mjw_forward run all three themselves, the stage entry points above run none */

@@ -51,7 +51,9 @@ constexpr int SP_LDS_ITEMS_MAX = 48 * 1024;  // per-item contact counts of the c
 
 // opt-in phase timers of this path (build with -DMJW_PROFILE; tools/sparse_prof.py): s_memtime
 // deltas summed over waves, read back with mjw_prof_read_sparse
-enum : int { SPH_KIN = 0, SPH_FLEX, SPH_CRB, SPH_COLL, SPH_CON, SPH_VEL, SPH_ACT, SPH_ACC, SPH_SINIT, SPH_SLS, SPH_SUPD, SPH_SCG, SPH_N };
+// SPH_NPASS / SPH_NITER (counts, not cycles): the row passes of the line searches (the jv + alpha = 0
+// pass, the Newton-step pass and one per bracketing iteration) and the CG iterations, summed over worlds
+enum : int { SPH_KIN = 0, SPH_FLEX, SPH_CRB, SPH_COLL, SPH_CON, SPH_VEL, SPH_ACT, SPH_ACC, SPH_SINIT, SPH_SLS, SPH_SUPD, SPH_SCG, SPH_NPASS, SPH_NITER, SPH_N };
 #ifdef MJW_PROFILE
 static __device__ unsigned long long g_sprof[SPH_N];
 #define SPROF_T0() unsigned long long _spt = __builtin_amdgcn_s_memtime()
@@ -61,9 +63,14 @@ static __device__ unsigned long long g_sprof[SPH_N];
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_sprof[ph], _nt - _spt);            \
     _spt = _nt;                                                                  \
   } while (0)
+#define SPROF_COUNT(ph, n)                                  \
+  do {                                                      \
+    if (threadIdx.x == 0) atomicAdd(&g_sprof[ph], (unsigned long long)(n)); \
+  } while (0)
 #else
 #define SPROF_T0() (void)0
 #define SPROF_MARK(ph) (void)0
+#define SPROF_COUNT(ph, n) (void)0
 #endif
 constexpr int NWAVE = BLK / 64;
 enum : int { EQ_FLEX = 4 };
@@ -2964,6 +2971,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
   } else {
   const float lo_alpha_in = -safe_div(p0[1], p0[2]);
   float lo_in[3] = {0, 0, 0};
+  SPROF_COUNT(SPH_NPASS, 2);  // the jv + alpha = 0 pass above and this one
   eval_rows<1, ELL>(c, &lo_alpha_in, lo_in);
   block_sum_db<3>(lo_in, sm, c.rphase);
   {
@@ -2989,6 +2997,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
       const float mid_alpha = 0.5f * (lo_alpha + hi_alpha);
       float v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       const float al[3] = {lo_next_alpha, hi_next_alpha, mid_alpha};
+      SPROF_COUNT(SPH_NPASS, 1);
       eval_rows<3, ELL>(c, al, v9);
       block_sum_db<9>(v9, sm, c.rphase);
       float lo_next[3], hi_next[3], mid[3], g[3];
@@ -3248,6 +3257,7 @@ __global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_ker
       c.search_dot = block_sum1_db(s2, sm, c.rphase);
       niter++;
       SPROF_MARK(SPH_SCG);
+      SPROF_COUNT(SPH_NITER, 1);
       const float improvement = (c.prev_cost - c.cost) * scale;
       const float gradient = sqrtf(c.grad_dot) * scale;
       if (improvement < tol || gradient < tol || niter == m.opt_iterations) break;

@@ -1680,8 +1680,9 @@ __device__ __forceinline__ void transmission(const mjw_model_t& m, const mjw_dat
 // velocity (forward.py:592-613): actuator velocity, com_vel, passive, rne
 // -------------------------------------------------------------------------------------------
 // POS_LDS: the position stage ran in this launch, so the body / geom frames are in LDS (else they are read
-// from the Data)
-template <bool TEN, bool POS_LDS>
+// from the Data).  PARTS (the stage launches, sub_kernel): bit 0 actuator velocity + com_vel, bit 1 passive,
+// bit 2 tendon bias + rne; the step runs all three
+template <bool TEN, bool POS_LDS, int PARTS = 7>
 __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
   const int wid = w.wid, lane = w.lane;
   float* s = w.s;
@@ -1689,6 +1690,13 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
   const float* qvel = s + L.qvel;
   const float* qpos = s + L.qpos;
   const int nv = m.nv;
+  float* cvel = s + L.cvel;
+  float* cdof_dot = s + L.cdof_dot;
+  float* cacc = s + L.cacc;
+  const float* cd = s + L.cdof;
+  float* spring = s + L.vec;
+  float* damper = s + L.vec + nv;
+  if constexpr ((PARTS & 1) != 0) {
   // forward.py:540-562
   for (int a = lane; a < m.nu; a += LPW) {
     float v = 0.0f;
@@ -1699,10 +1707,6 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
   // smooth.py:1935-2038 com_vel.  Inside a body the joint loop adds cdof*qvel joint by joint
   // and takes cdof_dot = cvel_partial x cdof; the partial sum is split into the parent's cvel
   // (level pass, LDS only) and the body-local part (one pass over dofs in parallel).
-  float* cvel = s + L.cvel;
-  float* cdof_dot = s + L.cdof_dot;
-  float* cacc = s + L.cacc;
-  const float* cd = s + L.cdof;
   float* dv = s + L.cfrc;  // per-body local increments (cfrc is produced later)
   for (int b = lane; b < m.nbody; b += LPW) {
     float acc[6] = {0, 0, 0, 0, 0, 0};
@@ -1741,11 +1745,11 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
   WSYNC();
   for (int e = lane; e < m.nbody * 6; e += LPW) d.cvel[(long)wid * m.nbody * 6 + e] = cvel[e];
   for (int e = lane; e < nv * 6; e += LPW) d.cdof_dot[(long)wid * nv * 6 + e] = cdof_dot[e];
+  }
+  if constexpr ((PARTS & 2) != 0) {
   // passive.py:70-179, 535-563
   const int dsbl_spring = m.opt_disableflags & DSBL_SPRING, dsbl_damper = m.opt_disableflags & DSBL_DAMPER;
   float* qfrc_passive = s + L.qfrc_passive;
-  float* spring = s + L.vec;
-  float* damper = s + L.vec + nv;
   for (int i = lane; i < nv; i += LPW) { spring[i] = 0.0f; damper[i] = 0.0f; }
   WSYNC();
   if (!(dsbl_spring && dsbl_damper)) {
@@ -1842,6 +1846,8 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
     d.qfrc_passive[gi] = p;
     if (TEN) spring[i] = gcomp;  // kept for the actuation stage of this launch (L.vec is free until the solver)
   }
+  }
+  if constexpr ((PARTS & 4) != 0) {
   // smooth.py:1878-1932 tendon_bias: armature J (Jdot qvel) of the spatial tendons, kept in damper[] (free
   // after the passive forces) until qfrc_bias is written; needs cvel before rne reuses its slot
   const bool ten_bias = TEN && m.nten_spatial;
@@ -1909,6 +1915,7 @@ __device__ __forceinline__ void fwd_velocity(const mjw_model_t& m, const mjw_dat
     d.qfrc_bias[(long)wid * nv + i] = v;
   }
   WSYNC();
+  }
 }
 
 // forward.py:616-927 (actuator force, qfrc_actuator); VEL_LDS: the velocity stage ran in this launch and
@@ -2760,6 +2767,79 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) st
 }
 
 // -------------------------------------------------------------------------------------------
+// stage launches (the reference's finer stage functions, mujoco_warp/__init__.py:26-112): one stage of one
+// world per wave, its inputs the Data fields the earlier stages wrote (an edit a caller made to them is what
+// the stage reads, as in the reference), its outputs written to the Data.  Dense-path models only.
+// -------------------------------------------------------------------------------------------
+// the position-stage LDS state (frames, com / inertia, cdof, crb, qM) of world w.wid from the Data
+__device__ __forceinline__ void load_pos_fields(const mjw_model_t& m, const mjw_data_t& d, const Lay& L, WS& w) {
+  const int wid = w.wid, lane = w.lane;
+  float* s = w.s;
+  const long nb = m.nbody, ng = m.ngeom, nj = m.njnt, nv = m.nv;
+  auto cp = [&](int off, const float* src, long n) {
+    for (long e = lane; e < n; e += LPW) s[off + e] = src[e];
+  };
+  cp(L.xpos, d.xpos + wid * nb * 3, nb * 3);
+  cp(L.xquat, d.xquat + wid * nb * 4, nb * 4);
+  cp(L.xmat, d.xmat + wid * nb * 9, nb * 9);
+  cp(L.xipos, d.xipos + wid * nb * 3, nb * 3);
+  cp(L.ximat, d.ximat + wid * nb * 9, nb * 9);
+  cp(L.xanchor, d.xanchor + wid * nj * 3, nj * 3);
+  cp(L.xaxis, d.xaxis + wid * nj * 3, nj * 3);
+  cp(L.gxpos, d.geom_xpos + wid * ng * 3, ng * 3);
+  cp(L.gxmat, d.geom_xmat + wid * ng * 9, ng * 9);
+  cp(L.subtree_com, d.subtree_com + wid * nb * 3, nb * 3);
+  cp(L.cinert, d.cinert + wid * nb * 10, nb * 10);
+  cp(L.crb, d.crb + wid * nb * 10, nb * 10);
+  cp(L.cdof, d.cdof + wid * nv * 6, nv * 6);
+  const int nvs = L.nvs, np = m.nv_pad;
+  for (long e = lane; e < nv * nvs; e += LPW) {
+    const int r = (int)(e / nvs), c = (int)(e - (long)r * nvs);
+    s[L.qM + e] = c < nv ? d.qM[(long)wid * np * np + r * np + c] : 0.0f;
+  }
+}
+
+// SUB_*: the stage a sub_kernel launch runs (include/mjw_amd.h MJW_STAGE_*)
+enum : int { SUB_KINEMATICS = 1, SUB_COM_POS = 2, SUB_CAMLIGHT = 3, SUB_TENDON = 4, SUB_CRB = 5, SUB_MAKE_CONSTRAINT = 6,
+             SUB_TRANSMISSION = 7, SUB_COM_VEL = 8, SUB_PASSIVE = 9, SUB_RNE = 10 };
+template <int SUB>
+__global__ void __launch_bounds__(64) sub_kernel(const mjw_model_t m, const mjw_data_t d, const Lay L, int w0) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  WS w;
+  w.s = smem;
+  w.si = reinterpret_cast<int*>(smem);
+  w.wid = w0 + (int)blockIdx.x;
+  w.lane = lane_id();
+  if (w.wid >= d.nworld) return;
+  load_state(m, d, L, w);
+  if constexpr (SUB != SUB_KINEMATICS) load_pos_fields(m, d, L, w);
+  if constexpr (SUB >= SUB_COM_VEL) {
+    // the velocity stage's inputs beyond the frames: the actuator moment rows (com_vel's actuator velocity)
+    // and com_vel's outputs for passive / rne
+    load_smooth(m, d, L, w, ST_VEL);
+    const long nb = m.nbody, nv = m.nv;
+    for (long e = w.lane; e < nb * 6; e += LPW) w.s[L.cvel + e] = d.cvel[w.wid * nb * 6 + e];
+    for (long e = w.lane; e < nv * 6; e += LPW) w.s[L.cdof_dot + e] = d.cdof_dot[w.wid * nv * 6 + e];
+  }
+  WSYNC();
+  if constexpr (SUB == SUB_KINEMATICS) kinematics(m, d, L, w);
+  if constexpr (SUB == SUB_COM_POS) com_pos(m, d, L, w);
+  if constexpr (SUB == SUB_CAMLIGHT) camlight(m, d, L, w);
+  if constexpr (SUB == SUB_TENDON) {
+    if (m.ntendon) {
+      const TenFrames f{d.site_xpos + (long)w.wid * m.nsite * 3, w.s + L.gxpos, w.s + L.gxmat, w.s + L.subtree_com, w.s + L.cdof};
+      tendon_pos(m, d, w.s + L.qpos, f, w.wid, w.lane);
+    }
+  }
+  if constexpr (SUB == SUB_CRB) crb_qM<true>(m, d, L, w);
+  if constexpr (SUB == SUB_MAKE_CONSTRAINT) collision_and_constraints<true, true, true>(m, d, L, w);
+  if constexpr (SUB == SUB_TRANSMISSION) transmission<true>(m, d, L, w);
+  if constexpr (SUB == SUB_COM_VEL) fwd_velocity<true, true, 1>(m, d, L, w);
+  if constexpr (SUB == SUB_PASSIVE) fwd_velocity<true, true, 2>(m, d, L, w);
+  if constexpr (SUB == SUB_RNE) fwd_velocity<true, true, 4>(m, d, L, w);
+}
+
+// -------------------------------------------------------------------------------------------
 // collision pre-pass: one wave per world recomputes the geom frames (the forward kernel's own
 // kinematics()) and, for the pairs with a pre-pass slot (nxn_ccdid >= 0), applies the broadphase
 // filter and writes each survivor's contact record to d.ccd_out, which the forward kernel's
@@ -3481,6 +3561,47 @@ const char* mjw_kernel_name(int id) {
   }
   return "unknown";
 }
+// one stage of every world (sub_kernel); the stages the step fuses, launched on their own for the reference's
+// stage functions.  BODY transmissions accumulate over the position stage's contacts, so the transmission
+// stage of a model with them is the caller's full position launch (stages.py).
+int mjw_stage(const mjw_model_t* m, const mjw_data_t* d, int stage, void* stream) {
+  using namespace mjw;
+  if (!m || !d) { g_err = "mjw_stage: null model/data"; return -1; }
+  if (m->is_sparse || m->nv > 64 || m->nbody > 4096) { g_err = "mjw_stage: dense-path models only"; return -2; }
+  if (stage == SUB_TRANSMISSION && m->nbodytrn) { g_err = "mjw_stage: BODY transmissions need the position launch"; return -4; }
+  if (d->nworld <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const Lay L = make_layout(*m, d->njmax, false);
+  const size_t lds = (size_t)L.total * 4;
+  if (lds > 160 * 1024) { g_err = "mjw_stage: per-world LDS working set exceeds 160 KiB"; return -3; }
+  if (stage == SUB_MAKE_CONSTRAINT) {
+    const int rc = set_err((hipError_t)pool_ranges_launch(d, s), "mjw_stage");
+    if (rc) return rc;
+  }
+#define MJW_SUB_CASE(K)                                                                                                   \
+  case K: {                                                                                                                \
+    static std::once_flag once;                                                                                            \
+    std::call_once(once, [] { (void)hipFuncSetAttribute((const void*)sub_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); }); \
+    hipLaunchKernelGGL(sub_kernel<K>, dim3(d->nworld), dim3(64), lds, s, *m, *d, L, 0);                                    \
+    break;                                                                                                                 \
+  }
+  switch (stage) {
+    MJW_SUB_CASE(SUB_KINEMATICS)
+    MJW_SUB_CASE(SUB_COM_POS)
+    MJW_SUB_CASE(SUB_CAMLIGHT)
+    MJW_SUB_CASE(SUB_TENDON)
+    MJW_SUB_CASE(SUB_CRB)
+    MJW_SUB_CASE(SUB_MAKE_CONSTRAINT)
+    MJW_SUB_CASE(SUB_TRANSMISSION)
+    MJW_SUB_CASE(SUB_COM_VEL)
+    MJW_SUB_CASE(SUB_PASSIVE)
+    MJW_SUB_CASE(SUB_RNE)
+    default: g_err = "mjw_stage: unknown stage id"; return -4;
+  }
+#undef MJW_SUB_CASE
+  return set_err(hipGetLastError(), "mjw_stage");
+}
+
 int mjw_forward(const mjw_model_t* m, const mjw_data_t* d, void* stream) {
   return run(m, d, stream, mjw::ST_POS | mjw::ST_VEL | mjw::ST_ACT | mjw::ST_ACC | mjw::ST_SOLVE, "mjw_forward");
 }

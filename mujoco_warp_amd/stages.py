@@ -1,14 +1,18 @@
-"""The reference's finer-grained stage and support functions, on this build's fused launches.
+"""The reference's finer-grained stage and support functions.
 
 `mujoco_warp` exposes every pipeline stage as its own function (mujoco_warp/__init__.py:26-112:
-`kinematics`, `com_pos`, `crb`, `collision`, `make_constraint`, `rne`, ...).  Here a stage group runs as
-one HIP launch, so each of these functions runs the launch that contains it:
+`kinematics`, `com_pos`, `crb`, `collision`, `make_constraint`, `rne`, ...).  The step fuses them into
+one launch per stage group; on their own they run as follows:
 
-* position stage (`mjw_fwd_position`): kinematics, com_pos, camlight, flex, tendon, crb, collision,
-  make_constraint, transmission -- each computes its reference outputs from `qpos` / `mocap_*` (and the
-  stage's other outputs along with them; an input the reference would read from an earlier stage's output,
-  e.g. a hand-edited `d.xipos` before `com_pos`, is recomputed from `qpos`, not taken from `d`);
-* velocity stage (`mjw_fwd_velocity`): com_vel, passive, rne (flg_acc = False);
+* dense-path models (round 6): `kinematics`, `com_pos`, `camlight`, `tendon`, `crb`, `make_constraint`,
+  `transmission`, `com_vel`, `passive` and `rne` each launch that one stage (`mjw_stage`, one wave per
+  world): its inputs are the Data fields the earlier stages wrote -- a caller's edit of e.g. `d.xipos`
+  before `com_pos` is what `com_pos` reads, as in the reference -- and only its own outputs are written;
+* `collision` and `flex`, and every stage of sparse / flex models (the workgroup-per-world pipeline):
+  the launch that contains the stage (`mjw_fwd_position` / `mjw_fwd_velocity`), which recomputes the
+  stage's inputs from `qpos` / `qvel` and writes the group's other outputs along with it; so does
+  `transmission` for models with BODY (adhesion) transmissions, which accumulate over the collision's
+  contacts;
 * `factor_m`: the acceleration stage launch, whose dense kernel factors qM into qLD
   (it also refreshes qfrc_smooth / qacc_smooth from the current force inputs);
 * `rne_postconstraint`: the sensor kernel's acceleration stage (cacc, cfrc_int, cfrc_ext).
@@ -31,39 +35,64 @@ from . import types
 from .types import Data, DisableBit, JointType, Model
 
 
-# -- stage-group aliases --------------------------------------------------------------------------
+# -- stages ---------------------------------------------------------------------------------------
 def _position(m: Model, d: Data):
   _call("mjw_fwd_position", m, d)
 
 
+# include/mjw_amd.h MJW_STAGE_*
+STAGE_IDS = {"kinematics": 1, "com_pos": 2, "camlight": 3, "tendon": 4, "crb": 5, "make_constraint": 6, "transmission": 7,
+             "com_vel": 8, "passive": 9, "rne": 10}
+
+
+def _stage(name: str, m: Model, d: Data) -> bool:
+  """Launch one stage (mjw_stage) on a dense-path model; False when the model needs the stage group's
+  launch instead (sparse / flex models, BODY transmissions)."""
+  if m.is_sparse or (name == "transmission" and int(m.nbodytrn) > 0):
+    return False
+  from . import _lib
+  from .forward import _stream
+  from .io import cdata, cmodel
+
+  L = _lib.lib()
+  _lib.check(L.mjw_stage(cmodel(m), cdata(d), STAGE_IDS[name], _stream(d)), f"mjw_stage({name})")
+  return True
+
+
 def kinematics(m: Model, d: Data):
-  """Forward kinematics (smooth.py:357-415): the position-stage launch."""
-  _position(m, d)
+  """Forward kinematics (smooth.py:357-415): body, joint, geom and site frames from qpos / mocap."""
+  if not _stage("kinematics", m, d):
+    _position(m, d)
 
 
 def com_pos(m: Model, d: Data):
-  """subtree_com, cinert, cdof (smooth.py:463-632): the position-stage launch."""
-  _position(m, d)
+  """subtree_com, cinert, cdof (smooth.py:601-632) from the frames in d."""
+  if not _stage("com_pos", m, d):
+    _position(m, d)
 
 
 def camlight(m: Model, d: Data):
-  """Camera / light frames (smooth.py:635-803): the position-stage launch."""
-  _position(m, d)
+  """Camera / light frames (smooth.py:635-803) from the frames and subtree_com in d."""
+  if not _stage("camlight", m, d):
+    _position(m, d)
 
 
 def flex(m: Model, d: Data):
-  """Flex vertex positions and edge lengths / Jacobians (smooth.py:419-460): the position-stage launch."""
+  """Flex vertex positions and edge lengths / Jacobians (smooth.py:419-460): the position-stage launch
+  (flexes run on the sparse pipeline)."""
   _position(m, d)
 
 
 def tendon(m: Model, d: Data):
-  """Tendon lengths and Jacobians (smooth.py:3627-3700): the position-stage launch."""
-  _position(m, d)
+  """Tendon lengths and Jacobians (smooth.py:3627-3700) from qpos and the frames in d."""
+  if not _stage("tendon", m, d):
+    _position(m, d)
 
 
 def crb(m: Model, d: Data):
-  """Composite rigid-body inertia and qM (smooth.py:806-912): the position-stage launch."""
-  _position(m, d)
+  """Composite rigid-body inertia and qM (smooth.py:888-912, tendon armature included) from cinert / cdof."""
+  if not _stage("crb", m, d):
+    _position(m, d)
 
 
 def collision(m: Model, d: Data):
@@ -155,33 +184,42 @@ def primitive_narrowphase(m: Model, d: Data, ctx: CollisionContext, collision_ta
 
 
 def make_constraint(m: Model, d: Data):
-  """Constraint rows d.efc (constraint.py:2718-2779): the position-stage launch, whose rows come from the
-  contacts it collides; after a caller edited d.contact, `mjw_contact_rows` rebuilds them from the pool."""
-  _position(m, d)
+  """Constraint rows d.efc (constraint.py:2718-2779) from the contacts in d.contact and the frames in d
+  (dense path; the sparse path reruns its position launch)."""
+  if not _stage("make_constraint", m, d):
+    _position(m, d)
 
 
 def transmission(m: Model, d: Data):
-  """Actuator lengths and moments (smooth.py:2605-2700): the position-stage launch."""
-  _position(m, d)
+  """Actuator lengths and moments (smooth.py:2605-2700) from the frames in d (BODY transmissions: the
+  position-stage launch, their moments sum over its contacts)."""
+  if not _stage("transmission", m, d):
+    _position(m, d)
 
 
 def com_vel(m: Model, d: Data):
-  """cvel, cdof_dot (smooth.py:1935-2038): the velocity-stage launch."""
-  _call("mjw_fwd_velocity", m, d)
+  """cvel, cdof_dot (smooth.py:1935-2038) and actuator_velocity from qvel and the frames in d."""
+  if not _stage("com_vel", m, d):
+    _call("mjw_fwd_velocity", m, d)
 
 
 def passive(m: Model, d: Data):
-  """qfrc_spring / damper / passive (passive.py:535-563): the velocity-stage launch (then the passive
-  callback, as fwd_velocity)."""
-  fwd_velocity(m, d)
+  """qfrc_spring / damper / gravcomp / fluid / passive (passive.py:535-563) from the state in d, then the
+  passive callback (as fwd_velocity calls it)."""
+  if not _stage("passive", m, d):
+    fwd_velocity(m, d)
+    return
+  if m.callback.passive is not None:
+    m.callback.passive(m, d)
 
 
 def rne(m: Model, d: Data, flg_acc: bool = False):
-  """qfrc_bias = RNE with zero acceleration (smooth.py:1276-1300, flg_acc = False): the velocity-stage
-  launch.  flg_acc = True (the inverse-dynamics use, out of this build's scope) is refused."""
+  """qfrc_bias = RNE with zero acceleration (smooth.py:1276-1300, flg_acc = False) from cvel / cdof_dot
+  in d.  flg_acc = True (the inverse-dynamics use, out of this build's scope) is refused."""
   if flg_acc:
     raise NotImplementedError("rne(flg_acc=True) (inverse dynamics) is not part of this build")
-  _call("mjw_fwd_velocity", m, d)
+  if not _stage("rne", m, d):
+    _call("mjw_fwd_velocity", m, d)
 
 
 def factor_m(m: Model, d: Data):

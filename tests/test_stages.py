@@ -2,7 +2,8 @@
 (mujoco_warp_amd/stages.py).
 
 CPU: every name the reference exports exists here, except the subsystems DESIGN.md §7 leaves out.
-GPU: the stage aliases reproduce the fused step's fields; the support functions agree with what the HIP
+GPU: the stage functions, chained, reproduce the fused step's fields and each reads the earlier stages'
+Data fields (an edit there is what it sees); the support functions agree with what the HIP
 kernels computed from the same state -- jac' qvel with the body's cvel, xfrc_accumulate with the xfrc part
 of qfrc_smooth, solve_m with qacc_smooth (dense humanoid and sparse cloth), subtree_vel's root entries with
 the directly summed momenta, and energy_pos + energy_vel conserved along a frictionless pendulum rollout.
@@ -67,6 +68,85 @@ def test_gpu_stage_aliases_match_forward():
   for name in ("xpos", "xquat", "subtree_com", "cinert", "cdof", "qM", "qLD", "actuator_length", "cvel", "cdof_dot", "qfrc_bias",
                "qfrc_passive", "qacc_smooth", "qacc", "cacc", "cfrc_int"):
     np.testing.assert_allclose(np_(getattr(d2, name)), np_(getattr(d, name)), rtol=1e-5, atol=1e-5, err_msg=name)
+
+
+@pytest.mark.gpu
+def test_gpu_stages_read_the_data_fields():
+  """Each stage function reads the Data fields the earlier stages wrote and writes only its own outputs
+  (smooth.py:357-415 kinematics, 601-632 com_pos, 888-912 crb, 1276-1300 rne; constraint.py:2718-2779):
+  kinematics leaves qM alone; com_pos takes an edited xipos; crb takes an edited cinert; rne with cvel and
+  cdof_dot zeroed gives the bias of the same state at rest; make_constraint rebuilds forward's rows."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+
+  mjm, m, d = _humanoid(8)
+  mjw.forward(m, d)
+  torch.cuda.synchronize()
+  base = {k: getattr(d, k).clone() for k in ("xpos", "xipos", "subtree_com", "cinert", "qM", "qfrc_bias", "cvel", "cdof_dot")}
+  efc = (d.nefc.clone(), d.efc.J.clone(), d.efc.D.clone(), d.efc.aref.clone(), d.efc.type.clone())
+  # kinematics: frames from qpos, nothing downstream touched
+  d.qM.fill_(7.0)
+  mjw.kinematics(m, d)
+  torch.cuda.synchronize()
+  assert torch.all(d.qM == 7.0)
+  np.testing.assert_allclose(np_(d.xpos), np_(base["xpos"]), rtol=0, atol=1e-6)
+  d.qM.copy_(base["qM"])
+  # com_pos: an edited xipos moves subtree_com as the mass-weighted subtree mean says
+  nb = mjm.nbody
+  delta = torch.zeros_like(d.xipos)
+  delta[:, 1:, 0] = 0.05  # every body shifted by 5 cm in x
+  d.xipos.add_(delta)
+  mjw.com_pos(m, d)
+  torch.cuda.synchronize()
+  xipos = np_(d.xipos)
+  mass = np.asarray(mjm.body_mass, np.float64)
+  for b in range(1, nb):
+    sub = [j for j in range(b, nb) if _ancestor(mjm, j, b)]
+    want = (mass[sub, None] * xipos[:, sub, :]).sum(axis=1) / mass[sub].sum()
+    np.testing.assert_allclose(np_(d.subtree_com)[:, b], want, rtol=0, atol=2e-6)
+  assert np.abs(np_(d.subtree_com)[:, 1, 0] - np_(base["subtree_com"])[:, 1, 0] - 0.05).max() < 1e-5
+  # crb: twice the inertias give twice the mass matrix outside the armature diagonal
+  d.xipos.copy_(base["xipos"])
+  mjw.com_pos(m, d)
+  d.cinert.mul_(2.0)
+  mjw.crb(m, d)
+  torch.cuda.synchronize()
+  arm = np.diag(np.asarray(mjm.dof_armature, np.float64))
+  nv = mjm.nv
+  q0 = np_(base["qM"])[:, :nv, :nv]
+  np.testing.assert_allclose(np_(d.qM)[:, :nv, :nv], 2.0 * (q0 - arm) + arm, rtol=1e-5, atol=1e-5)
+  d.cinert.copy_(base["cinert"])
+  mjw.crb(m, d)
+  # rne at rest: cvel = cdof_dot = 0 leaves gravity only, as forward on the same state with qvel = 0
+  d.cvel.zero_()
+  d.cdof_dot.zero_()
+  mjw.rne(m, d)
+  torch.cuda.synchronize()
+  _, m2, d2 = _humanoid(8)
+  d2.qvel.zero_()
+  mjw.forward(m2, d2)
+  torch.cuda.synchronize()
+  np.testing.assert_allclose(np_(d.qfrc_bias), np_(d2.qfrc_bias), rtol=1e-5, atol=1e-4)
+  # com_vel restores cvel / cdof_dot from qvel; make_constraint rebuilds forward's rows from d.contact
+  mjw.com_vel(m, d)
+  mjw.make_constraint(m, d)
+  torch.cuda.synchronize()
+  np.testing.assert_allclose(np_(d.cvel), np_(base["cvel"]), rtol=1e-5, atol=1e-5)
+  np.testing.assert_allclose(np_(d.cdof_dot), np_(base["cdof_dot"]), rtol=1e-5, atol=1e-5)
+  assert torch.equal(d.nefc, efc[0])
+  for w in range(8):
+    n = int(d.nefc[w])
+    assert torch.equal(d.efc.type[w, :n], efc[4][w, :n])
+    np.testing.assert_allclose(np_(d.efc.J[w, :n]), np_(efc[1][w, :n]), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(np_(d.efc.D[w, :n]), np_(efc[2][w, :n]), rtol=1e-5)
+    np.testing.assert_allclose(np_(d.efc.aref[w, :n]), np_(efc[3][w, :n]), rtol=1e-5, atol=1e-5)
+
+
+def _ancestor(mjm, j, b):
+  while j > b:
+    j = int(mjm.body_parentid[j])
+  return j == b
 
 
 @pytest.mark.gpu

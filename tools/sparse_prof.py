@@ -41,7 +41,7 @@ if cfg["key"] is not None:
 m = mjw.put_model(mjm, device="cuda")
 d = mjw.put_data(mjm, mjd, nworld=nworld, nconmax=cfg["nconmax"], njmax=cfg["njmax"], device="cuda", m=m)
 L = _lib.lib()
-buf = (ctypes.c_ulonglong * len(PHASES))()
+buf = (ctypes.c_ulonglong * (len(PHASES) + 2))()  # + the line-search row-pass and CG-iteration counts
 for i in range(warmup):
   mjw.ctrl_noise(m, d, i, center=center)
   mjw.step(m, d)
@@ -55,9 +55,12 @@ for i in range(nsteps):
 e1.record()
 torch.cuda.synchronize()
 L.mjw_prof_read_sparse(buf, 0)
-tot = sum(buf) or 1
+npass, niter = buf[len(PHASES)], buf[len(PHASES) + 1]
+tot = sum(buf[:len(PHASES)]) or 1
 out = {"model": which, "nworld": nworld, "ms_per_step": e0.elapsed_time(e1) / nsteps,
        "nefc_mean": float(d.nefc.float().mean()), "solver_niter_mean": float(d.solver_niter.float().mean()),
+       "cg_iterations_per_world_step": niter / (nworld * nsteps),
+       "linesearch_row_passes_per_cg_iteration": npass / max(niter, 1),
        "wave_cycles_per_world_step": {p: buf[i] / (nworld * nsteps) for i, p in enumerate(PHASES)},
        "share": {p: round(buf[i] / tot, 4) for i, p in enumerate(PHASES)}}
 print(json.dumps(out, indent=1))
