@@ -239,7 +239,10 @@ enum : int {
   PH_LOAD = 0, PH_KIN, PH_COM, PH_CAM, PH_CRB, PH_COLL, PH_TRN, PH_VEL, PH_ACT, PH_ACC, PH_GSOLVE, PH_GEULER,
   PH_DFACTOR, PH_DSOLVE, PH_DEULER,
   // sub-phases of PH_COLL (reported separately, not added to the total)
-  PH_C_ROWS0, PH_C_BROAD, PH_C_NARROW, PH_C_POOL, PH_C_JROWS, PH_C_SCAL, PH_C_TAIL, PH_N
+  PH_C_ROWS0, PH_C_BROAD, PH_C_NARROW, PH_C_POOL, PH_C_JROWS, PH_C_SCAL, PH_C_TAIL,
+  // parts of PH_DSOLVE (counted in it as well): Newton's Hessian build (MFMA over row pairs) and its
+  // Cholesky factor + solve, per solver iteration
+  PH_NT_H, PH_NT_CHOL, PH_N
 };
 #ifdef MJW_PROFILE
 static __device__ unsigned long long g_prof[PH_N];

@@ -491,7 +491,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
   // the qM staging and the factorisation instead of stalling each phase
   const int nq = m.nq;
   const bool qpos_lds = nq <= 64;
-  float pf_qfrc_smooth = 0.0f, pf_warm = 0.0f, pf_qvel = 0.0f, pf_qpos = 0.0f, pf_D = 0.0f, pf_aref = 0.0f, pf_fl = 0.0f;
+  float pf_qfrc_smooth = 0.0f, pf_warm = 0.0f, pf_qvel = 0.0f, pf_qpos = 0.0f, pf_D = 0.0f, pf_aref = 0.0f, pf_fl = 0.0f, pf_time = 0.0f;
   int pf_nefc = 0, pf_ne = 0, pf_nf = 0;
   if ((FLAGS & (DF_FACTOR | DF_SOLVE)) && dof) pf_qfrc_smooth = d.qfrc_smooth[gi];
   if (FLAGS & DF_SOLVE) {
@@ -508,6 +508,9 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
   if (FLAGS & DF_EULER) {
     if (dof) pf_qvel = d.qvel[gi];
     if (qpos_lds && lane < nq) pf_qpos = d.qpos[(long)wid * nq + lane];
+    // the time too: read at the end, after the solve's stores, its load would wait for all of them (vmcnt
+    // counts loads and stores in issue order)
+    if (lane == 0) pf_time = d.time[wid];
   }
 
   PROF_T0();
@@ -717,6 +720,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
             }
           }
           __syncthreads();
+          PROF_T0_SUB();
           f32x16 H = Mm;
           const int npair = (nefc + 1) >> 1;
           for (int t = 0; t < npair; t++) {
@@ -744,8 +748,10 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
             f32x4 v = rw[q];
             a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
           }
+          PROF_MARK_SUB(PH_NT_H);
           chol_factor<NB>(a, lane, S);
           Mgrad = chol_solve<NB>(a, S, lane, grad);
+          PROF_MARK_SUB(PH_NT_CHOL);
         } else {
           __syncthreads();
           Mgrad = symv(Mi, vd2, h);
@@ -1008,7 +1014,7 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       __syncthreads();
       if (lane < nq) d.qpos[(long)wid * nq + lane] = vq[lane];
     }
-    if (lane == 0) d.time[wid] = d.time[wid] + dt;
+    if (lane == 0) d.time[wid] = pf_time + dt;
   }
   PROF_MARK(PH_DEULER);
 }

@@ -26,7 +26,8 @@ from mujoco_warp_amd import _lib, mjcf  # noqa: E402
 PHASES = ["load", "kinematics", "com_pos", "camlight", "crb_qM", "collision+constraints", "transmission", "fwd_velocity",
           "fwd_actuation", "fwd_acceleration", "generic_solve", "generic_euler", "dense_factor", "dense_solve", "dense_euler"]
 # sub-phases of collision+constraints (not part of the total)
-SUB = ["c:eq_friction_limits", "c:broadphase", "c:narrowphase_staging", "c:pool_write", "c:contact_J", "c:row_scalars", "c:tail"]
+SUB = ["c:eq_friction_limits", "c:broadphase", "c:narrowphase_staging", "c:pool_write", "c:contact_J", "c:row_scalars", "c:tail",
+       "newton:H_build", "newton:H_cholesky"]
 nworld = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 solver = sys.argv[3] if len(sys.argv) > 3 else "CG"
@@ -68,5 +69,5 @@ s = sum(tot) or 1
 out = {"nworld": nworld, "solver": solver, "ms_per_step": e0.elapsed_time(e1) / nsteps,
        "wave_cycles_per_world_step": {p: tot[i] / (nworld * nsteps) for i, p in enumerate(PHASES) if tot[i]},
        "share": {p: round(tot[i] / s, 4) for i, p in enumerate(PHASES) if tot[i]},
-       "collision_subphase_cycles_per_world_step": {p: a[len(PHASES) + i] / (nworld * nsteps) for i, p in enumerate(SUB)}}
+       "subphase_cycles_per_world_step": {p: (a[len(PHASES) + i] + b[len(PHASES) + i]) / (nworld * nsteps) for i, p in enumerate(SUB)}}
 print(json.dumps(out, indent=1))

@@ -15,11 +15,15 @@ for s in $steps; do
     prof)
       timeout -k 10 300 python -u tools/phase_prof.py 8192 20 CG humanoid 5 > gpurun_out/r06_phase_humanoid.log 2>&1 || { tail -5 gpurun_out/r06_phase_humanoid.log; exit 1; }
       cat gpurun_out/r06_phase_humanoid.log ;;
+    nprof)
+      timeout -k 10 300 python -u tools/phase_prof.py 8192 20 NEWTON humanoid 5 > gpurun_out/r06_phase_humanoid_newton.log 2>&1 || { tail -5 gpurun_out/r06_phase_humanoid_newton.log; exit 1; }
+      cat gpurun_out/r06_phase_humanoid_newton.log ;;
     sprof)
       timeout -k 10 300 python -u tools/sparse_prof.py aloha_cloth 1024 5 20 > gpurun_out/r06_sparse_prof_aloha_cloth.log 2>&1 || { tail -5 gpurun_out/r06_sparse_prof_aloha_cloth.log; exit 1; }
       cat gpurun_out/r06_sparse_prof_aloha_cloth.log ;;
     pmc)
       ROUND=r06 timeout -k 10 900 bash tools/profile_model.sh humanoid > gpurun_out/prof_humanoid.log 2>&1 || { tail -5 gpurun_out/prof_humanoid.log; exit 1; }
+      cp gpurun_out/pmc_humanoid_r06.json profiles/ || exit 1
       cat gpurun_out/r06_humanoid_sq_counters.txt | grep -A12 step_kernel ;;
     bench)
       timeout -k 10 400 python3 -u bench.py > gpurun_out/r06_bench_humanoid.log 2>&1 || { tail -5 gpurun_out/r06_bench_humanoid.log; exit 1; }
