@@ -195,7 +195,8 @@ typedef struct mjw_model_t {
   MJW_MODEL_INT_ARRAYS(MJW_DECL_IA)
 } mjw_model_t;
 
-/* world-order workspace (mjw_data_t.sched): MJW_SCHED_BUCKETS histogram words, as many cursors, a flag */
+/* world-order workspace (mjw_data_t.sched): non-null enables the longest-first order (its words are spare since
+   round 6: the counter-reset kernel histograms world_key itself) */
 #define MJW_SCHED_BUCKETS 32
 #define MJW_SCHED_WORDS (2 * MJW_SCHED_BUCKETS + 2)
 

@@ -156,6 +156,55 @@ __device__ __forceinline__ float chol_solve(const float (&a)[32], const float* S
   return b;
 }
 
+// LDL' in place (A = L1 D L1', L1 unit lower), rows in lanes: the factor + solve of the matrices that are
+// factored for one solve and need no L (Newton's Hessian every iteration, the implicit-Euler matrix).
+// Per column: one pivot readlane, one reciprocal, and the trailing update's readlane + FMA pairs, whose
+// readlanes read the unscaled column (they do not wait on the reciprocal) -- no per-column lane selects.
+// A lane's entries right of its own column pick up rounding-level residue during the loop; they only
+// ever update entries of that same lane right of its column, and are cleared at the end.
+// On return a[k] (lane c) = L1[c][k] for k < c and 0 otherwise (the unit diagonal is implicit), S holds
+// the same rows and S[c * DSS + 32] (the scratch's padding column) = 1 / D[c] (1 past NB).
+template <int NB = 32>
+__device__ __forceinline__ void ldl_factor(float (&a)[32], int lane, float* S) {
+  const int c = lane & 31;
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    const float col = a[j];
+    const float r = __builtin_amdgcn_rcpf(rdlane(col, j));
+    S[j * DSS + 32] = r;  // the same value from every lane
+    a[j] = col * r;
+#pragma unroll
+    for (int k = j + 1; k < NB; k++) a[k] = fmaf(-a[j], rdlane(col, k), a[k]);
+  }
+#pragma unroll
+  for (int j = NB; j < 32; j++) S[j * DSS + 32] = 1.0f;
+#pragma unroll
+  for (int k = 0; k < NB; k++) a[k] = k < c ? a[k] : 0.0f;
+  __syncthreads();
+  if (lane < 32) {
+    f32x4* rw = reinterpret_cast<f32x4*>(S + c * DSS);
+#pragma unroll
+    for (int q = 0; q < 8; q++) rw[q] = f32x4{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
+  }
+  __syncthreads();
+}
+
+// (L1 D L1') x = b for a dof vector b (lane c, both halves; b = 0 past NB) with ldl_factor's a / S:
+// L1 z = b right-looking with the multipliers in registers (lanes at or above the column add an exact
+// zero), x = D^-1 z, then L1' x right-looking backward with the rows of L1 from S -- one readlane and one
+// FMA per column and sweep, no selects
+template <int NB = 32>
+__device__ __forceinline__ float ldl_solve(const float (&a)[32], const float* S, int lane, float b) {
+  const int c = lane & 31;
+  const float rd = S[c * DSS + 32];
+#pragma unroll
+  for (int k = 0; k < NB - 1; k++) b = fmaf(-a[k], rdlane(b, k), b);
+  b *= rd;
+#pragma unroll
+  for (int k = NB - 1; k > 0; k--) b = fmaf(-S[k * DSS + c], rdlane(b, k), b);
+  return b;
+}
+
 // stage an n x n block (global row stride gs) into S with identity padding to 32x32,
 // plus an optional diagonal term
 // (all 16 loads per lane are issued before the first LDS write: one global-latency wait per
@@ -749,8 +798,8 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
             a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
           }
           PROF_MARK_SUB(PH_NT_H);
-          chol_factor<NB>(a, lane, S);
-          Mgrad = chol_solve<NB>(a, S, lane, grad);
+          ldl_factor<NB>(a, lane, S);
+          Mgrad = ldl_solve<NB>(a, S, lane, grad);
           PROF_MARK_SUB(PH_NT_CHOL);
         } else {
           __syncthreads();
@@ -893,14 +942,11 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
 
   PROF_MARK(PH_DSOLVE);
 #if MJW_SCHED_EARLY
-  // the next step's longest-first order (see dense_kernel): the bucket count is bumped here, before the
-  // integration, not as the wave's last instruction -- a wave leaves its slot only once its memory
-  // operations are done, and a same-address atomic issued last held every slot a while longer
-  if ((FLAGS & DF_SOLVE) && d.sched && lane == 0) {
-    const int key = MJW_SCHED_BUCKETS - 1 - min(niter_out >> 1, MJW_SCHED_BUCKETS - 1);
-    d.world_key[wid] = key;
-    atomicAdd(d.sched + key, 1);
-  }
+  // the next step's longest-first order (see dense_kernel): this world's iteration bucket, stored here,
+  // before the integration; the counter-reset kernel of the next step histograms the buckets itself (no
+  // atomics here: same-address bucket atomics held the wave slots while they drained)
+  if ((FLAGS & DF_SOLVE) && d.sched && lane == 0)
+    d.world_key[wid] = MJW_SCHED_BUCKETS - 1 - min(niter_out >> 1, MJW_SCHED_BUCKETS - 1);
 #endif
   if (FLAGS & DF_EULER) {
     // ---- forward.py:51-354 (_advance + euler)
@@ -967,8 +1013,8 @@ __device__ __forceinline__ void dense_world(const mjw_model_t& m, const mjw_data
       stage_rows(nv, S, lane, a, Md);
       __syncthreads();
       // one solve with the factor (forward + backward sweep), no explicit inverse
-      chol_factor<NB>(a, lane, S);
-      qacc_adv = chol_solve<NB>(a, S, lane, dof ? ma : 0.0f);
+      ldl_factor<NB>(a, lane, S);
+      qacc_adv = ldl_solve<NB>(a, S, lane, dof ? ma : 0.0f);
       if (!dof) qacc_adv = 0.0f;
     }
     // activations (forward.py:132-168)

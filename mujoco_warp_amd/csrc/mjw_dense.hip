@@ -35,16 +35,15 @@ dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {
   dense_world<FLAGS, NEWTON, ELL, NB>(m, d, wid, sm);
   if (!MJW_SCHED_EARLY && (FLAGS & DF_SOLVE) && d.sched && (threadIdx.x & 63) == 0) {
     // the next step's order: bucket by this step's iterations, most iterations first
-    const int key = MJW_SCHED_BUCKETS - 1 - min(d.solver_niter[wid] >> 1, MJW_SCHED_BUCKETS - 1);
-    d.world_key[wid] = key;
-    atomicAdd(d.sched + key, 1);
+    d.world_key[wid] = MJW_SCHED_BUCKETS - 1 - min(d.solver_niter[wid] >> 1, MJW_SCHED_BUCKETS - 1);
   }
   WLOG_END(wid, (FLAGS & DF_SOLVE) ? d.solver_niter[wid] : 0);
 }
 
 // device self-checks of the primitives above (mjw_selftest): which = 0 -> per-wave dsum and
 // xhalf_add of 64-lane chunks; which = 1 -> spd_inverse of 32x32 row-major SPD matrices; which = 2 ->
-// the same with the factor bound NB = 16 (matrices that are the identity past row / column 16)
+// the same with the factor bound NB = 16 (matrices that are the identity past row / column 16);
+// which = 3 / 4 -> ldl_factor + ldl_solve (NB = 32 / 28) of one right-hand side per matrix
 __global__ void __launch_bounds__(64) selftest_kernel(int which, const float* in, float* out, int n) {
   __shared__ __attribute__((aligned(16))) float S[DS_WORDS];
   const int w = blockIdx.x, lane = threadIdx.x;
@@ -54,6 +53,23 @@ __global__ void __launch_bounds__(64) selftest_kernel(int which, const float* in
     float t = dsum(x);
     if (lane == 0) out[w] = t;
     out[n + w * 64 + lane] = xhalf_add(x);
+  } else if (which == 3 || which == 4) {
+    // ldl_factor + ldl_solve of (32x32 SPD, 32-vector) pairs, 1056 floats each; which = 4: NB = 28 (input
+    // identity past 28, right-hand side 0 there)
+    float a[32];
+    f32x16 M;
+    const float* g = in + (long)w * 1056;
+    stage_spd(g, 32, 32, nullptr, 0.0f, S, lane, a, M);
+    const float b = g[1024 + (lane & 31)];
+    float x;
+    if (which == 4) {
+      ldl_factor<28>(a, lane, S);
+      x = ldl_solve<28>(a, S, lane, b);
+    } else {
+      ldl_factor<32>(a, lane, S);
+      x = ldl_solve<32>(a, S, lane, b);
+    }
+    if (lane < 32) out[(long)w * 32 + lane] = x;
   } else {
     float a[32];
     f32x16 M;

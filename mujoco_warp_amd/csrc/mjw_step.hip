@@ -3078,13 +3078,18 @@ __global__ void __launch_bounds__(256) primitive_narrowphase_kernel(const mjw_mo
 // hipMemsetAsync: in a captured hipGraph the 4-byte memset node was observed to race the
 // forward kernel (stale counts, contacts dropped past the pool), kernel nodes stay ordered
 //
-// It also builds the dense kernel's longest-first world order for this step: the dense kernel of the
-// previous step histogrammed each world's solver-iteration bucket (sched[0, NB), world_key); a counting
-// sort over the buckets in this one workgroup (LDS cursors) writes world_order, a permutation of the
-// worlds with the most iterations first.  The order is built only when the histogram counts every world
-// exactly once (the last dense pass covered all worlds with the order enabled) and no bucket holds 7/8 of
-// them; otherwise world_order is the identity.  Measured: the same scatter done with global atomics inside the forward kernel serialised
-// on the 32 bucket counters and cost the forward kernel what it saved the dense kernel.
+// It also builds the dense kernel's longest-first world order for this step from the iteration bucket the
+// previous step's solving dense kernel stored per world (world_key, plain stores): a counting sort over the
+// buckets in this one workgroup writes world_order, a permutation of the worlds with the most iterations
+// first.  The histogram is counted here with LDS atomics, not by the dense kernels: they used to bump the
+// 32 bucket words with a global atomicAdd per world, and with one bucket holding nearly every world
+// (franka, 1-2 Newton iterations) those same-address atomics held each wave's slot until they drained --
+// franka's dense kernel measured 0.246 ms with them against 0.147 ms with the order off
+// (profiles/r06_ab_order.log).  (A wave-aggregated count -- one ballot and one LDS add per distinct key
+// of a 64-world chunk -- measured 0.022 ms for this kernel against 0.009 ms: humanoid CG has ~20 keys.)
+// The histogram and the scatter read the same keys (clamped to the bucket range), so world_order is a
+// permutation whatever the keys hold; stale keys only cost order quality.  One bucket holding 7/8 of the
+// worlds orders nothing: world_order is then the identity.
 constexpr int RESET_THREADS = 1024;
 __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* nacon, int* ncollision, int* sched, int* world_order,
                                                                        const int* world_key, int nworld) {
@@ -3093,35 +3098,46 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
   if (!sched) return;
   constexpr int NB = MJW_SCHED_BUCKETS;
   static_assert(NB <= 64, "one wave scans the buckets");
+  __shared__ int hist[NB];
   __shared__ int cursor[NB];
   __shared__ int valid;
+  if (t < NB) hist[t] = 0;
+  // the keys of the first KPT * RESET_THREADS worlds stay in registers for the scatter (all loads issued
+  // before the first LDS add)
+  constexpr int KPT = 16;
+  int kk[KPT];
+#pragma unroll
+  for (int q = 0; q < KPT; q++) {
+    const int w = t + q * RESET_THREADS;
+    kk[q] = w < nworld ? min(max(world_key[w], 0), NB - 1) : -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < KPT; q++)
+    if (kk[q] >= 0) atomicAdd(&hist[kk[q]], 1);
+  for (int w = t + KPT * RESET_THREADS; w < nworld; w += RESET_THREADS) atomicAdd(&hist[min(max(world_key[w], 0), NB - 1)], 1);
+  __syncthreads();
   if (t < 64) {
-    const int h = t < NB ? sched[t] : 0;
+    const int h = t < NB ? hist[t] : 0;
     int x = h;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(x, o);
       if (t >= o) x += y;
     }
-    const int total = __shfl(x, 63);
     int hmax = h;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) hmax = max(hmax, __shfl_xor(hmax, o));
-    if (t < NB) {
-      cursor[t] = x - h;
-      sched[t] = 0;
-    }
-    // one bucket holding nearly every world (franka: 1-2 Newton iterations each) orders nothing and
-    // serialises the LDS atomics on one address (18 us at 16k worlds): identity order then
-    if (t == 0) valid = total == nworld && hmax < nworld - (nworld >> 3);
+    if (t < NB) cursor[t] = x - h;
+    if (t == 0) valid = hmax < nworld - (nworld >> 3);
   }
   __syncthreads();
   if (valid) {
-    for (int w = t; w < nworld; w += RESET_THREADS) {
-      const int k = min(max(world_key[w], 0), NB - 1);
-      const int pos = atomicAdd(&cursor[k], 1);
-      if (pos < nworld) world_order[pos] = w;
-    }
+#pragma unroll
+    for (int q = 0; q < KPT; q++)
+      if (kk[q] >= 0) world_order[atomicAdd(&cursor[kk[q]], 1)] = t + q * RESET_THREADS;
+    for (int w = t + KPT * RESET_THREADS; w < nworld; w += RESET_THREADS)
+      world_order[atomicAdd(&cursor[min(max(world_key[w], 0), NB - 1)], 1)] = w;
   } else {
     for (int w = t; w < nworld; w += RESET_THREADS) world_order[w] = w;
   }
@@ -3342,9 +3358,13 @@ int step_fused(const mjw_model_t* m, const mjw_data_t* d, hipStream_t s, const c
   const bool ccd = m->nxn_ccd > 0 && d->naconmax > 0 && !(fl & (DSBL_CONSTRAINT | DSBL_CONTACT));
   if (!lean || ccd || implicit_int || m->opt_cone == CONE_ELLIPTIC || m->opt_integrator == INT_RK4 || m->nv <= 16 || m->nv > 28)
     return kNotFused;
-  // CG only: the Newton dense half needs 131-134 VGPRs and spills at the fused kernel's 128 (humanoid
-  // Newton measured 0.513 -> 0.558 ms fused)
-  if (m->opt_solver == SOLVER_NEWTON) return kNotFused;
+  // CG by default: the Newton dense half needs 131-134 VGPRs and spills at the fused kernel's 128 (humanoid
+  // Newton measured 0.513 -> 0.558 ms fused, round 5); MJW_FUSED_NEWTON=1 launches it fused (A/B runs)
+  static const bool newton_on = [] {
+    const char* e = getenv("MJW_FUSED_NEWTON");
+    return e && e[0] == '1';
+  }();
+  if (m->opt_solver == SOLVER_NEWTON) return newton_on ? launch_step_fused<true>(m, d, s, name) : kNotFused;
   return launch_step_fused<false>(m, d, s, name);
 }
 

@@ -226,3 +226,33 @@ def test_gpu_world_order_does_not_change_results():
   assert sorted(order.tolist()) == list(range(nworld))
   assert np.all(np.diff(key4[order]) >= 0)
   assert len(np.unique(key4)) > 1
+
+
+@pytest.mark.gpu
+def test_gpu_world_order_from_any_keys():
+  """The counter-reset kernel builds world_order from world_key alone (no histogram the dense kernels
+  count): any key values -- out of range, stale -- give a permutation sorted by the clamped key, and one
+  bucket holding 7/8 of the worlds or more gives the identity (franka: every world 1-2 Newton iterations)."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from tests.common import gpu_from_state, humanoid_model, random_states
+
+  mjm = humanoid_model("CG")
+  nworld = 1000
+  qpos, qvel, ctrl = random_states(mjm, nworld, seed=91)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl)
+  rng = np.random.default_rng(91)
+  keys = rng.integers(-5, 40, size=nworld).astype(np.int32)
+  d.world_key.copy_(torch.as_tensor(keys, device=d.world_key.device))
+  mjw.step(m, d)
+  torch.cuda.synchronize()
+  order = d.world_order.cpu().numpy()
+  assert sorted(order.tolist()) == list(range(nworld))
+  assert np.all(np.diff(np.clip(keys, 0, 31)[order]) >= 0)
+  keys = np.full(nworld, 3, np.int32)
+  keys[: nworld // 8 - 1] = 7
+  d.world_key.copy_(torch.as_tensor(keys, device=d.world_key.device))
+  mjw.step(m, d)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(d.world_order.cpu().numpy(), np.arange(nworld))

@@ -76,3 +76,30 @@ def test_spd_inverse_factor_bound_16():
   assert err.max() < 1e-4, err.max()
   np.testing.assert_array_equal(out16[:, 16:, 16:], np.tile(np.eye(16), (n, 1, 1)))
   np.testing.assert_array_equal(out16, out32)  # the skipped steps are exact no-ops
+
+
+@pytest.mark.parametrize("which,nb", [(3, 32), (4, 28)])
+def test_ldl_solve(which, nb):
+  """ldl_factor + ldl_solve (Newton's Hessian and the implicit-Euler matrix, mjw_dense.h): the solution of
+  random SPD systems of every size up to the factor bound, identity-padded to 32 (as the dense kernel
+  stages them), against numpy in fp64; a diagonal system is solved exactly up to the reciprocal."""
+  rng = np.random.default_rng(3 + which)
+  n = 96
+  M = np.tile(np.eye(32), (n, 1, 1))
+  b = np.zeros((n, 32))
+  for i in range(n):
+    k = 1 + i % nb
+    A = rng.normal(size=(k, k))
+    M[i, :k, :k] = A @ A.T / k + np.eye(k) * 0.3
+    b[i, :k] = rng.normal(size=k)
+  M[0] = np.diag(np.arange(1, 33, dtype=np.float64))
+  M[0, nb:, nb:] = np.eye(32 - nb)
+  b[0] = 0.0
+  b[0, :nb] = np.arange(1, nb + 1)
+  x = np.concatenate([M.reshape(n, -1), b], axis=1).astype(np.float32)
+  out = _run(which, x, n * 32).reshape(n, 32)
+  want = np.linalg.solve(M.astype(np.float32).astype(np.float64), b.astype(np.float32).astype(np.float64)[..., None])[..., 0]
+  err = np.abs(out - want).max(axis=1) / np.maximum(np.abs(want).max(axis=1), 1e-30)
+  assert err.max() < 1e-4, err.max()
+  np.testing.assert_allclose(out[0, :nb], 1.0, rtol=5e-7)
+  assert np.all(out[:, nb:] == 0.0)
