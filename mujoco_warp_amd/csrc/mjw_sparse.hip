@@ -43,6 +43,24 @@ namespace sp {
 // the solve, and 256 with a 64 VGPR cap were 12-25 % slower; so was capping the solve's residency
 // to fit the per-world row state in the 256 MB MALL: DESIGN 3.6)
 constexpr int BLK = 256;
+// A/B switches of the round-6 CG pass changes (tools/build_variants.py, same-box lines in
+// profiles/r06_sparse_ab.log): loading a J'f column's first JTS entries / a jv batch's JVS slots per row up
+// front (both slower: aloha_cloth 38.4 K and 43.4 K env-steps/s against 45.2 K without them -- more lines
+// in flight on a launch that already streams 3.2 TB/s), the small-tree register path (+4 %: 42.9 -> 45.2 K
+// ... with the rest as shipped) and the solve's 4-worlds-per-CU register cap (without it the inlined CG
+// loop takes 152 VGPRs, 3 worlds per CU, 34.0 K)
+#ifndef MJW_SP_JTPF
+#define MJW_SP_JTPF 0
+#endif
+#ifndef MJW_SP_JVPF
+#define MJW_SP_JVPF 0
+#endif
+#ifndef MJW_SP_TREE
+#define MJW_SP_TREE 1
+#endif
+#ifndef MJW_SP_SOLVE_MINBLK
+#define MJW_SP_SOLVE_MINBLK 4
+#endif
 constexpr int SOLVE_LDS_THREADS = 1024;
 constexpr int SP_LDS_SEARCH_MAX = 8192;  // the CG search direction lives in LDS up to this nv
 constexpr int SORTN = 32;  // J-transpose segments up to this length are sorted in registers
@@ -53,7 +71,11 @@ constexpr int SP_LDS_ITEMS_MAX = 48 * 1024;  // per-item contact counts of the c
 // deltas summed over waves, read back with mjw_prof_read_sparse
 // SPH_NPASS / SPH_NITER (counts, not cycles): the row passes of the line searches (the jv + alpha = 0
 // pass, the Newton-step pass and one per bracketing iteration) and the CG iterations, summed over worlds
-enum : int { SPH_KIN = 0, SPH_FLEX, SPH_CRB, SPH_COLL, SPH_CON, SPH_VEL, SPH_ACT, SPH_ACC, SPH_SINIT, SPH_SLS, SPH_SUPD, SPH_SCG, SPH_NPASS, SPH_NITER, SPH_N };
+// SPH_S_*: sub-phases of the CG iteration (also counted in SPH_SLS / SPH_SUPD): the line search's M x search
+// (mul_m_trees), its jv + alpha = 0 pass, its remaining row passes; update_constraint's row pass, its J'f
+// (transposed-index gathers); update_gradient's preconditioner (solve_trees / the Newton direction)
+enum : int { SPH_KIN = 0, SPH_FLEX, SPH_CRB, SPH_COLL, SPH_CON, SPH_VEL, SPH_ACT, SPH_ACC, SPH_SINIT, SPH_SLS, SPH_SUPD, SPH_SCG, SPH_NPASS, SPH_NITER,
+             SPH_S_MULM, SPH_S_JV, SPH_S_LSP, SPH_S_UCR, SPH_S_JTF, SPH_S_TREES, SPH_N };
 #ifdef MJW_PROFILE
 static __device__ unsigned long long g_sprof[SPH_N];
 #define SPROF_T0() unsigned long long _spt = __builtin_amdgcn_s_memtime()
@@ -67,7 +89,16 @@ static __device__ unsigned long long g_sprof[SPH_N];
   do {                                                      \
     if (threadIdx.x == 0) atomicAdd(&g_sprof[ph], (unsigned long long)(n)); \
   } while (0)
+#define SPROF_T0_SUB() unsigned long long _spts = __builtin_amdgcn_s_memtime()
+#define SPROF_MARK_SUB(ph)                                                       \
+  do {                                                                           \
+    unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_sprof[ph], _nt - _spts);           \
+    _spts = _nt;                                                                 \
+  } while (0)
 #else
+#define SPROF_T0_SUB() (void)0
+#define SPROF_MARK_SUB(ph) (void)0
 #define SPROF_T0() (void)0
 #define SPROF_MARK(ph) (void)0
 #define SPROF_COUNT(ph, n) (void)0
@@ -642,34 +673,129 @@ __device__ __forceinline__ void chain_load(const mjw_model_t& m, const float* A,
   }
 }
 
+// branched trees of at most TREE dofs (an arm whose two fingers hang off the wrist): x (and y) in registers,
+// the sparse loops of the general path below unchanged, each indexed access to a dof of the tree done as a
+// compare-select over the tree's TREE registers (no register array indexed at run time, no stack).  The
+// updates are the general path's, in its order, so the result is bitwise its result -- without its chain of
+// dependent global read-modify-writes (one tree's thread walked ~60 per call: aloha_cloth's preconditioner
+// measured 10.7 % of the step's wave-cycles, profiles/r06_sparse_prof.json)
+constexpr int TREE = 8;
+template <int T>
+__device__ __forceinline__ float tree_get(const float (&v)[T], int j) {
+  float g = 0.0f;
+#pragma unroll
+  for (int i = 0; i < T; i++) g = j == i ? v[i] : g;
+  return g;
+}
+// x = (L' D L)^-1 x for the tree of dofs [a, a + n), n <= T (smooth.py:2813-2846, as solve_trees)
+template <int T>
+__device__ __forceinline__ void tree_solve_small(const mjw_model_t& m, const float* LD, float* x, int a, int n) {
+  float xs[T];
+#pragma unroll
+  for (int k = 0; k < T; k++) xs[k] = k < n ? x[a + k] : 0.0f;
+#pragma unroll
+  for (int k = T - 1; k >= 0; k--) {
+    if (k >= n) continue;
+    const int adr = m.M_rowadr[a + k], nnz = m.M_rownnz[a + k];
+    const float xk = xs[k];
+#pragma unroll
+    for (int p = 0; p < T - 1; p++) {
+      if (p >= nnz - 1) break;
+      const int cj = m.M_colind[adr + p] - a;
+      const float v = LD[adr + p];
+#pragma unroll
+      for (int j = 0; j < k; j++)
+        if (cj == j) xs[j] -= v * xk;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < T; k++)
+    if (k < n) xs[k] /= LD[m.M_rowadr[a + k] + m.M_rownnz[a + k] - 1];
+#pragma unroll
+  for (int k = 0; k < T; k++) {
+    if (k >= n) continue;
+    const int adr = m.M_rowadr[a + k], nnz = m.M_rownnz[a + k];
+    float sk = xs[k];
+#pragma unroll
+    for (int p = 0; p < T - 1; p++) {
+      if (p >= nnz - 1) break;
+      sk -= LD[adr + p] * tree_get<T>(xs, m.M_colind[adr + p] - a);
+    }
+    xs[k] = sk;
+  }
+#pragma unroll
+  for (int k = 0; k < T; k++)
+    if (k < n) x[a + k] = xs[k];
+}
+// y = M x for the tree of dofs [a, a + n), n <= T (support.py:67-101, as mul_m_trees' general path)
+template <int T>
+__device__ __forceinline__ void tree_mul_small(const mjw_model_t& m, const float* M, const float* x, float* y, int a, int n) {
+  float xs[T], ys[T];
+#pragma unroll
+  for (int k = 0; k < T; k++) {
+    xs[k] = k < n ? x[a + k] : 0.0f;
+    ys[k] = 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < T; k++) {
+    if (k >= n) continue;
+    const int adr = m.M_rowadr[a + k], nnz = m.M_rownnz[a + k];
+    float sk = M[adr + nnz - 1] * xs[k];
+#pragma unroll
+    for (int p = 0; p < T - 1; p++) {
+      if (p >= nnz - 1) break;
+      const int i = m.M_colind[adr + p] - a;
+      const float v = M[adr + p];
+      sk += v * tree_get<T>(xs, i);
+#pragma unroll
+      for (int j = 0; j < k; j++)
+        if (i == j) ys[j] += v * xs[k];
+    }
+    ys[k] += sk;
+  }
+#pragma unroll
+  for (int k = 0; k < T; k++)
+    if (k < n) y[a + k] = ys[k];
+}
+
+// x = (L' D L)^-1 x of one tree held dense in registers (chain_load / tree_load)
+template <int T>
+__device__ __forceinline__ void tree_solve_regs(const float (&L)[T][T], float (&xs)[T], int n) {
+#pragma unroll
+  for (int k = T - 1; k >= 0; k--)
+    if (k < n) {
+#pragma unroll
+      for (int p = 0; p < k; p++) xs[p] -= L[k][p] * xs[k];
+    }
+#pragma unroll
+  for (int k = 0; k < T; k++)
+    if (k < n) xs[k] /= L[k][k];
+#pragma unroll
+  for (int k = 0; k < T; k++)
+    if (k < n) {
+      float sk = xs[k];
+#pragma unroll
+      for (int p = 0; p < k; p++) sk -= L[k][p] * xs[p];
+      xs[k] = sk;
+    }
+}
+
 // x = (L' D L)^-1 x in place, per tree (smooth.py:2813-2846)
-__device__ void solve_trees(const mjw_model_t& m, const float* LD, float* x) {
+__device__ __forceinline__ void solve_trees(const mjw_model_t& m, const float* LD, float* x) {
   for (int t = tid(); t < m.ntree; t += nthr()) {
     const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
+    const int n = e - a;
     if (chain_tree(m, a, e)) {
-      const int n = e - a;
       float L[CHAIN][CHAIN], xs[CHAIN];
       chain_load(m, LD, x, a, n, L, xs);
-#pragma unroll
-      for (int k = CHAIN - 1; k >= 0; k--)
-        if (k < n) {
-#pragma unroll
-          for (int p = 0; p < k; p++) xs[p] -= L[k][p] * xs[k];
-        }
-#pragma unroll
-      for (int k = 0; k < CHAIN; k++)
-        if (k < n) xs[k] /= L[k][k];
-#pragma unroll
-      for (int k = 0; k < CHAIN; k++)
-        if (k < n) {
-          float sk = xs[k];
-#pragma unroll
-          for (int p = 0; p < k; p++) sk -= L[k][p] * xs[p];
-          xs[k] = sk;
-        }
+      tree_solve_regs<CHAIN>(L, xs, n);
 #pragma unroll
       for (int k = 0; k < CHAIN; k++)
         if (k < n) x[a + k] = xs[k];
+      continue;
+    }
+    if (MJW_SP_TREE && n <= TREE) {
+      tree_solve_small<TREE>(m, LD, x, a, n);
       continue;
     }
     for (int k = e - 1; k >= a; k--) {
@@ -687,25 +813,35 @@ __device__ void solve_trees(const mjw_model_t& m, const float* LD, float* x) {
   }
 }
 
+// y = M x of one tree held dense in registers (rows k < n of y)
+template <int T>
+__device__ __forceinline__ void tree_mul_regs(const float (&L)[T][T], const float (&xs)[T], int n, float* y) {
+#pragma unroll
+  for (int k = 0; k < T; k++)
+    if (k < n) {
+      float sk = L[k][k] * xs[k];
+#pragma unroll
+      for (int p = 0; p < k; p++) sk += L[k][p] * xs[p];
+#pragma unroll
+      for (int j = k + 1; j < T; j++)
+        if (j < n) sk += L[j][k] * xs[j];
+      y[k] = sk;
+    }
+}
+
 // y = M x (support.py:67-101 sparse mul_m), per tree: lower rows plus their transposes
-__device__ void mul_m_trees(const mjw_model_t& m, const float* M, const float* x, float* y) {
+__device__ __forceinline__ void mul_m_trees(const mjw_model_t& m, const float* M, const float* x, float* y) {
   for (int t = tid(); t < m.ntree; t += nthr()) {
     const int a = m.tree_dofadr[t], e = m.tree_dofadr[t + 1];
+    const int n = e - a;
     if (chain_tree(m, a, e)) {
-      const int n = e - a;
       float L[CHAIN][CHAIN], xs[CHAIN];
       chain_load(m, M, x, a, n, L, xs);
-#pragma unroll
-      for (int k = 0; k < CHAIN; k++)
-        if (k < n) {
-          float sk = L[k][k] * xs[k];
-#pragma unroll
-          for (int p = 0; p < k; p++) sk += L[k][p] * xs[p];
-#pragma unroll
-          for (int j = k + 1; j < CHAIN; j++)
-            if (j < n) sk += L[j][k] * xs[j];
-          y[a + k] = sk;
-        }
+      tree_mul_regs<CHAIN>(L, xs, n, y + a);
+      continue;
+    }
+    if (MJW_SP_TREE && n <= TREE) {
+      tree_mul_small<TREE>(m, M, x, y, a, n);
       continue;
     }
     for (int k = a; k < e; k++) y[k] = 0.0f;
@@ -2571,6 +2707,8 @@ __device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, 
 // each thread loads RU rows (r0, r0 + nthr(), ...: the same per-thread order as a plain strided loop,
 // hence the same sums) before evaluating any of them.
 constexpr int RU = 4;  // 8 and 16 rows in flight per thread measured 14 % and 73 % slower on aloha_cloth
+constexpr int JVS = 8;  // J slots per row the jv pass loads up front (wider rows finish slot by slot)
+constexpr int JTS = 16;  // entries per dof column J'f loads up front (longer columns finish one by one)
 template <int NA, bool ELL = false>
 __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas, float* o) {
   if (ELL) {
@@ -2613,7 +2751,8 @@ __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas
 
 // `alpha`: the linesearch step still to be applied to Jaref (fused here: Jaref += alpha * jv)
 template <bool ELL = false>
-__device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
+__device__ __forceinline__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
+  SPROF_T0_SUB();
   float cost = 0.0f;
   if (ELL) {
     // a cone row reads its contact's other rows: Jaref is advanced for every row first
@@ -2679,9 +2818,29 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
   }
   }
   __syncthreads();
+  SPROF_MARK_SUB(SPH_S_UCR);
   float g = 0.0f;
   for (int i = tid(); i < c.nv; i += nthr()) {
     float s = 0.0f;
+#if MJW_SP_JTPF
+    // (MJW_SP_JTPF, off: measured slower) the column's first JTS entries loaded at once (indices and
+    // values), then their force gathers at once; same summation order
+    const int pa = c.JT_adr[i], pb = c.JT_adr[i + 1];
+    int ri[JTS];
+    float vi[JTS], fi[JTS];
+#pragma unroll
+    for (int k = 0; k < JTS; k++) {
+      const bool a = pa + k < pb;
+      ri[k] = a ? c.JT16[pa + k] : 0;
+      vi[k] = a ? c.JT_val[pa + k] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < JTS; k++) fi[k] = pa + k < pb ? c.force[ri[k]] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < JTS; k++)
+      if (pa + k < pb) s += vi[k] * fi[k];
+    for (int p = pa + JTS; p < pb; p++) s += c.JT_val[p] * c.force[c.JT16[p]];
+#else
     // 4 entries in flight (index loads, then the dependent force gathers), same summation order
     const int pa = c.JT_adr[i], pb = c.JT_adr[i + 1];
     int p = pa;
@@ -2695,11 +2854,13 @@ __device__ void update_constraint(SolveCtx& c, Smem& sm, float alpha = 0.0f) {
       s += v3 * f3;
     }
     for (; p < pb; p++) s += c.JT_val[p] * c.force[c.JT16[p]];
+#endif
     c.qfrc_c[i] = s;
     g += (c.Ma[i] - c.qfrc_s[i]) * (c.qacc[i] - c.qacc_s[i]);
   }
   float v[2] = {cost, g};
   block_sum_db<2>(v, sm, c.rphase);
+  SPROF_MARK_SUB(SPH_S_JTF);
   c.prev_cost = c.cost;
   c.gauss = 0.5f * v[1];
   c.cost = v[0] + 0.5f * v[1];
@@ -2857,7 +3018,8 @@ __device__ void newton_direction(const mjw_model_t& m, SolveCtx& c) {
 }
 
 template <bool ELL = false>
-__device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
+__device__ __forceinline__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
+  SPROF_T0_SUB();
   float gd = 0.0f;
   for (int i = tid(); i < c.nv; i += nthr()) {
     const float g = c.Ma[i] - c.qfrc_s[i] - c.qfrc_c[i];
@@ -2869,6 +3031,7 @@ __device__ void update_gradient(const mjw_model_t& m, SolveCtx& c, Smem& sm) {
   if (c.newton) newton_direction<ELL>(m, c);
   else solve_trees(m, c.LD, c.Mgrad);
   __syncthreads();
+  SPROF_MARK_SUB(SPH_S_TREES);
 }
 
 __device__ __forceinline__ bool in_bracket(const float* x, const float* y) {
@@ -2877,12 +3040,67 @@ __device__ __forceinline__ bool in_bracket(const float* x, const float* y) {
 
 // returns the step; qacc / Ma are updated here, Jaref by update_constraint
 template <bool ELL = false>
-__device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm) {
+__device__ __forceinline__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm) {
+  SPROF_T0_SUB();
   mul_m_trees(m, c.M, c.search, c.mv);
+#ifdef MJW_PROFILE
+  __syncthreads();  // (profile build only: the sub-phase ends when every tree is done)
+#endif
+  SPROF_MARK_SUB(SPH_S_MULM);
   // jv = J search, fused with the alpha = 0 evaluation of each row (same thread)
   // equality rows are quadratic for every step size: their cost 0.5 D (Jaref + a jv)^2 is folded
   // into the Gauss quadratic once here (v5[5..7]), and the line-search passes skip them
   float v5[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#if MJW_SP_JVPF
+  for (int r0 = tid(); r0 < c.nefc; r0 += RU * nthr()) {
+    // (MJW_SP_JVPF, off: measured slower) RU rows interleaved; every slot load of the batch (the first JVS
+    // slots of each row, masked by its non-zero count), D and Jaref issued before the first gather; the
+    // per-row summation order (slots ascending) is unchanged
+    int nz[RU];
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+      const int r = r0 + u * nthr();
+      nz[u] = r < c.nefc ? c.Jnnz[r] : 0;
+    }
+    float v[RU][JVS], Dv[RU], jav[RU];
+    int col[RU][JVS];
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+      const int r = r0 + u * nthr();
+      const bool ok = r < c.nefc;
+      Dv[u] = ok ? c.D[r] : 0.0f;
+      jav[u] = ok ? c.Jaref[r] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < JVS; k++) {
+        const long q = (long)k * c.P + r;
+        v[u][k] = k < nz[u] ? c.J[q] : 0.0f;
+        col[u][k] = k < nz[u] ? c.Jcol16[q] : 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+    const int r = r0 + u * nthr();
+    if (r >= c.nefc) continue;  // (not break: the loop must unroll, or v / col go to scratch)
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < JVS; k++)
+      if (k < nz[u]) s += v[u][k] * c.search[col[u][k]];
+    for (int k = JVS; k < nz[u]; k++) {  // rows wider than JVS slots (models with long chains)
+      const long q = (long)k * c.P + r;
+      s += c.J[q] * c.search[c.Jcol16[q]];
+    }
+    c.jv[r] = s;
+    if (r < c.ne) {
+      const float D = Dv[u], ja = jav[u];
+      v5[5] += 0.5f * D * ja * ja;
+      v5[6] += D * ja * s;
+      v5[7] += 0.5f * D * s * s;
+    } else if (!ELL || r < c.ne + c.nf || c.ell->type[r] != CNSTR_CONTACT_ELLIPTIC) {
+      eval_row_v(c, r, Dv[u], jav[u], s, 0.0f, v5);
+    }
+    }
+  }
+#else
   for (int r0 = tid(); r0 < c.nefc; r0 += RU * nthr()) {
     // RU rows interleaved so their (column -> search) gathers overlap; per-row order unchanged
     int nz[RU], kmax = 0;
@@ -2910,7 +3128,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
 #pragma unroll
     for (int u = 0; u < RU; u++) {
     const int r = r0 + u * nthr();
-    if (r >= c.nefc) break;
+    if (r >= c.nefc) continue;
     const float s = acc[u];
     c.jv[r] = s;
     if (r < c.ne) {
@@ -2923,7 +3141,9 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
     }
     }
   }
+#endif
   __syncthreads();
+  SPROF_MARK_SUB(SPH_S_JV);
   if (ELL) {  // the cones at alpha = 0, once every row's jv is in
     for (int r = c.ne + c.nf + tid(); r < c.nefc; r += nthr()) {
       if (c.ell->type[r] != CNSTR_CONTACT_ELLIPTIC) continue;
@@ -3028,6 +3248,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
     alpha = lo_alpha_in;
   }
   }
+  SPROF_MARK_SUB(SPH_S_LSP);
   for (int i = tid(); i < c.nv; i += nthr()) {
     c.qacc[i] += alpha * c.search[i];
     c.Ma[i] += alpha * c.mv[i];
@@ -3043,7 +3264,7 @@ __device__ float linesearch(const mjw_model_t& m, SolveCtx& c, int wid, Smem& sm
 // several times per CG iteration, then stop streaming it through HBM (sparse_launch picks it when
 // 2 * njmax floats fit the LDS of a CU).
 template <int PART>
-__global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK) solve_kernel(const mjw_model_t m, const mjw_data_t d) {
+__global__ void __launch_bounds__(PART == 2 ? SOLVE_LDS_THREADS : BLK, PART == 2 ? 1 : MJW_SP_SOLVE_MINBLK) solve_kernel(const mjw_model_t m, const mjw_data_t d) {
   // PART 3: PART 1 for elliptic-cone models (the cone rows of a contact are evaluated together)
   constexpr bool ELL = PART == 3;
   __shared__ Smem sm;

@@ -41,7 +41,8 @@ if cfg["key"] is not None:
 m = mjw.put_model(mjm, device="cuda")
 d = mjw.put_data(mjm, mjd, nworld=nworld, nconmax=cfg["nconmax"], njmax=cfg["njmax"], device="cuda", m=m)
 L = _lib.lib()
-buf = (ctypes.c_ulonglong * (len(PHASES) + 2))()  # + the line-search row-pass and CG-iteration counts
+SUB = ["cg:mul_m", "cg:jv_pass", "cg:ls_passes", "cg:constraint_rows", "cg:JTf", "cg:precondition"]
+buf = (ctypes.c_ulonglong * (len(PHASES) + 2 + len(SUB)))()  # + the line-search row-pass and CG-iteration counts, sub-phases
 for i in range(warmup):
   mjw.ctrl_noise(m, d, i, center=center)
   mjw.step(m, d)
@@ -62,5 +63,7 @@ out = {"model": which, "nworld": nworld, "ms_per_step": e0.elapsed_time(e1) / ns
        "cg_iterations_per_world_step": niter / (nworld * nsteps),
        "linesearch_row_passes_per_cg_iteration": npass / max(niter, 1),
        "wave_cycles_per_world_step": {p: buf[i] / (nworld * nsteps) for i, p in enumerate(PHASES)},
-       "share": {p: round(buf[i] / tot, 4) for i, p in enumerate(PHASES)}}
+       "share": {p: round(buf[i] / tot, 4) for i, p in enumerate(PHASES)},
+       "cg_subphase_cycles_per_world_step": {p: buf[len(PHASES) + 2 + i] / (nworld * nsteps) for i, p in enumerate(SUB)},
+       "cg_subphase_share_of_total": {p: round(buf[len(PHASES) + 2 + i] / tot, 4) for i, p in enumerate(SUB)}}
 print(json.dumps(out, indent=1))
