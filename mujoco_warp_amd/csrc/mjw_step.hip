@@ -1171,7 +1171,15 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       if (pass) plist[npass + rank] = p;
       npass += __popcll(bal);
     }
-    if (!POOL && lane == 0 && npass > 0) atomicAdd(d.ncollision, npass);
+    // the broadphase count joins the world's first contact-slot reservation below when ncollision sits
+    // right after nacon (io.py allocates them so): one 64-bit atomic per world instead of two same-address
+    // 32-bit ones -- the separate ncollision atomic measured 2.5 % of the step kernel (humanoid CG, 0.453 ->
+    // 0.443 ms without it) and 5 % of the Newton forward kernel (profiles/r06_ab_ncoll.log); the combined atomic
+    // against the two: step kernel 0.493 -> 0.442 ms, Newton forward 0.310 -> 0.247 ms (profiles/r06_ab_cnt64.log)
+    const bool cnt64 = d.ncollision == d.nacon + 1;
+    int pend = POOL ? 0 : npass;
+    if (!cnt64 && pend > 0 && lane == 0) atomicAdd(d.ncollision, pend);
+    if (!cnt64) pend = 0;
     WSYNC();
     PROF_MARK_SUB(PH_C_BROAD);
     const float* geom_margin = MR(geom_margin);
@@ -1349,9 +1357,16 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       int nstage = min(CM, running - rbeg);
       PROF_MARK_SUB(PH_C_NARROW);
       if (nstage <= 0) break;
-      // global pool slot for this round (one atomic per world per round)
+      // global pool slot for this round (one atomic per world per round; the first also adds the
+      // broadphase count into ncollision, the high word)
       int gbase = 0;
-      if (!POOL && lane == 0) gbase = atomicAdd(d.nacon, nstage);
+      if (!POOL && lane == 0) {
+        if (pend > 0)
+          gbase = (int)(unsigned)atomicAdd(reinterpret_cast<unsigned long long*>(d.nacon), ((unsigned long long)pend << 32) | (unsigned)nstage);
+        else
+          gbase = atomicAdd(d.nacon, nstage);
+      }
+      pend = 0;
       gbase = __shfl(gbase, 0, 64);
       WSYNC();
       // rows per staged contact (pyramidal: 1 or 2*(condim-1); elliptic: condim), prefix over contacts
@@ -1510,6 +1525,7 @@ __device__ __forceinline__ void collision_and_constraints(const mjw_model_t& m, 
       if (running <= rend) break;
       round++;
     }
+    if (pend > 0 && lane == 0) atomicAdd(d.ncollision, pend);  // no contact staged: the count alone
   }
   (void)ncon_total;
   if (TEN && m.ntendon && !dsbl_constraint) {
@@ -3098,10 +3114,16 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
   if (!sched) return;
   constexpr int NB = MJW_SCHED_BUCKETS;
   static_assert(NB <= 64, "one wave scans the buckets");
-  __shared__ int hist[NB];
+  // a 64-world chunk whose worlds share one key is counted with one LDS add by its first lane: with one
+  // bucket holding every world (franka, 16 k worlds) per-lane adds serialised 64 ways in every
+  // wave-instruction (0.024 ms for this kernel); mixed chunks add per lane, into per-wave histograms (row
+  // stride NB + 1)
+  constexpr int NWV = RESET_THREADS / 64;
+  __shared__ int hist[NWV * (NB + 1)];
   __shared__ int cursor[NB];
   __shared__ int valid;
-  if (t < NB) hist[t] = 0;
+  const int wv = t >> 6, lane = t & 63;
+  for (int i = t; i < NWV * (NB + 1); i += RESET_THREADS) hist[i] = 0;
   // the keys of the first KPT * RESET_THREADS worlds stay in registers for the scatter (all loads issued
   // before the first LDS add)
   constexpr int KPT = 16;
@@ -3112,10 +3134,26 @@ __global__ void __launch_bounds__(RESET_THREADS) reset_counters_kernel(int* naco
     kk[q] = w < nworld ? min(max(world_key[w], 0), NB - 1) : -1;
   }
   __syncthreads();
+  int* hw = hist + wv * (NB + 1);
 #pragma unroll
-  for (int q = 0; q < KPT; q++)
-    if (kk[q] >= 0) atomicAdd(&hist[kk[q]], 1);
-  for (int w = t + KPT * RESET_THREADS; w < nworld; w += RESET_THREADS) atomicAdd(&hist[min(max(world_key[w], 0), NB - 1)], 1);
+  for (int q = 0; q < KPT; q++) {
+    const int k = kk[q];
+    const int k0 = __shfl(k, 0);
+    if (__ballot(k != k0 && k >= 0) == 0ull) {  // every valid key equals the first lane's
+      const int n = __popcll(__ballot(k >= 0));
+      if (lane == 0 && k0 >= 0) atomicAdd(&hw[k0], n);
+    } else if (k >= 0) {
+      atomicAdd(&hw[k], 1);
+    }
+  }
+  for (int w = t + KPT * RESET_THREADS; w < nworld; w += RESET_THREADS) atomicAdd(&hw[min(max(world_key[w], 0), NB - 1)], 1);
+  __syncthreads();
+  if (t < NB) {
+    int h = 0;
+#pragma unroll
+    for (int v = 0; v < NWV; v++) h += hist[v * (NB + 1) + t];
+    hist[t] = h;  // (row 0, bucket t: read back only by thread t's own wave below)
+  }
   __syncthreads();
   if (t < 64) {
     const int h = t < NB ? hist[t] : 0;

@@ -734,8 +734,11 @@ def _alloc_data(m, nworld, nconmax, njmax, naconmax, device, nccdmax=None, njmax
   for name, shp in cint.items():
     _set_data_field(d, name, torch.zeros((naconmax,) + shp, dtype=torch.int32, device=device))
   d.contact.efc_address.fill_(-1)
-  d.nacon = torch.zeros(1, dtype=torch.int32, device=device)
-  d.ncollision = torch.zeros(1, dtype=torch.int32, device=device)
+  # nacon and ncollision adjacent (one 8-B aligned allocation): the dense step kernel adds a world's
+  # broadphase pairs and its contact slots with one 64-bit atomic (mjw_step.hip collision_and_constraints)
+  counters = torch.zeros(2, dtype=torch.int32, device=device)
+  d.nacon = counters[0:1]
+  d.ncollision = counters[1:2]
   # MJW_SCHED=0: no longest-first world order for the dense kernel (A/B runs)
   d.sched = None if os.environ.get("MJW_SCHED") == "0" else torch.zeros(_lib.SCHED_WORDS, dtype=torch.int32, device=device)
   d.efc.J_rowadr = torch.zeros((nworld, 0), dtype=torch.int32, device=device)
