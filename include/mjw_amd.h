@@ -208,7 +208,8 @@ typedef struct mjw_data_t {
   int32_t world_offset; /* global id of world 0 (multi-GPU sharding); affects ctrl noise only */
   int32_t pad_;
   int32_t* nacon;      /* (1,) contacts written this step (may exceed naconmax) */
-  int32_t* ncollision; /* (1,) broadphase pairs this step */
+  int32_t* ncollision; /* (1,) broadphase pairs this step; when ncollision == nacon + 1 (one 8-B aligned pair,
+                          as put_data allocates them) the step adds both with one 64-bit atomic per world */
   int32_t* sched;      /* (MJW_SCHED_WORDS,) world-order workspace of the dense path: histogram of
                         * the previous step's solver-iteration buckets, bucket cursors, valid flag */
 #define MJW_DECL_DRA(name, n) float* name;

@@ -20,9 +20,13 @@ namespace mjw {
 #define MJW_DENSE_WPE 4  // NB = 28 (A/B builds: 3)
 #endif
 // (Newton keeps 3: at 4 its NB = 28 instances allocate more registers, not fewer -- apollo's dense
-// kernel measured 0.153 -> 0.173 ms)
+// kernel measured 0.153 -> 0.173 ms; again with the LDL' Hessian solve in round 6, MJW_DENSE_WPE_NEWTON=4:
+// humanoid Newton 0.182 -> 0.193 ms, apollo 0.133 -> 0.136 ms, profiles/r06_ab_newton_wpe.log)
+#ifndef MJW_DENSE_WPE_NEWTON
+#define MJW_DENSE_WPE_NEWTON 3
+#endif
 template <int FLAGS, bool NEWTON, int NB>
-constexpr int dense_waves_per_eu() { return FLAGS == DF_EULER ? 6 : (NB <= 16 ? 4 : (NB <= 28 && !NEWTON ? MJW_DENSE_WPE : 3)); }
+constexpr int dense_waves_per_eu() { return FLAGS == DF_EULER ? 6 : (NB <= 16 ? 4 : (NB <= 28 ? (NEWTON ? MJW_DENSE_WPE_NEWTON : MJW_DENSE_WPE) : 3)); }
 template <int FLAGS, bool NEWTON, bool ELL, int NB>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(dense_waves_per_eu<FLAGS, NEWTON, NB>())))
 dense_kernel(const mjw_model_t m, const mjw_data_t d, int w0) {

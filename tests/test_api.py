@@ -256,3 +256,31 @@ def test_gpu_world_order_from_any_keys():
   mjw.step(m, d)
   torch.cuda.synchronize()
   np.testing.assert_array_equal(d.world_order.cpu().numpy(), np.arange(nworld))
+
+
+@pytest.mark.gpu
+def test_gpu_pool_counters_adjacent_or_not():
+  """io.py allocates nacon and ncollision adjacent, and the dense step adds a world's broadphase count and
+  its contact-slot reservation with one 64-bit atomic (mjw_step.hip collision_and_constraints); a caller
+  that swaps in its own ncollision tensor gets the two 32-bit atomics instead: same counts, same state."""
+  import torch
+
+  import mujoco_warp_amd as mjw
+  from tests.common import gpu_from_state, humanoid_model, np_, random_states
+
+  mjm = humanoid_model("CG")
+  nworld = 300
+  qpos, qvel, ctrl = random_states(mjm, nworld, seed=92)
+  m, d = gpu_from_state(mjm, qpos, qvel, ctrl)
+  m2, d2 = gpu_from_state(mjm, qpos, qvel, ctrl)
+  assert d.ncollision.data_ptr() == d.nacon.data_ptr() + 4
+  d2.ncollision = torch.zeros(1, dtype=torch.int32, device=d2.nacon.device)
+  assert d2.ncollision.data_ptr() != d2.nacon.data_ptr() + 4
+  for _ in range(3):
+    mjw.step(m, d)
+    mjw.step(m2, d2)
+  torch.cuda.synchronize()
+  assert int(d.nacon[0]) == int(d2.nacon[0]) > 0
+  assert int(d.ncollision[0]) == int(d2.ncollision[0]) > 0
+  for f in ("qpos", "qvel", "qacc"):
+    assert np.array_equal(np_(getattr(d, f)), np_(getattr(d2, f))), f
