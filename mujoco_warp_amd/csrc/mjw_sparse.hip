@@ -43,22 +43,13 @@ namespace sp {
 // the solve, and 256 with a 64 VGPR cap were 12-25 % slower; so was capping the solve's residency
 // to fit the per-world row state in the 256 MB MALL: DESIGN 3.6)
 constexpr int BLK = 256;
-// A/B switches of the round-6 CG pass changes (tools/build_variants.py, same-box lines in
-// profiles/r06_sparse_ab.log): loading a J'f column's first JTS entries / a jv batch's JVS slots per row up
-// front (both slower: aloha_cloth 38.4 K and 43.4 K env-steps/s against 45.2 K without them -- more lines
-// in flight on a launch that already streams 3.2 TB/s), the small-tree register path (+4 %: 42.9 -> 45.2 K
-// ... with the rest as shipped) and the solve's 4-worlds-per-CU register cap (without it the inlined CG
-// loop takes 152 VGPRs, 3 worlds per CU, 34.0 K).  Mode 2 of each prefetch switch loads in chunks (jv: JVC
-// slots of RU rows, J'f: JTC entries); same box, profiles/r06_sparse_ab2.log: 45.1 K as shipped, 41.8 K with
-// the 4-slot jv chunks, 43.9 K with 2-slot ones, 40.3 K with 8-entry J'f chunks -- every form that puts more
-// loads in flight per thread is slower: the passes are bound by the memory pipeline's throughput (vector
-// memory instructions and lines), not by the latency of one thread's chain
-#ifndef MJW_SP_JTPF
-#define MJW_SP_JTPF 0
-#endif
-#ifndef MJW_SP_JVPF
-#define MJW_SP_JVPF 0
-#endif
+// Round-6 A/B switches of the CG passes (tools/build_variants.py, same-box lines in profiles/r06_sparse_ab.log
+// and r06_sparse_ab2.log): the small-tree register path (+4 %: aloha_cloth 42.9 -> 45.2 K env-steps/s) and
+// the solve's 4-worlds-per-CU register cap (without it the inlined CG loop takes 152 VGPRs, 3 worlds per CU,
+// 34.0 K).  Measured and removed (the code is in commit 5781637): loading a jv batch's J slots / a J'f
+// column's entries up front, whole (43.4 K / 38.4 K) or in chunks (4- / 2-slot jv chunks 41.8 K / 43.9 K,
+// 8-entry J'f chunks 40.3 K, against 45.1 K): every form that puts more loads in flight per thread is slower
+// -- the passes are bound by the memory pipeline's throughput, not by the latency of one thread's chain
 #ifndef MJW_SP_TREE
 #define MJW_SP_TREE 1
 #endif
@@ -762,7 +753,7 @@ __device__ __forceinline__ void tree_mul_small(const mjw_model_t& m, const float
     if (k < n) y[a + k] = ys[k];
 }
 
-// x = (L' D L)^-1 x of one tree held dense in registers (chain_load / tree_load)
+// x = (L' D L)^-1 x of one chain tree held dense in registers (chain_load)
 template <int T>
 __device__ __forceinline__ void tree_solve_regs(const float (&L)[T][T], float (&xs)[T], int n) {
 #pragma unroll
@@ -2719,16 +2710,6 @@ __device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, 
 // each thread loads RU rows (r0, r0 + nthr(), ...: the same per-thread order as a plain strided loop,
 // hence the same sums) before evaluating any of them.
 constexpr int RU = 4;  // 8 and 16 rows in flight per thread measured 14 % and 73 % slower on aloha_cloth
-constexpr int JVS = 8;  // J slots per row the jv pass loads up front (wider rows finish slot by slot)
-#ifndef MJW_SP_JVC
-#define MJW_SP_JVC 4
-#endif
-#ifndef MJW_SP_JTC
-#define MJW_SP_JTC 8
-#endif
-constexpr int JVC = MJW_SP_JVC;  // jv pass slot chunk (MJW_SP_JVPF == 2)
-constexpr int JTC = MJW_SP_JTC;  // J'f entry chunk (MJW_SP_JTPF == 2)
-constexpr int JTS = 16;  // entries per dof column J'f loads up front (longer columns finish one by one)
 template <int NA, bool ELL = false>
 __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas, float* o) {
   if (ELL) {
@@ -2842,43 +2823,6 @@ __device__ __forceinline__ void update_constraint(SolveCtx& c, Smem& sm, float a
   float g = 0.0f;
   for (int i = tid(); i < c.nv; i += nthr()) {
     float s = 0.0f;
-#if MJW_SP_JTPF == 1
-    // (MJW_SP_JTPF, off: measured slower) the column's first JTS entries loaded at once (indices and
-    // values), then their force gathers at once; same summation order
-    const int pa = c.JT_adr[i], pb = c.JT_adr[i + 1];
-    int ri[JTS];
-    float vi[JTS], fi[JTS];
-#pragma unroll
-    for (int k = 0; k < JTS; k++) {
-      const bool a = pa + k < pb;
-      ri[k] = a ? c.JT16[pa + k] : 0;
-      vi[k] = a ? c.JT_val[pa + k] : 0.0f;
-    }
-#pragma unroll
-    for (int k = 0; k < JTS; k++) fi[k] = pa + k < pb ? c.force[ri[k]] : 0.0f;
-#pragma unroll
-    for (int k = 0; k < JTS; k++)
-      if (pa + k < pb) s += vi[k] * fi[k];
-    for (int p = pa + JTS; p < pb; p++) s += c.JT_val[p] * c.force[c.JT16[p]];
-#elif MJW_SP_JTPF == 2
-    // chunks of JTC entries: the chunk's indices and values, then its force gathers, all issued at once
-    const int pa = c.JT_adr[i], pb = c.JT_adr[i + 1];
-    for (int p0 = pa; p0 < pb; p0 += JTC) {
-      int ri[JTC];
-      float vi[JTC], fi[JTC];
-#pragma unroll
-      for (int k = 0; k < JTC; k++) {
-        const bool a = p0 + k < pb;
-        ri[k] = a ? c.JT16[p0 + k] : 0;
-        vi[k] = a ? c.JT_val[p0 + k] : 0.0f;
-      }
-#pragma unroll
-      for (int k = 0; k < JTC; k++) fi[k] = p0 + k < pb ? c.force[ri[k]] : 0.0f;
-#pragma unroll
-      for (int k = 0; k < JTC; k++)
-        if (p0 + k < pb) s += vi[k] * fi[k];
-    }
-#else
     // 4 entries in flight (index loads, then the dependent force gathers), same summation order
     const int pa = c.JT_adr[i], pb = c.JT_adr[i + 1];
     int p = pa;
@@ -2892,7 +2836,6 @@ __device__ __forceinline__ void update_constraint(SolveCtx& c, Smem& sm, float a
       s += v3 * f3;
     }
     for (; p < pb; p++) s += c.JT_val[p] * c.force[c.JT16[p]];
-#endif
     c.qfrc_c[i] = s;
     g += (c.Ma[i] - c.qfrc_s[i]) * (c.qacc[i] - c.qacc_s[i]);
   }
@@ -3089,104 +3032,6 @@ __device__ __forceinline__ float linesearch(const mjw_model_t& m, SolveCtx& c, i
   // equality rows are quadratic for every step size: their cost 0.5 D (Jaref + a jv)^2 is folded
   // into the Gauss quadratic once here (v5[5..7]), and the line-search passes skip them
   float v5[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#if MJW_SP_JVPF == 1
-  for (int r0 = tid(); r0 < c.nefc; r0 += RU * nthr()) {
-    // (MJW_SP_JVPF, off: measured slower) RU rows interleaved; every slot load of the batch (the first JVS
-    // slots of each row, masked by its non-zero count), D and Jaref issued before the first gather; the
-    // per-row summation order (slots ascending) is unchanged
-    int nz[RU];
-#pragma unroll
-    for (int u = 0; u < RU; u++) {
-      const int r = r0 + u * nthr();
-      nz[u] = r < c.nefc ? c.Jnnz[r] : 0;
-    }
-    float v[RU][JVS], Dv[RU], jav[RU];
-    int col[RU][JVS];
-#pragma unroll
-    for (int u = 0; u < RU; u++) {
-      const int r = r0 + u * nthr();
-      const bool ok = r < c.nefc;
-      Dv[u] = ok ? c.D[r] : 0.0f;
-      jav[u] = ok ? c.Jaref[r] : 0.0f;
-#pragma unroll
-      for (int k = 0; k < JVS; k++) {
-        const long q = (long)k * c.P + r;
-        v[u][k] = k < nz[u] ? c.J[q] : 0.0f;
-        col[u][k] = k < nz[u] ? c.Jcol16[q] : 0;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < RU; u++) {
-    const int r = r0 + u * nthr();
-    if (r >= c.nefc) continue;  // (not break: the loop must unroll, or v / col go to scratch)
-    float s = 0.0f;
-#pragma unroll
-    for (int k = 0; k < JVS; k++)
-      if (k < nz[u]) s += v[u][k] * c.search[col[u][k]];
-    for (int k = JVS; k < nz[u]; k++) {  // rows wider than JVS slots (models with long chains)
-      const long q = (long)k * c.P + r;
-      s += c.J[q] * c.search[c.Jcol16[q]];
-    }
-    c.jv[r] = s;
-    if (r < c.ne) {
-      const float D = Dv[u], ja = jav[u];
-      v5[5] += 0.5f * D * ja * ja;
-      v5[6] += D * ja * s;
-      v5[7] += 0.5f * D * s * s;
-    } else if (!ELL || r < c.ne + c.nf || c.ell->type[r] != CNSTR_CONTACT_ELLIPTIC) {
-      eval_row_v(c, r, Dv[u], jav[u], s, 0.0f, v5);
-    }
-    }
-  }
-#elif MJW_SP_JVPF == 2
-  for (int r0 = tid(); r0 < c.nefc; r0 += RU * nthr()) {
-    // RU rows interleaved, their slots in chunks of JVC: each chunk's J values and columns for all RU rows
-    // are loaded before its first gather (one memory round trip per chunk instead of one per slot); the
-    // per-row summation order (slots ascending) is unchanged
-    int nz[RU], kmax = 0;
-    float acc[RU];
-#pragma unroll
-    for (int u = 0; u < RU; u++) {
-      const int r = r0 + u * nthr();
-      nz[u] = r < c.nefc ? c.Jnnz[r] : 0;
-      kmax = max(kmax, nz[u]);
-      acc[u] = 0.0f;
-    }
-    for (int k0 = 0; k0 < kmax; k0 += JVC) {
-      float v[RU][JVC];
-      int col[RU][JVC];
-#pragma unroll
-      for (int u = 0; u < RU; u++)
-#pragma unroll
-        for (int j = 0; j < JVC; j++) {
-          const int k = k0 + j;
-          const long q = (long)k * c.P + r0 + u * nthr();
-          v[u][j] = k < nz[u] ? c.J[q] : 0.0f;
-          col[u][j] = k < nz[u] ? c.Jcol16[q] : 0;
-        }
-#pragma unroll
-      for (int u = 0; u < RU; u++)
-#pragma unroll
-        for (int j = 0; j < JVC; j++)
-          if (k0 + j < nz[u]) acc[u] += v[u][j] * c.search[col[u][j]];
-    }
-#pragma unroll
-    for (int u = 0; u < RU; u++) {
-    const int r = r0 + u * nthr();
-    if (r >= c.nefc) continue;
-    const float s = acc[u];
-    c.jv[r] = s;
-    if (r < c.ne) {
-      const float D = c.D[r], ja = c.Jaref[r];
-      v5[5] += 0.5f * D * ja * ja;
-      v5[6] += D * ja * s;
-      v5[7] += 0.5f * D * s * s;
-    } else if (!ELL || r < c.ne + c.nf || c.ell->type[r] != CNSTR_CONTACT_ELLIPTIC) {
-      eval_row(c, r, 0.0f, v5);
-    }
-    }
-  }
-#else
   for (int r0 = tid(); r0 < c.nefc; r0 += RU * nthr()) {
     // RU rows interleaved so their (column -> search) gathers overlap; per-row order unchanged
     int nz[RU], kmax = 0;
@@ -3227,7 +3072,6 @@ __device__ __forceinline__ float linesearch(const mjw_model_t& m, SolveCtx& c, i
     }
     }
   }
-#endif
   __syncthreads();
   SPROF_MARK_SUB(SPH_S_JV);
   if (ELL) {  // the cones at alpha = 0, once every row's jv is in
