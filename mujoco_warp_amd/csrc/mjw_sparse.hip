@@ -2709,7 +2709,8 @@ __device__ __forceinline__ void eval_row(const SolveCtx& c, int r, float alpha, 
 // eval_row at NA step sizes over every row (o: NA x 3 sums).  The row passes are latency bound, so
 // each thread loads RU rows (r0, r0 + nthr(), ...: the same per-thread order as a plain strided loop,
 // hence the same sums) before evaluating any of them.
-constexpr int RU = 4;  // 8 and 16 rows in flight per thread measured 14 % and 73 % slower on aloha_cloth
+constexpr int RU = 4;  // 8 and 16 rows in flight per thread measured 14 % and 73 % slower on aloha_cloth, 2 and 1
+                       // 3 % and 5 % slower (round 6, profiles/r06_sparse_ab_ru.log)
 template <int NA, bool ELL = false>
 __device__ __forceinline__ void eval_rows(const SolveCtx& c, const float* alphas, float* o) {
   if (ELL) {
