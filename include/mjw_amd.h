@@ -33,7 +33,7 @@
 
 #include <stdint.h>
 
-#define MJW_ABI_VERSION 33
+#define MJW_ABI_VERSION 34
 
 /* ---- model: int scalars ---- */
 #define MJW_MODEL_INT_SCALARS(X)                                                                   \
@@ -309,13 +309,17 @@ int mjw_ctrl_noise(const mjw_model_t* m, const mjw_data_t* d, const float* cente
  * (collision_core.py:345-365), each `naconmax` long: collision_pair (2 ints, type-ordered geoms),
  * collision_pairid (2 ints: explicit <pair> id or -1 / -2 excluded, collision-sensor id or -1),
  * collision_worldid.  Both read the geom frames d.geom_xpos / d.geom_xmat of the position stage.
- * mjw_nxn_broadphase replaces nxn_broadphase (collision_driver.py:697-731) and serves sap_broadphase
- * (:602-640, the same candidate set): survivors of opt_broadphase_filter over the filtered NXN list,
- * counted in d.ncollision (which the caller zeroes), slots past naconmax dropped.
+ * mjw_nxn_broadphase replaces nxn_broadphase (collision_driver.py:697-731): survivors of
+ * opt_broadphase_filter over the filtered NXN list, counted in d.ncollision (which the caller zeroes), slots
+ * past naconmax dropped.  mjw_sap_broadphase replaces sap_broadphase (:554-643): bounding spheres projected on
+ * the reference's fixed direction and sorted per world (ngeom <= 4096), the sweep's candidates (_sap_range
+ * :421-441) that are NXN pairs through the same filter, appended the same way (round 6; ABI 34).
  * mjw_primitive_narrowphase replaces primitive_narrowphase (collision_primitive.py:1461-1549): contacts of
  * the candidates [0, min(ncollision, naconmax)) whose type pair (t1 <= t2) has bit 8 t1 + t2 set in
  * typemask, appended to the contact pool at d.nacon as write_contact does (collision_core.py:160-232). */
 int mjw_nxn_broadphase(const mjw_model_t* m, const mjw_data_t* d, int* collision_pair, int* collision_pairid, int* collision_worldid,
+                       void* stream);
+int mjw_sap_broadphase(const mjw_model_t* m, const mjw_data_t* d, int* collision_pair, int* collision_pairid, int* collision_worldid,
                        void* stream);
 int mjw_primitive_narrowphase(const mjw_model_t* m, const mjw_data_t* d, const int* collision_pair, const int* collision_pairid,
                               const int* collision_worldid, unsigned long long typemask, void* stream);

@@ -3013,6 +3013,100 @@ __global__ void __launch_bounds__(256) nxn_broadphase_kernel(const mjw_model_t m
 // come from make_constraint).  Same geometry routines as the fused path: plane-sphere / capsule,
 // sphere-sphere / capsule / box, capsule-capsule / box (narrowphase), plane-box corners, plane-ellipsoid /
 // cylinder / mesh and sphere-cylinder (the pre-pass routines).
+// collision_driver.py:554-643 sap_broadphase (SAP_TILE / SAP_SEGMENTED; one workgroup per world here): every
+// geom's bounding sphere (rbound + margin; planes unbounded) projected on the reference's fixed direction, the
+// lower ends sorted in LDS (bitonic, padded to a power of two), and for each sorted geom i the candidates j in
+// (i, min(ngeom - 1, first j with lower_j > upper_i)] (:421-441 _sap_range with _binary_search :362-370, the
+// first geom past the overlap included, as there); a candidate that is not an NXN pair (excluded: contype /
+// conaffinity, parent, self, <exclude>) is skipped, the others pass the same broadphase filter as the NXN
+// path (or always, with a collision-sensor id) and are appended as mjw_nxn_broadphase does
+constexpr int SAP_MAX_GEOM = 4096;  // LDS: lower / index of the padded sort + upper per geom
+__global__ void __launch_bounds__(256) sap_broadphase_kernel(const mjw_model_t m, const mjw_data_t d, int* cpair, int* cpairid, int* cworld) {
+  extern __shared__ __attribute__((aligned(16))) float sap_sh[];
+  const int wid = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+  if (wid >= d.nworld) return;
+  const int ng = m.ngeom;
+  int np2 = 1;
+  while (np2 < ng) np2 <<= 1;
+  float* lo = sap_sh;
+  int* ix = reinterpret_cast<int*>(sap_sh + np2);
+  float* up = sap_sh + 2 * np2;
+  const float* gx = d.geom_xpos + (long)wid * ng * 3;
+  const float* gm = d.geom_xmat + (long)wid * ng * 9;
+  const float* geom_rbound = MR(geom_rbound);
+  const float* geom_margin = MR(geom_margin);
+  float dir[3] = {0.5935f, 0.7790f, 0.1235f};
+  const float dn = 1.0f / sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+  for (int i = 0; i < 3; i++) dir[i] *= dn;
+  for (int g = t; g < np2; g += nt) {
+    if (g < ng) {
+      float rb = geom_rbound[g];
+      if (rb == 0.0f) rb = MJW_MAXVAL;  // a plane
+      const float radius = rb + geom_margin[g];
+      const float center = dir[0] * gx[3 * g] + dir[1] * gx[3 * g + 1] + dir[2] * gx[3 * g + 2];
+      const bool nan = center != center;
+      lo[g] = nan ? MJW_MAXVAL : center - radius;
+      up[g] = nan ? MJW_MAXVAL : center + radius;
+      ix[g] = g;
+    } else {
+      lo[g] = __builtin_huge_valf();  // padding sorts last
+      ix[g] = -1;
+    }
+  }
+  __syncthreads();
+  // bitonic sort of (lo, ix) ascending
+  for (int k = 2; k <= np2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < np2; i += nt) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool asc = (i & k) == 0;
+          const float a = lo[i], b = lo[l];
+          if ((a > b) == asc) {
+            lo[i] = b; lo[l] = a;
+            const int x = ix[i]; ix[i] = ix[l]; ix[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = t; i < ng; i += nt) {
+    const int g1 = ix[i];
+    const float upper = up[g1];
+    int a = i + 1, b = ng;  // first position past i whose lower end exceeds upper
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (lo[mid] > upper) b = mid;
+      else a = mid + 1;
+    }
+    const int limit = min(ng - 1, b);
+    for (int j = i + 1; j <= limit; j++) {
+      const int g2 = ix[j];
+      const int ga = min(g1, g2), gb = max(g1, g2);
+      const long key = (long)ga * ng + gb;
+      // the NXN pair of (ga, gb): the filtered list is in upper-triangle order (its entries type-ordered)
+      int pa = 0, pb = m.nxn, p = -1;
+      while (pa < pb) {
+        const int mid = (pa + pb) >> 1;
+        const int h1 = m.nxn_geom_pair[2 * mid], h2 = m.nxn_geom_pair[2 * mid + 1];
+        const long km = (long)min(h1, h2) * ng + max(h1, h2);
+        if (km == key) { p = mid; break; }
+        if (km < key) pa = mid + 1;
+        else pb = mid;
+      }
+      if (p < 0) continue;
+      if (!(m.nxn_pairid[2 * p + 1] >= 0 || broadphase_filter_g(m, gx, gm, wid, ga, gb))) continue;
+      const int k = atomicAdd(d.ncollision, 1);
+      if (k >= d.naconmax) continue;
+      cpair[2 * k] = m.nxn_geom_pair[2 * p];
+      cpair[2 * k + 1] = m.nxn_geom_pair[2 * p + 1];
+      cpairid[2 * k] = m.nxn_pairid[2 * p];
+      cpairid[2 * k + 1] = m.nxn_pairid[2 * p + 1];
+      cworld[k] = wid;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) primitive_narrowphase_kernel(const mjw_model_t m, const mjw_data_t d, const int* cpair, const int* cpairid,
                                                                     const int* cworld, unsigned long long typemask) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3705,6 +3799,26 @@ int mjw_nxn_broadphase(const mjw_model_t* m, const mjw_data_t* d, int* collision
   hipLaunchKernelGGL(mjw::nxn_broadphase_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *m, *d, collision_pair,
                      collision_pairid, collision_worldid);
   return set_err(hipGetLastError(), "mjw_nxn_broadphase");
+}
+
+int mjw_sap_broadphase(const mjw_model_t* m, const mjw_data_t* d, int* collision_pair, int* collision_pairid, int* collision_worldid,
+                       void* stream) {
+  if (d->nworld <= 0 || m->nxn <= 0) return 0;
+  if (!collision_pair || !collision_pairid || !collision_worldid) return set_err(hipErrorInvalidValue, "mjw_sap_broadphase: null context array");
+  if (m->ngeom > mjw::SAP_MAX_GEOM) {
+    g_err = "mjw_sap_broadphase: more than " + std::to_string(mjw::SAP_MAX_GEOM) + " geoms (the LDS sort)";
+    return -2;
+  }
+  int np2 = 1;
+  while (np2 < m->ngeom) np2 <<= 1;
+  const size_t lds = (size_t)(2 * np2 + m->ngeom) * 4;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute((const void*)mjw::sap_broadphase_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  hipLaunchKernelGGL(mjw::sap_broadphase_kernel, dim3(d->nworld), dim3(256), lds, (hipStream_t)stream, *m, *d, collision_pair, collision_pairid,
+                     collision_worldid);
+  return set_err(hipGetLastError(), "mjw_sap_broadphase");
 }
 
 int mjw_primitive_narrowphase(const mjw_model_t* m, const mjw_data_t* d, const int* collision_pair, const int* collision_pairid,

@@ -144,10 +144,18 @@ def nxn_broadphase(m: Model, d: Data, ctx: CollisionContext):
 
 
 def sap_broadphase(m: Model, d: Data, ctx: CollisionContext):
-  """collision_driver.py:602-640: sweep-and-prune is the reference's device for large geom counts; it
-  yields the same candidate set as nxn_broadphase (the same filtered pairs through the same filters, order
-  aside), which is what this build computes for it."""
-  nxn_broadphase(m, d, ctx)
+  """collision_driver.py:554-643 sweep-and-prune: per world the geoms' bounding spheres (rbound + margin,
+  planes unbounded) projected on the reference's fixed direction and sorted in LDS, each sorted geom's
+  candidates up to the first one past its overlap (_sap_range :421-441), those that are NXN pairs through the
+  broadphase filter (or with a collision-sensor id) appended to `ctx` as nxn_broadphase does, d.ncollision
+  counting them.  One workgroup per world (mjw_sap_broadphase, ngeom <= 4096)."""
+  from . import _lib
+  from .io import cdata, cmodel
+  from .forward import _stream
+
+  L = _lib.lib()
+  pp, pi, pw = _ctx_ptrs(d, ctx)
+  _lib.check(L.mjw_sap_broadphase(cmodel(m), cdata(d), pp, pi, pw, _stream(d)), "mjw_sap_broadphase")
 
 
 # the PRIMITIVE entries of collision_driver.py:43-77 (type-ordered pairs)

@@ -196,3 +196,48 @@ def test_gpu_primitive_narrowphase_matches_fused_collision():
   assert only and all((int(mjm.geom_type[r[1]]), int(mjm.geom_type[r[2]])) == (0, 2) for r in only)
   with pytest.raises(NotImplementedError):
     mjw.primitive_narrowphase(m, d, ctx, [(mjw.GeomType.BOX, mjw.GeomType.BOX)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("filt", [2, 3])
+def test_gpu_sap_equals_nxn_on_a_crowd(filt):
+  """sap_broadphase (the sort-and-sweep of collision_driver.py:554-643, mjw_sap_broadphase) on 120 spheres and
+  a plane in 3 worlds: with the sphere filter a pair passes only if its bounding spheres overlap, so their
+  projections overlap and the sweep reaches it -- the candidate set equals nxn_broadphase's, pair for pair,
+  including the plane's pairs (a plane's projection is unbounded); excluded pairs (parent / contype) stay out."""
+  import mujoco_warp_amd as mjw
+
+  rng = np.random.default_rng(7)
+  bodies = []
+  for i in range(120):
+    p = rng.uniform(-0.6, 0.6, 3) + np.array([0.0, 0.0, 0.7])
+    r = rng.uniform(0.04, 0.12)
+    ct = ' contype="2" conaffinity="2"' if i % 17 == 0 else ""  # a few never collide with the others
+    bodies.append(f'<body pos="{p[0]:.4f} {p[1]:.4f} {p[2]:.4f}"><freejoint/><geom type="sphere" size="{r:.4f}"{ct}/></body>')
+  xml = f'<mujoco><worldbody><geom type="plane" size="5 5 .1"/>{"".join(bodies)}</worldbody></mujoco>'
+  mjm = mjw.load_model_from_string(xml)
+  m = mjw.put_model(mjm, device="cuda")
+  m.opt.broadphase_filter = filt
+  nworld = 3
+  d = mjw.make_data(mjm, nworld=nworld, nconmax=4000, njmax=64, device="cuda", m=m)
+  q = np.tile(mjm.qpos0, (nworld, 1))
+  for w in range(1, nworld):  # shift the crowd per world so the worlds differ
+    q[w, 0::7] += rng.normal(0, 0.05, 120)
+    q[w, 2::7] += rng.normal(0, 0.05, 120)
+  d.qpos[:] = torch.as_tensor(q, dtype=torch.float32, device="cuda")
+  mjw.kinematics(m, d)
+  sets = []
+  for bp in (mjw.nxn_broadphase, mjw.sap_broadphase):
+    d.ncollision.zero_()
+    ctx = mjw.create_collision_context(d.naconmax, device=d)
+    bp(m, d, ctx)
+    torch.cuda.synchronize()
+    n = int(d.ncollision[0])
+    assert n < d.naconmax
+    pairs = ctx.collision_pair.cpu().numpy()[:n]
+    worlds = ctx.collision_worldid.cpu().numpy()[:n]
+    got = {(int(w), int(a), int(b)) for w, (a, b) in zip(worlds, pairs)}
+    assert len(got) == n
+    sets.append(got)
+  assert sets[0] == sets[1]
+  assert len(sets[0]) > 3 * nworld  # the crowd touches itself and the plane
