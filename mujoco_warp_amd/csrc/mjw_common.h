@@ -245,27 +245,38 @@ enum : int {
   PH_NT_H, PH_NT_CHOL, PH_N
 };
 #ifdef MJW_PROFILE
-static __device__ unsigned long long g_prof[PH_N];
+// PROF_COPIES copies of every phase counter, a wave adding into copy (workgroup id mod PROF_COPIES): with
+// one counter per phase, 8192 waves' same-address atomics serialised and the profile build ran the humanoid
+// step 2.5x slower than the product build, inflating whichever phase followed each mark (round 6)
+constexpr int PROF_COPIES = 64;
+static __device__ unsigned long long g_prof[PH_N * PROF_COPIES];
+#define PROF_SLOT(ph) (&g_prof[(ph) * PROF_COPIES + (blockIdx.x & (PROF_COPIES - 1))])
 #define PROF_T0() unsigned long long _pt = __builtin_amdgcn_s_memtime()
 #define PROF_T0_SUB() unsigned long long _pts = __builtin_amdgcn_s_memtime()
 #define PROF_MARK_SUB(ph)                                                        \
   do {                                                                           \
     unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[ph], _nt - _pts);             \
+    if ((threadIdx.x & 63) == 0) atomicAdd(PROF_SLOT(ph), _nt - _pts);           \
     _pts = _nt;                                                                  \
   } while (0)
 #define PROF_MARK(ph)                                                            \
   do {                                                                           \
     unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[ph], _nt - _pt);              \
+    if ((threadIdx.x & 63) == 0) atomicAdd(PROF_SLOT(ph), _nt - _pt);            \
     _pt = _nt;                                                                   \
   } while (0)
 #define MJW_PROF_READER(fname)                                                                  \
   extern "C" int fname(unsigned long long* out, int reset) {                                    \
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(mjw::g_prof), sizeof(unsigned long long) * mjw::PH_N); \
+    static unsigned long long c[mjw::PH_N * mjw::PROF_COPIES];                                  \
+    hipError_t e = hipMemcpyFromSymbol(c, HIP_SYMBOL(mjw::g_prof), sizeof(c));                  \
+    for (int p = 0; p < mjw::PH_N; p++) {                                                       \
+      unsigned long long t = 0;                                                                 \
+      for (int k = 0; k < mjw::PROF_COPIES; k++) t += c[p * mjw::PROF_COPIES + k];              \
+      out[p] = t;                                                                               \
+    }                                                                                           \
     if (e == hipSuccess && reset) {                                                             \
-      unsigned long long z[mjw::PH_N] = {};                                                     \
-      e = hipMemcpyToSymbol(HIP_SYMBOL(mjw::g_prof), z, sizeof(z));                              \
+      for (auto& v : c) v = 0;                                                                  \
+      e = hipMemcpyToSymbol(HIP_SYMBOL(mjw::g_prof), c, sizeof(c));                              \
     }                                                                                           \
     return (int)e;                                                                              \
   }

@@ -72,23 +72,27 @@ constexpr int SP_LDS_ITEMS_MAX = 48 * 1024;  // per-item contact counts of the c
 enum : int { SPH_KIN = 0, SPH_FLEX, SPH_CRB, SPH_COLL, SPH_CON, SPH_VEL, SPH_ACT, SPH_ACC, SPH_SINIT, SPH_SLS, SPH_SUPD, SPH_SCG, SPH_NPASS, SPH_NITER,
              SPH_S_MULM, SPH_S_JV, SPH_S_LSP, SPH_S_UCR, SPH_S_JTF, SPH_S_TREES, SPH_N };
 #ifdef MJW_PROFILE
-static __device__ unsigned long long g_sprof[SPH_N];
+// SPROF_COPIES copies per counter, a workgroup adding into copy (world mod SPROF_COPIES): same-address
+// atomics from every wave would serialise and distort the phases they follow (as in mjw_common.h)
+constexpr int SPROF_COPIES = 64;
+static __device__ unsigned long long g_sprof[SPH_N * SPROF_COPIES];
+#define SPROF_SLOT(ph) (&g_sprof[(ph) * SPROF_COPIES + (blockIdx.x & (SPROF_COPIES - 1))])
 #define SPROF_T0() unsigned long long _spt = __builtin_amdgcn_s_memtime()
 #define SPROF_MARK(ph)                                                           \
   do {                                                                           \
     unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_sprof[ph], _nt - _spt);            \
+    if ((threadIdx.x & 63) == 0) atomicAdd(SPROF_SLOT(ph), _nt - _spt);          \
     _spt = _nt;                                                                  \
   } while (0)
 #define SPROF_COUNT(ph, n)                                  \
   do {                                                      \
-    if (threadIdx.x == 0) atomicAdd(&g_sprof[ph], (unsigned long long)(n)); \
+    if (threadIdx.x == 0) atomicAdd(SPROF_SLOT(ph), (unsigned long long)(n)); \
   } while (0)
 #define SPROF_T0_SUB() unsigned long long _spts = __builtin_amdgcn_s_memtime()
 #define SPROF_MARK_SUB(ph)                                                       \
   do {                                                                           \
     unsigned long long _nt = __builtin_amdgcn_s_memtime();                       \
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_sprof[ph], _nt - _spts);           \
+    if ((threadIdx.x & 63) == 0) atomicAdd(SPROF_SLOT(ph), _nt - _spts);         \
     _spts = _nt;                                                                 \
   } while (0)
 #else
@@ -3524,10 +3528,16 @@ __global__ void __launch_bounds__(BLK) euler_kernel(const mjw_model_t m, const m
 
 #ifdef MJW_PROFILE
 extern "C" int mjw_prof_read_sparse(unsigned long long* out, int reset) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(sp::g_sprof), sizeof(unsigned long long) * sp::SPH_N);
+  static unsigned long long c[sp::SPH_N * sp::SPROF_COPIES];
+  hipError_t e = hipMemcpyFromSymbol(c, HIP_SYMBOL(sp::g_sprof), sizeof(c));
+  for (int p = 0; p < sp::SPH_N; p++) {
+    unsigned long long t = 0;
+    for (int k = 0; k < sp::SPROF_COPIES; k++) t += c[p * sp::SPROF_COPIES + k];
+    out[p] = t;
+  }
   if (e == hipSuccess && reset) {
-    unsigned long long z[sp::SPH_N] = {};
-    e = hipMemcpyToSymbol(HIP_SYMBOL(sp::g_sprof), z, sizeof(z));
+    for (auto& v : c) v = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(sp::g_sprof), c, sizeof(c));
   }
   return (int)e;
 }
